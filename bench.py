@@ -1,0 +1,146 @@
+#!/usr/bin/env python
+"""Headline benchmark: NMF replicates/sec at K=10, n_iter=100 (BASELINE.json).
+
+Config ("PBMC-scale"): a synthetic 10,000-cell x 2,000-HVG
+normalised-counts matrix (planted programs, Poisson counts, per-gene unit-variance
+scaling exactly as cNMF's norm_counts, cnmf.py:670-681), K = 10, and the reference's
+factorize settings (cnmf.py:757-771): online MU, Frobenius, tol 1e-4, chunk 5000,
+online_chunk_max_iter = max_NMF_iter = 1000, random init from the ledger seeds.
+
+One *step* = factorising one ledger batch of ``--n-iter`` (default 100) replicates to
+convergence on each GPU -- the whole cNMF ``factorize`` work for that batch (init,
+every pass, every inner solve, convergence checks; spectra copied back to the host as
+factorize persists them).  Scaling is *weak*: every rank factorises its own 100
+replicates (round-robin ledger shard, as ``worker_filter``), so the job does 100*N
+replicates per step.  ``value`` is whole-job replicates/sec.
+
+Run: ``python bench.py [--gpus N --steps K --warmup W]``; for N > 1 under
+``torch.distributed.run`` (one process per GPU, RCCL over xGMI).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+BASELINE_REPS_PER_SEC = 0.5  # PBMC3k, 120 replicates in ~240 s (CPU, sklearn cNMF)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--cells", type=int, default=10000)
+    ap.add_argument("--genes", type=int, default=2000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--n-iter", type=int, default=100, help="replicates per GPU per step")
+    ap.add_argument("--seed", type=int, default=14)
+    ap.add_argument("--algo", default="mu")
+    ap.add_argument("--mode", default="online")
+    ap.add_argument("--beta-loss", default="frobenius")
+    ap.add_argument("--max-nmf-iter", type=int, default=1000)
+    ap.add_argument("--batch-size", type=int, default=5000)
+    ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available() and not args.cpu
+    if use_cuda:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    else:
+        dev = torch.device("cpu")
+    if world > 1:
+        dist.init_process_group(backend="nccl" if use_cuda else "gloo",
+                                device_id=dev if use_cuda else None)
+
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = normalized_counts_matrix(args.cells, args.genes, n_programs=args.k, seed=0)
+    Xd = torch.from_numpy(X).to(dev)
+    opts = NMFOptions(n_components=args.k, init="random", beta_loss=args.beta_loss,
+                      algo=args.algo, mode=args.mode, tol=1e-4,
+                      online_chunk_size=args.batch_size,
+                      online_chunk_max_iter=args.max_nmf_iter)
+    solver = NMFBatchSolver(Xd, opts)
+
+    # Ledger seeds exactly as cNMF.prepare draws them (cnmf.py:738-741), one ledger batch
+    # per step; rank r takes every world-th replicate (worker_filter, cnmf.py:53-54).
+    n_total = args.n_iter * world
+    nsteps = args.warmup + args.steps
+    np.random.seed(args.seed)
+    all_seeds = np.random.randint(low=1, high=(2 ** 31) - 1, size=n_total * nsteps)
+
+    def step(i: int):
+        seeds = all_seeds[i * n_total:(i + 1) * n_total][rank::world]
+        res = solver.run([int(s) for s in seeds])
+        spectra = res.W.cpu()  # factorize persists spectra (cnmf.py:889-892)
+        return res, spectra
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    barrier()
+    t0 = time.perf_counter()
+    passes = []
+    for i in range(args.warmup, nsteps):
+        res, _ = step(i)
+        passes.append(float(np.mean(res.n_iter)))
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1000.0 * elapsed / args.steps
+    reps_per_sec = n_total * args.steps / elapsed
+    if rank == 0:
+        out = {
+            "metric": "NMF replicates/sec (K=10, n_iter=100)",
+            "value": round(reps_per_sec, 3),
+            "unit": "replicates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(reps_per_sec / BASELINE_REPS_PER_SEC, 2),
+            "dtype": "fp32",
+            "data": "synthetic (planted-program Poisson counts, unit-variance genes; random-init W,H)",
+            "config": {
+                "model": f"cNMF factorize: online MU frobenius, K={args.k}",
+                "global_batch": n_total,
+                "seq_len": None,
+                "cells": args.cells,
+                "genes": args.genes,
+                "n_iter_per_gpu": args.n_iter,
+                "parallelism": f"replicate-parallel x{world}",
+                "device": "cpu" if not use_cuda else torch.cuda.get_device_name(dev),
+                "mean_passes": round(float(np.mean(passes)), 2) if passes else None,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

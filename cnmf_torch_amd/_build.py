@@ -1,0 +1,148 @@
+"""In-tree native build for cnmf_torch_amd.
+
+Builds two extension modules next to the Python sources so they travel with the
+repository snapshot to the GPU box:
+
+* ``cnmf_torch_amd/ops/_hip*.so`` -- every ``csrc/kernels/*.hip`` kernel plus the
+  pybind11 bindings, compiled by ``hipcc --offload-arch=gfx950`` (CDNA4 only).
+* ``cnmf_torch_amd/utils/_h5io*.so`` -- the native HDF5 layer used for h5ad I/O,
+  compiled by the host C++ compiler against libhdf5.
+
+Object files are cached under ``build/native`` and rebuilt when a source or any
+header is newer.  Usage: ``python -m cnmf_torch_amd._build [--force] [-j N]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+BUILD = os.path.join(ROOT, "build", "native")
+PKG = os.path.join(ROOT, "cnmf_torch_amd")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+ARCH = os.environ.get("CNMF_OFFLOAD_ARCH", "gfx950")
+
+HIP_OUT = os.path.join(PKG, "ops", "_hip" + EXT)
+H5_OUT = os.path.join(PKG, "utils", "_h5io" + EXT)
+
+HDF5_PREFIXES = [os.environ.get("CNMF_HDF5_PREFIX", ""), "/opt/conda", "/usr", "/usr/local"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC)")
+
+
+def _py_includes() -> list[str]:
+    import pybind11
+
+    return ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"]]
+
+
+def _headers() -> list[str]:
+    return glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
+
+
+def _stale(out: str, deps: list[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("command failed:\n  " + " ".join(cmd) + "\n" + r.stdout)
+
+
+def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
+    hipcc = _hipcc()
+    os.makedirs(BUILD, exist_ok=True)
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    srcs.append(os.path.join(CSRC, "bindings.cpp"))
+    hdrs = _headers()
+    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + CSRC,
+              "-Wno-unused-result", "-munsafe-fp-atomics"]
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(BUILD, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + hdrs):
+            extra = _py_includes() if s.endswith(".cpp") else []
+            todo.append([hipcc, "-c", s, "-o", o] + common + extra)
+    if todo:
+        if verbose:
+            print(f"[cnmf build] compiling {len(todo)} HIP/C++ unit(s) for {ARCH}", flush=True)
+        with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+            for f in [ex.submit(_run, c) for c in todo]:
+                f.result()
+    if force or todo or _stale(HIP_OUT, objs):
+        tmp = HIP_OUT + ".tmp"
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)
+        os.replace(tmp, HIP_OUT)
+        if verbose:
+            print(f"[cnmf build] linked {os.path.relpath(HIP_OUT, ROOT)}", flush=True)
+    return HIP_OUT
+
+
+def _hdf5_prefix() -> str:
+    for p in HDF5_PREFIXES:
+        if p and os.path.exists(os.path.join(p, "include", "hdf5.h")) and glob.glob(
+                os.path.join(p, "lib", "libhdf5.so*")):
+            return p
+    raise RuntimeError("libhdf5 headers/libs not found (set CNMF_HDF5_PREFIX)")
+
+
+def build_h5(force: bool = False, verbose: bool = True) -> str:
+    src = os.path.join(CSRC, "h5ad", "h5io.cpp")
+    if not (force or _stale(H5_OUT, [src])):
+        return H5_OUT
+    prefix = _hdf5_prefix()
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    tmp = H5_OUT + ".tmp"
+    cmd = [cxx, "-O2", "-shared", "-fPIC", "-std=c++17", src, "-o", tmp,
+           "-I" + os.path.join(prefix, "include")] + _py_includes() + [
+           "-L" + os.path.join(prefix, "lib"), "-lhdf5",
+           "-Wl,-rpath," + os.path.join(prefix, "lib")]
+    if verbose:
+        print(f"[cnmf build] compiling native h5ad layer against {prefix}", flush=True)
+    _run(cmd)
+    os.replace(tmp, H5_OUT)
+    return H5_OUT
+
+
+def build_all(force: bool = False, jobs: int = 8, verbose: bool = True) -> list[str]:
+    with cf.ThreadPoolExecutor(max_workers=2) as ex:
+        fh = ex.submit(build_hip, force, jobs, verbose)
+        f5 = ex.submit(build_h5, force, verbose)
+        return [fh.result(), f5.result()]
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--only", choices=["hip", "h5"], default=None)
+    a = ap.parse_args(argv)
+    if a.only == "hip":
+        print(build_hip(a.force, a.jobs))
+    elif a.only == "h5":
+        print(build_h5(a.force))
+    else:
+        for p in build_all(a.force, a.jobs):
+            print(p)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

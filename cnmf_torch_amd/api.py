@@ -1,0 +1,626 @@
+"""The ``cNMF`` pipeline object (L5 API; cnmf.py:390-1384).
+
+Same constructor, stage methods, arguments, artifact names and on-disk layout as the
+reference, on the MI355X-native engine:
+
+* ``factorize`` groups the worker's ledger rows by K and solves each group as ONE
+  replicate batch on the device (models/nmf.py) instead of one replicate at a time,
+  still writing one ``spectra.k_%d.iter_%d.df.npz`` per replicate (atomic writes).
+* ``refit_usage`` / ``refit_spectra`` use the fused on-device refit (models/refit.py).
+* ``consensus`` runs the pairwise distances, density filter, medians and silhouette on
+  the device; KMeans uses sklearn's exact algorithm by default
+  (``kmeans_backend='device'`` runs it on the GPU instead).
+* multi-worker / multi-GPU: ``factorize(worker_i, total_workers)`` keeps the
+  round-robin ledger sharding of cnmf.py:53-54 (CLI ``--worker-index`` restored);
+  ``cnmf_torch_amd.parallel`` launches one rank per GPU over torch.distributed.
+"""
+from __future__ import annotations
+
+import datetime
+import errno
+import itertools
+import json
+import os
+import shutil
+import time
+import uuid
+import warnings
+
+import numpy as np
+import pandas as pd
+import scipy.sparse as sp
+import torch
+
+from .models.consensus import (cluster_medians, kmeans, l2_normalize_rows, local_density,
+                               pairwise_distances, silhouette)
+from .models.hvg import compute_tpm, get_highvar_genes, get_highvar_genes_sparse, get_mean_var
+from .models.nmf import NMFBatchSolver, NMFOptions
+from .models.ols import efficient_ols_all_cols
+from .models.pp import scale as pp_scale
+from .models.refit import fit_H_online, fit_spectra_online
+from .parallel.ledger import worker_filter
+from .utils.anndata_lite import AnnData
+from .utils.h5ad import read_h5ad, write_h5ad
+from .utils.io import (check_dir_exists, dump_yaml, load_df_from_npz, load_yaml, read_10x_mtx,
+                       read_any, read_counts_table, save_df_to_npz, save_df_to_text,
+                       write_text_atomic)
+from .utils.timing import StageTimer, append_jsonl
+
+_PATHS = {
+    "normalized_counts": ("tmp", "{name}.norm_counts.h5ad"),
+    "nmf_replicate_parameters": ("tmp", "{name}.nmf_params.df.npz"),
+    "nmf_run_parameters": ("tmp", "{name}.nmf_idvrun_params.yaml"),
+    "nmf_genes_list": ("top", "{name}.overdispersed_genes.txt"),
+    "tpm": ("tmp", "{name}.tpm.h5ad"),
+    "tpm_stats": ("tmp", "{name}.tpm_stats.df.npz"),
+    "iter_spectra": ("tmp", "{name}.spectra.k_%d.iter_%d.df.npz"),
+    "iter_usages": ("tmp", "{name}.usages.k_%d.iter_%d.df.npz"),
+    "merged_spectra": ("tmp", "{name}.spectra.k_%d.merged.df.npz"),
+    "local_density_cache": ("tmp", "{name}.local_density_cache.k_%d.merged.df.npz"),
+    "consensus_spectra": ("tmp", "{name}.spectra.k_%d.dt_%s.consensus.df.npz"),
+    "consensus_spectra__txt": ("top", "{name}.spectra.k_%d.dt_%s.consensus.txt"),
+    "consensus_usages": ("tmp", "{name}.usages.k_%d.dt_%s.consensus.df.npz"),
+    "consensus_usages__txt": ("top", "{name}.usages.k_%d.dt_%s.consensus.txt"),
+    "consensus_stats": ("tmp", "{name}.stats.k_%d.dt_%s.df.npz"),
+    "clustering_plot": ("top", "{name}.clustering.k_%d.dt_%s.png"),
+    "gene_spectra_score": ("tmp", "{name}.gene_spectra_score.k_%d.dt_%s.df.npz"),
+    "gene_spectra_score__txt": ("top", "{name}.gene_spectra_score.k_%d.dt_%s.txt"),
+    "gene_spectra_tpm": ("tmp", "{name}.gene_spectra_tpm.k_%d.dt_%s.df.npz"),
+    "gene_spectra_tpm__txt": ("top", "{name}.gene_spectra_tpm.k_%d.dt_%s.txt"),
+    "starcat_spectra": ("tmp", "{name}.starcat_spectra.k_%d.dt_%s.df.npz"),
+    "starcat_spectra__txt": ("top", "{name}.starcat_spectra.k_%d.dt_%s.txt"),
+    "k_selection_plot": ("top", "{name}.k_selection.png"),
+    "k_selection_stats": ("top", "{name}.k_selection_stats.df.npz"),
+    # additions (not in the reference): per-replicate solver records
+    "replicate_log": ("tmp", "{name}.replicates.jsonl"),
+}
+
+# nmf-torch run_nmf defaults that the reference leaves implicit
+_SOLVER_DEFAULTS = dict(fp_precision="float", online_max_pass=20, online_h_tol=0.05,
+                        online_w_tol=0.05, batch_max_iter=500, batch_hals_tol=0.05,
+                        batch_hals_max_iter=200)
+
+
+def _dt_str(density_threshold) -> str:
+    return str(density_threshold).replace(".", "_")
+
+
+def _device(use_gpu: bool, device=None) -> torch.device:
+    if device is not None:
+        return torch.device(device)
+    if use_gpu and torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _dense32(X) -> np.ndarray:
+    if sp.issparse(X):
+        return X.astype(np.float32).toarray()
+    return np.asarray(X, dtype=np.float32)
+
+
+class cNMF:
+    """Consensus NMF pipeline (cnmf.py:390)."""
+
+    def __init__(self, output_dir: str = ".", name: str | None = None):
+        self.output_dir = output_dir
+        if name is None:
+            now = datetime.datetime.now()
+            name = "%s_%s" % (now.strftime("%Y_%m_%d"), uuid.uuid4().hex[:6])
+        self.name = name
+        self.paths = None
+        self.timer = StageTimer()
+        self._initialize_dirs()
+
+    # ------------------------------------------------------------------ paths
+    def _initialize_dirs(self):
+        if self.paths is not None:
+            return
+        top = os.path.join(self.output_dir, self.name)
+        tmp = os.path.join(top, "cnmf_tmp")
+        check_dir_exists(self.output_dir)
+        check_dir_exists(top)
+        check_dir_exists(tmp)
+        self.paths = {k: os.path.join(tmp if where == "tmp" else top, pat.format(name=self.name))
+                      for k, (where, pat) in _PATHS.items()}
+
+    # ------------------------------------------------------------------ prepare
+    def prepare(self, counts_fn, components, n_iter=100, densify=False, tpm_fn=None, seed=None,
+                beta_loss="frobenius", num_highvar_genes=2000, genes_file=None, alpha_usage=0.0,
+                alpha_spectra=0.0, init="random", total_workers=-1, use_gpu=False,
+                batch_size=5000, max_NMF_iter=1000, algo="mu", mode="online"):
+        """Load counts, select over-dispersed genes, variance-normalise, write the
+        replicate ledger (cnmf.py:458-596).  ``algo``/``mode`` are additions (defaults =
+        the reference's hard-coded 'mu'/'online')."""
+        with self.timer("prepare"):
+            input_counts = read_any(counts_fn, densify)
+            if sp.issparse(input_counts.X) and densify:
+                input_counts.X = np.array(input_counts.X.todense())
+
+            if tpm_fn is None:
+                tpm = compute_tpm(input_counts)
+                write_h5ad(self.paths["tpm"], tpm)
+            elif tpm_fn.endswith(".mtx") or tpm_fn.endswith(".mtx.gz"):
+                tpm = read_10x_mtx(os.path.dirname(tpm_fn))
+                write_h5ad(self.paths["tpm"], tpm)
+            elif tpm_fn.endswith(".h5ad"):
+                shutil.copyfile(tpm_fn, self.paths["tpm"])
+                tpm = read_h5ad(self.paths["tpm"])
+            else:
+                tpm = read_counts_table(tpm_fn, densify)
+                write_h5ad(self.paths["tpm"], tpm)
+
+            if sp.issparse(tpm.X):
+                gene_tpm_mean, gene_tpm_var = get_mean_var(tpm.X)
+                gene_tpm_std = gene_tpm_var ** 0.5
+            else:
+                gene_tpm_mean = np.array(tpm.X.mean(axis=0)).reshape(-1)
+                gene_tpm_std = np.array(tpm.X.std(axis=0, ddof=0)).reshape(-1)
+            stats = pd.DataFrame([gene_tpm_mean, gene_tpm_std], index=["__mean", "__std"],
+                                 columns=tpm.var.index).T
+            save_df_to_npz(stats, self.paths["tpm_stats"])
+
+            highvargenes = None
+            if genes_file is not None:
+                with open(genes_file) as fh:
+                    highvargenes = fh.read().rstrip().split("\n")
+
+            norm_counts = self.get_norm_counts(input_counts, tpm,
+                                               num_highvar_genes=num_highvar_genes,
+                                               high_variance_genes_filter=highvargenes)
+            self.save_norm_counts(norm_counts)
+            replicate_params, run_params = self.get_nmf_iter_params(
+                ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
+                alpha_usage=alpha_usage, alpha_spectra=alpha_spectra, init=init,
+                total_workers=total_workers, use_gpu=use_gpu, batch_size=batch_size,
+                max_iter=max_NMF_iter, algo=algo, mode=mode)
+            self.save_nmf_iter_params(replicate_params, run_params)
+
+    def get_norm_counts(self, counts, tpm, high_variance_genes_filter=None,
+                        num_highvar_genes=None):
+        """HVG subset of the raw counts, genes scaled to unit variance (cnmf.py:624-693)."""
+        if high_variance_genes_filter is None:
+            if sp.issparse(tpm.X):
+                gstats, _ = get_highvar_genes_sparse(tpm.X, numgenes=num_highvar_genes)
+            else:
+                gstats, _ = get_highvar_genes(np.array(tpm.X), numgenes=num_highvar_genes)
+            high_variance_genes_filter = list(tpm.var.index[gstats.high_var.values])
+
+        norm_counts = counts[:, high_variance_genes_filter].copy()
+        norm_counts.X = norm_counts.X.astype(np.float64)
+        if sp.issparse(tpm.X):
+            norm_counts = pp_scale(norm_counts, zero_center=False)
+            if np.isnan(norm_counts.X.data).sum() > 0:
+                print("Warning NaNs in normalized counts matrix")
+        else:
+            X = norm_counts.X.toarray() if sp.issparse(norm_counts.X) else norm_counts.X
+            with np.errstate(divide="ignore", invalid="ignore"):
+                X = X / X.std(axis=0, ddof=1)
+            norm_counts.X = X
+            if np.isnan(norm_counts.X).sum().sum() > 0:
+                print("Warning NaNs in normalized counts matrix")
+
+        write_text_atomic(self.paths["nmf_genes_list"], "\n".join(high_variance_genes_filter))
+
+        zerocells = np.array(norm_counts.X.sum(axis=1) == 0).reshape(-1)
+        if zerocells.sum() > 0:
+            examples = norm_counts.obs.index[np.ravel(zerocells)]
+            raise Exception(
+                "Error: %d cells have zero counts of overdispersed genes. E.g. %s. Filter those "
+                "cells and re-run or adjust the number of overdispersed genes. Quitting!"
+                % (zerocells.sum(), ", ".join(examples[:4])))
+        return norm_counts
+
+    def save_norm_counts(self, norm_counts):
+        self._initialize_dirs()
+        write_h5ad(self.paths["normalized_counts"], norm_counts)
+
+    def get_nmf_iter_params(self, ks, n_iter=100, random_state_seed=None,
+                            beta_loss="frobenius", alpha_usage=0.0, alpha_spectra=0.0,
+                            init="random", total_workers=-1, use_gpu=False, batch_size=5000,
+                            max_iter=1000, algo="mu", mode="online"):
+        """Replicate ledger + solver kwargs (cnmf.py:701-777).  Seeds are numpy-legacy
+        exact: ``np.random.seed(seed); randint(1, 2**31-1, len(ks)*n_iter)``."""
+        if isinstance(ks, (int, np.integer)):
+            ks = [ks]
+        k_list = sorted(set(list(ks)))
+        n_runs = len(ks) * n_iter
+        np.random.seed(seed=random_state_seed)
+        nmf_seeds = np.random.randint(low=1, high=(2 ** 31) - 1, size=n_runs)
+        rows = []
+        for i, (k, r) in enumerate(itertools.product(k_list, range(n_iter))):
+            done = os.path.exists(self.paths["iter_spectra"] % (k, r))
+            rows.append([int(k), int(r), int(nmf_seeds[i]), bool(done)])
+        replicate_params = pd.DataFrame(rows, columns=["n_components", "iter", "nmf_seed",
+                                                       "completed"])
+        n_completed = int(replicate_params["completed"].sum())
+        if n_completed > 0:
+            warnings.warn(
+                f"{n_completed} runs already appear completed. If this is unexpected, consider "
+                "re-initializing the cnmf object with a different run name or output directory",
+                UserWarning)
+        kwargs = dict(alpha_W=alpha_spectra, alpha_H=alpha_usage, l1_ratio_H=0.0,
+                      l1_ratio_W=0.0, beta_loss=beta_loss, algo=algo, tol=1e-4, mode=mode,
+                      online_chunk_max_iter=max_iter, online_chunk_size=batch_size, init=init,
+                      n_jobs=total_workers, use_gpu=use_gpu)
+        kwargs.update(_SOLVER_DEFAULTS)
+        return replicate_params, kwargs
+
+    def update_nmf_iter_params(self):
+        """Refresh the ``completed`` column from the files on disk (cnmf.py:780-795)."""
+        kwargs = load_yaml(self.paths["nmf_run_parameters"])
+        rp = load_df_from_npz(self.paths["nmf_replicate_parameters"])
+        rp["completed"] = [
+            os.path.exists(self.paths["iter_spectra"] % (int(k), int(i)))
+            for k, i in zip(rp["n_components"], rp["iter"])]
+        remaining = int((rp["completed"] == False).sum())  # noqa: E712
+        print("{n} NMF runs are currently incomplete".format(n=remaining))
+        self.save_nmf_iter_params(rp, kwargs)
+
+    def save_nmf_iter_params(self, replicate_params, run_params):
+        self._initialize_dirs()
+        save_df_to_npz(replicate_params, self.paths["nmf_replicate_parameters"])
+        dump_yaml(run_params, self.paths["nmf_run_parameters"])
+
+    # ------------------------------------------------------------------ factorize
+    def _solver_options(self, kwargs: dict, k: int) -> NMFOptions:
+        kw = dict(_SOLVER_DEFAULTS)
+        kw.update(kwargs)
+        return NMFOptions.from_kwargs(k, **kw)
+
+    def _nmf(self, X, nmf_kwargs):
+        """One replicate (cnmf.py:805-821): returns (spectra K x G, usages N x K)."""
+        k = int(nmf_kwargs["n_components"])
+        dev = _device(bool(nmf_kwargs.get("use_gpu", False)))
+        Xt = torch.from_numpy(_dense32(X)).to(dev)
+        res = NMFBatchSolver(Xt, self._solver_options(nmf_kwargs, k)).run(
+            [int(nmf_kwargs["random_state"])])
+        return res.spectra(0).cpu().numpy(), res.usages(0).cpu().numpy()
+
+    def factorize(self, worker_i=0, total_workers=1, skip_completed_runs=False, device=None,
+                  replicate_batch: int | None = None, save_usages: bool = False, verbose=True):
+        """Run this worker's share of the replicate ledger (cnmf.py:839-892).
+
+        Jobs with the same K are solved together in batches of ``replicate_batch``
+        replicates (default: all of them that fit the device memory budget)."""
+        with self.timer("factorize"):
+            run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
+            norm_counts = read_h5ad(self.paths["normalized_counts"])
+            kwargs = load_yaml(self.paths["nmf_run_parameters"])
+            if not skip_completed_runs:
+                jobs = list(worker_filter(range(len(run_params)), worker_i, total_workers))
+            else:
+                done = run_params["completed"].astype(bool).values
+                jobs = list(worker_filter(list(run_params.index[~done]), worker_i, total_workers))
+            if not jobs:
+                return
+            dev = _device(bool(kwargs.get("use_gpu", False)), device)
+            if dev.type == "cpu" and kwargs.get("n_jobs", -1) not in (None, -1):
+                torch.set_num_threads(max(1, int(kwargs["n_jobs"])))
+            X = torch.from_numpy(_dense32(norm_counts.X)).to(dev)
+            genes = norm_counts.var.index
+            cells = norm_counts.obs.index
+            fault_after = int(os.environ.get("CNMF_FAULT_AFTER_REPLICATES", "0") or 0)
+            written = 0
+            by_k: dict[int, list[int]] = {}
+            for idx in jobs:
+                by_k.setdefault(int(run_params.iloc[idx]["n_components"]), []).append(idx)
+            solvers: dict[int, NMFBatchSolver] = {}
+            for k, idxs in by_k.items():
+                bs = replicate_batch or self._auto_batch(X, k, len(idxs), dev)
+                if k not in solvers:
+                    solvers[k] = NMFBatchSolver(X, self._solver_options(kwargs, k))
+                for b0 in range(0, len(idxs), bs):
+                    grp = idxs[b0:b0 + bs]
+                    for idx in grp:
+                        if verbose:
+                            print("[Worker %d]. Starting task %d." % (worker_i, idx), flush=True)
+                    seeds = [int(run_params.iloc[i]["nmf_seed"]) for i in grp]
+                    t0 = time.perf_counter()
+                    res = solvers[k].run(seeds)
+                    W = res.W.cpu().numpy()
+                    wall = time.perf_counter() - t0
+                    for r, idx in enumerate(grp):
+                        it = int(run_params.iloc[idx]["iter"])
+                        spectra = pd.DataFrame(W[r * k:(r + 1) * k],
+                                               index=np.arange(1, k + 1), columns=genes)
+                        save_df_to_npz(spectra, self.paths["iter_spectra"] % (k, it))
+                        if save_usages:
+                            us = pd.DataFrame(res.usages(r).cpu().numpy(), index=cells,
+                                              columns=np.arange(1, k + 1))
+                            save_df_to_npz(us, self.paths["iter_usages"] % (k, it))
+                        append_jsonl(self.paths["replicate_log"], {
+                            "k": k, "iter": it, "seed": seeds[r], "worker": worker_i,
+                            "err": float(res.err[r]), "n_pass": int(res.n_iter[r]),
+                            "converged": bool(res.converged[r]),
+                            "h_inner_iters": int(res.stats["h_inner_iters"][r]),
+                            "w_inner_iters": int(res.stats["w_inner_iters"][r]),
+                            "batch_size": len(grp), "batch_wall_s": wall,
+                            "device": str(dev)})
+                        written += 1
+                        if fault_after and written >= fault_after:
+                            raise RuntimeError(
+                                f"CNMF_FAULT_AFTER_REPLICATES={fault_after}: injected failure")
+
+    @staticmethod
+    def _auto_batch(X: torch.Tensor, k: int, n_jobs: int, dev: torch.device) -> int:
+        """Largest replicate batch whose working set fits ~40% of free device memory."""
+        N, G = X.shape
+        per_rep = 4 * k * (N + 3 * G + 2 * min(N, 5000)) + 4 * k * k * 4
+        if dev.type == "cuda":
+            free, _ = torch.cuda.mem_get_info(dev)
+            budget = 0.4 * free
+        else:
+            budget = 8e9
+        return int(max(1, min(n_jobs, budget // max(per_rep, 1))))
+
+    # ------------------------------------------------------------------ combine
+    def combine(self, components=None, skip_missing_files=False):
+        if isinstance(components, (int, np.integer)):
+            ks = [int(components)]
+        elif components is None:
+            run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
+            ks = sorted(set(int(k) for k in run_params.n_components))
+        else:
+            ks = components
+        for k in ks:
+            self.combine_nmf(k, skip_missing_files=skip_missing_files)
+
+    def combine_nmf(self, k, skip_missing_files=False, remove_individual_iterations=False):
+        """Concatenate replicate spectra for one K (cnmf.py:895-920)."""
+        run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
+        print("Combining factorizations for k=%d." % k)
+        sub = run_params[run_params.n_components == k].sort_values("iter")
+        parts = []
+        for _, p in sub.iterrows():
+            fn = self.paths["iter_spectra"] % (int(p["n_components"]), int(p["iter"]))
+            if not os.path.exists(fn):
+                if not skip_missing_files:
+                    print("Missing file: %s, run with skip_missing=True to override" % fn)
+                    raise FileNotFoundError(errno.ENOENT, os.strerror(errno.ENOENT), fn)
+                print("Missing file: %s. Skipping." % fn)
+                continue
+            spectra = load_df_from_npz(fn)
+            spectra.index = ["iter%d_topic%d" % (int(p["iter"]), t + 1) for t in range(k)]
+            parts.append(spectra)
+        if parts:
+            combined = pd.concat(parts, axis=0)
+            save_df_to_npz(combined, self.paths["merged_spectra"] % k)
+            if remove_individual_iterations:
+                for _, p in sub.iterrows():
+                    fn = self.paths["iter_spectra"] % (int(p["n_components"]), int(p["iter"]))
+                    if os.path.exists(fn):
+                        os.remove(fn)
+            return combined
+        print("No spectra found for k=%d" % k)
+        return parts
+
+    # ------------------------------------------------------------------ refits
+    def _refit_kwargs(self):
+        return load_yaml(self.paths["nmf_run_parameters"])
+
+    def refit_usage(self, X, spectra, usage=None, device=None):
+        """Refit usages with spectra fixed (cnmf.py:923-976): online MU, h_tol 0.05."""
+        kw = self._refit_kwargs()
+        dev = _device(bool(kw.get("use_gpu", False)), device)
+        return fit_H_online(X, spectra, H_init=usage, chunk_size=kw["online_chunk_size"],
+                            chunk_max_iter=kw["online_chunk_max_iter"], h_tol=0.05,
+                            l1_reg_H=kw.get("l1_ratio_H", 0.0), l2_reg_H=0.0, epsilon=1e-16,
+                            device=dev)
+
+    def refit_spectra(self, X, usage, device=None):
+        """Refit spectra with usages fixed (cnmf.py:979-994)."""
+        kw = self._refit_kwargs()
+        dev = _device(bool(kw.get("use_gpu", False)), device)
+        u = usage.values if isinstance(usage, pd.DataFrame) else np.asarray(usage)
+        return fit_spectra_online(X, u, chunk_size=kw["online_chunk_size"],
+                                  chunk_max_iter=kw["online_chunk_max_iter"], h_tol=0.05,
+                                  l1_reg=kw.get("l1_ratio_H", 0.0), device=dev)
+
+    # ------------------------------------------------------------------ consensus
+    def consensus(self, k, density_threshold=0.5, local_neighborhood_size=0.30,
+                  show_clustering=True, build_ref=True, skip_density_and_return_after_stats=False,
+                  close_clustergram_fig=False, refit_usage=True, normalize_tpm_spectra=False,
+                  norm_counts=None, kmeans_backend="sklearn", device=None):
+        """Consensus spectra/usages for one K (cnmf.py:997-1256)."""
+        with self.timer(f"consensus_k{k}"):
+            return self._consensus(k, density_threshold, local_neighborhood_size, show_clustering,
+                                   build_ref, skip_density_and_return_after_stats,
+                                   close_clustergram_fig, refit_usage, normalize_tpm_spectra,
+                                   norm_counts, kmeans_backend, device)
+
+    def _consensus(self, k, density_threshold, local_neighborhood_size, show_clustering,
+                   build_ref, skip_stats, close_fig, refit_usage, normalize_tpm_spectra,
+                   norm_counts, kmeans_backend, device):
+        kw = self._refit_kwargs()
+        dev = _device(bool(kw.get("use_gpu", False)), device)
+        merged = load_df_from_npz(self.paths["merged_spectra"] % k)
+        if norm_counts is None:
+            norm_counts = read_h5ad(self.paths["normalized_counts"])
+        dt_str = "2" if skip_stats else str(density_threshold)
+        dt_repl = dt_str.replace(".", "_")
+        n_neighbors = int(local_neighborhood_size * merged.shape[0] / k)
+
+        S = torch.as_tensor(merged.values, dtype=torch.float64, device=dev)
+        L2 = l2_normalize_rows(S)
+        names = merged.index
+        topics_dist = None
+        density_filter = None
+        local_dens = None
+        if not skip_stats:
+            cache = self.paths["local_density_cache"] % k
+            local_dens = self._load_density_cache(cache, n_neighbors, names)
+            if local_dens is None:
+                topics_dist = pairwise_distances(L2)
+                dens = local_density(topics_dist, n_neighbors).cpu().numpy()
+                local_dens = pd.DataFrame(dens, columns=["local_density"], index=names)
+                save_df_to_npz(local_dens, cache)
+                write_text_atomic(cache + ".meta.json", json.dumps(
+                    {"n_neighbors": n_neighbors, "n_spectra": int(len(names))}))
+            density_filter = (local_dens.iloc[:, 0] < density_threshold).values
+            keep = torch.as_tensor(np.flatnonzero(density_filter), device=dev)
+            L2 = L2.index_select(0, keep)
+            names = names[density_filter]
+            if L2.shape[0] == 0:
+                raise RuntimeError("Zero components remain after density filtering. Consider "
+                                   "increasing density threshold")
+        labels = kmeans(L2, k, n_init=10, random_state=1, backend=kmeans_backend) + 1
+        label_series = pd.Series(labels, index=names)
+        median_np = cluster_medians(L2, labels, sorted(set(labels))).cpu().numpy()
+        median_spectra = pd.DataFrame(median_np, index=sorted(set(labels)), columns=merged.columns)
+
+        rf_usages = self.refit_usage(norm_counts.X, median_spectra, device=dev)
+        rf_usages = pd.DataFrame(rf_usages, index=norm_counts.obs.index, columns=median_spectra.index)
+
+        if skip_stats:
+            d = pairwise_distances(L2)
+            sil = silhouette(d, labels)
+            err = self._prediction_error(norm_counts.X, rf_usages.values, median_spectra.values, dev)
+            return pd.DataFrame([k, density_threshold, sil, err],
+                                index=["k", "local_density_threshold", "silhouette",
+                                       "prediction_error"], columns=["stats"])
+
+        norm_usages = rf_usages.div(rf_usages.sum(axis=1), axis=0)
+        reorder = norm_usages.sum(axis=0).sort_values(ascending=False)
+        rf_usages = rf_usages.loc[:, reorder.index]
+        norm_usages = norm_usages.loc[:, reorder.index]
+        median_spectra = median_spectra.loc[reorder.index, :]
+        new_cols = np.arange(1, rf_usages.shape[1] + 1)
+        rf_usages.columns = new_cols
+        norm_usages.columns = new_cols
+        median_spectra.index = new_cols
+
+        tpm = read_h5ad(self.paths["tpm"])
+        tpm_stats = load_df_from_npz(self.paths["tpm_stats"])
+        spectra_tpm = self.refit_spectra(tpm.X, norm_usages.astype(tpm.X.dtype), device=dev)
+        spectra_tpm = pd.DataFrame(spectra_tpm, index=new_cols, columns=tpm.var.index)
+        if normalize_tpm_spectra:
+            spectra_tpm = spectra_tpm.div(spectra_tpm.sum(axis=1), axis=0) * 1e6
+
+        usage_coef = efficient_ols_all_cols(rf_usages.values, tpm.X, normalize_y=True, device=dev)
+        usage_coef = pd.DataFrame(usage_coef, index=new_cols, columns=tpm.var.index)
+
+        if refit_usage:
+            with open(self.paths["nmf_genes_list"]) as fh:
+                hvgs = fh.read().split("\n")
+            norm_tpm = tpm[:, hvgs]
+            if sp.issparse(norm_tpm.X):
+                norm_tpm = pp_scale(norm_tpm, zero_center=False)
+            else:
+                norm_tpm.X = norm_tpm.X / norm_tpm.X.std(axis=0, ddof=1)
+            spectra_tpm_rf = spectra_tpm.loc[:, hvgs]
+            spectra_tpm_rf = spectra_tpm_rf.div(tpm_stats.loc[hvgs, "__std"], axis=1)
+            rf = self.refit_usage(norm_tpm.X, spectra_tpm_rf.astype(norm_tpm.X.dtype), device=dev)
+            rf_usages = pd.DataFrame(rf, index=norm_counts.obs.index, columns=spectra_tpm_rf.index)
+
+        p = self.paths
+        save_df_to_npz(median_spectra, p["consensus_spectra"] % (k, dt_repl))
+        save_df_to_npz(rf_usages, p["consensus_usages"] % (k, dt_repl))
+        save_df_to_text(median_spectra, p["consensus_spectra__txt"] % (k, dt_repl))
+        save_df_to_text(rf_usages, p["consensus_usages__txt"] % (k, dt_repl))
+        save_df_to_npz(spectra_tpm, p["gene_spectra_tpm"] % (k, dt_repl))
+        save_df_to_text(spectra_tpm, p["gene_spectra_tpm__txt"] % (k, dt_repl))
+        save_df_to_npz(usage_coef, p["gene_spectra_score"] % (k, dt_repl))
+        save_df_to_text(usage_coef, p["gene_spectra_score__txt"] % (k, dt_repl))
+
+        if show_clustering:
+            from .utils.plotting import clustergram
+
+            if topics_dist is None:
+                topics_dist = pairwise_distances(L2)
+            else:
+                keep = torch.as_tensor(np.flatnonzero(density_filter), device=topics_dist.device)
+                topics_dist = topics_dist.index_select(0, keep).index_select(1, keep)
+            clustergram(topics_dist.cpu().numpy(), label_series, local_dens, density_filter,
+                        density_threshold, p["clustering_plot"] % (k, dt_repl), close=close_fig)
+        if build_ref:
+            self.build_reference(k, density_threshold)
+
+    def _load_density_cache(self, cache: str, n_neighbors: int, names):
+        """Density cache keyed on K AND the neighbourhood (SURVEY.md §5.2 fix): a cache
+        written with a different n_neighbors or spectra set is recomputed."""
+        if not os.path.isfile(cache):
+            return None
+        meta_fn = cache + ".meta.json"
+        if os.path.isfile(meta_fn):
+            with open(meta_fn) as fh:
+                meta = json.load(fh)
+            if meta.get("n_neighbors") != n_neighbors or meta.get("n_spectra") != len(names):
+                return None
+        df = load_df_from_npz(cache)
+        if len(df) != len(names):
+            return None
+        return df
+
+    @staticmethod
+    def _prediction_error(X, usages: np.ndarray, spectra: np.ndarray, dev) -> float:
+        """||X - U S||_F^2 via the trace identity, streamed (never materialises U S)."""
+        U = torch.as_tensor(usages, dtype=torch.float64, device=dev)
+        S = torch.as_tensor(spectra, dtype=torch.float64, device=dev)
+        n = X.shape[0]
+        x_sq = 0.0
+        cross = 0.0
+        for a in range(0, n, 16384):
+            b = min(n, a + 16384)
+            blk = X[a:b]
+            blk = blk.toarray() if sp.issparse(blk) else np.asarray(blk)
+            xb = torch.as_tensor(blk, dtype=torch.float64, device=dev)
+            x_sq += float((xb * xb).sum())
+            cross += float(((U[a:b].t() @ xb) * S).sum())
+        quad = float(((U.t() @ U) * (S @ S.t())).sum())
+        return x_sq - 2.0 * cross + quad
+
+    # ------------------------------------------------------------------ reference / k-sel
+    def build_reference(self, k, density_threshold=0.5, target_sum=1e6):
+        """starCAT reference spectra (cnmf.py:1259-1290)."""
+        dt = _dt_str(density_threshold)
+        spectra_tpm = pd.read_csv(self.paths["gene_spectra_tpm__txt"] % (k, dt), index_col=0,
+                                  sep="\t")
+        with open(self.paths["nmf_genes_list"]) as fh:
+            hvgs = fh.read().split("\n")
+        tpm_stats = load_df_from_npz(self.paths["tpm_stats"])
+        tpm_stats.index = spectra_tpm.columns
+        renorm = spectra_tpm.div(spectra_tpm.sum(axis=1), axis=0) * target_sum
+        varnorm = renorm.div(tpm_stats["__std"])
+        ref = varnorm[hvgs].copy()
+        ref.index = "GEP" + ref.index.astype("str")
+        save_df_to_npz(ref, self.paths["starcat_spectra"] % (k, dt))
+        save_df_to_text(ref, self.paths["starcat_spectra__txt"] % (k, dt))
+
+    def k_selection_plot(self, close_fig=False, kmeans_backend="sklearn"):
+        """Stability (silhouette) and error per K (cnmf.py:1293-1332)."""
+        run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
+        norm_counts = read_h5ad(self.paths["normalized_counts"])
+        stats = []
+        for k in sorted(set(int(x) for x in run_params.n_components)):
+            stats.append(self.consensus(k, skip_density_and_return_after_stats=True,
+                                        show_clustering=False, close_clustergram_fig=True,
+                                        norm_counts=norm_counts,
+                                        kmeans_backend=kmeans_backend).stats)
+        stats = pd.DataFrame(stats).reset_index(drop=True)
+        save_df_to_npz(stats, self.paths["k_selection_stats"])
+        from .utils.plotting import k_selection
+
+        k_selection(stats, self.paths["k_selection_plot"], close=close_fig)
+        return stats
+
+    def load_results(self, K, density_threshold, n_top_genes=100, norm_usage=True):
+        """(usage, spectra_scores, spectra_tpm, top_genes) (cnmf.py:1335-1384)."""
+        dt = _dt_str(density_threshold)
+        spectra_scores = pd.read_csv(self.paths["gene_spectra_score__txt"] % (K, dt), sep="\t",
+                                     index_col=0).T
+        spectra_tpm = pd.read_csv(self.paths["gene_spectra_tpm__txt"] % (K, dt), sep="\t",
+                                  index_col=0).T
+        usage = pd.read_csv(self.paths["consensus_usages__txt"] % (K, dt), sep="\t", index_col=0)
+        if norm_usage:
+            usage = usage.div(usage.sum(axis=1), axis=0)
+        try:
+            usage.columns = [int(x) for x in usage.columns]
+        except ValueError:
+            print("Usage matrix columns include non integer values")
+        top_genes = []
+        for gep in spectra_scores.columns:
+            top_genes.append(list(spectra_scores.sort_values(by=gep, ascending=False)
+                                  .index[:n_top_genes]))
+        top_genes = pd.DataFrame(top_genes, index=spectra_scores.columns).T
+        return usage, spectra_scores, spectra_tpm, top_genes

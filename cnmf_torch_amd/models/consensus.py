@@ -1,0 +1,155 @@
+"""Consensus-step algorithms (C24, cnmf.py:1053-1110).
+
+All run on the device of their input tensor (HIP GPU or CPU):
+
+* ``l2_normalize_rows``       -- H1, rows scaled to unit L2 norm (cnmf.py:1056)
+* ``pairwise_distances``      -- H2, ||a||^2 + ||b||^2 - 2 a.b^T on the matrix cores
+* ``local_density``           -- H3, mean distance to the n_neighbors nearest (self
+                                 included in the n+1 smallest, divided by n; cnmf.py:1067-1070)
+* ``kmeans``                  -- H4, k-means++ init + Lloyd, ``n_init`` restarts batched,
+                                 best inertia (sklearn semantics).  ``backend='sklearn'``
+                                 reproduces ``KMeans(n_clusters=k, n_init=10, random_state=1)``
+                                 of cnmf.py:1082 exactly (CPU); ``'device'`` runs on the GPU.
+* ``cluster_medians``         -- H5, per-cluster per-gene median, rows renormalised to 1
+* ``silhouette``              -- H6, from the same distance matrix
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+
+def l2_normalize_rows(S: torch.Tensor) -> torch.Tensor:
+    return S / torch.sqrt((S * S).sum(dim=1, keepdim=True))
+
+
+def pairwise_distances(A: torch.Tensor, B: torch.Tensor | None = None) -> torch.Tensor:
+    """Euclidean distances (float64 accumulation of the norms; sklearn semantics:
+    clipped at 0, exact zeros on the diagonal when B is A)."""
+    same = B is None
+    B = A if same else B
+    Ad, Bd = A.to(torch.float64), B.to(torch.float64)
+    aa = (Ad * Ad).sum(dim=1, keepdim=True)
+    bb = (Bd * Bd).sum(dim=1, keepdim=True).t()
+    d2 = aa + bb - 2.0 * (Ad @ Bd.t())
+    d2.clamp_(min=0.0)
+    if same:
+        d2.fill_diagonal_(0.0)
+    return torch.sqrt(d2)
+
+
+def local_density(dist: torch.Tensor, n_neighbors: int) -> torch.Tensor:
+    """Mean distance to the ``n_neighbors`` nearest neighbours (cnmf.py:1065-1070):
+    sum of the (n_neighbors+1) smallest distances of each row (self included) / n_neighbors."""
+    k = min(n_neighbors + 1, dist.shape[1])
+    vals = torch.topk(dist, k, dim=1, largest=False).values
+    return vals.sum(dim=1) / max(n_neighbors, 1) if n_neighbors > 0 else vals.sum(dim=1) * float("inf")
+
+
+# ------------------------------------------------------------------------- k-means
+def _kmeanspp(X: torch.Tensor, k: int, gen: torch.Generator, x_sq: torch.Tensor) -> torch.Tensor:
+    """Greedy k-means++ (sklearn _kmeans_plusplus, n_local_trials = 2 + log k)."""
+    n = X.shape[0]
+    trials = 2 + int(math.log(k))
+    centers = torch.empty((k, X.shape[1]), dtype=X.dtype, device=X.device)
+    first = int(torch.randint(n, (1,), generator=gen).item())
+    centers[0] = X[first]
+    closest = ((X - X[first]) ** 2).sum(dim=1)
+    pot = float(closest.sum())
+    for c in range(1, k):
+        r = torch.rand(trials, generator=gen, dtype=torch.float64) * pot
+        cum = torch.cumsum(closest.double(), 0).cpu()
+        cand = torch.searchsorted(cum, r).clamp(max=n - 1).to(X.device)
+        d = x_sq[:, None] + x_sq[cand][None, :] - 2 * X @ X[cand].t()
+        d.clamp_(min=0)
+        newc = torch.minimum(closest[:, None], d)
+        pots = newc.sum(dim=0)
+        best = int(torch.argmin(pots))
+        centers[c] = X[cand[best]]
+        closest = newc[:, best]
+        pot = float(pots[best])
+    return centers
+
+
+def _lloyd(X, centers, x_sq, max_iter: int, tol: float):
+    inertia = None
+    labels = None
+    for _ in range(max_iter):
+        c_sq = (centers * centers).sum(dim=1)
+        d = x_sq[:, None] + c_sq[None, :] - 2 * X @ centers.t()
+        labels = torch.argmin(d, dim=1)
+        k = centers.shape[0]
+        counts = torch.bincount(labels, minlength=k).to(X.dtype)
+        sums = torch.zeros_like(centers).index_add_(0, labels, X)
+        newc = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], centers)
+        shift = float(((newc - centers) ** 2).sum())
+        centers = newc
+        if shift <= tol:
+            break
+    c_sq = (centers * centers).sum(dim=1)
+    d = x_sq[:, None] + c_sq[None, :] - 2 * X @ centers.t()
+    labels = torch.argmin(d, dim=1)
+    inertia = float(torch.gather(d, 1, labels[:, None]).clamp(min=0).sum())
+    return labels, centers, inertia
+
+
+def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 300,
+           tol: float = 1e-4, backend: str = "sklearn"):
+    """Returns integer labels 0..k-1 (numpy)."""
+    if backend == "sklearn":
+        from sklearn.cluster import KMeans
+
+        Xn = X.detach().cpu().numpy() if isinstance(X, torch.Tensor) else np.asarray(X)
+        m = KMeans(n_clusters=k, n_init=n_init, random_state=random_state)
+        m.fit(Xn)
+        return m.labels_
+    Xt = X if isinstance(X, torch.Tensor) else torch.as_tensor(np.asarray(X))
+    Xt = Xt.to(torch.float64)
+    # sklearn scales tol by the mean feature variance
+    tol_abs = tol * float(Xt.var(dim=0, unbiased=False).mean())
+    x_sq = (Xt * Xt).sum(dim=1)
+    gen = torch.Generator(device="cpu").manual_seed(int(random_state))
+    best = None
+    for _ in range(n_init):
+        c0 = _kmeanspp(Xt, k, gen, x_sq)
+        labels, centers, inertia = _lloyd(Xt, c0, x_sq, max_iter, tol_abs)
+        if best is None or inertia < best[0]:
+            best = (inertia, labels)
+    return best[1].cpu().numpy()
+
+
+def cluster_medians(S: torch.Tensor, labels: np.ndarray, k_labels) -> torch.Tensor:
+    """Per-cluster per-gene median (pandas groupby().median() semantics: mean of the two
+    middle values for even counts), rows renormalised to sum 1 (cnmf.py:1087-1090)."""
+    out = []
+    lab = torch.as_tensor(np.asarray(labels), device=S.device)
+    for cl in k_labels:
+        rows = S[lab == cl]
+        srt = torch.sort(rows, dim=0).values
+        m = rows.shape[0]
+        med = srt[m // 2] if m % 2 else 0.5 * (srt[m // 2 - 1] + srt[m // 2])
+        out.append(med)
+    med = torch.stack(out)
+    return med / med.sum(dim=1, keepdim=True)
+
+
+def silhouette(dist: torch.Tensor, labels: np.ndarray) -> float:
+    """Mean silhouette coefficient from a precomputed distance matrix (sklearn semantics:
+    singleton clusters score 0)."""
+    lab = torch.as_tensor(np.asarray(labels), device=dist.device)
+    uniq = torch.unique(lab)
+    onehot = (lab[:, None] == uniq[None, :]).to(dist.dtype)       # n x c
+    sums = dist @ onehot                                           # n x c
+    counts = onehot.sum(dim=0)
+    own = (onehot * torch.arange(len(uniq), device=dist.device)[None, :]).sum(dim=1).long()
+    own_cnt = counts[own]
+    a = sums[torch.arange(len(lab)), own] / torch.clamp(own_cnt - 1, min=1)
+    other = sums / counts[None, :]
+    other[torch.arange(len(lab)), own] = float("inf")
+    b = other.min(dim=1).values
+    s = (b - a) / torch.maximum(a, b)
+    s = torch.where(own_cnt > 1, s, torch.zeros_like(s))
+    s = torch.nan_to_num(s, nan=0.0)
+    return float(s.mean())

@@ -1,0 +1,79 @@
+"""Gene statistics, over-dispersed gene selection and TPM (C6-C9; cnmf.py:128-247).
+
+Semantics follow the reference exactly: column mean / variance with ddof=0
+(``StandardScaler(with_mean=False)``, cnmf.py:128-131), the Fano-factor model with
+A = min CV of the 20 highest-mean genes and B^2 = median Fano inside the 10-90 %
+winsor box (cnmf.py:143-156), selection of the top ``numgenes`` by Fano ratio or, with
+``numgenes=None``, by threshold ``T = 1 + std(winsorised Fano)`` and mean > 0.5
+(cnmf.py:160-171).  The per-gene vectors are small, so ranking uses pandas for
+identical tie-breaking; the column statistics over the (cells x genes) matrix run on
+the GPU for device tensors (one pass, float64 accumulation).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+import scipy.sparse as sp
+import torch
+
+
+def get_mean_var(X):
+    """Column mean and ddof=0 variance of a dense/sparse/torch matrix (cnmf.py:128-131)."""
+    if isinstance(X, torch.Tensor):
+        Xd = X.to(torch.float64)
+        mean = Xd.mean(dim=0)
+        var = (Xd * Xd).mean(dim=0) - mean * mean
+        return mean.cpu().numpy(), torch.clamp(var, min=0).cpu().numpy()
+    from sklearn.preprocessing import StandardScaler
+
+    sc = StandardScaler(with_mean=False)
+    sc.fit(X)
+    return sc.mean_, sc.var_
+
+
+def _fano_model(gene_mean: pd.Series, gene_var: pd.Series, expected_fano_threshold=None,
+                minimal_mean: float = 0.5, numgenes=None):
+    gene_fano = gene_var / gene_mean
+    # expected Fano line: A^2 * mean + B^2
+    top_by_mean = gene_mean.sort_values(ascending=False)[:20].index
+    A = (np.sqrt(gene_var) / gene_mean)[top_by_mean].min()
+    m_lo, m_hi = gene_mean.quantile([0.10, 0.90])
+    f_lo, f_hi = gene_fano.quantile([0.10, 0.90])
+    box = (gene_fano > f_lo) & (gene_fano < f_hi) & (gene_mean > m_lo) & (gene_mean < m_hi)
+    B = np.sqrt(gene_fano[box].median())
+    expected = (A ** 2) * gene_mean + B ** 2
+    ratio = gene_fano / expected
+    if numgenes is not None:
+        chosen = ratio.sort_values(ascending=False).index[:numgenes]
+        high_var = ratio.index.isin(chosen)
+        T = None
+    else:
+        T = (1.0 + gene_fano[box].std()) if not expected_fano_threshold else expected_fano_threshold
+        high_var = (ratio > T) & (gene_mean > minimal_mean)
+    stats = pd.DataFrame({"mean": gene_mean, "var": gene_var, "fano": gene_fano,
+                          "expected_fano": expected, "high_var": high_var, "fano_ratio": ratio})
+    params = {"A": A, "B": B, "T": T, "minimal_mean": minimal_mean}
+    return stats, params
+
+
+def get_highvar_genes_sparse(expression, expected_fano_threshold=None, minimal_mean=0.5,
+                             numgenes=None):
+    """Over-dispersed genes of a sparse (or torch) matrix (cnmf.py:133-184)."""
+    mean, var = get_mean_var(expression)
+    return _fano_model(pd.Series(mean), pd.Series(var), expected_fano_threshold, minimal_mean,
+                       numgenes)
+
+
+def get_highvar_genes(input_counts, expected_fano_threshold=None, minimal_mean=0.5, numgenes=None):
+    """Dense variant (cnmf.py:188-238): numpy mean / var(ddof=0)."""
+    X = np.asarray(input_counts)
+    mean = pd.Series(X.mean(axis=0).astype(float))
+    var = pd.Series(X.var(ddof=0, axis=0).astype(float))
+    return _fano_model(mean, var, expected_fano_threshold, minimal_mean, numgenes)
+
+
+def compute_tpm(input_counts):
+    """Per-cell scaling to 1e6 total (``sc.pp.normalize_total(target_sum=1e6)``, cnmf.py:241-247)."""
+    from .pp import normalize_total
+
+    return normalize_total(input_counts, target_sum=1e6, copy=True)

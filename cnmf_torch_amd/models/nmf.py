@@ -1,0 +1,740 @@
+"""Replicate-batched NMF engine (replaces nmf-torch ``run_nmf``).
+
+The reference factorises one replicate at a time (``cNMF._nmf`` -> ``run_nmf``,
+cnmf.py:805-821, serial loop cnmf.py:882-892).  Here a *batch* of R replicates that
+share X and K is solved together:
+
+* the data-side products are single fat GEMMs over the whole batch
+  (``W_all @ X_c^T`` is (R*K x G)(G x c), ``H_all^T @ X_c`` is (R*K x c)(c x G));
+* the per-replicate inner loops (H with W fixed, W with H fixed) are ONE launch of the
+  fused solve kernel for every replicate (csrc/kernels/solve.hip), converging on device;
+* the Frobenius loss comes for free from sufficient statistics (trace trick) in the
+  W-solve epilogue -- no extra pass over X;
+* replicates that have converged are compacted out of the batch so later passes only
+  pay for live ones; every replicate still runs exactly its own convergence history.
+
+Layouts: ``W`` is (R*K, G) row-major (replicate r = rows r*K..r*K+K-1) and the usages
+are kept TRANSPOSED, ``HT`` (R*K, N), so a replicate's chunk block is K rows of
+contiguous cells -- coalesced for the solve kernel and directly the GEMM operand.
+
+Algorithms (nmf-torch surface; cnmf.py:757-771 fixes algo='mu', mode='online'):
+  algo  in {'mu', 'hals'}       (HALS: Frobenius only)
+  mode  in {'online', 'batch'}
+  beta_loss in {'frobenius', 'kullback-leibler', 'itakura-saito'} or a float
+Online (Mairal-style sufficient statistics): per pass, chunks of ``online_chunk_size``
+rows; H-step on the chunk to ``online_h_tol`` (relative change over the chunk, as
+cnmf.py:375-378), accumulate A += h^T h, B += h^T x, then W-step to ``online_w_tol``.
+A pass ends with the loss; stop when (prev - cur) / init < tol or after
+``online_max_pass`` passes.  Chunks are taken in row order (deterministic and identical
+for every replicate of a batch -- required for batching; documented deviation from a
+shuffled order).  For beta != 2, the W-step accumulates the MU numerator/denominator
+with the current W and applies one multiplicative step per chunk.
+Batch: alternate one H-step and one W-step (HALS: inner loops to ``batch_hals_tol``),
+loss every ``loss_every`` iterations, stop as sklearn's MU solver does.
+
+Data parallel (cell-sharded) runs pass a communicator: the flat per-chunk ``[dB | dA]``
+increment is all-reduced once per online step, so W, the loss and every convergence
+decision are identical on all ranks while H rows stay rank-local.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field, asdict
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..parallel.comm import LocalComm
+from ..utils import rng
+
+BETA_LOSS = {"frobenius": 2.0, "kullback-leibler": 1.0, "itakura-saito": 0.0}
+
+
+def beta_value(beta_loss) -> float:
+    if isinstance(beta_loss, str):
+        if beta_loss not in BETA_LOSS:
+            raise ValueError(f"beta_loss must be one of {list(BETA_LOSS)} or a number, got {beta_loss!r}")
+        return BETA_LOSS[beta_loss]
+    return float(beta_loss)
+
+
+@dataclass
+class NMFOptions:
+    n_components: int
+    init: str = "random"
+    beta_loss: object = "frobenius"
+    algo: str = "mu"
+    mode: str = "online"
+    tol: float = 1e-4
+    alpha_W: float = 0.0        # spectra regularisation (nmf-torch W = cnmf spectra)
+    l1_ratio_W: float = 0.0
+    alpha_H: float = 0.0        # usage regularisation
+    l1_ratio_H: float = 0.0
+    fp_precision: str = "float"
+    batch_max_iter: int = 500
+    batch_hals_tol: float = 0.05
+    batch_hals_max_iter: int = 200
+    online_max_pass: int = 20
+    online_chunk_size: int = 5000
+    online_chunk_max_iter: int = 200
+    online_h_tol: float = 0.05
+    online_w_tol: float = 0.05
+    online_stats: str = "pass"  # "pass": A,B reset each pass (Mairal); "exact": A=H^T H, B=H^T X of current H
+    online_inner_conv: str = "loss"  # 'loss': block objective every inner_check_every steps; 'iterate'
+    inner_check_every: int = 10
+    loss_every: int = 10
+    eps: float = 1e-16
+
+    @classmethod
+    def from_kwargs(cls, n_components: int, **kw) -> "NMFOptions":
+        names = set(cls.__dataclass_fields__)
+        return cls(n_components=int(n_components), **{k: v for k, v in kw.items() if k in names})
+
+    def validate(self) -> None:
+        if self.algo not in ("mu", "hals"):
+            raise ValueError(f"algo must be 'mu' or 'hals', got {self.algo!r}")
+        if self.mode not in ("online", "batch"):
+            raise ValueError(f"mode must be 'online' or 'batch', got {self.mode!r}")
+        if self.algo == "hals" and beta_value(self.beta_loss) != 2.0:
+            raise ValueError("HALS is defined for the Frobenius loss only")
+        if self.init not in ("random", "nndsvd", "nndsvda", "nndsvdar"):
+            raise ValueError(f"unsupported init {self.init!r}")
+        if self.fp_precision not in ("float", "double"):
+            raise ValueError("fp_precision must be 'float' or 'double'")
+
+    @property
+    def dtype(self) -> torch.dtype:
+        return torch.float32 if self.fp_precision == "float" else torch.float64
+
+    @property
+    def l1_W(self):
+        return self.alpha_W * self.l1_ratio_W
+
+    @property
+    def l2_W(self):
+        return self.alpha_W * (1.0 - self.l1_ratio_W)
+
+    @property
+    def l1_H(self):
+        return self.alpha_H * self.l1_ratio_H
+
+    @property
+    def l2_H(self):
+        return self.alpha_H * (1.0 - self.l1_ratio_H)
+
+
+@dataclass
+class NMFResult:
+    """Batch result.  ``HT`` is (R*K, N_local) (usages transposed); ``W`` (R*K, G)."""
+
+    HT: torch.Tensor
+    W: torch.Tensor
+    err: np.ndarray
+    n_iter: np.ndarray
+    converged: np.ndarray
+    seeds: list
+    K: int
+    stats: dict = field(default_factory=dict)
+
+    def usages(self, r: int) -> torch.Tensor:
+        K = self.K
+        return self.HT[r * K:(r + 1) * K].t()
+
+    def spectra(self, r: int) -> torch.Tensor:
+        K = self.K
+        return self.W[r * K:(r + 1) * K]
+
+
+# =============================================================================== init
+def _global_mean(X: torch.Tensor, comm) -> float:
+    s = comm.allreduce_scalar(float(X.sum(dtype=torch.float64)))
+    n = comm.allreduce_scalar(float(X.numel()))
+    return s / max(n, 1.0)
+
+
+def _nndsvd(X: torch.Tensor, K: int, variant: str, comm, eps: float = 1e-6, seed: int = 0):
+    """sklearn's NNDSVD init (sklearn/decomposition/_nmf.py:316-366) via the Gram
+    eigendecomposition, so it works on a cell-sharded X (only G x G and norms are
+    all-reduced).  Returns (H (N_loc x K), W (K x G)) in X's dtype."""
+    Xd = X.to(torch.float64)
+    C = Xd.t() @ Xd
+    comm.allreduce_(C)
+    evals, evecs = torch.linalg.eigh(C)
+    order = torch.argsort(evals, descending=True)[:K]
+    S = torch.sqrt(torch.clamp(evals[order], min=0.0))
+    V = evecs[:, order].t()                       # K x G
+    U = (Xd @ V.t()) / torch.clamp(S, min=1e-300)  # N_loc x K
+    Wsk = torch.zeros_like(U)                     # sklearn W = usages
+    Hsk = torch.zeros_like(V)                     # sklearn H = spectra
+    Wsk[:, 0] = torch.sqrt(S[0]) * torch.abs(U[:, 0])
+    Hsk[0, :] = torch.sqrt(S[0]) * torch.abs(V[0, :])
+    for j in range(1, K):
+        x, y = U[:, j], V[j, :]
+        xp, yp = torch.clamp(x, min=0), torch.clamp(y, min=0)
+        xn, yn = torch.clamp(-x, min=0), torch.clamp(-y, min=0)
+        xpn = math.sqrt(comm.allreduce_scalar(float((xp * xp).sum())))
+        xnn = math.sqrt(comm.allreduce_scalar(float((xn * xn).sum())))
+        ypn, ynn = float(torch.linalg.norm(yp)), float(torch.linalg.norm(yn))
+        mp, mn = xpn * ypn, xnn * ynn
+        if mp > mn:
+            u, v, sigma = xp / max(xpn, 1e-300), yp / max(ypn, 1e-300), mp
+        else:
+            u, v, sigma = xn / max(xnn, 1e-300), yn / max(ynn, 1e-300), mn
+        lbd = math.sqrt(float(S[j]) * sigma)
+        Wsk[:, j] = lbd * u
+        Hsk[j, :] = lbd * v
+    Wsk[Wsk < eps] = 0
+    Hsk[Hsk < eps] = 0
+    if variant in ("nndsvda", "nndsvdar"):
+        avg = _global_mean(X, comm)
+        if variant == "nndsvda":
+            Wsk[Wsk == 0] = avg
+            Hsk[Hsk == 0] = avg
+        else:
+            g = torch.Generator(device="cpu").manual_seed(int(seed))
+            a = avg / 100.0
+            rw = torch.abs(torch.randn(Wsk.shape, generator=g, dtype=torch.float64)) * a
+            rh = torch.abs(torch.randn(Hsk.shape, generator=g, dtype=torch.float64)) * a
+            Wsk = torch.where(Wsk == 0, rw.to(Wsk.device), Wsk)
+            Hsk = torch.where(Hsk == 0, rh.to(Hsk.device), Hsk)
+    return Wsk.to(X.dtype), Hsk.to(X.dtype)
+
+
+def init_factors(X: torch.Tensor, K: int, seeds, init: str = "random", comm=None,
+                 row_offset: int = 0):
+    """Initial (HT (R*K x N_loc), W (R*K x G)) for a replicate batch.
+
+    random: |N(0,1)| * sqrt(mean(X)/K) from Philox keyed by each replicate's seed
+    (H stream 0 over the canonical N x K matrix, W stream 1 over K x G), identical on
+    every device and for every rank/batch placement.
+    """
+    comm = comm or LocalComm()
+    R = len(seeds)
+    N, G = X.shape
+    dev, dt = X.device, X.dtype
+    HT = torch.empty((R * K, N), device=dev, dtype=dt)
+    W = torch.empty((R * K, G), device=dev, dtype=dt)
+    if init == "random":
+        avg = math.sqrt(_global_mean(X, comm) / K)
+        seeds_t = torch.tensor([int(s) for s in seeds], dtype=torch.int64)
+        scales = torch.full((R,), avg, dtype=torch.float32)
+        if N:
+            # HT viewed as (R, N, K): element (r, j, k) -> HT[r*K + k, j]
+            ops.philox_fill(HT.as_strided((R, N, K), (K * N, 1, N)), seeds_t, scales,
+                            rng.STREAM_H, 0, row_offset)
+        ops.philox_fill(W.view(R, K, G), seeds_t, scales, rng.STREAM_W, 0, 0)
+    else:
+        Hn, Wn = _nndsvd(X, K, init, comm, seed=int(seeds[0]) if len(seeds) else 0)
+        for r in range(R):
+            HT[r * K:(r + 1) * K].copy_(Hn.t())
+            W[r * K:(r + 1) * K].copy_(Wn)
+    return HT, W
+
+
+# =============================================================================== state
+class _Batch:
+    """Live replicate batch with an active-prefix layout: live replicates occupy
+    positions [0, n_act); finished ones are moved behind them (``order`` maps position ->
+    original replicate id)."""
+
+    def __init__(self, HT, W, K, R):
+        self.HT, self.W, self.K, self.R = HT, W, K, R
+        self.order = list(range(R))
+        self.n_act = R
+        dev = W.device
+        self.err_init = torch.zeros(R, dtype=torch.float64)
+        self.err_prev = torch.zeros(R, dtype=torch.float64)
+        self.err = torch.zeros(R, dtype=torch.float64)
+        self.n_iter = np.zeros(R, dtype=np.int64)
+        self.converged = np.zeros(R, dtype=bool)
+        self.h_iters = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.w_iters = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.A = None   # (R, K, K) sufficient statistics (online 'exact' mode)
+        self.B = None   # (R*K, G)
+
+    def views(self):
+        K, n = self.K, self.n_act
+        return self.HT[:n * K], self.W[:n * K]
+
+    def retire(self, done_pos: np.ndarray) -> None:
+        """Mark positions (< n_act) finished and compact the live prefix."""
+        if done_pos.size == 0:
+            return
+        n, K = self.n_act, self.K
+        keep = [p for p in range(n) if p not in set(done_pos.tolist())]
+        perm = keep + sorted(done_pos.tolist()) + list(range(n, self.R))
+        if perm != list(range(self.R)):
+            rows = torch.cat([torch.arange(p * K, (p + 1) * K) for p in perm]).to(self.W.device)
+            self.HT = self.HT.index_select(0, rows)
+            self.W = self.W.index_select(0, rows)
+            if self.B is not None:
+                self.B = self.B.index_select(0, rows)
+                self.A = self.A.index_select(0, torch.tensor(perm, device=self.A.device))
+            pidx = torch.tensor(perm)
+            for name in ("err_init", "err_prev", "err"):
+                setattr(self, name, getattr(self, name)[pidx])
+            didx = pidx.to(self.W.device)
+            self.h_iters = self.h_iters[didx]
+            self.w_iters = self.w_iters[didx]
+            self.n_iter = self.n_iter[perm]
+            self.converged = self.converged[perm]
+            self.order = [self.order[p] for p in perm]
+        self.n_act = len(keep)
+
+    def finalize(self):
+        """Restore original replicate order."""
+        inv = np.argsort(np.asarray(self.order))
+        K = self.K
+        rows = torch.cat([torch.arange(p * K, (p + 1) * K) for p in inv]).to(self.W.device)
+        HT = self.HT.index_select(0, rows)
+        W = self.W.index_select(0, rows)
+        idx = torch.tensor(inv)
+        didx = idx.to(self.W.device)
+        return (HT, W, self.err[idx].numpy(), self.n_iter[inv], self.converged[inv],
+                self.h_iters[didx].cpu().numpy(), self.w_iters[didx].cpu().numpy())
+
+
+# =============================================================================== engine
+def _chunks(n_rows: int, c: int, n_steps: int):
+    out = []
+    for s in range(n_steps):
+        a = min(s * c, n_rows)
+        b = min(a + c, n_rows)
+        out.append((a, b))
+    return out
+
+
+class NMFBatchSolver:
+    """Solve R replicates (same X, same K, different seeds) together."""
+
+    def __init__(self, X: torch.Tensor, opts: NMFOptions, comm=None, row_offset: int = 0,
+                 profile: bool = False):
+        opts.validate()
+        self.opts = opts
+        self.comm = comm or LocalComm()
+        self.X = X if X.dtype == opts.dtype else X.to(opts.dtype)
+        self.row_offset = row_offset
+        self.beta = beta_value(opts.beta_loss)
+        self.profile = profile
+        self.timings: dict[str, float] = {}
+        # ||X||_F^2 (global) for the trace-trick loss
+        self.x_sq = self.comm.allreduce_scalar(float((self.X.to(torch.float64) ** 2).sum()))
+
+    # ------------------------------------------------------------------ public
+    def run(self, seeds, HT0=None, W0=None) -> NMFResult:
+        o = self.opts
+        K = int(o.n_components)
+        R = len(seeds)
+        t0 = time.perf_counter()
+        if HT0 is None or W0 is None:
+            HT, W = init_factors(self.X, K, seeds, o.init, self.comm, self.row_offset)
+        else:
+            HT, W = HT0.to(self.X.dtype).clone(), W0.to(self.X.dtype).clone()
+        st = _Batch(HT, W, K, R)
+        if self.beta == 2.0:
+            if o.mode == "online":
+                self._online_frob(st)
+            else:
+                self._batch_frob(st)
+        else:
+            if o.mode == "online":
+                self._online_beta(st)
+            else:
+                self._batch_beta(st)
+        HT, W, err, n_iter, conv, hi, wi = st.finalize()
+        stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": hi.tolist(),
+                 "w_inner_iters": wi.tolist()}
+        return NMFResult(HT=HT, W=W, err=err, n_iter=n_iter, converged=conv, seeds=list(seeds),
+                         K=K, stats=stats)
+
+    # ------------------------------------------------------------------ helpers
+    def _check_convergence(self, st: _Batch, err_now: torch.Tensor, step: int,
+                           final: bool) -> None:
+        """Update per-replicate errors (positions < n_act), retire converged ones."""
+        n = st.n_act
+        st.err[:n] = err_now[:n]
+        done = []
+        for p in range(n):
+            rel = (float(st.err_prev[p]) - float(st.err[p])) / max(float(st.err_init[p]), 1e-300)
+            st.n_iter[p] = step
+            if rel < self.opts.tol:
+                st.converged[p] = True
+                done.append(p)
+            elif final:
+                done.append(p)
+            else:
+                st.err_prev[p] = st.err[p]
+        st.retire(np.asarray(done, dtype=np.int64))
+
+    def _frob_err_from_stats(self, lin: torch.Tensor, quad: torch.Tensor) -> torch.Tensor:
+        v = self.x_sq - 2.0 * lin.double().cpu() + quad.double().cpu()
+        return torch.sqrt(torch.clamp(v, min=0.0))
+
+    def _init_err(self, st: _Batch) -> None:
+        e = self.loss(st.HT, st.W, st.K)
+        st.err_init[:] = e
+        st.err_prev[:] = e
+        st.err[:] = e
+
+    # ------------------------------------------------------------------ loss (any beta)
+    def loss(self, HT: torch.Tensor, W: torch.Tensor, K: int, row_chunk: int = 4096) -> torch.Tensor:
+        """sqrt(2 * D_beta(X || H W)) per replicate (sklearn square_root=True), global."""
+        R = W.shape[0] // K
+        X = self.X
+        N, G = X.shape
+        W3 = W.view(R, K, G)
+        if self.beta == 2.0:
+            # ||X||^2 - 2 <HT X, W> + <HT HT^T, W W^T>
+            B = HT @ X
+            A = torch.bmm(HT.view(R, K, N), HT.view(R, K, N).transpose(1, 2))
+            lin = (B.view(R, K, G) * W3).sum(dim=(1, 2)).double()
+            quad = (A * torch.bmm(W3, W3.transpose(1, 2))).sum(dim=(1, 2)).double()
+            lin = self.comm.allreduce_(lin.contiguous())
+            quad = self.comm.allreduce_(quad.contiguous())
+            return torch.sqrt(torch.clamp(self.x_sq - 2 * lin.cpu() + quad.cpu(), min=0.0))
+        tot = torch.zeros(R, dtype=torch.float64, device=X.device)
+        for a in range(0, N, row_chunk):
+            b = min(N, a + row_chunk)
+            xc = X[a:b]
+            h = HT[:, a:b].reshape(R, K, b - a).transpose(1, 2)
+            tot += _beta_div(xc, torch.bmm(h, W3), self.beta, self.opts.eps)
+        self.comm.allreduce_(tot)
+        return torch.sqrt(torch.clamp(2.0 * tot.cpu(), min=0.0))
+
+    # ------------------------------------------------------------------ online frobenius
+    def _online_frob(self, st: _Batch) -> None:
+        o, comm = self.opts, self.comm
+        K = st.K
+        X = self.X
+        N, G = X.shape
+        dev, dt = X.device, X.dtype
+        c = max(1, int(o.online_chunk_size))
+        n_steps = comm.allreduce_max_int((N + c - 1) // c)
+        chunks = _chunks(N, c, n_steps)
+        algo = o.algo
+        cmode = 1 if o.online_inner_conv == "loss" else 0
+        exact = o.online_stats == "exact"
+        if exact:
+            # sufficient statistics of the CURRENT H over all cells: A = H^T H, B = H^T X
+            R = st.R
+            flat0 = torch.empty(R * K * G + R * K * K, device=dev, dtype=dt)
+            torch.mm(st.HT, X, out=flat0[:R * K * G].view(R * K, G))
+            H3 = st.HT.view(R, K, N)
+            torch.bmm(H3, H3.transpose(1, 2), out=flat0[R * K * G:].view(R, K, K))
+            comm.allreduce_(flat0)
+            st.B = flat0[:R * K * G].view(R * K, G)
+            st.A = flat0[R * K * G:].view(R, K, K)
+            st.A, st.B = st.A.clone(), st.B.clone()
+            W3 = st.W.view(R, K, G)
+            lin = (st.B.view(R, K, G) * W3).sum(dim=(1, 2)).double()
+            quad = (st.A * torch.bmm(W3, W3.transpose(1, 2))).sum(dim=(1, 2)).double()
+            e = self._frob_err_from_stats(lin, quad)
+            st.err_init[:] = e
+            st.err_prev[:] = e
+            st.err[:] = e
+        else:
+            self._init_err(st)
+        for p in range(int(o.online_max_pass)):
+            n = st.n_act
+            if n == 0:
+                break
+            HT, W = st.views()
+            W3 = W.view(n, K, G)
+            H3 = HT.view(n, K, N)
+            # one flat buffer per step: [dB (n*K*G) | dA (n*K*K)] -> ONE all-reduce per step
+            flat = torch.empty(n * K * G + n * K * K, device=dev, dtype=dt)
+            dB = flat[:n * K * G].view(n * K, G)
+            dA = flat[n * K * G:].view(n, K, K)
+            if exact:
+                A, B = st.A[:n], st.B[:n * K]
+            else:
+                A = torch.zeros((n, K, K), device=dev, dtype=dt)
+                B = torch.zeros((n * K, G), device=dev, dtype=dt)
+            lin = torch.zeros(n, device=dev, dtype=torch.float32)
+            quad = torch.zeros(n, device=dev, dtype=torch.float32)
+            it_h = torch.zeros(n, device=dev, dtype=torch.int32)
+            it_w = torch.zeros(n, device=dev, dtype=torch.int32)
+            for s, (a, b) in enumerate(chunks):
+                cw = b - a
+                if cw > 0:
+                    xc = X[a:b]
+                    hview = H3[:, :, a:b]                                # (n, K, cw) strided
+                    h_old = hview.clone() if exact else None
+                    WWT = torch.bmm(W3, W3.transpose(1, 2))
+                    numerT = W @ xc.t()                                  # (n*K, cw) GEMM
+                    ops.solve(algo, hview, numerT.view(n, K, cw), _as(WWT, dt),
+                              max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
+                              l1_den=o.l1_H, l2=o.l2_H, eps=o.eps, iters_out=it_h,
+                              conv_mode=cmode, check_every=o.inner_check_every)
+                    st.h_iters[:n] += it_h.to(torch.int64)
+                    if exact:
+                        # replace the chunk's old contribution: d = h_new - h_old
+                        torch.bmm(hview, hview.transpose(1, 2), out=dA)
+                        dA -= torch.bmm(h_old, h_old.transpose(1, 2))
+                        h_old.neg_().add_(hview)
+                        torch.mm(h_old.view(n * K, cw), xc, out=dB)      # (n*K, G) GEMM
+                    else:
+                        torch.mm(HT[:, a:b], xc, out=dB)                 # (n*K, G) GEMM
+                        torch.bmm(hview, hview.transpose(1, 2), out=dA)
+                else:
+                    flat.zero_()
+                comm.allreduce_(flat)
+                B += dB
+                A += dA
+                last = s == len(chunks) - 1
+                ops.solve(algo, W3, B.view(n, K, G), _as(A, dt),
+                          max_iter=o.online_chunk_max_iter, tol=o.online_w_tol,
+                          l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
+                          lin_out=lin if last else None, quad_out=quad if last else None,
+                          iters_out=it_w, conv_mode=cmode, check_every=o.inner_check_every)
+                st.w_iters[:n] += it_w.to(torch.int64)
+            err = self._frob_err_from_stats(lin, quad)
+            self._check_convergence(st, err, p + 1, final=(p + 1 == int(o.online_max_pass)))
+
+    # ------------------------------------------------------------------ batch frobenius
+    def _batch_frob(self, st: _Batch) -> None:
+        o, comm = self.opts, self.comm
+        K = st.K
+        X = self.X
+        N, G = X.shape
+        dev, dt = X.device, X.dtype
+        self._init_err(st)
+        hals = o.algo == "hals"
+        h_iter = o.batch_hals_max_iter if hals else 1
+        h_tol = o.batch_hals_tol if hals else -1.0
+        for it in range(int(o.batch_max_iter)):
+            n = st.n_act
+            if n == 0:
+                break
+            HT, W = st.views()
+            W3 = W.view(n, K, G)
+            # H-step over all local cells
+            WWT = torch.bmm(W3, W3.transpose(1, 2))
+            numerT = W @ X.t()
+            nsplit = 1 if hals else max(1, (N + 8191) // 8192)
+            ops.solve(o.algo, HT.view(n, K, N), numerT.view(n, K, N), _as(WWT, dt),
+                      max_iter=h_iter, tol=h_tol, l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
+                      nsplit=nsplit if not hals else 1)
+            del numerT
+            # W-step from the new H
+            flat = torch.empty(n * K * G + n * K * K, device=dev, dtype=dt)
+            B = flat[:n * K * G].view(n * K, G)
+            A = flat[n * K * G:].view(n, K, K)
+            torch.mm(HT, X, out=B)
+            H3 = HT.view(n, K, N)
+            torch.bmm(H3, H3.transpose(1, 2), out=A)
+            comm.allreduce_(flat)
+            check = (it + 1) % max(1, int(o.loss_every)) == 0 or it + 1 == int(o.batch_max_iter)
+            lin = torch.zeros(n, device=dev, dtype=torch.float32) if check else None
+            quad = torch.zeros(n, device=dev, dtype=torch.float32) if check else None
+            ops.solve(o.algo, W3, B.view(n, K, G), _as(A, dt),
+                      max_iter=h_iter, tol=h_tol, l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
+                      lin_out=lin, quad_out=quad)
+            if check:
+                err = self._frob_err_from_stats(lin, quad)
+                self._check_convergence(st, err, it + 1, final=(it + 1 == int(o.batch_max_iter)))
+
+    # ------------------------------------------------------------------ beta-divergence MU
+    def _beta_gamma(self) -> float:
+        b = self.beta
+        if b < 1:
+            return 1.0 / (2.0 - b)
+        if b > 2:
+            return 1.0 / (b - 1.0)
+        return 1.0
+
+    def _beta_h_step(self, xc, h, W3, l1, l2):
+        """One MU step for h (R, c, K) given W3 (R, K, G); sklearn _multiplicative_update_h."""
+        eps = self.opts.eps
+        WH = torch.bmm(h, W3)
+        num, den = _beta_num_den(xc, WH, W3.transpose(1, 2), self.beta, eps, side="h")
+        den = den + l1 + l2 * h
+        den = torch.where(den == 0, torch.full_like(den, eps), den)
+        delta = num / den
+        g = self._beta_gamma()
+        if g != 1.0:
+            delta = delta ** g
+        return h * delta
+
+    def _online_beta(self, st: _Batch) -> None:
+        o, comm = self.opts, self.comm
+        K = st.K
+        X = self.X
+        N, G = X.shape
+        c = max(1, int(o.online_chunk_size))
+        n_steps = comm.allreduce_max_int((N + c - 1) // c)
+        chunks = _chunks(N, c, n_steps)
+        self._init_err(st)
+        g = self._beta_gamma()
+        for p in range(int(o.online_max_pass)):
+            n = st.n_act
+            if n == 0:
+                break
+            HT, W = st.views()
+            W3 = W.view(n, K, G)
+            num_acc = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
+            den_acc = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
+            for (a, b) in chunks:
+                cw = b - a
+                flat = torch.zeros(2 * n * K * G, device=X.device, dtype=X.dtype)
+                if cw > 0:
+                    xc = X[a:b]
+                    h = HT[:, a:b].reshape(n, K, cw).transpose(1, 2).contiguous()
+                    active = torch.ones(n, dtype=torch.bool)
+                    for _ in range(int(o.online_chunk_max_iter)):
+                        idx = torch.nonzero(active).flatten()
+                        if idx.numel() == 0:
+                            break
+                        di = idx.to(X.device)
+                        ha = h[di]
+                        hn = self._beta_h_step(xc, ha, W3[di], o.l1_H, o.l2_H)
+                        rel = (torch.linalg.vector_norm(hn - ha, dim=(1, 2)) /
+                               (torch.linalg.vector_norm(ha, dim=(1, 2)) + o.eps)).cpu()
+                        h[di] = hn
+                        st.h_iters[di] += 1
+                        active[idx[rel < o.online_h_tol]] = False
+                    HT[:, a:b] = h.transpose(1, 2).reshape(n * K, cw)
+                    WH = torch.bmm(h, W3)
+                    nW, dW = _beta_num_den(xc, WH, h.transpose(1, 2), self.beta, o.eps, side="w")
+                    flat[:n * K * G] = nW.reshape(-1)
+                    flat[n * K * G:] = dW.expand(n, K, G).reshape(-1)
+                comm.allreduce_(flat)
+                num_acc += flat[:n * K * G].view(n, K, G)
+                den_acc += flat[n * K * G:].view(n, K, G)
+                den = den_acc + o.l1_W + o.l2_W * W3
+                den = torch.where(den == 0, torch.full_like(den, o.eps), den)
+                delta = num_acc / den
+                if g != 1.0:
+                    delta = delta ** g
+                W3.mul_(delta)
+                st.w_iters[:n] += 1
+            err = self.loss(HT, W, K).to(torch.float64)
+            self._check_convergence(st, err, p + 1, final=(p + 1 == int(o.online_max_pass)))
+
+    def _batch_beta(self, st: _Batch, row_chunk: int = 4096) -> None:
+        o, comm = self.opts, self.comm
+        K = st.K
+        X = self.X
+        N, G = X.shape
+        self._init_err(st)
+        g = self._beta_gamma()
+        for it in range(int(o.batch_max_iter)):
+            n = st.n_act
+            if n == 0:
+                break
+            HT, W = st.views()
+            W3 = W.view(n, K, G)
+            for a in range(0, N, row_chunk):
+                b = min(N, a + row_chunk)
+                h = HT[:, a:b].reshape(n, K, b - a).transpose(1, 2)
+                hn = self._beta_h_step(X[a:b], h, W3, o.l1_H, o.l2_H)
+                HT[:, a:b] = hn.transpose(1, 2).reshape(n * K, b - a)
+            flat = torch.zeros(2 * n * K * G, device=X.device, dtype=X.dtype)
+            for a in range(0, N, row_chunk):
+                b = min(N, a + row_chunk)
+                h = HT[:, a:b].reshape(n, K, b - a).transpose(1, 2)
+                WH = torch.bmm(h, W3)
+                nW, dW = _beta_num_den(X[a:b], WH, h.transpose(1, 2), self.beta, o.eps, side="w")
+                flat[:n * K * G] += nW.reshape(-1)
+                flat[n * K * G:] += dW.expand(n, K, G).reshape(-1)
+            comm.allreduce_(flat)
+            den = flat[n * K * G:].view(n, K, G) + o.l1_W + o.l2_W * W3
+            den = torch.where(den == 0, torch.full_like(den, o.eps), den)
+            delta = flat[:n * K * G].view(n, K, G) / den
+            if g != 1.0:
+                delta = delta ** g
+            W3.mul_(delta)
+            if (it + 1) % max(1, int(o.loss_every)) == 0 or it + 1 == int(o.batch_max_iter):
+                err = self.loss(HT, W, K)
+                self._check_convergence(st, err, it + 1, final=(it + 1 == int(o.batch_max_iter)))
+
+
+def _as(t: torch.Tensor, dt: torch.dtype) -> torch.Tensor:
+    """Contiguous copy/view of ``t`` in ``dt`` (solve kernels take dense grams)."""
+    return t.contiguous() if t.dtype == dt else t.to(dt).contiguous()
+
+
+def _beta_num_den(xc, WH, other, beta: float, eps: float, side: str):
+    """MU numerator/denominator pieces for beta-divergence.
+
+    side='h': xc (c,G), WH (R,c,G), other = W^T (R,G,K) -> (R,c,K) num, den
+    side='w': other = h^T (R,K,c) -> (R,K,G) num, den (den may broadcast)
+    """
+    if beta == 1.0:
+        WHs = torch.clamp(WH, min=eps)
+        Q = xc.unsqueeze(0) / WHs
+        if side == "h":
+            num = torch.bmm(Q, other)
+            den = other.sum(dim=1, keepdim=True)            # (R,1,K): row sums of W
+        else:
+            num = torch.bmm(other, Q)
+            den = other.sum(dim=2, keepdim=True)            # (R,K,1): column sums of H
+        return num, den
+    WHs = torch.clamp(WH, min=eps)
+    if beta == 0.0:
+        P1 = WHs.reciprocal()
+        Q = xc.unsqueeze(0) * P1 * P1
+    else:
+        P1 = WHs ** (beta - 1.0)
+        Q = xc.unsqueeze(0) * WHs ** (beta - 2.0)
+    if side == "h":
+        return torch.bmm(Q, other), torch.bmm(P1, other)
+    return torch.bmm(other, Q), torch.bmm(other, P1)
+
+
+def _beta_div(xc: torch.Tensor, WH: torch.Tensor, beta: float, eps: float) -> torch.Tensor:
+    """Per-replicate sum of the beta divergence D(xc || WH) (sklearn _beta_divergence)."""
+    X = xc.unsqueeze(0).to(torch.float64)
+    Y = torch.clamp(WH.to(torch.float64), min=eps)
+    if beta == 1.0:
+        pos = X > 0
+        t = torch.where(pos, X * torch.log(torch.where(pos, X, torch.ones_like(X)) / Y), torch.zeros_like(Y))
+        return (t - X + Y).sum(dim=(1, 2))
+    if beta == 0.0:
+        d = torch.clamp(X / Y, min=eps)
+        return (d - torch.log(d) - 1.0).sum(dim=(1, 2))
+    return ((X ** beta + (beta - 1.0) * Y ** beta - beta * X * Y ** (beta - 1.0)) /
+            (beta * (beta - 1.0))).sum(dim=(1, 2))
+
+
+# =============================================================================== api
+def run_nmf_batch(X, n_components: int, seeds, comm=None, row_offset: int = 0, device=None,
+                  **kwargs) -> NMFResult:
+    """Factorise ``X`` (cells x genes) once per seed; see module docstring."""
+    if not isinstance(X, torch.Tensor):
+        X = torch.as_tensor(np.asarray(X))
+    if device is not None:
+        X = X.to(device)
+    opts = NMFOptions.from_kwargs(n_components, **kwargs)
+    return NMFBatchSolver(X, opts, comm=comm, row_offset=row_offset).run(list(seeds))
+
+
+def run_nmf(X, n_components: int, init: str = "random", beta_loss="frobenius", algo: str = "mu",
+            mode: str = "online", tol: float = 1e-4, n_jobs: int = -1, random_state: int = 0,
+            use_gpu: bool = False, alpha_W: float = 0.0, l1_ratio_W: float = 0.0,
+            alpha_H: float = 0.0, l1_ratio_H: float = 0.0, fp_precision: str = "float",
+            batch_max_iter: int = 500, batch_hals_tol: float = 0.05,
+            batch_hals_max_iter: int = 200, online_max_pass: int = 20,
+            online_chunk_size: int = 5000, online_chunk_max_iter: int = 200,
+            online_h_tol: float = 0.05, online_w_tol: float = 0.05):
+    """Single-replicate drop-in for nmf-torch's ``run_nmf`` (cnmf.py:17, 819).
+
+    Returns (H: N x K usages, W: K x G spectra, err) as numpy arrays.  ``n_jobs`` only
+    sets CPU threads; ``use_gpu`` selects the current HIP device.
+    """
+    if n_jobs is not None and n_jobs > 0:
+        torch.set_num_threads(int(n_jobs))
+    dev = torch.device("cuda") if (use_gpu and torch.cuda.is_available()) else torch.device("cpu")
+    res = run_nmf_batch(X, n_components, [int(random_state)], device=dev, init=init,
+                        beta_loss=beta_loss, algo=algo, mode=mode, tol=tol, alpha_W=alpha_W,
+                        l1_ratio_W=l1_ratio_W, alpha_H=alpha_H, l1_ratio_H=l1_ratio_H,
+                        fp_precision=fp_precision, batch_max_iter=batch_max_iter,
+                        batch_hals_tol=batch_hals_tol, batch_hals_max_iter=batch_hals_max_iter,
+                        online_max_pass=online_max_pass, online_chunk_size=online_chunk_size,
+                        online_chunk_max_iter=online_chunk_max_iter, online_h_tol=online_h_tol,
+                        online_w_tol=online_w_tol)
+    H = res.usages(0).cpu().numpy()
+    W = res.spectra(0).cpu().numpy()
+    return H, W, float(res.err[0])

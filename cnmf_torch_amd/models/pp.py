@@ -1,0 +1,255 @@
+"""scanpy-equivalent preprocessing primitives used by cNMF and Preprocess.
+
+The reference calls scanpy for these (SURVEY.md §2.3 "scanpy functions"); scanpy is
+not a dependency here, so each is re-implemented with the same numerics:
+
+* ``normalize_total`` -- per-cell scaling to ``target_sum`` (int input -> float32,
+  zero-count cells left at zero), preprocess.py:224, cnmf.py:246.
+* ``scale`` with ``zero_center=False`` -- divide genes by their ddof=1 std (zero std
+  -> 1), optional ``max_value`` clip, cnmf.py:675, preprocess.py:22.
+* ``filter_genes`` / ``filter_cells`` -- min_cells / min_counts, preprocess.py:92,105.
+* ``highly_variable_genes(flavor='seurat_v3')`` -- variance-stabilised ranking with a
+  local quadratic (loess, span 0.3) fit of log10 variance on log10 mean; skmisc's
+  loess is not installed, so a direct tricube-weighted local regression is used
+  (``surface='direct'`` equivalent; parity with skmisc's interpolated surface is
+  within loess smoothing noise -- "parity unpinned").
+* ``pca`` -- zero-centred truncated PCA via a (device) SVD, preprocess.py:310.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+import scipy.sparse as sp
+import torch
+
+from ..utils.anndata_lite import AnnData, to_lite
+
+
+def _row_sums(X) -> np.ndarray:
+    return np.asarray(X.sum(axis=1)).reshape(-1)
+
+
+def normalize_total(adata, target_sum: float | None = None, copy: bool = False, inplace=True):
+    adata = to_lite(adata)
+    ad = adata.copy() if copy else adata
+    X = ad.X
+    if np.issubdtype(X.dtype, np.integer):
+        X = X.astype(np.float32)
+    counts = _row_sums(X).astype(np.float64)
+    after = np.median(counts[counts > 0]) if target_sum is None else float(target_sum)
+    counts = counts + (counts == 0)
+    scale = (after / counts)
+    if sp.issparse(X):
+        X = sp.csr_matrix(X) if not sp.isspmatrix_csr(X) else X
+        X = X.copy() if X is ad.X and not copy else X
+        X.data = (X.data * np.repeat(scale, np.diff(X.indptr)).astype(X.dtype)).astype(X.dtype)
+    else:
+        X = np.array(X, copy=True) if X is ad.X and not copy else X
+        X = (X / (counts / after)[:, None].astype(X.dtype)).astype(X.dtype)
+    ad.X = X
+    return ad
+
+
+def _mean_var_ddof1(X):
+    n = X.shape[0]
+    if sp.issparse(X):
+        mean = np.asarray(X.mean(axis=0, dtype=np.float64)).reshape(-1)
+        mean_sq = np.asarray(X.multiply(X).mean(axis=0, dtype=np.float64)).reshape(-1)
+    else:
+        mean = np.mean(X, axis=0, dtype=np.float64)
+        mean_sq = np.mean(np.multiply(X, X, dtype=np.float64), axis=0)
+    var = mean_sq - mean ** 2
+    if n > 1:
+        var *= n / (n - 1)
+    return mean, var
+
+
+def scale(adata, zero_center: bool = False, max_value: float | None = None, copy: bool = False):
+    if zero_center:
+        raise NotImplementedError("only zero_center=False is used by cNMF")
+    adata = to_lite(adata)
+    ad = adata.copy() if copy else adata
+    X = ad.X
+    if np.issubdtype(X.dtype, np.integer):
+        X = X.astype(np.float64)
+    _, var = _mean_var_ddof1(X)
+    std = np.sqrt(var)
+    std[std == 0] = 1.0
+    if sp.issparse(X):
+        X = sp.csr_matrix(X, copy=True)
+        X.data = (X.data / std[X.indices]).astype(X.data.dtype)
+        if max_value is not None:
+            X.data[X.data > max_value] = max_value
+    else:
+        X = (X / std.astype(X.dtype) if X.dtype == np.float32 else X / std)
+        if max_value is not None:
+            X = np.minimum(X, max_value)
+    ad.X = X
+    return ad
+
+
+def filter_genes(adata, min_cells: int | None = None, min_counts: float | None = None):
+    adata = to_lite(adata)
+    X = adata.X
+    if min_cells is not None:
+        n_cells = np.asarray((X > 0).sum(axis=0)).reshape(-1)
+        keep = n_cells >= min_cells
+        adata.var["n_cells"] = n_cells
+    else:
+        tot = np.asarray(X.sum(axis=0)).reshape(-1)
+        keep = tot >= min_counts
+        adata.var["n_counts"] = tot
+    sub = adata[:, keep]
+    adata.X, adata.var = sub.X, sub.var
+    adata.varm = sub.varm
+    return adata
+
+
+def filter_cells(adata, min_counts: float | None = None, min_genes: int | None = None):
+    adata = to_lite(adata)
+    X = adata.X
+    if min_counts is not None:
+        tot = _row_sums(X)
+        keep = tot >= min_counts
+        adata.obs["n_counts"] = tot
+    else:
+        ng = np.asarray((X > 0).sum(axis=1)).reshape(-1)
+        keep = ng >= min_genes
+        adata.obs["n_genes"] = ng
+    sub = adata[keep, :]
+    adata.X, adata.obs, adata.obsm = sub.X, sub.obs, sub.obsm
+    adata.layers = sub.layers
+    return adata
+
+
+# ----------------------------------------------------------------------------- loess
+def loess_fit(x: np.ndarray, y: np.ndarray, span: float = 0.3, degree: int = 2,
+              device=None) -> np.ndarray:
+    """Direct local polynomial regression (tricube weights, nearest span*n points).
+
+    Batched on the device: for each evaluation point the k nearest neighbours are
+    found by sorting x once and sliding a window, then a weighted least-squares fit of
+    the given degree is solved for all points at once."""
+    n = x.shape[0]
+    k = max(degree + 1, int(np.ceil(span * n)))
+    k = min(k, n)
+    order = np.argsort(x, kind="mergesort")
+    xs, ys = x[order].astype(np.float64), y[order].astype(np.float64)
+    # window start for each point: nearest-k contiguous window in sorted order
+    starts = np.zeros(n, dtype=np.int64)
+    lo = 0
+    for i in range(n):
+        if lo > i:
+            lo = i
+        while lo + k < n and (xs[lo + k] - xs[i]) < (xs[i] - xs[lo]):
+            lo += 1
+        lo = min(lo, n - k)
+        starts[i] = lo
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    X = torch.as_tensor(xs, device=dev)
+    Y = torch.as_tensor(ys, device=dev)
+    idx = torch.as_tensor(starts, device=dev)[:, None] + torch.arange(k, device=dev)[None, :]
+    xw = X[idx]                                   # (n, k)
+    yw = Y[idx]
+    d = torch.abs(xw - X[:, None])
+    h = d.max(dim=1, keepdim=True).values
+    h = torch.where(h > 0, h * 1.0000001, torch.ones_like(h))
+    w = torch.clamp(1 - (d / h) ** 3, min=0) ** 3
+    cols = [torch.ones_like(xw)]
+    for p in range(1, degree + 1):
+        cols.append((xw - X[:, None]) ** p)
+    V = torch.stack(cols, dim=2)                  # (n, k, degree+1)
+    Vw = V * w[..., None]
+    A = Vw.transpose(1, 2) @ V
+    b = (Vw.transpose(1, 2) @ yw[..., None])
+    A = A + 1e-10 * torch.eye(degree + 1, device=dev, dtype=A.dtype)
+    coef = torch.linalg.solve(A, b)[..., 0]
+    fitted_sorted = coef[:, 0].cpu().numpy()
+    out = np.empty(n)
+    out[order] = fitted_sorted
+    return out
+
+
+def highly_variable_genes(adata, flavor: str = "seurat_v3", n_top_genes: int = 2000,
+                          batch_key: str | None = None, span: float = 0.3, inplace: bool = True):
+    """Seurat v3 HVG selection on raw counts (preprocess.py:295)."""
+    if flavor != "seurat_v3":
+        raise NotImplementedError("only flavor='seurat_v3' is used by Preprocess")
+    adata = to_lite(adata)
+    X = adata.X
+    batches = (pd.Series(np.zeros(adata.n_obs, dtype=int)) if batch_key is None
+               else adata.obs[batch_key].astype("category").cat.codes.reset_index(drop=True))
+    norm_vars = []
+    means_all, vars_all = _mean_var_ddof1(X)
+    for b in np.unique(batches.values):
+        rows = np.flatnonzero(batches.values == b)
+        Xb = X[rows]
+        mean, var = _mean_var_ddof1(Xb)
+        not_const = var > 0
+        est = np.zeros(X.shape[1], dtype=np.float64)
+        est[not_const] = loess_fit(np.log10(mean[not_const]), np.log10(var[not_const]), span=span)
+        reg_std = np.sqrt(10 ** est)
+        N = Xb.shape[0]
+        clip = reg_std * np.sqrt(N) + mean
+        if sp.issparse(Xb):
+            Xc = sp.csr_matrix(Xb, dtype=np.float64, copy=True)
+            Xc.data = np.minimum(Xc.data, clip[Xc.indices])
+            sq = np.asarray(Xc.multiply(Xc).sum(axis=0)).reshape(-1)
+            s1 = np.asarray(Xc.sum(axis=0)).reshape(-1)
+        else:
+            Xc = np.minimum(np.asarray(Xb, dtype=np.float64), clip[None, :])
+            sq = (Xc ** 2).sum(axis=0)
+            s1 = Xc.sum(axis=0)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            nv = (1.0 / ((N - 1) * reg_std ** 2)) * (N * mean ** 2 + sq - 2 * s1 * mean)
+        norm_vars.append(np.nan_to_num(nv, nan=0.0))
+    norm_vars = np.vstack(norm_vars)
+    ranked = np.argsort(np.argsort(-norm_vars, axis=1, kind="stable"), axis=1, kind="stable").astype(float)
+    ranked[ranked >= n_top_genes] = np.nan
+    n_batches = (~np.isnan(ranked)).sum(axis=0)
+    with np.errstate(all="ignore"):
+        median_rank = np.nanmedian(ranked, axis=0)
+    df = pd.DataFrame({"means": means_all, "variances": vars_all,
+                       "variances_norm": norm_vars.mean(axis=0),
+                       "highly_variable_rank": median_rank,
+                       "highly_variable_nbatches": n_batches}, index=adata.var.index)
+    srt = df.sort_values(["highly_variable_nbatches", "highly_variable_rank"],
+                         ascending=[False, True], na_position="last")
+    hv = np.zeros(len(df), dtype=bool)
+    hv[df.index.get_indexer(srt.index[:n_top_genes])] = True
+    df["highly_variable"] = hv
+    for c in df.columns:
+        adata.var[c] = df[c].values
+    return adata if inplace else df
+
+
+def pca(adata, n_comps: int = 50, zero_center: bool = True, use_highly_variable: bool = False,
+        device=None, random_state: int = 0):
+    """Zero-centred PCA -> obsm['X_pca'], varm['PCs'], uns['pca'] (preprocess.py:310)."""
+    adata = to_lite(adata)
+    X = adata.X
+    cols = np.arange(adata.n_vars)
+    if use_highly_variable and "highly_variable" in adata.var:
+        cols = np.flatnonzero(adata.var["highly_variable"].values)
+    Xs = X[:, cols]
+    Xd = Xs.toarray() if sp.issparse(Xs) else np.asarray(Xs)
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    T = torch.as_tensor(Xd, dtype=torch.float64, device=dev)
+    if zero_center:
+        T = T - T.mean(dim=0, keepdim=True)
+    n_comps = min(n_comps, min(T.shape) - 1) if min(T.shape) > 1 else 1
+    U, S, Vh = torch.linalg.svd(T, full_matrices=False)
+    U, S, Vh = U[:, :n_comps], S[:n_comps], Vh[:n_comps]
+    # deterministic sign: largest |loading| positive (sklearn svd_flip u-based)
+    sign = torch.sign(U[torch.argmax(torch.abs(U), dim=0), torch.arange(U.shape[1], device=dev)])
+    sign[sign == 0] = 1
+    U, Vh = U * sign, Vh * sign[:, None]
+    Xp = (U * S).cpu().numpy()
+    adata.obsm["X_pca"] = Xp
+    PCs = np.zeros((adata.n_vars, n_comps))
+    PCs[cols] = Vh.t().cpu().numpy()
+    adata.varm["PCs"] = PCs
+    var = (S ** 2 / max(T.shape[0] - 1, 1)).cpu().numpy()
+    total = float((T ** 2).sum().cpu()) / max(T.shape[0] - 1, 1)
+    adata.uns["pca"] = {"variance": var, "variance_ratio": var / total if total > 0 else var}
+    return adata

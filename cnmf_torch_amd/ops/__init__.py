@@ -1,0 +1,151 @@
+"""Op layer: one entry point per hot operation, dispatched by device.
+
+* CUDA/HIP tensors -> the hand-written gfx950 kernels in ``_hip`` (csrc/kernels).
+  If the extension is missing on a GPU run the op raises; there is no silent
+  fallback to eager PyTorch for a native op.
+* CPU tensors -> the PyTorch reference implementations in :mod:`.reference`, which
+  are also the numerics oracle the GPU tests compare against (fp32 and fp64).
+
+Every native op validates shapes/strides/dtypes on the host before launching, so a
+kernel is never handed an operand layout it does not assume.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import reference
+
+import importlib
+
+_HIP_ERR: Exception | None = None
+try:  # the HIP runtime must come from torch's copy -> import torch first (done above)
+    _hip = importlib.import_module(__name__ + "._hip")
+except Exception as e:  # pragma: no cover - depends on the build
+    _hip = None
+    _HIP_ERR = e
+
+ALGO_MU = 0
+ALGO_HALS = 1
+ALGOS = {"mu": ALGO_MU, "hals": ALGO_HALS}
+
+
+def native_available() -> bool:
+    return _hip is not None
+
+
+def native_error() -> Exception | None:
+    return _HIP_ERR
+
+
+def _require_native():
+    if _hip is None:
+        raise RuntimeError(
+            "cnmf_torch_amd HIP extension is not available on a GPU run "
+            f"(build it with `python -m cnmf_torch_amd._build`): {_HIP_ERR}")
+    return _hip
+
+
+def use_native(t: torch.Tensor) -> bool:
+    """True when ``t`` lives on the GPU (the HIP path is then mandatory)."""
+    if t.device.type != "cuda":
+        return False
+    if os.environ.get("CNMF_FORCE_TORCH_OPS") == "1":  # debugging aid only, never default
+        return False
+    _require_native()
+    return True
+
+
+def _stream_ptr(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check_block_view(name: str, t: torch.Tensor, R: int, K: int, n: int):
+    if t.dim() != 3 or tuple(t.shape) != (R, K, n):
+        raise ValueError(f"{name}: expected shape {(R, K, n)}, got {tuple(t.shape)}")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: HIP solve requires float32, got {t.dtype}")
+    if n > 1 and t.stride(2) != 1:
+        raise ValueError(f"{name}: innermost (column) stride must be 1, got {t.stride()}")
+
+
+# ----------------------------------------------------------------------------- solve
+def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
+          rep_index: torch.Tensor | None = None, max_iter: int = 1, tol: float = -1.0,
+          l1_num: float = 0.0, l1_den: float = 0.0, l2: float = 0.0, eps: float = 1e-16,
+          lin_out: torch.Tensor | None = None, quad_out: torch.Tensor | None = None,
+          iters_out: torch.Tensor | None = None, nsplit: int = 1, conv_mode: int = 0,
+          check_every: int = 10) -> None:
+    """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
+    ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
+
+    Only replicates listed in ``rep_index`` (int32, default all) are touched.
+    ``nsplit > 1`` runs a single fixed step with columns split over blocks (batch mode).
+    ``conv_mode`` 0: stop when ||dx||/(||x||+eps) < tol (checked every step);
+    1: stop when the block objective's relative change over ``check_every`` steps < tol.
+    """
+    a = ALGOS[algo]
+    R, K, n = x.shape
+    if not use_native(x) or x.dtype != torch.float32:  # fp64 (fp_precision='double') -> torch
+        return reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
+                               eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every)
+    h = _hip
+    if K > h.solve_max_k():
+        return reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
+                               eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every)
+    _check_block_view("x", x, R, K, n)
+    _check_block_view("numer", numer, R, K, n)
+    if gram.shape != (R, K, K) or gram.dtype != torch.float32:
+        raise ValueError(f"gram: expected float32 {(R, K, K)}, got {gram.dtype} {tuple(gram.shape)}")
+    gram = gram.contiguous()
+    devs = {x.device, numer.device, gram.device}
+    if len(devs) != 1:
+        raise ValueError(f"solve operands on different devices: {devs}")
+    if rep_index is not None:
+        if rep_index.dtype != torch.int32 or rep_index.device != x.device:
+            raise ValueError("rep_index must be int32 on the same device")
+        nblocks = int(rep_index.numel())
+        ri = rep_index.data_ptr()
+    else:
+        nblocks, ri = R, 0
+    if nblocks == 0 or n == 0:
+        return
+    if nsplit > 1 and max_iter != 1:
+        raise ValueError("nsplit > 1 requires max_iter == 1 (no convergence test)")
+    for name, t, dt in (("lin_out", lin_out, torch.float32), ("quad_out", quad_out, torch.float32),
+                        ("iters_out", iters_out, torch.int32)):
+        if t is not None and (t.dtype != dt or t.numel() < R or not t.is_contiguous()):
+            raise ValueError(f"{name}: expected contiguous {dt} with >= {R} elements")
+    if nsplit > 1:
+        for t in (lin_out, quad_out):
+            if t is not None:
+                t.zero_()
+    threads = min(h.solve_max_threads(K), max(64, ((min(n, 4096 * 4) + 63) // 64) * 64))
+    threads = min(threads, h.solve_max_threads(K))
+    h.solve(a, K, x.data_ptr(), x.stride(0), x.stride(1), numer.data_ptr(), numer.stride(0),
+            numer.stride(1), gram.data_ptr(), K * K, ri, nblocks, n, int(max_iter), float(tol),
+            float(l1_num), float(l1_den), float(l2), float(eps),
+            lin_out.data_ptr() if lin_out is not None else 0,
+            quad_out.data_ptr() if quad_out is not None else 0,
+            iters_out.data_ptr() if iters_out is not None else 0, int(max(1, nsplit)),
+            int(conv_mode), int(check_every), int(threads), _stream_ptr(x))
+
+
+# ----------------------------------------------------------------------------- init
+def philox_fill(out: torch.Tensor, seeds: torch.Tensor, scales: torch.Tensor, stream: int,
+                mode: int = 0, row_offset: int = 0) -> None:
+    """Fill ``out`` viewed as (R, rows, cols) (any strides) with replicate r's Philox
+    stream: ``|N(0,1)|*scale[r]`` (mode 0) or ``U(0,1)*scale[r]`` (mode 1)."""
+    if out.dim() != 3:
+        raise ValueError("out must be (R, rows, cols)")
+    R, rows, cols = out.shape
+    if seeds.numel() != R or scales.numel() != R:
+        raise ValueError("one seed and one scale per replicate")
+    if not use_native(out) or out.dtype != torch.float32:
+        return reference.philox_fill(out, seeds, scales, stream, mode, row_offset)
+    seeds_d = seeds.to(device=out.device, dtype=torch.int64).contiguous()
+    scales_d = scales.to(device=out.device, dtype=torch.float32).contiguous()
+    _hip.philox_fill(out.data_ptr(), rows, cols, out.stride(1), out.stride(2), out.stride(0),
+                     int(row_offset), seeds_d.data_ptr(), scales_d.data_ptr(), R, int(stream),
+                     int(mode), _stream_ptr(out))

@@ -1,0 +1,106 @@
+"""Communicator abstraction used by the solvers.
+
+``LocalComm`` is the single-process no-op.  ``DistComm`` wraps a ``torch.distributed``
+process group: backend ``nccl`` (= RCCL on ROCm, over xGMI between the GPUs of a
+node) for device tensors, ``gloo`` for CPU tests.  The NMF solvers only ever issue
+*one fused all-reduce per online step* (the flat ``[B | A]`` sufficient-statistics
+buffer) plus a few scalars at init, so the interface is tiny.
+"""
+from __future__ import annotations
+
+import torch
+
+
+class LocalComm:
+    rank = 0
+    world_size = 1
+
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def allreduce_scalar(self, v: float) -> float:
+        return float(v)
+
+    def allreduce_max_int(self, v: int) -> int:
+        return int(v)
+
+    def barrier(self) -> None:
+        pass
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        return t
+
+    def all_gather_object(self, obj):
+        return [obj]
+
+    @property
+    def is_distributed(self) -> bool:
+        return False
+
+
+class DistComm(LocalComm):
+    """torch.distributed-backed communicator (one process per GPU)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self._dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    def _dev(self):
+        if self.backend == "nccl":
+            return torch.device("cuda", torch.cuda.current_device())
+        return torch.device("cpu")
+
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world_size == 1:
+            return t
+        if self.backend != "nccl" and t.device.type != "cpu":
+            host = t.cpu()
+            self._dist.all_reduce(host, group=self.group)
+            t.copy_(host)
+            return t
+        self._dist.all_reduce(t, group=self.group)
+        return t
+
+    def allreduce_scalar(self, v: float) -> float:
+        if self.world_size == 1:
+            return float(v)
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self._dev())
+        self._dist.all_reduce(t, group=self.group)
+        return float(t.item())
+
+    def allreduce_max_int(self, v: int) -> int:
+        if self.world_size == 1:
+            return int(v)
+        t = torch.tensor([int(v)], dtype=torch.int64, device=self._dev())
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def barrier(self) -> None:
+        if self.world_size > 1:
+            if self.backend == "nccl":
+                self._dist.barrier(group=self.group, device_ids=[torch.cuda.current_device()])
+            else:
+                self._dist.barrier(group=self.group)
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        if self.world_size > 1:
+            self._dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def all_gather_object(self, obj):
+        if self.world_size == 1:
+            return [obj]
+        out = [None] * self.world_size
+        self._dist.all_gather_object(out, obj, group=self.group)
+        return out

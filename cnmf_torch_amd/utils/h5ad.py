@@ -1,0 +1,284 @@
+"""AnnData on-disk (h5ad) layout over the native HDF5 layer (``_h5io``).
+
+Implements the encoding the reference relies on through scanpy (cnmf.py:519, 545, 698;
+preprocess.py:242-243): root ``encoding-type=anndata``; ``X`` as a dense dataset or a
+``csr_matrix``/``csc_matrix`` group (``data``/``indices``/``indptr`` + ``shape`` attr);
+``obs``/``var`` as ``dataframe`` groups (``_index`` string array, ``column-order``,
+numeric/bool/string/categorical columns); ``obsm``/``varm``/``layers``/``uns`` dicts.
+Files written here are readable by anndata>=0.8 and vice versa.  ``read_X_rows`` reads a
+row range of X (dense hyperslab, or CSR ``indptr`` slice) for streaming large inputs.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+import scipy.sparse as sp
+
+from .anndata_lite import AnnData
+
+_NATIVE_ERR = None
+try:
+    from . import _h5io  # type: ignore
+except ImportError as e:  # pragma: no cover - exercised only without a build
+    _h5io = None
+    _NATIVE_ERR = e
+
+
+def _lib():
+    if _h5io is None:
+        raise ImportError(
+            "cnmf_torch_amd native h5ad layer is not built (run `python -m cnmf_torch_amd._build`)"
+            f": {_NATIVE_ERR}")
+    return _h5io
+
+
+# ----------------------------------------------------------------------------- write
+def _set_enc(f, path, etype, ever):
+    f.set_attr(path, "encoding-type", etype)
+    f.set_attr(path, "encoding-version", ever)
+
+
+def _write_matrix(f, path: str, X, compression: int) -> None:
+    if sp.issparse(X):
+        fmt = "csc" if sp.isspmatrix_csc(X) or getattr(X, "format", "") == "csc" else "csr"
+        X = X.tocsc() if fmt == "csc" else X.tocsr()
+        f.create_group(path)
+        _set_enc(f, path, f"{fmt}_matrix", "0.1.0")
+        f.set_attr(path, "shape", np.asarray(X.shape, dtype=np.int64))
+        f.write_array(path + "/data", np.ascontiguousarray(X.data), compression)
+        f.write_array(path + "/indices", np.ascontiguousarray(X.indices), compression)
+        f.write_array(path + "/indptr", np.ascontiguousarray(X.indptr), compression)
+    else:
+        X = np.ascontiguousarray(np.asarray(X))
+        f.write_array(path, X, compression)
+        _set_enc(f, path, "array", "0.2.0")
+
+
+def _write_strings(f, path, values) -> None:
+    f.write_strings(path, [str(v) for v in values])
+    _set_enc(f, path, "string-array", "0.2.0")
+
+
+def _write_column(f, path: str, col: pd.Series, compression: int) -> None:
+    if isinstance(col.dtype, pd.CategoricalDtype):
+        f.create_group(path)
+        _set_enc(f, path, "categorical", "0.2.0")
+        f.set_attr(path, "ordered", bool(col.cat.ordered))
+        codes = col.cat.codes.values
+        f.write_array(path + "/codes", np.ascontiguousarray(codes), compression)
+        _set_enc(f, path + "/codes", "array", "0.2.0")
+        cats = col.cat.categories
+        if cats.dtype.kind in "iuf":
+            f.write_array(path + "/categories", np.asarray(cats.values), compression)
+            _set_enc(f, path + "/categories", "array", "0.2.0")
+        else:
+            _write_strings(f, path + "/categories", cats.values)
+        return
+    vals = col.values
+    if vals.dtype.kind in "iufb":
+        f.write_array(path, np.ascontiguousarray(vals), compression)
+        _set_enc(f, path, "array", "0.2.0")
+    else:
+        _write_strings(f, path, vals)
+
+
+def _write_frame(f, path: str, df: pd.DataFrame, compression: int) -> None:
+    f.create_group(path)
+    _set_enc(f, path, "dataframe", "0.2.0")
+    idx_name = "_index"
+    cols = [str(c) for c in df.columns]
+    if idx_name in cols:
+        idx_name = "__index_level_0__"
+    f.set_attr(path, "_index", idx_name)
+    f.set_attr(path, "column-order", cols)
+    _write_strings(f, f"{path}/{idx_name}", df.index.values)
+    for c, name in zip(df.columns, cols):
+        _write_column(f, f"{path}/{name}", df[c], compression)
+
+
+def _write_dict(f, path: str, d: dict, compression: int) -> None:
+    f.create_group(path)
+    _set_enc(f, path, "dict", "0.1.0")
+    for k, v in d.items():
+        p = f"{path}/{k}"
+        if isinstance(v, dict):
+            _write_dict(f, p, v, compression)
+        elif isinstance(v, pd.DataFrame):
+            _write_frame(f, p, v, compression)
+        elif isinstance(v, str):
+            f.write_strings(p, [v])
+            _set_enc(f, p, "string-array", "0.2.0")
+        elif sp.issparse(v) or isinstance(v, np.ndarray):
+            _write_matrix(f, p, v, compression)
+        elif isinstance(v, (list, tuple)):
+            arr = np.asarray(v)
+            if arr.dtype.kind in "iufb":
+                _write_matrix(f, p, arr, compression)
+            else:
+                _write_strings(f, p, arr)
+        elif isinstance(v, (int, float, bool, np.generic)):
+            f.write_array(p, np.asarray(v))
+            _set_enc(f, p, "numeric-scalar", "0.2.0")
+        # other objects (figures, models) are not serialisable -> skipped, like anndata warns
+
+
+def write_h5ad(path: str, adata, compression=None) -> None:
+    """Write an AnnData(-like) object to ``path`` atomically."""
+    from .io import atomic_path
+
+    lib = _lib()
+    comp = 4 if compression == "gzip" else int(compression or 0)
+    with atomic_path(path, suffix=".h5ad") as tmp:
+        f = lib.File(tmp, "w")
+        try:
+            _set_enc(f, "/", "anndata", "0.1.0")
+            _write_matrix(f, "/X", adata.X, comp)
+            _write_frame(f, "/obs", adata.obs, comp)
+            _write_frame(f, "/var", adata.var, comp)
+            for key in ("obsm", "varm", "layers", "obsp", "varp"):
+                d = getattr(adata, key, None) or {}
+                f.create_group("/" + key)
+                _set_enc(f, "/" + key, "dict", "0.1.0")
+                for k, v in d.items():
+                    if isinstance(v, pd.DataFrame):
+                        _write_frame(f, f"/{key}/{k}", v, comp)
+                    else:
+                        _write_matrix(f, f"/{key}/{k}", v, comp)
+            _write_dict(f, "/uns", dict(getattr(adata, "uns", {}) or {}), comp)
+        finally:
+            f.close()
+
+
+# ----------------------------------------------------------------------------- read
+def _enc(attrs: dict) -> str:
+    e = attrs.get("encoding-type")
+    if e is None and "h5sparse_format" in attrs:  # anndata < 0.7
+        return attrs["h5sparse_format"] + "_matrix"
+    return e or ""
+
+
+def _read_matrix(f, path: str):
+    if f.kind(path) == "dataset":
+        return np.asarray(f.read(path))
+    attrs = f.attrs(path)
+    enc = _enc(attrs)
+    if enc in ("csr_matrix", "csc_matrix"):
+        shape = tuple(int(s) for s in np.asarray(attrs.get("shape", attrs.get("h5sparse_shape"))))
+        data = f.read(path + "/data")
+        indices = f.read(path + "/indices")
+        indptr = f.read(path + "/indptr")
+        cls = sp.csr_matrix if enc == "csr_matrix" else sp.csc_matrix
+        return cls((data, indices, indptr), shape=shape)
+    raise ValueError(f"unsupported matrix encoding {enc!r} at {path}")
+
+
+def _read_column(f, path: str):
+    if f.kind(path) == "group":
+        attrs = f.attrs(path)
+        if _enc(attrs) == "categorical":
+            codes = np.asarray(f.read(path + "/codes"))
+            cats = f.read(path + "/categories")
+            cats = np.asarray(cats) if not isinstance(cats, list) else cats
+            return pd.Categorical.from_codes(codes, categories=cats,
+                                             ordered=bool(attrs.get("ordered", False)))
+        if _enc(attrs) in ("nullable-integer", "nullable-boolean"):
+            vals = np.asarray(f.read(path + "/values"))
+            mask = np.asarray(f.read(path + "/mask"))
+            s = pd.array(vals, dtype="Int64" if _enc(attrs) == "nullable-integer" else "boolean")
+            s[mask] = pd.NA
+            return s
+        raise ValueError(f"unsupported column encoding at {path}")
+    v = f.read(path)
+    return np.asarray(v, dtype=object) if isinstance(v, list) else np.asarray(v)
+
+
+def _read_frame(f, path: str) -> pd.DataFrame:
+    if f.kind(path) != "group":
+        raise ValueError(
+            f"{path} is stored in the legacy (anndata<0.7) compound format, which is not "
+            "supported; re-save the file with a current anndata")
+    attrs = f.attrs(path)
+    idx_name = attrs.get("_index", "_index")
+    order = attrs.get("column-order", [])
+    if isinstance(order, np.ndarray):
+        order = list(order)
+    index = f.read(f"{path}/{idx_name}") if f.exists(f"{path}/{idx_name}") else None
+    cols = {}
+    for c in order:
+        cols[c] = _read_column(f, f"{path}/{c}")
+    n = len(index) if index is not None else (len(next(iter(cols.values()))) if cols else 0)
+    idx = pd.Index([str(i) for i in index]) if index is not None else pd.RangeIndex(n).astype(str)
+    df = pd.DataFrame(cols, index=idx)
+    if order:
+        df = df[list(order)]
+    return df
+
+
+def _read_dict(f, path: str) -> dict:
+    out = {}
+    if not f.exists(path):
+        return out
+    for k in f.list(path):
+        p = f"{path}/{k}"
+        try:
+            if f.kind(p) == "group":
+                enc = _enc(f.attrs(p))
+                if enc in ("csr_matrix", "csc_matrix"):
+                    out[k] = _read_matrix(f, p)
+                elif enc == "dataframe":
+                    out[k] = _read_frame(f, p)
+                else:
+                    out[k] = _read_dict(f, p)
+            else:
+                v = f.read(p)
+                if isinstance(v, list) and len(v) == 1 and _enc(f.attrs(p)) == "string-array":
+                    v = v[0]
+                out[k] = v
+        except (ValueError, OSError):
+            continue
+    return out
+
+
+def read_h5ad(path: str, backed=None) -> AnnData:
+    """Read an .h5ad file into an :class:`AnnData`."""
+    lib = _lib()
+    with lib.File(str(path), "r") as f:
+        X = _read_matrix(f, "/X") if f.exists("/X") else None
+        obs = _read_frame(f, "/obs")
+        var = _read_frame(f, "/var")
+        obsm = {k: _read_matrix(f, f"/obsm/{k}") for k in f.list("/obsm")} if f.exists(
+            "/obsm") else {}
+        varm = {k: _read_matrix(f, f"/varm/{k}") for k in f.list("/varm")} if f.exists(
+            "/varm") else {}
+        layers = {k: _read_matrix(f, f"/layers/{k}") for k in f.list("/layers")} if f.exists(
+            "/layers") else {}
+        uns = _read_dict(f, "/uns")
+    return AnnData(X=X, obs=obs, var=var, obsm=obsm, varm=varm, layers=layers, uns=uns)
+
+
+def h5ad_shape(path: str) -> tuple[int, int]:
+    lib = _lib()
+    with lib.File(str(path), "r") as f:
+        if f.kind("/X") == "dataset":
+            s = f.shape("/X")
+            return int(s[0]), int(s[1])
+        shp = np.asarray(f.attrs("/X")["shape"])
+        return int(shp[0]), int(shp[1])
+
+
+def read_X_rows(path: str, start: int, stop: int):
+    """Rows [start, stop) of X as dense ndarray or CSR, without loading the whole file."""
+    lib = _lib()
+    with lib.File(str(path), "r") as f:
+        if f.kind("/X") == "dataset":
+            return np.asarray(f.read("/X", start, stop))
+        attrs = f.attrs("/X")
+        if _enc(attrs) != "csr_matrix":
+            return _read_matrix(f, "/X")[start:stop]
+        shape = tuple(int(s) for s in np.asarray(attrs["shape"]))
+        stop = min(stop, shape[0])
+        indptr = np.asarray(f.read("/X/indptr", start, stop + 1))
+        lo, hi = int(indptr[0]), int(indptr[-1])
+        data = np.asarray(f.read("/X/data", lo, hi))
+        indices = np.asarray(f.read("/X/indices", lo, hi))
+        return sp.csr_matrix((data, indices, indptr - lo), shape=(stop - start, shape[1]))

@@ -1,0 +1,210 @@
+"""File-level persistence layer (SURVEY.md §1 L4, §2.2 on-disk contract).
+
+Re-implements the reference's DataFrame npz codec (cnmf.py:32-41), TSV writer
+(cnmf.py:35-36) and directory helper (cnmf.py:43-51) with two fixes from SURVEY.md
+§5.2: every write is atomic (temp file + ``os.replace``), so a killed worker never
+leaves a truncated ``.df.npz`` that the resume ledger would count as complete, and
+string/number index arrays are stored as plain numpy dtypes so our own files load
+with ``allow_pickle=False``.  Files written by the original cnmf (object arrays) are
+still readable: ``load_df_from_npz`` retries with pickle enabled for those.
+"""
+from __future__ import annotations
+
+import contextlib
+import errno
+import gzip
+import io
+import os
+import tempfile
+import warnings
+
+import numpy as np
+import pandas as pd
+import yaml
+
+
+# --------------------------------------------------------------------------- atomic
+@contextlib.contextmanager
+def atomic_path(final_path: str, suffix: str = ""):
+    """Yield a temp path in the destination directory; rename over ``final_path``
+    on success, delete on failure.  ``suffix`` keeps extensions numpy/matplotlib
+    key off (e.g. ``.npz``)."""
+    d = os.path.dirname(os.path.abspath(final_path)) or "."
+    os.makedirs(d, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(prefix=".tmp_" + os.path.basename(final_path) + ".", suffix=suffix,
+                               dir=d)
+    os.close(fd)
+    try:
+        yield tmp
+        os.replace(tmp, final_path)
+    except BaseException:
+        with contextlib.suppress(OSError):
+            os.remove(tmp)
+        raise
+
+
+def write_text_atomic(path: str, text: str) -> None:
+    with atomic_path(path) as tmp:
+        with open(tmp, "w") as fh:
+            fh.write(text)
+
+
+# --------------------------------------------------------------------------- npz codec
+def _plain_array(values) -> np.ndarray:
+    """Convert an index/columns array to a non-object dtype when possible."""
+    arr = np.asarray(values)
+    if arr.dtype != object:
+        return arr
+    if len(arr) == 0:
+        return arr.astype(str)
+    if all(isinstance(v, str) for v in arr):
+        return arr.astype(str)
+    if all(isinstance(v, (int, np.integer)) and not isinstance(v, (bool, np.bool_)) for v in arr):
+        return arr.astype(np.int64)
+    if all(isinstance(v, (float, np.floating, int, np.integer)) for v in arr):
+        return arr.astype(np.float64)
+    return arr
+
+
+def _plain_values(df: pd.DataFrame) -> np.ndarray:
+    vals = df.values
+    if vals.dtype != object:
+        return vals
+    # mixed numeric/bool columns (e.g. the replicate ledger) -> int64 when lossless
+    kinds = {np.dtype(t).kind for t in df.dtypes}
+    if kinds <= {"i", "u", "b"}:
+        return df.astype(np.int64).values
+    if kinds <= {"i", "u", "b", "f"}:
+        return df.astype(np.float64).values
+    return vals
+
+
+def save_df_to_npz(obj: pd.DataFrame, filename: str) -> None:
+    """np.savez_compressed(data, index, columns) -- same keys as cnmf.py:32-33."""
+    filename = str(filename)
+    with atomic_path(filename, suffix=".npz") as tmp:
+        np.savez_compressed(tmp, data=_plain_values(obj), index=_plain_array(obj.index.values),
+                            columns=_plain_array(obj.columns.values))
+
+
+def load_df_from_npz(filename: str, allow_pickle_fallback: bool = True) -> pd.DataFrame:
+    """Inverse of :func:`save_df_to_npz` (cnmf.py:38-41)."""
+    filename = str(filename)
+    try:
+        with np.load(filename, allow_pickle=False) as f:
+            return pd.DataFrame(data=f["data"], index=f["index"], columns=f["columns"])
+    except ValueError as e:
+        if not allow_pickle_fallback or "allow_pickle" not in str(e):
+            raise
+        # Files produced by the original cnmf store object arrays.
+        with np.load(filename, allow_pickle=True) as f:
+            return pd.DataFrame(data=f["data"], index=f["index"], columns=f["columns"])
+
+
+def save_df_to_text(obj: pd.DataFrame, filename: str) -> None:
+    """Tab-separated text, as cnmf.py:35-36."""
+    filename = str(filename)
+    with atomic_path(filename) as tmp:
+        obj.to_csv(tmp, sep="\t")
+
+
+def check_dir_exists(path: str) -> None:
+    """mkdir -p tolerating EEXIST (cnmf.py:43-51)."""
+    try:
+        os.makedirs(path)
+    except OSError as exception:
+        if exception.errno != errno.EEXIST:
+            raise
+
+
+# --------------------------------------------------------------------------- yaml
+def dump_yaml(obj: dict, path: str) -> None:
+    with atomic_path(path) as tmp:
+        with open(tmp, "w") as fh:
+            yaml.safe_dump(_yaml_clean(obj), fh)
+
+
+def load_yaml(path: str) -> dict:
+    with open(path) as fh:
+        return yaml.safe_load(fh)
+
+
+def _yaml_clean(o):
+    if isinstance(o, dict):
+        return {str(k): _yaml_clean(v) for k, v in o.items()}
+    if isinstance(o, (list, tuple)):
+        return [_yaml_clean(v) for v in o]
+    if isinstance(o, np.generic):
+        return o.item()
+    return o
+
+
+# --------------------------------------------------------------------------- 10x mtx
+def _open_maybe_gz(path: str):
+    if os.path.exists(path):
+        return open(path, "rb")
+    if os.path.exists(path + ".gz"):
+        return gzip.open(path + ".gz", "rb")
+    raise FileNotFoundError(path)
+
+
+def read_10x_mtx(path: str, var_names: str = "gene_symbols", make_unique: bool = True):
+    """Read a 10x Genomics ``matrix.mtx[.gz]`` directory (cnmf.py:520-522 semantics of
+    ``sc.read_10x_mtx``): cells x genes CSR float32, gene symbols as var names."""
+    import scipy.io
+    import scipy.sparse as sp
+
+    from .anndata_lite import AnnData
+
+    with _open_maybe_gz(os.path.join(path, "matrix.mtx")) as fh:
+        m = scipy.io.mmread(fh)
+    X = sp.csr_matrix(m.T, dtype=np.float32)
+    genes_file = None
+    for cand in ("features.tsv", "genes.tsv"):
+        if os.path.exists(os.path.join(path, cand)) or os.path.exists(
+                os.path.join(path, cand + ".gz")):
+            genes_file = cand
+            break
+    if genes_file is None:
+        raise FileNotFoundError(f"no features.tsv/genes.tsv in {path}")
+    with _open_maybe_gz(os.path.join(path, genes_file)) as fh:
+        genes = pd.read_csv(fh, sep="\t", header=None)
+    with _open_maybe_gz(os.path.join(path, "barcodes.tsv")) as fh:
+        barcodes = pd.read_csv(fh, sep="\t", header=None)[0].astype(str).values
+    ids = genes[0].astype(str).values
+    symbols = genes[1].astype(str).values if genes.shape[1] > 1 else ids
+    names = symbols if var_names == "gene_symbols" else ids
+    var = pd.DataFrame(index=pd.Index(names))
+    var["gene_ids"] = ids
+    if genes.shape[1] > 2:
+        var["feature_types"] = genes[2].astype(str).values
+    ad = AnnData(X=X, obs=pd.DataFrame(index=pd.Index(barcodes)), var=var)
+    if make_unique:
+        ad.var_names_make_unique()
+    return ad
+
+
+def read_counts_table(counts_fn: str, densify: bool):
+    """Load ``.npz`` (DataFrame codec) or TSV counts into an AnnData (cnmf.py:524-537)."""
+    import scipy.sparse as sp
+
+    from .anndata_lite import AnnData
+
+    if counts_fn.endswith(".npz"):
+        df = load_df_from_npz(counts_fn)
+    else:
+        df = pd.read_csv(counts_fn, sep="\t", index_col=0)
+    X = df.values if densify else sp.csr_matrix(df.values)
+    return AnnData(X=X, obs=pd.DataFrame(index=df.index.astype(str)),
+                   var=pd.DataFrame(index=df.columns.astype(str)))
+
+
+def read_any(path: str, densify: bool = False):
+    """Dispatch on extension the way cNMF.prepare does (cnmf.py:518-541)."""
+    from .h5ad import read_h5ad
+
+    if path.endswith(".h5ad"):
+        return read_h5ad(path)
+    if path.endswith(".mtx") or path.endswith(".mtx.gz"):
+        return read_10x_mtx(os.path.dirname(path))
+    return read_counts_table(path, densify)

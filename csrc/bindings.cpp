@@ -1,0 +1,53 @@
+// pybind11 entry points for the HIP kernels.  No torch headers: the Python ops layer
+// (cnmf_torch_amd/ops/__init__.py) validates shapes, dtypes, devices and strides on
+// the host and hands raw device pointers plus the current HIP stream here.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "kernels/launchers.h"
+
+namespace py = pybind11;
+
+static void check(hipError_t e, const char* what) {
+  if (e != hipSuccess)
+    throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+static T* P(uintptr_t v) { return reinterpret_cast<T*>(v); }
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "cnmf_torch_amd native HIP kernels (gfx950)";
+
+  m.def("solve_max_k", []() { return cnmf_solve_max_k(); });
+  m.def("solve_max_threads", [](int K) { return cnmf_solve_max_threads(K); });
+
+  m.def("solve",
+        [](int algo, int K, uintptr_t x, long long x_rs, long long ldx, uintptr_t numer,
+           long long n_rs, long long ldn, uintptr_t gram, long long g_rs, uintptr_t rep_index,
+           int nblocks, int ncols, int max_iter, float tol, float l1_num, float l1_den, float l2,
+           float eps, uintptr_t lin_out, uintptr_t quad_out, uintptr_t iters_out, int nsplit,
+           int conv_mode, int check_every, int threads, uintptr_t stream) {
+          check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
+                           P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
+                           max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
+                           P<float>(quad_out), P<int>(iters_out), nsplit, conv_mode,
+                           check_every, threads,
+                           reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_solve");
+        });
+
+  m.def("philox_fill",
+        [](uintptr_t out, long long rows, long long cols, long long s_row, long long s_col,
+           long long rep_stride, long long row_offset, uintptr_t seeds, uintptr_t scales, int R,
+           unsigned stream_id, int mode, uintptr_t stream) {
+          check(cnmf_philox_fill(P<float>(out), rows, cols, s_row, s_col, rep_stride, row_offset,
+                                 P<const unsigned long long>(seeds), P<const float>(scales), R,
+                                 stream_id, mode, reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_philox_fill");
+        });
+}

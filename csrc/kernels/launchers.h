@@ -1,0 +1,20 @@
+// C ABI of every HIP launcher compiled into cnmf_torch_amd/ops/_hip*.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+extern "C" {
+
+int cnmf_solve_max_k();
+int cnmf_solve_max_threads(int K);
+hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, const float* numer,
+                      long long n_rs, long long ldn, const float* gram, long long g_rs,
+                      const int* rep_index, int nblocks, int ncols, int max_iter, float tol,
+                      float l1_num, float l1_den, float l2, float eps, float* lin_out,
+                      float* quad_out, int* iters_out, int nsplit, int conv_mode,
+                      int check_every, int threads, hipStream_t stream);
+
+hipError_t cnmf_philox_fill(float* out, long long rows, long long cols, long long s_row,
+                            long long s_col, long long rep_stride, long long row_offset,
+                            const unsigned long long* seeds, const float* scales, int R,
+                            unsigned int stream_id, int mode, hipStream_t stream);
+}

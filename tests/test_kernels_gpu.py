@@ -1,0 +1,141 @@
+"""HIP kernel numerics vs the PyTorch reference (fp32 on CPU, and fp64 oracle).
+
+Every test here runs the native gfx950 kernels; they fail (not skip) on a GPU box if
+the extension did not load.
+"""
+import numpy as np
+import pytest
+import torch
+
+from cnmf_torch_amd import ops
+from cnmf_torch_amd.ops import reference
+from cnmf_torch_amd.utils.rng import philox_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(R, K, n, seed=0, dtype=torch.float32):
+    g = torch.Generator().manual_seed(seed)
+    W = torch.rand((R, K, 64), generator=g, dtype=torch.float64) + 0.05
+    gram = torch.bmm(W, W.transpose(1, 2))
+    x_true = torch.rand((R, K, n), generator=g, dtype=torch.float64)
+    numer = torch.bmm(gram, x_true) * (1 + 0.05 * torch.rand((R, K, n), generator=g, dtype=torch.float64))
+    x0 = torch.rand((R, K, n), generator=g, dtype=torch.float64) + 0.1
+    return x0.to(dtype), numer.to(dtype), gram.to(dtype)
+
+
+def test_native_extension_loaded():
+    assert ops.native_available(), f"HIP extension failed to load: {ops.native_error()}"
+
+
+@pytest.mark.parametrize("algo", ["mu", "hals"])
+@pytest.mark.parametrize("K", [3, 10, 17, 32])
+@pytest.mark.parametrize("conv_mode", [0, 1])
+def test_solve_matches_reference(algo, K, conv_mode):
+    R, n = 6, 3001
+    x0, numer, gram = _problem(R, K, n, seed=K)
+    dev = torch.device("cuda")
+    # fixed iteration count (tol < 0) isolates the arithmetic from convergence decisions
+    for max_iter, tol in ((7, -1.0), (200, 1e-3)):
+        xg = x0.clone().to(dev)
+        lin_g = torch.zeros(R, device=dev)
+        quad_g = torch.zeros(R, device=dev)
+        it_g = torch.zeros(R, dtype=torch.int32, device=dev)
+        ops.solve(algo, xg, numer.to(dev), gram.to(dev), max_iter=max_iter, tol=tol,
+                  lin_out=lin_g, quad_out=quad_g, iters_out=it_g, conv_mode=conv_mode,
+                  check_every=5)
+        xr = x0.clone().double()
+        lin_r = torch.zeros(R, dtype=torch.float64)
+        quad_r = torch.zeros(R, dtype=torch.float64)
+        it_r = torch.zeros(R, dtype=torch.int32)
+        reference.solve(ops.ALGOS[algo], xr, numer.double(), gram.double(), None, max_iter, tol,
+                        0.0, 0.0, 0.0, 1e-16, lin_r, quad_r, it_r, 1, conv_mode, 5)
+        torch.cuda.synchronize()
+        if tol < 0:
+            assert it_g.cpu().tolist() == [max_iter] * R
+            torch.testing.assert_close(xg.cpu().double(), xr, rtol=2e-4, atol=1e-4)
+        else:
+            # convergence decisions may differ by a step at the boundary; compare solutions
+            diff = (xg.cpu().double() - xr).norm() / xr.norm()
+            assert diff < 5e-3, diff
+        torch.testing.assert_close(lin_g.cpu().double(), lin_r, rtol=1e-3, atol=1e-3)
+        torch.testing.assert_close(quad_g.cpu().double(), quad_r, rtol=1e-3, atol=1e-3)
+
+
+def test_solve_strided_and_rep_index():
+    R, K, N = 5, 7, 2000
+    dev = torch.device("cuda")
+    HT = torch.rand((R * K, N), device=dev) + 0.1
+    numer = torch.rand((R * K, 600), device=dev)
+    W = torch.rand((R, K, 40), device=dev)
+    gram = torch.bmm(W, W.transpose(1, 2))
+    ref = HT.clone().cpu()
+    view = HT.view(R, K, N)[:, :, 300:900]
+    rep = torch.tensor([0, 3], dtype=torch.int32, device=dev)
+    ops.solve("mu", view, numer.view(R, K, 600), gram, rep_index=rep, max_iter=4)
+    rview = ref.view(R, K, N)[:, :, 300:900]
+    reference.solve(0, rview, numer.cpu().view(R, K, 600), gram.cpu(), rep.cpu(), 4, -1.0, 0, 0, 0,
+                    1e-16, None, None, None)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(HT.cpu(), ref, rtol=1e-4, atol=1e-6)
+    # untouched replicates / columns really are untouched
+    untouched = HT.view(R, K, N)[1]
+    assert torch.equal(untouched.cpu(), ref.view(R, K, N)[1])
+
+
+def test_solve_split_columns():
+    R, K, n = 4, 9, 50000
+    x0, numer, gram = _problem(R, K, n, seed=3)
+    dev = torch.device("cuda")
+    xg = x0.clone().to(dev)
+    lin = torch.zeros(R, device=dev)
+    quad = torch.zeros(R, device=dev)
+    ops.solve("mu", xg, numer.to(dev), gram.to(dev), max_iter=1, nsplit=7, lin_out=lin,
+              quad_out=quad)
+    xr = x0.clone().double()
+    lr = torch.zeros(R, dtype=torch.float64)
+    qr = torch.zeros(R, dtype=torch.float64)
+    reference.solve(0, xr, numer.double(), gram.double(), None, 1, -1.0, 0, 0, 0, 1e-16, lr, qr,
+                    None)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(xg.cpu().double(), xr, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(lin.cpu().double(), lr, rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_philox_matches_numpy(mode):
+    dev = torch.device("cuda")
+    R, rows, cols = 3, 1001, 7
+    seeds = torch.tensor([1, 123456789, 2**31 - 2], dtype=torch.int64)
+    scales = torch.tensor([1.0, 0.5, 2.0])
+    out = torch.empty((R, rows, cols), device=dev)
+    ops.philox_fill(out, seeds, scales, 5, mode)
+    torch.cuda.synchronize()
+    for r in range(R):
+        ref = philox_matrix(int(seeds[r]), 5, rows, cols, mode) * float(scales[r])
+        np.testing.assert_allclose(out[r].cpu().numpy(), ref, rtol=2e-6, atol=1e-7)
+    # transposed layout + row offset (cell-sharded init)
+    HT = torch.empty((R * cols, 333), device=dev)
+    ops.philox_fill(HT.as_strided((R, 333, cols), (cols * 333, 1, 333)), seeds, scales, 5, mode,
+                    row_offset=17)
+    torch.cuda.synchronize()
+    for r in range(R):
+        ref = philox_matrix(int(seeds[r]), 5, 333, cols, mode, row_offset=17) * float(scales[r])
+        np.testing.assert_allclose(HT[r * cols:(r + 1) * cols].t().cpu().numpy(), ref, rtol=2e-6,
+                                   atol=1e-7)
+
+
+@pytest.mark.parametrize("algo", ["mu", "hals"])
+@pytest.mark.parametrize("mode", ["online", "batch"])
+def test_nmf_batch_gpu_matches_cpu(algo, mode):
+    from cnmf_torch_amd.models.nmf import run_nmf_batch
+
+    rs = np.random.default_rng(0)
+    N, G, K = 1500, 400, 6
+    X = (rs.gamma(1, 1, (N, K)) @ rs.gamma(0.5, 1, (K, G)) + 0.1 * rs.random((N, G))).astype(
+        np.float32)
+    kw = dict(algo=algo, mode=mode, online_chunk_size=700, online_max_pass=5, batch_max_iter=40)
+    g = run_nmf_batch(X, K, [11, 12, 13], device="cuda", **kw)
+    c = run_nmf_batch(X, K, [11, 12, 13], device="cpu", **kw)
+    # same init, same algorithm: errors agree to fp32 reassociation noise
+    np.testing.assert_allclose(g.err, c.err, rtol=2e-2)
