@@ -283,60 +283,91 @@ class cNMF:
 
         Jobs with the same K are solved together in batches of ``replicate_batch``
         replicates (default: all of them that fit the device memory budget)."""
-        with self.timer("factorize"):
+        run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
+        if not skip_completed_runs:
+            jobs = list(worker_filter(range(len(run_params)), worker_i, total_workers))
+        else:
+            done = run_params["completed"].astype(bool).values
+            jobs = list(worker_filter(list(run_params.index[~done]), worker_i, total_workers))
+        self.factorize_jobs(jobs, worker_label=worker_i, device=device,
+                            replicate_batch=replicate_batch, save_usages=save_usages,
+                            verbose=verbose, run_params=run_params)
+
+    def factorize_jobs(self, jobs, worker_label=0, device=None, replicate_batch=None,
+                       save_usages=False, verbose=True, run_params=None, comm=None,
+                       row_range=None):
+        """Factorise an explicit list of ledger rows.
+
+        ``comm``/``row_range`` run the cell-sharded data-parallel solver: this rank holds
+        rows [row_range) of norm_counts, the sufficient statistics are all-reduced per
+        step and only rank 0 writes spectra (usages stay rank-local)."""
+        if run_params is None:
             run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
-            norm_counts = read_h5ad(self.paths["normalized_counts"])
+        if not jobs:
+            return
+        with self.timer("factorize"):
             kwargs = load_yaml(self.paths["nmf_run_parameters"])
-            if not skip_completed_runs:
-                jobs = list(worker_filter(range(len(run_params)), worker_i, total_workers))
-            else:
-                done = run_params["completed"].astype(bool).values
-                jobs = list(worker_filter(list(run_params.index[~done]), worker_i, total_workers))
-            if not jobs:
-                return
             dev = _device(bool(kwargs.get("use_gpu", False)), device)
             if dev.type == "cpu" and kwargs.get("n_jobs", -1) not in (None, -1):
                 torch.set_num_threads(max(1, int(kwargs["n_jobs"])))
-            X = torch.from_numpy(_dense32(norm_counts.X)).to(dev)
+            if row_range is None:
+                norm_counts = read_h5ad(self.paths["normalized_counts"])
+                Xh = norm_counts.X
+                row0 = 0
+            else:
+                from .utils.h5ad import read_X_rows, read_h5ad_annotations
+
+                norm_counts = read_h5ad_annotations(self.paths["normalized_counts"])
+                row0 = int(row_range[0])
+                Xh = read_X_rows(self.paths["normalized_counts"], row_range[0], row_range[1])
+            X = torch.from_numpy(_dense32(Xh)).to(dev)
+            del Xh
             genes = norm_counts.var.index
-            cells = norm_counts.obs.index
+            cells = norm_counts.obs.index[row0:row0 + X.shape[0]]
+            writer = comm is None or comm.rank == 0
             fault_after = int(os.environ.get("CNMF_FAULT_AFTER_REPLICATES", "0") or 0)
             written = 0
             by_k: dict[int, list[int]] = {}
             for idx in jobs:
                 by_k.setdefault(int(run_params.iloc[idx]["n_components"]), []).append(idx)
-            solvers: dict[int, NMFBatchSolver] = {}
             for k, idxs in by_k.items():
                 bs = replicate_batch or self._auto_batch(X, k, len(idxs), dev)
-                if k not in solvers:
-                    solvers[k] = NMFBatchSolver(X, self._solver_options(kwargs, k))
+                if comm is not None:
+                    bs = -comm.allreduce_max_int(-bs)  # identical batching on every rank
+                solver = NMFBatchSolver(X, self._solver_options(kwargs, k), comm=comm,
+                                        row_offset=row0)
                 for b0 in range(0, len(idxs), bs):
                     grp = idxs[b0:b0 + bs]
-                    for idx in grp:
-                        if verbose:
-                            print("[Worker %d]. Starting task %d." % (worker_i, idx), flush=True)
+                    if verbose:
+                        for idx in grp:
+                            print("[Worker %s]. Starting task %d." % (worker_label, idx), flush=True)
                     seeds = [int(run_params.iloc[i]["nmf_seed"]) for i in grp]
                     t0 = time.perf_counter()
-                    res = solvers[k].run(seeds)
+                    res = solver.run(seeds)
                     W = res.W.cpu().numpy()
                     wall = time.perf_counter() - t0
                     for r, idx in enumerate(grp):
                         it = int(run_params.iloc[idx]["iter"])
-                        spectra = pd.DataFrame(W[r * k:(r + 1) * k],
-                                               index=np.arange(1, k + 1), columns=genes)
-                        save_df_to_npz(spectra, self.paths["iter_spectra"] % (k, it))
+                        if writer:
+                            spectra = pd.DataFrame(W[r * k:(r + 1) * k],
+                                                   index=np.arange(1, k + 1), columns=genes)
+                            save_df_to_npz(spectra, self.paths["iter_spectra"] % (k, it))
+                            append_jsonl(self.paths["replicate_log"], {
+                                "k": k, "iter": it, "seed": seeds[r], "worker": worker_label,
+                                "err": float(res.err[r]), "n_pass": int(res.n_iter[r]),
+                                "converged": bool(res.converged[r]),
+                                "h_inner_iters": int(res.stats["h_inner_iters"][r]),
+                                "w_inner_iters": int(res.stats["w_inner_iters"][r]),
+                                "batch_size": len(grp), "batch_wall_s": wall,
+                                "device": str(dev),
+                                "world": 1 if comm is None else comm.world_size})
                         if save_usages:
                             us = pd.DataFrame(res.usages(r).cpu().numpy(), index=cells,
                                               columns=np.arange(1, k + 1))
-                            save_df_to_npz(us, self.paths["iter_usages"] % (k, it))
-                        append_jsonl(self.paths["replicate_log"], {
-                            "k": k, "iter": it, "seed": seeds[r], "worker": worker_i,
-                            "err": float(res.err[r]), "n_pass": int(res.n_iter[r]),
-                            "converged": bool(res.converged[r]),
-                            "h_inner_iters": int(res.stats["h_inner_iters"][r]),
-                            "w_inner_iters": int(res.stats["w_inner_iters"][r]),
-                            "batch_size": len(grp), "batch_wall_s": wall,
-                            "device": str(dev)})
+                            fn = self.paths["iter_usages"] % (k, it)
+                            if comm is not None and comm.world_size > 1:
+                                fn = fn.replace(".df.npz", ".rank%d.df.npz" % comm.rank)
+                            save_df_to_npz(us, fn)
                         written += 1
                         if fault_after and written >= fault_after:
                             raise RuntimeError(

@@ -1,0 +1,279 @@
+"""Harmony batch correction on the device (C30, C37; preprocess.py:9-18, 342-388).
+
+The reference calls ``harmonypy.run_harmony`` (not installed here) and then applies the
+mixture-of-experts ridge correction to the *expression* matrix.  This module re-derives
+the published algorithm (Korsunsky et al. 2019) with the harmonypy conventions:
+
+* Z_cos = cosine-normalised PCs (after max-scaling), one-hot design Phi (B x N),
+  Phi_moe = [1; Phi], lamb = diag([0, lamb...]), K = min(round(N/30), 100) clusters,
+  sigma = 0.1, block_size = 0.05, window 3, eps_kmeans 1e-5, eps_harmony 1e-4;
+* init: k-means++ (sklearn KMeans(n_init=10, max_iter=25, random_state)) on Z_cos;
+* clustering: Y = normalised Z_cos R^T; dist = 2(1 - Y^T Z_cos); R updated block by
+  block in a random order (numpy RandomState(random_state), as run_harmony seeds it)
+  with the diversity penalty ((E+1)/(O+1))^theta;
+* objective = sum R*dist + sigma*sum R log R + cross-entropy term.
+
+Everything except the block order and convergence bookkeeping runs as batched tensor
+ops on the GPU.  ``moe_correct_ridge`` is batched over clusters: the K ridge systems
+are formed with two GEMMs over cells and the correction is ONE
+(features x K(B+1)) x (K(B+1) x cells) GEMM, streamed over cell chunks, instead of the
+reference's K sequential rank-(B+1) updates.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pandas as pd
+import torch
+
+
+def _design(meta: pd.DataFrame, vars_use) -> tuple[np.ndarray, np.ndarray]:
+    if isinstance(vars_use, str):
+        vars_use = [vars_use]
+    blocks, counts = [], []
+    for v in vars_use:
+        d = pd.get_dummies(meta[v].astype("category")).to_numpy().T.astype(np.float64)
+        blocks.append(d)
+        counts.append(d.shape[0])
+    return np.vstack(blocks), np.asarray(counts)
+
+
+class HarmonyResult:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def _entropy_sum(R: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
+    y = R * torch.log(R)
+    y = torch.where(torch.isfinite(y), y, torch.zeros_like(y))
+    return (y * sigma[:, None]).sum()
+
+
+class Harmony:
+    def __init__(self, Z, Phi, Phi_moe, Pr_b, sigma, theta, lamb, K, max_iter_harmony=10,
+                 max_iter_kmeans=20, epsilon_kmeans=1e-5, epsilon_harmony=1e-4,
+                 block_size=0.05, random_state=0, init_backend="sklearn", device=None,
+                 verbose=False):
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        dt = torch.float64
+        self.dev, self.dt = dev, dt
+        self.Z_orig = torch.as_tensor(np.asarray(Z), dtype=dt, device=dev)
+        self.Z_corr = self.Z_orig.clone()
+        Zc = self.Z_orig / self.Z_orig.max(dim=0).values
+        self.Z_cos = Zc / torch.linalg.vector_norm(Zc, dim=0)
+        self.Phi = torch.as_tensor(Phi, dtype=dt, device=dev)
+        self.Phi_moe = torch.as_tensor(Phi_moe, dtype=dt, device=dev)
+        self.Pr_b = torch.as_tensor(Pr_b, dtype=dt, device=dev)
+        self.sigma = torch.as_tensor(sigma, dtype=dt, device=dev)
+        self.theta = torch.as_tensor(theta, dtype=dt, device=dev)
+        self.lamb = torch.as_tensor(lamb, dtype=dt, device=dev)
+        self.K = int(K)
+        self.N = self.Z_orig.shape[1]
+        self.window_size = 3
+        self.block_size = block_size
+        self.max_iter_kmeans = max_iter_kmeans
+        self.eps_k, self.eps_h = epsilon_kmeans, epsilon_harmony
+        self.rs = np.random.RandomState(random_state)
+        self.random_state = random_state
+        self.objective_kmeans: list[float] = []
+        self.objective_harmony: list[float] = []
+        self.kmeans_rounds: list[int] = []
+        self.verbose = verbose
+        self._init_cluster(init_backend)
+        self._harmonize(max_iter_harmony)
+
+    # ------------------------------------------------------------------ init
+    def _init_cluster(self, backend: str):
+        from .consensus import kmeans as _km
+
+        X = self.Z_cos.t()
+        if backend == "sklearn":
+            from sklearn.cluster import KMeans
+
+            m = KMeans(n_clusters=self.K, init="k-means++", n_init=10, max_iter=25,
+                       random_state=self.random_state)
+            m.fit(X.cpu().numpy())
+            Y = torch.as_tensor(m.cluster_centers_.T, dtype=self.dt, device=self.dev)
+        else:
+            labels = torch.as_tensor(_km(X, self.K, n_init=10, random_state=self.random_state,
+                                         max_iter=25, backend="device"), device=self.dev)
+            onehot = (labels[None, :] == torch.arange(self.K, device=self.dev)[:, None]).to(self.dt)
+            Y = (X.t() @ onehot.t()) / onehot.sum(dim=1).clamp(min=1)[None, :]
+        self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
+        self.dist_mat = 2 * (1 - self.Y.t() @ self.Z_cos)
+        R = -self.dist_mat / self.sigma[:, None]
+        R = R - R.max(dim=0).values
+        R = torch.exp(R)
+        self.R = R / R.sum(dim=0)
+        self.E = torch.outer(self.R.sum(dim=1), self.Pr_b)
+        self.O = self.R @ self.Phi.t()
+        self._objective()
+        self.objective_harmony.append(self.objective_kmeans[-1])
+
+    def _objective(self):
+        kmeans_error = (self.R * self.dist_mat).sum()
+        ent = _entropy_sum(self.R, self.sigma)
+        x = self.R * self.sigma[:, None]
+        z = torch.log((self.O + 1) / (self.E + 1))
+        w = (self.theta[None, :] * z) @ self.Phi
+        cross = (x * w).sum()
+        self.objective_kmeans.append(float(kmeans_error + ent + cross))
+
+    # ------------------------------------------------------------------ loops
+    def _harmonize(self, iters: int):
+        for _ in range(1, iters + 1):
+            self._cluster()
+            self.Z_cos, self.Z_corr, self.W = moe_correct_ridge_pcs(
+                self.Z_orig, self.R, self.Phi_moe, self.lamb)
+            if self._converged(1):
+                break
+
+    def _cluster(self):
+        self.dist_mat = 2 * (1 - self.Y.t() @ self.Z_cos)
+        i = 0
+        for i in range(self.max_iter_kmeans):
+            Y = self.Z_cos @ self.R.t()
+            self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
+            self.dist_mat = 2 * (1 - self.Y.t() @ self.Z_cos)
+            self._update_R()
+            self._objective()
+            if i > self.window_size and self._converged(0):
+                break
+        self.kmeans_rounds.append(i)
+        self.objective_harmony.append(self.objective_kmeans[-1])
+
+    def _update_R(self):
+        sd = -self.dist_mat / self.sigma[:, None]
+        sd = sd - sd.max(dim=0).values
+        sd = torch.exp(sd)
+        order = np.arange(self.N)
+        self.rs.shuffle(order)
+        n_blocks = int(math.ceil(1 / self.block_size))
+        for b in np.array_split(order, n_blocks):
+            bi = torch.as_tensor(b, device=self.dev)
+            Rb = self.R[:, bi]
+            Pb = self.Phi[:, bi]
+            self.E -= torch.outer(Rb.sum(dim=1), self.Pr_b)
+            self.O -= Rb @ Pb.t()
+            pen = torch.pow((self.E + 1) / (self.O + 1), self.theta[None, :]) @ Pb
+            Rn = sd[:, bi] * pen
+            Rn = Rn / Rn.abs().sum(dim=0)
+            self.R[:, bi] = Rn
+            self.E += torch.outer(Rn.sum(dim=1), self.Pr_b)
+            self.O += Rn @ Pb.t()
+
+    def _converged(self, kind: int) -> bool:
+        if kind == 0:
+            ok = self.objective_kmeans
+            n = len(ok)
+            old = sum(ok[n - 2 - i] for i in range(self.window_size))
+            new = sum(ok[n - 1 - i] for i in range(self.window_size))
+            return abs(old - new) / abs(old) < self.eps_k
+        old, new = self.objective_harmony[-2], self.objective_harmony[-1]
+        return (old - new) / abs(old) < self.eps_h
+
+    def result(self) -> HarmonyResult:
+        return HarmonyResult(Z_corr=self.Z_corr.cpu().numpy(), Z_cos=self.Z_cos.cpu().numpy(),
+                             R=self.R.cpu().numpy(), K=self.K, Phi=self.Phi.cpu().numpy(),
+                             Phi_moe=self.Phi_moe.cpu().numpy(), lamb=self.lamb.cpu().numpy(),
+                             objective_harmony=list(self.objective_harmony),
+                             kmeans_rounds=list(self.kmeans_rounds), _R_t=self.R,
+                             _Phi_moe_t=self.Phi_moe, _lamb_t=self.lamb)
+
+
+def run_harmony(data_mat, meta_data: pd.DataFrame, vars_use, theta=None, lamb=None,
+                sigma=0.1, nclust=None, tau=0, block_size=0.05, max_iter_harmony=10,
+                max_iter_kmeans=20, epsilon_cluster=1e-5, epsilon_harmony=1e-4,
+                random_state=0, init_backend="sklearn", device=None, verbose=False):
+    """harmonypy.run_harmony equivalent (cells x dims or dims x cells input)."""
+    N = meta_data.shape[0]
+    Z = np.asarray(data_mat, dtype=np.float64)
+    if Z.shape[1] != N:
+        Z = Z.T
+    if Z.shape[1] != N:
+        raise ValueError("data_mat and meta_data do not have the same number of cells")
+    if nclust is None:
+        nclust = int(min(round(N / 30.0), 100))
+    sigma = np.repeat(float(sigma), nclust) if np.isscalar(sigma) else np.asarray(sigma)
+    Phi, phi_n = _design(meta_data, vars_use)
+    if theta is None:
+        theta = np.repeat([1.0] * len(phi_n), phi_n)
+    elif np.isscalar(theta):
+        theta = np.repeat([float(theta)] * len(phi_n), phi_n)
+    else:
+        theta = np.repeat(np.asarray(theta, dtype=float), phi_n)
+    if lamb is None:
+        lamb = np.repeat([1.0] * len(phi_n), phi_n)
+    elif np.isscalar(lamb):
+        lamb = np.repeat([float(lamb)] * len(phi_n), phi_n)
+    else:
+        lamb = np.repeat(np.asarray(lamb, dtype=float), phi_n)
+    N_b = Phi.sum(axis=1)
+    Pr_b = N_b / N
+    if tau > 0:
+        theta = theta * (1 - np.exp(-(N_b / (nclust * tau)) ** 2))
+    lamb_mat = np.diag(np.insert(lamb, 0, 0))
+    Phi_moe = np.vstack((np.ones((1, N)), Phi))
+    ho = Harmony(Z, Phi, Phi_moe, Pr_b, sigma, theta, lamb_mat, nclust, max_iter_harmony,
+                 max_iter_kmeans, epsilon_cluster, epsilon_harmony, block_size, random_state,
+                 init_backend, device, verbose)
+    return ho.result()
+
+
+def _ridge_weights(Z: torch.Tensor, R: torch.Tensor, Phi_moe: torch.Tensor, lamb: torch.Tensor,
+                   chunk: int = 65536) -> torch.Tensor:
+    """W_k = (Phi_Rk Phi_moe^T + lamb)^-1 Phi_Rk Z^T for all clusters; W_k[0] = 0.
+    Returns (K*(B+1), F) with Z (F x N)."""
+    K, N = R.shape
+    B1 = Phi_moe.shape[0]
+    F = Z.shape[0]
+    # sum_n R[k,n] P[b,n] P[c,n] via pair products: (K x N) @ (N x B1*B1)
+    PP = (Phi_moe[:, None, :] * Phi_moe[None, :, :]).reshape(B1 * B1, N)
+    A = (R @ PP.t()).reshape(K, B1, B1) + lamb[None]
+    Y = torch.zeros((K * B1, F), dtype=Z.dtype, device=Z.device)
+    for a in range(0, N, chunk):
+        b = min(N, a + chunk)
+        RP = (R[:, None, a:b] * Phi_moe[None, :, a:b]).reshape(K * B1, b - a)
+        Y += RP @ Z[:, a:b].t()
+    W = torch.linalg.solve(A, Y.view(K, B1, F))
+    W[:, 0, :] = 0
+    return W.reshape(K * B1, F)
+
+
+def _apply_correction(Z: torch.Tensor, W: torch.Tensor, R: torch.Tensor, Phi_moe: torch.Tensor,
+                      chunk: int = 65536) -> torch.Tensor:
+    K, N = R.shape
+    B1 = Phi_moe.shape[0]
+    out = Z.clone()
+    for a in range(0, N, chunk):
+        b = min(N, a + chunk)
+        RP = (R[:, None, a:b] * Phi_moe[None, :, a:b]).reshape(K * B1, b - a)
+        out[:, a:b] -= W.t() @ RP
+    return out
+
+
+def moe_correct_ridge_pcs(Z_orig: torch.Tensor, R: torch.Tensor, Phi_moe: torch.Tensor,
+                          lamb: torch.Tensor):
+    W = _ridge_weights(Z_orig, R, Phi_moe, lamb)
+    Z_corr = _apply_correction(Z_orig, W, R, Phi_moe)
+    Z_cos = Z_corr / torch.linalg.vector_norm(Z_corr, dim=0)
+    return Z_cos, Z_corr, W
+
+
+def moe_correct_ridge(Z_orig, Z_cos, Z_corr, R, W, K, Phi_Rk, Phi_moe, lamb, device=None,
+                      dtype=torch.float64):
+    """preprocess.py:9-18 signature: returns (Z_cos, Z_corr, W_last, Phi_Rk_last) for a
+    features x cells matrix ``Z_orig`` (numpy in, numpy out)."""
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    Zt = torch.as_tensor(np.asarray(Z_orig), dtype=dtype, device=dev)
+    Rt = torch.as_tensor(np.asarray(R), dtype=dtype, device=dev)[:int(K)]
+    Pt = torch.as_tensor(np.asarray(Phi_moe), dtype=dtype, device=dev)
+    Lt = torch.as_tensor(np.asarray(lamb), dtype=dtype, device=dev)
+    Wall = _ridge_weights(Zt, Rt, Pt, Lt)
+    Zc = _apply_correction(Zt, Wall, Rt, Pt)
+    Zcos = Zc / torch.linalg.vector_norm(Zc, dim=0)
+    B1 = Pt.shape[0]
+    W_last = Wall[(int(K) - 1) * B1:].cpu().numpy()
+    Phi_Rk = (Pt * Rt[int(K) - 1]).cpu().numpy()
+    return Zcos.cpu().numpy(), Zc.cpu().numpy(), W_last, Phi_Rk

@@ -1,0 +1,92 @@
+"""Multi-GPU stage drivers.
+
+One process per GPU (``torchrun --nproc-per-node N``), ``torch.distributed`` with
+backend ``nccl`` (RCCL over xGMI) for device work, ``gloo`` on CPU:
+
+* ``distributed_factorize`` -- replicate parallelism: every rank takes a round-robin
+  share of each K's replicates (ranks get the same K-mix, so batches stay balanced),
+  solves them as device batches and writes its spectra files; a barrier closes the
+  stage.  No collectives during the solves -- seeds are per replicate, so spectra are
+  bit-identical to a single-GPU run of the same ledger.
+* ``dp_factorize`` -- cell-sharded data parallelism for matrices too big for one GPU:
+  rank r holds a contiguous row block of norm_counts, every replicate batch runs on all
+  ranks with the per-step ``[dB | dA]`` statistics all-reduced (one RCCL call per
+  online step), rank 0 writes the (replicated) spectra.
+* fault tolerance: a restart with ``skip_completed_runs=True`` re-shards only the
+  incomplete ledger rows over the surviving world size (resume by ledger, §5.3).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from .comm import DistComm, LocalComm
+from .ledger import shard_by_k
+
+
+def init_distributed(backend: str | None = None):
+    """Initialise torch.distributed from torchrun's env vars; returns (comm, device)."""
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available() and backend != "gloo"
+    dev = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(dev)
+    if world <= 1:
+        return LocalComm(), dev
+    if not dist.is_initialized():
+        dist.init_process_group(backend=backend or ("nccl" if use_cuda else "gloo"),
+                                device_id=dev if use_cuda else None)
+    return DistComm(), dev
+
+
+def _incomplete_jobs(obj, run_params, skip_completed_runs: bool):
+    if not skip_completed_runs:
+        return list(range(len(run_params)))
+    done = [os.path.exists(obj.paths["iter_spectra"] % (int(k), int(i)))
+            for k, i in zip(run_params["n_components"], run_params["iter"])]
+    return [i for i, d in enumerate(done) if not d]
+
+
+def distributed_factorize(obj, skip_completed_runs: bool = False, replicate_batch=None,
+                          save_usages: bool = False, backend: str | None = None, verbose=True):
+    from ..utils.io import load_df_from_npz
+
+    comm, dev = init_distributed(backend)
+    run_params = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
+    jobs = _incomplete_jobs(obj, run_params, skip_completed_runs)
+    mine = shard_by_k(run_params, jobs, comm.rank, comm.world_size)
+    obj.factorize_jobs(mine, worker_label=comm.rank, device=dev,
+                       replicate_batch=replicate_batch, save_usages=save_usages,
+                       verbose=verbose, run_params=run_params)
+    comm.barrier()
+    return comm
+
+
+def row_block(n_rows: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous, balanced row block of ``rank`` (first n % world ranks get one more)."""
+    base, extra = divmod(n_rows, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def dp_factorize(obj, skip_completed_runs: bool = False, replicate_batch=None,
+                 save_usages: bool = False, backend: str | None = None, verbose=True):
+    from ..utils.h5ad import h5ad_shape
+    from ..utils.io import load_df_from_npz
+
+    comm, dev = init_distributed(backend)
+    run_params = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
+    jobs = _incomplete_jobs(obj, run_params, skip_completed_runs)
+    n_rows, _ = h5ad_shape(obj.paths["normalized_counts"])
+    rr = row_block(n_rows, comm.rank, comm.world_size)
+    obj.factorize_jobs(jobs, worker_label=comm.rank, device=dev,
+                       replicate_batch=replicate_batch, save_usages=save_usages,
+                       verbose=verbose and comm.rank == 0, run_params=run_params,
+                       comm=comm if comm.world_size > 1 else None, row_range=rr)
+    comm.barrier()
+    return comm

@@ -1,0 +1,1 @@
+"""I/O, AnnData container, RNG twin, timing, plotting, synthetic data."""

@@ -282,3 +282,12 @@ def read_X_rows(path: str, start: int, stop: int):
         data = np.asarray(f.read("/X/data", lo, hi))
         indices = np.asarray(f.read("/X/indices", lo, hi))
         return sp.csr_matrix((data, indices, indptr - lo), shape=(stop - start, shape[1]))
+
+
+def read_h5ad_annotations(path: str) -> AnnData:
+    """obs/var only (X left as None): what a cell-sharded rank needs besides its rows."""
+    lib = _lib()
+    with lib.File(str(path), "r") as f:
+        obs = _read_frame(f, "/obs")
+        var = _read_frame(f, "/var")
+    return AnnData(X=None, obs=obs, var=var)

@@ -1,0 +1,124 @@
+"""Figures: consensus clustergram (C25, cnmf.py:1160-1253), K-selection plot (C27,
+cnmf.py:1311-1332) and the Preprocess QC histograms (C32).  matplotlib, Agg backend."""
+from __future__ import annotations
+
+import numpy as np
+import pandas as pd
+
+
+def _plt():
+    import matplotlib
+
+    if matplotlib.get_backend().lower() not in ("agg", "module://matplotlib_inline.backend_inline"):
+        try:
+            matplotlib.use("Agg")
+        except Exception:
+            pass
+    import matplotlib.pyplot as plt
+
+    return plt
+
+
+def _leaf_order(dist: np.ndarray, labels: pd.Series) -> list[int]:
+    """Clusters in label order; spectra inside a cluster by average-linkage leaves."""
+    from scipy.cluster.hierarchy import leaves_list, linkage
+    from scipy.spatial.distance import squareform
+
+    order: list[int] = []
+    lab = labels.values
+    for cl in sorted(set(lab)):
+        members = np.flatnonzero(lab == cl)
+        if members.size > 1:
+            sub = squareform(dist[np.ix_(members, members)], checks=False)
+            sub[sub < 0] = 0
+            order += list(members[leaves_list(linkage(sub, "average"))])
+        else:
+            order += list(members)
+    return order
+
+
+def clustergram(dist: np.ndarray, labels: pd.Series, local_density: pd.DataFrame | None,
+                density_filter: np.ndarray | None, density_threshold: float, path: str,
+                close: bool = False):
+    from matplotlib import gridspec
+
+    plt = _plt()
+    order = _leaf_order(dist, labels)
+    D = dist[np.ix_(order, order)]
+    widths, heights = [0.5, 9, 0.5, 4, 1], [0.5, 9]
+    fig = plt.figure(figsize=(sum(widths), sum(heights)))
+    gs = gridspec.GridSpec(2, 5, fig, 0.01, 0.01, 0.98, 0.98, height_ratios=heights,
+                           width_ratios=widths, wspace=0, hspace=0)
+    ax = fig.add_subplot(gs[1, 1], xticks=[], yticks=[])
+    im = ax.imshow(D, interpolation="none", cmap="viridis", aspect="auto", rasterized=True)
+    lab = labels.values[order]
+    left = fig.add_subplot(gs[1, 0], xticks=[], yticks=[])
+    left.imshow(lab.reshape(-1, 1), interpolation="none", cmap="Spectral", aspect="auto",
+                rasterized=True)
+    top = fig.add_subplot(gs[0, 1], xticks=[], yticks=[])
+    top.imshow(lab.reshape(1, -1), interpolation="none", cmap="Spectral", aspect="auto",
+               rasterized=True)
+    hgs = gridspec.GridSpecFromSubplotSpec(3, 1, subplot_spec=gs[1, 3], wspace=0, hspace=0)
+    hax = fig.add_subplot(hgs[0, 0], title="Local density histogram")
+    if local_density is not None:
+        hax.hist(local_density.values, bins=np.linspace(0, 1, 50))
+    hax.yaxis.tick_right()
+    xl, yl = hax.get_xlim(), hax.get_ylim()
+    if density_threshold < xl[1]:
+        hax.axvline(density_threshold, linestyle="--", color="k")
+        hax.text(density_threshold + 0.02, yl[1] * 0.95, "filtering\nthreshold\n\n", va="top")
+    hax.set_xlim(xl)
+    if density_filter is not None:
+        removed = int((~density_filter).sum())
+        hax.set_xlabel("Mean distance to k nearest neighbors\n\n%d/%d (%.0f%%) spectra above "
+                       "threshold\nwere removed prior to clustering"
+                       % (removed, len(density_filter), 100 * removed / max(len(density_filter), 1)))
+    cgs = gridspec.GridSpecFromSubplotSpec(8, 1, subplot_spec=hgs[1, 0], wspace=0, hspace=0)
+    cax = fig.add_subplot(cgs[4, 0], title="Euclidean Distance")
+    fig.colorbar(im, cax=cax, ticks=np.linspace(float(D.min()), float(D.max()), 3),
+                 orientation="horizontal")
+    from .io import atomic_path
+
+    with atomic_path(path, suffix=".png") as tmp:
+        fig.savefig(tmp, dpi=250)
+    if close:
+        plt.close(fig)
+    return fig
+
+
+def k_selection(stats: pd.DataFrame, path: str, close: bool = False):
+    plt = _plt()
+    fig = plt.figure(figsize=(6, 4))
+    ax1 = fig.add_subplot(111)
+    ax2 = ax1.twinx()
+    ax1.plot(stats.k, stats.silhouette, "o-", color="b")
+    ax1.set_ylabel("Stability", color="b", fontsize=15)
+    for t in ax1.get_yticklabels():
+        t.set_color("b")
+    ax2.plot(stats.k, stats.prediction_error, "o-", color="r")
+    ax2.set_ylabel("Error", color="r", fontsize=15)
+    for t in ax2.get_yticklabels():
+        t.set_color("r")
+    ax1.set_xlabel("Number of Components", fontsize=15)
+    ax1.grid(True)
+    plt.tight_layout()
+    from .io import atomic_path
+
+    with atomic_path(path, suffix=".png") as tmp:
+        fig.savefig(tmp, dpi=250)
+    if close:
+        plt.close(fig)
+    return fig
+
+
+def count_hist(X, num_cells: int = 1000, title="Quantile thresholded normalized count distribution"):
+    import scipy.sparse as sp
+
+    plt = _plt()
+    z = X[:num_cells]
+    z = z.toarray() if sp.issparse(z) else np.asarray(z)
+    y = z.reshape(-1)
+    fig, ax = plt.subplots()
+    ax.hist(y[y > 0], bins=100)
+    ax.set_title(title)
+    return fig

@@ -1,0 +1,63 @@
+"""Tracing / observability.
+
+* ``StageTimer`` -- wall-clock per pipeline stage, with device synchronisation so GPU
+  work is attributed to the stage that launched it; ``CNMF_TRACE=1`` prints each stage.
+* ``append_jsonl`` -- per-replicate solver records (K, seed, passes, inner iterations,
+  final loss, convergence, batch wall time) appended next to the ledger.
+* ``record_function`` ranges show up in torch.profiler / rocprofv3 ``--marker-trace``.
+"""
+from __future__ import annotations
+
+import contextlib
+import json
+import os
+import threading
+import time
+from collections import defaultdict
+
+import torch
+
+_lock = threading.Lock()
+
+
+def _sync():
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+
+
+class StageTimer:
+    def __init__(self):
+        self.totals: dict[str, float] = defaultdict(float)
+        self.counts: dict[str, int] = defaultdict(int)
+
+    @contextlib.contextmanager
+    def __call__(self, name: str):
+        _sync()
+        t0 = time.perf_counter()
+        with torch.autograd.profiler.record_function(f"cnmf::{name}"):
+            try:
+                yield
+            finally:
+                _sync()
+                dt = time.perf_counter() - t0
+                self.totals[name] += dt
+                self.counts[name] += 1
+                if os.environ.get("CNMF_TRACE") == "1":
+                    print(f"[cnmf trace] {name}: {dt:.3f} s", flush=True)
+
+    def summary(self) -> dict:
+        return {k: {"seconds": round(v, 6), "calls": self.counts[k]} for k, v in self.totals.items()}
+
+
+def append_jsonl(path: str, record: dict) -> None:
+    line = json.dumps(record, sort_keys=True) + "\n"
+    with _lock:
+        with open(path, "a") as fh:
+            fh.write(line)
+
+
+def read_jsonl(path: str) -> list[dict]:
+    if not os.path.exists(path):
+        return []
+    with open(path) as fh:
+        return [json.loads(l) for l in fh if l.strip()]

@@ -1,0 +1,166 @@
+"""End-to-end CPU pipeline (BASELINE.json config 1: 1k cells x 500 genes, K=5, n_iter=5)
+plus resume / worker sharding / CLI behaviour the reference never tested."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from cnmf_torch_amd import cNMF, load_df_from_npz, save_df_to_npz
+from cnmf_torch_amd.utils.synthetic import simulate_counts
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def counts_file(tmp_path_factory):
+    d = tmp_path_factory.mktemp("data")
+    X, cells, genes, U, S = simulate_counts(1000, 500, 5, seed=3, sparse=False, return_truth=True)
+    fn = d / "counts.df.npz"
+    save_df_to_npz(pd.DataFrame(X, index=cells, columns=genes), str(fn))
+    return str(fn), S, genes
+
+
+@pytest.fixture(scope="module")
+def run_dir(tmp_path_factory, counts_file):
+    out = tmp_path_factory.mktemp("run")
+    obj = cNMF(output_dir=str(out), name="sim")
+    obj.prepare(counts_file[0], components=[4, 5, 6], n_iter=6, seed=14, num_highvar_genes=300,
+                batch_size=400)
+    obj.factorize(worker_i=0, total_workers=1)
+    obj.combine()
+    return obj
+
+
+def test_factorize_outputs(run_dir):
+    obj = run_dir
+    for k in (4, 5, 6):
+        for it in range(6):
+            assert os.path.exists(obj.paths["iter_spectra"] % (k, it))
+        merged = load_df_from_npz(obj.paths["merged_spectra"] % k)
+        assert merged.shape[0] == 6 * k
+        assert merged.index[0] == "iter0_topic1"
+        assert (merged.values >= 0).all()
+    log = [l for l in open(obj.paths["replicate_log"])]
+    assert len(log) == 18
+
+
+def test_consensus_artifacts_and_recovery(run_dir, counts_file):
+    obj = run_dir
+    obj.consensus(5, density_threshold=0.5, show_clustering=True, close_clustergram_fig=True)
+    dt = "0_5"
+    p = obj.paths
+    for key in ("consensus_spectra", "consensus_usages", "gene_spectra_tpm", "gene_spectra_score",
+                "starcat_spectra"):
+        assert os.path.exists(p[key] % (5, dt)), key
+    for key in ("consensus_spectra__txt", "consensus_usages__txt", "gene_spectra_tpm__txt",
+                "gene_spectra_score__txt", "starcat_spectra__txt", "clustering_plot"):
+        assert os.path.exists(p[key] % (5, dt)), key
+    usage, scores, tpm_spectra, top = obj.load_results(5, 0.5, n_top_genes=20)
+    assert usage.shape == (1000, 5)
+    np.testing.assert_allclose(usage.sum(axis=1).values, 1.0, rtol=1e-6)
+    assert top.shape == (20, 5)
+    # planted programs are recovered: each true program matches a consensus GEP
+    _, S_true, genes = counts_file
+    gt = pd.DataFrame(S_true, columns=genes)
+    est = tpm_spectra.T
+    A = gt.values / np.linalg.norm(gt.values, axis=1, keepdims=True)
+    B = est[gt.columns].values
+    B = B / np.linalg.norm(B, axis=1, keepdims=True)
+    sims = A @ B.T
+    from scipy.optimize import linear_sum_assignment
+
+    r, c = linear_sum_assignment(-sims)
+    assert sims[r, c].min() > 0.9, sims[r, c]
+    starcat = load_df_from_npz(p["starcat_spectra"] % (5, dt))
+    assert list(starcat.index) == [f"GEP{i}" for i in range(1, 6)]
+
+
+def test_k_selection(run_dir):
+    stats = run_dir.k_selection_plot(close_fig=True)
+    assert list(stats.k) == [4, 5, 6]
+    assert os.path.exists(run_dir.paths["k_selection_plot"])
+    assert (stats.prediction_error > 0).all()
+    assert stats.silhouette.between(-1, 1).all()
+
+
+def test_resume_and_worker_sharding(tmp_path, counts_file):
+    obj = cNMF(output_dir=str(tmp_path), name="res")
+    obj.prepare(counts_file[0], components=[5], n_iter=4, seed=1, num_highvar_genes=200)
+    # worker 1 of 2 takes the odd ledger rows only
+    obj.factorize(worker_i=1, total_workers=2)
+    made = [os.path.exists(obj.paths["iter_spectra"] % (5, i)) for i in range(4)]
+    assert made == [False, True, False, True]
+    obj.update_nmf_iter_params()
+    rp = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
+    assert rp["completed"].astype(bool).tolist() == made
+    obj.factorize(skip_completed_runs=True)
+    assert all(os.path.exists(obj.paths["iter_spectra"] % (5, i)) for i in range(4))
+
+
+def test_replicate_batching_invariance(tmp_path, counts_file):
+    """Same seed -> same spectra whether solved alone or inside a batch."""
+    obj = cNMF(output_dir=str(tmp_path), name="inv")
+    obj.prepare(counts_file[0], components=[5], n_iter=3, seed=2, num_highvar_genes=200)
+    obj.factorize(replicate_batch=3)
+    a = [load_df_from_npz(obj.paths["iter_spectra"] % (5, i)).values for i in range(3)]
+    for i in range(3):
+        os.remove(obj.paths["iter_spectra"] % (5, i))
+    obj.factorize(replicate_batch=1)
+    b = [load_df_from_npz(obj.paths["iter_spectra"] % (5, i)).values for i in range(3)]
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-6)
+
+
+def test_fault_injection_then_resume(tmp_path, counts_file, monkeypatch):
+    obj = cNMF(output_dir=str(tmp_path), name="fault")
+    obj.prepare(counts_file[0], components=[5], n_iter=4, seed=3, num_highvar_genes=200)
+    monkeypatch.setenv("CNMF_FAULT_AFTER_REPLICATES", "2")
+    with pytest.raises(RuntimeError, match="injected failure"):
+        obj.factorize(replicate_batch=4)
+    monkeypatch.delenv("CNMF_FAULT_AFTER_REPLICATES")
+    obj.update_nmf_iter_params()
+    rp = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
+    assert int(rp["completed"].astype(bool).sum()) == 2
+    obj.factorize(skip_completed_runs=True)
+    obj.combine()
+    assert load_df_from_npz(obj.paths["merged_spectra"] % 5).shape[0] == 20
+    # no temp files left behind by atomic writes
+    assert not [f for f in os.listdir(os.path.dirname(obj.paths["iter_spectra"]))
+                if f.startswith(".tmp_")]
+
+
+def test_combine_skip_missing(tmp_path, counts_file):
+    obj = cNMF(output_dir=str(tmp_path), name="miss")
+    obj.prepare(counts_file[0], components=[5], n_iter=3, seed=4, num_highvar_genes=200)
+    obj.factorize(worker_i=0, total_workers=3)
+    with pytest.raises(FileNotFoundError):
+        obj.combine()
+    obj.combine(skip_missing_files=True)
+    assert load_df_from_npz(obj.paths["merged_spectra"] % 5).shape[0] == 5
+
+
+def test_cli_end_to_end(tmp_path, counts_file):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    base = [sys.executable, "-m", "cnmf_torch_amd"]
+    common = ["--output-dir", str(tmp_path), "--name", "cli"]
+
+    def run(*a):
+        r = subprocess.run(base + list(a) + common, env=env, capture_output=True, text=True,
+                           timeout=600)
+        assert r.returncode == 0, r.stdout + r.stderr
+        return r.stdout
+
+    run("prepare", "-c", counts_file[0], "-k", "4", "5", "-n", "6", "--seed", "7",
+        "--numgenes", "200")
+    out = run("factorize", "--worker-index", "0", "--total-workers", "1")
+    assert "[Worker 0]. Starting task 0." in out
+    run("combine")
+    run("consensus", "-k", "5", "--local-density-threshold", "2.0", "--show-clustering")
+    run("k_selection_plot")
+    d = tmp_path / "cli"
+    assert (d / "cli.spectra.k_5.dt_2_0.consensus.txt").exists()
+    assert (d / "cli.clustering.k_5.dt_2_0.png").exists()
+    assert (d / "cli.k_selection.png").exists()
