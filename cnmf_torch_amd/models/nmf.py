@@ -310,8 +310,12 @@ class NMFBatchSolver:
     """Solve R replicates (same X, same K, different seeds) together."""
 
     def __init__(self, X: torch.Tensor, opts: NMFOptions, comm=None, row_offset: int = 0,
-                 profile: bool = False):
+                 profile: bool = False, schedule=None):
         opts.validate()
+        # optional explicit online schedule: list of steps, each a list of (row_start,
+        # row_end) blocks solved independently before one W update (used to emulate the
+        # cell-sharded schedule in a single process)
+        self.schedule = schedule
         self.opts = opts
         self.comm = comm or LocalComm()
         self.X = X if X.dtype == opts.dtype else X.to(opts.dtype)
@@ -350,6 +354,13 @@ class NMFBatchSolver:
                          K=K, stats=stats)
 
     # ------------------------------------------------------------------ helpers
+    def _steps(self, N: int):
+        if self.schedule is not None:
+            return self.schedule
+        c = max(1, int(self.opts.online_chunk_size))
+        n_steps = self.comm.allreduce_max_int((N + c - 1) // c)
+        return [[blk] for blk in _chunks(N, c, n_steps)]
+
     def _check_convergence(self, st: _Batch, err_now: torch.Tensor, step: int,
                            final: bool) -> None:
         """Update per-replicate errors (positions < n_act), retire converged ones."""
@@ -410,9 +421,7 @@ class NMFBatchSolver:
         X = self.X
         N, G = X.shape
         dev, dt = X.device, X.dtype
-        c = max(1, int(o.online_chunk_size))
-        n_steps = comm.allreduce_max_int((N + c - 1) // c)
-        chunks = _chunks(N, c, n_steps)
+        steps = self._steps(N)
         algo = o.algo
         cmode = 1 if o.online_inner_conv == "loss" else 0
         exact = o.online_stats == "exact"
@@ -456,9 +465,12 @@ class NMFBatchSolver:
             quad = torch.zeros(n, device=dev, dtype=torch.float32)
             it_h = torch.zeros(n, device=dev, dtype=torch.int32)
             it_w = torch.zeros(n, device=dev, dtype=torch.int32)
-            for s, (a, b) in enumerate(chunks):
-                cw = b - a
-                if cw > 0:
+            for s, blocks in enumerate(steps):
+                first = True
+                for (a, b) in blocks:
+                    cw = b - a
+                    if cw <= 0:
+                        continue
                     xc = X[a:b]
                     hview = H3[:, :, a:b]                                # (n, K, cw) strided
                     h_old = hview.clone() if exact else None
@@ -471,19 +483,25 @@ class NMFBatchSolver:
                     st.h_iters[:n] += it_h.to(torch.int64)
                     if exact:
                         # replace the chunk's old contribution: d = h_new - h_old
-                        torch.bmm(hview, hview.transpose(1, 2), out=dA)
-                        dA -= torch.bmm(h_old, h_old.transpose(1, 2))
-                        h_old.neg_().add_(hview)
-                        torch.mm(h_old.view(n * K, cw), xc, out=dB)      # (n*K, G) GEMM
+                        hh = torch.bmm(hview, hview.transpose(1, 2))
+                        hh -= torch.bmm(h_old, h_old.transpose(1, 2))
+                        hlhs = h_old.neg_().add_(hview).view(n * K, cw)
                     else:
-                        torch.mm(HT[:, a:b], xc, out=dB)                 # (n*K, G) GEMM
-                        torch.bmm(hview, hview.transpose(1, 2), out=dA)
-                else:
+                        hh = torch.bmm(hview, hview.transpose(1, 2))
+                        hlhs = HT[:, a:b]
+                    if first:
+                        torch.mm(hlhs, xc, out=dB)                       # (n*K, G) GEMM
+                        dA.copy_(hh)
+                        first = False
+                    else:
+                        dB.addmm_(hlhs, xc)
+                        dA += hh
+                if first:
                     flat.zero_()
                 comm.allreduce_(flat)
                 B += dB
                 A += dA
-                last = s == len(chunks) - 1
+                last = s == len(steps) - 1
                 ops.solve(algo, W3, B.view(n, K, G), _as(A, dt),
                           max_iter=o.online_chunk_max_iter, tol=o.online_w_tol,
                           l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
@@ -563,9 +581,7 @@ class NMFBatchSolver:
         K = st.K
         X = self.X
         N, G = X.shape
-        c = max(1, int(o.online_chunk_size))
-        n_steps = comm.allreduce_max_int((N + c - 1) // c)
-        chunks = _chunks(N, c, n_steps)
+        steps = self._steps(N)
         self._init_err(st)
         g = self._beta_gamma()
         for p in range(int(o.online_max_pass)):
@@ -576,10 +592,12 @@ class NMFBatchSolver:
             W3 = W.view(n, K, G)
             num_acc = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
             den_acc = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
-            for (a, b) in chunks:
-                cw = b - a
+            for blocks in steps:
                 flat = torch.zeros(2 * n * K * G, device=X.device, dtype=X.dtype)
-                if cw > 0:
+                for (a, b) in blocks:
+                    cw = b - a
+                    if cw <= 0:
+                        continue
                     xc = X[a:b]
                     h = HT[:, a:b].reshape(n, K, cw).transpose(1, 2).contiguous()
                     active = torch.ones(n, dtype=torch.bool)
@@ -598,8 +616,8 @@ class NMFBatchSolver:
                     HT[:, a:b] = h.transpose(1, 2).reshape(n * K, cw)
                     WH = torch.bmm(h, W3)
                     nW, dW = _beta_num_den(xc, WH, h.transpose(1, 2), self.beta, o.eps, side="w")
-                    flat[:n * K * G] = nW.reshape(-1)
-                    flat[n * K * G:] = dW.expand(n, K, G).reshape(-1)
+                    flat[:n * K * G] += nW.reshape(-1)
+                    flat[n * K * G:] += dW.expand(n, K, G).reshape(-1)
                 comm.allreduce_(flat)
                 num_acc += flat[:n * K * G].view(n, K, G)
                 den_acc += flat[n * K * G:].view(n, K, G)

@@ -1,0 +1,62 @@
+"""Worker entry points for multi-process tests (spawned with torch.multiprocessing)."""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["RANK"] = str(rank)
+    os.environ["WORLD_SIZE"] = str(world)
+    os.environ["LOCAL_RANK"] = str(rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+
+
+def dp_solver_worker(rank, world, port, X, K, seeds, opts_kw, out_dir):
+    _init(rank, world, port)
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.parallel.comm import DistComm
+    from cnmf_torch_amd.parallel.runner import row_block
+
+    a, b = row_block(X.shape[0], rank, world)
+    Xl = torch.from_numpy(X[a:b])
+    solver = NMFBatchSolver(Xl, NMFOptions(n_components=K, **opts_kw), comm=DistComm(),
+                            row_offset=a)
+    res = solver.run(seeds)
+    np.save(os.path.join(out_dir, f"W{rank}.npy"), res.W.numpy())
+    np.save(os.path.join(out_dir, f"HT{rank}.npy"), res.HT.numpy())
+    np.save(os.path.join(out_dir, f"err{rank}.npy"), res.err)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def factorize_worker(rank, world, port, output_dir, name, mode):
+    _init(rank, world, port)
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.parallel.runner import distributed_factorize, dp_factorize
+
+    obj = cNMF(output_dir=output_dir, name=name)
+    if mode == "replicate":
+        distributed_factorize(obj, backend="gloo", verbose=False)
+    else:
+        dp_factorize(obj, backend="gloo", verbose=False)
+    dist.destroy_process_group()
+
+
+def comm_worker(rank, world, port, out_dir):
+    _init(rank, world, port)
+    from cnmf_torch_amd.parallel.comm import DistComm
+
+    c = DistComm()
+    t = torch.full((5,), float(rank + 1))
+    c.allreduce_(t)
+    s = c.allreduce_scalar(rank + 0.5)
+    m = c.allreduce_max_int(rank * 10)
+    g = c.all_gather_object({"r": rank})
+    np.save(os.path.join(out_dir, f"comm{rank}.npy"),
+            np.array([t[0].item(), s, m, len(g), g[world - 1]["r"]]))
+    dist.destroy_process_group()
