@@ -76,7 +76,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           l1_num: float = 0.0, l1_den: float = 0.0, l2: float = 0.0, eps: float = 1e-16,
           lin_out: torch.Tensor | None = None, quad_out: torch.Tensor | None = None,
           iters_out: torch.Tensor | None = None, nsplit: int = 1, conv_mode: int = 0,
-          check_every: int = 10) -> None:
+          check_every: int = 10, variant: str = "auto") -> None:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -84,6 +84,8 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     ``nsplit > 1`` runs a single fixed step with columns split over blocks (batch mode).
     ``conv_mode`` 0: stop when ||dx||/(||x||+eps) < tol (checked every step);
     1: stop when the block objective's relative change over ``check_every`` steps < tol.
+    ``variant``: 'auto' (register-resident kernel when the block fits, else streaming),
+    'stream' or 'reg' (tests / A-B benchmarks).
     """
     a = ALGOS[algo]
     R, K, n = x.shape
@@ -129,7 +131,8 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             lin_out.data_ptr() if lin_out is not None else 0,
             quad_out.data_ptr() if quad_out is not None else 0,
             iters_out.data_ptr() if iters_out is not None else 0, int(max(1, nsplit)),
-            int(conv_mode), int(check_every), int(threads), _stream_ptr(x))
+            int(conv_mode), int(check_every), int(threads),
+            {"auto": 0, "stream": 1, "reg": 2}[variant], _stream_ptr(x))
 
 
 # ----------------------------------------------------------------------------- init

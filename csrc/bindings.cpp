@@ -25,18 +25,19 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("solve_max_k", []() { return cnmf_solve_max_k(); });
   m.def("solve_max_threads", [](int K) { return cnmf_solve_max_threads(K); });
+  m.def("solve_reg_max_cols", [](int K) { return cnmf_solve_reg_max_cols(K); });
 
   m.def("solve",
         [](int algo, int K, uintptr_t x, long long x_rs, long long ldx, uintptr_t numer,
            long long n_rs, long long ldn, uintptr_t gram, long long g_rs, uintptr_t rep_index,
            int nblocks, int ncols, int max_iter, float tol, float l1_num, float l1_den, float l2,
            float eps, uintptr_t lin_out, uintptr_t quad_out, uintptr_t iters_out, int nsplit,
-           int conv_mode, int check_every, int threads, uintptr_t stream) {
+           int conv_mode, int check_every, int threads, int variant, uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
                            max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
                            P<float>(quad_out), P<int>(iters_out), nsplit, conv_mode,
-                           check_every, threads,
+                           check_every, threads, variant,
                            reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");
         });

@@ -1,17 +1,16 @@
 // Fused, replicate-batched NNLS-style inner solvers for NMF.
 //
-// Both halves of a Frobenius NMF step reduce to the same problem
-//     minimise_x  ||numer - Gram x|| style updates, independently per column j,
-// with a convergence test on the WHOLE (replicate, chunk) block:
+// Both halves of a Frobenius NMF step reduce to the same problem, independently per
+// column j, with a convergence test on the WHOLE (replicate, chunk) block:
 //   H-side  (cnmf.py:352-381 fit_H_online; nmf-torch online H step):
 //       x = h^T (K x c), numer = W x^T (K x c), Gram = W W^T
 //   W-side  (nmf-torch online/batch W step):
 //       x = W (K x G),   numer = B = sum h^T x,  Gram = A = sum h^T h
-// One workgroup owns one replicate's block, iterates the update in-place from L2,
-// reduces ||dx|| and ||x|| on device and stops when ||dx||/(||x||+eps) < tol.  There
-// is no per-iteration kernel launch and no host sync (the reference syncs every
-// iteration at cnmf.py:377).  A grid covers every active replicate of a batch, so one
-// launch drives the whole replicate grid.
+// One workgroup owns one replicate's block and iterates the update in place (the block
+// stays L2-resident), reducing ||dx||, ||x|| or the block objective on device.  There is
+// no per-iteration kernel launch and no host sync (the reference syncs every iteration
+// at cnmf.py:377).  A grid covers every active replicate of a batch, so one launch
+// drives the whole replicate grid.
 //
 // ALGO 0 = multiplicative update (MU):  x <- x * numer / (Gram x + l2 x + l1_den),
 //          rate := 0 where the denominator < eps (cnmf.py:370-372).
@@ -19,73 +18,140 @@
 //          x_k <- max(0, x_k + (numer_k - l1_den - (Gram x)_k - l2 x_k) / (Gram_kk + l2)).
 // Optional epilogue: lin_out[r] = <numer, x>, quad_out[r] = sum_j x_j^T Gram x_j, which
 // give the exact Frobenius loss from sufficient statistics (trace trick, G7).
+//
+// Memory path: each sweep a thread handles U columns at a time and issues all 2*U*K
+// loads of the group before any arithmetic (U*K loads in flight per lane hide the L2
+// latency that dominated the one-column-at-a-time version: 273 us/solve in
+// profiles/r1_bench_v0_kernel_stats.txt).  Loads/stores are buffer operations: the
+// column is the per-lane VGPR offset, component k*ld the SGPR soffset, so the K
+// addresses of a column cost no VGPRs.  Gram products read one LDS row per component
+// (every lane the same word: broadcast), row by row behind a compiler memory fence and
+// an opaque LDS base, so the K*K loop-invariant Gram values are never hoisted into
+// registers (that hoisting spilled hundreds of VGPRs at K >= 7).
 #include <hip/hip_runtime.h>
 #include "common.h"
+#include "solve_params.h"
 
 namespace cnmf {
 
-struct SolveParams {
-  float* x;
-  long long x_rs, ldx;
-  const float* numer;
-  long long n_rs, ldn;
-  const float* gram;
-  long long g_rs;
-  const int* rep_index;
-  int ncols, max_iter;
-  float tol, l1_num, l1_den, l2, eps;
-  float* lin_out;
-  float* quad_out;
-  int* iters_out;
-  int nsplit;       // >1: blockIdx.y splits the columns; single fixed step, no convergence test
-  int conv_mode;    // 0: ||dx||/(||x||+eps) < tol after every step (cnmf.py:375-378)
-                    // 1: block objective checked every `check_every` steps,
-                    //    |f_prev - f| / |f_prev| < tol  (nmf-torch online inner loops)
-  int check_every;
+template <int K>
+constexpr int solve_max_threads() { return 1024; }
+
+// Columns per thread per group: keep ~(2U+1)K live floats well under the 128-VGPR cap.
+template <int K>
+constexpr int cols_per_group() { return (20 / K) < 1 ? 1 : ((20 / K) > 4 ? 4 : (20 / K)); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+
+#define CNMF_MEMBAR() asm volatile("" ::: "memory")
+
+// raw_buffer_{load,store}_b32 move 32-bit integers: bit-cast, never value-convert.
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+__device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
+}
+
+// A zero the compiler cannot see through, produced inside the column loop: indexing the
+// LDS Gram with it stops LICM from hoisting all K*K loop-invariant Gram reads into
+// registers (K*K VGPRs -> spills at K >= 7).  Every lane reads the same LDS word.
+typedef __attribute__((address_space(3))) float lds_float;
+
+__device__ __forceinline__ const lds_float* opaque(const lds_float* p) {
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+template <int K, int U>
+struct ColGroup {
+  float x[U][K];
+  float n[U][K];
+  int vo[U];
+  bool ok[U];
 };
+
+template <int K, int U>
+__device__ __forceinline__ void load_group(ColGroup<K, U>& cg, int j, int T, int end,
+                                           __amdgpu_buffer_rsrc_t rx, int sx,
+                                           __amdgpu_buffer_rsrc_t rn, int sn, float l1n) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = j + u * T;
+    cg.ok[u] = c < end;
+    cg.vo[u] = cg.ok[u] ? c * 4 : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      cg.x[u][k] = buf_ld(rx, cg.vo[u], k * sx);
+      cg.n[u][k] = buf_ld(rn, cg.vo[u], k * sn);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      cg.x[u][k] = cg.ok[u] ? cg.x[u][k] : 0.f;
+      float t = cg.ok[u] ? cg.n[u][k] : 0.f;
+      if (l1n > 0.f) t = fmaxf(t - l1n, 0.f);
+      cg.n[u][k] = t;
+    }
+  }
+}
 
 // Block objective (x2, dropping the constant ||X||^2):
 //   f(x) = sum_j x_j^T Gram x_j - 2 numer_j . x_j + 2 l1 |x_j|_1 + l2 |x_j|^2
-template <int K>
-__device__ __forceinline__ float block_objective(const float* __restrict__ x, long long ldx,
-                                                 const float* __restrict__ nu, long long ldn,
-                                                 const float* sG, int j0, int n, float l1_num,
+template <int K, int U>
+__device__ __forceinline__ float block_objective(__amdgpu_buffer_rsrc_t rx, int sx,
+                                                 __amdgpu_buffer_rsrc_t rn, int sn,
+                                                 const lds_float* sG, int j0, int n, float l1_num,
                                                  float l1, float l2, float* sred) {
   float q = 0.f, l = 0.f;
-  for (int j = j0 + threadIdx.x; j < n; j += blockDim.x) {
-    float xv[K];
+  const int T = blockDim.x;
+  for (int j = j0 + threadIdx.x; j < n; j += U * T) {
+    CNMF_MEMBAR();
+    ColGroup<K, U> cg;
+    load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, l1_num);
+    const lds_float* gz = opaque(sG);
 #pragma unroll
-    for (int k = 0; k < K; ++k) xv[k] = x[k * ldx + j];
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      float gx = 0.f;
+      for (int k = 0; k < K; ++k) {
+        CNMF_MEMBAR();
+        float gx = 0.f;
 #pragma unroll
-      for (int kk = 0; kk < K; ++kk) gx = fmaf(sG[k * K + kk], xv[kk], gx);
-      float t = nu[k * ldn + j];
-      if (l1_num > 0.f) t = fmaxf(t - l1_num, 0.f);
-      q = fmaf(xv[k], gx + l2 * xv[k], q);
-      l = fmaf(xv[k], t - l1, l);
+        for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], cg.x[u][kk], gx);
+        q = fmaf(cg.x[u][k], gx + l2 * cg.x[u][k], q);
+        l = fmaf(cg.x[u][k], cg.n[u][k] - l1, l);
+      }
     }
   }
   block_sum2(q, l, sred);
   return q - 2.f * l;
 }
 
-template <int K>
-constexpr int solve_max_threads() { return K <= 16 ? 1024 : 512; }
-
 template <int K, int ALGO>
-__global__ __launch_bounds__(solve_max_threads<K>()) void solve_kernel(SolveParams p) {
-  __shared__ float sG[K * K];
+__global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
+  constexpr int U = cols_per_group<K>();
+  __shared__ float sGm[K * K];
   __shared__ float sred[2 * 16];
+  const lds_float* sG = (const lds_float*)sGm;  // LDS (addrspace 3): ds_read, 32-bit address
   const int rep = p.rep_index ? p.rep_index[blockIdx.x] : (int)blockIdx.x;
   float* __restrict__ x = p.x + (long long)rep * p.x_rs;
   const float* __restrict__ nu = p.numer + (long long)rep * p.n_rs;
   const float* __restrict__ g = p.gram + (long long)rep * p.g_rs;
-  for (int i = threadIdx.x; i < K * K; i += blockDim.x) sG[i] = g[i];
+  for (int i = threadIdx.x; i < K * K; i += blockDim.x) sGm[i] = g[i];
   __syncthreads();
 
-  const long long ldx = p.ldx, ldn = p.ldn;
+  const __amdgpu_buffer_rsrc_t rx = rsrc_of(x);
+  const __amdgpu_buffer_rsrc_t rn = rsrc_of(nu);
+  const int sx = (int)(p.ldx * 4), sn = (int)(p.ldn * 4);
+  const int T = blockDim.x;
   // Column range of this block: the whole block (nsplit == 1) or one of nsplit slices.
   int j0 = 0, n = p.ncols;
   if (p.nsplit > 1) {
@@ -96,84 +162,96 @@ __global__ __launch_bounds__(solve_max_threads<K>()) void solve_kernel(SolvePara
   const bool check_conv = p.nsplit <= 1;
   const bool loss_conv = check_conv && p.conv_mode == 1;
   const int every = p.check_every > 0 ? p.check_every : 1;
+  const float l1 = p.l1_den, l2 = p.l2, eps = p.eps;
   float f_prev = 0.f;
   bool have_prev = false;
   int it = 0;
   while (true) {
     if (loss_conv && it % every == 0) {
-      const float f = block_objective<K>(x, ldx, nu, ldn, sG, j0, n, p.l1_num, p.l1_den, p.l2,
-                                         sred);
+      const float f = block_objective<K, U>(rx, sx, rn, sn, sG, j0, n, p.l1_num, l1, l2, sred);
       if (have_prev && fabsf(f_prev - f) <= p.tol * fabsf(f_prev)) break;
       f_prev = f;
       have_prev = true;
     }
     if (it >= p.max_iter) break;
     float d2 = 0.f, x2 = 0.f;
-    for (int j = j0 + threadIdx.x; j < n; j += blockDim.x) {
-      float xv[K], nv[K];
+    for (int j = j0 + threadIdx.x; j < n; j += U * T) {
+      CNMF_MEMBAR();
+      ColGroup<K, U> cg;
+      load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, p.l1_num);
+      const lds_float* gz = opaque(sG);
 #pragma unroll
-      for (int k = 0; k < K; ++k) xv[k] = x[k * ldx + j];
+      for (int u = 0; u < U; ++u) {
+        if (ALGO == 0) {
+          // Jacobi step, row-wise: xn_k from the OLD x, written back after all k
+          float xn[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        float t = nu[k * ldn + j];
-        if (p.l1_num > 0.f) t = fmaxf(t - p.l1_num, 0.f);
-        nv[k] = t;
+          for (int k = 0; k < K; ++k) {
+            CNMF_MEMBAR();
+            float den = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk) den = fmaf(gz[k * K + kk], cg.x[u][kk], den);
+            den = fmaf(l2, cg.x[u][k], den) + l1;
+            xn[k] = (den < eps) ? 0.f : cg.x[u][k] * (cg.n[u][k] * __builtin_amdgcn_rcpf(den));
+          }
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            const float d = xn[k] - cg.x[u][k];
+            d2 = fmaf(d, d, d2);
+            x2 = fmaf(cg.x[u][k], cg.x[u][k], x2);
+            cg.x[u][k] = xn[k];
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < K; ++k) {
+            CNMF_MEMBAR();
+            float gx = 0.f;
+#pragma unroll
+            for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], cg.x[u][kk], gx);
+            const float diag = gz[k * K + k] + l2;
+            const float old = cg.x[u][k];
+            float xn = old;
+            if (diag > eps) xn = fmaxf(old + (cg.n[u][k] - l1 - gx - l2 * old) / diag, 0.f);
+            const float d = xn - old;
+            d2 = fmaf(d, d, d2);
+            x2 = fmaf(old, old, x2);
+            cg.x[u][k] = xn;
+          }
+        }
       }
-      if (ALGO == 0) {
-        float xn[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-          float den = 0.f;
+      for (int u = 0; u < U; ++u) {
+        if (cg.ok[u]) {
 #pragma unroll
-          for (int kk = 0; kk < K; ++kk) den = fmaf(sG[k * K + kk], xv[kk], den);
-          den = fmaf(p.l2, xv[k], den) + p.l1_den;
-          xn[k] = (den < p.eps) ? 0.f : xv[k] * (nv[k] / den);
+          for (int k = 0; k < K; ++k)
+            buf_st(cg.x[u][k], rx, cg.vo[u], k * sx);
         }
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const float d = xn[k] - xv[k];
-          d2 = fmaf(d, d, d2);
-          x2 = fmaf(xv[k], xv[k], x2);
-          x[k * ldx + j] = xn[k];
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          float gx = 0.f;
-#pragma unroll
-          for (int kk = 0; kk < K; ++kk) gx = fmaf(sG[k * K + kk], xv[kk], gx);
-          const float diag = sG[k * K + k] + p.l2;
-          const float old = xv[k];
-          float xn = old;
-          if (diag > p.eps) xn = fmaxf(old + (nv[k] - p.l1_den - gx - p.l2 * old) / diag, 0.f);
-          const float d = xn - old;
-          d2 = fmaf(d, d, d2);
-          x2 = fmaf(old, old, x2);
-          xv[k] = xn;
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) x[k * ldx + j] = xv[k];
       }
     }
     ++it;
     if (!check_conv || loss_conv) continue;
     block_sum2(d2, x2, sred);
-    if (sqrtf(d2) / (sqrtf(x2) + p.eps) < p.tol) break;
+    if (sqrtf(d2) / (sqrtf(x2) + eps) < p.tol) break;
   }
 
   if (p.lin_out || p.quad_out) {
     float lin = 0.f, quad = 0.f;
-    for (int j = j0 + threadIdx.x; j < n; j += blockDim.x) {
-      float xv[K];
+    for (int j = j0 + threadIdx.x; j < n; j += U * T) {
+      CNMF_MEMBAR();
+      ColGroup<K, U> cg;
+      load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, 0.f);
+      const lds_float* gz = opaque(sG);
 #pragma unroll
-      for (int k = 0; k < K; ++k) xv[k] = x[k * ldx + j];
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        lin = fmaf(nu[k * ldn + j], xv[k], lin);
-        float gx = 0.f;
+        for (int k = 0; k < K; ++k) {
+          CNMF_MEMBAR();
+          float gx = 0.f;
 #pragma unroll
-        for (int kk = 0; kk < K; ++kk) gx = fmaf(sG[k * K + kk], xv[kk], gx);
-        quad = fmaf(xv[k], gx, quad);
+          for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], cg.x[u][kk], gx);
+          lin = fmaf(cg.n[u][k], cg.x[u][k], lin);
+          quad = fmaf(cg.x[u][k], gx, quad);
+        }
       }
     }
     block_sum2(lin, quad, sred);
@@ -211,7 +289,9 @@ hipError_t launch_solve_k(int algo, const SolveParams& p, int nblocks, int threa
 
 extern "C" int cnmf_solve_max_k() { return 32; }
 
-extern "C" int cnmf_solve_max_threads(int K) { return K <= 16 ? 1024 : 512; }
+extern "C" int cnmf_solve_max_threads(int K) { return 1024; }
+
+extern "C" int cnmf_solve_reg_max_cols(int K) { return 0; }
 
 extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx,
                                  const float* numer, long long n_rs, long long ldn,
@@ -219,8 +299,11 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  int nblocks, int ncols, int max_iter, float tol, float l1_num,
                                  float l1_den, float l2, float eps, float* lin_out,
                                  float* quad_out, int* iters_out, int nsplit, int conv_mode,
-                                 int check_every, int threads, hipStream_t stream) {
+                                 int check_every, int threads, int variant,
+                                 hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
+  // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
+  if ((long long)K * (ldx > ldn ? ldx : ldn) * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
   cnmf::SolveParams p;
   p.x = x; p.x_rs = x_rs; p.ldx = ldx;
   p.numer = numer; p.n_rs = n_rs; p.ldn = ldn;
@@ -232,6 +315,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.nsplit = nsplit;
   p.conv_mode = conv_mode;
   p.check_every = check_every;
+  (void)variant;
   switch (K) {
     CNMF_K_CASE(1) CNMF_K_CASE(2) CNMF_K_CASE(3) CNMF_K_CASE(4) CNMF_K_CASE(5) CNMF_K_CASE(6)
     CNMF_K_CASE(7) CNMF_K_CASE(8) CNMF_K_CASE(9) CNMF_K_CASE(10) CNMF_K_CASE(11)

@@ -1,0 +1,26 @@
+// Parameter block shared by the streaming (solve.hip) and register-resident
+// (solve_reg.hip) fused solve kernels.
+#pragma once
+
+namespace cnmf {
+
+struct SolveParams {
+  float* x;                 // solution, replicate r at x + r*x_rs, row (component) stride ldx
+  long long x_rs, ldx;
+  const float* numer;       // numerator, same layout as x
+  long long n_rs, ldn;
+  const float* gram;        // K x K per replicate
+  long long g_rs;
+  const int* rep_index;     // blockIdx.x -> replicate (nullptr = identity)
+  int ncols, max_iter;
+  float tol, l1_num, l1_den, l2, eps;
+  float* lin_out;           // optional <numer, x>
+  float* quad_out;          // optional sum_j x_j^T Gram x_j
+  int* iters_out;           // optional steps taken
+  int nsplit;               // >1: blockIdx.y splits the columns; single fixed step
+  int conv_mode;            // 0: ||dx||/(||x||+eps) < tol each step (cnmf.py:375-378)
+                            // 1: block objective every `check_every` steps (nmf-torch online)
+  int check_every;
+};
+
+}  // namespace cnmf
