@@ -235,22 +235,24 @@ def init_factors(X: torch.Tensor, K: int, seeds, init: str = "random", comm=None
 
 # =============================================================================== state
 class _Batch:
-    """Live replicate batch with an active-prefix layout: live replicates occupy
-    positions [0, n_act); finished ones are moved behind them (``order`` maps position ->
-    original replicate id)."""
+    """Live replicate batch with an active-prefix layout.
+
+    Live replicates occupy positions [0, n_act); ``compact`` moves finished ones behind
+    them (``order`` maps position -> original replicate id).  Convergence state lives on
+    the device (``state``: float64 err_init/err_prev/err, int32 active/converged/n_pass)
+    so the solves can skip finished replicates without a host round trip."""
 
     def __init__(self, HT, W, K, R):
         self.HT, self.W, self.K, self.R = HT, W, K, R
         self.order = list(range(R))
         self.n_act = R
         dev = W.device
-        self.err_init = torch.zeros(R, dtype=torch.float64)
-        self.err_prev = torch.zeros(R, dtype=torch.float64)
-        self.err = torch.zeros(R, dtype=torch.float64)
-        self.n_iter = np.zeros(R, dtype=np.int64)
-        self.converged = np.zeros(R, dtype=bool)
-        self.h_iters = torch.zeros(R, dtype=torch.int64, device=dev)
-        self.w_iters = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.state = {k: torch.zeros(R, dtype=torch.float64, device=dev)
+                      for k in ("err_init", "err_prev", "err")}
+        for k in ("active", "converged", "n_pass"):
+            self.state[k] = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.h_iters = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.w_iters = torch.zeros(R, dtype=torch.int32, device=dev)
         self.A = None   # (R, K, K) sufficient statistics (online 'exact' mode)
         self.B = None   # (R*K, G)
 
@@ -258,45 +260,119 @@ class _Batch:
         K, n = self.K, self.n_act
         return self.HT[:n * K], self.W[:n * K]
 
-    def retire(self, done_pos: np.ndarray) -> None:
-        """Mark positions (< n_act) finished and compact the live prefix."""
-        if done_pos.size == 0:
-            return
+    def active_mask(self) -> torch.Tensor:
+        return self.state["active"][:self.n_act]
+
+    def compact(self) -> None:
+        """Sync point: move still-active replicates to the front and shrink n_act."""
         n, K = self.n_act, self.K
-        keep = [p for p in range(n) if p not in set(done_pos.tolist())]
-        perm = keep + sorted(done_pos.tolist()) + list(range(n, self.R))
-        if perm != list(range(self.R)):
-            rows = torch.cat([torch.arange(p * K, (p + 1) * K) for p in perm]).to(self.W.device)
-            self.HT = self.HT.index_select(0, rows)
-            self.W = self.W.index_select(0, rows)
-            if self.B is not None:
-                self.B = self.B.index_select(0, rows)
-                self.A = self.A.index_select(0, torch.tensor(perm, device=self.A.device))
-            pidx = torch.tensor(perm)
-            for name in ("err_init", "err_prev", "err"):
-                setattr(self, name, getattr(self, name)[pidx])
-            didx = pidx.to(self.W.device)
-            self.h_iters = self.h_iters[didx]
-            self.w_iters = self.w_iters[didx]
-            self.n_iter = self.n_iter[perm]
-            self.converged = self.converged[perm]
-            self.order = [self.order[p] for p in perm]
+        act = self.state["active"][:n].cpu().numpy() != 0
+        keep = [p for p in range(n) if act[p]]
+        if len(keep) == n:
+            return
+        done = [p for p in range(n) if not act[p]]
+        perm = keep + done + list(range(n, self.R))
+        dev = self.W.device
+        rows = torch.cat([torch.arange(p * K, (p + 1) * K) for p in perm]).to(dev)
+        self.HT = self.HT.index_select(0, rows)
+        self.W = self.W.index_select(0, rows)
+        if self.B is not None:
+            self.B = self.B.index_select(0, rows)
+            self.A = self.A.index_select(0, torch.tensor(perm, device=self.A.device))
+        pidx = torch.tensor(perm, device=dev)
+        self.state = {k: v[pidx] for k, v in self.state.items()}
+        self.h_iters = self.h_iters[pidx]
+        self.w_iters = self.w_iters[pidx]
+        self.order = [self.order[p] for p in perm]
         self.n_act = len(keep)
+
+    def set_err(self, err: torch.Tensor, pass_idx: int, tol: float, final: bool,
+                init: bool = False) -> None:
+        """Host-computed per-position errors (beta != 2 paths) -> same bookkeeping as the
+        device convergence kernel."""
+        n = self.n_act
+        st = self.state
+        e = err[:n].to(device=st["err"].device, dtype=torch.float64)
+        if init:
+            for k in ("err_init", "err_prev", "err"):
+                st[k][:n] = e
+            st["active"][:n] = 1
+            return
+        act = st["active"][:n] != 0
+        st["err"][:n] = torch.where(act, e, st["err"][:n])
+        st["n_pass"][:n] = torch.where(act, torch.full_like(st["n_pass"][:n], pass_idx),
+                                       st["n_pass"][:n])
+        rel = (st["err_prev"][:n] - e) / torch.clamp(st["err_init"][:n], min=1e-300)
+        conv = act & (rel < tol)
+        stop = conv | (act & bool(final))
+        st["converged"][:n] = torch.where(conv, torch.ones_like(st["converged"][:n]),
+                                          st["converged"][:n])
+        st["err_prev"][:n] = torch.where(act & ~stop, e, st["err_prev"][:n])
+        st["active"][:n] = torch.where(stop, torch.zeros_like(st["active"][:n]),
+                                       st["active"][:n])
 
     def finalize(self):
         """Restore original replicate order."""
         inv = np.argsort(np.asarray(self.order))
         K = self.K
-        rows = torch.cat([torch.arange(p * K, (p + 1) * K) for p in inv]).to(self.W.device)
+        dev = self.W.device
+        rows = torch.cat([torch.arange(p * K, (p + 1) * K) for p in inv]).to(dev)
         HT = self.HT.index_select(0, rows)
         W = self.W.index_select(0, rows)
-        idx = torch.tensor(inv)
-        didx = idx.to(self.W.device)
-        return (HT, W, self.err[idx].numpy(), self.n_iter[inv], self.converged[inv],
-                self.h_iters[didx].cpu().numpy(), self.w_iters[didx].cpu().numpy())
+        idx = torch.tensor(inv, device=dev)
+        st = {k: v[idx].cpu().numpy() for k, v in self.state.items()}
+        return (HT, W, st["err"], st["n_pass"].astype(np.int64), st["converged"].astype(bool),
+                self.h_iters[idx].cpu().numpy(), self.w_iters[idx].cpu().numpy())
 
 
-# =============================================================================== engine
+class _PassPipeline:
+    """Host side of the speculative pass loop.
+
+    Pass p is enqueued before the host knows whether pass p-1 finished everybody: the
+    active flags of pass p-1 are copied to pinned memory asynchronously and read one pass
+    behind, so the GPU never drains at a pass boundary.  When flags show that enough
+    replicates finished, the host synchronises once and compacts the batch."""
+
+    def __init__(self, st: _Batch, compact_frac: float = 0.25):
+        self.st = st
+        self.cuda = st.W.device.type == "cuda"
+        self.frac = compact_frac
+        self.pending = None   # (event, host_flags, n)
+
+    def after_enqueue(self) -> bool:
+        """Call after enqueueing a pass (incl. its convergence update).  Returns False
+        when the loop should stop."""
+        st = self.st
+        n = st.n_act
+        if not self.cuda:
+            n_live = int((st.state["active"][:n] != 0).sum())
+            if n_live == 0:
+                return False
+            if n - n_live >= max(1, int(self.frac * n)):
+                st.compact()
+            return True
+        flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        flags.copy_(st.state["active"][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        prev, self.pending = self.pending, (ev, flags, n)
+        if prev is None:
+            return True
+        pev, pflags, pn = prev
+        pev.synchronize()
+        if pn != n:                       # a compaction happened in between: stale layout
+            return True
+        n_live = int((pflags != 0).sum())
+        if n_live == 0:                   # everything had finished one pass ago
+            return False
+        if n - n_live >= max(1, int(self.frac * n)):
+            torch.cuda.current_stream().synchronize()
+            st.compact()
+            self.pending = None
+            return st.n_act > 0
+        return True
+
+
 def _chunks(n_rows: int, c: int, n_steps: int):
     out = []
     for s in range(n_steps):
@@ -363,31 +439,30 @@ class NMFBatchSolver:
 
     def _check_convergence(self, st: _Batch, err_now: torch.Tensor, step: int,
                            final: bool) -> None:
-        """Update per-replicate errors (positions < n_act), retire converged ones."""
-        n = st.n_act
-        st.err[:n] = err_now[:n]
-        done = []
-        for p in range(n):
-            rel = (float(st.err_prev[p]) - float(st.err[p])) / max(float(st.err_init[p]), 1e-300)
-            st.n_iter[p] = step
-            if rel < self.opts.tol:
-                st.converged[p] = True
-                done.append(p)
-            elif final:
-                done.append(p)
-            else:
-                st.err_prev[p] = st.err[p]
-        st.retire(np.asarray(done, dtype=np.int64))
-
-    def _frob_err_from_stats(self, lin: torch.Tensor, quad: torch.Tensor) -> torch.Tensor:
-        v = self.x_sq - 2.0 * lin.double().cpu() + quad.double().cpu()
-        return torch.sqrt(torch.clamp(v, min=0.0))
+        """Host-side convergence step for the beta != 2 paths (errors computed on host)."""
+        st.set_err(err_now, step, self.opts.tol, final)
+        st.compact()
 
     def _init_err(self, st: _Batch) -> None:
-        e = self.loss(st.HT, st.W, st.K)
-        st.err_init[:] = e
-        st.err_prev[:] = e
-        st.err[:] = e
+        st.set_err(self.loss(st.HT, st.W, st.K), 0, self.opts.tol, False, init=True)
+
+    def _init_err_frob(self, st: _Batch) -> None:
+        """Initial Frobenius error of every replicate, on device (conv kernel, init mode)."""
+        R, K = st.R, st.K
+        X = self.X
+        G = X.shape[1]
+        W3 = st.W.view(R, K, G)
+        stats = torch.empty(R * K * G + R * K * K, device=X.device, dtype=X.dtype)
+        B = stats[:R * K * G].view(R * K, G)
+        A = stats[R * K * G:].view(R, K, K)
+        torch.mm(st.HT, X, out=B)
+        H3 = st.HT.view(R, K, X.shape[0])
+        torch.bmm(H3, H3.transpose(1, 2), out=A)
+        self.comm.allreduce_(stats)
+        lin = (B.view(R, K, G) * W3).sum(dim=(1, 2)).float().contiguous()
+        quad = (A * torch.bmm(W3, W3.transpose(1, 2))).sum(dim=(1, 2)).float().contiguous()
+        ops.conv_update(lin, quad, self.x_sq, st.state, R, 0, self.opts.tol, False, init=True)
+        return A, B
 
     # ------------------------------------------------------------------ loss (any beta)
     def loss(self, HT: torch.Tensor, W: torch.Tensor, K: int, row_chunk: int = 4096) -> torch.Tensor:
@@ -425,47 +500,43 @@ class NMFBatchSolver:
         algo = o.algo
         cmode = 1 if o.online_inner_conv == "loss" else 0
         exact = o.online_stats == "exact"
+        dist = comm.is_distributed
+        A0, B0 = self._init_err_frob(st)
         if exact:
-            # sufficient statistics of the CURRENT H over all cells: A = H^T H, B = H^T X
-            R = st.R
-            flat0 = torch.empty(R * K * G + R * K * K, device=dev, dtype=dt)
-            torch.mm(st.HT, X, out=flat0[:R * K * G].view(R * K, G))
-            H3 = st.HT.view(R, K, N)
-            torch.bmm(H3, H3.transpose(1, 2), out=flat0[R * K * G:].view(R, K, K))
-            comm.allreduce_(flat0)
-            st.B = flat0[:R * K * G].view(R * K, G)
-            st.A = flat0[R * K * G:].view(R, K, K)
-            st.A, st.B = st.A.clone(), st.B.clone()
-            W3 = st.W.view(R, K, G)
-            lin = (st.B.view(R, K, G) * W3).sum(dim=(1, 2)).double()
-            quad = (st.A * torch.bmm(W3, W3.transpose(1, 2))).sum(dim=(1, 2)).double()
-            e = self._frob_err_from_stats(lin, quad)
-            st.err_init[:] = e
-            st.err_prev[:] = e
-            st.err[:] = e
-        else:
-            self._init_err(st)
-        for p in range(int(o.online_max_pass)):
+            st.A, st.B = A0.clone(), B0.clone()
+        del A0, B0
+        max_pass = int(o.online_max_pass)
+        pipe = _PassPipeline(st)
+        n_alloc = -1
+        for p in range(max_pass):
             n = st.n_act
             if n == 0:
                 break
+            if n != n_alloc:   # (re)allocate per-n workspaces once, not per pass
+                n_alloc = n
+                flat = torch.empty(n * K * G + n * K * K, device=dev, dtype=dt)
+                dB = flat[:n * K * G].view(n * K, G)
+                dA = flat[n * K * G:].view(n, K, K)
+                if not exact:
+                    A = torch.empty((n, K, K), device=dev, dtype=dt)
+                    B = torch.empty((n * K, G), device=dev, dtype=dt)
+                lin = torch.zeros(n, device=dev, dtype=torch.float32)
+                quad = torch.zeros(n, device=dev, dtype=torch.float32)
             HT, W = st.views()
             W3 = W.view(n, K, G)
             H3 = HT.view(n, K, N)
-            # one flat buffer per step: [dB (n*K*G) | dA (n*K*K)] -> ONE all-reduce per step
-            flat = torch.empty(n * K * G + n * K * K, device=dev, dtype=dt)
-            dB = flat[:n * K * G].view(n * K, G)
-            dA = flat[n * K * G:].view(n, K, K)
             if exact:
                 A, B = st.A[:n], st.B[:n * K]
             else:
-                A = torch.zeros((n, K, K), device=dev, dtype=dt)
-                B = torch.zeros((n * K, G), device=dev, dtype=dt)
-            lin = torch.zeros(n, device=dev, dtype=torch.float32)
-            quad = torch.zeros(n, device=dev, dtype=torch.float32)
-            it_h = torch.zeros(n, device=dev, dtype=torch.int32)
-            it_w = torch.zeros(n, device=dev, dtype=torch.int32)
+                A.zero_()
+                B.zero_()
+            active = st.active_mask()
+            h_it = st.h_iters[:n]
+            w_it = st.w_iters[:n]
             for s, blocks in enumerate(steps):
+                # DP: increments go to the flat buffer (one all-reduce per step); single
+                # process: GEMMs accumulate straight into A / B (beta = 1)
+                accA, accB = (dA, dB) if dist else (A, B)
                 first = True
                 for (a, b) in blocks:
                     cw = b - a
@@ -476,40 +547,47 @@ class NMFBatchSolver:
                     h_old = hview.clone() if exact else None
                     WWT = torch.bmm(W3, W3.transpose(1, 2))
                     numerT = W @ xc.t()                                  # (n*K, cw) GEMM
-                    ops.solve(algo, hview, numerT.view(n, K, cw), _as(WWT, dt),
+                    ops.solve(algo, hview, numerT.view(n, K, cw), WWT,
                               max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
-                              l1_den=o.l1_H, l2=o.l2_H, eps=o.eps, iters_out=it_h,
-                              conv_mode=cmode, check_every=o.inner_check_every)
-                    st.h_iters[:n] += it_h.to(torch.int64)
+                              l1_den=o.l1_H, l2=o.l2_H, eps=o.eps, iters_out=h_it,
+                              conv_mode=cmode, check_every=o.inner_check_every, active=active)
                     if exact:
                         # replace the chunk's old contribution: d = h_new - h_old
                         hh = torch.bmm(hview, hview.transpose(1, 2))
                         hh -= torch.bmm(h_old, h_old.transpose(1, 2))
                         hlhs = h_old.neg_().add_(hview).view(n * K, cw)
+                        zero_first = dist and first
+                        if zero_first:
+                            torch.mm(hlhs, xc, out=accB)
+                            accA.copy_(hh)
+                        else:
+                            accB.addmm_(hlhs, xc)
+                            accA += hh
                     else:
-                        hh = torch.bmm(hview, hview.transpose(1, 2))
-                        hlhs = HT[:, a:b]
+                        if dist and first:
+                            torch.mm(HT[:, a:b], xc, out=accB)           # (n*K, G) GEMM
+                            torch.bmm(hview, hview.transpose(1, 2), out=accA)
+                        else:
+                            accB.addmm_(HT[:, a:b], xc)                  # B += h^T x
+                            accA.baddbmm_(hview, hview.transpose(1, 2))  # A += h^T h
+                    first = False
+                if dist:
                     if first:
-                        torch.mm(hlhs, xc, out=dB)                       # (n*K, G) GEMM
-                        dA.copy_(hh)
-                        first = False
-                    else:
-                        dB.addmm_(hlhs, xc)
-                        dA += hh
-                if first:
-                    flat.zero_()
-                comm.allreduce_(flat)
-                B += dB
-                A += dA
+                        flat.zero_()
+                    comm.allreduce_(flat)
+                    B += dB
+                    A += dA
                 last = s == len(steps) - 1
-                ops.solve(algo, W3, B.view(n, K, G), _as(A, dt),
+                ops.solve(algo, W3, B.view(n, K, G), A.contiguous(),
                           max_iter=o.online_chunk_max_iter, tol=o.online_w_tol,
                           l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
                           lin_out=lin if last else None, quad_out=quad if last else None,
-                          iters_out=it_w, conv_mode=cmode, check_every=o.inner_check_every)
-                st.w_iters[:n] += it_w.to(torch.int64)
-            err = self._frob_err_from_stats(lin, quad)
-            self._check_convergence(st, err, p + 1, final=(p + 1 == int(o.online_max_pass)))
+                          iters_out=w_it, conv_mode=cmode, check_every=o.inner_check_every,
+                          active=active)
+            ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()}, n,
+                            p + 1, o.tol, final=(p + 1 == max_pass))
+            if not pipe.after_enqueue():
+                break
 
     # ------------------------------------------------------------------ batch frobenius
     def _batch_frob(self, st: _Batch) -> None:
@@ -518,41 +596,51 @@ class NMFBatchSolver:
         X = self.X
         N, G = X.shape
         dev, dt = X.device, X.dtype
-        self._init_err(st)
+        self._init_err_frob(st)
         hals = o.algo == "hals"
         h_iter = o.batch_hals_max_iter if hals else 1
         h_tol = o.batch_hals_tol if hals else -1.0
-        for it in range(int(o.batch_max_iter)):
+        max_it = int(o.batch_max_iter)
+        every = max(1, int(o.loss_every))
+        pipe = _PassPipeline(st)
+        n_alloc = -1
+        for it in range(max_it):
             n = st.n_act
             if n == 0:
                 break
+            if n != n_alloc:
+                n_alloc = n
+                flat = torch.empty(n * K * G + n * K * K, device=dev, dtype=dt)
+                B = flat[:n * K * G].view(n * K, G)
+                A = flat[n * K * G:].view(n, K, K)
+                lin = torch.zeros(n, device=dev, dtype=torch.float32)
+                quad = torch.zeros(n, device=dev, dtype=torch.float32)
             HT, W = st.views()
             W3 = W.view(n, K, G)
+            active = st.active_mask()
             # H-step over all local cells
             WWT = torch.bmm(W3, W3.transpose(1, 2))
             numerT = W @ X.t()
             nsplit = 1 if hals else max(1, (N + 8191) // 8192)
-            ops.solve(o.algo, HT.view(n, K, N), numerT.view(n, K, N), _as(WWT, dt),
+            ops.solve(o.algo, HT.view(n, K, N), numerT.view(n, K, N), WWT,
                       max_iter=h_iter, tol=h_tol, l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
-                      nsplit=nsplit if not hals else 1)
+                      nsplit=nsplit, active=active, iters_out=st.h_iters[:n])
             del numerT
             # W-step from the new H
-            flat = torch.empty(n * K * G + n * K * K, device=dev, dtype=dt)
-            B = flat[:n * K * G].view(n * K, G)
-            A = flat[n * K * G:].view(n, K, K)
             torch.mm(HT, X, out=B)
             H3 = HT.view(n, K, N)
             torch.bmm(H3, H3.transpose(1, 2), out=A)
             comm.allreduce_(flat)
-            check = (it + 1) % max(1, int(o.loss_every)) == 0 or it + 1 == int(o.batch_max_iter)
-            lin = torch.zeros(n, device=dev, dtype=torch.float32) if check else None
-            quad = torch.zeros(n, device=dev, dtype=torch.float32) if check else None
-            ops.solve(o.algo, W3, B.view(n, K, G), _as(A, dt),
+            check = (it + 1) % every == 0 or it + 1 == max_it
+            ops.solve(o.algo, W3, B.view(n, K, G), A.contiguous(),
                       max_iter=h_iter, tol=h_tol, l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
-                      lin_out=lin, quad_out=quad)
+                      lin_out=lin if check else None, quad_out=quad if check else None,
+                      active=active, iters_out=st.w_iters[:n])
             if check:
-                err = self._frob_err_from_stats(lin, quad)
-                self._check_convergence(st, err, it + 1, final=(it + 1 == int(o.batch_max_iter)))
+                ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
+                                n, it + 1, o.tol, final=(it + 1 == max_it))
+                if not pipe.after_enqueue():
+                    break
 
     # ------------------------------------------------------------------ beta-divergence MU
     def _beta_gamma(self) -> float:
@@ -611,7 +699,7 @@ class NMFBatchSolver:
                         rel = (torch.linalg.vector_norm(hn - ha, dim=(1, 2)) /
                                (torch.linalg.vector_norm(ha, dim=(1, 2)) + o.eps)).cpu()
                         h[di] = hn
-                        st.h_iters[di] += 1
+                        st.h_iters[di] += 1  # noqa: E501
                         active[idx[rel < o.online_h_tol]] = False
                     HT[:, a:b] = h.transpose(1, 2).reshape(n * K, cw)
                     WH = torch.bmm(h, W3)

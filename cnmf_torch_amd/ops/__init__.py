@@ -76,7 +76,8 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           l1_num: float = 0.0, l1_den: float = 0.0, l2: float = 0.0, eps: float = 1e-16,
           lin_out: torch.Tensor | None = None, quad_out: torch.Tensor | None = None,
           iters_out: torch.Tensor | None = None, nsplit: int = 1, conv_mode: int = 0,
-          check_every: int = 10, variant: str = "auto") -> None:
+          check_every: int = 10, variant: str = "auto",
+          active: torch.Tensor | None = None) -> None:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -84,18 +85,20 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     ``nsplit > 1`` runs a single fixed step with columns split over blocks (batch mode).
     ``conv_mode`` 0: stop when ||dx||/(||x||+eps) < tol (checked every step);
     1: stop when the block objective's relative change over ``check_every`` steps < tol.
-    ``variant``: 'auto' (register-resident kernel when the block fits, else streaming),
-    'stream' or 'reg' (tests / A-B benchmarks).
+    ``iters_out`` ACCUMULATES the steps taken (zero it for per-call counts).
+    ``active`` (int32, one flag per replicate): replicates with 0 are left untouched.
     """
     a = ALGOS[algo]
     R, K, n = x.shape
     if not use_native(x) or x.dtype != torch.float32:  # fp64 (fp_precision='double') -> torch
         return reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
-                               eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every)
+                               eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every,
+                               active)
     h = _hip
     if K > h.solve_max_k():
         return reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
-                               eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every)
+                               eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every,
+                               active)
     _check_block_view("x", x, R, K, n)
     _check_block_view("numer", numer, R, K, n)
     if gram.shape != (R, K, K) or gram.dtype != torch.float32:
@@ -116,7 +119,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     if nsplit > 1 and max_iter != 1:
         raise ValueError("nsplit > 1 requires max_iter == 1 (no convergence test)")
     for name, t, dt in (("lin_out", lin_out, torch.float32), ("quad_out", quad_out, torch.float32),
-                        ("iters_out", iters_out, torch.int32)):
+                        ("iters_out", iters_out, torch.int32), ("active", active, torch.int32)):
         if t is not None and (t.dtype != dt or t.numel() < R or not t.is_contiguous()):
             raise ValueError(f"{name}: expected contiguous {dt} with >= {R} elements")
     if nsplit > 1:
@@ -132,7 +135,33 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             quad_out.data_ptr() if quad_out is not None else 0,
             iters_out.data_ptr() if iters_out is not None else 0, int(max(1, nsplit)),
             int(conv_mode), int(check_every), int(threads),
-            {"auto": 0, "stream": 1, "reg": 2}[variant], _stream_ptr(x))
+            {"auto": 0, "stream": 1, "reg": 2}[variant],
+            active.data_ptr() if active is not None else 0, _stream_ptr(x))
+
+
+# ----------------------------------------------------------------------------- convergence
+def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict, n: int,
+                pass_idx: int, tol: float, final: bool, init: bool = False) -> None:
+    """Per-replicate Frobenius error from (lin, quad) and the (prev - cur)/init < tol
+    stopping rule, entirely on the device (csrc/kernels/conv.hip).  ``state`` holds
+    float64 err_init/err_prev/err and int32 active/converged/n_pass tensors."""
+    if n <= 0:
+        return
+    if not use_native(lin):
+        return reference.conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init)
+    for t in (lin, quad):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < n:
+            raise ValueError("lin/quad must be contiguous float32 with >= n entries")
+    for k, dt in (("err_init", torch.float64), ("err_prev", torch.float64), ("err", torch.float64),
+                  ("active", torch.int32), ("converged", torch.int32), ("n_pass", torch.int32)):
+        t = state[k]
+        if t.dtype != dt or not t.is_contiguous() or t.numel() < n or t.device != lin.device:
+            raise ValueError(f"state[{k}] must be contiguous {dt} on {lin.device}")
+    _hip.conv_update(lin.data_ptr(), quad.data_ptr(), float(x_sq), state["err_init"].data_ptr(),
+                     state["err_prev"].data_ptr(), state["err"].data_ptr(),
+                     state["active"].data_ptr(), state["converged"].data_ptr(),
+                     state["n_pass"].data_ptr(), int(n), int(pass_idx), float(tol), int(final),
+                     int(init), _stream_ptr(lin))
 
 
 # ----------------------------------------------------------------------------- init

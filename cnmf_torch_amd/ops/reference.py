@@ -34,10 +34,13 @@ def _step(algo, Xa, Na, Ga, l1_den, l2, eps):
 
 
 def solve(algo: int, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2, eps,
-          lin_out, quad_out, iters_out, nsplit=1, conv_mode=0, check_every=10) -> None:
+          lin_out, quad_out, iters_out, nsplit=1, conv_mode=0, check_every=10,
+          active=None) -> None:
     R, K, n = x.shape
     reps = (torch.arange(R, device=x.device) if rep_index is None
             else rep_index.to(device=x.device, dtype=torch.long))
+    if active is not None:
+        reps = reps[active.to(x.device)[reps] != 0]
     if reps.numel() == 0:
         return
     X = x[reps].clone()
@@ -89,7 +92,7 @@ def solve(algo: int, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l
         if quad_out is not None:
             quad_out[reps] = quad.to(quad_out.dtype)
     if iters_out is not None:
-        iters_out[reps] = iters.to(iters_out.dtype)
+        iters_out[reps] += iters.to(iters_out.dtype)
 
 
 def philox_fill(out: torch.Tensor, seeds, scales, stream: int, mode: int = 0,
@@ -100,3 +103,28 @@ def philox_fill(out: torch.Tensor, seeds, scales, stream: int, mode: int = 0,
     for r in range(R):
         m = torch.from_numpy(philox_matrix(seeds[r], stream, rows, cols, mode, row_offset))
         out[r].copy_((m * scales[r]).to(out.dtype))
+
+
+def conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init=False):
+    e = torch.sqrt(torch.clamp(x_sq - 2.0 * lin[:n].double() + quad[:n].double(), min=0.0))
+    e = e.to(state["err"].device)
+    if init:
+        for k in ("err_init", "err_prev", "err"):
+            state[k][:n] = e
+        state["active"][:n] = 1
+        state["converged"][:n] = 0
+        state["n_pass"][:n] = 0
+        return
+    act = state["active"][:n] != 0
+    state["err"][:n] = torch.where(act, e, state["err"][:n])
+    state["n_pass"][:n] = torch.where(act, torch.full_like(state["n_pass"][:n], pass_idx),
+                                      state["n_pass"][:n])
+    rel = (state["err_prev"][:n] - e) / torch.clamp(state["err_init"][:n], min=1e-300)
+    conv = act & (rel < tol)
+    stop = conv | (act & bool(final))
+    state["converged"][:n] = torch.where(conv, torch.ones_like(state["converged"][:n]),
+                                         state["converged"][:n])
+    keep = act & ~stop
+    state["err_prev"][:n] = torch.where(keep, e, state["err_prev"][:n])
+    state["active"][:n] = torch.where(stop, torch.zeros_like(state["active"][:n]),
+                                      state["active"][:n])

@@ -32,14 +32,26 @@ PYBIND11_MODULE(_hip, m) {
            long long n_rs, long long ldn, uintptr_t gram, long long g_rs, uintptr_t rep_index,
            int nblocks, int ncols, int max_iter, float tol, float l1_num, float l1_den, float l2,
            float eps, uintptr_t lin_out, uintptr_t quad_out, uintptr_t iters_out, int nsplit,
-           int conv_mode, int check_every, int threads, int variant, uintptr_t stream) {
+           int conv_mode, int check_every, int threads, int variant, uintptr_t active,
+           uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
                            max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
                            P<float>(quad_out), P<int>(iters_out), nsplit, conv_mode,
-                           check_every, threads, variant,
+                           check_every, threads, variant, P<const int>(active),
                            reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");
+        });
+
+  m.def("conv_update",
+        [](uintptr_t lin, uintptr_t quad, double x_sq, uintptr_t err_init, uintptr_t err_prev,
+           uintptr_t err, uintptr_t active, uintptr_t converged, uintptr_t n_pass, int n,
+           int pass, double tol, int final_pass, int init, uintptr_t stream) {
+          check(cnmf_conv_update(P<const float>(lin), P<const float>(quad), x_sq,
+                                 P<double>(err_init), P<double>(err_prev), P<double>(err),
+                                 P<int>(active), P<int>(converged), P<int>(n_pass), n, pass, tol,
+                                 final_pass, init, reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_conv_update");
         });
 
   m.def("philox_fill",

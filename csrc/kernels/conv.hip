@@ -1,0 +1,54 @@
+// On-device convergence bookkeeping for a replicate batch (one thread per replicate).
+//
+// Frobenius loss from the W-solve epilogue's sufficient statistics:
+//   err = sqrt(max(||X||^2 - 2 <B, W> + <A, W W^T>, 0))  (sklearn square_root=True)
+// and the nmf-torch / sklearn stopping rule (prev - cur) / init < tol.
+// Keeping this on the device lets the host enqueue pass p+1 before it has read pass p's
+// result: the solves skip replicates whose `active` flag dropped, so the host only polls
+// the flags one pass behind instead of draining the GPU at every pass boundary.
+#include <hip/hip_runtime.h>
+
+namespace cnmf {
+
+__global__ void conv_update_kernel(const float* lin, const float* quad, double x_sq,
+                                   double* err_init, double* err_prev, double* err, int* active,
+                                   int* converged, int* n_pass, int n, int pass, double tol,
+                                   int final_pass, int init) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const double e = sqrt(fmax(x_sq - 2.0 * (double)lin[r] + (double)quad[r], 0.0));
+  if (init) {  // error of the initial factors
+    err_init[r] = e;
+    err_prev[r] = e;
+    err[r] = e;
+    active[r] = 1;
+    converged[r] = 0;
+    n_pass[r] = 0;
+    return;
+  }
+  if (!active[r]) return;
+  err[r] = e;
+  n_pass[r] = pass;
+  const double denom = err_init[r] > 1e-300 ? err_init[r] : 1e-300;
+  if ((err_prev[r] - e) / denom < tol) {
+    active[r] = 0;
+    converged[r] = 1;
+  } else if (final_pass) {
+    active[r] = 0;
+  } else {
+    err_prev[r] = e;
+  }
+}
+
+}  // namespace cnmf
+
+extern "C" hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq,
+                                       double* err_init, double* err_prev, double* err,
+                                       int* active, int* converged, int* n_pass, int n, int pass,
+                                       double tol, int final_pass, int init, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(cnmf::conv_update_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, lin,
+                     quad, x_sq, err_init, err_prev, err, active, converged, n_pass, n, pass, tol,
+                     final_pass, init);
+  return hipGetLastError();
+}

@@ -11,7 +11,13 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       const int* rep_index, int nblocks, int ncols, int max_iter, float tol,
                       float l1_num, float l1_den, float l2, float eps, float* lin_out,
                       float* quad_out, int* iters_out, int nsplit, int conv_mode,
-                      int check_every, int threads, int variant, hipStream_t stream);
+                      int check_every, int threads, int variant, const int* active,
+                      hipStream_t stream);
+
+hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
+                            double* err_prev, double* err, int* active, int* converged,
+                            int* n_pass, int n, int pass, double tol, int final_pass,
+                            int init, hipStream_t stream);
 int cnmf_solve_reg_max_cols(int K);
 
 hipError_t cnmf_philox_fill(float* out, long long rows, long long cols, long long s_row,

@@ -142,6 +142,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
   __shared__ float sred[2 * 16];
   const lds_float* sG = (const lds_float*)sGm;  // LDS (addrspace 3): ds_read, 32-bit address
   const int rep = p.rep_index ? p.rep_index[blockIdx.x] : (int)blockIdx.x;
+  if (p.active && p.active[rep] == 0) return;  // converged replicate: untouched (uniform)
   float* __restrict__ x = p.x + (long long)rep * p.x_rs;
   const float* __restrict__ nu = p.numer + (long long)rep * p.n_rs;
   const float* __restrict__ g = p.gram + (long long)rep * p.g_rs;
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
       }
     }
   }
-  if (p.iters_out && threadIdx.x == 0 && blockIdx.y == 0) p.iters_out[rep] = it;
+  if (p.iters_out && threadIdx.x == 0 && blockIdx.y == 0) p.iters_out[rep] += it;
 }
 
 template <int K>
@@ -300,7 +301,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  float l1_den, float l2, float eps, float* lin_out,
                                  float* quad_out, int* iters_out, int nsplit, int conv_mode,
                                  int check_every, int threads, int variant,
-                                 hipStream_t stream) {
+                                 const int* active, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
   if ((long long)K * (ldx > ldn ? ldx : ldn) * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
@@ -315,6 +316,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.nsplit = nsplit;
   p.conv_mode = conv_mode;
   p.check_every = check_every;
+  p.active = active;
   (void)variant;
   switch (K) {
     CNMF_K_CASE(1) CNMF_K_CASE(2) CNMF_K_CASE(3) CNMF_K_CASE(4) CNMF_K_CASE(5) CNMF_K_CASE(6)

@@ -16,7 +16,8 @@ struct SolveParams {
   float tol, l1_num, l1_den, l2, eps;
   float* lin_out;           // optional <numer, x>
   float* quad_out;          // optional sum_j x_j^T Gram x_j
-  int* iters_out;           // optional steps taken
+  int* iters_out;           // optional: += steps taken (accumulates across calls)
+  const int* active;        // optional per-replicate flag: 0 -> the block returns at once
   int nsplit;               // >1: blockIdx.y splits the columns; single fixed step
   int conv_mode;            // 0: ||dx||/(||x||+eps) < tol each step (cnmf.py:375-378)
                             // 1: block objective every `check_every` steps (nmf-torch online)
