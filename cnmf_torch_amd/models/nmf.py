@@ -424,6 +424,8 @@ class NMFBatchSolver:
             else:
                 self._batch_beta(st)
         HT, W, err, n_iter, conv, hi, wi = st.finalize()
+        if self.X.device.type == "cuda":
+            ops.coop_check(self.X.device)
         stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": hi.tolist(),
                  "w_inner_iters": wi.tolist()}
         return NMFResult(HT=HT, W=W, err=err, n_iter=n_iter, converged=conv, seeds=list(seeds),

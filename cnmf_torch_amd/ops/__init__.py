@@ -77,7 +77,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           lin_out: torch.Tensor | None = None, quad_out: torch.Tensor | None = None,
           iters_out: torch.Tensor | None = None, nsplit: int = 1, conv_mode: int = 0,
           check_every: int = 10, variant: str = "auto",
-          active: torch.Tensor | None = None) -> None:
+          active: torch.Tensor | None = None, coop: int | str = "auto") -> None:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -87,6 +87,10 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     1: stop when the block objective's relative change over ``check_every`` steps < tol.
     ``iters_out`` ACCUMULATES the steps taken (zero it for per-call counts).
     ``active`` (int32, one flag per replicate): replicates with 0 are left untouched.
+    ``coop``: number S of workgroups cooperating on ONE replicate's columns while still
+    converging as a unit (cross-workgroup deterministic reductions, see coop_sum2 in
+    solve.hip); "auto" picks S so that all S*nblocks workgroups are co-resident on the
+    256 CUs, 1 disables.  Results are independent of S up to fp32 summation order.
     """
     a = ALGOS[algo]
     R, K, n = x.shape
@@ -126,8 +130,21 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
         for t in (lin_out, quad_out):
             if t is not None:
                 t.zero_()
-    threads = min(h.solve_max_threads(K), max(64, ((min(n, 4096 * 4) + 63) // 64) * 64))
-    threads = min(threads, h.solve_max_threads(K))
+    S = 1
+    if nsplit <= 1:
+        S = _coop_split(n, nblocks, x.device) if coop == "auto" else max(1, int(coop))
+    if S > 1 and nblocks * S > _coop_resident(x.device):
+        raise ValueError(f"coop={S} x {nblocks} blocks exceeds co-resident workgroups")
+    n_slice = (n + S - 1) // S
+    threads = min(h.solve_max_threads(K), max(64, ((min(n_slice, 4096 * 4) + 63) // 64) * 64))
+    ws_slots = ws_count = ws_flag = 0
+    epochs = 0
+    if S > 1:
+        epochs = (max_iter // max(1, check_every) + 3) if conv_mode == 1 else (max_iter + 2)
+        ws = _coop_workspace(x.device, _stream_ptr(x), R, epochs, S)
+        ws["count"][: R * epochs].zero_()
+        ws_slots, ws_count, ws_flag = (ws["slots"].data_ptr(), ws["count"].data_ptr(),
+                                       ws["flag"].data_ptr())
     h.solve(a, K, x.data_ptr(), x.stride(0), x.stride(1), numer.data_ptr(), numer.stride(0),
             numer.stride(1), gram.data_ptr(), K * K, ri, nblocks, n, int(max_iter), float(tol),
             float(l1_num), float(l1_den), float(l2), float(eps),
@@ -136,7 +153,59 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             iters_out.data_ptr() if iters_out is not None else 0, int(max(1, nsplit)),
             int(conv_mode), int(check_every), int(threads),
             {"auto": 0, "stream": 1, "reg": 2}[variant],
-            active.data_ptr() if active is not None else 0, _stream_ptr(x))
+            active.data_ptr() if active is not None else 0, int(S), ws_slots, ws_count,
+            int(epochs), ws_flag, _stream_ptr(x))
+
+
+# Cooperative-split bookkeeping.  A launch of S*nblocks 1024-thread workgroups is only safe
+# (spin-waits terminate) when every workgroup is resident at once: one such workgroup per
+# CU on gfx950, so the budget is the CU count minus a margin for concurrent kernels.
+_COOP_WS: dict = {}
+_COOP_RESIDENT: dict = {}
+COOP_COLS_PER_WG = 1024
+
+
+def _coop_resident(dev: torch.device) -> int:
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _COOP_RESIDENT:
+        cus = torch.cuda.get_device_properties(key).multi_processor_count
+        _COOP_RESIDENT[key] = max(1, cus - 16)
+    return _COOP_RESIDENT[key]
+
+
+def _coop_split(n: int, nblocks: int, dev: torch.device) -> int:
+    if os.environ.get("CNMF_SOLVE_COOP") == "0":
+        return 1
+    want = (n + COOP_COLS_PER_WG - 1) // COOP_COLS_PER_WG
+    return max(1, min(want, _coop_resident(dev) // max(1, nblocks), 16))
+
+
+def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int) -> dict:
+    """Per-(device, stream) scratch: slots [R*epochs*S*2] f32, counters [R*epochs] i32,
+    timeout flag.  Reused across launches on the same stream (stream order serialises)."""
+    key = (str(dev), stream)
+    ws = _COOP_WS.get(key)
+    need_slots, need_count = R * epochs * S * 2, R * epochs
+    if ws is None or ws["slots"].numel() < need_slots or ws["count"].numel() < need_count:
+        flag = ws["flag"] if ws is not None else torch.zeros(1, dtype=torch.int32, device=dev)
+        ws = {"slots": torch.empty(max(need_slots, 1 << 16), dtype=torch.float32, device=dev),
+              "count": torch.empty(max(need_count, 1 << 14), dtype=torch.int32, device=dev),
+              "flag": flag}
+        _COOP_WS[key] = ws
+    return ws
+
+
+def coop_check(device: torch.device | None = None) -> None:
+    """Raise if any cooperative solve on ``device`` gave up waiting (non-resident
+    workgroups) -- its results would be wrong.  Synchronises; call once per run."""
+    for key, ws in _COOP_WS.items():
+        if device is not None and key[0] != str(device):
+            continue
+        v = int(ws["flag"].item())
+        if v:
+            ws["flag"].zero_()
+            raise RuntimeError(f"cooperative solve failed on {key[0]} (code {v}): "
+                               "workgroups were not co-resident; set CNMF_SOLVE_COOP=0")
 
 
 # ----------------------------------------------------------------------------- convergence

@@ -104,6 +104,54 @@ __device__ __forceinline__ void load_group(ColGroup<K, U>& cg, int j, int T, int
   }
 }
 
+// Cross-workgroup sum of (a, b) for the S workgroups of one replicate, epoch `e`.
+// Each workgroup stores its block totals to its own slot (plain store), drains, then
+// arrives on the epoch counter with an agent-scope release; after all S arrived every
+// workgroup sums the S slots in slice order -> identical, deterministic totals
+// everywhere.  Spins are bounded: on timeout the flag is raised and the host fails.
+// (Recipe: cdna_hip_programming.md Guideline 16 -- release before the counter add,
+// acquire after the poll, vmcnt drained around the fence.)
+__device__ __forceinline__ void coop_sum2(const SolveParams& p, int rep, int e, float& a,
+                                          float& b, float* sred) {
+  const int S = gridDim.y;
+  const int slice = blockIdx.y;
+  if (S <= 1) return;
+  if (e >= p.coop_epochs) {  // workspace too small: treat as timeout (host sizes it)
+    if (threadIdx.x == 0) atomicExch(p.coop_timeout, 2);
+    return;
+  }
+  float* slots = p.coop_slots + (((long long)rep * p.coop_epochs + e) * S) * 2;
+  int* cnt = p.coop_count + (long long)rep * p.coop_epochs + e;
+  if (threadIdx.x == 0) {
+    slots[2 * slice] = a;
+    slots[2 * slice + 1] = b;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {
+        atomicExch(p.coop_timeout, 1);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    float ta = 0.f, tb = 0.f;
+    for (int s2 = 0; s2 < S; ++s2) {
+      ta += __hip_atomic_load(slots + 2 * s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tb += __hip_atomic_load(slots + 2 * s2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sred[0] = ta;
+    sred[1] = tb;
+  }
+  __syncthreads();
+  a = sred[0];
+  b = sred[1];
+  __syncthreads();
+}
+
 // Block objective (x2, dropping the constant ||X||^2):
 //   f(x) = sum_j x_j^T Gram x_j - 2 numer_j . x_j + 2 l1 |x_j|_1 + l2 |x_j|^2
 template <int K, int U>
@@ -153,14 +201,18 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
   const __amdgpu_buffer_rsrc_t rn = rsrc_of(nu);
   const int sx = (int)(p.ldx * 4), sn = (int)(p.ldn * 4);
   const int T = blockDim.x;
-  // Column range of this block: the whole block (nsplit == 1) or one of nsplit slices.
+  // Column range of this block: the whole block, one of nsplit fixed-step slices, or one
+  // of S cooperative slices (gridDim.y) that still converge together.
   int j0 = 0, n = p.ncols;
-  if (p.nsplit > 1) {
-    const int per = (p.ncols + p.nsplit - 1) / p.nsplit;
-    j0 = blockIdx.y * per;
+  const bool coop = p.coop_slots != nullptr && gridDim.y > 1;
+  if (p.nsplit > 1 || coop) {
+    const int parts = coop ? (int)gridDim.y : p.nsplit;
+    const int per = (p.ncols + parts - 1) / parts;
+    j0 = min(p.ncols, (int)blockIdx.y * per);
     n = min(p.ncols, j0 + per);
   }
   const bool check_conv = p.nsplit <= 1;
+  int epoch = 0;
   const bool loss_conv = check_conv && p.conv_mode == 1;
   const int every = p.check_every > 0 ? p.check_every : 1;
   const float l1 = p.l1_den, l2 = p.l2, eps = p.eps;
@@ -169,7 +221,11 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
   int it = 0;
   while (true) {
     if (loss_conv && it % every == 0) {
-      const float f = block_objective<K, U>(rx, sx, rn, sn, sG, j0, n, p.l1_num, l1, l2, sred);
+      float f = block_objective<K, U>(rx, sx, rn, sn, sG, j0, n, p.l1_num, l1, l2, sred);
+      if (coop) {
+        float unused = 0.f;
+        coop_sum2(p, rep, epoch++, f, unused, sred);
+      }
       if (have_prev && fabsf(f_prev - f) <= p.tol * fabsf(f_prev)) break;
       f_prev = f;
       have_prev = true;
@@ -232,6 +288,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
     ++it;
     if (!check_conv || loss_conv) continue;
     block_sum2(d2, x2, sred);
+    if (coop) coop_sum2(p, rep, epoch++, d2, x2, sred);
     if (sqrtf(d2) / (sqrtf(x2) + eps) < p.tol) break;
   }
 
@@ -256,7 +313,8 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
       }
     }
     block_sum2(lin, quad, sred);
-    if (threadIdx.x == 0) {
+    if (coop) coop_sum2(p, rep, epoch++, lin, quad, sred);
+    if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
       if (check_conv) {
         if (p.lin_out) p.lin_out[rep] = lin;
         if (p.quad_out) p.quad_out[rep] = quad;
@@ -274,7 +332,8 @@ hipError_t launch_solve_k(int algo, const SolveParams& p, int nblocks, int threa
                           hipStream_t s) {
   const int tmax = solve_max_threads<K>();
   if (threads > tmax) threads = tmax;
-  const dim3 grid(nblocks, p.nsplit > 1 ? p.nsplit : 1);
+  const int gy = p.nsplit > 1 ? p.nsplit : (p.coop_slots ? p.coop_epochs_split : 1);
+  const dim3 grid(nblocks, gy);
   if (algo == 0)
     hipLaunchKernelGGL((solve_kernel<K, 0>), grid, dim3(threads), 0, s, p);
   else
@@ -301,7 +360,9 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  float l1_den, float l2, float eps, float* lin_out,
                                  float* quad_out, int* iters_out, int nsplit, int conv_mode,
                                  int check_every, int threads, int variant,
-                                 const int* active, hipStream_t stream) {
+                                 const int* active, int coop_split, float* coop_slots,
+                                 int* coop_count, int coop_epochs, int* coop_timeout,
+                                 hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
   if ((long long)K * (ldx > ldn ? ldx : ldn) * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
@@ -317,6 +378,12 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.conv_mode = conv_mode;
   p.check_every = check_every;
   p.active = active;
+  p.coop_slots = coop_split > 1 ? coop_slots : nullptr;
+  p.coop_count = coop_count;
+  p.coop_epochs = coop_epochs;
+  p.coop_timeout = coop_timeout;
+  p.coop_epochs_split = coop_split > 1 ? coop_split : 1;
+  if (coop_split > 1 && nsplit > 1) return hipErrorInvalidValue;
   (void)variant;
   switch (K) {
     CNMF_K_CASE(1) CNMF_K_CASE(2) CNMF_K_CASE(3) CNMF_K_CASE(4) CNMF_K_CASE(5) CNMF_K_CASE(6)

@@ -22,6 +22,13 @@ struct SolveParams {
   int conv_mode;            // 0: ||dx||/(||x||+eps) < tol each step (cnmf.py:375-378)
                             // 1: block objective every `check_every` steps (nmf-torch online)
   int check_every;
+  // Cooperative split (gridDim.y = S > 1 workgroups per replicate, WITH convergence):
+  // per-epoch partial sums are exchanged through global memory (deterministic order).
+  float* coop_slots;        // [R][coop_epochs][S][2], no zeroing needed
+  int* coop_count;          // [R][coop_epochs], zeroed by the host before every launch
+  int coop_epochs;
+  int* coop_timeout;        // set to 1 if a spin gave up (residency violated)
+  int coop_epochs_split;    // launch-side: S (gridDim.y) for the cooperative split
 };
 
 }  // namespace cnmf

@@ -83,6 +83,58 @@ def test_solve_strided_and_rep_index():
     assert torch.equal(untouched.cpu(), ref.view(R, K, N)[1])
 
 
+@pytest.mark.parametrize("algo", ["mu", "hals"])
+@pytest.mark.parametrize("conv_mode", [0, 1])
+def test_solve_coop_split_matches_single_workgroup(algo, conv_mode):
+    """S workgroups per replicate (cross-WG reductions) == one workgroup per replicate."""
+    R, K, n = 5, 10, 9001
+    x0, numer, gram = _problem(R, K, n, seed=3)
+    dev = torch.device("cuda")
+    numer, gram = numer.to(dev), gram.to(dev)
+    outs = {}
+    for S in (1, 2, 3, 7):
+        for max_iter, tol in ((9, -1.0), (300, 1e-4)):
+            xg = x0.clone().to(dev)
+            lin = torch.zeros(R, device=dev)
+            quad = torch.zeros(R, device=dev)
+            it = torch.zeros(R, dtype=torch.int32, device=dev)
+            ops.solve(algo, xg, numer, gram, max_iter=max_iter, tol=tol, lin_out=lin,
+                      quad_out=quad, iters_out=it, conv_mode=conv_mode, check_every=5, coop=S)
+            outs[(S, tol)] = (xg.cpu(), lin.cpu(), quad.cpu(), it.cpu())
+    ops.coop_check(dev)
+    for S in (2, 3, 7):
+        for tol in (-1.0, 1e-4):
+            x1, l1, q1, i1 = outs[(1, tol)]
+            xs, ls, qs, is_ = outs[(S, tol)]
+            if tol < 0:
+                assert torch.equal(xs, x1)          # column updates are independent of S
+                assert is_.tolist() == [9] * R
+            else:
+                assert (is_ - i1).abs().max() <= 5
+                assert ((xs - x1).norm() / x1.norm()) < 2e-3
+            torch.testing.assert_close(ls, l1, rtol=1e-4, atol=1e-3)
+            torch.testing.assert_close(qs, q1, rtol=1e-4, atol=1e-3)
+
+
+def test_solve_coop_with_active_mask_and_rep_index():
+    R, K, n = 8, 7, 5000
+    x0, numer, gram = _problem(R, K, n, seed=5)
+    dev = torch.device("cuda")
+    active = torch.tensor([1, 0, 1, 1, 0, 1, 1, 1], dtype=torch.int32, device=dev)
+    ri = torch.tensor([0, 1, 2, 5, 7], dtype=torch.int32, device=dev)
+    res = []
+    for S in (1, 4):
+        xg = x0.clone().to(dev)
+        ops.solve("mu", xg, numer.to(dev), gram.to(dev), rep_index=ri, max_iter=50, tol=1e-5,
+                  conv_mode=1, check_every=5, active=active, coop=S)
+        res.append(xg.cpu())
+    ops.coop_check(dev)
+    untouched = [1, 3, 4, 6]
+    for r in untouched:
+        assert torch.equal(res[1][r], x0[r])
+    torch.testing.assert_close(res[1], res[0], rtol=2e-3, atol=1e-4)
+
+
 def test_solve_split_columns():
     R, K, n = 4, 9, 50000
     x0, numer, gram = _problem(R, K, n, seed=3)
