@@ -125,7 +125,7 @@ def main() -> int:
             "dtype": "fp32",
             "data": "synthetic (planted-program Poisson counts, unit-variance genes; random-init W,H)",
             "config": {
-                "model": f"cNMF factorize: online MU frobenius, K={args.k}",
+                "model": f"cNMF factorize: {args.mode} {args.algo.upper()} {args.beta_loss}, K={args.k}",
                 "global_batch": n_total,
                 "seq_len": None,
                 "cells": args.cells,

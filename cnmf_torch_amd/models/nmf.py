@@ -482,12 +482,9 @@ class NMFBatchSolver:
             lin = self.comm.allreduce_(lin.contiguous())
             quad = self.comm.allreduce_(quad.contiguous())
             return torch.sqrt(torch.clamp(self.x_sq - 2 * lin.cpu() + quad.cpu(), min=0.0))
-        tot = torch.zeros(R, dtype=torch.float64, device=X.device)
-        for a in range(0, N, row_chunk):
-            b = min(N, a + row_chunk)
-            xc = X[a:b]
-            h = HT[:, a:b].reshape(R, K, b - a).transpose(1, 2)
-            tot += _beta_div(xc, torch.bmm(h, W3), self.beta, self.opts.eps)
+        _, _, tot = ops.beta_contract("h", X, HT.view(R, K, N), W3, self.beta, self.opts.eps,
+                                      want_num=False, want_loss=True)
+        tot = tot.to(torch.float64).contiguous()
         self.comm.allreduce_(tot)
         return torch.sqrt(torch.clamp(2.0 * tot.cpu(), min=0.0))
 
@@ -653,107 +650,109 @@ class NMFBatchSolver:
             return 1.0 / (b - 1.0)
         return 1.0
 
-    def _beta_h_step(self, xc, h, W3, l1, l2):
-        """One MU step for h (R, c, K) given W3 (R, K, G); sklearn _multiplicative_update_h."""
+    def _mu_apply(self, x3: torch.Tensor, num: torch.Tensor, den: torch.Tensor, l1: float,
+                  l2: float, mask: torch.Tensor | None = None) -> None:
+        """x3 *= ((num / (den + l1 + l2 x3)) ** gamma) in place (sklearn's MU update with the
+        zero-denominator guard); ``mask`` (R,1,1 bool) leaves other replicates untouched."""
         eps = self.opts.eps
-        WH = torch.bmm(h, W3)
-        num, den = _beta_num_den(xc, WH, W3.transpose(1, 2), self.beta, eps, side="h")
-        den = den + l1 + l2 * h
-        den = torch.where(den == 0, torch.full_like(den, eps), den)
-        delta = num / den
+        d = den + l1 if l2 == 0.0 else den + l1 + l2 * x3
+        d = torch.where(d == 0, torch.full_like(d, eps), d)
+        delta = num / d
         g = self._beta_gamma()
         if g != 1.0:
-            delta = delta ** g
-        return h * delta
+            delta = delta.pow_(g)
+        if mask is not None:
+            delta = torch.where(mask, delta, torch.ones_like(delta))
+        x3.mul_(delta)
+
+    def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, tol=None, iters=None):
+        """One fused MU step of the usages H3c (R, K, c) in place against W3 on rows xc;
+        with ``tol`` the per-replicate inner stopping rule runs on device (clears act)."""
+        ops.beta_update_h(xc, H3c, W3, self.beta, self.opts.eps, l1, l2, self._beta_gamma(),
+                          act=act, tol=tol, iters=iters)
+
+    def _beta_w_stats(self, xc, H3c, W3):
+        """(num, den) W-side MU statistics of rows xc (den broadcastable to (R,K,G))."""
+        num, den, _ = ops.beta_contract("w", xc, H3c, W3, self.beta, self.opts.eps)
+        if den is None:
+            den = H3c.sum(dim=2, keepdim=True)              # KL: row sums of H
+        return num, den
 
     def _online_beta(self, st: _Batch) -> None:
+        """Online beta-MU (nmf-torch mode='online', beta != 2): per chunk, the usages are
+        iterated to ``online_h_tol`` (relative change, per replicate, on device), then the
+        W-side statistics of the chunk are accumulated (all-reduced under DP) and W takes
+        one MU step with the running pass statistics."""
         o, comm = self.opts, self.comm
         K = st.K
         X = self.X
         N, G = X.shape
         steps = self._steps(N)
         self._init_err(st)
-        g = self._beta_gamma()
+        max_it = int(o.online_chunk_max_iter)
         for p in range(int(o.online_max_pass)):
             n = st.n_act
             if n == 0:
                 break
             HT, W = st.views()
             W3 = W.view(n, K, G)
+            H3 = HT.view(n, K, N)
             num_acc = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
             den_acc = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
+            live = st.active_mask().clone()
             for blocks in steps:
                 flat = torch.zeros(2 * n * K * G, device=X.device, dtype=X.dtype)
+                fnum = flat[:n * K * G].view(n, K, G)
+                fden = flat[n * K * G:].view(n, K, G)
                 for (a, b) in blocks:
-                    cw = b - a
-                    if cw <= 0:
+                    if b <= a:
                         continue
                     xc = X[a:b]
-                    h = HT[:, a:b].reshape(n, K, cw).transpose(1, 2).contiguous()
-                    active = torch.ones(n, dtype=torch.bool)
-                    for _ in range(int(o.online_chunk_max_iter)):
-                        idx = torch.nonzero(active).flatten()
-                        if idx.numel() == 0:
+                    hc = H3[:, :, a:b]
+                    act = live.clone()
+                    for it in range(max_it):
+                        self._beta_h_update(xc, hc, W3, o.l1_H, o.l2_H, act, o.online_h_tol,
+                                            st.h_iters[:n])
+                        if (it + 1) % 8 == 0 and int(act.sum()) == 0:
                             break
-                        di = idx.to(X.device)
-                        ha = h[di]
-                        hn = self._beta_h_step(xc, ha, W3[di], o.l1_H, o.l2_H)
-                        rel = (torch.linalg.vector_norm(hn - ha, dim=(1, 2)) /
-                               (torch.linalg.vector_norm(ha, dim=(1, 2)) + o.eps)).cpu()
-                        h[di] = hn
-                        st.h_iters[di] += 1  # noqa: E501
-                        active[idx[rel < o.online_h_tol]] = False
-                    HT[:, a:b] = h.transpose(1, 2).reshape(n * K, cw)
-                    WH = torch.bmm(h, W3)
-                    nW, dW = _beta_num_den(xc, WH, h.transpose(1, 2), self.beta, o.eps, side="w")
-                    flat[:n * K * G] += nW.reshape(-1)
-                    flat[n * K * G:] += dW.expand(n, K, G).reshape(-1)
+                    nW, dW = self._beta_w_stats(xc, hc, W3)
+                    fnum += nW
+                    fden += dW
                 comm.allreduce_(flat)
-                num_acc += flat[:n * K * G].view(n, K, G)
-                den_acc += flat[n * K * G:].view(n, K, G)
-                den = den_acc + o.l1_W + o.l2_W * W3
-                den = torch.where(den == 0, torch.full_like(den, o.eps), den)
-                delta = num_acc / den
-                if g != 1.0:
-                    delta = delta ** g
-                W3.mul_(delta)
-                st.w_iters[:n] += 1
+                num_acc += fnum
+                den_acc += fden
+                self._mu_apply(W3, num_acc, den_acc, o.l1_W, o.l2_W,
+                               (live != 0).view(n, 1, 1))
+                st.w_iters[:n] += live
             err = self.loss(HT, W, K).to(torch.float64)
             self._check_convergence(st, err, p + 1, final=(p + 1 == int(o.online_max_pass)))
 
-    def _batch_beta(self, st: _Batch, row_chunk: int = 4096) -> None:
+    def _batch_beta(self, st: _Batch) -> None:
+        """Batch beta-MU (sklearn _fit_multiplicative_update order: usages, then spectra);
+        the W-side statistics are all-reduced under DP, the loss is checked every
+        ``loss_every`` iterations."""
         o, comm = self.opts, self.comm
         K = st.K
         X = self.X
         N, G = X.shape
         self._init_err(st)
-        g = self._beta_gamma()
         for it in range(int(o.batch_max_iter)):
             n = st.n_act
             if n == 0:
                 break
             HT, W = st.views()
             W3 = W.view(n, K, G)
-            for a in range(0, N, row_chunk):
-                b = min(N, a + row_chunk)
-                h = HT[:, a:b].reshape(n, K, b - a).transpose(1, 2)
-                hn = self._beta_h_step(X[a:b], h, W3, o.l1_H, o.l2_H)
-                HT[:, a:b] = hn.transpose(1, 2).reshape(n * K, b - a)
-            flat = torch.zeros(2 * n * K * G, device=X.device, dtype=X.dtype)
-            for a in range(0, N, row_chunk):
-                b = min(N, a + row_chunk)
-                h = HT[:, a:b].reshape(n, K, b - a).transpose(1, 2)
-                WH = torch.bmm(h, W3)
-                nW, dW = _beta_num_den(X[a:b], WH, h.transpose(1, 2), self.beta, o.eps, side="w")
-                flat[:n * K * G] += nW.reshape(-1)
-                flat[n * K * G:] += dW.expand(n, K, G).reshape(-1)
-            comm.allreduce_(flat)
-            den = flat[n * K * G:].view(n, K, G) + o.l1_W + o.l2_W * W3
-            den = torch.where(den == 0, torch.full_like(den, o.eps), den)
-            delta = flat[:n * K * G].view(n, K, G) / den
-            if g != 1.0:
-                delta = delta ** g
-            W3.mul_(delta)
+            H3 = HT.view(n, K, N)
+            self._beta_h_update(X, H3, W3, o.l1_H, o.l2_H)
+            nW, dW = self._beta_w_stats(X, H3, W3)
+            if comm.is_distributed:
+                flat = torch.cat([nW.reshape(-1), dW.expand(n, K, G).reshape(-1)])
+                comm.allreduce_(flat)
+                nW = flat[:n * K * G].view(n, K, G)
+                dW = flat[n * K * G:].view(n, K, G)
+            self._mu_apply(W3, nW, dW, o.l1_W, o.l2_W)
+            st.h_iters[:n] += 1
+            st.w_iters[:n] += 1
             if (it + 1) % max(1, int(o.loss_every)) == 0 or it + 1 == int(o.batch_max_iter):
                 err = self.loss(HT, W, K)
                 self._check_convergence(st, err, it + 1, final=(it + 1 == int(o.batch_max_iter)))
@@ -762,49 +761,6 @@ class NMFBatchSolver:
 def _as(t: torch.Tensor, dt: torch.dtype) -> torch.Tensor:
     """Contiguous copy/view of ``t`` in ``dt`` (solve kernels take dense grams)."""
     return t.contiguous() if t.dtype == dt else t.to(dt).contiguous()
-
-
-def _beta_num_den(xc, WH, other, beta: float, eps: float, side: str):
-    """MU numerator/denominator pieces for beta-divergence.
-
-    side='h': xc (c,G), WH (R,c,G), other = W^T (R,G,K) -> (R,c,K) num, den
-    side='w': other = h^T (R,K,c) -> (R,K,G) num, den (den may broadcast)
-    """
-    if beta == 1.0:
-        WHs = torch.clamp(WH, min=eps)
-        Q = xc.unsqueeze(0) / WHs
-        if side == "h":
-            num = torch.bmm(Q, other)
-            den = other.sum(dim=1, keepdim=True)            # (R,1,K): row sums of W
-        else:
-            num = torch.bmm(other, Q)
-            den = other.sum(dim=2, keepdim=True)            # (R,K,1): column sums of H
-        return num, den
-    WHs = torch.clamp(WH, min=eps)
-    if beta == 0.0:
-        P1 = WHs.reciprocal()
-        Q = xc.unsqueeze(0) * P1 * P1
-    else:
-        P1 = WHs ** (beta - 1.0)
-        Q = xc.unsqueeze(0) * WHs ** (beta - 2.0)
-    if side == "h":
-        return torch.bmm(Q, other), torch.bmm(P1, other)
-    return torch.bmm(other, Q), torch.bmm(other, P1)
-
-
-def _beta_div(xc: torch.Tensor, WH: torch.Tensor, beta: float, eps: float) -> torch.Tensor:
-    """Per-replicate sum of the beta divergence D(xc || WH) (sklearn _beta_divergence)."""
-    X = xc.unsqueeze(0).to(torch.float64)
-    Y = torch.clamp(WH.to(torch.float64), min=eps)
-    if beta == 1.0:
-        pos = X > 0
-        t = torch.where(pos, X * torch.log(torch.where(pos, X, torch.ones_like(X)) / Y), torch.zeros_like(Y))
-        return (t - X + Y).sum(dim=(1, 2))
-    if beta == 0.0:
-        d = torch.clamp(X / Y, min=eps)
-        return (d - torch.log(d) - 1.0).sum(dim=(1, 2))
-    return ((X ** beta + (beta - 1.0) * Y ** beta - beta * X * Y ** (beta - 1.0)) /
-            (beta * (beta - 1.0))).sum(dim=(1, 2))
 
 
 # =============================================================================== api

@@ -233,6 +233,132 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
                      int(init), _stream_ptr(lin))
 
 
+# ----------------------------------------------------------------------------- beta MU
+def beta_mode(beta: float) -> int:
+    return 0 if beta == 1.0 else (1 if beta == 0.0 else 2)
+
+
+def beta_contract(side: str, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor,
+                  beta: float, eps: float, want_num: bool = True, want_loss: bool = False,
+                  active: torch.Tensor | None = None, splits: int | None = None):
+    """Fused beta-divergence MU contraction (csrc/kernels/beta_mu.hip).
+
+    ``X`` (N, G) with unit column stride; ``HT3`` (R, K, N) and ``W3`` (R, K, G) views with
+    unit inner stride.  With P = max(HT^T W, eps), Q = X P^(beta-2), D = P^(beta-1):
+      side "h": num = W Q^T (R,K,N), den = W D^T (None when beta == 1: den is rowsum W)
+      side "w": num = HT Q  (R,K,G), den = HT D  (None when beta == 1: den is rowsum HT)
+    ``want_loss`` (side "h") also returns sum D_beta(X || P) per replicate (float64).
+    Replicates whose ``active`` flag is 0 are skipped (their outputs are unspecified).
+    """
+    s = {"h": 0, "w": 1}[side]
+    R, K, N = HT3.shape
+    G = W3.shape[2]
+    if X.shape != (N, G) or W3.shape[:2] != (R, K):
+        raise ValueError(f"beta_contract: X {tuple(X.shape)}, HT3 {tuple(HT3.shape)}, "
+                         f"W3 {tuple(W3.shape)} are inconsistent")
+    if not use_native(HT3) or HT3.dtype != torch.float32 or K > _hip.beta_max_k():
+        return reference.beta_contract(s, X, HT3, W3, beta, eps, want_num, want_loss, active)
+    for name, t in (("X", X), ("HT3", HT3), ("W3", W3)):
+        if t.dtype != torch.float32 or t.device != HT3.device:
+            raise ValueError(f"{name}: float32 on {HT3.device} required")
+        if t.stride(-1) != 1:
+            raise ValueError(f"{name}: unit inner stride required, got {t.stride()}")
+    if active is not None and (active.dtype != torch.int32 or active.numel() < R
+                               or not active.is_contiguous()):
+        raise ValueError("active: contiguous int32 with >= R entries")
+    if s == 1 and not want_num:
+        raise ValueError("side 'w' computes the numerator")
+    mode = beta_mode(beta)
+    dev = HT3.device
+    if s == 0:
+        out_shape = (R, K, N)
+        n_split = 1
+    else:
+        out_shape = (R, K, G)
+        if splits is None:
+            units = ((G + 63) // 64) * R
+            n_split = max(1, min(64, -(-2048 // max(1, units)), N // 1024 or 1))
+        else:
+            n_split = max(1, int(splits))
+    num = den = loss = None
+    if want_num:
+        num = torch.empty((n_split,) + out_shape, device=dev, dtype=torch.float32)
+        if mode != 0:
+            den = torch.empty_like(num)
+    n_strips = (N + 63) // 64
+    if want_loss and s == 0:
+        loss = torch.zeros((R, n_strips), device=dev, dtype=torch.float64)
+    _hip.beta_contract(s, mode, X.data_ptr(), X.stride(0), HT3.data_ptr(), HT3.stride(0),
+                       HT3.stride(1), W3.data_ptr(), W3.stride(0), W3.stride(1), N, G, K, R,
+                       float(beta), float(eps), num.data_ptr() if num is not None else 0,
+                       den.data_ptr() if den is not None else 0,
+                       loss.data_ptr() if loss is not None else 0,
+                       active.data_ptr() if active is not None else 0, n_split, 0, 0, 0.0, 0.0,
+                       1.0, 0.0, 0, 0, 0, 0, _stream_ptr(HT3))
+    if num is not None:
+        num = num[0] if n_split == 1 else num.sum(0)
+        if den is not None:
+            den = den[0] if n_split == 1 else den.sum(0)
+    if loss is not None:
+        loss = loss.sum(1)
+    return num, den, loss
+
+
+_BETA_WS: dict = {}
+
+
+def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float, eps: float,
+                  l1: float = 0.0, l2: float = 0.0, gamma: float = 1.0,
+                  act: torch.Tensor | None = None, tol: float | None = None,
+                  iters: torch.Tensor | None = None) -> None:
+    """One fused in-place beta-MU step of the usages: HT3 *= (num/(den+l1+l2 HT3))^gamma
+    with num/den from the H-side contraction -- the numerator never leaves registers.
+
+    ``act`` (int32 (R,), optional) gates replicates; with ``tol`` the kernel also applies
+    the inner stopping rule on device: act[r] = 0 once ||dh||/(||h||+eps) < tol, and
+    iters[r] += 1 for every replicate that stepped."""
+    R, K, N = HT3.shape
+    G = W3.shape[2]
+    if not use_native(HT3) or HT3.dtype != torch.float32 or K > _hip.beta_max_k():
+        return reference.beta_update_h(X, HT3, W3, beta, eps, l1, l2, gamma, act, tol, iters)
+    if X.shape != (N, G) or W3.shape[:2] != (R, K):
+        raise ValueError("beta_update_h: inconsistent shapes")
+    for name, t in (("X", X), ("HT3", HT3), ("W3", W3)):
+        if t.dtype != torch.float32 or t.device != HT3.device or t.stride(-1) != 1:
+            raise ValueError(f"{name}: float32, unit inner stride, on {HT3.device} required")
+    for name, t in (("act", act), ("iters", iters)):
+        if t is not None and (t.dtype != torch.int32 or t.numel() < R or not t.is_contiguous()):
+            raise ValueError(f"{name}: contiguous int32 with >= R entries")
+    if tol is not None and act is None:
+        raise ValueError("the inner stopping rule needs an act array")
+    mode = beta_mode(beta)
+    dev = HT3.device
+    den_vec = W3.sum(dim=2).contiguous() if mode == 0 else None
+    if den_vec is not None and den_vec.dtype != torch.float32:
+        den_vec = den_vec.float()
+    n_strips = (N + 63) // 64
+    part = counter = None
+    if tol is not None:
+        key = (str(dev), _stream_ptr(HT3))
+        ws = _BETA_WS.get(key)
+        if ws is None or ws["part"].numel() < R * n_strips * 2 or ws["counter"].numel() < R:
+            ws = {"part": torch.empty(max(R * n_strips * 2, 1 << 12), device=dev),
+                  "counter": torch.zeros(max(R, 1024), dtype=torch.int32, device=dev)}
+            _BETA_WS[key] = ws
+        part, counter = ws["part"], ws["counter"]
+    _hip.beta_contract(0, mode, X.data_ptr(), X.stride(0), HT3.data_ptr(), HT3.stride(0),
+                       HT3.stride(1), W3.data_ptr(), W3.stride(0), W3.stride(1), N, G, K, R,
+                       float(beta), float(eps), 0, 0, 0,
+                       act.data_ptr() if act is not None else 0, 1, 1,
+                       den_vec.data_ptr() if den_vec is not None else 0, float(l1), float(l2),
+                       float(gamma), float(tol if tol is not None else 0.0),
+                       part.data_ptr() if part is not None else 0,
+                       counter.data_ptr() if counter is not None else 0,
+                       act.data_ptr() if (act is not None and tol is not None) else 0,
+                       iters.data_ptr() if (iters is not None and tol is not None) else 0,
+                       _stream_ptr(HT3))
+
+
 # ----------------------------------------------------------------------------- init
 def philox_fill(out: torch.Tensor, seeds: torch.Tensor, scales: torch.Tensor, stream: int,
                 mode: int = 0, row_offset: int = 0) -> None:

@@ -128,3 +128,88 @@ def conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init=False):
     state["err_prev"][:n] = torch.where(keep, e, state["err_prev"][:n])
     state["active"][:n] = torch.where(stop, torch.zeros_like(state["active"][:n]),
                                       state["active"][:n])
+
+
+def beta_terms(X: torch.Tensor, P: torch.Tensor, beta: float, eps: float):
+    """Q = X * P^(beta-2), D = P^(beta-1) with P clamped at eps (beta_mu.hip)."""
+    Pc = torch.clamp(P, min=eps)
+    if beta == 1.0:
+        return X / Pc, None
+    if beta == 0.0:
+        r = Pc.reciprocal()
+        return X * r * r, r
+    return X * Pc ** (beta - 2.0), Pc ** (beta - 1.0)
+
+
+def beta_loss_terms(X: torch.Tensor, P: torch.Tensor, beta: float, eps: float) -> torch.Tensor:
+    Pc = torch.clamp(P, min=eps)
+    if beta == 1.0:
+        pos = X > 0
+        t = torch.where(pos, X * torch.log(torch.where(pos, X, torch.ones_like(X)) / Pc),
+                        torch.zeros_like(Pc))
+        return t - X + Pc
+    if beta == 0.0:
+        d = torch.clamp(X / Pc, min=eps)
+        return d - torch.log(d) - 1.0
+    return (X ** beta + (beta - 1.0) * Pc ** beta - beta * X * Pc ** (beta - 1.0)) / (
+        beta * (beta - 1.0))
+
+
+def beta_contract(side: int, X, HT3, W3, beta: float, eps: float, want_num: bool = True,
+                  want_loss: bool = False, active=None, row_chunk: int = 4096):
+    """Reference of cnmf_beta_contract: returns (num, den, loss) with num/den (R,K,N) for
+    side 0 (H) and (R,K,G) for side 1 (W); den is None for beta == 1; loss (R,) float64
+    (side 0 only) or None.  Inactive replicates get zeros."""
+    R, K, N = HT3.shape
+    G = W3.shape[2]
+    dt = HT3.dtype
+    out_n = N if side == 0 else G
+    num = torch.zeros((R, K, out_n), dtype=dt, device=HT3.device) if want_num else None
+    den = (torch.zeros((R, K, out_n), dtype=dt, device=HT3.device)
+           if (want_num and beta != 1.0) else None)
+    loss = torch.zeros(R, dtype=torch.float64, device=HT3.device) if (want_loss and side == 0) else None
+    reps = range(R) if active is None else [r for r in range(R) if int(active[r]) != 0]
+    for r in reps:
+        for a in range(0, N, row_chunk):
+            b = min(N, a + row_chunk)
+            x = X[a:b].to(dt)
+            h = HT3[r, :, a:b]                      # (K, c)
+            P = h.t() @ W3[r]                       # (c, G)
+            Q, D = beta_terms(x, P, beta, eps)
+            if want_num:
+                if side == 0:
+                    num[r, :, a:b] = W3[r] @ Q.t()
+                    if D is not None:
+                        den[r, :, a:b] = W3[r] @ D.t()
+                else:
+                    num[r] += h @ Q
+                    if D is not None:
+                        den[r] += h @ D
+            if loss is not None:
+                loss[r] += beta_loss_terms(x.double(), P.double(), beta, eps).sum()
+    return num, den, loss
+
+
+def beta_update_h(X, HT3, W3, beta, eps, l1=0.0, l2=0.0, gamma=1.0, act=None, tol=None,
+                  iters=None):
+    """Reference of the fused in-place usage update (beta_mu.hip, upd != 0)."""
+    R = HT3.shape[0]
+    num, den, _ = beta_contract(0, X, HT3, W3, beta, eps, True, False, act)
+    if den is None:
+        den = W3.sum(dim=2, keepdim=True)
+    d = den + l1 + l2 * HT3
+    d = torch.where(d == 0, torch.full_like(d, eps), d)
+    delta = num / d
+    if gamma != 1.0:
+        delta = delta ** gamma
+    live = torch.ones(R, dtype=torch.bool, device=HT3.device) if act is None else (act[:R] != 0)
+    delta = torch.where(live.view(R, 1, 1), delta, torch.ones_like(delta))
+    if tol is not None:
+        dn = torch.linalg.vector_norm((HT3 * (delta - 1.0)).double(), dim=(1, 2))
+        hn = torch.linalg.vector_norm(HT3.double(), dim=(1, 2))
+    HT3.mul_(delta)
+    if tol is not None:
+        stop = live & (dn / (hn + eps) < tol)
+        act[:R][stop] = 0
+        if iters is not None:
+            iters[:R] += live.to(iters.dtype)

@@ -57,6 +57,23 @@ PYBIND11_MODULE(_hip, m) {
                 "cnmf_conv_update");
         });
 
+  m.def("beta_max_k", []() { return cnmf_beta_max_k(); });
+  m.def("beta_contract",
+        [](int side, int mode, uintptr_t X, long long ldx, uintptr_t HT, long long h_rs,
+           long long ldh, uintptr_t W, long long w_rs, long long ldw, int N, int G, int K, int R,
+           float beta, float eps, uintptr_t num, uintptr_t den, uintptr_t loss, uintptr_t active,
+           int splits, int upd, uintptr_t den_vec, float l1, float l2, float gamma, float tol,
+           uintptr_t part, uintptr_t counter, uintptr_t act, uintptr_t iters, uintptr_t stream) {
+          check(cnmf_beta_contract(side, mode, P<const float>(X), ldx, P<const float>(HT), h_rs,
+                                   ldh, P<const float>(W), w_rs, ldw, N, G, K, R, beta, eps,
+                                   P<float>(num), P<float>(den), P<double>(loss),
+                                   P<const int>(active), splits, upd, P<const float>(den_vec),
+                                   l1, l2, gamma, tol, P<float>(part), P<int>(counter),
+                                   P<int>(act), P<int>(iters),
+                                   reinterpret_cast<hipStream_t>(stream)),
+                "beta_contract");
+        });
+
   m.def("philox_fill",
         [](uintptr_t out, long long rows, long long cols, long long s_row, long long s_col,
            long long rep_stride, long long row_offset, uintptr_t seeds, uintptr_t scales, int R,

@@ -21,6 +21,15 @@ hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, do
                             int init, hipStream_t stream);
 int cnmf_solve_reg_max_cols(int K);
 
+int cnmf_beta_max_k();
+hipError_t cnmf_beta_contract(int side, int mode, const float* X, long long ldx, const float* HT,
+                              long long h_rs, long long ldh, const float* W, long long w_rs,
+                              long long ldw, int N, int G, int K, int R, float beta, float eps,
+                              float* num, float* den, double* loss, const int* active,
+                              int splits, int upd, const float* den_vec, float l1, float l2,
+                              float gamma, float tol, float* part, int* counter, int* act,
+                              int* iters, hipStream_t stream);
+
 hipError_t cnmf_philox_fill(float* out, long long rows, long long cols, long long s_row,
                             long long s_col, long long rep_stride, long long row_offset,
                             const unsigned long long* seeds, const float* scales, int R,

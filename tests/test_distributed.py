@@ -36,11 +36,16 @@ def test_comm_primitives(tmp_path):
         assert t == 6.0 and abs(s - 4.5) < 1e-12 and m == 20 and n == 3 and last == 2
 
 
-@pytest.mark.parametrize("algo,mode", [("mu", "online"), ("hals", "online"), ("mu", "batch")])
-def test_dp_solver_matches_single_process(tmp_path, algo, mode):
+@pytest.mark.parametrize("algo,mode,beta_loss", [("mu", "online", "frobenius"),
+                                                 ("hals", "online", "frobenius"),
+                                                 ("mu", "batch", "frobenius"),
+                                                 ("mu", "batch", "kullback-leibler"),
+                                                 ("mu", "online", "kullback-leibler")])
+def test_dp_solver_matches_single_process(tmp_path, algo, mode, beta_loss):
     X = normalized_counts_matrix(603, 120, n_programs=4, seed=1)
     K, seeds, world = 4, [5, 6, 7], 2
-    kw = dict(algo=algo, mode=mode, online_chunk_size=100, online_max_pass=6, batch_max_iter=30)
+    kw = dict(algo=algo, mode=mode, online_chunk_size=100, online_max_pass=6, batch_max_iter=30,
+              beta_loss=beta_loss)
     _spawn(W.dp_solver_worker, world, X, K, seeds, kw, str(tmp_path))
     # single-process emulation of the sharded schedule: step s = {rank0 chunk s, rank1 chunk s}
     blocks = [row_block(X.shape[0], r, world) for r in range(world)]

@@ -177,17 +177,88 @@ def test_philox_matches_numpy(mode):
                                    atol=1e-7)
 
 
-@pytest.mark.parametrize("algo", ["mu", "hals"])
+@pytest.mark.parametrize("algo,beta_loss", [("mu", "frobenius"), ("hals", "frobenius"),
+                                            ("mu", "kullback-leibler")])
 @pytest.mark.parametrize("mode", ["online", "batch"])
-def test_nmf_batch_gpu_matches_cpu(algo, mode):
+def test_nmf_batch_gpu_matches_cpu(algo, mode, beta_loss):
     from cnmf_torch_amd.models.nmf import run_nmf_batch
 
     rs = np.random.default_rng(0)
     N, G, K = 1500, 400, 6
     X = (rs.gamma(1, 1, (N, K)) @ rs.gamma(0.5, 1, (K, G)) + 0.1 * rs.random((N, G))).astype(
         np.float32)
-    kw = dict(algo=algo, mode=mode, online_chunk_size=700, online_max_pass=5, batch_max_iter=40)
+    kw = dict(algo=algo, mode=mode, online_chunk_size=700, online_max_pass=5, batch_max_iter=40,
+              beta_loss=beta_loss)
     g = run_nmf_batch(X, K, [11, 12, 13], device="cuda", **kw)
     c = run_nmf_batch(X, K, [11, 12, 13], device="cpu", **kw)
     # same init, same algorithm: errors agree to fp32 reassociation noise
     np.testing.assert_allclose(g.err, c.err, rtol=2e-2)
+
+
+@pytest.mark.parametrize("beta", [1.0, 0.0, 1.5])
+@pytest.mark.parametrize("K", [3, 10, 17, 32])
+def test_beta_contract_matches_reference(beta, K):
+    """Fused MFMA beta-MU contraction (beta_mu.hip) vs a float64 PyTorch reference."""
+    g = torch.Generator().manual_seed(K)
+    R, N, G = 3, 1000 + 37, 300 + 5          # ragged vs the 64-wide strips / 256 chunks
+    X = torch.rand((N + 3, G), generator=g, dtype=torch.float64)
+    X[X < 0.3] = 0.0                          # zeros exercise the KL x>0 branch
+    HT = torch.rand((R * K, N), generator=g, dtype=torch.float64) + 0.05
+    W = torch.rand((R * K, G), generator=g, dtype=torch.float64) + 0.05
+    dev = torch.device("cuda")
+    Xs = X[2:N + 2]                           # row-offset view (unaligned base pointer)
+    active = torch.tensor([1, 0, 1], dtype=torch.int32)
+    eps = 1e-10
+    for side in ("h", "w"):
+        ref = reference.beta_contract(0 if side == "h" else 1, Xs, HT.view(R, K, N),
+                                      W.view(R, K, G), beta, eps, True, side == "h")
+        out = ops.beta_contract(side, Xs.float().to(dev), HT.float().to(dev).view(R, K, N),
+                                W.float().to(dev).view(R, K, G), beta, eps, True, side == "h",
+                                active=active.to(dev))
+        for r in (0, 2):
+            torch.testing.assert_close(out[0][r].cpu().double(), ref[0][r], rtol=2e-4, atol=1e-4)
+            if beta != 1.0:
+                torch.testing.assert_close(out[1][r].cpu().double(), ref[1][r], rtol=2e-4,
+                                           atol=1e-4)
+            if side == "h":
+                torch.testing.assert_close(out[2][r].cpu(), ref[2][r], rtol=1e-4, atol=1e-3)
+        if beta == 1.0:
+            assert out[1] is None
+    # W-side split over cells == unsplit
+    a = ops.beta_contract("w", X[:N].float().to(dev), HT.float().to(dev).view(R, K, N),
+                          W.float().to(dev).view(R, K, G), beta, eps, splits=1)[0]
+    b = ops.beta_contract("w", X[:N].float().to(dev), HT.float().to(dev).view(R, K, N),
+                          W.float().to(dev).view(R, K, G), beta, eps, splits=5)[0]
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("beta", [1.0, 0.0])
+def test_beta_update_h_fused_matches_reference(beta):
+    """In-place fused usage update + on-device inner stopping rule == reference."""
+    g = torch.Generator().manual_seed(1)
+    R, K, N, G = 4, 10, 777, 260
+    X = torch.rand((N, G), generator=g, dtype=torch.float64)
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.05
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.05
+    dev = torch.device("cuda")
+    act0 = torch.tensor([1, 1, 0, 1], dtype=torch.int32)
+    # replicate 3 starts at its own fixed point-ish (tiny change) -> should stop
+    ref_h = HT.clone()
+    ref_act, ref_it = act0.clone(), torch.zeros(R, dtype=torch.int32)
+    gpu_h = HT.float().to(dev)
+    gpu_act, gpu_it = act0.to(dev), torch.zeros(R, dtype=torch.int32, device=dev)
+    for _ in range(6):
+        reference.beta_update_h(X, ref_h, W, beta, 1e-10, 0.01, 0.02, 1.0 if beta else 0.5,
+                                ref_act, 0.02, ref_it)
+        ops.beta_update_h(X.float().to(dev), gpu_h, W.float().to(dev), beta, 1e-10, 0.01, 0.02,
+                          1.0 if beta else 0.5, gpu_act, 0.02, gpu_it)
+    torch.testing.assert_close(gpu_h.cpu().double(), ref_h, rtol=1e-4, atol=1e-5)
+    assert gpu_act.cpu().tolist() == ref_act.tolist()
+    assert gpu_it.cpu().tolist() == ref_it.tolist()
+    assert torch.equal(gpu_h[2].cpu(), HT[2].float())       # inactive replicate untouched
+    # plain update (no act / tol): batch mode
+    h1 = HT.float().to(dev)
+    ops.beta_update_h(X.float().to(dev), h1, W.float().to(dev), beta, 1e-10)
+    h2 = HT.clone()
+    reference.beta_update_h(X, h2, W, beta, 1e-10)
+    torch.testing.assert_close(h1.cpu().double(), h2, rtol=1e-4, atol=1e-5)

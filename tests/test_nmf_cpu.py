@@ -1,0 +1,90 @@
+"""CPU numerics of the replicate-batched NMF engine (models/nmf.py) against scikit-learn.
+
+sklearn's ``non_negative_factorization(solver='mu')`` is the reference math the SURVEY
+points at for the beta-divergence updates (sklearn/decomposition/_nmf.py:526-728); with
+``init='custom'`` and the same starting factors, the batch MU trajectory must agree.
+"""
+import numpy as np
+import pytest
+import torch
+from sklearn.decomposition import non_negative_factorization
+
+from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions, run_nmf
+from cnmf_torch_amd.ops import reference
+from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+EPS32 = float(np.finfo(np.float32).eps)
+
+
+def _data(n=240, g=90, seed=0):
+    X = normalized_counts_matrix(n, g, n_programs=4, seed=seed).astype(np.float64)
+    return X + 0.01  # strictly positive: sklearn zeroes sub-eps factors for beta <= 1
+
+
+@pytest.mark.parametrize("beta_loss,beta", [("kullback-leibler", 1.0), ("itakura-saito", 0.0),
+                                            (1.5, 1.5)])
+def test_batch_beta_mu_matches_sklearn(beta_loss, beta):
+    X = _data()
+    K, n_it = 4, 25
+    rng = np.random.default_rng(3)
+    H0 = rng.random((X.shape[0], K)) + 0.1      # usages  (sklearn W)
+    W0 = rng.random((K, X.shape[1])) + 0.1      # spectra (sklearn H)
+    Wsk, Hsk, _ = non_negative_factorization(X, W=H0.copy(), H=W0.copy(), n_components=K,
+                                             init="custom", solver="mu", beta_loss=beta_loss,
+                                             max_iter=n_it, tol=0.0)
+    opts = NMFOptions(n_components=K, beta_loss=beta_loss, mode="batch", batch_max_iter=n_it,
+                      tol=-1.0, fp_precision="double", eps=EPS32, loss_every=5)
+    res = NMFBatchSolver(torch.from_numpy(X), opts).run(
+        [1], HT0=torch.from_numpy(H0.T.copy()), W0=torch.from_numpy(W0))
+    np.testing.assert_allclose(res.usages(0).numpy(), Wsk, rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(res.spectra(0).numpy(), Hsk, rtol=1e-7, atol=1e-9)
+    # reported error = sqrt(2 * D_beta) of the final factors
+    P = Wsk @ Hsk
+    D = float(reference.beta_loss_terms(torch.from_numpy(X), torch.from_numpy(P), beta,
+                                        EPS32).sum())
+    assert abs(res.err[0] - np.sqrt(2 * D)) <= 1e-9 * max(1.0, np.sqrt(2 * D))
+
+
+def test_beta_contract_reference_identities():
+    """side 'h'/'w' numerators are the two contractions of Q = X / (HT^T W)."""
+    g = torch.Generator().manual_seed(0)
+    R, K, N, G = 2, 3, 50, 40
+    X = torch.rand((N, G), generator=g, dtype=torch.float64)
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.1
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.1
+    nh, dh, loss = reference.beta_contract(0, X, HT, W, 1.0, 1e-12, True, True)
+    nw, dw, _ = reference.beta_contract(1, X, HT, W, 1.0, 1e-12, True, False)
+    assert dh is None and dw is None
+    for r in range(R):
+        Q = X / (HT[r].t() @ W[r])
+        torch.testing.assert_close(nh[r], W[r] @ Q.t())
+        torch.testing.assert_close(nw[r], HT[r] @ Q)
+        P = HT[r].t() @ W[r]
+        kl = (X * torch.log(X / P) - X + P).sum()
+        torch.testing.assert_close(loss[r], kl)
+
+
+@pytest.mark.parametrize("mode", ["online", "batch"])
+def test_kl_decreases_and_recovers(mode):
+    X = _data(400, 120, seed=2)
+    H, W, err = run_nmf(X, 4, beta_loss="kullback-leibler", mode=mode, random_state=5,
+                        online_chunk_size=150, batch_max_iter=200, tol=1e-5)
+    assert H.shape == (400, 4) and W.shape == (4, 120)
+    assert np.all(H >= 0) and np.all(W >= 0)
+    # the error must be well below that of the random init and below a rank-1 model
+    P1 = np.outer(X.sum(1), X.sum(0)) / X.sum()
+    kl1 = float(reference.beta_loss_terms(torch.from_numpy(X), torch.from_numpy(P1), 1.0,
+                                          1e-16).sum())
+    assert err < 0.8 * np.sqrt(2 * kl1), (err, np.sqrt(2 * kl1))
+
+
+def test_online_kl_passes_monotone_errors():
+    X = _data(300, 80, seed=4)
+    opts = NMFOptions(n_components=3, beta_loss="kullback-leibler", mode="online",
+                      online_chunk_size=100, online_max_pass=6, tol=-1.0, fp_precision="double")
+    solver = NMFBatchSolver(torch.from_numpy(X), opts)
+    errs = []
+    for p in (1, 2, 4, 6):
+        solver.opts.online_max_pass = p
+        errs.append(float(solver.run([7]).err[0]))
+    assert all(b <= a * (1 + 1e-9) for a, b in zip(errs, errs[1:])), errs
