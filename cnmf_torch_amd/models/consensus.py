@@ -20,32 +20,26 @@ import math
 import numpy as np
 import torch
 
+from .. import ops
+
 
 def l2_normalize_rows(S: torch.Tensor) -> torch.Tensor:
     return S / torch.sqrt((S * S).sum(dim=1, keepdim=True))
 
 
 def pairwise_distances(A: torch.Tensor, B: torch.Tensor | None = None) -> torch.Tensor:
-    """Euclidean distances (float64 accumulation of the norms; sklearn semantics:
-    clipped at 0, exact zeros on the diagonal when B is A)."""
-    same = B is None
-    B = A if same else B
-    Ad, Bd = A.to(torch.float64), B.to(torch.float64)
-    aa = (Ad * Ad).sum(dim=1, keepdim=True)
-    bb = (Bd * Bd).sum(dim=1, keepdim=True).t()
-    d2 = aa + bb - 2.0 * (Ad @ Bd.t())
-    d2.clamp_(min=0.0)
-    if same:
-        d2.fill_diagonal_(0.0)
-    return torch.sqrt(d2)
+    """Euclidean distances in float64 (sklearn semantics: clipped at 0, exact zeros on the
+    diagonal when B is A).  GPU: f64 MFMA kernel (ops.pairwise_dist)."""
+    return ops.pairwise_dist(A, B)
 
 
 def local_density(dist: torch.Tensor, n_neighbors: int) -> torch.Tensor:
     """Mean distance to the ``n_neighbors`` nearest neighbours (cnmf.py:1065-1070):
-    sum of the (n_neighbors+1) smallest distances of each row (self included) / n_neighbors."""
+    sum of the (n_neighbors+1) smallest distances of each row (self included) / n_neighbors.
+    GPU: exact radix-select kernel (ops.knn_sum)."""
     k = min(n_neighbors + 1, dist.shape[1])
-    vals = torch.topk(dist, k, dim=1, largest=False).values
-    return vals.sum(dim=1) / max(n_neighbors, 1) if n_neighbors > 0 else vals.sum(dim=1) * float("inf")
+    tot = ops.knn_sum(dist, k)
+    return tot / max(n_neighbors, 1) if n_neighbors > 0 else tot * float("inf")
 
 
 # ------------------------------------------------------------------------- k-means
@@ -56,14 +50,13 @@ def _kmeanspp(X: torch.Tensor, k: int, gen: torch.Generator, x_sq: torch.Tensor)
     centers = torch.empty((k, X.shape[1]), dtype=X.dtype, device=X.device)
     first = int(torch.randint(n, (1,), generator=gen).item())
     centers[0] = X[first]
-    closest = ((X - X[first]) ** 2).sum(dim=1)
+    closest = ops.pairwise_dist(X, X[first:first + 1], squared=True)[:, 0]
     pot = float(closest.sum())
     for c in range(1, k):
         r = torch.rand(trials, generator=gen, dtype=torch.float64) * pot
         cum = torch.cumsum(closest.double(), 0).cpu()
         cand = torch.searchsorted(cum, r).clamp(max=n - 1).to(X.device)
-        d = x_sq[:, None] + x_sq[cand][None, :] - 2 * X @ X[cand].t()
-        d.clamp_(min=0)
+        d = ops.pairwise_dist(X, X[cand], squared=True)
         newc = torch.minimum(closest[:, None], d)
         pots = newc.sum(dim=0)
         best = int(torch.argmin(pots))
@@ -73,31 +66,40 @@ def _kmeanspp(X: torch.Tensor, k: int, gen: torch.Generator, x_sq: torch.Tensor)
     return centers
 
 
-def _lloyd(X, centers, x_sq, max_iter: int, tol: float):
-    inertia = None
-    labels = None
+def _lloyd_batched(X: torch.Tensor, centers: torch.Tensor, max_iter: int, tol: float):
+    """Lloyd iterations for all restarts at once: centers (n_init, k, d).  Assignment is
+    one f64 MFMA distance launch over the n_init*k centroids + a segmented argmin
+    (ops.seg_argmin); restarts that stop moving (shift <= tol) are frozen.
+    Returns (labels (n, n_init), inertia (n_init,))."""
+    n_init, k, d = centers.shape
+    n = X.shape[0]
+    live = torch.ones(n_init, dtype=torch.bool, device=X.device)
+    offs = (torch.arange(n_init, device=X.device) * k)[None, :]
     for _ in range(max_iter):
-        c_sq = (centers * centers).sum(dim=1)
-        d = x_sq[:, None] + c_sq[None, :] - 2 * X @ centers.t()
-        labels = torch.argmin(d, dim=1)
-        k = centers.shape[0]
-        counts = torch.bincount(labels, minlength=k).to(X.dtype)
-        sums = torch.zeros_like(centers).index_add_(0, labels, X)
-        newc = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], centers)
-        shift = float(((newc - centers) ** 2).sum())
-        centers = newc
-        if shift <= tol:
+        C = centers.reshape(n_init * k, d)
+        lab, _ = ops.seg_argmin(ops.pairwise_dist(X, C, squared=True), k)
+        flat = (lab + offs).t().reshape(-1)                       # restart-major
+        sums = torch.zeros((n_init * k, d), dtype=X.dtype, device=X.device)
+        for r in range(n_init):
+            sums.index_add_(0, flat[r * n:(r + 1) * n], X)
+        counts = torch.bincount(flat, minlength=n_init * k).to(X.dtype)
+        newc = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], C)
+        newc = newc.view(n_init, k, d)
+        shift = ((newc - centers) ** 2).sum(dim=(1, 2))
+        centers = torch.where(live[:, None, None], newc, centers)
+        live = live & (shift > tol)
+        if not bool(live.any()):
             break
-    c_sq = (centers * centers).sum(dim=1)
-    d = x_sq[:, None] + c_sq[None, :] - 2 * X @ centers.t()
-    labels = torch.argmin(d, dim=1)
-    inertia = float(torch.gather(d, 1, labels[:, None]).clamp(min=0).sum())
-    return labels, centers, inertia
+    lab, mind = ops.seg_argmin(ops.pairwise_dist(X, centers.reshape(n_init * k, d),
+                                                 squared=True), k)
+    return lab, mind.sum(dim=0)
 
 
 def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 300,
            tol: float = 1e-4, backend: str = "sklearn"):
-    """Returns integer labels 0..k-1 (numpy)."""
+    """Returns integer labels 0..k-1 (numpy).  ``backend='sklearn'`` is the reference's
+    KMeans(n_clusters=k, n_init=10, random_state=1) (cnmf.py:1082) bit for bit;
+    ``'device'`` runs k-means++ + batched Lloyd on the tensor's device (HIP kernels)."""
     if backend == "sklearn":
         from sklearn.cluster import KMeans
 
@@ -111,13 +113,10 @@ def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 3
     tol_abs = tol * float(Xt.var(dim=0, unbiased=False).mean())
     x_sq = (Xt * Xt).sum(dim=1)
     gen = torch.Generator(device="cpu").manual_seed(int(random_state))
-    best = None
-    for _ in range(n_init):
-        c0 = _kmeanspp(Xt, k, gen, x_sq)
-        labels, centers, inertia = _lloyd(Xt, c0, x_sq, max_iter, tol_abs)
-        if best is None or inertia < best[0]:
-            best = (inertia, labels)
-    return best[1].cpu().numpy()
+    c0 = torch.stack([_kmeanspp(Xt, k, gen, x_sq) for _ in range(n_init)])
+    labels, inertia = _lloyd_batched(Xt, c0, max_iter, tol_abs)
+    best = int(torch.argmin(inertia))
+    return labels[:, best].cpu().numpy()
 
 
 def cluster_medians(S: torch.Tensor, labels: np.ndarray, k_labels) -> torch.Tensor:

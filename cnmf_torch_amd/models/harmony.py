@@ -27,6 +27,8 @@ import numpy as np
 import pandas as pd
 import torch
 
+from .. import ops
+
 
 def _design(meta: pd.DataFrame, vars_use) -> tuple[np.ndarray, np.ndarray]:
     if isinstance(vars_use, str):
@@ -54,7 +56,7 @@ class Harmony:
     def __init__(self, Z, Phi, Phi_moe, Pr_b, sigma, theta, lamb, K, max_iter_harmony=10,
                  max_iter_kmeans=20, epsilon_kmeans=1e-5, epsilon_harmony=1e-4,
                  block_size=0.05, random_state=0, init_backend="sklearn", device=None,
-                 verbose=False):
+                 verbose=False, phi_n=None):
         dev = torch.device(device) if device is not None else torch.device("cpu")
         dt = torch.float64
         self.dev, self.dt = dev, dt
@@ -80,6 +82,15 @@ class Harmony:
         self.objective_harmony: list[float] = []
         self.kmeans_rounds: list[int] = []
         self.verbose = verbose
+        # fused HIP R-update (harmony.hip) needs each cell's batch index per covariate
+        self._native = (phi_n is not None and
+                        ops.harmony_native_ok(self.Phi, self.K, self.Phi.shape[0]))
+        if self._native:
+            offs = np.concatenate([[0], np.cumsum(phi_n)[:-1]]).astype(np.int64)
+            Pn = np.asarray(Phi)
+            bidx = np.stack([o + Pn[o:o + c].argmax(axis=0) for o, c in zip(offs, phi_n)])
+            self.bidx = torch.as_tensor(bidx.astype(np.int32), device=dev).contiguous()
+            self._ws: dict = {}
         self._init_cluster(init_backend)
         self._harmonize(max_iter_harmony)
 
@@ -101,11 +112,14 @@ class Harmony:
             onehot = (labels[None, :] == torch.arange(self.K, device=self.dev)[:, None]).to(self.dt)
             Y = (X.t() @ onehot.t()) / onehot.sum(dim=1).clamp(min=1)[None, :]
         self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
-        self.dist_mat = 2 * (1 - self.Y.t() @ self.Z_cos)
+        self._dist()
         R = -self.dist_mat / self.sigma[:, None]
         R = R - R.max(dim=0).values
         R = torch.exp(R)
         self.R = R / R.sum(dim=0)
+        if self._native:   # cell-major storage; self.R stays a (K, N) view of it
+            self.Rt = self.R.t().contiguous()
+            self.R = self.Rt.t()
         self.E = torch.outer(self.R.sum(dim=1), self.Pr_b)
         self.O = self.R @ self.Phi.t()
         self._objective()
@@ -129,13 +143,21 @@ class Harmony:
             if self._converged(1):
                 break
 
+    def _dist(self):
+        """dist = 2 (1 - Y^T Z_cos); cell-major (N, K) for the native R update."""
+        if self._native:
+            self.distT = 2 * (1 - self.Z_cos.t() @ self.Y)
+            self.dist_mat = self.distT.t()
+        else:
+            self.dist_mat = 2 * (1 - self.Y.t() @ self.Z_cos)
+
     def _cluster(self):
-        self.dist_mat = 2 * (1 - self.Y.t() @ self.Z_cos)
+        self._dist()
         i = 0
         for i in range(self.max_iter_kmeans):
             Y = self.Z_cos @ self.R.t()
             self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
-            self.dist_mat = 2 * (1 - self.Y.t() @ self.Z_cos)
+            self._dist()
             self._update_R()
             self._objective()
             if i > self.window_size and self._converged(0):
@@ -144,10 +166,20 @@ class Harmony:
         self.objective_harmony.append(self.objective_kmeans[-1])
 
     def _update_R(self):
+        order = np.arange(self.N)
+        if self._native:
+            self.rs.shuffle(order)
+            n_blocks = int(math.ceil(1 / self.block_size))
+            self.E = self.E.contiguous()
+            self.O = self.O.contiguous()
+            for b in np.array_split(order, n_blocks):
+                cells = torch.as_tensor(b.astype(np.int32), device=self.dev)
+                ops.harmony_block_update(self.Rt, self.distT, self.sigma, cells, self.bidx,
+                                         self.E, self.O, self.Pr_b, self.theta, self._ws)
+            return
         sd = -self.dist_mat / self.sigma[:, None]
         sd = sd - sd.max(dim=0).values
         sd = torch.exp(sd)
-        order = np.arange(self.N)
         self.rs.shuffle(order)
         n_blocks = int(math.ceil(1 / self.block_size))
         for b in np.array_split(order, n_blocks):
@@ -217,7 +249,7 @@ def run_harmony(data_mat, meta_data: pd.DataFrame, vars_use, theta=None, lamb=No
     Phi_moe = np.vstack((np.ones((1, N)), Phi))
     ho = Harmony(Z, Phi, Phi_moe, Pr_b, sigma, theta, lamb_mat, nclust, max_iter_harmony,
                  max_iter_kmeans, epsilon_cluster, epsilon_harmony, block_size, random_state,
-                 init_backend, device, verbose)
+                 init_backend, device, verbose, phi_n=phi_n)
     return ho.result()
 
 

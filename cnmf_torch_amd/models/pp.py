@@ -53,12 +53,16 @@ def normalize_total(adata, target_sum: float | None = None, copy: bool = False, 
 def _mean_var_ddof1(X):
     n = X.shape[0]
     if sp.issparse(X):
-        mean = np.asarray(X.mean(axis=0, dtype=np.float64)).reshape(-1)
-        mean_sq = np.asarray(X.multiply(X).mean(axis=0, dtype=np.float64)).reshape(-1)
+        # scanpy's sparse path: sklearn's centred two-pass variance (exact 0 for constant
+        # genes); the dense path below is scanpy's E[x^2] - E[x]^2
+        from sklearn.utils.sparsefuncs import mean_variance_axis
+
+        mean, var = mean_variance_axis(sp.csr_matrix(X, dtype=np.float64), axis=0)
+        mean, var = np.asarray(mean, dtype=np.float64), np.asarray(var, dtype=np.float64)
     else:
         mean = np.mean(X, axis=0, dtype=np.float64)
         mean_sq = np.mean(np.multiply(X, X, dtype=np.float64), axis=0)
-    var = mean_sq - mean ** 2
+        var = mean_sq - mean ** 2
     if n > 1:
         var *= n / (n - 1)
     return mean, var

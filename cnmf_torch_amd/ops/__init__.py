@@ -359,6 +359,122 @@ def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: fl
                        _stream_ptr(HT3))
 
 
+# ----------------------------------------------------------------------------- consensus
+def _f64_rows(t: torch.Tensor) -> torch.Tensor:
+    t = t.to(torch.float64)
+    return t if t.stride(-1) == 1 else t.contiguous()
+
+
+def pairwise_dist(A: torch.Tensor, B: torch.Tensor | None = None,
+                  squared: bool = False) -> torch.Tensor:
+    """Euclidean distances between the rows of A (n, d) and B (m, d) in float64
+    (sklearn euclidean_distances: |a|^2 + |b|^2 - 2ab clipped at 0, zero diagonal when B
+    is A).  GPU: f64 MFMA tiles in consensus.hip."""
+    same = B is None
+    Ad = _f64_rows(A)
+    Bd = Ad if same else _f64_rows(B)
+    if Ad.shape[1] != Bd.shape[1]:
+        raise ValueError("pairwise_dist: feature dimensions differ")
+    na = (Ad * Ad).sum(dim=1)
+    nb = na if same else (Bd * Bd).sum(dim=1)
+    if not use_native(Ad):
+        d2 = na[:, None] + nb[None, :] - 2.0 * (Ad @ Bd.t())
+        d2.clamp_(min=0.0)
+        if same:
+            d2.fill_diagonal_(0.0)
+        return d2 if squared else torch.sqrt(d2)
+    n, m = Ad.shape[0], Bd.shape[0]
+    D = torch.empty((n, m), dtype=torch.float64, device=Ad.device)
+    _hip.pairdist(Ad.data_ptr(), Ad.stride(0), Bd.data_ptr(), Bd.stride(0), na.data_ptr(),
+                  nb.data_ptr(), n, m, Ad.shape[1], D.data_ptr(), m, int(same), int(squared),
+                  _stream_ptr(Ad))
+    return D
+
+
+def knn_sum(D: torch.Tensor, k: int) -> torch.Tensor:
+    """Per row of the non-negative float64 matrix D, the sum of its k smallest entries
+    (exact, ties included).  GPU: radix select in consensus.hip."""
+    n, m = D.shape
+    if not 1 <= k <= m:
+        raise ValueError(f"knn_sum: need 1 <= k <= {m}, got {k}")
+    if not use_native(D):
+        return torch.topk(D, k, dim=1, largest=False).values.sum(dim=1)
+    Dd = _f64_rows(D)
+    out = torch.empty(n, dtype=torch.float64, device=D.device)
+    _hip.knn_sum(Dd.data_ptr(), Dd.stride(0), n, m, int(k), out.data_ptr(), _stream_ptr(Dd))
+    return out
+
+
+def seg_argmin(D: torch.Tensor, k: int, row_add: torch.Tensor | None = None,
+               col_add: torch.Tensor | None = None):
+    """For D (n, nseg*k): per row and segment s, argmin_j (row_add[i] + col_add[s*k+j] +
+    D[i, s*k+j]) and its value clipped at 0 -> (labels int64 (n, nseg), min float64)."""
+    n, mm = D.shape
+    if k < 1 or mm % k:
+        raise ValueError("seg_argmin: columns must be a multiple of k")
+    nseg = mm // k
+    if not use_native(D):
+        V = D.to(torch.float64)
+        if row_add is not None:
+            V = V + row_add.to(torch.float64)[:, None]
+        if col_add is not None:
+            V = V + col_add.to(torch.float64)[None, :]
+        V = V.view(n, nseg, k)
+        mn, lab = V.min(dim=2)
+        return lab, mn.clamp(min=0.0)
+    Dd = _f64_rows(D)
+    ra = row_add.to(torch.float64).contiguous() if row_add is not None else None
+    ca = col_add.to(torch.float64).contiguous() if col_add is not None else None
+    lab = torch.empty((n, nseg), dtype=torch.int32, device=D.device)
+    mind = torch.empty((n, nseg), dtype=torch.float64, device=D.device)
+    _hip.seg_argmin(Dd.data_ptr(), Dd.stride(0), n, nseg, k, ra.data_ptr() if ra is not None else 0,
+                    ca.data_ptr() if ca is not None else 0, lab.data_ptr(), mind.data_ptr(),
+                    _stream_ptr(Dd))
+    return lab.long(), mind
+
+
+# ----------------------------------------------------------------------------- harmony
+def harmony_native_ok(t: torch.Tensor, K: int, B: int) -> bool:
+    """True when the fused Harmony R-update kernels handle this problem on ``t``'s device."""
+    return use_native(t) and K <= 128 and K * B <= _hip.harmony_max_kb()
+
+
+def harmony_block_update(Rt: torch.Tensor, distT: torch.Tensor, sigma: torch.Tensor,
+                         cells: torch.Tensor, bidx: torch.Tensor, E: torch.Tensor,
+                         O: torch.Tensor, Pr_b: torch.Tensor, theta: torch.Tensor,
+                         ws: dict) -> None:
+    """One Harmony block update on device (harmony.hip): remove the block's old R from
+    E/O, recompute the diversity penalty, reassign R for the block's cells, add back.
+    Rt/distT (N, K) float64 contiguous; cells int32 (nb,); bidx int32 (nvar, N);
+    E/O (K, B) float64; ``ws`` caches the partial-sum workspace and arrival counter."""
+    N, K = Rt.shape
+    B = E.shape[1]
+    nvar = bidx.shape[0]
+    nb = int(cells.numel())
+    for name, t, dt in (("Rt", Rt, torch.float64), ("distT", distT, torch.float64),
+                        ("E", E, torch.float64), ("O", O, torch.float64),
+                        ("cells", cells, torch.int32), ("bidx", bidx, torch.int32)):
+        if t.dtype != dt or not t.is_contiguous() or t.device != Rt.device:
+            raise ValueError(f"{name}: contiguous {dt} on {Rt.device} required")
+    if distT.shape != (N, K) or O.shape != (K, B) or bidx.shape[1] != N:
+        raise ValueError("harmony_block_update: inconsistent shapes")
+    chunk = max(32, -(-nb // 256))
+    n_wg = -(-nb // chunk)
+    need = n_wg * K * (B + 1)
+    if ws.get("part") is None or ws["part"].numel() < need:
+        ws["part"] = torch.empty(need, dtype=torch.float64, device=Rt.device)
+    if ws.get("counter") is None:
+        ws["counter"] = torch.zeros(1, dtype=torch.int32, device=Rt.device)
+        ws["pen"] = torch.empty((K, B), dtype=torch.float64, device=Rt.device)
+    st = _stream_ptr(Rt)
+    args = (Rt.data_ptr(), distT.data_ptr(), sigma.data_ptr(), cells.data_ptr(), bidx.data_ptr(),
+            nb, N, K, B, nvar, chunk, E.data_ptr(), O.data_ptr(), Pr_b.data_ptr(),
+            theta.data_ptr(), ws["pen"].data_ptr(), ws["part"].data_ptr(),
+            ws["counter"].data_ptr(), st)
+    _hip.harmony_block(0, *args)
+    _hip.harmony_block(1, *args)
+
+
 # ----------------------------------------------------------------------------- init
 def philox_fill(out: torch.Tensor, seeds: torch.Tensor, scales: torch.Tensor, stream: int,
                 mode: int = 0, row_offset: int = 0) -> None:

@@ -74,6 +74,42 @@ PYBIND11_MODULE(_hip, m) {
                 "beta_contract");
         });
 
+  m.def("pairdist", [](uintptr_t A, long long lda, uintptr_t B, long long ldb, uintptr_t na,
+                       uintptr_t nb, int n, int mm, int kdim, uintptr_t D, long long ldd, int same,
+                       int squared, uintptr_t stream) {
+    check(cnmf_pairdist(P<const double>(A), lda, P<const double>(B), ldb, P<const double>(na),
+                        P<const double>(nb), n, mm, kdim, P<double>(D), ldd, same, squared,
+                        reinterpret_cast<hipStream_t>(stream)),
+          "pairdist");
+  });
+  m.def("knn_sum", [](uintptr_t D, long long ldd, int n, int mm, int k, uintptr_t out,
+                      uintptr_t stream) {
+    check(cnmf_knn_sum(P<const double>(D), ldd, n, mm, k, P<double>(out),
+                       reinterpret_cast<hipStream_t>(stream)),
+          "knn_sum");
+  });
+  m.def("seg_argmin", [](uintptr_t D, long long ldd, int n, int nseg, int k, uintptr_t row_add,
+                         uintptr_t col_add, uintptr_t labels, uintptr_t mind, uintptr_t stream) {
+    check(cnmf_seg_argmin(P<const double>(D), ldd, n, nseg, k, P<const double>(row_add),
+                          P<const double>(col_add), P<int>(labels), P<double>(mind),
+                          reinterpret_cast<hipStream_t>(stream)),
+          "seg_argmin");
+  });
+
+  m.def("harmony_max_kb", []() { return cnmf_harmony_max_kb(); });
+  m.def("harmony_block", [](int op, uintptr_t Rt, uintptr_t distT, uintptr_t sigma,
+                            uintptr_t cells, uintptr_t bidx, int nb, int N, int K, int B,
+                            int nvar, int chunk, uintptr_t E, uintptr_t O, uintptr_t Pr_b,
+                            uintptr_t theta, uintptr_t Pen, uintptr_t part, uintptr_t counter,
+                            uintptr_t stream) {
+    check(cnmf_harmony_block(op, P<double>(Rt), P<const double>(distT), P<const double>(sigma),
+                             P<const int>(cells), P<const int>(bidx), nb, N, K, B, nvar, chunk,
+                             P<double>(E), P<double>(O), P<const double>(Pr_b),
+                             P<const double>(theta), P<double>(Pen), P<double>(part),
+                             P<int>(counter), reinterpret_cast<hipStream_t>(stream)),
+          "harmony_block");
+  });
+
   m.def("philox_fill",
         [](uintptr_t out, long long rows, long long cols, long long s_row, long long s_col,
            long long rep_stride, long long row_offset, uintptr_t seeds, uintptr_t scales, int R,

@@ -30,6 +30,22 @@ hipError_t cnmf_beta_contract(int side, int mode, const float* X, long long ldx,
                               float gamma, float tol, float* part, int* counter, int* act,
                               int* iters, hipStream_t stream);
 
+hipError_t cnmf_pairdist(const double* A, long long lda, const double* B, long long ldb,
+                         const double* na, const double* nb, int n, int m, int kdim, double* D,
+                         long long ldd, int same, int squared, hipStream_t stream);
+hipError_t cnmf_knn_sum(const double* D, long long ldd, int n, int m, int k, double* out,
+                        hipStream_t stream);
+hipError_t cnmf_seg_argmin(const double* D, long long ldd, int n, int nseg, int k,
+                           const double* row_add, const double* col_add, int* labels,
+                           double* mind, hipStream_t stream);
+
+int cnmf_harmony_max_kb();
+hipError_t cnmf_harmony_block(int op, double* Rt, const double* distT, const double* sigma,
+                              const int* cells, const int* bidx, int nb, int N, int K, int B,
+                              int nvar, int chunk, double* E, double* O, const double* Pr_b,
+                              const double* theta, double* Pen, double* part, int* counter,
+                              hipStream_t stream);
+
 hipError_t cnmf_philox_fill(float* out, long long rows, long long cols, long long s_row,
                             long long s_col, long long rep_stride, long long row_offset,
                             const unsigned long long* seeds, const float* scales, int R,

@@ -7,6 +7,7 @@ import sys
 import numpy as np
 import pandas as pd
 import pytest
+import torch
 
 from cnmf_torch_amd import cNMF, load_df_from_npz, save_df_to_npz
 from cnmf_torch_amd.utils.synthetic import simulate_counts
@@ -164,3 +165,21 @@ def test_cli_end_to_end(tmp_path, counts_file):
     assert (d / "cli.spectra.k_5.dt_2_0.consensus.txt").exists()
     assert (d / "cli.clustering.k_5.dt_2_0.png").exists()
     assert (d / "cli.k_selection.png").exists()
+
+
+def test_device_kmeans_backend_on_cpu_matches_sklearn_partition():
+    from sklearn.metrics import adjusted_rand_score
+
+    from cnmf_torch_amd.models.consensus import kmeans, local_density, pairwise_distances
+
+    rs = np.random.default_rng(1)
+    centers = rs.normal(size=(4, 30)) * 4
+    truth = rs.integers(0, 4, 300)
+    X = centers[truth] + rs.normal(size=(300, 30))
+    a = kmeans(torch.from_numpy(X), 4, backend="device")
+    b = kmeans(X, 4, backend="sklearn")
+    assert adjusted_rand_score(a, b) > 0.99
+    D = pairwise_distances(torch.from_numpy(X))
+    dens = local_density(D, 5).numpy()
+    exp = np.sort(D.numpy(), axis=1)[:, :6].sum(1) / 5
+    np.testing.assert_allclose(dens, exp)

@@ -1,0 +1,166 @@
+"""Preprocess / Harmony / h5ad / scanpy-equivalent helpers (C30-C38).
+
+harmonypy and scanpy are not installed in this environment, so Harmony is checked on its
+defining properties (objective decreases, batch structure is removed from the corrected
+PCs, deterministic for a seed) -- parity with harmonypy itself is unpinned.
+"""
+import numpy as np
+import pandas as pd
+import pytest
+import scipy.sparse as sp
+import torch
+
+from cnmf_torch_amd import Preprocess
+from cnmf_torch_amd.models import pp
+from cnmf_torch_amd.models.harmony import moe_correct_ridge, run_harmony
+from cnmf_torch_amd.utils.anndata_lite import AnnData
+from cnmf_torch_amd.utils.h5ad import read_h5ad, write_h5ad
+from cnmf_torch_amd.utils.synthetic import simulate_counts
+
+
+def _batched_pcs(n=600, d=10, n_batch=3, seed=0):
+    rs = np.random.default_rng(seed)
+    n_types = 3
+    types = rs.integers(0, n_types, n)
+    batch = rs.integers(0, n_batch, n)
+    centers = rs.normal(size=(n_types, d)) * 3
+    shifts = rs.normal(size=(n_batch, d)) * 2
+    Z = centers[types] + shifts[batch] + 0.3 * rs.normal(size=(n, d))
+    meta = pd.DataFrame({"batch": pd.Categorical([f"b{b}" for b in batch]),
+                         "type": types})
+    return Z, meta, types, batch
+
+
+def _batch_separation(Z, batch):
+    """Between-batch centroid spread relative to the total spread."""
+    mu = Z.mean(0)
+    cb = np.stack([Z[batch == b].mean(0) for b in np.unique(batch)])
+    return float(np.linalg.norm(cb - mu, axis=1).mean() / np.linalg.norm(Z - mu, axis=1).mean())
+
+
+def test_harmony_removes_batch_effect_and_is_deterministic():
+    Z, meta, types, batch = _batched_pcs()
+    res = run_harmony(Z, meta, "batch", max_iter_harmony=10, random_state=0)
+    Zc = res.Z_corr.T
+    assert Zc.shape == Z.shape
+    assert _batch_separation(Zc, batch) < 0.7 * _batch_separation(Z, batch)
+    # cell types stay separated
+    assert _batch_separation(Zc, types) > 0.5 * _batch_separation(Z, types)
+    obj = res.objective_harmony
+    assert obj[-1] <= obj[0]
+    assert res.R.shape == (res.K, Z.shape[0])
+    np.testing.assert_allclose(res.R.sum(0), 1.0, rtol=1e-10)
+    res2 = run_harmony(Z, meta, "batch", max_iter_harmony=10, random_state=0)
+    np.testing.assert_allclose(res2.Z_corr, res.Z_corr, rtol=1e-10, atol=1e-12)  # threaded BLAS
+
+
+def test_harmony_two_covariates():
+    Z, meta, types, batch = _batched_pcs(n=450, n_batch=2, seed=3)
+    meta["donor"] = pd.Categorical(np.random.default_rng(1).integers(0, 3, len(meta)).astype(str))
+    res = run_harmony(Z, meta, ["batch", "donor"], max_iter_harmony=5, random_state=1)
+    assert res.Phi.shape[0] == 2 + 3
+    assert np.isfinite(res.Z_corr).all()
+
+
+def test_moe_correct_ridge_matches_sequential_formula():
+    """Batched ridge correction == the reference's per-cluster loop (preprocess.py:9-18)."""
+    rs = np.random.default_rng(0)
+    F, N, K, B = 7, 80, 4, 2
+    Z = rs.random((F, N))
+    R = rs.random((K, N))
+    R /= R.sum(0)
+    b = rs.integers(0, B, N)
+    Phi = np.zeros((B, N))
+    Phi[b, np.arange(N)] = 1
+    Phi_moe = np.vstack([np.ones((1, N)), Phi])
+    lamb = np.diag([0.0, 1.0, 1.0])
+    Zc = Z.copy()
+    for i in range(K):
+        Phi_Rk = Phi_moe * R[i]
+        x = Phi_Rk @ Phi_moe.T + lamb
+        W = np.linalg.inv(x) @ Phi_Rk @ Z.T
+        W[0, :] = 0
+        Zc -= W.T @ Phi_Rk
+    Zcos = Zc / np.linalg.norm(Zc, ord=2, axis=0)
+    got_cos, got_corr, W_last, Phi_Rk_last = moe_correct_ridge(Z, None, None, R, None, K, None,
+                                                                Phi_moe, lamb)
+    np.testing.assert_allclose(got_corr, Zc, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(got_cos, Zcos, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(W_last, W, rtol=1e-10, atol=1e-12)
+
+
+def test_h5ad_roundtrip(tmp_path):
+    rs = np.random.default_rng(0)
+    X = sp.random(40, 25, density=0.3, format="csr", random_state=1, dtype=np.float32)
+    obs = pd.DataFrame({"batch": pd.Categorical(rs.choice(["a", "b"], 40)),
+                        "n": rs.integers(0, 9, 40), "ok": rs.random(40) > 0.5,
+                        "score": rs.random(40)}, index=[f"c{i}" for i in range(40)])
+    var = pd.DataFrame({"gene_ids": [f"ENSG{i}" for i in range(25)],
+                        "highly_variable": rs.random(25) > 0.5},
+                       index=[f"g{i}" for i in range(25)])
+    ad = AnnData(X=X, obs=obs, var=var)
+    ad.obsm["X_pca"] = rs.random((40, 3))
+    fn = str(tmp_path / "t.h5ad")
+    write_h5ad(fn, ad)
+    back = read_h5ad(fn)
+    assert sp.issparse(back.X)
+    np.testing.assert_array_equal(back.X.toarray(), X.toarray())
+    pd.testing.assert_index_equal(back.obs.index, obs.index)
+    assert list(back.obs["batch"].astype(str)) == list(obs["batch"].astype(str))
+    np.testing.assert_array_equal(back.obs["ok"].values.astype(bool), obs["ok"].values)
+    np.testing.assert_allclose(back.obs["score"].values, obs["score"].values)
+    np.testing.assert_array_equal(back.var["highly_variable"].values.astype(bool),
+                                  var["highly_variable"].values)
+    np.testing.assert_allclose(back.obsm["X_pca"], ad.obsm["X_pca"])
+    dense = AnnData(X=X.toarray().astype(np.float64), obs=obs, var=var)
+    write_h5ad(fn, dense)
+    np.testing.assert_array_equal(read_h5ad(fn).X, dense.X)
+
+
+def test_pp_scale_and_normalize_semantics():
+    rs = np.random.default_rng(0)
+    X = rs.poisson(2.0, (50, 8)).astype(np.float64)
+    X[:, 3] = 5.0                                   # zero-variance gene stays unscaled
+    ad = AnnData(X=X.copy())
+    pp.scale(ad, zero_center=False)
+    sd = X.std(axis=0, ddof=1)
+    exp = X.copy()
+    exp[:, sd > 0] /= sd[sd > 0]
+    np.testing.assert_allclose(ad.X, exp)
+    ad2 = pp.normalize_total(AnnData(X=X.copy()), target_sum=1e4, copy=True)
+    np.testing.assert_allclose(ad2.X.sum(1), 1e4)
+    Xs = sp.csr_matrix(X)
+    ad3 = AnnData(X=Xs.copy())
+    pp.scale(ad3, zero_center=False)
+    np.testing.assert_allclose(ad3.X.toarray(), exp)
+
+
+def test_preprocess_for_cnmf_with_and_without_harmony(tmp_path):
+    Xc, cells, genes = simulate_counts(300, 120, 3, seed=2, sparse=True)
+    rs = np.random.default_rng(0)
+    obs = pd.DataFrame({"batch": pd.Categorical(rs.choice(["x", "y"], 300))}, index=cells)
+    ad = AnnData(X=sp.csr_matrix(Xc), obs=obs, var=pd.DataFrame(index=genes))
+    p = Preprocess(random_seed=0)
+    filt = p.filter_adata(ad, min_cells_per_gene=3, min_counts_per_cell=10, makeplots=False)
+    assert filt.shape[0] <= 300 and filt.shape[1] <= 120
+    out, tp10k, hvgs = p.preprocess_for_cnmf(filt, n_top_rna_genes=40, makeplots=False,
+                                             save_output_base=str(tmp_path / "pp"))
+    assert len(hvgs) == 40 and out.shape[1] == 40
+    np.testing.assert_allclose(np.asarray(tp10k.X.sum(1)).ravel(), 1e4, rtol=1e-6)
+    assert (tmp_path / "pp.Corrected.HVG.Varnorm.h5ad").exists()
+    out_h, _, _ = p.preprocess_for_cnmf(filt, harmony_vars="batch", n_top_rna_genes=40,
+                                        makeplots=False, max_iter_harmony=3, device="cpu")
+    Xh = out_h.X.toarray() if sp.issparse(out_h.X) else out_h.X
+    assert Xh.shape == (filt.shape[0], 40) and (Xh >= 0).all()
+    assert "X_pca_harmony" in out_h.obsm
+
+
+def test_select_features_mi():
+    Xc, cells, genes = simulate_counts(200, 60, 3, seed=5, sparse=False)
+    labels = np.random.default_rng(0).integers(0, 3, 200)
+    ad = AnnData(X=Xc.astype(np.float64), var=pd.DataFrame(index=genes),
+                 obs=pd.DataFrame(index=cells))
+    out = Preprocess(random_seed=0).select_features_MI(ad, labels, n_top_features=10,
+                                                       makeplots=False)
+    assert out.var["highly_variable"].sum() == 10
+    assert {"MI", "MI_Rank", "MI_diff"} <= set(out.var.columns)
