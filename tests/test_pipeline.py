@@ -183,3 +183,22 @@ def test_device_kmeans_backend_on_cpu_matches_sklearn_partition():
     dens = local_density(D, 5).numpy()
     exp = np.sort(D.numpy(), axis=1)[:, :6].sum(1) / 5
     np.testing.assert_allclose(dens, exp)
+
+
+def test_run_parallel_driver_with_workers(tmp_path):
+    """C39: prepare -> N worker-index processes -> combine -> k_selection_plot."""
+    Xc, cells, genes = simulate_counts(150, 80, 3, seed=3, sparse=False)
+    fn = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(Xc, index=cells, columns=genes), fn)
+    cmd = [sys.executable, "-m", "cnmf_torch_amd.run_parallel", "--output-dir", str(tmp_path),
+           "--name", "rp", "-c", fn, "-k", "3", "4", "-n", "4", "--seed", "2", "--numgenes", "50",
+           "--workers", "2", "--gpus", "0"]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    obj = cNMF(output_dir=str(tmp_path), name="rp")
+    for k in (3, 4):
+        merged = load_df_from_npz(obj.paths["merged_spectra"] % k)
+        assert merged.shape == (4 * k, 50)
+    assert not any("iter_" in f for f in os.listdir(os.path.join(str(tmp_path), "rp", "cnmf_tmp")))
+    assert os.path.exists(obj.paths["k_selection_stats"])

@@ -1,0 +1,102 @@
+"""Golden-output regression test (the reference's tests/test_reproducibility.py strategy).
+
+Inputs are regenerated deterministically; golden outputs live in tests/data/golden and
+are produced by tools/make_test_data.py (CPU float64-oracle run of this pipeline).  As
+in the reference, the consensus stage is run on the golden *merged spectra* so that the
+consensus / refit / OLS / starCAT outputs are checked independently of factorization,
+with the reference's tolerance (sum of squared differences < 1e-4).  The prepare outputs
+are compared exactly (ledger, YAML, gene list) or within tolerance (TPM stats).
+"""
+import os
+import shutil
+import sys
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "tools"))
+
+import make_test_data as mtd  # noqa: E402
+from cnmf_torch_amd import cNMF, load_df_from_npz  # noqa: E402
+
+TOLERANCE = 1e-4
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "golden")
+
+
+def _golden(obj: cNMF, ds: str, path: str) -> str:
+    rel = os.path.relpath(path, os.path.join(obj.output_dir, obj.name))
+    return os.path.join(GOLDEN, ds, rel.replace(obj.name, ds))
+
+
+def _prepare(tmp_path, ds):
+    cfg = mtd.DATASETS[ds]
+    counts = mtd.write_counts(cfg, str(tmp_path / "in"))
+    obj = cNMF(output_dir=str(tmp_path), name="test_cNMF")
+    obj.prepare(counts, components=cfg["k_values"], n_iter=cfg["n_iter"],
+                num_highvar_genes=cfg["nhvg"], seed=mtd.SEED)
+    return cfg, obj
+
+
+def _consensus_and_compare(obj, cfg, ds, device=None):
+    for k in cfg["k_values"]:
+        shutil.copy(_golden(obj, ds, obj.paths["merged_spectra"] % k),
+                    obj.paths["merged_spectra"] % k)
+    for k, thr in cfg["consensus"]:
+        obj.consensus(k, density_threshold=thr, show_clustering=False, device=device)
+    for key in mtd.GOLDEN_KEYS:
+        for k, thr in cfg["consensus"]:
+            fn = obj.paths[key] % (k, str(thr).replace(".", "_"))
+            assert os.path.exists(fn), fn
+            test_df = load_df_from_npz(fn)
+            ref_df = load_df_from_npz(_golden(obj, ds, fn))
+            assert list(test_df.index) == list(ref_df.index)
+            assert list(test_df.columns) == list(ref_df.columns)
+            rms = float(((test_df.values - ref_df.values) ** 2).sum())
+            assert rms < TOLERANCE, (fn, rms)
+
+
+@pytest.mark.parametrize("ds", sorted(mtd.DATASETS))
+def test_cnmf_end_to_end(tmp_path, ds):
+    cfg, obj = _prepare(tmp_path, ds)
+    # prepare outputs
+    rp = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
+    ref_rp = load_df_from_npz(_golden(obj, ds, obj.paths["nmf_replicate_parameters"]))
+    cols = ["n_components", "iter", "nmf_seed"]
+    assert rp[cols].equals(ref_rp[cols])
+    with open(obj.paths["nmf_run_parameters"]) as f, \
+            open(_golden(obj, ds, obj.paths["nmf_run_parameters"])) as g:
+        assert yaml.safe_load(f) == yaml.safe_load(g)
+    with open(obj.paths["nmf_genes_list"]) as f, \
+            open(_golden(obj, ds, obj.paths["nmf_genes_list"])) as g:
+        assert f.read().split("\n") == g.read().split("\n")
+    ts = load_df_from_npz(obj.paths["tpm_stats"])
+    ref_ts = load_df_from_npz(_golden(obj, ds, obj.paths["tpm_stats"]))
+    assert float(((ts - ref_ts) ** 2).sum().sum()) < TOLERANCE
+    # consensus on the golden merged spectra
+    _consensus_and_compare(obj, cfg, ds, device="cpu")
+
+
+def test_factorize_reproduces_golden_merged_spectra(tmp_path):
+    """A fresh CPU factorize of the first K reproduces the golden replicate spectra."""
+    ds = "simulated_example_data"
+    cfg, obj = _prepare(tmp_path, ds)
+    k = cfg["k_values"][0]
+    obj.factorize(device="cpu")
+    obj.combine(components=[k])
+    got = load_df_from_npz(obj.paths["merged_spectra"] % k)
+    ref = load_df_from_npz(_golden(obj, ds, obj.paths["merged_spectra"] % k))
+    assert list(got.index) == list(ref.index)
+    rel = np.linalg.norm(got.values - ref.values) / np.linalg.norm(ref.values)
+    assert rel < 1e-3, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ds", sorted(mtd.DATASETS))
+def test_gpu_consensus_matches_golden(tmp_path, ds):
+    """Consensus with the HIP kernels (distances, density, refits, OLS) == CPU golden."""
+    assert torch.cuda.is_available()
+    cfg, obj = _prepare(tmp_path, ds)
+    _consensus_and_compare(obj, cfg, ds, device="cuda")
