@@ -16,6 +16,7 @@ reference, on the MI355X-native engine:
 """
 from __future__ import annotations
 
+import concurrent.futures as cf
 import datetime
 import errno
 import itertools
@@ -86,10 +87,20 @@ def _dt_str(density_threshold) -> str:
 
 
 def _device(use_gpu: bool, device=None) -> torch.device:
+    """Explicit ``device`` > $CNMF_DEVICE > the local GPU when one is visible > CPU.
+
+    The reference's ``use_gpu`` (default False) selected nmf-torch's CUDA path; this
+    framework is GPU-first, so a visible MI355X is used unless told otherwise.
+    ``use_gpu=True`` without a GPU falls back to the CPU with a warning (nmf-torch
+    falls back silently)."""
+    if device is None:
+        device = os.environ.get("CNMF_DEVICE") or None
     if device is not None:
         return torch.device(device)
-    if use_gpu and torch.cuda.is_available():
+    if torch.cuda.is_available():
         return torch.device("cuda", torch.cuda.current_device())
+    if use_gpu:
+        warnings.warn("use_gpu=True but no GPU is visible; running on the CPU")
     return torch.device("cpu")
 
 
@@ -327,6 +338,15 @@ class cNMF:
             writer = comm is None or comm.rank == 0
             fault_after = int(os.environ.get("CNMF_FAULT_AFTER_REPLICATES", "0") or 0)
             written = 0
+            # replicate files are compressed + written by a small thread pool (zlib drops
+            # the GIL) while the next batch runs on the GPU; every file is still atomic
+            pool = cf.ThreadPoolExecutor(max_workers=4)
+            pending: list = []
+
+            def _flush():
+                for f in pending:
+                    f.result()
+                pending.clear()
             by_k: dict[int, list[int]] = {}
             for idx in jobs:
                 by_k.setdefault(int(run_params.iloc[idx]["n_components"]), []).append(idx)
@@ -351,7 +371,8 @@ class cNMF:
                         if writer:
                             spectra = pd.DataFrame(W[r * k:(r + 1) * k],
                                                    index=np.arange(1, k + 1), columns=genes)
-                            save_df_to_npz(spectra, self.paths["iter_spectra"] % (k, it))
+                            pending.append(pool.submit(save_df_to_npz, spectra,
+                                                       self.paths["iter_spectra"] % (k, it)))
                             append_jsonl(self.paths["replicate_log"], {
                                 "k": k, "iter": it, "seed": seeds[r], "worker": worker_label,
                                 "err": float(res.err[r]), "n_pass": int(res.n_iter[r]),
@@ -367,11 +388,15 @@ class cNMF:
                             fn = self.paths["iter_usages"] % (k, it)
                             if comm is not None and comm.world_size > 1:
                                 fn = fn.replace(".df.npz", ".rank%d.df.npz" % comm.rank)
-                            save_df_to_npz(us, fn)
+                            pending.append(pool.submit(save_df_to_npz, us, fn))
                         written += 1
                         if fault_after and written >= fault_after:
+                            _flush()
+                            pool.shutdown()
                             raise RuntimeError(
                                 f"CNMF_FAULT_AFTER_REPLICATES={fault_after}: injected failure")
+            _flush()
+            pool.shutdown()
 
     @staticmethod
     def _auto_batch(X: torch.Tensor, k: int, n_jobs: int, dev: torch.device) -> int:
@@ -394,15 +419,17 @@ class cNMF:
             ks = sorted(set(int(k) for k in run_params.n_components))
         else:
             ks = components
-        for k in ks:
-            self.combine_nmf(k, skip_missing_files=skip_missing_files)
+        # the K merges are independent; their zlib work runs concurrently (GIL released)
+        with cf.ThreadPoolExecutor(max_workers=max(1, min(len(ks), 8))) as ex:
+            list(ex.map(lambda k: self.combine_nmf(k, skip_missing_files=skip_missing_files),
+                        ks))
 
     def combine_nmf(self, k, skip_missing_files=False, remove_individual_iterations=False):
         """Concatenate replicate spectra for one K (cnmf.py:895-920)."""
         run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
         print("Combining factorizations for k=%d." % k)
         sub = run_params[run_params.n_components == k].sort_values("iter")
-        parts = []
+        present = []
         for _, p in sub.iterrows():
             fn = self.paths["iter_spectra"] % (int(p["n_components"]), int(p["iter"]))
             if not os.path.exists(fn):
@@ -411,8 +438,12 @@ class cNMF:
                     raise FileNotFoundError(errno.ENOENT, os.strerror(errno.ENOENT), fn)
                 print("Missing file: %s. Skipping." % fn)
                 continue
-            spectra = load_df_from_npz(fn)
-            spectra.index = ["iter%d_topic%d" % (int(p["iter"]), t + 1) for t in range(k)]
+            present.append((int(p["iter"]), fn))
+        with cf.ThreadPoolExecutor(max_workers=8) as ex:   # zlib inflate drops the GIL
+            loaded = list(ex.map(lambda t: load_df_from_npz(t[1]), present))
+        parts = []
+        for (it, _), spectra in zip(present, loaded):
+            spectra.index = ["iter%d_topic%d" % (it, t + 1) for t in range(k)]
             parts.append(spectra)
         if parts:
             combined = pd.concat(parts, axis=0)

@@ -79,12 +79,29 @@ def _plain_values(df: pd.DataFrame) -> np.ndarray:
     return vals
 
 
+NPZ_COMPRESSLEVEL = int(os.environ.get("CNMF_NPZ_LEVEL", "1"))
+
+
+def _savez_deflate(path: str, arrays: dict, level: int) -> None:
+    """np.savez_compressed with a selectable zlib level (numpy hard-codes the default,
+    ~4x slower than level 1 on spectra-sized float arrays).  Same member names
+    (``<key>.npy``) and ZIP_DEFLATED format, so np.load / the reference read it."""
+    import zipfile
+
+    with zipfile.ZipFile(path, mode="w", compression=zipfile.ZIP_DEFLATED,
+                         compresslevel=level, allowZip64=True) as zf:
+        for key, arr in arrays.items():
+            with zf.open(key + ".npy", "w", force_zip64=True) as fh:
+                np.lib.format.write_array(fh, np.asanyarray(arr), allow_pickle=False)
+
+
 def save_df_to_npz(obj: pd.DataFrame, filename: str) -> None:
-    """np.savez_compressed(data, index, columns) -- same keys as cnmf.py:32-33."""
+    """Compressed npz with keys data / index / columns -- the cnmf.py:32-33 contract."""
     filename = str(filename)
     with atomic_path(filename, suffix=".npz") as tmp:
-        np.savez_compressed(tmp, data=_plain_values(obj), index=_plain_array(obj.index.values),
-                            columns=_plain_array(obj.columns.values))
+        _savez_deflate(tmp, {"data": _plain_values(obj),
+                             "index": _plain_array(obj.index.values),
+                             "columns": _plain_array(obj.columns.values)}, NPZ_COMPRESSLEVEL)
 
 
 def load_df_from_npz(filename: str, allow_pickle_fallback: bool = True) -> pd.DataFrame:

@@ -1,0 +1,470 @@
+// Fused, replicate-batched NNLS-style inner solvers for NMF.
+//
+// Both halves of a Frobenius NMF step reduce to the same problem, independently per
+// column j, with a convergence test on the WHOLE (replicate, chunk) block:
+//   H-side  (cnmf.py:352-381 fit_H_online; nmf-torch online H step):
+//       x = h^T (K x c), numer = W x^T (K x c), Gram = W W^T
+//   W-side  (nmf-torch online/batch W step):
+//       x = W (K x G),   numer = B = sum h^T x,  Gram = A = sum h^T h
+// One workgroup owns one replicate's block and iterates the update in place (the block
+// stays L2-resident), reducing ||dx||, ||x|| or the block objective on device.  There is
+// no per-iteration kernel launch and no host sync (the reference syncs every iteration
+// at cnmf.py:377).  A grid covers every active replicate of a batch, so one launch
+// drives the whole replicate grid.
+//
+// ALGO 0 = multiplicative update (MU):  x <- x * numer / (Gram x + l2 x + l1_den),
+//          rate := 0 where the denominator < eps (cnmf.py:370-372).
+// ALGO 1 = HALS (Gauss-Seidel over components):
+//          x_k <- max(0, x_k + (numer_k - l1_den - (Gram x)_k - l2 x_k) / (Gram_kk + l2)).
+// Optional epilogue: lin_out[r] = <numer, x>, quad_out[r] = sum_j x_j^T Gram x_j, which
+// give the exact Frobenius loss from sufficient statistics (trace trick, G7).
+//
+// Memory path: each sweep a thread handles U columns at a time and issues all 2*U*K
+// loads of the group before any arithmetic (U*K loads in flight per lane hide the L2
+// latency that dominated the one-column-at-a-time version: 273 us/solve in
+// profiles/r1_bench_v0_kernel_stats.txt).  Loads/stores are buffer operations: the
+// column is the per-lane VGPR offset, component k*ld the SGPR soffset, so the K
+// addresses of a column cost no VGPRs.  Gram products read one LDS row per component
+// (every lane the same word: broadcast), row by row behind a compiler memory fence and
+// an opaque LDS base, so the K*K loop-invariant Gram values are never hoisted into
+// registers (that hoisting spilled hundreds of VGPRs at K >= 7).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "common.h"
+#include "solve_params.h"
+
+namespace cnmf {
+
+template <int K>
+constexpr int solve_max_threads() { return 1024; }
+
+// Columns per thread per group: keep ~(2U+1)K live floats well under the 128-VGPR cap.
+__host__ __device__ constexpr int cols_per_group_rt(int K) {
+  return (20 / K) < 1 ? 1 : ((20 / K) > 4 ? 4 : (20 / K));
+}
+template <int K>
+constexpr int cols_per_group() { return cols_per_group_rt(K); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+
+#define CNMF_MEMBAR() asm volatile("" ::: "memory")
+
+// raw_buffer_{load,store}_b32 move 32-bit integers: bit-cast, never value-convert.
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+}
+__device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, int vo, int so) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, vo, so, 0);
+}
+
+// A zero the compiler cannot see through, produced inside the column loop: indexing the
+// LDS Gram with it stops LICM from hoisting all K*K loop-invariant Gram reads into
+// registers (K*K VGPRs -> spills at K >= 7).  Every lane reads the same LDS word.
+typedef __attribute__((address_space(3))) float lds_float;
+
+__device__ __forceinline__ const lds_float* opaque(const lds_float* p) {
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+template <int K, int U>
+struct ColGroup {
+  float x[U][K];
+  float n[U][K];
+  int vo[U];
+  bool ok[U];
+};
+
+template <int K, int U>
+__device__ __forceinline__ void load_group(ColGroup<K, U>& cg, int j, int T, int end,
+                                           __amdgpu_buffer_rsrc_t rx, int sx,
+                                           __amdgpu_buffer_rsrc_t rn, int sn, float l1n) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = j + u * T;
+    cg.ok[u] = c < end;
+    cg.vo[u] = cg.ok[u] ? c * 4 : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      cg.x[u][k] = buf_ld(rx, cg.vo[u], k * sx);
+      cg.n[u][k] = buf_ld(rn, cg.vo[u], k * sn);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      cg.x[u][k] = cg.ok[u] ? cg.x[u][k] : 0.f;
+      float t = cg.ok[u] ? cg.n[u][k] : 0.f;
+      if (l1n > 0.f) t = fmaxf(t - l1n, 0.f);
+      cg.n[u][k] = t;
+    }
+  }
+}
+
+// Cross-workgroup sum of (a, b) for the S workgroups of one replicate, epoch `e`.
+// Each workgroup stores its block totals to its own slot (plain store), drains, then
+// arrives on the epoch counter with an agent-scope release; after all S arrived every
+// workgroup sums the S slots in slice order -> identical, deterministic totals
+// everywhere.  Spins are bounded: on timeout the flag is raised and the host fails.
+// (Recipe: cdna_hip_programming.md Guideline 16 -- release before the counter add,
+// acquire after the poll, vmcnt drained around the fence.)
+__device__ __forceinline__ void coop_sum2(const SolveParams& p, int rep, int e, float& a,
+                                          float& b, float* sred) {
+  const int S = gridDim.y;
+  const int slice = blockIdx.y;
+  if (S <= 1) return;
+  if (e >= p.coop_epochs) {  // workspace too small: treat as timeout (host sizes it)
+    if (threadIdx.x == 0) atomicExch(p.coop_timeout, 2);
+    return;
+  }
+  float* slots = p.coop_slots + (((long long)rep * p.coop_epochs + e) * S) * 2;
+  int* cnt = p.coop_count + (long long)rep * p.coop_epochs + e;
+  if (threadIdx.x == 0) {
+    slots[2 * slice] = a;
+    slots[2 * slice + 1] = b;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {
+        atomicExch(p.coop_timeout, 1);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    float ta = 0.f, tb = 0.f;
+    for (int s2 = 0; s2 < S; ++s2) {
+      ta += __hip_atomic_load(slots + 2 * s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tb += __hip_atomic_load(slots + 2 * s2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sred[0] = ta;
+    sred[1] = tb;
+  }
+  __syncthreads();
+  a = sred[0];
+  b = sred[1];
+  __syncthreads();
+}
+
+// Per-group pieces shared by the streaming and the register-resident paths.  They are
+// macros on purpose: as __forceinline__ functions taking the ColGroup by reference the
+// compiler inlines them too late to scalarise the group, and the K=20 kernel went from
+// 111 VGPRs / 0 spills to 128 VGPRs / 148 spills.  They expect K, U, ALGO, sG, l1, l2,
+// eps and the accumulators (q, l / d2, x2 / lin, quad) in scope.
+// Objective terms (x2, dropping the constant ||X||^2):
+//   f(x) = sum_j x_j^T Gram x_j - 2 numer_j . x_j + 2 l1 |x_j|_1 + l2 |x_j|^2
+#define CNMF_OBJECTIVE_GROUP(CG)                                                                  \
+  do {                                                                                            \
+  const lds_float* gz = opaque(sG);                                                               \
+_Pragma("unroll")                                                                                    \
+  for (int u = 0; u < U; ++u) {                                                                   \
+_Pragma("unroll")                                                                                    \
+    for (int k = 0; k < K; ++k) {                                                                 \
+      CNMF_MEMBAR();                                                                              \
+      float gx = 0.f;                                                                             \
+_Pragma("unroll")                                                                                    \
+      for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], (CG).x[u][kk], gx);                \
+      q = fmaf((CG).x[u][k], gx + l2 * (CG).x[u][k], q);                                          \
+      l = fmaf((CG).x[u][k], (CG).n[u][k] - l1, l);                                               \
+    }                                                                                             \
+  }                                                                                               \
+  } while (0)
+
+
+// One MU (Jacobi, row-wise) or HALS (Gauss-Seidel) sweep over the group's columns,
+// accumulating |dx|^2 and |x_old|^2.  Padded columns hold x = numer = 0 and stay 0.
+#define CNMF_UPDATE_GROUP(CG)                                                                     \
+  do {                                                                                            \
+  const lds_float* gz = opaque(sG);                                                               \
+_Pragma("unroll")                                                                                    \
+  for (int u = 0; u < U; ++u) {                                                                   \
+    if (ALGO == 0) {                                                                              \
+      float xn[K];                                                                                \
+_Pragma("unroll")                                                                                    \
+      for (int k = 0; k < K; ++k) {                                                               \
+        CNMF_MEMBAR();                                                                            \
+        float den = 0.f;                                                                          \
+_Pragma("unroll")                                                                                    \
+        for (int kk = 0; kk < K; ++kk) den = fmaf(gz[k * K + kk], (CG).x[u][kk], den);            \
+        den = fmaf(l2, (CG).x[u][k], den) + l1;                                                   \
+        xn[k] = (den < eps) ? 0.f : (CG).x[u][k] * ((CG).n[u][k] * __builtin_amdgcn_rcpf(den));   \
+      }                                                                                           \
+_Pragma("unroll")                                                                                    \
+      for (int k = 0; k < K; ++k) {                                                               \
+        const float d = xn[k] - (CG).x[u][k];                                                     \
+        d2 = fmaf(d, d, d2);                                                                      \
+        x2 = fmaf((CG).x[u][k], (CG).x[u][k], x2);                                                \
+        (CG).x[u][k] = xn[k];                                                                     \
+      }                                                                                           \
+    } else {                                                                                      \
+_Pragma("unroll")                                                                                    \
+      for (int k = 0; k < K; ++k) {                                                               \
+        CNMF_MEMBAR();                                                                            \
+        float gx = 0.f;                                                                           \
+_Pragma("unroll")                                                                                    \
+        for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], (CG).x[u][kk], gx);              \
+        const float diag = gz[k * K + k] + l2;                                                    \
+        const float old = (CG).x[u][k];                                                           \
+        float xn = old;                                                                           \
+        if (diag > eps) xn = fmaxf(old + ((CG).n[u][k] - l1 - gx - l2 * old) / diag, 0.f);        \
+        const float d = xn - old;                                                                 \
+        d2 = fmaf(d, d, d2);                                                                      \
+        x2 = fmaf(old, old, x2);                                                                  \
+        (CG).x[u][k] = xn;                                                                        \
+      }                                                                                           \
+    }                                                                                             \
+  }                                                                                               \
+  } while (0)
+
+
+#define CNMF_LINQUAD_GROUP(CG)                                                                    \
+  do {                                                                                            \
+  const lds_float* gz = opaque(sG);                                                               \
+_Pragma("unroll")                                                                                    \
+  for (int u = 0; u < U; ++u) {                                                                   \
+_Pragma("unroll")                                                                                    \
+    for (int k = 0; k < K; ++k) {                                                                 \
+      CNMF_MEMBAR();                                                                              \
+      float gx = 0.f;                                                                             \
+_Pragma("unroll")                                                                                    \
+      for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], (CG).x[u][kk], gx);                \
+      lin = fmaf((CG).n[u][k], (CG).x[u][k], lin);                                                \
+      quad = fmaf((CG).x[u][k], gx, quad);                                                        \
+    }                                                                                             \
+  }                                                                                               \
+  } while (0)
+
+
+template <int K, int U>
+__device__ __forceinline__ void store_group(const ColGroup<K, U>& cg, __amdgpu_buffer_rsrc_t rx,
+                                            int sx) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (cg.ok[u]) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) buf_st(cg.x[u][k], rx, cg.vo[u], k * sx);
+    }
+  }
+}
+
+template <int K, int U>
+__device__ __forceinline__ float block_objective(__amdgpu_buffer_rsrc_t rx, int sx,
+                                                 __amdgpu_buffer_rsrc_t rn, int sn,
+                                                 const lds_float* sG, int j0, int n, float l1_num,
+                                                 float l1, float l2, float* sred) {
+  float q = 0.f, l = 0.f;
+  const int T = blockDim.x;
+  for (int j = j0 + threadIdx.x; j < n; j += U * T) {
+    CNMF_MEMBAR();
+    ColGroup<K, U> cg;
+    load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, l1_num);
+    CNMF_OBJECTIVE_GROUP(cg);
+  }
+  block_sum2(q, l, sred);
+  return q - 2.f * l;
+}
+
+// RES = 1: register-resident variant, launched only when every slice fits one column
+// group per thread (host check in cnmf_solve); RES = 0: streaming variant.
+template <int K, int ALGO, int RES>
+__global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
+  // resident: one column per thread (its x and numer live in VGPRs for the whole solve)
+  constexpr int U = RES ? 1 : cols_per_group<K>();
+  __shared__ float sGm[K * K];
+  __shared__ float sred[2 * 16];
+  const lds_float* sG = (const lds_float*)sGm;  // LDS (addrspace 3): ds_read, 32-bit address
+  const int rep = p.rep_index ? p.rep_index[blockIdx.x] : (int)blockIdx.x;
+  if (p.active && p.active[rep] == 0) return;  // converged replicate: untouched (uniform)
+  float* __restrict__ x = p.x + (long long)rep * p.x_rs;
+  const float* __restrict__ nu = p.numer + (long long)rep * p.n_rs;
+  const float* __restrict__ g = p.gram + (long long)rep * p.g_rs;
+  for (int i = threadIdx.x; i < K * K; i += blockDim.x) sGm[i] = g[i];
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t rx = rsrc_of(x);
+  const __amdgpu_buffer_rsrc_t rn = rsrc_of(nu);
+  const int sx = (int)(p.ldx * 4), sn = (int)(p.ldn * 4);
+  const int T = blockDim.x;
+  // Column range of this block: the whole block, one of nsplit fixed-step slices, or one
+  // of S cooperative slices (gridDim.y) that still converge together.
+  int j0 = 0, n = p.ncols;
+  const bool coop = p.coop_slots != nullptr && gridDim.y > 1;
+  if (p.nsplit > 1 || coop) {
+    const int parts = coop ? (int)gridDim.y : p.nsplit;
+    const int per = (p.ncols + parts - 1) / parts;
+    j0 = min(p.ncols, (int)blockIdx.y * per);
+    n = min(p.ncols, j0 + per);
+  }
+  const bool check_conv = p.nsplit <= 1;
+  int epoch = 0;
+  const bool loss_conv = check_conv && p.conv_mode == 1;
+  const int every = p.check_every > 0 ? p.check_every : 1;
+  const float l1 = p.l1_den, l2 = p.l2, eps = p.eps;
+  float f_prev = 0.f;
+  bool have_prev = false;
+  int it = 0;
+  // Register-resident path: the slice fits one column group per thread, so x and numer
+  // stay in VGPRs for every iteration (no per-iteration global round trip -- that
+  // latency, not arithmetic, bounded the streaming loop on small slices).
+  constexpr bool resident = RES != 0;
+  ColGroup<K, U> rg;
+  if constexpr (resident) {
+    load_group<K, U>(rg, j0 + threadIdx.x, T, n, rx, sx, rn, sn, p.l1_num);
+    while (true) {
+      if (loss_conv && it % every == 0) {
+        float q = 0.f, l = 0.f;
+        CNMF_OBJECTIVE_GROUP(rg);
+        block_sum2(q, l, sred);
+        float f = q - 2.f * l;
+        if (coop) {
+          float unused = 0.f;
+          coop_sum2(p, rep, epoch++, f, unused, sred);
+        }
+        if (have_prev && fabsf(f_prev - f) <= p.tol * fabsf(f_prev)) break;
+        f_prev = f;
+        have_prev = true;
+      }
+      if (it >= p.max_iter) break;
+      float d2 = 0.f, x2 = 0.f;
+      CNMF_UPDATE_GROUP(rg);
+      ++it;
+      if (!check_conv || loss_conv) continue;
+      block_sum2(d2, x2, sred);
+      if (coop) coop_sum2(p, rep, epoch++, d2, x2, sred);
+      if (sqrtf(d2) / (sqrtf(x2) + eps) < p.tol) break;
+    }
+    store_group<K, U>(rg, rx, sx);
+  } else {
+    while (true) {
+      if (loss_conv && it % every == 0) {
+        float f = block_objective<K, U>(rx, sx, rn, sn, sG, j0, n, p.l1_num, l1, l2, sred);
+        if (coop) {
+          float unused = 0.f;
+          coop_sum2(p, rep, epoch++, f, unused, sred);
+        }
+        if (have_prev && fabsf(f_prev - f) <= p.tol * fabsf(f_prev)) break;
+        f_prev = f;
+        have_prev = true;
+      }
+      if (it >= p.max_iter) break;
+      float d2 = 0.f, x2 = 0.f;
+      for (int j = j0 + threadIdx.x; j < n; j += U * T) {
+        CNMF_MEMBAR();
+        ColGroup<K, U> cg;
+        load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, p.l1_num);
+        CNMF_UPDATE_GROUP(cg);
+        store_group<K, U>(cg, rx, sx);
+      }
+      ++it;
+      if (!check_conv || loss_conv) continue;
+      block_sum2(d2, x2, sred);
+      if (coop) coop_sum2(p, rep, epoch++, d2, x2, sred);
+      if (sqrtf(d2) / (sqrtf(x2) + eps) < p.tol) break;
+    }
+  }
+
+  if (p.lin_out || p.quad_out) {
+    float lin = 0.f, quad = 0.f;
+    if constexpr (resident) {
+      // epilogue uses the raw numerator (no l1 shift), as the streaming reload does
+      if (p.l1_num > 0.f) {
+        ColGroup<K, U> cg;
+        load_group<K, U>(cg, j0 + threadIdx.x, T, n, rx, sx, rn, sn, 0.f);
+        CNMF_LINQUAD_GROUP(cg);
+      } else {
+        CNMF_LINQUAD_GROUP(rg);
+      }
+    } else {
+      for (int j = j0 + threadIdx.x; j < n; j += U * T) {
+        CNMF_MEMBAR();
+        ColGroup<K, U> cg;
+        load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, 0.f);
+        CNMF_LINQUAD_GROUP(cg);
+      }
+    }
+    block_sum2(lin, quad, sred);
+    if (coop) coop_sum2(p, rep, epoch++, lin, quad, sred);
+    if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
+      if (check_conv) {
+        if (p.lin_out) p.lin_out[rep] = lin;
+        if (p.quad_out) p.quad_out[rep] = quad;
+      } else {  // split columns: caller zeroed the outputs
+        if (p.lin_out) atomicAdd(p.lin_out + rep, lin);
+        if (p.quad_out) atomicAdd(p.quad_out + rep, quad);
+      }
+    }
+  }
+  if (p.iters_out && threadIdx.x == 0 && blockIdx.y == 0) p.iters_out[rep] += it;
+}
+
+template <int K, int RES>
+hipError_t launch_solve_k(int algo, const SolveParams& p, int nblocks, int threads,
+                          hipStream_t s) {
+  if (threads > 1024) threads = 1024;
+  const int gy = p.nsplit > 1 ? p.nsplit : (p.coop_slots ? p.coop_epochs_split : 1);
+  const dim3 grid(nblocks, gy);
+  if (algo == 0)
+    hipLaunchKernelGGL((solve_kernel<K, 0, RES>), grid, dim3(threads), 0, s, p);
+  else
+    hipLaunchKernelGGL((solve_kernel<K, 1, RES>), grid, dim3(threads), 0, s, p);
+  return hipGetLastError();
+}
+
+#define CNMF_SOLVE_K_SWITCH(RES)                                                          \
+  switch (K) {                                                                            \
+    case 1: return launch_solve_k<1, RES>(algo, p, nblocks, threads, s);                  \
+    case 2: return launch_solve_k<2, RES>(algo, p, nblocks, threads, s);                  \
+    case 3: return launch_solve_k<3, RES>(algo, p, nblocks, threads, s);                  \
+    case 4: return launch_solve_k<4, RES>(algo, p, nblocks, threads, s);                  \
+    case 5: return launch_solve_k<5, RES>(algo, p, nblocks, threads, s);                  \
+    case 6: return launch_solve_k<6, RES>(algo, p, nblocks, threads, s);                  \
+    case 7: return launch_solve_k<7, RES>(algo, p, nblocks, threads, s);                  \
+    case 8: return launch_solve_k<8, RES>(algo, p, nblocks, threads, s);                  \
+    case 9: return launch_solve_k<9, RES>(algo, p, nblocks, threads, s);                  \
+    case 10: return launch_solve_k<10, RES>(algo, p, nblocks, threads, s);                \
+    case 11: return launch_solve_k<11, RES>(algo, p, nblocks, threads, s);                \
+    case 12: return launch_solve_k<12, RES>(algo, p, nblocks, threads, s);                \
+    case 13: return launch_solve_k<13, RES>(algo, p, nblocks, threads, s);                \
+    case 14: return launch_solve_k<14, RES>(algo, p, nblocks, threads, s);                \
+    case 15: return launch_solve_k<15, RES>(algo, p, nblocks, threads, s);                \
+    case 16: return launch_solve_k<16, RES>(algo, p, nblocks, threads, s);                \
+    case 17: return launch_solve_k<17, RES>(algo, p, nblocks, threads, s);                \
+    case 18: return launch_solve_k<18, RES>(algo, p, nblocks, threads, s);                \
+    case 19: return launch_solve_k<19, RES>(algo, p, nblocks, threads, s);                \
+    case 20: return launch_solve_k<20, RES>(algo, p, nblocks, threads, s);                \
+    case 21: return launch_solve_k<21, RES>(algo, p, nblocks, threads, s);                \
+    case 22: return launch_solve_k<22, RES>(algo, p, nblocks, threads, s);                \
+    case 23: return launch_solve_k<23, RES>(algo, p, nblocks, threads, s);                \
+    case 24: return launch_solve_k<24, RES>(algo, p, nblocks, threads, s);                \
+    case 25: return launch_solve_k<25, RES>(algo, p, nblocks, threads, s);                \
+    case 26: return launch_solve_k<26, RES>(algo, p, nblocks, threads, s);                \
+    case 27: return launch_solve_k<27, RES>(algo, p, nblocks, threads, s);                \
+    case 28: return launch_solve_k<28, RES>(algo, p, nblocks, threads, s);                \
+    case 29: return launch_solve_k<29, RES>(algo, p, nblocks, threads, s);                \
+    case 30: return launch_solve_k<30, RES>(algo, p, nblocks, threads, s);                \
+    case 31: return launch_solve_k<31, RES>(algo, p, nblocks, threads, s);                \
+    case 32: return launch_solve_k<32, RES>(algo, p, nblocks, threads, s);                \
+    default: return hipErrorInvalidValue;                                                 \
+  }
+
+// register-resident variant: K <= kResidentMaxK (one column per thread; beyond that the
+// live x / numer / x_new set of a column no longer fits 128 VGPRs without spilling)
+constexpr int kResidentMaxK = 16;
+
+// one per translation unit (solve.hip / solve_res.hip compile in parallel)
+hipError_t launch_solve_stream(int K, int algo, const SolveParams& p, int nblocks, int threads,
+                               hipStream_t s);
+hipError_t launch_solve_resident(int K, int algo, const SolveParams& p, int nblocks,
+                                 int threads, hipStream_t s);
+
+}  // namespace cnmf

@@ -328,3 +328,38 @@ def test_harmony_native_matches_cpu():
         np.testing.assert_allclose(gpu.R, cpu.R, rtol=1e-6, atol=1e-9)
         np.testing.assert_allclose(gpu.Z_corr, cpu.Z_corr, rtol=1e-6, atol=1e-8)
         assert gpu.kmeans_rounds == cpu.kmeans_rounds
+
+
+@pytest.mark.parametrize("algo,K", [("mu", 3), ("mu", 10), ("mu", 13), ("hals", 10), ("hals", 16)])
+@pytest.mark.parametrize("conv_mode", [0, 1])
+def test_solve_register_resident_variant(algo, K, conv_mode):
+    """variant='reg' (x, numer in VGPRs across iterations) == streaming == fp64 reference."""
+    R, n = 4, 1000
+    x0, numer, gram = _problem(R, K, n, seed=K + 7)
+    dev = torch.device("cuda")
+    outs = {}
+    for variant in ("stream", "reg"):
+        for max_iter, tol in ((6, -1.0), (300, 1e-4)):
+            xg = x0.clone().to(dev)
+            lin = torch.zeros(R, device=dev)
+            quad = torch.zeros(R, device=dev)
+            it = torch.zeros(R, dtype=torch.int32, device=dev)
+            ops.solve(algo, xg, numer.to(dev), gram.to(dev), max_iter=max_iter, tol=tol,
+                      lin_out=lin, quad_out=quad, iters_out=it, conv_mode=conv_mode,
+                      check_every=5, variant=variant, coop=1)
+            outs[(variant, tol)] = (xg.cpu(), lin.cpu(), quad.cpu(), it.cpu())
+    xr = x0.clone().double()
+    reference.solve(ops.ALGOS[algo], xr, numer.double(), gram.double(), None, 6, -1.0,
+                    0.0, 0.0, 0.0, 1e-16, None, None, None, 1, conv_mode, 5)
+    torch.testing.assert_close(outs[("reg", -1.0)][0].double(), xr, rtol=2e-4, atol=1e-4)
+    assert torch.equal(outs[("reg", -1.0)][0], outs[("stream", -1.0)][0])
+    a, b = outs[("reg", 1e-4)], outs[("stream", 1e-4)]
+    assert (a[3] - b[3]).abs().max() <= 5
+    assert ((a[0] - b[0]).norm() / b[0].norm()) < 2e-3
+    torch.testing.assert_close(a[1], b[1], rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(a[2], b[2], rtol=1e-3, atol=1e-3)
+    # coop split into resident slices
+    xg = x0.clone().to(dev)
+    ops.solve(algo, xg, numer.to(dev), gram.to(dev), max_iter=6, tol=-1.0, conv_mode=conv_mode,
+              check_every=5, variant="reg", coop=3)
+    assert torch.equal(xg.cpu(), outs[("reg", -1.0)][0])
