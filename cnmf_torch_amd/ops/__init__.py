@@ -213,7 +213,9 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
                 pass_idx: int, tol: float, final: bool, init: bool = False) -> None:
     """Per-replicate Frobenius error from (lin, quad) and the (prev - cur)/init < tol
     stopping rule, entirely on the device (csrc/kernels/conv.hip).  ``state`` holds
-    float64 err_init/err_prev/err and int32 active/converged/n_pass tensors."""
+    float64 err_init/err_prev/err and int32 active/converged/n_pass tensors.
+    ``pass_idx < 0`` counts passes on the device (n_pass += 1), so the launch has no
+    per-pass host argument and can live in a captured graph."""
     if n <= 0:
         return
     if not use_native(lin):

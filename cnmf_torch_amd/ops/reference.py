@@ -117,8 +117,9 @@ def conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init=False):
         return
     act = state["active"][:n] != 0
     state["err"][:n] = torch.where(act, e, state["err"][:n])
-    state["n_pass"][:n] = torch.where(act, torch.full_like(state["n_pass"][:n], pass_idx),
-                                      state["n_pass"][:n])
+    new_pass = (torch.full_like(state["n_pass"][:n], pass_idx) if pass_idx >= 0
+                else state["n_pass"][:n] + 1)              # pass_idx < 0: count passes
+    state["n_pass"][:n] = torch.where(act, new_pass, state["n_pass"][:n])
     rel = (state["err_prev"][:n] - e) / torch.clamp(state["err_init"][:n], min=1e-300)
     conv = act & (rel < tol)
     stop = conv | (act & bool(final))

@@ -28,7 +28,7 @@ __global__ void conv_update_kernel(const float* lin, const float* quad, double x
   }
   if (!active[r]) return;
   err[r] = e;
-  n_pass[r] = pass;
+  n_pass[r] = pass >= 0 ? pass : n_pass[r] + 1;   // pass < 0: count on device (graphs)
   const double denom = err_init[r] > 1e-300 ? err_init[r] : 1e-300;
   if ((err_prev[r] - e) / denom < tol) {
     active[r] = 0;

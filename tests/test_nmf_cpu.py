@@ -88,3 +88,12 @@ def test_online_kl_passes_monotone_errors():
         solver.opts.online_max_pass = p
         errs.append(float(solver.run([7]).err[0]))
     assert all(b <= a * (1 + 1e-9) for a, b in zip(errs, errs[1:])), errs
+
+
+def test_pass_counts_and_convergence_flags():
+    X = _data(200, 60, seed=6).astype(np.float32)
+    opts = NMFOptions(n_components=3, online_chunk_size=80, online_max_pass=7, tol=1e-3)
+    res = NMFBatchSolver(torch.from_numpy(X), opts).run([1, 2, 3])
+    assert ((res.n_iter >= 1) & (res.n_iter <= 7)).all(), res.n_iter
+    # a replicate that did not converge ran every pass
+    assert all(c or n == 7 for c, n in zip(res.converged, res.n_iter))
