@@ -46,6 +46,8 @@ def main() -> int:
     ap.add_argument("--max-nmf-iter", type=int, default=1000)
     ap.add_argument("--batch-size", type=int, default=5000)
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="replicate groups solved concurrently on separate HIP streams")
     args = ap.parse_args()
 
     import torch
@@ -84,7 +86,7 @@ def main() -> int:
 
     def step(i: int):
         seeds = all_seeds[i * n_total:(i + 1) * n_total][rank::world]
-        res = solver.run([int(s) for s in seeds])
+        res = solver.run_concurrent([int(s) for s in seeds], n_streams=args.streams)
         spectra = res.W.cpu()  # factorize persists spectra (cnmf.py:889-892)
         return res, spectra
 
@@ -132,6 +134,7 @@ def main() -> int:
                 "genes": args.genes,
                 "n_iter_per_gpu": args.n_iter,
                 "parallelism": f"replicate-parallel x{world}",
+                "streams_per_gpu": args.streams,
                 "device": "cpu" if not use_cuda else torch.cuda.get_device_name(dev),
                 "mean_passes": round(float(np.mean(passes)), 2) if passes else None,
             },

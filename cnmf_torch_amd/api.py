@@ -363,7 +363,8 @@ class cNMF:
                             print("[Worker %s]. Starting task %d." % (worker_label, idx), flush=True)
                     seeds = [int(run_params.iloc[i]["nmf_seed"]) for i in grp]
                     t0 = time.perf_counter()
-                    res = solver.run(seeds)
+                    res = solver.run_concurrent(seeds, n_streams=int(
+                        os.environ.get("CNMF_STREAMS", "1")))
                     W = res.W.cpu().numpy()
                     wall = time.perf_counter() - t0
                     for r, idx in enumerate(grp):

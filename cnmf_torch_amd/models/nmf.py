@@ -445,6 +445,51 @@ class NMFBatchSolver:
         return NMFResult(HT=HT, W=W, err=err, n_iter=n_iter, converged=conv, seeds=list(seeds),
                          K=K, stats=stats)
 
+    def run_concurrent(self, seeds, n_streams: int = 2, min_group: int = 8) -> NMFResult:
+        """Split the replicates into ``n_streams`` groups solved concurrently, each on its
+        own HIP stream (one host thread per stream).  One group's latency-bound inner solves
+        then overlap another group's GEMMs; results are identical to ``run`` on each group.
+        The cooperative solves of the groups share the co-residency budget
+        (ops.coop_share), so their spin-waiting workgroups can always all be resident.
+
+        Measured on the bench shape (100 replicates, 10k x 2k, K=10) this is SLOWER than
+        one stream (2 streams 34 ms, 3: 40 ms, 4: 70 ms vs 19.9 ms): the halved coop
+        budget lengthens the tail solves and the host threads contend for the GIL.  Kept
+        opt-in (bench --streams, CNMF_STREAMS) for shapes with few, long passes."""
+        seeds = list(seeds)
+        if (self.X.device.type != "cuda" or n_streams <= 1 or self.comm.is_distributed
+                or len(seeds) < n_streams * min_group):
+            return self.run(seeds)
+        import concurrent.futures as cf
+
+        bounds = np.linspace(0, len(seeds), n_streams + 1).astype(int)
+        groups = [seeds[bounds[i]:bounds[i + 1]] for i in range(n_streams)]
+        dev = self.X.device
+        ops.coop_prepare(dev)   # device queries from the main thread (fail in workers)
+        main = torch.cuda.current_stream(dev)
+        streams = [torch.cuda.Stream(dev) for _ in groups]
+        for s_ in streams:
+            s_.wait_stream(main)
+
+        def work(i):
+            torch.cuda.set_device(dev)
+            with torch.cuda.stream(streams[i]), ops.coop_share(n_streams):
+                return self.run(groups[i])
+
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(max_workers=n_streams) as ex:
+            parts = list(ex.map(work, range(n_streams)))
+        for s_ in streams:
+            main.wait_stream(s_)
+        stats = {"wall_s": time.perf_counter() - t0, "streams": n_streams,
+                 "h_inner_iters": sum((p_.stats["h_inner_iters"] for p_ in parts), []),
+                 "w_inner_iters": sum((p_.stats["w_inner_iters"] for p_ in parts), [])}
+        return NMFResult(HT=torch.cat([p_.HT for p_ in parts]), W=torch.cat([p_.W for p_ in parts]),
+                         err=np.concatenate([p_.err for p_ in parts]),
+                         n_iter=np.concatenate([p_.n_iter for p_ in parts]),
+                         converged=np.concatenate([p_.converged for p_ in parts]),
+                         seeds=seeds, K=parts[0].K, stats=stats)
+
     # ------------------------------------------------------------------ helpers
     def _steps(self, N: int):
         if self.schedule is not None:

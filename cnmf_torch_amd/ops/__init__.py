@@ -11,7 +11,9 @@ kernel is never handed an operand layout it does not assume.
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import threading
 
 import torch
 
@@ -163,6 +165,27 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
 _COOP_WS: dict = {}
 _COOP_RESIDENT: dict = {}
 COOP_COLS_PER_WG = 1024
+_TLS = threading.local()
+
+
+@contextlib.contextmanager
+def coop_share(n: int):
+    """Within this context (per host thread) cooperative solves use 1/n of the
+    co-residency budget: n streams running cooperative solves at once can then never
+    hold the whole chip with workgroups that wait for siblings that cannot be placed."""
+    prev = getattr(_TLS, "share", 1)
+    _TLS.share = max(1, int(n))
+    try:
+        yield
+    finally:
+        _TLS.share = prev
+
+
+def coop_prepare(dev: torch.device) -> None:
+    """Cache the device's co-residency budget (call from the thread that owns the
+    device before handing work to helper threads)."""
+    if dev.type == "cuda":
+        _coop_resident(dev)
 
 
 def _coop_resident(dev: torch.device) -> int:
@@ -170,7 +193,7 @@ def _coop_resident(dev: torch.device) -> int:
     if key not in _COOP_RESIDENT:
         cus = torch.cuda.get_device_properties(key).multi_processor_count
         _COOP_RESIDENT[key] = max(1, cus - 16)
-    return _COOP_RESIDENT[key]
+    return max(1, _COOP_RESIDENT[key] // getattr(_TLS, "share", 1))
 
 
 def _coop_split(n: int, nblocks: int, dev: torch.device) -> int:

@@ -383,3 +383,23 @@ def test_online_pass_graph_replay_matches_eager(monkeypatch):
     np.testing.assert_array_equal(g.err, e.err)
     np.testing.assert_array_equal(g.n_iter, e.n_iter)
     assert (g.n_iter >= 1).all() and (g.n_iter <= 8).all()   # passes counted on device
+
+
+def test_run_concurrent_streams_match_serial_groups():
+    """Two replicate groups on two HIP streams (shared coop budget) == each group alone."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+
+    rs = np.random.default_rng(5)
+    N, G, K = 4000, 600, 9
+    X = torch.from_numpy((rs.gamma(1, 1, (N, K)) @ rs.gamma(0.5, 1, (K, G)) +
+                          0.1 * rs.random((N, G))).astype(np.float32)).cuda()
+    solver = NMFBatchSolver(X, NMFOptions(n_components=K, online_chunk_size=1500,
+                                          online_max_pass=6))
+    seeds = list(range(100, 132))
+    both = solver.run_concurrent(seeds, n_streams=2)
+    with ops.coop_share(2):      # same cooperative split as inside run_concurrent
+        a = solver.run(seeds[:16])
+        b = solver.run(seeds[16:])
+    np.testing.assert_array_equal(both.W.cpu().numpy(),
+                                  torch.cat([a.W, b.W]).cpu().numpy())
+    np.testing.assert_array_equal(both.err, np.concatenate([a.err, b.err]))
