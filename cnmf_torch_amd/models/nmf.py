@@ -150,7 +150,9 @@ class NMFResult:
 
 # =============================================================================== init
 def _global_mean(X: torch.Tensor, comm) -> float:
-    s = comm.allreduce_scalar(float(X.sum(dtype=torch.float64)))
+    # float64 accumulation over row blocks (a dtype= reduction would copy X to float64)
+    s = comm.allreduce_scalar(sum(float(X[a:a + (1 << 16)].sum(dtype=torch.float64))
+                                  for a in range(0, X.shape[0], 1 << 16)))
     n = comm.allreduce_scalar(float(X.numel()))
     return s / max(n, 1.0)
 
@@ -159,14 +161,21 @@ def _nndsvd(X: torch.Tensor, K: int, variant: str, comm, eps: float = 1e-6, seed
     """sklearn's NNDSVD init (sklearn/decomposition/_nmf.py:316-366) via the Gram
     eigendecomposition, so it works on a cell-sharded X (only G x G and norms are
     all-reduced).  Returns (H (N_loc x K), W (K x G)) in X's dtype."""
-    Xd = X.to(torch.float64)
-    C = Xd.t() @ Xd
+    rows = 1 << 16    # float64 row blocks: never a full float64 copy of X
+    G = X.shape[1]
+    C = torch.zeros((G, G), dtype=torch.float64, device=X.device)
+    for a in range(0, X.shape[0], rows):
+        xb = X[a:a + rows].to(torch.float64)
+        C.addmm_(xb.t(), xb)
     comm.allreduce_(C)
     evals, evecs = torch.linalg.eigh(C)
     order = torch.argsort(evals, descending=True)[:K]
     S = torch.sqrt(torch.clamp(evals[order], min=0.0))
     V = evecs[:, order].t()                       # K x G
-    U = (Xd @ V.t()) / torch.clamp(S, min=1e-300)  # N_loc x K
+    U = torch.cat([X[a:a + rows].to(torch.float64) @ V.t()
+                   for a in range(0, X.shape[0], rows)]) if X.shape[0] else \
+        torch.zeros((0, K), dtype=torch.float64, device=X.device)
+    U = U / torch.clamp(S, min=1e-300)            # N_loc x K
     Wsk = torch.zeros_like(U)                     # sklearn W = usages
     Hsk = torch.zeros_like(V)                     # sklearn H = spectra
     Wsk[:, 0] = torch.sqrt(S[0]) * torch.abs(U[:, 0])
@@ -380,6 +389,16 @@ class _PassPipeline:
         return True
 
 
+def _sq_norm(X: torch.Tensor, rows: int = 1 << 16) -> float:
+    """||X||_F^2 accumulated in float64 over row blocks (no full float64 copy of X:
+    a 10M x 5k matrix would need 400 GB)."""
+    tot = torch.zeros((), dtype=torch.float64, device=X.device)
+    for a in range(0, X.shape[0], rows):
+        xb = X[a:a + rows]
+        tot += torch.linalg.vector_norm(xb, dtype=torch.float64) ** 2
+    return float(tot)
+
+
 def _graphs_enabled(X: torch.Tensor) -> bool:
     """Capture repeated passes into HIP graphs (GPU only, opt-in: CNMF_GRAPHS=1).  Off by
     default: a compaction changes the layout every few passes, and re-capturing cost more
@@ -414,7 +433,7 @@ class NMFBatchSolver:
         self.profile = profile
         self.timings: dict[str, float] = {}
         # ||X||_F^2 (global) for the trace-trick loss
-        self.x_sq = self.comm.allreduce_scalar(float((self.X.to(torch.float64) ** 2).sum()))
+        self.x_sq = self.comm.allreduce_scalar(_sq_norm(self.X))
 
     # ------------------------------------------------------------------ public
     def run(self, seeds, HT0=None, W0=None) -> NMFResult:

@@ -97,3 +97,19 @@ def test_pass_counts_and_convergence_flags():
     assert ((res.n_iter >= 1) & (res.n_iter <= 7)).all(), res.n_iter
     # a replicate that did not converge ran every pass
     assert all(c or n == 7 for c, n in zip(res.converged, res.n_iter))
+
+
+@pytest.mark.parametrize("variant", ["nndsvd", "nndsvda"])
+def test_nndsvd_init_matches_sklearn(variant):
+    from sklearn.decomposition._nmf import _initialize_nmf
+
+    from cnmf_torch_amd.models.nmf import _nndsvd
+    from cnmf_torch_amd.parallel.comm import LocalComm
+
+    X = _data(150, 70, seed=8)
+    K = 4
+    Wsk, Hsk = _initialize_nmf(X, K, init=variant, random_state=0)
+    H, W = _nndsvd(torch.from_numpy(X), K, variant, LocalComm())
+    # randomized vs exact SVD: agree to the randomized solver's accuracy
+    np.testing.assert_allclose(H.numpy(), Wsk, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(W.numpy(), Hsk, rtol=1e-5, atol=1e-6)

@@ -1,0 +1,148 @@
+"""Large-N benchmarks (BASELINE.json configs 3 and 4) on synthetic data generated on the
+device, so host RAM never holds the matrix.
+
+    # config 3: 1M cells x 2k genes, K=10, replicate-parallel (this GPU's share of 200)
+    python tools/bench_large.py --cells 1000000 --genes 2000 --k 10 --reps 25
+    # config 4: 10M cells x 5k genes, K=20, cell-sharded data parallel
+    torchrun --nproc-per-node 8 tools/bench_large.py --cells 10000000 --genes 5000 --k 20 --dp
+    python tools/bench_large.py --cells 10000000 --genes 5000 --k 20 --dp   # whole 200 GB on 1 GPU
+
+With ``--dp`` each rank owns rows [N*r/W, N*(r+1)/W) of X and the solver all-reduces the
+[dB | dA] sufficient statistics once per online step over RCCL (NMFBatchSolver with a
+DistComm); without it every rank factorises its own replicates of the full matrix.
+Data: planted programs (lognormal spectra, Dirichlet usages, Poisson counts), each gene
+scaled to unit variance like cNMF's norm_counts; the generator is seeded per row block,
+so the matrix is identical for any world size.  Prints one JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions  # noqa: E402
+from cnmf_torch_amd.parallel.comm import DistComm, LocalComm  # noqa: E402
+
+BLOCK = 1 << 17  # rows per generator block (seeded by block index)
+
+
+def device_counts(N, G, P, r0, r1, dev, comm, seed=0):
+    """Rows [r0, r1) of the planted-program matrix, scaled to global unit variance."""
+    gs = torch.Generator(device=dev).manual_seed(seed)
+    base = torch.empty(G, device=dev).log_normal_(0.0, 1.0, generator=gs)
+    S = base.repeat(P, 1)
+    nprog = max(1, int(0.15 * G))
+    for k in range(P):
+        idx = torch.randperm(G, device=dev, generator=gs)[:nprog]
+        S[k, idx] *= torch.empty(nprog, device=dev).log_normal_(1.5, 0.5, generator=gs)
+    S /= S.sum(dim=1, keepdim=True)
+    X = torch.empty((r1 - r0, G), device=dev, dtype=torch.float32)
+    b0 = r0 // BLOCK
+    for b in range(b0, (r1 + BLOCK - 1) // BLOCK):
+        lo, hi = max(r0, b * BLOCK), min(r1, (b + 1) * BLOCK)
+        g = torch.Generator(device=dev).manual_seed(seed * 1_000_003 + b + 1)
+        n = (b + 1) * BLOCK - b * BLOCK
+        gam = -torch.log(torch.rand((n, P), device=dev, generator=g).clamp_min_(1e-12))  # Exp(1)
+        U = gam ** (1.0 / 0.3)                                       # skewed mixture weights
+        U /= U.sum(dim=1, keepdim=True)
+        lib = torch.empty(n, device=dev).log_normal_(float(np.log(2000.0)), 0.35, generator=g)
+        lam = (U @ S) * lib[:, None]
+        cnt = torch.poisson(lam, generator=g)
+        X[lo - r0:hi - r0] = cnt[lo - b * BLOCK:hi - b * BLOCK]
+        del gam, U, lam, cnt
+    stats = torch.zeros(2 * G, dtype=torch.float64, device=dev)
+    for i in range(0, X.shape[0], BLOCK):          # float64 sums without a float64 copy of X
+        xb = X[i:i + BLOCK].double()
+        stats[:G] += xb.sum(dim=0)
+        stats[G:] += (xb * xb).sum(dim=0)
+        del xb
+    comm.allreduce_(stats)
+    mean = stats[:G] / N
+    var = (stats[G:] / N - mean ** 2) * (N / max(N - 1, 1))
+    sd = torch.sqrt(var.clamp_min(0)).float()
+    sd[sd == 0] = 1.0
+    X /= sd
+    return X
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=1_000_000)
+    ap.add_argument("--genes", type=int, default=2000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=25, help="replicates per step (per rank unless --dp)")
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=0)
+    ap.add_argument("--dp", action="store_true", help="cell-sharded data parallel")
+    ap.add_argument("--max-pass", type=int, default=20)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    comm = DistComm() if (world > 1 and a.dp) else LocalComm()
+    N, G = a.cells, a.genes
+    if a.dp:
+        r0, r1 = N * rank // world, N * (rank + 1) // world
+    else:
+        r0, r1 = 0, N
+    t0 = time.perf_counter()
+    X = device_counts(N, G, a.k, r0, r1, dev, comm)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    opts = NMFOptions(n_components=a.k, tol=1e-4, online_chunk_size=5000,
+                      online_chunk_max_iter=1000, online_max_pass=a.max_pass)
+    solver = NMFBatchSolver(X, opts, comm=comm, row_offset=r0)
+    np.random.seed(14)
+    seeds = np.random.randint(1, 2 ** 31 - 1, size=(a.warmup + a.steps) * a.reps * world)
+    for i in range(a.warmup):
+        solver.run([int(s) for s in seeds[i * a.reps:(i + 1) * a.reps]])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    passes = []
+    for i in range(a.warmup, a.warmup + a.steps):
+        if a.dp:   # every rank works on the same replicates (its own rows)
+            mine = seeds[i * a.reps:(i + 1) * a.reps]
+        else:      # replicate-parallel: each rank its own slice of the ledger
+            blk = seeds[i * a.reps * world:(i + 1) * a.reps * world]
+            mine = blk[rank::world]
+        res = solver.run([int(s) for s in mine])
+        _ = res.W.cpu()
+        passes.append(float(np.mean(res.n_iter)))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    total_reps = a.reps * a.steps * (1 if a.dp else world)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "NMF replicates/sec (large N)", "value": round(total_reps / el, 4),
+            "unit": "replicates/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "s_per_step": round(el / a.steps, 3), "mean_passes": round(float(np.mean(passes)), 2),
+            "data_gen_s": round(t_gen, 2), "dtype": "fp32",
+            "config": {"cells": N, "genes": G, "k": a.k, "replicates_per_step": a.reps * (
+                1 if a.dp else world), "parallelism": f"{'dp' if a.dp else 'replicate'}x{world}",
+                "hbm_gb_X_per_gpu": round(X.numel() * 4 / 1e9, 2)},
+            "data": "synthetic planted-program Poisson counts generated on device"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
