@@ -82,7 +82,9 @@ def _lloyd_batched(X: torch.Tensor, centers: torch.Tensor, max_iter: int, tol: f
         sums = torch.zeros((n_init * k, d), dtype=X.dtype, device=X.device)
         for r in range(n_init):
             sums.index_add_(0, flat[r * n:(r + 1) * n], X)
-        counts = torch.bincount(flat, minlength=n_init * k).to(X.dtype)
+        # scatter-add of ones (torch.bincount is ~0.4 s per call on ROCm at 5M points)
+        counts = torch.zeros(n_init * k, dtype=X.dtype, device=X.device).index_add_(
+            0, flat, torch.ones(flat.numel(), dtype=X.dtype, device=X.device))
         newc = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], C)
         newc = newc.view(n_init, k, d)
         shift = ((newc - centers) ** 2).sum(dim=(1, 2))

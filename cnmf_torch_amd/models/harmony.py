@@ -172,8 +172,12 @@ class Harmony:
             n_blocks = int(math.ceil(1 / self.block_size))
             self.E = self.E.contiguous()
             self.O = self.O.contiguous()
+            # one host->device copy of the round's order; blocks are device slices of it
+            order_d = torch.from_numpy(order.astype(np.int32)).to(self.dev, non_blocking=False)
+            a = 0
             for b in np.array_split(order, n_blocks):
-                cells = torch.as_tensor(b.astype(np.int32), device=self.dev)
+                cells = order_d[a:a + b.size]
+                a += b.size
                 ops.harmony_block_update(self.Rt, self.distT, self.sigma, cells, self.bidx,
                                          self.E, self.O, self.Pr_b, self.theta, self._ws)
             return

@@ -42,17 +42,24 @@ def stdscale_quantile_celing(_adata, max_value=None, quantile_thresh=None):
         X = ad.X
         if sp.issparse(X):
             n_total = X.shape[0] * X.shape[1]
-            data = np.sort(X.data)
-            n_zero = n_total - data.size
+            n_zero = n_total - X.data.size
             # np.quantile (linear) over the virtual full vector [zeros..., data...]
+            # (scaled counts are >= 0); only the two order statistics needed are selected
+            # (O(nnz) partition, not a sort of all stored values)
             pos = quantile_thresh * (n_total - 1)
             lo, hi = int(np.floor(pos)), int(np.ceil(pos))
+            if X.data.size and X.data.min() < 0:
+                full = np.concatenate([np.zeros(n_zero, X.data.dtype), X.data])
+                thr = float(np.quantile(full, quantile_thresh))
+            else:
+                want = sorted({i - n_zero for i in (lo, hi) if i >= n_zero})
+                part = np.partition(X.data, want) if want else None
 
-            def at(i):
-                return 0.0 if i < n_zero else float(data[i - n_zero])
+                def at(i):
+                    return 0.0 if i < n_zero else float(part[i - n_zero])
 
-            thr = at(lo) + (at(hi) - at(lo)) * (pos - lo)
-            X.data[X.data > thr] = thr
+                thr = at(lo) + (at(hi) - at(lo)) * (pos - lo)
+            np.minimum(X.data, X.data.dtype.type(thr), out=X.data)
         else:
             thr = np.quantile(X.reshape(-1), quantile_thresh)
             X[X > thr] = thr
@@ -203,10 +210,12 @@ class Preprocess:
         return ad, hvgs
 
     def harmony_correct_X(self, X, obs, pca, harmony_vars, theta=1, max_iter_harmony=20,
-                          device=None, init_backend="sklearn"):
+                          device=None, init_backend=None):
         """Harmony on the PCs, then the MOE ridge correction applied to the expression
         matrix itself, clamped at 0 (preprocess.py:342-388).  Returns (X_corr, X_pca_harmony)."""
         dev = torch.device(device) if device is not None else _default_device()
+        if init_backend is None:   # harmonypy's sklearn KMeans init on CPU; k-means on the GPU
+            init_backend = "device" if dev.type == "cuda" else "sklearn"
         res = run_harmony(pca, obs, harmony_vars, max_iter_harmony=max_iter_harmony, theta=theta,
                           device=dev, init_backend=init_backend)
         X_pca_harmony = res.Z_corr.T

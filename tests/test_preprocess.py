@@ -164,3 +164,30 @@ def test_select_features_mi():
                                                        makeplots=False)
     assert out.var["highly_variable"].sum() == 10
     assert {"MI", "MI_Rank", "MI_diff"} <= set(out.var.columns)
+
+
+def test_pca_matches_sklearn():
+    from sklearn.decomposition import PCA
+
+    rs = np.random.default_rng(0)
+    X = rs.normal(size=(300, 40)) @ rs.normal(size=(40, 40)) + rs.normal(size=40)
+    ad = pp.pca(AnnData(X=X.copy()), n_comps=10)
+    ref = PCA(n_components=10, svd_solver="full").fit(X)
+    Z = ref.transform(X)
+    got = ad.obsm["X_pca"]
+    # same subspace and scores up to per-component sign
+    for j in range(10):
+        s = np.sign(np.dot(got[:, j], Z[:, j]))
+        np.testing.assert_allclose(got[:, j] * s, Z[:, j], rtol=1e-6, atol=1e-8)
+    np.testing.assert_allclose(ad.uns["pca"]["variance"], ref.explained_variance_, rtol=1e-8)
+
+
+def test_quantile_ceiling_sparse_matches_dense():
+    from cnmf_torch_amd.preprocess import stdscale_quantile_celing
+
+    rs = np.random.default_rng(2)
+    X = rs.poisson(0.4, (400, 60)).astype(np.float64)
+    for q in (0.9, 0.999, 0.5):
+        a = stdscale_quantile_celing(AnnData(X=sp.csr_matrix(X)), quantile_thresh=q)
+        b = stdscale_quantile_celing(AnnData(X=X.copy()), quantile_thresh=q)
+        np.testing.assert_allclose(a.X.toarray(), b.X, rtol=1e-12, atol=1e-12)
