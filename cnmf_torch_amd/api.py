@@ -45,7 +45,20 @@ from .utils.h5ad import read_h5ad, write_h5ad
 from .utils.io import (check_dir_exists, dump_yaml, load_df_from_npz, load_yaml, read_10x_mtx,
                        read_any, read_counts_table, save_df_to_npz, save_df_to_text,
                        write_text_atomic)
-from .utils.timing import StageTimer, append_jsonl
+from .utils.log import get_logger
+from .utils.timing import StageTimer, append_jsonl, read_jsonl
+
+log = get_logger("cnmf_torch_amd.api")
+
+
+def _sha256(path: str) -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    with open(path, "rb") as fh:
+        for chunk in iter(lambda: fh.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
 
 _PATHS = {
     "normalized_counts": ("tmp", "{name}.norm_counts.h5ad"),
@@ -74,6 +87,7 @@ _PATHS = {
     "k_selection_stats": ("top", "{name}.k_selection_stats.df.npz"),
     # additions (not in the reference): per-replicate solver records
     "replicate_log": ("tmp", "{name}.replicates.jsonl"),
+    "replicate_manifest": ("tmp", "{name}.spectra_manifest.jsonl"),
 }
 
 # nmf-torch run_nmf defaults that the reference leaves implicit
@@ -342,6 +356,12 @@ class cNMF:
             # the GIL) while the next batch runs on the GPU; every file is still atomic
             pool = cf.ThreadPoolExecutor(max_workers=4)
             pending: list = []
+            manifest = self.paths["replicate_manifest"]
+
+            def _write_spectra(df, path, k_, it_):
+                save_df_to_npz(df, path)
+                append_jsonl(manifest, {"k": k_, "iter": it_, "file": os.path.basename(path),
+                                        "sha256": _sha256(path), "bytes": os.path.getsize(path)})
 
             def _flush():
                 for f in pending:
@@ -367,13 +387,15 @@ class cNMF:
                         os.environ.get("CNMF_STREAMS", "1")))
                     W = res.W.cpu().numpy()
                     wall = time.perf_counter() - t0
+                    log.info("k=%d: %d replicates in %.3f s (%.1f replicates/s) on %s", k,
+                             len(grp), wall, len(grp) / max(wall, 1e-9), dev)
                     for r, idx in enumerate(grp):
                         it = int(run_params.iloc[idx]["iter"])
                         if writer:
                             spectra = pd.DataFrame(W[r * k:(r + 1) * k],
                                                    index=np.arange(1, k + 1), columns=genes)
-                            pending.append(pool.submit(save_df_to_npz, spectra,
-                                                       self.paths["iter_spectra"] % (k, it)))
+                            pending.append(pool.submit(_write_spectra, spectra,
+                                                       self.paths["iter_spectra"] % (k, it), k, it))
                             append_jsonl(self.paths["replicate_log"], {
                                 "k": k, "iter": it, "seed": seeds[r], "worker": worker_label,
                                 "err": float(res.err[r]), "n_pass": int(res.n_iter[r]),
@@ -410,6 +432,29 @@ class cNMF:
         else:
             budget = 8e9
         return int(max(1, min(n_jobs, budget // max(per_rep, 1))))
+
+    def verify_replicates(self, components=None) -> list[dict]:
+        """Check every replicate spectra file against the write manifest (sha256 recorded
+        after each atomic write).  Returns one record per problem: missing file, file not
+        in the manifest, or checksum mismatch (SURVEY.md §5.2 sidecar manifest)."""
+        run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
+        latest = {}
+        for rec in read_jsonl(self.paths["replicate_manifest"]):
+            latest[rec["file"]] = rec
+        problems = []
+        for _, p in run_params.iterrows():
+            k, it = int(p["n_components"]), int(p["iter"])
+            if components is not None and k not in set(components):
+                continue
+            fn = self.paths["iter_spectra"] % (k, it)
+            base = os.path.basename(fn)
+            if not os.path.exists(fn):
+                problems.append({"k": k, "iter": it, "problem": "missing"})
+            elif base not in latest:
+                problems.append({"k": k, "iter": it, "problem": "not in manifest"})
+            elif _sha256(fn) != latest[base]["sha256"]:
+                problems.append({"k": k, "iter": it, "problem": "checksum mismatch"})
+        return problems
 
     # ------------------------------------------------------------------ combine
     def combine(self, components=None, skip_missing_files=False):

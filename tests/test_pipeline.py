@@ -202,3 +202,20 @@ def test_run_parallel_driver_with_workers(tmp_path):
         assert merged.shape == (4 * k, 50)
     assert not any("iter_" in f for f in os.listdir(os.path.join(str(tmp_path), "rp", "cnmf_tmp")))
     assert os.path.exists(obj.paths["k_selection_stats"])
+
+
+def test_replicate_manifest_detects_corruption(tmp_path):
+    Xc, cells, genes = simulate_counts(120, 70, 3, seed=4, sparse=False)
+    fn = str(tmp_path / "c.df.npz")
+    save_df_to_npz(pd.DataFrame(Xc, index=cells, columns=genes), fn)
+    obj = cNMF(output_dir=str(tmp_path), name="man")
+    obj.prepare(fn, components=[3], n_iter=3, seed=1, num_highvar_genes=40)
+    obj.factorize(verbose=False)
+    assert obj.verify_replicates() == []
+    victim = obj.paths["iter_spectra"] % (3, 1)
+    with open(victim, "r+b") as fh:
+        fh.seek(40)
+        fh.write(b"\x00\x01\x02")
+    os.remove(obj.paths["iter_spectra"] % (3, 2))
+    probs = {(p["iter"], p["problem"]) for p in obj.verify_replicates()}
+    assert probs == {(1, "checksum mismatch"), (2, "missing")}
