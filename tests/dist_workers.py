@@ -60,3 +60,39 @@ def comm_worker(rank, world, port, out_dir):
     np.save(os.path.join(out_dir, f"comm{rank}.npy"),
             np.array([t[0].item(), s, m, len(g), g[world - 1]["r"]]))
     dist.destroy_process_group()
+
+
+def fault_worker(rank, world, port, output_dir, name, fault_rank):
+    """Replicate-parallel factorize where ``fault_rank`` dies after one replicate
+    (CNMF_FAULT_AFTER_REPLICATES); every rank records how it ended and exits."""
+    import datetime
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    if rank == fault_rank:
+        os.environ["CNMF_FAULT_AFTER_REPLICATES"] = "1"
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=30))
+    torch.set_num_threads(1)
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.parallel.runner import distributed_factorize
+
+    status = "ok"
+    try:
+        distributed_factorize(cNMF(output_dir=output_dir, name=name), backend="gloo",
+                              verbose=False)
+    except Exception as e:  # the injected fault, or the peer's disappearance
+        status = type(e).__name__ + ": " + str(e)[:200]
+    with open(os.path.join(output_dir, f"status{rank}.txt"), "w") as fh:
+        fh.write(status)
+    os._exit(0)
+
+
+def resume_worker(rank, world, port, output_dir, name):
+    _init(rank, world, port)
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.parallel.runner import distributed_factorize
+
+    distributed_factorize(cNMF(output_dir=output_dir, name=name), skip_completed_runs=True,
+                          backend="gloo", verbose=False)
+    dist.destroy_process_group()

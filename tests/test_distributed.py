@@ -99,3 +99,28 @@ def test_distributed_factorize_matches_serial(prepared, mode):
         assert set(e_dp) == set(e_se)
         for key in e_dp:
             assert 0.9 < e_dp[key] / e_se[key] < 1.1, (key, e_dp[key], e_se[key])
+
+
+def test_rank_failure_then_resume_on_a_different_world_size(prepared):
+    """a rank dies mid-factorize; a restart with --skip-completed-runs
+    semantics on a different world size re-shards only the missing replicates, and the
+    final spectra equal a serial run (seeds are per replicate, not per rank)."""
+    d, fn = prepared
+    name = "fault"
+    obj = cNMF(output_dir=str(d), name=name)
+    obj.prepare(fn, components=[3, 4], n_iter=3, seed=5, num_highvar_genes=100)
+    _spawn(W.fault_worker, 2, str(d), name, 1)
+    st1 = (d / "status1.txt").read_text()
+    assert "injected failure" in st1
+    done = [os.path.exists(obj.paths["iter_spectra"] % (k, i)) for k in (3, 4) for i in range(3)]
+    assert 0 < sum(done) < 6
+    obj.update_nmf_iter_params()
+    _spawn(W.resume_worker, 3, str(d), name)
+    serial = cNMF(output_dir=str(d), name=name + "_serial")
+    serial.prepare(fn, components=[3, 4], n_iter=3, seed=5, num_highvar_genes=100)
+    serial.factorize(verbose=False)
+    for k in (3, 4):
+        for i in range(3):
+            a = load_df_from_npz(obj.paths["iter_spectra"] % (k, i)).values
+            b = load_df_from_npz(serial.paths["iter_spectra"] % (k, i)).values
+            np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-6)

@@ -403,3 +403,35 @@ def test_run_concurrent_streams_match_serial_groups():
     np.testing.assert_array_equal(both.W.cpu().numpy(),
                                   torch.cat([a.W, b.W]).cpu().numpy())
     np.testing.assert_array_equal(both.err, np.concatenate([a.err, b.err]))
+
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.too_slow,
+                                                                  HealthCheck.function_scoped_fixture])
+@given(seed=st.integers(0, 10_000), R=st.integers(1, 6), K=st.integers(1, 32),
+       n=st.integers(1, 5000), algo=st.sampled_from(["mu", "hals"]),
+       pad=st.integers(0, 7), coop=st.sampled_from(["auto", 1, 3]),
+       variant=st.sampled_from(["auto", "stream"]))
+def test_solve_random_shapes_match_reference(seed, R, K, n, algo, pad, coop, variant):
+    """Random (R, K, n), padded leading dimensions (strided views), both variants and
+    cooperative splits: fixed-step results == fp64 reference."""
+    g = torch.Generator().manual_seed(seed)
+    W = torch.rand((R, K, 2 * K + 3), generator=g, dtype=torch.float64) + 0.05
+    gram = torch.bmm(W, W.transpose(1, 2))
+    numer = torch.rand((R, K, n), generator=g, dtype=torch.float64) * K
+    x0 = torch.rand((R, K, n), generator=g, dtype=torch.float64) + 0.1
+    dev = torch.device("cuda")
+    xs = torch.zeros((R, K, n + pad), device=dev)
+    xs[:, :, :n] = x0.float().to(dev)
+    xv = xs[:, :, :n]                                     # ldx = n + pad
+    ops.solve(algo, xv, numer.float().to(dev), gram.float().to(dev), max_iter=3, tol=-1.0,
+              coop=coop, variant=variant)
+    xr = x0.clone()
+    reference.solve(ops.ALGOS[algo], xr, numer, gram, None, 3, -1.0, 0.0, 0.0, 0.0, 1e-16,
+                    None, None, None, 1, 0, 10)
+    torch.testing.assert_close(xv.cpu().double(), xr, rtol=5e-4, atol=5e-4)
+    assert torch.all(xs[:, :, n:] == 0)                   # padding untouched
+    ops.coop_check(dev)
