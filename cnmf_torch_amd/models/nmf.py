@@ -537,10 +537,10 @@ class NMFBatchSolver:
         A = stats[R * K * G:].view(R, K, K)
         torch.mm(st.HT, X, out=B)
         H3 = st.HT.view(R, K, X.shape[0])
-        torch.bmm(H3, H3.transpose(1, 2), out=A)
+        ops.gram(H3, out=A)
         self.comm.allreduce_(stats)
         lin = (B.view(R, K, G) * W3).sum(dim=(1, 2)).float().contiguous()
-        quad = (A * torch.bmm(W3, W3.transpose(1, 2))).sum(dim=(1, 2)).float().contiguous()
+        quad = (A * ops.gram(W3)).sum(dim=(1, 2)).float().contiguous()
         ops.conv_update(lin, quad, self.x_sq, st.state, R, 0, self.opts.tol, False, init=True)
         return A, B
 
@@ -554,9 +554,9 @@ class NMFBatchSolver:
         if self.beta == 2.0:
             # ||X||^2 - 2 <HT X, W> + <HT HT^T, W W^T>
             B = HT @ X
-            A = torch.bmm(HT.view(R, K, N), HT.view(R, K, N).transpose(1, 2))
+            A = ops.gram(HT.view(R, K, N))
             lin = (B.view(R, K, G) * W3).sum(dim=(1, 2)).double()
-            quad = (A * torch.bmm(W3, W3.transpose(1, 2))).sum(dim=(1, 2)).double()
+            quad = (A * ops.gram(W3)).sum(dim=(1, 2)).double()
             lin = self.comm.allreduce_(lin.contiguous())
             quad = self.comm.allreduce_(quad.contiguous())
             return torch.sqrt(torch.clamp(self.x_sq - 2 * lin.cpu() + quad.cpu(), min=0.0))
@@ -601,6 +601,7 @@ class NMFBatchSolver:
                     B = torch.empty((n * K, G), device=dev, dtype=dt)
                 lin = torch.zeros(n, device=dev, dtype=torch.float32)
                 quad = torch.zeros(n, device=dev, dtype=torch.float32)
+                wwt_buf = torch.empty((n, K, K), device=dev, dtype=dt)
             final = p + 1 == max_pass
 
             def enqueue_pass(pass_arg: int, final: bool) -> None:
@@ -628,7 +629,7 @@ class NMFBatchSolver:
                         xc = X[a:b]
                         hview = H3[:, :, a:b]                            # (n, K, cw) strided
                         h_old = hview.clone() if exact else None
-                        WWT = torch.bmm(W3, W3.transpose(1, 2))
+                        WWT = ops.gram(W3, out=wwt_buf, active=active)   # MFMA Gram
                         numerT = W @ xc.t()                              # (n*K, cw) GEMM
                         ops.solve(algo, hview, numerT.view(n, K, cw), WWT,
                                   max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
@@ -649,10 +650,11 @@ class NMFBatchSolver:
                         else:
                             if dist and first:
                                 torch.mm(HT[:, a:b], xc, out=accB)       # (n*K, G) GEMM
-                                torch.bmm(hview, hview.transpose(1, 2), out=accA)
+                                ops.gram(hview, out=accA)
                             else:
                                 accB.addmm_(HT[:, a:b], xc)              # B += h^T x
-                                accA.baddbmm_(hview, hview.transpose(1, 2))  # A += h^T h
+                                ops.gram(hview, out=accA, accumulate=True,   # A += h^T h
+                                         active=active)
                         first = False
                     if dist:
                         if first:
@@ -726,7 +728,7 @@ class NMFBatchSolver:
             W3 = W.view(n, K, G)
             active = st.active_mask()
             # H-step over all local cells
-            WWT = torch.bmm(W3, W3.transpose(1, 2))
+            WWT = ops.gram(W3, active=st.active_mask())
             numerT = W @ X.t()
             nsplit = 1 if hals else max(1, (N + 8191) // 8192)
             ops.solve(o.algo, HT.view(n, K, N), numerT.view(n, K, N), WWT,
@@ -736,7 +738,7 @@ class NMFBatchSolver:
             # W-step from the new H
             torch.mm(HT, X, out=B)
             H3 = HT.view(n, K, N)
-            torch.bmm(H3, H3.transpose(1, 2), out=A)
+            ops.gram(H3, out=A)
             comm.allreduce_(flat)
             check = (it + 1) % every == 0 or it + 1 == max_it
             ops.solve(o.algo, W3, B.view(n, K, G), A.contiguous(),

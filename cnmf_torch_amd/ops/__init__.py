@@ -384,6 +384,40 @@ def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: fl
                        _stream_ptr(HT3))
 
 
+# ----------------------------------------------------------------------------- gram
+def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
+         active: torch.Tensor | None = None) -> torch.Tensor:
+    """out[r] (+)= X3[r] X3[r]^T for X3 (R, K, n) with unit column stride (any row and
+    replicate strides), K <= 32: one MFMA workgroup per replicate (gram.hip).  Replicates
+    whose ``active`` flag is 0 keep their ``out`` untouched."""
+    R, K, n = X3.shape
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs an out tensor")
+        out = torch.empty((R, K, K), device=X3.device, dtype=X3.dtype)
+    if not use_native(X3) or X3.dtype != torch.float32 or K > 32:
+        g = torch.bmm(X3, X3.transpose(1, 2))
+        if active is not None:
+            keep = (active[:R] != 0).view(R, 1, 1)
+            g = torch.where(keep, out + g if accumulate else g, out)
+            out.copy_(g)
+        elif accumulate:
+            out += g
+        else:
+            out.copy_(g)
+        return out
+    if out.shape != (R, K, K) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous float32 (R, K, K) tensor")
+    if n > 1 and X3.stride(2) != 1:
+        raise ValueError("X3 needs unit column stride")
+    if active is not None and (active.dtype != torch.int32 or active.numel() < R):
+        raise ValueError("active: int32 with >= R entries")
+    _hip.gram(X3.data_ptr(), X3.stride(0), X3.stride(1), R, K, n, out.data_ptr(), K * K,
+              int(bool(accumulate)), active.data_ptr() if active is not None else 0,
+              _stream_ptr(X3))
+    return out
+
+
 # ----------------------------------------------------------------------------- consensus
 def _f64_rows(t: torch.Tensor) -> torch.Tensor:
     t = t.to(torch.float64)

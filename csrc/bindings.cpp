@@ -110,6 +110,14 @@ PYBIND11_MODULE(_hip, m) {
           "harmony_block");
   });
 
+  m.def("gram", [](uintptr_t X, long long x_rs, long long ldx, int R, int K, int n,
+                   uintptr_t out, long long o_rs, int accumulate, uintptr_t active,
+                   uintptr_t stream) {
+    check(cnmf_gram(P<const float>(X), x_rs, ldx, R, K, n, P<float>(out), o_rs, accumulate,
+                    P<const int>(active), reinterpret_cast<hipStream_t>(stream)),
+          "gram");
+  });
+
   m.def("philox_fill",
         [](uintptr_t out, long long rows, long long cols, long long s_row, long long s_col,
            long long rep_stride, long long row_offset, uintptr_t seeds, uintptr_t scales, int R,

@@ -1,0 +1,97 @@
+// Batched small Gram matrices on MFMA: out[r] (+)= X_r X_r^T for X_r = K x n (K <= 32),
+// the hh^T / WW^T products of every NMF step.
+//
+// hipBLASLt runs these (R x K x n)(R x n x K) batched GEMMs with a 16x16 macro tile at
+// ~3 % MFMA utilisation (profiles/r1_pmc_summary.txt: 20 us per call at K=10, n=5000,
+// R=100).  Here one 1024-thread workgroup owns one replicate: each wave streams 16-column
+// slabs, every lane loads ONE float4 (row m = lane&15, columns 4q..4q+3 with q = lane>>4)
+// and feeds each of its four elements as both the A and the B operand of
+// v_mfma_f32_16x16x4_f32 -- A[row m][k q] = X[m][c], B[k q][col m] = X[m][c] -- so the
+// k index is a permutation of the column order shared by both operands and
+// D[i][j] = sum_c X[i][c] X[j][c] needs no data movement.  K in (16, 32] uses the 2 x 2
+// tile grid.  The 16 per-wave partial tiles are summed in wave order through LDS
+// (deterministic), then written or accumulated.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace cnmf {
+
+typedef float gf32x4 __attribute__((ext_vector_type(4)));
+
+template <int T>  // T = 1 (K <= 16) or 2 (K <= 32) tiles per dimension
+__global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X, long long x_rs,
+                                                    long long ldx, int K, int n,
+                                                    float* __restrict__ out, long long o_rs,
+                                                    int accumulate, const int* active) {
+  __shared__ float red[16][T * T * 16 * 16 + 1];
+  const int rep = blockIdx.x;
+  if (active && active[rep] == 0) return;
+  const float* __restrict__ x = X + (long long)rep * x_rs;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int m = lane & 15, q = lane >> 4;
+  gf32x4 acc[T][T];
+#pragma unroll
+  for (int a = 0; a < T; ++a)
+#pragma unroll
+    for (int b = 0; b < T; ++b) acc[a][b] = gf32x4{0.f, 0.f, 0.f, 0.f};
+  const bool vec = (ldx & 3) == 0 && (((uintptr_t)x) & 15) == 0;
+  for (int c0 = wave * 16; c0 < n; c0 += nw * 16) {
+    const int c = c0 + 4 * q;
+    float v[T][4];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = m + 16 * t;
+      const float* xr = x + (long long)row * ldx;
+      if (row < K && vec && c + 3 < n) {
+        const float4 f = *reinterpret_cast<const float4*>(xr + c);
+        v[t][0] = f.x; v[t][1] = f.y; v[t][2] = f.z; v[t][3] = f.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[t][j] = (row < K && c + j < n) ? xr[c + j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int b = 0; b < T; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[a][j], v[b][j], acc[a][b], 0, 0, 0);
+  }
+  // C/D map: row 4q + i, col m (register i)
+#pragma unroll
+  for (int a = 0; a < T; ++a)
+#pragma unroll
+    for (int b = 0; b < T; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        red[wave][((a * T + b) * 16 + 4 * q + i) * 16 + m] = acc[a][b][i];
+  __syncthreads();
+  float* o = out + (long long)rep * o_rs;
+  for (int e = threadIdx.x; e < K * K; e += blockDim.x) {
+    const int i = e / K, j = e % K;
+    const int a = i >> 4, b = j >> 4;
+    const int slot = ((a * T + b) * 16 + (i & 15)) * 16 + (j & 15);
+    float s = 0.f;
+    for (int w = 0; w < nw; ++w) s += red[w][slot];
+    o[e] = accumulate ? o[e] + s : s;
+  }
+}
+
+}  // namespace cnmf
+
+extern "C" hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K, int n,
+                                float* out, long long o_rs, int accumulate, const int* active,
+                                hipStream_t stream) {
+  if (R <= 0) return hipSuccess;
+  if (K < 1 || K > 32 || n < 0) return hipErrorInvalidValue;
+  const int threads = n >= 16 * 16 ? 1024 : 64 * ((n + 15) / 16 > 0 ? ((n + 15) / 16) : 1);
+  if (K <= 16)
+    hipLaunchKernelGGL((cnmf::gram_kernel<1>), dim3(R), dim3(threads), 0, stream, X, x_rs, ldx, K,
+                       n, out, o_rs, accumulate, active);
+  else
+    hipLaunchKernelGGL((cnmf::gram_kernel<2>), dim3(R), dim3(threads), 0, stream, X, x_rs, ldx, K,
+                       n, out, o_rs, accumulate, active);
+  return hipGetLastError();
+}

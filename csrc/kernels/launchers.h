@@ -46,6 +46,10 @@ hipError_t cnmf_harmony_block(int op, double* Rt, const double* distT, const dou
                               const double* theta, double* Pen, double* part, int* counter,
                               hipStream_t stream);
 
+hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K, int n,
+                     float* out, long long o_rs, int accumulate, const int* active,
+                     hipStream_t stream);
+
 hipError_t cnmf_philox_fill(float* out, long long rows, long long cols, long long s_row,
                             long long s_col, long long rep_stride, long long row_offset,
                             const unsigned long long* seeds, const float* scales, int R,

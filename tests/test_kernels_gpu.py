@@ -435,3 +435,27 @@ def test_solve_random_shapes_match_reference(seed, R, K, n, algo, pad, coop, var
     torch.testing.assert_close(xv.cpu().double(), xr, rtol=5e-4, atol=5e-4)
     assert torch.all(xs[:, :, n:] == 0)                   # padding untouched
     ops.coop_check(dev)
+
+
+@pytest.mark.parametrize("K", [1, 5, 10, 16, 17, 32])
+def test_gram_kernel_matches_bmm(K):
+    """MFMA batched Gram (gram.hip): strided / offset views, ragged n, accumulate, active."""
+    g = torch.Generator().manual_seed(K)
+    R, N = 5, 1237
+    H = torch.rand((R, K, N), generator=g, dtype=torch.float64)
+    dev = torch.device("cuda")
+    Hd = H.float().to(dev)
+    for a, b in ((0, N), (3, 1001), (17, 18), (5, 5)):
+        view = Hd[:, :, a:b]                                 # unaligned base, ragged width
+        ref = torch.bmm(H[:, :, a:b], H[:, :, a:b].transpose(1, 2))
+        got = ops.gram(view)
+        torch.testing.assert_close(got.cpu().double(), ref, rtol=1e-5, atol=1e-4)
+    out = torch.full((R, K, K), 2.0, device=dev)
+    active = torch.tensor([1, 0, 1, 1, 0], dtype=torch.int32, device=dev)
+    ops.gram(Hd, out=out, accumulate=True, active=active)
+    ref = 2.0 + torch.bmm(H, H.transpose(1, 2))
+    for r in range(R):
+        if active[r]:
+            torch.testing.assert_close(out[r].cpu().double(), ref[r], rtol=1e-5, atol=1e-3)
+        else:
+            assert torch.all(out[r] == 2.0)
