@@ -54,12 +54,13 @@ def _kmeanspp(X: torch.Tensor, k: int, gen: torch.Generator, x_sq: torch.Tensor)
     pot = float(closest.sum())
     for c in range(1, k):
         r = torch.rand(trials, generator=gen, dtype=torch.float64) * pot
-        cum = torch.cumsum(closest.double(), 0).cpu()
-        cand = torch.searchsorted(cum, r).clamp(max=n - 1).to(X.device)
+        # candidate sampling stays on the device (no per-centre D2H of the potentials)
+        cum = torch.cumsum(closest.double(), 0)
+        cand = torch.searchsorted(cum, r.to(cum.device)).clamp(max=n - 1).to(X.device)
         d = ops.pairwise_dist(X, X[cand], squared=True)
         newc = torch.minimum(closest[:, None], d)
         pots = newc.sum(dim=0)
-        best = int(torch.argmin(pots))
+        best = torch.argmin(pots)
         centers[c] = X[cand[best]]
         closest = newc[:, best]
         pot = float(pots[best])
@@ -73,6 +74,8 @@ def _lloyd_batched(X: torch.Tensor, centers: torch.Tensor, max_iter: int, tol: f
     Returns (labels (n, n_init), inertia (n_init,))."""
     n_init, k, d = centers.shape
     n = X.shape[0]
+    if ops.kmeans_fused_ok(X, k):
+        return _lloyd_fused(X, centers, max_iter, tol)
     live = torch.ones(n_init, dtype=torch.bool, device=X.device)
     offs = (torch.arange(n_init, device=X.device) * k)[None, :]
     for _ in range(max_iter):
@@ -95,6 +98,24 @@ def _lloyd_batched(X: torch.Tensor, centers: torch.Tensor, max_iter: int, tol: f
     lab, mind = ops.seg_argmin(ops.pairwise_dist(X, centers.reshape(n_init * k, d),
                                                  squared=True), k)
     return lab, mind.sum(dim=0)
+
+
+def _lloyd_fused(X: torch.Tensor, centers: torch.Tensor, max_iter: int, tol: float):
+    """Low-dimensional Lloyd (d <= 64, e.g. Harmony's k-means init on cells x PCs): one
+    fused assign+accumulate launch per iteration for every restart (ops.kmeans_step,
+    kmeans.hip) -- no (n x n_init*k) distance matrix, no atomics; same freezing rule."""
+    n_init, k, d = centers.shape
+    live = torch.ones(n_init, dtype=torch.bool, device=X.device)
+    for _ in range(max_iter):
+        _, sums, counts, _ = ops.kmeans_step(X, centers, live=live)
+        newc = torch.where(counts[..., None] > 0, sums / counts.clamp(min=1)[..., None], centers)
+        shift = ((newc - centers) ** 2).sum(dim=(1, 2))
+        centers = torch.where(live[:, None, None], newc, centers)
+        live = live & (shift > tol)
+        if not bool(live.any()):
+            break
+    lab, _, _, mind = ops.kmeans_step(X, centers, want_sums=False, want_dist=True)
+    return lab.t(), mind.sum(dim=1)
 
 
 def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 300,

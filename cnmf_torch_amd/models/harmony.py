@@ -313,3 +313,38 @@ def moe_correct_ridge(Z_orig, Z_cos, Z_corr, R, W, K, Phi_Rk, Phi_moe, lamb, dev
     W_last = Wall[(int(K) - 1) * B1:].cpu().numpy()
     Phi_Rk = (Pt * Rt[int(K) - 1]).cpu().numpy()
     return Zcos.cpu().numpy(), Zc.cpu().numpy(), W_last, Phi_Rk
+
+
+def moe_correct_expression(X: torch.Tensor, R, Phi_moe, lamb, K: int | None = None,
+                           chunk: int = 65536) -> torch.Tensor:
+    """The MOE ridge correction of preprocess.py:9-18 applied to a device-resident
+    (cells x features) expression matrix, in place of the features x cells numpy
+    round trip: W_k = (Phi_Rk Phi_moe^T + lamb)^-1 Phi_Rk X (W_k[0] = 0, intercept kept),
+    X -= sum_k Phi_Rk^T W_k -- batched over clusters into GEMMs streamed over cell
+    chunks, float64 arithmetic, result stored in X's dtype (numpy's in-place
+    float32 -= float64 of the reference).  Returns the corrected matrix (new tensor)."""
+    dev = X.device
+    Rt = torch.as_tensor(np.asarray(R), dtype=torch.float64).to(dev)
+    if K is not None:
+        Rt = Rt[:int(K)]
+    Pt = torch.as_tensor(np.asarray(Phi_moe), dtype=torch.float64).to(dev)
+    Lt = torch.as_tensor(np.asarray(lamb), dtype=torch.float64).to(dev)
+    Kc, N = Rt.shape
+    B1 = Pt.shape[0]
+    F = X.shape[1]
+    PP = (Pt[:, None, :] * Pt[None, :, :]).reshape(B1 * B1, N)
+    A = (Rt @ PP.t()).reshape(Kc, B1, B1) + Lt[None]
+    Y = torch.zeros((Kc * B1, F), dtype=torch.float64, device=dev)
+    for a in range(0, N, chunk):
+        b = min(N, a + chunk)
+        RP = (Rt[:, None, a:b] * Pt[None, :, a:b]).reshape(Kc * B1, b - a)
+        Y += RP @ X[a:b].to(torch.float64)
+    W = torch.linalg.solve(A, Y.view(Kc, B1, F))
+    W[:, 0, :] = 0
+    W = W.reshape(Kc * B1, F)
+    out = torch.empty_like(X)
+    for a in range(0, N, chunk):
+        b = min(N, a + chunk)
+        RP = (Rt[:, None, a:b] * Pt[None, :, a:b]).reshape(Kc * B1, b - a)
+        out[a:b] = (X[a:b].to(torch.float64) - RP.t() @ W).to(X.dtype)
+    return out

@@ -175,8 +175,13 @@ def loess_fit(x: np.ndarray, y: np.ndarray, span: float = 0.3, degree: int = 2,
 
 
 def highly_variable_genes(adata, flavor: str = "seurat_v3", n_top_genes: int = 2000,
-                          batch_key: str | None = None, span: float = 0.3, inplace: bool = True):
-    """Seurat v3 HVG selection on raw counts (preprocess.py:295)."""
+                          batch_key: str | None = None, span: float = 0.3, inplace: bool = True,
+                          device_csr=None):
+    """Seurat v3 HVG selection on raw counts (preprocess.py:295).
+
+    ``device_csr``: the same counts already resident on the GPU as an
+    :class:`ops.sparse.DeviceCSR` -- the per-gene mean/variance and the clipped second
+    moments are then column-statistics kernels over the stored entries (one batch)."""
     if flavor != "seurat_v3":
         raise NotImplementedError("only flavor='seurat_v3' is used by Preprocess")
     adata = to_lite(adata)
@@ -184,18 +189,28 @@ def highly_variable_genes(adata, flavor: str = "seurat_v3", n_top_genes: int = 2
     batches = (pd.Series(np.zeros(adata.n_obs, dtype=int)) if batch_key is None
                else adata.obs[batch_key].astype("category").cat.codes.reset_index(drop=True))
     norm_vars = []
-    means_all, vars_all = _mean_var_ddof1(X)
+    dev_stats = device_csr is not None and batch_key is None
+    if dev_stats:
+        from ..ops import sparse as sops
+
+        m_t, v_t = sops.mean_var(device_csr, ddof=1)
+        means_all, vars_all = m_t.cpu().numpy(), v_t.cpu().numpy()
+    else:
+        means_all, vars_all = _mean_var_ddof1(X)
     for b in np.unique(batches.values):
         rows = np.flatnonzero(batches.values == b)
-        Xb = X[rows]
-        mean, var = _mean_var_ddof1(Xb)
+        Xb = X if dev_stats else X[rows]
+        mean, var = (means_all, vars_all) if dev_stats else _mean_var_ddof1(Xb)
         not_const = var > 0
         est = np.zeros(X.shape[1], dtype=np.float64)
         est[not_const] = loess_fit(np.log10(mean[not_const]), np.log10(var[not_const]), span=span)
         reg_std = np.sqrt(10 ** est)
         N = Xb.shape[0]
         clip = reg_std * np.sqrt(N) + mean
-        if sp.issparse(Xb):
+        if dev_stats:
+            s1_t, sq_t, _ = sops.col_stats(device_csr, clip=clip)
+            s1, sq = s1_t.cpu().numpy(), sq_t.cpu().numpy()
+        elif sp.issparse(Xb):
             Xc = sp.csr_matrix(Xb, dtype=np.float64, copy=True)
             Xc.data = np.minimum(Xc.data, clip[Xc.indices])
             sq = np.asarray(Xc.multiply(Xc).sum(axis=0)).reshape(-1)
@@ -239,6 +254,20 @@ def pca(adata, n_comps: int = 50, zero_center: bool = True, use_highly_variable:
     Xd = Xs.toarray() if sp.issparse(Xs) else np.asarray(Xs)
     dev = torch.device(device) if device is not None else torch.device("cpu")
     T = torch.as_tensor(Xd, dtype=torch.float64, device=dev)
+    Xp, Vh, var, ratio = pca_tensor(T, n_comps, zero_center)
+    adata.obsm["X_pca"] = Xp
+    PCs = np.zeros((adata.n_vars, Vh.shape[0]))
+    PCs[cols] = Vh.T
+    adata.varm["PCs"] = PCs
+    adata.uns["pca"] = {"variance": var, "variance_ratio": ratio}
+    return adata
+
+
+def pca_tensor(T: torch.Tensor, n_comps: int = 50, zero_center: bool = True):
+    """Zero-centred PCA of a (cells x features) tensor on its device (float64):
+    returns numpy (scores (n, c), components (c, features), variance, variance_ratio)."""
+    T = T.to(torch.float64)
+    dev = T.device
     if zero_center:
         T = T - T.mean(dim=0, keepdim=True)
     n_comps = min(n_comps, min(T.shape) - 1) if min(T.shape) > 1 else 1
@@ -254,12 +283,6 @@ def pca(adata, n_comps: int = 50, zero_center: bool = True, use_highly_variable:
     sign = torch.sign(XS[torch.argmax(torch.abs(XS), dim=0), torch.arange(XS.shape[1], device=dev)])
     sign[sign == 0] = 1
     XS, Vh = XS * sign, Vh * sign[:, None]
-    Xp = XS.cpu().numpy()
-    adata.obsm["X_pca"] = Xp
-    PCs = np.zeros((adata.n_vars, n_comps))
-    PCs[cols] = Vh.t().cpu().numpy()
-    adata.varm["PCs"] = PCs
     var = (S ** 2 / max(T.shape[0] - 1, 1)).cpu().numpy()
     total = float((T ** 2).sum().cpu()) / max(T.shape[0] - 1, 1)
-    adata.uns["pca"] = {"variance": var, "variance_ratio": var / total if total > 0 else var}
-    return adata
+    return XS.cpu().numpy(), Vh.cpu().numpy(), var, (var / total if total > 0 else var)

@@ -492,6 +492,61 @@ def seg_argmin(D: torch.Tensor, k: int, row_add: torch.Tensor | None = None,
     return lab.long(), mind
 
 
+def kmeans_fused_ok(X: torch.Tensor, k: int) -> bool:
+    """True when the fused low-dimensional Lloyd step (kmeans.hip) handles (X, k)."""
+    return use_native(X) and bool(_hip.kmeans_fits(int(k), int(X.shape[1])))
+
+
+def kmeans_step(X: torch.Tensor, C: torch.Tensor, live: torch.Tensor | None = None,
+                want_sums: bool = True, want_dist: bool = False):
+    """One Lloyd step for every restart: X (n, d) float64, C (n_init, k, d) float64.
+
+    Returns (labels int64 (n_init, n), sums (n_init, k, d) | None, counts (n_init, k) | None,
+    mind float64 (n_init, n) | None): the nearest centroid of every point (exact squared
+    distance, first index on ties), the per-cluster sums/counts of the assigned points
+    (fixed-order, deterministic) and the squared distances.  Restarts with live == 0 are
+    skipped on the GPU (their outputs are unspecified).  GPU: kmeans.hip."""
+    n, d = X.shape
+    n_init, k, d2 = C.shape
+    if d2 != d:
+        raise ValueError("kmeans_step: feature dimensions differ")
+    Xd = _f64_rows(X)
+    Cd = C.to(torch.float64).contiguous()
+    if not use_native(Xd):
+        xsq = (Xd * Xd).sum(dim=1)
+        csq = (Cd * Cd).sum(dim=2)
+        D = (xsq[None, :, None] + csq[:, None, :]
+             - 2.0 * torch.einsum("nd,rkd->rnk", Xd, Cd)).clamp_(min=0.0)
+        mind, lab = D.min(dim=2)
+        sums = cnt = None
+        if want_sums:
+            sums = torch.zeros((n_init, k, d), dtype=torch.float64)
+            cnt = torch.zeros((n_init, k), dtype=torch.float64)
+            for r in range(n_init):
+                sums[r].index_add_(0, lab[r], Xd)
+                cnt[r].index_add_(0, lab[r], torch.ones(n, dtype=torch.float64))
+        return lab, sums, cnt, (mind if want_dist else None)
+    if not _hip.kmeans_fits(int(k), int(d)):
+        raise ValueError(f"kmeans_step: k={k}, d={d} exceeds the fused kernel's LDS budget")
+    dev = Xd.device
+    nblk = int(_hip.kmeans_blocks(n))
+    lab = torch.empty((n_init, n), dtype=torch.int32, device=dev)
+    mind = torch.empty((n_init, n), dtype=torch.float64, device=dev) if want_dist else None
+    psum = pcnt = None
+    if want_sums:
+        psum = torch.empty((nblk, n_init, k, d), dtype=torch.float64, device=dev)
+        pcnt = torch.empty((nblk, n_init, k), dtype=torch.float64, device=dev)
+    lv = live.to(device=dev, dtype=torch.int32).contiguous() if live is not None else None
+    _hip.kmeans_step(Xd.data_ptr(), Xd.stride(0), n, d, Cd.data_ptr(), int(k), int(n_init),
+                     lv.data_ptr() if lv is not None else 0, lab.data_ptr(),
+                     mind.data_ptr() if mind is not None else 0,
+                     psum.data_ptr() if psum is not None else 0,
+                     pcnt.data_ptr() if pcnt is not None else 0, _stream_ptr(Xd))
+    sums = psum.sum(dim=0) if want_sums else None
+    cnt = pcnt.sum(dim=0) if want_sums else None
+    return lab.long(), sums, cnt, mind
+
+
 # ----------------------------------------------------------------------------- harmony
 def harmony_native_ok(t: torch.Tensor, K: int, B: int) -> bool:
     """True when the fused Harmony R-update kernels handle this problem on ``t``'s device."""

@@ -146,12 +146,30 @@ class Preprocess:
         else:
             raise Exception("data should either be an AnnData object or a list of 2 AnnData objects")
 
-        tp10k = pp.normalize_total(adata_RNA, target_sum=librarysize_targetsum, copy=True)
+        dev = torch.device(device) if device is not None else _default_device()
+        dX = _device_counts(adata_RNA, dev) if harmony_vars is not None else None
+        if dX is not None:
+            # TP10K from the resident counts: one row-sum + one scaling pass on the device
+            from .ops import sparse as sops
+
+            rs = librarysize_targetsum / _nonzero(sops.row_sums(dX))
+            f64 = adata_RNA.X.dtype == np.float64       # normalize_total keeps float64
+            data = sops.transform(dX, row_scale=rs, round_mid=not f64,
+                                  out_dtype=torch.float64 if f64 else torch.float32)
+            data = data.cpu().numpy()
+            X0 = adata_RNA.X
+            tp10k = AnnData(X=sp.csr_matrix((data, X0.indices, X0.indptr), shape=X0.shape),
+                            obs=adata_RNA.obs, var=adata_RNA.var,
+                            obsm=dict(adata_RNA.obsm), varm=dict(adata_RNA.varm),
+                            uns=dict(adata_RNA.uns))
+        else:
+            tp10k = pp.normalize_total(adata_RNA, target_sum=librarysize_targetsum, copy=True)
         adata_RNA, hvgs = self.normalize_batchcorrect(
             adata_RNA, harmony_vars=harmony_vars, n_top_genes=n_top_rna_genes,
             librarysize_targetsum=librarysize_targetsum, max_scaled_thresh=max_scaled_thresh,
             quantile_thresh=quantile_thresh, theta=theta, makeplots=makeplots,
-            max_iter_harmony=max_iter_harmony, device=device)
+            max_iter_harmony=max_iter_harmony, device=dev, _device_csr=dX)
+        del dX
 
         if adata_ADT is not None:
             adata_ADT = adata_ADT[adata_RNA.obs.index, :]
@@ -170,17 +188,29 @@ class Preprocess:
     def normalize_batchcorrect(self, _adata, normalize_librarysize=False, harmony_vars=None,
                                n_top_genes=None, librarysize_targetsum=1e4,
                                max_scaled_thresh=None, quantile_thresh=.9999, theta=1,
-                               makeplots=True, max_iter_harmony=20, device=None):
-        """Seurat-v3 HVGs, scaling + quantile ceiling, optional Harmony (preprocess.py:250-338)."""
+                               makeplots=True, max_iter_harmony=20, device=None,
+                               _device_csr=None):
+        """Seurat-v3 HVGs, scaling + quantile ceiling, optional Harmony (preprocess.py:250-338).
+
+        On a GPU with sparse counts and ``harmony_vars``, the counts are uploaded once and
+        every step runs on the device (:meth:`_harmony_device`)."""
         ad = to_lite(_adata)
+        dev = torch.device(device) if device is not None else _default_device()
+        dX = _device_csr
+        if dX is None and harmony_vars is not None:
+            dX = _device_counts(ad, dev)
         if n_top_genes is not None:
-            pp.highly_variable_genes(ad, flavor="seurat_v3", n_top_genes=n_top_genes)
+            pp.highly_variable_genes(ad, flavor="seurat_v3", n_top_genes=n_top_genes,
+                                     device_csr=dX)
         elif "highly_variable" not in ad.var.columns:
             raise Exception("If a numeric value for n_top_genes is not provided, you must include "
                             "a highly_variable column in _adata")
         hv = ad.var["highly_variable"].values.astype(bool)
-        dev = torch.device(device) if device is not None else _default_device()
-        if harmony_vars is not None:
+        if harmony_vars is not None and dX is not None:
+            ad = self._harmony_device(ad, dX, hv, normalize_librarysize, harmony_vars,
+                                      librarysize_targetsum, max_scaled_thresh, quantile_thresh,
+                                      theta, makeplots, max_iter_harmony)
+        elif harmony_vars is not None:
             anorm = pp.normalize_total(ad, target_sum=librarysize_targetsum, copy=True)
             anorm = anorm[:, hv]
             anorm = stdscale_quantile_celing(anorm, max_value=max_scaled_thresh,
@@ -208,6 +238,71 @@ class Preprocess:
                 make_count_hist(ad, num_cells=1000)
         hvgs = list(ad.var.index)
         return ad, hvgs
+
+    def _harmony_device(self, ad, A, hv, normalize_librarysize, harmony_vars, target_sum,
+                        max_scaled_thresh, quantile_thresh, theta, makeplots, max_iter_harmony):
+        """The harmony branch of normalize_batchcorrect (preprocess.py:300-324) with the
+        counts resident on the GPU as CSR (ops.sparse): normalize_total, the HVG subset,
+        scale(zero_center=False) with both ceilings and the densification are fused
+        into column-statistics / densify kernel passes; PCA, Harmony and the MOE ridge
+        correction consume the dense device matrices directly.  One D2H of the corrected
+        matrix at the end.  The corrected X keeps the input's float dtype (the
+        reference's in-place ``Z_corr -= ...`` on the float32 matrix)."""
+        from .models.harmony import moe_correct_expression
+        from .ops import sparse as sops
+        from .utils.anndata_lite import _take
+
+        n = A.shape[0]
+        cols = np.flatnonzero(hv)
+        nh = int(cols.size)
+        cmap = np.full(A.shape[1], -1, np.int32)
+        cmap[cols] = np.arange(nh, dtype=np.int32)
+        rs = target_sum / _nonzero(sops.row_sums(A))
+        f64 = ad.X.dtype == np.float64
+        # host dtypes: normalize_total -> float32 unless float64; scale of integer -> float64
+        norm_dt = torch.float64 if f64 else torch.float32
+        raw_dt = torch.float64 if (f64 or np.issubdtype(ad.X.dtype, np.integer)) else torch.float32
+
+        def scaled(row_scale, out_dtype):
+            # stdscale_quantile_celing of the (normalised) HVG subset, densified
+            xf = dict(row_scale=row_scale, col_map=cmap,
+                      round_mid=row_scale is not None and out_dtype == torch.float32)
+            _, var = sops.mean_var(A, ddof=1, n_out=nh, **xf)
+            std = torch.sqrt(var)
+            std[std == 0] = 1.0
+            mv = float("inf") if max_scaled_thresh is None else float(max_scaled_thresh)
+            if quantile_thresh is not None:
+                vals = sops.transform(A, col_div=std, max_value=mv, out_dtype=out_dtype, **xf)
+                thr = sops.quantile_with_zeros(vals, n * nh, quantile_thresh)
+                del vals
+                if out_dtype == torch.float32:
+                    thr = float(np.float32(thr))
+                mv = min(mv, thr)
+            return sops.densify(A, n_out=nh, col_div=std, max_value=mv, out_dtype=out_dtype, **xf)
+
+        anorm = scaled(rs, norm_dt)
+        if makeplots:
+            make_count_hist(AnnData(X=anorm[:1000].cpu().numpy()), num_cells=1000)
+        X_pca = pp.pca_tensor(anorm, 50, zero_center=True)[0]
+        if normalize_librarysize:
+            src = anorm
+        else:
+            del anorm
+            src = scaled(None, raw_dt)
+        res = run_harmony(X_pca, ad.obs, harmony_vars, max_iter_harmony=max_iter_harmony,
+                          theta=theta, device=src.device, init_backend="device")
+        Xc = moe_correct_expression(src, res.R, res.Phi_moe, res.lamb, K=res.K)
+        del src
+        Xc.clamp_(min=0)
+        out = AnnData(X=Xc.cpu().numpy(), obs=ad.obs, var=ad.var.iloc[cols],
+                      obsm=dict(ad.obsm),
+                      varm={k: (v[cols] if not isinstance(v, pd.DataFrame) else v.iloc[cols])
+                            for k, v in ad.varm.items()},
+                      layers={k: _take(v, slice(None), cols) for k, v in ad.layers.items()},
+                      uns=dict(ad.uns))
+        out.obsm["X_pca"] = X_pca
+        out.obsm["X_pca_harmony"] = res.Z_corr.T
+        return out
 
     def harmony_correct_X(self, X, obs, pca, harmony_vars, theta=1, max_iter_harmony=20,
                           device=None, init_backend=None):
@@ -255,6 +350,21 @@ class Preprocess:
             ad.var[v] = resdf[v].reindex(ad.var.index).values
         ad.var["highly_variable"] = ad.var["MI_Rank"] < n_top_features
         return ad
+
+
+def _nonzero(t: torch.Tensor) -> torch.Tensor:
+    """normalize_total's guard: zero-count cells are divided by 1 (stay zero)."""
+    return t + (t == 0)
+
+
+def _device_counts(ad, dev):
+    """The counts of ``ad`` as a device CSR when the device pipeline applies (GPU and a
+    sparse matrix), else None."""
+    if dev.type != "cuda" or not sp.issparse(ad.X):
+        return None
+    from .ops import sparse as sops
+
+    return sops.DeviceCSR.from_scipy(ad.X, device=dev)
 
 
 def _is_anndata(o) -> bool:

@@ -96,6 +96,68 @@ PYBIND11_MODULE(_hip, m) {
           "seg_argmin");
   });
 
+  m.def("kmeans_blocks", [](int n) { return cnmf_kmeans_blocks(n); });
+  m.def("kmeans_fits", [](int k, int d) { return cnmf_kmeans_fits(k, d); });
+  m.def("kmeans_step", [](uintptr_t X, long long ldx, int n, int d, uintptr_t C, int k,
+                          int n_init, uintptr_t live, uintptr_t labels, uintptr_t mind,
+                          uintptr_t psum, uintptr_t pcnt, uintptr_t stream) {
+    check(cnmf_kmeans_step(P<const double>(X), ldx, n, d, P<const double>(C), k, n_init,
+                           P<const int>(live), P<int>(labels), P<double>(mind), P<double>(psum),
+                           P<double>(pcnt), reinterpret_cast<hipStream_t>(stream)),
+          "kmeans_step");
+  });
+
+  m.def("csr_row_sums", [](uintptr_t indptr, uintptr_t data, int f64, int n, uintptr_t out,
+                           uintptr_t stream) {
+    check(cnmf_csr_row_sums(P<const long long>(indptr), P<const void>(data), f64, n,
+                            P<double>(out), reinterpret_cast<hipStream_t>(stream)),
+          "csr_row_sums");
+  });
+  m.def("csr_stats_blocks", [](int n) { return cnmf_csr_stats_blocks(n); });
+  m.def("csr_col_stats",
+        [](uintptr_t indptr, uintptr_t indices, uintptr_t data, int f64, int n, int n_out,
+           uintptr_t row_scale, uintptr_t col_map, uintptr_t col_div, uintptr_t clip,
+           double max_value, int round_mid, uintptr_t center, uintptr_t psum, uintptr_t psq,
+           uintptr_t pcnt, uintptr_t stream) {
+          check(cnmf_csr_col_stats(P<const long long>(indptr), P<const int>(indices),
+                                   P<const void>(data), f64, n, n_out,
+                                   P<const double>(row_scale), P<const int>(col_map),
+                                   P<const double>(col_div), P<const double>(clip), max_value,
+                                   round_mid, P<const double>(center), P<double>(psum),
+                                   P<double>(psq), P<double>(pcnt),
+                                   reinterpret_cast<hipStream_t>(stream)),
+                "csr_col_stats");
+        });
+  m.def("csr_transform",
+        [](uintptr_t indptr, uintptr_t indices, uintptr_t data, int f64, int n,
+           uintptr_t row_scale, uintptr_t col_map, uintptr_t col_div, uintptr_t clip,
+           double max_value, int round_mid, uintptr_t out, int out_f64, uintptr_t stream) {
+          check(cnmf_csr_transform(P<const long long>(indptr), P<const int>(indices),
+                                   P<const void>(data), f64, n, P<const double>(row_scale),
+                                   P<const int>(col_map), P<const double>(col_div),
+                                   P<const double>(clip), max_value, round_mid, P<void>(out),
+                                   out_f64, reinterpret_cast<hipStream_t>(stream)),
+                "csr_transform");
+        });
+  m.def("csr_densify",
+        [](uintptr_t indptr, uintptr_t indices, uintptr_t data, int f64, int n,
+           uintptr_t row_scale, uintptr_t col_map, uintptr_t col_div, uintptr_t clip,
+           double max_value, int round_mid, uintptr_t out, int out_f64, long long ldo,
+           uintptr_t stream) {
+          check(cnmf_csr_densify(P<const long long>(indptr), P<const int>(indices),
+                                 P<const void>(data), f64, n, P<const double>(row_scale),
+                                 P<const int>(col_map), P<const double>(col_div),
+                                 P<const double>(clip), max_value, round_mid, P<void>(out),
+                                 out_f64, ldo, reinterpret_cast<hipStream_t>(stream)),
+                "csr_densify");
+        });
+  m.def("radix_hist", [](uintptr_t x, long long m, unsigned prefix, unsigned mask, int shift,
+                         uintptr_t hist, uintptr_t stream) {
+    check(cnmf_radix_hist(P<const float>(x), m, prefix, mask, shift,
+                          P<unsigned long long>(hist), reinterpret_cast<hipStream_t>(stream)),
+          "radix_hist");
+  });
+
   m.def("harmony_max_kb", []() { return cnmf_harmony_max_kb(); });
   m.def("harmony_block", [](int op, uintptr_t Rt, uintptr_t distT, uintptr_t sigma,
                             uintptr_t cells, uintptr_t bidx, int nb, int N, int K, int B,

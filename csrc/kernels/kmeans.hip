@@ -1,0 +1,155 @@
+// Fused Lloyd step for low-dimensional k-means (Harmony's k-means init over cells in PC
+// space: harmonypy's KMeans(k ~ N/30 <= 100, n_init=10, max_iter=25) on N x d PCs,
+// d <= 64; consensus k-means at K x G spectra keeps the MFMA distance path).
+//
+// One launch per Lloyd iteration for ALL restarts (grid.y = restart):
+//   phase A  every thread owns one point per round: the point lives in registers
+//            (d padded to DP, a compile-time multiple of 16), the restart's centroids sit
+//            in LDS and are read as broadcast b128 loads; the thread keeps the argmin of
+//            the exact squared distance sum_j (x_j - c_j)^2 (first index on ties, as numpy
+//            argmin), writes its label (and the distance for the inertia).
+//   phase B  the round's points are added to the workgroup's centroid accumulator in LDS:
+//            thread j (< d) walks the round's 256 points IN ORDER and adds x[p][j] to
+//            acc[label[p]][j] (distinct addresses per lane, no atomics); thread 255 counts.
+//            Coalesced: for each p the d threads read one contiguous row of X.
+//   flush    the workgroup writes its partial sums/counts; the host sums the partials over
+//            workgroups with a fixed-order reduction -> bitwise deterministic centroids.
+// The (n x n_init*k) distance matrix of the MFMA path (4 GB at 500k cells x 10 x 100) is
+// never materialised.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace cnmf {
+
+constexpr int kKmThreads = 256;
+constexpr int kKmRounds = 4;   // rounds of 256 points per workgroup
+
+template <int DP>
+__global__ void __launch_bounds__(kKmThreads)
+    kmeans_step_kernel(const double* __restrict__ X, long long ldx, int n, int d,
+                       const double* __restrict__ C, int k, const int* __restrict__ live,
+                       int* __restrict__ labels, double* __restrict__ mind,
+                       double* __restrict__ psum, double* __restrict__ pcnt) {
+  extern __shared__ double smem[];
+  double* sC = smem;                       // k * DP centroids (zero padded)
+  double* sAcc = sC + (long long)k * DP;   // k * DP accumulator
+  double* sCnt = sAcc + (long long)k * DP; // k counts
+  int* sLab = reinterpret_cast<int*>(sCnt + k);   // 256 labels of the current round
+  const int r = blockIdx.y;
+  const int n_init = gridDim.y;
+  if (live != nullptr && live[r] == 0) return;    // frozen restart: partials unused
+  const int tid = threadIdx.x;
+  const double* Cr = C + (long long)r * k * d;
+  for (int e = tid; e < k * DP; e += kKmThreads) {
+    const int c = e / DP, j = e % DP;
+    sC[e] = j < d ? Cr[(long long)c * d + j] : 0.0;
+    sAcc[e] = 0.0;
+  }
+  for (int c = tid; c < k; c += kKmThreads) sCnt[c] = 0.0;
+  __syncthreads();
+
+  const long long base = (long long)blockIdx.x * (kKmThreads * kKmRounds);
+  for (int round = 0; round < kKmRounds; ++round) {
+    const long long p0 = base + (long long)round * kKmThreads;
+    if (p0 >= n) break;                              // uniform across the workgroup
+    const long long i = p0 + tid;
+    // ---- phase A: assignment
+    int arg = -1;
+    if (i < n) {
+      double x[DP];
+      const double* xr = X + i * ldx;
+#pragma unroll
+      for (int j = 0; j < DP; ++j) x[j] = j < d ? xr[j] : 0.0;
+      double best = 0.0;
+      arg = 0;
+      for (int c = 0; c < k; ++c) {
+        const double2* cc = reinterpret_cast<const double2*>(sC + (long long)c * DP);
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < DP / 2; ++j) {
+          const double2 v = cc[j];
+          const double a = x[2 * j] - v.x, b = x[2 * j + 1] - v.y;
+          s0 = fma(a, a, s0);
+          s1 = fma(b, b, s1);
+        }
+        const double s = s0 + s1;
+        if (c == 0 || s < best) {
+          best = s;
+          arg = c;
+        }
+      }
+      labels[(long long)r * n + i] = arg;
+      if (mind != nullptr) mind[(long long)r * n + i] = best;
+    }
+    sLab[tid] = arg;
+    __syncthreads();
+    // ---- phase B: ordered accumulation (only when partial sums are wanted)
+    if (psum != nullptr) {
+      const int np = (int)((n - p0) < kKmThreads ? (n - p0) : kKmThreads);
+      if (tid < d) {
+        const double* col = X + p0 * ldx + tid;
+        for (int p = 0; p < np; ++p) {
+          const int c = sLab[p];
+          sAcc[c * DP + tid] += col[(long long)p * ldx];
+        }
+      } else if (tid == kKmThreads - 1) {
+        for (int p = 0; p < np; ++p) sCnt[sLab[p]] += 1.0;
+      }
+    }
+    __syncthreads();
+  }
+  if (psum != nullptr) {
+    const long long slot = (long long)blockIdx.x * n_init + r;
+    double* ps = psum + slot * k * d;
+    for (int e = tid; e < k * d; e += kKmThreads) ps[e] = sAcc[(e / d) * DP + (e % d)];
+    for (int c = tid; c < k; c += kKmThreads) pcnt[slot * k + c] = sCnt[c];
+  }
+}
+
+template <int DP>
+static hipError_t launch_kmeans(const double* X, long long ldx, int n, int d, const double* C,
+                                int k, int n_init, const int* live, int* labels, double* mind,
+                                double* psum, double* pcnt, hipStream_t stream) {
+  const size_t lds = (size_t)(2 * (size_t)k * DP + k) * sizeof(double) + kKmThreads * sizeof(int);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_step_kernel<DP>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const int per = kKmThreads * kKmRounds;
+  const dim3 grid((unsigned)((n + per - 1) / per), (unsigned)n_init);
+  hipLaunchKernelGGL(kmeans_step_kernel<DP>, grid, dim3(kKmThreads), lds, stream, X, ldx, n, d, C,
+                     k, live, labels, mind, psum, pcnt);
+  return hipGetLastError();
+}
+
+}  // namespace cnmf
+
+extern "C" int cnmf_kmeans_blocks(int n) {
+  const int per = cnmf::kKmThreads * cnmf::kKmRounds;
+  return (n + per - 1) / per;
+}
+
+// Largest k * DP the LDS budget (160 KiB per CU) holds: 2 * k * DP + k doubles + labels.
+extern "C" int cnmf_kmeans_fits(int k, int d) {
+  if (k < 1 || d < 1 || d > 64) return 0;
+  const int dp = (d + 15) / 16 * 16;
+  const size_t lds = (size_t)(2 * (size_t)k * dp + k) * sizeof(double) +
+                     cnmf::kKmThreads * sizeof(int);
+  return lds <= 156 * 1024 ? 1 : 0;
+}
+
+extern "C" hipError_t cnmf_kmeans_step(const double* X, long long ldx, int n, int d,
+                                       const double* C, int k, int n_init, const int* live,
+                                       int* labels, double* mind, double* psum, double* pcnt,
+                                       hipStream_t stream) {
+  if (n <= 0 || n_init <= 0) return hipSuccess;
+  if (!cnmf_kmeans_fits(k, d)) return hipErrorInvalidValue;
+  const int dp = (d + 15) / 16 * 16;
+  switch (dp) {
+    case 16: return cnmf::launch_kmeans<16>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
+    case 32: return cnmf::launch_kmeans<32>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
+    case 48: return cnmf::launch_kmeans<48>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
+    default: return cnmf::launch_kmeans<64>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
+  }
+}

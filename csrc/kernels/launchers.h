@@ -50,6 +50,32 @@ hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K
                      float* out, long long o_rs, int accumulate, const int* active,
                      hipStream_t stream);
 
+int cnmf_kmeans_blocks(int n);
+int cnmf_kmeans_fits(int k, int d);
+hipError_t cnmf_kmeans_step(const double* X, long long ldx, int n, int d, const double* C, int k,
+                            int n_init, const int* live, int* labels, double* mind, double* psum,
+                            double* pcnt, hipStream_t stream);
+
+hipError_t cnmf_csr_row_sums(const long long* indptr, const void* data, int f64, int n,
+                             double* out, hipStream_t stream);
+int cnmf_csr_stats_blocks(int n);
+hipError_t cnmf_csr_col_stats(const long long* indptr, const int* indices, const void* data,
+                              int f64, int n, int n_out, const double* row_scale,
+                              const int* col_map, const double* col_div, const double* clip,
+                              double max_value, int round_mid, const double* center,
+                              double* psum, double* psq, double* pcnt, hipStream_t stream);
+hipError_t cnmf_csr_transform(const long long* indptr, const int* indices, const void* data,
+                              int f64, int n, const double* row_scale, const int* col_map,
+                              const double* col_div, const double* clip, double max_value,
+                              int round_mid, void* out, int out_f64, hipStream_t stream);
+hipError_t cnmf_csr_densify(const long long* indptr, const int* indices, const void* data,
+                            int f64, int n, const double* row_scale, const int* col_map,
+                            const double* col_div, const double* clip, double max_value,
+                            int round_mid, void* out, int out_f64, long long ldo,
+                            hipStream_t stream);
+hipError_t cnmf_radix_hist(const float* x, long long m, unsigned int prefix, unsigned int mask,
+                           int shift, unsigned long long* hist, hipStream_t stream);
+
 hipError_t cnmf_philox_fill(float* out, long long rows, long long cols, long long s_row,
                             long long s_col, long long rep_stride, long long row_offset,
                             const unsigned long long* seeds, const float* scales, int R,

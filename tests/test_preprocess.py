@@ -191,3 +191,49 @@ def test_quantile_ceiling_sparse_matches_dense():
         a = stdscale_quantile_celing(AnnData(X=sp.csr_matrix(X)), quantile_thresh=q)
         b = stdscale_quantile_celing(AnnData(X=X.copy()), quantile_thresh=q)
         np.testing.assert_allclose(a.X.toarray(), b.X, rtol=1e-12, atol=1e-12)
+
+
+def test_moe_correct_expression_matches_ridge():
+    """Device-resident (cells x features) MOE correction == preprocess.py:9-18 formula."""
+    from cnmf_torch_amd.models.harmony import moe_correct_expression
+
+    rs = np.random.default_rng(1)
+    F, N, K, B = 6, 90, 3, 3
+    X = rs.random((N, F))
+    R = rs.random((K, N))
+    R /= R.sum(0)
+    b = rs.integers(0, B, N)
+    Phi = np.zeros((B, N))
+    Phi[b, np.arange(N)] = 1
+    Phi_moe = np.vstack([np.ones((1, N)), Phi])
+    lamb = np.diag([0.0] + [1.0] * B)
+    _, Zc, _, _ = moe_correct_ridge(X.T, None, None, R, None, K, None, Phi_moe, lamb)
+    got = moe_correct_expression(torch.from_numpy(X), R, Phi_moe, lamb, K=K, chunk=32)
+    np.testing.assert_allclose(got.numpy(), Zc.T, rtol=1e-10, atol=1e-12)
+    got32 = moe_correct_expression(torch.from_numpy(X.astype(np.float32)), R, Phi_moe, lamb)
+    assert got32.dtype == torch.float32
+
+
+@pytest.mark.gpu
+def test_device_harmony_pipeline_matches_host():
+    """normalize_batchcorrect(harmony) with the counts resident on the GPU (fused CSR
+    kernels) selects the same HVGs and produces the same PCs as the host pipeline."""
+    Xc, cells, genes = simulate_counts(3000, 400, 4, seed=3, sparse=True)
+    rs = np.random.default_rng(0)
+    obs = pd.DataFrame({"batch": pd.Categorical(rs.choice(["x", "y", "z"], 3000))}, index=cells)
+    ad = AnnData(X=sp.csr_matrix(Xc, dtype=np.float32), obs=obs, var=pd.DataFrame(index=genes))
+    p = Preprocess(random_seed=0)
+    d_out, d_hv = p.normalize_batchcorrect(ad.copy(), harmony_vars=["batch"], n_top_genes=100,
+                                           makeplots=False, max_iter_harmony=3, device="cuda")
+    h_out, h_hv = p.normalize_batchcorrect(ad.copy(), harmony_vars=["batch"], n_top_genes=100,
+                                           makeplots=False, max_iter_harmony=3, device="cpu")
+    assert d_hv == h_hv
+    np.testing.assert_allclose(d_out.obsm["X_pca"], h_out.obsm["X_pca"], rtol=1e-4, atol=1e-4)
+    assert d_out.X.shape == (3000, 100) and d_out.X.dtype == np.float32
+    assert (d_out.X >= 0).all() and np.isfinite(d_out.X).all()
+    # TP10K from the device matches the host normalisation (to one float32 ulp: the
+    # device sums a cell's counts in float64, scipy in float32)
+    _, tp_d, _ = p.preprocess_for_cnmf(ad.copy(), harmony_vars=["batch"], n_top_rna_genes=100,
+                                       makeplots=False, max_iter_harmony=2, device="cuda")
+    tp_h = pp.normalize_total(ad.copy(), target_sum=1e4, copy=True)
+    np.testing.assert_allclose(tp_d.X.toarray(), tp_h.X.toarray(), rtol=2.5e-7, atol=0)

@@ -1,0 +1,137 @@
+"""Device CSR preprocessing ops (ops/sparse.py, csrc/kernels/sparse.hip).
+
+CPU: the torch paths against numpy / scipy / sklearn semantics (the host pipeline of
+models/pp.py).  GPU: the HIP kernels against those torch paths -- bitwise where the
+operation order is the same, to float64 rounding for the reductions.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+from cnmf_torch_amd.ops import sparse as sops
+
+
+def _counts(n=300, m=70, density=0.2, seed=0, dtype=np.float32):
+    rs = np.random.default_rng(seed)
+    X = sp.random(n, m, density=density, format="csr", random_state=rs,
+                  data_rvs=lambda k: rs.integers(1, 30, k)).astype(dtype)
+    X[5] = 0            # an empty row
+    X = X.tocsr()
+    X.eliminate_zeros()
+    X[:, 3] = 0         # an empty column
+    X = X.tocsr()
+    X.eliminate_zeros()
+    return X
+
+
+def _dev():
+    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+def test_row_sums_and_mean_var_match_sklearn():
+    from sklearn.utils.sparsefuncs import mean_variance_axis
+
+    X = _counts()
+    A = sops.DeviceCSR.from_scipy(X)
+    np.testing.assert_allclose(sops.row_sums(A).numpy(), np.asarray(X.sum(1)).ravel())
+    mean, var = sops.mean_var(A)
+    m_ref, v_ref = mean_variance_axis(X.astype(np.float64), axis=0)
+    np.testing.assert_allclose(mean.numpy(), m_ref, rtol=1e-13)
+    np.testing.assert_allclose(var.numpy(), v_ref, rtol=1e-12, atol=1e-14)
+    _, var1 = sops.mean_var(A, ddof=1)
+    np.testing.assert_allclose(var1.numpy(), v_ref * X.shape[0] / (X.shape[0] - 1), rtol=1e-12)
+
+
+def test_transform_matches_host_pipeline():
+    """normalize_total -> column subset -> scale(zero_center=False, max_value) in one pass
+    equals the host CSR pipeline (same sparsity, values to one float32 ulp: the gene std
+    comes from a different float64 summation order than sklearn's)."""
+    from cnmf_torch_amd.models import pp
+    from cnmf_torch_amd.utils.anndata_lite import AnnData
+
+    X = _counts()
+    ad = AnnData(X=X.copy())
+    norm = pp.normalize_total(ad, target_sum=1e4, copy=True)
+    keep = np.zeros(X.shape[1], bool)
+    keep[::3] = True
+    sub = norm[:, keep]
+    host = pp.scale(sub, zero_center=False, max_value=4.0).X.tocsr()
+
+    A = sops.DeviceCSR.from_scipy(X)
+    rsum = sops.row_sums(A)
+    rs = 1e4 / (rsum + (rsum == 0))
+    cmap = np.full(X.shape[1], -1, np.int32)
+    cmap[keep] = np.arange(keep.sum())
+    _, var = sops.mean_var(A, ddof=1, row_scale=rs, col_map=cmap, n_out=int(keep.sum()),
+                           round_mid=True)
+    std = torch.sqrt(var)
+    std[std == 0] = 1.0
+    vals = sops.transform(A, row_scale=rs, col_map=cmap, col_div=std, max_value=4.0,
+                          round_mid=True)
+    got = vals[vals >= 0].numpy()
+    np.testing.assert_allclose(got, host.data, rtol=3e-7, atol=0)
+    D = sops.densify(A, n_out=int(keep.sum()), row_scale=rs, col_map=cmap, col_div=std,
+                     max_value=4.0, round_mid=True)
+    np.testing.assert_allclose(D.numpy(), host.toarray(), rtol=3e-7, atol=0)
+
+
+def test_quantile_with_zeros_matches_numpy():
+    rs = np.random.default_rng(3)
+    vals = rs.random(1000).astype(np.float32) * 10
+    vals[::7] = -1.0                       # dropped entries
+    n_total = 5000
+    stored = vals[vals >= 0]
+    full = np.concatenate([np.zeros(n_total - stored.size, np.float32), stored])
+    for q in (0.5, 0.9, 0.9999, 0.0, 1.0):
+        got = sops.quantile_with_zeros(torch.from_numpy(vals), n_total, q)
+        assert got == pytest.approx(float(np.quantile(full, q)), rel=1e-6, abs=1e-7)
+
+
+def test_col_stats_clip_matches_numpy():
+    X = _counts(seed=2)
+    clip = np.linspace(1, 20, X.shape[1])
+    A = sops.DeviceCSR.from_scipy(X)
+    s, q, k = sops.col_stats(A, clip=clip)
+    Xc = X.astype(np.float64).copy()
+    Xc.data = np.minimum(Xc.data, clip[Xc.indices])
+    np.testing.assert_allclose(s.numpy(), np.asarray(Xc.sum(0)).ravel(), rtol=1e-13)
+    np.testing.assert_allclose(q.numpy(), np.asarray(Xc.multiply(Xc).sum(0)).ravel(), rtol=1e-13)
+    np.testing.assert_array_equal(k.numpy(), np.diff(X.tocsc().indptr))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("m", [70, 4000])
+def test_sparse_kernels_match_torch(dtype, m):
+    X = _counts(n=2500, m=m, density=0.05 if m > 1000 else 0.2, seed=m, dtype=dtype)
+    Ac = sops.DeviceCSR.from_scipy(X)
+    Ag = sops.DeviceCSR.from_scipy(X, device="cuda")
+    torch.testing.assert_close(sops.row_sums(Ag).cpu(), sops.row_sums(Ac), rtol=1e-13, atol=0)
+    rs = np.random.default_rng(0).random(X.shape[0]) + 0.5
+    cmap = np.where(np.arange(m) % 4 == 1, -1, 0).astype(np.int32)
+    cmap[cmap == 0] = np.arange((cmap == 0).sum())
+    nout = int((cmap >= 0).sum())
+    div = np.random.default_rng(1).random(nout) + 0.5
+    clip = np.random.default_rng(2).random(nout) * 30
+    xf = dict(row_scale=rs, col_map=cmap, n_out=nout, col_div=div, clip=clip, max_value=25.0,
+              round_mid=True)
+    for a, b in zip(sops.col_stats(Ag, **xf), sops.col_stats(Ac, **xf)):
+        torch.testing.assert_close(a.cpu(), b, rtol=1e-12, atol=1e-12)
+    mg, vg = sops.mean_var(Ag, ddof=1, **xf)
+    mc, vc = sops.mean_var(Ac, ddof=1, **xf)
+    torch.testing.assert_close(mg.cpu(), mc, rtol=1e-12, atol=1e-14)
+    torch.testing.assert_close(vg.cpu(), vc, rtol=1e-10, atol=1e-13)
+    # determinism
+    assert torch.equal(sops.col_stats(Ag, **xf)[1], sops.col_stats(Ag, **xf)[1])
+    xf.pop("n_out")
+    for od in (torch.float32, torch.float64):
+        assert torch.equal(sops.transform(Ag, out_dtype=od, **xf).cpu(),
+                           sops.transform(Ac, out_dtype=od, **xf))
+        assert torch.equal(sops.densify(Ag, n_out=nout, out_dtype=od, **xf).cpu(),
+                           sops.densify(Ac, n_out=nout, out_dtype=od, **xf))
+    vals = sops.transform(Ag, **xf)
+    n_total = X.shape[0] * nout
+    for q in (0.5, 0.99, 0.9999):
+        assert sops.quantile_with_zeros(vals, n_total, q) == \
+            sops.quantile_with_zeros(vals.cpu(), n_total, q)
