@@ -39,6 +39,7 @@ from .models.nmf import NMFBatchSolver, NMFOptions
 from .models.ols import efficient_ols_all_cols
 from .models.pp import scale as pp_scale
 from .models.refit import fit_H_online, fit_spectra_online
+from .ops import sparse as sops
 from .parallel.ledger import worker_filter
 from .utils.anndata_lite import AnnData
 from .utils.h5ad import read_h5ad, write_h5ad
@@ -118,6 +119,13 @@ def _device(use_gpu: bool, device=None) -> torch.device:
     return torch.device("cpu")
 
 
+def _device_csr(X, dev: torch.device):
+    """A sparse host matrix uploaded once as a device CSR when running on a GPU, else None."""
+    if dev.type != "cuda" or not sp.issparse(X):
+        return None
+    return sops.DeviceCSR.from_scipy(X, device=dev)
+
+
 def _dense32(X) -> np.ndarray:
     if sp.issparse(X):
         return X.astype(np.float32).toarray()
@@ -176,7 +184,9 @@ class cNMF:
                 write_h5ad(self.paths["tpm"], tpm)
 
             if sp.issparse(tpm.X):
-                gene_tpm_mean, gene_tpm_var = get_mean_var(tpm.X)
+                dT = _device_csr(tpm.X, _device(use_gpu))
+                gene_tpm_mean, gene_tpm_var = get_mean_var(dT if dT is not None else tpm.X)
+                del dT
                 gene_tpm_std = gene_tpm_var ** 0.5
             else:
                 gene_tpm_mean = np.array(tpm.X.mean(axis=0)).reshape(-1)
@@ -577,7 +587,10 @@ class cNMF:
         median_np = cluster_medians(L2, labels, sorted(set(labels))).cpu().numpy()
         median_spectra = pd.DataFrame(median_np, index=sorted(set(labels)), columns=merged.columns)
 
-        rf_usages = self.refit_usage(norm_counts.X, median_spectra, device=dev)
+        ncX = _device_csr(norm_counts.X, dev)
+        rf_usages = self.refit_usage(ncX if ncX is not None else norm_counts.X, median_spectra,
+                                     device=dev)
+        del ncX
         rf_usages = pd.DataFrame(rf_usages, index=norm_counts.obs.index, columns=median_spectra.index)
 
         if skip_stats:
@@ -600,26 +613,45 @@ class cNMF:
 
         tpm = read_h5ad(self.paths["tpm"])
         tpm_stats = load_df_from_npz(self.paths["tpm_stats"])
-        spectra_tpm = self.refit_spectra(tpm.X, norm_usages.astype(tpm.X.dtype), device=dev)
+        # sparse TPM on the GPU: uploaded once as CSR; the spectra refit, the OLS and the
+        # scaled-HVG usage refit below are CSR kernel passes over it (ops.sparse)
+        dT = _device_csr(tpm.X, dev)
+        tpmX = dT if dT is not None else tpm.X
+        spectra_tpm = self.refit_spectra(tpmX, norm_usages.astype(tpm.X.dtype), device=dev)
         spectra_tpm = pd.DataFrame(spectra_tpm, index=new_cols, columns=tpm.var.index)
         if normalize_tpm_spectra:
             spectra_tpm = spectra_tpm.div(spectra_tpm.sum(axis=1), axis=0) * 1e6
 
-        usage_coef = efficient_ols_all_cols(rf_usages.values, tpm.X, normalize_y=True, device=dev)
+        usage_coef = efficient_ols_all_cols(rf_usages.values, tpmX, normalize_y=True, device=dev)
         usage_coef = pd.DataFrame(usage_coef, index=new_cols, columns=tpm.var.index)
 
         if refit_usage:
             with open(self.paths["nmf_genes_list"]) as fh:
                 hvgs = fh.read().split("\n")
-            norm_tpm = tpm[:, hvgs]
-            if sp.issparse(norm_tpm.X):
-                norm_tpm = pp_scale(norm_tpm, zero_center=False)
+            if dT is not None:
+                # scale(tpm[:, hvgs], zero_center=False) as a lazy view of the resident CSR
+                pos = tpm.var.index.get_indexer(hvgs)
+                if (pos < 0).any():
+                    raise KeyError(f"HVGs missing from the TPM matrix: {list(np.array(hvgs)[pos < 0][:5])}")
+                cmap = np.full(tpm.shape[1], -1, np.int32)
+                cmap[pos] = np.arange(len(hvgs), dtype=np.int32)
+                _, var = sops.mean_var(dT, ddof=1, col_map=cmap, n_out=len(hvgs))
+                std = torch.sqrt(var)
+                std[std == 0] = 1.0
+                norm_X = dT.view(col_map=cmap, col_div=std, n_out=len(hvgs))
+                norm_dtype = tpm.X.dtype
             else:
-                norm_tpm.X = norm_tpm.X / norm_tpm.X.std(axis=0, ddof=1)
+                norm_tpm = tpm[:, hvgs]
+                if sp.issparse(norm_tpm.X):
+                    norm_tpm = pp_scale(norm_tpm, zero_center=False)
+                else:
+                    norm_tpm.X = norm_tpm.X / norm_tpm.X.std(axis=0, ddof=1)
+                norm_X, norm_dtype = norm_tpm.X, norm_tpm.X.dtype
             spectra_tpm_rf = spectra_tpm.loc[:, hvgs]
             spectra_tpm_rf = spectra_tpm_rf.div(tpm_stats.loc[hvgs, "__std"], axis=1)
-            rf = self.refit_usage(norm_tpm.X, spectra_tpm_rf.astype(norm_tpm.X.dtype), device=dev)
+            rf = self.refit_usage(norm_X, spectra_tpm_rf.astype(norm_dtype), device=dev)
             rf_usages = pd.DataFrame(rf, index=norm_counts.obs.index, columns=spectra_tpm_rf.index)
+        del dT, tpmX
 
         p = self.paths
         save_df_to_npz(median_spectra, p["consensus_spectra"] % (k, dt_repl))

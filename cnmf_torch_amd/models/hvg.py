@@ -18,7 +18,13 @@ import torch
 
 
 def get_mean_var(X):
-    """Column mean and ddof=0 variance of a dense/sparse/torch matrix (cnmf.py:128-131)."""
+    """Column mean and ddof=0 variance of a dense/sparse/torch matrix or a device CSR
+    (cnmf.py:128-131)."""
+    from ..ops import sparse as sops
+
+    if isinstance(X, sops.DeviceCSR):
+        mean, var = sops.mean_var(X, ddof=0)
+        return mean.cpu().numpy(), var.cpu().numpy()
     if isinstance(X, torch.Tensor):
         Xd = X.to(torch.float64)
         mean = Xd.mean(dim=0)

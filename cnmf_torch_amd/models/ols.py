@@ -16,6 +16,7 @@ import numpy as np
 import scipy.sparse as sp
 import torch
 
+from ..ops import sparse as sops
 from .hvg import get_mean_var
 
 
@@ -25,22 +26,27 @@ def efficient_ols_all_cols(X, Y, batch_size: int = 1024, normalize_y: bool = Fal
     if Y.shape[0] != n:
         raise ValueError("X and Y must have the same number of rows.")
     dev = torch.device(device) if device is not None else torch.device("cpu")
-    Xt = torch.as_tensor(np.asarray(X), dtype=torch.float64, device=dev)
+    if isinstance(Y, sops.DeviceCSR):
+        dev = Y.device
+    Xt = torch.as_tensor(np.asarray(X), dtype=torch.float64).to(dev)
     XtX = Xt.t() @ Xt
-    XtY = torch.zeros((p, Y.shape[1]), dtype=torch.float64, device=dev)
-    step = max(int(batch_size), 1) * 16
-    for a in range(0, n, step):
-        b = min(n, a + step)
-        blk = Y[a:b]
-        if sp.issparse(blk):
-            blk = blk.tocoo()
-            idx = torch.as_tensor(np.vstack([blk.row, blk.col]), dtype=torch.long, device=dev)
-            vals = torch.as_tensor(blk.data, dtype=torch.float64, device=dev)
-            Yb = torch.sparse_coo_tensor(idx, vals, blk.shape, device=dev)
-            XtY += torch.sparse.mm(Yb.t(), Xt[a:b]).t()
-        else:
-            Yb = torch.as_tensor(np.asarray(blk), dtype=torch.float64, device=dev)
-            XtY += Xt[a:b].t() @ Yb
+    if isinstance(Y, sops.DeviceCSR):     # resident CSR: one transposed-SpMM kernel pass
+        XtY = sops.tspmm(Y, Xt).t()
+    else:
+        XtY = torch.zeros((p, Y.shape[1]), dtype=torch.float64, device=dev)
+        step = max(int(batch_size), 1) * 16
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            blk = Y[a:b]
+            if sp.issparse(blk):
+                blk = blk.tocoo()
+                idx = torch.as_tensor(np.vstack([blk.row, blk.col]), dtype=torch.long, device=dev)
+                vals = torch.as_tensor(blk.data, dtype=torch.float64, device=dev)
+                Yb = torch.sparse_coo_tensor(idx, vals, blk.shape, device=dev)
+                XtY += torch.sparse.mm(Yb.t(), Xt[a:b]).t()
+            else:
+                Yb = torch.as_tensor(np.asarray(blk), dtype=torch.float64, device=dev)
+                XtY += Xt[a:b].t() @ Yb
     if normalize_y:
         mean, var = get_mean_var(Y)
         var = np.array(var, dtype=np.float64)

@@ -24,6 +24,7 @@ import scipy.sparse as sp
 import torch
 
 from .. import ops
+from ..ops import sparse as sops
 from ..utils import rng
 
 
@@ -44,7 +45,11 @@ def _block_to_device(blk, device, dtype):
 
 
 def numer_rows(W: torch.Tensor, X, block: int = 16384) -> torch.Tensor:
-    """W (K x G, device) times X^T for X (n x G) in any format -> (K x n) on W's device."""
+    """W (K x G, device) times X^T for X (n x G) in any format -> (K x n) on W's device.
+    A device CSR (ops.sparse.DeviceCSR, possibly a scaled/subset view) goes through the
+    CSR SpMM kernel; nothing is densified."""
+    if isinstance(X, sops.DeviceCSR):
+        return sops.spmm(X, W.t()).t().contiguous().to(W.dtype)
     n = X.shape[0]
     out = torch.empty((W.shape[0], n), device=W.device, dtype=W.dtype)
     if isinstance(X, torch.Tensor) and X.device == W.device:
@@ -58,7 +63,10 @@ def numer_rows(W: torch.Tensor, X, block: int = 16384) -> torch.Tensor:
 
 
 def numer_cols(U: torch.Tensor, X, block: int = 16384) -> torch.Tensor:
-    """U^T X for U (n x K, device) and X (n x G) in any format -> (K x G)."""
+    """U^T X for U (n x K, device) and X (n x G) in any format -> (K x G).  A device CSR
+    goes through the deterministic transposed-SpMM kernel (float64 accumulation)."""
+    if isinstance(X, sops.DeviceCSR):
+        return sops.tspmm(X, U).t().to(U.dtype).contiguous()
     n, G = X.shape
     out = torch.zeros((U.shape[1], G), device=U.device, dtype=U.dtype)
     if isinstance(X, torch.Tensor) and X.device == U.device:

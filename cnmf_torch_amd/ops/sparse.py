@@ -31,12 +31,26 @@ class DeviceCSR:
     """A (n x m) CSR matrix on a torch device: indptr int64, indices int32, data float32
     or float64 (integer counts are stored as float32, as normalize_total casts them)."""
 
-    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, data: torch.Tensor, shape):
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, data: torch.Tensor, shape,
+                 xf: dict | None = None):
         self.indptr = indptr
         self.indices = indices
         self.data = data
-        self.shape = (int(shape[0]), int(shape[1]))
+        self.xf = dict(xf or {})     # lazy transform of the stored values (see view())
+        n_out = self.xf.pop("n_out", None)
+        self.shape = (int(shape[0]), int(shape[1] if n_out is None else n_out))
+        self.n_stored_cols = int(shape[1])
         self._rows = None
+
+    def view(self, *, n_out: int | None = None, **xf) -> "DeviceCSR":
+        """The same stored matrix seen through a transform (row_scale, col_map, col_div,
+        clip, max_value, round_mid; see the module docstring), e.g. the scaled HVG
+        subset of a TPM matrix -- consumed by every op below without materialising it."""
+        V = DeviceCSR(self.indptr, self.indices, self.data, (self.shape[0], self.n_stored_cols),
+                      {**self.xf, **xf})
+        V.shape = (self.shape[0], int(n_out) if n_out is not None else self.shape[1])
+        V._rows = self._rows
+        return V
 
     @classmethod
     def from_scipy(cls, m, device=None, dtype=None) -> "DeviceCSR":
@@ -94,6 +108,17 @@ def _map(col_map, dev):
     return torch.as_tensor(col_map, dtype=torch.int32).to(dev).contiguous()
 
 
+def _merge(A, row_scale, col_map, col_div, clip, max_value, round_mid):
+    """Explicit transform arguments override the view's own."""
+    x = A.xf
+    return (row_scale if row_scale is not None else x.get("row_scale"),
+            col_map if col_map is not None else x.get("col_map"),
+            col_div if col_div is not None else x.get("col_div"),
+            clip if clip is not None else x.get("clip"),
+            max_value if max_value is not None else x.get("max_value"),
+            bool(round_mid or x.get("round_mid", False)))
+
+
 def _xform_ref(A: DeviceCSR, row_scale, col_map, col_div, clip, max_value, round_mid):
     """(kept mask, output column, transformed float64 value) of every entry -- the torch
     twin of csr_transform (same operation order and roundings)."""
@@ -136,6 +161,8 @@ def col_stats(A: DeviceCSR, *, row_scale=None, col_map=None, n_out: int | None =
     float64, of the transformed values v (see module docstring).  Deterministic."""
     dev = A.device
     n_out = int(n_out if n_out is not None else A.shape[1])
+    row_scale, col_map, col_div, clip, max_value, round_mid = _merge(
+        A, row_scale, col_map, col_div, clip, max_value, round_mid)
     rs, cm, cd, cl, ce = (_f64(row_scale, dev), _map(col_map, dev), _f64(col_div, dev),
                           _f64(clip, dev), _f64(center, dev))
     mv = float("inf") if max_value is None else float(max_value)
@@ -182,6 +209,8 @@ def transform(A: DeviceCSR, *, row_scale=None, col_map=None, col_div=None, clip=
     """Transformed value of every stored entry (dropped columns -> -1), same layout as
     A.data."""
     dev = A.device
+    row_scale, col_map, col_div, clip, max_value, round_mid = _merge(
+        A, row_scale, col_map, col_div, clip, max_value, round_mid)
     rs, cm, cd, cl = _f64(row_scale, dev), _map(col_map, dev), _f64(col_div, dev), _f64(clip, dev)
     mv = float("inf") if max_value is None else float(max_value)
     if not use_native(A.data):
@@ -204,6 +233,8 @@ def densify(A: DeviceCSR, *, n_out: int | None = None, row_scale=None, col_map=N
     """Dense (n x n_out) matrix of the transformed entries (zeros elsewhere)."""
     dev = A.device
     n_out = int(n_out if n_out is not None else A.shape[1])
+    row_scale, col_map, col_div, clip, max_value, round_mid = _merge(
+        A, row_scale, col_map, col_div, clip, max_value, round_mid)
     rs, cm, cd, cl = _f64(row_scale, dev), _map(col_map, dev), _f64(col_div, dev), _f64(clip, dev)
     mv = float("inf") if max_value is None else float(max_value)
     out = torch.zeros((A.shape[0], n_out), dtype=out_dtype, device=dev)
@@ -217,6 +248,67 @@ def densify(A: DeviceCSR, *, n_out: int | None = None, row_scale=None, col_map=N
                      _ptr(cl), mv, int(round_mid), out.data_ptr(), int(out_dtype == torch.float64),
                      n_out, _stream_ptr(A.data))
     return out
+
+
+def _xf_args(A: DeviceCSR):
+    x = A.xf
+    dev = A.device
+    rs, cm = _f64(x.get("row_scale"), dev), _map(x.get("col_map"), dev)
+    cd, cl = _f64(x.get("col_div"), dev), _f64(x.get("clip"), dev)
+    mv = x.get("max_value")
+    mv = float("inf") if mv is None else float(mv)
+    return rs, cm, cd, cl, mv, bool(x.get("round_mid", False))
+
+
+def spmm(A: DeviceCSR, B: torch.Tensor) -> torch.Tensor:
+    """T(A) @ B for B (A.shape[1] x K) -> (n x K) float32 (the refit numerator x W^T)."""
+    K = B.shape[1]
+    if B.shape[0] != A.shape[1]:
+        raise ValueError(f"spmm: B has {B.shape[0]} rows, A has {A.shape[1]} columns")
+    rs, cm, cd, cl, mv, rm = _xf_args(A)
+    if not use_native(A.data):
+        keep, c, v = _xform_ref(A, rs, cm, cd, cl, mv, rm)
+        rows, c, v = A.row_ids()[keep], c[keep], v[keep].float()
+        out = torch.zeros((A.shape[0], K), dtype=torch.float32)
+        return out.index_add_(0, rows, v[:, None] * B.float()[c])
+    _require_native()
+    if K > 64:
+        raise ValueError("spmm: K <= 64 supported by the CSR kernel")
+    Bf = B.to(device=A.device, dtype=torch.float32).contiguous()
+    out = torch.empty((A.shape[0], K), dtype=torch.float32, device=A.device)
+    _hip.csr_spmm(A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(),
+                  int(A.data.dtype == torch.float64), A.shape[0], _ptr(rs), _ptr(cm), _ptr(cd),
+                  _ptr(cl), mv, int(rm), Bf.data_ptr(), K, out.data_ptr(), _stream_ptr(A.data))
+    return out
+
+
+def tspmm(A: DeviceCSR, B: torch.Tensor) -> torch.Tensor:
+    """T(A)^T @ B for B (n x K) float32/float64 -> (A.shape[1] x K) float64, deterministic
+    (the spectra-refit numerator U^T X and the OLS X^T Y)."""
+    K = B.shape[1]
+    if B.shape[0] != A.shape[0]:
+        raise ValueError(f"tspmm: B has {B.shape[0]} rows, A has {A.shape[0]}")
+    n_out = A.shape[1]
+    rs, cm, cd, cl, mv, rm = _xf_args(A)
+    if not use_native(A.data):
+        keep, c, v = _xform_ref(A, rs, cm, cd, cl, mv, rm)
+        rows, c, v = A.row_ids()[keep], c[keep], v[keep]
+        out = torch.zeros((n_out, K), dtype=torch.float64)
+        return out.index_add_(0, c, v[:, None] * B.double()[rows])
+    _require_native()
+    if K > 64:
+        raise ValueError("tspmm: K <= 64 supported by the CSR kernel")
+    Bd = B.to(A.device)
+    if Bd.dtype not in (torch.float32, torch.float64):
+        Bd = Bd.double()
+    Bd = Bd.contiguous()
+    nb = int(_hip.csr_tspmm_blocks(A.shape[0]))
+    part = torch.empty((nb, n_out, K), dtype=torch.float64, device=A.device)
+    _hip.csr_tspmm(A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(),
+                   int(A.data.dtype == torch.float64), A.shape[0], n_out, _ptr(rs), _ptr(cm),
+                   _ptr(cd), _ptr(cl), mv, int(rm), Bd.data_ptr(),
+                   int(Bd.dtype == torch.float64), K, part.data_ptr(), _stream_ptr(A.data))
+    return part.sum(dim=0)
 
 
 def kth_nonneg(x: torch.Tensor, k: int) -> float:

@@ -151,6 +151,30 @@ PYBIND11_MODULE(_hip, m) {
                                  out_f64, ldo, reinterpret_cast<hipStream_t>(stream)),
                 "csr_densify");
         });
+  m.def("csr_spmm",
+        [](uintptr_t indptr, uintptr_t indices, uintptr_t data, int f64, int n,
+           uintptr_t row_scale, uintptr_t col_map, uintptr_t col_div, uintptr_t clip,
+           double max_value, int round_mid, uintptr_t B, int K, uintptr_t out, uintptr_t stream) {
+          check(cnmf_csr_spmm(P<const long long>(indptr), P<const int>(indices),
+                              P<const void>(data), f64, n, P<const double>(row_scale),
+                              P<const int>(col_map), P<const double>(col_div),
+                              P<const double>(clip), max_value, round_mid, P<const float>(B), K,
+                              P<float>(out), reinterpret_cast<hipStream_t>(stream)),
+                "csr_spmm");
+        });
+  m.def("csr_tspmm_blocks", [](int n) { return cnmf_csr_tspmm_blocks(n); });
+  m.def("csr_tspmm",
+        [](uintptr_t indptr, uintptr_t indices, uintptr_t data, int f64, int n, int n_out,
+           uintptr_t row_scale, uintptr_t col_map, uintptr_t col_div, uintptr_t clip,
+           double max_value, int round_mid, uintptr_t B, int b_f64, int K, uintptr_t part,
+           uintptr_t stream) {
+          check(cnmf_csr_tspmm(P<const long long>(indptr), P<const int>(indices),
+                               P<const void>(data), f64, n, n_out, P<const double>(row_scale),
+                               P<const int>(col_map), P<const double>(col_div),
+                               P<const double>(clip), max_value, round_mid, P<const void>(B),
+                               b_f64, K, P<double>(part), reinterpret_cast<hipStream_t>(stream)),
+                "csr_tspmm");
+        });
   m.def("radix_hist", [](uintptr_t x, long long m, unsigned prefix, unsigned mask, int shift,
                          uintptr_t hist, uintptr_t stream) {
     check(cnmf_radix_hist(P<const float>(x), m, prefix, mask, shift,

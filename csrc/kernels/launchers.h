@@ -73,6 +73,16 @@ hipError_t cnmf_csr_densify(const long long* indptr, const int* indices, const v
                             const double* col_div, const double* clip, double max_value,
                             int round_mid, void* out, int out_f64, long long ldo,
                             hipStream_t stream);
+hipError_t cnmf_csr_spmm(const long long* indptr, const int* indices, const void* data, int f64,
+                         int n, const double* row_scale, const int* col_map,
+                         const double* col_div, const double* clip, double max_value,
+                         int round_mid, const float* B, int K, float* out, hipStream_t stream);
+int cnmf_csr_tspmm_blocks(int n);
+hipError_t cnmf_csr_tspmm(const long long* indptr, const int* indices, const void* data, int f64,
+                          int n, int n_out, const double* row_scale, const int* col_map,
+                          const double* col_div, const double* clip, double max_value,
+                          int round_mid, const void* B, int b_f64, int K, double* part,
+                          hipStream_t stream);
 hipError_t cnmf_radix_hist(const float* x, long long m, unsigned int prefix, unsigned int mask,
                            int shift, unsigned long long* hist, hipStream_t stream);
 

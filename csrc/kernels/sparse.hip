@@ -174,6 +174,92 @@ __global__ void __launch_bounds__(256) radix_hist_kernel(const float* __restrict
   if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
 }
 
+// ---------------------------------------------------------------------------- SpMM
+// out (n x K) = T(A) . B with B (n_out x K) dense float32: one wave per row, each lane
+// accumulates K partial dot products over its entries, then K wave reductions (fixed
+// order -> deterministic).  The usage refit numerator x W^T of fit_H_online (cnmf.py:
+// 358-362) on a sparse / transformed (scaled HVG subset) matrix without densifying it.
+template <class T, int KB>
+__global__ void __launch_bounds__(256) csr_spmm_kernel(const long long* __restrict__ indptr,
+                                                       const int* __restrict__ indices,
+                                                       const T* __restrict__ data, int n,
+                                                       CsrXform t, const float* __restrict__ B,
+                                                       int K, float* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const double rs = t.row_scale ? t.row_scale[row] : 1.0;
+  float acc[KB];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) acc[k] = 0.f;
+  for (long long j = indptr[row] + lane; j < indptr[row + 1]; j += 64) {
+    int c = indices[j];
+    if (t.col_map) c = t.col_map[c];
+    if (c < 0) continue;
+    const float v = (float)xform(t, (double)data[j], rs, c);
+    const float* b = B + (long long)c * K;
+#pragma unroll
+    for (int k = 0; k < KB; ++k)
+      if (k < K) acc[k] = fmaf(v, b[k], acc[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    if (k < K) {
+      const float s = wave_sum(acc[k]);
+      if (lane == k) out[(long long)row * K + k] = s;
+    }
+  }
+}
+
+// out (n_out x K) = T(A)^T . B with B (n x K) dense: per-wave LDS tiles of (columns x K)
+// float64 accumulators, rows walked in order by their wave (distinct columns per row ->
+// no conflicts), waves combined in fixed order into per-workgroup partials.  The spectra
+// refit numerator U^T X (cnmf.py:994) and the OLS X^T Y (cnmf.py:103-120) on CSR.
+constexpr int kTsLds = 4608;   // doubles per wave: 4 waves x 4608 x 8 B = 144 KiB
+template <class T, class TB, int KB>
+__global__ void __launch_bounds__(256) csr_tspmm_kernel(const long long* __restrict__ indptr,
+                                                        const int* __restrict__ indices,
+                                                        const T* __restrict__ data, int n,
+                                                        int n_out, int rows_per_block,
+                                                        CsrXform t, const TB* __restrict__ B,
+                                                        int K, double* __restrict__ part) {
+  extern __shared__ double smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double* acc = smem + (size_t)wave * kTsLds;
+  const int tc = kTsLds / K;   // columns per tile
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(n, r0 + rows_per_block);
+  for (int t0 = 0; t0 < n_out; t0 += tc) {
+    const int tw = min(tc, n_out - t0);
+    for (int e = threadIdx.x; e < 4 * kTsLds; e += 256) smem[e] = 0.0;
+    __syncthreads();
+    for (int row = r0 + wave; row < r1; row += 4) {
+      double bk[KB];
+#pragma unroll
+      for (int k = 0; k < KB; ++k) bk[k] = k < K ? (double)B[(long long)row * K + k] : 0.0;
+      const double rs = t.row_scale ? t.row_scale[row] : 1.0;
+      const long long e = indptr[row + 1];
+      for (long long j = indptr[row] + lane; j < e; j += 64) {
+        int c = indices[j];
+        if (t.col_map) c = t.col_map[c];
+        c -= t0;
+        if (c < 0 || c >= tw) continue;
+        const double v = xform(t, (double)data[j], rs, c + t0);
+        double* a = acc + (long long)c * K;
+#pragma unroll
+        for (int k = 0; k < KB; ++k)
+          if (k < K) a[k] = fma(v, bk[k], a[k]);
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < tw * K; e += 256) {
+      const double s = smem[e] + smem[kTsLds + e] + smem[2 * kTsLds + e] + smem[3 * kTsLds + e];
+      part[((size_t)blockIdx.x * n_out + t0) * K + e] = s;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace cnmf
 
 using cnmf::CsrXform;
@@ -287,4 +373,66 @@ extern "C" hipError_t cnmf_radix_hist(const float* x, long long m, unsigned int 
   hipLaunchKernelGGL(cnmf::radix_hist_kernel, dim3((unsigned)nb), dim3(256), 0, stream, x, m,
                      prefix, mask, shift, hist);
   return hipGetLastError();
+}
+
+extern "C" hipError_t cnmf_csr_spmm(const long long* indptr, const int* indices, const void* data,
+                                    int f64, int n, const double* row_scale, const int* col_map,
+                                    const double* col_div, const double* clip, double max_value,
+                                    int round_mid, const float* B, int K, float* out,
+                                    hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (K < 1 || K > 64) return hipErrorInvalidValue;
+  const dim3 grid((n + 3) / 4);
+  const CsrXform t = make_xform(row_scale, col_map, col_div, clip, max_value, round_mid);
+#define CNMF_SP(TI, KB)                                                                      \
+  hipLaunchKernelGGL((cnmf::csr_spmm_kernel<TI, KB>), grid, dim3(256), 0, stream, indptr,     \
+                     indices, (const TI*)data, n, t, B, K, out)
+  if (f64) {
+    if (K <= 16) CNMF_SP(double, 16); else if (K <= 32) CNMF_SP(double, 32); else CNMF_SP(double, 64);
+  } else {
+    if (K <= 16) CNMF_SP(float, 16); else if (K <= 32) CNMF_SP(float, 32); else CNMF_SP(float, 64);
+  }
+#undef CNMF_SP
+  return hipGetLastError();
+}
+
+extern "C" int cnmf_csr_tspmm_blocks(int n) {
+  int nb = (n + 255) / 256;
+  return nb < 256 ? (nb > 0 ? nb : 1) : 256;
+}
+
+template <class TI, class TB, int KB>
+static hipError_t launch_tspmm(const long long* indptr, const int* indices, const void* data,
+                               int n, int n_out, CsrXform t, const void* B, int K, double* part,
+                               hipStream_t stream) {
+  const size_t lds = (size_t)4 * cnmf::kTsLds * sizeof(double);
+  hipError_t e = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&cnmf::csr_tspmm_kernel<TI, TB, KB>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const int nb = cnmf_csr_tspmm_blocks(n);
+  const int rpb = (n + nb - 1) / nb;
+  hipLaunchKernelGGL((cnmf::csr_tspmm_kernel<TI, TB, KB>), dim3(nb), dim3(256), lds, stream,
+                     indptr, indices, (const TI*)data, n, n_out, rpb, t, (const TB*)B, K, part);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t cnmf_csr_tspmm(const long long* indptr, const int* indices,
+                                     const void* data, int f64, int n, int n_out,
+                                     const double* row_scale, const int* col_map,
+                                     const double* col_div, const double* clip, double max_value,
+                                     int round_mid, const void* B, int b_f64, int K,
+                                     double* part, hipStream_t stream) {
+  if (n <= 0 || n_out <= 0) return hipSuccess;
+  if (K < 1 || K > 64) return hipErrorInvalidValue;
+  const CsrXform t = make_xform(row_scale, col_map, col_div, clip, max_value, round_mid);
+#define CNMF_TS(TI, TB)                                                                           \
+  return K <= 16 ? launch_tspmm<TI, TB, 16>(indptr, indices, data, n, n_out, t, B, K, part, stream) \
+       : K <= 32 ? launch_tspmm<TI, TB, 32>(indptr, indices, data, n, n_out, t, B, K, part, stream) \
+                 : launch_tspmm<TI, TB, 64>(indptr, indices, data, n, n_out, t, B, K, part, stream)
+  if (f64 && b_f64) { CNMF_TS(double, double); }
+  if (f64) { CNMF_TS(double, float); }
+  if (b_f64) { CNMF_TS(float, double); }
+  CNMF_TS(float, float);
+#undef CNMF_TS
 }

@@ -135,3 +135,70 @@ def test_sparse_kernels_match_torch(dtype, m):
     for q in (0.5, 0.99, 0.9999):
         assert sops.quantile_with_zeros(vals, n_total, q) == \
             sops.quantile_with_zeros(vals.cpu(), n_total, q)
+
+
+def test_spmm_tspmm_views_match_dense():
+    """CSR products through a lazy scaled-subset view == dense numpy on the same matrix."""
+    X = _counts(n=400, m=90, seed=4)
+    A = sops.DeviceCSR.from_scipy(X)
+    hv = np.array([5, 1, 40, 7, 88, 60])                 # unsorted subset, like an HVG list
+    cmap = np.full(X.shape[1], -1, np.int32)
+    cmap[hv] = np.arange(hv.size)
+    std = np.random.default_rng(0).random(hv.size) + 0.5
+    V = A.view(col_map=cmap, col_div=std, n_out=hv.size)
+    assert V.shape == (400, hv.size)
+    D = (X[:, hv].toarray().astype(np.float64) / std).astype(np.float32)
+    np.testing.assert_array_equal(sops.densify(V).numpy(), D)
+    B = np.random.default_rng(1).random((hv.size, 7)).astype(np.float32)
+    np.testing.assert_allclose(sops.spmm(V, torch.from_numpy(B)).numpy(), D @ B, rtol=1e-5)
+    U = np.random.default_rng(2).random((400, 7))
+    np.testing.assert_allclose(sops.tspmm(V, torch.from_numpy(U)).numpy(),
+                               D.astype(np.float64).T @ U, rtol=1e-6)
+    np.testing.assert_allclose(sops.tspmm(A, torch.from_numpy(U)).numpy(),
+                               X.toarray().astype(np.float64).T @ U, rtol=1e-12)
+
+
+def test_refit_and_ols_accept_device_csr():
+    from cnmf_torch_amd.models.ols import efficient_ols_all_cols
+    from cnmf_torch_amd.models.refit import fit_H_online, fit_spectra_online
+
+    X = _counts(n=500, m=60, seed=6)
+    A = sops.DeviceCSR.from_scipy(X)
+    W = np.random.default_rng(0).random((4, 60))
+    h1 = fit_H_online(X, W, chunk_size=128, random_state=3)
+    h2 = fit_H_online(A, W, chunk_size=128, random_state=3)
+    np.testing.assert_allclose(h2, h1, rtol=1e-4, atol=1e-6)
+    U = np.random.default_rng(1).random((500, 4))
+    s1 = fit_spectra_online(X, U, chunk_size=32, random_state=3)
+    s2 = fit_spectra_online(A, U, chunk_size=32, random_state=3)
+    np.testing.assert_allclose(s2, s1, rtol=1e-4, atol=1e-6)
+    b1 = efficient_ols_all_cols(U, X, normalize_y=True)
+    b2 = efficient_ols_all_cols(U, A, normalize_y=True)
+    # StandardScaler keeps float32 input in float32 for the z-score statistics; the CSR
+    # path accumulates them in float64
+    np.testing.assert_allclose(b2, b1, rtol=1e-5, atol=1e-9)
+    b3 = efficient_ols_all_cols(U, X.astype(np.float64), normalize_y=True)
+    np.testing.assert_allclose(b2, b3, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [3, 10, 40])
+def test_spmm_tspmm_kernels_match_torch(K):
+    X = _counts(n=3000, m=2500, density=0.03, seed=K)
+    Ac = sops.DeviceCSR.from_scipy(X)
+    Ag = sops.DeviceCSR.from_scipy(X, device="cuda")
+    cmap = np.where(np.arange(2500) % 3 == 0, -1, 0).astype(np.int32)
+    cmap[cmap == 0] = np.random.default_rng(K).permutation(int((cmap == 0).sum()))
+    nout = int((cmap >= 0).sum())
+    std = np.random.default_rng(0).random(nout) + 0.5
+    xf = dict(col_map=cmap, col_div=std, n_out=nout)
+    Vc, Vg = Ac.view(**xf), Ag.view(**xf)
+    B = torch.rand((nout, K))
+    torch.testing.assert_close(sops.spmm(Vg, B.cuda()).cpu(), sops.spmm(Vc, B), rtol=1e-5,
+                               atol=1e-5)
+    U = torch.rand((3000, K), dtype=torch.float64)
+    got = sops.tspmm(Vg, U.cuda())
+    torch.testing.assert_close(got.cpu(), sops.tspmm(Vc, U), rtol=1e-12, atol=1e-12)
+    assert torch.equal(got, sops.tspmm(Vg, U.cuda()))          # deterministic
+    torch.testing.assert_close(sops.tspmm(Ag, U.float().cuda()).cpu(),
+                               sops.tspmm(Ac, U.float()), rtol=1e-12, atol=1e-10)
