@@ -126,6 +126,34 @@ def _device_csr(X, dev: torch.device):
     return sops.DeviceCSR.from_scipy(X, device=dev)
 
 
+def _norm_counts_dense_device(counts, genes, guard_zero_std: bool, dev) -> AnnData:
+    """get_norm_counts for a dense count matrix on the GPU (cnmf.py:670-681): the HVG
+    column gather, the float64 cast and the unit-variance scaling run on the device; one
+    H2D of the counts and one D2H of the float64 result.  ``guard_zero_std`` selects
+    scanpy's scale (E[x^2] - E[x]^2, ddof=1, std 0 -> 1; used when the TPM is sparse)
+    over numpy's ``X / X.std(ddof=1)`` (two-pass, no guard)."""
+    cols = counts.var.index.get_indexer(list(genes))
+    if (cols < 0).any():
+        raise KeyError(f"genes missing from the counts: {list(np.array(genes)[cols < 0][:5])}")
+    T = torch.from_numpy(np.ascontiguousarray(counts.X)).to(dev)
+    T = T.index_select(1, torch.as_tensor(cols, device=dev)).to(torch.float64)
+    n = T.shape[0]
+    if guard_zero_std:
+        mean = T.mean(dim=0)
+        var = (T * T).mean(dim=0) - mean * mean
+        if n > 1:
+            var *= n / (n - 1)
+        std = torch.sqrt(var)
+        std[std == 0] = 1.0
+    else:
+        std = T.std(dim=0, unbiased=True)
+    T /= std
+    out = AnnData(X=T.cpu().numpy(), obs=counts.obs, var=counts.var.iloc[cols],
+                  obsm=dict(counts.obsm), uns=dict(counts.uns))
+    out.uns["_scaled_on_device"] = True
+    return out
+
+
 def _dense32(X) -> np.ndarray:
     if sp.issparse(X):
         return X.astype(np.float32).toarray()
@@ -221,9 +249,17 @@ class cNMF:
                 gstats, _ = get_highvar_genes(np.array(tpm.X), numgenes=num_highvar_genes)
             high_variance_genes_filter = list(tpm.var.index[gstats.high_var.values])
 
-        norm_counts = counts[:, high_variance_genes_filter].copy()
-        norm_counts.X = norm_counts.X.astype(np.float64)
-        if sp.issparse(tpm.X):
+        dev = _device(False)
+        if not sp.issparse(counts.X) and dev.type == "cuda":
+            norm_counts = _norm_counts_dense_device(counts, high_variance_genes_filter,
+                                                    guard_zero_std=sp.issparse(tpm.X), dev=dev)
+        else:
+            norm_counts = counts[:, high_variance_genes_filter].copy()
+            norm_counts.X = norm_counts.X.astype(np.float64)
+        if norm_counts.uns.pop("_scaled_on_device", False):
+            if np.isnan(norm_counts.X).sum() > 0:
+                print("Warning NaNs in normalized counts matrix")
+        elif sp.issparse(tpm.X):
             norm_counts = pp_scale(norm_counts, zero_center=False)
             if np.isnan(norm_counts.X.data).sum() > 0:
                 print("Warning NaNs in normalized counts matrix")

@@ -202,3 +202,27 @@ def test_spmm_tspmm_kernels_match_torch(K):
     assert torch.equal(got, sops.tspmm(Vg, U.cuda()))          # deterministic
     torch.testing.assert_close(sops.tspmm(Ag, U.float().cuda()).cpu(),
                                sops.tspmm(Ac, U.float()), rtol=1e-12, atol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sparse_tpm", [True, False])
+def test_norm_counts_dense_device_matches_host(sparse_tpm, tmp_path, monkeypatch):
+    """get_norm_counts on a dense count matrix: GPU gather+scale == host numpy path."""
+    import pandas as pd
+
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.utils.anndata_lite import AnnData
+
+    rs = np.random.default_rng(0)
+    X = rs.poisson(2.0, (800, 120)).astype(np.float32)
+    X[:, 7] = 3.0                                   # constant gene
+    counts = AnnData(X=X, obs=pd.DataFrame(index=[f"c{i}" for i in range(800)]),
+                     var=pd.DataFrame(index=[f"g{j}" for j in range(120)]))
+    tpm = AnnData(X=sp.csr_matrix(X) if sparse_tpm else X.copy(), obs=counts.obs, var=counts.var)
+    genes = [f"g{j}" for j in (5, 7, 90, 3, 44)]
+    obj = cNMF(output_dir=str(tmp_path), name="nc")
+    got = obj.get_norm_counts(counts, tpm, high_variance_genes_filter=genes)
+    monkeypatch.setenv("CNMF_DEVICE", "cpu")
+    ref = obj.get_norm_counts(counts, tpm, high_variance_genes_filter=genes)
+    assert list(got.var.index) == genes
+    np.testing.assert_allclose(got.X, ref.X, rtol=1e-12, atol=0, equal_nan=True)
