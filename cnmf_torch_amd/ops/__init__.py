@@ -63,6 +63,7 @@ def _stream_ptr(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+
 def _check_block_view(name: str, t: torch.Tensor, R: int, K: int, n: int):
     if t.dim() != 3 or tuple(t.shape) != (R, K, n):
         raise ValueError(f"{name}: expected shape {(R, K, n)}, got {tuple(t.shape)}")
