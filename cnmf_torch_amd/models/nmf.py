@@ -244,6 +244,14 @@ def init_factors(X: torch.Tensor, K: int, seeds, init: str = "random", comm=None
 
 
 # =============================================================================== state
+def _to_device(a: np.ndarray, dev: torch.device) -> torch.Tensor:
+    """int64 host index array -> device, without a synchronising pageable copy."""
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64))
+    if dev.type == "cuda":
+        return t.pin_memory().to(dev, non_blocking=True)
+    return t
+
+
 class _Batch:
     """Live replicate batch with an active-prefix layout.
 
@@ -274,28 +282,35 @@ class _Batch:
     def active_mask(self) -> torch.Tensor:
         return self.state["active"][:self.n_act]
 
-    def compact(self) -> None:
-        """Sync point: move still-active replicates to the front and shrink n_act."""
+    def compact(self, act_host: np.ndarray | None = None) -> None:
+        """Move still-active replicates to the front and shrink n_act.
+
+        ``act_host`` (bool per position) may be a STALE host copy of the active flags
+        (read one pass behind): flags only ever go 1 -> 0, so every position it marks
+        inactive really is finished, and positions that finished since stay in the
+        prefix with active = 0 (skipped by the solves) until the next compaction.  The
+        permutation is then applied in stream order with no host synchronisation."""
         n, K = self.n_act, self.K
-        act = self.state["active"][:n].cpu().numpy() != 0
-        keep = [p for p in range(n) if act[p]]
-        if len(keep) == n:
+        if act_host is None:
+            act_host = self.state["active"][:n].cpu().numpy() != 0
+        act = np.asarray(act_host[:n], dtype=bool)
+        keep = np.flatnonzero(act)
+        if keep.size == n:
             return
-        done = [p for p in range(n) if not act[p]]
-        perm = keep + done + list(range(n, self.R))
+        perm = np.concatenate([keep, np.flatnonzero(~act), np.arange(n, self.R)])
         dev = self.W.device
-        rows = torch.cat([torch.arange(p * K, (p + 1) * K) for p in perm]).to(dev)
+        rows = _to_device((perm[:, None] * K + np.arange(K)).reshape(-1), dev)
         self.HT = self.HT.index_select(0, rows)
         self.W = self.W.index_select(0, rows)
+        pidx = _to_device(perm, dev)
         if self.B is not None:
             self.B = self.B.index_select(0, rows)
-            self.A = self.A.index_select(0, torch.tensor(perm, device=self.A.device))
-        pidx = torch.tensor(perm, device=dev)
-        self.state = {k: v[pidx] for k, v in self.state.items()}
-        self.h_iters = self.h_iters[pidx]
-        self.w_iters = self.w_iters[pidx]
+            self.A = self.A.index_select(0, pidx)
+        self.state = {k: v.index_select(0, pidx) for k, v in self.state.items()}
+        self.h_iters = self.h_iters.index_select(0, pidx)
+        self.w_iters = self.w_iters.index_select(0, pidx)
         self.order = [self.order[p] for p in perm]
-        self.n_act = len(keep)
+        self.n_act = int(keep.size)
         self.layout_version += 1
 
     def set_err(self, err: torch.Tensor, pass_idx: int, tol: float, final: bool,
@@ -328,10 +343,10 @@ class _Batch:
         inv = np.argsort(np.asarray(self.order))
         K = self.K
         dev = self.W.device
-        rows = torch.cat([torch.arange(p * K, (p + 1) * K) for p in inv]).to(dev)
+        rows = _to_device((inv[:, None] * K + np.arange(K)).reshape(-1), dev)
         HT = self.HT.index_select(0, rows)
         W = self.W.index_select(0, rows)
-        idx = torch.tensor(inv, device=dev)
+        idx = _to_device(inv, dev)
         # one packed device->host copy instead of eight small synchronising ones
         keys = ("err", "n_pass", "converged")
         packed = torch.stack([self.state[k][idx].to(torch.float64) for k in keys] +
@@ -382,8 +397,8 @@ class _PassPipeline:
         if n_live == 0:                   # everything had finished one pass ago
             return False
         if n - n_live >= max(1, int(self.frac * n)):
-            torch.cuda.current_stream().synchronize()
-            st.compact()
+            # compact on the one-pass-stale flags, in stream order: no drain of the GPU
+            st.compact(pflags.numpy() != 0)
             self.pending = None
             return st.n_act > 0
         return True
@@ -691,10 +706,17 @@ class NMFBatchSolver:
                 else:
                     enqueue_pass(-1, final)
             else:
+                t_h = time.perf_counter()
                 enqueue_pass(-1, final)
+                if self.profile:
+                    self.timings.setdefault("host_pass", []).append(
+                        (n, time.perf_counter() - t_h))
             last_key = key
+            t_w = time.perf_counter()
             if not pipe.after_enqueue():
                 break
+            if self.profile:
+                self.timings.setdefault("wait_pass", []).append((n, time.perf_counter() - t_w))
         if graph is not None:
             torch.cuda.current_stream().synchronize()
 

@@ -13,7 +13,9 @@ extern "C" int cnmf_solve_max_k() { return 32; }
 
 extern "C" int cnmf_solve_max_threads(int K) { return 1024; }
 
-extern "C" int cnmf_solve_reg_max_cols(int K) { return 0; }
+extern "C" int cnmf_solve_reg_max_cols(int K) {
+  return K <= cnmf::kResidentMaxK ? 1024 * cnmf::res_max_cols(K) : 0;
+}
 
 extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx,
                                  const float* numer, long long n_rs, long long ldn,
@@ -48,14 +50,17 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   if (coop_split > 1 && nsplit > 1) return hipErrorInvalidValue;
   if (K < 1 || K > 32) return hipErrorInvalidValue;
   // variant: 0 auto, 1 streaming, 2 register-resident.  Resident needs every slice to
-  // fit one column group per thread; it then runs with just enough threads for that.
+  // fit U <= res_max_cols(K) columns per thread of a <= 1024-thread workgroup; it runs
+  // with the smallest such U and just enough threads for the slice.
   const int parts = nsplit > 1 ? nsplit : (coop_split > 1 ? coop_split : 1);
   const int per = (ncols + parts - 1) / parts;
-  const int t_res = ((per + 63) / 64) * 64;   // one column per thread
-  // MU keeps x_new[K] as well: it spills past K = 13 (HALS updates in place: 16)
-  const bool fits = t_res <= 1024 && K <= (algo == 0 ? 13 : cnmf::kResidentMaxK);
+  const int U = per <= 1024 ? 1 : (per + 1023) / 1024;
+  const bool fits = K <= cnmf::kResidentMaxK && U <= cnmf::res_max_cols(K);
   if (variant == 2 && !fits) return hipErrorInvalidValue;
-  if ((variant == 0 && fits) || variant == 2)
-    return cnmf::launch_solve_resident(K, algo, p, nblocks, t_res < 64 ? 64 : t_res, stream);
+  if ((variant == 0 && fits) || variant == 2) {
+    int t_res = (((per + U - 1) / U + 63) / 64) * 64;
+    if (t_res < 64) t_res = 64;
+    return cnmf::launch_solve_resident(K, U, algo, p, nblocks, t_res, stream);
+  }
   return cnmf::launch_solve_stream(K, algo, p, nblocks, threads, stream);
 }

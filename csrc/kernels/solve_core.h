@@ -38,9 +38,22 @@ namespace cnmf {
 template <int K>
 constexpr int solve_max_threads() { return 1024; }
 
+// Gram rows live in LDS padded to a multiple of 4 floats, so a row is read with KP/4
+// ds_read_b128 broadcasts (every lane the same address) instead of K ds_read_b32.
+__host__ __device__ constexpr int gram_pad(int K) { return (K + 3) & ~3; }
+
+// Register-resident variant with U columns per thread: x and x_new live in VGPRs, the
+// numerator is staged once in LDS (thread-major, odd row stride: conflict-free b32
+// reads).  U is capped where the 1024-thread (128-VGPR) instantiation still compiles
+// without spills (hipcc -Rpass-analysis=kernel-resource-usage, ROCm 7.2): U*K <= 33,
+// except K = 15 (U = 2 spills 20 VGPRs).
+__host__ __device__ constexpr int res_max_cols(int K) {
+  return K == 15 ? 1 : ((33 / K) < 1 ? 1 : ((33 / K) > 4 ? 4 : (33 / K)));
+}
+
 // Columns per thread per group: keep ~(2U+1)K live floats well under the 128-VGPR cap.
 __host__ __device__ constexpr int cols_per_group_rt(int K) {
-  return (20 / K) < 1 ? 1 : ((20 / K) > 4 ? 4 : (20 / K));
+  return (16 / K) < 1 ? 1 : ((16 / K) > 4 ? 4 : (16 / K));
 }
 template <int K>
 constexpr int cols_per_group() { return cols_per_group_rt(K); }
@@ -64,16 +77,18 @@ __device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, int vo
 // LDS Gram with it stops LICM from hoisting all K*K loop-invariant Gram reads into
 // registers (K*K VGPRs -> spills at K >= 7).  Every lane reads the same LDS word.
 typedef __attribute__((address_space(3))) float lds_float;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
 
 __device__ __forceinline__ const lds_float* opaque(const lds_float* p) {
   asm volatile("" : "+v"(p));
   return p;
 }
 
-template <int K, int U>
+template <int K, int U, bool HasN = true>
 struct ColGroup {
   float x[U][K];
-  float n[U][K];
+  float n[HasN ? U : 1][HasN ? K : 1];
   int vo[U];
   bool ok[U];
 };
@@ -156,26 +171,42 @@ __device__ __forceinline__ void coop_sum2(const SolveParams& p, int rep, int e, 
   __syncthreads();
 }
 
+// Row k of the padded LDS Gram into row[KP] (KP/4 broadcast b128 reads).
+#define CNMF_GRAM_ROW(GZ, k, row)                                                                 \
+  float row[KP];                                                                                  \
+  do {                                                                                            \
+    const lds_f32x4* rp_ = (const lds_f32x4*)((GZ) + (k) * KP);                                   \
+_Pragma("unroll")                                                                                    \
+    for (int q_ = 0; q_ < KP / 4; ++q_) {                                                         \
+      const f32x4 v_ = rp_[q_];                                                                   \
+      row[4 * q_] = v_.x; row[4 * q_ + 1] = v_.y; row[4 * q_ + 2] = v_.z; row[4 * q_ + 3] = v_.w; \
+    }                                                                                             \
+  } while (0)
+
 // Per-group pieces shared by the streaming and the register-resident paths.  They are
 // macros on purpose: as __forceinline__ functions taking the ColGroup by reference the
 // compiler inlines them too late to scalarise the group, and the K=20 kernel went from
-// 111 VGPRs / 0 spills to 128 VGPRs / 148 spills.  They expect K, U, ALGO, sG, l1, l2,
-// eps and the accumulators (q, l / d2, x2 / lin, quad) in scope.
+// 111 VGPRs / 0 spills to 128 VGPRs / 148 spills.  They expect K, KP, U, ALGO, sG, l1,
+// l2, eps and the accumulators (q, l / d2, x2 / lin, quad) in scope; NV(u, k) names the
+// numerator of column u, component k (a register of the group, or the LDS stage).
+// Objective / epilogue loop order: Gram row k is read once (KP/4 broadcast b128) and
+// used for all U columns.
 // Objective terms (x2, dropping the constant ||X||^2):
 //   f(x) = sum_j x_j^T Gram x_j - 2 numer_j . x_j + 2 l1 |x_j|_1 + l2 |x_j|^2
-#define CNMF_OBJECTIVE_GROUP(CG)                                                                  \
+#define CNMF_OBJECTIVE_GROUP(CG, NV)                                                              \
   do {                                                                                            \
   const lds_float* gz = opaque(sG);                                                               \
 _Pragma("unroll")                                                                                    \
-  for (int u = 0; u < U; ++u) {                                                                   \
+  for (int k = 0; k < K; ++k) {                                                                   \
+    CNMF_MEMBAR();                                                                                \
+    CNMF_GRAM_ROW(gz, k, row);                                                                    \
 _Pragma("unroll")                                                                                    \
-    for (int k = 0; k < K; ++k) {                                                                 \
-      CNMF_MEMBAR();                                                                              \
+    for (int u = 0; u < U; ++u) {                                                                 \
       float gx = 0.f;                                                                             \
 _Pragma("unroll")                                                                                    \
-      for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], (CG).x[u][kk], gx);                \
+      for (int kk = 0; kk < K; ++kk) gx = fmaf(row[kk], (CG).x[u][kk], gx);                       \
       q = fmaf((CG).x[u][k], gx + l2 * (CG).x[u][k], q);                                          \
-      l = fmaf((CG).x[u][k], (CG).n[u][k] - l1, l);                                               \
+      l = fmaf((CG).x[u][k], NV(u, k) - l1, l);                                                   \
     }                                                                                             \
   }                                                                                               \
   } while (0)
@@ -183,7 +214,9 @@ _Pragma("unroll")                                                               
 
 // One MU (Jacobi, row-wise) or HALS (Gauss-Seidel) sweep over the group's columns,
 // accumulating |dx|^2 and |x_old|^2.  Padded columns hold x = numer = 0 and stay 0.
-#define CNMF_UPDATE_GROUP(CG)                                                                     \
+// Column-outer: only one column's K new values are live at a time (U*K would spill the
+// resident variant); the Gram rows are re-read per column as b128 broadcasts.
+#define CNMF_UPDATE_GROUP(CG, NV)                                                                 \
   do {                                                                                            \
   const lds_float* gz = opaque(sG);                                                               \
 _Pragma("unroll")                                                                                    \
@@ -193,11 +226,12 @@ _Pragma("unroll")                                                               
 _Pragma("unroll")                                                                                    \
       for (int k = 0; k < K; ++k) {                                                               \
         CNMF_MEMBAR();                                                                            \
+        CNMF_GRAM_ROW(gz, k, row);                                                                \
         float den = 0.f;                                                                          \
 _Pragma("unroll")                                                                                    \
-        for (int kk = 0; kk < K; ++kk) den = fmaf(gz[k * K + kk], (CG).x[u][kk], den);            \
+        for (int kk = 0; kk < K; ++kk) den = fmaf(row[kk], (CG).x[u][kk], den);                   \
         den = fmaf(l2, (CG).x[u][k], den) + l1;                                                   \
-        xn[k] = (den < eps) ? 0.f : (CG).x[u][k] * ((CG).n[u][k] * __builtin_amdgcn_rcpf(den));   \
+        xn[k] = (den < eps) ? 0.f : (CG).x[u][k] * (NV(u, k) * __builtin_amdgcn_rcpf(den));       \
       }                                                                                           \
 _Pragma("unroll")                                                                                    \
       for (int k = 0; k < K; ++k) {                                                               \
@@ -210,13 +244,14 @@ _Pragma("unroll")                                                               
 _Pragma("unroll")                                                                                    \
       for (int k = 0; k < K; ++k) {                                                               \
         CNMF_MEMBAR();                                                                            \
+        CNMF_GRAM_ROW(gz, k, row);                                                                \
         float gx = 0.f;                                                                           \
 _Pragma("unroll")                                                                                    \
-        for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], (CG).x[u][kk], gx);              \
-        const float diag = gz[k * K + k] + l2;                                                    \
+        for (int kk = 0; kk < K; ++kk) gx = fmaf(row[kk], (CG).x[u][kk], gx);                     \
+        const float diag = row[k] + l2;                                                           \
         const float old = (CG).x[u][k];                                                           \
         float xn = old;                                                                           \
-        if (diag > eps) xn = fmaxf(old + ((CG).n[u][k] - l1 - gx - l2 * old) / diag, 0.f);        \
+        if (diag > eps) xn = fmaxf(old + (NV(u, k) - l1 - gx - l2 * old) / diag, 0.f);            \
         const float d = xn - old;                                                                 \
         d2 = fmaf(d, d, d2);                                                                      \
         x2 = fmaf(old, old, x2);                                                                  \
@@ -227,26 +262,34 @@ _Pragma("unroll")                                                               
   } while (0)
 
 
-#define CNMF_LINQUAD_GROUP(CG)                                                                    \
+#define CNMF_LINQUAD_GROUP(CG, NV)                                                                \
   do {                                                                                            \
   const lds_float* gz = opaque(sG);                                                               \
 _Pragma("unroll")                                                                                    \
-  for (int u = 0; u < U; ++u) {                                                                   \
+  for (int k = 0; k < K; ++k) {                                                                   \
+    CNMF_MEMBAR();                                                                                \
+    CNMF_GRAM_ROW(gz, k, row);                                                                    \
 _Pragma("unroll")                                                                                    \
-    for (int k = 0; k < K; ++k) {                                                                 \
-      CNMF_MEMBAR();                                                                              \
+    for (int u = 0; u < U; ++u) {                                                                 \
       float gx = 0.f;                                                                             \
 _Pragma("unroll")                                                                                    \
-      for (int kk = 0; kk < K; ++kk) gx = fmaf(gz[k * K + kk], (CG).x[u][kk], gx);                \
-      lin = fmaf((CG).n[u][k], (CG).x[u][k], lin);                                                \
+      for (int kk = 0; kk < K; ++kk) gx = fmaf(row[kk], (CG).x[u][kk], gx);                       \
+      lin = fmaf(NV(u, k), (CG).x[u][k], lin);                                                    \
       quad = fmaf((CG).x[u][k], gx, quad);                                                        \
     }                                                                                             \
   }                                                                                               \
   } while (0)
 
+// numerator accessors for the macros above
+#define CNMF_NREG_CG(u, k) (cg.n[u][k])
+#define CNMF_NREG_RG(u, k) (rg.n[u][k])
+// LDS numerator stage: thread-major rows of NS = (U*K)|1 words (odd stride: conflict-free
+// b32 reads; one base VGPR, per-(u,k) immediate offsets)
+#define CNMF_NLDS(u, k) (sNt[(u) * K + (k)])
 
-template <int K, int U>
-__device__ __forceinline__ void store_group(const ColGroup<K, U>& cg, __amdgpu_buffer_rsrc_t rx,
+
+template <int K, int U, bool HasN>
+__device__ __forceinline__ void store_group(const ColGroup<K, U, HasN>& cg, __amdgpu_buffer_rsrc_t rx,
                                             int sx) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -262,33 +305,42 @@ __device__ __forceinline__ float block_objective(__amdgpu_buffer_rsrc_t rx, int 
                                                  __amdgpu_buffer_rsrc_t rn, int sn,
                                                  const lds_float* sG, int j0, int n, float l1_num,
                                                  float l1, float l2, float* sred) {
+  constexpr int KP = gram_pad(K);
   float q = 0.f, l = 0.f;
   const int T = blockDim.x;
   for (int j = j0 + threadIdx.x; j < n; j += U * T) {
     CNMF_MEMBAR();
     ColGroup<K, U> cg;
     load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, l1_num);
-    CNMF_OBJECTIVE_GROUP(cg);
+    CNMF_OBJECTIVE_GROUP(cg, CNMF_NREG_CG);
   }
   block_sum2(q, l, sred);
   return q - 2.f * l;
 }
 
-// RES = 1: register-resident variant, launched only when every slice fits one column
-// group per thread (host check in cnmf_solve); RES = 0: streaming variant.
+// RES = 0: streaming variant (U = cols_per_group columns per thread per sweep, x and
+// numer re-read from L2 every iteration).  RES = U >= 1: register-resident variant, U
+// columns per thread: x in VGPRs for the whole solve, numerator staged once in LDS.
+// Launched only when every slice fits U columns per thread (host check in cnmf_solve).
 template <int K, int ALGO, int RES>
 __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
-  // resident: one column per thread (its x and numer live in VGPRs for the whole solve)
-  constexpr int U = RES ? 1 : cols_per_group<K>();
-  __shared__ float sGm[K * K];
+  constexpr int U = RES ? RES : cols_per_group<K>();
+  constexpr int KP = gram_pad(K);
+  constexpr bool resident = RES != 0;
+  __shared__ __attribute__((aligned(16))) float sGm[K * KP];
   __shared__ float sred[2 * 16];
+  constexpr int NS = (U * K) | 1;
+  __shared__ float sNm[resident ? NS * 1024 : 1];
   const lds_float* sG = (const lds_float*)sGm;  // LDS (addrspace 3): ds_read, 32-bit address
   const int rep = p.rep_index ? p.rep_index[blockIdx.x] : (int)blockIdx.x;
   if (p.active && p.active[rep] == 0) return;  // converged replicate: untouched (uniform)
   float* __restrict__ x = p.x + (long long)rep * p.x_rs;
   const float* __restrict__ nu = p.numer + (long long)rep * p.n_rs;
   const float* __restrict__ g = p.gram + (long long)rep * p.g_rs;
-  for (int i = threadIdx.x; i < K * K; i += blockDim.x) sGm[i] = g[i];
+  for (int i = threadIdx.x; i < K * KP; i += blockDim.x) {
+    const int r = i / KP, c = i - r * KP;
+    sGm[i] = c < K ? g[r * K + c] : 0.f;
+  }
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t rx = rsrc_of(x);
@@ -313,17 +365,35 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
   float f_prev = 0.f;
   bool have_prev = false;
   int it = 0;
-  // Register-resident path: the slice fits one column group per thread, so x and numer
-  // stay in VGPRs for every iteration (no per-iteration global round trip -- that
-  // latency, not arithmetic, bounded the streaming loop on small slices).
-  constexpr bool resident = RES != 0;
-  ColGroup<K, U> rg;
   if constexpr (resident) {
-    load_group<K, U>(rg, j0 + threadIdx.x, T, n, rx, sx, rn, sn, p.l1_num);
+    // Register-resident path: x stays in VGPRs for every iteration and the numerator in
+    // LDS (no per-iteration global round trip -- that latency/L2 traffic, not
+    // arithmetic, bounded the streaming loop).  Each thread reads back only the LDS
+    // words it wrote, so staging needs no barrier.
+    float* sNt = sNm + threadIdx.x * NS;
+    ColGroup<K, U, false> rg;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = j0 + threadIdx.x + u * T;
+      rg.ok[u] = c < n;
+      rg.vo[u] = rg.ok[u] ? c * 4 : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const float xv = buf_ld(rx, rg.vo[u], k * sx);
+        float nv = buf_ld(rn, rg.vo[u], k * sn);
+        rg.x[u][k] = rg.ok[u] ? xv : 0.f;
+        nv = rg.ok[u] ? nv : 0.f;
+        if (p.l1_num > 0.f) nv = fmaxf(nv - p.l1_num, 0.f);
+        CNMF_NLDS(u, k) = nv;
+      }
+    }
     while (true) {
       if (loss_conv && it % every == 0) {
         float q = 0.f, l = 0.f;
-        CNMF_OBJECTIVE_GROUP(rg);
+        CNMF_OBJECTIVE_GROUP(rg, CNMF_NLDS);
         block_sum2(q, l, sred);
         float f = q - 2.f * l;
         if (coop) {
@@ -336,7 +406,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
       }
       if (it >= p.max_iter) break;
       float d2 = 0.f, x2 = 0.f;
-      CNMF_UPDATE_GROUP(rg);
+      CNMF_UPDATE_GROUP(rg, CNMF_NLDS);
       ++it;
       if (!check_conv || loss_conv) continue;
       block_sum2(d2, x2, sred);
@@ -344,6 +414,28 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
       if (sqrtf(d2) / (sqrtf(x2) + eps) < p.tol) break;
     }
     store_group<K, U>(rg, rx, sx);
+    if (p.lin_out || p.quad_out) {
+      float lin = 0.f, quad = 0.f;
+      if (p.l1_num > 0.f) {
+        // epilogue uses the raw numerator (no l1 shift), as the streaming reload does
+        ColGroup<K, U> cg;
+        load_group<K, U>(cg, j0 + threadIdx.x, T, n, rx, sx, rn, sn, 0.f);
+        CNMF_LINQUAD_GROUP(cg, CNMF_NREG_CG);
+      } else {
+        CNMF_LINQUAD_GROUP(rg, CNMF_NLDS);
+      }
+      block_sum2(lin, quad, sred);
+      if (coop) coop_sum2(p, rep, epoch++, lin, quad, sred);
+      if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
+        if (check_conv) {
+          if (p.lin_out) p.lin_out[rep] = lin;
+          if (p.quad_out) p.quad_out[rep] = quad;
+        } else {  // split columns: caller zeroed the outputs
+          if (p.lin_out) atomicAdd(p.lin_out + rep, lin);
+          if (p.quad_out) atomicAdd(p.quad_out + rep, quad);
+        }
+      }
+    }
   } else {
     while (true) {
       if (loss_conv && it % every == 0) {
@@ -362,7 +454,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
         CNMF_MEMBAR();
         ColGroup<K, U> cg;
         load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, p.l1_num);
-        CNMF_UPDATE_GROUP(cg);
+        CNMF_UPDATE_GROUP(cg, CNMF_NREG_CG);
         store_group<K, U>(cg, rx, sx);
       }
       ++it;
@@ -371,36 +463,24 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
       if (coop) coop_sum2(p, rep, epoch++, d2, x2, sred);
       if (sqrtf(d2) / (sqrtf(x2) + eps) < p.tol) break;
     }
-  }
-
-  if (p.lin_out || p.quad_out) {
-    float lin = 0.f, quad = 0.f;
-    if constexpr (resident) {
-      // epilogue uses the raw numerator (no l1 shift), as the streaming reload does
-      if (p.l1_num > 0.f) {
-        ColGroup<K, U> cg;
-        load_group<K, U>(cg, j0 + threadIdx.x, T, n, rx, sx, rn, sn, 0.f);
-        CNMF_LINQUAD_GROUP(cg);
-      } else {
-        CNMF_LINQUAD_GROUP(rg);
-      }
-    } else {
+    if (p.lin_out || p.quad_out) {
+      float lin = 0.f, quad = 0.f;
       for (int j = j0 + threadIdx.x; j < n; j += U * T) {
         CNMF_MEMBAR();
         ColGroup<K, U> cg;
         load_group<K, U>(cg, j, T, n, rx, sx, rn, sn, 0.f);
-        CNMF_LINQUAD_GROUP(cg);
+        CNMF_LINQUAD_GROUP(cg, CNMF_NREG_CG);
       }
-    }
-    block_sum2(lin, quad, sred);
-    if (coop) coop_sum2(p, rep, epoch++, lin, quad, sred);
-    if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
-      if (check_conv) {
-        if (p.lin_out) p.lin_out[rep] = lin;
-        if (p.quad_out) p.quad_out[rep] = quad;
-      } else {  // split columns: caller zeroed the outputs
-        if (p.lin_out) atomicAdd(p.lin_out + rep, lin);
-        if (p.quad_out) atomicAdd(p.quad_out + rep, quad);
+      block_sum2(lin, quad, sred);
+      if (coop) coop_sum2(p, rep, epoch++, lin, quad, sred);
+      if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
+        if (check_conv) {
+          if (p.lin_out) p.lin_out[rep] = lin;
+          if (p.quad_out) p.quad_out[rep] = quad;
+        } else {  // split columns: caller zeroed the outputs
+          if (p.lin_out) atomicAdd(p.lin_out + rep, lin);
+          if (p.quad_out) atomicAdd(p.quad_out + rep, quad);
+        }
       }
     }
   }
@@ -457,14 +537,47 @@ hipError_t launch_solve_k(int algo, const SolveParams& p, int nblocks, int threa
     default: return hipErrorInvalidValue;                                                 \
   }
 
-// register-resident variant: K <= kResidentMaxK (one column per thread; beyond that the
-// live x / numer / x_new set of a column no longer fits 128 VGPRs without spilling)
+// register-resident variant: K <= kResidentMaxK, U <= res_max_cols(K) columns per thread
 constexpr int kResidentMaxK = 16;
 
-// one per translation unit (solve.hip / solve_res.hip compile in parallel)
+// Resident launch for U columns per thread: instantiated only where U <= res_max_cols(K).
+template <int K, int U>
+hipError_t launch_solve_res_ku(int algo, const SolveParams& p, int nblocks, int threads,
+                               hipStream_t s) {
+  if constexpr (U > res_max_cols(K) || K > kResidentMaxK) {
+    return hipErrorInvalidValue;
+  } else {
+    return launch_solve_k<K, U>(algo, p, nblocks, threads, s);
+  }
+}
+
+#define CNMF_SOLVE_RES_SWITCH(U)                                                          \
+  switch (K) {                                                                            \
+    case 1: return launch_solve_res_ku<1, U>(algo, p, nblocks, threads, s);               \
+    case 2: return launch_solve_res_ku<2, U>(algo, p, nblocks, threads, s);               \
+    case 3: return launch_solve_res_ku<3, U>(algo, p, nblocks, threads, s);               \
+    case 4: return launch_solve_res_ku<4, U>(algo, p, nblocks, threads, s);               \
+    case 5: return launch_solve_res_ku<5, U>(algo, p, nblocks, threads, s);               \
+    case 6: return launch_solve_res_ku<6, U>(algo, p, nblocks, threads, s);               \
+    case 7: return launch_solve_res_ku<7, U>(algo, p, nblocks, threads, s);               \
+    case 8: return launch_solve_res_ku<8, U>(algo, p, nblocks, threads, s);               \
+    case 9: return launch_solve_res_ku<9, U>(algo, p, nblocks, threads, s);               \
+    case 10: return launch_solve_res_ku<10, U>(algo, p, nblocks, threads, s);             \
+    case 11: return launch_solve_res_ku<11, U>(algo, p, nblocks, threads, s);             \
+    case 12: return launch_solve_res_ku<12, U>(algo, p, nblocks, threads, s);             \
+    case 13: return launch_solve_res_ku<13, U>(algo, p, nblocks, threads, s);             \
+    case 14: return launch_solve_res_ku<14, U>(algo, p, nblocks, threads, s);             \
+    case 15: return launch_solve_res_ku<15, U>(algo, p, nblocks, threads, s);             \
+    case 16: return launch_solve_res_ku<16, U>(algo, p, nblocks, threads, s);             \
+    default: return hipErrorInvalidValue;                                                 \
+  }
+
+// one per translation unit (solve.hip / solve_res.hip / solve_res34.hip build in parallel)
 hipError_t launch_solve_stream(int K, int algo, const SolveParams& p, int nblocks, int threads,
                                hipStream_t s);
-hipError_t launch_solve_resident(int K, int algo, const SolveParams& p, int nblocks,
+hipError_t launch_solve_resident(int K, int U, int algo, const SolveParams& p, int nblocks,
                                  int threads, hipStream_t s);
+hipError_t launch_solve_resident34(int K, int U, int algo, const SolveParams& p, int nblocks,
+                                   int threads, hipStream_t s);
 
 }  // namespace cnmf

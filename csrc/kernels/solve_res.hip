@@ -1,28 +1,12 @@
-// Register-resident instantiations of the fused inner solve (see solve_core.h):
-// compiled as a separate unit so the two variant sets build in parallel.
+// Register-resident instantiations of the fused inner solve (see solve_core.h), U = 1..2
+// columns per thread; U = 3..4 live in solve_res34.hip so the sets build in parallel.
 #include "solve_core.h"
 
 namespace cnmf {
-hipError_t launch_solve_resident(int K, int algo, const SolveParams& p, int nblocks,
+hipError_t launch_solve_resident(int K, int U, int algo, const SolveParams& p, int nblocks,
                                  int threads, hipStream_t s) {
-  switch (K) {
-    case 1: return launch_solve_k<1, 1>(algo, p, nblocks, threads, s);
-    case 2: return launch_solve_k<2, 1>(algo, p, nblocks, threads, s);
-    case 3: return launch_solve_k<3, 1>(algo, p, nblocks, threads, s);
-    case 4: return launch_solve_k<4, 1>(algo, p, nblocks, threads, s);
-    case 5: return launch_solve_k<5, 1>(algo, p, nblocks, threads, s);
-    case 6: return launch_solve_k<6, 1>(algo, p, nblocks, threads, s);
-    case 7: return launch_solve_k<7, 1>(algo, p, nblocks, threads, s);
-    case 8: return launch_solve_k<8, 1>(algo, p, nblocks, threads, s);
-    case 9: return launch_solve_k<9, 1>(algo, p, nblocks, threads, s);
-    case 10: return launch_solve_k<10, 1>(algo, p, nblocks, threads, s);
-    case 11: return launch_solve_k<11, 1>(algo, p, nblocks, threads, s);
-    case 12: return launch_solve_k<12, 1>(algo, p, nblocks, threads, s);
-    case 13: return launch_solve_k<13, 1>(algo, p, nblocks, threads, s);
-    case 14: return launch_solve_k<14, 1>(algo, p, nblocks, threads, s);
-    case 15: return launch_solve_k<15, 1>(algo, p, nblocks, threads, s);
-    case 16: return launch_solve_k<16, 1>(algo, p, nblocks, threads, s);
-    default: return hipErrorInvalidValue;   // K > kResidentMaxK: streaming only
-  }
+  if (U == 1) { CNMF_SOLVE_RES_SWITCH(1) }
+  if (U == 2) { CNMF_SOLVE_RES_SWITCH(2) }
+  return launch_solve_resident34(K, U, algo, p, nblocks, threads, s);
 }
 }  // namespace cnmf
