@@ -797,11 +797,46 @@ class NMFBatchSolver:
             delta = torch.where(mask, delta, torch.ones_like(delta))
         x3.mul_(delta)
 
-    def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, tol=None, iters=None):
+    def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, tol=None, iters=None,
+                       den_vec=None):
         """One fused MU step of the usages H3c (R, K, c) in place against W3 on rows xc;
         with ``tol`` the per-replicate inner stopping rule runs on device (clears act)."""
         ops.beta_update_h(xc, H3c, W3, self.beta, self.opts.eps, l1, l2, self._beta_gamma(),
-                          act=act, tol=tol, iters=iters)
+                          act=act, tol=tol, iters=iters, den_vec=den_vec)
+
+    def _beta_h_solve(self, xc, hc, W3, act, iters, block: int = 8) -> None:
+        """Inner usage loop of one chunk: up to ``online_chunk_max_iter`` fused MU steps,
+        each replicate stopping on device at ``online_h_tol`` (clears its ``act`` flag).
+        Steps are enqueued in blocks; whether anybody is still active is read from a
+        pinned copy one block late, so the GPU always has a block queued and the host
+        never drains the stream (launches for finished replicates exit at once)."""
+        o = self.opts
+        W3 = W3.contiguous() if W3.stride(-1) != 1 else W3
+        den_vec = (W3.sum(dim=2, dtype=torch.float32).contiguous()
+                   if self.beta == 1.0 and xc.device.type == "cuda" else None)
+        max_it = int(o.online_chunk_max_iter)
+        cuda = xc.device.type == "cuda"
+        pending = None
+        it = 0
+        while it < max_it:
+            m = min(block, max_it - it)
+            for _ in range(m):
+                self._beta_h_update(xc, hc, W3, o.l1_H, o.l2_H, act, o.online_h_tol, iters,
+                                    den_vec)
+            it += m
+            if not cuda:
+                if int(act.sum()) == 0:
+                    break
+                continue
+            flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            flag.copy_(act.max().view(1), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            prev, pending = pending, (ev, flag)
+            if prev is not None:
+                prev[0].synchronize()
+                if int(prev[1][0]) == 0:
+                    break
 
     def _beta_w_stats(self, xc, H3c, W3):
         """(num, den) W-side MU statistics of rows xc (den broadcastable to (R,K,G))."""
@@ -810,19 +845,33 @@ class NMFBatchSolver:
             den = H3c.sum(dim=2, keepdim=True)              # KL: row sums of H
         return num, den
 
+    def _loss_dev(self, HT: torch.Tensor, W: torch.Tensor, K: int) -> torch.Tensor:
+        """sqrt(2 * D_beta(X || H W)) per replicate (beta != 2) as a float64 DEVICE tensor
+        (no host round trip; all-reduced under DP)."""
+        R = W.shape[0] // K
+        N, G = self.X.shape
+        _, _, tot = ops.beta_contract("h", self.X, HT.view(R, K, N), W.view(R, K, G), self.beta,
+                                      self.opts.eps, want_num=False, want_loss=True)
+        tot = tot.to(torch.float64).contiguous()
+        self.comm.allreduce_(tot)
+        return torch.sqrt(torch.clamp(2.0 * tot, min=0.0))
+
     def _online_beta(self, st: _Batch) -> None:
         """Online beta-MU (nmf-torch mode='online', beta != 2): per chunk, the usages are
         iterated to ``online_h_tol`` (relative change, per replicate, on device), then the
         W-side statistics of the chunk are accumulated (all-reduced under DP) and W takes
-        one MU step with the running pass statistics."""
+        one MU step with the running pass statistics.  The pass loss and the stop rule
+        stay on the device; the host reads the active flags one pass late through the
+        same speculative pass pipeline as the Frobenius path."""
         o, comm = self.opts, self.comm
         K = st.K
         X = self.X
         N, G = X.shape
         steps = self._steps(N)
         self._init_err(st)
-        max_it = int(o.online_chunk_max_iter)
-        for p in range(int(o.online_max_pass)):
+        pipe = _PassPipeline(st)
+        max_pass = int(o.online_max_pass)
+        for p in range(max_pass):
             n = st.n_act
             if n == 0:
                 break
@@ -842,11 +891,7 @@ class NMFBatchSolver:
                     xc = X[a:b]
                     hc = H3[:, :, a:b]
                     act = live.clone()
-                    for it in range(max_it):
-                        self._beta_h_update(xc, hc, W3, o.l1_H, o.l2_H, act, o.online_h_tol,
-                                            st.h_iters[:n])
-                        if (it + 1) % 8 == 0 and int(act.sum()) == 0:
-                            break
+                    self._beta_h_solve(xc, hc, W3, act, st.h_iters[:n])
                     nW, dW = self._beta_w_stats(xc, hc, W3)
                     fnum += nW
                     fden += dW
@@ -856,8 +901,10 @@ class NMFBatchSolver:
                 self._mu_apply(W3, num_acc, den_acc, o.l1_W, o.l2_W,
                                (live != 0).view(n, 1, 1))
                 st.w_iters[:n] += live
-            err = self.loss(HT, W, K).to(torch.float64)
-            self._check_convergence(st, err, p + 1, final=(p + 1 == int(o.online_max_pass)))
+            final = p + 1 == max_pass
+            st.set_err(self._loss_dev(HT, W, K), p + 1, o.tol, final)
+            if not pipe.after_enqueue():
+                break
 
     def _batch_beta(self, st: _Batch) -> None:
         """Batch beta-MU (sklearn _fit_multiplicative_update order: usages, then spectra);
@@ -868,6 +915,7 @@ class NMFBatchSolver:
         X = self.X
         N, G = X.shape
         self._init_err(st)
+        pipe = _PassPipeline(st)
         for it in range(int(o.batch_max_iter)):
             n = st.n_act
             if n == 0:
@@ -875,19 +923,24 @@ class NMFBatchSolver:
             HT, W = st.views()
             W3 = W.view(n, K, G)
             H3 = HT.view(n, K, N)
-            self._beta_h_update(X, H3, W3, o.l1_H, o.l2_H)
+            # finished replicates may sit in the batch until the next (stale-flag)
+            # compaction: the active flags gate both updates and the iteration counts
+            live = st.active_mask().clone()
+            self._beta_h_update(X, H3, W3, o.l1_H, o.l2_H, act=live)
             nW, dW = self._beta_w_stats(X, H3, W3)
             if comm.is_distributed:
                 flat = torch.cat([nW.reshape(-1), dW.expand(n, K, G).reshape(-1)])
                 comm.allreduce_(flat)
                 nW = flat[:n * K * G].view(n, K, G)
                 dW = flat[n * K * G:].view(n, K, G)
-            self._mu_apply(W3, nW, dW, o.l1_W, o.l2_W)
-            st.h_iters[:n] += 1
-            st.w_iters[:n] += 1
+            self._mu_apply(W3, nW, dW, o.l1_W, o.l2_W, (live != 0).view(n, 1, 1))
+            st.h_iters[:n] += live
+            st.w_iters[:n] += live
             if (it + 1) % max(1, int(o.loss_every)) == 0 or it + 1 == int(o.batch_max_iter):
-                err = self.loss(HT, W, K)
-                self._check_convergence(st, err, it + 1, final=(it + 1 == int(o.batch_max_iter)))
+                st.set_err(self._loss_dev(HT, W, K), it + 1, o.tol,
+                           final=(it + 1 == int(o.batch_max_iter)))
+                if not pipe.after_enqueue():
+                    break
 
 
 def _as(t: torch.Tensor, dt: torch.dtype) -> torch.Tensor:

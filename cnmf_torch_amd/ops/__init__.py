@@ -336,13 +336,15 @@ _BETA_WS: dict = {}
 def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float, eps: float,
                   l1: float = 0.0, l2: float = 0.0, gamma: float = 1.0,
                   act: torch.Tensor | None = None, tol: float | None = None,
-                  iters: torch.Tensor | None = None) -> None:
+                  iters: torch.Tensor | None = None,
+                  den_vec: torch.Tensor | None = None) -> None:
     """One fused in-place beta-MU step of the usages: HT3 *= (num/(den+l1+l2 HT3))^gamma
     with num/den from the H-side contraction -- the numerator never leaves registers.
 
     ``act`` (int32 (R,), optional) gates replicates; with ``tol`` the kernel also applies
     the inner stopping rule on device: act[r] = 0 once ||dh||/(||h||+eps) < tol, and
-    iters[r] += 1 for every replicate that stepped."""
+    iters[r] += 1 for every replicate that stepped.  ``den_vec`` (KL only): the row sums
+    of W3 as contiguous float32 (R, K) -- pass it when W3 is fixed across many steps."""
     R, K, N = HT3.shape
     G = W3.shape[2]
     if not use_native(HT3) or HT3.dtype != torch.float32 or K > _hip.beta_max_k():
@@ -359,9 +361,13 @@ def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: fl
         raise ValueError("the inner stopping rule needs an act array")
     mode = beta_mode(beta)
     dev = HT3.device
-    den_vec = W3.sum(dim=2).contiguous() if mode == 0 else None
-    if den_vec is not None and den_vec.dtype != torch.float32:
-        den_vec = den_vec.float()
+    if mode != 0:
+        den_vec = None
+    elif den_vec is None:
+        den_vec = W3.sum(dim=2, dtype=torch.float32).contiguous()
+    elif (den_vec.shape != (R, K) or den_vec.dtype != torch.float32
+          or not den_vec.is_contiguous() or den_vec.device != dev):
+        raise ValueError("den_vec: contiguous float32 (R, K) on the device required")
     n_strips = (N + 63) // 64
     part = counter = None
     if tol is not None:

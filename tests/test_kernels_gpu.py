@@ -396,6 +396,51 @@ def test_solve_register_resident_variant(algo, K, conv_mode):
     assert torch.equal(xg.cpu(), outs[("reg", -1.0)][0])
 
 
+@pytest.mark.parametrize("algo", ["mu", "hals"])
+@pytest.mark.parametrize("K,n", [(3, 3900), (8, 4000), (10, 2600), (11, 3000), (12, 2048)])
+def test_solve_resident_multi_column(algo, K, n):
+    """Resident variant with U = ceil(n / 1024) columns per thread (numerator staged in
+    LDS) == streaming variant bit for bit on fixed steps, == fp64 reference; with the
+    loss stopping rule the two agree to fp32 summation order."""
+    R = 3
+    x0, numer, gram = _problem(R, K, n, seed=K + 101)
+    dev = torch.device("cuda")
+    outs = {}
+    for variant in ("stream", "reg"):
+        xg = x0.clone().to(dev)
+        ops.solve(algo, xg, numer.to(dev), gram.to(dev), max_iter=7, tol=-1.0, conv_mode=0,
+                  variant=variant, coop=1)
+        outs[variant] = xg.cpu()
+    assert torch.equal(outs["reg"], outs["stream"])
+    xr = x0.clone().double()
+    reference.solve(ops.ALGOS[algo], xr, numer.double(), gram.double(), None, 7, -1.0,
+                    0.0, 0.0, 0.0, 1e-16, None, None, None, 1, 0, 5)
+    torch.testing.assert_close(outs["reg"].double(), xr, rtol=2e-4, atol=1e-4)
+    res = {}
+    for variant in ("stream", "reg"):
+        xg = x0.clone().to(dev)
+        lin = torch.zeros(R, device=dev)
+        quad = torch.zeros(R, device=dev)
+        ops.solve(algo, xg, numer.to(dev), gram.to(dev), max_iter=200, tol=1e-4, conv_mode=1,
+                  check_every=5, lin_out=lin, quad_out=quad, variant=variant, coop=1)
+        res[variant] = (xg.cpu(), lin.cpu(), quad.cpu())
+    a, b = res["reg"], res["stream"]
+    assert ((a[0] - b[0]).norm() / b[0].norm()) < 2e-3
+    torch.testing.assert_close(a[1], b[1], rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(a[2], b[2], rtol=1e-3, atol=1e-3)
+
+
+def test_solve_resident_rejects_oversized_slice():
+    """A slice wider than res_max_cols(K) * 1024 columns cannot run resident."""
+    K, n = 12, 4000                                   # U would be 4 > res_max_cols(12) = 2
+    x0, numer, gram = _problem(1, K, n, seed=1)
+    with pytest.raises(RuntimeError):
+        ops.solve("mu", x0.cuda(), numer.cuda(), gram.cuda(), max_iter=2, variant="reg",
+                  coop=1)
+    assert ops._hip.solve_reg_max_cols(12) == 2048
+    assert ops._hip.solve_reg_max_cols(10) == 3072
+
+
 def test_online_pass_graph_replay_matches_eager(monkeypatch):
     """Passes replayed from a captured HIP graph == eagerly launched passes, bit for bit."""
     from cnmf_torch_amd.models.nmf import run_nmf_batch
