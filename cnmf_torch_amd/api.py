@@ -45,6 +45,7 @@ from .utils.anndata_lite import AnnData
 from .utils.h5ad import read_h5ad, write_h5ad
 from .utils.io import (check_dir_exists, dump_yaml, load_df_from_npz, load_yaml, read_10x_mtx,
                        read_any, read_counts_table, save_df_to_npz, save_df_to_text,
+                       NPZ_TMP_LEVEL,
                        write_text_atomic)
 from .utils.log import get_logger
 from .utils.timing import StageTimer, append_jsonl, read_jsonl
@@ -152,6 +153,16 @@ def _norm_counts_dense_device(counts, genes, guard_zero_std: bool, dev) -> AnnDa
                   obsm=dict(counts.obsm), uns=dict(counts.uns))
     out.uns["_scaled_on_device"] = True
     return out
+
+
+def _load_npz_arrays(fn: str):
+    """(data, index, columns) arrays of a .df.npz without building a DataFrame."""
+    try:
+        with np.load(fn, allow_pickle=False) as f:
+            return f["data"], f["index"], f["columns"]
+    except ValueError:
+        df = load_df_from_npz(fn)          # object arrays from the original cnmf
+        return df.values, df.index.values, df.columns.values
 
 
 def _dense32(X) -> np.ndarray:
@@ -405,7 +416,7 @@ class cNMF:
             manifest = self.paths["replicate_manifest"]
 
             def _write_spectra(df, path, k_, it_):
-                save_df_to_npz(df, path)
+                save_df_to_npz(df, path, level=NPZ_TMP_LEVEL)
                 append_jsonl(manifest, {"k": k_, "iter": it_, "file": os.path.basename(path),
                                         "sha256": _sha256(path), "bytes": os.path.getsize(path)})
 
@@ -532,14 +543,19 @@ class cNMF:
                 continue
             present.append((int(p["iter"]), fn))
         with cf.ThreadPoolExecutor(max_workers=8) as ex:   # zlib inflate drops the GIL
-            loaded = list(ex.map(lambda t: load_df_from_npz(t[1]), present))
-        parts = []
-        for (it, _), spectra in zip(present, loaded):
-            spectra.index = ["iter%d_topic%d" % (it, t + 1) for t in range(k)]
-            parts.append(spectra)
-        if parts:
-            combined = pd.concat(parts, axis=0)
-            save_df_to_npz(combined, self.paths["merged_spectra"] % k)
+            loaded = list(ex.map(lambda t: _load_npz_arrays(t[1]), present))
+        if loaded:
+            # one concatenated array instead of one DataFrame per replicate (pd.concat of
+            # 100 frames with 2k string columns was the cost of this stage); every
+            # replicate must carry the same gene columns
+            cols = loaded[0][2]
+            for (_, fn), (_, _, c) in zip(present, loaded):
+                if c.shape != cols.shape or not np.array_equal(c, cols):
+                    raise ValueError(f"{fn}: gene columns differ from the other replicates")
+            index = ["iter%d_topic%d" % (it, t + 1) for it, _ in present for t in range(k)]
+            combined = pd.DataFrame(np.concatenate([d for d, _, _ in loaded], axis=0),
+                                    index=index, columns=cols)
+            save_df_to_npz(combined, self.paths["merged_spectra"] % k, level=NPZ_TMP_LEVEL)
             if remove_individual_iterations:
                 for _, p in sub.iterrows():
                     fn = self.paths["iter_spectra"] % (int(p["n_components"]), int(p["iter"]))
@@ -547,7 +563,7 @@ class cNMF:
                         os.remove(fn)
             return combined
         print("No spectra found for k=%d" % k)
-        return parts
+        return []
 
     # ------------------------------------------------------------------ refits
     def _refit_kwargs(self):
@@ -710,7 +726,10 @@ class cNMF:
             clustergram(topics_dist.cpu().numpy(), label_series, local_dens, density_filter,
                         density_threshold, p["clustering_plot"] % (k, dt_repl), close=close_fig)
         if build_ref:
-            self.build_reference(k, density_threshold)
+            # the reference re-reads the TSV it just wrote (cnmf.py:1273); float64 text is
+            # an exact round trip, so the in-memory frame gives the same reference
+            mem = spectra_tpm if (spectra_tpm.dtypes == np.float64).all() else None
+            self.build_reference(k, density_threshold, _spectra_tpm=mem)
 
     def _load_density_cache(self, cache: str, n_neighbors: int, names):
         """Density cache keyed on K AND the neighbourhood (SURVEY.md §5.2 fix): a cache
@@ -747,11 +766,15 @@ class cNMF:
         return x_sq - 2.0 * cross + quad
 
     # ------------------------------------------------------------------ reference / k-sel
-    def build_reference(self, k, density_threshold=0.5, target_sum=1e6):
+    def build_reference(self, k, density_threshold=0.5, target_sum=1e6, _spectra_tpm=None):
         """starCAT reference spectra (cnmf.py:1259-1290)."""
         dt = _dt_str(density_threshold)
-        spectra_tpm = pd.read_csv(self.paths["gene_spectra_tpm__txt"] % (k, dt), index_col=0,
-                                  sep="\t")
+        if _spectra_tpm is not None:
+            spectra_tpm = _spectra_tpm.copy()
+            spectra_tpm.columns = spectra_tpm.columns.astype(str)
+        else:
+            spectra_tpm = pd.read_csv(self.paths["gene_spectra_tpm__txt"] % (k, dt),
+                                      index_col=0, sep="\t")
         with open(self.paths["nmf_genes_list"]) as fh:
             hvgs = fh.read().split("\n")
         tpm_stats = load_df_from_npz(self.paths["tpm_stats"])

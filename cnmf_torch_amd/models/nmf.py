@@ -41,6 +41,7 @@ from __future__ import annotations
 import math
 import os
 import time
+import weakref
 from dataclasses import dataclass, field, asdict
 
 import numpy as np
@@ -404,14 +405,28 @@ class _PassPipeline:
         return True
 
 
+_SQ_NORM_CACHE: dict = {}
+
+
 def _sq_norm(X: torch.Tensor, rows: int = 1 << 16) -> float:
     """||X||_F^2 accumulated in float64 over row blocks (no full float64 copy of X:
-    a 10M x 5k matrix would need 400 GB)."""
+    a 10M x 5k matrix would need 400 GB).  Memoised per tensor storage and version
+    (factorize builds one solver per K over the same resident X); an in-place
+    modification of X bumps its version and invalidates the entry, and a weak reference
+    guards against a new tensor reusing a freed address."""
+    key = (id(X), X.data_ptr(), tuple(X.shape), tuple(X.stride()), X.dtype, X._version)
+    hit = _SQ_NORM_CACHE.get(key)
+    if hit is not None and hit[0]() is X:      # same live tensor object, same contents
+        return hit[1]
     tot = torch.zeros((), dtype=torch.float64, device=X.device)
     for a in range(0, X.shape[0], rows):
         xb = X[a:a + rows]
-        tot += torch.linalg.vector_norm(xb, dtype=torch.float64) ** 2
-    return float(tot)
+        tot += torch.linalg.vector_norm(xb, dtype=torch.float64).square()
+    val = float(tot)
+    if len(_SQ_NORM_CACHE) > 16:
+        _SQ_NORM_CACHE.clear()
+    _SQ_NORM_CACHE[key] = (weakref.ref(X), val)
+    return val
 
 
 def _graphs_enabled(X: torch.Tensor) -> bool:

@@ -80,28 +80,36 @@ def _plain_values(df: pd.DataFrame) -> np.ndarray:
 
 
 NPZ_COMPRESSLEVEL = int(os.environ.get("CNMF_NPZ_LEVEL", "1"))
+# Intermediate files under cnmf_tmp/ that only this pipeline re-reads (per-replicate and
+# merged spectra): stored uncompressed by default -- float64 spectra barely deflate and
+# zlib dominated combine.  Still a standard .npz that np.load reads.
+NPZ_TMP_LEVEL = int(os.environ.get("CNMF_NPZ_TMP_LEVEL", "0"))
 
 
 def _savez_deflate(path: str, arrays: dict, level: int) -> None:
     """np.savez_compressed with a selectable zlib level (numpy hard-codes the default,
     ~4x slower than level 1 on spectra-sized float arrays).  Same member names
-    (``<key>.npy``) and ZIP_DEFLATED format, so np.load / the reference read it."""
+    (``<key>.npy``) and ZIP_DEFLATED format, so np.load / the reference read it.
+    ``level`` 0 stores the members uncompressed (ZIP_STORED, as np.savez)."""
     import zipfile
 
-    with zipfile.ZipFile(path, mode="w", compression=zipfile.ZIP_DEFLATED,
-                         compresslevel=level, allowZip64=True) as zf:
+    comp = zipfile.ZIP_DEFLATED if level > 0 else zipfile.ZIP_STORED
+    with zipfile.ZipFile(path, mode="w", compression=comp,
+                         compresslevel=level if level > 0 else None, allowZip64=True) as zf:
         for key, arr in arrays.items():
             with zf.open(key + ".npy", "w", force_zip64=True) as fh:
                 np.lib.format.write_array(fh, np.asanyarray(arr), allow_pickle=False)
 
 
-def save_df_to_npz(obj: pd.DataFrame, filename: str) -> None:
-    """Compressed npz with keys data / index / columns -- the cnmf.py:32-33 contract."""
+def save_df_to_npz(obj: pd.DataFrame, filename: str, level: int | None = None) -> None:
+    """Compressed npz with keys data / index / columns -- the cnmf.py:32-33 contract.
+    ``level``: zlib level (default NPZ_COMPRESSLEVEL; 0 = stored, for intermediates)."""
     filename = str(filename)
     with atomic_path(filename, suffix=".npz") as tmp:
         _savez_deflate(tmp, {"data": _plain_values(obj),
                              "index": _plain_array(obj.index.values),
-                             "columns": _plain_array(obj.columns.values)}, NPZ_COMPRESSLEVEL)
+                             "columns": _plain_array(obj.columns.values)},
+                       NPZ_COMPRESSLEVEL if level is None else int(level))
 
 
 def load_df_from_npz(filename: str, allow_pickle_fallback: bool = True) -> pd.DataFrame:

@@ -77,6 +77,12 @@ def test_consensus_artifacts_and_recovery(run_dir, counts_file):
     assert sims[r, c].min() > 0.9, sims[r, c]
     starcat = load_df_from_npz(p["starcat_spectra"] % (5, dt))
     assert list(starcat.index) == [f"GEP{i}" for i in range(1, 6)]
+    # consensus builds the reference from the in-memory TPM spectra; the standalone call
+    # re-reads the TSV as the reference does (cnmf.py:1273): identical bits
+    obj.build_reference(5, 0.5)
+    again = load_df_from_npz(p["starcat_spectra"] % (5, dt))
+    assert again.equals(starcat)
+    assert list(again.columns) == list(starcat.columns)
 
 
 def test_k_selection(run_dir):
