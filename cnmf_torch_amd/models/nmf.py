@@ -642,8 +642,10 @@ class NMFBatchSolver:
                     A_, B_ = st.A[:n], st.B[:n * K]
                 else:
                     A_, B_ = A, B
-                    A_.zero_()
-                    B_.zero_()
+                    if dist:        # single process: the pass's first chunk overwrites
+                        A_.zero_()
+                        B_.zero_()
+                pass_first = True
                 active = st.active_mask()
                 h_it = st.h_iters[:n]
                 w_it = st.w_iters[:n]
@@ -681,11 +683,15 @@ class NMFBatchSolver:
                             if dist and first:
                                 torch.mm(HT[:, a:b], xc, out=accB)       # (n*K, G) GEMM
                                 ops.gram(hview, out=accA)
+                            elif not dist and pass_first:
+                                torch.mm(HT[:, a:b], xc, out=accB)       # B = h^T x
+                                ops.gram(hview, out=accA, active=active)  # A = h^T h
                             else:
                                 accB.addmm_(HT[:, a:b], xc)              # B += h^T x
                                 ops.gram(hview, out=accA, accumulate=True,   # A += h^T h
                                          active=active)
                         first = False
+                        pass_first = False
                     if dist:
                         if first:
                             flat.zero_()

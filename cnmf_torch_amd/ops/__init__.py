@@ -145,9 +145,18 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     if S > 1:
         epochs = (max_iter // max(1, check_every) + 3) if conv_mode == 1 else (max_iter + 2)
         ws = _coop_workspace(x.device, _stream_ptr(x), R, epochs, S)
-        ws["count"][: R * epochs].zero_()
+        if torch.cuda.is_current_stream_capturing():
+            # a graph replays fixed arguments: zero the counters in the graph and use a
+            # generation eager launches never reach
+            ws["count"][: R * epochs].zero_()
+            gen = 0xFFFFFFFF
+        else:
+            ws["gen"] += 1                  # tags this launch's arrivals: no zeroing
+            gen = ws["gen"]
         ws_slots, ws_count, ws_flag = (ws["slots"].data_ptr(), ws["count"].data_ptr(),
                                        ws["flag"].data_ptr())
+    else:
+        gen = 0
     h.solve(a, K, x.data_ptr(), x.stride(0), x.stride(1), numer.data_ptr(), numer.stride(0),
             numer.stride(1), gram.data_ptr(), K * K, ri, nblocks, n, int(max_iter), float(tol),
             float(l1_num), float(l1_den), float(l2), float(eps),
@@ -157,7 +166,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             int(conv_mode), int(check_every), int(threads),
             {"auto": 0, "stream": 1, "reg": 2}[variant],
             active.data_ptr() if active is not None else 0, int(S), ws_slots, ws_count,
-            int(epochs), ws_flag, _stream_ptr(x))
+            int(gen), int(epochs), ws_flag, _stream_ptr(x))
 
 
 # Cooperative-split bookkeeping.  A launch of S*nblocks 1024-thread workgroups is only safe
@@ -205,7 +214,8 @@ def _coop_split(n: int, nblocks: int, dev: torch.device) -> int:
 
 
 def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int) -> dict:
-    """Per-(device, stream) scratch: slots [R*epochs*S*2] f32, counters [R*epochs] i32,
+    """Per-(device, stream) scratch: slots [R*epochs*S*2] f32, generation-tagged arrival
+    counters [R*epochs] (int64, zeroed once at allocation), the launch generation and the
     timeout flag.  Reused across launches on the same stream (stream order serialises)."""
     key = (str(dev), stream)
     ws = _COOP_WS.get(key)
@@ -213,7 +223,8 @@ def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int)
     if ws is None or ws["slots"].numel() < need_slots or ws["count"].numel() < need_count:
         flag = ws["flag"] if ws is not None else torch.zeros(1, dtype=torch.int32, device=dev)
         ws = {"slots": torch.empty(max(need_slots, 1 << 16), dtype=torch.float32, device=dev),
-              "count": torch.empty(max(need_count, 1 << 14), dtype=torch.int32, device=dev),
+              "count": torch.zeros(max(need_count, 1 << 14), dtype=torch.int64, device=dev),
+              "gen": ws["gen"] if ws is not None else 0,
               "flag": flag}
         _COOP_WS[key] = ws
     return ws

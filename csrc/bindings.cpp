@@ -33,14 +33,16 @@ PYBIND11_MODULE(_hip, m) {
            int nblocks, int ncols, int max_iter, float tol, float l1_num, float l1_den, float l2,
            float eps, uintptr_t lin_out, uintptr_t quad_out, uintptr_t iters_out, int nsplit,
            int conv_mode, int check_every, int threads, int variant, uintptr_t active,
-           int coop_split, uintptr_t coop_slots, uintptr_t coop_count, int coop_epochs,
+           int coop_split, uintptr_t coop_slots, uintptr_t coop_count, unsigned coop_gen,
+           int coop_epochs,
            uintptr_t coop_timeout, uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
                            max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
                            P<float>(quad_out), P<int>(iters_out), nsplit, conv_mode,
                            check_every, threads, variant, P<const int>(active), coop_split,
-                           P<float>(coop_slots), P<int>(coop_count), coop_epochs,
+                           P<float>(coop_slots), P<unsigned long long>(coop_count), coop_gen,
+                           coop_epochs,
                            P<int>(coop_timeout),
                            reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");

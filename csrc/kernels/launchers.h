@@ -12,7 +12,8 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       float l1_num, float l1_den, float l2, float eps, float* lin_out,
                       float* quad_out, int* iters_out, int nsplit, int conv_mode,
                       int check_every, int threads, int variant, const int* active,
-                      int coop_split, float* coop_slots, int* coop_count, int coop_epochs,
+                      int coop_split, float* coop_slots, unsigned long long* coop_count,
+                      unsigned coop_gen, int coop_epochs,
                       int* coop_timeout, hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,

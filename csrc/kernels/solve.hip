@@ -25,7 +25,8 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  float* quad_out, int* iters_out, int nsplit, int conv_mode,
                                  int check_every, int threads, int variant,
                                  const int* active, int coop_split, float* coop_slots,
-                                 int* coop_count, int coop_epochs, int* coop_timeout,
+                                 unsigned long long* coop_count, unsigned coop_gen,
+                                 int coop_epochs, int* coop_timeout,
                                  hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
@@ -44,6 +45,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.active = active;
   p.coop_slots = coop_split > 1 ? coop_slots : nullptr;
   p.coop_count = coop_count;
+  p.coop_gen = coop_gen;
   p.coop_epochs = coop_epochs;
   p.coop_timeout = coop_timeout;
   p.coop_epochs_split = coop_split > 1 ? coop_split : 1;

@@ -140,16 +140,28 @@ __device__ __forceinline__ void coop_sum2(const SolveParams& p, int rep, int e, 
     return;
   }
   float* slots = p.coop_slots + (((long long)rep * p.coop_epochs + e) * S) * 2;
-  int* cnt = p.coop_count + (long long)rep * p.coop_epochs + e;
+  unsigned long long* cnt = p.coop_count + (long long)rep * p.coop_epochs + e;
+  const unsigned long long tag = (unsigned long long)p.coop_gen << 32;
+  constexpr unsigned long long kHi = 0xffffffff00000000ull;
   if (threadIdx.x == 0) {
     slots[2 * slice] = a;
     slots[2 * slice + 1] = b;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // arrive: a counter still tagged with an older launch restarts at 1
+    unsigned long long old = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+      const unsigned long long want = (old & kHi) == tag ? old + 1 : (tag | 1ull);
+      if (__hip_atomic_compare_exchange_strong(cnt, &old, want, __ATOMIC_RELAXED,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        break;
+    }
     unsigned spins = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < S) {
+    while (true) {
+      const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+      if ((v & kHi) == tag && (int)(v & 0xffffffffull) >= S) break;
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1u << 24)) {
         atomicExch(p.coop_timeout, 1);

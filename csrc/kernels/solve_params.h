@@ -25,7 +25,11 @@ struct SolveParams {
   // Cooperative split (gridDim.y = S > 1 workgroups per replicate, WITH convergence):
   // per-epoch partial sums are exchanged through global memory (deterministic order).
   float* coop_slots;        // [R][coop_epochs][S][2], no zeroing needed
-  int* coop_count;          // [R][coop_epochs], zeroed by the host before every launch
+  // [R][coop_epochs] arrival counters, (generation << 32) | arrivals: the first arrival
+  // of launch `coop_gen` restarts a counter, so the host never zeroes them (allocated
+  // zeroed once; coop_gen >= 1 strictly increases per launch on a workspace)
+  unsigned long long* coop_count;
+  unsigned coop_gen;
   int coop_epochs;
   int* coop_timeout;        // set to 1 if a spin gave up (residency violated)
   int coop_epochs_split;    // launch-side: S (gridDim.y) for the cooperative split
