@@ -30,34 +30,46 @@ __global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X,
   const float* __restrict__ x = X + (long long)rep * x_rs;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int m = lane & 15, q = lane >> 4;
-  gf32x4 acc[T][T];
+  // Two accumulator sets (even / odd column of each float4) halve the dependent MFMA
+  // chain, and GU slabs per iteration keep GU float4 loads in flight per lane (one
+  // load per dependent chain was latency-bound: 16 us for K=10, n=5000, R=100).
+  constexpr int GU = 4;
+  gf32x4 acc[2][T][T];
 #pragma unroll
-  for (int a = 0; a < T; ++a)
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int b = 0; b < T; ++b) acc[a][b] = gf32x4{0.f, 0.f, 0.f, 0.f};
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+      for (int b = 0; b < T; ++b) acc[h][a][b] = gf32x4{0.f, 0.f, 0.f, 0.f};
   const bool vec = (ldx & 3) == 0 && (((uintptr_t)x) & 15) == 0;
-  for (int c0 = wave * 16; c0 < n; c0 += nw * 16) {
-    const int c = c0 + 4 * q;
-    float v[T][4];
+  for (int c00 = wave * 16; c00 < n; c00 += GU * nw * 16) {
+    float v[GU][T][4];
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const int row = m + 16 * t;
-      const float* xr = x + (long long)row * ldx;
-      if (row < K && vec && c + 3 < n) {
-        const float4 f = *reinterpret_cast<const float4*>(xr + c);
-        v[t][0] = f.x; v[t][1] = f.y; v[t][2] = f.z; v[t][3] = f.w;
-      } else {
+    for (int u = 0; u < GU; ++u) {
+      const int c = c00 + u * nw * 16 + 4 * q;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[t][j] = (row < K && c + j < n) ? xr[c + j] : 0.f;
+      for (int t = 0; t < T; ++t) {
+        const int row = m + 16 * t;
+        const float* xr = x + (long long)row * ldx;
+        if (row < K && vec && c + 3 < n) {
+          const float4 f = *reinterpret_cast<const float4*>(xr + c);
+          v[u][t][0] = f.x; v[u][t][1] = f.y; v[u][t][2] = f.z; v[u][t][3] = f.w;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[u][t][j] = (row < K && c + j < n) ? xr[c + j] : 0.f;
+        }
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int u = 0; u < GU; ++u)
 #pragma unroll
-      for (int a = 0; a < T; ++a)
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int b = 0; b < T; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[a][j], v[b][j], acc[a][b], 0, 0, 0);
+        for (int a = 0; a < T; ++a)
+#pragma unroll
+          for (int b = 0; b < T; ++b)
+            acc[j & 1][a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[u][a][j], v[u][b][j],
+                                                                  acc[j & 1][a][b], 0, 0, 0);
   }
   // C/D map: row 4q + i, col m (register i)
 #pragma unroll
@@ -66,7 +78,7 @@ __global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X,
     for (int b = 0; b < T; ++b)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        red[wave][((a * T + b) * 16 + 4 * q + i) * 16 + m] = acc[a][b][i];
+        red[wave][((a * T + b) * 16 + 4 * q + i) * 16 + m] = acc[0][a][b][i] + acc[1][a][b][i];
   __syncthreads();
   float* o = out + (long long)rep * o_rs;
   for (int e = threadIdx.x; e < K * K; e += blockDim.x) {
