@@ -18,7 +18,8 @@ are kept TRANSPOSED, ``HT`` (R*K, N), so a replicate's chunk block is K rows of
 contiguous cells -- coalesced for the solve kernel and directly the GEMM operand.
 
 Algorithms (nmf-torch surface; cnmf.py:757-771 fixes algo='mu', mode='online'):
-  algo  in {'mu', 'hals'}       (HALS: Frobenius only)
+  algo  in {'mu', 'hals', 'bpp'} (HALS, BPP: Frobenius only; bpp = exact NNLS half-steps,
+                                 models/bpp.py)
   mode  in {'online', 'batch'}
   beta_loss in {'frobenius', 'kullback-leibler', 'itakura-saito'} or a float
 Online (Mairal-style sufficient statistics): per pass, chunks of ``online_chunk_size``
@@ -48,6 +49,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from .bpp import nnls_bpp, objective_terms as bpp_objective_terms
 from ..parallel.comm import LocalComm
 from ..utils import rng
 
@@ -95,12 +97,12 @@ class NMFOptions:
         return cls(n_components=int(n_components), **{k: v for k, v in kw.items() if k in names})
 
     def validate(self) -> None:
-        if self.algo not in ("mu", "hals"):
-            raise ValueError(f"algo must be 'mu' or 'hals', got {self.algo!r}")
+        if self.algo not in ("mu", "hals", "bpp"):
+            raise ValueError(f"algo must be 'mu', 'hals' or 'bpp', got {self.algo!r}")
         if self.mode not in ("online", "batch"):
             raise ValueError(f"mode must be 'online' or 'batch', got {self.mode!r}")
-        if self.algo == "hals" and beta_value(self.beta_loss) != 2.0:
-            raise ValueError("HALS is defined for the Frobenius loss only")
+        if self.algo in ("hals", "bpp") and beta_value(self.beta_loss) != 2.0:
+            raise ValueError(f"{self.algo.upper()} is defined for the Frobenius loss only")
         if self.init not in ("random", "nndsvd", "nndsvda", "nndsvdar"):
             raise ValueError(f"unsupported init {self.init!r}")
         if self.fp_precision not in ("float", "double"):
@@ -429,6 +431,31 @@ def _sq_norm(X: torch.Tensor, rows: int = 1 << 16) -> float:
     return val
 
 
+def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch.Tensor,
+                 **kw) -> None:
+    """One half-step on x3 (R, K, n) in place.  'mu' / 'hals' run the fused iterative
+    kernels (ops.solve); 'bpp' solves every column's NNLS exactly (models/bpp.py) and
+    fills the same optional outputs: lin/quad (trace-trick loss terms) and iters."""
+    if algo != "bpp":
+        ops.solve(algo, x3, numer3, gram3, **kw)
+        return
+    R = x3.shape[0]
+    active = kw.get("active")
+    xn = nnls_bpp(gram3, numer3, l1=kw.get("l1_den", 0.0), l2=kw.get("l2", 0.0))
+    live = None if active is None else (active[:R] != 0)
+    x3.copy_(xn if live is None else torch.where(live.view(R, 1, 1), xn, x3))
+    lin_out, quad_out = kw.get("lin_out"), kw.get("quad_out")
+    if lin_out is not None or quad_out is not None:
+        lin, quad = bpp_objective_terms(x3, numer3, gram3)
+        for out, v in ((lin_out, lin), (quad_out, quad)):
+            if out is not None:
+                v = v.to(out.dtype)
+                out[:R] = v if live is None else torch.where(live, v, out[:R])
+    iters = kw.get("iters_out")
+    if iters is not None:
+        iters[:R] += 1 if live is None else live.to(iters.dtype)
+
+
 def _graphs_enabled(X: torch.Tensor) -> bool:
     """Capture repeated passes into HIP graphs (GPU only, opt-in: CNMF_GRAPHS=1).  Off by
     default: a compaction changes the layout every few passes, and re-capturing cost more
@@ -663,7 +690,7 @@ class NMFBatchSolver:
                         h_old = hview.clone() if exact else None
                         WWT = ops.gram(W3, out=wwt_buf, active=active)   # MFMA Gram
                         numerT = W @ xc.t()                              # (n*K, cw) GEMM
-                        ops.solve(algo, hview, numerT.view(n, K, cw), WWT,
+                        _inner_solve(algo, hview, numerT.view(n, K, cw), WWT,
                                   max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
                                   l1_den=o.l1_H, l2=o.l2_H, eps=o.eps, iters_out=h_it,
                                   conv_mode=cmode, check_every=o.inner_check_every,
@@ -699,7 +726,7 @@ class NMFBatchSolver:
                         B_ += dB
                         A_ += dA
                     last = s_ == len(steps) - 1
-                    ops.solve(algo, W3, B_.view(n, K, G), A_.contiguous(),
+                    _inner_solve(algo, W3, B_.view(n, K, G), A_.contiguous(),
                               max_iter=o.online_chunk_max_iter, tol=o.online_w_tol,
                               l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
                               lin_out=lin if last else None, quad_out=quad if last else None,
@@ -774,7 +801,7 @@ class NMFBatchSolver:
             WWT = ops.gram(W3, active=st.active_mask())
             numerT = W @ X.t()
             nsplit = 1 if hals else max(1, (N + 8191) // 8192)
-            ops.solve(o.algo, HT.view(n, K, N), numerT.view(n, K, N), WWT,
+            _inner_solve(o.algo, HT.view(n, K, N), numerT.view(n, K, N), WWT,
                       max_iter=h_iter, tol=h_tol, l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
                       nsplit=nsplit, active=active, iters_out=st.h_iters[:n])
             del numerT
@@ -784,7 +811,7 @@ class NMFBatchSolver:
             ops.gram(H3, out=A)
             comm.allreduce_(flat)
             check = (it + 1) % every == 0 or it + 1 == max_it
-            ops.solve(o.algo, W3, B.view(n, K, G), A.contiguous(),
+            _inner_solve(o.algo, W3, B.view(n, K, G), A.contiguous(),
                       max_iter=h_iter, tol=h_tol, l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
                       lin_out=lin if check else None, quad_out=quad if check else None,
                       active=active, iters_out=st.w_iters[:n])
