@@ -15,7 +15,7 @@ backup rule (only the largest infeasible index, after three exchanges that did n
 shrink the infeasible set) that guarantees termination.
 
 Batched form: all columns of all replicates are pivoted together.  A column's masked
-system ``G o (F F^T) + diag(1 - F)`` is SPD whenever G is, so one batched Cholesky
+system ``G o (F F^T) + diag(1 - F)`` is SPD whenever G is, so one batched LU
 factorisation + solve per pivot round covers every column (float64; K <= 32 systems
 are far below an MFMA tile, the batched LAPACK path is the right tool).  Columns that
 are already feasible keep their solution.
@@ -30,8 +30,8 @@ def nnls_bpp(G: torch.Tensor, B: torch.Tensor, l1: float = 0.0, l2: float = 0.0,
     """Solve min_{x>=0} 1/2 x^T (G + l2 I) x - (b - l1)^T x for every column of ``B``.
 
     G: (R, K, K) symmetric PSD; B: (R, K, n).  Returns X (R, K, n) in B's dtype.  Columns
-    are processed in chunks of ``col_chunk`` per replicate to bound the (R, c, K, K)
-    float64 workspace.
+    are processed in chunks (at most ``col_chunk`` per replicate and 2^16 systems per
+    chunk) to bound the (R, c, K, K) float64 workspace and the batched factorisations.
     """
     R, K, n = B.shape
     if G.shape != (R, K, K):
@@ -44,8 +44,9 @@ def nnls_bpp(G: torch.Tensor, B: torch.Tensor, l1: float = 0.0, l2: float = 0.0,
     # a relative ridge keeps rank-deficient Grams (duplicate components) factorisable
     ridge = 1e-12 * Gd.diagonal(dim1=1, dim2=2).mean(dim=1).clamp_min(1e-300)
     Gd = Gd + ridge.view(R, 1, 1) * eye
-    for a in range(0, n, col_chunk):
-        b = min(n, a + col_chunk)
+    step = max(1, min(col_chunk, (1 << 16) // max(1, R)))
+    for a in range(0, n, step):
+        b = min(n, a + step)
         rhs = B[:, :, a:b].to(torch.float64).transpose(1, 2)         # (R, c, K)
         if l1:
             rhs = rhs - l1
@@ -84,16 +85,43 @@ def _bpp_block(G: torch.Tensor, b: torch.Tensor, max_rounds: int | None) -> torc
         Fm = F.to(torch.float64)
         A = Gc * (Fm.unsqueeze(3) * Fm.unsqueeze(2)) + torch.diag_embed(1.0 - Fm)
         rhs = (b * Fm).unsqueeze(3)
-        L, info = torch.linalg.cholesky_ex(A)
-        sol = torch.cholesky_solve(rhs, L).squeeze(3)
-        bad = info != 0
-        if bool(bad.any()):                                            # not SPD: least squares
-            sol[bad] = torch.linalg.lstsq(A[bad].cpu(), rhs[bad].cpu()).solution.squeeze(2).to(dev)
+        sol, bad = _spd_solve(A.reshape(-1, K, K), rhs.reshape(-1, K, 1))
+        if bool(bad.any()):
+            # an fp32-accumulated Gram can be indefinite at the 1e-7 level: retry those
+            # systems with a ridge of that size, in float64 on the host (rare)
+            Ab = A.reshape(-1, K, K)[bad].cpu()
+            rb = rhs.reshape(-1, K, 1)[bad].cpu()
+            lift = 1e-6 * Ab.diagonal(dim1=1, dim2=2).abs().mean(dim=1).clamp_min(1e-300)
+            Ab = Ab + lift.view(-1, 1, 1) * torch.eye(K, dtype=Ab.dtype)
+            sol[bad] = (torch.linalg.pinv(Ab, hermitian=True) @ rb).squeeze(2).to(dev)
+        sol = sol.view(R, c, K)
         sol = sol * Fm
         x = torch.where(live.unsqueeze(2), sol, x)
         yn = torch.einsum("rkl,rcl->rck", G, x) - b
         y = torch.where(live.unsqueeze(2), yn * (1.0 - Fm), y)
     return x.clamp_min(0.0)
+
+
+def _spd_solve(A: torch.Tensor, rhs: torch.Tensor):
+    """Batched LU solve of (m, K, K) SPD systems, at most 2^14 per factorisation call.
+    Every solution is verified by its residual (on the GPU, batched Cholesky at large
+    batch sizes returned garbage for some well-posed systems without flagging them).
+    Returns the (m, K) solutions and a mask of systems that failed the check."""
+    m, K = A.shape[0], A.shape[1]
+    sol = torch.empty((m, K), dtype=A.dtype, device=A.device)
+    bad = torch.zeros(m, dtype=torch.bool, device=A.device)
+    step = 1 << 14
+    for a in range(0, m, step):
+        b = min(m, a + step)
+        s, info = torch.linalg.solve_ex(A[a:b], rhs[a:b])
+        s = s.squeeze(2)
+        sol[a:b] = s
+        # residual check: a factorisation that silently broke down leaves a large residual
+        res = (A[a:b] @ s.unsqueeze(2) - rhs[a:b]).squeeze(2).abs().amax(dim=1)
+        scale = rhs[a:b].squeeze(2).abs().amax(dim=1) + A[a:b].abs().amax(dim=(1, 2)) * \
+            s.abs().amax(dim=1)
+        bad[a:b] = (info != 0) | ~torch.isfinite(s).all(dim=1) | (res > 1e-8 * scale + 1e-300)
+    return sol, bad
 
 
 def objective_terms(x3: torch.Tensor, numer3: torch.Tensor, gram3: torch.Tensor):

@@ -367,9 +367,11 @@ class _PassPipeline:
     behind, so the GPU never drains at a pass boundary.  When flags show that enough
     replicates finished, the host synchronises once and compacts the batch."""
 
-    def __init__(self, st: _Batch, compact_frac: float = 0.25):
+    def __init__(self, st: _Batch, compact_frac: float | None = None):
         self.st = st
         self.cuda = st.W.device.type == "cuda"
+        if compact_frac is None:
+            compact_frac = float(os.environ.get("CNMF_COMPACT_FRAC", "0.25"))
         self.frac = compact_frac
         self.pending = None   # (event, host_flags, n)
 
@@ -439,10 +441,17 @@ def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch
     if algo != "bpp":
         ops.solve(algo, x3, numer3, gram3, **kw)
         return
-    R = x3.shape[0]
+    R, K = x3.shape[0], x3.shape[1]
     active = kw.get("active")
-    xn = nnls_bpp(gram3, numer3, l1=kw.get("l1_den", 0.0), l2=kw.get("l2", 0.0))
     live = None if active is None else (active[:R] != 0)
+    g, b = gram3, numer3
+    if live is not None:
+        # finished replicates' statistics are stale (possibly never written): give them a
+        # trivial, finite system; their result is discarded below
+        keep = live.view(R, 1, 1)
+        g = torch.where(keep, gram3, torch.eye(K, dtype=gram3.dtype, device=gram3.device))
+        b = torch.where(keep, numer3, torch.zeros((), dtype=numer3.dtype, device=numer3.device))
+    xn = nnls_bpp(g, b, l1=kw.get("l1_den", 0.0), l2=kw.get("l2", 0.0))
     x3.copy_(xn if live is None else torch.where(live.view(R, 1, 1), xn, x3))
     lin_out, quad_out = kw.get("lin_out"), kw.get("quad_out")
     if lin_out is not None or quad_out is not None:
