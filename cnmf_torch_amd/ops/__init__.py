@@ -430,10 +430,24 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
         raise ValueError("X3 needs unit column stride")
     if active is not None and (active.dtype != torch.int32 or active.numel() < R):
         raise ValueError("active: int32 with >= R entries")
+    # few replicates: split the columns over S workgroups per replicate (one workgroup per
+    # replicate left most of the chip idle at R = 8) and reduce the partials in order
+    S = 1 if R >= 64 else max(1, min((n + 255) // 256, 512 // max(1, R)))
+    part = 0
+    if S > 1:
+        key = (str(X3.device), _stream_ptr(X3))
+        ws = _GRAM_WS.get(key)
+        if ws is None or ws.numel() < S * R * K * K:
+            ws = torch.empty(max(S * R * K * K, 1 << 14), dtype=torch.float32, device=X3.device)
+            _GRAM_WS[key] = ws
+        part = ws.data_ptr()
     _hip.gram(X3.data_ptr(), X3.stride(0), X3.stride(1), R, K, n, out.data_ptr(), K * K,
               int(bool(accumulate)), active.data_ptr() if active is not None else 0,
-              _stream_ptr(X3))
+              part, int(S), _stream_ptr(X3))
     return out
+
+
+_GRAM_WS: dict = {}
 
 
 # ----------------------------------------------------------------------------- consensus

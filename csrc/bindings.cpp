@@ -200,9 +200,10 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("gram", [](uintptr_t X, long long x_rs, long long ldx, int R, int K, int n,
                    uintptr_t out, long long o_rs, int accumulate, uintptr_t active,
-                   uintptr_t stream) {
+                   uintptr_t part, int S, uintptr_t stream) {
     check(cnmf_gram(P<const float>(X), x_rs, ldx, R, K, n, P<float>(out), o_rs, accumulate,
-                    P<const int>(active), reinterpret_cast<hipStream_t>(stream)),
+                    P<const int>(active), P<float>(part), S,
+                    reinterpret_cast<hipStream_t>(stream)),
           "gram");
   });
 

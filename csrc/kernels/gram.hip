@@ -23,11 +23,15 @@ template <int T>  // T = 1 (K <= 16) or 2 (K <= 32) tiles per dimension
 __global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X, long long x_rs,
                                                     long long ldx, int K, int n,
                                                     float* __restrict__ out, long long o_rs,
-                                                    int accumulate, const int* active) {
+                                                    int accumulate, const int* active,
+                                                    float* __restrict__ part, int per) {
   __shared__ float red[16][T * T * 16 * 16 + 1];
   const int rep = blockIdx.x;
   if (active && active[rep] == 0) return;
   const float* __restrict__ x = X + (long long)rep * x_rs;
+  // column split (gridDim.y > 1, few replicates): slice [c_beg, c_end) -> partial K x K
+  const int c_beg = part ? (int)blockIdx.y * per : 0;
+  const int c_end = part ? min(n, c_beg + per) : n;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int m = lane & 15, q = lane >> 4;
   // Two accumulator sets (even / odd column of each float4) halve the dependent MFMA
@@ -42,7 +46,7 @@ __global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X,
 #pragma unroll
       for (int b = 0; b < T; ++b) acc[h][a][b] = gf32x4{0.f, 0.f, 0.f, 0.f};
   const bool vec = (ldx & 3) == 0 && (((uintptr_t)x) & 15) == 0;
-  for (int c00 = wave * 16; c00 < n; c00 += GU * nw * 16) {
+  for (int c00 = c_beg + wave * 16; c00 < c_end; c00 += GU * nw * 16) {
     float v[GU][T][4];
 #pragma unroll
     for (int u = 0; u < GU; ++u) {
@@ -51,12 +55,12 @@ __global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X,
       for (int t = 0; t < T; ++t) {
         const int row = m + 16 * t;
         const float* xr = x + (long long)row * ldx;
-        if (row < K && vec && c + 3 < n) {
+        if (row < K && vec && c + 3 < c_end) {
           const float4 f = *reinterpret_cast<const float4*>(xr + c);
           v[u][t][0] = f.x; v[u][t][1] = f.y; v[u][t][2] = f.z; v[u][t][3] = f.w;
         } else {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[u][t][j] = (row < K && c + j < n) ? xr[c + j] : 0.f;
+          for (int j = 0; j < 4; ++j) v[u][t][j] = (row < K && c + j < c_end) ? xr[c + j] : 0.f;
         }
       }
     }
@@ -80,13 +84,29 @@ __global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X,
       for (int i = 0; i < 4; ++i)
         red[wave][((a * T + b) * 16 + 4 * q + i) * 16 + m] = acc[0][a][b][i] + acc[1][a][b][i];
   __syncthreads();
-  float* o = out + (long long)rep * o_rs;
+  float* o = part ? part + ((long long)blockIdx.y * gridDim.x + rep) * K * K
+                  : out + (long long)rep * o_rs;
   for (int e = threadIdx.x; e < K * K; e += blockDim.x) {
     const int i = e / K, j = e % K;
     const int a = i >> 4, b = j >> 4;
     const int slot = ((a * T + b) * 16 + (i & 15)) * 16 + (j & 15);
     float s = 0.f;
     for (int w = 0; w < nw; ++w) s += red[w][slot];
+    o[e] = (accumulate && !part) ? o[e] + s : s;
+  }
+}
+
+// Second stage of the column-split Gram: out[r] (+)= sum of the S partials in split
+// order (deterministic).
+__global__ void gram_reduce_kernel(const float* __restrict__ part, int S, int R, int K,
+                                   float* __restrict__ out, long long o_rs, int accumulate,
+                                   const int* active) {
+  const int rep = blockIdx.x;
+  if (active && active[rep] == 0) return;
+  float* o = out + (long long)rep * o_rs;
+  for (int e = threadIdx.x; e < K * K; e += blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += part[((long long)z * R + rep) * K * K + e];
     o[e] = accumulate ? o[e] + s : s;
   }
 }
@@ -95,15 +115,24 @@ __global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X,
 
 extern "C" hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K, int n,
                                 float* out, long long o_rs, int accumulate, const int* active,
-                                hipStream_t stream) {
+                                float* part, int S, hipStream_t stream) {
   if (R <= 0) return hipSuccess;
-  if (K < 1 || K > 32 || n < 0) return hipErrorInvalidValue;
-  const int threads = n >= 16 * 16 ? 1024 : 64 * ((n + 15) / 16 > 0 ? ((n + 15) / 16) : 1);
+  if (K < 1 || K > 32 || n < 0 || S < 1) return hipErrorInvalidValue;
+  if (S > 1 && !part) return hipErrorInvalidValue;
+  // slice width: a multiple of 16 columns keeps the float4 slabs aligned
+  const int per = S > 1 ? (((n + S - 1) / S + 15) / 16) * 16 : n;
+  const int cols = S > 1 ? per : n;
+  const int threads = cols >= 16 * 16 ? 1024 : 64 * ((cols + 15) / 16 > 0 ? ((cols + 15) / 16) : 1);
+  const dim3 grid(R, S);
+  float* pp = S > 1 ? part : nullptr;
   if (K <= 16)
-    hipLaunchKernelGGL((cnmf::gram_kernel<1>), dim3(R), dim3(threads), 0, stream, X, x_rs, ldx, K,
-                       n, out, o_rs, accumulate, active);
+    hipLaunchKernelGGL((cnmf::gram_kernel<1>), grid, dim3(threads), 0, stream, X, x_rs, ldx, K,
+                       n, out, o_rs, accumulate, active, pp, per);
   else
-    hipLaunchKernelGGL((cnmf::gram_kernel<2>), dim3(R), dim3(threads), 0, stream, X, x_rs, ldx, K,
-                       n, out, o_rs, accumulate, active);
+    hipLaunchKernelGGL((cnmf::gram_kernel<2>), grid, dim3(threads), 0, stream, X, x_rs, ldx, K,
+                       n, out, o_rs, accumulate, active, pp, per);
+  if (S > 1)
+    hipLaunchKernelGGL(cnmf::gram_reduce_kernel, dim3(R), dim3(256), 0, stream, part, S, R, K,
+                       out, o_rs, accumulate, active);
   return hipGetLastError();
 }

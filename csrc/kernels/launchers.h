@@ -49,7 +49,7 @@ hipError_t cnmf_harmony_block(int op, double* Rt, const double* distT, const dou
 
 hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K, int n,
                      float* out, long long o_rs, int accumulate, const int* active,
-                     hipStream_t stream);
+                     float* part, int S, hipStream_t stream);
 
 int cnmf_kmeans_blocks(int n);
 int cnmf_kmeans_fits(int k, int d);

@@ -550,7 +550,7 @@ hipError_t launch_solve_k(int algo, const SolveParams& p, int nblocks, int threa
   }
 
 // register-resident variant: K <= kResidentMaxK, U <= res_max_cols(K) columns per thread
-constexpr int kResidentMaxK = 16;
+constexpr int kResidentMaxK = 24;
 
 // Resident launch for U columns per thread: instantiated only where U <= res_max_cols(K).
 template <int K, int U>
@@ -581,6 +581,14 @@ hipError_t launch_solve_res_ku(int algo, const SolveParams& p, int nblocks, int 
     case 14: return launch_solve_res_ku<14, U>(algo, p, nblocks, threads, s);             \
     case 15: return launch_solve_res_ku<15, U>(algo, p, nblocks, threads, s);             \
     case 16: return launch_solve_res_ku<16, U>(algo, p, nblocks, threads, s);             \
+    case 17: return launch_solve_res_ku<17, U>(algo, p, nblocks, threads, s);             \
+    case 18: return launch_solve_res_ku<18, U>(algo, p, nblocks, threads, s);             \
+    case 19: return launch_solve_res_ku<19, U>(algo, p, nblocks, threads, s);             \
+    case 20: return launch_solve_res_ku<20, U>(algo, p, nblocks, threads, s);             \
+    case 21: return launch_solve_res_ku<21, U>(algo, p, nblocks, threads, s);             \
+    case 22: return launch_solve_res_ku<22, U>(algo, p, nblocks, threads, s);             \
+    case 23: return launch_solve_res_ku<23, U>(algo, p, nblocks, threads, s);             \
+    case 24: return launch_solve_res_ku<24, U>(algo, p, nblocks, threads, s);             \
     default: return hipErrorInvalidValue;                                                 \
   }
 

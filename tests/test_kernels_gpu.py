@@ -361,7 +361,8 @@ def test_harmony_native_matches_cpu():
         assert gpu.kmeans_rounds == cpu.kmeans_rounds
 
 
-@pytest.mark.parametrize("algo,K", [("mu", 3), ("mu", 10), ("mu", 13), ("hals", 10), ("hals", 16)])
+@pytest.mark.parametrize("algo,K", [("mu", 3), ("mu", 10), ("mu", 13), ("hals", 10), ("hals", 16),
+                                    ("mu", 20), ("hals", 24)])
 @pytest.mark.parametrize("conv_mode", [0, 1])
 def test_solve_register_resident_variant(algo, K, conv_mode):
     """variant='reg' (x, numer in VGPRs across iterations) == streaming == fp64 reference."""
@@ -514,6 +515,18 @@ def test_solve_random_shapes_match_reference(seed, R, K, n, algo, pad, coop, var
 
 
 @pytest.mark.parametrize("K", [1, 5, 10, 16, 17, 32])
+def test_gram_column_split_matches_single_workgroup(K):
+    """Few replicates (column-split Gram + ordered reduce) == many-replicate path (one
+    workgroup per replicate) on the same blocks, to fp32 summation order."""
+    g = torch.Generator().manual_seed(K + 1)
+    H = torch.rand((80, K, 5000), generator=g).cuda()
+    full = ops.gram(H)                      # R = 80: one workgroup per replicate
+    few = ops.gram(H[:8])                   # R = 8: S column slices per replicate
+    torch.testing.assert_close(few, full[:8], rtol=2e-6, atol=1e-3)
+    assert torch.equal(few, ops.gram(H[:8]))          # deterministic
+
+
+@pytest.mark.parametrize("K", [1, 5, 10, 16, 17, 20, 32])
 def test_gram_kernel_matches_bmm(K):
     """MFMA batched Gram (gram.hip): strided / offset views, ragged n, accumulate, active."""
     g = torch.Generator().manual_seed(K)
