@@ -1,3 +1,6 @@
+"""Probe: host enqueue time vs GPU wait per online pass of the bench shape
+(NMFBatchSolver(profile=True) records both; 3 runs of 100 replicates).  The output is
+profiles/r1_host_probe_v25.log."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch, collections
