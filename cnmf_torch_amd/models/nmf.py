@@ -601,7 +601,7 @@ class NMFBatchSolver:
         stats = torch.empty(R * K * G + R * K * K, device=X.device, dtype=X.dtype)
         B = stats[:R * K * G].view(R * K, G)
         A = stats[R * K * G:].view(R, K, K)
-        torch.mm(st.HT, X, out=B)
+        B.addmm_(st.HT, X, beta=0.0)     # (not torch.mm(out=): ~0.4 ms host per call)
         H3 = st.HT.view(R, K, X.shape[0])
         ops.gram(H3, out=A)
         self.comm.allreduce_(stats)
@@ -710,17 +710,17 @@ class NMFBatchSolver:
                             hh -= torch.bmm(h_old, h_old.transpose(1, 2))
                             hlhs = h_old.neg_().add_(hview).view(n * K, cw)
                             if dist and first:
-                                torch.mm(hlhs, xc, out=accB)
+                                accB.addmm_(hlhs, xc, beta=0.0)
                                 accA.copy_(hh)
                             else:
                                 accB.addmm_(hlhs, xc)
                                 accA += hh
                         else:
                             if dist and first:
-                                torch.mm(HT[:, a:b], xc, out=accB)       # (n*K, G) GEMM
+                                accB.addmm_(HT[:, a:b], xc, beta=0.0)    # (n*K, G) GEMM
                                 ops.gram(hview, out=accA)
                             elif not dist and pass_first:
-                                torch.mm(HT[:, a:b], xc, out=accB)       # B = h^T x
+                                accB.addmm_(HT[:, a:b], xc, beta=0.0)    # B = h^T x
                                 ops.gram(hview, out=accA, active=active)  # A = h^T h
                             else:
                                 accB.addmm_(HT[:, a:b], xc)              # B += h^T x
@@ -815,7 +815,7 @@ class NMFBatchSolver:
                       nsplit=nsplit, active=active, iters_out=st.h_iters[:n])
             del numerT
             # W-step from the new H
-            torch.mm(HT, X, out=B)
+            B.addmm_(HT, X, beta=0.0)
             H3 = HT.view(n, K, N)
             ops.gram(H3, out=A)
             comm.allreduce_(flat)
