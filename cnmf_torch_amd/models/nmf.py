@@ -275,6 +275,8 @@ class _Batch:
         self.h_iters = torch.zeros(R, dtype=torch.int32, device=dev)
         self.w_iters = torch.zeros(R, dtype=torch.int32, device=dev)
         self.layout_version = 0   # bumped by compact(): captured graphs key on it
+        self.bucket = max(1, int(os.environ.get("CNMF_COMPACT_BUCKET",
+                                                "8" if W.device.type == "cuda" else "1")))
         self.A = None   # (R, K, K) sufficient statistics (online 'exact' mode)
         self.B = None   # (R*K, G)
 
@@ -284,6 +286,12 @@ class _Batch:
 
     def active_mask(self) -> torch.Tensor:
         return self.state["active"][:self.n_act]
+
+    def padded(self, n_live: int) -> int:
+        """Prefix length ``compact`` shrinks to when ``n_live`` replicates are live."""
+        if n_live <= 0:
+            return 0
+        return min(self.n_act, -(-n_live // self.bucket) * self.bucket)
 
     def compact(self, act_host: np.ndarray | None = None) -> None:
         """Move still-active replicates to the front and shrink n_act.
@@ -298,7 +306,12 @@ class _Batch:
             act_host = self.state["active"][:n].cpu().numpy() != 0
         act = np.asarray(act_host[:n], dtype=bool)
         keep = np.flatnonzero(act)
-        if keep.size == n:
+        # the live prefix is rounded up to a multiple of `bucket` replicates (padded with
+        # finished ones, which every kernel skips): batch shapes then repeat from step to
+        # step, so the GEMM library's per-shape heuristics are cached after warm-up
+        # instead of costing a host stall at every compaction
+        n_new = self.padded(keep.size)
+        if n_new == n:
             return
         perm = np.concatenate([keep, np.flatnonzero(~act), np.arange(n, self.R)])
         dev = self.W.device
@@ -313,7 +326,7 @@ class _Batch:
         self.h_iters = self.h_iters.index_select(0, pidx)
         self.w_iters = self.w_iters.index_select(0, pidx)
         self.order = [self.order[p] for p in perm]
-        self.n_act = int(keep.size)
+        self.n_act = int(n_new)
         self.layout_version += 1
 
     def set_err(self, err: torch.Tensor, pass_idx: int, tol: float, final: bool,
@@ -384,7 +397,7 @@ class _PassPipeline:
             n_live = int((st.state["active"][:n] != 0).sum())
             if n_live == 0:
                 return False
-            if n - n_live >= max(1, int(self.frac * n)):
+            if n - st.padded(n_live) >= max(1, int(self.frac * n)):
                 st.compact()
             return True
         flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
@@ -401,7 +414,7 @@ class _PassPipeline:
         n_live = int((pflags != 0).sum())
         if n_live == 0:                   # everything had finished one pass ago
             return False
-        if n - n_live >= max(1, int(self.frac * n)):
+        if n - st.padded(n_live) >= max(1, int(self.frac * n)):
             # compact on the one-pass-stale flags, in stream order: no drain of the GPU
             st.compact(pflags.numpy() != 0)
             self.pending = None
