@@ -786,17 +786,29 @@ class cNMF:
         save_df_to_npz(ref, self.paths["starcat_spectra"] % (k, dt))
         save_df_to_text(ref, self.paths["starcat_spectra__txt"] % (k, dt))
 
-    def k_selection_plot(self, close_fig=False, kmeans_backend="sklearn"):
-        """Stability (silhouette) and error per K (cnmf.py:1293-1332)."""
+    def k_selection_plot(self, close_fig=False, kmeans_backend="sklearn", comm=None,
+                         device=None):
+        """Stability (silhouette) and error per K (cnmf.py:1293-1332).
+
+        With ``comm`` (one rank per GPU) the Ks are dealt round-robin over the ranks, each
+        rank runs its Ks' stats on its own device, and rank 0 gathers the rows (Python
+        objects, a few floats per K) and writes the npz and the plot."""
         run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
         norm_counts = read_h5ad(self.paths["normalized_counts"])
-        stats = []
-        for k in sorted(set(int(x) for x in run_params.n_components)):
-            stats.append(self.consensus(k, skip_density_and_return_after_stats=True,
-                                        show_clustering=False, close_clustergram_fig=True,
-                                        norm_counts=norm_counts,
-                                        kmeans_backend=kmeans_backend).stats)
-        stats = pd.DataFrame(stats).reset_index(drop=True)
+        ks = sorted(set(int(x) for x in run_params.n_components))
+        rank, world = (0, 1) if comm is None else (comm.rank, comm.world_size)
+        rows = {}
+        for k in ks[rank::world]:
+            rows[k] = self.consensus(k, skip_density_and_return_after_stats=True,
+                                     show_clustering=False, close_clustergram_fig=True,
+                                     norm_counts=norm_counts, kmeans_backend=kmeans_backend,
+                                     device=device).stats
+        if world > 1:
+            for part in comm.all_gather_object(rows):
+                rows.update(part)
+            if rank != 0:
+                return None
+        stats = pd.DataFrame([rows[k] for k in ks]).reset_index(drop=True)
         save_df_to_npz(stats, self.paths["k_selection_stats"])
         from .utils.plotting import k_selection
 

@@ -118,12 +118,26 @@ def main(argv=None) -> int:
             ks = sorted(set(int(k) for k in rp.n_components))
         else:
             ks = args.components
-        for k in ks:
-            obj.consensus(k, args.local_density_threshold, args.local_neighborhood_size,
-                          args.show_clustering, args.build_reference, close_clustergram_fig=True,
-                          kmeans_backend=args.kmeans_backend, device=args.device)
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            from .parallel.runner import distributed_consensus
+
+            distributed_consensus(obj, ks, args.local_density_threshold,
+                                  args.local_neighborhood_size, args.show_clustering,
+                                  args.build_reference, kmeans_backend=args.kmeans_backend)
+        else:
+            for k in ks:
+                obj.consensus(k, args.local_density_threshold, args.local_neighborhood_size,
+                              args.show_clustering, args.build_reference,
+                              close_clustergram_fig=True, kmeans_backend=args.kmeans_backend,
+                              device=args.device)
     elif args.command == "k_selection_plot":
-        obj.k_selection_plot(close_fig=True, kmeans_backend=args.kmeans_backend)
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            from .parallel.runner import distributed_k_selection
+
+            distributed_k_selection(obj, kmeans_backend=args.kmeans_backend)
+        else:
+            obj.k_selection_plot(close_fig=True, kmeans_backend=args.kmeans_backend,
+                                 device=args.device)
     return 0
 
 

@@ -12,6 +12,8 @@ backend ``nccl`` (RCCL over xGMI) for device work, ``gloo`` on CPU:
   rank r holds a contiguous row block of norm_counts, every replicate batch runs on all
   ranks with the per-step ``[dB | dA]`` statistics all-reduced (one RCCL call per
   online step), rank 0 writes the (replicated) spectra.
+* ``distributed_consensus`` / ``distributed_k_selection`` -- K parallelism for the
+  post-factorize stages: each rank takes a round-robin share of the Ks.
 * fault tolerance: a restart with ``skip_completed_runs=True`` re-shards only the
   incomplete ledger rows over the surviving world size (resume by ledger, §5.3).
 """
@@ -65,6 +67,30 @@ def distributed_factorize(obj, skip_completed_runs: bool = False, replicate_batc
                        verbose=verbose, run_params=run_params)
     comm.barrier()
     return comm
+
+
+def distributed_consensus(obj, ks, density_threshold=0.5, local_neighborhood_size=0.30,
+                          show_clustering=True, build_ref=True, kmeans_backend="sklearn",
+                          backend: str | None = None):
+    """K-parallel consensus: rank r runs ``consensus`` for ``ks[r::world]`` on its own GPU.
+    Every K writes its own artifacts (consensus/score/TPM files, density cache, plot), so
+    the ranks share no files and need no collective beyond the closing barrier."""
+    comm, dev = init_distributed(backend)
+    for k in sorted(ks)[comm.rank::comm.world_size]:
+        obj.consensus(k, density_threshold, local_neighborhood_size, show_clustering,
+                      build_ref, close_clustergram_fig=True, kmeans_backend=kmeans_backend,
+                      device=dev)
+    comm.barrier()
+    return comm
+
+
+def distributed_k_selection(obj, kmeans_backend="sklearn", backend: str | None = None):
+    """K-parallel ``k_selection_plot``: stats per K on every rank, rank 0 writes."""
+    comm, dev = init_distributed(backend)
+    stats = obj.k_selection_plot(close_fig=True, kmeans_backend=kmeans_backend, comm=comm,
+                                 device=dev)
+    comm.barrier()
+    return stats
 
 
 def row_block(n_rows: int, rank: int, world: int) -> tuple[int, int]:

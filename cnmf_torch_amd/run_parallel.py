@@ -8,6 +8,7 @@ The reference shells out to ``cnmf.py prepare``, GNU ``parallel`` over
   factorize`` -- each rank takes a deterministic slice of the replicate ledger and
   batches its replicates through the HIP solver (RCCL only for the final barrier);
 * ``--gpus 1``: a single in-process factorize;
+* ``k_selection_plot`` and ``consensus`` run K-parallel over min(N, #K) ranks;
 * ``--workers N`` (no torchrun): N plain worker processes with ``--worker-index``, each
   pinned to one device via HIP_VISIBLE_DEVICES -- the reference's shared-filesystem
   pattern, useful when ranks must not share a process group.
@@ -107,10 +108,20 @@ def main(argv=None) -> int:
         pattern = os.path.join(a.output_dir, a.name, "cnmf_tmp", "*.iter_*.df.npz")
         for fn in glob.glob(pattern):
             os.remove(fn)
-    _run([py, "-m", "cnmf_torch_amd", "k_selection_plot"] + base)
+    # k-selection and consensus are K-parallel: one rank per GPU, Ks dealt round-robin
+    n_k = len(set(a.components))
+    kpar = min(a.gpus or 1, n_k) if not a.workers else 1
+    launch = [py, "-m", "cnmf_torch_amd"]
+    if kpar > 1:
+        launch = [py, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={kpar}",
+                  "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                  "-m", "cnmf_torch_amd"]
+    _run(launch + ["k_selection_plot"] + base, env=env)
     if a.local_density_threshold is not None:
-        _run([py, "-m", "cnmf_torch_amd", "consensus"] + base +
-             ["--local-density-threshold", str(a.local_density_threshold)])
+        if kpar > 1:
+            launch[launch.index("--master-port") + 1] = str(_free_port())
+        _run(launch + ["consensus"] + base +
+             ["--local-density-threshold", str(a.local_density_threshold)], env=env)
     return 0
 
 

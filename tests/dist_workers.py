@@ -96,3 +96,15 @@ def resume_worker(rank, world, port, output_dir, name):
     distributed_factorize(cNMF(output_dir=output_dir, name=name), skip_completed_runs=True,
                           backend="gloo", verbose=False)
     dist.destroy_process_group()
+
+
+def consensus_worker(rank, world, port, output_dir, name, ks):
+    _init(rank, world, port)
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.parallel.runner import distributed_consensus, distributed_k_selection
+
+    obj = cNMF(output_dir=output_dir, name=name)
+    distributed_k_selection(obj, backend="gloo")
+    distributed_consensus(obj, ks, density_threshold=0.5, show_clustering=False,
+                          backend="gloo")
+    dist.destroy_process_group()

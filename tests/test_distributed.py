@@ -101,6 +101,40 @@ def test_distributed_factorize_matches_serial(prepared, mode):
             assert 0.9 < e_dp[key] / e_se[key] < 1.1, (key, e_dp[key], e_se[key])
 
 
+def test_k_parallel_consensus_and_k_selection_match_serial(prepared):
+    """distributed_consensus / distributed_k_selection (Ks dealt over 2 gloo ranks) write
+    the same artifacts as the serial stages."""
+    import glob
+
+    d, fn = prepared
+    obj = cNMF(output_dir=str(d), name="kpar")
+    obj.prepare(fn, components=[3, 4, 5], n_iter=4, seed=5, num_highvar_genes=120,
+                batch_size=150)
+    obj.factorize()
+    obj.combine()
+    keys = ("consensus_spectra", "consensus_usages", "gene_spectra_score",
+            "gene_spectra_tpm", "starcat_spectra")
+    ser_stats = obj.k_selection_plot(close_fig=True)
+    ser = {}
+    for k in (3, 4, 5):
+        obj.consensus(k, 0.5, show_clustering=False, close_clustergram_fig=True)
+        ser.update({(key, k): load_df_from_npz(obj.paths[key] % (k, "0_5")).values
+                    for key in keys})
+    # drop every serial output (and the density caches) so the ranks recompute them
+    outs = [obj.paths["k_selection_stats"]] + [obj.paths[key] % (k, "0_5")
+                                               for key in keys for k in (3, 4, 5)]
+    outs += glob.glob(str(d / "kpar" / "cnmf_tmp" / "*local_density_cache*"))
+    for f in outs:
+        os.remove(f)
+    _spawn(W.consensus_worker, 2, str(d), "kpar", [3, 4, 5])
+    par_stats = load_df_from_npz(obj.paths["k_selection_stats"])
+    np.testing.assert_allclose(par_stats.values.astype(float),
+                               ser_stats.values.astype(float), rtol=1e-6)
+    for (key, k), v in ser.items():
+        np.testing.assert_allclose(load_df_from_npz(obj.paths[key] % (k, "0_5")).values, v,
+                                   rtol=1e-6, atol=1e-12, err_msg=f"{key} k={k}")
+
+
 def test_rank_failure_then_resume_on_a_different_world_size(prepared):
     """a rank dies mid-factorize; a restart with --skip-completed-runs
     semantics on a different world size re-shards only the missing replicates, and the

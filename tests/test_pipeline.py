@@ -210,6 +210,26 @@ def test_run_parallel_driver_with_workers(tmp_path):
     assert os.path.exists(obj.paths["k_selection_stats"])
 
 
+def test_run_parallel_driver_with_torchrun_ranks(tmp_path):
+    """C39 over torchrun (gloo on the CPU here, RCCL on GPUs): replicate-parallel
+    factorize, then K-parallel k_selection_plot and consensus over 2 ranks."""
+    Xc, cells, genes = simulate_counts(150, 80, 3, seed=3, sparse=False)
+    fn = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(Xc, index=cells, columns=genes), fn)
+    cmd = [sys.executable, "-m", "cnmf_torch_amd.run_parallel", "--output-dir", str(tmp_path),
+           "--name", "rt", "-c", fn, "-k", "3", "4", "5", "-n", "4", "--seed", "2",
+           "--numgenes", "50", "--gpus", "2", "--local-density-threshold", "2.0"]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    obj = cNMF(output_dir=str(tmp_path), name="rt")
+    stats = load_df_from_npz(obj.paths["k_selection_stats"])
+    assert list(stats["k"].astype(int)) == [3, 4, 5]
+    for k in (3, 4, 5):
+        assert load_df_from_npz(obj.paths["consensus_spectra"] % (k, "2_0")).shape == (k, 50)
+        assert load_df_from_npz(obj.paths["consensus_usages"] % (k, "2_0")).shape == (150, k)
+
+
 def test_replicate_manifest_detects_corruption(tmp_path):
     Xc, cells, genes = simulate_counts(120, 70, 3, seed=4, sparse=False)
     fn = str(tmp_path / "c.df.npz")
