@@ -54,7 +54,7 @@ def build_parser() -> argparse.ArgumentParser:
                    help="[prepare] Treat the input data as non-sparse (default False)")
     p.add_argument("--batch_size", type=int, default=5000,
                    help="[prepare] Size of batch for online NMF learning.")
-    p.add_argument("--algo", type=str, default="mu", choices=["mu", "hals", "bpp"],
+    p.add_argument("--algo", type=str, default="mu", choices=["mu", "hals", "halsvar", "bpp"],
                    help="[prepare] NMF update rule (addition; reference fixes mu)")
     p.add_argument("--mode", type=str, default="online", choices=["online", "batch"],
                    help="[prepare] NMF mode (addition; reference fixes online)")

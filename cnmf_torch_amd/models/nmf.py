@@ -18,8 +18,9 @@ are kept TRANSPOSED, ``HT`` (R*K, N), so a replicate's chunk block is K rows of
 contiguous cells -- coalesced for the solve kernel and directly the GEMM operand.
 
 Algorithms (nmf-torch surface; cnmf.py:757-771 fixes algo='mu', mode='online'):
-  algo  in {'mu', 'hals', 'bpp'} (HALS, BPP: Frobenius only; bpp = exact NNLS half-steps,
-                                 models/bpp.py)
+  algo  in {'mu', 'hals', 'halsvar', 'bpp'} (all but MU: Frobenius only; bpp = exact
+                                 NNLS half-steps, models/bpp.py; halsvar = HALS inner loops
+                                 run to ``batch_hals_tol`` to mimic bpp's exact half-steps)
   mode  in {'online', 'batch'}
   beta_loss in {'frobenius', 'kullback-leibler', 'itakura-saito'} or a float
 Online (Mairal-style sufficient statistics): per pass, chunks of ``online_chunk_size``
@@ -30,8 +31,12 @@ A pass ends with the loss; stop when (prev - cur) / init < tol or after
 for every replicate of a batch -- required for batching; documented deviation from a
 shuffled order).  For beta != 2, the W-step accumulates the MU numerator/denominator
 with the current W and applies one multiplicative step per chunk.
-Batch: alternate one H-step and one W-step (HALS: inner loops to ``batch_hals_tol``),
-loss every ``loss_every`` iterations, stop as sklearn's MU solver does.
+Batch: alternate one H-step and one W-step -- one MU / HALS sweep each ('mu', 'hals'),
+HALS inner loops to ``batch_hals_tol`` / ``batch_hals_max_iter`` ('halsvar'), or an exact
+NNLS solve ('bpp') -- loss every ``loss_every`` iterations, stop as sklearn's MU solver
+does.  In online mode 'halsvar' equals 'hals' (the chunk solves already iterate to
+``online_h_tol`` / ``online_w_tol``).  nmf-torch is not installed here, so the
+hals / halsvar split follows its documented parameter roles (parity unpinned).
 
 Data parallel (cell-sharded) runs pass a communicator: the flat per-chunk ``[dB | dA]``
 increment is all-reduced once per online step, so W, the loss and every convergence
@@ -97,11 +102,11 @@ class NMFOptions:
         return cls(n_components=int(n_components), **{k: v for k, v in kw.items() if k in names})
 
     def validate(self) -> None:
-        if self.algo not in ("mu", "hals", "bpp"):
-            raise ValueError(f"algo must be 'mu', 'hals' or 'bpp', got {self.algo!r}")
+        if self.algo not in ("mu", "hals", "halsvar", "bpp"):
+            raise ValueError(f"algo must be 'mu', 'hals', 'halsvar' or 'bpp', got {self.algo!r}")
         if self.mode not in ("online", "batch"):
             raise ValueError(f"mode must be 'online' or 'batch', got {self.mode!r}")
-        if self.algo in ("hals", "bpp") and beta_value(self.beta_loss) != 2.0:
+        if self.algo in ("hals", "halsvar", "bpp") and beta_value(self.beta_loss) != 2.0:
             raise ValueError(f"{self.algo.upper()} is defined for the Frobenius loss only")
         if self.init not in ("random", "nndsvd", "nndsvda", "nndsvdar"):
             raise ValueError(f"unsupported init {self.init!r}")
@@ -452,7 +457,7 @@ def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch
     kernels (ops.solve); 'bpp' solves every column's NNLS exactly (models/bpp.py) and
     fills the same optional outputs: lin/quad (trace-trick loss terms) and iters."""
     if algo != "bpp":
-        ops.solve(algo, x3, numer3, gram3, **kw)
+        ops.solve("hals" if algo == "halsvar" else algo, x3, numer3, gram3, **kw)
         return
     R, K = x3.shape[0], x3.shape[1]
     active = kw.get("active")
@@ -798,9 +803,9 @@ class NMFBatchSolver:
         N, G = X.shape
         dev, dt = X.device, X.dtype
         self._init_err_frob(st)
-        hals = o.algo == "hals"
-        h_iter = o.batch_hals_max_iter if hals else 1
-        h_tol = o.batch_hals_tol if hals else -1.0
+        inner = o.algo == "halsvar"          # HALS loops to tolerance; else one sweep
+        h_iter = o.batch_hals_max_iter if inner else 1
+        h_tol = o.batch_hals_tol if inner else -1.0
         max_it = int(o.batch_max_iter)
         every = max(1, int(o.loss_every))
         pipe = _PassPipeline(st)
@@ -822,7 +827,7 @@ class NMFBatchSolver:
             # H-step over all local cells
             WWT = ops.gram(W3, active=st.active_mask())
             numerT = W @ X.t()
-            nsplit = 1 if hals else max(1, (N + 8191) // 8192)
+            nsplit = 1 if inner else max(1, (N + 8191) // 8192)
             _inner_solve(o.algo, HT.view(n, K, N), numerT.view(n, K, N), WWT,
                       max_iter=h_iter, tol=h_tol, l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
                       nsplit=nsplit, active=active, iters_out=st.h_iters[:n])

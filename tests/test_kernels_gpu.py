@@ -178,7 +178,7 @@ def test_philox_matches_numpy(mode):
 
 
 @pytest.mark.parametrize("algo,beta_loss", [("mu", "frobenius"), ("hals", "frobenius"),
-                                            ("mu", "kullback-leibler")])
+                                            ("halsvar", "frobenius"), ("mu", "kullback-leibler")])
 @pytest.mark.parametrize("mode", ["online", "batch"])
 def test_nmf_batch_gpu_matches_cpu(algo, mode, beta_loss):
     from cnmf_torch_amd.models.nmf import run_nmf_batch

@@ -113,3 +113,20 @@ def test_nndsvd_init_matches_sklearn(variant):
     # randomized vs exact SVD: agree to the randomized solver's accuracy
     np.testing.assert_allclose(H.numpy(), Wsk, rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(W.numpy(), Hsk, rtol=1e-5, atol=1e-6)
+
+
+def test_halsvar_inner_loops_and_online_equivalence():
+    """'halsvar' (batch): HALS half-steps iterated to batch_hals_tol reach a lower error
+    per outer iteration than one-sweep 'hals'; online, both are the same chunk solves."""
+    X = torch.from_numpy(normalized_counts_matrix(300, 120, 5, seed=21))
+    errs = {}
+    for algo in ("hals", "halsvar"):
+        _, _, errs[algo] = run_nmf(X, 5, algo=algo, mode="batch", batch_max_iter=5, tol=-1.0,
+                                   random_state=3)
+    assert errs["halsvar"] < errs["hals"]
+    on = {a: run_nmf(X, 5, algo=a, mode="online", online_chunk_size=100, online_max_pass=4,
+                     random_state=3) for a in ("hals", "halsvar")}
+    for x, y in zip(on["hals"], on["halsvar"]):
+        np.testing.assert_array_equal(x, y)
+    with pytest.raises(ValueError):
+        NMFOptions(n_components=3, algo="halsvar", beta_loss="kullback-leibler").validate()
