@@ -33,8 +33,8 @@ BASELINE_REPS_PER_SEC = 0.5  # PBMC3k, 120 replicates in ~240 s (CP
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cells", type=int, default=10000)
     ap.add_argument("--genes", type=int, default=2000)
     ap.add_argument("--k", type=int, default=10)
