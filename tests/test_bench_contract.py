@@ -1,0 +1,45 @@
+"""bench.py contract: one JSON line from rank 0, whole-job value, max-over-ranks timing.
+Runs the multi-rank path on the CPU (gloo, 2 ranks via torch.distributed.run)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _bench(extra, nproc):
+    tiny = ["--cpu", "--cells", "300", "--genes", "60", "--k", "4", "--n-iter", "3",
+            "--batch-size", "100", "--max-nmf-iter", "50", "--steps", "2", "--warmup", "1"]
+    if nproc == 1:
+        cmd = [sys.executable, "bench.py"] + tiny + extra
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1", "--master-port",
+               str(_port()), "bench.py", "--gpus", str(nproc)] + tiny + extra
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 only
+    return json.loads(lines[0])
+
+
+def test_bench_json_contract_two_ranks():
+    out = _bench([], 2)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in out, key
+    assert out["n_gpus"] == 2 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["scaling"] == "weak" and out["higher_is_better"] is True
+    assert out["config"]["global_batch"] == 6            # 3 replicates per rank
+    # value is the whole-job rate: global replicates * steps / (max-rank) elapsed
+    rate = 6 * 2 / (out["ms_per_step"] * 2 / 1000.0)
+    assert abs(out["value"] - rate) / out["value"] < 0.01
