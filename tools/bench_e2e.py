@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--threshold", type=float, default=0.1)
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--profile", default=None, help="cProfile every stage into this file")
+    ap.add_argument("--kmeans-backend", default="sklearn", choices=["sklearn", "device"],
+                    help="sklearn = the reference's exact KMeans; device = batched GPU restarts")
     a = ap.parse_args()
     work = a.workdir or tempfile.mkdtemp(prefix="cnmf_e2e_")
     X, cells, genes = simulate_counts(a.cells, a.genes, a.programs, seed=0, sparse=True)
@@ -53,10 +55,12 @@ def main():
     kmid = ks[len(ks) // 2]
     stages = [("factorize", lambda: obj.factorize(verbose=False)),
               ("combine", obj.combine),
-              ("k_selection_plot", lambda: obj.k_selection_plot(close_fig=True)),
+              ("k_selection_plot", lambda: obj.k_selection_plot(close_fig=True,
+                                                               kmeans_backend=a.kmeans_backend)),
               ("consensus", lambda: obj.consensus(kmid, density_threshold=a.threshold,
                                                   show_clustering=True,
-                                                  close_clustergram_fig=True))]
+                                                  close_clustergram_fig=True,
+                                                  kmeans_backend=a.kmeans_backend))]
     prof_out = open(a.profile, "w") if a.profile else None
     for name, fn in stages:
         if prof_out:
@@ -82,7 +86,7 @@ def main():
         "metric": "cNMF end-to-end wall-clock", "unit": "s", "value": round(total, 3),
         "stages_s": {k: round(v, 3) for k, v in t.items()},
         "factorize_replicates_per_s": round(n_rep / t["factorize"], 2),
-        "config": {"cells": a.cells, "genes": a.genes, "hvg": a.hvg, "k": [a.kmin, a.kmax],
+        "config": {"kmeans_backend": a.kmeans_backend, "cells": a.cells, "genes": a.genes, "hvg": a.hvg, "k": [a.kmin, a.kmax],
                    "n_iter": a.n_iter, "replicates": n_rep,
                    "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"},
         "data": "synthetic sparse counts (planted programs)"}))
