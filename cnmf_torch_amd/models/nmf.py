@@ -93,6 +93,10 @@ class NMFOptions:
     online_stats: str = "pass"  # "pass": A,B reset each pass (Mairal); "exact": A=H^T H, B=H^T X of current H
     online_inner_conv: str = "loss"  # 'loss': block objective every inner_check_every steps; 'iterate'
     inner_check_every: int = 10
+    # beta != 2 online spectra iterations stop on the relative iterate change (the block
+    # objective would cost a pass over the chunk per evaluation); online_w_tol's 0.05 stops
+    # them after one step, which left online KL/IS unconverged after 20 passes
+    online_beta_w_tol: float = 5e-3
     loss_every: int = 10
     eps: float = 1e-16
 
@@ -880,15 +884,20 @@ class NMFBatchSolver:
                           act=act, tol=tol, iters=iters, den_vec=den_vec)
 
     def _beta_h_solve(self, xc, hc, W3, act, iters, block: int = 8) -> None:
-        """Inner usage loop of one chunk: up to ``online_chunk_max_iter`` fused MU steps,
-        each replicate stopping on device at ``online_h_tol`` (clears its ``act`` flag).
-        Steps are enqueued in blocks; whether anybody is still active is read from a
-        pinned copy one block late, so the GPU always has a block queued and the host
-        never drains the stream (launches for finished replicates exit at once)."""
+        """Inner usage loop of one chunk: up to ``online_chunk_max_iter`` fused MU steps.
+        Each replicate stops on device: with ``online_inner_conv='loss'`` when the chunk's
+        beta-divergence changed by <= ``online_h_tol`` (relative) over
+        ``inner_check_every`` steps (the Frobenius solve's block-objective rule), else on
+        the relative iterate change.  Steps are enqueued in blocks; whether anybody is
+        still active is read from a pinned copy one block late, so the GPU always has a
+        block queued and the host never drains the stream (launches for finished
+        replicates exit at once)."""
         o = self.opts
         W3 = W3.contiguous() if W3.stride(-1) != 1 else W3
         den_vec = (W3.sum(dim=2, dtype=torch.float32).contiguous()
                    if self.beta == 1.0 and xc.device.type == "cuda" else None)
+        cmode = 1 if o.online_inner_conv == "loss" else 0
+        hstate = torch.zeros((W3.shape[0], 2), dtype=torch.float64, device=xc.device)
         max_it = int(o.online_chunk_max_iter)
         cuda = xc.device.type == "cuda"
         pending = None
@@ -896,8 +905,10 @@ class NMFBatchSolver:
         while it < max_it:
             m = min(block, max_it - it)
             for _ in range(m):
-                self._beta_h_update(xc, hc, W3, o.l1_H, o.l2_H, act, o.online_h_tol, iters,
-                                    den_vec)
+                ops.beta_update_h(xc, hc, W3, self.beta, o.eps, o.l1_H, o.l2_H,
+                                  self._beta_gamma(), act=act, tol=o.online_h_tol, iters=iters,
+                                  den_vec=den_vec, conv_mode=cmode,
+                                  check_every=o.inner_check_every, hstate=hstate)
             it += m
             if not cuda:
                 if int(act.sum()) == 0:
@@ -920,6 +931,84 @@ class NMFBatchSolver:
             den = H3c.sum(dim=2, keepdim=True)              # KL: row sums of H
         return num, den
 
+    def _beta_w_solve(self, blocks, H3, W3, An, Ad, live, iters, block: int = 4) -> None:
+        """Spectra iterations of one online step (rows ``blocks``; all-reduced under DP).
+
+        Anchored incremental majorisation: every chunk c visited this pass contributes
+        An += W_c^(1/gamma) * num_c and Ad += den_c, its MU statistics anchored at the
+        spectra W_c it was last stepped from, so W = ((An)/(Ad))^gamma minimises the sum
+        of the visited chunks' beta-MU majorisers (for one chunk: exactly sklearn's MU
+        step, sklearn/decomposition/_nmf.py:526-728; Lefevre et al. 2011's online IS-NMF
+        statistics, generalised to any beta).  The current chunk's term is re-anchored at
+        every iteration until |dW|/|W| < ``online_beta_w_tol`` or
+        ``online_chunk_max_iter``; its last anchor then joins An/Ad."""
+        o = self.opts
+        kl = self.beta == 1.0
+        n, K, G = W3.shape
+        X = self.X
+        dev, dt = X.device, X.dtype
+        g = self._beta_gamma()
+        rows = [(a, b) for (a, b) in blocks if b > a]
+        hsum = None
+        if kl:
+            hsum = torch.zeros((n, K), device=dev, dtype=dt)
+            for (a, b) in rows:
+                hsum += H3[:, :, a:b].sum(dim=2)
+            self.comm.allreduce_(hsum)
+        an_out = torch.zeros((n, K, G), device=dev, dtype=dt)
+        dn_out = None if kl else torch.zeros((n, K, G), device=dev, dtype=dt)
+        act = live.clone()
+        cuda = dev.type == "cuda"
+        dist = self.comm.is_distributed
+        max_it = int(o.online_chunk_max_iter)
+        pending = None
+        it = 0
+        while it < max_it:
+            m = min(block, max_it - it)
+            for _ in range(m):
+                num = den = None
+                for (a, b) in rows:
+                    nW, dW, _ = ops.beta_contract("w", X[a:b], H3[:, :, a:b], W3, self.beta,
+                                                  o.eps, active=act, reduce=False)
+                    if num is None:
+                        num, den = nW, dW
+                    else:   # several blocks of one step (single-process DP emulation)
+                        num = torch.cat([num, nW])
+                        den = torch.cat([den, dW]) if dW is not None else None
+                if num is None:    # no local rows (DP rank beyond the data)
+                    num = torch.zeros((1, n, K, G), device=dev, dtype=dt)
+                    den = None if kl else torch.zeros_like(num)
+                if dist:
+                    num = num.sum(0, keepdim=True)
+                    flat = num.reshape(-1) if kl else torch.cat(
+                        [num.reshape(-1), den.sum(0).reshape(-1)])
+                    self.comm.allreduce_(flat)
+                    num = flat[:n * K * G].view(1, n, K, G)
+                    den = None if kl else flat[n * K * G:].view(1, n, K, G)
+                ops.beta_w_update(W3, num.contiguous(), None if kl else den.contiguous(), hsum,
+                                  An, Ad, an_out, dn_out, self.beta, g, o.l1_W, o.l2_W, o.eps,
+                                  o.online_beta_w_tol, act, iters)
+            it += m
+            if not cuda:
+                if int(act.sum()) == 0:
+                    break
+                continue
+            flag = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            flag.copy_(act.max().view(1), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            prev, pending = pending, (ev, flag)
+            if prev is not None:
+                prev[0].synchronize()
+                if int(prev[1][0]) == 0:
+                    break
+        keep = (live != 0).view(n, 1, 1)
+        An += torch.where(keep, an_out, 0.0)
+        if kl:
+            Ad += torch.where(keep.view(n, 1), hsum, 0.0)
+        else:
+            Ad += torch.where(keep, dn_out, 0.0)
+
     def _loss_dev(self, HT: torch.Tensor, W: torch.Tensor, K: int) -> torch.Tensor:
         """sqrt(2 * D_beta(X || H W)) per replicate (beta != 2) as a float64 DEVICE tensor
         (no host round trip; all-reduced under DP)."""
@@ -932,17 +1021,19 @@ class NMFBatchSolver:
         return torch.sqrt(torch.clamp(2.0 * tot, min=0.0))
 
     def _online_beta(self, st: _Batch) -> None:
-        """Online beta-MU (nmf-torch mode='online', beta != 2): per chunk, the usages are
-        iterated to ``online_h_tol`` (relative change, per replicate, on device), then the
-        W-side statistics of the chunk are accumulated (all-reduced under DP) and W takes
-        one MU step with the running pass statistics.  The pass loss and the stop rule
-        stay on the device; the host reads the active flags one pass late through the
-        same speculative pass pipeline as the Frobenius path."""
-        o, comm = self.opts, self.comm
+        """Online beta-MU (nmf-torch mode='online', beta != 2; the mode the reference CLI
+        hard-codes, cnmf.py:765, for every --beta-loss, cnmf.py:1426).  Per step the usages
+        of its chunk are iterated to ``online_h_tol`` (_beta_h_solve), then the spectra to
+        ``online_beta_w_tol`` against the pass's anchored statistics (_beta_w_solve).  The
+        statistics restart every pass, as the Frobenius path's.  The pass loss and the
+        (prev - cur) / init < tol stop rule stay on the device; the host reads the active
+        flags one pass late through the same speculative pass pipeline."""
+        o = self.opts
         K = st.K
         X = self.X
         N, G = X.shape
         steps = self._steps(N)
+        kl = self.beta == 1.0
         self._init_err(st)
         pipe = _PassPipeline(st)
         max_pass = int(o.online_max_pass)
@@ -953,29 +1044,16 @@ class NMFBatchSolver:
             HT, W = st.views()
             W3 = W.view(n, K, G)
             H3 = HT.view(n, K, N)
-            num_acc = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
-            den_acc = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
+            An = torch.zeros((n, K, G), device=X.device, dtype=X.dtype)
+            Ad = torch.zeros((n, K) if kl else (n, K, G), device=X.device, dtype=X.dtype)
             live = st.active_mask().clone()
             for blocks in steps:
-                flat = torch.zeros(2 * n * K * G, device=X.device, dtype=X.dtype)
-                fnum = flat[:n * K * G].view(n, K, G)
-                fden = flat[n * K * G:].view(n, K, G)
                 for (a, b) in blocks:
                     if b <= a:
                         continue
-                    xc = X[a:b]
-                    hc = H3[:, :, a:b]
                     act = live.clone()
-                    self._beta_h_solve(xc, hc, W3, act, st.h_iters[:n])
-                    nW, dW = self._beta_w_stats(xc, hc, W3)
-                    fnum += nW
-                    fden += dW
-                comm.allreduce_(flat)
-                num_acc += fnum
-                den_acc += fden
-                self._mu_apply(W3, num_acc, den_acc, o.l1_W, o.l2_W,
-                               (live != 0).view(n, 1, 1))
-                st.w_iters[:n] += live
+                    self._beta_h_solve(X[a:b], H3[:, :, a:b], W3, act, st.h_iters[:n])
+                self._beta_w_solve(blocks, H3, W3, An, Ad, live, st.w_iters[:n])
             final = p + 1 == max_pass
             st.set_err(self._loss_dev(HT, W, K), p + 1, o.tol, final)
             if not pipe.after_enqueue():

@@ -64,6 +64,15 @@ def _stream_ptr(t: torch.Tensor) -> int:
 
 
 
+def _native_dtype_k(op: str, dtype: torch.dtype, K: int, max_k: int) -> None:
+    """A GPU operand outside what the native kernel handles is an error, never a silent
+    switch to eager PyTorch (module contract)."""
+    if dtype != torch.float32:
+        raise TypeError(f"{op}: the native gfx950 kernel computes in float32, got {dtype}")
+    if K > max_k:
+        raise ValueError(f"{op}: K={K} exceeds the native kernel's maximum {max_k}")
+
+
 def _check_block_view(name: str, t: torch.Tensor, R: int, K: int, n: int):
     if t.dim() != 3 or tuple(t.shape) != (R, K, n):
         raise ValueError(f"{name}: expected shape {(R, K, n)}, got {tuple(t.shape)}")
@@ -277,7 +286,8 @@ def beta_mode(beta: float) -> int:
 
 def beta_contract(side: str, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor,
                   beta: float, eps: float, want_num: bool = True, want_loss: bool = False,
-                  active: torch.Tensor | None = None, splits: int | None = None):
+                  active: torch.Tensor | None = None, splits: int | None = None,
+                  reduce: bool = True):
     """Fused beta-divergence MU contraction (csrc/kernels/beta_mu.hip).
 
     ``X`` (N, G) with unit column stride; ``HT3`` (R, K, N) and ``W3`` (R, K, G) views with
@@ -286,6 +296,8 @@ def beta_contract(side: str, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tenso
       side "w": num = HT Q  (R,K,G), den = HT D  (None when beta == 1: den is rowsum HT)
     ``want_loss`` (side "h") also returns sum D_beta(X || P) per replicate (float64).
     Replicates whose ``active`` flag is 0 are skipped (their outputs are unspecified).
+    ``reduce=False`` (side "w") returns num/den as (splits, R, K, G) partials, the operand
+    layout of :func:`beta_w_update` (which sums them itself).
     """
     s = {"h": 0, "w": 1}[side]
     R, K, N = HT3.shape
@@ -293,8 +305,14 @@ def beta_contract(side: str, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tenso
     if X.shape != (N, G) or W3.shape[:2] != (R, K):
         raise ValueError(f"beta_contract: X {tuple(X.shape)}, HT3 {tuple(HT3.shape)}, "
                          f"W3 {tuple(W3.shape)} are inconsistent")
-    if not use_native(HT3) or HT3.dtype != torch.float32 or K > _hip.beta_max_k():
-        return reference.beta_contract(s, X, HT3, W3, beta, eps, want_num, want_loss, active)
+    if not use_native(HT3):
+        num, den, loss = reference.beta_contract(s, X, HT3, W3, beta, eps, want_num, want_loss,
+                                                 active)
+        if not reduce and num is not None:
+            num = num.unsqueeze(0)
+            den = den.unsqueeze(0) if den is not None else None
+        return num, den, loss
+    _native_dtype_k("beta_contract", HT3.dtype, K, _hip.beta_max_k())
     for name, t in (("X", X), ("HT3", HT3), ("W3", W3)):
         if t.dtype != torch.float32 or t.device != HT3.device:
             raise ValueError(f"{name}: float32 on {HT3.device} required")
@@ -331,7 +349,9 @@ def beta_contract(side: str, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tenso
                        den.data_ptr() if den is not None else 0,
                        loss.data_ptr() if loss is not None else 0,
                        active.data_ptr() if active is not None else 0, n_split, 0, 0, 0.0, 0.0,
-                       1.0, 0.0, 0, 0, 0, 0, _stream_ptr(HT3))
+                       1.0, 0.0, 0, 0, 0, 0, 0, 1, 0, _stream_ptr(HT3))
+    if num is not None and not reduce:
+        return num, den, None
     if num is not None:
         num = num[0] if n_split == 1 else num.sum(0)
         if den is not None:
@@ -348,18 +368,29 @@ def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: fl
                   l1: float = 0.0, l2: float = 0.0, gamma: float = 1.0,
                   act: torch.Tensor | None = None, tol: float | None = None,
                   iters: torch.Tensor | None = None,
-                  den_vec: torch.Tensor | None = None) -> None:
+                  den_vec: torch.Tensor | None = None, conv_mode: int = 0,
+                  check_every: int = 10, hstate: torch.Tensor | None = None) -> None:
     """One fused in-place beta-MU step of the usages: HT3 *= (num/(den+l1+l2 HT3))^gamma
     with num/den from the H-side contraction -- the numerator never leaves registers.
 
     ``act`` (int32 (R,), optional) gates replicates; with ``tol`` the kernel also applies
     the inner stopping rule on device: act[r] = 0 once ||dh||/(||h||+eps) < tol, and
     iters[r] += 1 for every replicate that stepped.  ``den_vec`` (KL only): the row sums
-    of W3 as contiguous float32 (R, K) -- pass it when W3 is fixed across many steps."""
+    of W3 as contiguous float32 (R, K) -- pass it when W3 is fixed across many steps.
+    ``conv_mode`` 1 replaces the iterate-change rule by the block objective: the chunk's
+    beta-divergence (of the usages BEFORE the step) is recorded every ``check_every``
+    steps in ``hstate`` (float64 (R, 2): last objective, steps; zero it before a solve)
+    and a replicate stops after a step where it changed by <= tol relative."""
     R, K, N = HT3.shape
     G = W3.shape[2]
-    if not use_native(HT3) or HT3.dtype != torch.float32 or K > _hip.beta_max_k():
-        return reference.beta_update_h(X, HT3, W3, beta, eps, l1, l2, gamma, act, tol, iters)
+    if tol is not None and conv_mode == 1 and (
+            hstate is None or hstate.dtype != torch.float64 or hstate.numel() < 2 * R
+            or not hstate.is_contiguous() or hstate.device != HT3.device):
+        raise ValueError("conv_mode 1 needs hstate: contiguous float64 (R, 2) on the device")
+    if not use_native(HT3):
+        return reference.beta_update_h(X, HT3, W3, beta, eps, l1, l2, gamma, act, tol, iters,
+                                       conv_mode, check_every, hstate)
+    _native_dtype_k("beta_update_h", HT3.dtype, K, _hip.beta_max_k())
     if X.shape != (N, G) or W3.shape[:2] != (R, K):
         raise ValueError("beta_update_h: inconsistent shapes")
     for name, t in (("X", X), ("HT3", HT3), ("W3", W3)):
@@ -384,8 +415,8 @@ def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: fl
     if tol is not None:
         key = (str(dev), _stream_ptr(HT3))
         ws = _BETA_WS.get(key)
-        if ws is None or ws["part"].numel() < R * n_strips * 2 or ws["counter"].numel() < R:
-            ws = {"part": torch.empty(max(R * n_strips * 2, 1 << 12), device=dev),
+        if ws is None or ws["part"].numel() < R * n_strips * 3 or ws["counter"].numel() < R:
+            ws = {"part": torch.empty(max(R * n_strips * 3, 1 << 12), device=dev),
                   "counter": torch.zeros(max(R, 1024), dtype=torch.int32, device=dev)}
             _BETA_WS[key] = ws
         part, counter = ws["part"], ws["counter"]
@@ -399,7 +430,61 @@ def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: fl
                        counter.data_ptr() if counter is not None else 0,
                        act.data_ptr() if (act is not None and tol is not None) else 0,
                        iters.data_ptr() if (iters is not None and tol is not None) else 0,
+                       int(conv_mode), int(check_every),
+                       hstate.data_ptr() if (hstate is not None and tol is not None) else 0,
                        _stream_ptr(HT3))
+
+
+def beta_w_update(W3: torch.Tensor, num: torch.Tensor, den: torch.Tensor | None,
+                  hsum: torch.Tensor | None, An: torch.Tensor, Ad: torch.Tensor,
+                  an_out: torch.Tensor, dn_out: torch.Tensor | None, beta: float, gamma: float,
+                  l1: float, l2: float, eps: float, tol: float, act: torch.Tensor,
+                  iters: torch.Tensor | None = None) -> None:
+    """One anchored online beta-MU step of the spectra, in place (beta_mu.hip
+    beta_w_update_kernel):  an = W^(1/gamma) num,  W <- ((An + an) / (Ad + den + l1 +
+    l2 W))^gamma, with num/den the (splits, R, K, G) partials of the chunk's W-side
+    contraction at the current W (den None for KL, whose denominator is ``hsum`` (R, K),
+    the chunk's usage sums; ``Ad`` is then (R, K)).  ``an_out``/``dn_out`` receive the
+    step's anchored statistics.  Replicates with act == 0 are untouched; the others stop
+    (act -> 0) once |dW| / (|W| + eps) < tol, and count the step in ``iters``."""
+    R, K, G = W3.shape
+    kl = beta == 1.0
+    if not use_native(W3):
+        return reference.beta_w_update(W3, num, den, hsum, An, Ad, an_out, dn_out, beta, gamma,
+                                       l1, l2, eps, tol, act, iters)
+    _native_dtype_k("beta_w_update", W3.dtype, K, 1 << 30)
+    splits = num.shape[0]
+    want = {"num": (num, (splits, R, K, G)), "An": (An, (R, K, G)), "an_out": (an_out, (R, K, G)),
+            "Ad": (Ad, (R, K) if kl else (R, K, G))}
+    if kl:
+        want["hsum"] = (hsum, (R, K))
+    else:
+        want["den"] = (den, (splits, R, K, G))
+        want["dn_out"] = (dn_out, (R, K, G))
+    for name, (t, shp) in want.items():
+        if (t is None or tuple(t.shape) != shp or t.dtype != torch.float32
+                or not t.is_contiguous() or t.device != W3.device):
+            raise ValueError(f"beta_w_update: {name} must be contiguous float32 {shp}")
+    if W3.stride(2) != 1:
+        raise ValueError("beta_w_update: W3 needs unit inner stride")
+    for name, t in (("act", act), ("iters", iters)):
+        if t is not None and (t.dtype != torch.int32 or t.numel() < R or not t.is_contiguous()):
+            raise ValueError(f"{name}: contiguous int32 with >= R entries")
+    nb = int(_hip.beta_w_update_blocks(K, G))
+    key = (str(W3.device), _stream_ptr(W3), "w")
+    ws = _BETA_WS.get(key)
+    if ws is None or ws["part"].numel() < R * nb * 2 or ws["counter"].numel() < R:
+        ws = {"part": torch.empty(max(R * nb * 2, 1 << 12), device=W3.device),
+              "counter": torch.zeros(max(R, 1024), dtype=torch.int32, device=W3.device)}
+        _BETA_WS[key] = ws
+    _hip.beta_w_update(beta_mode(beta), W3.data_ptr(), W3.stride(0), W3.stride(1),
+                       num.data_ptr(), den.data_ptr() if den is not None else 0,
+                       hsum.data_ptr() if hsum is not None else 0, An.data_ptr(), Ad.data_ptr(),
+                       an_out.data_ptr(), dn_out.data_ptr() if dn_out is not None else 0,
+                       R, K, G, splits, float(gamma), float(l1), float(l2), float(eps),
+                       float(tol), ws["part"].data_ptr(), ws["counter"].data_ptr(),
+                       act.data_ptr(), iters.data_ptr() if iters is not None else 0,
+                       _stream_ptr(W3))
 
 
 # ----------------------------------------------------------------------------- gram

@@ -192,10 +192,11 @@ def beta_contract(side: int, X, HT3, W3, beta: float, eps: float, want_num: bool
 
 
 def beta_update_h(X, HT3, W3, beta, eps, l1=0.0, l2=0.0, gamma=1.0, act=None, tol=None,
-                  iters=None):
+                  iters=None, conv_mode=0, check_every=10, hstate=None):
     """Reference of the fused in-place usage update (beta_mu.hip, upd != 0)."""
     R = HT3.shape[0]
-    num, den, _ = beta_contract(0, X, HT3, W3, beta, eps, True, False, act)
+    loss_rule = tol is not None and conv_mode == 1
+    num, den, f = beta_contract(0, X, HT3, W3, beta, eps, True, loss_rule, act)
     if den is None:
         den = W3.sum(dim=2, keepdim=True)
     d = den + l1 + l2 * HT3
@@ -205,12 +206,51 @@ def beta_update_h(X, HT3, W3, beta, eps, l1=0.0, l2=0.0, gamma=1.0, act=None, to
         delta = delta ** gamma
     live = torch.ones(R, dtype=torch.bool, device=HT3.device) if act is None else (act[:R] != 0)
     delta = torch.where(live.view(R, 1, 1), delta, torch.ones_like(delta))
-    if tol is not None:
+    if tol is not None and not loss_rule:
         dn = torch.linalg.vector_norm((HT3 * (delta - 1.0)).double(), dim=(1, 2))
         hn = torch.linalg.vector_norm(HT3.double(), dim=(1, 2))
     HT3.mul_(delta)
     if tol is not None:
-        stop = live & (dn / (hn + eps) < tol)
+        if loss_rule:
+            hs = hstate.view(-1, 2)[:R]
+            f = f.to(hs.device)
+            steps = hs[:, 1].long()
+            every = max(1, int(check_every))
+            at_check = live & (steps % every == 0)
+            conv = at_check & (steps > 0) & ((hs[:, 0] - f).abs() <= tol * hs[:, 0].abs())
+            hs[:, 0] = torch.where(at_check, f, hs[:, 0])
+            hs[:, 1] = torch.where(live, hs[:, 1] + 1, hs[:, 1])
+            stop = conv
+        else:
+            stop = live & (dn / (hn + eps) < tol)
         act[:R][stop] = 0
         if iters is not None:
             iters[:R] += live.to(iters.dtype)
+
+
+def beta_w_update(W3, num, den, hsum, An, Ad, an_out, dn_out, beta, gamma, l1, l2, eps, tol,
+                  act, iters=None):
+    """Reference of the anchored online spectra step (beta_mu.hip beta_w_update_kernel)."""
+    R = W3.shape[0]
+    live = act[:R] != 0
+    if not bool(live.any()):
+        return
+    nu = num.sum(0)
+    kl = beta == 1.0
+    dn = hsum.unsqueeze(2).expand_as(nu) if kl else den.sum(0)
+    ad = Ad.unsqueeze(2) if kl else Ad
+    an = W3 ** (1.0 / gamma) * nu
+    B = ad + dn + l1 + l2 * W3
+    B = torch.where(B == 0, torch.full_like(B, eps), B)
+    Wn = ((An + an) / B) ** gamma
+    m = live.view(R, 1, 1)
+    d = torch.linalg.vector_norm(torch.where(m, Wn - W3, 0).double(), dim=(1, 2))
+    o = torch.linalg.vector_norm(W3.double(), dim=(1, 2))
+    W3.copy_(torch.where(m, Wn, W3))
+    an_out.copy_(torch.where(m, an, an_out))
+    if not kl:
+        dn_out.copy_(torch.where(m, dn, dn_out))
+    stop = live & (d / (o + eps) < tol)
+    act[:R][stop] = 0
+    if iters is not None:
+        iters[:R] += live.to(iters.dtype)

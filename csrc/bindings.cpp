@@ -65,15 +65,30 @@ PYBIND11_MODULE(_hip, m) {
            long long ldh, uintptr_t W, long long w_rs, long long ldw, int N, int G, int K, int R,
            float beta, float eps, uintptr_t num, uintptr_t den, uintptr_t loss, uintptr_t active,
            int splits, int upd, uintptr_t den_vec, float l1, float l2, float gamma, float tol,
-           uintptr_t part, uintptr_t counter, uintptr_t act, uintptr_t iters, uintptr_t stream) {
+           uintptr_t part, uintptr_t counter, uintptr_t act, uintptr_t iters, int conv_mode,
+           int check_every, uintptr_t hstate, uintptr_t stream) {
           check(cnmf_beta_contract(side, mode, P<const float>(X), ldx, P<const float>(HT), h_rs,
                                    ldh, P<const float>(W), w_rs, ldw, N, G, K, R, beta, eps,
                                    P<float>(num), P<float>(den), P<double>(loss),
                                    P<const int>(active), splits, upd, P<const float>(den_vec),
                                    l1, l2, gamma, tol, P<float>(part), P<int>(counter),
-                                   P<int>(act), P<int>(iters),
-                                   reinterpret_cast<hipStream_t>(stream)),
+                                   P<int>(act), P<int>(iters), conv_mode, check_every,
+                                   P<double>(hstate), reinterpret_cast<hipStream_t>(stream)),
                 "beta_contract");
+        });
+  m.def("beta_w_update_blocks", [](int K, int G) { return cnmf_beta_w_update_blocks(K, G); });
+  m.def("beta_w_update",
+        [](int mode, uintptr_t W, long long w_rs, long long ldw, uintptr_t num, uintptr_t den,
+           uintptr_t hsum, uintptr_t An, uintptr_t Ad, uintptr_t an_out, uintptr_t dn_out, int R,
+           int K, int G, int splits, float gamma, float l1, float l2, float eps, float tol,
+           uintptr_t part, uintptr_t counter, uintptr_t act, uintptr_t iters, uintptr_t stream) {
+          check(cnmf_beta_w_update(mode, P<float>(W), w_rs, ldw, P<const float>(num),
+                                   P<const float>(den), P<const float>(hsum), P<const float>(An),
+                                   P<const float>(Ad), P<float>(an_out), P<float>(dn_out), R, K,
+                                   G, splits, gamma, l1, l2, eps, tol, P<float>(part),
+                                   P<int>(counter), P<int>(act), P<int>(iters),
+                                   reinterpret_cast<hipStream_t>(stream)),
+                "beta_w_update");
         });
 
   m.def("pairdist", [](uintptr_t A, long long lda, uintptr_t B, long long ldb, uintptr_t na,

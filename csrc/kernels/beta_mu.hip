@@ -61,10 +61,18 @@ struct BetaParams {
   float* HTw;           // writable alias of HT
   const float* den_vec; // (R, K) rowsums of W for KL
   float l1, l2, gamma, tol;
-  float* part;          // (R, n_strips, 2)
+  float* part;          // (R, n_strips, 3): |dh|^2, |h|^2, chunk loss
   int* counter;         // (R), zero before the first launch, left zero after every launch
   int* act;             // (R) active flags (the `active` input is usually this array)
   int* iters;           // (R)
+  // Inner stopping rule.  conv_mode 0: relative iterate change |dh|/(|h|+eps) < tol after
+  // every step.  conv_mode 1 (block objective, as the Frobenius solve's conv_mode 1): the
+  // chunk's beta-divergence D(x | h W) -- computed from the same P tiles the step uses --
+  // is recorded every `check_every` steps in hstate[r] = {f_prev, steps}; a replicate
+  // stops after the step at which |f_prev - f| <= tol |f_prev|.  The host zeroes hstate
+  // before each chunk solve.
+  int conv_mode, check_every;
+  double* hstate;       // (R, 2)
 };
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -145,6 +153,7 @@ __global__ void __launch_bounds__(kBetaThreads) beta_h_kernel(BetaParams p) {
     den[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const bool want_num = p.num != nullptr || p.upd;
+  const bool want_loss = p.loss != nullptr || (p.upd && p.part && p.conv_mode == 1);
   float lsum = 0.f;
   const float* __restrict__ xrow = p.X + (long long)(n_ok ? n : 0) * p.ldx;
 
@@ -181,7 +190,7 @@ __global__ void __launch_bounds__(kBetaThreads) beta_h_kernel(BetaParams p) {
         beta_terms<MODE>(xv[i], pc, p.beta, qv[i], dv[i]);
         qv[i] = ok ? qv[i] : 0.f;
         dv[i] = ok ? dv[i] : 0.f;
-        if (p.loss && ok) lsum += beta_loss_term<MODE>(xv[i], pc, p.beta, p.eps);
+        if (want_loss && ok) lsum += beta_loss_term<MODE>(xv[i], pc, p.beta, p.eps);
       }
       if (want_num) {
 #pragma unroll
@@ -223,26 +232,53 @@ __global__ void __launch_bounds__(kBetaThreads) beta_h_kernel(BetaParams p) {
     if (p.part) {
       __shared__ float sp[2 * (kBetaThreads / 64)];
       __shared__ int s_last;
+      __shared__ double sl[kBetaThreads / 64];
       block_sum2(d2, o2, sp);
+      double lt = 0.0;
+      if (p.conv_mode == 1) {
+        const double v = wave_sum((double)lsum);
+        if (lane == 0) sl[wave] = v;
+        __syncthreads();
+        for (int w = 0; w < kBetaThreads / 64; ++w) lt += sl[w];
+      }
       if (threadIdx.x == 0) {
-        float* pp = p.part + ((long long)rep * p.n_strips + strip) * 2;
+        // publish (cdna_hip_programming.md G16): plain stores -> drain -> agent release ->
+        // drain -> arrival counter
+        float* pp = p.part + ((long long)rep * p.n_strips + strip) * 3;
         pp[0] = d2;
         pp[1] = o2;
-        __threadfence();
-        const int prev = atomicAdd(p.counter + rep, 1);
+        pp[2] = (float)lt;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int prev = __hip_atomic_fetch_add(p.counter + rep, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
         s_last = (prev == p.n_strips - 1);
       }
       __syncthreads();
       if (s_last && threadIdx.x == 0) {
-        __threadfence();
-        double td = 0.0, to = 0.0;
-        const float* pr = p.part + (long long)rep * p.n_strips * 2;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        double td = 0.0, to = 0.0, tl = 0.0;
+        const float* pr = p.part + (long long)rep * p.n_strips * 3;
         for (int s2 = 0; s2 < p.n_strips; ++s2) {
-          td += __hip_atomic_load(pr + 2 * s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          to += __hip_atomic_load(pr + 2 * s2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          td += __hip_atomic_load(pr + 3 * s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          to += __hip_atomic_load(pr + 3 * s2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tl += __hip_atomic_load(pr + 3 * s2 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const double rel = sqrt(td) / (sqrt(to) + (double)p.eps);
-        if (rel < (double)p.tol) p.act[rep] = 0;
+        if (p.conv_mode == 1) {
+          double* hs = p.hstate + 2 * (long long)rep;
+          const int steps = (int)hs[1];
+          const int every = p.check_every > 0 ? p.check_every : 1;
+          if (steps % every == 0) {
+            if (steps > 0 && fabs(hs[0] - tl) <= (double)p.tol * fabs(hs[0])) p.act[rep] = 0;
+            hs[0] = tl;
+          }
+          hs[1] = (double)(steps + 1);
+        } else {
+          const double rel = sqrt(td) / (sqrt(to) + (double)p.eps);
+          if (rel < (double)p.tol) p.act[rep] = 0;
+        }
         if (p.iters) p.iters[rep] += 1;
         p.counter[rep] = 0;
       }
@@ -361,6 +397,102 @@ __global__ void __launch_bounds__(kBetaThreads) beta_w_kernel(BetaParams p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------- W update
+// One step of the online beta-MU spectra update with anchored sufficient statistics
+// (models/nmf.py _online_beta).  Per element, with num/den the chunk's W-side MU
+// statistics at the current W (summed over the contraction's split partials):
+//   an = W^(1/gamma) num          (the chunk's majoriser, anchored at this W)
+//   W' = ((An + an) / (Ad + den + l1 + l2 W))^gamma
+// where An/Ad hold the anchored statistics of the chunks already visited this pass.
+// an (and den, beta != 1) are written out so the caller can add the final anchor to
+// An/Ad.  For KL den is the chunk's per-component usage sum (hsum, (R, K)).  The
+// replicate's relative change |W' - W| / (|W| + eps) is reduced by the last-arriving
+// workgroup, which clears act[r] below tol and counts the step in iters[r].
+struct BetaWUpd {
+  float* W;
+  long long w_rs, ldw;
+  const float* num;     // (splits, R, K, G) contiguous
+  const float* den;     // same (beta != 1) or nullptr
+  const float* hsum;    // (R, K) (beta == 1)
+  const float* An;      // (R, K, G)
+  const float* Ad;      // (R, K, G) or (R, K) for beta == 1
+  float* an_out;        // (R, K, G)
+  float* dn_out;        // (R, K, G) (beta != 1) or nullptr
+  int R, K, G, splits, mode;
+  float gamma, l1, l2, eps, tol;
+  float* part;          // (R, nb, 2)
+  int* counter;
+  int* act;
+  int* iters;
+};
+
+__global__ void __launch_bounds__(256) beta_w_update_kernel(BetaWUpd p) {
+  const int rep = blockIdx.y;
+  if (p.act[rep] == 0) return;
+  const int nb = gridDim.x;
+  const long long KG = (long long)p.K * p.G;
+  const long long rstride = (long long)p.R * KG;
+  float d2 = 0.f, o2 = 0.f;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < KG;
+       e += (long long)nb * blockDim.x) {
+    const int k = (int)(e / p.G), g = (int)(e - (long long)k * p.G);
+    float* wp = p.W + rep * p.w_rs + k * p.ldw + g;
+    const float w = *wp;
+    const long long o = rep * KG + e;
+    float nu = 0.f, dn = 0.f;
+    for (int s = 0; s < p.splits; ++s) {
+      nu += p.num[s * rstride + o];
+      if (p.mode != kKL) dn += p.den[s * rstride + o];
+    }
+    if (p.mode == kKL) dn = p.hsum[rep * p.K + k];
+    float wg;                                   // W^(1/gamma)
+    if (p.gamma == 1.f) wg = w;
+    else if (p.gamma == 0.5f) wg = w * w;
+    else wg = __powf(w, 1.f / p.gamma);
+    const float an = wg * nu;
+    const float A = p.An[o] + an;
+    float B = (p.mode == kKL ? p.Ad[rep * p.K + k] : p.Ad[o]) + dn + p.l1 + p.l2 * w;
+    if (B == 0.f) B = p.eps;
+    float wn = A / B;
+    if (p.gamma == 0.5f) wn = sqrtf(wn);
+    else if (p.gamma != 1.f) wn = __powf(wn, p.gamma);
+    *wp = wn;
+    p.an_out[o] = an;
+    if (p.mode != kKL) p.dn_out[o] = dn;
+    d2 = fmaf(wn - w, wn - w, d2);
+    o2 = fmaf(w, w, o2);
+  }
+  __shared__ float sp[2 * 4];
+  __shared__ int s_last;
+  block_sum2(d2, o2, sp);
+  if (threadIdx.x == 0) {
+    float* pp = p.part + ((long long)rep * nb + blockIdx.x) * 2;
+    pp[0] = d2;
+    pp[1] = o2;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(p.counter + rep, 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == nb - 1);
+  }
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double td = 0.0, to = 0.0;
+    const float* pr = p.part + (long long)rep * nb * 2;
+    for (int b = 0; b < nb; ++b) {
+      td += __hip_atomic_load(pr + 2 * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      to += __hip_atomic_load(pr + 2 * b + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (sqrt(td) / (sqrt(to) + (double)p.eps) < (double)p.tol) p.act[rep] = 0;
+    if (p.iters) p.iters[rep] += 1;
+    p.counter[rep] = 0;
+  }
+}
+
 template <int KP4, int MODE>
 hipError_t launch_beta(int side, const BetaParams& p, hipStream_t s) {
   const int units = side == 0 ? p.n_strips : p.n_strips * p.splits;
@@ -402,13 +534,15 @@ extern "C" hipError_t cnmf_beta_contract(int side, int mode, const float* X, lon
                                          int splits, int upd, const float* den_vec, float l1,
                                          float l2, float gamma, float tol, float* part,
                                          int* counter, int* act, int* iters,
+                                         int conv_mode, int check_every, double* hstate,
                                          hipStream_t stream) {
   if (R <= 0 || N <= 0 || G <= 0) return hipSuccess;
   if (K < 1 || K > 32 || (side != 0 && side != 1)) return hipErrorInvalidValue;
   if (side == 1 && num == nullptr) return hipErrorInvalidValue;
   if (mode != 0 && num != nullptr && den == nullptr) return hipErrorInvalidValue;
   if (upd && (side != 0 || (mode == 0 && den_vec == nullptr) ||
-              (part != nullptr && (counter == nullptr || act == nullptr))))
+              (part != nullptr && (counter == nullptr || act == nullptr)) ||
+              (part != nullptr && conv_mode == 1 && hstate == nullptr)))
     return hipErrorInvalidValue;
   cnmf::BetaParams p;
   p.X = X; p.ldx = ldx;
@@ -427,6 +561,7 @@ extern "C" hipError_t cnmf_beta_contract(int side, int mode, const float* X, lon
   p.l1 = l1; p.l2 = l2; p.gamma = gamma; p.tol = tol;
   p.part = upd ? part : nullptr;
   p.counter = counter; p.act = act; p.iters = iters;
+  p.conv_mode = conv_mode; p.check_every = check_every; p.hstate = hstate;
   if (upd) p.num = nullptr;
   switch (mode) {
     case 0: return cnmf::launch_beta_mode<cnmf::kKL>(side, p, stream);
@@ -434,4 +569,34 @@ extern "C" hipError_t cnmf_beta_contract(int side, int mode, const float* X, lon
     case 2: return cnmf::launch_beta_mode<cnmf::kGeneral>(side, p, stream);
     default: return hipErrorInvalidValue;
   }
+}
+
+extern "C" int cnmf_beta_w_update_blocks(int K, int G) {
+  const long long kg = (long long)K * G;
+  long long nb = (kg + 2047) / 2048;
+  return (int)(nb < 1 ? 1 : (nb > 64 ? 64 : nb));
+}
+
+extern "C" hipError_t cnmf_beta_w_update(int mode, float* W, long long w_rs, long long ldw,
+                                         const float* num, const float* den, const float* hsum,
+                                         const float* An, const float* Ad, float* an_out,
+                                         float* dn_out, int R, int K, int G, int splits,
+                                         float gamma, float l1, float l2, float eps, float tol,
+                                         float* part, int* counter, int* act, int* iters,
+                                         hipStream_t stream) {
+  if (R <= 0) return hipSuccess;
+  if (K < 1 || G < 1 || splits < 1 || act == nullptr || part == nullptr || counter == nullptr)
+    return hipErrorInvalidValue;
+  if (mode == cnmf::kKL ? hsum == nullptr : (den == nullptr || dn_out == nullptr))
+    return hipErrorInvalidValue;
+  cnmf::BetaWUpd p;
+  p.W = W; p.w_rs = w_rs; p.ldw = ldw;
+  p.num = num; p.den = den; p.hsum = hsum; p.An = An; p.Ad = Ad;
+  p.an_out = an_out; p.dn_out = dn_out;
+  p.R = R; p.K = K; p.G = G; p.splits = splits; p.mode = mode;
+  p.gamma = gamma; p.l1 = l1; p.l2 = l2; p.eps = eps; p.tol = tol;
+  p.part = part; p.counter = counter; p.act = act; p.iters = iters;
+  const dim3 grid((unsigned)cnmf_beta_w_update_blocks(K, G), (unsigned)R);
+  hipLaunchKernelGGL(cnmf::beta_w_update_kernel, grid, dim3(256), 0, stream, p);
+  return hipGetLastError();
 }

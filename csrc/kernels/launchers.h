@@ -29,6 +29,14 @@ hipError_t cnmf_beta_contract(int side, int mode, const float* X, long long ldx,
                               float* num, float* den, double* loss, const int* active,
                               int splits, int upd, const float* den_vec, float l1, float l2,
                               float gamma, float tol, float* part, int* counter, int* act,
+                              int* iters, int conv_mode, int check_every, double* hstate,
+                              hipStream_t stream);
+int cnmf_beta_w_update_blocks(int K, int G);
+hipError_t cnmf_beta_w_update(int mode, float* W, long long w_rs, long long ldw,
+                              const float* num, const float* den, const float* hsum,
+                              const float* An, const float* Ad, float* an_out, float* dn_out,
+                              int R, int K, int G, int splits, float gamma, float l1, float l2,
+                              float eps, float tol, float* part, int* counter, int* act,
                               int* iters, hipStream_t stream);
 
 hipError_t cnmf_pairdist(const double* A, long long lda, const double* B, long long ldb,

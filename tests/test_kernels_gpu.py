@@ -193,6 +193,11 @@ def test_nmf_batch_gpu_matches_cpu(algo, mode, beta_loss):
     c = run_nmf_batch(X, K, [11, 12, 13], device="cpu", **kw)
     # same init, same algorithm: errors agree to fp32 reassociation noise
     np.testing.assert_allclose(g.err, c.err, rtol=2e-2)
+    # ... and so do the factors and the convergence bookkeeping
+    assert np.abs(g.n_iter - c.n_iter).max() <= 1, (g.n_iter, c.n_iter)
+    Wg, Wc = g.W.cpu().numpy(), c.W.cpu().numpy()
+    cos = (Wg * Wc).sum(1) / (np.linalg.norm(Wg, axis=1) * np.linalg.norm(Wc, axis=1) + 1e-30)
+    assert np.median(cos) > 0.99, np.sort(cos)[:5]
 
 
 @pytest.mark.parametrize("beta", [1.0, 0.0, 1.5])
@@ -548,3 +553,92 @@ def test_gram_kernel_matches_bmm(K):
             torch.testing.assert_close(out[r].cpu().double(), ref[r], rtol=1e-5, atol=1e-3)
         else:
             assert torch.all(out[r] == 2.0)
+
+
+@pytest.mark.parametrize("beta", [1.0, 0.0, 1.5])
+def test_beta_w_update_matches_reference(beta):
+    """Anchored online spectra step (beta_w_update_kernel) vs the float64 reference,
+    including the on-device relative-change stop and inactive replicates."""
+    g = torch.Generator().manual_seed(5)
+    R, K, N, G = 4, 7, 500, 333
+    gamma = 0.5 if beta < 1 else 1.0
+    kl = beta == 1.0
+    X = torch.rand((N, G), generator=g, dtype=torch.float64) + 0.05
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.1
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.1
+    An = torch.rand((R, K, G), generator=g, dtype=torch.float64)
+    Ad = torch.rand((R, K) if kl else (R, K, G), generator=g, dtype=torch.float64) + 0.5
+    dev = torch.device("cuda")
+    act0 = torch.tensor([1, 0, 1, 1], dtype=torch.int32)
+    hsum = HT.sum(dim=2) if kl else None
+    # CPU reference (float64)
+    Wr, anr = W.clone(), torch.zeros_like(W)
+    dnr = None if kl else torch.zeros_like(W)
+    ar, itr = act0.clone(), torch.zeros(R, dtype=torch.int32)
+    # GPU
+    Wg = W.float().to(dev)
+    ang = torch.zeros((R, K, G), device=dev)
+    dng = None if kl else torch.zeros((R, K, G), device=dev)
+    ag, itg = act0.to(dev), torch.zeros(R, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        nr, dr, _ = reference.beta_contract(1, X, HT, Wr, beta, 1e-10, True, False)
+        reference.beta_w_update(Wr, nr.unsqueeze(0), None if kl else dr.unsqueeze(0), hsum, An,
+                                Ad, anr, dnr, beta, gamma, 0.01, 0.02, 1e-10, 1e-3, ar, itr)
+        ng, dg, _ = ops.beta_contract("w", X.float().to(dev), HT.float().to(dev), Wg, beta,
+                                      1e-10, active=ag, reduce=False)
+        ops.beta_w_update(Wg, ng, dg, hsum.float().to(dev) if kl else None,
+                          An.float().to(dev), Ad.float().to(dev), ang, dng, beta, gamma, 0.01,
+                          0.02, 1e-10, 1e-3, ag, itg)
+    torch.cuda.synchronize()
+    live = [0, 2, 3]
+    torch.testing.assert_close(Wg.cpu().double()[live], Wr[live], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(ang.cpu().double()[live], anr[live], rtol=1e-4, atol=1e-4)
+    assert torch.equal(Wg[1].cpu(), W[1].float())            # inactive replicate untouched
+    assert itg.cpu().tolist() == itr.tolist()
+    assert ag.cpu().tolist() == ar.tolist()
+
+
+def test_beta_update_h_loss_rule_matches_reference():
+    """conv_mode 1 (block beta-divergence every check_every steps) on device == reference."""
+    g = torch.Generator().manual_seed(6)
+    R, K, N, G = 5, 6, 900, 210
+    X = torch.rand((N, G), generator=g, dtype=torch.float64) + 0.02
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.05
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.05
+    dev = torch.device("cuda")
+    hr, ar = HT.clone(), torch.ones(R, dtype=torch.int32)
+    itr, hsr = torch.zeros(R, dtype=torch.int32), torch.zeros((R, 2), dtype=torch.float64)
+    hg, ag = HT.float().to(dev), torch.ones(R, dtype=torch.int32, device=dev)
+    itg = torch.zeros(R, dtype=torch.int32, device=dev)
+    hsg = torch.zeros((R, 2), dtype=torch.float64, device=dev)
+    Xg, Wg = X.float().to(dev), W.float().to(dev)
+    for _ in range(40):
+        reference.beta_update_h(X, hr, W, 1.0, 1e-10, act=ar, tol=0.02, iters=itr, conv_mode=1,
+                                check_every=4, hstate=hsr)
+        ops.beta_update_h(Xg, hg, Wg, 1.0, 1e-10, act=ag, tol=0.02, iters=itg, conv_mode=1,
+                          check_every=4, hstate=hsg)
+    torch.cuda.synchronize()
+    assert itg.cpu().tolist() == itr.tolist(), (itg, itr)
+    assert ag.cpu().tolist() == ar.tolist()
+    torch.testing.assert_close(hsg.cpu()[:, 0], hsr[:, 0], rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(hg.cpu().double(), hr, rtol=2e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("beta_loss", ["kullback-leibler", "itakura-saito"])
+def test_online_beta_gpu_converges_like_cpu(beta_loss):
+    """Online beta-MU on the GPU converges (flags, passes) and lands within 1 % of batch,
+    with passes / inner iteration counts close to the CPU run of the same algorithm."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(3000, 400, n_programs=6, seed=0))
+    kw = dict(beta_loss=beta_loss, online_chunk_size=1000, online_chunk_max_iter=1000,
+              batch_max_iter=2000)
+    seeds = [1, 2, 3]
+    on_g = NMFBatchSolver(X.cuda(), NMFOptions(n_components=6, mode="online", **kw)).run(seeds)
+    on_c = NMFBatchSolver(X, NMFOptions(n_components=6, mode="online", **kw)).run(seeds)
+    ba_g = NMFBatchSolver(X.cuda(), NMFOptions(n_components=6, mode="batch", **kw)).run(seeds)
+    assert on_g.converged.all() and (on_g.n_iter < 20).all(), on_g.n_iter
+    assert (np.abs(on_g.err - ba_g.err) / ba_g.err < 0.01).all(), (on_g.err, ba_g.err)
+    np.testing.assert_allclose(on_g.err, on_c.err, rtol=5e-3)
+    assert np.abs(on_g.n_iter - on_c.n_iter).max() <= 3, (on_g.n_iter, on_c.n_iter)

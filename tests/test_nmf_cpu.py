@@ -130,3 +130,74 @@ def test_halsvar_inner_loops_and_online_equivalence():
         np.testing.assert_array_equal(x, y)
     with pytest.raises(ValueError):
         NMFOptions(n_components=3, algo="halsvar", beta_loss="kullback-leibler").validate()
+
+
+@pytest.mark.parametrize("beta_loss", ["kullback-leibler", "itakura-saito"])
+def test_online_beta_converges_close_to_batch(beta_loss):
+    """Online beta-MU (the mode the reference CLI hard-codes, cnmf.py:765, for every
+    --beta-loss, cnmf.py:1426) must converge like the Frobenius path: converged=True in
+    fewer than online_max_pass passes, final error within 1 % of batch MU."""
+    X = normalized_counts_matrix(3000, 400, n_programs=6, seed=0)
+    kw = dict(beta_loss=beta_loss, online_chunk_size=1000, online_chunk_max_iter=1000,
+              batch_max_iter=2000)
+    on = NMFBatchSolver(torch.from_numpy(X), NMFOptions(n_components=6, mode="online", **kw)).run([1, 2])
+    ba = NMFBatchSolver(torch.from_numpy(X), NMFOptions(n_components=6, mode="batch", **kw)).run([1, 2])
+    assert on.converged.all(), (on.n_iter, on.err)
+    assert (on.n_iter < 20).all(), on.n_iter
+    assert (np.abs(on.err - ba.err) / ba.err < 0.01).all(), (on.err, ba.err)
+    # the usage loop ran several steps per chunk (block-objective rule), not ~1
+    assert min(on.stats["h_inner_iters"]) >= 5 * 3 * min(on.n_iter)
+
+
+@pytest.mark.parametrize("beta,gamma", [(1.0, 1.0), (0.0, 0.5), (1.5, 1.0)])
+def test_beta_w_update_single_chunk_is_sklearn_mu_step(beta, gamma):
+    """With no earlier chunk statistics the anchored online spectra step is exactly one
+    multiplicative update W <- W (num/den)^gamma (sklearn _nmf.py:526-728)."""
+    g = torch.Generator().manual_seed(2)
+    R, K, N, G = 2, 3, 60, 40
+    X = torch.rand((N, G), generator=g, dtype=torch.float64) + 0.05
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.1
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.1
+    num, den, _ = reference.beta_contract(1, X, HT, W, beta, 1e-16, True, False)
+    if den is None:
+        den = HT.sum(dim=2, keepdim=True).expand_as(num)
+    expect = W * (num / den) ** gamma
+    Wc = W.clone()
+    kl = beta == 1.0
+    An = torch.zeros_like(W)
+    Ad = torch.zeros((R, K), dtype=W.dtype) if kl else torch.zeros_like(W)
+    an = torch.zeros_like(W)
+    dn = None if kl else torch.zeros_like(W)
+    nW, dW, _ = reference.beta_contract(1, X, HT, W, beta, 1e-16, True, False)
+    act = torch.ones(R, dtype=torch.int32)
+    it = torch.zeros(R, dtype=torch.int32)
+    reference.beta_w_update(Wc, nW.unsqueeze(0), None if kl else dW.unsqueeze(0),
+                            HT.sum(dim=2) if kl else None, An, Ad, an, dn, beta, gamma, 0.0,
+                            0.0, 1e-16, 1e-12, act, it)
+    torch.testing.assert_close(Wc, expect)
+    torch.testing.assert_close(an, W ** (1.0 / gamma) * num)
+    assert it.tolist() == [1, 1]
+
+
+def test_beta_h_loss_rule_checks_every_n_steps():
+    """conv_mode 1 of the fused usage step: the objective is recorded every check_every
+    steps and a replicate stops only at a check (never from the iterate change)."""
+    g = torch.Generator().manual_seed(4)
+    R, K, N, G = 3, 4, 80, 50
+    X = torch.rand((N, G), generator=g, dtype=torch.float64) + 0.05
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.1
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.1
+    act = torch.ones(R, dtype=torch.int32)
+    it = torch.zeros(R, dtype=torch.int32)
+    hs = torch.zeros((R, 2), dtype=torch.float64)
+    stopped_at = {}
+    for step in range(60):
+        reference.beta_update_h(X, HT, W, 1.0, 1e-16, act=act, tol=0.05, iters=it,
+                                conv_mode=1, check_every=5, hstate=hs)
+        for r in range(R):
+            if act[r] == 0 and r not in stopped_at:
+                stopped_at[r] = step
+        if act.sum() == 0:
+            break
+    assert stopped_at, "loose tolerance must stop"
+    assert all(s % 5 == 0 and s >= 5 for s in stopped_at.values()), stopped_at
