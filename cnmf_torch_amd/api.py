@@ -44,11 +44,10 @@ from .parallel.ledger import worker_filter
 from .utils.anndata_lite import AnnData
 from .utils.h5ad import read_h5ad, write_h5ad
 from .utils.io import (check_dir_exists, dump_yaml, load_df_from_npz, load_yaml, read_10x_mtx,
-                       read_any, read_counts_table, save_df_to_npz, save_df_to_text,
-                       NPZ_TMP_LEVEL,
-                       write_text_atomic)
+                       NpzTemplate, npy_bytes, read_any, read_counts_table, save_arrays_npz_digest, save_df_to_npz,
+                       save_df_to_text, NPZ_TMP_LEVEL, write_text_atomic)
 from .utils.log import get_logger
-from .utils.timing import StageTimer, append_jsonl, read_jsonl
+from .utils.timing import StageTimer, append_jsonl_many, read_jsonl
 
 log = get_logger("cnmf_torch_amd.api")
 
@@ -377,118 +376,165 @@ class cNMF:
 
     def factorize_jobs(self, jobs, worker_label=0, device=None, replicate_batch=None,
                        save_usages=False, verbose=True, run_params=None, comm=None,
-                       row_range=None):
+                       row_range=None, row_segments=None):
         """Factorise an explicit list of ledger rows.
 
-        ``comm``/``row_range`` run the cell-sharded data-parallel solver: this rank holds
-        rows [row_range) of norm_counts, the sufficient statistics are all-reduced per
-        step and only rank 0 writes spectra (usages stay rank-local)."""
+        ``comm`` with ``row_segments`` (global [start, stop) row segments, e.g.
+        parallel.runner.dp_row_segments) or ``row_range`` (one contiguous block) runs the
+        cell-sharded data-parallel solver: this rank holds those rows of norm_counts, the
+        sufficient statistics are all-reduced once per online step (one step per
+        segment) and only rank 0 writes spectra (usages stay rank-local)."""
         if run_params is None:
             run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
         if not jobs:
             return
+        if row_range is not None and row_segments is None:
+            row_segments = [tuple(int(v) for v in row_range)]
+            contiguous = True
+        else:
+            contiguous = False
         with self.timer("factorize"):
             kwargs = load_yaml(self.paths["nmf_run_parameters"])
             dev = _device(bool(kwargs.get("use_gpu", False)), device)
             if dev.type == "cpu" and kwargs.get("n_jobs", -1) not in (None, -1):
                 torch.set_num_threads(max(1, int(kwargs["n_jobs"])))
-            if row_range is None:
+            row_map = schedule = None
+            if row_segments is None:
                 norm_counts = read_h5ad(self.paths["normalized_counts"])
                 Xh = norm_counts.X
-                row0 = 0
+                cell_idx = np.arange(norm_counts.shape[0])
             else:
-                from .utils.h5ad import read_X_rows, read_h5ad_annotations
+                from .parallel.runner import dp_layout
+                from .utils.h5ad import read_X_row_segments, read_h5ad_annotations
 
                 norm_counts = read_h5ad_annotations(self.paths["normalized_counts"])
-                row0 = int(row_range[0])
-                Xh = read_X_rows(self.paths["normalized_counts"], row_range[0], row_range[1])
+                Xh = read_X_row_segments(self.paths["normalized_counts"], row_segments)
+                row_map, schedule = dp_layout(row_segments)
+                if contiguous:          # one block: the solver's own chunking
+                    schedule = None
+                cell_idx = np.concatenate([np.arange(a, b) for a, b in row_segments]) \
+                    if row_segments else np.zeros(0, dtype=np.int64)
             X = torch.from_numpy(_dense32(Xh)).to(dev)
             del Xh
             genes = norm_counts.var.index
-            cells = norm_counts.obs.index[row0:row0 + X.shape[0]]
+            cells = norm_counts.obs.index[cell_idx]
             writer = comm is None or comm.rank == 0
             fault_after = int(os.environ.get("CNMF_FAULT_AFTER_REPLICATES", "0") or 0)
             written = 0
-            # replicate files are compressed + written by a small thread pool (zlib drops
-            # the GIL) while the next batch runs on the GPU; every file is still atomic
-            pool = cf.ThreadPoolExecutor(max_workers=4)
+            # replicate files are encoded + hashed + written by a small thread pool (numpy
+            # and zlib drop the GIL) while the next batch runs on the GPU; every file is
+            # still atomic, and its sha256 is taken from the bytes in memory
+            pool = cf.ThreadPoolExecutor(max_workers=8)
             pending: list = []
             manifest = self.paths["replicate_manifest"]
+            gene_arr = np.asarray(genes.values).astype(str)
+            index_npy = {}
+            tmpl = NpzTemplate({"columns": gene_arr}) if NPZ_TMP_LEVEL <= 0 else None
 
-            def _write_spectra(df, path, k_, it_):
-                save_df_to_npz(df, path, level=NPZ_TMP_LEVEL)
-                append_jsonl(manifest, {"k": k_, "iter": it_, "file": os.path.basename(path),
-                                        "sha256": _sha256(path), "bytes": os.path.getsize(path)})
+            def _write_spectra(data, path, k_, it_):
+                if tmpl is not None:
+                    digest, size = tmpl.write(path, {"index": index_npy[k_], "data": data})
+                else:
+                    digest, size = save_arrays_npz_digest(
+                        path, {"data": data, "index": index_npy[k_], "columns": gene_arr},
+                        level=NPZ_TMP_LEVEL)
+                return {"k": k_, "iter": it_, "file": os.path.basename(path), "sha256": digest,
+                        "bytes": size}
 
             def _flush():
-                for f in pending:
-                    f.result()
+                recs = [f.result() for f in pending]
                 pending.clear()
-            by_k: dict[int, list[int]] = {}
-            for idx in jobs:
-                by_k.setdefault(int(run_params.iloc[idx]["n_components"]), []).append(idx)
-            for k, idxs in by_k.items():
-                bs = replicate_batch or self._auto_batch(X, k, len(idxs), dev)
-                if comm is not None:
-                    bs = -comm.allreduce_max_int(-bs)  # identical batching on every rank
-                solver = NMFBatchSolver(X, self._solver_options(kwargs, k), comm=comm,
-                                        row_offset=row0)
-                for b0 in range(0, len(idxs), bs):
-                    grp = idxs[b0:b0 + bs]
-                    if verbose:
-                        for idx in grp:
-                            print("[Worker %s]. Starting task %d." % (worker_label, idx), flush=True)
-                    seeds = [int(run_params.iloc[i]["nmf_seed"]) for i in grp]
-                    t0 = time.perf_counter()
-                    res = solver.run_concurrent(seeds, n_streams=int(
-                        os.environ.get("CNMF_STREAMS", "1")))
-                    W = res.W.cpu().numpy()
-                    wall = time.perf_counter() - t0
-                    log.info("k=%d: %d replicates in %.3f s (%.1f replicates/s) on %s", k,
-                             len(grp), wall, len(grp) / max(wall, 1e-9), dev)
-                    for r, idx in enumerate(grp):
-                        it = int(run_params.iloc[idx]["iter"])
-                        if writer:
-                            spectra = pd.DataFrame(W[r * k:(r + 1) * k],
-                                                   index=np.arange(1, k + 1), columns=genes)
-                            pending.append(pool.submit(_write_spectra, spectra,
-                                                       self.paths["iter_spectra"] % (k, it), k, it))
-                            append_jsonl(self.paths["replicate_log"], {
-                                "k": k, "iter": it, "seed": seeds[r], "worker": worker_label,
-                                "err": float(res.err[r]), "n_pass": int(res.n_iter[r]),
-                                "converged": bool(res.converged[r]),
-                                "h_inner_iters": int(res.stats["h_inner_iters"][r]),
-                                "w_inner_iters": int(res.stats["w_inner_iters"][r]),
-                                "batch_size": len(grp), "batch_wall_s": wall,
-                                "device": str(dev),
-                                "world": 1 if comm is None else comm.world_size})
-                        if save_usages:
-                            us = pd.DataFrame(res.usages(r).cpu().numpy(), index=cells,
-                                              columns=np.arange(1, k + 1))
-                            fn = self.paths["iter_usages"] % (k, it)
-                            if comm is not None and comm.world_size > 1:
-                                fn = fn.replace(".df.npz", ".rank%d.df.npz" % comm.rank)
-                            pending.append(pool.submit(save_df_to_npz, us, fn))
-                        written += 1
-                        if fault_after and written >= fault_after:
-                            _flush()
-                            pool.shutdown()
-                            raise RuntimeError(
-                                f"CNMF_FAULT_AFTER_REPLICATES={fault_after}: injected failure")
+                append_jsonl_many(manifest, [r for r in recs if r is not None])
+
+            nc = run_params["n_components"].to_numpy().astype(np.int64)
+            itv = run_params["iter"].to_numpy().astype(np.int64)
+            sdv = run_params["nmf_seed"].to_numpy().astype(np.int64)
+            jobs = sorted(jobs, key=lambda i: (int(nc[i]), i))
+            solver = NMFBatchSolver(X, self._solver_options(kwargs, int(nc[jobs[0]])),
+                                    comm=comm, row_map=row_map, schedule=schedule)
+            # Frobenius: the whole K x n_iter grid is ONE ragged batch (one pass loop, one
+            # data-side GEMM per chunk for every K) as far as device memory allows;
+            # beta != 2 solves one K at a time
+            for grp in self._job_batches(X, jobs, nc, dev, replicate_batch, comm,
+                                         mixed=solver.beta == 2.0):
+                if verbose:
+                    for idx in grp:
+                        print("[Worker %s]. Starting task %d." % (worker_label, idx), flush=True)
+                seeds = [int(sdv[i]) for i in grp]
+                ks = [int(nc[i]) for i in grp]
+                t0 = time.perf_counter()
+                if len(set(ks)) == 1 and int(os.environ.get("CNMF_STREAMS", "1")) > 1:
+                    solver.opts.n_components = ks[0]
+                    res = solver.run_concurrent(seeds, n_streams=int(os.environ["CNMF_STREAMS"]))
+                else:
+                    res = solver.run(seeds, ks=ks)
+                W = res.W.cpu().numpy()
+                wall = time.perf_counter() - t0
+                log.info("K=%s: %d replicates in %.3f s (%.1f replicates/s) on %s",
+                         sorted(set(ks)), len(grp), wall, len(grp) / max(wall, 1e-9), dev)
+                recs = []
+                for k in set(ks):
+                    index_npy.setdefault(k, npy_bytes(np.arange(1, k + 1)))
+                for r, idx in enumerate(grp):
+                    k, it = ks[r], int(itv[idx])
+                    if writer:
+                        pending.append(pool.submit(_write_spectra, W[res.rows(r)],
+                                                   self.paths["iter_spectra"] % (k, it), k, it))
+                        recs.append({
+                            "k": k, "iter": it, "seed": seeds[r], "worker": worker_label,
+                            "err": float(res.err[r]), "n_pass": int(res.n_iter[r]),
+                            "converged": bool(res.converged[r]),
+                            "h_inner_iters": int(res.stats["h_inner_iters"][r]),
+                            "w_inner_iters": int(res.stats["w_inner_iters"][r]),
+                            "batch_size": len(grp), "batch_wall_s": wall,
+                            "device": str(dev),
+                            "world": 1 if comm is None else comm.world_size})
+                    if save_usages:
+                        us = pd.DataFrame(res.usages(r).cpu().numpy(), index=cells,
+                                          columns=np.arange(1, k + 1))
+                        fn = self.paths["iter_usages"] % (k, it)
+                        if comm is not None and comm.world_size > 1:
+                            fn = fn.replace(".df.npz", ".rank%d.df.npz" % comm.rank)
+                        pending.append(pool.submit(lambda d, f: save_df_to_npz(d, f), us, fn))
+                    written += 1
+                    if fault_after and written >= fault_after:
+                        append_jsonl_many(self.paths["replicate_log"], recs)
+                        _flush()
+                        pool.shutdown()
+                        raise RuntimeError(
+                            f"CNMF_FAULT_AFTER_REPLICATES={fault_after}: injected failure")
+                append_jsonl_many(self.paths["replicate_log"], recs)
             _flush()
             pool.shutdown()
 
-    @staticmethod
-    def _auto_batch(X: torch.Tensor, k: int, n_jobs: int, dev: torch.device) -> int:
-        """Largest replicate batch whose working set fits ~40% of free device memory."""
+    def _job_batches(self, X: torch.Tensor, jobs, nc, dev, replicate_batch, comm, mixed):
+        """Consecutive runs of the K-sorted ``jobs`` solved as one batch each: up to
+        ``replicate_batch`` replicates, within ~40 % of free device memory, and (unless
+        ``mixed``) of a single K.  Identical on every rank under DP."""
         N, G = X.shape
-        per_rep = 4 * k * (N + 3 * G + 2 * min(N, 5000)) + 4 * k * k * 4
+        per_row = 4 * (N + 3 * G + 2 * min(N, 5000)) + 64
         if dev.type == "cuda":
             free, _ = torch.cuda.mem_get_info(dev)
-            budget = 0.4 * free
+            budget = int(0.4 * free)
         else:
-            budget = 8e9
-        return int(max(1, min(n_jobs, budget // max(per_rep, 1))))
+            budget = int(8e9)
+        max_rows = max(1, budget // per_row)
+        max_reps = int(replicate_batch) if replicate_batch else 1 << 30
+        if comm is not None:
+            max_rows = -comm.allreduce_max_int(-max_rows)
+            max_reps = -comm.allreduce_max_int(-max_reps)
+        out, cur, rows = [], [], 0
+        for i in jobs:
+            k = int(nc[i])
+            if cur and (len(cur) >= max_reps or rows + k > max_rows
+                        or (not mixed and int(nc[cur[-1]]) != k)):
+                out.append(cur)
+                cur, rows = [], 0
+            cur.append(i)
+            rows += k
+        if cur:
+            out.append(cur)
+        return out
 
     def verify_replicates(self, components=None) -> list[dict]:
         """Check every replicate spectra file against the write manifest (sha256 recorded

@@ -140,7 +140,10 @@ class NMFOptions:
 
 @dataclass
 class NMFResult:
-    """Batch result.  ``HT`` is (R*K, N_local) (usages transposed); ``W`` (R*K, G)."""
+    """Batch result in the callers' replicate order.  ``HT`` (sum_r K_r, N_local) holds the
+    usages transposed and ``W`` (sum_r K_r, G) the spectra; replicate r owns rows
+    ``offs[r] : offs[r] + ks[r]`` of both.  ``K`` is the common K of a single-K batch
+    (None for a mixed-K batch)."""
 
     HT: torch.Tensor
     W: torch.Tensor
@@ -148,16 +151,24 @@ class NMFResult:
     n_iter: np.ndarray
     converged: np.ndarray
     seeds: list
-    K: int
+    K: int | None
     stats: dict = field(default_factory=dict)
+    ks: np.ndarray | None = None
+
+    def __post_init__(self):
+        if self.ks is None:
+            self.ks = np.full(len(self.seeds), int(self.K), dtype=np.int64)
+        self.ks = np.asarray(self.ks, dtype=np.int64)
+        self.offs = np.concatenate([[0], np.cumsum(self.ks)[:-1]]).astype(np.int64)
+
+    def rows(self, r: int) -> slice:
+        return slice(int(self.offs[r]), int(self.offs[r] + self.ks[r]))
 
     def usages(self, r: int) -> torch.Tensor:
-        K = self.K
-        return self.HT[r * K:(r + 1) * K].t()
+        return self.HT[self.rows(r)].t()
 
     def spectra(self, r: int) -> torch.Tensor:
-        K = self.K
-        return self.W[r * K:(r + 1) * K]
+        return self.W[self.rows(r)]
 
 
 # =============================================================================== init
@@ -224,34 +235,50 @@ def _nndsvd(X: torch.Tensor, K: int, variant: str, comm, eps: float = 1e-6, seed
     return Wsk.to(X.dtype), Hsk.to(X.dtype)
 
 
-def init_factors(X: torch.Tensor, K: int, seeds, init: str = "random", comm=None,
-                 row_offset: int = 0):
-    """Initial (HT (R*K x N_loc), W (R*K x G)) for a replicate batch.
+def init_into(HT: torch.Tensor, W: torch.Tensor, X: torch.Tensor, K: int, seeds,
+              init: str = "random", comm=None, row_offset: int = 0,
+              mean: float | None = None, row_map=None) -> None:
+    """Fill the row blocks HT (R*K x N_loc) and W (R*K x G) with the initial factors of R
+    replicates of rank K (contiguous row blocks of a possibly larger ragged batch).
 
     random: |N(0,1)| * sqrt(mean(X)/K) from Philox keyed by each replicate's seed
     (H stream 0 over the canonical N x K matrix, W stream 1 over K x G), identical on
-    every device and for every rank/batch placement.
-    """
+    every device and for every rank/batch placement.  ``mean`` (global mean of X) may be
+    passed to skip its pass over X.  ``row_map`` [(local_start, local_stop,
+    global_start)] places non-contiguous global rows (a chunk-interleaved DP shard);
+    default: local rows are global rows ``row_offset + i``."""
     comm = comm or LocalComm()
     R = len(seeds)
     N, G = X.shape
-    dev, dt = X.device, X.dtype
-    HT = torch.empty((R * K, N), device=dev, dtype=dt)
-    W = torch.empty((R * K, G), device=dev, dtype=dt)
     if init == "random":
-        avg = math.sqrt(_global_mean(X, comm) / K)
+        if mean is None:
+            mean = _global_mean(X, comm)
+        avg = math.sqrt(mean / K)
         seeds_t = torch.tensor([int(s) for s in seeds], dtype=torch.int64)
         scales = torch.full((R,), avg, dtype=torch.float32)
-        if N:
-            # HT viewed as (R, N, K): element (r, j, k) -> HT[r*K + k, j]
-            ops.philox_fill(HT.as_strided((R, N, K), (K * N, 1, N)), seeds_t, scales,
-                            rng.STREAM_H, 0, row_offset)
+        ld = HT.stride(0)
+        for la, lb, ga in (row_map if row_map is not None else [(0, N, row_offset)]):
+            if lb > la:
+                # HT columns [la, lb) viewed as (R, n, K): element (r, j, k) -> HT[r*K+k, la+j]
+                ops.philox_fill(HT.as_strided((R, lb - la, K), (K * ld, 1, ld),
+                                              HT.storage_offset() + la),
+                                seeds_t, scales, rng.STREAM_H, 0, ga)
         ops.philox_fill(W.view(R, K, G), seeds_t, scales, rng.STREAM_W, 0, 0)
     else:
         Hn, Wn = _nndsvd(X, K, init, comm, seed=int(seeds[0]) if len(seeds) else 0)
         for r in range(R):
             HT[r * K:(r + 1) * K].copy_(Hn.t())
             W[r * K:(r + 1) * K].copy_(Wn)
+
+
+def init_factors(X: torch.Tensor, K: int, seeds, init: str = "random", comm=None,
+                 row_offset: int = 0):
+    """Initial (HT (R*K x N_loc), W (R*K x G)) for a single-K replicate batch."""
+    R = len(seeds)
+    N, G = X.shape
+    HT = torch.empty((R * K, N), device=X.device, dtype=X.dtype)
+    W = torch.empty((R * K, G), device=X.device, dtype=X.dtype)
+    init_into(HT, W, X, K, seeds, init, comm, row_offset)
     return HT, W
 
 
@@ -264,17 +291,69 @@ def _to_device(a: np.ndarray, dev: torch.device) -> torch.Tensor:
     return t
 
 
+def _ranges(starts: np.ndarray, sizes: np.ndarray) -> np.ndarray:
+    """Concatenation of ``arange(s, s + n)`` over the (start, size) pairs."""
+    starts = np.asarray(starts, dtype=np.int64)
+    sizes = np.asarray(sizes, dtype=np.int64)
+    tot = int(sizes.sum())
+    if tot == 0:
+        return np.zeros(0, dtype=np.int64)
+    first = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    return np.repeat(starts - first, sizes) + np.arange(tot, dtype=np.int64)
+
+
+@dataclass(frozen=True)
+class _Group:
+    """A run of live positions sharing one K: positions [p0, p0 + n), rows
+    [r0, r0 + n*K) of HT / W and K*K-blocks [q0, q0 + n*K*K) of the flat Gram buffers."""
+
+    K: int
+    p0: int
+    n: int
+    r0: int
+    q0: int
+
+    @property
+    def pos(self) -> slice:
+        return slice(self.p0, self.p0 + self.n)
+
+    @property
+    def rows(self) -> slice:
+        return slice(self.r0, self.r0 + self.n * self.K)
+
+    @property
+    def sq(self) -> slice:
+        return slice(self.q0, self.q0 + self.n * self.K * self.K)
+
+    def rep3(self, t: torch.Tensor) -> torch.Tensor:
+        """(n, K, cols) view of this group's rows of a (rows, cols) tensor or view."""
+        return t[self.rows].unflatten(0, (self.n, self.K))
+
+    def gram3(self, flat: torch.Tensor) -> torch.Tensor:
+        """(n, K, K) view of this group's block of a flat per-position K*K buffer."""
+        return flat[self.sq].view(self.n, self.K, self.K)
+
+
 class _Batch:
-    """Live replicate batch with an active-prefix layout.
+    """Live replicate batch with an active-prefix, K-grouped (ragged) layout.
 
-    Live replicates occupy positions [0, n_act); ``compact`` moves finished ones behind
-    them (``order`` maps position -> original replicate id).  Convergence state lives on
-    the device (``state``: float64 err_init/err_prev/err, int32 active/converged/n_pass)
-    so the solves can skip finished replicates without a host round trip."""
+    Replicate position p has rank ``kpos[p]`` and owns ``kpos[p]`` consecutive rows of
+    HT (usages transposed) and W (spectra).  Live replicates occupy positions [0, n_act),
+    sorted by K, so the live rows of EVERY K form one contiguous prefix: the data-side
+    GEMMs of a chunk are single launches over the whole K x n_iter replicate grid while
+    the per-replicate solves/Grams run once per K group (``groups``).  ``compact``
+    moves finished replicates behind the live ones (``order`` maps position -> original
+    replicate id).  Convergence state lives on the device (``state``: float64
+    err_init/err_prev/err, int32 active/converged/n_pass) so the solves skip finished
+    replicates without a host round trip."""
 
-    def __init__(self, HT, W, K, R):
-        self.HT, self.W, self.K, self.R = HT, W, K, R
-        self.order = list(range(R))
+    def __init__(self, HT, W, kpos):
+        self.HT, self.W = HT, W
+        self.kpos = np.asarray(kpos, dtype=np.int64)
+        if np.any(np.diff(self.kpos) < 0):
+            raise ValueError("replicate positions must be sorted by K")
+        R = self.R = int(self.kpos.size)
+        self.order = np.arange(R, dtype=np.int64)
         self.n_act = R
         dev = W.device
         self.state = {k: torch.zeros(R, dtype=torch.float64, device=dev)
@@ -286,21 +365,66 @@ class _Batch:
         self.layout_version = 0   # bumped by compact(): captured graphs key on it
         self.bucket = max(1, int(os.environ.get("CNMF_COMPACT_BUCKET",
                                                 "8" if W.device.type == "cuda" else "1")))
-        self.A = None   # (R, K, K) sufficient statistics (online 'exact' mode)
-        self.B = None   # (R*K, G)
+        self.A = None   # flat per-position K*K sufficient statistics (online 'exact' mode)
+        self.B = None   # (rows, G)
+        self._layout()
+
+    def _layout(self) -> None:
+        groups = []
+        p = r = q = 0
+        while p < self.n_act:
+            K = int(self.kpos[p])
+            e = p
+            while e < self.n_act and self.kpos[e] == K:
+                e += 1
+            groups.append(_Group(K, p, e - p, r, q))
+            r += (e - p) * K
+            q += (e - p) * K * K
+            p = e
+        self.groups = groups
+        self.rows_act = r
+        self.sq_act = q
+
+    @property
+    def K(self) -> int:
+        """The common K of a single-K batch (the beta != 2 paths need one)."""
+        ks = np.unique(self.kpos)
+        if ks.size != 1:
+            raise ValueError(f"mixed-K batch (K in {ks.tolist()}) has no single K")
+        return int(ks[0])
+
+    @property
+    def uniform(self) -> bool:
+        return np.unique(self.kpos).size == 1
 
     def views(self):
-        K, n = self.K, self.n_act
-        return self.HT[:n * K], self.W[:n * K]
+        return self.HT[:self.rows_act], self.W[:self.rows_act]
 
     def active_mask(self) -> torch.Tensor:
         return self.state["active"][:self.n_act]
 
-    def padded(self, n_live: int) -> int:
-        """Prefix length ``compact`` shrinks to when ``n_live`` replicates are live."""
-        if n_live <= 0:
-            return 0
-        return min(self.n_act, -(-n_live // self.bucket) * self.bucket)
+    def _plan(self, act: np.ndarray):
+        """(positions kept in the prefix per group, positions moved behind) for the
+        host active flags ``act`` of the current prefix.  Each group's live prefix is
+        rounded up to a multiple of ``bucket`` replicates (padded with finished ones of
+        the same K, which every kernel skips): batch shapes then repeat from step to
+        step, so per-shape GEMM tuning is reused instead of re-chosen at every
+        compaction."""
+        keep, rest = [], []
+        for g in self.groups:
+            idx = np.arange(g.p0, g.p0 + g.n)
+            live = idx[act[idx]]
+            dead = idx[~act[idx]]
+            n_keep = 0 if live.size == 0 else min(g.n, -(-live.size // self.bucket) * self.bucket)
+            pad = n_keep - live.size
+            keep.append(np.concatenate([live, dead[:pad]]))
+            rest.append(dead[pad:])
+        return keep, rest
+
+    def prefix_len(self, act_host: np.ndarray) -> int:
+        """Live-prefix length ``compact`` would shrink to for these flags."""
+        act = np.asarray(act_host[:self.n_act], dtype=bool)
+        return int(sum(k.size for k in self._plan(act)[0]))
 
     def compact(self, act_host: np.ndarray | None = None) -> None:
         """Move still-active replicates to the front and shrink n_act.
@@ -310,33 +434,34 @@ class _Batch:
         inactive really is finished, and positions that finished since stay in the
         prefix with active = 0 (skipped by the solves) until the next compaction.  The
         permutation is then applied in stream order with no host synchronisation."""
-        n, K = self.n_act, self.K
+        n = self.n_act
         if act_host is None:
             act_host = self.state["active"][:n].cpu().numpy() != 0
         act = np.asarray(act_host[:n], dtype=bool)
-        keep = np.flatnonzero(act)
-        # the live prefix is rounded up to a multiple of `bucket` replicates (padded with
-        # finished ones, which every kernel skips): batch shapes then repeat from step to
-        # step, so the GEMM library's per-shape heuristics are cached after warm-up
-        # instead of costing a host stall at every compaction
-        n_new = self.padded(keep.size)
+        keep, rest = self._plan(act)
+        n_new = int(sum(k.size for k in keep))
         if n_new == n:
             return
-        perm = np.concatenate([keep, np.flatnonzero(~act), np.arange(n, self.R)])
+        perm = np.concatenate(keep + rest + [np.arange(n, self.R)]).astype(np.int64)
         dev = self.W.device
-        rows = _to_device((perm[:, None] * K + np.arange(K)).reshape(-1), dev)
+        roff = np.concatenate([[0], np.cumsum(self.kpos)[:-1]])
+        rows = _to_device(_ranges(roff[perm], self.kpos[perm]), dev)
         self.HT = self.HT.index_select(0, rows)
         self.W = self.W.index_select(0, rows)
         pidx = _to_device(perm, dev)
         if self.B is not None:
             self.B = self.B.index_select(0, rows)
-            self.A = self.A.index_select(0, pidx)
+            sq = self.kpos * self.kpos
+            qoff = np.concatenate([[0], np.cumsum(sq)[:-1]])
+            self.A = self.A.index_select(0, _to_device(_ranges(qoff[perm], sq[perm]), dev))
         self.state = {k: v.index_select(0, pidx) for k, v in self.state.items()}
         self.h_iters = self.h_iters.index_select(0, pidx)
         self.w_iters = self.w_iters.index_select(0, pidx)
-        self.order = [self.order[p] for p in perm]
-        self.n_act = int(n_new)
+        self.order = self.order[perm]
+        self.kpos = self.kpos[perm]
+        self.n_act = n_new
         self.layout_version += 1
+        self._layout()
 
     def set_err(self, err: torch.Tensor, pass_idx: int, tol: float, final: bool,
                 init: bool = False) -> None:
@@ -364,11 +489,12 @@ class _Batch:
                                        st["active"][:n])
 
     def finalize(self):
-        """Restore original replicate order."""
-        inv = np.argsort(np.asarray(self.order))
-        K = self.K
+        """Restore original replicate order: (HT, W, ks, err, n_pass, converged,
+        h_iters, w_iters), rows of replicate r at offs[r] : offs[r] + ks[r]."""
+        inv = np.argsort(self.order)
         dev = self.W.device
-        rows = _to_device((inv[:, None] * K + np.arange(K)).reshape(-1), dev)
+        roff = np.concatenate([[0], np.cumsum(self.kpos)[:-1]])
+        rows = _to_device(_ranges(roff[inv], self.kpos[inv]), dev)
         HT = self.HT.index_select(0, rows)
         W = self.W.index_select(0, rows)
         idx = _to_device(inv, dev)
@@ -377,7 +503,7 @@ class _Batch:
         packed = torch.stack([self.state[k][idx].to(torch.float64) for k in keys] +
                              [self.h_iters[idx].to(torch.float64),
                               self.w_iters[idx].to(torch.float64)]).cpu().numpy()
-        return (HT, W, packed[0], packed[1].astype(np.int64), packed[2] != 0,
+        return (HT, W, self.kpos[inv], packed[0], packed[1].astype(np.int64), packed[2] != 0,
                 packed[3].astype(np.int64), packed[4].astype(np.int64))
 
 
@@ -406,7 +532,7 @@ class _PassPipeline:
             n_live = int((st.state["active"][:n] != 0).sum())
             if n_live == 0:
                 return False
-            if n - st.padded(n_live) >= max(1, int(self.frac * n)):
+            if n - st.prefix_len(st.state["active"][:n].numpy() != 0) >= max(1, int(self.frac * n)):
                 st.compact()
             return True
         flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
@@ -423,9 +549,10 @@ class _PassPipeline:
         n_live = int((pflags != 0).sum())
         if n_live == 0:                   # everything had finished one pass ago
             return False
-        if n - st.padded(n_live) >= max(1, int(self.frac * n)):
+        flags_np = pflags.numpy() != 0
+        if n - st.prefix_len(flags_np) >= max(1, int(self.frac * n)):
             # compact on the one-pass-stale flags, in stream order: no drain of the GPU
-            st.compact(pflags.numpy() != 0)
+            st.compact(flags_np)
             self.pending = None
             return st.n_act > 0
         return True
@@ -487,6 +614,107 @@ def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch
         iters[:R] += 1 if live is None else live.to(iters.dtype)
 
 
+def _count_units(X: torch.Tensor, rows: int = 1 << 16):
+    """Per-gene unit u (G,) with X == C * u for a non-negative INTEGER matrix C, or None.
+
+    cNMF's normalised counts are raw counts over a per-gene std (cnmf.py:670-681), so the
+    unit of column g is (count 1) / std_g: the smallest positive entry m of the column
+    over its smallest count d.  d is tried as 1..8, then (highly expressed genes whose
+    every count exceeds 8) as round(m / gap) with gap the smallest difference between
+    distinct entries; a column of zeros gets u = 1.  Accepted only if every entry of every
+    column is an integer multiple of its unit to fp32 rounding (|X/u - round(X/u)| <=
+    4e-7 * X/u + 1e-4) and C < 65536."""
+    N, G = X.shape
+    if N == 0 or bool((X < 0).any()):
+        return None
+    inf = torch.tensor(float("inf"), device=X.device, dtype=X.dtype)
+    mn = torch.full((G,), float("inf"), device=X.device, dtype=X.dtype)
+    for a in range(0, N, rows):
+        xb = X[a:a + rows]
+        mn = torch.minimum(mn, torch.where(xb > 0, xb, inf).amin(0))
+    mn = torch.where(torch.isfinite(mn), mn, torch.ones_like(mn))
+    unit = torch.full_like(mn, float("nan"))
+
+    def accept(cand):
+        todo = torch.isnan(unit)
+        bad = torch.zeros(G, dtype=torch.bool, device=X.device)
+        for a in range(0, N, rows):
+            c = X[a:a + rows] / cand
+            bad |= ((c - torch.round(c)).abs() > 4e-7 * c + 1e-4).any(0)
+            bad |= (c >= 65535.5).any(0)
+        return torch.where(todo & ~bad & torch.isfinite(cand) & (cand > 0), cand, unit)
+
+    for d in range(1, 9):
+        unit = accept(mn / d)
+        if not bool(torch.isnan(unit).any()):
+            return unit.contiguous()
+    todo = torch.isnan(unit).nonzero().flatten()
+    if todo.numel() > 64:
+        return None
+    gaps = torch.full_like(mn, float("nan"))
+    for g in todo.tolist():
+        v = torch.unique(X[:, g])
+        v = v[v > 0]
+        dv = torch.diff(v)
+        if dv.numel():
+            gaps[g] = mn[g] / torch.round(mn[g] / dv.min()).clamp(min=1)
+    unit = accept(gaps)
+    if bool(torch.isnan(unit).any()):
+        return None
+    return unit.contiguous()
+
+
+class _XPlanes:
+    """Exact bf16 planes of the data matrix for the split-precision GEMMs
+    (ops.gemm_planes), built once per solver: ``x`` (pb, N+pad, Gp) with genes on k (the
+    H-side numerator W X_c^T) and ``xt`` (pb, G, Np) with cells on k (the statistics
+    H_c^T X_c).  Integer data (cNMF norm counts) is stored as its count matrix C in one
+    bf16 plane (C <= 256) or two (C < 65536) with the per-gene ``unit`` folded into the
+    other operand / the output columns; other data as three planes of X itself."""
+
+    def __init__(self, X: torch.Tensor):
+        N, G = X.shape
+        self.N, self.G = N, G
+        unit = _count_units(X)
+        if unit is not None:
+            C = torch.empty_like(X)
+            for a in range(0, N, 1 << 16):
+                torch.round(X[a:a + (1 << 16)] / unit, out=C[a:a + (1 << 16)])
+            cmax = float(C.max()) if C.numel() else 0.0
+            self.pb = 1 if cmax <= 256 else 2
+        else:
+            C, self.pb = X, 3
+        self.unit = unit
+        self.Gp = -(-G // 64) * 64
+        self.Np = -(-N // 64) * 64 + 64
+        self.x = torch.zeros((self.pb, N + 128, self.Gp), dtype=torch.int16, device=X.device)
+        ops.split_planes(C, self.x)
+        self.xt = torch.zeros((self.pb, G, self.Np), dtype=torch.int16, device=X.device)
+        for a in range(0, N, 1 << 16):
+            blk = C[a:a + (1 << 16)].t().contiguous()          # (G, cells of the block)
+            ops.split_planes(blk, self.xt[:, :, a:a + -(-blk.shape[1] // 4) * 4])
+        if unit is not None and self.pb < 3:
+            # the planes must hold the counts exactly
+            from ..ops import reference as _ref
+            back = _ref.planes_to_f64(self.x[:, :N, :G]).sum(0)
+            if not torch.equal(back, C.to(torch.float64)):
+                raise RuntimeError("integer planes are not exact")
+        del C
+
+    @staticmethod
+    def build(X: torch.Tensor):
+        """Planes for X when the split GEMM path applies (GPU, fp32, memory), else None."""
+        if X.device.type != "cuda" or X.dtype != torch.float32 or \
+                os.environ.get("CNMF_GEMM", "planes") != "planes":
+            return None
+        N, G = X.shape
+        need = 2 * 3 * ((N + 128) * (-(-G // 64) * 64) + G * (-(-N // 64) * 64 + 64)) + 8 * N * G
+        free, _ = torch.cuda.mem_get_info(X.device)
+        if need > 0.5 * free:
+            return None
+        return _XPlanes(X)
+
+
 def _graphs_enabled(X: torch.Tensor) -> bool:
     """Capture repeated passes into HIP graphs (GPU only, opt-in: CNMF_GRAPHS=1).  Off by
     default: a compaction changes the layout every few passes, and re-capturing cost more
@@ -507,7 +735,7 @@ class NMFBatchSolver:
     """Solve R replicates (same X, same K, different seeds) together."""
 
     def __init__(self, X: torch.Tensor, opts: NMFOptions, comm=None, row_offset: int = 0,
-                 profile: bool = False, schedule=None):
+                 profile: bool = False, schedule=None, row_map=None):
         opts.validate()
         # optional explicit online schedule: list of steps, each a list of (row_start,
         # row_end) blocks solved independently before one W update (used to emulate the
@@ -517,23 +745,57 @@ class NMFBatchSolver:
         self.comm = comm or LocalComm()
         self.X = X if X.dtype == opts.dtype else X.to(opts.dtype)
         self.row_offset = row_offset
+        # [(local_start, local_stop, global_start)]: where this rank's rows sit in the
+        # global matrix (a chunk-interleaved DP shard; see parallel.runner.dp_row_segments)
+        self.row_map = row_map
         self.beta = beta_value(opts.beta_loss)
         self.profile = profile
         self.timings: dict[str, float] = {}
         # ||X||_F^2 (global) for the trace-trick loss
         self.x_sq = self.comm.allreduce_scalar(_sq_norm(self.X))
+        self._mean_x = None
+        self._xp = False            # split-GEMM planes of X: False = not built yet
+        self._ws: dict = {}
 
     # ------------------------------------------------------------------ public
-    def run(self, seeds, HT0=None, W0=None) -> NMFResult:
+    def run(self, seeds, HT0=None, W0=None, ks=None) -> NMFResult:
+        """Factorise one replicate per seed.  ``ks`` (one K per seed; default
+        ``opts.n_components`` for all) may mix ranks: the Frobenius solvers then run the
+        whole K x n_iter grid as ONE ragged batch (one pass loop, one data-side GEMM per
+        chunk for every K).  The beta != 2 solvers take one K at a time; a mixed-K
+        request is split by K for them."""
         o = self.opts
-        K = int(o.n_components)
+        seeds = [int(s_) for s_ in seeds]
         R = len(seeds)
+        ks = np.full(R, int(o.n_components), dtype=np.int64) if ks is None else \
+            np.asarray([int(k) for k in ks], dtype=np.int64)
+        if ks.size != R:
+            raise ValueError(f"{R} seeds but {ks.size} ranks")
+        if R and ks.min() < 1:
+            raise ValueError("every K must be >= 1")
+        if self.beta != 2.0 and np.unique(ks).size > 1:
+            return self._run_split_by_k(seeds, ks)
         t0 = time.perf_counter()
+        pos = np.argsort(ks, kind="stable")            # positions grouped by K
+        kpos = ks[pos]
         if HT0 is None or W0 is None:
-            HT, W = init_factors(self.X, K, seeds, o.init, self.comm, self.row_offset)
+            N, G = self.X.shape
+            tot = int(kpos.sum())
+            HT = torch.empty((tot, N), device=self.X.device, dtype=self.X.dtype)
+            W = torch.empty((tot, G), device=self.X.device, dtype=self.X.dtype)
+            r0 = 0
+            for K in np.unique(kpos):
+                sel = pos[kpos == K]
+                rows = slice(r0, r0 + sel.size * int(K))
+                init_into(HT[rows], W[rows], self.X, int(K), [seeds[i] for i in sel], o.init,
+                          self.comm, self.row_offset, mean=self._mean(), row_map=self.row_map)
+                r0 = rows.stop
         else:
+            if np.unique(ks).size > 1:
+                raise ValueError("explicit initial factors need a single K")
             HT, W = HT0.to(self.X.dtype).clone(), W0.to(self.X.dtype).clone()
-        st = _Batch(HT, W, K, R)
+        st = _Batch(HT, W, kpos)
+        st.order = pos.astype(np.int64).copy()
         if self.beta == 2.0:
             if o.mode == "online":
                 self._online_frob(st)
@@ -544,13 +806,98 @@ class NMFBatchSolver:
                 self._online_beta(st)
             else:
                 self._batch_beta(st)
-        HT, W, err, n_iter, conv, hi, wi = st.finalize()
+        HT, W, ks_out, err, n_iter, conv, hi, wi = st.finalize()
         if self.X.device.type == "cuda":
             ops.coop_check(self.X.device)
         stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": hi.tolist(),
                  "w_inner_iters": wi.tolist()}
+        uni = np.unique(ks_out)
+        return NMFResult(HT=HT, W=W, err=err, n_iter=n_iter, converged=conv, seeds=seeds,
+                         K=int(uni[0]) if uni.size == 1 else None, stats=stats, ks=ks_out)
+
+    def _run_split_by_k(self, seeds, ks) -> NMFResult:
+        """One single-K run per distinct K, merged back into the callers' order."""
+        t0 = time.perf_counter()
+        parts = {}
+        for K in np.unique(ks):
+            idx = np.flatnonzero(ks == K)
+            parts[int(K)] = (idx, self.run([seeds[i] for i in idx], ks=[int(K)] * idx.size))
+        R = len(seeds)
+        err, n_iter = np.zeros(R), np.zeros(R, dtype=np.int64)
+        conv = np.zeros(R, dtype=bool)
+        hi, wi = [0] * R, [0] * R
+        offs = np.concatenate([[0], np.cumsum(ks)[:-1]])
+        dev = self.X.device
+        HT = torch.empty((int(ks.sum()), self.X.shape[0]), device=dev, dtype=self.X.dtype)
+        W = torch.empty((int(ks.sum()), self.X.shape[1]), device=dev, dtype=self.X.dtype)
+        for K, (idx, res) in parts.items():
+            rows = _to_device(_ranges(offs[idx], ks[idx]), dev)
+            HT.index_copy_(0, rows, res.HT)
+            W.index_copy_(0, rows, res.W)
+            err[idx], n_iter[idx], conv[idx] = res.err, res.n_iter, res.converged
+            for j, i in enumerate(idx):
+                hi[i] = res.stats["h_inner_iters"][j]
+                wi[i] = res.stats["w_inner_iters"][j]
+        stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": hi, "w_inner_iters": wi}
         return NMFResult(HT=HT, W=W, err=err, n_iter=n_iter, converged=conv, seeds=list(seeds),
-                         K=K, stats=stats)
+                         K=None, stats=stats, ks=ks)
+
+    # ------------------------------------------------------------------ data-side GEMMs
+    def _planes(self):
+        """X planes for the split-precision MFMA GEMMs, or None (CPU, fp64, memory)."""
+        if self._xp is False:
+            self._xp = _XPlanes.build(self.X)
+        return self._xp
+
+    def _plane_buf(self, key: str, rows: int, cols: int) -> torch.Tensor:
+        """(3, rows, cols) int16 workspace, reused while the shape holds."""
+        if self.X.device.type == "cuda":     # run_concurrent: one workspace per stream
+            key = (key, torch.cuda.current_stream(self.X.device).cuda_stream)
+        buf = self._ws.get(key)
+        if buf is None or buf.shape[1] < rows or buf.shape[2] != cols:
+            buf = torch.zeros((3, rows, cols), dtype=torch.int16, device=self.X.device)
+            self._ws[key] = buf
+        return buf
+
+    def split_w(self, W: torch.Tensor):
+        """Planes of the spectra (times the count unit) for numer_gemm; call after every
+        change of W."""
+        xp = self._planes()
+        if xp is None:
+            return None
+        wpl = self._plane_buf("w", W.shape[0], xp.Gp)
+        ops.split_planes(W, wpl[:, :W.shape[0]], col_mul=xp.unit)
+        return wpl
+
+    def numer_gemm(self, W: torch.Tensor, wpl, a: int, b: int) -> torch.Tensor:
+        """numer = W X[a:b]^T (rows(W), b - a) -- split-precision MFMA when available."""
+        xp = self._planes()
+        if xp is None or wpl is None:
+            return W @ self.X[a:b].t()
+        out = torch.empty((W.shape[0], b - a), device=W.device, dtype=W.dtype)
+        ops.gemm_planes(out, wpl, xp.x[:, a:], W.shape[0], b - a, xp.Gp)
+        return out
+
+    def stats_gemm(self, B: torch.Tensor, HT: torch.Tensor, a: int, b: int,
+                   accumulate: bool) -> None:
+        """B (+)= HT[:, a:b] X[a:b]  (rows(HT), G) -- split-precision MFMA when available
+        (and the chunk start is 8-aligned for the planes' k offset)."""
+        xp = self._planes()
+        if xp is None or a % 8:
+            B.addmm_(HT[:, a:b], self.X[a:b], beta=1.0 if accumulate else 0.0)
+            return
+        bk = ops.planes_bk(xp.pb)
+        kd = -(-(b - a) // bk) * bk
+        hpl = self._plane_buf("h", HT.shape[0], kd)
+        ops.split_planes(HT[:, a:b], hpl[:, :HT.shape[0]])
+        ops.gemm_planes(B, hpl, xp.xt[:, :, a:], HT.shape[0], xp.G, kd, accumulate=accumulate,
+                        col_scale=xp.unit)
+
+    def _mean(self) -> float:
+        """Global mean of X (random init scale), one pass per solver."""
+        if self._mean_x is None:
+            self._mean_x = _global_mean(self.X, self.comm)
+        return self._mean_x
 
     def run_concurrent(self, seeds, n_streams: int = 2, min_group: int = 8) -> NMFResult:
         """Split the replicates into ``n_streams`` groups solved concurrently, each on its
@@ -573,6 +920,8 @@ class NMFBatchSolver:
         groups = [seeds[bounds[i]:bounds[i + 1]] for i in range(n_streams)]
         dev = self.X.device
         ops.coop_prepare(dev)   # device queries from the main thread (fail in workers)
+        if self.beta == 2.0:
+            self._planes()      # built once here, not raced by the worker threads
         main = torch.cuda.current_stream(dev)
         streams = [torch.cuda.Stream(dev) for _ in groups]
         for s_ in streams:
@@ -612,42 +961,58 @@ class NMFBatchSolver:
         st.compact()
 
     def _init_err(self, st: _Batch) -> None:
-        st.set_err(self.loss(st.HT, st.W, st.K), 0, self.opts.tol, False, init=True)
+        st.set_err(self.loss(st.HT, st.W, st.kpos if self.beta == 2.0 else st.K), 0,
+                   self.opts.tol, False, init=True)
 
-    def _init_err_frob(self, st: _Batch) -> None:
-        """Initial Frobenius error of every replicate, on device (conv kernel, init mode)."""
-        R, K = st.R, st.K
+    def _init_err_frob(self, st: _Batch):
+        """Initial Frobenius error of every replicate, on device (conv kernel, init mode).
+        Returns the statistics (flat per-position K*K block A, rows B) of the initial H."""
         X = self.X
         G = X.shape[1]
-        W3 = st.W.view(R, K, G)
-        stats = torch.empty(R * K * G + R * K * K, device=X.device, dtype=X.dtype)
-        B = stats[:R * K * G].view(R * K, G)
-        A = stats[R * K * G:].view(R, K, K)
-        B.addmm_(st.HT, X, beta=0.0)     # (not torch.mm(out=): ~0.4 ms host per call)
-        H3 = st.HT.view(R, K, X.shape[0])
-        ops.gram(H3, out=A)
+        HT, W = st.views()
+        rows, sq = st.rows_act, st.sq_act
+        stats = torch.empty(rows * G + sq, device=X.device, dtype=X.dtype)
+        B = stats[:rows * G].view(rows, G)
+        A = stats[rows * G:]
+        self.stats_gemm(B, HT, 0, X.shape[0], accumulate=False)
+        for g in st.groups:
+            ops.gram(g.rep3(HT), out=g.gram3(A))
         self.comm.allreduce_(stats)
-        lin = (B.view(R, K, G) * W3).sum(dim=(1, 2)).float().contiguous()
-        quad = (A * ops.gram(W3)).sum(dim=(1, 2)).float().contiguous()
-        ops.conv_update(lin, quad, self.x_sq, st.state, R, 0, self.opts.tol, False, init=True)
+        lin = torch.empty(st.n_act, device=X.device, dtype=torch.float32)
+        quad = torch.empty_like(lin)
+        for g in st.groups:
+            W3 = g.rep3(W)
+            lin[g.pos] = (g.rep3(B) * W3).sum(dim=(1, 2)).float()
+            quad[g.pos] = (g.gram3(A) * ops.gram(W3)).sum(dim=(1, 2)).float()
+        ops.conv_update(lin, quad, self.x_sq, st.state, st.n_act, 0, self.opts.tol, False,
+                        init=True)
         return A, B
 
     # ------------------------------------------------------------------ loss (any beta)
-    def loss(self, HT: torch.Tensor, W: torch.Tensor, K: int, row_chunk: int = 4096) -> torch.Tensor:
-        """sqrt(2 * D_beta(X || H W)) per replicate (sklearn square_root=True), global."""
-        R = W.shape[0] // K
+    def loss(self, HT: torch.Tensor, W: torch.Tensor, K, row_chunk: int = 4096) -> torch.Tensor:
+        """sqrt(2 * D_beta(X || H W)) per replicate (sklearn square_root=True), global.
+        ``K`` is one rank for all replicates or one rank per replicate (rows in order)."""
         X = self.X
         N, G = X.shape
-        W3 = W.view(R, K, G)
         if self.beta == 2.0:
-            # ||X||^2 - 2 <HT X, W> + <HT HT^T, W W^T>
+            kk = np.full(W.shape[0] // int(K), int(K)) if np.isscalar(K) else np.asarray(K)
+            # ||X||^2 - 2 <HT X, W> + <HT HT^T, W W^T>, per replicate
             B = HT @ X
-            A = ops.gram(HT.view(R, K, N))
-            lin = (B.view(R, K, G) * W3).sum(dim=(1, 2)).double()
-            quad = (A * ops.gram(W3)).sum(dim=(1, 2)).double()
+            lin = torch.empty(kk.size, dtype=torch.float64, device=X.device)
+            quad = torch.empty_like(lin)
+            r0 = 0
+            for i, k in enumerate(kk):
+                rs = slice(r0, r0 + int(k))
+                h, w = HT[rs], W[rs]
+                lin[i] = (B[rs] * w).sum().double()
+                quad[i] = ((h @ h.t()) * (w @ w.t())).sum().double()
+                r0 = rs.stop
             lin = self.comm.allreduce_(lin.contiguous())
             quad = self.comm.allreduce_(quad.contiguous())
             return torch.sqrt(torch.clamp(self.x_sq - 2 * lin.cpu() + quad.cpu(), min=0.0))
+        K = int(K)
+        R = W.shape[0] // K
+        W3 = W.view(R, K, G)
         _, _, tot = ops.beta_contract("h", X, HT.view(R, K, N), W3, self.beta, self.opts.eps,
                                       want_num=False, want_loss=True)
         tot = tot.to(torch.float64).contiguous()
@@ -657,7 +1022,6 @@ class NMFBatchSolver:
     # ------------------------------------------------------------------ online frobenius
     def _online_frob(self, st: _Batch) -> None:
         o, comm = self.opts, self.comm
-        K = st.K
         X = self.X
         N, G = X.shape
         dev, dt = X.device, X.dtype
@@ -672,32 +1036,31 @@ class NMFBatchSolver:
         del A0, B0
         max_pass = int(o.online_max_pass)
         pipe = _PassPipeline(st)
-        n_alloc = -1
+        n_alloc = None
         graphs = _graphs_enabled(X) and not dist
         graph, graph_key, last_key = None, None, None
         for p in range(max_pass):
             n = st.n_act
             if n == 0:
                 break
-            if n != n_alloc:   # (re)allocate per-n workspaces once, not per pass
-                n_alloc = n
-                flat = torch.empty(n * K * G + n * K * K, device=dev, dtype=dt)
-                dB = flat[:n * K * G].view(n * K, G)
-                dA = flat[n * K * G:].view(n, K, K)
+            rows, sq = st.rows_act, st.sq_act
+            if (rows, sq, n) != n_alloc:   # (re)allocate per-layout workspaces, not per pass
+                n_alloc = (rows, sq, n)
+                flat = torch.empty(rows * G + sq, device=dev, dtype=dt)
+                dB = flat[:rows * G].view(rows, G)
+                dA = flat[rows * G:]
                 if not exact:
-                    A = torch.empty((n, K, K), device=dev, dtype=dt)
-                    B = torch.empty((n * K, G), device=dev, dtype=dt)
+                    A = torch.empty(sq, device=dev, dtype=dt)
+                    B = torch.empty((rows, G), device=dev, dtype=dt)
                 lin = torch.zeros(n, device=dev, dtype=torch.float32)
                 quad = torch.zeros(n, device=dev, dtype=torch.float32)
-                wwt_buf = torch.empty((n, K, K), device=dev, dtype=dt)
+                wwt_buf = torch.empty(sq, device=dev, dtype=dt)
             final = p + 1 == max_pass
 
             def enqueue_pass(pass_arg: int, final: bool) -> None:
                 HT, W = st.views()
-                W3 = W.view(n, K, G)
-                H3 = HT.view(n, K, N)
                 if exact:
-                    A_, B_ = st.A[:n], st.B[:n * K]
+                    A_, B_ = st.A[:sq], st.B[:rows]
                 else:
                     A_, B_ = A, B
                     if dist:        # single process: the pass's first chunk overwrites
@@ -707,47 +1070,52 @@ class NMFBatchSolver:
                 active = st.active_mask()
                 h_it = st.h_iters[:n]
                 w_it = st.w_iters[:n]
+                groups = st.groups
                 for s_, blocks in enumerate(steps):
                     # DP: increments go to the flat buffer (one all-reduce per step); single
                     # process: GEMMs accumulate straight into A / B (beta = 1)
                     accA, accB = (dA, dB) if dist else (A_, B_)
                     first = True
+                    wpl = None if exact else self.split_w(W)   # W changed in the last step
                     for (a, b) in blocks:
                         cw = b - a
                         if cw <= 0:
                             continue
                         xc = X[a:b]
-                        hview = H3[:, :, a:b]                            # (n, K, cw) strided
-                        h_old = hview.clone() if exact else None
-                        WWT = ops.gram(W3, out=wwt_buf, active=active)   # MFMA Gram
-                        numerT = W @ xc.t()                              # (n*K, cw) GEMM
-                        _inner_solve(algo, hview, numerT.view(n, K, cw), WWT,
-                                  max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
-                                  l1_den=o.l1_H, l2=o.l2_H, eps=o.eps, iters_out=h_it,
-                                  conv_mode=cmode, check_every=o.inner_check_every,
-                                  active=active)
+                        hcols = HT[:, a:b]                               # (rows, cw) strided
+                        h_old = hcols.clone() if exact else None
+                        numerT = self.numer_gemm(W, wpl, a, b)   # ONE GEMM, every K
+                        for g in groups:
+                            ga = active[g.pos]
+                            WWT = ops.gram(g.rep3(W), out=g.gram3(wwt_buf), active=ga)
+                            _inner_solve(algo, g.rep3(hcols), g.rep3(numerT), WWT,
+                                         max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
+                                         l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
+                                         iters_out=h_it[g.pos], conv_mode=cmode,
+                                         check_every=o.inner_check_every, active=ga)
                         if exact:
                             # replace the chunk's old contribution: d = h_new - h_old
-                            hh = torch.bmm(hview, hview.transpose(1, 2))
-                            hh -= torch.bmm(h_old, h_old.transpose(1, 2))
-                            hlhs = h_old.neg_().add_(hview).view(n * K, cw)
-                            if dist and first:
-                                accB.addmm_(hlhs, xc, beta=0.0)
-                                accA.copy_(hh)
-                            else:
-                                accB.addmm_(hlhs, xc)
-                                accA += hh
+                            for g in groups:
+                                hv, ho = g.rep3(hcols), g.rep3(h_old)
+                                hh = torch.bmm(hv, hv.transpose(1, 2))
+                                hh -= torch.bmm(ho, ho.transpose(1, 2))
+                                if dist and first:
+                                    g.gram3(accA).copy_(hh)
+                                else:
+                                    g.gram3(accA).add_(hh)
+                            hlhs = h_old.neg_().add_(hcols)
+                            accB.addmm_(hlhs, xc, beta=0.0 if (dist and first) else 1.0)
                         else:
-                            if dist and first:
-                                accB.addmm_(HT[:, a:b], xc, beta=0.0)    # (n*K, G) GEMM
-                                ops.gram(hview, out=accA)
-                            elif not dist and pass_first:
-                                accB.addmm_(HT[:, a:b], xc, beta=0.0)    # B = h^T x
-                                ops.gram(hview, out=accA, active=active)  # A = h^T h
+                            if (dist and first) or (not dist and pass_first):
+                                self.stats_gemm(accB, HT, a, b, False)  # B = h^T x, every K
+                                for g in groups:                       # A = h^T h
+                                    ops.gram(g.rep3(hcols), out=g.gram3(accA),
+                                             active=None if dist else active[g.pos])
                             else:
-                                accB.addmm_(HT[:, a:b], xc)              # B += h^T x
-                                ops.gram(hview, out=accA, accumulate=True,   # A += h^T h
-                                         active=active)
+                                self.stats_gemm(accB, HT, a, b, True)   # B += h^T x
+                                for g in groups:                       # A += h^T h
+                                    ops.gram(g.rep3(hcols), out=g.gram3(accA),
+                                             accumulate=True, active=active[g.pos])
                         first = False
                         pass_first = False
                     if dist:
@@ -757,12 +1125,14 @@ class NMFBatchSolver:
                         B_ += dB
                         A_ += dA
                     last = s_ == len(steps) - 1
-                    _inner_solve(algo, W3, B_.view(n, K, G), A_.contiguous(),
-                              max_iter=o.online_chunk_max_iter, tol=o.online_w_tol,
-                              l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
-                              lin_out=lin if last else None, quad_out=quad if last else None,
-                              iters_out=w_it, conv_mode=cmode,
-                              check_every=o.inner_check_every, active=active)
+                    for g in groups:
+                        _inner_solve(algo, g.rep3(W), g.rep3(B_), g.gram3(A_),
+                                     max_iter=o.online_chunk_max_iter, tol=o.online_w_tol,
+                                     l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
+                                     lin_out=lin[g.pos] if last else None,
+                                     quad_out=quad[g.pos] if last else None,
+                                     iters_out=w_it[g.pos], conv_mode=cmode,
+                                     check_every=o.inner_check_every, active=active[g.pos])
                 ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
                                 n, pass_arg, o.tol, final=final)
 
@@ -802,7 +1172,6 @@ class NMFBatchSolver:
     # ------------------------------------------------------------------ batch frobenius
     def _batch_frob(self, st: _Batch) -> None:
         o, comm = self.opts, self.comm
-        K = st.K
         X = self.X
         N, G = X.shape
         dev, dt = X.device, X.dtype
@@ -813,39 +1182,44 @@ class NMFBatchSolver:
         max_it = int(o.batch_max_iter)
         every = max(1, int(o.loss_every))
         pipe = _PassPipeline(st)
-        n_alloc = -1
+        n_alloc = None
         for it in range(max_it):
             n = st.n_act
             if n == 0:
                 break
-            if n != n_alloc:
-                n_alloc = n
-                flat = torch.empty(n * K * G + n * K * K, device=dev, dtype=dt)
-                B = flat[:n * K * G].view(n * K, G)
-                A = flat[n * K * G:].view(n, K, K)
+            rows, sq = st.rows_act, st.sq_act
+            if (rows, sq, n) != n_alloc:
+                n_alloc = (rows, sq, n)
+                flat = torch.empty(rows * G + sq, device=dev, dtype=dt)
+                B = flat[:rows * G].view(rows, G)
+                A = flat[rows * G:]
                 lin = torch.zeros(n, device=dev, dtype=torch.float32)
                 quad = torch.zeros(n, device=dev, dtype=torch.float32)
+                wwt = torch.empty(sq, device=dev, dtype=dt)
             HT, W = st.views()
-            W3 = W.view(n, K, G)
             active = st.active_mask()
-            # H-step over all local cells
-            WWT = ops.gram(W3, active=st.active_mask())
-            numerT = W @ X.t()
+            # H-step over all local cells: one numerator GEMM for every K
+            numerT = self.numer_gemm(W, self.split_w(W), 0, N)
             nsplit = 1 if inner else max(1, (N + 8191) // 8192)
-            _inner_solve(o.algo, HT.view(n, K, N), numerT.view(n, K, N), WWT,
-                      max_iter=h_iter, tol=h_tol, l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
-                      nsplit=nsplit, active=active, iters_out=st.h_iters[:n])
+            for g in st.groups:
+                WWT = ops.gram(g.rep3(W), out=g.gram3(wwt), active=active[g.pos])
+                _inner_solve(o.algo, g.rep3(HT), g.rep3(numerT), WWT,
+                             max_iter=h_iter, tol=h_tol, l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
+                             nsplit=nsplit, active=active[g.pos],
+                             iters_out=st.h_iters[g.pos])
             del numerT
             # W-step from the new H
-            B.addmm_(HT, X, beta=0.0)
-            H3 = HT.view(n, K, N)
-            ops.gram(H3, out=A)
+            self.stats_gemm(B, HT, 0, N, accumulate=False)
+            for g in st.groups:
+                ops.gram(g.rep3(HT), out=g.gram3(A))
             comm.allreduce_(flat)
             check = (it + 1) % every == 0 or it + 1 == max_it
-            _inner_solve(o.algo, W3, B.view(n, K, G), A.contiguous(),
-                      max_iter=h_iter, tol=h_tol, l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
-                      lin_out=lin if check else None, quad_out=quad if check else None,
-                      active=active, iters_out=st.w_iters[:n])
+            for g in st.groups:
+                _inner_solve(o.algo, g.rep3(W), g.rep3(B), g.gram3(A),
+                             max_iter=h_iter, tol=h_tol, l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
+                             lin_out=lin[g.pos] if check else None,
+                             quad_out=quad[g.pos] if check else None,
+                             active=active[g.pos], iters_out=st.w_iters[g.pos])
             if check:
                 ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
                                 n, it + 1, o.tol, final=(it + 1 == max_it))

@@ -95,6 +95,10 @@ def chunked_solve(HT: torch.Tensor, numerT: torch.Tensor, gram: torch.Tensor, ch
         a = full * c
         ops.solve(algo, HT[:, a:].unsqueeze(0), numerT[:, a:].unsqueeze(0), g1,
                   max_iter=chunk_max_iter, tol=h_tol, l1_num=l1_num, l2=l2, eps=eps)
+    if HT.device.type == "cuda":
+        # few chunks take the cooperative path: a solve whose workgroups could not all be
+        # resident gave up waiting -> its usages are wrong; fail here, not downstream
+        ops.coop_check(HT.device)
     return HT
 
 

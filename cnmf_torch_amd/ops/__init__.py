@@ -242,8 +242,13 @@ def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int)
 def coop_check(device: torch.device | None = None) -> None:
     """Raise if any cooperative solve on ``device`` gave up waiting (non-resident
     workgroups) -- its results would be wrong.  Synchronises; call once per run."""
+    want = None
+    if device is not None:
+        device = torch.device(device)
+        want = str(torch.device("cuda", device.index if device.index is not None
+                                else torch.cuda.current_device()))
     for key, ws in _COOP_WS.items():
-        if device is not None and key[0] != str(device):
+        if want is not None and key[0] != want:
             continue
         v = int(ws["flag"].item())
         if v:
@@ -723,3 +728,116 @@ def philox_fill(out: torch.Tensor, seeds: torch.Tensor, scales: torch.Tensor, st
     _hip.philox_fill(out.data_ptr(), rows, cols, out.stride(1), out.stride(2), out.stride(0),
                      int(row_offset), seeds_d.data_ptr(), scales_d.data_ptr(), R, int(stream),
                      int(mode), _stream_ptr(out))
+
+
+# ----------------------------------------------------------------------------- split GEMM
+def planes_bk(pb: int) -> int:
+    """k granularity (BK) of the split-precision GEMM for ``pb`` B planes."""
+    return 32
+
+
+_GEMM_TILES = {0: (128, 128), 1: (128, 256), 2: (256, 128), 3: (64, 128)}
+_GEMM_SLAB: dict = {}
+
+
+def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
+    """(tile variant, k split) for an M x N x Kd split GEMM: the largest tile that still
+    gives every CU a workgroup, else k-split slices (deterministic slab reduction) until
+    ~2 workgroups per CU.  CNMF_GEMM_VARIANT / CNMF_GEMM_KSPLIT override (benchmarks)."""
+    cus = 256
+    nk = Kd // planes_bk(pb)
+    v_env, k_env = os.environ.get("CNMF_GEMM_VARIANT"), os.environ.get("CNMF_GEMM_KSPLIT")
+
+    def tiles(v):
+        tm, tn = _GEMM_TILES[v]
+        return -(-M // tm) * -(-N // tn)
+
+    # measured on MI355X (profiles/r2_gemm_planes_sweep.log): 128x256 tiles win once they
+    # alone fill the chip; below that 128x128 tiles with a k split
+    v = int(v_env) if v_env is not None else (1 if tiles(1) >= cus else 0)
+    ksplit = 1
+    if k_env is not None:
+        ksplit = int(k_env)
+    else:
+        t = tiles(v)
+        while t * ksplit < 2 * cus and nk // (2 * ksplit) >= 4:
+            ksplit *= 2
+    return v, max(1, min(ksplit, nk))
+
+
+def split_planes(S: torch.Tensor, out: torch.Tensor, col_mul: torch.Tensor | None = None) -> None:
+    """Exact bf16 split of the fp32 matrix ``S`` (rows, cols; unit column stride), times
+    the optional per-column factor ``col_mul``, into ``out`` (P, rows_out >= rows,
+    cols_pad) int16 (bf16 bit patterns; any 4-aligned row pitch): plane 0 = rn(v),
+    plane 1 = rn(v - plane 0), plane 2 = rn of the rest (v == sum of the planes for every
+    normal fp32 value when P == 3).  Columns [cols, cols_pad) are written as zeros (the
+    GEMM's k padding)."""
+    rows, cols = S.shape
+    P_, rows_out, ld = out.shape
+    pitch = out.stride(1)
+    if out.dtype != torch.int16 or out.stride(2) != 1 or rows_out < rows or pitch % 4 \
+            or out.stride(0) % 4 or ld > pitch or out.data_ptr() % 8:
+        raise ValueError("out: int16 (P, rows, cols_pad) planes, unit column stride, "
+                         "4-aligned pitches, 8-byte aligned base")
+    if cols > ld or ld % 4 or not 1 <= P_ <= 3:
+        raise ValueError(f"split_planes: cols {cols} vs cols_pad {ld}, planes {P_}")
+    if S.dtype != torch.float32 or (cols > 1 and S.stride(1) != 1):
+        raise ValueError("S: float32 with unit column stride required")
+    if col_mul is not None and (col_mul.dtype != torch.float32 or col_mul.numel() < cols
+                                or not col_mul.is_contiguous()):
+        raise ValueError("col_mul: contiguous float32 with >= cols entries")
+    if not use_native(S):
+        out[:, :rows].copy_(reference.split_planes(S if col_mul is None else S * col_mul[:cols],
+                                                   P_, ld))
+        return
+    _hip.split_planes(S.data_ptr(), S.stride(0), rows, cols, ld,
+                      col_mul.data_ptr() if col_mul is not None else 0, out.data_ptr(), pitch,
+                      out.stride(0), P_, _stream_ptr(S))
+
+
+def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: int, Kd: int,
+                accumulate: bool = False, col_scale: torch.Tensor | None = None) -> None:
+    """C[:M, :N] (+)= col_scale * sum_{i + j <= 2} A[i][:M, :Kd] . B[j][:N, :Kd]^T on the bf16
+    matrix cores (gemm_planes.hip): the fp32-accurate product of the fp32 matrices whose
+    exact bf16 splits are A (3 planes) and B (1-3 planes; 1 or 2 when B holds integers).
+    A/B: int16 (P, rows, ld) views with unit k stride (row offsets / k offsets are just
+    views); k must be zero-padded in A up to ``Kd`` (a multiple of planes_bk)."""
+    pa, a_rows, _ = A.shape
+    pb, b_rows, _ = B.shape
+    for name, t in (("A", A), ("B", B)):
+        if t.dtype != torch.int16 or t.stride(2) != 1 or t.stride(1) % 8 or t.stride(0) % 8:
+            raise ValueError(f"{name}: int16 planes with unit k stride, 8-aligned strides")
+        if t.data_ptr() % 16:
+            raise ValueError(f"{name}: 16-byte aligned base required (k offset % 8 == 0)")
+        if t.shape[2] < Kd:
+            raise ValueError(f"{name}: k extent {t.shape[2]} < Kd {Kd}")
+    if pa != 3 or not 1 <= pb <= 3 or Kd % planes_bk(pb) or M > a_rows or N > b_rows:
+        raise ValueError(f"gemm_planes: planes {pa}/{pb}, Kd {Kd}, M {M}/{a_rows}, N {N}/{b_rows}")
+    if C.dtype != torch.float32 or C.stride(1) != 1 or C.shape[0] < M or C.shape[1] < N:
+        raise ValueError("C: float32 (>= M, >= N) with unit column stride required")
+    if col_scale is not None and (col_scale.dtype != torch.float32 or col_scale.numel() < N
+                                  or not col_scale.is_contiguous()):
+        raise ValueError("col_scale: contiguous float32 with >= N entries")
+    if not use_native(C):
+        prod = reference.gemm_planes(A[:, :M, :Kd], B[:, :N, :Kd])
+        if col_scale is not None:
+            prod = prod * col_scale[:N].double()
+        if accumulate:
+            C[:M, :N] += prod.to(C.dtype)
+        else:
+            C[:M, :N] = prod.to(C.dtype)
+        return
+    variant, ksplit = gemm_plan(M, N, Kd, pb)
+    slab = 0
+    if ksplit > 1:
+        key = (str(C.device), _stream_ptr(C))
+        ws = _GEMM_SLAB.get(key)
+        if ws is None or ws.numel() < ksplit * M * N:
+            ws = torch.empty(max(ksplit * M * N, 1 << 20), dtype=torch.float32, device=C.device)
+            _GEMM_SLAB[key] = ws
+        slab = ws.data_ptr()
+    _hip.gemm_planes(A.data_ptr(), A.stride(1), A.stride(0), a_rows, B.data_ptr(), B.stride(1),
+                     B.stride(0), b_rows, C.data_ptr(), C.stride(0),
+                     col_scale.data_ptr() if col_scale is not None else 0, int(M), int(N),
+                     int(Kd), pa, pb, int(bool(accumulate)), int(variant), int(ksplit), slab,
+                     _stream_ptr(C))

@@ -254,3 +254,42 @@ def beta_w_update(W3, num, den, hsum, An, Ad, an_out, dn_out, beta, gamma, l1, l
     act[:R][stop] = 0
     if iters is not None:
         iters[:R] += live.to(iters.dtype)
+
+
+def _bf16_rn_bits(v: torch.Tensor) -> torch.Tensor:
+    """Round-to-nearest-even bf16 bit patterns (int32 holding 16 bits) of finite fp32."""
+    u = v.contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    u = (u + 0x7FFF + ((u >> 16) & 1)) >> 16
+    return (u & 0xFFFF).to(torch.int32)
+
+
+def _bits_to_f32(h: torch.Tensor) -> torch.Tensor:
+    return (h.to(torch.int64) << 16).to(torch.int32).view(torch.float32)
+
+
+def split_planes(S: torch.Tensor, nplanes: int, ld: int) -> torch.Tensor:
+    """(nplanes, rows, ld) int16 bf16 planes of fp32 S (columns beyond S are zero)."""
+    rows, cols = S.shape
+    out = torch.zeros((nplanes, rows, ld), dtype=torch.int16, device=S.device)
+    r = S.to(torch.float32)
+    for p in range(nplanes):
+        h = _bf16_rn_bits(r)
+        out[p, :, :cols] = h.to(torch.int16)   # wraps to the same 16-bit pattern
+        r = r - _bits_to_f32(h)
+    return out
+
+
+def planes_to_f64(P: torch.Tensor) -> torch.Tensor:
+    """bf16 planes (P, rows, k) int16 -> their float64 values, per plane."""
+    return _bits_to_f32(P.to(torch.int32) & 0xFFFF).to(torch.float64)
+
+
+def gemm_planes(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """sum_{i + j <= 2} A_i B_j^T in float64 (oracle of ops.gemm_planes)."""
+    Af, Bf = planes_to_f64(A), planes_to_f64(B)
+    out = torch.zeros((A.shape[1], B.shape[1]), dtype=torch.float64, device=A.device)
+    for i in range(A.shape[0]):
+        for j in range(B.shape[0]):
+            if i + j <= 2:
+                out += Af[i] @ Bf[j].t()
+    return out

@@ -100,19 +100,60 @@ def row_block(n_rows: int, rank: int, world: int) -> tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
+def dp_row_segments(n_rows: int, chunk: int, rank: int, world: int,
+                    align: int = 8) -> list[tuple[int, int]]:
+    """Global row segments held by ``rank`` in a chunk-interleaved cell shard: every
+    online chunk [s*c, (s+1)*c) is split over ALL ranks (boundaries rounded down to
+    ``align`` rows), so online step s on every rank works on its slice of the SAME global
+    chunk and the all-reduced statistics of the step are exactly the single-GPU chunk's.
+    The factorisation path is therefore independent of the world size, and every rank
+    is busy in every step."""
+    c = max(1, int(chunk))
+    segs = []
+    for a in range(0, n_rows, c):
+        b = min(n_rows, a + c)
+        n = b - a
+
+        def cut(r):
+            if r <= 0:
+                return a
+            if r >= world:
+                return b
+            return a + (n * r // world) // align * align
+
+        segs.append((cut(rank), cut(rank + 1)))
+    return segs
+
+
+def dp_layout(segments):
+    """(row_map [(local_a, local_b, global_a)], online schedule [[(local_a, local_b)]])
+    of a rank's segments, one step per global chunk."""
+    row_map, sched, off = [], [], 0
+    for a, b in segments:
+        n = max(0, b - a)
+        row_map.append((off, off + n, a))
+        sched.append([(off, off + n)])
+        off += n
+    return row_map, sched
+
+
 def dp_factorize(obj, skip_completed_runs: bool = False, replicate_batch=None,
                  save_usages: bool = False, backend: str | None = None, verbose=True):
+    """Cell-sharded factorize: every rank holds a chunk-interleaved shard of norm_counts
+    (dp_row_segments) and all ranks solve every replicate batch together, all-reducing
+    the [dB | dA] statistics once per online step; rank 0 writes the spectra."""
     from ..utils.h5ad import h5ad_shape
-    from ..utils.io import load_df_from_npz
+    from ..utils.io import load_df_from_npz, load_yaml
 
     comm, dev = init_distributed(backend)
     run_params = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
     jobs = _incomplete_jobs(obj, run_params, skip_completed_runs)
     n_rows, _ = h5ad_shape(obj.paths["normalized_counts"])
-    rr = row_block(n_rows, comm.rank, comm.world_size)
+    chunk = int(load_yaml(obj.paths["nmf_run_parameters"]).get("online_chunk_size", 5000))
+    segs = dp_row_segments(n_rows, chunk, comm.rank, comm.world_size)
     obj.factorize_jobs(jobs, worker_label=comm.rank, device=dev,
                        replicate_batch=replicate_batch, save_usages=save_usages,
                        verbose=verbose and comm.rank == 0, run_params=run_params,
-                       comm=comm if comm.world_size > 1 else None, row_range=rr)
+                       comm=comm if comm.world_size > 1 else None, row_segments=segs)
     comm.barrier()
     return comm

@@ -284,6 +284,34 @@ def read_X_rows(path: str, start: int, stop: int):
         return sp.csr_matrix((data, indices, indptr - lo), shape=(stop - start, shape[1]))
 
 
+def read_X_row_segments(path: str, segments):
+    """Rows of X for a list of [start, stop) segments, concatenated in order (dense
+    ndarray or CSR); the file is opened once."""
+    lib = _lib()
+    parts = []
+    with lib.File(str(path), "r") as f:
+        dense = f.kind("/X") == "dataset"
+        attrs = None if dense else f.attrs("/X")
+        if not dense and _enc(attrs) != "csr_matrix":
+            full = _read_matrix(f, "/X")
+            return np.concatenate([np.asarray(full[a:b]) for a, b in segments]) if segments \
+                else np.asarray(full[:0])
+        shape = None if dense else tuple(int(x) for x in np.asarray(attrs["shape"]))
+        for a, b in segments:
+            if dense:
+                parts.append(np.asarray(f.read("/X", a, max(a, b))))
+                continue
+            b = min(max(a, b), shape[0])
+            indptr = np.asarray(f.read("/X/indptr", a, b + 1))
+            lo, hi = int(indptr[0]), int(indptr[-1])
+            data = np.asarray(f.read("/X/data", lo, hi))
+            indices = np.asarray(f.read("/X/indices", lo, hi))
+            parts.append(sp.csr_matrix((data, indices, indptr - lo), shape=(b - a, shape[1])))
+    if dense:
+        return np.concatenate(parts) if parts else np.zeros((0, 0))
+    return sp.vstack(parts, format="csr")
+
+
 def read_h5ad_annotations(path: str) -> AnnData:
     """obs/var only (X left as None): what a cell-sharded rank needs besides its rows."""
     lib = _lib()

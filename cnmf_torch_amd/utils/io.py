@@ -101,6 +101,126 @@ def _savez_deflate(path: str, arrays: dict, level: int) -> None:
                 np.lib.format.write_array(fh, np.asanyarray(arr), allow_pickle=False)
 
 
+def npy_bytes(arr) -> bytes:
+    """The .npy encoding of ``arr`` (pickle-free)."""
+    buf = io.BytesIO()
+    np.lib.format.write_array(buf, np.ascontiguousarray(arr), allow_pickle=False)
+    return buf.getvalue()
+
+
+def _zip_entry(name: str, payload: bytes, off: int):
+    """(local header + name, central-directory record) of one stored ZIP member."""
+    import struct
+    import zlib
+
+    nm = name.encode()
+    crc = zlib.crc32(payload) & 0xFFFFFFFF
+    n = len(payload)
+    if n >= 0xFFFFFFFF or off >= 0xFFFFFFFF:
+        raise ValueError("member too large for the stored-zip fast path")
+    head = struct.pack("<IHHHHHIIIHH", 0x04034B50, 20, 0, 0, 0, 33, crc, n, n, len(nm), 0) + nm
+    cent = struct.pack("<IHHHHHHIIIHHHHHII", 0x02014B50, 20, 20, 0, 0, 0, 33, crc, n, n,
+                       len(nm), 0, 0, 0, 0, 0o600 << 16, off) + nm
+    return head, cent
+
+
+def _zip_end(n_members: int, cd_size: int, cd_off: int) -> bytes:
+    import struct
+
+    return struct.pack("<IHHHHIIH", 0x06054B50, 0, 0, n_members, n_members, cd_size, cd_off, 0)
+
+
+def _zip_stored(members) -> bytes:
+    """A minimal PKZIP archive of uncompressed (stored) members -- exactly what
+    ``np.savez`` writes (np.load reads it), assembled with one crc32 per member instead
+    of zipfile's per-member Python machinery."""
+    out, central, off = [], [], 0
+    for name, payload in members:
+        head, cent = _zip_entry(name, payload, off)
+        central.append(cent)
+        out += [head, payload]
+        off += len(head) + len(payload)
+    cd = b"".join(central)
+    return b"".join(out) + cd + _zip_end(len(central), len(cd), off)
+
+
+class NpzTemplate:
+    """Writer for many .npz files that share members (the per-replicate spectra files
+    all carry the same gene names): the shared members are encoded, checksummed and
+    sha256-hashed ONCE, and every file is then [shared members][own members][central
+    directory], written atomically with its sha256 continued from the shared prefix.
+    A standard stored ZIP: np.load / load_df_from_npz read it."""
+
+    def __init__(self, shared: dict):
+        import hashlib
+
+        self.prefix_parts, self.central, off = [], [], 0
+        for k, v in shared.items():
+            payload = v if isinstance(v, bytes) else npy_bytes(v)
+            head, cent = _zip_entry(k + ".npy", payload, off)
+            self.prefix_parts += [head, payload]
+            self.central.append(cent)
+            off += len(head) + len(payload)
+        self.prefix_len = off
+        self.sha = hashlib.sha256()
+        for part in self.prefix_parts:
+            self.sha.update(part)
+
+    def write(self, path: str, own: dict) -> tuple[str, int]:
+        parts, central, off = [], list(self.central), self.prefix_len
+        for k, v in own.items():
+            payload = v if isinstance(v, bytes) else npy_bytes(v)
+            head, cent = _zip_entry(k + ".npy", payload, off)
+            parts += [head, payload]
+            central.append(cent)
+            off += len(head) + len(payload)
+        cd = b"".join(central)
+        parts += [cd, _zip_end(len(central), len(cd), off)]
+        h = self.sha.copy()
+        for part in parts:
+            h.update(part)
+        with atomic_path(path, suffix=".npz") as tmp:
+            with open(tmp, "wb") as fh:
+                fh.writelines(self.prefix_parts)
+                fh.writelines(parts)
+        return h.hexdigest(), off + len(cd) + 22
+
+
+def npz_bytes(arrays: dict, level: int = 0) -> bytes:
+    """The bytes of an .npz holding ``arrays`` (same members as :func:`_savez_deflate`).
+    Values may be arrays or already-encoded .npy ``bytes`` (shared members such as the
+    gene names are encoded once per factorize, not once per file)."""
+    if level <= 0:
+        return _zip_stored([(k + ".npy", v if isinstance(v, bytes) else npy_bytes(v))
+                            for k, v in arrays.items()])
+    buf = io.BytesIO()
+    _savez_deflate(buf, {k: (np.load(io.BytesIO(v)) if isinstance(v, bytes) else v)
+                         for k, v in arrays.items()}, level)
+    return buf.getvalue()
+
+
+def write_bytes_atomic(path: str, data: bytes) -> None:
+    with atomic_path(path, suffix=".npz" if path.endswith(".npz") else "") as tmp:
+        with open(tmp, "wb") as fh:
+            fh.write(data)
+
+
+def save_arrays_npz_digest(path: str, arrays: dict, level: int = 0) -> tuple[str, int]:
+    """Atomically write an .npz of ``arrays``; returns (sha256 hex, size) of the bytes
+    written, hashed in memory (no re-read of the file for the replicate manifest)."""
+    import hashlib
+
+    data = npz_bytes(arrays, level)
+    write_bytes_atomic(path, data)
+    return hashlib.sha256(data).hexdigest(), len(data)
+
+
+def df_npz_arrays(obj: pd.DataFrame) -> dict:
+    """The data / index / columns arrays :func:`save_df_to_npz` stores for ``obj``."""
+    return {"data": _plain_values(obj), "index": _plain_array(obj.index.values),
+            "columns": _plain_array(obj.columns.values)}
+
+
 def save_df_to_npz(obj: pd.DataFrame, filename: str, level: int | None = None) -> None:
     """Compressed npz with keys data / index / columns -- the cnmf.py:32-33 contract.
     ``level``: zlib level (default NPZ_COMPRESSLEVEL; 0 = stored, for intermediates)."""

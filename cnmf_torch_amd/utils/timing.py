@@ -50,14 +50,37 @@ class StageTimer:
 
 
 def append_jsonl(path: str, record: dict) -> None:
-    line = json.dumps(record, sort_keys=True) + "\n"
+    append_jsonl_many(path, [record])
+
+
+def append_jsonl_many(path: str, records) -> None:
+    """Append many records with ONE open/write (factorize logs a whole replicate batch at
+    a time: one open per replicate cost 0.37 s per 900 replicates)."""
+    text = "".join(json.dumps(r, sort_keys=True) + "\n" for r in records)
+    if not text:
+        return
     with _lock:
         with open(path, "a") as fh:
-            fh.write(line)
+            fh.write(text)
 
 
 def read_jsonl(path: str) -> list[dict]:
+    """Records of a JSONL log.  A line that does not decode -- the torn tail a process
+    killed mid-append leaves behind (fault injection / resume) -- is skipped with a
+    warning instead of failing the whole read."""
     if not os.path.exists(path):
         return []
+    out, bad = [], 0
     with open(path) as fh:
-        return [json.loads(l) for l in fh if l.strip()]
+        for line in fh:
+            if not line.strip():
+                continue
+            try:
+                out.append(json.loads(line))
+            except json.JSONDecodeError:
+                bad += 1
+    if bad:
+        import warnings
+
+        warnings.warn(f"{path}: skipped {bad} undecodable line(s) (torn append?)")
+    return out

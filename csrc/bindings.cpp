@@ -231,4 +231,27 @@ PYBIND11_MODULE(_hip, m) {
                                  stream_id, mode, reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_philox_fill");
         });
+
+  m.def("gemm_planes_bk", [](int pb) { return cnmf_gemm_planes_bk(pb); });
+  m.def("gemm_planes_tile", [](int v, int which) { return cnmf_gemm_planes_tile(v, which); });
+  m.def("gemm_planes",
+        [](uintptr_t A, long long lda, long long a_plane, int a_rows, uintptr_t B,
+           long long ldb, long long b_plane, int b_rows, uintptr_t C, long long ldc,
+           uintptr_t col_scale, int M, int N, int Kd, int pa, int pb, int accumulate,
+           int variant, int ksplit, uintptr_t slab, uintptr_t stream) {
+          check(cnmf_gemm_planes(P<const unsigned short>(A), lda, a_plane, a_rows,
+                                 P<const unsigned short>(B), ldb, b_plane, b_rows, P<float>(C),
+                                 ldc, P<const float>(col_scale), M, N, Kd, pa, pb, accumulate,
+                                 variant, ksplit, P<float>(slab),
+                                 reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_gemm_planes");
+        });
+  m.def("split_planes",
+        [](uintptr_t S, long long lds, int rows, int cols, int cols_pad, uintptr_t col_mul,
+           uintptr_t Pl, long long ldp, long long plane, int nplanes, uintptr_t stream) {
+          check(cnmf_split_planes(P<const float>(S), lds, rows, cols, cols_pad,
+                                  P<const float>(col_mul), P<unsigned short>(Pl), ldp, plane,
+                                  nplanes, reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_split_planes");
+        });
 }

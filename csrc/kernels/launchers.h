@@ -99,4 +99,15 @@ hipError_t cnmf_philox_fill(float* out, long long rows, long long cols, long lon
                             long long s_col, long long rep_stride, long long row_offset,
                             const unsigned long long* seeds, const float* scales, int R,
                             unsigned int stream_id, int mode, hipStream_t stream);
+int cnmf_gemm_planes_bk(int pb);
+int cnmf_gemm_planes_tile(int v, int which);
+hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_plane, int a_rows,
+                            const unsigned short* B, long long ldb, long long b_plane, int b_rows,
+                            float* C, long long ldc, const float* col_scale, int M, int N,
+                            int Kd, int pa, int pb, int accumulate, int variant, int ksplit,
+                            float* slab, hipStream_t stream);
+hipError_t cnmf_split_planes(const float* S, long long lds, int rows, int cols, int cols_pad,
+                             const float* col_mul, unsigned short* P, long long ldp,
+                             long long plane, int nplanes, hipStream_t stream);
+
 }

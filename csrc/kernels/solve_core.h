@@ -128,59 +128,75 @@ __device__ __forceinline__ void load_group(ColGroup<K, U>& cg, int j, int T, int
 // arrives on the epoch counter with an agent-scope release; after all S arrived every
 // workgroup sums the S slots in slice order -> identical, deterministic totals
 // everywhere.  Spins are bounded: on timeout the flag is raised and the host fails.
+// Returns false once the launch's timeout flag is up (this or any earlier exchange gave
+// up): the caller then stops iterating, so slices that diverged never wait for each
+// other again and the launch drains quickly.
 // (Recipe: cdna_hip_programming.md Guideline 16 -- release before the counter add,
 // acquire after the poll, vmcnt drained around the fence.)
-__device__ __forceinline__ void coop_sum2(const SolveParams& p, int rep, int e, float& a,
+__device__ __forceinline__ bool coop_sum2(const SolveParams& p, int rep, int e, float& a,
                                           float& b, float* sred) {
   const int S = gridDim.y;
   const int slice = blockIdx.y;
-  if (S <= 1) return;
+  if (S <= 1) return true;
   if (e >= p.coop_epochs) {  // workspace too small: treat as timeout (host sizes it)
     if (threadIdx.x == 0) atomicExch(p.coop_timeout, 2);
-    return;
+    return false;
   }
   float* slots = p.coop_slots + (((long long)rep * p.coop_epochs + e) * S) * 2;
   unsigned long long* cnt = p.coop_count + (long long)rep * p.coop_epochs + e;
   const unsigned long long tag = (unsigned long long)p.coop_gen << 32;
   constexpr unsigned long long kHi = 0xffffffff00000000ull;
   if (threadIdx.x == 0) {
-    slots[2 * slice] = a;
-    slots[2 * slice + 1] = b;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // arrive: a counter still tagged with an older launch restarts at 1
-    unsigned long long old = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (true) {
-      const unsigned long long want = (old & kHi) == tag ? old + 1 : (tag | 1ull);
-      if (__hip_atomic_compare_exchange_strong(cnt, &old, want, __ATOMIC_RELAXED,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        break;
-    }
-    unsigned spins = 0;
-    while (true) {
-      const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
-      if ((v & kHi) == tag && (int)(v & 0xffffffffull) >= S) break;
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {
-        atomicExch(p.coop_timeout, 1);
-        break;
+    int ok = __hip_atomic_load(p.coop_timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    if (ok) {
+      slots[2 * slice] = a;
+      slots[2 * slice + 1] = b;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // arrive: a counter still tagged with an older launch restarts at 1
+      unsigned long long old = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (true) {
+        const unsigned long long want = (old & kHi) == tag ? old + 1 : (tag | 1ull);
+        if (__hip_atomic_compare_exchange_strong(cnt, &old, want, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+          break;
       }
+      unsigned spins = 0;
+      while (true) {
+        const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+        if ((v & kHi) == tag && (int)(v & 0xffffffffull) >= S) break;
+        __builtin_amdgcn_s_sleep(2);
+        ++spins;
+        if ((spins & 1023u) == 0 &&
+            __hip_atomic_load(p.coop_timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+          ok = 0;  // another replicate's exchange already gave up: stop waiting
+          break;
+        }
+        if (spins > (1u << 24)) {
+          atomicExch(p.coop_timeout, 1);
+          ok = 0;
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      float ta = 0.f, tb = 0.f;
+      for (int s2 = 0; s2 < S; ++s2) {
+        ta += __hip_atomic_load(slots + 2 * s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tb += __hip_atomic_load(slots + 2 * s2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      sred[0] = ta;
+      sred[1] = tb;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    float ta = 0.f, tb = 0.f;
-    for (int s2 = 0; s2 < S; ++s2) {
-      ta += __hip_atomic_load(slots + 2 * s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      tb += __hip_atomic_load(slots + 2 * s2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    sred[0] = ta;
-    sred[1] = tb;
+    sred[2] = ok ? 1.f : 0.f;
   }
   __syncthreads();
   a = sred[0];
   b = sred[1];
+  const bool good = sred[2] != 0.f;
   __syncthreads();
+  return good;
 }
 
 // Row k of the padded LDS Gram into row[KP] (KP/4 broadcast b128 reads).
@@ -340,7 +356,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
   constexpr int KP = gram_pad(K);
   constexpr bool resident = RES != 0;
   __shared__ __attribute__((aligned(16))) float sGm[K * KP];
-  __shared__ float sred[2 * 16];
+  __shared__ float sred[2 * 16 + 1];
   constexpr int NS = (U * K) | 1;
   __shared__ float sNm[resident ? NS * 1024 : 1];
   const lds_float* sG = (const lds_float*)sGm;  // LDS (addrspace 3): ds_read, 32-bit address
@@ -410,7 +426,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
         float f = q - 2.f * l;
         if (coop) {
           float unused = 0.f;
-          coop_sum2(p, rep, epoch++, f, unused, sred);
+          if (!coop_sum2(p, rep, epoch++, f, unused, sred)) break;
         }
         if (have_prev && fabsf(f_prev - f) <= p.tol * fabsf(f_prev)) break;
         f_prev = f;
@@ -422,7 +438,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
       ++it;
       if (!check_conv || loss_conv) continue;
       block_sum2(d2, x2, sred);
-      if (coop) coop_sum2(p, rep, epoch++, d2, x2, sred);
+      if (coop && !coop_sum2(p, rep, epoch++, d2, x2, sred)) break;
       if (sqrtf(d2) / (sqrtf(x2) + eps) < p.tol) break;
     }
     store_group<K, U>(rg, rx, sx);
@@ -437,7 +453,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
         CNMF_LINQUAD_GROUP(rg, CNMF_NLDS);
       }
       block_sum2(lin, quad, sred);
-      if (coop) coop_sum2(p, rep, epoch++, lin, quad, sred);
+      if (coop) (void)coop_sum2(p, rep, epoch++, lin, quad, sred);
       if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
         if (check_conv) {
           if (p.lin_out) p.lin_out[rep] = lin;
@@ -454,7 +470,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
         float f = block_objective<K, U>(rx, sx, rn, sn, sG, j0, n, p.l1_num, l1, l2, sred);
         if (coop) {
           float unused = 0.f;
-          coop_sum2(p, rep, epoch++, f, unused, sred);
+          if (!coop_sum2(p, rep, epoch++, f, unused, sred)) break;
         }
         if (have_prev && fabsf(f_prev - f) <= p.tol * fabsf(f_prev)) break;
         f_prev = f;
@@ -472,7 +488,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
       ++it;
       if (!check_conv || loss_conv) continue;
       block_sum2(d2, x2, sred);
-      if (coop) coop_sum2(p, rep, epoch++, d2, x2, sred);
+      if (coop && !coop_sum2(p, rep, epoch++, d2, x2, sred)) break;
       if (sqrtf(d2) / (sqrtf(x2) + eps) < p.tol) break;
     }
     if (p.lin_out || p.quad_out) {
@@ -484,7 +500,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
         CNMF_LINQUAD_GROUP(cg, CNMF_NREG_CG);
       }
       block_sum2(lin, quad, sred);
-      if (coop) coop_sum2(p, rep, epoch++, lin, quad, sred);
+      if (coop) (void)coop_sum2(p, rep, epoch++, lin, quad, sred);
       if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
         if (check_conv) {
           if (p.lin_out) p.lin_out[rep] = lin;

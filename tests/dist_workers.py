@@ -20,13 +20,16 @@ def dp_solver_worker(rank, world, port, X, K, seeds, opts_kw, out_dir):
     _init(rank, world, port)
     from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
     from cnmf_torch_amd.parallel.comm import DistComm
-    from cnmf_torch_amd.parallel.runner import row_block
+    from cnmf_torch_amd.parallel.runner import dp_layout, dp_row_segments
 
-    a, b = row_block(X.shape[0], rank, world)
-    Xl = torch.from_numpy(X[a:b])
+    segs = dp_row_segments(X.shape[0], opts_kw["online_chunk_size"], rank, world)
+    row_map, sched = dp_layout(segs)
+    Xl = torch.from_numpy(np.concatenate([X[a:b] for a, b in segs]))
     solver = NMFBatchSolver(Xl, NMFOptions(n_components=K, **opts_kw), comm=DistComm(),
-                            row_offset=a)
-    res = solver.run(seeds)
+                            row_map=row_map, schedule=sched)
+    res = solver.run(seeds, ks=opts_kw.get("_ks"))
+    np.save(os.path.join(out_dir, f"rows{rank}.npy"),
+            np.concatenate([np.arange(a, b) for a, b in segs]))
     np.save(os.path.join(out_dir, f"W{rank}.npy"), res.W.numpy())
     np.save(os.path.join(out_dir, f"HT{rank}.npy"), res.HT.numpy())
     np.save(os.path.join(out_dir, f"err{rank}.npy"), res.err)

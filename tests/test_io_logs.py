@@ -1,0 +1,90 @@
+"""Replicate logs / manifest robustness."""
+import json
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from cnmf_torch_amd.utils.io import load_df_from_npz, save_arrays_npz_digest
+from cnmf_torch_amd.utils.timing import append_jsonl_many, read_jsonl
+
+
+def test_read_jsonl_skips_a_torn_tail(tmp_path):
+    p = str(tmp_path / "log.jsonl")
+    append_jsonl_many(p, [{"a": 1}, {"a": 2}])
+    with open(p, "a") as fh:
+        fh.write('{"a": 3, "b"')          # process killed mid-append
+    with pytest.warns(UserWarning, match="undecodable"):
+        recs = read_jsonl(p)
+    assert recs == [{"a": 1}, {"a": 2}]
+
+
+def test_npz_digest_matches_file_and_loads_as_dataframe(tmp_path):
+    import hashlib
+
+    p = str(tmp_path / "x.df.npz")
+    data = np.arange(12, dtype=np.float32).reshape(3, 4)
+    digest, size = save_arrays_npz_digest(p, {"data": data, "index": np.arange(1, 4),
+                                              "columns": np.array(["g1", "g2", "g3", "g4"])})
+    raw = open(p, "rb").read()
+    assert hashlib.sha256(raw).hexdigest() == digest and len(raw) == size
+    df = load_df_from_npz(p)
+    assert list(df.columns) == ["g1", "g2", "g3", "g4"] and list(df.index) == [1, 2, 3]
+    np.testing.assert_array_equal(df.values, data)
+
+
+def test_verify_replicates_survives_torn_manifest(tmp_path):
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.utils.synthetic import simulate_counts
+    from cnmf_torch_amd.utils.io import save_df_to_npz
+
+    X, cells, genes = simulate_counts(300, 400, 3, seed=0, sparse=False)
+    counts = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(X, index=cells, columns=genes), counts)
+    obj = cNMF(output_dir=str(tmp_path), name="t")
+    obj.prepare(counts, components=[3, 4], n_iter=2, seed=1, num_highvar_genes=200)
+    obj.factorize(verbose=False)
+    assert obj.verify_replicates() == []
+    with open(obj.paths["replicate_manifest"], "a") as fh:
+        fh.write('{"k": 3, "it')
+    with pytest.warns(UserWarning):
+        assert obj.verify_replicates() == []
+    recs = read_jsonl(obj.paths["replicate_log"])
+    assert sorted((r["k"], r["iter"]) for r in recs) == [(3, 0), (3, 1), (4, 0), (4, 1)]
+    assert all(json.dumps(r) for r in recs)
+
+
+def test_stored_zip_fast_path_is_a_standard_npz(tmp_path):
+    import zipfile
+
+    from cnmf_torch_amd.utils.io import npy_bytes, npz_bytes
+
+    cols = np.array(["a", "bb", "ccc"])
+    raw = npz_bytes({"data": np.ones((2, 3), np.float32), "index": np.arange(1, 3),
+                     "columns": npy_bytes(cols)})
+    p = tmp_path / "f.npz"
+    p.write_bytes(raw)
+    with zipfile.ZipFile(p) as zf:
+        assert zf.testzip() is None
+        assert sorted(zf.namelist()) == ["columns.npy", "data.npy", "index.npy"]
+    with np.load(p, allow_pickle=False) as f:
+        np.testing.assert_array_equal(f["columns"], cols)
+        np.testing.assert_array_equal(f["data"], np.ones((2, 3), np.float32))
+
+
+def test_npz_template_files_load_and_hash(tmp_path):
+    import hashlib
+
+    from cnmf_torch_amd.utils.io import NpzTemplate
+
+    genes = np.array(["g%d" % i for i in range(50)])
+    t = NpzTemplate({"columns": genes})
+    for k in (3, 5):
+        p = str(tmp_path / f"s{k}.df.npz")
+        data = np.random.default_rng(k).random((k, 50)).astype(np.float32)
+        digest, size = t.write(p, {"index": np.arange(1, k + 1), "data": data})
+        raw = open(p, "rb").read()
+        assert hashlib.sha256(raw).hexdigest() == digest and len(raw) == size
+        df = load_df_from_npz(p)
+        np.testing.assert_array_equal(df.values, data)
+        assert list(df.index) == list(range(1, k + 1)) and list(df.columns) == list(genes)

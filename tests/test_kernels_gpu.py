@@ -642,3 +642,135 @@ def test_online_beta_gpu_converges_like_cpu(beta_loss):
     assert (np.abs(on_g.err - ba_g.err) / ba_g.err < 0.01).all(), (on_g.err, ba_g.err)
     np.testing.assert_allclose(on_g.err, on_c.err, rtol=5e-3)
     assert np.abs(on_g.n_iter - on_c.n_iter).max() <= 3, (on_g.n_iter, on_c.n_iter)
+
+
+def test_refit_raises_when_a_cooperative_solve_timed_out():
+    """A raised cooperative-timeout flag (workgroups not co-resident) must surface as an
+    error from the usage refit, and the kernels must stop waiting on it."""
+    from cnmf_torch_amd.models.refit import fit_H_online
+
+    rs = np.random.default_rng(1)
+    X = rs.random((3000, 200)).astype(np.float32)
+    W = rs.random((5, 200)).astype(np.float32)
+    H = fit_H_online(X, W, chunk_size=3000, device="cuda")     # one chunk -> coop split
+    assert np.isfinite(H).all()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ws = ops._COOP_WS.get((str(dev), torch.cuda.current_stream().cuda_stream))
+    assert ws is not None, "the refit did not take the cooperative path"
+    ws["flag"].fill_(1)
+    with pytest.raises(RuntimeError, match="cooperative solve failed"):
+        fit_H_online(X, W, chunk_size=3000, device="cuda")
+    ops.coop_check(torch.device("cuda"))    # flag consumed by the raise: clean again
+    assert int(ws["flag"].item()) == 0
+
+
+@pytest.mark.parametrize("mode", ["online", "batch"])
+def test_mixed_k_ragged_batch_gpu_matches_single_k(mode):
+    """The K x n_iter grid as ONE ragged batch on the GPU == per-K batches."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+
+    rs = np.random.default_rng(3)
+    N, G = 2000, 300
+    X = torch.from_numpy((rs.gamma(1, 1, (N, 8)) @ rs.gamma(0.5, 1, (8, G))
+                          + 0.1 * rs.random((N, G))).astype(np.float32)).cuda()
+    kw = dict(mode=mode, online_chunk_size=900, online_max_pass=8, batch_max_iter=60)
+    ks = [5, 7, 5, 13, 7, 13, 5, 7, 24, 5]
+    seeds = list(range(31, 41))
+    mixed = NMFBatchSolver(X, NMFOptions(n_components=5, **kw)).run(seeds, ks=ks)
+    for K in sorted(set(ks)):
+        idx = [i for i, k in enumerate(ks) if k == K]
+        ref = NMFBatchSolver(X, NMFOptions(n_components=K, **kw)).run([seeds[i] for i in idx])
+        for j, i in enumerate(idx):
+            assert abs(int(mixed.n_iter[i]) - int(ref.n_iter[j])) <= 1
+            np.testing.assert_allclose(mixed.err[i], ref.err[j], rtol=2e-3)
+            a, b = mixed.spectra(i).cpu().numpy(), ref.spectra(j).cpu().numpy()
+            cos = (a * b).sum(1) / (np.linalg.norm(a, axis=1) * np.linalg.norm(b, axis=1))
+            assert cos.min() > 0.98, cos
+
+
+@pytest.mark.parametrize("rows,cols", [(37, 50), (300, 2000), (1, 7)])
+def test_split_planes_bitwise_matches_reference(rows, cols):
+    g = torch.Generator().manual_seed(rows)
+    S = (torch.rand((rows, cols), generator=g) * 50 - 5) ** 3
+    mul = torch.rand(cols, generator=g) + 0.5
+    ld = -(-cols // 64) * 64
+    out = torch.zeros((3, rows, ld), dtype=torch.int16, device="cuda")
+    ops.split_planes(S.cuda(), out, col_mul=mul.cuda())
+    ref = reference.split_planes(S * mul, 3, ld)
+    assert torch.equal(out.cpu(), ref)
+    # exact: the planes sum back to the scaled fp32 input
+    back = reference.planes_to_f64(out.cpu()).sum(0)[:, :cols]
+    assert torch.equal(back.float(), S * mul)
+
+
+@pytest.mark.parametrize("pb", [1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(1000, 5000, 2000), (83, 130, 96), (8100, 700, 320)])
+def test_gemm_planes_matches_fp64(pb, M, N, K):
+    """Split-precision MFMA GEMM == the fp64 product to fp32-GEMM accuracy, including
+    ragged edges, a B row offset, accumulation and a per-column output scale."""
+    g = torch.Generator().manual_seed(M + N + pb)
+    bk = ops.planes_bk(pb)
+    Kd = -(-K // bk) * bk
+    A = torch.rand((M, K), generator=g)
+    if pb < 3:   # integer "counts" held exactly in pb planes
+        B = torch.randint(0, 200 if pb == 1 else 3000, (N + 40, K), generator=g).float()
+    else:
+        B = torch.rand((N + 40, K), generator=g)
+    scale = torch.rand(N, generator=g) + 0.5
+    Ap = torch.zeros((3, M, Kd), dtype=torch.int16, device="cuda")
+    Bp = torch.zeros((pb, N + 40, Kd), dtype=torch.int16, device="cuda")
+    ops.split_planes(A.cuda(), Ap)
+    ops.split_planes(B.cuda(), Bp)
+    if pb < 3:
+        assert torch.equal(reference.planes_to_f64(Bp.cpu()).sum(0)[:, :K], B.double())
+    C0 = torch.rand((M, N), generator=g)
+    C = C0.clone().cuda()
+    ops.gemm_planes(C, Ap, Bp[:, 40:], M, N, Kd, accumulate=True, col_scale=scale.cuda())
+    ref = C0.double() + (A.double() @ B[40:].double().t()) * scale.double()
+    err = (C.cpu().double() - ref).abs().max() / ref.abs().max()
+    # an fp32 GEMM over K terms: ~K * 2^-24 worst case, far less in practice
+    assert err < 4e-7 * max(1.0, K / 256), float(err)
+    C2 = torch.empty((M, N), device="cuda")
+    ops.gemm_planes(C2, Ap, Bp[:, 40:], M, N, Kd)
+    ref2 = A.double() @ B[40:].double().t()
+    assert float((C2.cpu().double() - ref2).abs().max() / ref2.abs().max()) < 4e-7 * max(1.0, K / 256)
+
+
+def test_count_units_detects_scaled_counts():
+    from cnmf_torch_amd.models.nmf import _XPlanes, _count_units
+
+    rs = np.random.default_rng(0)
+    C = rs.poisson(rs.gamma(0.3, 3, (1, 400)), (3000, 400)).astype(np.float64)
+    C[:, 5] = 0
+    C[:, 7] = 2 * rs.integers(1, 5, 3000)          # smallest count 2
+    std = C.std(0, ddof=1)
+    std[std == 0] = 1
+    X = torch.from_numpy((C / std).astype(np.float32)).cuda()
+    u = _count_units(X)
+    assert u is not None
+    back = torch.round(X / u) * u
+    assert float(((back - X).abs() / X.abs().clamp(min=1e-30)).max()) < 3e-7
+    xp = _XPlanes(X)
+    assert xp.pb == (1 if C.max() <= 256 else 2)
+    assert _count_units(X + 0.01 * torch.rand_like(X)) is None
+
+
+def test_split_gemm_solver_matches_fp32_library_gemm(monkeypatch):
+    """The NMF solve with the split-precision MFMA GEMMs == the same solve on the fp32
+    library GEMMs (CNMF_GEMM=torch) to fp32 reassociation noise."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(3000, 500, n_programs=6, seed=1)).cuda()
+    kw = dict(online_chunk_size=1000, online_max_pass=10)
+    seeds = list(range(1, 9))
+    ks = [5, 6, 7, 6, 5, 7, 9, 9]
+    planes = NMFBatchSolver(X, NMFOptions(n_components=5, **kw))
+    a = planes.run(seeds, ks=ks)
+    assert planes._planes() is not None and planes._planes().pb in (1, 2)
+    monkeypatch.setenv("CNMF_GEMM", "torch")
+    lib = NMFBatchSolver(X, NMFOptions(n_components=5, **kw))
+    b = lib.run(seeds, ks=ks)
+    assert lib._planes() is None
+    np.testing.assert_allclose(a.err, b.err, rtol=1e-4)
+    assert np.abs(a.n_iter - b.n_iter).max() <= 1

@@ -201,3 +201,41 @@ def test_beta_h_loss_rule_checks_every_n_steps():
             break
     assert stopped_at, "loose tolerance must stop"
     assert all(s % 5 == 0 and s >= 5 for s in stopped_at.values()), stopped_at
+
+
+@pytest.mark.parametrize("mode,algo", [("online", "mu"), ("online", "hals"), ("batch", "mu"),
+                                       ("online", "bpp")])
+def test_mixed_k_ragged_batch_matches_single_k_runs(mode, algo):
+    """The whole K x n_iter grid in ONE ragged batch (one pass loop, one data-side GEMM per
+    chunk for every K) gives every replicate exactly its single-K run: same passes, same
+    convergence flags, same factors up to fp64 summation order."""
+    X = torch.from_numpy(_data(300, 80, seed=2))
+    kw = dict(mode=mode, algo=algo, online_chunk_size=110, online_max_pass=6,
+              batch_max_iter=40, fp_precision="double")
+    ks = [3, 5, 3, 4, 5, 4, 3]
+    seeds = [11, 12, 13, 14, 15, 16, 17]
+    solver = NMFBatchSolver(X, NMFOptions(n_components=3, **kw))
+    mixed = solver.run(seeds, ks=ks)
+    assert mixed.K is None and list(mixed.ks) == ks
+    for K in sorted(set(ks)):
+        idx = [i for i, k in enumerate(ks) if k == K]
+        ref = NMFBatchSolver(X, NMFOptions(n_components=K, **kw)).run([seeds[i] for i in idx])
+        for j, i in enumerate(idx):
+            assert mixed.n_iter[i] == ref.n_iter[j]
+            assert mixed.converged[i] == ref.converged[j]
+            np.testing.assert_allclose(mixed.err[i], ref.err[j], rtol=1e-9)
+            np.testing.assert_allclose(mixed.spectra(i).numpy(), ref.spectra(j).numpy(),
+                                       rtol=1e-7, atol=1e-10)
+            np.testing.assert_allclose(mixed.usages(i).numpy(), ref.usages(j).numpy(),
+                                       rtol=1e-7, atol=1e-10)
+
+
+def test_mixed_k_beta_request_splits_by_k():
+    X = torch.from_numpy(_data(200, 60, seed=4))
+    kw = dict(beta_loss="kullback-leibler", online_chunk_size=100, online_max_pass=3,
+              fp_precision="double")
+    solver = NMFBatchSolver(X, NMFOptions(n_components=2, **kw))
+    res = solver.run([5, 6, 7], ks=[4, 2, 4])
+    ref4 = NMFBatchSolver(X, NMFOptions(n_components=4, **kw)).run([5, 7])
+    np.testing.assert_allclose(res.spectra(2).numpy(), ref4.spectra(1).numpy(), rtol=1e-9)
+    assert res.spectra(1).shape == (2, 60)
