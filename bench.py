@@ -8,14 +8,23 @@ factorize settings (cnmf.py:757-771): online MU, Frobenius, tol 1e-4, chunk 5000
 online_chunk_max_iter = max_NMF_iter = 1000, random init from the ledger seeds.
 
 One *step* = factorising one ledger batch of ``--n-iter`` (default 100) replicates to
-convergence on each GPU -- the whole cNMF ``factorize`` work for that batch (init,
-every pass, every inner solve, convergence checks; spectra copied back to the host as
-factorize persists them).  Scaling is *weak*: every rank factorises its own 100
-replicates (round-robin ledger shard, as ``worker_filter``), so the job does 100*N
-replicates per step.  ``value`` is whole-job replicates/sec.
+convergence -- the whole cNMF ``factorize`` work for that batch (init, every pass, every
+inner solve, convergence checks; spectra copied back to the host as factorize persists
+them).  ``value`` is whole-job replicates/sec.  ``--mode`` picks the multi-GPU scaling:
 
-Run: ``python bench.py [--gpus N --steps K --warmup W]``; for N > 1 under
-``torch.distributed.run`` (one process per GPU, RCCL over xGMI).
+* ``weak`` (default): every rank factorises its own 100 replicates (round-robin ledger
+  shard, as ``worker_filter``): the job does 100*N replicates per step.
+* ``strong``: one 100-replicate ledger batch per step, dealt round-robin over the ranks.
+* ``dp``: one 100-replicate batch per step solved by ALL ranks together on a
+  chunk-interleaved cell shard of X (parallel.runner.dp_row_segments) with the
+  per-step ``[dB | dA]`` statistics all-reduced on RCCL -- the config for matrices too
+  large for one GPU (BASELINE config 4); same factorisation path as one GPU.
+
+``--kmin/--kmax`` replace the single K by the K x n_iter grid of BASELINE config 2
+(K = kmin..kmax, ``--n-iter`` replicates each) solved as ONE ragged batch per step.
+
+Run: ``python bench.py [--gpus N --steps K --warmup W --mode weak|strong|dp]``; for
+N > 1 under ``torch.distributed.run`` (one process per GPU, RCCL over xGMI).
 """
 from __future__ import annotations
 
@@ -41,7 +50,11 @@ def main() -> int:
     ap.add_argument("--n-iter", type=int, default=100, help="replicates per GPU per step")
     ap.add_argument("--seed", type=int, default=14)
     ap.add_argument("--algo", default="mu")
-    ap.add_argument("--mode", default="online")
+    ap.add_argument("--nmf-mode", default="online", choices=["online", "batch"])
+    ap.add_argument("--mode", default="weak", choices=["weak", "strong", "dp"],
+                    help="multi-GPU scaling mode (see module docstring)")
+    ap.add_argument("--kmin", type=int, default=None)
+    ap.add_argument("--kmax", type=int, default=None)
     ap.add_argument("--beta-loss", default="frobenius")
     ap.add_argument("--max-nmf-iter", type=int, default=1000)
     ap.add_argument("--batch-size", type=int, default=5000)
@@ -67,26 +80,44 @@ def main() -> int:
                                 device_id=dev if use_cuda else None)
 
     from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.parallel.comm import DistComm
+    from cnmf_torch_amd.parallel.runner import dp_layout, dp_row_segments
     from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
 
     X = normalized_counts_matrix(args.cells, args.genes, n_programs=args.k, seed=0)
+    comm = row_map = schedule = None
+    if args.mode == "dp" and world > 1:
+        segs = dp_row_segments(X.shape[0], args.batch_size, rank, world)
+        X = np.concatenate([X[a:b] for a, b in segs])
+        row_map, schedule = dp_layout(segs)
+        comm = DistComm()
     Xd = torch.from_numpy(X).to(dev)
     opts = NMFOptions(n_components=args.k, init="random", beta_loss=args.beta_loss,
-                      algo=args.algo, mode=args.mode, tol=1e-4,
+                      algo=args.algo, mode=args.nmf_mode, tol=1e-4,
                       online_chunk_size=args.batch_size,
                       online_chunk_max_iter=args.max_nmf_iter)
-    solver = NMFBatchSolver(Xd, opts)
+    solver = NMFBatchSolver(Xd, opts, comm=comm, row_map=row_map, schedule=schedule)
 
     # Ledger seeds exactly as cNMF.prepare draws them (cnmf.py:738-741), one ledger batch
-    # per step; rank r takes every world-th replicate (worker_filter, cnmf.py:53-54).
-    n_total = args.n_iter * world
+    # per step; weak/strong: rank r takes every world-th replicate (worker_filter,
+    # cnmf.py:53-54); dp: every rank takes all of them.
+    grid = list(range(args.kmin, args.kmax + 1)) if args.kmin is not None else [args.k]
+    per_batch = args.n_iter * len(grid)
+    n_total = per_batch * world if args.mode == "weak" else per_batch
     nsteps = args.warmup + args.steps
     np.random.seed(args.seed)
     all_seeds = np.random.randint(low=1, high=(2 ** 31) - 1, size=n_total * nsteps)
+    all_ks = np.tile(np.repeat(grid, args.n_iter), n_total // per_batch)
 
     def step(i: int):
-        seeds = all_seeds[i * n_total:(i + 1) * n_total][rank::world]
-        res = solver.run_concurrent([int(s) for s in seeds], n_streams=args.streams)
+        seeds = all_seeds[i * n_total:(i + 1) * n_total]
+        ks = all_ks
+        if args.mode != "dp":
+            seeds, ks = seeds[rank::world], ks[rank::world]
+        if len(grid) == 1:
+            res = solver.run_concurrent([int(s) for s in seeds], n_streams=args.streams)
+        else:
+            res = solver.run([int(s) for s in seeds], ks=[int(k) for k in ks])
         spectra = res.W.cpu()  # factorize persists spectra (cnmf.py:889-892)
         return res, spectra
 
@@ -113,8 +144,14 @@ def main() -> int:
     ms_per_step = 1000.0 * elapsed / args.steps
     reps_per_sec = n_total * args.steps / elapsed
     if rank == 0:
+        metric = "NMF replicates/sec (K=10, n_iter=100)" if grid == [10] and args.n_iter == 100 \
+            else f"NMF replicates/sec (K={grid[0]}..{grid[-1]}, n_iter={args.n_iter})" \
+            if len(grid) > 1 else f"NMF replicates/sec (K={args.k}, n_iter={args.n_iter})"
+        par = {"weak": f"replicate-parallel x{world}",
+               "strong": f"replicate-parallel x{world} (fixed {n_total}-replicate ledger)",
+               "dp": f"cell-sharded DP x{world} (RCCL all-reduce per online step)"}[args.mode]
         out = {
-            "metric": "NMF replicates/sec (K=10, n_iter=100)",
+            "metric": metric,
             "value": round(reps_per_sec, 3),
             "unit": "replicates/s",
             "n_gpus": world,
@@ -122,18 +159,20 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.mode == "weak" else "strong",
             "vs_baseline": round(reps_per_sec / BASELINE_REPS_PER_SEC, 2),
             "dtype": "fp32",
             "data": "synthetic (planted-program Poisson counts, unit-variance genes; random-init W,H)",
             "config": {
-                "model": f"cNMF factorize: {args.mode} {args.algo.upper()} {args.beta_loss}, K={args.k}",
+                "model": f"cNMF factorize: {args.nmf_mode} {args.algo.upper()} {args.beta_loss}, "
+                         f"K={args.k if len(grid) == 1 else f'{grid[0]}..{grid[-1]}'}",
                 "global_batch": n_total,
                 "seq_len": None,
                 "cells": args.cells,
                 "genes": args.genes,
                 "n_iter_per_gpu": args.n_iter,
-                "parallelism": f"replicate-parallel x{world}",
+                "parallelism": par,
+                "scaling_mode": args.mode,
                 "streams_per_gpu": args.streams,
                 "device": "cpu" if not use_cuda else torch.cuda.get_device_name(dev),
                 "mean_passes": round(float(np.mean(passes)), 2) if passes else None,

@@ -63,6 +63,11 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--replicate-batch", type=int, default=None,
                    help="[factorize] Replicates solved together per launch (default: auto)")
     p.add_argument("--device", type=str, default=None, help="[factorize/consensus] torch device override")
+    p.add_argument("--dp", action="store_true", default=False,
+                   help="[factorize] cell-sharded data parallelism under torchrun: every rank "
+                        "holds a shard of the cells, all ranks solve every replicate with the "
+                        "statistics all-reduced on RCCL (for matrices too big for one GPU); "
+                        "default under torchrun is replicate parallelism")
     p.add_argument("--save-usages", action="store_true", default=False,
                    help="[factorize] Also persist per-replicate usages (iter_usages files)")
     p.add_argument("--skip-missing-files", action="store_true", default=False,
@@ -96,7 +101,12 @@ def main(argv=None) -> int:
                     batch_size=args.batch_size, algo=args.algo, mode=args.mode)
     elif args.command == "factorize":
         world = int(os.environ.get("WORLD_SIZE", "1"))
-        if world > 1 and args.worker_index is None:
+        if args.dp:
+            from .parallel.runner import dp_factorize
+
+            dp_factorize(obj, skip_completed_runs=args.skip_completed_runs,
+                         replicate_batch=args.replicate_batch, save_usages=args.save_usages)
+        elif world > 1 and args.worker_index is None:
             from .parallel.runner import distributed_factorize
 
             distributed_factorize(obj, skip_completed_runs=args.skip_completed_runs,

@@ -60,6 +60,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--gpus", type=int, default=1, help="ranks for torchrun factorize")
     p.add_argument("--workers", type=int, default=None,
                    help="independent --worker-index processes instead of torchrun")
+    p.add_argument("--dp", action="store_true",
+                   help="cell-sharded data parallel factorize over --gpus ranks (one matrix "
+                        "too big for one GPU) instead of replicate parallelism")
     p.add_argument("--keep-iterations", action="store_true",
                    help="keep cnmf_tmp/*.iter_*.df.npz after combine (reference deletes them)")
     p.add_argument("--local-density-threshold", type=float, default=None,
@@ -99,7 +102,10 @@ def main(argv=None) -> int:
     elif a.gpus > 1:
         _run([py, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-              "-m", "cnmf_torch_amd", "factorize"] + base, env=env)
+              "-m", "cnmf_torch_amd", "factorize"] + base + (["--dp"] if a.dp else []),
+             env=env)
+    elif a.dp:
+        _run([py, "-m", "cnmf_torch_amd", "factorize", "--dp"] + base, env=env)
     else:
         _run([py, "-m", "cnmf_torch_amd", "factorize"] + base, env=env)
 

@@ -43,3 +43,26 @@ def test_bench_json_contract_two_ranks():
     # value is the whole-job rate: global replicates * steps / (max-rank) elapsed
     rate = 6 * 2 / (out["ms_per_step"] * 2 / 1000.0)
     assert abs(out["value"] - rate) / out["value"] < 0.01
+
+
+def test_bench_strong_and_dp_modes_two_ranks():
+    strong = _bench(["--mode", "strong"], 2)
+    assert strong["scaling"] == "strong" and strong["config"]["global_batch"] == 3
+    dp = _bench(["--mode", "dp"], 2)
+    assert dp["scaling"] == "strong" and dp["config"]["global_batch"] == 3
+    assert dp["config"]["parallelism"].startswith("cell-sharded DP x2")
+    rate = 3 * 2 / (dp["ms_per_step"] * 2 / 1000.0)
+    assert abs(dp["value"] - rate) / dp["value"] < 0.01
+
+
+def test_bench_dp_mode_same_factorisation_as_one_rank():
+    """The DP bench solves the same replicates as the one-GPU bench: same mean passes."""
+    one = _bench(["--mode", "dp"], 1)
+    two = _bench(["--mode", "dp"], 2)
+    assert abs(one["config"]["mean_passes"] - two["config"]["mean_passes"]) <= 0.5
+
+
+def test_bench_k_grid_ragged_batch():
+    out = _bench(["--kmin", "3", "--kmax", "5"], 1)
+    assert out["config"]["global_batch"] == 9 and out["metric"].startswith(
+        "NMF replicates/sec (K=3..5")

@@ -774,3 +774,26 @@ def test_split_gemm_solver_matches_fp32_library_gemm(monkeypatch):
     assert lib._planes() is None
     np.testing.assert_allclose(a.err, b.err, rtol=1e-4)
     assert np.abs(a.n_iter - b.n_iter).max() <= 1
+
+
+def test_coop_solve_with_a_concurrent_kernel_stream():
+    """Cooperative (spin-waiting) solves while another stream keeps the chip busy (the
+    situation of an RCCL kernel resident beside the solver under DP): results equal the
+    isolated solve and no cooperative wait gives up."""
+    x0, numer, gram = _problem(6, 10, 20000, seed=11)
+    ref_x = x0.clone().cuda()
+    ops.solve("mu", ref_x, numer.cuda(), gram.cuda(), max_iter=200, tol=1e-4, conv_mode=1)
+    side = torch.cuda.Stream()
+    big = torch.rand((4096, 4096), device="cuda")
+    x = x0.clone().cuda()
+    nu, gr = numer.cuda(), gram.cuda()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+        for _ in range(20):
+            big = torch.tanh(big @ big * 1e-3)
+    for _ in range(3):
+        x.copy_(x0.cuda())
+        ops.solve("mu", x, nu, gr, max_iter=200, tol=1e-4, conv_mode=1)
+    torch.cuda.synchronize()
+    ops.coop_check(torch.device("cuda"))
+    np.testing.assert_allclose(x.cpu().numpy(), ref_x.cpu().numpy(), rtol=1e-5, atol=1e-7)

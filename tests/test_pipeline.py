@@ -12,6 +12,16 @@ import torch
 from cnmf_torch_amd import cNMF, load_df_from_npz, save_df_to_npz
 from cnmf_torch_amd.utils.synthetic import simulate_counts
 
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -245,3 +255,30 @@ def test_replicate_manifest_detects_corruption(tmp_path):
     os.remove(obj.paths["iter_spectra"] % (3, 2))
     probs = {(p["iter"], p["problem"]) for p in obj.verify_replicates()}
     assert probs == {(1, "checksum mismatch"), (2, "missing")}
+
+
+def test_cli_dp_factorize_over_torchrun_matches_serial(tmp_path):
+    """`cnmf factorize --dp` under torchrun (2 gloo ranks here, RCCL on GPUs): the
+    chunk-interleaved cell shard all-reduces the same chunks as a single process, so the
+    replicate spectra equal a serial factorize to fp32 summation order."""
+    Xc, cells, genes = simulate_counts(400, 120, 3, seed=6, sparse=False)
+    fn = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(Xc, index=cells, columns=genes), fn)
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    objs = {}
+    for name in ("dp", "serial"):
+        obj = cNMF(output_dir=str(tmp_path), name=name)
+        obj.prepare(fn, components=[3, 4], n_iter=2, seed=3, num_highvar_genes=60, batch_size=96)
+        objs[name] = obj
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "cnmf_torch_amd", "factorize", "--output-dir", str(tmp_path), "--name", "dp",
+           "--dp"]
+    r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    objs["serial"].factorize(verbose=False)
+    for k in (3, 4):
+        for i in range(2):
+            a = load_df_from_npz(objs["dp"].paths["iter_spectra"] % (k, i)).values
+            b = load_df_from_npz(objs["serial"].paths["iter_spectra"] % (k, i)).values
+            np.testing.assert_allclose(a, b, rtol=5e-3, atol=1e-6)
