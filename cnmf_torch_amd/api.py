@@ -199,10 +199,19 @@ class cNMF:
     def prepare(self, counts_fn, components, n_iter=100, densify=False, tpm_fn=None, seed=None,
                 beta_loss="frobenius", num_highvar_genes=2000, genes_file=None, alpha_usage=0.0,
                 alpha_spectra=0.0, init="random", total_workers=-1, use_gpu=False,
-                batch_size=5000, max_NMF_iter=1000, algo="mu", mode="online"):
+                batch_size=5000, max_NMF_iter=1000, algo="mu", mode="online", comm=None):
         """Load counts, select over-dispersed genes, variance-normalise, write the
         replicate ledger (cnmf.py:458-596).  ``algo``/``mode`` are additions (defaults =
-        the reference's hard-coded 'mu'/'online')."""
+        the reference's hard-coded 'mu'/'online').  With a multi-rank ``comm`` the cells
+        are sharded over the ranks and the per-gene statistics are all-reduced
+        (:meth:`_prepare_sharded`)."""
+        if comm is not None and comm.world_size > 1:
+            return self._prepare_sharded(
+                comm, counts_fn, components, n_iter=n_iter, densify=densify, tpm_fn=tpm_fn,
+                seed=seed, beta_loss=beta_loss, num_highvar_genes=num_highvar_genes,
+                genes_file=genes_file, alpha_usage=alpha_usage, alpha_spectra=alpha_spectra,
+                init=init, total_workers=total_workers, use_gpu=use_gpu, batch_size=batch_size,
+                max_NMF_iter=max_NMF_iter, algo=algo, mode=mode)
         with self.timer("prepare"):
             input_counts = read_any(counts_fn, densify)
             if sp.issparse(input_counts.X) and densify:
@@ -248,6 +257,121 @@ class cNMF:
                 total_workers=total_workers, use_gpu=use_gpu, batch_size=batch_size,
                 max_iter=max_NMF_iter, algo=algo, mode=mode)
             self.save_nmf_iter_params(replicate_params, run_params)
+
+    def _prepare_sharded(self, comm, counts_fn, components, n_iter, densify, tpm_fn, seed,
+                         beta_loss, num_highvar_genes, genes_file, alpha_usage, alpha_spectra,
+                         init, total_workers, use_gpu, batch_size, max_NMF_iter, algo, mode):
+        """Cell-sharded prepare: rank r holds a contiguous block of
+        cells (partial h5ad read), computes its TPM rows, and the per-gene statistics --
+        TPM mean/variance for tpm_stats and the over-dispersion model, the ddof=1 std of
+        the HVG counts for the unit-variance scaling -- are combined across ranks by
+        all-reduces (two-pass: global mean first, then centred sums of squares, so the
+        variances equal the single-process ones to summation order).  Rank 0 gathers the
+        row blocks and writes the artifacts of the single-process prepare."""
+        from .parallel.runner import row_block
+        from .utils.h5ad import h5ad_shape, read_X_rows, read_h5ad_annotations
+
+        rank, world = comm.rank, comm.world_size
+        with self.timer("prepare"):
+            if tpm_fn is not None:
+                raise NotImplementedError("sharded prepare computes the TPM itself "
+                                          "(tpm_fn: run prepare on one rank)")
+            if str(counts_fn).endswith(".h5ad"):
+                n_rows, _ = h5ad_shape(counts_fn)
+                a, b = row_block(n_rows, rank, world)
+                ann = read_h5ad_annotations(counts_fn)
+                counts = AnnData(X=read_X_rows(counts_fn, a, b), obs=ann.obs.iloc[a:b],
+                                 var=ann.var)
+            else:
+                full = read_any(counts_fn, densify)
+                n_rows = full.shape[0]
+                a, b = row_block(n_rows, rank, world)
+                counts = AnnData(X=full.X[a:b], obs=full.obs.iloc[a:b], var=full.var)
+                del full
+            if sp.issparse(counts.X) and densify:
+                counts.X = np.asarray(counts.X.todense())
+            sparse_in = sp.issparse(counts.X)
+            tpm = compute_tpm(counts)
+
+            def col_sum(M):
+                return np.asarray(M.sum(axis=0), dtype=np.float64).reshape(-1)
+
+            def mean_var(M, ddof):
+                """Global column mean / variance of the row-sharded M (two-pass)."""
+                n = comm.allreduce_scalar(float(M.shape[0]))
+                s1 = torch.from_numpy(col_sum(M))
+                comm.allreduce_(s1)
+                mean = s1.numpy() / max(n, 1.0)
+                if sp.issparse(M):
+                    Mc = M.tocsc() if not sp.isspmatrix_csc(M) else M
+                    d = Mc.data.astype(np.float64) - np.repeat(mean, np.diff(Mc.indptr))
+                    nnz = np.diff(Mc.indptr).astype(np.float64)
+                    m2 = np.bincount(np.repeat(np.arange(M.shape[1]), np.diff(Mc.indptr)),
+                                     weights=d * d, minlength=M.shape[1])
+                    m2 = m2 + (M.shape[0] - nnz) * mean * mean
+                else:
+                    d = np.asarray(M, dtype=np.float64) - mean
+                    m2 = (d * d).sum(axis=0)
+                m2 = torch.from_numpy(np.ascontiguousarray(m2, dtype=np.float64))
+                comm.allreduce_(m2)
+                return mean, m2.numpy() / max(n - ddof, 1.0)
+
+            gene_tpm_mean, gene_tpm_var = mean_var(tpm.X, 0)
+            if tpm.X.dtype == np.float32:     # sklearn's StandardScaler keeps the input dtype
+                gene_tpm_mean = gene_tpm_mean.astype(np.float32)
+                gene_tpm_var = gene_tpm_var.astype(np.float32)
+            gene_tpm_std = gene_tpm_var ** 0.5
+            stats = pd.DataFrame([gene_tpm_mean, gene_tpm_std], index=["__mean", "__std"],
+                                 columns=tpm.var.index).T
+            if genes_file is not None:
+                with open(genes_file) as fh:
+                    hvgs = fh.read().rstrip().split("\n")
+            else:
+                from .models.hvg import _fano_model
+
+                gstats, _ = _fano_model(pd.Series(gene_tpm_mean), pd.Series(gene_tpm_var),
+                                        None, 0.5, num_highvar_genes)
+                hvgs = list(tpm.var.index[gstats.high_var.values])
+            cols = counts.var.index.get_indexer(hvgs)
+            if (cols < 0).any():
+                raise KeyError(f"genes missing from the counts: {list(np.array(hvgs)[cols < 0][:5])}")
+            Xh = counts.X[:, cols]
+            Xh = Xh.astype(np.float64) if sp.issparse(Xh) else np.asarray(Xh, dtype=np.float64)
+            _, hv_var = mean_var(Xh, 1)
+            std = np.sqrt(hv_var)
+            if sparse_in:          # scanpy scale(zero_center=False): std 0 -> 1
+                std[std == 0] = 1.0
+                Xh = sp.csr_matrix(Xh)
+                Xh.data = Xh.data / std[Xh.indices]
+            else:                  # dense reference path: X / X.std(ddof=1), no guard
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    Xh = Xh / std
+            zero = np.asarray(Xh.sum(axis=1)).reshape(-1) == 0
+            n_zero = int(comm.allreduce_scalar(float(zero.sum())))
+            if n_zero > 0:
+                ex = counts.obs.index[zero][:4]
+                raise Exception(
+                    "Error: %d cells have zero counts of overdispersed genes. E.g. %s. Filter "
+                    "those cells and re-run or adjust the number of overdispersed genes. "
+                    "Quitting!" % (n_zero, ", ".join(ex)))
+            parts = comm.gather_object((tpm.X, Xh, counts.obs), dst=0)
+            if rank == 0:
+                stack = (lambda ms: sp.vstack(ms, format="csr")) if sparse_in else np.concatenate
+                obs = pd.concat([p_[2] for p_ in parts])
+                write_h5ad(self.paths["tpm"], AnnData(X=stack([p_[0] for p_ in parts]), obs=obs,
+                                                      var=tpm.var))
+                save_df_to_npz(stats, self.paths["tpm_stats"])
+                write_text_atomic(self.paths["nmf_genes_list"], "\n".join(hvgs))
+                norm = AnnData(X=stack([p_[1] for p_ in parts]), obs=obs,
+                               var=counts.var.iloc[cols])
+                self.save_norm_counts(norm)
+                replicate_params, run_params = self.get_nmf_iter_params(
+                    ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
+                    alpha_usage=alpha_usage, alpha_spectra=alpha_spectra, init=init,
+                    total_workers=total_workers, use_gpu=use_gpu, batch_size=batch_size,
+                    max_iter=max_NMF_iter, algo=algo, mode=mode)
+                self.save_nmf_iter_params(replicate_params, run_params)
+            comm.barrier()
 
     def get_norm_counts(self, counts, tpm, high_variance_genes_filter=None,
                         num_highvar_genes=None):

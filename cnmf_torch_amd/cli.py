@@ -87,18 +87,27 @@ def build_parser() -> argparse.ArgumentParser:
     return p
 
 
+def _prepare_kwargs(args) -> dict:
+    return dict(counts_fn=args.counts, components=args.components, n_iter=args.n_iter,
+                densify=args.densify, tpm_fn=args.tpm, seed=args.seed,
+                beta_loss=args.beta_loss, max_NMF_iter=args.max_nmf_iter,
+                num_highvar_genes=args.numgenes, genes_file=args.genes_file, init=args.init,
+                total_workers=args.total_workers, use_gpu=args.use_gpu,
+                batch_size=args.batch_size, algo=args.algo, mode=args.mode)
+
+
 def main(argv=None) -> int:
     args = build_parser().parse_args(argv)
     from .api import cNMF
 
     obj = cNMF(output_dir=args.output_dir, name=args.name)
     if args.command == "prepare":
-        obj.prepare(args.counts, components=args.components, n_iter=args.n_iter,
-                    densify=args.densify, tpm_fn=args.tpm, seed=args.seed,
-                    beta_loss=args.beta_loss, max_NMF_iter=args.max_nmf_iter,
-                    num_highvar_genes=args.numgenes, genes_file=args.genes_file, init=args.init,
-                    total_workers=args.total_workers, use_gpu=args.use_gpu,
-                    batch_size=args.batch_size, algo=args.algo, mode=args.mode)
+        comm = None
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:     # under torchrun: cell-sharded
+            from .parallel.runner import init_distributed
+
+            comm, _ = init_distributed()
+        obj.prepare(comm=comm, **_prepare_kwargs(args))
     elif args.command == "factorize":
         world = int(os.environ.get("WORLD_SIZE", "1"))
         if args.dp:

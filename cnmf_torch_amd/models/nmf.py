@@ -614,53 +614,50 @@ def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch
         iters[:R] += 1 if live is None else live.to(iters.dtype)
 
 
-def _count_units(X: torch.Tensor, rows: int = 1 << 16):
+def _count_units(X: torch.Tensor, stats=None):
     """Per-gene unit u (G,) with X == C * u for a non-negative INTEGER matrix C, or None.
 
     cNMF's normalised counts are raw counts over a per-gene std (cnmf.py:670-681), so the
     unit of column g is (count 1) / std_g: the smallest positive entry m of the column
-    over its smallest count d.  d is tried as 1..8, then (highly expressed genes whose
-    every count exceeds 8) as round(m / gap) with gap the smallest difference between
-    distinct entries; a column of zeros gets u = 1.  Accepted only if every entry of every
-    column is an integer multiple of its unit to fp32 rounding (|X/u - round(X/u)| <=
-    4e-7 * X/u + 1e-4) and C < 65536."""
+    over its smallest count d.  d is tried as 1..8 (one fused pass, ops.count_unit_check),
+    then -- highly expressed genes whose every count exceeds 8 -- as round(m / gap) with
+    gap the smallest difference between distinct entries; a column of zeros gets u = 1.
+    Accepted only if every entry of every column is an integer multiple of its unit to
+    fp32 rounding (|X/u - round(X/u)| <= 4e-7 * X/u + 1e-4) and C < 65536.  ``stats``:
+    the (min_pos, sumsq, neg) of ops.colstats when already computed."""
     N, G = X.shape
-    if N == 0 or bool((X < 0).any()):
+    if N == 0:
         return None
-    inf = torch.tensor(float("inf"), device=X.device, dtype=X.dtype)
-    mn = torch.full((G,), float("inf"), device=X.device, dtype=X.dtype)
-    for a in range(0, N, rows):
-        xb = X[a:a + rows]
-        mn = torch.minimum(mn, torch.where(xb > 0, xb, inf).amin(0))
-    mn = torch.where(torch.isfinite(mn), mn, torch.ones_like(mn))
-    unit = torch.full_like(mn, float("nan"))
-
-    def accept(cand):
-        todo = torch.isnan(unit)
-        bad = torch.zeros(G, dtype=torch.bool, device=X.device)
-        for a in range(0, N, rows):
-            c = X[a:a + rows] / cand
-            bad |= ((c - torch.round(c)).abs() > 4e-7 * c + 1e-4).any(0)
-            bad |= (c >= 65535.5).any(0)
-        return torch.where(todo & ~bad & torch.isfinite(cand) & (cand > 0), cand, unit)
-
-    for d in range(1, 9):
-        unit = accept(mn / d)
-        if not bool(torch.isnan(unit).any()):
-            return unit.contiguous()
+    mn, _, neg = stats if stats is not None else ops.colstats(X)
+    if bool(neg.any()):
+        return None
+    empty = ~torch.isfinite(mn)
+    mn = torch.where(empty, torch.ones_like(mn), mn)
+    bad = ops.count_unit_check(X, mn)
+    ok = (bad & 0xFF) != 0xFF
+    # smallest d whose bit is clear: lowest zero bit of bad
+    inv = (~bad) & 0xFF
+    d = torch.zeros_like(bad)
+    for k in range(8, 0, -1):
+        d = torch.where((inv >> (k - 1)) & 1 != 0, torch.full_like(d, k), d)
+    unit = torch.where(ok, mn / d.clamp(min=1).to(mn.dtype), torch.full_like(mn, float("nan")))
+    unit = torch.where(empty, torch.ones_like(mn), unit)
     todo = torch.isnan(unit).nonzero().flatten()
+    if todo.numel() == 0:
+        return unit.contiguous()
     if todo.numel() > 64:
         return None
-    gaps = torch.full_like(mn, float("nan"))
     for g in todo.tolist():
         v = torch.unique(X[:, g])
         v = v[v > 0]
         dv = torch.diff(v)
-        if dv.numel():
-            gaps[g] = mn[g] / torch.round(mn[g] / dv.min()).clamp(min=1)
-    unit = accept(gaps)
-    if bool(torch.isnan(unit).any()):
-        return None
+        if dv.numel() == 0:
+            return None
+        u = mn[g] / torch.round(mn[g] / dv.min()).clamp(min=1)
+        c = X[:, g] / u
+        if bool((((c - torch.round(c)).abs() > 4e-7 * c + 1e-4) | (c >= 65535.5)).any()):
+            return None
+        unit[g] = u
     return unit.contiguous()
 
 
@@ -672,10 +669,10 @@ class _XPlanes:
     bf16 plane (C <= 256) or two (C < 65536) with the per-gene ``unit`` folded into the
     other operand / the output columns; other data as three planes of X itself."""
 
-    def __init__(self, X: torch.Tensor):
+    def __init__(self, X: torch.Tensor, stats=None):
         N, G = X.shape
         self.N, self.G = N, G
-        unit = _count_units(X)
+        unit = _count_units(X, stats)
         if unit is not None:
             C = torch.empty_like(X)
             for a in range(0, N, 1 << 16):
@@ -702,7 +699,7 @@ class _XPlanes:
         del C
 
     @staticmethod
-    def build(X: torch.Tensor):
+    def build(X: torch.Tensor, stats=None):
         """Planes for X when the split GEMM path applies (GPU, fp32, memory), else None."""
         if X.device.type != "cuda" or X.dtype != torch.float32 or \
                 os.environ.get("CNMF_GEMM", "planes") != "planes":
@@ -712,7 +709,7 @@ class _XPlanes:
         free, _ = torch.cuda.mem_get_info(X.device)
         if need > 0.5 * free:
             return None
-        return _XPlanes(X)
+        return _XPlanes(X, stats)
 
 
 def _graphs_enabled(X: torch.Tensor) -> bool:
@@ -751,8 +748,15 @@ class NMFBatchSolver:
         self.beta = beta_value(opts.beta_loss)
         self.profile = profile
         self.timings: dict[str, float] = {}
-        # ||X||_F^2 (global) for the trace-trick loss
-        self.x_sq = self.comm.allreduce_scalar(_sq_norm(self.X))
+        # ||X||_F^2 (global) for the trace-trick loss; on the GPU from the fused column
+        # statistics pass that also feeds the split-GEMM count detection
+        self._colstats = None
+        if self.X.device.type == "cuda" and self.X.dtype == torch.float32 and self.X.numel():
+            self._colstats = ops.colstats(self.X)
+            local_sq = float(self._colstats[1].sum())
+        else:
+            local_sq = _sq_norm(self.X)
+        self.x_sq = self.comm.allreduce_scalar(local_sq)
         self._mean_x = None
         self._xp = False            # split-GEMM planes of X: False = not built yet
         self._ws: dict = {}
@@ -846,7 +850,7 @@ class NMFBatchSolver:
     def _planes(self):
         """X planes for the split-precision MFMA GEMMs, or None (CPU, fp64, memory)."""
         if self._xp is False:
-            self._xp = _XPlanes.build(self.X)
+            self._xp = _XPlanes.build(self.X, self._colstats)
         return self._xp
 
     def _plane_buf(self, key: str, rows: int, cols: int) -> torch.Tensor:

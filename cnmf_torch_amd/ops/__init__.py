@@ -841,3 +841,38 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
                      col_scale.data_ptr() if col_scale is not None else 0, int(M), int(N),
                      int(Kd), pa, pb, int(bool(accumulate)), int(variant), int(ksplit), slab,
                      _stream_ptr(C))
+
+
+# ----------------------------------------------------------------------------- column stats
+def colstats(X: torch.Tensor):
+    """Per column of the fp32 matrix X (unit column stride): smallest positive entry
+    (inf if none), float64 sum of squares, any-negative flag -- one pass, deterministic
+    (colstats.hip)."""
+    N, G = X.shape
+    if X.dtype != torch.float32 or (G > 1 and X.stride(1) != 1):
+        raise ValueError("colstats: float32 with unit column stride required")
+    if not use_native(X):
+        return reference.colstats(X)
+    dev = X.device
+    nb = int(_hip.colstats_blocks(N))
+    pmin = torch.empty((nb, G), dtype=torch.float32, device=dev)
+    psq = torch.empty((nb, G), dtype=torch.float64, device=dev)
+    pneg = torch.empty((nb, G), dtype=torch.int32, device=dev)
+    mn = torch.empty(G, dtype=torch.float32, device=dev)
+    sq = torch.empty(G, dtype=torch.float64, device=dev)
+    neg = torch.empty(G, dtype=torch.int32, device=dev)
+    _hip.colstats(X.data_ptr(), X.stride(0), N, G, pmin.data_ptr(), psq.data_ptr(),
+                  pneg.data_ptr(), mn.data_ptr(), sq.data_ptr(), neg.data_ptr(), _stream_ptr(X))
+    return mn, sq, neg
+
+
+def count_unit_check(X: torch.Tensor, mn: torch.Tensor) -> torch.Tensor:
+    """int32 (G,) bit masks: bit d-1 set when some entry of the column is not an integer
+    multiple of mn/d (d = 1..8) to fp32 rounding (or the multiple exceeds 65535)."""
+    N, G = X.shape
+    if not use_native(X):
+        return reference.count_unit_check(X, mn)
+    bad = torch.zeros(G, dtype=torch.int32, device=X.device)
+    _hip.count_unit_check(X.data_ptr(), X.stride(0), N, G, mn.contiguous().data_ptr(),
+                          bad.data_ptr(), _stream_ptr(X))
+    return bad

@@ -293,3 +293,23 @@ def gemm_planes(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
             if i + j <= 2:
                 out += Af[i] @ Bf[j].t()
     return out
+
+
+def colstats(X: torch.Tensor):
+    inf = torch.tensor(float("inf"), dtype=X.dtype, device=X.device)
+    mn = torch.where(X > 0, X, inf).amin(0) if X.shape[0] else \
+        torch.full((X.shape[1],), float("inf"), dtype=X.dtype, device=X.device)
+    sq = (X.to(torch.float64) ** 2).sum(0)
+    neg = (X < 0).any(0).to(torch.int32)
+    return mn, sq, neg
+
+
+def count_unit_check(X: torch.Tensor, mn: torch.Tensor) -> torch.Tensor:
+    bad = torch.zeros(X.shape[1], dtype=torch.int32, device=X.device)
+    ok_col = (mn > 0) & torch.isfinite(mn)
+    for d in range(1, 9):
+        c = X / (mn / d)
+        off = ((c - torch.round(c)).abs() > 4e-7 * c + 1e-4) | (c >= 65535.5)
+        off &= X != 0
+        bad |= (off.any(0) & ok_col).to(torch.int32) << (d - 1)
+    return bad

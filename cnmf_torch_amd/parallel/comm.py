@@ -33,6 +33,9 @@ class LocalComm:
     def all_gather_object(self, obj):
         return [obj]
 
+    def gather_object(self, obj, dst: int = 0):
+        return [obj]
+
     @property
     def is_distributed(self) -> bool:
         return False
@@ -103,4 +106,12 @@ class DistComm(LocalComm):
             return [obj]
         out = [None] * self.world_size
         self._dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def gather_object(self, obj, dst: int = 0):
+        """Python objects of every rank on ``dst`` (list in rank order), None elsewhere."""
+        if self.world_size == 1:
+            return [obj]
+        out = [None] * self.world_size if self.rank == dst else None
+        self._dist.gather_object(obj, out, dst=dst, group=self.group)
         return out

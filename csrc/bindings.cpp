@@ -254,4 +254,21 @@ PYBIND11_MODULE(_hip, m) {
                                   nplanes, reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_split_planes");
         });
+
+  m.def("colstats_blocks", [](int N) { return cnmf_colstats_blocks(N); });
+  m.def("colstats",
+        [](uintptr_t X, long long ldx, int N, int G, uintptr_t pmin, uintptr_t psq,
+           uintptr_t pneg, uintptr_t mn, uintptr_t sq, uintptr_t neg, uintptr_t stream) {
+          check(cnmf_colstats(P<const float>(X), ldx, N, G, P<float>(pmin), P<double>(psq),
+                              P<int>(pneg), P<float>(mn), P<double>(sq), P<int>(neg),
+                              reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_colstats");
+        });
+  m.def("count_unit_check",
+        [](uintptr_t X, long long ldx, int N, int G, uintptr_t mn, uintptr_t bad,
+           uintptr_t stream) {
+          check(cnmf_count_unit_check(P<const float>(X), ldx, N, G, P<const float>(mn),
+                                      P<unsigned>(bad), reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_count_unit_check");
+        });
 }

@@ -110,4 +110,10 @@ hipError_t cnmf_split_planes(const float* S, long long lds, int rows, int cols, 
                              const float* col_mul, unsigned short* P, long long ldp,
                              long long plane, int nplanes, hipStream_t stream);
 
+int cnmf_colstats_blocks(int N);
+hipError_t cnmf_colstats(const float* X, long long ldx, int N, int G, float* pmin, double* psq,
+                         int* pneg, float* mn, double* sq, int* neg, hipStream_t stream);
+hipError_t cnmf_count_unit_check(const float* X, long long ldx, int N, int G, const float* mn,
+                                 unsigned* bad, hipStream_t stream);
+
 }

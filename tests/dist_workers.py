@@ -111,3 +111,12 @@ def consensus_worker(rank, world, port, output_dir, name, ks):
     distributed_consensus(obj, ks, density_threshold=0.5, show_clustering=False,
                           backend="gloo")
     dist.destroy_process_group()
+
+
+def prepare_worker(rank, world, port, output_dir, name, counts_fn, kw):
+    _init(rank, world, port)
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.parallel.comm import DistComm
+
+    cNMF(output_dir=output_dir, name=name).prepare(counts_fn, comm=DistComm(), **kw)
+    dist.destroy_process_group()

@@ -184,3 +184,40 @@ def test_rank_failure_then_resume_on_a_different_world_size(prepared):
             a = load_df_from_npz(obj.paths["iter_spectra"] % (k, i)).values
             b = load_df_from_npz(serial.paths["iter_spectra"] % (k, i)).values
             np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("fmt", ["h5ad_sparse", "npz_dense"])
+def test_sharded_prepare_matches_single_process(tmp_path, fmt):
+    """Cell-sharded prepare over 3 gloo ranks (all-reduced two-pass gene statistics) writes
+    the same artifacts as the single-process prepare."""
+    from cnmf_torch_amd.utils.anndata_lite import AnnData
+    from cnmf_torch_amd.utils.h5ad import read_h5ad, write_h5ad
+
+    Xc, cells, genes = simulate_counts(500, 300, 4, seed=21, sparse=(fmt == "h5ad_sparse"))
+    if fmt == "h5ad_sparse":
+        fn = str(tmp_path / "counts.h5ad")
+        write_h5ad(fn, AnnData(X=Xc, obs=pd.DataFrame(index=cells), var=pd.DataFrame(index=genes)))
+    else:
+        fn = str(tmp_path / "counts.df.npz")
+        save_df_to_npz(pd.DataFrame(Xc, index=cells, columns=genes), fn)
+    kw = dict(components=[3, 4], n_iter=3, seed=7, num_highvar_genes=120)
+    _spawn(W.prepare_worker, 3, str(tmp_path), "sh", fn, kw)
+    ser = cNMF(output_dir=str(tmp_path), name="se")
+    ser.prepare(fn, **kw)
+    sh = cNMF(output_dir=str(tmp_path), name="sh")
+    assert open(sh.paths["nmf_genes_list"]).read() == open(ser.paths["nmf_genes_list"]).read()
+    # float32 TPM: sklearn accumulates the single-process statistics in float32
+    np.testing.assert_allclose(load_df_from_npz(sh.paths["tpm_stats"]).values,
+                               load_df_from_npz(ser.paths["tpm_stats"]).values, rtol=2e-6)
+    a, b = read_h5ad(sh.paths["normalized_counts"]), read_h5ad(ser.paths["normalized_counts"])
+    xa = a.X.toarray() if hasattr(a.X, "toarray") else a.X
+    xb = b.X.toarray() if hasattr(b.X, "toarray") else b.X
+    np.testing.assert_allclose(xa, xb, rtol=1e-10, atol=1e-12)
+    assert list(a.obs.index) == list(b.obs.index) and list(a.var.index) == list(b.var.index)
+    ta, tb = read_h5ad(sh.paths["tpm"]), read_h5ad(ser.paths["tpm"])
+    xa = ta.X.toarray() if hasattr(ta.X, "toarray") else ta.X
+    xb = tb.X.toarray() if hasattr(tb.X, "toarray") else tb.X
+    np.testing.assert_allclose(xa, xb, rtol=1e-6)
+    pa = load_df_from_npz(sh.paths["nmf_replicate_parameters"])
+    pb = load_df_from_npz(ser.paths["nmf_replicate_parameters"])
+    assert pa.equals(pb)

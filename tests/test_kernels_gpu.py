@@ -797,3 +797,19 @@ def test_coop_solve_with_a_concurrent_kernel_stream():
     torch.cuda.synchronize()
     ops.coop_check(torch.device("cuda"))
     np.testing.assert_allclose(x.cpu().numpy(), ref_x.cpu().numpy(), rtol=1e-5, atol=1e-7)
+
+
+def test_colstats_and_count_unit_check_match_reference():
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(3001, 517, n_programs=6, seed=3))
+    X[:, 7] = 0
+    X[5, 9] = -1.0
+    for M in (X, X + 0.001 * torch.rand_like(X)):
+        mn, sq, neg = ops.colstats(M.cuda())
+        rmn, rsq, rneg = reference.colstats(M)
+        assert torch.equal(mn.cpu(), rmn) and torch.equal(neg.cpu(), rneg)
+        np.testing.assert_allclose(sq.cpu().numpy(), rsq.numpy(), rtol=1e-12)
+        fmn = torch.where(torch.isfinite(rmn), rmn, torch.ones_like(rmn))
+        assert torch.equal(ops.count_unit_check(M.cuda(), fmn.cuda()).cpu(),
+                           reference.count_unit_check(M, fmn))
