@@ -31,6 +31,7 @@ ARCH = os.environ.get("CNMF_OFFLOAD_ARCH", "gfx950")
 
 HIP_OUT = os.path.join(PKG, "ops", "_hip" + EXT)
 H5_OUT = os.path.join(PKG, "utils", "_h5io" + EXT)
+NPZ_OUT = os.path.join(PKG, "utils", "_npzio" + EXT)
 
 HDF5_PREFIXES = [os.environ.get("CNMF_HDF5_PREFIX", ""), "/opt/conda", "/usr", "/usr/local"]
 
@@ -121,23 +122,41 @@ def build_h5(force: bool = False, verbose: bool = True) -> str:
     return H5_OUT
 
 
+def build_npz(force: bool = False, verbose: bool = True) -> str:
+    """Native replicate-file writer (csrc/io/npzio.cpp): host C++, std::thread, no deps."""
+    src = os.path.join(CSRC, "io", "npzio.cpp")
+    if not (force or _stale(NPZ_OUT, [src])):
+        return NPZ_OUT
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    tmp = NPZ_OUT + ".tmp"
+    if verbose:
+        print("[cnmf build] compiling native npz writer", flush=True)
+    _run([cxx, "-O3", "-shared", "-fPIC", "-std=c++17", "-pthread", src, "-o", tmp]
+         + _py_includes())
+    os.replace(tmp, NPZ_OUT)
+    return NPZ_OUT
+
+
 def build_all(force: bool = False, jobs: int = 8, verbose: bool = True) -> list[str]:
-    with cf.ThreadPoolExecutor(max_workers=2) as ex:
+    with cf.ThreadPoolExecutor(max_workers=3) as ex:
         fh = ex.submit(build_hip, force, jobs, verbose)
         f5 = ex.submit(build_h5, force, verbose)
-        return [fh.result(), f5.result()]
+        fn = ex.submit(build_npz, force, verbose)
+        return [fh.result(), f5.result(), fn.result()]
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 1))
-    ap.add_argument("--only", choices=["hip", "h5"], default=None)
+    ap.add_argument("--only", choices=["hip", "h5", "npz"], default=None)
     a = ap.parse_args(argv)
     if a.only == "hip":
         print(build_hip(a.force, a.jobs))
     elif a.only == "h5":
         print(build_h5(a.force))
+    elif a.only == "npz":
+        print(build_npz(a.force))
     else:
         for p in build_all(a.force, a.jobs):
             print(p)

@@ -44,8 +44,8 @@ from .parallel.ledger import worker_filter
 from .utils.anndata_lite import AnnData
 from .utils.h5ad import read_h5ad, write_h5ad
 from .utils.io import (check_dir_exists, dump_yaml, load_df_from_npz, load_yaml, read_10x_mtx,
-                       NpzTemplate, npy_bytes, read_any, read_counts_table, save_arrays_npz_digest, save_df_to_npz,
-                       save_df_to_text, NPZ_TMP_LEVEL, write_text_atomic)
+                       read_any, read_counts_table, save_arrays_npz_digest, save_df_to_npz,
+                       save_df_to_text, NPZ_TMP_LEVEL, write_spectra_batch, write_text_atomic)
 from .utils.log import get_logger
 from .utils.timing import StageTimer, append_jsonl_many, read_jsonl
 
@@ -548,27 +548,31 @@ class cNMF:
             # replicate files are encoded + hashed + written by a small thread pool (numpy
             # and zlib drop the GIL) while the next batch runs on the GPU; every file is
             # still atomic, and its sha256 is taken from the bytes in memory
-            pool = cf.ThreadPoolExecutor(max_workers=8)
+            pool = cf.ThreadPoolExecutor(max_workers=4)
             pending: list = []
             manifest = self.paths["replicate_manifest"]
             gene_arr = np.asarray(genes.values).astype(str)
-            index_npy = {}
-            tmpl = NpzTemplate({"columns": gene_arr}) if NPZ_TMP_LEVEL <= 0 else None
 
-            def _write_spectra(data, path, k_, it_):
-                if tmpl is not None:
-                    digest, size = tmpl.write(path, {"index": index_npy[k_], "data": data})
+            def _write_batch(paths_b, W_, offs_, ks_, its_):
+                if NPZ_TMP_LEVEL <= 0:
+                    done = write_spectra_batch(paths_b, W_, offs_, ks_, gene_arr)
                 else:
-                    digest, size = save_arrays_npz_digest(
-                        path, {"data": data, "index": index_npy[k_], "columns": gene_arr},
-                        level=NPZ_TMP_LEVEL)
-                return {"k": k_, "iter": it_, "file": os.path.basename(path), "sha256": digest,
-                        "bytes": size}
+                    done = [save_arrays_npz_digest(
+                        p_, {"data": W_[o_:o_ + k_], "index": np.arange(1, k_ + 1),
+                             "columns": gene_arr}, level=NPZ_TMP_LEVEL)
+                        for p_, o_, k_ in zip(paths_b, offs_, ks_)]
+                return [{"k": int(k_), "iter": int(i_), "file": os.path.basename(p_),
+                         "sha256": d_, "bytes": int(n_)}
+                        for p_, k_, i_, (d_, n_) in zip(paths_b, ks_, its_, done)]
 
             def _flush():
-                recs = [f.result() for f in pending]
+                recs = []
+                for f in pending:
+                    r_ = f.result()
+                    if isinstance(r_, list):
+                        recs.extend(r_)
                 pending.clear()
-                append_jsonl_many(manifest, [r for r in recs if r is not None])
+                append_jsonl_many(manifest, recs)
 
             nc = run_params["n_components"].to_numpy().astype(np.int64)
             itv = run_params["iter"].to_numpy().astype(np.int64)
@@ -597,13 +601,18 @@ class cNMF:
                 log.info("K=%s: %d replicates in %.3f s (%.1f replicates/s) on %s",
                          sorted(set(ks)), len(grp), wall, len(grp) / max(wall, 1e-9), dev)
                 recs = []
-                for k in set(ks):
-                    index_npy.setdefault(k, npy_bytes(np.arange(1, k + 1)))
+                # fault injection (tests): only the replicates before the fault are written
+                n_ok = len(grp) if not fault_after else max(0, min(len(grp), fault_after - written))
+                if writer and n_ok:
+                    # every replicate file of the batch in one native multi-threaded call
+                    # (utils.io.write_spectra_batch), overlapped with the next batch's solve
+                    paths_b = [self.paths["iter_spectra"] % (ks[r], int(itv[i]))
+                               for r, i in enumerate(grp[:n_ok])]
+                    pending.append(pool.submit(_write_batch, paths_b, W, res.offs[:n_ok],
+                                               ks[:n_ok], [int(itv[i]) for i in grp[:n_ok]]))
                 for r, idx in enumerate(grp):
                     k, it = ks[r], int(itv[idx])
                     if writer:
-                        pending.append(pool.submit(_write_spectra, W[res.rows(r)],
-                                                   self.paths["iter_spectra"] % (k, it), k, it))
                         recs.append({
                             "k": k, "iter": it, "seed": seeds[r], "worker": worker_label,
                             "err": float(res.err[r]), "n_pass": int(res.n_iter[r]),

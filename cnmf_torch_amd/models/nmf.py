@@ -628,24 +628,23 @@ def _count_units(X: torch.Tensor, stats=None):
     N, G = X.shape
     if N == 0:
         return None
-    mn, _, neg = stats if stats is not None else ops.colstats(X)
-    if bool(neg.any()):
+    mn_t, _, neg = stats if stats is not None else ops.colstats(X)
+    empty_t = ~torch.isfinite(mn_t)
+    mn_t = torch.where(empty_t, torch.ones_like(mn_t), mn_t)
+    bad_t = ops.count_unit_check(X, mn_t)
+    # one host round trip for the per-gene decisions
+    host = torch.stack([mn_t.double(), bad_t.double(), neg.double(), empty_t.double()]).cpu().numpy()
+    mn, bad, neg_h, empty = host[0], host[1].astype(np.int64), host[2] != 0, host[3] != 0
+    if neg_h.any():
         return None
-    empty = ~torch.isfinite(mn)
-    mn = torch.where(empty, torch.ones_like(mn), mn)
-    bad = ops.count_unit_check(X, mn)
-    ok = (bad & 0xFF) != 0xFF
-    # smallest d whose bit is clear: lowest zero bit of bad
-    inv = (~bad) & 0xFF
-    d = torch.zeros_like(bad)
+    inv = (~bad) & 0xFF                         # bit d-1 set: d works
+    d = np.zeros(G, dtype=np.int64)
     for k in range(8, 0, -1):
-        d = torch.where((inv >> (k - 1)) & 1 != 0, torch.full_like(d, k), d)
-    unit = torch.where(ok, mn / d.clamp(min=1).to(mn.dtype), torch.full_like(mn, float("nan")))
-    unit = torch.where(empty, torch.ones_like(mn), unit)
-    todo = torch.isnan(unit).nonzero().flatten()
-    if todo.numel() == 0:
-        return unit.contiguous()
-    if todo.numel() > 64:
+        d = np.where((inv >> (k - 1)) & 1, k, d)
+    unit = np.where(d > 0, mn / np.maximum(d, 1), np.nan)
+    unit[empty] = 1.0
+    todo = np.flatnonzero(np.isnan(unit))
+    if todo.size > 64:
         return None
     for g in todo.tolist():
         v = torch.unique(X[:, g])
@@ -653,12 +652,15 @@ def _count_units(X: torch.Tensor, stats=None):
         dv = torch.diff(v)
         if dv.numel() == 0:
             return None
-        u = mn[g] / torch.round(mn[g] / dv.min()).clamp(min=1)
+        u = float(mn[g]) / max(1.0, round(float(mn[g]) / float(dv.min())))
         c = X[:, g] / u
         if bool((((c - torch.round(c)).abs() > 4e-7 * c + 1e-4) | (c >= 65535.5)).any()):
             return None
         unit[g] = u
-    return unit.contiguous()
+    # mn / d in float32 arithmetic, as the device check evaluated it
+    return torch.from_numpy((mn.astype(np.float32) / np.maximum(d, 1).astype(np.float32))
+                            .astype(np.float32) if todo.size == 0 else unit.astype(np.float32)
+                            ).to(X.device).contiguous()
 
 
 class _XPlanes:
@@ -710,6 +712,20 @@ class _XPlanes:
         if need > 0.5 * free:
             return None
         return _XPlanes(X, stats)
+
+
+def native_rank(K: int) -> int:
+    """The rank the GPU kernels run a rank-K replicate at: K itself for K <= 32, else K
+    padded to a multiple of 8 (<= 64) with zero components -- a zero row of W / H stays
+    zero under MU (rate 0 where the denominator vanishes) and HALS (zero diagonal), and
+    contributes nothing to the Gram matrices or the loss, so the padded solve IS the
+    rank-K solve (cnmf.py:1416 takes any -k)."""
+    K = int(K)
+    if K <= 32:
+        return K
+    if K > 64:
+        raise ValueError(f"K={K}: the native kernels cover K <= 64")
+    return -(-K // 8) * 8
 
 
 def _graphs_enabled(X: torch.Tensor) -> bool:
@@ -780,23 +796,40 @@ class NMFBatchSolver:
         if self.beta != 2.0 and np.unique(ks).size > 1:
             return self._run_split_by_k(seeds, ks)
         t0 = time.perf_counter()
-        pos = np.argsort(ks, kind="stable")            # positions grouped by K
-        kpos = ks[pos]
+        # wide ranks run padded on the GPU kernels (native_rank); bpp solves on torch linalg
+        pad = self.X.device.type == "cuda" and o.algo != "bpp" and self.beta == 2.0 \
+            and bool((ks > 32).any())
+        kp = np.array([native_rank(k) for k in ks], dtype=np.int64) if pad else ks
+        pos = np.lexsort((np.arange(R), kp, ks))     # positions grouped by K
+        kpos = kp[pos]
         if HT0 is None or W0 is None:
             N, G = self.X.shape
             tot = int(kpos.sum())
-            HT = torch.empty((tot, N), device=self.X.device, dtype=self.X.dtype)
-            W = torch.empty((tot, G), device=self.X.device, dtype=self.X.dtype)
+            HT = torch.zeros((tot, N), device=self.X.device, dtype=self.X.dtype)
+            W = torch.zeros((tot, G), device=self.X.device, dtype=self.X.dtype)
             r0 = 0
-            for K in np.unique(kpos):
-                sel = pos[kpos == K]
-                rows = slice(r0, r0 + sel.size * int(K))
-                init_into(HT[rows], W[rows], self.X, int(K), [seeds[i] for i in sel], o.init,
-                          self.comm, self.row_offset, mean=self._mean(), row_map=self.row_map)
+            for K in np.unique(ks[pos]):
+                sel = pos[ks[pos] == K]
+                Kp = int(kp[sel[0]])
+                rows = slice(r0, r0 + sel.size * Kp)
+                if Kp == K:
+                    init_into(HT[rows], W[rows], self.X, int(K), [seeds[i] for i in sel],
+                              o.init, self.comm, self.row_offset, mean=self._mean(),
+                              row_map=self.row_map)
+                else:   # rank-K init in the first K rows of each padded block
+                    h_ = torch.empty((sel.size * int(K), N), device=HT.device, dtype=HT.dtype)
+                    w_ = torch.empty((sel.size * int(K), G), device=W.device, dtype=W.dtype)
+                    init_into(h_, w_, self.X, int(K), [seeds[i] for i in sel], o.init,
+                              self.comm, self.row_offset, mean=self._mean(),
+                              row_map=self.row_map)
+                    HT[rows].view(sel.size, Kp, N)[:, :K] = h_.view(sel.size, K, N)
+                    W[rows].view(sel.size, Kp, G)[:, :K] = w_.view(sel.size, K, G)
                 r0 = rows.stop
         else:
             if np.unique(ks).size > 1:
                 raise ValueError("explicit initial factors need a single K")
+            if pad:
+                raise ValueError("explicit initial factors need K <= 32 on the GPU")
             HT, W = HT0.to(self.X.dtype).clone(), W0.to(self.X.dtype).clone()
         st = _Batch(HT, W, kpos)
         st.order = pos.astype(np.int64).copy()
@@ -811,6 +844,11 @@ class NMFBatchSolver:
             else:
                 self._batch_beta(st)
         HT, W, ks_out, err, n_iter, conv, hi, wi = st.finalize()
+        if pad:     # drop the zero padding components: rows [0, K) of each block
+            offp = np.concatenate([[0], np.cumsum(ks_out)[:-1]])
+            keep = _to_device(_ranges(offp, ks), HT.device)
+            HT, W = HT.index_select(0, keep), W.index_select(0, keep)
+            ks_out = ks
         if self.X.device.type == "cuda":
             ops.coop_check(self.X.device)
         stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": hi.tolist(),

@@ -106,15 +106,18 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     """
     a = ALGOS[algo]
     R, K, n = x.shape
-    if not use_native(x) or x.dtype != torch.float32:  # fp64 (fp_precision='double') -> torch
+    if not use_native(x):
         return reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
                                eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every,
                                active)
     h = _hip
-    if K > h.solve_max_k():
-        return reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
-                               eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every,
-                               active)
+    # a GPU operand the kernels do not cover is an error, never a silent eager fallback:
+    # fp32 only; K in 1..32 or a padded wide rank (the engine pads K <= 64 to a multiple
+    # of 8, models/nmf.py native_rank)
+    _native_dtype_k("solve", x.dtype, K, h.solve_max_k())
+    if not h.solve_native_k(K):
+        raise ValueError(f"solve: K={K} has no kernel instantiation (pad it to a multiple "
+                         "of 8, see models.nmf.native_rank)")
     _check_block_view("x", x, R, K, n)
     _check_block_view("numer", numer, R, K, n)
     if gram.shape != (R, K, K) or gram.dtype != torch.float32:
@@ -503,7 +506,10 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
         if accumulate:
             raise ValueError("accumulate needs an out tensor")
         out = torch.empty((R, K, K), device=X3.device, dtype=X3.dtype)
-    if not use_native(X3) or X3.dtype != torch.float32 or K > 32:
+    native = use_native(X3)
+    if native:
+        _native_dtype_k("gram", X3.dtype, K, 64)
+    else:
         g = torch.bmm(X3, X3.transpose(1, 2))
         if active is not None:
             keep = (active[:R] != 0).view(R, 1, 1)

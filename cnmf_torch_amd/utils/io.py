@@ -186,6 +186,43 @@ class NpzTemplate:
         return h.hexdigest(), off + len(cd) + 22
 
 
+try:  # native batch writer (csrc/io/npzio.cpp); the Python NpzTemplate is the fallback
+    from . import _npzio  # type: ignore
+except Exception:  # pragma: no cover - depends on the build
+    _npzio = None
+
+
+def npy_header(shape, dtype) -> bytes:
+    """The .npy header bytes of a C-ordered array of ``shape`` / ``dtype``."""
+    import numpy.lib.format as fmt
+
+    buf = io.BytesIO()
+    fmt.write_array_header_1_0(buf, {"descr": fmt.dtype_to_descr(np.dtype(dtype)),
+                                     "fortran_order": False, "shape": tuple(shape)})
+    return buf.getvalue()
+
+
+def write_spectra_batch(paths, data: np.ndarray, offs, ks, columns) -> list[tuple[str, int]]:
+    """Write one ``.df.npz`` per replicate -- data rows ``offs[i] : offs[i] + ks[i]`` of the
+    float32 matrix ``data``, index 1..K, the shared gene ``columns`` -- atomically, and
+    return their (sha256, size).  Native threads when the extension is built (no GIL),
+    else the Python :class:`NpzTemplate`."""
+    data = np.ascontiguousarray(data, dtype=np.float32)
+    G = data.shape[1]
+    kset = sorted(set(int(k) for k in ks))
+    if _npzio is not None:
+        cols = npy_bytes(np.asarray(columns))
+        return [tuple(r) for r in _npzio.write_spectra_batch(
+            [str(p) for p in paths], data, [int(o) for o in offs], [int(k) for k in ks], cols,
+            {k: npy_bytes(np.arange(1, k + 1)) for k in kset},
+            {k: npy_header((k, G), np.float32) for k in kset},
+            max(1, min(32, (os.cpu_count() or 1))))]
+    tmpl = NpzTemplate({"columns": np.asarray(columns)})
+    idx = {k: npy_bytes(np.arange(1, k + 1)) for k in kset}
+    return [tmpl.write(str(p), {"index": idx[int(k)], "data": data[o:o + int(k)]})
+            for p, o, k in zip(paths, offs, ks)]
+
+
 def npz_bytes(arrays: dict, level: int = 0) -> bytes:
     """The bytes of an .npz holding ``arrays`` (same members as :func:`_savez_deflate`).
     Values may be arrays or already-encoded .npy ``bytes`` (shared members such as the

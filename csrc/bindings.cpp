@@ -25,6 +25,7 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("solve_max_k", []() { return cnmf_solve_max_k(); });
   m.def("solve_max_threads", [](int K) { return cnmf_solve_max_threads(K); });
+  m.def("solve_native_k", [](int K) { return cnmf_solve_native_k(K); });
   m.def("solve_reg_max_cols", [](int K) { return cnmf_solve_reg_max_cols(K); });
 
   m.def("solve",

@@ -1,0 +1,296 @@
+// Native batch writer of the per-replicate spectra files (cnmf.py:889-892 writes one
+// ``spectra.k_%d.iter_%d.df.npz`` per replicate; cNMF factorize produces them by the
+// thousand).  Each file is the stored (uncompressed) PKZIP that np.savez writes, with the
+// members columns.npy (the gene names, shared by every file), index.npy (1..K) and
+// data.npy (K x G float32 spectra).  Files are written atomically (temp file + rename)
+// on a pool of native threads, and each one's SHA-256 -- recorded in the replicate
+// manifest -- is computed from the bytes in memory, continuing a
+// precomputed midstate over the shared prefix.  No Python, no GIL: the Python writer
+// spent ~0.1 ms of interpreter time per file under the GIL.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <array>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <unistd.h>
+
+namespace py = pybind11;
+
+namespace {
+
+// ------------------------------------------------------------------ CRC-32 (zlib polynomial)
+struct Crc32 {
+  uint32_t t[8][256];
+  Crc32() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+  }
+  uint32_t update(uint32_t crc, const uint8_t* p, size_t n) const {
+    crc = ~crc;
+    while (n >= 8) {  // slicing-by-8
+      uint32_t a, b;
+      std::memcpy(&a, p, 4);
+      std::memcpy(&b, p + 4, 4);
+      a ^= crc;
+      crc = t[7][a & 0xFF] ^ t[6][(a >> 8) & 0xFF] ^ t[5][(a >> 16) & 0xFF] ^ t[4][a >> 24] ^
+            t[3][b & 0xFF] ^ t[2][(b >> 8) & 0xFF] ^ t[1][(b >> 16) & 0xFF] ^ t[0][b >> 24];
+      p += 8;
+      n -= 8;
+    }
+    while (n--) crc = t[0][(crc ^ *p++) & 0xFF] ^ (crc >> 8);
+    return ~crc;
+  }
+};
+const Crc32& crc_tables() {
+  static const Crc32 c;
+  return c;
+}
+
+// ------------------------------------------------------------------ SHA-256 (FIPS 180-4)
+struct Sha256 {
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint8_t buf[64];
+  size_t blen = 0;
+  uint64_t total = 0;
+
+  static uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+  void block(const uint8_t* p) {
+    static const uint32_t K[64] = {
+        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4,
+        0xab1c5ed5, 0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe,
+        0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f,
+        0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7,
+        0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc,
+        0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b,
+        0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116,
+        0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+        0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+        0xc67178f2};
+    uint32_t w[64];
+    for (int i = 0; i < 16; ++i)
+      w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 |
+             (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+    for (int i = 16; i < 64; ++i) {
+      const uint32_t s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
+      const uint32_t s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
+      w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t t1 = hh + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) +
+                          K[i] + w[i];
+      const uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+  void update(const uint8_t* p, size_t n) {
+    total += n;
+    if (blen) {
+      const size_t take = std::min(n, 64 - blen);
+      std::memcpy(buf + blen, p, take);
+      blen += take;
+      p += take;
+      n -= take;
+      if (blen == 64) {
+        block(buf);
+        blen = 0;
+      }
+    }
+    while (n >= 64) {
+      block(p);
+      p += 64;
+      n -= 64;
+    }
+    if (n) {
+      std::memcpy(buf, p, n);
+      blen = n;
+    }
+  }
+  std::string hex() {
+    const uint64_t bits = total * 8;
+    const uint8_t one = 0x80, zero = 0;
+    update(&one, 1);
+    while (blen != 56) update(&zero, 1);
+    uint8_t len[8];
+    for (int i = 0; i < 8; ++i) len[i] = (uint8_t)(bits >> (56 - 8 * i));
+    update(len, 8);
+    static const char* d = "0123456789abcdef";
+    std::string s(64, '0');
+    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 8; ++j) s[i * 8 + j] = d[(h[i] >> (28 - 4 * j)) & 0xF];
+    return s;
+  }
+};
+
+// ------------------------------------------------------------------ stored ZIP records
+void put16(std::string& s, uint32_t v) { s.push_back((char)(v & 0xFF)); s.push_back((char)(v >> 8)); }
+void put32(std::string& s, uint32_t v) { put16(s, v & 0xFFFF); put16(s, v >> 16); }
+
+std::string local_header(const std::string& name, uint32_t crc, uint32_t size) {
+  std::string s;
+  put32(s, 0x04034B50); put16(s, 20); put16(s, 0); put16(s, 0); put16(s, 0); put16(s, 33);
+  put32(s, crc); put32(s, size); put32(s, size); put16(s, (uint32_t)name.size()); put16(s, 0);
+  return s + name;
+}
+std::string central_record(const std::string& name, uint32_t crc, uint32_t size, uint32_t off) {
+  std::string s;
+  put32(s, 0x02014B50); put16(s, 20); put16(s, 20); put16(s, 0); put16(s, 0); put16(s, 0);
+  put16(s, 33); put32(s, crc); put32(s, size); put32(s, size); put16(s, (uint32_t)name.size());
+  put16(s, 0); put16(s, 0); put16(s, 0); put16(s, 0); put32(s, 0600u << 16); put32(s, off);
+  return s + name;
+}
+
+struct Member {  // a fully encoded member: local header + payload bytes, central record
+  std::string local, payload;
+  uint32_t crc = 0;
+};
+
+}  // namespace
+
+// paths[i] gets members columns (shared) + index (per K) + data (rows offs[i]..offs[i]+ks[i]
+// of `data`, with the .npy header data_hdr[K]).  Returns [(sha256 hex, size)].
+static std::vector<std::pair<std::string, long long>> write_spectra_batch(
+    const std::vector<std::string>& paths, py::array_t<float, py::array::c_style> data,
+    const std::vector<long long>& offs, const std::vector<int>& ks, py::bytes columns_npy,
+    const std::map<int, py::bytes>& index_npy, const std::map<int, py::bytes>& data_hdr,
+    int threads) {
+  const size_t n = paths.size();
+  if (offs.size() != n || ks.size() != n) throw std::invalid_argument("paths/offs/ks lengths");
+  if (data.ndim() != 2) throw std::invalid_argument("data must be 2-D float32");
+  const long long rows = data.shape(0), G = data.shape(1);
+  for (size_t i = 0; i < n; ++i)
+    if (offs[i] < 0 || ks[i] < 1 || offs[i] + ks[i] > rows)
+      throw std::invalid_argument("replicate rows out of range");
+  const Crc32& crc = crc_tables();
+  // shared prefix: the columns member
+  Member col;
+  col.payload = std::string(columns_npy);
+  col.crc = crc.update(0, (const uint8_t*)col.payload.data(), col.payload.size());
+  col.local = local_header("columns.npy", col.crc, (uint32_t)col.payload.size());
+  Sha256 mid;
+  mid.update((const uint8_t*)col.local.data(), col.local.size());
+  mid.update((const uint8_t*)col.payload.data(), col.payload.size());
+  const uint32_t off_index = (uint32_t)(col.local.size() + col.payload.size());
+  std::map<int, Member> idx;
+  std::map<int, std::string> hdr;
+  for (int K : ks) {
+    if (idx.count(K)) continue;
+    auto it = index_npy.find(K);
+    auto ht = data_hdr.find(K);
+    if (it == index_npy.end() || ht == data_hdr.end())
+      throw std::invalid_argument("missing index/header bytes for a K");
+    Member m;
+    m.payload = std::string(it->second);
+    m.crc = crc.update(0, (const uint8_t*)m.payload.data(), m.payload.size());
+    m.local = local_header("index.npy", m.crc, (uint32_t)m.payload.size());
+    idx[K] = std::move(m);
+    hdr[K] = std::string(ht->second);
+  }
+  const float* base = data.data();
+  std::vector<std::pair<std::string, long long>> out(n);
+  std::vector<std::string> errors(n);
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    std::vector<uint8_t> body;
+    for (size_t i; (i = next.fetch_add(1)) < n;) {
+      const int K = ks[i];
+      const Member& im = idx.at(K);
+      const std::string& h = hdr.at(K);
+      const uint8_t* raw = (const uint8_t*)(base + offs[i] * G);
+      const size_t raw_n = (size_t)K * G * sizeof(float);
+      uint32_t dcrc = crc.update(0, (const uint8_t*)h.data(), h.size());
+      dcrc = crc.update(dcrc, raw, raw_n);
+      const uint32_t dsize = (uint32_t)(h.size() + raw_n);
+      const uint32_t off_data = off_index + (uint32_t)(im.local.size() + im.payload.size());
+      const std::string dlocal = local_header("data.npy", dcrc, dsize);
+      const uint32_t off_cd = off_data + (uint32_t)(dlocal.size() + dsize);
+      std::string cd = central_record("columns.npy", col.crc, (uint32_t)col.payload.size(), 0) +
+                       central_record("index.npy", im.crc, (uint32_t)im.payload.size(), off_index) +
+                       central_record("data.npy", dcrc, dsize, off_data);
+      std::string end;
+      put32(end, 0x06054B50); put16(end, 0); put16(end, 0); put16(end, 3); put16(end, 3);
+      put32(end, (uint32_t)cd.size()); put32(end, off_cd); put16(end, 0);
+      Sha256 sh = mid;
+      auto feed = [&](const void* p, size_t len) { sh.update((const uint8_t*)p, len); };
+      feed(im.local.data(), im.local.size());
+      feed(im.payload.data(), im.payload.size());
+      feed(dlocal.data(), dlocal.size());
+      feed(h.data(), h.size());
+      feed(raw, raw_n);
+      feed(cd.data(), cd.size());
+      feed(end.data(), end.size());
+      const std::string tmp = paths[i] + ".tmp" + std::to_string(::getpid()) + "_" +
+                              std::to_string(i);
+      FILE* f = std::fopen(tmp.c_str(), "wb");
+      bool ok = f != nullptr;
+      auto put = [&](const void* p, size_t len) {
+        if (ok && len) ok = std::fwrite(p, 1, len, f) == len;
+      };
+      put(col.local.data(), col.local.size());
+      put(col.payload.data(), col.payload.size());
+      put(im.local.data(), im.local.size());
+      put(im.payload.data(), im.payload.size());
+      put(dlocal.data(), dlocal.size());
+      put(h.data(), h.size());
+      put(raw, raw_n);
+      put(cd.data(), cd.size());
+      put(end.data(), end.size());
+      if (f && std::fclose(f) != 0) ok = false;
+      if (!ok || std::rename(tmp.c_str(), paths[i].c_str()) != 0) {
+        std::remove(tmp.c_str());
+        errors[i] = "write failed: " + paths[i];
+        continue;
+      }
+      out[i] = {sh.hex(), (long long)off_cd + (long long)cd.size() + (long long)end.size()};
+    }
+  };
+  {
+    py::gil_scoped_release nogil;
+    const int nt = std::max(1, std::min<int>(threads, (int)n));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  }
+  for (auto& e : errors)
+    if (!e.empty()) throw std::runtime_error(e);
+  return out;
+}
+
+static std::string sha256_hex(py::bytes b) {
+  std::string s(b);
+  Sha256 h;
+  h.update((const uint8_t*)s.data(), s.size());
+  return h.hex();
+}
+
+static unsigned crc32_bytes(py::bytes b) {
+  std::string s(b);
+  return crc_tables().update(0, (const uint8_t*)s.data(), s.size());
+}
+
+PYBIND11_MODULE(_npzio, m) {
+  m.doc() = "cnmf_torch_amd native replicate-file writer (stored npz, crc32, sha256)";
+  m.def("write_spectra_batch", &write_spectra_batch, py::arg("paths"), py::arg("data"),
+        py::arg("offs"), py::arg("ks"), py::arg("columns_npy"), py::arg("index_npy"),
+        py::arg("data_hdr"), py::arg("threads") = 16);
+  m.def("sha256_hex", &sha256_hex);
+  m.def("crc32", &crc32_bytes);
+}

@@ -1,4 +1,4 @@
-// Batched small Gram matrices on MFMA: out[r] (+)= X_r X_r^T for X_r = K x n (K <= 32),
+// Batched small Gram matrices on MFMA: out[r] (+)= X_r X_r^T for X_r = K x n (K <= 64),
 // the hh^T / WW^T products of every NMF step.
 //
 // hipBLASLt runs these (R x K x n)(R x n x K) batched GEMMs with a 16x16 macro tile at
@@ -19,13 +19,18 @@ namespace cnmf {
 
 typedef float gf32x4 __attribute__((ext_vector_type(4)));
 
-template <int T>  // T = 1 (K <= 16) or 2 (K <= 32) tiles per dimension
-__global__ void __launch_bounds__(1024) gram_kernel(const float* __restrict__ X, long long x_rs,
-                                                    long long ldx, int K, int n,
-                                                    float* __restrict__ out, long long o_rs,
-                                                    int accumulate, const int* active,
-                                                    float* __restrict__ part, int per) {
-  __shared__ float red[16][T * T * 16 * 16 + 1];
+// T = 1 (K <= 16), 2 (K <= 32) or 4 (K <= 64) tiles per dimension.  T = 4 keeps 32
+// accumulator tiles per lane: 256-thread workgroups (the register budget of one wave per
+// SIMD, and the per-wave LDS reduction slab fits).
+template <int T>
+constexpr int gram_max_threads() { return T == 4 ? 256 : 1024; }
+
+template <int T>
+__global__ void __launch_bounds__(gram_max_threads<T>()) gram_kernel(
+    const float* __restrict__ X, long long x_rs, long long ldx, int K, int n,
+    float* __restrict__ out, long long o_rs, int accumulate, const int* active,
+    float* __restrict__ part, int per) {
+  __shared__ float red[gram_max_threads<T>() / 64][T * T * 16 * 16 + 1];
   const int rep = blockIdx.x;
   if (active && active[rep] == 0) return;
   const float* __restrict__ x = X + (long long)rep * x_rs;
@@ -117,19 +122,24 @@ extern "C" hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, i
                                 float* out, long long o_rs, int accumulate, const int* active,
                                 float* part, int S, hipStream_t stream) {
   if (R <= 0) return hipSuccess;
-  if (K < 1 || K > 32 || n < 0 || S < 1) return hipErrorInvalidValue;
+  if (K < 1 || K > 64 || n < 0 || S < 1) return hipErrorInvalidValue;
   if (S > 1 && !part) return hipErrorInvalidValue;
   // slice width: a multiple of 16 columns keeps the float4 slabs aligned
   const int per = S > 1 ? (((n + S - 1) / S + 15) / 16) * 16 : n;
   const int cols = S > 1 ? per : n;
-  const int threads = cols >= 16 * 16 ? 1024 : 64 * ((cols + 15) / 16 > 0 ? ((cols + 15) / 16) : 1);
+  const int tmax = K > 32 ? 256 : 1024;
+  int threads = cols >= 16 * 16 ? 1024 : 64 * ((cols + 15) / 16 > 0 ? ((cols + 15) / 16) : 1);
+  if (threads > tmax) threads = tmax;
   const dim3 grid(R, S);
   float* pp = S > 1 ? part : nullptr;
   if (K <= 16)
     hipLaunchKernelGGL((cnmf::gram_kernel<1>), grid, dim3(threads), 0, stream, X, x_rs, ldx, K,
                        n, out, o_rs, accumulate, active, pp, per);
-  else
+  else if (K <= 32)
     hipLaunchKernelGGL((cnmf::gram_kernel<2>), grid, dim3(threads), 0, stream, X, x_rs, ldx, K,
+                       n, out, o_rs, accumulate, active, pp, per);
+  else
+    hipLaunchKernelGGL((cnmf::gram_kernel<4>), grid, dim3(threads), 0, stream, X, x_rs, ldx, K,
                        n, out, o_rs, accumulate, active, pp, per);
   if (S > 1)
     hipLaunchKernelGGL(cnmf::gram_reduce_kernel, dim3(R), dim3(256), 0, stream, part, S, R, K,

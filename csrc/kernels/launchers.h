@@ -6,6 +6,7 @@ extern "C" {
 
 int cnmf_solve_max_k();
 int cnmf_solve_max_threads(int K);
+int cnmf_solve_native_k(int K);
 hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, const float* numer,
                       long long n_rs, long long ldn, const float* gram, long long g_rs,
                       const int* rep_index, int nblocks, int ncols, int max_iter, float tol,

@@ -9,9 +9,14 @@ hipError_t launch_solve_stream(int K, int algo, const SolveParams& p, int nblock
 }
 }  // namespace cnmf
 
-extern "C" int cnmf_solve_max_k() { return 32; }
+extern "C" int cnmf_solve_max_k() { return 64; }
 
-extern "C" int cnmf_solve_max_threads(int K) { return 1024; }
+// ranks the kernels are instantiated for: 1..32 and the padded wide ranks 40..64
+extern "C" int cnmf_solve_native_k(int K) {
+  return (K >= 1 && K <= 32) || K == 40 || K == 48 || K == 56 || K == 64;
+}
+
+extern "C" int cnmf_solve_max_threads(int K) { return K > 32 ? 256 : 1024; }
 
 extern "C" int cnmf_solve_reg_max_cols(int K) {
   return K <= cnmf::kResidentMaxK ? 1024 * cnmf::res_max_cols(K) : 0;
@@ -50,7 +55,8 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.coop_timeout = coop_timeout;
   p.coop_epochs_split = coop_split > 1 ? coop_split : 1;
   if (coop_split > 1 && nsplit > 1) return hipErrorInvalidValue;
-  if (K < 1 || K > 32) return hipErrorInvalidValue;
+  if (!cnmf_solve_native_k(K)) return hipErrorInvalidValue;
+  if (K > 32) return cnmf::launch_solve_wide(K, algo, p, nblocks, threads, stream);
   // variant: 0 auto, 1 streaming, 2 register-resident.  Resident needs every slice to
   // fit U <= res_max_cols(K) columns per thread of a <= 1024-thread workgroup; it runs
   // with the smallest such U and just enough threads for the slice.

@@ -350,8 +350,14 @@ __device__ __forceinline__ float block_objective(__amdgpu_buffer_rsrc_t rx, int 
 // numer re-read from L2 every iteration).  RES = U >= 1: register-resident variant, U
 // columns per thread: x in VGPRs for the whole solve, numerator staged once in LDS.
 // Launched only when every slice fits U columns per thread (host check in cnmf_solve).
+// Launch bound per K: K > 32 (the padded wide ranks 40..64, streaming only) keeps a
+// column's K values, its numerator and the new values live at once (~3K VGPRs), which
+// only fits the 512-register budget of one wave per SIMD: 256-thread workgroups.
+template <int K>
+constexpr int solve_block_threads() { return K > 32 ? 256 : 1024; }
+
 template <int K, int ALGO, int RES>
-__global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
+__global__ __launch_bounds__(solve_block_threads<K>()) void solve_kernel(SolveParams p) {
   constexpr int U = RES ? RES : cols_per_group<K>();
   constexpr int KP = gram_pad(K);
   constexpr bool resident = RES != 0;
@@ -518,7 +524,7 @@ __global__ __launch_bounds__(1024) void solve_kernel(SolveParams p) {
 template <int K, int RES>
 hipError_t launch_solve_k(int algo, const SolveParams& p, int nblocks, int threads,
                           hipStream_t s) {
-  if (threads > 1024) threads = 1024;
+  if (threads > solve_block_threads<K>()) threads = solve_block_threads<K>();
   const int gy = p.nsplit > 1 ? p.nsplit : (p.coop_slots ? p.coop_epochs_split : 1);
   const dim3 grid(nblocks, gy);
   if (algo == 0)
@@ -562,6 +568,16 @@ hipError_t launch_solve_k(int algo, const SolveParams& p, int nblocks, int threa
     case 30: return launch_solve_k<30, RES>(algo, p, nblocks, threads, s);                \
     case 31: return launch_solve_k<31, RES>(algo, p, nblocks, threads, s);                \
     case 32: return launch_solve_k<32, RES>(algo, p, nblocks, threads, s);                \
+    default: return hipErrorInvalidValue;                                                 \
+  }
+
+// wide ranks (K padded to a multiple of 8 by the NMF engine), streaming variant only
+#define CNMF_SOLVE_WIDE_SWITCH()                                                          \
+  switch (K) {                                                                            \
+    case 40: return launch_solve_k<40, 0>(algo, p, nblocks, threads, s);                  \
+    case 48: return launch_solve_k<48, 0>(algo, p, nblocks, threads, s);                  \
+    case 56: return launch_solve_k<56, 0>(algo, p, nblocks, threads, s);                  \
+    case 64: return launch_solve_k<64, 0>(algo, p, nblocks, threads, s);                  \
     default: return hipErrorInvalidValue;                                                 \
   }
 
@@ -611,6 +627,8 @@ hipError_t launch_solve_res_ku(int algo, const SolveParams& p, int nblocks, int 
 // one per translation unit (solve.hip / solve_res.hip / solve_res34.hip build in parallel)
 hipError_t launch_solve_stream(int K, int algo, const SolveParams& p, int nblocks, int threads,
                                hipStream_t s);
+hipError_t launch_solve_wide(int K, int algo, const SolveParams& p, int nblocks, int threads,
+                             hipStream_t s);
 hipError_t launch_solve_resident(int K, int U, int algo, const SolveParams& p, int nblocks,
                                  int threads, hipStream_t s);
 hipError_t launch_solve_resident34(int K, int U, int algo, const SolveParams& p, int nblocks,

@@ -813,3 +813,55 @@ def test_colstats_and_count_unit_check_match_reference():
         fmn = torch.where(torch.isfinite(rmn), rmn, torch.ones_like(rmn))
         assert torch.equal(ops.count_unit_check(M.cuda(), fmn.cuda()).cpu(),
                            reference.count_unit_check(M, fmn))
+
+
+@pytest.mark.parametrize("algo", ["mu", "hals"])
+@pytest.mark.parametrize("K", [40, 48, 64])
+@pytest.mark.parametrize("conv_mode", [0, 1])
+def test_solve_wide_k_matches_fp64_reference(algo, K, conv_mode):
+    """Wide ranks (the padded K in (32, 64]) on the 256-thread streaming instantiations."""
+    x0, numer, gram = _problem(3, K, 3000, seed=K)
+    xg = x0.clone().cuda()
+    it_g = torch.zeros(3, dtype=torch.int32, device="cuda")
+    ops.solve(algo, xg, numer.cuda(), gram.cuda(), max_iter=40, tol=1e-3, conv_mode=conv_mode,
+              iters_out=it_g)
+    xr = x0.double().clone()
+    it_r = torch.zeros(3, dtype=torch.int32)
+    ops.solve(algo, xr, numer.double(), gram.double(), max_iter=40, tol=1e-3,
+              conv_mode=conv_mode, iters_out=it_r)
+    assert (it_g.cpu() - it_r).abs().max() <= 1
+    np.testing.assert_allclose(xg.cpu().double().numpy(), xr.numpy(), rtol=2e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("K", [33, 40, 64])
+def test_gram_wide_k_matches_bmm(K):
+    X = torch.rand((5, K, 3001), dtype=torch.float32)
+    out = ops.gram(X.cuda())
+    ref = torch.bmm(X.double(), X.double().transpose(1, 2))
+    np.testing.assert_allclose(out.cpu().double().numpy(), ref.numpy(), rtol=1e-5)
+
+
+def test_solve_rejects_uninstantiated_k_loudly():
+    x0, numer, gram = _problem(2, 37, 100)
+    with pytest.raises(ValueError, match="pad"):
+        ops.solve("mu", x0.cuda(), numer.cuda(), gram.cuda(), max_iter=2)
+
+
+@pytest.mark.parametrize("K", [37, 64])
+def test_nmf_wide_k_gpu_matches_cpu(K):
+    """K > 32: padded to a multiple of 8 on the GPU (zero components), same factorisation
+    as the CPU oracle at the true K."""
+    from cnmf_torch_amd.models.nmf import run_nmf_batch
+
+    rs = np.random.default_rng(K)
+    N, G = 1200, 300
+    X = (rs.gamma(1, 1, (N, 12)) @ rs.gamma(0.5, 1, (12, G)) + 0.1 * rs.random((N, G))).astype(
+        np.float32)
+    kw = dict(online_chunk_size=600, online_max_pass=4)
+    g = run_nmf_batch(X, K, [3, 4], device="cuda", **kw)
+    c = run_nmf_batch(X, K, [3, 4], device="cpu", **kw)
+    assert g.W.shape == (2 * K, G) and g.HT.shape == (2 * K, N)
+    np.testing.assert_allclose(g.err, c.err, rtol=2e-2)
+    Wg, Wc = g.W.cpu().numpy(), c.W.cpu().numpy()
+    cos = (Wg * Wc).sum(1) / (np.linalg.norm(Wg, axis=1) * np.linalg.norm(Wc, axis=1) + 1e-30)
+    assert np.median(cos) > 0.98, np.sort(cos)[:5]
