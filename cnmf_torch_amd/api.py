@@ -9,7 +9,8 @@ reference, on the MI355X-native engine:
 * ``refit_usage`` / ``refit_spectra`` use the fused on-device refit (models/refit.py).
 * ``consensus`` runs the pairwise distances, density filter, medians and silhouette on
   the device; KMeans uses sklearn's exact algorithm by default
-  (``kmeans_backend='device'`` runs it on the GPU instead).
+  (``kmeans_backend='auto'`` -- the default -- runs the batched k-means on the GPU when one
+  is in use; ``'sklearn'`` is the reference's exact CPU KMeans).
 * multi-worker / multi-GPU: ``factorize(worker_i, total_workers)`` keeps the
   round-robin ledger sharding of cnmf.py:53-54 (CLI ``--worker-index`` restored);
   ``cnmf_torch_amd.parallel`` launches one rank per GPU over torch.distributed.
@@ -152,6 +153,23 @@ def _norm_counts_dense_device(counts, genes, guard_zero_std: bool, dev) -> AnnDa
                   obsm=dict(counts.obsm), uns=dict(counts.uns))
     out.uns["_scaled_on_device"] = True
     return out
+
+
+def _resident_X(adata, dev: torch.device):
+    """``adata.X`` on the device, uploaded once per AnnData object and device and reused
+    by every K of k_selection_plot (refit numerators, prediction error): a DeviceCSR for
+    sparse X, a float32 tensor for dense X; the host matrix itself on the CPU.  The
+    cached copy is keyed on the identity of ``adata.X``."""
+    if dev.type != "cuda":
+        return adata.X
+    cache = adata.__dict__.setdefault("_cnmf_device_X", {})
+    key = (str(dev), id(adata.X))
+    if key not in cache:
+        cache.clear()
+        X = adata.X
+        cache[key] = (_device_csr(X, dev) if sp.issparse(X)
+                      else torch.as_tensor(np.asarray(X, dtype=np.float32)).to(dev))
+    return cache[key]
 
 
 def _load_npz_arrays(fn: str):
@@ -770,7 +788,7 @@ class cNMF:
     def consensus(self, k, density_threshold=0.5, local_neighborhood_size=0.30,
                   show_clustering=True, build_ref=True, skip_density_and_return_after_stats=False,
                   close_clustergram_fig=False, refit_usage=True, normalize_tpm_spectra=False,
-                  norm_counts=None, kmeans_backend="sklearn", device=None):
+                  norm_counts=None, kmeans_backend="auto", device=None):
         """Consensus spectra/usages for one K (cnmf.py:997-1256)."""
         with self.timer(f"consensus_k{k}"):
             return self._consensus(k, density_threshold, local_neighborhood_size, show_clustering,
@@ -818,16 +836,14 @@ class cNMF:
         median_np = cluster_medians(L2, labels, sorted(set(labels))).cpu().numpy()
         median_spectra = pd.DataFrame(median_np, index=sorted(set(labels)), columns=merged.columns)
 
-        ncX = _device_csr(norm_counts.X, dev)
-        rf_usages = self.refit_usage(ncX if ncX is not None else norm_counts.X, median_spectra,
-                                     device=dev)
-        del ncX
+        ncX = _resident_X(norm_counts, dev)
+        rf_usages = self.refit_usage(ncX, median_spectra, device=dev)
         rf_usages = pd.DataFrame(rf_usages, index=norm_counts.obs.index, columns=median_spectra.index)
 
         if skip_stats:
             d = pairwise_distances(L2)
             sil = silhouette(d, labels)
-            err = self._prediction_error(norm_counts.X, rf_usages.values, median_spectra.values, dev)
+            err = self._prediction_error(ncX, rf_usages.values, median_spectra.values, dev)
             return pd.DataFrame([k, density_threshold, sil, err],
                                 index=["k", "local_density_threshold", "silhouette",
                                        "prediction_error"], columns=["stats"])
@@ -928,9 +944,22 @@ class cNMF:
 
     @staticmethod
     def _prediction_error(X, usages: np.ndarray, spectra: np.ndarray, dev) -> float:
-        """||X - U S||_F^2 via the trace identity, streamed (never materialises U S)."""
+        """||X - U S||_F^2 via the trace identity, streamed (never materialises U S).  A
+        device-resident X (dense tensor or DeviceCSR, see _resident_X) is used in place."""
         U = torch.as_tensor(usages, dtype=torch.float64, device=dev)
         S = torch.as_tensor(spectra, dtype=torch.float64, device=dev)
+        quad = float(((U.t() @ U) * (S @ S.t())).sum())
+        if isinstance(X, sops.DeviceCSR) and not X.xf:
+            d = X.data.to(torch.float64)
+            UtX = sops.tspmm(X, U).t().to(torch.float64)              # (K, G)
+            return float((d * d).sum()) - 2.0 * float((UtX * S).sum()) + quad
+        if isinstance(X, torch.Tensor):
+            x_sq = cross = 0.0
+            for a in range(0, X.shape[0], 16384):
+                xb = X[a:a + 16384].to(device=dev, dtype=torch.float64)
+                x_sq += float((xb * xb).sum())
+                cross += float(((U[a:a + 16384].t() @ xb) * S).sum())
+            return x_sq - 2.0 * cross + quad
         n = X.shape[0]
         x_sq = 0.0
         cross = 0.0
@@ -965,7 +994,7 @@ class cNMF:
         save_df_to_npz(ref, self.paths["starcat_spectra"] % (k, dt))
         save_df_to_text(ref, self.paths["starcat_spectra__txt"] % (k, dt))
 
-    def k_selection_plot(self, close_fig=False, kmeans_backend="sklearn", comm=None,
+    def k_selection_plot(self, close_fig=False, kmeans_backend="auto", comm=None,
                          device=None):
         """Stability (silhouette) and error per K (cnmf.py:1293-1332).
 

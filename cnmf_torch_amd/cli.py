@@ -82,8 +82,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="[consensus] Generates a reference spectra for use in starCAT")
     p.add_argument("--no-build-reference", dest="build_reference", action="store_false",
                    help="[consensus] Do not build the starCAT reference")
-    p.add_argument("--kmeans-backend", type=str, default="sklearn", choices=["sklearn", "device"],
-                   help="[consensus] sklearn (exact reference KMeans) or device (GPU)")
+    p.add_argument("--kmeans-backend", type=str, default="auto",
+                   choices=["auto", "sklearn", "device"],
+                   help="[consensus] auto (device on GPU, else sklearn), sklearn (the "
+                        "reference's exact KMeans) or device (batched GPU k-means)")
     return p
 
 

@@ -44,26 +44,38 @@ def local_density(dist: torch.Tensor, n_neighbors: int) -> torch.Tensor:
 
 # ------------------------------------------------------------------------- k-means
 def _kmeanspp(X: torch.Tensor, k: int, gen: torch.Generator, x_sq: torch.Tensor) -> torch.Tensor:
-    """Greedy k-means++ (sklearn _kmeans_plusplus, n_local_trials = 2 + log k)."""
-    n = X.shape[0]
+    """Greedy k-means++ (sklearn _kmeans_plusplus, n_local_trials = 2 + log k), one
+    restart (the CPU path; the GPU runs every restart at once in _kmeanspp_batched)."""
+    return _kmeanspp_batched(X, k, gen, 1)[0]
+
+
+def _kmeanspp_batched(X: torch.Tensor, k: int, gen: torch.Generator, n_init: int) -> torch.Tensor:
+    """Greedy k-means++ for ``n_init`` restarts at once (sklearn _kmeans_plusplus with
+    n_local_trials = 2 + log k): every centre step scores all restarts' candidates with
+    ONE distance launch (n x n_init*trials, f64 MFMA), and the candidate sampling (inverse
+    CDF of each restart's potential) stays on the device -- the uniforms are drawn up
+    front from the host generator, so there is no device->host sync per centre.
+    Returns (n_init, k, d)."""
+    n, d = X.shape
+    dev = X.device
     trials = 2 + int(math.log(k))
-    centers = torch.empty((k, X.shape[1]), dtype=X.dtype, device=X.device)
-    first = int(torch.randint(n, (1,), generator=gen).item())
-    centers[0] = X[first]
-    closest = ops.pairwise_dist(X, X[first:first + 1], squared=True)[:, 0]
-    pot = float(closest.sum())
+    first = torch.randint(n, (n_init,), generator=gen)
+    u = torch.rand((max(k - 1, 0), n_init, trials), generator=gen, dtype=torch.float64)
+    first, u = first.to(dev), u.to(dev)
+    centers = torch.empty((n_init, k, d), dtype=X.dtype, device=dev)
+    centers[:, 0] = X[first]
+    closest = ops.pairwise_dist(X, X[first], squared=True)           # (n, n_init)
+    ar = torch.arange(n_init, device=dev)
     for c in range(1, k):
-        r = torch.rand(trials, generator=gen, dtype=torch.float64) * pot
-        # candidate sampling stays on the device (no per-centre D2H of the potentials)
-        cum = torch.cumsum(closest.double(), 0)
-        cand = torch.searchsorted(cum, r.to(cum.device)).clamp(max=n - 1).to(X.device)
-        d = ops.pairwise_dist(X, X[cand], squared=True)
-        newc = torch.minimum(closest[:, None], d)
-        pots = newc.sum(dim=0)
-        best = torch.argmin(pots)
-        centers[c] = X[cand[best]]
-        closest = newc[:, best]
-        pot = float(pots[best])
+        cum = torch.cumsum(closest.double(), 0)                       # (n, n_init)
+        r = u[c - 1] * cum[-1][:, None]                               # (n_init, trials)
+        cand = torch.searchsorted(cum.t().contiguous(), r).clamp(max=n - 1)
+        dcand = ops.pairwise_dist(X, X[cand.reshape(-1)], squared=True)
+        dcand = dcand.view(n, n_init, trials)
+        newc = torch.minimum(closest[:, :, None], dcand)              # (n, n_init, trials)
+        best = torch.argmin(newc.sum(dim=0), dim=1)                   # (n_init,)
+        centers[:, c] = X[cand[ar, best]]
+        closest = newc[:, ar, best]
     return centers
 
 
@@ -119,10 +131,15 @@ def _lloyd_fused(X: torch.Tensor, centers: torch.Tensor, max_iter: int, tol: flo
 
 
 def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 300,
-           tol: float = 1e-4, backend: str = "sklearn"):
+           tol: float = 1e-4, backend: str = "auto"):
     """Returns integer labels 0..k-1 (numpy).  ``backend='sklearn'`` is the reference's
     KMeans(n_clusters=k, n_init=10, random_state=1) (cnmf.py:1082) bit for bit;
-    ``'device'`` runs k-means++ + batched Lloyd on the tensor's device (HIP kernels)."""
+    ``'device'`` runs batched k-means++ + batched Lloyd (same algorithm, own RNG stream)
+    on the tensor's device (HIP kernels); ``'auto'`` (default) = device for GPU tensors,
+    sklearn otherwise."""
+    if backend == "auto":
+        backend = "device" if isinstance(X, torch.Tensor) and X.device.type == "cuda" \
+            else "sklearn"
     if backend == "sklearn":
         from sklearn.cluster import KMeans
 
@@ -134,9 +151,8 @@ def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 3
     Xt = Xt.to(torch.float64)
     # sklearn scales tol by the mean feature variance
     tol_abs = tol * float(Xt.var(dim=0, unbiased=False).mean())
-    x_sq = (Xt * Xt).sum(dim=1)
     gen = torch.Generator(device="cpu").manual_seed(int(random_state))
-    c0 = torch.stack([_kmeanspp(Xt, k, gen, x_sq) for _ in range(n_init)])
+    c0 = _kmeanspp_batched(Xt, k, gen, n_init)
     labels, inertia = _lloyd_batched(Xt, c0, max_iter, tol_abs)
     best = int(torch.argmin(inertia))
     return labels[:, best].cpu().numpy()
@@ -144,16 +160,29 @@ def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 3
 
 def cluster_medians(S: torch.Tensor, labels: np.ndarray, k_labels) -> torch.Tensor:
     """Per-cluster per-gene median (pandas groupby().median() semantics: mean of the two
-    middle values for even counts), rows renormalised to sum 1 (cnmf.py:1087-1090)."""
-    out = []
-    lab = torch.as_tensor(np.asarray(labels), device=S.device)
-    for cl in k_labels:
-        rows = S[lab == cl]
-        srt = torch.sort(rows, dim=0).values
-        m = rows.shape[0]
-        med = srt[m // 2] if m % 2 else 0.5 * (srt[m // 2 - 1] + srt[m // 2])
-        out.append(med)
-    med = torch.stack(out)
+    middle values for even counts), rows renormalised to sum 1 (cnmf.py:1087-1090).
+
+    Segmented on the device with no loop over clusters: every gene column is sorted by
+    value, then stably by cluster, so each cluster's values form an ascending segment and
+    its median sits at fixed offsets of the segment -- two sorts and gathers for all
+    clusters and genes at once, exact."""
+    lab = np.asarray(labels)
+    order = {c: i for i, c in enumerate(k_labels)}
+    rank = np.array([order.get(c, -1) for c in lab], dtype=np.int64)
+    keep = rank >= 0
+    R = S if keep.all() else S[torch.as_tensor(np.flatnonzero(keep), device=S.device)]
+    rk = rank[keep]
+    counts = np.bincount(rk, minlength=len(k_labels))
+    if (counts == 0).any():
+        raise ValueError("cluster_medians: an empty cluster")
+    vals, i1 = torch.sort(R, dim=0)                                   # by value, per gene
+    lab_t = torch.as_tensor(rk, device=S.device)
+    _, i2 = torch.sort(lab_t[i1], dim=0, stable=True)                 # then by cluster
+    seg = torch.gather(vals, 0, i2)
+    start = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    lo_i = torch.as_tensor(start + (counts - 1) // 2, device=S.device)
+    hi_i = torch.as_tensor(start + counts // 2, device=S.device)
+    med = 0.5 * (seg[lo_i] + seg[hi_i])
     return med / med.sum(dim=1, keepdim=True)
 
 

@@ -70,7 +70,7 @@ def distributed_factorize(obj, skip_completed_runs: bool = False, replicate_batc
 
 
 def distributed_consensus(obj, ks, density_threshold=0.5, local_neighborhood_size=0.30,
-                          show_clustering=True, build_ref=True, kmeans_backend="sklearn",
+                          show_clustering=True, build_ref=True, kmeans_backend="auto",
                           backend: str | None = None):
     """K-parallel consensus: rank r runs ``consensus`` for ``ks[r::world]`` on its own GPU.
     Every K writes its own artifacts (consensus/score/TPM files, density cache, plot), so
@@ -84,7 +84,7 @@ def distributed_consensus(obj, ks, density_threshold=0.5, local_neighborhood_siz
     return comm
 
 
-def distributed_k_selection(obj, kmeans_backend="sklearn", backend: str | None = None):
+def distributed_k_selection(obj, kmeans_backend="auto", backend: str | None = None):
     """K-parallel ``k_selection_plot``: stats per K on every rank, rank 0 writes."""
     comm, dev = init_distributed(backend)
     stats = obj.k_selection_plot(close_fig=True, kmeans_backend=kmeans_backend, comm=comm,

@@ -830,7 +830,7 @@ def test_solve_wide_k_matches_fp64_reference(algo, K, conv_mode):
     ops.solve(algo, xr, numer.double(), gram.double(), max_iter=40, tol=1e-3,
               conv_mode=conv_mode, iters_out=it_r)
     assert (it_g.cpu() - it_r).abs().max() <= 1
-    np.testing.assert_allclose(xg.cpu().double().numpy(), xr.numpy(), rtol=2e-3, atol=1e-5)
+    np.testing.assert_allclose(xg.cpu().double().numpy(), xr.numpy(), rtol=2e-3, atol=1e-4)
 
 
 @pytest.mark.parametrize("K", [33, 40, 64])
@@ -865,3 +865,44 @@ def test_nmf_wide_k_gpu_matches_cpu(K):
     Wg, Wc = g.W.cpu().numpy(), c.W.cpu().numpy()
     cos = (Wg * Wc).sum(1) / (np.linalg.norm(Wg, axis=1) * np.linalg.norm(Wc, axis=1) + 1e-30)
     assert np.median(cos) > 0.98, np.sort(cos)[:5]
+
+
+def test_device_kmeans_inertia_matches_sklearn_over_seeds():
+    """The default GPU k-means (batched k-means++ + batched Lloyd) reaches sklearn's
+    KMeans(n_init=10) inertia on replicate-spectra-like data (consensus clustering)."""
+    from sklearn.cluster import KMeans
+
+    from cnmf_torch_amd.models.consensus import kmeans
+
+    worse = 0
+    ratios = []
+    for seed in range(20):
+        rs = np.random.default_rng(seed)
+        k, reps, G = 7, 40, 300
+        centers = rs.gamma(0.5, 1, (k, G))
+        S = np.concatenate([c * rs.lognormal(0, 0.15, (reps, G)) for c in centers])
+        S /= np.linalg.norm(S, axis=1, keepdims=True)
+        lab = kmeans(torch.from_numpy(S).cuda(), k, n_init=10, random_state=1, backend="device")
+
+        def inertia(lb):
+            return sum(((S[lb == c] - S[lb == c].mean(0)) ** 2).sum() for c in np.unique(lb))
+        ref = KMeans(n_clusters=k, n_init=10, random_state=1).fit(S).labels_
+        r = inertia(lab) / inertia(ref)
+        ratios.append(r)
+        worse += r > 1 + 1e-9
+    assert worse <= 1 and np.mean(ratios) <= 1 + 1e-6, ratios
+
+
+def test_cluster_medians_device_matches_pandas():
+    import pandas as pd
+
+    from cnmf_torch_amd.models.consensus import cluster_medians
+
+    rs = np.random.default_rng(1)
+    S = rs.random((301, 123))
+    S /= np.linalg.norm(S, axis=1, keepdims=True)
+    lab = rs.integers(1, 9, 301)
+    got = cluster_medians(torch.from_numpy(S).cuda(), lab, sorted(set(lab))).cpu().numpy()
+    ref = pd.DataFrame(S).groupby(lab).median()
+    ref = ref.div(ref.sum(axis=1), axis=0).values
+    np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-15)

@@ -39,7 +39,7 @@ def main():
     ap.add_argument("--threshold", type=float, default=0.1)
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--profile", default=None, help="cProfile every stage into this file")
-    ap.add_argument("--kmeans-backend", default="sklearn", choices=["sklearn", "device"],
+    ap.add_argument("--kmeans-backend", default="auto", choices=["auto", "sklearn", "device"],
                     help="sklearn = the reference's exact KMeans; device = batched GPU restarts")
     a = ap.parse_args()
     work = a.workdir or tempfile.mkdtemp(prefix="cnmf_e2e_")
