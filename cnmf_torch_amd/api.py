@@ -24,6 +24,7 @@ import itertools
 import json
 import os
 import shutil
+import sys
 import time
 import uuid
 import warnings
@@ -39,7 +40,7 @@ from .models.hvg import compute_tpm, get_highvar_genes, get_highvar_genes_sparse
 from .models.nmf import NMFBatchSolver, NMFOptions
 from .models.ols import efficient_ols_all_cols
 from .models.pp import scale as pp_scale
-from .models.refit import fit_H_online, fit_spectra_online
+from .models.refit import col_block, fit_H_online, fit_spectra_online, gene_blocks
 from .ops import sparse as sops
 from .parallel.ledger import worker_filter
 from .utils.anndata_lite import AnnData
@@ -775,30 +776,50 @@ class cNMF:
                             l1_reg_H=kw.get("l1_ratio_H", 0.0), l2_reg_H=0.0, epsilon=1e-16,
                             device=dev)
 
-    def refit_spectra(self, X, usage, device=None):
-        """Refit spectra with usages fixed (cnmf.py:979-994)."""
+    def refit_spectra(self, X, usage, device=None, comm=None):
+        """Refit spectra with usages fixed (cnmf.py:979-994).  With a multi-rank ``comm``
+        the genes are sharded over the ranks in whole refit chunks (tensor/gene-axis
+        parallelism) and the K x G blocks are all-gathered."""
         kw = self._refit_kwargs()
         dev = _device(bool(kw.get("use_gpu", False)), device)
         u = usage.values if isinstance(usage, pd.DataFrame) else np.asarray(usage)
-        return fit_spectra_online(X, u, chunk_size=kw["online_chunk_size"],
-                                  chunk_max_iter=kw["online_chunk_max_iter"], h_tol=0.05,
-                                  l1_reg=kw.get("l1_ratio_H", 0.0), device=dev)
+        args = dict(chunk_size=kw["online_chunk_size"], chunk_max_iter=kw["online_chunk_max_iter"],
+                    h_tol=0.05, l1_reg=kw.get("l1_ratio_H", 0.0), device=dev)
+        if comm is None or comm.world_size == 1:
+            return fit_spectra_online(X, u, **args)
+        g0, g1 = gene_blocks(X.shape[1], kw["online_chunk_size"], comm.world_size)[comm.rank]
+        part = fit_spectra_online(col_block(X, g0, g1), u, col_offset=g0, **args) if g1 > g0 \
+            else np.zeros((u.shape[1], 0), dtype=np.float32)
+        return np.concatenate(comm.all_gather_object(part), axis=1)
 
     # ------------------------------------------------------------------ consensus
     def consensus(self, k, density_threshold=0.5, local_neighborhood_size=0.30,
                   show_clustering=True, build_ref=True, skip_density_and_return_after_stats=False,
                   close_clustergram_fig=False, refit_usage=True, normalize_tpm_spectra=False,
-                  norm_counts=None, kmeans_backend="auto", device=None):
-        """Consensus spectra/usages for one K (cnmf.py:997-1256)."""
+                  norm_counts=None, kmeans_backend="auto", device=None, comm=None):
+        """Consensus spectra/usages for one K (cnmf.py:997-1256).  With a multi-rank
+        ``comm`` the two all-gene passes -- the TPM spectra refit and the OLS gene scores
+        over G_all -- are sharded over the ranks by gene blocks (the clustering is
+        replicated); rank 0 writes the artifacts."""
         with self.timer(f"consensus_k{k}"):
             return self._consensus(k, density_threshold, local_neighborhood_size, show_clustering,
                                    build_ref, skip_density_and_return_after_stats,
                                    close_clustergram_fig, refit_usage, normalize_tpm_spectra,
-                                   norm_counts, kmeans_backend, device)
+                                   norm_counts, kmeans_backend, device, comm)
 
     def _consensus(self, k, density_threshold, local_neighborhood_size, show_clustering,
                    build_ref, skip_stats, close_fig, refit_usage, normalize_tpm_spectra,
-                   norm_counts, kmeans_backend, device):
+                   norm_counts, kmeans_backend, device, comm=None):
+        tp = comm is not None and comm.world_size > 1
+        writer = not tp or comm.rank == 0
+        # a closed clustergram is drawn by a child process that imports matplotlib while
+        # this stage computes (utils.plotting.PlotWorker)
+        plot_worker = None
+        if show_clustering and close_fig and writer and not skip_stats and \
+                "matplotlib.pyplot" not in sys.modules:
+            from .utils.plotting import PlotWorker
+
+            plot_worker = PlotWorker()
         kw = self._refit_kwargs()
         dev = _device(bool(kw.get("use_gpu", False)), device)
         merged = load_df_from_npz(self.paths["merged_spectra"] % k)
@@ -821,9 +842,10 @@ class cNMF:
                 topics_dist = pairwise_distances(L2)
                 dens = local_density(topics_dist, n_neighbors).cpu().numpy()
                 local_dens = pd.DataFrame(dens, columns=["local_density"], index=names)
-                save_df_to_npz(local_dens, cache)
-                write_text_atomic(cache + ".meta.json", json.dumps(
-                    {"n_neighbors": n_neighbors, "n_spectra": int(len(names))}))
+                if writer:
+                    save_df_to_npz(local_dens, cache)
+                    write_text_atomic(cache + ".meta.json", json.dumps(
+                        {"n_neighbors": n_neighbors, "n_spectra": int(len(names))}))
             density_filter = (local_dens.iloc[:, 0] < density_threshold).values
             keep = torch.as_tensor(np.flatnonzero(density_filter), device=dev)
             L2 = L2.index_select(0, keep)
@@ -864,12 +886,22 @@ class cNMF:
         # scaled-HVG usage refit below are CSR kernel passes over it (ops.sparse)
         dT = _device_csr(tpm.X, dev)
         tpmX = dT if dT is not None else tpm.X
-        spectra_tpm = self.refit_spectra(tpmX, norm_usages.astype(tpm.X.dtype), device=dev)
+        spectra_tpm = self.refit_spectra(tpmX, norm_usages.astype(tpm.X.dtype), device=dev,
+                                         comm=comm if tp else None)
         spectra_tpm = pd.DataFrame(spectra_tpm, index=new_cols, columns=tpm.var.index)
         if normalize_tpm_spectra:
             spectra_tpm = spectra_tpm.div(spectra_tpm.sum(axis=1), axis=0) * 1e6
 
-        usage_coef = efficient_ols_all_cols(rf_usages.values, tpmX, normalize_y=True, device=dev)
+        if tp:   # gene-sharded OLS: each rank z-scores and solves its gene block
+            g0, g1 = gene_blocks(tpm.shape[1], self._refit_kwargs()["online_chunk_size"],
+                                 comm.world_size)[comm.rank]
+            part = efficient_ols_all_cols(rf_usages.values, col_block(tpmX, g0, g1),
+                                          normalize_y=True, device=dev) if g1 > g0 else \
+                np.zeros((rf_usages.shape[1], 0))
+            usage_coef = np.concatenate(comm.all_gather_object(part), axis=1)
+        else:
+            usage_coef = efficient_ols_all_cols(rf_usages.values, tpmX, normalize_y=True,
+                                                device=dev)
         usage_coef = pd.DataFrame(usage_coef, index=new_cols, columns=tpm.var.index)
 
         if refit_usage:
@@ -900,6 +932,8 @@ class cNMF:
             rf_usages = pd.DataFrame(rf, index=norm_counts.obs.index, columns=spectra_tpm_rf.index)
         del dT, tpmX
 
+        if not writer:
+            return None
         p = self.paths
         save_df_to_npz(median_spectra, p["consensus_spectra"] % (k, dt_repl))
         save_df_to_npz(rf_usages, p["consensus_usages"] % (k, dt_repl))
@@ -918,13 +952,27 @@ class cNMF:
             else:
                 keep = torch.as_tensor(np.flatnonzero(density_filter), device=topics_dist.device)
                 topics_dist = topics_dist.index_select(0, keep).index_select(1, keep)
-            clustergram(topics_dist.cpu().numpy(), label_series, local_dens, density_filter,
-                        density_threshold, p["clustering_plot"] % (k, dt_repl), close=close_fig)
+            if plot_worker is not None:
+                plot_worker.submit(
+                    "clustergram", p["clustering_plot"] % (k, dt_repl),
+                    dist=topics_dist.cpu().numpy(), labels=label_series.values,
+                    names=np.asarray(label_series.index).astype(str),
+                    local_density=(local_dens.values.reshape(-1) if local_dens is not None
+                                   else np.zeros(0)),
+                    density_filter=(density_filter if density_filter is not None
+                                    else np.zeros(0, dtype=bool)),
+                    density_threshold=np.float64(density_threshold))
+            else:
+                clustergram(topics_dist.cpu().numpy(), label_series, local_dens, density_filter,
+                            density_threshold, p["clustering_plot"] % (k, dt_repl),
+                            close=close_fig)
         if build_ref:
             # the reference re-reads the TSV it just wrote (cnmf.py:1273); float64 text is
             # an exact round trip, so the in-memory frame gives the same reference
             mem = spectra_tpm if (spectra_tpm.dtypes == np.float64).all() else None
             self.build_reference(k, density_threshold, _spectra_tpm=mem)
+        if plot_worker is not None:
+            plot_worker.wait()
 
     def _load_density_cache(self, cache: str, n_neighbors: int, names):
         """Density cache keyed on K AND the neighbourhood (SURVEY.md §5.2 fix): a cache
@@ -1002,9 +1050,14 @@ class cNMF:
         rank runs its Ks' stats on its own device, and rank 0 gathers the rows (Python
         objects, a few floats per K) and writes the npz and the plot."""
         run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
+        rank, world = (0, 1) if comm is None else (comm.rank, comm.world_size)
+        plot_worker = None
+        if close_fig and rank == 0 and "matplotlib.pyplot" not in sys.modules:
+            from .utils.plotting import PlotWorker
+
+            plot_worker = PlotWorker()   # imports matplotlib while the stats compute
         norm_counts = read_h5ad(self.paths["normalized_counts"])
         ks = sorted(set(int(x) for x in run_params.n_components))
-        rank, world = (0, 1) if comm is None else (comm.rank, comm.world_size)
         rows = {}
         for k in ks[rank::world]:
             rows[k] = self.consensus(k, skip_density_and_return_after_stats=True,
@@ -1018,9 +1071,17 @@ class cNMF:
                 return None
         stats = pd.DataFrame([rows[k] for k in ks]).reset_index(drop=True)
         save_df_to_npz(stats, self.paths["k_selection_stats"])
-        from .utils.plotting import k_selection
+        if plot_worker is not None:
+            plot_worker.submit("k_selection", self.paths["k_selection_plot"],
+                               k=stats["k"].to_numpy(dtype=np.float64),
+                               silhouette=stats["silhouette"].to_numpy(dtype=np.float64),
+                               prediction_error=stats["prediction_error"].to_numpy(
+                                   dtype=np.float64))
+            plot_worker.wait()
+        else:
+            from .utils.plotting import k_selection
 
-        k_selection(stats, self.paths["k_selection_plot"], close=close_fig)
+            k_selection(stats, self.paths["k_selection_plot"], close=close_fig)
         return stats
 
     def load_results(self, K, density_threshold, n_top_genes=100, norm_usage=True):

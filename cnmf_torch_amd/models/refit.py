@@ -102,7 +102,8 @@ def chunked_solve(HT: torch.Tensor, numerT: torch.Tensor, gram: torch.Tensor, ch
     return HT
 
 
-def _init_HT(K: int, n: int, H_init, device, dtype, random_state: int) -> torch.Tensor:
+def _init_HT(K: int, n: int, H_init, device, dtype, random_state: int,
+             row_offset: int = 0) -> torch.Tensor:
     if H_init is not None:
         H0 = torch.as_tensor(np.asarray(_to_numpy_2d(H_init)), dtype=dtype)
         return torch.clamp(H0, min=0.0).t().contiguous().to(device)
@@ -110,8 +111,35 @@ def _init_HT(K: int, n: int, H_init, device, dtype, random_state: int) -> torch.
     if n:
         ops.philox_fill(HT.as_strided((1, n, K), (K * n, 1, n)),
                         torch.tensor([int(random_state)]), torch.tensor([1.0]), rng.STREAM_REFIT,
-                        mode=1)
+                        mode=1, row_offset=int(row_offset))
     return HT
+
+
+def col_block(X, g0: int, g1: int):
+    """Columns [g0, g1) of X (dense numpy/torch, scipy sparse or a plain DeviceCSR, the
+    latter as a lazy column-map view) -- a rank's gene block under gene-axis sharding."""
+    if isinstance(X, sops.DeviceCSR):
+        if X.xf:
+            raise ValueError("col_block: transformed DeviceCSR views are not sharded")
+        cmap = np.full(X.shape[1], -1, np.int32)
+        cmap[g0:g1] = np.arange(g1 - g0, dtype=np.int32)
+        return X.view(col_map=cmap, n_out=g1 - g0)
+    if isinstance(X, pd.DataFrame):
+        return X.iloc[:, g0:g1]
+    return X[:, g0:g1]
+
+
+def gene_blocks(G: int, chunk: int, world: int) -> list[tuple[int, int]]:
+    """Gene-axis shards made of WHOLE refit chunks (the chunked solve's convergence is
+    decided per chunk), so a sharded spectra refit equals the unsharded one."""
+    c = max(1, int(chunk))
+    n_chunks = -(-G // c) if G else 0
+    out = []
+    for r in range(world):
+        a = (n_chunks * r // world) * c
+        b = min(G, (n_chunks * (r + 1) // world) * c)
+        out.append((min(a, G), b))
+    return out
 
 
 def fit_H_online(X, W, H_init=None, chunk_size: int = 5000, chunk_max_iter: int = 200,
@@ -137,10 +165,13 @@ def fit_H_online(X, W, H_init=None, chunk_size: int = 5000, chunk_max_iter: int 
 
 def fit_spectra_online(X, usage, chunk_size: int = 5000, chunk_max_iter: int = 200,
                        h_tol: float = 0.05, l1_reg: float = 0.0, epsilon: float = 1e-16,
-                       device="cpu", random_state: int = 0):
+                       device="cpu", random_state: int = 0, col_offset: int = 0):
     """Refit spectra S (K x G) >= 0 minimising ||X - U S|| with usages U (n x K) fixed.
 
-    Equals ``fit_H_online(X.T, U.T).T`` (cnmf.py:994): chunks run over genes."""
+    Equals ``fit_H_online(X.T, U.T).T`` (cnmf.py:994): chunks run over genes.
+    ``col_offset``: X holds the genes [col_offset, col_offset + G) of a larger matrix (a
+    gene-sharded rank): the seeded init is taken at those genes, so shards reproduce
+    the unsharded refit when they hold whole chunks (gene_blocks)."""
     dev = torch.device(device)
     Ut = torch.as_tensor(np.asarray(_to_numpy_2d(usage), dtype=np.float32)).to(dev)
     Xv = X.values if isinstance(X, pd.DataFrame) else X
@@ -148,6 +179,6 @@ def fit_spectra_online(X, usage, chunk_size: int = 5000, chunk_max_iter: int = 2
     G = Xv.shape[1]
     numerT = numer_cols(Ut, Xv)          # (K x G) = (X^T U)^T
     gram = Ut.t() @ Ut
-    ST = _init_HT(K, G, None, dev, torch.float32, random_state)
+    ST = _init_HT(K, G, None, dev, torch.float32, random_state, row_offset=col_offset)
     chunked_solve(ST, numerT, gram, chunk_size, chunk_max_iter, h_tol, l1_num=l1_reg, eps=epsilon)
     return ST.cpu().numpy()

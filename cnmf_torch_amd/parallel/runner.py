@@ -72,14 +72,24 @@ def distributed_factorize(obj, skip_completed_runs: bool = False, replicate_batc
 def distributed_consensus(obj, ks, density_threshold=0.5, local_neighborhood_size=0.30,
                           show_clustering=True, build_ref=True, kmeans_backend="auto",
                           backend: str | None = None):
-    """K-parallel consensus: rank r runs ``consensus`` for ``ks[r::world]`` on its own GPU.
-    Every K writes its own artifacts (consensus/score/TPM files, density cache, plot), so
-    the ranks share no files and need no collective beyond the closing barrier."""
+    """Consensus over the ranks.  With at least as many Ks as ranks: K parallelism (rank r
+    runs ``consensus`` for ``ks[r::world]`` on its own GPU; every K writes its own
+    artifacts, so the ranks share no files).  With fewer Ks than ranks (typically the one
+    chosen K): every K runs on ALL ranks with its all-gene passes (TPM spectra refit, OLS
+    gene scores over G_all) sharded by gene blocks -- tensor / gene-axis parallelism."""
     comm, dev = init_distributed(backend)
-    for k in sorted(ks)[comm.rank::comm.world_size]:
-        obj.consensus(k, density_threshold, local_neighborhood_size, show_clustering,
-                      build_ref, close_clustergram_fig=True, kmeans_backend=kmeans_backend,
-                      device=dev)
+    ks = sorted(ks)
+    if len(ks) >= comm.world_size or comm.world_size == 1:
+        for k in ks[comm.rank::comm.world_size]:
+            obj.consensus(k, density_threshold, local_neighborhood_size, show_clustering,
+                          build_ref, close_clustergram_fig=True, kmeans_backend=kmeans_backend,
+                          device=dev)
+    else:
+        for k in ks:
+            obj.consensus(k, density_threshold, local_neighborhood_size,
+                          show_clustering and comm.rank == 0, build_ref,
+                          close_clustergram_fig=True, kmeans_backend=kmeans_backend, device=dev,
+                          comm=comm)
     comm.barrier()
     return comm
 

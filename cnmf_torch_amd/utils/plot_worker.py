@@ -1,0 +1,30 @@
+"""Child process of plotting.PlotWorker: import matplotlib at once (overlapping the
+parent's GPU work), then draw every job read from stdin and exit at EOF."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import matplotlib  # noqa: E402
+
+matplotlib.use("Agg")
+import matplotlib.pyplot  # noqa: E402,F401
+import numpy as np  # noqa: E402
+
+import plotting  # noqa: E402  (this directory: numpy / pandas / matplotlib only)
+
+
+def main() -> int:
+    for line in sys.stdin:
+        if not line.strip():
+            continue
+        job = json.loads(line)
+        with np.load(job["npz"], allow_pickle=False) as f:
+            arrays = {k: f[k] for k in f.files}
+        plotting.draw_job(job["kind"], job["path"], arrays)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,6 +1,19 @@
 """Figures: consensus clustergram (C25, cnmf.py:1160-1253), K-selection plot (C27,
-cnmf.py:1311-1332) and the Preprocess QC histograms (C32).  matplotlib, Agg backend."""
+cnmf.py:1311-1332) and the Preprocess QC histograms (C32).  matplotlib, Agg backend.
+
+Figures that the caller closes anyway (``close=True``: CLI and pipeline runs) can be drawn
+by :class:`PlotWorker`, a child Python process started when a stage begins: it imports
+matplotlib (~0.8 s on a fresh box, where its .pyc files are compiled) while the stage
+computes on the GPU, then draws the same figure with the same code.  This module imports
+only numpy/pandas at the top, so the worker never loads torch or touches the GPU.
+"""
 from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
 
 import numpy as np
 import pandas as pd
@@ -77,13 +90,25 @@ def clustergram(dist: np.ndarray, labels: pd.Series, local_density: pd.DataFrame
     cax = fig.add_subplot(cgs[4, 0], title="Euclidean Distance")
     fig.colorbar(im, cax=cax, ticks=np.linspace(float(D.min()), float(D.max()), 3),
                  orientation="horizontal")
-    from .io import atomic_path
-
-    with atomic_path(path, suffix=".png") as tmp:
-        fig.savefig(tmp, dpi=250)
+    _save(fig, path)
     if close:
         plt.close(fig)
     return fig
+
+
+def _save(fig, path: str) -> None:
+    """Atomic PNG write (temp file in the destination directory + rename)."""
+    d = os.path.dirname(os.path.abspath(path)) or "."
+    fd, tmp = tempfile.mkstemp(prefix=".tmp_" + os.path.basename(path) + ".", suffix=".png",
+                               dir=d)
+    os.close(fd)
+    try:
+        fig.savefig(tmp, dpi=250)
+        os.replace(tmp, path)
+    except BaseException:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+        raise
 
 
 def k_selection(stats: pd.DataFrame, path: str, close: bool = False):
@@ -102,10 +127,7 @@ def k_selection(stats: pd.DataFrame, path: str, close: bool = False):
     ax1.set_xlabel("Number of Components", fontsize=15)
     ax1.grid(True)
     plt.tight_layout()
-    from .io import atomic_path
-
-    with atomic_path(path, suffix=".png") as tmp:
-        fig.savefig(tmp, dpi=250)
+    _save(fig, path)
     if close:
         plt.close(fig)
     return fig
@@ -122,3 +144,58 @@ def count_hist(X, num_cells: int = 1000, title="Quantile thresholded normalized 
     ax.hist(y[y > 0], bins=100)
     ax.set_title(title)
     return fig
+
+
+class PlotWorker:
+    """Out-of-process figure drawer (see the module docstring).  ``submit`` hands one
+    figure job to the child (arrays through a temporary .npz); ``wait`` blocks until the
+    child has written every figure.  Any failure of the child falls back to drawing in
+    this process, so figures are never lost."""
+
+    def __init__(self):
+        env = dict(os.environ, MPLBACKEND="Agg", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "plot_worker.py")
+        self.jobs = []
+        self.proc = subprocess.Popen([sys.executable, script], stdin=subprocess.PIPE,
+                                     stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env,
+                                     text=True)
+
+    def submit(self, kind: str, path: str, **arrays) -> None:
+        fd, npz = tempfile.mkstemp(suffix=".npz")
+        os.close(fd)
+        np.savez(npz, **{k: np.asarray(v) for k, v in arrays.items()})
+        self.jobs.append((kind, path, npz))
+        self.proc.stdin.write(json.dumps({"kind": kind, "path": path, "npz": npz}) + "\n")
+        self.proc.stdin.flush()
+
+    def wait(self, timeout: float = 300.0) -> None:
+        ok = False
+        try:
+            out, err = self.proc.communicate(timeout=timeout)
+            ok = self.proc.returncode == 0 and all(os.path.exists(p) for _, p, _ in self.jobs)
+        except Exception:
+            self.proc.kill()
+        if not ok:   # draw here instead
+            for kind, path, npz in self.jobs:
+                with np.load(npz, allow_pickle=False) as f:
+                    draw_job(kind, path, {k: f[k] for k in f.files})
+        for _, _, npz in self.jobs:
+            if os.path.exists(npz):
+                os.remove(npz)
+
+
+def draw_job(kind: str, path: str, a: dict) -> None:
+    """Draw one PlotWorker job from its arrays (in the worker, or as the fallback)."""
+    if kind == "k_selection":
+        stats = pd.DataFrame({"k": a["k"], "silhouette": a["silhouette"],
+                              "prediction_error": a["prediction_error"]})
+        k_selection(stats, path, close=True)
+    elif kind == "clustergram":
+        labels = pd.Series(a["labels"], index=a["names"])
+        dens = (pd.DataFrame(a["local_density"], columns=["local_density"])
+                if a["local_density"].size else None)
+        filt = a["density_filter"].astype(bool) if a["density_filter"].size else None
+        clustergram(a["dist"], labels, dens, filt, float(a["density_threshold"]), path,
+                    close=True)
+    else:
+        raise ValueError(kind)

@@ -120,3 +120,13 @@ def prepare_worker(rank, world, port, output_dir, name, counts_fn, kw):
 
     cNMF(output_dir=output_dir, name=name).prepare(counts_fn, comm=DistComm(), **kw)
     dist.destroy_process_group()
+
+
+def tp_consensus_worker(rank, world, port, output_dir, name, k):
+    _init(rank, world, port)
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.parallel.runner import distributed_consensus
+
+    distributed_consensus(cNMF(output_dir=output_dir, name=name), [k], density_threshold=0.5,
+                          show_clustering=False, backend="gloo")
+    dist.destroy_process_group()

@@ -221,3 +221,26 @@ def test_sharded_prepare_matches_single_process(tmp_path, fmt):
     pa = load_df_from_npz(sh.paths["nmf_replicate_parameters"])
     pb = load_df_from_npz(ser.paths["nmf_replicate_parameters"])
     assert pa.equals(pb)
+
+
+def test_gene_sharded_consensus_matches_serial(prepared):
+    """One K on 3 gloo ranks: the TPM spectra refit and the OLS gene scores over G_all are
+    sharded by whole refit chunks (tensor / gene-axis parallelism) and all-gathered; the
+    artifacts equal the serial consensus."""
+    d, fn = prepared
+    obj = cNMF(output_dir=str(d), name="tp")
+    obj.prepare(fn, components=[4], n_iter=4, seed=8, num_highvar_genes=120, batch_size=60)
+    obj.factorize(verbose=False)
+    obj.combine()
+    keys = ("consensus_spectra", "consensus_usages", "gene_spectra_score", "gene_spectra_tpm",
+            "starcat_spectra")
+    obj.consensus(4, 0.5, show_clustering=False, close_clustergram_fig=True)
+    ser = {key: load_df_from_npz(obj.paths[key] % (4, "0_5")) for key in keys}
+    for key in keys:
+        os.remove(obj.paths[key] % (4, "0_5"))
+    _spawn(W.tp_consensus_worker, 3, str(d), "tp", 4)
+    for key in keys:
+        got = load_df_from_npz(obj.paths[key] % (4, "0_5"))
+        assert list(got.columns) == list(ser[key].columns), key
+        np.testing.assert_allclose(got.values, ser[key].values, rtol=1e-5, atol=1e-9,
+                                   err_msg=key)

@@ -282,3 +282,30 @@ def test_cli_dp_factorize_over_torchrun_matches_serial(tmp_path):
             a = load_df_from_npz(objs["dp"].paths["iter_spectra"] % (k, i)).values
             b = load_df_from_npz(objs["serial"].paths["iter_spectra"] % (k, i)).values
             np.testing.assert_allclose(a, b, rtol=5e-3, atol=1e-6)
+
+
+def test_figures_drawn_by_plot_worker_process(tmp_path):
+    """Closed figures (CLI / pipeline) are drawn by a child process that imports matplotlib
+    while the stage computes: the stage process itself never imports pyplot."""
+    Xc, cells, genes = simulate_counts(150, 80, 3, seed=3, sparse=False)
+    fn = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(Xc, index=cells, columns=genes), fn)
+    code = f"""
+import os, sys
+sys.path.insert(0, {repr(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))})
+from cnmf_torch_amd import cNMF
+o = cNMF(output_dir={repr(str(tmp_path))}, name="pw")
+o.prepare({repr(fn)}, components=[3, 4], n_iter=10, seed=1, num_highvar_genes=50)
+o.factorize(verbose=False); o.combine()
+o.k_selection_plot(close_fig=True)
+o.consensus(3, 2.0, show_clustering=True, close_clustergram_fig=True)
+assert 'matplotlib.pyplot' not in sys.modules
+assert os.path.getsize(o.paths['k_selection_plot']) > 1000
+assert os.path.getsize(o.paths['clustering_plot'] % (3, '2_0')) > 1000
+print('ok')
+"""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    env.pop("MPLBACKEND", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                       timeout=600)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

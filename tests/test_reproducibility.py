@@ -40,12 +40,13 @@ def _prepare(tmp_path, ds):
     return cfg, obj
 
 
-def _consensus_and_compare(obj, cfg, ds, device=None, rel_tol=None):
+def _consensus_and_compare(obj, cfg, ds, device=None, rel_tol=None, kmeans_backend="sklearn"):
     for k in cfg["k_values"]:
         shutil.copy(_golden(obj, ds, obj.paths["merged_spectra"] % k),
                     obj.paths["merged_spectra"] % k)
     for k, thr in cfg["consensus"]:
-        obj.consensus(k, density_threshold=thr, show_clustering=False, device=device)
+        obj.consensus(k, density_threshold=thr, show_clustering=False, device=device,
+                      kmeans_backend=kmeans_backend)
     for key in mtd.GOLDEN_KEYS:
         for k, thr in cfg["consensus"]:
             fn = obj.paths[key] % (k, str(thr).replace(".", "_"))
@@ -102,7 +103,18 @@ def test_factorize_reproduces_golden_merged_spectra(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("ds", sorted(mtd.DATASETS))
 def test_gpu_consensus_matches_golden(tmp_path, ds):
-    """Consensus with the HIP kernels (distances, density, refits, OLS) == CPU golden."""
+    """Consensus with the HIP kernels (distances, density, refits, OLS) == CPU golden,
+    with the reference's exact KMeans (kmeans_backend='sklearn')."""
     assert torch.cuda.is_available()
     cfg, obj = _prepare(tmp_path, ds)
     _consensus_and_compare(obj, cfg, ds, device="cuda", rel_tol=1e-10)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ds", sorted(mtd.DATASETS))
+def test_gpu_device_kmeans_consensus_close_to_golden(tmp_path, ds):
+    """The GPU default (batched device k-means, own RNG stream) clusters the replicate
+    spectra like sklearn up to boundary points: outputs within 1e-2 relative."""
+    assert torch.cuda.is_available()
+    cfg, obj = _prepare(tmp_path, ds)
+    _consensus_and_compare(obj, cfg, ds, device="cuda", rel_tol=1e-2, kmeans_backend="device")
