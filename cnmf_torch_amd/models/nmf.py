@@ -590,6 +590,7 @@ def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch
     if algo != "bpp":
         ops.solve("hals" if algo == "halsvar" else algo, x3, numer3, gram3, **kw)
         return
+    planes, colmul = kw.pop("planes", None), kw.pop("planes_colmul", None)
     R, K = x3.shape[0], x3.shape[1]
     active = kw.get("active")
     live = None if active is None else (active[:R] != 0)
@@ -612,6 +613,8 @@ def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch
     iters = kw.get("iters_out")
     if iters is not None:
         iters[:R] += 1 if live is None else live.to(iters.dtype)
+    if planes is not None:   # bpp: the same planes epilogue, as a separate split
+        ops.split_planes(x3.reshape(R * K, x3.shape[2]), planes, col_mul=colmul)
 
 
 def _count_units(X: torch.Tensor, stats=None):
@@ -903,13 +906,39 @@ class NMFBatchSolver:
 
     def split_w(self, W: torch.Tensor):
         """Planes of the spectra (times the count unit) for numer_gemm; call after every
-        change of W."""
+        change of W that the W-solve epilogue did not emit (init, compaction)."""
         xp = self._planes()
         if xp is None:
             return None
         wpl = self._plane_buf("w", W.shape[0], xp.Gp)
         ops.split_planes(W, wpl[:, :W.shape[0]], col_mul=xp.unit)
+        self._w_fresh = self._w_key(W)
         return wpl
+
+    def _w_key(self, W: torch.Tensor):
+        return (W.data_ptr(), W.shape[0], getattr(self, "_layout_version", None))
+
+    def w_planes(self, W: torch.Tensor):
+        """The spectra planes, split only when the W-solve epilogue has not already
+        written them for this W buffer / layout (solve(planes=...) below)."""
+        xp = self._planes()
+        if xp is None:
+            return None
+        if getattr(self, "_w_fresh", None) == self._w_key(W):
+            return self._plane_buf("w", W.shape[0], xp.Gp)
+        return self.split_w(W)
+
+    def solve_planes(self, kind: str, rows: int, cols: int | None = None):
+        """(planes buffer, column multiplier) a solve epilogue writes for the next GEMM:
+        kind 'w' -> the spectra planes (genes on k, times the count unit); 'h' -> the
+        usages planes of a chunk of ``cols`` cells (k padded to the GEMM's BK)."""
+        xp = self._planes()
+        if xp is None:
+            return None, None
+        if kind == "w":
+            return self._plane_buf("w", rows, xp.Gp), xp.unit
+        bk = ops.planes_bk(xp.pb)
+        return self._plane_buf("h", rows, -(-cols // bk) * bk), None
 
     def numer_gemm(self, W: torch.Tensor, wpl, a: int, b: int) -> torch.Tensor:
         """numer = W X[a:b]^T (rows(W), b - a) -- split-precision MFMA when available."""
@@ -921,9 +950,10 @@ class NMFBatchSolver:
         return out
 
     def stats_gemm(self, B: torch.Tensor, HT: torch.Tensor, a: int, b: int,
-                   accumulate: bool) -> None:
+                   accumulate: bool, presplit: bool = False) -> None:
         """B (+)= HT[:, a:b] X[a:b]  (rows(HT), G) -- split-precision MFMA when available
-        (and the chunk start is 8-aligned for the planes' k offset)."""
+        (and the chunk start is 8-aligned for the planes' k offset).  ``presplit``: the
+        H-solve epilogue already wrote the usages planes (solve_planes('h'))."""
         xp = self._planes()
         if xp is None or a % 8:
             B.addmm_(HT[:, a:b], self.X[a:b], beta=1.0 if accumulate else 0.0)
@@ -931,7 +961,8 @@ class NMFBatchSolver:
         bk = ops.planes_bk(xp.pb)
         kd = -(-(b - a) // bk) * bk
         hpl = self._plane_buf("h", HT.shape[0], kd)
-        ops.split_planes(HT[:, a:b], hpl[:, :HT.shape[0]])
+        if not presplit:
+            ops.split_planes(HT[:, a:b], hpl[:, :HT.shape[0]])
         ops.gemm_planes(B, hpl, xp.xt[:, :, a:], HT.shape[0], xp.G, kd, accumulate=accumulate,
                         col_scale=xp.unit)
 
@@ -1118,7 +1149,8 @@ class NMFBatchSolver:
                     # process: GEMMs accumulate straight into A / B (beta = 1)
                     accA, accB = (dA, dB) if dist else (A_, B_)
                     first = True
-                    wpl = None if exact else self.split_w(W)   # W changed in the last step
+                    self._layout_version = st.layout_version
+                    wpl = None if exact else self.w_planes(W)  # emitted by the last W-solve
                     for (a, b) in blocks:
                         cw = b - a
                         if cw <= 0:
@@ -1127,6 +1159,10 @@ class NMFBatchSolver:
                         hcols = HT[:, a:b]                               # (rows, cw) strided
                         h_old = hcols.clone() if exact else None
                         numerT = self.numer_gemm(W, wpl, a, b)   # ONE GEMM, every K
+                        # the H-solve epilogue writes the usages' bf16 planes for the
+                        # statistics GEMM (no separate split pass), unless unaligned
+                        hpl, _ = (None, None) if (exact or a % 8) else \
+                            self.solve_planes("h", rows, b - a)
                         for g in groups:
                             ga = active[g.pos]
                             WWT = ops.gram(g.rep3(W), out=g.gram3(wwt_buf), active=ga)
@@ -1134,7 +1170,8 @@ class NMFBatchSolver:
                                          max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
                                          l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
                                          iters_out=h_it[g.pos], conv_mode=cmode,
-                                         check_every=o.inner_check_every, active=ga)
+                                         check_every=o.inner_check_every, active=ga,
+                                         planes=None if hpl is None else hpl[:, g.rows])
                         if exact:
                             # replace the chunk's old contribution: d = h_new - h_old
                             for g in groups:
@@ -1149,12 +1186,14 @@ class NMFBatchSolver:
                             accB.addmm_(hlhs, xc, beta=0.0 if (dist and first) else 1.0)
                         else:
                             if (dist and first) or (not dist and pass_first):
-                                self.stats_gemm(accB, HT, a, b, False)  # B = h^T x, every K
+                                self.stats_gemm(accB, HT, a, b, False,   # B = h^T x, every K
+                                                presplit=hpl is not None)
                                 for g in groups:                       # A = h^T h
                                     ops.gram(g.rep3(hcols), out=g.gram3(accA),
                                              active=None if dist else active[g.pos])
                             else:
-                                self.stats_gemm(accB, HT, a, b, True)   # B += h^T x
+                                self.stats_gemm(accB, HT, a, b, True,   # B += h^T x
+                                                presplit=hpl is not None)
                                 for g in groups:                       # A += h^T h
                                     ops.gram(g.rep3(hcols), out=g.gram3(accA),
                                              accumulate=True, active=active[g.pos])
@@ -1167,6 +1206,7 @@ class NMFBatchSolver:
                         B_ += dB
                         A_ += dA
                     last = s_ == len(steps) - 1
+                    wpl_out, unit = (None, None) if exact else self.solve_planes("w", rows)
                     for g in groups:
                         _inner_solve(algo, g.rep3(W), g.rep3(B_), g.gram3(A_),
                                      max_iter=o.online_chunk_max_iter, tol=o.online_w_tol,
@@ -1174,7 +1214,11 @@ class NMFBatchSolver:
                                      lin_out=lin[g.pos] if last else None,
                                      quad_out=quad[g.pos] if last else None,
                                      iters_out=w_it[g.pos], conv_mode=cmode,
-                                     check_every=o.inner_check_every, active=active[g.pos])
+                                     check_every=o.inner_check_every, active=active[g.pos],
+                                     planes=None if wpl_out is None else wpl_out[:, g.rows],
+                                     planes_colmul=unit)
+                    if wpl_out is not None:
+                        self._w_fresh = self._w_key(W)
                 ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
                                 n, pass_arg, o.tol, final=final)
 
@@ -1240,28 +1284,36 @@ class NMFBatchSolver:
                 wwt = torch.empty(sq, device=dev, dtype=dt)
             HT, W = st.views()
             active = st.active_mask()
+            self._layout_version = st.layout_version
             # H-step over all local cells: one numerator GEMM for every K
-            numerT = self.numer_gemm(W, self.split_w(W), 0, N)
+            numerT = self.numer_gemm(W, self.w_planes(W), 0, N)
             nsplit = 1 if inner else max(1, (N + 8191) // 8192)
+            hpl, _ = self.solve_planes("h", rows, N)
             for g in st.groups:
                 WWT = ops.gram(g.rep3(W), out=g.gram3(wwt), active=active[g.pos])
                 _inner_solve(o.algo, g.rep3(HT), g.rep3(numerT), WWT,
                              max_iter=h_iter, tol=h_tol, l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
                              nsplit=nsplit, active=active[g.pos],
-                             iters_out=st.h_iters[g.pos])
+                             iters_out=st.h_iters[g.pos],
+                             planes=None if hpl is None else hpl[:, g.rows])
             del numerT
             # W-step from the new H
-            self.stats_gemm(B, HT, 0, N, accumulate=False)
+            self.stats_gemm(B, HT, 0, N, accumulate=False, presplit=hpl is not None)
             for g in st.groups:
                 ops.gram(g.rep3(HT), out=g.gram3(A))
             comm.allreduce_(flat)
             check = (it + 1) % every == 0 or it + 1 == max_it
+            wpl_out, unit = self.solve_planes("w", rows)
             for g in st.groups:
                 _inner_solve(o.algo, g.rep3(W), g.rep3(B), g.gram3(A),
                              max_iter=h_iter, tol=h_tol, l1_den=o.l1_W, l2=o.l2_W, eps=o.eps,
                              lin_out=lin[g.pos] if check else None,
                              quad_out=quad[g.pos] if check else None,
-                             active=active[g.pos], iters_out=st.w_iters[g.pos])
+                             active=active[g.pos], iters_out=st.w_iters[g.pos],
+                             planes=None if wpl_out is None else wpl_out[:, g.rows],
+                             planes_colmul=unit)
+            if wpl_out is not None:
+                self._w_fresh = self._w_key(W)
             if check:
                 ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
                                 n, it + 1, o.tol, final=(it + 1 == max_it))

@@ -89,7 +89,8 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           lin_out: torch.Tensor | None = None, quad_out: torch.Tensor | None = None,
           iters_out: torch.Tensor | None = None, nsplit: int = 1, conv_mode: int = 0,
           check_every: int = 10, variant: str = "auto",
-          active: torch.Tensor | None = None, coop: int | str = "auto") -> None:
+          active: torch.Tensor | None = None, coop: int | str = "auto",
+          planes: torch.Tensor | None = None, planes_colmul: torch.Tensor | None = None) -> None:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -103,13 +104,19 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     converging as a unit (cross-workgroup deterministic reductions, see coop_sum2 in
     solve.hip); "auto" picks S so that all S*nblocks workgroups are co-resident on the
     256 CUs, 1 disables.  Results are independent of S up to fp32 summation order.
+    ``planes`` (3, R*K, cols_pad) int16, optional: the kernel's epilogue also writes the
+    final x (times ``planes_colmul`` per column) as exact bf16 planes -- the A operand of
+    the next split-precision GEMM (ops.gemm_planes) -- zeroing columns [n, cols_pad).
     """
     a = ALGOS[algo]
     R, K, n = x.shape
     if not use_native(x):
-        return reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
-                               eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every,
-                               active)
+        reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
+                        eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every,
+                        active)
+        if planes is not None:
+            split_planes(x.reshape(R * K, n), planes, col_mul=planes_colmul)
+        return
     h = _hip
     # a GPU operand the kernels do not cover is an error, never a silent eager fallback:
     # fp32 only; K in 1..32 or a padded wide rank (the engine pads K <= 64 to a multiple
@@ -169,6 +176,18 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                                        ws["flag"].data_ptr())
     else:
         gen = 0
+    pl_ptr = pl_rs = pl_ld = pl_plane = pl_cols = 0
+    if planes is not None:
+        if (planes.dtype != torch.int16 or planes.dim() != 3 or planes.shape[0] != 3
+                or planes.shape[1] < R * K or planes.stride(2) != 1 or planes.shape[2] < n
+                or planes.device != x.device):
+            raise ValueError("planes: int16 (3, >= R*K, >= n) with unit column stride")
+        if planes_colmul is not None and (planes_colmul.dtype != torch.float32
+                                          or planes_colmul.numel() < n
+                                          or not planes_colmul.is_contiguous()):
+            raise ValueError("planes_colmul: contiguous float32 with >= n entries")
+        pl_ptr, pl_ld, pl_plane = planes.data_ptr(), planes.stride(1), planes.stride(0)
+        pl_rs, pl_cols = K * pl_ld, planes.shape[2]
     h.solve(a, K, x.data_ptr(), x.stride(0), x.stride(1), numer.data_ptr(), numer.stride(0),
             numer.stride(1), gram.data_ptr(), K * K, ri, nblocks, n, int(max_iter), float(tol),
             float(l1_num), float(l1_den), float(l2), float(eps),
@@ -178,7 +197,9 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             int(conv_mode), int(check_every), int(threads),
             {"auto": 0, "stream": 1, "reg": 2}[variant],
             active.data_ptr() if active is not None else 0, int(S), ws_slots, ws_count,
-            int(gen), int(epochs), ws_flag, _stream_ptr(x))
+            int(gen), int(epochs), ws_flag, pl_ptr, int(pl_rs), int(pl_ld), int(pl_plane),
+            planes_colmul.data_ptr() if (planes is not None and planes_colmul is not None) else 0,
+            int(pl_cols), _stream_ptr(x))
 
 
 # Cooperative-split bookkeeping.  A launch of S*nblocks 1024-thread workgroups is only safe
@@ -759,14 +780,26 @@ def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
         return -(-M // tm) * -(-N // tn)
 
     # measured on MI355X (profiles/r2_gemm_planes_sweep.log): 128x256 tiles win once they
-    # alone fill the chip; below that 128x128 tiles with a k split
-    v = int(v_env) if v_env is not None else (1 if tiles(1) >= cus else 0)
+    # alone fill the chip; 64x128 tiles when those give two workgroups per CU without a
+    # k split (no reduction pass); 128x256 with a k split for few, long tiles; and for a
+    # few rows (the tail passes) 128x128 tiles with a deep k split
+    target = cus
+    if v_env is not None:
+        v = int(v_env)
+    elif tiles(1) >= cus:
+        v = 1
+    elif tiles(3) >= 2 * cus:
+        v = 3
+    elif M > 128:
+        v = 1
+    else:
+        v, target = 0, 2 * cus
     ksplit = 1
     if k_env is not None:
         ksplit = int(k_env)
     else:
         t = tiles(v)
-        while t * ksplit < 2 * cus and nk // (2 * ksplit) >= 4:
+        while t * ksplit < target and nk // (2 * ksplit) >= 4:
             ksplit *= 2
     return v, max(1, min(ksplit, nk))
 

@@ -15,7 +15,9 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       int check_every, int threads, int variant, const int* active,
                       int coop_split, float* coop_slots, unsigned long long* coop_count,
                       unsigned coop_gen, int coop_epochs,
-                      int* coop_timeout, hipStream_t stream);
+                      int* coop_timeout, unsigned short* planes, long long pl_rs,
+                      long long pl_ld, long long pl_plane, const float* pl_colmul,
+                      int pl_cols, hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,

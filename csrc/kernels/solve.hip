@@ -32,6 +32,8 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  const int* active, int coop_split, float* coop_slots,
                                  unsigned long long* coop_count, unsigned coop_gen,
                                  int coop_epochs, int* coop_timeout,
+                                 unsigned short* planes, long long pl_rs, long long pl_ld,
+                                 long long pl_plane, const float* pl_colmul, int pl_cols,
                                  hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
@@ -54,6 +56,9 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.coop_epochs = coop_epochs;
   p.coop_timeout = coop_timeout;
   p.coop_epochs_split = coop_split > 1 ? coop_split : 1;
+  p.planes = planes; p.pl_rs = pl_rs; p.pl_ld = pl_ld; p.pl_plane = pl_plane;
+  p.pl_colmul = pl_colmul; p.pl_cols = pl_cols;
+  if (planes && pl_cols < ncols) return hipErrorInvalidValue;
   if (coop_split > 1 && nsplit > 1) return hipErrorInvalidValue;
   if (!cnmf_solve_native_k(K)) return hipErrorInvalidValue;
   if (K > 32) return cnmf::launch_solve_wide(K, algo, p, nblocks, threads, stream);

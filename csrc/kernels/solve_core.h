@@ -199,6 +199,42 @@ __device__ __forceinline__ bool coop_sum2(const SolveParams& p, int rep, int e, 
   return good;
 }
 
+__device__ __forceinline__ unsigned short solve_f2bf_rn(float f) {
+  unsigned u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+// Final x of this block's columns [j0, n) as three exact bf16 planes (x = hi + mid + lo,
+// each residual exact in fp32), times pl_colmul; the last slice also zeroes the GEMM's
+// k padding [ncols, pl_cols).  Reads x back from L2 (just stored by this block).
+template <int K>
+__device__ __forceinline__ void emit_planes(const SolveParams& p, int rep, int j0, int n,
+                                            bool last_slice) {
+  const float* __restrict__ x = p.x + (long long)rep * p.x_rs;
+  unsigned short* __restrict__ pl = p.planes + (long long)rep * p.pl_rs;
+  // this block's columns [j0, n), then (last slice only) the padding [ncols, pl_cols)
+  const int pad = last_slice ? max(0, p.pl_cols - p.ncols) : 0;
+  const int span = (n - j0) + pad;
+  for (int i = threadIdx.x; i < span; i += blockDim.x) {
+    const bool real = i < n - j0;
+    const int c = real ? j0 + i : p.ncols + (i - (n - j0));
+    const float m = (real && p.pl_colmul) ? p.pl_colmul[c] : 1.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float v = real ? x[(long long)k * p.ldx + c] * m : 0.f;
+      const unsigned short h0 = solve_f2bf_rn(v);
+      const float r1 = v - __uint_as_float((unsigned)h0 << 16);
+      const unsigned short h1 = solve_f2bf_rn(r1);
+      const float r2 = r1 - __uint_as_float((unsigned)h1 << 16);
+      const long long o = (long long)k * p.pl_ld + c;
+      pl[o] = h0;
+      pl[p.pl_plane + o] = h1;
+      pl[2 * p.pl_plane + o] = solve_f2bf_rn(r2);
+    }
+  }
+}
+
 // Row k of the padded LDS Gram into row[KP] (KP/4 broadcast b128 reads).
 #define CNMF_GRAM_ROW(GZ, k, row)                                                                 \
   float row[KP];                                                                                  \
@@ -517,6 +553,10 @@ __global__ __launch_bounds__(solve_block_threads<K>()) void solve_kernel(SolvePa
         }
       }
     }
+  }
+  if (p.planes) {
+    __syncthreads();   // every thread's final x stores precede the re-read (same block)
+    emit_planes<K>(p, rep, j0, n, gridDim.y <= 1 || blockIdx.y == gridDim.y - 1);
   }
   if (p.iters_out && threadIdx.x == 0 && blockIdx.y == 0) p.iters_out[rep] += it;
 }

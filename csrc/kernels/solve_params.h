@@ -33,6 +33,13 @@ struct SolveParams {
   int coop_epochs;
   int* coop_timeout;        // set to 1 if a spin gave up (residency violated)
   int coop_epochs_split;    // launch-side: S (gridDim.y) for the cooperative split
+  // Optional epilogue feeding the split-precision GEMM (gemm_planes.hip): the final x
+  // times pl_colmul[col] (optional) split exactly into three bf16 planes at
+  // planes + p*pl_plane + rep*pl_rs + k*pl_ld + col, columns [ncols, pl_cols) zeroed.
+  unsigned short* planes;
+  long long pl_rs, pl_ld, pl_plane;
+  const float* pl_colmul;
+  int pl_cols;
 };
 
 }  // namespace cnmf

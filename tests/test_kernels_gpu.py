@@ -906,3 +906,23 @@ def test_cluster_medians_device_matches_pandas():
     ref = pd.DataFrame(S).groupby(lab).median()
     ref = ref.div(ref.sum(axis=1), axis=0).values
     np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.parametrize("coop,nsplit", [(1, 1), ("auto", 1), (1, 3)])
+@pytest.mark.parametrize("K", [6, 10, 40])
+def test_solve_planes_epilogue_equals_split_of_result(coop, nsplit, K):
+    """The solve epilogue's bf16 planes (fused A-operand split for the next GEMM) are
+    bit-identical to ops.split_planes of the final x, times the column multiplier, with
+    the k padding zeroed."""
+    R, n = 4, 5000
+    x0, numer, gram = _problem(R, K, n, seed=K + 7)
+    x = x0.clone().cuda()
+    pad = -(-n // 32) * 32 + 32
+    planes = torch.full((3, R * K, pad), 77, dtype=torch.int16, device="cuda")
+    colmul = (torch.rand(n) + 0.5).cuda()
+    kw = dict(max_iter=1 if nsplit > 1 else 30, tol=-1.0 if nsplit > 1 else 1e-3,
+              nsplit=nsplit, coop=coop)
+    ops.solve("mu", x, numer.cuda(), gram.cuda(), planes=planes, planes_colmul=colmul, **kw)
+    ref = torch.zeros((3, R * K, pad), dtype=torch.int16, device="cuda")
+    ops.split_planes(x.reshape(R * K, n), ref, col_mul=colmul)
+    assert torch.equal(planes, ref)
