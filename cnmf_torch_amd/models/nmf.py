@@ -44,6 +44,7 @@ decision are identical on all ranks while H rows stay rank-local.
 """
 from __future__ import annotations
 
+import itertools
 import math
 import os
 import time
@@ -291,6 +292,9 @@ def _to_device(a: np.ndarray, dev: torch.device) -> torch.Tensor:
     return t
 
 
+_BATCH_UIDS = itertools.count()
+
+
 def _ranges(starts: np.ndarray, sizes: np.ndarray) -> np.ndarray:
     """Concatenation of ``arange(s, s + n)`` over the (start, size) pairs."""
     starts = np.asarray(starts, dtype=np.int64)
@@ -363,6 +367,7 @@ class _Batch:
         self.h_iters = torch.zeros(R, dtype=torch.int32, device=dev)
         self.w_iters = torch.zeros(R, dtype=torch.int32, device=dev)
         self.layout_version = 0   # bumped by compact(): captured graphs key on it
+        self.uid = next(_BATCH_UIDS)   # never reused (unlike id()): plane-cache keys
         self.bucket = max(1, int(os.environ.get("CNMF_COMPACT_BUCKET",
                                                 "8" if W.device.type == "cuda" else "1")))
         self.A = None   # flat per-position K*K sufficient statistics (online 'exact' mode)
@@ -632,12 +637,12 @@ def _count_units(X: torch.Tensor, stats=None):
     if N == 0:
         return None
     mn_t, _, neg = stats if stats is not None else ops.colstats(X)
-    empty_t = ~torch.isfinite(mn_t)
-    mn_t = torch.where(empty_t, torch.ones_like(mn_t), mn_t)
-    bad_t = ops.count_unit_check(X, mn_t)
+    bad_t = ops.count_unit_check(X, mn_t)     # skips empty columns (min_pos = inf)
     # one host round trip for the per-gene decisions
-    host = torch.stack([mn_t.double(), bad_t.double(), neg.double(), empty_t.double()]).cpu().numpy()
-    mn, bad, neg_h, empty = host[0], host[1].astype(np.int64), host[2] != 0, host[3] != 0
+    host = torch.stack([mn_t.double(), bad_t.double(), neg.double()]).cpu().numpy()
+    mn, bad, neg_h = host[0], host[1].astype(np.int64), host[2] != 0
+    empty = ~np.isfinite(mn)
+    mn = np.where(empty, 1.0, mn)
     if neg_h.any():
         return None
     inv = (~bad) & 0xFF                         # bit d-1 set: d works
@@ -683,7 +688,11 @@ class _XPlanes:
             for a in range(0, N, 1 << 16):
                 torch.round(X[a:a + (1 << 16)] / unit, out=C[a:a + (1 << 16)])
             cmax = float(C.max()) if C.numel() else 0.0
+            # integers 0..256 are exact in one bf16 plane, 0..65535 in two (hi + the
+            # exact residual): the split below is lossless by construction
             self.pb = 1 if cmax <= 256 else 2
+            if cmax >= 65536:
+                unit, C, self.pb = None, X, 3
         else:
             C, self.pb = X, 3
         self.unit = unit
@@ -695,12 +704,6 @@ class _XPlanes:
         for a in range(0, N, 1 << 16):
             blk = C[a:a + (1 << 16)].t().contiguous()          # (G, cells of the block)
             ops.split_planes(blk, self.xt[:, :, a:a + -(-blk.shape[1] // 4) * 4])
-        if unit is not None and self.pb < 3:
-            # the planes must hold the counts exactly
-            from ..ops import reference as _ref
-            back = _ref.planes_to_f64(self.x[:, :N, :G]).sum(0)
-            if not torch.equal(back, C.to(torch.float64)):
-                raise RuntimeError("integer planes are not exact")
         del C
 
     @staticmethod
@@ -779,6 +782,7 @@ class NMFBatchSolver:
         self._mean_x = None
         self._xp = False            # split-GEMM planes of X: False = not built yet
         self._ws: dict = {}
+        self._w_fresh: dict = {}    # stream -> key of the W its "w" planes hold
 
     # ------------------------------------------------------------------ public
     def run(self, seeds, HT0=None, W0=None, ks=None) -> NMFResult:
@@ -904,7 +908,11 @@ class NMFBatchSolver:
             self._ws[key] = buf
         return buf
 
-    def split_w(self, W: torch.Tensor):
+    def _stream_key(self):
+        return torch.cuda.current_stream(self.X.device).cuda_stream \
+            if self.X.device.type == "cuda" else None
+
+    def split_w(self, W: torch.Tensor, st: "_Batch"):
         """Planes of the spectra (times the count unit) for numer_gemm; call after every
         change of W that the W-solve epilogue did not emit (init, compaction)."""
         xp = self._planes()
@@ -912,21 +920,27 @@ class NMFBatchSolver:
             return None
         wpl = self._plane_buf("w", W.shape[0], xp.Gp)
         ops.split_planes(W, wpl[:, :W.shape[0]], col_mul=xp.unit)
-        self._w_fresh = self._w_key(W)
+        self.mark_w_fresh(W, st)
         return wpl
 
-    def _w_key(self, W: torch.Tensor):
-        return (W.data_ptr(), W.shape[0], getattr(self, "_layout_version", None))
+    def mark_w_fresh(self, W: torch.Tensor, st: "_Batch") -> None:
+        """The current stream's "w" planes hold W of batch ``st`` at its current layout.
+        Kept per stream (run_concurrent solves batches on several host threads, and a
+        HIP-graph capture runs on a stream of its own whose buffer eager passes never
+        wrote)."""
+        self._w_fresh[self._stream_key()] = (W.data_ptr(), W.shape[0], st.uid,
+                                             st.layout_version)
 
-    def w_planes(self, W: torch.Tensor):
+    def w_planes(self, W: torch.Tensor, st: "_Batch"):
         """The spectra planes, split only when the W-solve epilogue has not already
         written them for this W buffer / layout (solve(planes=...) below)."""
         xp = self._planes()
         if xp is None:
             return None
-        if getattr(self, "_w_fresh", None) == self._w_key(W):
+        if self._w_fresh.get(self._stream_key()) == (W.data_ptr(), W.shape[0], st.uid,
+                                                     st.layout_version):
             return self._plane_buf("w", W.shape[0], xp.Gp)
-        return self.split_w(W)
+        return self.split_w(W, st)
 
     def solve_planes(self, kind: str, rows: int, cols: int | None = None):
         """(planes buffer, column multiplier) a solve epilogue writes for the next GEMM:
@@ -946,7 +960,8 @@ class NMFBatchSolver:
         if xp is None or wpl is None:
             return W @ self.X[a:b].t()
         out = torch.empty((W.shape[0], b - a), device=W.device, dtype=W.dtype)
-        ops.gemm_planes(out, wpl, xp.x[:, a:], W.shape[0], b - a, xp.Gp)
+        ops.gemm_planes(out, wpl[:ops.gemm_a_planes(xp.Gp)], xp.x[:, a:], W.shape[0], b - a,
+                        xp.Gp)
         return out
 
     def stats_gemm(self, B: torch.Tensor, HT: torch.Tensor, a: int, b: int,
@@ -963,8 +978,8 @@ class NMFBatchSolver:
         hpl = self._plane_buf("h", HT.shape[0], kd)
         if not presplit:
             ops.split_planes(HT[:, a:b], hpl[:, :HT.shape[0]])
-        ops.gemm_planes(B, hpl, xp.xt[:, :, a:], HT.shape[0], xp.G, kd, accumulate=accumulate,
-                        col_scale=xp.unit)
+        ops.gemm_planes(B, hpl[:ops.gemm_a_planes(kd)], xp.xt[:, :, a:], HT.shape[0], xp.G, kd,
+                        accumulate=accumulate, col_scale=xp.unit)
 
     def _mean(self) -> float:
         """Global mean of X (random init scale), one pass per solver."""
@@ -1149,8 +1164,7 @@ class NMFBatchSolver:
                     # process: GEMMs accumulate straight into A / B (beta = 1)
                     accA, accB = (dA, dB) if dist else (A_, B_)
                     first = True
-                    self._layout_version = st.layout_version
-                    wpl = None if exact else self.w_planes(W)  # emitted by the last W-solve
+                    wpl = None if exact else self.w_planes(W, st)  # the last W-solve's
                     for (a, b) in blocks:
                         cw = b - a
                         if cw <= 0:
@@ -1218,7 +1232,7 @@ class NMFBatchSolver:
                                      planes=None if wpl_out is None else wpl_out[:, g.rows],
                                      planes_colmul=unit)
                     if wpl_out is not None:
-                        self._w_fresh = self._w_key(W)
+                        self.mark_w_fresh(W, st)
                 ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
                                 n, pass_arg, o.tol, final=final)
 
@@ -1238,6 +1252,9 @@ class NMFBatchSolver:
                         graphs, graph = False, None
                 if graph is not None:
                     graph.replay()
+                    # the replay's W-solves wrote the capture stream's planes: this
+                    # stream's copy now holds an older W
+                    self._w_fresh.pop(self._stream_key(), None)
                 else:
                     enqueue_pass(-1, final)
             else:
@@ -1284,9 +1301,8 @@ class NMFBatchSolver:
                 wwt = torch.empty(sq, device=dev, dtype=dt)
             HT, W = st.views()
             active = st.active_mask()
-            self._layout_version = st.layout_version
             # H-step over all local cells: one numerator GEMM for every K
-            numerT = self.numer_gemm(W, self.w_planes(W), 0, N)
+            numerT = self.numer_gemm(W, self.w_planes(W, st), 0, N)
             nsplit = 1 if inner else max(1, (N + 8191) // 8192)
             hpl, _ = self.solve_planes("h", rows, N)
             for g in st.groups:
@@ -1313,7 +1329,7 @@ class NMFBatchSolver:
                              planes=None if wpl_out is None else wpl_out[:, g.rows],
                              planes_colmul=unit)
             if wpl_out is not None:
-                self._w_fresh = self._w_key(W)
+                self.mark_w_fresh(W, st)
             if check:
                 ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
                                 n, it + 1, o.tol, final=(it + 1 == max_it))

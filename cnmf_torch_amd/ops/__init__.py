@@ -104,6 +104,9 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     converging as a unit (cross-workgroup deterministic reductions, see coop_sum2 in
     solve.hip); "auto" picks S so that all S*nblocks workgroups are co-resident on the
     256 CUs, 1 disables.  Results are independent of S up to fp32 summation order.
+    ``variant``: "auto" runs MU with K <= 16 on the matrix-core kernel (solve_mfma.hip:
+    Gram x on v_mfma_f32_16x16x4_f32, iterate in VGPRs) whenever its slices fit, else
+    the VALU kernels ("stream" / "reg" force those; "mfma" forces the former).
     ``planes`` (3, R*K, cols_pad) int16, optional: the kernel's epilogue also writes the
     final x (times ``planes_colmul`` per column) as exact bf16 planes -- the A operand of
     the next split-precision GEMM (ops.gemm_planes) -- zeroing columns [n, cols_pad).
@@ -152,11 +155,25 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
         for t in (lin_out, quad_out):
             if t is not None:
                 t.zero_()
-    S = 1
-    if nsplit <= 1:
-        S = _coop_split(n, nblocks, x.device) if coop == "auto" else max(1, int(coop))
-    if S > 1 and nblocks * S > _coop_resident(x.device):
-        raise ValueError(f"coop={S} x {nblocks} blocks exceeds co-resident workgroups")
+    # matrix-core variant (csrc/kernels/solve_mfma.hip): MU with K <= 16 whenever every
+    # slice fits one 256-thread workgroup's register tiles; four of its workgroups are
+    # co-resident per CU, so its cooperative budget is 4x the 1024-thread one
+    S = None
+    if variant in ("auto", "mfma") and a == 0 and h.solve_mfma_max_cols(K) > 0 \
+            and os.environ.get("CNMF_SOLVE_MFMA", "1") != "0":
+        S = _mfma_split(n, nblocks, K, nsplit, coop, x.device)
+    if S is not None:
+        vcode = 3
+    elif variant == "mfma":
+        raise ValueError(f"solve: variant 'mfma' does not cover algo={algo} K={K} n={n} "
+                         f"with {nblocks} replicates")
+    else:
+        vcode = {"auto": 0, "stream": 1, "reg": 2}[variant]
+        S = 1
+        if nsplit <= 1:
+            S = _coop_split(n, nblocks, x.device) if coop == "auto" else max(1, int(coop))
+        if S > 1 and nblocks * S > _coop_resident(x.device):
+            raise ValueError(f"coop={S} x {nblocks} blocks exceeds co-resident workgroups")
     n_slice = (n + S - 1) // S
     threads = min(h.solve_max_threads(K), max(64, ((min(n_slice, 4096 * 4) + 63) // 64) * 64))
     ws_slots = ws_count = ws_flag = 0
@@ -165,15 +182,14 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
         epochs = (max_iter // max(1, check_every) + 3) if conv_mode == 1 else (max_iter + 2)
         ws = _coop_workspace(x.device, _stream_ptr(x), R, epochs, S)
         if torch.cuda.is_current_stream_capturing():
-            # a graph replays fixed arguments: zero the counters in the graph and use a
-            # generation eager launches never reach
-            ws["count"][: R * epochs].zero_()
+            # a graph replays fixed arguments: zero this launch's granules in the graph
+            # and tag them with a generation eager launches never reach
+            ws["slots"][: R * epochs * S * 2].zero_()
             gen = 0xFFFFFFFF
         else:
             ws["gen"] += 1                  # tags this launch's arrivals: no zeroing
             gen = ws["gen"]
-        ws_slots, ws_count, ws_flag = (ws["slots"].data_ptr(), ws["count"].data_ptr(),
-                                       ws["flag"].data_ptr())
+        ws_slots, ws_count, ws_flag = ws["slots"].data_ptr(), 0, ws["flag"].data_ptr()
     else:
         gen = 0
     pl_ptr = pl_rs = pl_ld = pl_plane = pl_cols = 0
@@ -194,8 +210,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             lin_out.data_ptr() if lin_out is not None else 0,
             quad_out.data_ptr() if quad_out is not None else 0,
             iters_out.data_ptr() if iters_out is not None else 0, int(max(1, nsplit)),
-            int(conv_mode), int(check_every), int(threads),
-            {"auto": 0, "stream": 1, "reg": 2}[variant],
+            int(conv_mode), int(check_every), int(threads), vcode,
             active.data_ptr() if active is not None else 0, int(S), ws_slots, ws_count,
             int(gen), int(epochs), ws_flag, pl_ptr, int(pl_rs), int(pl_ld), int(pl_plane),
             planes_colmul.data_ptr() if (planes is not None and planes_colmul is not None) else 0,
@@ -234,7 +249,10 @@ def coop_prepare(dev: torch.device) -> None:
 def _coop_resident(dev: torch.device) -> int:
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     if key not in _COOP_RESIDENT:
-        cus = torch.cuda.get_device_properties(key).multi_processor_count
+        # the HIP attribute, not torch.cuda.get_device_properties: its first call
+        # initialises amdsmi (~26 ms inside the first factorize)
+        cus = _hip.cu_count(key) if _hip is not None else \
+            torch.cuda.get_device_properties(key).multi_processor_count
         _COOP_RESIDENT[key] = max(1, cus - 16)
     return max(1, _COOP_RESIDENT[key] // getattr(_TLS, "share", 1))
 
@@ -246,17 +264,42 @@ def _coop_split(n: int, nblocks: int, dev: torch.device) -> int:
     return max(1, min(want, _coop_resident(dev) // max(1, nblocks), 16))
 
 
+MFMA_WG_PER_CU = 4          # solve_mfma.hip: <= 128 VGPRs and <= 37 KB LDS per workgroup
+
+
+def _mfma_split(n: int, nblocks: int, K: int, nsplit: int, coop, dev: torch.device):
+    """Slices per replicate for the matrix-core solve, or None when it cannot run: with
+    nsplit > 1 the caller's slices must each fit a workgroup; otherwise S cooperative
+    slices (all co-resident) -- at least enough for the tiles, then more while the
+    budget allows so the grid fills the chip, up to ~256 columns per slice."""
+    cap = _hip.solve_mfma_max_cols(K)
+    if nsplit > 1:   # fixed-step column split: no cooperative slices
+        return 1 if -(-n // nsplit) <= cap else None
+    s_min = -(-n // cap)
+    if coop != "auto":
+        S = max(1, int(coop))
+        return S if S >= s_min and (S == 1 or nblocks * S <= MFMA_WG_PER_CU *
+                                    _coop_resident(dev)) else None
+    if s_min > 1 and os.environ.get("CNMF_SOLVE_COOP") == "0":
+        return None
+    budget = MFMA_WG_PER_CU * _coop_resident(dev)
+    if nblocks * s_min > budget and s_min > 1:
+        return None
+    S = max(s_min, min(budget // max(1, nblocks), -(-n // 256), 32))
+    return max(1, S)
+
+
 def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int) -> dict:
-    """Per-(device, stream) scratch: slots [R*epochs*S*2] f32, generation-tagged arrival
-    counters [R*epochs] (int64, zeroed once at allocation), the launch generation and the
-    timeout flag.  Reused across launches on the same stream (stream order serialises)."""
+    """Per-(device, stream) scratch: {generation, value} granules [R*epochs*S*2] (int64,
+    zeroed once at allocation; coop_sum2 in csrc/kernels/solve_core.h), the launch
+    generation and the timeout flag.  Reused across launches on the same stream (stream
+    order serialises); the generation only grows, so granules need no re-zeroing."""
     key = (str(dev), stream)
     ws = _COOP_WS.get(key)
-    need_slots, need_count = R * epochs * S * 2, R * epochs
-    if ws is None or ws["slots"].numel() < need_slots or ws["count"].numel() < need_count:
+    need_slots = R * epochs * S * 2
+    if ws is None or ws["slots"].numel() < need_slots:
         flag = ws["flag"] if ws is not None else torch.zeros(1, dtype=torch.int32, device=dev)
-        ws = {"slots": torch.empty(max(need_slots, 1 << 16), dtype=torch.float32, device=dev),
-              "count": torch.zeros(max(need_count, 1 << 14), dtype=torch.int64, device=dev),
+        ws = {"slots": torch.zeros(max(need_slots, 1 << 16), dtype=torch.int64, device=dev),
               "gen": ws["gen"] if ws is not None else 0,
               "flag": flag}
         _COOP_WS[key] = ws
@@ -767,6 +810,17 @@ _GEMM_TILES = {0: (128, 128), 1: (128, 256), 2: (256, 128), 3: (64, 128)}
 _GEMM_SLAB: dict = {}
 
 
+def gemm_a_planes(Kd: int) -> int:
+    """A planes the engine's split GEMMs use for a reduction of length Kd: 2 (hi + mid,
+    representation error <= 2^-16 relative) once Kd >= 1024 -- that bound is inside the
+    fp32 GEMM's own n * 2^-24 bound from n = 256 on, and from ~1000 on the measured error
+    is also below the fp32 library GEMM's (test_gemm_two_a_planes_within_fp32_library_error)
+    -- else 3 (exact).  CNMF_GEMM_APLANES=3 forces exact."""
+    if Kd < 1024 or os.environ.get("CNMF_GEMM_APLANES", "2") == "3":
+        return 3
+    return 2
+
+
 def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
     """(tile variant, k split) for an M x N x Kd split GEMM: the largest tile that still
     gives every CU a workgroup, else k-split slices (deterministic slab reduction) until
@@ -838,7 +892,8 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
                 accumulate: bool = False, col_scale: torch.Tensor | None = None) -> None:
     """C[:M, :N] (+)= col_scale * sum_{i + j <= 2} A[i][:M, :Kd] . B[j][:N, :Kd]^T on the bf16
     matrix cores (gemm_planes.hip): the fp32-accurate product of the fp32 matrices whose
-    exact bf16 splits are A (3 planes) and B (1-3 planes; 1 or 2 when B holds integers).
+    exact bf16 splits are A (3 planes; or its first 2, see gemm_a_planes) and B (1-3
+    planes; 1 or 2 when B holds integers).
     A/B: int16 (P, rows, ld) views with unit k stride (row offsets / k offsets are just
     views); k must be zero-padded in A up to ``Kd`` (a multiple of planes_bk)."""
     pa, a_rows, _ = A.shape
@@ -850,7 +905,7 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
             raise ValueError(f"{name}: 16-byte aligned base required (k offset % 8 == 0)")
         if t.shape[2] < Kd:
             raise ValueError(f"{name}: k extent {t.shape[2]} < Kd {Kd}")
-    if pa != 3 or not 1 <= pb <= 3 or Kd % planes_bk(pb) or M > a_rows or N > b_rows:
+    if not 2 <= pa <= 3 or not 1 <= pb <= 3 or Kd % planes_bk(pb) or M > a_rows or N > b_rows:
         raise ValueError(f"gemm_planes: planes {pa}/{pb}, Kd {Kd}, M {M}/{a_rows}, N {N}/{b_rows}")
     if C.dtype != torch.float32 or C.stride(1) != 1 or C.shape[0] < M or C.shape[1] < N:
         raise ValueError("C: float32 (>= M, >= N) with unit column stride required")

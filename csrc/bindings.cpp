@@ -23,10 +23,17 @@ static T* P(uintptr_t v) { return reinterpret_cast<T*>(v); }
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "cnmf_torch_amd native HIP kernels (gfx950)";
 
+  m.def("cu_count", [](int dev) {
+    int v = 0;
+    check(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev),
+          "hipDeviceGetAttribute");
+    return v;
+  });
   m.def("solve_max_k", []() { return cnmf_solve_max_k(); });
   m.def("solve_max_threads", [](int K) { return cnmf_solve_max_threads(K); });
   m.def("solve_native_k", [](int K) { return cnmf_solve_native_k(K); });
   m.def("solve_reg_max_cols", [](int K) { return cnmf_solve_reg_max_cols(K); });
+  m.def("solve_mfma_max_cols", [](int K) { return cnmf_solve_mfma_max_cols(K); });
 
   m.def("solve",
         [](int algo, int K, uintptr_t x, long long x_rs, long long ldx, uintptr_t numer,

@@ -9,6 +9,11 @@
 //     C = sum over plane pairs (i, j) with i + j <= 2 of  A_i . B_j^T      (fp32 accumulate)
 //
 // reproduces the fp32 GEMM to fp32 rounding (the dropped pairs are < 2^-24 relative).
+// With TWO A planes (PA = 2: hi + mid, |v - hi - mid| <= 2^-16 |v|) the product error is
+// <= 2^-16 sum|a b| -- inside the standard fp32 GEMM bound n 2^-24 sum|a b| for every
+// reduction length n >= 256, and from n ~ 1000 on measured below hipBLASLt's fp32 GEMM
+// error (tests:
+// test_gemm_two_a_planes_within_fp32_library_error); the engine uses it for k >= 1024.
 // The cNMF data matrix is counts / per-gene std: with the per-gene unit folded into the
 // OTHER operand (A's columns for numer, C's columns for B) the count matrix is held
 // exactly by ONE bf16 plane (counts <= 256) or two (< 65536), so the product costs 3 (or
@@ -320,13 +325,13 @@ static hipError_t launch_gemm(PlaneGemmParams p, hipStream_t s) {
 
 // tile variants: 0 = 128x128 (4 waves), 1 = 128x256 (8 waves), 2 = 256x128 (8 waves),
 // 3 = 64x128 (2 waves)
-template <int PB, int BK>
+template <int PA, int PB, int BK>
 static hipError_t launch_variant(int v, const PlaneGemmParams& p, hipStream_t s) {
   switch (v) {
-    case 0: return launch_gemm<3, PB, BK, 2, 2>(p, s);
-    case 1: return launch_gemm<3, PB, BK, 2, 4>(p, s);
-    case 2: return launch_gemm<3, PB, BK, 4, 2>(p, s);
-    default: return launch_gemm<3, PB, BK, 1, 2>(p, s);
+    case 0: return launch_gemm<PA, PB, BK, 2, 2>(p, s);
+    case 1: return launch_gemm<PA, PB, BK, 2, 4>(p, s);
+    case 2: return launch_gemm<PA, PB, BK, 4, 2>(p, s);
+    default: return launch_gemm<PA, PB, BK, 1, 2>(p, s);
   }
 }
 
@@ -348,7 +353,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
                                        float* slab, hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
   const int bk = cnmf_gemm_planes_bk(pb);
-  if (pa != 3 || pb < 1 || pb > 3 || Kd <= 0 || Kd % bk || lda % 8 || ldb % 8 ||
+  if (pa < 2 || pa > 3 || pb < 1 || pb > 3 || Kd <= 0 || Kd % bk || lda % 8 || ldb % 8 ||
       a_plane % 8 || b_plane % 8 || a_rows < 1 || b_rows < 1 || variant < 0 || variant > 3 ||
       ksplit < 1 || ksplit > Kd / bk || (ksplit > 1 && !slab))
     return hipErrorInvalidValue;
@@ -359,10 +364,13 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   p.M = M; p.N = N; p.Kd = Kd; p.accumulate = accumulate;
   p.ksplit = ksplit; p.slab = slab;
   hipError_t e;
-  switch (pb) {
-    case 1: e = cnmf::launch_variant<1, 32>(variant, p, stream); break;
-    case 2: e = cnmf::launch_variant<2, 32>(variant, p, stream); break;
-    default: e = cnmf::launch_variant<3, 32>(variant, p, stream); break;
+  switch (pa * 4 + pb) {
+    case 9: e = cnmf::launch_variant<2, 1, 32>(variant, p, stream); break;
+    case 10: e = cnmf::launch_variant<2, 2, 32>(variant, p, stream); break;
+    case 11: e = cnmf::launch_variant<2, 3, 32>(variant, p, stream); break;
+    case 13: e = cnmf::launch_variant<3, 1, 32>(variant, p, stream); break;
+    case 14: e = cnmf::launch_variant<3, 2, 32>(variant, p, stream); break;
+    default: e = cnmf::launch_variant<3, 3, 32>(variant, p, stream); break;
   }
   if (e != hipSuccess || ksplit == 1) return e;
   const long long total = (long long)M * N;

@@ -24,6 +24,7 @@ hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, do
                             int* n_pass, int n, int pass, double tol, int final_pass,
                             int init, hipStream_t stream);
 int cnmf_solve_reg_max_cols(int K);
+int cnmf_solve_mfma_max_cols(int K);
 
 int cnmf_beta_max_k();
 hipError_t cnmf_beta_contract(int side, int mode, const float* X, long long ldx, const float* HT,

@@ -10,6 +10,7 @@ hipError_t launch_solve_stream(int K, int algo, const SolveParams& p, int nblock
 }  // namespace cnmf
 
 extern "C" int cnmf_solve_max_k() { return 64; }
+extern "C" int cnmf_solve_mfma_max_cols(int K);
 
 // ranks the kernels are instantiated for: 1..32 and the padded wide ranks 40..64
 extern "C" int cnmf_solve_native_k(int K) {
@@ -50,8 +51,8 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.conv_mode = conv_mode;
   p.check_every = check_every;
   p.active = active;
-  p.coop_slots = coop_split > 1 ? coop_slots : nullptr;
-  p.coop_count = coop_count;
+  p.coop_slots = coop_split > 1 ? (unsigned long long*)coop_slots : nullptr;
+  (void)coop_count;   // unused since the granule exchange (kept in the C ABI)
   p.coop_gen = coop_gen;
   p.coop_epochs = coop_epochs;
   p.coop_timeout = coop_timeout;
@@ -60,9 +61,19 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.pl_colmul = pl_colmul; p.pl_cols = pl_cols;
   if (planes && pl_cols < ncols) return hipErrorInvalidValue;
   if (coop_split > 1 && nsplit > 1) return hipErrorInvalidValue;
+  if (coop_split > cnmf::kCoopMaxSlices) return hipErrorInvalidValue;
   if (!cnmf_solve_native_k(K)) return hipErrorInvalidValue;
+  if (variant == 3) {
+    // matrix-core variant (solve_mfma.hip): MU, K <= 16, every slice within one
+    // workgroup's tiles; the host picks the slicing (ops.solve / _mfma_split)
+    const int parts = nsplit > 1 ? nsplit : (coop_split > 1 ? coop_split : 1);
+    const int per = (ncols + parts - 1) / parts;
+    const int T = ((per + 15) / 16 + 3) / 4;
+    if (algo != 0 || per > cnmf_solve_mfma_max_cols(K)) return hipErrorInvalidValue;
+    return cnmf::launch_solve_mfma(K, p, nblocks, T < 1 ? 1 : T, stream);
+  }
   if (K > 32) return cnmf::launch_solve_wide(K, algo, p, nblocks, threads, stream);
-  // variant: 0 auto, 1 streaming, 2 register-resident.  Resident needs every slice to
+  // variant: 0 auto, 1 streaming, 2 register-resident (3 = mfma above).  Resident needs every slice to
   // fit U <= res_max_cols(K) columns per thread of a <= 1024-thread workgroup; it runs
   // with the smallest such U and just enough threads for the slice.
   const int parts = nsplit > 1 ? nsplit : (coop_split > 1 ? coop_split : 1);

@@ -35,6 +35,9 @@
 
 namespace cnmf {
 
+// cooperative slices per replicate (coop_sum2: one wave watches the 2 S granules)
+constexpr int kCoopMaxSlices = 32;
+
 template <int K>
 constexpr int solve_max_threads() { return 1024; }
 
@@ -124,15 +127,21 @@ __device__ __forceinline__ void load_group(ColGroup<K, U>& cg, int j, int T, int
 }
 
 // Cross-workgroup sum of (a, b) for the S workgroups of one replicate, epoch `e`.
-// Each workgroup stores its block totals to its own slot (plain store), drains, then
-// arrives on the epoch counter with an agent-scope release; after all S arrived every
-// workgroup sums the S slots in slice order -> identical, deterministic totals
-// everywhere.  Spins are bounded: on timeout the flag is raised and the host fails.
-// Returns false once the launch's timeout flag is up (this or any earlier exchange gave
-// up): the caller then stops iterating, so slices that diverged never wait for each
-// other again and the launch drains quickly.
-// (Recipe: cdna_hip_programming.md Guideline 16 -- release before the counter add,
-// acquire after the poll, vmcnt drained around the fence.)
+// The data IS the flag (cdna_hip_programming.md Guideline 16, form R2): each workgroup
+// publishes its two block totals as 8-byte {tag, value} granules with agent-scope atomic
+// (write-through) stores into its own slots of epoch e; one wave of every workgroup
+// re-reads the 2 S granules of the epoch (one lane each, relaxed agent-scope loads, no
+// fence) until every tag is this launch's, then sums the S slices in slice order ->
+// identical, deterministic totals everywhere.  No counter and no release/acquire fence:
+// those (a CAS arrival + an L2 writeback/invalidate per workgroup) made one exchange cost
+// ~3 us at S = 2 and ~15 us at S = 9.  Slots are never zeroed between eager launches (the
+// tag is the launch generation, strictly increasing per workspace); under a HIP graph
+// the captured memset zeroes them and the tag is 0xFFFFFFFF.  Spins are bounded: on
+// timeout the flag is raised and the host fails.  Returns false once the launch's
+// timeout flag is up (this or any earlier exchange gave up): the caller then stops
+// iterating, so slices that diverged never wait for each other again.
+typedef __attribute__((address_space(1))) unsigned long long gran_t;
+
 __device__ __forceinline__ bool coop_sum2(const SolveParams& p, int rep, int e, float& a,
                                           float& b, float* sred) {
   const int S = gridDim.y;
@@ -142,54 +151,50 @@ __device__ __forceinline__ bool coop_sum2(const SolveParams& p, int rep, int e, 
     if (threadIdx.x == 0) atomicExch(p.coop_timeout, 2);
     return false;
   }
-  float* slots = p.coop_slots + (((long long)rep * p.coop_epochs + e) * S) * 2;
-  unsigned long long* cnt = p.coop_count + (long long)rep * p.coop_epochs + e;
+  gran_t* g = (gran_t*)(p.coop_slots + (((long long)rep * p.coop_epochs + e) * S) * 2);
   const unsigned long long tag = (unsigned long long)p.coop_gen << 32;
-  constexpr unsigned long long kHi = 0xffffffff00000000ull;
-  if (threadIdx.x == 0) {
-    int ok = __hip_atomic_load(p.coop_timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-    if (ok) {
-      slots[2 * slice] = a;
-      slots[2 * slice + 1] = b;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // arrive: a counter still tagged with an older launch restarts at 1
-      unsigned long long old = __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while (true) {
-        const unsigned long long want = (old & kHi) == tag ? old + 1 : (tag | 1ull);
-        if (__hip_atomic_compare_exchange_strong(cnt, &old, want, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-          break;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    if (lane == 0) {
+      __hip_atomic_store(g + 2 * slice, tag | __float_as_uint(a), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 2 * slice + 1, tag | __float_as_uint(b), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    int ok = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(p.coop_timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0);
+    // lane i < 2 S watches granule i (S <= 32: one wave covers every slot)
+    unsigned long long v = tag;
+    unsigned spins = 0;
+    while (ok) {
+      if (lane < 2 * S) v = __hip_atomic_load(g + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all((v & 0xffffffff00000000ull) == tag)) break;
+      __builtin_amdgcn_s_sleep(2);
+      ++spins;
+      if ((spins & 1023u) == 0 &&
+          __builtin_amdgcn_readfirstlane(__hip_atomic_load(p.coop_timeout, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)) != 0)
+        ok = 0;   // another replicate's exchange already gave up: stop waiting (uniform)
+      if (spins > (1u << 22)) {
+        if (lane == 0) atomicExch(p.coop_timeout, 1);
+        ok = 0;
       }
-      unsigned spins = 0;
-      while (true) {
-        const unsigned long long v = __hip_atomic_load(cnt, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-        if ((v & kHi) == tag && (int)(v & 0xffffffffull) >= S) break;
-        __builtin_amdgcn_s_sleep(2);
-        ++spins;
-        if ((spins & 1023u) == 0 &&
-            __hip_atomic_load(p.coop_timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-          ok = 0;  // another replicate's exchange already gave up: stop waiting
-          break;
-        }
-        if (spins > (1u << 24)) {
-          atomicExch(p.coop_timeout, 1);
-          ok = 0;
-          break;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    // slice-ordered sums through LDS (sred[3 ..]): deterministic on every workgroup
+    if (lane < 2 * S) sred[3 + lane] = __uint_as_float((unsigned)v);
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
       float ta = 0.f, tb = 0.f;
-      for (int s2 = 0; s2 < S; ++s2) {
-        ta += __hip_atomic_load(slots + 2 * s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tb += __hip_atomic_load(slots + 2 * s2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ok) {
+        for (int s2 = 0; s2 < S; ++s2) {
+          ta += sred[3 + 2 * s2];
+          tb += sred[3 + 2 * s2 + 1];
+        }
       }
       sred[0] = ta;
       sred[1] = tb;
+      sred[2] = ok ? 1.f : 0.f;
     }
-    sred[2] = ok ? 1.f : 0.f;
   }
   __syncthreads();
   a = sred[0];
@@ -398,7 +403,7 @@ __global__ __launch_bounds__(solve_block_threads<K>()) void solve_kernel(SolvePa
   constexpr int KP = gram_pad(K);
   constexpr bool resident = RES != 0;
   __shared__ __attribute__((aligned(16))) float sGm[K * KP];
-  __shared__ float sred[2 * 16 + 1];
+  __shared__ float sred[3 + 2 * kCoopMaxSlices];
   constexpr int NS = (U * K) | 1;
   __shared__ float sNm[resident ? NS * 1024 : 1];
   const lds_float* sG = (const lds_float*)sGm;  // LDS (addrspace 3): ds_read, 32-bit address
@@ -671,6 +676,7 @@ hipError_t launch_solve_wide(int K, int algo, const SolveParams& p, int nblocks,
                              hipStream_t s);
 hipError_t launch_solve_resident(int K, int U, int algo, const SolveParams& p, int nblocks,
                                  int threads, hipStream_t s);
+hipError_t launch_solve_mfma(int K, const SolveParams& p, int nblocks, int T, hipStream_t s);
 hipError_t launch_solve_resident34(int K, int U, int algo, const SolveParams& p, int nblocks,
                                    int threads, hipStream_t s);
 

@@ -23,12 +23,10 @@ struct SolveParams {
                             // 1: block objective every `check_every` steps (nmf-torch online)
   int check_every;
   // Cooperative split (gridDim.y = S > 1 workgroups per replicate, WITH convergence):
-  // per-epoch partial sums are exchanged through global memory (deterministic order).
-  float* coop_slots;        // [R][coop_epochs][S][2], no zeroing needed
-  // [R][coop_epochs] arrival counters, (generation << 32) | arrivals: the first arrival
-  // of launch `coop_gen` restarts a counter, so the host never zeroes them (allocated
-  // zeroed once; coop_gen >= 1 strictly increases per launch on a workspace)
-  unsigned long long* coop_count;
+  // per-epoch partial sums are exchanged through global memory (deterministic order) as
+  // {tag = coop_gen, value} granules (coop_sum2 in solve_core.h), never zeroed between
+  // eager launches: coop_gen strictly increases per workspace.
+  unsigned long long* coop_slots;   // [R][coop_epochs][S][2] granules
   unsigned coop_gen;
   int coop_epochs;
   int* coop_timeout;        // set to 1 if a spin gave up (residency violated)

@@ -1,12 +1,13 @@
-#!/bin/bash
-# One GPU round: kernel tests, smoke, bench, and a kernel-trace profile of the bench.
-# usage (via gpurun): bash tools/gpu_check.sh <tag>
-set -o pipefail
-TAG=${1:-run}
-cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
+# One GPU validation pass: solve/GEMM kernel tests, solve probe, bench (default and with
+# the VALU solve / exact 3-plane GEMMs for A/B), kernel-trace profile of bench.py.
+# usage: bash tools/gpu_check.sh <outdir under gpurun_out>
+set -e
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu_$TAG.log 2>&1 && \
-timeout -k 10 200 python __graft_entry__.py smoke > gpurun_out/smoke_$TAG.log 2>&1 && \
-timeout -k 10 400 python bench.py --steps 3 --warmup 1 > gpurun_out/bench_$TAG.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python bench.py --steps 1 --warmup 0 > gpurun_out/prof_$TAG.log 2>&1
+out=gpurun_out/$1
+mkdir -p $out
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "solve or gemm or concurrent or graph or refit or coop or nmf" > $out/pytest.log 2>&1 || true
+timeout -k 10 200 python -u tools/solve_probe.py > $out/solve.log 2>&1
+timeout -k 10 120 python bench.py > $out/bench.log 2>&1
+CNMF_SOLVE_MFMA=0 timeout -k 10 120 python bench.py > $out/bench_nomfma.log 2>&1
+CNMF_GEMM_APLANES=3 timeout -k 10 120 python bench.py > $out/bench_3planes.log 2>&1
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- python3 bench.py --steps 10 --warmup 3 > $out/prof.log 2>&1

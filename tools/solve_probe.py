@@ -45,7 +45,8 @@ def main():
     K = a.k
     for R, n, label in ((100, 5000, "H-side n=100"), (50, 5000, "H-side n=50"),
                         (100, 2000, "W-side n=100")):
-        for variant, coop in (("stream", "auto"), ("stream", 1), ("reg", "auto")):
+        for variant, coop in (("stream", "auto"), ("stream", 1), ("reg", "auto"),
+                              ("mfma", "auto")):
             try:
                 t10 = case(R, K, n, 10, variant, coop)
                 t40 = case(R, K, n, 40, variant, coop)
@@ -53,11 +54,14 @@ def main():
                       f"40 it {t40:7.1f} us -> {(t40 - t10) / 30:6.2f} us/iter", flush=True)
             except Exception as e:  # variant not applicable to the shape
                 print(f"{label:14s} K={K} {variant:6s} coop={coop!s:4s}: n/a ({e})", flush=True)
-        for conv_mode in (1,):
-            t10 = case(R, K, n, 10, "auto", "auto", conv_mode)
-            t40 = case(R, K, n, 40, "auto", "auto", conv_mode)
-            print(f"{label:14s} K={K} auto   loss-conv : 10 it {t10:7.1f} us, 40 it {t40:7.1f} us "
-                  f"-> {(t40 - t10) / 30:6.2f} us/iter", flush=True)
+        for variant in ("reg", "mfma"):
+            try:
+                t10 = case(R, K, n, 10, variant, "auto", 1)
+                t40 = case(R, K, n, 40, variant, "auto", 1)
+                print(f"{label:14s} K={K} {variant:6s} loss-conv : 10 it {t10:7.1f} us, 40 it "
+                      f"{t40:7.1f} us -> {(t40 - t10) / 30:6.2f} us/iter", flush=True)
+            except Exception as e:
+                print(f"{label:14s} K={K} {variant:6s} loss-conv : n/a ({e})", flush=True)
 
 
 if __name__ == "__main__":
