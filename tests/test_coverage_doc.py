@@ -26,7 +26,8 @@ def test_named_files_exist():
     for name in set(re.findall(r"`([\w/]+\.(?:py|hip|cpp|md))`", doc)):
         cands = [os.path.join(ROOT, name), os.path.join(PKG, name),
                  os.path.join(ROOT, "tests", name), os.path.join(ROOT, "csrc", "kernels", name),
-                 os.path.join(ROOT, "csrc", "h5ad", name)]
+                 os.path.join(ROOT, "csrc", "h5ad", name),
+                 os.path.join(ROOT, "csrc", "io", name)]
         if not any(os.path.exists(c) for c in cands):
             missing.append(name)
     assert not missing, missing
