@@ -519,8 +519,12 @@ class cNMF:
 
     def factorize_jobs(self, jobs, worker_label=0, device=None, replicate_batch=None,
                        save_usages=False, verbose=True, run_params=None, comm=None,
-                       row_range=None, row_segments=None):
+                       row_range=None, row_segments=None, collect=None):
         """Factorise an explicit list of ledger rows.
+
+        ``collect`` (a dict): also keep every written replicate's spectra in memory,
+        ``collect[(k, iter)] = (k x G) float32``, plus ``collect["genes"]`` -- for the
+        in-memory gather of parallel.runner.gather_merged_spectra.
 
         ``comm`` with ``row_segments`` (global [start, stop) row segments, e.g.
         parallel.runner.dp_row_segments) or ``row_range`` (one contiguous block) runs the
@@ -629,6 +633,11 @@ class cNMF:
                                for r, i in enumerate(grp[:n_ok])]
                     pending.append(pool.submit(_write_batch, paths_b, W, res.offs[:n_ok],
                                                ks[:n_ok], [int(itv[i]) for i in grp[:n_ok]]))
+                    if collect is not None:
+                        collect["genes"] = gene_arr
+                        for r, i in enumerate(grp[:n_ok]):
+                            o = int(res.offs[r])
+                            collect[(ks[r], int(itv[i]))] = W[o:o + ks[r]]
                 for r, idx in enumerate(grp):
                     k, it = ks[r], int(itv[idx])
                     if writer:

@@ -70,6 +70,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "default under torchrun is replicate parallelism")
     p.add_argument("--save-usages", action="store_true", default=False,
                    help="[factorize] Also persist per-replicate usages (iter_usages files)")
+    p.add_argument("--gather-spectra", action="store_true", default=False,
+                   help="[factorize] under torchrun (replicate parallel): all-gather every "
+                        "replicate's spectra onto rank 0 over RCCL and write the merged "
+                        "spectra there (what combine assembles from the files)")
     p.add_argument("--skip-missing-files", action="store_true", default=False,
                    help="[combine] Ignore missing replicate files")
     p.add_argument("--local-density-threshold", type=float, default=0.5,
@@ -122,7 +126,8 @@ def main(argv=None) -> int:
 
             distributed_factorize(obj, skip_completed_runs=args.skip_completed_runs,
                                   replicate_batch=args.replicate_batch,
-                                  save_usages=args.save_usages)
+                                  save_usages=args.save_usages,
+                                  gather_spectra=args.gather_spectra)
         else:
             wi = args.worker_index if args.worker_index is not None else 0
             tw = args.total_workers if (args.worker_index is not None and args.total_workers > 0) else 1

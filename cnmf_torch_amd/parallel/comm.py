@@ -36,6 +36,9 @@ class LocalComm:
     def gather_object(self, obj, dst: int = 0):
         return [obj]
 
+    def all_gather_(self, t: torch.Tensor) -> list[torch.Tensor]:
+        return [t]
+
     @property
     def is_distributed(self) -> bool:
         return False
@@ -107,6 +110,18 @@ class DistComm(LocalComm):
         out = [None] * self.world_size
         self._dist.all_gather_object(out, obj, group=self.group)
         return out
+
+    def all_gather_(self, t: torch.Tensor) -> list[torch.Tensor]:
+        """Every rank's ``t`` (same shape and dtype everywhere), in rank order.  Device
+        tensors travel over RCCL (one ring all-gather on the xGMI links); under gloo a
+        device tensor is staged through the host."""
+        if self.world_size == 1:
+            return [t]
+        src = t if (self.backend == "nccl") == (t.device.type == "cuda") else \
+            t.to(self._dev())
+        out = [torch.empty_like(src) for _ in range(self.world_size)]
+        self._dist.all_gather(out, src.contiguous(), group=self.group)
+        return out if src is t else [o.to(t.device) for o in out]
 
     def gather_object(self, obj, dst: int = 0):
         """Python objects of every rank on ``dst`` (list in rank order), None elsewhere."""

@@ -55,18 +55,86 @@ def _incomplete_jobs(obj, run_params, skip_completed_runs: bool):
 
 
 def distributed_factorize(obj, skip_completed_runs: bool = False, replicate_batch=None,
-                          save_usages: bool = False, backend: str | None = None, verbose=True):
+                          save_usages: bool = False, backend: str | None = None, verbose=True,
+                          gather_spectra: bool = False):
+    """Replicate-parallel factorize.  ``gather_spectra``: the replicate spectra also go to
+    rank 0 by all-gather (RCCL) and rank 0 writes every K's merged spectra -- what
+    ``combine`` would assemble from the files; the per-replicate
+    files are still written as the durable checkpoint."""
     from ..utils.io import load_df_from_npz
 
     comm, dev = init_distributed(backend)
     run_params = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
     jobs = _incomplete_jobs(obj, run_params, skip_completed_runs)
     mine = shard_by_k(run_params, jobs, comm.rank, comm.world_size)
+    collect = {} if gather_spectra else None
     obj.factorize_jobs(mine, worker_label=comm.rank, device=dev,
                        replicate_batch=replicate_batch, save_usages=save_usages,
-                       verbose=verbose, run_params=run_params)
+                       verbose=verbose, run_params=run_params, collect=collect)
+    if gather_spectra:
+        gather_merged_spectra(obj, comm, collect, run_params, dev)
     comm.barrier()
     return comm
+
+
+def gather_merged_spectra(obj, comm, collect: dict, run_params, dev) -> None:
+    """Every K's replicate spectra onto rank 0 with one all-gather per K, then rank 0
+    writes ``merged_spectra`` exactly as ``combine_nmf`` would (rows by iteration,
+    ``iter%d_topic%d`` labels, gene columns).  Replicates solved in an earlier run (a
+    resume) are not in memory: rank 0 reads their files, as combine does; a K with a
+    replicate missing everywhere is left to ``combine``."""
+    import pandas as pd
+
+    from ..api import _load_npz_arrays
+    from ..utils.io import NPZ_TMP_LEVEL, save_df_to_npz
+
+    genes = collect.get("genes")
+    genes_all = comm.all_gather_object(None if genes is None else list(genes))
+    genes = next((g for g in genes_all if g is not None), None)
+    if genes is None:
+        return
+    G = len(genes)
+    tdev = dev if comm.is_distributed and getattr(comm, "backend", "") == "nccl" \
+        else torch.device("cpu")
+    ks = sorted(set(int(k) for k in run_params.n_components))
+    for k in ks:
+        its = sorted(int(i) for i in run_params.iter[run_params.n_components == k])
+        mine = [it for it in its if (k, it) in collect]
+        n_max = comm.allreduce_max_int(len(mine))
+        buf = torch.zeros((max(n_max, 1), k, G), dtype=torch.float32, device=tdev)
+        ids = torch.full((max(n_max, 1),), -1, dtype=torch.int64, device=tdev)
+        for j, it in enumerate(mine):
+            buf[j] = torch.from_numpy(np.ascontiguousarray(collect[(k, it)]))
+            ids[j] = it
+        parts = comm.all_gather_(buf)
+        id_parts = comm.all_gather_(ids)
+        if comm.rank != 0:
+            continue
+        got = {}
+        for b, i in zip(parts, id_parts):
+            for j, it in enumerate(i.cpu().tolist()):
+                if it >= 0:
+                    got[it] = b[j]
+        rows = []
+        for it in its:
+            if it in got:
+                rows.append(got[it].cpu().numpy())
+                continue
+            fn = obj.paths["iter_spectra"] % (k, it)
+            if not os.path.exists(fn):
+                rows = None
+                break
+            data, _, cols = _load_npz_arrays(fn)
+            if not np.array_equal(np.asarray(cols).astype(str), np.asarray(genes).astype(str)):
+                rows = None
+                break
+            rows.append(np.asarray(data, dtype=np.float32))
+        if rows is None:
+            continue
+        index = ["iter%d_topic%d" % (it, t + 1) for it in its for t in range(k)]
+        merged = pd.DataFrame(np.concatenate(rows, axis=0), index=index,
+                              columns=np.asarray(genes))
+        save_df_to_npz(merged, obj.paths["merged_spectra"] % k, level=NPZ_TMP_LEVEL)
 
 
 def distributed_consensus(obj, ks, density_threshold=0.5, local_neighborhood_size=0.30,

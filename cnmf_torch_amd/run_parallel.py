@@ -25,6 +25,7 @@ import glob
 import os
 import socket
 import subprocess
+import time
 import sys
 
 
@@ -86,6 +87,7 @@ def main(argv=None) -> int:
 
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    t_factorize = time.time()
     if a.workers:
         procs = []
         for w in range(a.workers):
@@ -100,16 +102,22 @@ def main(argv=None) -> int:
         if bad:
             raise SystemExit(f"{len(bad)} factorize worker(s) failed")
     elif a.gpus > 1:
+        # replicate parallel: the spectra also reach rank 0 by all-gather, which writes
+        # the merged spectra (combine below then only fills in what is missing)
         _run([py, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-              "-m", "cnmf_torch_amd", "factorize"] + base + (["--dp"] if a.dp else []),
-             env=env)
+              "-m", "cnmf_torch_amd", "factorize"] + base +
+             (["--dp"] if a.dp else ["--gather-spectra"]), env=env)
     elif a.dp:
         _run([py, "-m", "cnmf_torch_amd", "factorize", "--dp"] + base, env=env)
     else:
         _run([py, "-m", "cnmf_torch_amd", "factorize"] + base, env=env)
 
-    _run([py, "-m", "cnmf_torch_amd", "combine"] + base)
+    merged = [os.path.join(a.output_dir, a.name, "cnmf_tmp",
+                           "%s.spectra.k_%d.merged.df.npz" % (a.name, k))
+              for k in sorted(set(a.components))]
+    if not all(os.path.exists(m) and os.path.getmtime(m) >= t_factorize for m in merged):
+        _run([py, "-m", "cnmf_torch_amd", "combine"] + base)
     if not a.keep_iterations:
         pattern = os.path.join(a.output_dir, a.name, "cnmf_tmp", "*.iter_*.df.npz")
         for fn in glob.glob(pattern):

@@ -45,6 +45,9 @@ def factorize_worker(rank, world, port, output_dir, name, mode):
     obj = cNMF(output_dir=output_dir, name=name)
     if mode == "replicate":
         distributed_factorize(obj, backend="gloo", verbose=False)
+    elif mode == "gather":      # resume + gather: completed replicates come from files
+        distributed_factorize(obj, backend="gloo", verbose=False, gather_spectra=True,
+                              skip_completed_runs=True)
     else:
         dp_factorize(obj, backend="gloo", verbose=False)
     dist.destroy_process_group()

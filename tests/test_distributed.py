@@ -127,6 +127,32 @@ def test_distributed_factorize_matches_serial(prepared, mode):
             np.testing.assert_allclose(e_dp[key], e_se[key], rtol=1e-4, err_msg=str(key))
 
 
+def test_gathered_merged_spectra_equal_file_combine(prepared):
+    """distributed_factorize(gather_spectra=True): the replicate spectra reach rank 0 by
+    all-gather and rank 0 writes every K's merged spectra -- identical (values, row labels,
+    gene columns) to what combine assembles from the per-replicate files.  A replicate
+    solved in an earlier run (resume) is taken from its file."""
+    import os
+
+    d, fn = prepared
+    name = "gathered"
+    obj = cNMF(output_dir=str(d), name=name)
+    obj.prepare(fn, components=[3, 4], n_iter=3, seed=13, num_highvar_genes=120, batch_size=150)
+    # one replicate solved "earlier": only its file exists when the ranks start
+    rp = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
+    obj.factorize_jobs([0], run_params=rp, verbose=False)
+    _spawn(W.factorize_worker, 2, str(d), name, "gather")
+    gathered = {k: load_df_from_npz(obj.paths["merged_spectra"] % k) for k in (3, 4)}
+    for k in (3, 4):
+        os.remove(obj.paths["merged_spectra"] % k)
+    obj.combine()
+    for k in (3, 4):
+        ref = load_df_from_npz(obj.paths["merged_spectra"] % k)
+        assert list(gathered[k].index) == list(ref.index)
+        assert list(gathered[k].columns) == list(ref.columns)
+        np.testing.assert_array_equal(gathered[k].values, ref.values)
+
+
 def test_k_parallel_consensus_and_k_selection_match_serial(prepared):
     """distributed_consensus / distributed_k_selection (Ks dealt over 2 gloo ranks) write
     the same artifacts as the serial stages."""

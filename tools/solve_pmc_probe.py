@@ -13,6 +13,7 @@ from cnmf_torch_amd import ops  # noqa: E402
 
 def main():
     variant = sys.argv[1] if len(sys.argv) > 1 else "mfma"
+    every = int(sys.argv[2]) if len(sys.argv) > 2 else 10   # 1000: sweeps only
     R, K, n = 100, 10, 5000
     g = torch.Generator(device="cuda").manual_seed(0)
     W = torch.rand(R, K, 64, device="cuda", generator=g)
@@ -21,8 +22,8 @@ def main():
     numer = torch.rand(R, K, n, device="cuda", generator=g) * 16
     for _ in range(5):
         x = x0.clone()
-        ops.solve("mu", x, numer, gram, max_iter=40, tol=-1.0, conv_mode=1, check_every=10,
-                  variant=variant, coop="auto")
+        ops.solve("mu", x, numer, gram, max_iter=40, tol=-1.0, conv_mode=1,
+                  check_every=every, variant=variant, coop="auto")
     torch.cuda.synchronize()
     print("done", variant, flush=True)
 
