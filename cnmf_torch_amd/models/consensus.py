@@ -133,12 +133,15 @@ def _lloyd_fused(X: torch.Tensor, centers: torch.Tensor, max_iter: int, tol: flo
 
 
 def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 300,
-           tol: float = 1e-4, backend: str = "auto"):
+           tol: float = 1e-4, backend: str = "auto", device_restart_factor: int = 4):
     """Returns integer labels 0..k-1 (numpy).  ``backend='sklearn'`` is the reference's
     KMeans(n_clusters=k, n_init=10, random_state=1) (cnmf.py:1082) bit for bit;
     ``'device'`` runs batched k-means++ + batched Lloyd (same algorithm, own RNG stream)
     on the tensor's device (HIP kernels); ``'auto'`` (default) = device for GPU tensors,
-    sklearn otherwise."""
+    sklearn otherwise.  The device path runs ``device_restart_factor`` x ``n_init``
+    restarts: they share the same launches (nearly free), and with its own RNG stream 10
+    restarts reached sklearn's best inertia less often (5/10 vs 9/10 seeds on the K=8
+    golden spectra of tests/data; 40 restarts: 10/10)."""
     if backend == "auto":
         backend = "device" if isinstance(X, torch.Tensor) and X.device.type == "cuda" \
             else "sklearn"
@@ -154,7 +157,7 @@ def kmeans(X, k: int, n_init: int = 10, random_state: int = 1, max_iter: int = 3
     # sklearn scales tol by the mean feature variance
     tol_abs = tol * float(Xt.var(dim=0, unbiased=False).mean())
     gen = torch.Generator(device="cpu").manual_seed(int(random_state))
-    c0 = _kmeanspp_batched(Xt, k, gen, n_init)
+    c0 = _kmeanspp_batched(Xt, k, gen, n_init * max(1, int(device_restart_factor)))
     labels, inertia = _lloyd_batched(Xt, c0, max_iter, tol_abs)
     best = int(torch.argmin(inertia))
     return labels[:, best].cpu().numpy()

@@ -110,13 +110,70 @@ def test_gpu_consensus_matches_golden(tmp_path, ds):
     _consensus_and_compare(obj, cfg, ds, device="cuda", rel_tol=1e-10)
 
 
+def _consensus_outputs(obj, cfg, **kw) -> dict:
+    out = {}
+    for k, thr in cfg["consensus"]:
+        obj.consensus(k, density_threshold=thr, show_clustering=False, **kw)
+    for key in mtd.GOLDEN_KEYS:
+        for k, thr in cfg["consensus"]:
+            fn = obj.paths[key] % (k, str(thr).replace(".", "_"))
+            out[(key, k)] = load_df_from_npz(fn)
+    return out
+
+
+def _copy_golden_merged(obj, cfg, ds):
+    for k in cfg["k_values"]:
+        shutil.copy(_golden(obj, ds, obj.paths["merged_spectra"] % k),
+                    obj.paths["merged_spectra"] % k)
+
+
+@pytest.mark.parametrize("ds", sorted(mtd.DATASETS))
+def test_device_kmeans_inertia_not_worse_than_sklearn(tmp_path, monkeypatch, ds):
+    """The batched device k-means (own RNG stream, 4x the restarts in the same launches)
+    reaches sklearn's KMeans(n_init=10, random_state=1) inertia on every consensus input of
+    the golden datasets (run here through the torch reference ops on the CPU)."""
+    from sklearn.cluster import KMeans
+
+    import cnmf_torch_amd.api as api_mod
+    from cnmf_torch_amd.models.consensus import kmeans
+
+    seen = []
+    real = api_mod.kmeans
+
+    def spy(X, k, **kw):
+        seen.append((np.asarray(X.detach().cpu().numpy(), dtype=np.float64).copy(), k))
+        return real(X, k, **kw)
+
+    monkeypatch.setattr(api_mod, "kmeans", spy)
+    cfg, obj = _prepare(tmp_path, ds)
+    _copy_golden_merged(obj, cfg, ds)
+    _consensus_outputs(obj, cfg, device="cpu", kmeans_backend="sklearn")
+    assert len(seen) == len(cfg["consensus"])
+    for X, k in seen:
+        sk = KMeans(n_clusters=k, n_init=10, random_state=1).fit(X).inertia_
+        lab = kmeans(torch.as_tensor(X), k, n_init=10, random_state=1, backend="device")
+        C = np.stack([X[lab == c].mean(axis=0) for c in range(k)])
+        inertia = float(((X - C[lab]) ** 2).sum())
+        assert inertia <= sk * (1 + 1e-9), (k, inertia, sk)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("ds", sorted(mtd.DATASETS))
-def test_gpu_device_kmeans_consensus_close_to_golden(tmp_path, ds):
-    """The GPU default (batched device k-means, own RNG stream) clusters the replicate
-    spectra like sklearn up to boundary points: outputs within 5e-2 relative (the OLS
-    z-scores amplify a boundary replicate moving cluster most: ~1.6e-2 seen on the h5ad
-    dataset at K=7; the consensus spectra/usages themselves stay within ~1e-3)."""
+def test_gpu_device_kmeans_consensus_matches_cpu(tmp_path, ds):
+    """The GPU default (batched device k-means on the HIP distance / argmin kernels, then the
+    device refits and OLS) == the same pipeline through the CPU reference ops.  Both draw the
+    k-means++ uniforms from the same host generator, so the labels agree; the cluster
+    numbering of the device k-means is not sklearn's, and the consensus outputs depend on it
+    (the usage refit's init follows the component order, as in the reference), so the golden
+    comparison is the sklearn-backend test above."""
     assert torch.cuda.is_available()
     cfg, obj = _prepare(tmp_path, ds)
-    _consensus_and_compare(obj, cfg, ds, device="cuda", rel_tol=5e-2, kmeans_backend="device")
+    _copy_golden_merged(obj, cfg, ds)
+    ref = _consensus_outputs(obj, cfg, device="cpu", kmeans_backend="device")
+    got = _consensus_outputs(obj, cfg, device="cuda", kmeans_backend="device")
+    for key, r in ref.items():
+        g = got[key]
+        assert list(g.index) == list(r.index) and list(g.columns) == list(r.columns)
+        rms = float(((g.values - r.values) ** 2).sum())
+        ss = float((r.values ** 2).sum())
+        assert rms <= TOLERANCE or rms / ss < 1e-8, (key, rms, ss)
