@@ -75,12 +75,16 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + CSRC,
               "-Wno-unused-result", "-munsafe-fp-atomics"]
     objs, todo = [], []
+    # per-unit flags: the split-bf16 beta kernels keep their MFMA accumulators in VGPRs
+    # (the elementwise work reads every accumulator: AGPR copies cost ~30 % of the VALU)
+    unit_flags = {"beta_planes.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _stale(o, [s] + hdrs):
             extra = _py_includes() if s.endswith(".cpp") else []
-            todo.append([hipcc, "-c", s, "-o", o] + common + extra)
+            todo.append([hipcc, "-c", s, "-o", o] + common + extra +
+                        unit_flags.get(os.path.basename(s), []))
     if todo:
         if verbose:
             print(f"[cnmf build] compiling {len(todo)} HIP/C++ unit(s) for {ARCH}", flush=True)

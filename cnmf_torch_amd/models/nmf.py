@@ -783,6 +783,7 @@ class NMFBatchSolver:
         self._xp = False            # split-GEMM planes of X: False = not built yet
         self._ws: dict = {}
         self._w_fresh: dict = {}    # stream -> key of the W its "w" planes hold
+        self._XT = None             # X^T (G, N padded to 4) for the beta W-side kernel
 
     # ------------------------------------------------------------------ public
     def run(self, seeds, HT0=None, W0=None, ks=None) -> NMFResult:
@@ -1101,8 +1102,7 @@ class NMFBatchSolver:
         K = int(K)
         R = W.shape[0] // K
         W3 = W.view(R, K, G)
-        _, _, tot = ops.beta_contract("h", X, HT.view(R, K, N), W3, self.beta, self.opts.eps,
-                                      want_num=False, want_loss=True)
+        tot = ops.beta_loss(X, HT.view(R, K, N), W3, self.beta, self.opts.eps)
         tot = tot.to(torch.float64).contiguous()
         self.comm.allreduce_(tot)
         return torch.sqrt(torch.clamp(2.0 * tot.cpu(), min=0.0))
@@ -1360,40 +1360,65 @@ class NMFBatchSolver:
             delta = torch.where(mask, delta, torch.ones_like(delta))
         x3.mul_(delta)
 
-    def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, tol=None, iters=None,
-                       den_vec=None):
-        """One fused MU step of the usages H3c (R, K, c) in place against W3 on rows xc;
-        with ``tol`` the per-replicate inner stopping rule runs on device (clears act)."""
-        ops.beta_update_h(xc, H3c, W3, self.beta, self.opts.eps, l1, l2, self._beta_gamma(),
-                          act=act, tol=tol, iters=iters, den_vec=den_vec)
+    def _xt(self) -> torch.Tensor | None:
+        """X^T (G, N), leading dimension padded to a multiple of 4 (float4 loads), for the
+        W-side beta kernel (beta_planes.hip reads X along cells there); GPU only."""
+        if self.X.device.type != "cuda":
+            return None
+        if self._XT is None:
+            N, G = self.X.shape
+            buf = torch.zeros((G, -(-N // 4) * 4), device=self.X.device, dtype=self.X.dtype)
+            buf[:, :N] = self.X.t()
+            self._XT = buf[:, :N]
+        return self._XT
 
-    def _beta_h_solve(self, xc, hc, W3, act, iters, block: int = 8) -> None:
+    def _beta_panels(self, F3: torch.Tensor):
+        """Split-bf16 panels of a factor that stays fixed over the next kernel launches
+        (GPU only; the CPU reference works on the fp32 factor directly)."""
+        return ops.beta_panels(F3) if F3.device.type == "cuda" else None
+
+    def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, panels=None):
+        """One fused MU step of the usages H3c (R, K, c) in place against W3 on rows xc
+        (replicates with act == 0 untouched)."""
+        ops.beta_h_block(xc, H3c, W3, self.beta, self.opts.eps, 1, l1, l2, self._beta_gamma(),
+                         act=act, panels=panels)
+
+    def _beta_h_solve(self, xc, hc, W3, act, iters, wpan=None, block: int = 8) -> None:
         """Inner usage loop of one chunk: up to ``online_chunk_max_iter`` fused MU steps.
-        Each replicate stops on device: with ``online_inner_conv='loss'`` when the chunk's
-        beta-divergence changed by <= ``online_h_tol`` (relative) over
-        ``inner_check_every`` steps (the Frobenius solve's block-objective rule), else on
-        the relative iterate change.  Steps are enqueued in blocks; whether anybody is
-        still active is read from a pinned copy one block late, so the GPU always has a
-        block queued and the host never drains the stream (launches for finished
-        replicates exit at once)."""
+        With ``online_inner_conv='loss'`` (default) one launch runs ``inner_check_every``
+        steps, and the block objective -- the chunk's beta-divergence after the block
+        against the one before it -- stops a replicate once it changed by <=
+        ``online_h_tol`` (relative; the Frobenius solve's conv_mode-1 rule, checked every
+        ``inner_check_every`` steps); else one step per launch on the relative iterate
+        change.  The rule runs on the device; whether anybody is still active is read from
+        a pinned copy one launch group late, so the GPU always has work queued and the host
+        never drains the stream (launches for finished replicates exit at once)."""
         o = self.opts
         W3 = W3.contiguous() if W3.stride(-1) != 1 else W3
+        cuda = xc.device.type == "cuda"
         den_vec = (W3.sum(dim=2, dtype=torch.float32).contiguous()
-                   if self.beta == 1.0 and xc.device.type == "cuda" else None)
+                   if self.beta == 1.0 and cuda else None)
+        if cuda and wpan is None:
+            wpan = ops.beta_panels(W3)
         cmode = 1 if o.online_inner_conv == "loss" else 0
+        per = max(1, int(o.inner_check_every)) if cmode == 1 else 1
+        group = 1 if cmode == 1 else block
         hstate = torch.zeros((W3.shape[0], 2), dtype=torch.float64, device=xc.device)
         max_it = int(o.online_chunk_max_iter)
-        cuda = xc.device.type == "cuda"
         pending = None
         it = 0
+        first = True
         while it < max_it:
-            m = min(block, max_it - it)
-            for _ in range(m):
-                ops.beta_update_h(xc, hc, W3, self.beta, o.eps, o.l1_H, o.l2_H,
-                                  self._beta_gamma(), act=act, tol=o.online_h_tol, iters=iters,
-                                  den_vec=den_vec, conv_mode=cmode,
-                                  check_every=o.inner_check_every, hstate=hstate)
-            it += m
+            for _ in range(group):
+                if it >= max_it:
+                    break
+                m = min(per, max_it - it)
+                ops.beta_h_block(xc, hc, W3, self.beta, o.eps, m, o.l1_H, o.l2_H,
+                                 self._beta_gamma(), act=act, tol=o.online_h_tol, iters=iters,
+                                 conv_mode=cmode, hstate=hstate, loss_entry=first,
+                                 den_vec=den_vec, panels=wpan)
+                first = False
+                it += m
             if not cuda:
                 if int(act.sum()) == 0:
                     break
@@ -1408,11 +1433,15 @@ class NMFBatchSolver:
                 if int(prev[1][0]) == 0:
                     break
 
-    def _beta_w_stats(self, xc, H3c, W3):
+    def _beta_w_stats(self, xc, H3c, W3, xtc=None, active=None):
         """(num, den) W-side MU statistics of rows xc (den broadcastable to (R,K,G))."""
-        num, den, _ = ops.beta_contract("w", xc, H3c, W3, self.beta, self.opts.eps)
+        num, den = ops.beta_w_partials(xc, xtc, H3c, W3, self.beta, self.opts.eps,
+                                       active=active)
+        num = num.sum(0)
         if den is None:
             den = H3c.sum(dim=2, keepdim=True)              # KL: row sums of H
+        else:
+            den = den.sum(0)
         return num, den
 
     def _beta_w_solve(self, blocks, H3, W3, An, Ad, live, iters, block: int = 4) -> None:
@@ -1444,6 +1473,9 @@ class NMFBatchSolver:
         act = live.clone()
         cuda = dev.type == "cuda"
         dist = self.comm.is_distributed
+        XT = self._xt()
+        # the chunk's usages stay fixed over the spectra iterations: split them once
+        hpan = {(a, b): self._beta_panels(H3[:, :, a:b]) for (a, b) in rows}
         max_it = int(o.online_chunk_max_iter)
         pending = None
         it = 0
@@ -1452,8 +1484,9 @@ class NMFBatchSolver:
             for _ in range(m):
                 num = den = None
                 for (a, b) in rows:
-                    nW, dW, _ = ops.beta_contract("w", X[a:b], H3[:, :, a:b], W3, self.beta,
-                                                  o.eps, active=act, reduce=False)
+                    nW, dW = ops.beta_w_partials(X[a:b], XT[:, a:b] if XT is not None else None,
+                                                 H3[:, :, a:b], W3, self.beta, o.eps,
+                                                 active=act, panels=hpan[(a, b)])
                     if num is None:
                         num, den = nW, dW
                     else:   # several blocks of one step (single-process DP emulation)
@@ -1498,8 +1531,7 @@ class NMFBatchSolver:
         (no host round trip; all-reduced under DP)."""
         R = W.shape[0] // K
         N, G = self.X.shape
-        _, _, tot = ops.beta_contract("h", self.X, HT.view(R, K, N), W.view(R, K, G), self.beta,
-                                      self.opts.eps, want_num=False, want_loss=True)
+        tot = ops.beta_loss(self.X, HT.view(R, K, N), W.view(R, K, G), self.beta, self.opts.eps)
         tot = tot.to(torch.float64).contiguous()
         self.comm.allreduce_(tot)
         return torch.sqrt(torch.clamp(2.0 * tot, min=0.0))
@@ -1532,11 +1564,12 @@ class NMFBatchSolver:
             Ad = torch.zeros((n, K) if kl else (n, K, G), device=X.device, dtype=X.dtype)
             live = st.active_mask().clone()
             for blocks in steps:
+                wpan = self._beta_panels(W3)      # W is fixed over this step's usage solves
                 for (a, b) in blocks:
                     if b <= a:
                         continue
                     act = live.clone()
-                    self._beta_h_solve(X[a:b], H3[:, :, a:b], W3, act, st.h_iters[:n])
+                    self._beta_h_solve(X[a:b], H3[:, :, a:b], W3, act, st.h_iters[:n], wpan)
                 self._beta_w_solve(blocks, H3, W3, An, Ad, live, st.w_iters[:n])
             final = p + 1 == max_pass
             st.set_err(self._loss_dev(HT, W, K), p + 1, o.tol, final)
@@ -1564,7 +1597,7 @@ class NMFBatchSolver:
             # compaction: the active flags gate both updates and the iteration counts
             live = st.active_mask().clone()
             self._beta_h_update(X, H3, W3, o.l1_H, o.l2_H, act=live)
-            nW, dW = self._beta_w_stats(X, H3, W3)
+            nW, dW = self._beta_w_stats(X, H3, W3, self._xt(), active=live)
             if comm.is_distributed:
                 flat = torch.cat([nW.reshape(-1), dW.expand(n, K, G).reshape(-1)])
                 comm.allreduce_(flat)

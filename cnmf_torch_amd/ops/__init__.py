@@ -559,6 +559,179 @@ def beta_w_update(W3: torch.Tensor, num: torch.Tensor, den: torch.Tensor | None,
                        _stream_ptr(W3))
 
 
+# ------------------------------------------------------- beta MU on split bf16 planes
+_BP_WS: dict = {}
+
+
+def _bp_ws(dev, stream, R: int, n_strips: int) -> dict:
+    key = (str(dev), stream)
+    ws = _BP_WS.get(key)
+    if ws is None or ws["part"].numel() < R * n_strips * 4 or ws["counter"].numel() < R:
+        ws = {"part": torch.empty(max(R * n_strips * 4, 1 << 12), dtype=torch.float64,
+                                  device=dev),
+              "counter": torch.zeros(max(R, 1024), dtype=torch.int32, device=dev)}
+        _BP_WS[key] = ws
+    return ws
+
+
+def _bp_check(name: str, t: torch.Tensor, dev) -> None:
+    if t.dtype != torch.float32 or t.device != dev or t.stride(-1) != 1:
+        raise ValueError(f"{name}: float32 with unit inner stride on {dev} required, got "
+                         f"{t.dtype} {tuple(t.stride())} on {t.device}")
+
+
+def beta_panels(F3: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Split-bf16 operand panels of F3 (R, K, L), unit inner stride, K <= 32
+    (beta_planes.hip bp_panel_kernel): per replicate, chunks of 64 rows of the L axis,
+    each holding the three bf16 planes of the 6-term product layout and the two planes
+    of the permuted second-product layout.  Returns (R, panel_elems) int16."""
+    R, K, L = F3.shape
+    _native_dtype_k("beta_panels", F3.dtype, K, _hip.bp_max_k())
+    _bp_check("F3", F3, F3.device)
+    n = int(_hip.bp_panel_elems(K, L))
+    if out is None or out.shape != (R, n) or out.dtype != torch.int16 or not out.is_contiguous():
+        out = torch.empty((R, n), dtype=torch.int16, device=F3.device)
+    _hip.bp_panels(F3.data_ptr(), F3.stride(0), F3.stride(1), K, L, R, out.data_ptr(), n,
+                   _stream_ptr(F3))
+    return out
+
+
+def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float, eps: float,
+                 nsteps: int, l1: float = 0.0, l2: float = 0.0, gamma: float = 1.0,
+                 act: torch.Tensor | None = None, tol: float | None = None,
+                 iters: torch.Tensor | None = None, conv_mode: int = 1,
+                 hstate: torch.Tensor | None = None, loss_entry: bool = False,
+                 den_vec: torch.Tensor | None = None,
+                 panels: torch.Tensor | None = None) -> None:
+    """``nsteps`` fused beta-MU steps of the usages HT3 (R, K, N) in place against the
+    spectra W3 (R, K, G) on rows X (N, G), in ONE launch (beta_planes.hip, side 0):
+    HT3 *= (num / (den + l1 + l2 HT3))^gamma with num/den of the split-bf16 MFMA
+    contraction.  With ``tol`` the stopping rule runs on the device after the block:
+    conv_mode 1 -- the block objective D_beta(X | HT3^T W3) after the block against the one
+    before it (``loss_entry``: computed in this launch; else the value ``hstate`` (float64
+    (R, 2): last objective, checks) holds); conv_mode 0 -- relative change of the last
+    step.  act[r] -> 0 when the rule holds; iters[r] += nsteps.  ``panels``: the
+    :func:`beta_panels` of W3 (built here when omitted)."""
+    R, K, N = HT3.shape
+    G = W3.shape[2]
+    if X.shape != (N, G) or W3.shape[:2] != (R, K):
+        raise ValueError(f"beta_h_block: X {tuple(X.shape)}, HT3 {tuple(HT3.shape)}, "
+                         f"W3 {tuple(W3.shape)} are inconsistent")
+    if tol is not None and act is None:
+        raise ValueError("the stopping rule needs an act array")
+    if tol is not None and conv_mode == 1 and (
+            hstate is None or hstate.dtype != torch.float64 or hstate.numel() < 2 * R
+            or not hstate.is_contiguous() or hstate.device != HT3.device):
+        raise ValueError("conv_mode 1 needs hstate: contiguous float64 (R, 2) on the device")
+    if not use_native(HT3):
+        return reference.beta_h_block(X, HT3, W3, beta, eps, nsteps, l1, l2, gamma, act, tol,
+                                      iters, conv_mode, hstate, loss_entry)
+    dev = HT3.device
+    _native_dtype_k("beta_h_block", HT3.dtype, K, _hip.bp_max_k())
+    for name, t in (("X", X), ("HT3", HT3), ("W3", W3)):
+        _bp_check(name, t, dev)
+    for name, t in (("act", act), ("iters", iters)):
+        if t is not None and (t.dtype != torch.int32 or t.numel() < R or not t.is_contiguous()):
+            raise ValueError(f"{name}: contiguous int32 with >= R entries")
+    mode = beta_mode(beta)
+    if mode == 0 and nsteps > 0:
+        if den_vec is None:
+            den_vec = W3.sum(dim=2, dtype=torch.float32).contiguous()
+        elif (den_vec.shape != (R, K) or den_vec.dtype != torch.float32
+              or not den_vec.is_contiguous() or den_vec.device != dev):
+            raise ValueError("den_vec: contiguous float32 (R, K) on the device required")
+    else:
+        den_vec = None
+    if panels is None:
+        panels = beta_panels(W3)
+    n_strips = -(-N // int(_hip.bp_strip_cols(K)))
+    part = counter = 0
+    if tol is not None:
+        ws = _bp_ws(dev, _stream_ptr(HT3), R, n_strips)
+        part, counter = ws["part"].data_ptr(), ws["counter"].data_ptr()
+    _hip.bp_run(0, mode, X.data_ptr(), X.stride(0), panels.data_ptr(), panels.stride(0),
+                HT3.data_ptr(), HT3.stride(0), HT3.stride(1), K, N, G, R, 1, float(beta),
+                float(eps), 0, 0, int(nsteps), int(bool(loss_entry) and tol is not None),
+                int(tol is not None and conv_mode == 1),
+                den_vec.data_ptr() if den_vec is not None else 0, float(l1), float(l2),
+                float(gamma), float(tol if tol is not None else 0.0), int(conv_mode),
+                hstate.data_ptr() if (hstate is not None and tol is not None) else 0,
+                part, counter, act.data_ptr() if act is not None else 0,
+                iters.data_ptr() if (iters is not None and tol is not None) else 0,
+                act.data_ptr() if act is not None else 0, 0, _stream_ptr(HT3))
+
+
+def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float, eps: float,
+              active: torch.Tensor | None = None,
+              panels: torch.Tensor | None = None) -> torch.Tensor:
+    """sum D_beta(X || HT3^T W3) per replicate, float64 (R,) on the device (beta_planes.hip
+    side 0 in loss-only mode: the P contraction and the loss terms, no numerator)."""
+    R, K, N = HT3.shape
+    G = W3.shape[2]
+    if X.shape != (N, G) or W3.shape[:2] != (R, K):
+        raise ValueError("beta_loss: inconsistent shapes")
+    if not use_native(HT3):
+        return reference.beta_contract(0, X, HT3, W3, beta, eps, False, True, active)[2]
+    dev = HT3.device
+    _native_dtype_k("beta_loss", HT3.dtype, K, _hip.bp_max_k())
+    for name, t in (("X", X), ("HT3", HT3), ("W3", W3)):
+        _bp_check(name, t, dev)
+    if active is not None and (active.dtype != torch.int32 or active.numel() < R
+                               or not active.is_contiguous()):
+        raise ValueError("active: contiguous int32 with >= R entries")
+    if panels is None:
+        panels = beta_panels(W3)
+    n_strips = -(-N // int(_hip.bp_strip_cols(K)))
+    loss = torch.zeros((R, n_strips), dtype=torch.float64, device=dev)
+    _hip.bp_run(0, beta_mode(beta), X.data_ptr(), X.stride(0), panels.data_ptr(),
+                panels.stride(0), HT3.data_ptr(), HT3.stride(0), HT3.stride(1), K, N, G, R, 1,
+                float(beta), float(eps), 0, 0, 0, 0, 1, 0, 0.0, 0.0, 1.0, 0.0, 0, 0, 0, 0, 0,
+                0, active.data_ptr() if active is not None else 0, loss.data_ptr(),
+                _stream_ptr(HT3))
+    return loss.sum(1)
+
+
+def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
+                    W3: torch.Tensor, beta: float, eps: float,
+                    active: torch.Tensor | None = None, splits: int | None = None,
+                    panels: torch.Tensor | None = None):
+    """W-side beta-MU statistics of rows X (c, G) with the chunk's usages HT3 (R, K, c):
+    num = HT Q, den = HT D (None for KL) as (splits, R, K, G) partials -- the operand
+    layout of :func:`beta_w_update` (beta_planes.hip side 1: HT streamed from its split-bf16
+    panels, W3 the fixed operand, X read through its transpose ``XT`` (G, c))."""
+    R, K, c = HT3.shape
+    G = W3.shape[2]
+    if X.shape != (c, G) or W3.shape[:2] != (R, K):
+        raise ValueError("beta_w_partials: inconsistent shapes")
+    if not use_native(HT3):
+        num, den, _ = reference.beta_contract(1, X, HT3, W3, beta, eps, True, False, active)
+        return num.unsqueeze(0), (den.unsqueeze(0) if den is not None else None)
+    dev = HT3.device
+    _native_dtype_k("beta_w_partials", HT3.dtype, K, _hip.bp_max_k())
+    if XT is None or XT.shape != (G, c):
+        raise ValueError("beta_w_partials: XT (G, c) required on the device")
+    for name, t in (("XT", XT), ("HT3", HT3), ("W3", W3)):
+        _bp_check(name, t, dev)
+    if active is not None and (active.dtype != torch.int32 or active.numel() < R
+                               or not active.is_contiguous()):
+        raise ValueError("active: contiguous int32 with >= R entries")
+    if panels is None:
+        panels = beta_panels(HT3)
+    mode = beta_mode(beta)
+    if splits is None:
+        units = -(-G // int(_hip.bp_strip_cols(K))) * R
+        splits = max(1, min(16, -(-2048 // max(1, units))))
+    n_split = int(_hip.bp_splits(c, int(splits)))
+    num = torch.empty((n_split, R, K, G), dtype=torch.float32, device=dev)
+    den = torch.empty_like(num) if mode != 0 else None
+    _hip.bp_run(1, mode, XT.data_ptr(), XT.stride(0), panels.data_ptr(), panels.stride(0),
+                W3.data_ptr(), W3.stride(0), W3.stride(1), K, G, c, R, n_split, float(beta),
+                float(eps), num.data_ptr(), den.data_ptr() if den is not None else 0, 1, 0, 0,
+                0, 0.0, 0.0, 1.0, 0.0, 0, 0, 0, 0, 0, 0,
+                active.data_ptr() if active is not None else 0, 0, _stream_ptr(HT3))
+    return num, den
+
+
 # ----------------------------------------------------------------------------- gram
 def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
          active: torch.Tensor | None = None) -> torch.Tensor:

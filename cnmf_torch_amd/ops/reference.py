@@ -228,6 +228,53 @@ def beta_update_h(X, HT3, W3, beta, eps, l1=0.0, l2=0.0, gamma=1.0, act=None, to
             iters[:R] += live.to(iters.dtype)
 
 
+def beta_h_block(X, HT3, W3, beta, eps, nsteps, l1=0.0, l2=0.0, gamma=1.0, act=None, tol=None,
+                 iters=None, conv_mode=1, hstate=None, loss_entry=False):
+    """Reference of the multi-step usage solve block (beta_planes.hip, side 0): ``nsteps``
+    MU steps of the live replicates, then the stopping rule: conv_mode 1 compares the
+    beta-divergence after the block with the one before it (``loss_entry``: evaluated
+    here; else the value recorded in ``hstate`` by the previous block); conv_mode 0 reads
+    the relative change of the block's last step."""
+    R = HT3.shape[0]
+    live = torch.ones(R, dtype=torch.bool, device=HT3.device) if act is None else (act[:R] != 0)
+    rule = tol is not None
+    f_entry = None
+    if rule and conv_mode == 1 and loss_entry and nsteps > 0:
+        f_entry = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
+    dn = hn = None
+    for s in range(nsteps):
+        num, den, _ = beta_contract(0, X, HT3, W3, beta, eps, True, False, act)
+        if den is None:
+            den = W3.sum(dim=2, keepdim=True)
+        d = den + l1 + l2 * HT3
+        d = torch.where(d == 0, torch.full_like(d, eps), d)
+        delta = num / d
+        if gamma != 1.0:
+            delta = delta ** gamma
+        delta = torch.where(live.view(R, 1, 1), delta, torch.ones_like(delta))
+        if s == nsteps - 1 and rule and conv_mode == 0:
+            dn = torch.linalg.vector_norm((HT3 * (delta - 1.0)).double(), dim=(1, 2))
+            hn = torch.linalg.vector_norm(HT3.double(), dim=(1, 2))
+        HT3.mul_(delta)
+    if not rule:
+        return
+    if conv_mode == 1:
+        f_exit = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
+        hs = hstate.view(-1, 2)[:R]
+        f_prev = f_entry if loss_entry else hs[:, 0]
+        checked = torch.full_like(live, bool(loss_entry)) | (hs[:, 1] > 0)
+        stop = live & checked & ((f_prev - f_exit).abs() <= tol * f_prev.abs())
+        hs[:, 0] = torch.where(live, f_exit, hs[:, 0])
+        hs[:, 1] = torch.where(live, hs[:, 1] + 1, hs[:, 1])
+    elif nsteps > 0:
+        stop = live & (dn / (hn + eps) < tol)
+    else:
+        stop = torch.zeros_like(live)
+    act[:R][stop] = 0
+    if iters is not None:
+        iters[:R] += live.to(iters.dtype) * int(nsteps)
+
+
 def beta_w_update(W3, num, den, hsum, An, Ad, an_out, dn_out, beta, gamma, l1, l2, eps, tol,
                   act, iters=None):
     """Reference of the anchored online spectra step (beta_mu.hip beta_w_update_kernel)."""

@@ -101,6 +101,34 @@ PYBIND11_MODULE(_hip, m) {
                 "beta_w_update");
         });
 
+  m.def("bp_max_k", []() { return cnmf_bp_max_k(); });
+  m.def("bp_panel_elems", [](int K, int L) { return cnmf_bp_panel_elems(K, L); });
+  m.def("bp_strip_cols", [](int K) { return cnmf_bp_strip_cols(K); });
+  m.def("bp_splits", [](int Ls, int splits) { return cnmf_bp_splits(Ls, splits); });
+  m.def("bp_panels",
+        [](uintptr_t F, long long f_rs, long long ldf, int K, int L, int R, uintptr_t out,
+           long long out_rs, uintptr_t stream) {
+          check(cnmf_bp_panels(P<const float>(F), f_rs, ldf, K, L, R, P<unsigned short>(out),
+                               out_rs, reinterpret_cast<hipStream_t>(stream)),
+                "bp_panels");
+        });
+  m.def("bp_run",
+        [](int side, int mode, uintptr_t X, long long ldx, uintptr_t panel, long long panel_rs,
+           uintptr_t F, long long f_rs, long long ldf, int K, int Lf, int Ls, int R, int splits,
+           float beta, float eps, uintptr_t num, uintptr_t den, int nsteps, int loss_entry,
+           int loss_exit, uintptr_t den_vec, float l1, float l2, float gamma, float tol,
+           int conv_mode, uintptr_t hstate, uintptr_t part, uintptr_t counter, uintptr_t act,
+           uintptr_t iters, uintptr_t active, uintptr_t loss, uintptr_t stream) {
+          check(cnmf_bp_run(side, mode, P<const float>(X), ldx, P<const unsigned short>(panel),
+                            panel_rs, P<float>(F), f_rs, ldf, K, Lf, Ls, R, splits, beta, eps,
+                            P<float>(num), P<float>(den), nsteps, loss_entry, loss_exit,
+                            P<const float>(den_vec), l1, l2, gamma, tol, conv_mode,
+                            P<double>(hstate), P<double>(part), P<int>(counter), P<int>(act),
+                            P<int>(iters), P<const int>(active), P<double>(loss),
+                            reinterpret_cast<hipStream_t>(stream)),
+                "bp_run");
+        });
+
   m.def("pairdist", [](uintptr_t A, long long lda, uintptr_t B, long long ldb, uintptr_t na,
                        uintptr_t nb, int n, int mm, int kdim, uintptr_t D, long long ldd, int same,
                        int squared, uintptr_t stream) {

@@ -1,0 +1,696 @@
+// Fused beta-divergence MU on the bf16 matrix cores, fp32-accurate through split operands
+// (gfx950 / CDNA4), replicate-batched.  The hot loop of online/batch KL and IS NMF
+// (sklearn/decomposition/_nmf.py:526-728 is the math nmf-torch
+// runs as three eager ops per MU step: h@W, x/(hW), (.)@W^T).
+//
+// One workgroup owns one replicate and a strip of "fixed-axis" columns (cells on the
+// usage side H, genes on the spectra side W) and streams the other factor -- the
+// "streamed" operand, reduced over -- through LDS in chunks of 64 rows:
+//
+//   P   = S^T F + eps            (Ls x cols, never in memory: two 16 x 16 accumulator tiles
+//                                 per 32 streamed rows and 16 columns)
+//   Q   = X * P^(beta-2)         D = P^(beta-1)                      (VALU, registers)
+//   num = S Q   (K x cols)       den = S D   (beta != 1; KL: den = S 1, a host vector)
+//
+// H side: S = W (K x G), F = H^T, X as stored (cells x genes); W side: S = H^T of the
+// chunk, F = W, X^T.  Both products run on v_mfma_f32_16x16x32_bf16:
+//
+// * P is EXACT to fp32 rounding: every fp32 value v splits into three bf16 planes
+//   v = v0 + v1 + v2 (each residual exact), and the six plane products with i + j <= 2,
+//   {S0F0, S0F1, S1F0, S0F2, S1F1, S2F0}, are packed along the 32-deep MFMA reduction:
+//   slot s = t*K + k of term t, so K <= 10 costs two MFMAs per 16 x 16 tile (fp32 MFMA:
+//   three of twice the cycles).  The S planes come pre-arranged ("panels", built once per
+//   factor update by bp_panel_kernel), the F planes are built in registers once per step.
+// * num = S Q: the P accumulator of lane (q, m) holds streamed rows 4q+i (+16) of column
+//   m -- exactly the B-operand fragment of a 32-deep product over those rows, so Q goes
+//   from the accumulator through the VALU straight into the next MFMA, no lane movement
+//   (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand"); the
+//   S panel stores its columns in the matching permuted order.  Q splits into two bf16
+//   planes in registers (v_cvt_pk_bf16_f32), S into two: S0Q0 + S0Q1 + S1Q0 leaves
+//   <= 3 * 2^-16 relative per term, with random sign -- inside the fp32 accumulation
+//   error of the 2000-long reduction (the split-GEMM argument of gemm_planes.hip).
+//
+// The H-side kernel runs `nsteps` MU steps per launch: every workgroup's cells only
+// depend on their own usages and on W, so the steps need no cross-workgroup
+// synchronisation; the updated usages go back into the B-operand planes through a small
+// per-wave LDS exchange.  The block-objective stopping rule (beta-divergence of the chunk
+// every `nsteps` steps) is decided by the last-arriving workgroup of the replicate.  One
+// launch thus replaces `check_every` launches of the first-generation kernel
+// (beta_mu.hip), and the loss is only evaluated where the rule reads it.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "common.h"
+
+namespace cnmf {
+
+typedef short bp_v8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bp_b8 __attribute__((ext_vector_type(8)));
+typedef float bp_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int bp_u4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBpCH = 64;          // streamed rows per panel chunk (two 32-row blocks)
+constexpr int kBpWaves = 4;        // waves per workgroup
+constexpr int kBpThreads = 64 * kBpWaves;
+constexpr int kBpNS = kBpCH + 8;   // N-panel row stride (bf16 elements)
+
+__host__ __device__ constexpr int bp_np(int K) { return (6 * K + 31) / 32; }
+__host__ __device__ constexpr int bp_t(int K) { return (K + 15) / 16; }
+__host__ __device__ constexpr int bp_ps(int NP) { return 32 * NP + 8; }  // P-panel row stride
+// chunk stride (bf16 elements), padded to whole 16-byte pieces per thread so the staging
+// loads are unconditional (the tail of a chunk is never written nor read by the MFMAs)
+__host__ __device__ constexpr int bp_chunk(int NP, int T) {
+  return (kBpCH * bp_ps(NP) + 2 * 16 * T * kBpNS + kBpThreads * 8 - 1) / (kBpThreads * 8) *
+         (kBpThreads * 8);
+}
+__host__ __device__ constexpr int bp_ct(int T) { return 2; }  // column tiles per wave
+__host__ __device__ constexpr int bp_ks(int T) { return 16 * T + 1; }     // exchange stride
+
+enum BpMode { kBpKL = 0, kBpIS = 1, kBpGeneral = 2 };
+
+// plane of the streamed (a) / fixed (b) operand in product term t (0..5)
+__device__ __forceinline__ int bp_pa(int t) { return (0x210100 >> (4 * t)) & 15; }
+__device__ __forceinline__ int bp_pb(int t) { return (0x012010 >> (4 * t)) & 15; }
+
+__device__ __forceinline__ unsigned short bp_bits(__bf16 h) {
+  return __builtin_bit_cast(unsigned short, h);
+}
+
+// v = p0 + p1 + p2 exactly (finite v, away from the subnormal range)
+__device__ __forceinline__ void bp_split3(float v, unsigned short& p0, unsigned short& p1,
+                                          unsigned short& p2) {
+  const __bf16 h0 = (__bf16)v;
+  const float r1 = v - (float)h0;
+  const __bf16 h1 = (__bf16)r1;
+  const float r2 = r1 - (float)h1;
+  p0 = bp_bits(h0);
+  p1 = bp_bits(h1);
+  p2 = bp_bits((__bf16)r2);
+}
+
+// -------------------------------------------------------------------------------- panels
+// Per replicate r the panel buffer is nchunks x bp_chunk(NP, T) bf16: chunk c covers
+// streamed rows [64c, 64c + 64), zero beyond L:
+//   P panel  [64 rows][bp_ps(NP)]:  row l, slot t*K + k = plane bp_pa(t) of F[k][l]
+//   N panel  [2 planes][16T rows k][kBpNS]: plane p of F[k][l] at the permuted column of l
+//            (within a 32-row block: offset o = 16h + 4q + i  ->  8q + 4h + i)
+__global__ void __launch_bounds__(256) bp_panel_kernel(const float* __restrict__ F,
+                                                       long long f_rs, long long ldf, int K,
+                                                       int L, int nchunks, int R, int NP,
+                                                       int T, unsigned short* __restrict__ out,
+                                                       long long out_rs) {
+  const long long per = (long long)nchunks * kBpCH;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= per * R) return;
+  const int r = (int)(idx / per), l = (int)(idx - (long long)r * per);
+  const int PS = bp_ps(NP), CE = bp_chunk(NP, T);
+  unsigned short* ch = out + r * out_rs + (long long)(l / kBpCH) * CE;
+  const int lr = l % kBpCH, o = lr & 31;
+  unsigned short* prow = ch + lr * PS;
+  unsigned short* np0 = ch + kBpCH * PS;
+  unsigned short* np1 = np0 + 16 * T * kBpNS;
+  const int pos = (lr & 32) + ((o & 15) >> 2) * 8 + (o >> 4) * 4 + (o & 3);
+  const float* f = F + r * f_rs + l;
+  for (int k = 0; k < 16 * T; ++k) {
+    unsigned short a0 = 0, a1 = 0, a2 = 0;
+    if (k < K && l < L) bp_split3(f[(long long)k * ldf], a0, a1, a2);
+    if (k < K) {
+      prow[k] = a0;
+      prow[K + k] = a0;
+      prow[2 * K + k] = a1;
+      prow[3 * K + k] = a0;
+      prow[4 * K + k] = a1;
+      prow[5 * K + k] = a2;
+    }
+    np0[k * kBpNS + pos] = a0;
+    np1[k * kBpNS + pos] = a1;
+  }
+  for (int s = 6 * K; s < PS; ++s) prow[s] = 0;
+}
+
+// ------------------------------------------------------------------------------ main op
+struct BpParams {
+  const float* X;              // element (fixed col c, streamed row j) at X[c * ldx + j]
+  long long ldx;
+  int xvec;                    // ldx % 4 == 0 and X 16-byte aligned: float4 loads
+  const unsigned short* panel; // streamed operand panels, replicate r at panel + r*panel_rs
+  long long panel_rs;
+  float* F;                    // fixed operand, replicate r: F + r*f_rs, row k stride ldf
+  long long f_rs, ldf;
+  int K, Lf, Ls, R;
+  int n_strips, splits, chunks_per_split;
+  float beta, eps;
+  float* num;                  // side W: (splits, R, K, Lf)
+  float* den;                  //   same (beta != 1)
+  int nsteps;                  // side H: MU steps this launch (0: loss only)
+  int loss_entry, loss_exit;   // evaluate D(X | P) before the first / after the last step
+  const float* den_vec;        // KL: (R, K) row sums of W
+  float l1, l2, gamma, tol;
+  int conv_mode;               // 0: |dh|/|h| of the last step < tol; 1: block objective
+  double* hstate;              // (R, 2): objective at the last check, checks done
+  double* part;                // (R, n_strips, 4) partials: |dh|^2, |h|^2, f_entry, f_exit
+  int* counter;                // (R) arrival counters, zero between launches
+  int* act;                    // (R) active flags cleared by the stopping rule
+  int* iters;                  // (R) MU steps taken
+  const int* active;           // gate (0: workgroup exits)
+  double* loss;                // loss-only launches: (R, n_strips) partial objectives
+};
+
+template <int MODE>
+__device__ __forceinline__ void bp_terms(float x, float p, float beta, float& q, float& d) {
+  if (MODE == kBpKL) {
+    q = x * __builtin_amdgcn_rcpf(p);
+    d = 1.f;
+  } else if (MODE == kBpIS) {
+    const float r = __builtin_amdgcn_rcpf(p);
+    d = r;
+    q = x * r * r;
+  } else {
+    const float lp = __builtin_amdgcn_logf(p);  // log2
+    d = __builtin_amdgcn_exp2f((beta - 1.f) * lp);
+    q = x * __builtin_amdgcn_exp2f((beta - 2.f) * lp);
+  }
+}
+
+// D_beta term of (x, p); q = x P^(beta-2) and d = P^(beta-1) as bp_terms left them
+template <int MODE>
+__device__ __forceinline__ float bp_loss(float x, float p, float q, float d, float beta,
+                                         float eps) {
+  if (MODE == kBpKL) {
+    const float t = x > 0.f ? x * __logf(q) : 0.f;   // q = x / p
+    return t - x + p;
+  } else if (MODE == kBpIS) {
+    const float r = fmaxf(x * d, eps);                // d = 1 / p
+    return r - __logf(r) - 1.f;
+  } else {
+    return (__powf(x, beta) + (beta - 1.f) * __powf(p, beta) - beta * x * __powf(p, beta - 1.f)) /
+           (beta * (beta - 1.f));
+  }
+}
+
+// 8 fp32 values -> two bf16 planes (hi, residual)
+__device__ __forceinline__ void bp_split2(const float (&v)[8], bp_v8& b0, bp_v8& b1) {
+  bp_b8 h, l;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    h[e] = (__bf16)v[e];
+    l[e] = (__bf16)(v[e] - (float)h[e]);
+  }
+  b0 = __builtin_bit_cast(bp_v8, h);
+  b1 = __builtin_bit_cast(bp_v8, l);
+}
+
+__device__ __forceinline__ bp_f4 bp_mfma(bp_v8 a, bp_v8 b, bp_f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// x[col][j .. j+3] (zero beyond Ls / for an invalid column)
+__device__ __forceinline__ void bp_load4(const float* __restrict__ row, int j, int Ls, bool ok,
+                                         int xvec, float* out) {
+  if (ok && xvec && j + 3 < Ls) {
+    const float4 v = *reinterpret_cast<const float4*>(row + j);
+    out[0] = v.x; out[1] = v.y; out[2] = v.z; out[3] = v.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[i] = (ok && j + i < Ls) ? row[j + i] : 0.f;
+  }
+}
+
+template <int NP, int T, int MODE, bool UPD>
+__global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
+  constexpr int CT = bp_ct(T);
+  constexpr int PS = bp_ps(NP);
+  constexpr int CE = bp_chunk(NP, T);
+  constexpr int PIECES = CE * 2 / 16;
+  constexpr int PER_T = (PIECES + kBpThreads - 1) / kBpThreads;
+  constexpr int COLS = kBpWaves * CT * 16;
+  constexpr int KS = bp_ks(T);
+  static_assert(PIECES == PER_T * kBpThreads, "chunk must be whole pieces per thread");
+  extern __shared__ __attribute__((aligned(16))) unsigned char bp_smem[];
+  __shared__ double sred[4 * kBpWaves];
+  __shared__ int s_last;
+
+  // XCD-aware unit map: the replicates of one unit (strip, split) run back to back on one
+  // XCD, so its X rows stay in that L2
+  const int b = blockIdx.x, xcd = b & 7, local = b >> 3;
+  const int rep = local % p.R;
+  const int unit = (local / p.R) * 8 + xcd;
+  if (unit >= p.n_strips * p.splits) return;
+  if (p.active && p.active[rep] == 0) return;
+  const int strip = unit % p.n_strips, split = unit / p.n_strips;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4, m = lane & 15;
+  const int K = p.K;
+  const int col_w = strip * COLS + wave * CT * 16;
+  float* __restrict__ F = p.F + (long long)rep * p.f_rs;
+  const unsigned short* __restrict__ pan = p.panel + (long long)rep * p.panel_rs;
+  const int nch_all = (p.Ls + kBpCH - 1) / kBpCH;
+  const int c_begin = split * p.chunks_per_split;
+  const int c_end = min(nch_all, c_begin + p.chunks_per_split);
+  unsigned short* sbuf = reinterpret_cast<unsigned short*>(bp_smem);
+  float* sx = reinterpret_cast<float*>(bp_smem + 2 * CE * 2) + wave * (CT * 16) * KS;
+
+  bool cok[CT];
+  const float* xrow[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int col = col_w + 16 * ct + m;
+    cok[ct] = col < p.Lf;
+    xrow[ct] = p.X + (long long)(cok[ct] ? col : 0) * p.ldx;
+  }
+
+  // fixed operand in the accumulator layout: hc[ct][t][i] = F[16t + 4q + i][col]
+  bp_f4 hc[CT][T];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 16 * t + 4 * q + i;
+        hc[ct][t][i] = (k < K && cok[ct]) ? F[(long long)k * p.ldf + col_w + 16 * ct + m] : 0.f;
+      }
+
+  // B-operand planes of the fixed operand: slot s = 32j + 8q + e holds plane bp_pb(s / K)
+  // of F[s % K][col]; rebuilt through the wave's LDS exchange rows after every update
+  bp_v8 freg[CT][NP];
+  auto build_freg = [&]() {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sx[(16 * ct + m) * KS + 16 * t + 4 * q + i] = hc[ct][t][i];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int s0 = 32 * j + 8 * q;
+      int tt = s0 / K, kk = s0 - tt * K;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int pl = bp_pb(tt < 6 ? tt : 0);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          unsigned short a0 = 0, a1 = 0, a2 = 0;
+          if (tt < 6) bp_split3(sx[(16 * ct + m) * KS + kk], a0, a1, a2);
+          freg[ct][j][e] = (short)(pl == 0 ? a0 : (pl == 1 ? a1 : a2));
+        }
+        if (++kk == K) { kk = 0; ++tt; }
+      }
+    }
+    __syncthreads();
+  };
+  build_freg();
+
+  const int n_it = UPD ? p.nsteps + (p.loss_exit ? 1 : 0) : 1;
+  double f_entry = 0.0, f_exit = 0.0;
+  float d2 = 0.f, o2 = 0.f;
+  // panel chunk c -> registers -> LDS buffer bi (plain loads: the compiler counts them,
+  // so waiting for this block's X loads leaves the next chunk's panels in flight)
+  bp_u4 stg[PER_T];
+  auto load_chunk = [&](int c) {
+    const bp_u4* src = reinterpret_cast<const bp_u4*>(pan + (long long)c * CE);
+#pragma unroll
+    for (int u = 0; u < PER_T; ++u) stg[u] = src[u * kBpThreads + tid];
+  };
+  auto store_chunk = [&](int bi) {
+    bp_u4* dst = reinterpret_cast<bp_u4*>(sbuf + bi * CE);
+#pragma unroll
+    for (int u = 0; u < PER_T; ++u) dst[u * kBpThreads + tid] = stg[u];
+  };
+
+  for (int it = 0; it < n_it; ++it) {
+    const bool want_num = !UPD || it < p.nsteps;
+    const bool want_loss = UPD && ((it == 0 && p.loss_entry && p.nsteps > 0) || it == p.nsteps);
+    bp_f4 num[CT][T], den[CT][T];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        num[ct][t] = bp_f4{0.f, 0.f, 0.f, 0.f};
+        den[ct][t] = bp_f4{0.f, 0.f, 0.f, 0.f};
+      }
+    float lsum = 0.f;
+
+    if (c_begin < c_end) {
+      load_chunk(c_begin);
+      store_chunk(0);
+    }
+    __syncthreads();
+    // X of block b (32 streamed rows) for this lane's columns: float4 loads while the
+    // block is inside X (invalid columns read row 0 -- their F is zero and their outputs
+    // are discarded), guarded scalar loads at the tail
+    auto load_x = [&](int b, float (&dst)[CT][8]) {
+      const int j0 = (c_begin + (b >> 1)) * kBpCH + (b & 1) * 32;
+      if (p.xvec && j0 + 32 <= p.Ls) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const bp_f4 v0 = *reinterpret_cast<const bp_f4*>(xrow[ct] + j0 + 4 * q);
+          const bp_f4 v1 = *reinterpret_cast<const bp_f4*>(xrow[ct] + j0 + 16 + 4 * q);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            dst[ct][i] = v0[i];
+            dst[ct][4 + i] = v1[i];
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          bp_load4(xrow[ct], j0 + 4 * q, p.Ls, cok[ct], 0, &dst[ct][0]);
+          bp_load4(xrow[ct], j0 + 16 + 4 * q, p.Ls, cok[ct], 0, &dst[ct][4]);
+        }
+      }
+    };
+    // one 32-row block of the streamed axis: P tiles, elementwise terms, loss, numerator
+    // (WN, WL: numerator / loss wanted, as compile-time constants so that the hot
+    // variant -- numerator only -- is one straight-line block over both column tiles)
+    auto compute_block = [&](auto WN, auto WL, const float (&xv)[CT][8], int blk,
+                             const unsigned short* pb, int j0) {
+      constexpr bool kNum = decltype(WN)::value, kLoss = decltype(WL)::value;
+      const unsigned short* nb0 = pb + kBpCH * PS;
+      const unsigned short* nb1 = nb0 + 16 * T * kBpNS;
+        bp_v8 ap[2][NP];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int jj = 0; jj < NP; ++jj)
+            ap[a][jj] = *reinterpret_cast<const bp_v8*>(pb + (blk * 32 + 16 * a + m) * PS +
+                                                         32 * jj + 8 * q);
+        bp_v8 an0[T], an1[T];
+        if (kNum) {
+#pragma unroll
+          for (int t = 0; t < T; ++t) {
+            const int off = (16 * t + m) * kBpNS + blk * 32 + 8 * q;
+            an0[t] = *reinterpret_cast<const bp_v8*>(nb0 + off);
+            an1[t] = *reinterpret_cast<const bp_v8*>(nb1 + off);
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          bp_f4 P0 = {p.eps, p.eps, p.eps, p.eps}, P1 = P0;
+#pragma unroll
+          for (int jj = 0; jj < NP; ++jj) {
+            P0 = bp_mfma(ap[0][jj], freg[ct][jj], P0);
+            P1 = bp_mfma(ap[1][jj], freg[ct][jj], P1);
+          }
+          float qv[8], dv[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            bp_terms<MODE>(xv[ct][e], e < 4 ? P0[e] : P1[e - 4], p.beta, qv[e], dv[e]);
+          if (kLoss) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int j = j0 + (e >> 2) * 16 + 4 * q + (e & 3);
+              const float t = bp_loss<MODE>(xv[ct][e], e < 4 ? P0[e] : P1[e - 4], qv[e],
+                                            dv[e], p.beta, p.eps);
+              lsum += (cok[ct] && j < p.Ls) ? t : 0.f;
+            }
+          }
+          if (kNum) {
+            bp_v8 b0, b1;
+            bp_split2(qv, b0, b1);
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+              num[ct][t] = bp_mfma(an0[t], b0, num[ct][t]);
+              num[ct][t] = bp_mfma(an0[t], b1, num[ct][t]);
+              num[ct][t] = bp_mfma(an1[t], b0, num[ct][t]);
+            }
+            if (MODE != kBpKL) {
+              bp_split2(dv, b0, b1);
+#pragma unroll
+              for (int t = 0; t < T; ++t) {
+                den[ct][t] = bp_mfma(an0[t], b0, den[ct][t]);
+                den[ct][t] = bp_mfma(an0[t], b1, den[ct][t]);
+                den[ct][t] = bp_mfma(an1[t], b0, den[ct][t]);
+              }
+            }
+          }
+        }
+    };
+    // software pipeline over the chunks: block 0's X (xa) arrived during the previous
+    // chunk; block 1's X (xb), the next chunk's block-0 X and panels load behind the
+    // compute (the last chunk reloads itself into the idle buffer: no branch around the
+    // staging registers)
+    const int nblk = 2 * (c_end - c_begin);
+    float xa[CT][8], xb[CT][8];
+    if (nblk > 0) load_x(0, xa);
+    using kT = std::integral_constant<bool, true>;
+    using kF = std::integral_constant<bool, false>;
+    for (int c = c_begin; c < c_end; ++c) {
+      const int i2 = 2 * (c - c_begin), bi = (c - c_begin) & 1;
+      const unsigned short* pb = sbuf + bi * CE;
+      load_x(i2 + 1, xb);
+      load_chunk(min(c + 1, c_end - 1));
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && i2 + 2 < nblk) load_x(i2 + 2, xa);
+        const float(&xv)[CT][8] = h == 0 ? xa : xb;
+        const int j0 = c * kBpCH + 32 * h;
+        if (want_num && !want_loss) compute_block(kT{}, kF{}, xv, h, pb, j0);
+        else if (want_num) compute_block(kT{}, kT{}, xv, h, pb, j0);
+        else compute_block(kF{}, kT{}, xv, h, pb, j0);
+      }
+      store_chunk(bi ^ 1);
+      __syncthreads();
+    }
+
+    if (want_loss) {
+      if (it == p.nsteps) f_exit += (double)lsum;
+      else f_entry += (double)lsum;
+    }
+    if (UPD && want_num) {
+      const bool last = it + 1 == p.nsteps;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int k = 16 * t + 4 * q + i;
+            if (k < K && cok[ct]) {
+              const float h = hc[ct][t][i];
+              float dn = (MODE == kBpKL) ? p.den_vec[(long long)rep * K + k] : den[ct][t][i];
+              dn = dn + p.l1 + p.l2 * h;
+              if (dn == 0.f) dn = p.eps;
+              float delta = num[ct][t][i] / dn;
+              if (p.gamma != 1.f) delta = __powf(delta, p.gamma);
+              const float hn = h * delta;
+              if (last) {
+                d2 = fmaf(hn - h, hn - h, d2);
+                o2 = fmaf(h, h, o2);
+              }
+              hc[ct][t][i] = hn;
+            }
+          }
+      if (it + 1 < n_it) build_freg();
+    }
+    if (!UPD) {
+      const long long base = ((long long)split * p.R + rep) * K * p.Lf;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int k = 16 * t + 4 * q + i;
+            if (k < K && cok[ct]) {
+              const long long o = base + (long long)k * p.Lf + col_w + 16 * ct + m;
+              p.num[o] = num[ct][t][i];
+              if (MODE != kBpKL) p.den[o] = den[ct][t][i];
+            }
+          }
+    }
+  }
+
+  if (!UPD) return;
+  if (p.nsteps > 0) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 16 * t + 4 * q + i;
+          if (k < K && cok[ct]) F[(long long)k * p.ldf + col_w + 16 * ct + m] = hc[ct][t][i];
+        }
+  }
+  // workgroup partials: |dh|^2, |h|^2 (last step), objective at entry / exit
+  {
+    const double v0 = wave_sum((double)d2), v1 = wave_sum((double)o2);
+    const double v2 = wave_sum(f_entry), v3 = wave_sum(f_exit);
+    if (lane == 0) {
+      sred[wave * 4 + 0] = v0;
+      sred[wave * 4 + 1] = v1;
+      sred[wave * 4 + 2] = v2;
+      sred[wave * 4 + 3] = v3;
+    }
+    __syncthreads();
+  }
+  if (p.loss && tid == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < kBpWaves; ++w) tot += sred[w * 4 + 3];
+    p.loss[(long long)rep * p.n_strips + strip] = tot;
+  }
+  if (!p.part) return;
+  if (tid == 0) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int w = 0; w < kBpWaves; ++w)
+      for (int v = 0; v < 4; ++v) acc[v] += sred[w * 4 + v];
+    // publish (cdna_hip_programming.md G16): plain stores -> drain -> agent release ->
+    // drain -> arrival counter
+    double* pp = p.part + ((long long)rep * p.n_strips + strip) * 4;
+    for (int v = 0; v < 4; ++v) pp[v] = acc[v];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(p.counter + rep, 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == p.n_strips - 1);
+  }
+  __syncthreads();
+  if (s_last && tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double tot[4] = {0.0, 0.0, 0.0, 0.0};
+    const double* pr = p.part + (long long)rep * p.n_strips * 4;
+    for (int s2 = 0; s2 < p.n_strips; ++s2)
+      for (int v = 0; v < 4; ++v)
+        tot[v] += __hip_atomic_load(pr + 4 * s2 + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (p.conv_mode == 1) {
+      double* hs = p.hstate + 2 * (long long)rep;
+      const double f_prev = p.loss_entry ? tot[2] : hs[0];
+      if ((p.loss_entry || hs[1] > 0.0) && fabs(f_prev - tot[3]) <= (double)p.tol * fabs(f_prev))
+        p.act[rep] = 0;
+      hs[0] = tot[3];
+      hs[1] = hs[1] + 1.0;
+    } else if (p.nsteps > 0) {
+      const double rel = sqrt(tot[0]) / (sqrt(tot[1]) + (double)p.eps);
+      if (rel < (double)p.tol) p.act[rep] = 0;
+    }
+    if (p.iters) p.iters[rep] += p.nsteps;
+    p.counter[rep] = 0;
+  }
+}
+
+template <int NP, int T, int MODE, bool UPD>
+hipError_t bp_launch(const BpParams& p, hipStream_t s) {
+  constexpr int CT = bp_ct(T);
+  const size_t lds = (size_t)2 * bp_chunk(NP, T) * 2 +
+                     (size_t)kBpWaves * CT * 16 * bp_ks(T) * sizeof(float);
+  static bool attr_done = false;
+  if (!attr_done) {
+    const hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&bp_kernel<NP, T, MODE, UPD>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr_done = true;
+  }
+  const int units = p.n_strips * p.splits;
+  const int per_xcd = (units + 7) / 8;
+  const dim3 grid((unsigned)(per_xcd * p.R * 8));
+  hipLaunchKernelGGL((bp_kernel<NP, T, MODE, UPD>), grid, dim3(kBpThreads), lds, s, p);
+  return hipGetLastError();
+}
+
+template <int MODE, bool UPD>
+hipError_t bp_launch_k(const BpParams& p, hipStream_t s) {
+  switch (bp_np(p.K)) {
+    case 1: return bp_launch<1, 1, MODE, UPD>(p, s);
+    case 2: return bp_launch<2, 1, MODE, UPD>(p, s);
+    case 3: return bp_launch<3, 1, MODE, UPD>(p, s);
+    case 4: return bp_launch<4, 2, MODE, UPD>(p, s);
+    case 5: return bp_launch<5, 2, MODE, UPD>(p, s);
+    case 6: return bp_launch<6, 2, MODE, UPD>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <bool UPD>
+hipError_t bp_launch_mode(int mode, const BpParams& p, hipStream_t s) {
+  switch (mode) {
+    case kBpKL: return bp_launch_k<kBpKL, UPD>(p, s);
+    case kBpIS: return bp_launch_k<kBpIS, UPD>(p, s);
+    case kBpGeneral: return bp_launch_k<kBpGeneral, UPD>(p, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace cnmf
+
+extern "C" int cnmf_bp_max_k() { return 32; }
+
+// bf16 elements of one replicate's panel over a streamed axis of length L
+extern "C" long long cnmf_bp_panel_elems(int K, int L) {
+  if (K < 1 || K > 32) return -1;
+  const int NP = cnmf::bp_np(K), T = cnmf::bp_t(K);
+  return (long long)((L + cnmf::kBpCH - 1) / cnmf::kBpCH) * cnmf::bp_chunk(NP, T);
+}
+
+// fixed-axis columns per workgroup strip
+extern "C" int cnmf_bp_strip_cols(int K) {
+  return cnmf::kBpWaves * cnmf::bp_ct(cnmf::bp_t(K)) * 16;
+}
+
+extern "C" hipError_t cnmf_bp_panels(const float* F, long long f_rs, long long ldf, int K, int L,
+                                     int R, unsigned short* out, long long out_rs,
+                                     hipStream_t stream) {
+  if (R <= 0 || L <= 0) return hipSuccess;
+  if (K < 1 || K > 32) return hipErrorInvalidValue;
+  const int NP = cnmf::bp_np(K), T = cnmf::bp_t(K);
+  const int nchunks = (L + cnmf::kBpCH - 1) / cnmf::kBpCH;
+  const long long n = (long long)R * nchunks * cnmf::kBpCH;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  hipLaunchKernelGGL(cnmf::bp_panel_kernel, grid, dim3(256), 0, stream, F, f_rs, ldf, K, L,
+                     nchunks, R, NP, T, out, out_rs);
+  return hipGetLastError();
+}
+
+// side 0 (H, fused update; nsteps 0 = loss only into `loss`), side 1 (W, num/den partials)
+extern "C" hipError_t cnmf_bp_run(
+    int side, int mode, const float* X, long long ldx, const unsigned short* panel,
+    long long panel_rs, float* F, long long f_rs, long long ldf, int K, int Lf, int Ls, int R,
+    int splits, float beta, float eps, float* num, float* den, int nsteps, int loss_entry,
+    int loss_exit, const float* den_vec, float l1, float l2, float gamma, float tol,
+    int conv_mode, double* hstate, double* part, int* counter, int* act, int* iters,
+    const int* active, double* loss, hipStream_t stream) {
+  if (R <= 0 || Lf <= 0) return hipSuccess;
+  if (K < 1 || K > 32 || Ls <= 0 || (side != 0 && side != 1)) return hipErrorInvalidValue;
+  cnmf::BpParams p;
+  p.X = X; p.ldx = ldx;
+  p.xvec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  p.panel = panel; p.panel_rs = panel_rs;
+  p.F = F; p.f_rs = f_rs; p.ldf = ldf;
+  p.K = K; p.Lf = Lf; p.Ls = Ls; p.R = R;
+  p.n_strips = (Lf + cnmf_bp_strip_cols(K) - 1) / cnmf_bp_strip_cols(K);
+  const int nch = (Ls + cnmf::kBpCH - 1) / cnmf::kBpCH;
+  if (side == 0) splits = 1;
+  splits = splits < 1 ? 1 : (splits > nch ? nch : splits);
+  p.chunks_per_split = (nch + splits - 1) / splits;
+  p.splits = (nch + p.chunks_per_split - 1) / p.chunks_per_split;
+  p.beta = beta; p.eps = eps;
+  p.num = num; p.den = den;
+  p.nsteps = nsteps; p.loss_entry = loss_entry; p.loss_exit = loss_exit;
+  p.den_vec = den_vec;
+  p.l1 = l1; p.l2 = l2; p.gamma = gamma; p.tol = tol;
+  p.conv_mode = conv_mode; p.hstate = hstate; p.part = part;
+  p.counter = counter; p.act = act; p.iters = iters; p.active = active; p.loss = loss;
+  if (side == 1) {
+    if (num == nullptr || (mode != cnmf::kBpKL && den == nullptr)) return hipErrorInvalidValue;
+    return cnmf::bp_launch_mode<false>(mode, p, stream);
+  }
+  if (nsteps < 0 || (mode == cnmf::kBpKL && nsteps > 0 && den_vec == nullptr) ||
+      (part != nullptr && (counter == nullptr || act == nullptr)) ||
+      (part != nullptr && conv_mode == 1 && hstate == nullptr) ||
+      (nsteps == 0 && loss == nullptr && part == nullptr))
+    return hipErrorInvalidValue;
+  return cnmf::bp_launch_mode<true>(mode, p, stream);
+}
+
+// splits actually used by a side-1 launch (partials buffer extent)
+extern "C" int cnmf_bp_splits(int Ls, int splits) {
+  const int nch = (Ls + cnmf::kBpCH - 1) / cnmf::kBpCH;
+  splits = splits < 1 ? 1 : (splits > nch ? nch : splits);
+  const int per = (nch + splits - 1) / splits;
+  return (nch + per - 1) / per;
+}

@@ -43,6 +43,21 @@ hipError_t cnmf_beta_w_update(int mode, float* W, long long w_rs, long long ldw,
                               float eps, float tol, float* part, int* counter, int* act,
                               int* iters, hipStream_t stream);
 
+int cnmf_bp_max_k();
+long long cnmf_bp_panel_elems(int K, int L);
+int cnmf_bp_strip_cols(int K);
+int cnmf_bp_splits(int Ls, int splits);
+hipError_t cnmf_bp_panels(const float* F, long long f_rs, long long ldf, int K, int L, int R,
+                          unsigned short* out, long long out_rs, hipStream_t stream);
+hipError_t cnmf_bp_run(int side, int mode, const float* X, long long ldx,
+                       const unsigned short* panel, long long panel_rs, float* F, long long f_rs,
+                       long long ldf, int K, int Lf, int Ls, int R, int splits, float beta,
+                       float eps, float* num, float* den, int nsteps, int loss_entry,
+                       int loss_exit, const float* den_vec, float l1, float l2, float gamma,
+                       float tol, int conv_mode, double* hstate, double* part, int* counter,
+                       int* act, int* iters, const int* active, double* loss,
+                       hipStream_t stream);
+
 hipError_t cnmf_pairdist(const double* A, long long lda, const double* B, long long ldb,
                          const double* na, const double* nb, int n, int m, int kdim, double* D,
                          long long ldd, int same, int squared, hipStream_t stream);

@@ -269,6 +269,83 @@ def test_beta_update_h_fused_matches_reference(beta):
     torch.testing.assert_close(h1.cpu().double(), h2, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("beta", [1.0, 0.0, 1.5])
+@pytest.mark.parametrize("K,N,G", [(3, 1037, 305), (10, 777, 320), (17, 300, 131),
+                                   (32, 129, 64)])
+def test_split_bf16_beta_kernels_match_fp64(beta, K, N, G):
+    """beta_planes.hip (split-bf16 MFMA: exact 6-term P, 3-term num/den) vs the float64
+    reference: loss-only pass, W-side partials (float4 and scalar X paths: ragged G/N),
+    and one fused usage step."""
+    g = torch.Generator().manual_seed(K + N)
+    R = 3
+    X = torch.rand((N, G), generator=g, dtype=torch.float64)
+    X[X < 0.3] = 0.0
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.05
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.05
+    dev = torch.device("cuda")
+    eps = 1e-10
+    Xg, Hg, Wg = X.float().to(dev), HT.float().to(dev), W.float().to(dev)
+    active = torch.tensor([1, 0, 1], dtype=torch.int32, device=dev)
+    # loss
+    ref_loss = reference.beta_contract(0, X, HT, W, beta, eps, False, True)[2]
+    got = ops.beta_loss(Xg, Hg, Wg, beta, eps)
+    torch.testing.assert_close(got.cpu(), ref_loss, rtol=2e-5, atol=1e-6)
+    # W-side partials, two split counts
+    rn, rd, _ = reference.beta_contract(1, X, HT, W, beta, eps, True, False)
+    XT = Xg.t().contiguous()
+    for splits in (1, 3):
+        num, den = ops.beta_w_partials(Xg, XT, Hg, Wg, beta, eps, active=active, splits=splits)
+        for r in (0, 2):
+            torch.testing.assert_close(num.sum(0)[r].cpu().double(), rn[r], rtol=5e-5,
+                                       atol=1e-5)
+            if beta != 1.0:
+                torch.testing.assert_close(den.sum(0)[r].cpu().double(), rd[r], rtol=5e-5,
+                                           atol=1e-5)
+        assert (den is None) == (beta == 1.0)
+    # one fused usage step, no rule: every replicate
+    h1 = Hg.clone()
+    ops.beta_h_block(Xg, h1, Wg, beta, eps, 1, gamma=1.0 if beta else 0.5)
+    h2 = HT.clone()
+    reference.beta_h_block(X, h2, W, beta, eps, 1, gamma=1.0 if beta else 0.5)
+    torch.testing.assert_close(h1.cpu().double(), h2, rtol=5e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("beta", [1.0, 0.0])
+@pytest.mark.parametrize("conv_mode", [1, 0])
+def test_split_bf16_h_block_rule_matches_reference(beta, conv_mode):
+    """Multi-step usage blocks with the on-device stopping rule (last-arriving workgroup):
+    iterate, flags, step counts and the block-objective state == the fp64 reference."""
+    g = torch.Generator().manual_seed(7)
+    R, K, N, G = 4, 10, 1500, 260
+    X = torch.rand((N, G), generator=g, dtype=torch.float64)
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.05
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.05
+    dev = torch.device("cuda")
+    act0 = torch.tensor([1, 1, 0, 1], dtype=torch.int32)
+    tol = 0.05 if conv_mode == 1 else 0.02
+    nsteps = 5 if conv_mode == 1 else 1
+    ref_h, ref_act = HT.clone(), act0.clone()
+    ref_it, ref_hs = torch.zeros(R, dtype=torch.int32), torch.zeros((R, 2), dtype=torch.float64)
+    gh, gact = HT.float().to(dev), act0.to(dev)
+    git, ghs = torch.zeros(R, dtype=torch.int32, device=dev), torch.zeros(
+        (R, 2), dtype=torch.float64, device=dev)
+    Xg, Wg = X.float().to(dev), W.float().to(dev)
+    pan = ops.beta_panels(Wg)
+    for blk in range(4):
+        kw = dict(gamma=1.0 if beta else 0.5, tol=tol, conv_mode=conv_mode,
+                  loss_entry=blk == 0)
+        reference.beta_h_block(X, ref_h, W, beta, 1e-10, nsteps, 0.01, 0.0, act=ref_act,
+                               iters=ref_it, hstate=ref_hs, **kw)
+        ops.beta_h_block(Xg, gh, Wg, beta, 1e-10, nsteps, 0.01, 0.0, act=gact, iters=git,
+                         hstate=ghs, panels=pan, **kw)
+    torch.testing.assert_close(gh.cpu().double(), ref_h, rtol=2e-4, atol=1e-5)
+    assert gact.cpu().tolist() == ref_act.tolist()
+    assert git.cpu().tolist() == ref_it.tolist()
+    if conv_mode == 1:
+        torch.testing.assert_close(ghs.cpu(), ref_hs, rtol=1e-4, atol=1e-6)
+    assert torch.equal(gh[2].cpu(), HT[2].float())           # inactive replicate untouched
+
+
 def test_pairwise_dist_and_knn_density():
     """f64 MFMA distance tiles + radix-select neighbour sums vs sklearn/numpy."""
     from sklearn.metrics import euclidean_distances
