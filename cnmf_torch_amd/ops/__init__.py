@@ -602,7 +602,7 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
                  iters: torch.Tensor | None = None, conv_mode: int = 1,
                  hstate: torch.Tensor | None = None, loss_entry: bool = False,
                  den_vec: torch.Tensor | None = None,
-                 panels: torch.Tensor | None = None) -> None:
+                 panels: torch.Tensor | None = None, xsum: float | None = None) -> None:
     """``nsteps`` fused beta-MU steps of the usages HT3 (R, K, N) in place against the
     spectra W3 (R, K, G) on rows X (N, G), in ONE launch (beta_planes.hip, side 0):
     HT3 *= (num / (den + l1 + l2 HT3))^gamma with num/den of the split-bf16 MFMA
@@ -611,7 +611,8 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
     before it (``loss_entry``: computed in this launch; else the value ``hstate`` (float64
     (R, 2): last objective, checks) holds); conv_mode 0 -- relative change of the last
     step.  act[r] -> 0 when the rule holds; iters[r] += nsteps.  ``panels``: the
-    :func:`beta_panels` of W3 (built here when omitted)."""
+    :func:`beta_panels` of W3 (built here when omitted); ``xsum``: sum(X) in float64 (KL
+    objective; computed here -- one host sync -- when omitted)."""
     R, K, N = HT3.shape
     G = W3.shape[2]
     if X.shape != (N, G) or W3.shape[:2] != (R, K):
@@ -634,7 +635,8 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
         if t is not None and (t.dtype != torch.int32 or t.numel() < R or not t.is_contiguous()):
             raise ValueError(f"{name}: contiguous int32 with >= R entries")
     mode = beta_mode(beta)
-    if mode == 0 and nsteps > 0:
+    rule_loss = tol is not None and conv_mode == 1
+    if mode == 0 and (nsteps > 0 or rule_loss):
         if den_vec is None:
             den_vec = W3.sum(dim=2, dtype=torch.float32).contiguous()
         elif (den_vec.shape != (R, K) or den_vec.dtype != torch.float32
@@ -658,7 +660,10 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
                 hstate.data_ptr() if (hstate is not None and tol is not None) else 0,
                 part, counter, act.data_ptr() if act is not None else 0,
                 iters.data_ptr() if (iters is not None and tol is not None) else 0,
-                act.data_ptr() if act is not None else 0, 0, _stream_ptr(HT3))
+                act.data_ptr() if act is not None else 0, 0,
+                float(xsum if xsum is not None else (
+                    float(X.sum(dtype=torch.float64)) if (mode == 0 and rule_loss) else 0.0)),
+                _stream_ptr(HT3))
 
 
 def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float, eps: float,
@@ -681,14 +686,21 @@ def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float,
         raise ValueError("active: contiguous int32 with >= R entries")
     if panels is None:
         panels = beta_panels(W3)
+    mode = beta_mode(beta)
+    # KL: the kernel sums x log(x/p) + p; the -sum(x) term is added here on the device
+    wsum = W3.sum(dim=2, dtype=torch.float32).contiguous() if mode == 0 else None
     n_strips = -(-N // int(_hip.bp_strip_cols(K)))
     loss = torch.zeros((R, n_strips), dtype=torch.float64, device=dev)
-    _hip.bp_run(0, beta_mode(beta), X.data_ptr(), X.stride(0), panels.data_ptr(),
+    _hip.bp_run(0, mode, X.data_ptr(), X.stride(0), panels.data_ptr(),
                 panels.stride(0), HT3.data_ptr(), HT3.stride(0), HT3.stride(1), K, N, G, R, 1,
-                float(beta), float(eps), 0, 0, 0, 0, 1, 0, 0.0, 0.0, 1.0, 0.0, 0, 0, 0, 0, 0,
-                0, active.data_ptr() if active is not None else 0, loss.data_ptr(),
+                float(beta), float(eps), 0, 0, 0, 0, 1,
+                wsum.data_ptr() if wsum is not None else 0, 0.0, 0.0, 1.0, 0.0, 0, 0, 0, 0, 0,
+                0, active.data_ptr() if active is not None else 0, loss.data_ptr(), 0.0,
                 _stream_ptr(HT3))
-    return loss.sum(1)
+    tot = loss.sum(1)
+    if mode == 0:
+        tot = tot - X.sum(dtype=torch.float64)
+    return tot
 
 
 def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
@@ -728,7 +740,7 @@ def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
                 W3.data_ptr(), W3.stride(0), W3.stride(1), K, G, c, R, n_split, float(beta),
                 float(eps), num.data_ptr(), den.data_ptr() if den is not None else 0, 1, 0, 0,
                 0, 0.0, 0.0, 1.0, 0.0, 0, 0, 0, 0, 0, 0,
-                active.data_ptr() if active is not None else 0, 0, _stream_ptr(HT3))
+                active.data_ptr() if active is not None else 0, 0, 0.0, _stream_ptr(HT3))
     return num, den
 
 

@@ -118,13 +118,13 @@ PYBIND11_MODULE(_hip, m) {
            float beta, float eps, uintptr_t num, uintptr_t den, int nsteps, int loss_entry,
            int loss_exit, uintptr_t den_vec, float l1, float l2, float gamma, float tol,
            int conv_mode, uintptr_t hstate, uintptr_t part, uintptr_t counter, uintptr_t act,
-           uintptr_t iters, uintptr_t active, uintptr_t loss, uintptr_t stream) {
+           uintptr_t iters, uintptr_t active, uintptr_t loss, double xsum, uintptr_t stream) {
           check(cnmf_bp_run(side, mode, P<const float>(X), ldx, P<const unsigned short>(panel),
                             panel_rs, P<float>(F), f_rs, ldf, K, Lf, Ls, R, splits, beta, eps,
                             P<float>(num), P<float>(den), nsteps, loss_entry, loss_exit,
                             P<const float>(den_vec), l1, l2, gamma, tol, conv_mode,
                             P<double>(hstate), P<double>(part), P<int>(counter), P<int>(act),
-                            P<int>(iters), P<const int>(active), P<double>(loss),
+                            P<int>(iters), P<const int>(active), P<double>(loss), xsum,
                             reinterpret_cast<hipStream_t>(stream)),
                 "bp_run");
         });

@@ -155,6 +155,7 @@ struct BpParams {
   int* iters;                  // (R) MU steps taken
   const int* active;           // gate (0: workgroup exits)
   double* loss;                // loss-only launches: (R, n_strips) partial objectives
+  double xsum;                 // KL: sum of X over the rows (the objective's -sum x term)
 };
 
 template <int MODE>
@@ -178,8 +179,9 @@ template <int MODE>
 __device__ __forceinline__ float bp_loss(float x, float p, float q, float d, float beta,
                                          float eps) {
   if (MODE == kBpKL) {
-    const float t = x > 0.f ? x * __logf(q) : 0.f;   // q = x / p
-    return t - x + p;
+    // x log2(x / p) only (q = x / p): the linear part sum(p) - sum(x) of the KL objective
+    // is added per workgroup from the usage and spectra sums (bp_kernel)
+    return x > 0.f ? x * __builtin_amdgcn_logf(q) : 0.f;
   } else if (MODE == kBpIS) {
     const float r = fmaxf(x * d, eps);                // d = 1 / p
     return r - __logf(r) - 1.f;
@@ -456,8 +458,25 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
     }
 
     if (want_loss) {
-      if (it == p.nsteps) f_exit += (double)lsum;
-      else f_entry += (double)lsum;
+      double l = (double)lsum;
+      if (MODE == kBpKL) {
+        // sum x log(x/p) = ln 2 * sum x log2(x/p);  sum p = sum_k (sum_cols h_k) (sum_g w_k)
+        // (+ eps per element, negligible); - sum x is subtracted once per replicate
+        l *= 0.69314718055994530942;
+        float hp = 0.f;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int k = 16 * t + 4 * q + i;
+              if (k < K && cok[ct]) hp = fmaf(hc[ct][t][i], p.den_vec[(long long)rep * K + k], hp);
+            }
+        l += (double)hp;
+      }
+      if (it == p.nsteps) f_exit += l;
+      else f_entry += l;
     }
     if (UPD && want_num) {
       const bool last = it + 1 == p.nsteps;
@@ -557,6 +576,10 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
     for (int s2 = 0; s2 < p.n_strips; ++s2)
       for (int v = 0; v < 4; ++v)
         tot[v] += __hip_atomic_load(pr + 4 * s2 + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MODE == kBpKL) {
+      tot[2] -= p.xsum;
+      tot[3] -= p.xsum;
+    }
     if (p.conv_mode == 1) {
       double* hs = p.hstate + 2 * (long long)rep;
       const double f_prev = p.loss_entry ? tot[2] : hs[0];
@@ -653,7 +676,7 @@ extern "C" hipError_t cnmf_bp_run(
     int splits, float beta, float eps, float* num, float* den, int nsteps, int loss_entry,
     int loss_exit, const float* den_vec, float l1, float l2, float gamma, float tol,
     int conv_mode, double* hstate, double* part, int* counter, int* act, int* iters,
-    const int* active, double* loss, hipStream_t stream) {
+    const int* active, double* loss, double xsum, hipStream_t stream) {
   if (R <= 0 || Lf <= 0) return hipSuccess;
   if (K < 1 || K > 32 || Ls <= 0 || (side != 0 && side != 1)) return hipErrorInvalidValue;
   cnmf::BpParams p;
@@ -675,11 +698,12 @@ extern "C" hipError_t cnmf_bp_run(
   p.l1 = l1; p.l2 = l2; p.gamma = gamma; p.tol = tol;
   p.conv_mode = conv_mode; p.hstate = hstate; p.part = part;
   p.counter = counter; p.act = act; p.iters = iters; p.active = active; p.loss = loss;
+  p.xsum = xsum;
   if (side == 1) {
     if (num == nullptr || (mode != cnmf::kBpKL && den == nullptr)) return hipErrorInvalidValue;
     return cnmf::bp_launch_mode<false>(mode, p, stream);
   }
-  if (nsteps < 0 || (mode == cnmf::kBpKL && nsteps > 0 && den_vec == nullptr) ||
+  if (nsteps < 0 || (mode == cnmf::kBpKL && den_vec == nullptr) ||
       (part != nullptr && (counter == nullptr || act == nullptr)) ||
       (part != nullptr && conv_mode == 1 && hstate == nullptr) ||
       (nsteps == 0 && loss == nullptr && part == nullptr))

@@ -55,7 +55,7 @@ hipError_t cnmf_bp_run(int side, int mode, const float* X, long long ldx,
                        float eps, float* num, float* den, int nsteps, int loss_entry,
                        int loss_exit, const float* den_vec, float l1, float l2, float gamma,
                        float tol, int conv_mode, double* hstate, double* part, int* counter,
-                       int* act, int* iters, const int* active, double* loss,
+                       int* act, int* iters, const int* active, double* loss, double xsum,
                        hipStream_t stream);
 
 hipError_t cnmf_pairdist(const double* A, long long lda, const double* B, long long ldb,
