@@ -64,7 +64,7 @@ __host__ __device__ constexpr int bp_chunk(int NP, int T) {
   return (kBpCH * bp_ps(NP) + 2 * 16 * T * kBpNS + kBpThreads * 8 - 1) / (kBpThreads * 8) *
          (kBpThreads * 8);
 }
-__host__ __device__ constexpr int bp_ct(int T) { return 2; }  // column tiles per wave
+__host__ __device__ constexpr int bp_ct(int T) { return 2; }  // column tiles per wave (4: 820 vs 510 us per usage step)
 __host__ __device__ constexpr int bp_ks(int T) { return 16 * T + 1; }     // exchange stride
 
 enum BpMode { kBpKL = 0, kBpIS = 1, kBpGeneral = 2 };
@@ -388,46 +388,55 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
             an1[t] = *reinterpret_cast<const bp_v8*>(nb1 + off);
           }
         }
+        // phase 1: the P tiles of every column tile (independent MFMA chains), so the
+        // elementwise work of tile 0 overlaps the MFMAs of tile 1
+        bp_f4 P0[CT], P1[CT];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          bp_f4 P0 = {p.eps, p.eps, p.eps, p.eps}, P1 = P0;
+          P0[ct] = bp_f4{p.eps, p.eps, p.eps, p.eps};
+          P1[ct] = P0[ct];
 #pragma unroll
           for (int jj = 0; jj < NP; ++jj) {
-            P0 = bp_mfma(ap[0][jj], freg[ct][jj], P0);
-            P1 = bp_mfma(ap[1][jj], freg[ct][jj], P1);
+            P0[ct] = bp_mfma(ap[0][jj], freg[ct][jj], P0[ct]);
+            P1[ct] = bp_mfma(ap[1][jj], freg[ct][jj], P1[ct]);
           }
+        }
+        // phase 2: elementwise terms, loss, bf16 planes; phase 3: numerator MFMAs
+        bp_v8 qb0[CT], qb1[CT], db0[CT], db1[CT];
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
           float qv[8], dv[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            bp_terms<MODE>(xv[ct][e], e < 4 ? P0[e] : P1[e - 4], p.beta, qv[e], dv[e]);
+            bp_terms<MODE>(xv[ct][e], e < 4 ? P0[ct][e] : P1[ct][e - 4], p.beta, qv[e], dv[e]);
           if (kLoss) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const int j = j0 + (e >> 2) * 16 + 4 * q + (e & 3);
-              const float t = bp_loss<MODE>(xv[ct][e], e < 4 ? P0[e] : P1[e - 4], qv[e],
+              const float t = bp_loss<MODE>(xv[ct][e], e < 4 ? P0[ct][e] : P1[ct][e - 4], qv[e],
                                             dv[e], p.beta, p.eps);
               lsum += (cok[ct] && j < p.Ls) ? t : 0.f;
             }
           }
           if (kNum) {
-            bp_v8 b0, b1;
-            bp_split2(qv, b0, b1);
+            bp_split2(qv, qb0[ct], qb1[ct]);
+            if (MODE != kBpKL) bp_split2(dv, db0[ct], db1[ct]);
+          }
+        }
+        if (kNum) {
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
             for (int t = 0; t < T; ++t) {
-              num[ct][t] = bp_mfma(an0[t], b0, num[ct][t]);
-              num[ct][t] = bp_mfma(an0[t], b1, num[ct][t]);
-              num[ct][t] = bp_mfma(an1[t], b0, num[ct][t]);
-            }
-            if (MODE != kBpKL) {
-              bp_split2(dv, b0, b1);
-#pragma unroll
-              for (int t = 0; t < T; ++t) {
-                den[ct][t] = bp_mfma(an0[t], b0, den[ct][t]);
-                den[ct][t] = bp_mfma(an0[t], b1, den[ct][t]);
-                den[ct][t] = bp_mfma(an1[t], b0, den[ct][t]);
+              num[ct][t] = bp_mfma(an0[t], qb0[ct], num[ct][t]);
+              num[ct][t] = bp_mfma(an0[t], qb1[ct], num[ct][t]);
+              num[ct][t] = bp_mfma(an1[t], qb0[ct], num[ct][t]);
+              if (MODE != kBpKL) {
+                den[ct][t] = bp_mfma(an0[t], db0[ct], den[ct][t]);
+                den[ct][t] = bp_mfma(an0[t], db1[ct], den[ct][t]);
+                den[ct][t] = bp_mfma(an1[t], db0[ct], den[ct][t]);
               }
             }
-          }
         }
     };
     // software pipeline over the chunks: block 0's X (xa) arrived during the previous
