@@ -107,8 +107,11 @@ class Harmony:
             m.fit(X.cpu().numpy())
             Y = torch.as_tensor(m.cluster_centers_.T, dtype=self.dt, device=self.dev)
         else:
+            # (the consensus step runs 4x the restarts for sklearn-grade optima on a few
+            # hundred spectra; here the cells x PCs init only seeds the soft clustering)
             labels = torch.as_tensor(_km(X, self.K, n_init=10, random_state=self.random_state,
-                                         max_iter=25, backend="device"), device=self.dev)
+                                         max_iter=25, backend="device",
+                                         device_restart_factor=1), device=self.dev)
             onehot = (labels[None, :] == torch.arange(self.K, device=self.dev)[:, None]).to(self.dt)
             Y = (X.t() @ onehot.t()) / onehot.sum(dim=1).clamp(min=1)[None, :]
         self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
