@@ -607,10 +607,11 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
     spectra W3 (R, K, G) on rows X (N, G), in ONE launch (beta_planes.hip, side 0):
     HT3 *= (num / (den + l1 + l2 HT3))^gamma with num/den of the split-bf16 MFMA
     contraction.  With ``tol`` the stopping rule runs on the device after the block:
-    conv_mode 1 -- the block objective D_beta(X | HT3^T W3) after the block against the one
-    before it (``loss_entry``: computed in this launch; else the value ``hstate`` (float64
-    (R, 2): last objective, checks) holds); conv_mode 0 -- relative change of the last
-    step.  act[r] -> 0 when the rule holds; iters[r] += nsteps.  ``panels``: the
+    conv_mode 1 -- the block objective D_beta(X | HT3^T W3) at the iterate the block's last
+    step starts from (read off that step's own P pass; after the block when nsteps == 1)
+    against the previous one (``loss_entry``: the objective before the block, computed in
+    this launch; else the value ``hstate`` (float64 (R, 2): last objective, checks) holds);
+    conv_mode 0 -- relative change of the last step.  act[r] -> 0 when the rule holds; iters[r] += nsteps.  ``panels``: the
     :func:`beta_panels` of W3 (built here when omitted); ``xsum``: sum(X) in float64 (KL
     objective; computed here -- one host sync -- when omitted)."""
     R, K, N = HT3.shape

@@ -232,9 +232,10 @@ def beta_h_block(X, HT3, W3, beta, eps, nsteps, l1=0.0, l2=0.0, gamma=1.0, act=N
                  iters=None, conv_mode=1, hstate=None, loss_entry=False):
     """Reference of the multi-step usage solve block (beta_planes.hip, side 0): ``nsteps``
     MU steps of the live replicates, then the stopping rule: conv_mode 1 compares the
-    beta-divergence after the block with the one before it (``loss_entry``: evaluated
-    here; else the value recorded in ``hstate`` by the previous block); conv_mode 0 reads
-    the relative change of the block's last step."""
+    block's exit objective -- the beta-divergence at the iterate its last step starts from
+    (after the block for a one-step block) -- with the previous one (``loss_entry``: the
+    objective before the block, evaluated here; else the value ``hstate`` recorded);
+    conv_mode 0 reads the relative change of the block's last step."""
     R = HT3.shape[0]
     live = torch.ones(R, dtype=torch.bool, device=HT3.device) if act is None else (act[:R] != 0)
     rule = tol is not None
@@ -242,7 +243,12 @@ def beta_h_block(X, HT3, W3, beta, eps, nsteps, l1=0.0, l2=0.0, gamma=1.0, act=N
     if rule and conv_mode == 1 and loss_entry and nsteps > 0:
         f_entry = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
     dn = hn = None
+    f_exit = None
+    exit_in_last = nsteps >= 2
     for s in range(nsteps):
+        if rule and conv_mode == 1 and exit_in_last and s == nsteps - 1:
+            # the kernel reads the exit objective off the last step's P pass
+            f_exit = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
         num, den, _ = beta_contract(0, X, HT3, W3, beta, eps, True, False, act)
         if den is None:
             den = W3.sum(dim=2, keepdim=True)
@@ -259,7 +265,8 @@ def beta_h_block(X, HT3, W3, beta, eps, nsteps, l1=0.0, l2=0.0, gamma=1.0, act=N
     if not rule:
         return
     if conv_mode == 1:
-        f_exit = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
+        if f_exit is None:
+            f_exit = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
         hs = hstate.view(-1, 2)[:R]
         f_prev = f_entry if loss_entry else hs[:, 0]
         checked = torch.full_like(live, bool(loss_entry)) | (hs[:, 1] > 0)

@@ -305,7 +305,12 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
   };
   build_freg();
 
-  const int n_it = UPD ? p.nsteps + (p.loss_exit ? 1 : 0) : 1;
+  // The exit objective is read off the P pass of the block's LAST step (the iterate
+  // before that step's update, so no extra pass over X); with a single step per launch
+  // it would coincide with the entry objective, so it gets a P pass of its own then.
+  const bool exit_in_last = p.nsteps >= 2;
+  const int n_it = UPD ? p.nsteps + ((p.loss_exit && !exit_in_last) || p.nsteps == 0 ? 1 : 0)
+                       : 1;
   double f_entry = 0.0, f_exit = 0.0;
   float d2 = 0.f, o2 = 0.f;
   // panel chunk c -> registers -> LDS buffer bi (plain loads: the compiler counts them,
@@ -324,7 +329,9 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
 
   for (int it = 0; it < n_it; ++it) {
     const bool want_num = !UPD || it < p.nsteps;
-    const bool want_loss = UPD && ((it == 0 && p.loss_entry && p.nsteps > 0) || it == p.nsteps);
+    const bool is_exit = it == (exit_in_last ? p.nsteps - 1 : p.nsteps);
+    const bool is_entry = it == 0 && p.loss_entry && p.nsteps > 0;
+    const bool want_loss = UPD && (is_entry || (is_exit && (p.loss_exit || p.nsteps == 0)));
     bp_f4 num[CT][T], den[CT][T];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct)
@@ -484,8 +491,8 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
             }
         l += (double)hp;
       }
-      if (it == p.nsteps) f_exit += l;
-      else f_entry += l;
+      if (is_entry) f_entry += l;
+      if (is_exit) f_exit += l;
     }
     if (UPD && want_num) {
       const bool last = it + 1 == p.nsteps;
