@@ -1362,15 +1362,33 @@ class NMFBatchSolver:
 
     def _xt(self) -> torch.Tensor | None:
         """X^T (G, N), leading dimension padded to a multiple of 4 (float4 loads), for the
-        W-side beta kernel (beta_planes.hip reads X along cells there); GPU only."""
-        if self.X.device.type != "cuda":
+        W-side beta kernel (beta_planes.hip reads X along cells there); GPU only.  None
+        when a second copy of X would not fit next to it (e.g. the 200 GB 10M x 5k matrix
+        on one 288 GB GPU): the spectra side then runs the first-generation kernel
+        (beta_mu.hip), which reads X in place."""
+        if self.X.device.type != "cuda" or self._XT is False:
             return None
         if self._XT is None:
             N, G = self.X.shape
+            need = G * (-(-N // 4) * 4) * self.X.element_size()
+            free, _ = torch.cuda.mem_get_info(self.X.device)
+            if need > 0.5 * free:
+                self._XT = False
+                return None
             buf = torch.zeros((G, -(-N // 4) * 4), device=self.X.device, dtype=self.X.dtype)
             buf[:, :N] = self.X.t()
             self._XT = buf[:, :N]
         return self._XT
+
+    def _beta_w_partials(self, xc, xtc, H3c, W3, active, panels=None):
+        """(splits, R, K, G) W-side partials: split-bf16 kernel through X^T, or the fp32
+        kernel reading X in place when X^T is not kept (see _xt)."""
+        if xc.device.type == "cuda" and xtc is None:
+            num, den, _ = ops.beta_contract("w", xc, H3c, W3, self.beta, self.opts.eps,
+                                            active=active, reduce=False)
+            return num, den
+        return ops.beta_w_partials(xc, xtc, H3c, W3, self.beta, self.opts.eps, active=active,
+                                   panels=panels)
 
     def _chunk_xsum(self, xc: torch.Tensor) -> float:
         """sum(X) of a row block in float64 (the KL objective's linear term), cached per
@@ -1445,8 +1463,7 @@ class NMFBatchSolver:
 
     def _beta_w_stats(self, xc, H3c, W3, xtc=None, active=None):
         """(num, den) W-side MU statistics of rows xc (den broadcastable to (R,K,G))."""
-        num, den = ops.beta_w_partials(xc, xtc, H3c, W3, self.beta, self.opts.eps,
-                                       active=active)
+        num, den = self._beta_w_partials(xc, xtc, H3c, W3, active)
         num = num.sum(0)
         if den is None:
             den = H3c.sum(dim=2, keepdim=True)              # KL: row sums of H
@@ -1486,7 +1503,8 @@ class NMFBatchSolver:
         dist = self.comm.is_distributed
         XT = self._xt()
         # the chunk's usages stay fixed over the spectra iterations: split them once
-        hpan = {(a, b): self._beta_panels(H3[:, :, a:b]) for (a, b) in rows}
+        hpan = {(a, b): self._beta_panels(H3[:, :, a:b]) for (a, b) in rows} \
+            if XT is not None else {}
         max_it = int(o.online_chunk_max_iter)
         pending = None
         it = 0
@@ -1495,9 +1513,9 @@ class NMFBatchSolver:
             for _ in range(m):
                 num = den = None
                 for (a, b) in rows:
-                    nW, dW = ops.beta_w_partials(X[a:b], XT[:, a:b] if XT is not None else None,
-                                                 H3[:, :, a:b], W3, self.beta, o.eps,
-                                                 active=act, panels=hpan[(a, b)])
+                    nW, dW = self._beta_w_partials(X[a:b],
+                                                   XT[:, a:b] if XT is not None else None,
+                                                   H3[:, :, a:b], W3, act, hpan.get((a, b)))
                     if num is None:
                         num, den = nW, dW
                     else:   # several blocks of one step (single-process DP emulation)

@@ -721,6 +721,24 @@ def test_online_beta_gpu_converges_like_cpu(beta_loss):
     assert np.abs(on_g.n_iter - on_c.n_iter).max() <= 3, (on_g.n_iter, on_c.n_iter)
 
 
+def test_online_kl_without_xt_copy_matches():
+    """When X^T does not fit beside X the spectra side falls back to the fp32 kernel that
+    reads X in place (beta_mu.hip): same factorisation as the split-bf16 X^T path."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(3000, 400, n_programs=6, seed=0)).cuda()
+    opts = NMFOptions(n_components=6, beta_loss="kullback-leibler", online_chunk_size=1000,
+                      online_chunk_max_iter=1000)
+    a = NMFBatchSolver(X, opts).run([1, 2])
+    s = NMFBatchSolver(X, opts)
+    s._XT = False                       # as if the second copy of X had not fit
+    b = s.run([1, 2])
+    assert s._xt() is None
+    np.testing.assert_allclose(a.err, b.err, rtol=2e-3)
+    assert np.abs(a.n_iter - b.n_iter).max() <= 2, (a.n_iter, b.n_iter)
+
+
 def test_refit_raises_when_a_cooperative_solve_timed_out():
     """A raised cooperative-timeout flag (workgroups not co-resident) must surface as an
     error from the usage refit, and the kernels must stop waiting on it."""
