@@ -902,7 +902,7 @@ class NMFBatchSolver:
     def _plane_buf(self, key: str, rows: int, cols: int) -> torch.Tensor:
         """(3, rows, cols) int16 workspace, reused while the shape holds."""
         if self.X.device.type == "cuda":     # run_concurrent: one workspace per stream
-            key = (key, torch.cuda.current_stream(self.X.device).cuda_stream)
+            key = (key, ops._stream_ptr(self.X))
         buf = self._ws.get(key)
         if buf is None or buf.shape[1] < rows or buf.shape[2] != cols:
             buf = torch.zeros((3, rows, cols), dtype=torch.int16, device=self.X.device)
@@ -910,8 +910,7 @@ class NMFBatchSolver:
         return buf
 
     def _stream_key(self):
-        return torch.cuda.current_stream(self.X.device).cuda_stream \
-            if self.X.device.type == "cuda" else None
+        return ops._stream_ptr(self.X) if self.X.device.type == "cuda" else None
 
     def split_w(self, W: torch.Tensor, st: "_Batch"):
         """Planes of the spectra (times the count unit) for numer_gemm; call after every

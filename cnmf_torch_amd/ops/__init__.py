@@ -49,17 +49,40 @@ def _require_native():
     return _hip
 
 
+# Per-op debug / tuning knobs, read ONCE (at import, or by refresh_env()): every op
+# consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
+_ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
+             "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT")
+_ENV: dict = {}
+
+
+def refresh_env() -> None:
+    """Re-read the CNMF_* per-op knobs from the environment."""
+    _ENV.clear()
+    _ENV.update({k: os.environ.get(k) for k in _ENV_KEYS})
+
+
+refresh_env()
+
+
 def use_native(t: torch.Tensor) -> bool:
     """True when ``t`` lives on the GPU (the HIP path is then mandatory)."""
     if t.device.type != "cuda":
         return False
-    if os.environ.get("CNMF_FORCE_TORCH_OPS") == "1":  # debugging aid only, never default
+    if _ENV["CNMF_FORCE_TORCH_OPS"] == "1":  # debugging aid only, never default
         return False
     _require_native()
     return True
 
 
+# raw current-stream pointer without constructing a torch.cuda.Stream per op (700 per
+# bench step through torch.cuda.current_stream)
+_RAW_STREAM = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream_ptr(t: torch.Tensor) -> int:
+    if _RAW_STREAM is not None and t.device.type == "cuda":
+        return _RAW_STREAM(t.get_device())
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
@@ -160,7 +183,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     # co-resident per CU, so its cooperative budget is 4x the 1024-thread one
     S = None
     if variant in ("auto", "mfma") and a == 0 and h.solve_mfma_max_cols(K) > 0 \
-            and os.environ.get("CNMF_SOLVE_MFMA", "1") != "0":
+            and (_ENV["CNMF_SOLVE_MFMA"] or "1") != "0":
         S = _mfma_split(n, nblocks, K, nsplit, coop, x.device)
     if S is not None:
         vcode = 3
@@ -258,7 +281,7 @@ def _coop_resident(dev: torch.device) -> int:
 
 
 def _coop_split(n: int, nblocks: int, dev: torch.device) -> int:
-    if os.environ.get("CNMF_SOLVE_COOP") == "0":
+    if _ENV["CNMF_SOLVE_COOP"] == "0":
         return 1
     want = (n + COOP_COLS_PER_WG - 1) // COOP_COLS_PER_WG
     return max(1, min(want, _coop_resident(dev) // max(1, nblocks), 16))
@@ -280,7 +303,7 @@ def _mfma_split(n: int, nblocks: int, K: int, nsplit: int, coop, dev: torch.devi
         S = max(1, int(coop))
         return S if S >= s_min and (S == 1 or nblocks * S <= MFMA_WG_PER_CU *
                                     _coop_resident(dev)) else None
-    if s_min > 1 and os.environ.get("CNMF_SOLVE_COOP") == "0":
+    if s_min > 1 and _ENV["CNMF_SOLVE_COOP"] == "0":
         return None
     budget = MFMA_WG_PER_CU * _coop_resident(dev)
     if nblocks * s_min > budget and s_min > 1:
@@ -1002,7 +1025,7 @@ def gemm_a_planes(Kd: int) -> int:
     fp32 GEMM's own n * 2^-24 bound from n = 256 on, and from ~1000 on the measured error
     is also below the fp32 library GEMM's (test_gemm_two_a_planes_within_fp32_library_error)
     -- else 3 (exact).  CNMF_GEMM_APLANES=3 forces exact."""
-    if Kd < 1024 or os.environ.get("CNMF_GEMM_APLANES", "2") == "3":
+    if Kd < 1024 or (_ENV["CNMF_GEMM_APLANES"] or "2") == "3":
         return 3
     return 2
 
@@ -1013,7 +1036,7 @@ def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
     ~2 workgroups per CU.  CNMF_GEMM_VARIANT / CNMF_GEMM_KSPLIT override (benchmarks)."""
     cus = 256
     nk = Kd // planes_bk(pb)
-    v_env, k_env = os.environ.get("CNMF_GEMM_VARIANT"), os.environ.get("CNMF_GEMM_KSPLIT")
+    v_env, k_env = _ENV["CNMF_GEMM_VARIANT"], _ENV["CNMF_GEMM_KSPLIT"]
 
     def tiles(v):
         tm, tn = _GEMM_TILES[v]

@@ -56,6 +56,7 @@ def main():
             for vk in variants:
                 if vk is not None:
                     os.environ["CNMF_GEMM_VARIANT"], os.environ["CNMF_GEMM_KSPLIT"] = map(str, vk)
+                    ops.refresh_env()
                 t = timeit(lambda: ops.gemm_planes(C, Ap, Bp, M, N, Kd))
                 ops.gemm_planes(C, Ap, Bp, M, N, Kd)
                 err = float((C.double() - ref).abs().max() / ref.abs().max())
@@ -64,6 +65,7 @@ def main():
                                         float(f"{err:.2e}")]
                 os.environ.pop("CNMF_GEMM_VARIANT", None)
                 os.environ.pop("CNMF_GEMM_KSPLIT", None)
+                ops.refresh_env()
             rec["split_A_ms"] = round(timeit(lambda: ops.split_planes(A, Ap)) * 1e3, 4)
         print(json.dumps(rec), flush=True)
         out.append(rec)
