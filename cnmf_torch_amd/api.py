@@ -46,7 +46,8 @@ from .parallel.ledger import worker_filter
 from .utils.anndata_lite import AnnData
 from .utils.h5ad import read_h5ad, write_h5ad
 from .utils.io import (check_dir_exists, dump_yaml, load_df_from_npz, load_yaml, read_10x_mtx,
-                       read_any, read_counts_table, save_arrays_npz_digest, save_df_to_npz,
+                       read_any, read_counts_table, read_spectra_batch, save_arrays_npz_digest,
+                       save_df_to_npz,
                        save_df_to_text, NPZ_TMP_LEVEL, write_spectra_batch, write_text_atomic)
 from .utils.log import get_logger
 from .utils.timing import StageTimer, append_jsonl_many, read_jsonl
@@ -749,6 +750,21 @@ class cNMF:
                 print("Missing file: %s. Skipping." % fn)
                 continue
             present.append((int(p["iter"]), fn))
+        native = read_spectra_batch([fn for _, fn in present]) if present else None
+        if native is not None:     # stored npz parsed on native threads (csrc/io/npzio.cpp)
+            data, kk, cols = native
+            if any(int(x) != int(k) for x in kk):
+                raise ValueError(f"k={k}: a replicate file holds a different number of "
+                                 "components")
+            index = ["iter%d_topic%d" % (it, t + 1) for it, _ in present for t in range(k)]
+            combined = pd.DataFrame(data, index=index, columns=cols)
+            save_df_to_npz(combined, self.paths["merged_spectra"] % k, level=NPZ_TMP_LEVEL)
+            if remove_individual_iterations:
+                for _, p in sub.iterrows():
+                    fn = self.paths["iter_spectra"] % (int(p["n_components"]), int(p["iter"]))
+                    if os.path.exists(fn):
+                        os.remove(fn)
+            return combined
         with cf.ThreadPoolExecutor(max_workers=8) as ex:   # zlib inflate drops the GIL
             loaded = list(ex.map(lambda t: _load_npz_arrays(t[1]), present))
         if loaded:

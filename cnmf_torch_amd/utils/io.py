@@ -223,6 +223,24 @@ def write_spectra_batch(paths, data: np.ndarray, offs, ks, columns) -> list[tupl
             for p, o, k in zip(paths, offs, ks)]
 
 
+def read_spectra_batch(paths) -> tuple[np.ndarray, list, np.ndarray] | None:
+    """(data (sum K, G) float32, K per file, gene columns) of the replicate ``.df.npz``
+    files -- the stored npz :func:`write_spectra_batch` writes -- parsed on native threads
+    (csrc/io/npzio.cpp).  None when the extension is missing or a file needs numpy
+    (compressed members, other dtypes, object arrays of the original cnmf, gene names
+    that differ byte-wise from the first file's): the caller then reads them with numpy."""
+    if _npzio is None or not paths:
+        return None
+    try:
+        data, ks, cols = _npzio.read_spectra_batch([str(p) for p in paths],
+                                                    max(1, min(32, os.cpu_count() or 1)))
+    except ValueError as e:
+        if "unsupported" in str(e):
+            return None
+        raise
+    return data, list(ks), np.load(io.BytesIO(cols), allow_pickle=False)
+
+
 def npz_bytes(arrays: dict, level: int = 0) -> bytes:
     """The bytes of an .npz holding ``arrays`` (same members as :func:`_savez_deflate`).
     Values may be arrays or already-encoded .npy ``bytes`` (shared members such as the

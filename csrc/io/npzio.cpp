@@ -274,6 +274,146 @@ static std::vector<std::pair<std::string, long long>> write_spectra_batch(
   return out;
 }
 
+// ------------------------------------------------------------------ batch reader
+// Inverse of write_spectra_batch for `combine` (cnmf.py:895-920 reads every replicate
+// file of a K back): each stored npz is parsed natively -- end-of-central-directory,
+// central records, local headers, the data.npy header (<f4, C order, (K, G)) -- on a pool
+// of threads, and the spectra are copied into ONE float32 matrix.  The columns.npy
+// payloads must be byte-identical to the first file's.  Anything else (a deflated member,
+// another dtype, object arrays from the original cnmf, different gene-name bytes) is
+// reported as unsupported, and the caller takes the numpy path for the batch.
+namespace {
+
+uint32_t get16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+uint32_t get32(const uint8_t* p) { return get16(p) | (get16(p + 2) << 16); }
+
+struct NpzFile {
+  std::vector<uint8_t> bytes;
+  const uint8_t* data = nullptr;   // data.npy payload (float32, K x G)
+  const uint8_t* cols = nullptr;   // columns.npy payload
+  size_t cols_n = 0;
+  long long K = 0, G = 0;
+  std::string err;                 // non-empty: unsupported / unreadable
+};
+
+bool read_all(const std::string& path, std::vector<uint8_t>& out) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  bool ok = n > 0;
+  if (ok) {
+    out.resize((size_t)n);
+    ok = std::fread(out.data(), 1, (size_t)n, f) == (size_t)n;
+  }
+  std::fclose(f);
+  return ok;
+}
+
+// shape (K, G) of a float32 C-order .npy payload; false if it is anything else
+bool npy_f4_2d(const uint8_t* p, size_t n, long long& K, long long& G, size_t& hdr) {
+  if (n < 10 || std::memcmp(p, "\x93NUMPY", 6) != 0) return false;
+  const int major = p[6];
+  size_t hl, start;
+  if (major == 1) { hl = get16(p + 8); start = 10; }
+  else if (major == 2 || major == 3) { if (n < 12) return false; hl = get32(p + 8); start = 12; }
+  else return false;
+  if (start + hl > n) return false;
+  const std::string h((const char*)p + start, hl);
+  if (h.find("'descr': '<f4'") == std::string::npos) return false;
+  if (h.find("'fortran_order': False") == std::string::npos) return false;
+  const size_t sp = h.find("'shape': (");
+  if (sp == std::string::npos) return false;
+  long long a = -1, b = -1;
+  if (std::sscanf(h.c_str() + sp + 10, "%lld, %lld)", &a, &b) != 2 || a < 1 || b < 1) return false;
+  hdr = start + hl;
+  if (hdr + (size_t)(a * b) * 4 > n) return false;
+  K = a;
+  G = b;
+  return true;
+}
+
+void parse_npz(const std::string& path, NpzFile& f) {
+  if (!read_all(path, f.bytes)) { f.err = "unreadable: " + path; return; }
+  const uint8_t* b = f.bytes.data();
+  const size_t n = f.bytes.size();
+  if (n < 22) { f.err = "not a zip: " + path; return; }
+  size_t eocd = std::string::npos;
+  for (size_t i = n - 22 + 1; i-- > (n > 65557 ? n - 65557 : 0);)
+    if (get32(b + i) == 0x06054B50) { eocd = i; break; }
+  if (eocd == std::string::npos) { f.err = "no end of central directory: " + path; return; }
+  const uint32_t entries = get16(b + eocd + 10);
+  size_t cd = get32(b + eocd + 16);
+  for (uint32_t e = 0; e < entries; ++e) {
+    if (cd + 46 > n || get32(b + cd) != 0x02014B50) { f.err = "bad central record: " + path; return; }
+    const uint32_t method = get16(b + cd + 10), csize = get32(b + cd + 20);
+    const uint32_t nl = get16(b + cd + 28), xl = get16(b + cd + 30), cl = get16(b + cd + 32);
+    const uint32_t lo = get32(b + cd + 42);
+    const std::string name((const char*)b + cd + 46, nl);
+    cd += 46 + nl + xl + cl;
+    if (name != "data.npy" && name != "columns.npy") continue;
+    if (method != 0) { f.err = "compressed member: " + path; return; }
+    if (lo + 30 > n || get32(b + lo) != 0x04034B50) { f.err = "bad local header: " + path; return; }
+    const size_t pay = lo + 30 + get16(b + lo + 26) + get16(b + lo + 28);
+    if (pay + csize > n) { f.err = "truncated member: " + path; return; }
+    if (name == "columns.npy") {
+      f.cols = b + pay;
+      f.cols_n = csize;
+    } else {
+      size_t hdr = 0;
+      if (!npy_f4_2d(b + pay, csize, f.K, f.G, hdr)) { f.err = "data is not float32 2-D: " + path; return; }
+      f.data = b + pay + hdr;
+    }
+  }
+  if (!f.data || !f.cols) f.err = "missing data/columns member: " + path;
+}
+
+}  // namespace
+
+// -> (data (sum K, G) float32, [K per file], columns.npy bytes of the first file); raises
+// ValueError("unsupported: ...") when a file needs the numpy path
+static py::tuple read_spectra_batch(const std::vector<std::string>& paths, int threads) {
+  const size_t n = paths.size();
+  if (n == 0) throw std::invalid_argument("no files");
+  std::vector<NpzFile> files(n);
+  std::atomic<size_t> next{0};
+  auto run = [&](auto&& fn) {
+    next = 0;
+    py::gil_scoped_release nogil;
+    const int nt = std::max(1, std::min<int>(threads, (int)n));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(fn);
+    fn();
+    for (auto& t : pool) t.join();
+  };
+  run([&]() {
+    for (size_t i; (i = next.fetch_add(1)) < n;) parse_npz(paths[i], files[i]);
+  });
+  long long rows = 0;
+  std::vector<long long> offs(n);
+  std::vector<int> ks(n);
+  for (size_t i = 0; i < n; ++i) {
+    const NpzFile& f = files[i];
+    if (!f.err.empty()) throw py::value_error("unsupported: " + f.err);
+    if (f.G != files[0].G || f.cols_n != files[0].cols_n ||
+        std::memcmp(f.cols, files[0].cols, f.cols_n) != 0)
+      throw py::value_error("unsupported: gene columns differ from the first file: " + paths[i]);
+    offs[i] = rows;
+    ks[i] = (int)f.K;
+    rows += f.K;
+  }
+  const long long G = files[0].G;
+  py::array_t<float> out({rows, G});
+  float* dst = out.mutable_data();
+  run([&]() {
+    for (size_t i; (i = next.fetch_add(1)) < n;)
+      std::memcpy(dst + offs[i] * G, files[i].data, (size_t)files[i].K * G * sizeof(float));
+  });
+  py::bytes cols((const char*)files[0].cols, files[0].cols_n);
+  return py::make_tuple(out, ks, cols);
+}
+
 static std::string sha256_hex(py::bytes b) {
   std::string s(b);
   Sha256 h;
@@ -287,10 +427,11 @@ static unsigned crc32_bytes(py::bytes b) {
 }
 
 PYBIND11_MODULE(_npzio, m) {
-  m.doc() = "cnmf_torch_amd native replicate-file writer (stored npz, crc32, sha256)";
+  m.doc() = "cnmf_torch_amd native replicate-file writer/reader (stored npz, crc32, sha256)";
   m.def("write_spectra_batch", &write_spectra_batch, py::arg("paths"), py::arg("data"),
         py::arg("offs"), py::arg("ks"), py::arg("columns_npy"), py::arg("index_npy"),
         py::arg("data_hdr"), py::arg("threads") = 16);
+  m.def("read_spectra_batch", &read_spectra_batch, py::arg("paths"), py::arg("threads") = 16);
   m.def("sha256_hex", &sha256_hex);
   m.def("crc32", &crc32_bytes);
 }

@@ -88,3 +88,37 @@ def test_npz_template_files_load_and_hash(tmp_path):
         df = load_df_from_npz(p)
         np.testing.assert_array_equal(df.values, data)
         assert list(df.index) == list(range(1, k + 1)) and list(df.columns) == list(genes)
+
+
+def test_native_spectra_batch_reader(tmp_path):
+    """The native reader (csrc/io/npzio.cpp) returns exactly what the native writer wrote,
+    and declines (None -> numpy path) files it does not handle: deflated members,
+    gene-name bytes that differ from the first file's."""
+    import numpy as np
+    import pandas as pd
+
+    from cnmf_torch_amd.utils import io as cio
+
+    if cio._npzio is None:
+        pytest.skip("native npz extension not built")
+    G = 300
+    cols = np.array([f"g{i}" for i in range(G)])
+    ks = [5, 7, 5]
+    offs = [0, 5, 12]
+    data = np.random.default_rng(0).random((17, G)).astype(np.float32)
+    paths = [str(tmp_path / f"r{i}.df.npz") for i in range(3)]
+    cio.write_spectra_batch(paths, data, offs, ks, cols)
+    got = cio.read_spectra_batch(paths)
+    assert got is not None
+    np.testing.assert_array_equal(got[0], data)
+    assert got[1] == ks and list(got[2]) == list(cols)
+    # numpy reads the same files to the same arrays
+    with np.load(paths[1]) as f:
+        np.testing.assert_array_equal(f["data"], data[5:12])
+    # other gene-name bytes -> declined
+    other = [str(tmp_path / "o.df.npz")]
+    cio.write_spectra_batch(other, data[:5], [0], [5], np.array([f"x{i}" for i in range(G)]))
+    assert cio.read_spectra_batch(paths + other) is None
+    # a deflated file (e.g. written by the original cnmf) -> declined
+    cio.save_df_to_npz(pd.DataFrame(data[:5], columns=cols), paths[0], level=6)
+    assert cio.read_spectra_batch(paths) is None
