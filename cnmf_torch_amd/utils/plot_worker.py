@@ -1,5 +1,6 @@
 """Child process of plotting.PlotWorker: import matplotlib at once (overlapping the
-parent's GPU work), then draw every job read from stdin and exit at EOF."""
+parent's GPU work), then draw every job read from stdin, acknowledge each on stdout
+("ok <id>" / "err <id>"), and exit at EOF."""
 import json
 import os
 import sys
@@ -20,9 +21,13 @@ def main() -> int:
         if not line.strip():
             continue
         job = json.loads(line)
-        with np.load(job["npz"], allow_pickle=False) as f:
-            arrays = {k: f[k] for k in f.files}
-        plotting.draw_job(job["kind"], job["path"], arrays)
+        try:
+            with np.load(job["npz"], allow_pickle=False) as f:
+                arrays = {k: f[k] for k in f.files}
+            plotting.draw_job(job["kind"], job["path"], arrays)
+            print(f"ok {job['id']}", flush=True)
+        except Exception:
+            print(f"err {job['id']}", flush=True)
     return 0
 
 

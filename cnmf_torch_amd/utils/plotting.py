@@ -2,18 +2,23 @@
 cnmf.py:1311-1332) and the Preprocess QC histograms (C32).  matplotlib, Agg backend.
 
 Figures that the caller closes anyway (``close=True``: CLI and pipeline runs) can be drawn
-by :class:`PlotWorker`, a child Python process started when a stage begins: it imports
-matplotlib (~0.8 s on a fresh box, where its .pyc files are compiled) while the stage
-computes on the GPU, then draws the same figure with the same code.  This module imports
+by :class:`PlotWorker`, a child Python process started when the first such stage begins:
+it imports matplotlib (~0.8 s on a fresh box, where its .pyc files are compiled) while the
+stage computes on the GPU, then draws the same figure with the same code, and stays up for
+the following stages.  This module imports
 only numpy/pandas at the top, so the worker never loads torch or touches the GPU.
 """
 from __future__ import annotations
 
+import atexit
+import itertools
 import json
 import os
 import subprocess
 import sys
 import tempfile
+import threading
+import time
 
 import numpy as np
 import pandas as pd
@@ -146,42 +151,105 @@ def count_hist(X, num_cells: int = 1000, title="Quantile thresholded normalized 
     return fig
 
 
-class PlotWorker:
-    """Out-of-process figure drawer (see the module docstring).  ``submit`` hands one
-    figure job to the child (arrays through a temporary .npz); ``wait`` blocks until the
-    child has written every figure.  Any failure of the child falls back to drawing in
-    this process, so figures are never lost."""
+class _PlotProc:
+    """The figure-drawing child process, shared by every PlotWorker of this process: it
+    imports matplotlib once (~0.8-1 s on a fresh box), then draws job after job, and
+    acknowledges each on stdout ("ok <id>" / "err <id>").  Closed at interpreter exit."""
+
+    _inst = None
+    _lock = threading.Lock()
 
     def __init__(self):
         env = dict(os.environ, MPLBACKEND="Agg", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
         script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "plot_worker.py")
-        self.jobs = []
         self.proc = subprocess.Popen([sys.executable, script], stdin=subprocess.PIPE,
-                                     stdout=subprocess.PIPE, stderr=subprocess.PIPE, env=env,
-                                     text=True)
+                                     stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                     env=env, text=True, bufsize=1)
+        self.acks: dict = {}
+        self.alive = True
+        self.cv = threading.Condition()
+        self.reader = threading.Thread(target=self._read, daemon=True)
+        self.reader.start()
+
+    def _read(self) -> None:
+        try:
+            for line in self.proc.stdout:
+                parts = line.split()
+                if len(parts) == 2 and parts[0] in ("ok", "err"):
+                    with self.cv:
+                        self.acks[int(parts[1])] = parts[0] == "ok"
+                        self.cv.notify_all()
+        finally:
+            with self.cv:
+                self.alive = False
+                self.cv.notify_all()
+
+    def send(self, job: dict) -> bool:
+        try:
+            self.proc.stdin.write(json.dumps(job) + "\n")
+            self.proc.stdin.flush()
+            return True
+        except Exception:
+            return False
+
+    def result(self, jid: int, deadline: float):
+        """True / False once job ``jid`` is acknowledged; None if the child died or the
+        deadline passed first."""
+        with self.cv:
+            while jid not in self.acks and self.alive:
+                left = deadline - time.monotonic()
+                if left <= 0 or not self.cv.wait(timeout=left):
+                    if jid not in self.acks:
+                        return None
+            return self.acks.pop(jid, None)
+
+    def close(self) -> None:
+        try:
+            self.proc.stdin.close()
+            self.proc.wait(timeout=10)
+        except Exception:
+            self.proc.kill()
+
+    @classmethod
+    def get(cls) -> "_PlotProc":
+        with cls._lock:
+            if cls._inst is None or not cls._inst.alive or cls._inst.proc.poll() is not None:
+                cls._inst = cls()
+                atexit.register(cls._inst.close)
+            return cls._inst
+
+
+class PlotWorker:
+    """Out-of-process figure drawer (see the module docstring).  ``submit`` hands one
+    figure job to the shared child (arrays through a temporary .npz); ``wait`` blocks until
+    the child has written this worker's figures.  The child stays up for the next stage
+    (k_selection_plot then consensus import matplotlib once).  Any failure of the child
+    falls back to drawing in this process, so figures are never lost."""
+
+    _ids = itertools.count()
+
+    def __init__(self):
+        self.proc = _PlotProc.get()
+        self.jobs = []
 
     def submit(self, kind: str, path: str, **arrays) -> None:
         fd, npz = tempfile.mkstemp(suffix=".npz")
         os.close(fd)
         np.savez(npz, **{k: np.asarray(v) for k, v in arrays.items()})
-        self.jobs.append((kind, path, npz))
-        self.proc.stdin.write(json.dumps({"kind": kind, "path": path, "npz": npz}) + "\n")
-        self.proc.stdin.flush()
+        jid = next(self._ids)
+        sent = self.proc.send({"id": jid, "kind": kind, "path": path, "npz": npz})
+        self.jobs.append((jid, kind, path, npz, sent))
 
     def wait(self, timeout: float = 300.0) -> None:
-        ok = False
-        try:
-            out, err = self.proc.communicate(timeout=timeout)
-            ok = self.proc.returncode == 0 and all(os.path.exists(p) for _, p, _ in self.jobs)
-        except Exception:
-            self.proc.kill()
-        if not ok:   # draw here instead
-            for kind, path, npz in self.jobs:
+        deadline = time.monotonic() + timeout
+        for jid, kind, path, npz, sent in self.jobs:
+            ok = sent and self.proc.result(jid, deadline) is True and os.path.exists(path)
+            if not ok:   # draw here instead
                 with np.load(npz, allow_pickle=False) as f:
                     draw_job(kind, path, {k: f[k] for k in f.files})
-        for _, _, npz in self.jobs:
             if os.path.exists(npz):
                 os.remove(npz)
+        self.jobs = []
 
 
 def draw_job(kind: str, path: str, a: dict) -> None:

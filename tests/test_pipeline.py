@@ -286,7 +286,8 @@ def test_cli_dp_factorize_over_torchrun_matches_serial(tmp_path):
 
 def test_figures_drawn_by_plot_worker_process(tmp_path):
     """Closed figures (CLI / pipeline) are drawn by a child process that imports matplotlib
-    while the stage computes: the stage process itself never imports pyplot."""
+    while the stage computes, and serves the later stages too: the stage process itself
+    never imports pyplot."""
     Xc, cells, genes = simulate_counts(150, 80, 3, seed=3, sparse=False)
     fn = str(tmp_path / "counts.df.npz")
     save_df_to_npz(pd.DataFrame(Xc, index=cells, columns=genes), fn)
@@ -298,7 +299,10 @@ o = cNMF(output_dir={repr(str(tmp_path))}, name="pw")
 o.prepare({repr(fn)}, components=[3, 4], n_iter=10, seed=1, num_highvar_genes=50)
 o.factorize(verbose=False); o.combine()
 o.k_selection_plot(close_fig=True)
+from cnmf_torch_amd.utils.plotting import _PlotProc
+pid = _PlotProc._inst.proc.pid
 o.consensus(3, 2.0, show_clustering=True, close_clustergram_fig=True)
+assert _PlotProc._inst.proc.pid == pid      # one child, matplotlib imported once
 assert 'matplotlib.pyplot' not in sys.modules
 assert os.path.getsize(o.paths['k_selection_plot']) > 1000
 assert os.path.getsize(o.paths['clustering_plot'] % (3, '2_0')) > 1000
@@ -309,3 +313,25 @@ print('ok')
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
                        timeout=600)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_plot_worker_falls_back_when_the_child_dies(tmp_path):
+    """A dead figure child is replaced for the next stage, and a job it never acknowledged
+    is drawn in this process: figures are never lost."""
+    from cnmf_torch_amd.utils.plotting import PlotWorker, _PlotProc
+
+    w = PlotWorker()
+    w.proc.proc.kill()
+    w.proc.proc.wait()
+    path = str(tmp_path / "ksel.png")
+    w.submit("k_selection", path, k=np.array([3, 4]), silhouette=np.array([0.9, 0.8]),
+             prediction_error=np.array([10.0, 9.0]))
+    w.wait(timeout=60)
+    assert os.path.getsize(path) > 1000
+    w2 = PlotWorker()                         # a fresh child for the next stage
+    assert w2.proc is _PlotProc._inst and w2.proc.proc.poll() is None
+    path2 = str(tmp_path / "ksel2.png")
+    w2.submit("k_selection", path2, k=np.array([3, 4]), silhouette=np.array([0.9, 0.8]),
+              prediction_error=np.array([10.0, 9.0]))
+    w2.wait(timeout=120)
+    assert os.path.getsize(path2) > 1000
