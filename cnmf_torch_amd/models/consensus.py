@@ -66,16 +66,32 @@ def _kmeanspp_batched(X: torch.Tensor, k: int, gen: torch.Generator, n_init: int
     centers[:, 0] = X[first]
     closest = ops.pairwise_dist(X, X[first], squared=True)           # (n, n_init)
     ar = torch.arange(n_init, device=dev)
+    # Large n in few dimensions (Harmony's init: 500k cells x 20 PCs, 100 centres x 10
+    # restarts x 6 trials): the fused kernel scores every candidate without the
+    # (n x n_init*trials) float64 distance matrix, which cost ~1 GB of HBM traffic per
+    # centre (kmeans.hip kmeanspp_kernel).  Few points (consensus spectra): one MFMA
+    # distance launch per centre.
+    fused = n > 4096 and ops.kmeanspp_fused_ok(X, n_init * trials)
+    if fused:
+        closest = closest.contiguous()
     for c in range(1, k):
-        cum = torch.cumsum(closest.double(), 0)                       # (n, n_init)
-        r = u[c - 1] * cum[-1][:, None]                               # (n_init, trials)
-        cand = torch.searchsorted(cum.t().contiguous(), r).clamp(max=n - 1)
-        dcand = ops.pairwise_dist(X, X[cand.reshape(-1)], squared=True)
-        dcand = dcand.view(n, n_init, trials)
-        newc = torch.minimum(closest[:, :, None], dcand)              # (n, n_init, trials)
-        best = torch.argmin(newc.sum(dim=0), dim=1)                   # (n_init,)
+        # inverse CDF of each restart's potential; the scan runs along the contiguous
+        # dimension ((n_init, n) layout: the outer-dimension scan of an (n, n_init) tensor
+        # took 40 ms per centre at 200k points)
+        cum = torch.cumsum(closest.t().contiguous().double(), 1)      # (n_init, n)
+        r = u[c - 1] * cum[:, -1:]                                    # (n_init, trials)
+        cand = torch.searchsorted(cum, r).clamp(max=n - 1)
+        if fused:
+            pot = ops.kmeanspp_step(X, X[cand.reshape(-1)], closest, trials)
+            best = torch.argmin(pot, dim=1)                           # (n_init,)
+            ops.kmeanspp_step(X, X[cand[ar, best]], closest, 1, update=True)
+        else:
+            dcand = ops.pairwise_dist(X, X[cand.reshape(-1)], squared=True)
+            dcand = dcand.view(n, n_init, trials)
+            newc = torch.minimum(closest[:, :, None], dcand)          # (n, n_init, trials)
+            best = torch.argmin(newc.sum(dim=0), dim=1)               # (n_init,)
+            closest = newc[:, ar, best]
         centers[:, c] = X[cand[ar, best]]
-        closest = newc[:, ar, best]
     return centers
 
 

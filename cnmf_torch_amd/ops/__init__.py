@@ -893,6 +893,51 @@ def seg_argmin(D: torch.Tensor, k: int, row_add: torch.Tensor | None = None,
     return lab.long(), mind
 
 
+def kmeanspp_fused_ok(X: torch.Tensor, M: int) -> bool:
+    """True when the fused k-means++ step (kmeans.hip kmeanspp_kernel) handles X (n, d) with
+    M = n_init * trials candidates in LDS."""
+    return use_native(X) and bool(_hip.kmeanspp_fits(int(M), int(X.shape[1])))
+
+
+def kmeanspp_step(X: torch.Tensor, C: torch.Tensor, closest: torch.Tensor, trials: int,
+                  update: bool = False):
+    """Greedy k-means++ step for every restart (n_init = closest.shape[1]) without the
+    (n x n_init*trials) distance matrix.  X (n, d) float64; C (n_init*trials, d) the
+    candidates, restart r owning rows [r*trials, (r+1)*trials); closest (n, n_init) float64
+    contiguous.  update=False: returns the potentials sum_i min(closest[i, r],
+    |x_i - c_m|^2) as (n_init, trials); update=True (trials == 1): closest[i, r] =
+    min(closest[i, r], |x_i - c_r|^2) in place.  GPU: kmeans.hip kmeanspp_kernel."""
+    n, d = X.shape
+    M = C.shape[0]
+    n_init = closest.shape[1]
+    if M != n_init * trials or closest.shape[0] != n or C.shape[1] != d:
+        raise ValueError("kmeanspp_step: inconsistent shapes")
+    if not use_native(X):
+        D = ((X[:, None, :] - C[None, :, :]) ** 2).sum(dim=2).view(n, n_init, trials)
+        V = torch.minimum(closest[:, :, None], D)
+        if update:
+            closest.copy_(V[:, :, 0])
+            return None
+        return V.sum(dim=0)
+    Xd = _f64_rows(X)
+    Cd = C.to(torch.float64).contiguous()
+    if closest.dtype != torch.float64 or not closest.is_contiguous():
+        raise ValueError("closest: contiguous float64 required")
+    if not _hip.kmeanspp_fits(int(M), int(d)):
+        raise ValueError(f"kmeanspp_step: M={M}, d={d} exceeds the fused kernel's LDS budget")
+    if update:
+        if trials != 1:
+            raise ValueError("update needs one candidate per restart")
+        _hip.kmeanspp(Xd.data_ptr(), Xd.stride(0), n, d, Cd.data_ptr(), M, 1,
+                      closest.data_ptr(), n_init, 1, 0, _stream_ptr(X))
+        return None
+    nb = int(_hip.kmeanspp_blocks(n))
+    pot = torch.empty((nb, M), dtype=torch.float64, device=X.device)
+    _hip.kmeanspp(Xd.data_ptr(), Xd.stride(0), n, d, Cd.data_ptr(), M, trials,
+                  closest.data_ptr(), n_init, 0, pot.data_ptr(), _stream_ptr(X))
+    return pot.sum(dim=0).view(n_init, trials)
+
+
 def kmeans_fused_ok(X: torch.Tensor, k: int) -> bool:
     """True when the fused low-dimensional Lloyd step (kmeans.hip) handles (X, k)."""
     return use_native(X) and bool(_hip.kmeans_fits(int(k), int(X.shape[1])))

@@ -152,6 +152,15 @@ PYBIND11_MODULE(_hip, m) {
   });
 
   m.def("kmeans_blocks", [](int n) { return cnmf_kmeans_blocks(n); });
+  m.def("kmeanspp_blocks", [](int n) { return cnmf_kmeanspp_blocks(n); });
+  m.def("kmeanspp_fits", [](int M, int d) { return cnmf_kmeanspp_fits(M, d); });
+  m.def("kmeanspp", [](uintptr_t X, long long ldx, int n, int d, uintptr_t C, int M, int trials,
+                       uintptr_t closest, int n_init, int mode, uintptr_t pot, uintptr_t stream) {
+    check(cnmf_kmeanspp(P<const double>(X), ldx, n, d, P<const double>(C), M, trials,
+                        P<double>(closest), n_init, mode, P<double>(pot),
+                        reinterpret_cast<hipStream_t>(stream)),
+          "kmeanspp");
+  });
   m.def("kmeans_fits", [](int k, int d) { return cnmf_kmeans_fits(k, d); });
   m.def("kmeans_step", [](uintptr_t X, long long ldx, int n, int d, uintptr_t C, int k,
                           int n_init, uintptr_t live, uintptr_t labels, uintptr_t mind,

@@ -123,7 +123,107 @@ static hipError_t launch_kmeans(const double* X, long long ldx, int n, int d, co
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------- k-means++ step
+// Greedy k-means++ (sklearn _kmeans_plusplus) for every restart at once, low-dimensional
+// points (d <= 64): the M = n_init * trials candidates sit in LDS, every thread owns one
+// point in registers and, for each candidate m of restart r = m / trials, takes
+// min(closest[i][r], |x_i - c_m|^2).
+//   mode 0  per-workgroup partial potentials pot[block][m] (summed on the host in block
+//           order: deterministic) -- nothing (n x M) is materialised
+//   mode 1  the candidates are the chosen centres (trials = 1): closest[i][r] is
+//           lowered in place
+template <int DP>
+__global__ void __launch_bounds__(kKmThreads)
+    kmeanspp_kernel(const double* __restrict__ X, long long ldx, int n, int d,
+                    const double* __restrict__ C, int M, int trials,
+                    double* __restrict__ closest, int n_init, int mode,
+                    double* __restrict__ pot) {
+  extern __shared__ double smem[];
+  double* sC = smem;                      // M * DP candidates (zero padded)
+  double* sRed = sC + (long long)M * DP;  // (kKmThreads / 64) * M wave partials
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int e = tid; e < M * DP; e += kKmThreads) {
+    const int c = e / DP, j = e % DP;
+    sC[e] = j < d ? C[(long long)c * d + j] : 0.0;
+  }
+  __syncthreads();
+  const long long i = (long long)blockIdx.x * kKmThreads + tid;
+  const bool ok = i < n;
+  double x[DP];
+  const double* xr = X + (ok ? i : 0) * ldx;
+#pragma unroll
+  for (int j = 0; j < DP; ++j) x[j] = (ok && j < d) ? xr[j] : 0.0;
+  double* cl = closest + (ok ? i : 0) * n_init;
+  for (int m = 0; m < M; ++m) {
+    const double2* cc = reinterpret_cast<const double2*>(sC + (long long)m * DP);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < DP / 2; ++j) {
+      const double2 v = cc[j];
+      const double a = x[2 * j] - v.x, b = x[2 * j + 1] - v.y;
+      s0 = fma(a, a, s0);
+      s1 = fma(b, b, s1);
+    }
+    const int r = m / trials;
+    const double cur = ok ? cl[r] : 0.0;
+    const double v = ok ? fmin(cur, s0 + s1) : 0.0;
+    if (mode == 1) {
+      if (ok) cl[r] = v;
+    } else {
+      const double w = wave_sum(v);
+      if (lane == 0) sRed[wave * M + m] = w;
+    }
+  }
+  if (mode == 1) return;
+  __syncthreads();
+  for (int m = tid; m < M; m += kKmThreads) {
+    double t = 0.0;
+    for (int w = 0; w < kKmThreads / 64; ++w) t += sRed[w * M + m];
+    pot[(long long)blockIdx.x * M + m] = t;
+  }
+}
+
+template <int DP>
+static hipError_t launch_kmeanspp(const double* X, long long ldx, int n, int d, const double* C,
+                                  int M, int trials, double* closest, int n_init, int mode,
+                                  double* pot, hipStream_t stream) {
+  const size_t lds = ((size_t)M * DP + (size_t)(kKmThreads / 64) * M) * sizeof(double);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeanspp_kernel<DP>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const dim3 grid((unsigned)((n + kKmThreads - 1) / kKmThreads));
+  hipLaunchKernelGGL(kmeanspp_kernel<DP>, grid, dim3(kKmThreads), lds, stream, X, ldx, n, d, C,
+                     M, trials, closest, n_init, mode, pot);
+  return hipGetLastError();
+}
+
 }  // namespace cnmf
+
+extern "C" int cnmf_kmeanspp_blocks(int n) {
+  return (n + cnmf::kKmThreads - 1) / cnmf::kKmThreads;
+}
+
+extern "C" int cnmf_kmeanspp_fits(int M, int d) {
+  if (M < 1 || d < 1 || d > 64) return 0;
+  const int dp = (d + 15) / 16 * 16;
+  return ((size_t)M * dp + (size_t)(cnmf::kKmThreads / 64) * M) * sizeof(double) <= 150 * 1024;
+}
+
+extern "C" hipError_t cnmf_kmeanspp(const double* X, long long ldx, int n, int d,
+                                    const double* C, int M, int trials, double* closest,
+                                    int n_init, int mode, double* pot, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (!cnmf_kmeanspp_fits(M, d) || trials < 1 || M % trials || M / trials != n_init ||
+      (mode == 0 && pot == nullptr) || (mode != 0 && mode != 1))
+    return hipErrorInvalidValue;
+  const int dp = (d + 15) / 16 * 16;
+  switch (dp) {
+    case 16: return cnmf::launch_kmeanspp<16>(X, ldx, n, d, C, M, trials, closest, n_init, mode, pot, stream);
+    case 32: return cnmf::launch_kmeanspp<32>(X, ldx, n, d, C, M, trials, closest, n_init, mode, pot, stream);
+    case 48: return cnmf::launch_kmeanspp<48>(X, ldx, n, d, C, M, trials, closest, n_init, mode, pot, stream);
+    default: return cnmf::launch_kmeanspp<64>(X, ldx, n, d, C, M, trials, closest, n_init, mode, pot, stream);
+  }
+}
 
 extern "C" int cnmf_kmeans_blocks(int n) {
   const int per = cnmf::kKmThreads * cnmf::kKmRounds;

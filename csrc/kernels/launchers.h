@@ -79,6 +79,11 @@ hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K
                      float* part, int S, hipStream_t stream);
 
 int cnmf_kmeans_blocks(int n);
+int cnmf_kmeanspp_blocks(int n);
+int cnmf_kmeanspp_fits(int M, int d);
+hipError_t cnmf_kmeanspp(const double* X, long long ldx, int n, int d, const double* C, int M,
+                         int trials, double* closest, int n_init, int mode, double* pot,
+                         hipStream_t stream);
 int cnmf_kmeans_fits(int k, int d);
 hipError_t cnmf_kmeans_step(const double* X, long long ldx, int n, int d, const double* C, int k,
                             int n_init, const int* live, int* labels, double* mind, double* psum,

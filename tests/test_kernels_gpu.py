@@ -346,6 +346,42 @@ def test_split_bf16_h_block_rule_matches_reference(beta, conv_mode):
     assert torch.equal(gh[2].cpu(), HT[2].float())           # inactive replicate untouched
 
 
+@pytest.mark.parametrize("d", [7, 20, 50])
+def test_kmeanspp_fused_step_matches_reference(d):
+    """Fused k-means++ candidate scoring / closest update (kmeans.hip kmeanspp_kernel) vs
+    the float64 torch reference; ragged n (not a multiple of the 256-point blocks)."""
+    rs = np.random.default_rng(d)
+    n, n_init, trials = 5000 + 37, 10, 6
+    X = torch.from_numpy(rs.normal(size=(n, d)))
+    C = torch.from_numpy(rs.normal(size=(n_init * trials, d)))
+    closest = torch.from_numpy(rs.random((n, n_init)) * d)
+    ref = ops.kmeanspp_step(X, C, closest.clone(), trials)
+    got = ops.kmeanspp_step(X.cuda(), C.cuda(), closest.cuda().contiguous(), trials)
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-11, atol=1e-9)
+    ch = C[::trials].contiguous()
+    cr, cg = closest.clone(), closest.cuda().contiguous()
+    ops.kmeanspp_step(X, ch, cr, 1, update=True)
+    ops.kmeanspp_step(X.cuda(), ch.cuda(), cg, 1, update=True)
+    torch.testing.assert_close(cg.cpu(), cr, rtol=1e-12, atol=1e-12)
+
+
+def test_device_kmeans_large_n_uses_fused_init():
+    """Harmony-sized k-means (many points, few PCs) goes through the fused k-means++ path
+    and still separates planted clusters."""
+    from sklearn.metrics import adjusted_rand_score
+
+    from cnmf_torch_amd.models.consensus import kmeans
+
+    rs = np.random.default_rng(5)
+    centers = rs.normal(size=(8, 20)) * 6
+    truth = rs.integers(0, 8, 30000)
+    X = torch.from_numpy(centers[truth] + rs.normal(size=(30000, 20))).cuda()
+    assert ops.kmeanspp_fused_ok(X, 10 * (2 + int(np.log(8))))
+    got = kmeans(X, 8, n_init=10, random_state=0, max_iter=25, backend="device",
+                 device_restart_factor=1)
+    assert adjusted_rand_score(truth, got) > 0.99
+
+
 def test_pairwise_dist_and_knn_density():
     """f64 MFMA distance tiles + radix-select neighbour sums vs sklearn/numpy."""
     from sklearn.metrics import euclidean_distances

@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--n-iter", type=int, default=20)
     ap.add_argument("--max-iter-harmony", type=int, default=10)
+    ap.add_argument("--profile", default=None, help="cProfile the Harmony stage into this file")
     a = ap.parse_args()
     t = {}
     t0 = time.perf_counter()
@@ -74,9 +75,22 @@ def main():
     base = os.path.join(work, "hm")
     p = Preprocess(random_seed=0)
     t0 = time.perf_counter()
+    prof = None
+    if a.profile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     corrected, tp10k, hvgs = p.preprocess_for_cnmf(
         ad, harmony_vars=["cov0", "cov1", "cov2", "cov3"], n_top_rna_genes=a.hvg,
         makeplots=False, max_iter_harmony=a.max_iter_harmony, save_output_base=base)
+    if prof is not None:
+        import io
+        import pstats
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
+        with open(a.profile, "w") as fh:
+            fh.write(buf.getvalue())
     torch.cuda.synchronize() if torch.cuda.is_available() else None
     t["preprocess_harmony"] = time.perf_counter() - t0
     obj = cNMF(output_dir=work, name="hm_cnmf")
