@@ -55,6 +55,9 @@ def main() -> int:
                     help="multi-GPU scaling mode (see module docstring)")
     ap.add_argument("--kmin", type=int, default=None)
     ap.add_argument("--kmax", type=int, default=None)
+    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "xgmi"],
+                    help="dp mode: RCCL ring all-reduce or the one-shot xGMI peer-memory "
+                         "all-reduce (parallel/xgmi.py)")
     ap.add_argument("--beta-loss", default="frobenius")
     ap.add_argument("--max-nmf-iter", type=int, default=1000)
     ap.add_argument("--batch-size", type=int, default=5000)
@@ -90,6 +93,7 @@ def main() -> int:
         segs = dp_row_segments(X.shape[0], args.batch_size, rank, world)
         X = np.concatenate([X[a:b] for a, b in segs])
         row_map, schedule = dp_layout(segs)
+        os.environ["CNMF_ALLREDUCE"] = args.allreduce
         comm = DistComm()
     Xd = torch.from_numpy(X).to(dev)
     opts = NMFOptions(n_components=args.k, init="random", beta_loss=args.beta_loss,
@@ -149,7 +153,9 @@ def main() -> int:
             if len(grid) > 1 else f"NMF replicates/sec (K={args.k}, n_iter={args.n_iter})"
         par = {"weak": f"replicate-parallel x{world}",
                "strong": f"replicate-parallel x{world} (fixed {n_total}-replicate ledger)",
-               "dp": f"cell-sharded DP x{world} (RCCL all-reduce per online step)"}[args.mode]
+               "dp": f"cell-sharded DP x{world} ("
+                     f"{'one-shot xGMI' if args.allreduce == 'xgmi' else 'RCCL'} all-reduce "
+                     "per online step)"}[args.mode]
         out = {
             "metric": metric,
             "value": round(reps_per_sec, 3),
@@ -179,6 +185,8 @@ def main() -> int:
             },
         }
         print(json.dumps(out), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
     return 0

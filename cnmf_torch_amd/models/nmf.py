@@ -859,6 +859,9 @@ class NMFBatchSolver:
             ks_out = ks
         if self.X.device.type == "cuda":
             ops.coop_check(self.X.device)
+            check = getattr(self.comm, "check", None)
+            if check is not None:     # one-shot xGMI all-reduce gave up on a peer?
+                check()
         stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": hi.tolist(),
                  "w_inner_iters": wi.tolist()}
         uni = np.unique(ks_out)

@@ -57,6 +57,7 @@ class DistComm(LocalComm):
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        self._xgmi = None           # one-shot xGMI all-reduce (CNMF_ALLREDUCE=xgmi), lazy
 
     @property
     def is_distributed(self) -> bool:
@@ -67,9 +68,34 @@ class DistComm(LocalComm):
             return torch.device("cuda", torch.cuda.current_device())
         return torch.device("cpu")
 
+    def _xgmi_for(self, t: torch.Tensor):
+        """The one-shot xGMI reducer when it is enabled and takes ``t`` (float32 device
+        buffers up to its capacity; parallel/xgmi.py), else None.  Created collectively on
+        the first device all-reduce: every rank of a DP solve issues the same sequence."""
+        if t.device.type != "cuda":
+            return None
+        if self._xgmi is None:
+            from . import xgmi
+
+            self._xgmi = xgmi.XgmiAllReduce(self.group, t.device) if xgmi.wanted() else False
+        return self._xgmi if (self._xgmi and self._xgmi.supports(t)) else None
+
+    def check(self) -> None:
+        """Raise if a one-shot xGMI all-reduce gave up on a peer (host sync)."""
+        if self._xgmi:
+            self._xgmi.check()
+
+    def close(self) -> None:
+        if self._xgmi:
+            self._xgmi.close()
+        self._xgmi = None
+
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world_size == 1:
             return t
+        xg = self._xgmi_for(t)
+        if xg is not None:
+            return xg(t)
         if self.backend != "nccl" and t.device.type != "cpu":
             host = t.cpu()
             self._dist.all_reduce(host, group=self.group)

@@ -5,6 +5,7 @@
 #include <pybind11/pybind11.h>
 
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -317,5 +318,49 @@ PYBIND11_MODULE(_hip, m) {
           check(cnmf_count_unit_check(P<const float>(X), ldx, N, G, P<const float>(mn),
                                       P<unsigned>(bad), reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_count_unit_check");
+        });
+
+  // one-shot xGMI all-reduce (xgmi_allreduce.hip): workspace, IPC handles, launch
+  m.def("xgmi_data_offset", []() { return cnmf_xgmi_data_offset(); });
+  m.def("xgmi_max_ranks", []() { return cnmf_xgmi_max_ranks(); });
+  m.def("xgmi_max_blocks", []() { return cnmf_xgmi_max_blocks(); });
+  m.def("xgmi_alloc", [](long long cap) {
+    void* p = nullptr;
+    check(cnmf_xgmi_alloc(cap, &p), "cnmf_xgmi_alloc");
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("xgmi_free", [](uintptr_t p) { check(hipFree(P<void>(p)), "hipFree"); });
+  m.def("xgmi_handle", [](uintptr_t p) {
+    hipIpcMemHandle_t h;
+    check(hipIpcGetMemHandle(&h, P<void>(p)), "hipIpcGetMemHandle");
+    return py::bytes(reinterpret_cast<const char*>(&h), sizeof(h));
+  });
+  m.def("xgmi_open", [](py::bytes b) {
+    std::string s = b;
+    hipIpcMemHandle_t h;
+    if (s.size() != sizeof(h)) throw std::runtime_error("xgmi_open: bad IPC handle size");
+    std::memcpy(&h, s.data(), sizeof(h));
+    void* p = nullptr;
+    check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+    return reinterpret_cast<uintptr_t>(p);
+  });
+  m.def("xgmi_close", [](uintptr_t p) {
+    check(hipIpcCloseMemHandle(P<void>(p)), "hipIpcCloseMemHandle");
+  });
+  m.def("xgmi_wall_clock_khz", [](int dev) {
+    int v = 0;
+    check(hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev),
+          "hipDeviceGetAttribute");
+    return v;
+  });
+  m.def("xgmi_allreduce",
+        [](uintptr_t peers, int world, int rank, uintptr_t in, uintptr_t out, long long n,
+           long long cap, unsigned epoch, unsigned long long limit, uintptr_t timeout,
+           int blocks, uintptr_t stream) {
+          check(cnmf_xgmi_allreduce(P<const unsigned long long>(peers), world, rank,
+                                    P<const float>(in), P<float>(out), n, cap, epoch, limit,
+                                    P<int>(timeout), blocks,
+                                    reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_xgmi_allreduce");
         });
 }

@@ -140,4 +140,15 @@ hipError_t cnmf_colstats(const float* X, long long ldx, int N, int G, float* pmi
 hipError_t cnmf_count_unit_check(const float* X, long long ldx, int N, int G, const float* mn,
                                  unsigned* bad, hipStream_t stream);
 
+
+// xgmi_allreduce.hip: one-shot all-reduce over IPC-mapped peer workspaces
+long long cnmf_xgmi_data_offset();
+int cnmf_xgmi_max_ranks();
+int cnmf_xgmi_max_blocks();
+hipError_t cnmf_xgmi_alloc(long long cap, void** ptr);
+hipError_t cnmf_xgmi_allreduce(const unsigned long long* peers, int world, int rank,
+                               const float* in, float* out, long long n, long long cap,
+                               unsigned epoch, unsigned long long limit, int* timeout,
+                               int blocks, hipStream_t stream);
+
 }

@@ -133,3 +133,95 @@ def tp_consensus_worker(rank, world, port, output_dir, name, k):
     distributed_consensus(cNMF(output_dir=output_dir, name=name), [k], density_threshold=0.5,
                           show_clustering=False, backend="gloo")
     dist.destroy_process_group()
+
+
+def xgmi_worker(rank, world, port, out_dir):
+    """One-shot xGMI all-reduce against gloo's (several processes on ONE GPU here: the IPC
+    mapping and the flag handshake are the same as across the GPUs of a node)."""
+    _init(rank, world, port)
+    from cnmf_torch_amd.parallel.comm import DistComm
+    from cnmf_torch_amd.parallel.xgmi import XgmiAllReduce, XgmiTimeout
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    xg = XgmiAllReduce(None, dev, cap=1 << 16, timeout_ms=3000)
+    res = {}
+    # back-to-back calls without host syncs (both workspace parities in flight); sizes hit
+    # the float4 body, scalar tails and a buffer at capacity; an unaligned view too
+    sizes = [1, 3, 4, 1000, 4097, 1 << 16, 777, 65533, 5, 4096] * 6
+    ins, outs = [], []
+    for i, n in enumerate(sizes):
+        g = torch.Generator().manual_seed(1000 * i + rank)
+        t = torch.randn(n, generator=g).to(dev)
+        ins.append(t.cpu())
+        if i % 3 == 2:      # out of place
+            o = torch.empty_like(t)
+            outs.append(xg(t, o))
+        else:
+            outs.append(xg(t))
+    unal = torch.randn(1 << 12 | 1, generator=torch.Generator().manual_seed(rank)).to(dev)[1:]
+    ins.append(unal.cpu())
+    outs.append(xg(unal))
+    torch.cuda.synchronize()
+    xg.check()
+    for i, (a, o) in enumerate(zip(ins, outs)):
+        ref = a.clone()
+        dist.all_reduce(ref)
+        res[f"err{i}"] = float((o.cpu() - ref).abs().max())
+        res[f"sum{i}"] = o.cpu().numpy()
+    # DistComm routes device float32 buffers here under CNMF_ALLREDUCE=xgmi
+    os.environ["CNMF_ALLREDUCE"] = "xgmi"
+    comm = DistComm()
+    t = torch.full((10,), float(rank + 1), device=dev)
+    comm.allreduce_(t)
+    comm.check()
+    res["comm"] = t.cpu().numpy()
+    res["comm_is_xgmi"] = bool(comm._xgmi)
+    comm.close()
+    # a rank that never arrives: the kernel gives up after the limit and the flag raises
+    timed_out = False
+    dist.barrier()
+    xg.limit = xg.limit // 3000 * 200                       # 200 ms
+    if rank == 0:
+        xg(torch.ones(64, device=dev))
+        torch.cuda.synchronize()
+        try:
+            xg.check()
+        except XgmiTimeout:
+            timed_out = True
+    res["timed_out"] = timed_out
+    xg.close()
+    np.savez(os.path.join(out_dir, f"xgmi{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def xgmi_dp_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, allreduce):
+    """Cell-sharded DP solve on one GPU per process with the all-reduce over xGMI peer
+    memory or staged through gloo."""
+    os.environ["CNMF_ALLREDUCE"] = allreduce
+    # both ranks share one GPU here: no cooperative (co-residency assuming) solves
+    os.environ["CNMF_SOLVE_COOP"] = "0"
+    _init(rank, world, port)
+    from cnmf_torch_amd import ops
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+
+    ops.refresh_env()
+    from cnmf_torch_amd.parallel.comm import DistComm
+    from cnmf_torch_amd.parallel.runner import dp_layout, dp_row_segments
+
+    torch.cuda.set_device(0)
+    segs = dp_row_segments(X.shape[0], opts_kw["online_chunk_size"], rank, world)
+    row_map, sched = dp_layout(segs)
+    Xl = torch.from_numpy(np.concatenate([X[a:b] for a, b in segs])).cuda()
+    comm = DistComm()
+    solver = NMFBatchSolver(Xl, NMFOptions(n_components=K, **opts_kw), comm=comm,
+                            row_map=row_map, schedule=sched)
+    res = solver.run(seeds)
+    np.save(os.path.join(out_dir, f"W_{allreduce}{rank}.npy"), res.W.cpu().numpy())
+    np.save(os.path.join(out_dir, f"err_{allreduce}{rank}.npy"), res.err)
+    res_xg = bool(comm._xgmi)
+    np.save(os.path.join(out_dir, f"used_{allreduce}{rank}.npy"), np.array(res_xg))
+    comm.close()
+    dist.barrier()
+    dist.destroy_process_group()

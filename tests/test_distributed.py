@@ -28,7 +28,10 @@ def _spawn(fn, world, *args):
     mp.spawn(fn, args=(world, _port()) + args, nprocs=world, join=True)
 
 
-def test_comm_primitives(tmp_path):
+@pytest.mark.parametrize("allreduce", ["rccl", "xgmi"])
+def test_comm_primitives(tmp_path, monkeypatch, allreduce):
+    # CNMF_ALLREDUCE=xgmi only reroutes float32 DEVICE buffers: host tensors stay on gloo
+    monkeypatch.setenv("CNMF_ALLREDUCE", allreduce)
     _spawn(W.comm_worker, 3, str(tmp_path))
     for r in range(3):
         t, s, m, n, last = np.load(tmp_path / f"comm{r}.npy")
