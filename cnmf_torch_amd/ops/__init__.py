@@ -52,7 +52,7 @@ def _require_native():
 # Per-op debug / tuning knobs, read ONCE (at import, or by refresh_env()): every op
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
 _ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
-             "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT")
+             "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES")
 _ENV: dict = {}
 
 
@@ -1188,7 +1188,19 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
                      B.stride(0), b_rows, C.data_ptr(), C.stride(0),
                      col_scale.data_ptr() if col_scale is not None else 0, int(M), int(N),
                      int(Kd), pa, pb, int(bool(accumulate)), int(variant), int(ksplit), slab,
-                     _stream_ptr(C))
+                     gemm_stages(variant), _stream_ptr(C))
+
+
+def gemm_stages(variant: int) -> int:
+    """LDS pipeline depth of the split GEMM (k-steps in flight + 1; the kernel drops to 2
+    where 3 stages would not fit in LDS).  Measured on MI355X
+    (profiles/r2_gemm_stages_sweep.txt): the 8-wave tiles (128x256, 256x128; one
+    workgroup per CU) gain from a third stage (stats GEMM of the K-grid 442 -> 407 us),
+    the 2- and 4-wave tiles lose more occupancy than they gain latency cover (64x128
+    numerator 80 -> 108 us).  CNMF_GEMM_STAGES overrides (A/B runs)."""
+    if _ENV["CNMF_GEMM_STAGES"]:
+        return int(_ENV["CNMF_GEMM_STAGES"])
+    return 3 if variant in (1, 2) else 2
 
 
 # ----------------------------------------------------------------------------- column stats

@@ -76,7 +76,7 @@ __device__ __forceinline__ void glds16(const unsigned short* g, unsigned char* l
                                    (void __attribute__((address_space(3)))*)lds, 16, 0, 0);
 }
 
-template <int PA, int PB, int BK, int WM, int WN>
+template <int PA, int PB, int BK, int WM, int WN, int NS>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmParams p) {
   constexpr int NT = 64 * WM * WN;            // threads
   constexpr int BM = 64 * WM, BN = 64 * WN;   // each wave owns a 64 x 64 output block
@@ -88,9 +88,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
   constexpr int B_LD = BN * CPR / NT;
   constexpr int LOADS = PA * A_LD + PB * B_LD;
   static_assert(A_LD * NT == BM * CPR && B_LD * NT == BN * CPR, "tile / thread mismatch");
-  static_assert(LOADS < 64, "vmcnt is a 6-bit counter");
-  static_assert(2 * STAGE <= 160 * 1024, "LDS");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+  static_assert(NS >= 2 && NS <= 4, "2..4 stages");
+  static_assert((NS >= 4 ? 2 : 1) * LOADS < 64, "vmcnt is a 6-bit counter");
+  static_assert(NS * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE];
 
   // XCD-aware bijective remap; consecutive logical tiles share the M panel (the A
   // operand: three planes, the larger one), so an XCD keeps its A panels in its L2 and
@@ -147,16 +148,24 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-  if (kb < ke) issue(0, kb * BK);
+  // NS-stage ring: stage kt+NS-1 is issued right after the barrier that certifies every
+  // wave has finished multiplying stage kt-1 (whose slot it refills), so ONE barrier per
+  // k-step and NS-1 k-steps of loads in flight behind the MFMAs
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (kb + s < ke) issue(s, (kb + s) * BK);
   for (int kt = kb; kt < ke; ++kt) {
-    const int cur = (kt - kb) & 1;
-    if (kt + 1 < ke) {
-      issue(cur ^ 1, (kt + 1) * BK);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    const int cur = (kt - kb) % NS;
+    // stage kt has landed once at most min(NS-2, ke-1-kt) later stages are outstanding
+    const int later = min(NS - 2, ke - 1 - kt);
+    if (later >= 2) {
+      if constexpr (NS >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LOADS) : "memory");
+    } else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LOADS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's fragment reads of the slot refilled below have returned
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < ke) issue((kt - kb + NS - 1) % NS, (kt + NS - 1) * BK);
     const unsigned char* As = smem + cur * STAGE;
     const unsigned char* Bs = As + PA * A_TILE;
 #pragma unroll
@@ -192,10 +201,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
                 acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[i][mi], bfr[j][ni],
                                                                       acc[mi][ni], 0, 0, 0);
     }
-    // every wave's reads of `cur` have returned before anyone refills it (the compiler
-    // would otherwise leave the last ds_reads in flight across the barrier)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
   }
 
   if (p.ksplit > 1) {   // raw partial tile -> slab ks (reduced in order by gemm_reduce)
@@ -315,23 +320,30 @@ __global__ void gemm_reduce_kernel(const float* __restrict__ slab, int ksplit, i
 }
 
 template <int PA, int PB, int BK, int WM, int WN>
-static hipError_t launch_gemm(PlaneGemmParams p, hipStream_t s) {
+static hipError_t launch_gemm(PlaneGemmParams p, int stages, hipStream_t s) {
   p.tiles_m = (p.M + 64 * WM - 1) / (64 * WM);
   p.tiles_n = (p.N + 64 * WN - 1) / (64 * WN);
-  hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN>),
-                     dim3(p.tiles_m * p.tiles_n, p.ksplit), dim3(64 * WM * WN), 0, s, p);
+  const dim3 grid(p.tiles_m * p.tiles_n, p.ksplit), block(64 * WM * WN);
+  constexpr int stage_bytes = (PA * 64 * WM + PB * 64 * WN) * BK * 2;
+  if constexpr (3 * stage_bytes <= 160 * 1024) {
+    if (stages >= 3) {
+      hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN, 3>), grid, block, 0, s, p);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN, 2>), grid, block, 0, s, p);
   return hipGetLastError();
 }
 
 // tile variants: 0 = 128x128 (4 waves), 1 = 128x256 (8 waves), 2 = 256x128 (8 waves),
 // 3 = 64x128 (2 waves)
 template <int PA, int PB, int BK>
-static hipError_t launch_variant(int v, const PlaneGemmParams& p, hipStream_t s) {
+static hipError_t launch_variant(int v, const PlaneGemmParams& p, int stages, hipStream_t s) {
   switch (v) {
-    case 0: return launch_gemm<PA, PB, BK, 2, 2>(p, s);
-    case 1: return launch_gemm<PA, PB, BK, 2, 4>(p, s);
-    case 2: return launch_gemm<PA, PB, BK, 4, 2>(p, s);
-    default: return launch_gemm<PA, PB, BK, 1, 2>(p, s);
+    case 0: return launch_gemm<PA, PB, BK, 2, 2>(p, stages, s);
+    case 1: return launch_gemm<PA, PB, BK, 2, 4>(p, stages, s);
+    case 2: return launch_gemm<PA, PB, BK, 4, 2>(p, stages, s);
+    default: return launch_gemm<PA, PB, BK, 1, 2>(p, stages, s);
   }
 }
 
@@ -350,7 +362,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
                                        long long b_plane, int b_rows, float* C, long long ldc,
                                        const float* col_scale, int M, int N, int Kd, int pa,
                                        int pb, int accumulate, int variant, int ksplit,
-                                       float* slab, hipStream_t stream) {
+                                       float* slab, int stages, hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
   const int bk = cnmf_gemm_planes_bk(pb);
   if (pa < 2 || pa > 3 || pb < 1 || pb > 3 || Kd <= 0 || Kd % bk || lda % 8 || ldb % 8 ||
@@ -365,12 +377,12 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   p.ksplit = ksplit; p.slab = slab;
   hipError_t e;
   switch (pa * 4 + pb) {
-    case 9: e = cnmf::launch_variant<2, 1, 32>(variant, p, stream); break;
-    case 10: e = cnmf::launch_variant<2, 2, 32>(variant, p, stream); break;
-    case 11: e = cnmf::launch_variant<2, 3, 32>(variant, p, stream); break;
-    case 13: e = cnmf::launch_variant<3, 1, 32>(variant, p, stream); break;
-    case 14: e = cnmf::launch_variant<3, 2, 32>(variant, p, stream); break;
-    default: e = cnmf::launch_variant<3, 3, 32>(variant, p, stream); break;
+    case 9: e = cnmf::launch_variant<2, 1, 32>(variant, p, stages, stream); break;
+    case 10: e = cnmf::launch_variant<2, 2, 32>(variant, p, stages, stream); break;
+    case 11: e = cnmf::launch_variant<2, 3, 32>(variant, p, stages, stream); break;
+    case 13: e = cnmf::launch_variant<3, 1, 32>(variant, p, stages, stream); break;
+    case 14: e = cnmf::launch_variant<3, 2, 32>(variant, p, stages, stream); break;
+    default: e = cnmf::launch_variant<3, 3, 32>(variant, p, stages, stream); break;
   }
   if (e != hipSuccess || ksplit == 1) return e;
   const long long total = (long long)M * N;
