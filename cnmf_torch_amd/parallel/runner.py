@@ -46,12 +46,18 @@ def init_distributed(backend: str | None = None):
     return DistComm(), dev
 
 
-def _incomplete_jobs(obj, run_params, skip_completed_runs: bool):
+def _incomplete_jobs(obj, run_params, skip_completed_runs: bool, comm=None):
+    """Ledger rows still to solve.  Under several ranks the list is rank 0's: a rank that
+    looked later could see files a faster rank has already written in THIS run, deal
+    itself a different shard, and leave replicates that no rank solves."""
     if not skip_completed_runs:
         return list(range(len(run_params)))
     done = [os.path.exists(obj.paths["iter_spectra"] % (int(k), int(i)))
             for k, i in zip(run_params["n_components"], run_params["iter"])]
-    return [i for i, d in enumerate(done) if not d]
+    jobs = [i for i, d in enumerate(done) if not d]
+    if comm is not None and comm.is_distributed:
+        jobs = comm.all_gather_object(jobs)[0]
+    return jobs
 
 
 def distributed_factorize(obj, skip_completed_runs: bool = False, replicate_batch=None,
@@ -65,7 +71,7 @@ def distributed_factorize(obj, skip_completed_runs: bool = False, replicate_batc
 
     comm, dev = init_distributed(backend)
     run_params = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
-    jobs = _incomplete_jobs(obj, run_params, skip_completed_runs)
+    jobs = _incomplete_jobs(obj, run_params, skip_completed_runs, comm)
     mine = shard_by_k(run_params, jobs, comm.rank, comm.world_size)
     collect = {} if gather_spectra else None
     obj.factorize_jobs(mine, worker_label=comm.rank, device=dev,
@@ -225,7 +231,7 @@ def dp_factorize(obj, skip_completed_runs: bool = False, replicate_batch=None,
 
     comm, dev = init_distributed(backend)
     run_params = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
-    jobs = _incomplete_jobs(obj, run_params, skip_completed_runs)
+    jobs = _incomplete_jobs(obj, run_params, skip_completed_runs, comm)
     n_rows, _ = h5ad_shape(obj.paths["normalized_counts"])
     chunk = int(load_yaml(obj.paths["nmf_run_parameters"]).get("online_chunk_size", 5000))
     segs = dp_row_segments(n_rows, chunk, comm.rank, comm.world_size)

@@ -273,3 +273,25 @@ def test_gene_sharded_consensus_matches_serial(prepared):
         assert list(got.columns) == list(ser[key].columns), key
         np.testing.assert_allclose(got.values, ser[key].values, rtol=1e-5, atol=1e-9,
                                    err_msg=key)
+
+
+def test_incomplete_jobs_are_rank0s_list(prepared):
+    """Resume under several ranks: every rank deals its shard from rank 0's list of
+    unfinished replicates, not from its own later look at the files (a faster rank's
+    fresh files would otherwise shift the dealing and leave replicates unsolved)."""
+    from cnmf_torch_amd.parallel.runner import _incomplete_jobs
+
+    d, fn = prepared
+    obj = cNMF(output_dir=str(d), name="jobs_view")
+    obj.prepare(fn, components=[3], n_iter=4, seed=2, num_highvar_genes=100, batch_size=150)
+    rp = load_df_from_npz(obj.paths["nmf_replicate_parameters"])
+
+    class _Comm:
+        is_distributed = True
+
+        def all_gather_object(self, obj_):
+            return [[0, 1, 2, 3], obj_]          # rank 0 looked before any file existed
+
+    obj.factorize_jobs([0], run_params=rp, verbose=False)
+    assert _incomplete_jobs(obj, rp, True) == [1, 2, 3]
+    assert _incomplete_jobs(obj, rp, True, _Comm()) == [0, 1, 2, 3]
