@@ -595,6 +595,9 @@ def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch
     if algo != "bpp":
         ops.solve("hals" if algo == "halsvar" else algo, x3, numer3, gram3, **kw)
         return
+    gram_of = kw.pop("gram_of", None)
+    if gram3 is None:
+        gram3 = ops.gram(gram_of)
     planes, colmul = kw.pop("planes", None), kw.pop("planes_colmul", None)
     R, K = x3.shape[0], x3.shape[1]
     active = kw.get("active")
@@ -732,6 +735,9 @@ def native_rank(K: int) -> int:
     if K > 64:
         raise ValueError(f"K={K}: the native kernels cover K <= 64")
     return -(-K // 8) * 8
+
+
+_GRAM_PROLOGUE = os.environ.get("CNMF_SOLVE_GRAM_PROLOGUE", "0") == "1"
 
 
 def _graphs_enabled(X: torch.Tensor) -> bool:
@@ -1181,8 +1187,15 @@ class NMFBatchSolver:
                             self.solve_planes("h", rows, b - a)
                         for g in groups:
                             ga = active[g.pos]
-                            WWT = ops.gram(g.rep3(W), out=g.gram3(wwt_buf), active=ga)
+                            # W W^T: its own Gram launch.  CNMF_SOLVE_GRAM_PROLOGUE=1 has
+                            # the matrix-core solve form it in its prologue instead --
+                            # measured slower on the bench (every usage-slice workgroup
+                            # re-reads W at L2 latency: +9.4 ms of solve against -4.2 ms
+                            # of Gram launches per 13 steps; profiles/README.md)
+                            WWT = None if (algo == "mu" and _GRAM_PROLOGUE) else \
+                                ops.gram(g.rep3(W), out=g.gram3(wwt_buf), active=ga)
                             _inner_solve(algo, g.rep3(hcols), g.rep3(numerT), WWT,
+                                         gram_of=g.rep3(W) if WWT is None else None,
                                          max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
                                          l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
                                          iters_out=h_it[g.pos], conv_mode=cmode,

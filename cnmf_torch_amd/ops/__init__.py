@@ -113,9 +113,14 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           iters_out: torch.Tensor | None = None, nsplit: int = 1, conv_mode: int = 0,
           check_every: int = 10, variant: str = "auto",
           active: torch.Tensor | None = None, coop: int | str = "auto",
-          planes: torch.Tensor | None = None, planes_colmul: torch.Tensor | None = None) -> None:
+          planes: torch.Tensor | None = None, planes_colmul: torch.Tensor | None = None,
+          gram_of: torch.Tensor | None = None) -> None:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
+
+    ``gram_of`` (R, K, m) instead of ``gram`` (pass None): the system matrix is
+    F F^T of this factor -- the matrix-core kernel forms it in its prologue (no separate
+    Gram launch), the other kernels get it from :func:`gram`.
 
     Only replicates listed in ``rep_index`` (int32, default all) are touched.
     ``nsplit > 1`` runs a single fixed step with columns split over blocks (batch mode).
@@ -136,6 +141,13 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     """
     a = ALGOS[algo]
     R, K, n = x.shape
+    if gram is None:
+        if gram_of is None or gram_of.shape[:2] != (R, K):
+            raise ValueError("solve: pass gram (R, K, K) or gram_of (R, K, m)")
+    elif gram_of is not None:
+        raise ValueError("solve: gram and gram_of are exclusive")
+    if gram is None and not use_native(x):
+        gram = torch.bmm(gram_of, gram_of.transpose(1, 2))
     if not use_native(x):
         reference.solve(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2,
                         eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every,
@@ -153,10 +165,14 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                          "of 8, see models.nmf.native_rank)")
     _check_block_view("x", x, R, K, n)
     _check_block_view("numer", numer, R, K, n)
-    if gram.shape != (R, K, K) or gram.dtype != torch.float32:
-        raise ValueError(f"gram: expected float32 {(R, K, K)}, got {gram.dtype} {tuple(gram.shape)}")
-    gram = gram.contiguous()
-    devs = {x.device, numer.device, gram.device}
+    if gram is not None:
+        if gram.shape != (R, K, K) or gram.dtype != torch.float32:
+            raise ValueError(f"gram: expected float32 {(R, K, K)}, got {gram.dtype} "
+                             f"{tuple(gram.shape)}")
+        gram = gram.contiguous()
+    else:
+        _check_block_view("gram_of", gram_of, R, K, gram_of.shape[2])
+    devs = {x.device, numer.device, (gram if gram is not None else gram_of).device}
     if len(devs) != 1:
         raise ValueError(f"solve operands on different devices: {devs}")
     if rep_index is not None:
@@ -187,6 +203,10 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
         S = _mfma_split(n, nblocks, K, nsplit, coop, x.device)
     if S is not None:
         vcode = 3
+    elif gram is None:      # a VALU kernel: form the Gram first
+        gram = _gram_op(gram_of, active=active)
+    if S is not None:
+        pass
     elif variant == "mfma":
         raise ValueError(f"solve: variant 'mfma' does not cover algo={algo} K={K} n={n} "
                          f"with {nblocks} replicates")
@@ -227,8 +247,13 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             raise ValueError("planes_colmul: contiguous float32 with >= n entries")
         pl_ptr, pl_ld, pl_plane = planes.data_ptr(), planes.stride(1), planes.stride(0)
         pl_rs, pl_cols = K * pl_ld, planes.shape[2]
+    gs_ptr = gs_rs = gs_ld = gs_cols = 0
+    if gram is None:
+        gs_ptr, gs_rs, gs_ld, gs_cols = (gram_of.data_ptr(), gram_of.stride(0),
+                                         gram_of.stride(1), gram_of.shape[2])
     h.solve(a, K, x.data_ptr(), x.stride(0), x.stride(1), numer.data_ptr(), numer.stride(0),
-            numer.stride(1), gram.data_ptr(), K * K, ri, nblocks, n, int(max_iter), float(tol),
+            numer.stride(1), gram.data_ptr() if gram is not None else 0, K * K, ri, nblocks, n,
+            int(max_iter), float(tol),
             float(l1_num), float(l1_den), float(l2), float(eps),
             lin_out.data_ptr() if lin_out is not None else 0,
             quad_out.data_ptr() if quad_out is not None else 0,
@@ -237,7 +262,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             active.data_ptr() if active is not None else 0, int(S), ws_slots, ws_count,
             int(gen), int(epochs), ws_flag, pl_ptr, int(pl_rs), int(pl_ld), int(pl_plane),
             planes_colmul.data_ptr() if (planes is not None and planes_colmul is not None) else 0,
-            int(pl_cols), _stream_ptr(x))
+            int(pl_cols), gs_ptr, int(gs_rs), int(gs_ld), int(gs_cols), _stream_ptr(x))
 
 
 # Cooperative-split bookkeeping.  A launch of S*nblocks 1024-thread workgroups is only safe
@@ -817,6 +842,7 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
 
 
 _GRAM_WS: dict = {}
+_gram_op = gram    # ops.solve's `gram` argument shadows the function there
 
 
 # ----------------------------------------------------------------------------- consensus

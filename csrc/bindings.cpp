@@ -45,7 +45,8 @@ PYBIND11_MODULE(_hip, m) {
            int coop_split, uintptr_t coop_slots, uintptr_t coop_count, unsigned coop_gen,
            int coop_epochs,
            uintptr_t coop_timeout, uintptr_t planes, long long pl_rs, long long pl_ld,
-           long long pl_plane, uintptr_t pl_colmul, int pl_cols, uintptr_t stream) {
+           long long pl_plane, uintptr_t pl_colmul, int pl_cols, uintptr_t gsrc,
+           long long gs_rs, long long gs_ld, int gs_cols, uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
                            max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
@@ -55,6 +56,7 @@ PYBIND11_MODULE(_hip, m) {
                            coop_epochs,
                            P<int>(coop_timeout), P<unsigned short>(planes), pl_rs, pl_ld,
                            pl_plane, P<const float>(pl_colmul), pl_cols,
+                           P<const float>(gsrc), gs_rs, gs_ld, gs_cols,
                            reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");
         });

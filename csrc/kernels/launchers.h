@@ -17,7 +17,8 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       unsigned coop_gen, int coop_epochs,
                       int* coop_timeout, unsigned short* planes, long long pl_rs,
                       long long pl_ld, long long pl_plane, const float* pl_colmul,
-                      int pl_cols, hipStream_t stream);
+                      int pl_cols, const float* gsrc, long long gs_rs, long long gs_ld,
+                      int gs_cols, hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,

@@ -35,7 +35,8 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  int coop_epochs, int* coop_timeout,
                                  unsigned short* planes, long long pl_rs, long long pl_ld,
                                  long long pl_plane, const float* pl_colmul, int pl_cols,
-                                 hipStream_t stream) {
+                                 const float* gsrc, long long gs_rs, long long gs_ld,
+                                 int gs_cols, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
   if ((long long)K * (ldx > ldn ? ldx : ldn) * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
@@ -59,6 +60,9 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.coop_epochs_split = coop_split > 1 ? coop_split : 1;
   p.planes = planes; p.pl_rs = pl_rs; p.pl_ld = pl_ld; p.pl_plane = pl_plane;
   p.pl_colmul = pl_colmul; p.pl_cols = pl_cols;
+  p.gsrc = gsrc; p.gs_rs = gs_rs; p.gs_ld = gs_ld; p.gs_cols = gs_cols;
+  // the in-prologue Gram is a matrix-core kernel feature (K <= 16)
+  if (gsrc && (variant != 3 || K > 16 || gs_cols < 1)) return hipErrorInvalidValue;
   if (planes && pl_cols < ncols) return hipErrorInvalidValue;
   if (coop_split > 1 && nsplit > 1) return hipErrorInvalidValue;
   if (coop_split > cnmf::kCoopMaxSlices) return hipErrorInvalidValue;

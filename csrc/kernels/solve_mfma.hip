@@ -49,18 +49,63 @@ void solve_mfma_kernel(SolveParams p, int T) {
   constexpr int KS = (K + 3) / 4;   // 4-component k-steps (registers per column tile)
   __shared__ float sred[3 + 2 * kCoopMaxSlices];
   __shared__ float sN[TMAX * KS * 64 * kMfmaWaves];
+  static_assert(TMAX * KS * 64 * kMfmaWaves >= kMfmaWaves * 256, "Gram scratch in sN");
   const int rep = p.rep_index ? p.rep_index[blockIdx.x] : (int)blockIdx.x;
   if (p.active && p.active[rep] == 0) return;   // converged replicate: untouched (uniform)
   float* __restrict__ x = p.x + (long long)rep * p.x_rs;
   const float* __restrict__ nu = p.numer + (long long)rep * p.n_rs;
-  const float* __restrict__ gm = p.gram + (long long)rep * p.g_rs;
+  const float* __restrict__ gm = p.gsrc ? nullptr : p.gram + (long long)rep * p.g_rs;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
 
   // Gram fragments (A operand, rows permuted by pi): a[s] = Gram[pi(c)][4 s + g]
   float a[KS];
-  {
-    const int pm = 4 * (c & 3) + (c >> 2);
+  const int pm = 4 * (c & 3) + (c >> 2);
+  if (p.gsrc) {
+    // Gram = F F^T formed here (gram.hip's trick): lane (g, c) feeds F[c][col] as both
+    // A[m = c][k = g] and B[k = g][n = c], so D[i][j] = sum_col F[i][col] F[j][col] with
+    // the 4 columns of one float4 on the k index; waves take 16-column slabs, two
+    // accumulator chains; the 4 wave partials are summed in wave order through sN (not
+    // yet holding numerators), so the result is deterministic
+    const float* __restrict__ f = p.gsrc + (long long)rep * p.gs_rs;
+    const int gcols = p.gs_cols;
+    const long long fld = p.gs_ld;
+    f32x4m g0 = {0.f, 0.f, 0.f, 0.f}, g1 = {0.f, 0.f, 0.f, 0.f};
+    const bool rowok = c < K;
+    const bool fvec = (fld & 3) == 0 && (reinterpret_cast<uintptr_t>(f) & 15) == 0;
+#pragma unroll 4
+    for (int c0 = 16 * wave; c0 < gcols; c0 += 16 * kMfmaWaves) {
+      const int cc = c0 + 4 * g;
+      float v[4];
+      if (fvec && rowok && cc + 3 < gcols) {
+        const float4 t = *reinterpret_cast<const float4*>(f + (long long)c * fld + cc);
+        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = (rowok && cc + e < gcols) ? f[(long long)c * fld + cc + e] : 0.f;
+      }
+      g0 = __builtin_amdgcn_mfma_f32_16x16x4f32(v[0], v[0], g0, 0, 0, 0);
+      g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(v[1], v[1], g1, 0, 0, 0);
+      g0 = __builtin_amdgcn_mfma_f32_16x16x4f32(v[2], v[2], g0, 0, 0, 0);
+      g1 = __builtin_amdgcn_mfma_f32_16x16x4f32(v[3], v[3], g1, 0, 0, 0);
+    }
+    // lane (g, c) holds D[4 g + r][c]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sN[wave * 256 + (4 * g + r) * 16 + c] = g0[r] + g1[r];
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 4 * s + g;
+      float v = 0.f;
+      if (pm < K && k < K) {
+#pragma unroll
+        for (int w = 0; w < kMfmaWaves; ++w) v += sN[w * 256 + pm * 16 + k];
+      }
+      a[s] = v;
+    }
+    __syncthreads();   // sN is refilled with numerators below
+  } else {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k = 4 * s + g;

@@ -1175,3 +1175,34 @@ def test_gemm_two_a_planes_within_fp32_library_error(M, N, K):
     el = float((lib.cpu().double() - ref).abs().max() / scale)
     assert e3 <= e2 * 1.5 + 1e-9
     assert e2 <= max(el, 2e-7), (e2, e3, el)
+
+
+@pytest.mark.parametrize("K,m", [(3, 2000), (10, 2000), (10, 1997), (16, 333), (20, 2000)])
+def test_solve_gram_of_matches_explicit_gram(K, m):
+    """ops.solve(gram_of=F): the matrix-core kernel forms F F^T in its prologue (K <= 16;
+    unaligned widths take the scalar loads), the VALU kernels get ops.gram's -- same
+    iterates as passing the explicit Gram, fixed steps and converged cooperative solves,
+    untouched inactive replicates."""
+    R, n = 6, 2600
+    g = torch.Generator().manual_seed(K + m)
+    dev = torch.device("cuda")
+    F = (torch.rand((R, K, m + 3), generator=g) + 0.05).to(dev)[:, :, 1:m + 1]  # strided
+    gram = torch.bmm(F.double(), F.transpose(1, 2).double()).float()
+    x0 = torch.rand((R, K, n), generator=g) + 0.1
+    numer = (torch.bmm(gram.cpu(), torch.rand((R, K, n), generator=g))).to(dev)
+    active = torch.tensor([1, 1, 0, 1, 1, 1], dtype=torch.int32, device=dev)
+    for max_iter, tol, cm in ((6, -1.0, 0), (300, 1e-4, 1)):
+        outs = []
+        for use_of in (False, True):
+            xg = x0.clone().to(dev)
+            lin = torch.zeros(R, device=dev)
+            it = torch.zeros(R, dtype=torch.int32, device=dev)
+            ops.solve("mu", xg, numer, None if use_of else gram, max_iter=max_iter, tol=tol,
+                      conv_mode=cm, check_every=5, lin_out=lin, iters_out=it, active=active,
+                      gram_of=F if use_of else None)
+            outs.append((xg.cpu(), lin.cpu(), it.cpu()))
+        (xa, la, ia), (xb, lb, ib) = outs
+        torch.testing.assert_close(xb, xa, rtol=2e-5, atol=1e-6)
+        torch.testing.assert_close(lb, la, rtol=2e-5, atol=1e-4)
+        assert (ib - ia).abs().max() <= (0 if tol < 0 else 5)
+        assert torch.equal(xb[2], x0[2])
