@@ -51,8 +51,13 @@ def test_bench_strong_and_dp_modes_two_ranks():
     dp = _bench(["--mode", "dp"], 2)
     assert dp["scaling"] == "strong" and dp["config"]["global_batch"] == 3
     assert dp["config"]["parallelism"].startswith("cell-sharded DP x2")
+    assert "RCCL" in dp["config"]["parallelism"]
     rate = 3 * 2 / (dp["ms_per_step"] * 2 / 1000.0)
     assert abs(dp["value"] - rate) / dp["value"] < 0.01
+    # the xGMI option only reroutes device buffers: the CPU (gloo) run is unchanged
+    xg = _bench(["--mode", "dp", "--allreduce", "xgmi"], 2)
+    assert "one-shot xGMI" in xg["config"]["parallelism"]
+    assert xg["config"]["mean_passes"] == dp["config"]["mean_passes"]
 
 
 def test_bench_dp_mode_same_factorisation_as_one_rank():
