@@ -52,7 +52,7 @@ def _require_native():
 # Per-op debug / tuning knobs, read ONCE (at import, or by refresh_env()): every op
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
 _ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
-             "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES")
+             "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES", "CNMF_GEMM_BK")
 _ENV: dict = {}
 
 
@@ -1082,8 +1082,21 @@ def philox_fill(out: torch.Tensor, seeds: torch.Tensor, scales: torch.Tensor, st
 
 # ----------------------------------------------------------------------------- split GEMM
 def planes_bk(pb: int) -> int:
-    """k granularity (BK) of the split-precision GEMM for ``pb`` B planes."""
-    return 32
+    """k granularity the split-precision GEMM's plane buffers are padded to (a multiple of
+    both k-step depths, 32 and 64)."""
+    return 64
+
+
+def gemm_kstep(variant: int) -> int:
+    """k-step depth (BK) of the split GEMM: 64 = two MFMA k-steps per LDS stage and barrier
+    (the kernel drops to 32 where a 64-deep stage pair would not fit in LDS, or Kd is not
+    a multiple of 64).  Measured on MI355X (profiles/r2_gemm_bk_sweep.txt): the 8-wave
+    128x256 tiles gain (K=10 statistics GEMM 62 -> 60 us, K-grid GEMMs 410/393 -> 400/381 us,
+    as 2 stages of 64 against 3 of 32), the 2- and 4-wave tiles lose (64x128 numerator
+    77 -> 97 us).  CNMF_GEMM_BK overrides (A/B runs)."""
+    if _ENV["CNMF_GEMM_BK"]:
+        return int(_ENV["CNMF_GEMM_BK"])
+    return 64 if variant in (1, 2) else 32
 
 
 _GEMM_TILES = {0: (128, 128), 1: (128, 256), 2: (256, 128), 3: (64, 128)}
@@ -1175,7 +1188,8 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
     exact bf16 splits are A (3 planes; or its first 2, see gemm_a_planes) and B (1-3
     planes; 1 or 2 when B holds integers).
     A/B: int16 (P, rows, ld) views with unit k stride (row offsets / k offsets are just
-    views); k must be zero-padded in A up to ``Kd`` (a multiple of planes_bk)."""
+    views); k must be zero-padded in A up to ``Kd`` (a multiple of 32; of planes_bk for
+    the deep k-step)."""
     pa, a_rows, _ = A.shape
     pb, b_rows, _ = B.shape
     for name, t in (("A", A), ("B", B)):
@@ -1185,7 +1199,7 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
             raise ValueError(f"{name}: 16-byte aligned base required (k offset % 8 == 0)")
         if t.shape[2] < Kd:
             raise ValueError(f"{name}: k extent {t.shape[2]} < Kd {Kd}")
-    if not 2 <= pa <= 3 or not 1 <= pb <= 3 or Kd % planes_bk(pb) or M > a_rows or N > b_rows:
+    if not 2 <= pa <= 3 or not 1 <= pb <= 3 or Kd % 32 or M > a_rows or N > b_rows:
         raise ValueError(f"gemm_planes: planes {pa}/{pb}, Kd {Kd}, M {M}/{a_rows}, N {N}/{b_rows}")
     if C.dtype != torch.float32 or C.stride(1) != 1 or C.shape[0] < M or C.shape[1] < N:
         raise ValueError("C: float32 (>= M, >= N) with unit column stride required")
@@ -1214,7 +1228,7 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
                      B.stride(0), b_rows, C.data_ptr(), C.stride(0),
                      col_scale.data_ptr() if col_scale is not None else 0, int(M), int(N),
                      int(Kd), pa, pb, int(bool(accumulate)), int(variant), int(ksplit), slab,
-                     gemm_stages(variant), _stream_ptr(C))
+                     gemm_stages(variant), gemm_kstep(variant), _stream_ptr(C))
 
 
 def gemm_stages(variant: int) -> int:

@@ -288,11 +288,11 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t A, long long lda, long long a_plane, int a_rows, uintptr_t B,
            long long ldb, long long b_plane, int b_rows, uintptr_t C, long long ldc,
            uintptr_t col_scale, int M, int N, int Kd, int pa, int pb, int accumulate,
-           int variant, int ksplit, uintptr_t slab, int stages, uintptr_t stream) {
+           int variant, int ksplit, uintptr_t slab, int stages, int kstep, uintptr_t stream) {
           check(cnmf_gemm_planes(P<const unsigned short>(A), lda, a_plane, a_rows,
                                  P<const unsigned short>(B), ldb, b_plane, b_rows, P<float>(C),
                                  ldc, P<const float>(col_scale), M, N, Kd, pa, pb, accumulate,
-                                 variant, ksplit, P<float>(slab), stages,
+                                 variant, ksplit, P<float>(slab), stages, kstep,
                                  reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_gemm_planes");
         });

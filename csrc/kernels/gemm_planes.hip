@@ -321,10 +321,13 @@ __global__ void gemm_reduce_kernel(const float* __restrict__ slab, int ksplit, i
 
 template <int PA, int PB, int BK, int WM, int WN>
 static hipError_t launch_gemm(PlaneGemmParams p, int stages, hipStream_t s) {
+  constexpr int stage_bytes = (PA * 64 * WM + PB * 64 * WN) * BK * 2;
+  if constexpr (BK > 32 && 2 * stage_bytes > 160 * 1024) {
+    return launch_gemm<PA, PB, 32, WM, WN>(p, stages, s);   // deep k-step does not fit
+  } else {
   p.tiles_m = (p.M + 64 * WM - 1) / (64 * WM);
   p.tiles_n = (p.N + 64 * WN - 1) / (64 * WN);
   const dim3 grid(p.tiles_m * p.tiles_n, p.ksplit), block(64 * WM * WN);
-  constexpr int stage_bytes = (PA * 64 * WM + PB * 64 * WN) * BK * 2;
   if constexpr (3 * stage_bytes <= 160 * 1024) {
     if (stages >= 3) {
       hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN, 3>), grid, block, 0, s, p);
@@ -333,12 +336,13 @@ static hipError_t launch_gemm(PlaneGemmParams p, int stages, hipStream_t s) {
   }
   hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN, 2>), grid, block, 0, s, p);
   return hipGetLastError();
+  }
 }
 
 // tile variants: 0 = 128x128 (4 waves), 1 = 128x256 (8 waves), 2 = 256x128 (8 waves),
 // 3 = 64x128 (2 waves)
 template <int PA, int PB, int BK>
-static hipError_t launch_variant(int v, const PlaneGemmParams& p, int stages, hipStream_t s) {
+static hipError_t launch_variant_bk(int v, const PlaneGemmParams& p, int stages, hipStream_t s) {
   switch (v) {
     case 0: return launch_gemm<PA, PB, BK, 2, 2>(p, stages, s);
     case 1: return launch_gemm<PA, PB, BK, 2, 4>(p, stages, s);
@@ -347,9 +351,19 @@ static hipError_t launch_variant(int v, const PlaneGemmParams& p, int stages, hi
   }
 }
 
+// k-step depth: 64 (two MFMA k-steps per LDS stage and barrier: the second step's
+// fragment reads overlap the first step's MFMAs) where it fits and divides Kd, else 32
+template <int PA, int PB>
+static hipError_t launch_variant(int v, const PlaneGemmParams& p, int stages, int bk,
+                                 hipStream_t s) {
+  if (bk >= 64 && p.Kd % 64 == 0) return launch_variant_bk<PA, PB, 64>(v, p, stages, s);
+  return launch_variant_bk<PA, PB, 32>(v, p, stages, s);
+}
+
 }  // namespace cnmf
 
-extern "C" int cnmf_gemm_planes_bk(int pb) { return 32; }
+// k granularity the caller pads the planes to (a multiple of every k-step depth)
+extern "C" int cnmf_gemm_planes_bk(int pb) { return 64; }
 
 // Tile tables: rows of (M-tile, N-tile) per variant, for the host heuristics.
 extern "C" int cnmf_gemm_planes_tile(int v, int which) {
@@ -362,12 +376,14 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
                                        long long b_plane, int b_rows, float* C, long long ldc,
                                        const float* col_scale, int M, int N, int Kd, int pa,
                                        int pb, int accumulate, int variant, int ksplit,
-                                       float* slab, int stages, hipStream_t stream) {
+                                       float* slab, int stages, int kstep,
+                                       hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  const int bk = cnmf_gemm_planes_bk(pb);
+  const int bk = 32;   // smallest k-step depth: Kd must be a multiple of it
   if (pa < 2 || pa > 3 || pb < 1 || pb > 3 || Kd <= 0 || Kd % bk || lda % 8 || ldb % 8 ||
       a_plane % 8 || b_plane % 8 || a_rows < 1 || b_rows < 1 || variant < 0 || variant > 3 ||
-      ksplit < 1 || ksplit > Kd / bk || (ksplit > 1 && !slab))
+      ksplit < 1 || ksplit > Kd / (kstep >= 64 && Kd % 64 == 0 ? 64 : bk) ||
+      (ksplit > 1 && !slab))
     return hipErrorInvalidValue;
   cnmf::PlaneGemmParams p;
   p.A = A; p.lda = lda; p.a_plane = a_plane; p.a_rows = a_rows;
@@ -377,12 +393,12 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   p.ksplit = ksplit; p.slab = slab;
   hipError_t e;
   switch (pa * 4 + pb) {
-    case 9: e = cnmf::launch_variant<2, 1, 32>(variant, p, stages, stream); break;
-    case 10: e = cnmf::launch_variant<2, 2, 32>(variant, p, stages, stream); break;
-    case 11: e = cnmf::launch_variant<2, 3, 32>(variant, p, stages, stream); break;
-    case 13: e = cnmf::launch_variant<3, 1, 32>(variant, p, stages, stream); break;
-    case 14: e = cnmf::launch_variant<3, 2, 32>(variant, p, stages, stream); break;
-    default: e = cnmf::launch_variant<3, 3, 32>(variant, p, stages, stream); break;
+    case 9: e = cnmf::launch_variant<2, 1>(variant, p, stages, kstep, stream); break;
+    case 10: e = cnmf::launch_variant<2, 2>(variant, p, stages, kstep, stream); break;
+    case 11: e = cnmf::launch_variant<2, 3>(variant, p, stages, kstep, stream); break;
+    case 13: e = cnmf::launch_variant<3, 1>(variant, p, stages, kstep, stream); break;
+    case 14: e = cnmf::launch_variant<3, 2>(variant, p, stages, kstep, stream); break;
+    default: e = cnmf::launch_variant<3, 3>(variant, p, stages, kstep, stream); break;
   }
   if (e != hipSuccess || ksplit == 1) return e;
   const long long total = (long long)M * N;

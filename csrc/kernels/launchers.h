@@ -130,7 +130,7 @@ hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_
                             const unsigned short* B, long long ldb, long long b_plane, int b_rows,
                             float* C, long long ldc, const float* col_scale, int M, int N,
                             int Kd, int pa, int pb, int accumulate, int variant, int ksplit,
-                            float* slab, int stages, hipStream_t stream);
+                            float* slab, int stages, int kstep, hipStream_t stream);
 hipError_t cnmf_split_planes(const float* S, long long lds, int rows, int cols, int cols_pad,
                              const float* col_mul, unsigned short* P, long long ldp,
                              long long plane, int nplanes, hipStream_t stream);
