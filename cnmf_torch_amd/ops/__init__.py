@@ -52,7 +52,8 @@ def _require_native():
 # Per-op debug / tuning knobs, read ONCE (at import, or by refresh_env()): every op
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
 _ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
-             "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES", "CNMF_GEMM_BK")
+             "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES", "CNMF_GEMM_BK",
+             "CNMF_GEMM_SMALL")
 _ENV: dict = {}
 
 
@@ -1099,7 +1100,7 @@ def gemm_kstep(variant: int) -> int:
     return 64 if variant in (1, 2) else 32
 
 
-_GEMM_TILES = {0: (128, 128), 1: (128, 256), 2: (256, 128), 3: (64, 128)}
+_GEMM_TILES = {0: (128, 128), 1: (128, 256), 2: (256, 128), 3: (64, 128), 4: (64, 128)}
 _GEMM_SLAB: dict = {}
 
 
@@ -1136,7 +1137,10 @@ def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
     elif tiles(1) >= cus:
         v = 1
     elif tiles(3) >= 2 * cus:
-        v = 3
+        # 64 x 128 tiles as 4 waves of 32 x 64 (variant 4): twice the waves per output to
+        # hide LDS / barrier latency -- K=10 numerator 63.4 -> 60.1 us in the bench
+        # (profiles/r2_gemm_small_tile_sweep.log); CNMF_GEMM_SMALL=3: 2 waves of 64 x 64
+        v = 3 if (_ENV["CNMF_GEMM_SMALL"] or "4") == "3" else 4
     elif M > 128:
         v = 1
     else:

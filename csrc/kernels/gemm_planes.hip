@@ -76,10 +76,11 @@ __device__ __forceinline__ void glds16(const unsigned short* g, unsigned char* l
                                    (void __attribute__((address_space(3)))*)lds, 16, 0, 0);
 }
 
-template <int PA, int PB, int BK, int WM, int WN, int NS>
+template <int PA, int PB, int BK, int WM, int WN, int NS, int MI = 4>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmParams p) {
   constexpr int NT = 64 * WM * WN;            // threads
-  constexpr int BM = 64 * WM, BN = 64 * WN;   // each wave owns a 64 x 64 output block
+  constexpr int WR = 16 * MI;                 // each wave owns a WR x 64 output block
+  constexpr int BM = WR * WM, BN = 64 * WN;
   constexpr int CPR = BK / 8;                 // 16-byte chunks per tile row
   constexpr int A_TILE = BM * BK * 2;         // bytes per plane tile
   constexpr int B_TILE = BN * BK * 2;
@@ -142,9 +143,9 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
                base + PA * A_TILE + pl * B_TILE + (i * NT + wave * 64) * 16);
   };
 
-  f32x4v acc[4][4];
+  f32x4v acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
@@ -180,17 +181,17 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
           bfr[j][ni] = *(const bf16x8*)(Bs + j * B_TILE + row * (BK * 2) +
                                         ((c ^ swz<CPR>(row)) * 16));
         }
-      bf16x8 afr[PA][4];
+      bf16x8 afr[PA][MI];
 #pragma unroll
       for (int i = 0; i < PA; ++i)
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const int row = wm * 64 + mi * 16 + (lane & 15);
+        for (int mi = 0; mi < MI; ++mi) {
+          const int row = wm * WR + mi * 16 + (lane & 15);
           afr[i][mi] = *(const bf16x8*)(As + i * A_TILE + row * (BK * 2) +
                                         ((c ^ swz<CPR>(row)) * 16));
         }
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
@@ -206,13 +207,13 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
   if (p.ksplit > 1) {   // raw partial tile -> slab ks (reduced in order by gemm_reduce)
     float* sl = p.slab + (long long)ks * p.M * p.N;
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const int gn = n0 + wn * 64 + ni * 16 + (lane & 15);
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const int gm = m0 + wm * 64 + mi * 16 + (lane >> 4) * 4 + rr;
+          const int gm = m0 + wm * WR + mi * 16 + (lane >> 4) * 4 + rr;
           if (gm < p.M && gn < p.N) sl[(long long)gm * p.N + gn] = acc[mi][ni][rr];
         }
       }
@@ -229,11 +230,11 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
     gn[ni] = n0 + wn * 64 + ni * 16 + (lane & 15);
     sc[ni] = p.col_scale ? p.col_scale[min(gn[ni], p.N - 1)] : 1.f;
   }
-  const int gm0 = m0 + wm * 64 + (lane >> 4) * 4;
+  const int gm0 = m0 + wm * WR + (lane >> 4) * 4;
   if (p.accumulate) {
-    float old[4][4][4];
+    float old[MI][4][4];
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
           old[mi][ni][rr] = p.C[(long long)min(gm0 + mi * 16 + rr, p.M - 1) * p.ldc +
                                 min(gn[ni], p.N - 1)];
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
         }
   } else {
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
@@ -319,34 +320,35 @@ __global__ void gemm_reduce_kernel(const float* __restrict__ slab, int ksplit, i
   }
 }
 
-template <int PA, int PB, int BK, int WM, int WN>
+template <int PA, int PB, int BK, int WM, int WN, int MI = 4>
 static hipError_t launch_gemm(PlaneGemmParams p, int stages, hipStream_t s) {
-  constexpr int stage_bytes = (PA * 64 * WM + PB * 64 * WN) * BK * 2;
+  constexpr int stage_bytes = (PA * 16 * MI * WM + PB * 64 * WN) * BK * 2;
   if constexpr (BK > 32 && 2 * stage_bytes > 160 * 1024) {
-    return launch_gemm<PA, PB, 32, WM, WN>(p, stages, s);   // deep k-step does not fit
+    return launch_gemm<PA, PB, 32, WM, WN, MI>(p, stages, s);   // deep k-step does not fit
   } else {
-  p.tiles_m = (p.M + 64 * WM - 1) / (64 * WM);
+  p.tiles_m = (p.M + 16 * MI * WM - 1) / (16 * MI * WM);
   p.tiles_n = (p.N + 64 * WN - 1) / (64 * WN);
   const dim3 grid(p.tiles_m * p.tiles_n, p.ksplit), block(64 * WM * WN);
   if constexpr (3 * stage_bytes <= 160 * 1024) {
     if (stages >= 3) {
-      hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN, 3>), grid, block, 0, s, p);
+      hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN, 3, MI>), grid, block, 0, s, p);
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN, 2>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((gemm_planes_kernel<PA, PB, BK, WM, WN, 2, MI>), grid, block, 0, s, p);
   return hipGetLastError();
   }
 }
 
 // tile variants: 0 = 128x128 (4 waves), 1 = 128x256 (8 waves), 2 = 256x128 (8 waves),
-// 3 = 64x128 (2 waves)
+// 3 = 64x128 (2 waves), 4 = 64x128 (4 waves of 32 x 64: twice the waves per output)
 template <int PA, int PB, int BK>
 static hipError_t launch_variant_bk(int v, const PlaneGemmParams& p, int stages, hipStream_t s) {
   switch (v) {
     case 0: return launch_gemm<PA, PB, BK, 2, 2>(p, stages, s);
     case 1: return launch_gemm<PA, PB, BK, 2, 4>(p, stages, s);
     case 2: return launch_gemm<PA, PB, BK, 4, 2>(p, stages, s);
+    case 4: return launch_gemm<PA, PB, BK, 2, 2, 2>(p, stages, s);   // 64 x 128, 4 waves
     default: return launch_gemm<PA, PB, BK, 1, 2>(p, stages, s);
   }
 }
@@ -367,8 +369,8 @@ extern "C" int cnmf_gemm_planes_bk(int pb) { return 64; }
 
 // Tile tables: rows of (M-tile, N-tile) per variant, for the host heuristics.
 extern "C" int cnmf_gemm_planes_tile(int v, int which) {
-  static const int tm[4] = {128, 128, 256, 64}, tn[4] = {128, 256, 128, 128};
-  return which == 0 ? tm[v & 3] : tn[v & 3];
+  static const int tm[5] = {128, 128, 256, 64, 64}, tn[5] = {128, 256, 128, 128, 128};
+  return (v < 0 || v > 4) ? 0 : (which == 0 ? tm[v] : tn[v]);
 }
 
 extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_plane,
@@ -381,7 +383,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   if (M <= 0 || N <= 0) return hipSuccess;
   const int bk = 32;   // smallest k-step depth: Kd must be a multiple of it
   if (pa < 2 || pa > 3 || pb < 1 || pb > 3 || Kd <= 0 || Kd % bk || lda % 8 || ldb % 8 ||
-      a_plane % 8 || b_plane % 8 || a_rows < 1 || b_rows < 1 || variant < 0 || variant > 3 ||
+      a_plane % 8 || b_plane % 8 || a_rows < 1 || b_rows < 1 || variant < 0 || variant > 4 ||
       ksplit < 1 || ksplit > Kd / (kstep >= 64 && Kd % 64 == 0 ? 64 : bk) ||
       (ksplit > 1 && !slab))
     return hipErrorInvalidValue;

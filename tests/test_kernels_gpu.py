@@ -1206,3 +1206,32 @@ def test_solve_gram_of_matches_explicit_gram(K, m):
         torch.testing.assert_close(lb, la, rtol=2e-5, atol=1e-4)
         assert (ib - ia).abs().max() <= (0 if tol < 0 else 5)
         assert torch.equal(xb[2], x0[2])
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("bk,stages", [(32, 2), (32, 3), (64, 2)])
+def test_gemm_planes_every_tile_variant(monkeypatch, variant, bk, stages):
+    """Every tile variant (incl. the 4-wave 64 x 128 tile of 32 x 64 wave blocks), k-step
+    depth and LDS stage count, with and without a k split, == the fp64 product."""
+    M, N, K, pb = 301, 650, 1000, 1
+    g = torch.Generator().manual_seed(variant * 7 + bk + stages)
+    Kd = -(-K // ops.planes_bk(pb)) * ops.planes_bk(pb)
+    A = torch.rand((M, K), generator=g)
+    B = torch.randint(0, 200, (N, K), generator=g).float()
+    Ap = torch.zeros((3, M, Kd), dtype=torch.int16, device="cuda")
+    Bp = torch.zeros((pb, N, Kd), dtype=torch.int16, device="cuda")
+    ops.split_planes(A.cuda(), Ap)
+    ops.split_planes(B.cuda(), Bp)
+    ref = A.double() @ B.double().t()
+    for ks in (1, 3):
+        for k, v in (("CNMF_GEMM_VARIANT", variant), ("CNMF_GEMM_KSPLIT", ks),
+                     ("CNMF_GEMM_BK", bk), ("CNMF_GEMM_STAGES", stages)):
+            monkeypatch.setenv(k, str(v))
+        ops.refresh_env()
+        C = torch.empty((M, N), device="cuda")
+        ops.gemm_planes(C, Ap, Bp, M, N, Kd)
+        torch.cuda.synchronize()
+        err = float((C.cpu().double() - ref).abs().max() / ref.abs().max())
+        assert err < 1e-6 * K / 256, (variant, bk, stages, ks, err)
+    monkeypatch.undo()
+    ops.refresh_env()
