@@ -1097,10 +1097,11 @@ def gemm_kstep(variant: int) -> int:
     77 -> 97 us).  CNMF_GEMM_BK overrides (A/B runs)."""
     if _ENV["CNMF_GEMM_BK"]:
         return int(_ENV["CNMF_GEMM_BK"])
-    return 64 if variant in (1, 2) else 32
+    return 64 if variant in (1, 2, 5) else 32
 
 
-_GEMM_TILES = {0: (128, 128), 1: (128, 256), 2: (256, 128), 3: (64, 128), 4: (64, 128)}
+_GEMM_TILES = {0: (128, 128), 1: (128, 256), 2: (256, 128), 3: (64, 128), 4: (64, 128),
+               5: (128, 128)}
 _GEMM_SLAB: dict = {}
 
 
@@ -1244,7 +1245,7 @@ def gemm_stages(variant: int) -> int:
     numerator 80 -> 108 us).  CNMF_GEMM_STAGES overrides (A/B runs)."""
     if _ENV["CNMF_GEMM_STAGES"]:
         return int(_ENV["CNMF_GEMM_STAGES"])
-    return 3 if variant in (1, 2) else 2
+    return 3 if variant in (1, 2, 5) else 2
 
 
 # ----------------------------------------------------------------------------- column stats

@@ -341,7 +341,8 @@ static hipError_t launch_gemm(PlaneGemmParams p, int stages, hipStream_t s) {
 }
 
 // tile variants: 0 = 128x128 (4 waves), 1 = 128x256 (8 waves), 2 = 256x128 (8 waves),
-// 3 = 64x128 (2 waves), 4 = 64x128 (4 waves of 32 x 64: twice the waves per output)
+// 3 = 64x128 (2 waves), 4 = 64x128 (4 waves of 32 x 64: twice the waves per output),
+// 5 = 128x128 (8 waves of 32 x 64)
 template <int PA, int PB, int BK>
 static hipError_t launch_variant_bk(int v, const PlaneGemmParams& p, int stages, hipStream_t s) {
   switch (v) {
@@ -349,6 +350,7 @@ static hipError_t launch_variant_bk(int v, const PlaneGemmParams& p, int stages,
     case 1: return launch_gemm<PA, PB, BK, 2, 4>(p, stages, s);
     case 2: return launch_gemm<PA, PB, BK, 4, 2>(p, stages, s);
     case 4: return launch_gemm<PA, PB, BK, 2, 2, 2>(p, stages, s);   // 64 x 128, 4 waves
+    case 5: return launch_gemm<PA, PB, BK, 4, 2, 2>(p, stages, s);   // 128 x 128, 8 waves
     default: return launch_gemm<PA, PB, BK, 1, 2>(p, stages, s);
   }
 }
@@ -369,8 +371,9 @@ extern "C" int cnmf_gemm_planes_bk(int pb) { return 64; }
 
 // Tile tables: rows of (M-tile, N-tile) per variant, for the host heuristics.
 extern "C" int cnmf_gemm_planes_tile(int v, int which) {
-  static const int tm[5] = {128, 128, 256, 64, 64}, tn[5] = {128, 256, 128, 128, 128};
-  return (v < 0 || v > 4) ? 0 : (which == 0 ? tm[v] : tn[v]);
+  static const int tm[6] = {128, 128, 256, 64, 64, 128};
+  static const int tn[6] = {128, 256, 128, 128, 128, 128};
+  return (v < 0 || v > 5) ? 0 : (which == 0 ? tm[v] : tn[v]);
 }
 
 extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_plane,
@@ -383,7 +386,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   if (M <= 0 || N <= 0) return hipSuccess;
   const int bk = 32;   // smallest k-step depth: Kd must be a multiple of it
   if (pa < 2 || pa > 3 || pb < 1 || pb > 3 || Kd <= 0 || Kd % bk || lda % 8 || ldb % 8 ||
-      a_plane % 8 || b_plane % 8 || a_rows < 1 || b_rows < 1 || variant < 0 || variant > 4 ||
+      a_plane % 8 || b_plane % 8 || a_rows < 1 || b_rows < 1 || variant < 0 || variant > 5 ||
       ksplit < 1 || ksplit > Kd / (kstep >= 64 && Kd % 64 == 0 ? 64 : bk) ||
       (ksplit > 1 && !slab))
     return hipErrorInvalidValue;

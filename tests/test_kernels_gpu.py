@@ -1208,7 +1208,7 @@ def test_solve_gram_of_matches_explicit_gram(K, m):
         assert torch.equal(xb[2], x0[2])
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("bk,stages", [(32, 2), (32, 3), (64, 2)])
 def test_gemm_planes_every_tile_variant(monkeypatch, variant, bk, stages):
     """Every tile variant (incl. the 4-wave 64 x 128 tile of 32 x 64 wave blocks), k-step

@@ -51,7 +51,7 @@ def main():
             ops.split_planes(Bf, Bp)
             ref = A.double() @ Bf.double().t()
             rec[f"auto_plan_pb{pb}"] = ops.gemm_plan(M, N, Kd, pb)
-            variants = [None] + ([(v, k) for v in (0, 1, 2, 3, 4) for k in (1, 2, 4)] if pb == 1
+            variants = [None] + ([(v, k) for v in (0, 1, 2, 3, 4, 5) for k in (1, 2, 4)] if pb == 1
                                  else [])
             for vk in variants:
                 if vk is not None:
