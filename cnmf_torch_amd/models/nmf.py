@@ -330,12 +330,22 @@ class _Group:
         return slice(self.q0, self.q0 + self.n * self.K * self.K)
 
     def rep3(self, t: torch.Tensor) -> torch.Tensor:
-        """(n, K, cols) view of this group's rows of a (rows, cols) tensor or view."""
-        return t[self.rows].unflatten(0, (self.n, self.K))
+        """(n, K, cols) view of this group's rows of a (rows, cols) tensor or view.  One
+        as_strided (no slice + unflatten): ~12 of these per pass sit on the host's enqueue
+        path, which is what bounds the few-replicate tail passes."""
+        end = self.r0 + self.n * self.K
+        if end > t.shape[0]:
+            raise IndexError(f"group rows [{self.r0}, {end}) beyond {t.shape[0]}")
+        s0, s1 = t.stride()
+        return t.as_strided((self.n, self.K, t.shape[1]), (self.K * s0, s0, s1),
+                            t.storage_offset() + self.r0 * s0)
 
     def gram3(self, flat: torch.Tensor) -> torch.Tensor:
         """(n, K, K) view of this group's block of a flat per-position K*K buffer."""
-        return flat[self.sq].view(self.n, self.K, self.K)
+        if self.q0 + self.n * self.K * self.K > flat.shape[0]:
+            raise IndexError("group Gram block beyond the buffer")
+        K = self.K
+        return flat.as_strided((self.n, K, K), (K * K, K, 1), flat.storage_offset() + self.q0)
 
 
 class _Batch:
