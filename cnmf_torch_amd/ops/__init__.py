@@ -827,7 +827,7 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
         raise ValueError("active: int32 with >= R entries")
     # few replicates: split the columns over S workgroups per replicate (one workgroup per
     # replicate left most of the chip idle at R = 8) and reduce the partials in order
-    S = 1 if R >= 64 else max(1, min((n + 255) // 256, 512 // max(1, R)))
+    S = 1 if R >= _GRAM_SPLIT_MIN_R else max(1, min((n + 255) // 256, 512 // max(1, R)))
     part = 0
     if S > 1:
         key = (str(X3.device), _stream_ptr(X3))
@@ -843,6 +843,8 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
 
 
 _GRAM_WS: dict = {}
+# replicate count from which one workgroup per replicate fills the chip (no column split)
+_GRAM_SPLIT_MIN_R = int(os.environ.get("CNMF_GRAM_SPLIT_MIN_R", "64"))
 _gram_op = gram    # ops.solve's `gram` argument shadows the function there
 
 

@@ -240,4 +240,7 @@ def dp_factorize(obj, skip_completed_runs: bool = False, replicate_batch=None,
                        verbose=verbose and comm.rank == 0, run_params=run_params,
                        comm=comm if comm.world_size > 1 else None, row_segments=segs)
     comm.barrier()
+    close = getattr(comm, "close", None)
+    if close is not None:       # collective: unmaps the xGMI peer workspaces, if any
+        close()
     return comm
