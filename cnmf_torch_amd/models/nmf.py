@@ -377,6 +377,10 @@ class _Batch:
         self.h_iters = torch.zeros(R, dtype=torch.int32, device=dev)
         self.w_iters = torch.zeros(R, dtype=torch.int32, device=dev)
         self.layout_version = 0   # bumped by compact(): captured graphs key on it
+        # optional callback(orig_idx, kpos, host_rows, event): the final spectra of the
+        # replicates a compaction retires, copied to pinned memory (ready at `event`), so
+        # the caller can persist them while the rest of the batch is still solving
+        self.on_retire = None
         self.uid = next(_BATCH_UIDS)   # never reused (unlike id()): plane-cache keys
         self.bucket = max(1, int(os.environ.get("CNMF_COMPACT_BUCKET",
                                                 "8" if W.device.type == "cuda" else "1")))
@@ -477,6 +481,17 @@ class _Batch:
         self.n_act = n_new
         self.layout_version += 1
         self._layout()
+        if self.on_retire is not None and dev.type == "cuda":
+            # positions [n_new, n) are the newly finished ones (flags only go 1 -> 0); their
+            # spectra are final: every later kernel skips them, and this copy is in stream
+            # order after the last one that wrote them
+            roff_new = np.concatenate([[0], np.cumsum(self.kpos)])
+            ra, rb = int(roff_new[n_new]), int(roff_new[n])
+            host = torch.empty((rb - ra, self.W.shape[1]), dtype=self.W.dtype, pin_memory=True)
+            host.copy_(self.W[ra:rb], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self.on_retire(self.order[n_new:n].copy(), self.kpos[n_new:n].copy(), host, ev)
 
     def set_err(self, err: torch.Tensor, pass_idx: int, tol: float, final: bool,
                 init: bool = False) -> None:
@@ -802,12 +817,15 @@ class NMFBatchSolver:
         self._XT = None             # X^T (G, N padded to 4) for the beta W-side kernel
 
     # ------------------------------------------------------------------ public
-    def run(self, seeds, HT0=None, W0=None, ks=None) -> NMFResult:
+    def run(self, seeds, HT0=None, W0=None, ks=None, on_retire=None) -> NMFResult:
         """Factorise one replicate per seed.  ``ks`` (one K per seed; default
         ``opts.n_components`` for all) may mix ranks: the Frobenius solvers then run the
         whole K x n_iter grid as ONE ragged batch (one pass loop, one data-side GEMM per
         chunk for every K).  The beta != 2 solvers take one K at a time; a mixed-K
-        request is split by K for them."""
+        request is split by K for them.  ``on_retire`` (GPU, unpadded ranks): called
+        with (indices into ``seeds``, their K, pinned spectra rows, event) for the
+        replicates each compaction retires -- their final spectra, ready once the event
+        completes -- while the remaining ones keep solving (see _Batch.compact)."""
         o = self.opts
         seeds = [int(s_) for s_ in seeds]
         R = len(seeds)
@@ -818,6 +836,8 @@ class NMFBatchSolver:
         if R and ks.min() < 1:
             raise ValueError("every K must be >= 1")
         if self.beta != 2.0 and np.unique(ks).size > 1:
+            if on_retire is not None:
+                raise ValueError("on_retire needs a single K for beta != 2")
             return self._run_split_by_k(seeds, ks)
         t0 = time.perf_counter()
         # wide ranks run padded on the GPU kernels (native_rank); bpp solves on torch linalg
@@ -857,6 +877,8 @@ class NMFBatchSolver:
             HT, W = HT0.to(self.X.dtype).clone(), W0.to(self.X.dtype).clone()
         st = _Batch(HT, W, kpos)
         st.order = pos.astype(np.int64).copy()
+        if on_retire is not None and not pad:
+            st.on_retire = on_retire
         if self.beta == 2.0:
             if o.mode == "online":
                 self._online_frob(st)
