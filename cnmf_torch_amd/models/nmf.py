@@ -548,10 +548,21 @@ class _PassPipeline:
     def __init__(self, st: _Batch, compact_frac: float | None = None):
         self.st = st
         self.cuda = st.W.device.type == "cuda"
+        explicit = compact_frac is not None
         if compact_frac is None:
             compact_frac = float(os.environ.get("CNMF_COMPACT_FRAC", "0.25"))
         self.frac = compact_frac
+        # batches of <= 256 replicates compact later: at that size the GEMMs are latency-
+        # bound, so dropping finished replicates saves little GPU time while each
+        # compaction costs host enqueue time (permutation, re-split of W) -- measured on
+        # MI355X (profiles/r2_compact_frac_ab.txt): 100 replicates 10,487 -> 10,956 rep/s
+        # at 0.75 vs 0.25; the 900-replicate K grid loses 3.5 % at 0.5, so it keeps 0.25
+        self.frac_small = compact_frac if explicit else \
+            float(os.environ.get("CNMF_COMPACT_FRAC_SMALL", "0.75"))
         self.pending = None   # (event, host_flags, n)
+
+    def _frac(self, n: int) -> float:
+        return self.frac_small if n <= 256 else self.frac
 
     def after_enqueue(self) -> bool:
         """Call after enqueueing a pass (incl. its convergence update).  Returns False
@@ -562,7 +573,7 @@ class _PassPipeline:
             n_live = int((st.state["active"][:n] != 0).sum())
             if n_live == 0:
                 return False
-            if n - st.prefix_len(st.state["active"][:n].numpy() != 0) >= max(1, int(self.frac * n)):
+            if n - st.prefix_len(st.state["active"][:n].numpy() != 0) >= max(1, int(self._frac(n) * n)):
                 st.compact()
             return True
         flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
@@ -580,7 +591,7 @@ class _PassPipeline:
         if n_live == 0:                   # everything had finished one pass ago
             return False
         flags_np = pflags.numpy() != 0
-        if n - st.prefix_len(flags_np) >= max(1, int(self.frac * n)):
+        if n - st.prefix_len(flags_np) >= max(1, int(self._frac(n) * n)):
             # compact on the one-pass-stale flags, in stream order: no drain of the GPU
             st.compact(flags_np)
             self.pending = None
