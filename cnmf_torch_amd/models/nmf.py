@@ -545,7 +545,8 @@ class _PassPipeline:
     behind, so the GPU never drains at a pass boundary.  When flags show that enough
     replicates finished, the host synchronises once and compacts the batch."""
 
-    def __init__(self, st: _Batch, compact_frac: float | None = None):
+    def __init__(self, st: _Batch, compact_frac: float | None = None,
+                 late_small: bool = True):
         self.st = st
         self.cuda = st.W.device.type == "cuda"
         explicit = compact_frac is not None
@@ -557,7 +558,9 @@ class _PassPipeline:
         # compaction costs host enqueue time (permutation, re-split of W) -- measured on
         # MI355X (profiles/r2_compact_frac_ab.txt): 100 replicates 10,487 -> 10,956 rep/s
         # at 0.75 vs 0.25; the 900-replicate K grid loses 3.5 % at 0.5, so it keeps 0.25
-        self.frac_small = compact_frac if explicit else \
+        # (``late_small`` False: the beta != 2 solvers, GPU-bound at every batch size --
+        # their elementwise passes over X shrink with every retired replicate)
+        self.frac_small = compact_frac if (explicit or not late_small) else \
             float(os.environ.get("CNMF_COMPACT_FRAC_SMALL", "0.75"))
         self.pending = None   # (event, host_flags, n)
 
@@ -1634,7 +1637,7 @@ class NMFBatchSolver:
         steps = self._steps(N)
         kl = self.beta == 1.0
         self._init_err(st)
-        pipe = _PassPipeline(st)
+        pipe = _PassPipeline(st, late_small=False)
         max_pass = int(o.online_max_pass)
         for p in range(max_pass):
             n = st.n_act
@@ -1676,7 +1679,7 @@ class NMFBatchSolver:
         X = self.X
         N, G = X.shape
         self._init_err(st)
-        pipe = _PassPipeline(st)
+        pipe = _PassPipeline(st, late_small=False)
         for it in range(int(o.batch_max_iter)):
             n = st.n_act
             if n == 0:
