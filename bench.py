@@ -23,14 +23,27 @@ them).  ``value`` is whole-job replicates/sec.  ``--mode`` picks the multi-GPU s
 ``--kmin/--kmax`` replace the single K by the K x n_iter grid of BASELINE config 2
 (K = kmin..kmax, ``--n-iter`` replicates each) solved as ONE ragged batch per step.
 
-Run: ``python bench.py [--gpus N --steps K --warmup W --mode weak|strong|dp]``; for
-N > 1 under ``torch.distributed.run`` (one process per GPU, RCCL over xGMI).
+Run: ``python bench.py [--gpus N --steps K --warmup W --mode weak|strong|dp]``.  N > 1
+runs one process per GPU over RCCL (xGMI): either under ``torch.distributed.run`` (the
+driver's form; ``WORLD_SIZE`` must then equal ``--gpus``, else the run fails), or, when
+started without a launcher, bench.py starts ``torch.distributed.run`` itself as a CHILD
+process (before any GPU call; never an exec) and exits with its return code.  The JSON
+line carries the world size and backend the process group actually reported
+(``config.rccl_world``, ``config.backend``).  A weak-scaling run with N > 1 also times the
+strong-scaling form of the same step -- ONE ``--n-iter`` ledger batch dealt round-robin
+over the ranks -- and reports it as ``config.strong_value`` (replicates/s, whole job).
+
+Reference: the multi-worker factorize is GNU parallel over ``--worker-index``
+(/root/reference/Extras/run_parallel.py:48-51) with the round-robin ``worker_filter``
+(/root/reference/src/cnmf/cnmf.py:53-54, 876-880).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -66,12 +79,25 @@ def main() -> int:
                     help="replicate groups solved concurrently on separate HIP streams")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return _self_launch(args.gpus)
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} "
+              "ranks", file=sys.stderr, flush=True)
+        return 2
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # device_count() does not initialise the GPU on this image; is_available() does
+    if not args.cpu and world > 1 and 0 < torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks but only {torch.cuda.device_count()} GPUs visible",
+              file=sys.stderr, flush=True)
+        return 2
     use_cuda = torch.cuda.is_available() and not args.cpu
     if use_cuda:
         torch.cuda.set_device(local_rank)
@@ -113,9 +139,13 @@ def main() -> int:
     all_seeds = np.random.randint(low=1, high=(2 ** 31) - 1, size=n_total * nsteps)
     all_ks = np.tile(np.repeat(grid, args.n_iter), n_total // per_batch)
 
-    def step(i: int):
-        seeds = all_seeds[i * n_total:(i + 1) * n_total]
-        ks = all_ks
+    def step(i: int, strong: bool = False):
+        if strong:   # one ledger batch per step, dealt round-robin over the ranks
+            seeds = all_seeds[i * per_batch:(i + 1) * per_batch]
+            ks = all_ks[:per_batch]
+        else:
+            seeds = all_seeds[i * n_total:(i + 1) * n_total]
+            ks = all_ks
         if args.mode != "dp":
             seeds, ks = seeds[rank::world], ks[rank::world]
         if len(grid) == 1:
@@ -131,6 +161,13 @@ def main() -> int:
         if use_cuda:
             torch.cuda.synchronize()
 
+    def max_over_ranks(sec: float) -> float:
+        if world <= 1:
+            return sec
+        t = torch.tensor([sec], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     for i in range(args.warmup):
         step(i)
     barrier()
@@ -141,12 +178,25 @@ def main() -> int:
         passes.append(float(np.mean(res.n_iter)))
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
     reps_per_sec = n_total * args.steps / elapsed
+
+    strong_value = strong_ms = None
+    if world > 1 and args.mode == "weak":
+        # the same ledger batch per step, now split over the ranks (strong scaling)
+        for i in range(min(2, args.warmup)):
+            step(i, strong=True)
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(args.warmup, nsteps):
+            step(i, strong=True)
+        barrier()
+        el_s = max_over_ranks(time.perf_counter() - t0)
+        strong_ms = 1000.0 * el_s / args.steps
+        strong_value = per_batch * args.steps / el_s
+    rccl_world = dist.get_world_size() if world > 1 else 1
+    backend = dist.get_backend() if world > 1 else None
     if rank == 0:
         metric = "NMF replicates/sec (K=10, n_iter=100)" if grid == [10] and args.n_iter == 100 \
             else f"NMF replicates/sec (K={grid[0]}..{grid[-1]}, n_iter={args.n_iter})" \
@@ -182,6 +232,11 @@ def main() -> int:
                 "streams_per_gpu": args.streams,
                 "device": "cpu" if not use_cuda else torch.cuda.get_device_name(dev),
                 "mean_passes": round(float(np.mean(passes)), 2) if passes else None,
+                "rccl_world": rccl_world,
+                "backend": backend,
+                "strong_value": None if strong_value is None else round(strong_value, 3),
+                "strong_ms_per_step": None if strong_ms is None else round(strong_ms, 3),
+                "strong_global_batch": per_batch if strong_value is not None else None,
             },
         }
         print(json.dumps(out), flush=True)
@@ -190,6 +245,25 @@ def main() -> int:
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def _free_port() -> int:
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def _self_launch(n: int) -> int:
+    """``--gpus N`` without a launcher: run ``torch.distributed.run`` (N ranks, one per GPU,
+    rendezvous on 127.0.0.1) as a child process with the same arguments and return its
+    exit code.  Nothing here has touched the GPU (the parent never imports torch), and the
+    parent waits instead of exec'ing."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on these hosts
+    return subprocess.call(cmd, env=env)
 
 
 if __name__ == "__main__":

@@ -77,7 +77,10 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     objs, todo = [], []
     # per-unit flags: the split-bf16 beta kernels keep their MFMA accumulators in VGPRs
     # (the elementwise work reads every accumulator: AGPR copies cost ~30 % of the VALU)
-    unit_flags = {"beta_planes.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+    # the pipelined solve keeps its elementwise update scalar: SLP-packed v_pk_*_f32 beside
+    # MFMAs cost more issue cycles than the scalar pair (MI355X_MICROARCH.md cycle table)
+    unit_flags = {"beta_planes.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
+                  "solve_pipe.hip": ["-fno-slp-vectorize"]}
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)

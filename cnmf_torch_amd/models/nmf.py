@@ -911,9 +911,9 @@ class NMFBatchSolver:
             ks_out = ks
         if self.X.device.type == "cuda":
             ops.coop_check(self.X.device)
-            check = getattr(self.comm, "check", None)
-            if check is not None:     # one-shot xGMI all-reduce gave up on a peer?
-                check()
+        check = getattr(self.comm, "check", None)
+        if check is not None:     # one-shot xGMI all-reduce gave up on a peer?  Raise
+            check()               # before any caller can persist these spectra
         stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": hi.tolist(),
                  "w_inner_iters": wi.tolist()}
         uni = np.unique(ks_out)
@@ -1231,6 +1231,7 @@ class NMFBatchSolver:
                         # statistics GEMM (no separate split pass), unless unaligned
                         hpl, _ = (None, None) if (exact or a % 8) else \
                             self.solve_planes("h", rows, b - a)
+                        hpl_n = 3 if hpl is None else ops.gemm_a_planes(hpl.shape[2])
                         for g in groups:
                             ga = active[g.pos]
                             # W W^T: its own Gram launch.  CNMF_SOLVE_GRAM_PROLOGUE=1 has
@@ -1246,7 +1247,8 @@ class NMFBatchSolver:
                                          l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
                                          iters_out=h_it[g.pos], conv_mode=cmode,
                                          check_every=o.inner_check_every, active=ga,
-                                         planes=None if hpl is None else hpl[:, g.rows])
+                                         planes=None if hpl is None else hpl[:, g.rows],
+                                         planes_n=hpl_n)
                         if exact:
                             # replace the chunk's old contribution: d = h_new - h_old
                             for g in groups:
@@ -1282,6 +1284,7 @@ class NMFBatchSolver:
                         A_ += dA
                     last = s_ == len(steps) - 1
                     wpl_out, unit = (None, None) if exact else self.solve_planes("w", rows)
+                    wpl_n = 3 if wpl_out is None else ops.gemm_a_planes(wpl_out.shape[2])
                     for g in groups:
                         _inner_solve(algo, g.rep3(W), g.rep3(B_), g.gram3(A_),
                                      max_iter=o.online_chunk_max_iter, tol=o.online_w_tol,
@@ -1291,7 +1294,7 @@ class NMFBatchSolver:
                                      iters_out=w_it[g.pos], conv_mode=cmode,
                                      check_every=o.inner_check_every, active=active[g.pos],
                                      planes=None if wpl_out is None else wpl_out[:, g.rows],
-                                     planes_colmul=unit)
+                                     planes_colmul=unit, planes_n=wpl_n)
                     if wpl_out is not None:
                         self.mark_w_fresh(W, st)
                 ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},

@@ -53,7 +53,7 @@ def _require_native():
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
 _ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
              "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES", "CNMF_GEMM_BK",
-             "CNMF_GEMM_SMALL")
+             "CNMF_GEMM_SMALL", "CNMF_SOLVE_PIPE")
 _ENV: dict = {}
 
 
@@ -115,7 +115,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           check_every: int = 10, variant: str = "auto",
           active: torch.Tensor | None = None, coop: int | str = "auto",
           planes: torch.Tensor | None = None, planes_colmul: torch.Tensor | None = None,
-          gram_of: torch.Tensor | None = None) -> None:
+          gram_of: torch.Tensor | None = None, planes_n: int = 3) -> None:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -139,6 +139,10 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     ``planes`` (3, R*K, cols_pad) int16, optional: the kernel's epilogue also writes the
     final x (times ``planes_colmul`` per column) as exact bf16 planes -- the A operand of
     the next split-precision GEMM (ops.gemm_planes) -- zeroing columns [n, cols_pad).
+    ``planes_n``: how many of the three planes to write (the GEMM reads only its
+    ``gemm_a_planes(Kd)`` A planes; the rest would be dead stores).
+    MU with l1 = l2 = 0, the block-objective stop and K <= 16 runs the software-pipelined
+    matrix-core kernel (solve_pipe.hip) unless ``CNMF_SOLVE_PIPE=0``.
     """
     a = ALGOS[algo]
     R, K, n = x.shape
@@ -203,7 +207,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             and (_ENV["CNMF_SOLVE_MFMA"] or "1") != "0":
         S = _mfma_split(n, nblocks, K, nsplit, coop, x.device)
     if S is not None:
-        vcode = 3
+        vcode = 5 if _ENV["CNMF_SOLVE_PIPE"] == "0" else 3
     elif gram is None:      # a VALU kernel: form the Gram first
         gram = _gram_op(gram_of, active=active)
     if S is not None:
@@ -263,7 +267,8 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             active.data_ptr() if active is not None else 0, int(S), ws_slots, ws_count,
             int(gen), int(epochs), ws_flag, pl_ptr, int(pl_rs), int(pl_ld), int(pl_plane),
             planes_colmul.data_ptr() if (planes is not None and planes_colmul is not None) else 0,
-            int(pl_cols), gs_ptr, int(gs_rs), int(gs_ld), int(gs_cols), _stream_ptr(x))
+            int(pl_cols), int(planes_n), gs_ptr, int(gs_rs), int(gs_ld), int(gs_cols),
+            _stream_ptr(x))
 
 
 # Cooperative-split bookkeeping.  A launch of S*nblocks 1024-thread workgroups is only safe

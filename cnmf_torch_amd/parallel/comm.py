@@ -77,7 +77,14 @@ class DistComm(LocalComm):
         if self._xgmi is None:
             from . import xgmi
 
-            self._xgmi = xgmi.XgmiAllReduce(self.group, t.device) if xgmi.wanted() else False
+            self._xgmi = False
+            if xgmi.wanted():
+                try:
+                    self._xgmi = xgmi.XgmiAllReduce(self.group, t.device)
+                except xgmi.XgmiUnavailable as e:     # same decision on every rank
+                    import warnings
+
+                    warnings.warn(f"CNMF_ALLREDUCE=xgmi unavailable ({e}); using RCCL")
         return self._xgmi if (self._xgmi and self._xgmi.supports(t)) else None
 
     def check(self) -> None:

@@ -239,6 +239,11 @@ def dp_factorize(obj, skip_completed_runs: bool = False, replicate_batch=None,
                        replicate_batch=replicate_batch, save_usages=save_usages,
                        verbose=verbose and comm.rank == 0, run_params=run_params,
                        comm=comm if comm.world_size > 1 else None, row_segments=segs)
+    # a one-shot xGMI all-reduce that gave up on a peer leaves each rank with its own
+    # partial statistics: fail the stage (every solver run also checks before returning)
+    check = getattr(comm, "check", None)
+    if check is not None:
+        check()
     comm.barrier()
     close = getattr(comm, "close", None)
     if close is not None:       # collective: unmaps the xGMI peer workspaces, if any

@@ -39,6 +39,11 @@ class XgmiTimeout(RuntimeError):
     pass
 
 
+class XgmiUnavailable(RuntimeError):
+    """Some rank could not allocate or export a coherent workspace: every rank raises it
+    (the decision is taken collectively), and DistComm stays on RCCL."""
+
+
 class XgmiAllReduce:
     """Peer-mapped workspaces of every rank of ``group`` and the one-shot reduce.
 
@@ -67,11 +72,29 @@ class XgmiAllReduce:
         ms = int(timeout_ms if timeout_ms is not None
                  else os.environ.get("CNMF_XGMI_TIMEOUT_MS", DEFAULT_TIMEOUT_MS))
         self.limit = int(hip.xgmi_wall_clock_khz(self.device.index or 0)) * max(1, ms)
-        with torch.cuda.device(self.device):
-            self._base = hip.xgmi_alloc(self.cap)
-            handle = hip.xgmi_handle(self._base)
+        # Workspace memory: uncached (or fine-grained) device memory, never coarse-grained
+        # hipMalloc -- peers hand data over INSIDE a kernel, across GPUs, and only those
+        # kinds are coherent across devices while kernels run (xgmi_allreduce.hip,
+        # cnmf_xgmi_alloc).  Every rank reports success or its error and all ranks take
+        # the same decision, so a refusal on one rank cannot strand the others in a
+        # collective.
+        self._base, self.alloc_flags, handle, err = 0, 0, None, None
+        try:
+            with torch.cuda.device(self.device):
+                self._base, self.alloc_flags = hip.xgmi_alloc(self.cap)
+                handle = hip.xgmi_handle(self._base)
+        except RuntimeError as e:            # refused flag / IPC export on this rank
+            err = f"rank {self.rank}: {e}"
         handles = [None] * self.world
-        dist.all_gather_object(handles, handle, group=group)
+        dist.all_gather_object(handles, (handle, err), group=group)
+        errors = [e_ for _, e_ in handles if e_ is not None]
+        if errors:
+            if self._base:
+                with torch.cuda.device(self.device):
+                    hip.xgmi_free(self._base)
+            self.closed = True
+            raise XgmiUnavailable("; ".join(errors))
+        handles = [h_ for h_, _ in handles]
         self._opened = []
         peers = []
         with torch.cuda.device(self.device):
@@ -88,6 +111,15 @@ class XgmiAllReduce:
         self.closed = False
         # nobody's first flag store may land before every rank has mapped every workspace
         dist.barrier(group=group)
+
+    @property
+    def memory_kind(self) -> str:
+        """'uncached' or 'fine-grained': the allocation flags of this rank's workspace as
+        hipPointerGetAttributes reports them (never coarse-grained)."""
+        hip = _hip()
+        f = hip.ptr_alloc_flags(self._base)
+        return {hip.MALLOC_UNCACHED: "uncached", hip.MALLOC_FINEGRAINED: "fine-grained"}.get(
+            f, f"flags={f:#x}")
 
     def supports(self, t: torch.Tensor) -> bool:
         return (not self.closed and t.device == self.device and t.dtype == torch.float32

@@ -35,6 +35,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("solve_native_k", [](int K) { return cnmf_solve_native_k(K); });
   m.def("solve_reg_max_cols", [](int K) { return cnmf_solve_reg_max_cols(K); });
   m.def("solve_mfma_max_cols", [](int K) { return cnmf_solve_mfma_max_cols(K); });
+  m.def("solve_pipe_tiles", [](int K, int per) { return cnmf_solve_pipe_tiles(K, per); });
 
   m.def("solve",
         [](int algo, int K, uintptr_t x, long long x_rs, long long ldx, uintptr_t numer,
@@ -45,7 +46,7 @@ PYBIND11_MODULE(_hip, m) {
            int coop_split, uintptr_t coop_slots, uintptr_t coop_count, unsigned coop_gen,
            int coop_epochs,
            uintptr_t coop_timeout, uintptr_t planes, long long pl_rs, long long pl_ld,
-           long long pl_plane, uintptr_t pl_colmul, int pl_cols, uintptr_t gsrc,
+           long long pl_plane, uintptr_t pl_colmul, int pl_cols, int pl_n, uintptr_t gsrc,
            long long gs_rs, long long gs_ld, int gs_cols, uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
@@ -55,7 +56,7 @@ PYBIND11_MODULE(_hip, m) {
                            P<float>(coop_slots), P<unsigned long long>(coop_count), coop_gen,
                            coop_epochs,
                            P<int>(coop_timeout), P<unsigned short>(planes), pl_rs, pl_ld,
-                           pl_plane, P<const float>(pl_colmul), pl_cols,
+                           pl_plane, P<const float>(pl_colmul), pl_cols, pl_n,
                            P<const float>(gsrc), gs_rs, gs_ld, gs_cols,
                            reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");
@@ -328,9 +329,17 @@ PYBIND11_MODULE(_hip, m) {
   m.def("xgmi_max_blocks", []() { return cnmf_xgmi_max_blocks(); });
   m.def("xgmi_alloc", [](long long cap) {
     void* p = nullptr;
-    check(cnmf_xgmi_alloc(cap, &p), "cnmf_xgmi_alloc");
-    return reinterpret_cast<uintptr_t>(p);
+    unsigned mode = 0;
+    check(cnmf_xgmi_alloc(cap, &p, &mode), "cnmf_xgmi_alloc");
+    return py::make_tuple(reinterpret_cast<uintptr_t>(p), mode);
   });
+  m.def("ptr_alloc_flags", [](uintptr_t p) {
+    unsigned f = 0;
+    check(cnmf_ptr_alloc_flags(P<const void>(p), &f), "hipPointerGetAttributes");
+    return f;
+  });
+  m.attr("MALLOC_UNCACHED") = (unsigned)hipDeviceMallocUncached;
+  m.attr("MALLOC_FINEGRAINED") = (unsigned)hipDeviceMallocFinegrained;
   m.def("xgmi_free", [](uintptr_t p) { check(hipFree(P<void>(p)), "hipFree"); });
   m.def("xgmi_handle", [](uintptr_t p) {
     hipIpcMemHandle_t h;

@@ -17,8 +17,8 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       unsigned coop_gen, int coop_epochs,
                       int* coop_timeout, unsigned short* planes, long long pl_rs,
                       long long pl_ld, long long pl_plane, const float* pl_colmul,
-                      int pl_cols, const float* gsrc, long long gs_rs, long long gs_ld,
-                      int gs_cols, hipStream_t stream);
+                      int pl_cols, int pl_n, const float* gsrc, long long gs_rs,
+                      long long gs_ld, int gs_cols, hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,
@@ -26,6 +26,7 @@ hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, do
                             int init, hipStream_t stream);
 int cnmf_solve_reg_max_cols(int K);
 int cnmf_solve_mfma_max_cols(int K);
+int cnmf_solve_pipe_tiles(int K, int per);
 
 int cnmf_beta_max_k();
 hipError_t cnmf_beta_contract(int side, int mode, const float* X, long long ldx, const float* HT,
@@ -146,7 +147,8 @@ hipError_t cnmf_count_unit_check(const float* X, long long ldx, int N, int G, co
 long long cnmf_xgmi_data_offset();
 int cnmf_xgmi_max_ranks();
 int cnmf_xgmi_max_blocks();
-hipError_t cnmf_xgmi_alloc(long long cap, void** ptr);
+hipError_t cnmf_xgmi_alloc(long long cap, void** ptr, unsigned* mode);
+hipError_t cnmf_ptr_alloc_flags(const void* p, unsigned* flags);
 hipError_t cnmf_xgmi_allreduce(const unsigned long long* peers, int world, int rank,
                                const float* in, float* out, long long n, long long cap,
                                unsigned epoch, unsigned long long limit, int* timeout,

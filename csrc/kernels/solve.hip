@@ -11,6 +11,7 @@ hipError_t launch_solve_stream(int K, int algo, const SolveParams& p, int nblock
 
 extern "C" int cnmf_solve_max_k() { return 64; }
 extern "C" int cnmf_solve_mfma_max_cols(int K);
+extern "C" int cnmf_solve_pipe_tiles(int K, int per);
 
 // ranks the kernels are instantiated for: 1..32 and the padded wide ranks 40..64
 extern "C" int cnmf_solve_native_k(int K) {
@@ -35,7 +36,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  int coop_epochs, int* coop_timeout,
                                  unsigned short* planes, long long pl_rs, long long pl_ld,
                                  long long pl_plane, const float* pl_colmul, int pl_cols,
-                                 const float* gsrc, long long gs_rs, long long gs_ld,
+                                 int pl_n, const float* gsrc, long long gs_rs, long long gs_ld,
                                  int gs_cols, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
@@ -60,6 +61,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.coop_epochs_split = coop_split > 1 ? coop_split : 1;
   p.planes = planes; p.pl_rs = pl_rs; p.pl_ld = pl_ld; p.pl_plane = pl_plane;
   p.pl_colmul = pl_colmul; p.pl_cols = pl_cols;
+  p.pl_n = pl_n < 1 ? 1 : (pl_n > 3 ? 3 : pl_n);
   p.gsrc = gsrc; p.gs_rs = gs_rs; p.gs_ld = gs_ld; p.gs_cols = gs_cols;
   // the in-prologue Gram is a matrix-core kernel feature (K <= 16)
   if (gsrc && (variant != 3 || K > 16 || gs_cols < 1)) return hipErrorInvalidValue;
@@ -67,13 +69,19 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   if (coop_split > 1 && nsplit > 1) return hipErrorInvalidValue;
   if (coop_split > cnmf::kCoopMaxSlices) return hipErrorInvalidValue;
   if (!cnmf_solve_native_k(K)) return hipErrorInvalidValue;
-  if (variant == 3) {
-    // matrix-core variant (solve_mfma.hip): MU, K <= 16, every slice within one
-    // workgroup's tiles; the host picks the slicing (ops.solve / _mfma_split)
+  if (variant == 3 || variant == 5) {
+    // matrix-core variants, MU, K <= 16, every slice within one workgroup's tiles; the
+    // host picks the slicing (ops.solve / _mfma_split).  The software-pipelined kernel
+    // (solve_pipe.hip) takes the unregularised block-objective solves; solve_mfma.hip
+    // the rest (and everything under variant 5 = CNMF_SOLVE_PIPE=0)
     const int parts = nsplit > 1 ? nsplit : (coop_split > 1 ? coop_split : 1);
     const int per = (ncols + parts - 1) / parts;
     const int T = ((per + 15) / 16 + 3) / 4;
     if (algo != 0 || per > cnmf_solve_mfma_max_cols(K)) return hipErrorInvalidValue;
+    const int Tp = cnmf_solve_pipe_tiles(K, per);
+    if (variant == 3 && Tp > 0 && conv_mode == 1 && nsplit <= 1 && !gsrc && l1_num == 0.f &&
+        l1_den == 0.f && l2 == 0.f)
+      return cnmf::launch_solve_pipe(K, p, nblocks, Tp, p.pl_n, stream);
     return cnmf::launch_solve_mfma(K, p, nblocks, T < 1 ? 1 : T, stream);
   }
   if (K > 32) return cnmf::launch_solve_wide(K, algo, p, nblocks, threads, stream);

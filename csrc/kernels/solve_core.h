@@ -234,8 +234,8 @@ __device__ __forceinline__ void emit_planes(const SolveParams& p, int rep, int j
       const float r2 = r1 - __uint_as_float((unsigned)h1 << 16);
       const long long o = (long long)k * p.pl_ld + c;
       pl[o] = h0;
-      pl[p.pl_plane + o] = h1;
-      pl[2 * p.pl_plane + o] = solve_f2bf_rn(r2);
+      if (p.pl_n > 1) pl[p.pl_plane + o] = h1;
+      if (p.pl_n > 2) pl[2 * p.pl_plane + o] = solve_f2bf_rn(r2);
     }
   }
 }
@@ -677,6 +677,8 @@ hipError_t launch_solve_wide(int K, int algo, const SolveParams& p, int nblocks,
 hipError_t launch_solve_resident(int K, int U, int algo, const SolveParams& p, int nblocks,
                                  int threads, hipStream_t s);
 hipError_t launch_solve_mfma(int K, const SolveParams& p, int nblocks, int T, hipStream_t s);
+hipError_t launch_solve_pipe(int K, const SolveParams& p, int nblocks, int T, int pl_n,
+                             hipStream_t s);
 hipError_t launch_solve_resident34(int K, int U, int algo, const SolveParams& p, int nblocks,
                                    int threads, hipStream_t s);
 

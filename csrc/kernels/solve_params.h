@@ -38,6 +38,7 @@ struct SolveParams {
   long long pl_rs, pl_ld, pl_plane;
   const float* pl_colmul;
   int pl_cols;
+  int pl_n;                 // planes written (1..3): the consuming GEMM reads only its A planes
   // Optional (matrix-core kernel only): the system matrix is the Gram F F^T of the factor
   // F_r = gsrc + r*gs_rs (K x gs_cols, row stride gs_ld), formed in the prologue on the
   // matrix cores instead of being read from `gram` (W W^T fused into

@@ -93,7 +93,10 @@ __global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(
     }
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");    // peers' slices visible to every lane
+  // system-scope acquire: the flag loads above were system-scope acquires by the polling
+  // lanes; this fence orders every lane's slice loads after them.  The slices live in
+  // uncached / fine-grained memory (cnmf_xgmi_alloc), so the loads read the peer's HBM.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 
   // 3. sum the peers' slices in rank order
   const long long v0 = lo >> 2, v1 = hi >> 2;
@@ -128,13 +131,44 @@ int cnmf_xgmi_max_ranks() { return cnmf::kXgRanks; }
 int cnmf_xgmi_max_blocks() { return cnmf::kXgBlocks; }
 
 // Workspace for `cap` floats per parity; zeroed (flags start below every epoch >= 1).
-hipError_t cnmf_xgmi_alloc(long long cap, void** ptr) {
+//
+// Memory model.  Peers spin on flags that REMOTE GPUs store into this workspace while the
+// kernel runs, and read the peers' staged slices right after.  Plain hipMalloc memory is
+// coarse-grained: HIP makes it coherent across devices only at dispatch boundaries (a
+// reading GPU may serve a peer's line from its own L2), which is not enough for an
+// in-kernel hand-off between GPUs.  The workspace is therefore allocated UNCACHED
+// (hipDeviceMallocUncached: every access goes to the owning GPU's memory, never a stale
+// cached copy) and, where that flag is refused, FINE-GRAINED (coherent across devices at
+// system scope, which is the scope of the flag release/acquire pair below).  Coarse-grained
+// memory is never used: `mode` reports which kind was obtained (the allocation flags,
+// hipPointerGetAttributes reads them back) and the call fails if neither is available.
+hipError_t cnmf_xgmi_alloc(long long cap, void** ptr, unsigned* mode) {
   const size_t bytes = (size_t)cnmf::kXgDataOff + 2 * (size_t)cap * sizeof(float);
-  hipError_t e = hipMalloc(ptr, bytes);
+  const unsigned kinds[2] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained};
+  hipError_t e = hipErrorOutOfMemory;
+  *ptr = nullptr;
+  for (unsigned k : kinds) {
+    e = hipExtMallocWithFlags(ptr, bytes, k);
+    if (e == hipSuccess) {
+      *mode = k;
+      break;
+    }
+    (void)hipGetLastError();   // clear the sticky error of the refused flag
+    *ptr = nullptr;
+  }
   if (e != hipSuccess) return e;
   e = hipMemset(*ptr, 0, bytes);
   if (e != hipSuccess) return e;
   return hipDeviceSynchronize();
+}
+
+// allocation flags of a device pointer (0 = coarse-grained hipMalloc)
+hipError_t cnmf_ptr_alloc_flags(const void* p, unsigned* flags) {
+  hipPointerAttribute_t a;
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) return e;
+  *flags = a.allocationFlags;
+  return hipSuccess;
 }
 
 hipError_t cnmf_xgmi_allreduce(const unsigned long long* peers, int world, int rank,

@@ -145,7 +145,7 @@ def xgmi_worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     xg = XgmiAllReduce(None, dev, cap=1 << 16, timeout_ms=3000)
-    res = {}
+    res = {"memory_kind": xg.memory_kind}
     # back-to-back calls without host syncs (both workspace parities in flight); sizes hit
     # the float4 body, scalar tails and a buffer at capacity; an unaligned view too
     sizes = [1, 3, 4, 1000, 4097, 1 << 16, 777, 65533, 5, 4096] * 6

@@ -71,3 +71,34 @@ def test_bench_k_grid_ragged_batch():
     out = _bench(["--kmin", "3", "--kmax", "5"], 1)
     assert out["config"]["global_batch"] == 9 and out["metric"].startswith(
         "NMF replicates/sec (K=3..5")
+
+
+def test_bench_self_launches_n_ranks_without_a_launcher():
+    """``python bench.py --gpus 2`` with no torch.distributed.run in front starts the two
+    ranks itself (child launcher, never an exec) and reports the process-group world."""
+    tiny = ["--cpu", "--cells", "300", "--genes", "60", "--k", "4", "--n-iter", "3",
+            "--batch-size", "100", "--max-nmf-iter", "50", "--steps", "2", "--warmup", "1"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"] + tiny, cwd=ROOT,
+                       capture_output=True, text=True, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["rccl_world"] == 2
+    assert out["config"]["backend"] == "gloo"
+    # weak run also reports the strong form: one 3-replicate batch per step over 2 ranks
+    assert out["config"]["strong_global_batch"] == 3
+    assert out["config"]["strong_value"] > 0
+
+
+def test_bench_world_size_mismatch_fails():
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0",
+               CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, "bench.py", "--cpu", "--gpus", "2"], cwd=ROOT,
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=3" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -295,3 +295,23 @@ def test_incomplete_jobs_are_rank0s_list(prepared):
     obj.factorize_jobs([0], run_params=rp, verbose=False)
     assert _incomplete_jobs(obj, rp, True) == [1, 2, 3]
     assert _incomplete_jobs(obj, rp, True, _Comm()) == [0, 1, 2, 3]
+
+
+def test_solver_raises_when_the_communicator_reports_a_failed_collective():
+    """A communicator whose collective gave up (the xGMI all-reduce's timeout flag) makes
+    the solver raise before returning spectra a caller could persist."""
+    import torch
+
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.parallel.comm import LocalComm
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    class FailedComm(LocalComm):
+        def check(self):
+            raise RuntimeError("peer did not arrive")
+
+    X = torch.from_numpy(normalized_counts_matrix(200, 40, n_programs=3, seed=1))
+    solver = NMFBatchSolver(X, NMFOptions(n_components=3, online_chunk_size=100,
+                                          online_max_pass=2), comm=FailedComm())
+    with pytest.raises(RuntimeError, match="peer did not arrive"):
+        solver.run([1, 2])

@@ -1235,3 +1235,55 @@ def test_gemm_planes_every_tile_variant(monkeypatch, variant, bk, stages):
         assert err < 1e-6 * K / 256, (variant, bk, stages, ks, err)
     monkeypatch.undo()
     ops.refresh_env()
+
+
+@pytest.mark.parametrize("K", [1, 3, 5, 10, 12, 13, 16])
+@pytest.mark.parametrize("n,coop", [(500, 1), (3100, "auto"), (5000, "auto")])
+def test_solve_pipe_bitwise_equals_mfma_kernel(monkeypatch, K, n, coop):
+    """The software-pipelined matrix-core MU solve (solve_pipe.hip: compile-time tile
+    count, chain(i + 1) issued before the update of tile i, planes from registers) does
+    the SAME fp32 operations in the same order as solve_mfma_kernel: converged solves
+    (block objective, cooperative slices, an inactive replicate, rep_index) agree
+    bitwise in x, lin/quad, iteration counts and the emitted planes -- and the two
+    planes it writes are the first two of ops.split_planes of the result."""
+    R = 6
+    x0, numer, gram = _problem(R, K, n, seed=50 + K)
+    dev = torch.device("cuda")
+    numer_d, gram_d = numer.to(dev), gram.to(dev)
+    active = torch.tensor([1, 1, 0, 1, 1, 1], dtype=torch.int32, device=dev)
+    ri = torch.tensor([0, 2, 3, 5], dtype=torch.int32, device=dev)
+    pad = -(-n // 64) * 64 + 64
+    out = {}
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("CNMF_SOLVE_PIPE", pipe)
+        ops.refresh_env()
+        xg = x0.clone().to(dev)
+        lin = torch.zeros(R, device=dev)
+        quad = torch.zeros(R, device=dev)
+        it = torch.zeros(R, dtype=torch.int32, device=dev)
+        planes = torch.full((3, R * K, pad), 77, dtype=torch.int16, device=dev)
+        ops.solve("mu", xg, numer_d, gram_d, rep_index=ri, max_iter=200, tol=1e-4,
+                  lin_out=lin, quad_out=quad, iters_out=it, conv_mode=1, check_every=4,
+                  active=active, coop=coop, planes=planes, planes_n=2)
+        out[pipe] = (xg.cpu(), lin.cpu(), quad.cpu(), it.cpu(), planes.cpu())
+    monkeypatch.delenv("CNMF_SOLVE_PIPE")
+    ops.refresh_env()
+    ops.coop_check(dev)
+    for a, b in zip(out["1"], out["0"]):
+        assert torch.equal(a, b)
+    xp, _, _, itp, plp = out["1"]
+    assert itp[1].item() == 0 and itp[4].item() == 0 and itp[2].item() == 0  # untouched
+    assert torch.equal(xp[2], x0[2]) and torch.equal(xp[1], x0[1])
+    assert (itp[[0, 3, 5]] > 0).all()
+    ref = torch.zeros((3, R * K, pad), dtype=torch.int16, device=dev)
+    ops.split_planes(xp.to(dev).reshape(R * K, n), ref)
+    for r in (0, 3, 5):
+        rows = slice(r * K, (r + 1) * K)
+        assert torch.equal(plp[:2, rows], ref[:2, rows].cpu())
+        assert (plp[2, rows] == 77).all()          # the third plane is never written
+    # and against the fp64 reference solve of the same stopping rule
+    xr = x0.clone().double()
+    reference.solve(0, xr, numer.double(), gram.double(), None, 200, 1e-4, 0, 0, 0, 1e-16,
+                    None, None, None, 1, 1, 4)
+    for r in (0, 3, 5):
+        assert ((xp[r].double() - xr[r]).norm() / xr[r].norm()) < 1e-2

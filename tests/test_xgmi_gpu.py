@@ -28,6 +28,10 @@ def test_xgmi_allreduce_matches_gloo(tmp_path):
         assert bool(r["comm_is_xgmi"])
         np.testing.assert_array_equal(r["comm"], np.full(10, 3.0, dtype=np.float32))
     assert bool(r0["timed_out"]) and not bool(r1["timed_out"])
+    # the workspace peers hand data over in is coherent across devices while kernels run:
+    # uncached or fine-grained (hipPointerGetAttributes), never coarse-grained hipMalloc
+    for r in (r0, r1):
+        assert str(r["memory_kind"]) in ("uncached", "fine-grained"), r["memory_kind"]
 
 
 def test_xgmi_dp_solve_matches_gloo_staged(tmp_path):
