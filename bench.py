@@ -152,8 +152,27 @@ def main() -> int:
             res = solver.run_concurrent([int(s) for s in seeds], n_streams=args.streams)
         else:
             res = solver.run([int(s) for s in seeds], ks=[int(k) for k in ks])
-        spectra = res.W.cpu()  # factorize persists spectra (cnmf.py:889-892)
-        return res, spectra
+        return res, to_host(res.W)   # factorize persists spectra (cnmf.py:889-892)
+
+    # Spectra go to pinned host memory on a copy stream, as factorize overlaps its
+    # replicate-file writes with the next batch's solve; the barrier that closes the timed
+    # region synchronises the device, so every copy has landed inside it.
+    copy_stream = torch.cuda.Stream(dev) if use_cuda else None
+    host_bufs: dict = {}
+
+    def to_host(W):
+        if copy_stream is None:
+            return W.cpu()
+        key = tuple(W.shape)   # copies run in order on one stream: one buffer per shape
+        buf = host_bufs.get(key)
+        if buf is None:
+            buf = torch.empty(W.shape, dtype=W.dtype, pin_memory=True)
+            host_bufs[key] = buf
+        copy_stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(copy_stream):
+            buf.copy_(W, non_blocking=True)
+        W.record_stream(copy_stream)    # W's memory is not reused before the copy ran
+        return buf
 
     def barrier():
         if world > 1:

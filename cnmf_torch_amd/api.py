@@ -8,9 +8,12 @@ reference, on the MI355X-native engine:
   still writing one ``spectra.k_%d.iter_%d.df.npz`` per replicate (atomic writes).
 * ``refit_usage`` / ``refit_spectra`` use the fused on-device refit (models/refit.py).
 * ``consensus`` runs the pairwise distances, density filter, medians and silhouette on
-  the device; KMeans uses sklearn's exact algorithm by default
-  (``kmeans_backend='auto'`` -- the default -- runs the batched k-means on the GPU when one
-  is in use; ``'sklearn'`` is the reference's exact CPU KMeans).
+  the device.  KMeans: ``kmeans_backend='auto'`` (the default) runs the batched device
+  k-means (k-means++ + Lloyd, 4 x n_init restarts, best inertia; its own RNG stream, so
+  the partition can differ from sklearn's where two partitions have close inertia) when
+  the spectra are on a GPU, and sklearn on the CPU; ``'sklearn'`` is the reference's
+  exact ``KMeans(n_clusters=k, n_init=10, random_state=1)`` (cnmf.py:1082) on any device
+  -- the choice for bit-level parity with the reference.
 * multi-worker / multi-GPU: ``factorize(worker_i, total_workers)`` keeps the
   round-robin ledger sharding of cnmf.py:53-54 (CLI ``--worker-index`` restored);
   ``cnmf_torch_amd.parallel`` launches one rank per GPU over torch.distributed.

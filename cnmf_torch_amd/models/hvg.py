@@ -17,6 +17,32 @@ import scipy.sparse as sp
 import torch
 
 
+def sparse_mean_var(X):
+    """Column mean and ddof=0 variance of a scipy sparse matrix: sklearn's corrected
+    two-pass CSR algorithm (``sklearn.utils.sparsefuncs.mean_variance_axis``, which
+    ``StandardScaler(with_mean=False).fit`` runs, cnmf.py:128-131) re-expressed as
+    float64 bincounts that accumulate in the same (row-major data) order -- without
+    importing sklearn, whose import alone was ~1 s of every ``prepare``."""
+    X = sp.csr_matrix(X)
+    N, G = X.shape
+    data = np.asarray(X.data, dtype=np.float64)
+    idx = X.indices
+    nnz = np.bincount(idx, minlength=G)
+    mean = np.bincount(idx, weights=data, minlength=G) / float(N)
+    diff = data - mean[idx]
+    corr = np.bincount(idx, weights=diff, minlength=G)
+    var = np.bincount(idx, weights=diff * diff, minlength=G)
+    miss = (N - nnz).astype(np.float64)
+    has = nnz != N
+    corr = np.where(has, corr - miss * mean, corr)
+    corr = corr ** 2 / float(N)
+    var = np.where(has, var + miss * mean ** 2, var)
+    var = (var - corr) / float(N)
+    if X.dtype == np.float32:     # sklearn's float32 specialisation returns float32 values
+        return mean.astype(np.float32).astype(np.float64), var.astype(np.float32).astype(np.float64)
+    return mean, var
+
+
 def get_mean_var(X):
     """Column mean and ddof=0 variance of a dense/sparse/torch matrix or a device CSR
     (cnmf.py:128-131)."""
@@ -30,6 +56,8 @@ def get_mean_var(X):
         mean = Xd.mean(dim=0)
         var = (Xd * Xd).mean(dim=0) - mean * mean
         return mean.cpu().numpy(), torch.clamp(var, min=0).cpu().numpy()
+    if sp.issparse(X):
+        return sparse_mean_var(X)
     from sklearn.preprocessing import StandardScaler
 
     sc = StandardScaler(with_mean=False)

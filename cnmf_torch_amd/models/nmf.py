@@ -361,7 +361,7 @@ class _Batch:
     err_init/err_prev/err, int32 active/converged/n_pass) so the solves skip finished
     replicates without a host round trip."""
 
-    def __init__(self, HT, W, kpos):
+    def __init__(self, HT, W, kpos, arena: dict | None = None):
         self.HT, self.W = HT, W
         self.kpos = np.asarray(kpos, dtype=np.int64)
         if np.any(np.diff(self.kpos) < 0):
@@ -370,12 +370,25 @@ class _Batch:
         self.order = np.arange(R, dtype=np.int64)
         self.n_act = R
         dev = W.device
-        self.state = {k: torch.zeros(R, dtype=torch.float64, device=dev)
-                      for k in ("err_init", "err_prev", "err")}
-        for k in ("active", "converged", "n_pass"):
-            self.state[k] = torch.zeros(R, dtype=torch.int32, device=dev)
-        self.h_iters = torch.zeros(R, dtype=torch.int32, device=dev)
-        self.w_iters = torch.zeros(R, dtype=torch.int32, device=dev)
+        # arena (NMFBatchSolver._arena): HT, W and the per-replicate state live in tensors
+        # that persist across runs and are compacted IN PLACE, so every buffer a pass
+        # touches has the same address for the same layout in every run -- the condition
+        # for replaying one captured HIP graph per layout across ledger batches
+        self.inplace = arena is not None
+        self.arena = arena
+        self.graphs = False       # NMFBatchSolver.run: replay graphs per layout (arena only)
+        if arena is not None:
+            self.state = arena["state"]
+            for v in self.state.values():
+                v.zero_()
+            self.h_iters, self.w_iters = arena["h_iters"].zero_(), arena["w_iters"].zero_()
+        else:
+            self.state = {k: torch.zeros(R, dtype=torch.float64, device=dev)
+                          for k in ("err_init", "err_prev", "err")}
+            for k in ("active", "converged", "n_pass"):
+                self.state[k] = torch.zeros(R, dtype=torch.int32, device=dev)
+            self.h_iters = torch.zeros(R, dtype=torch.int32, device=dev)
+            self.w_iters = torch.zeros(R, dtype=torch.int32, device=dev)
         self.layout_version = 0   # bumped by compact(): captured graphs key on it
         # optional callback(orig_idx, kpos, host_rows, event): the final spectra of the
         # replicates a compaction retires, copied to pinned memory (ready at `event`), so
@@ -465,17 +478,24 @@ class _Batch:
         dev = self.W.device
         roff = np.concatenate([[0], np.cumsum(self.kpos)[:-1]])
         rows = _to_device(_ranges(roff[perm], self.kpos[perm]), dev)
-        self.HT = self.HT.index_select(0, rows)
-        self.W = self.W.index_select(0, rows)
         pidx = _to_device(perm, dev)
+        if self.inplace:     # same storage, permuted rows (arena: addresses never move)
+            for t, ix in ((self.HT, rows), (self.W, rows), (self.h_iters, pidx),
+                          (self.w_iters, pidx)):
+                t.copy_(t.index_select(0, ix))
+            for v in self.state.values():
+                v.copy_(v.index_select(0, pidx))
+        else:
+            self.HT = self.HT.index_select(0, rows)
+            self.W = self.W.index_select(0, rows)
+            self.state = {k: v.index_select(0, pidx) for k, v in self.state.items()}
+            self.h_iters = self.h_iters.index_select(0, pidx)
+            self.w_iters = self.w_iters.index_select(0, pidx)
         if self.B is not None:
             self.B = self.B.index_select(0, rows)
             sq = self.kpos * self.kpos
             qoff = np.concatenate([[0], np.cumsum(sq)[:-1]])
             self.A = self.A.index_select(0, _to_device(_ranges(qoff[perm], sq[perm]), dev))
-        self.state = {k: v.index_select(0, pidx) for k, v in self.state.items()}
-        self.h_iters = self.h_iters.index_select(0, pidx)
-        self.w_iters = self.w_iters.index_select(0, pidx)
         self.order = self.order[perm]
         self.kpos = self.kpos[perm]
         self.n_act = n_new
@@ -777,6 +797,10 @@ def native_rank(K: int) -> int:
 
 
 _GRAM_PROLOGUE = os.environ.get("CNMF_SOLVE_GRAM_PROLOGUE", "0") == "1"
+# fused step: split-K GEMMs of up to this many k slices hand their raw slabs to the
+# consuming solve; deeper splits (the few-replicate tail) are reduced by the GEMM's own
+# pass -- the solve would read every slab per element (CNMF_FUSED_MAX_SLABS overrides)
+_FUSED_MAX_SLABS = int(os.environ.get("CNMF_FUSED_MAX_SLABS", "4"))
 
 
 def _graphs_enabled(X: torch.Tensor) -> bool:
@@ -860,11 +884,16 @@ class NMFBatchSolver:
         kp = np.array([native_rank(k) for k in ks], dtype=np.int64) if pad else ks
         pos = np.lexsort((np.arange(R), kp, ks))     # positions grouped by K
         kpos = kp[pos]
+        arena = None
         if HT0 is None or W0 is None:
             N, G = self.X.shape
             tot = int(kpos.sum())
-            HT = torch.zeros((tot, N), device=self.X.device, dtype=self.X.dtype)
-            W = torch.zeros((tot, G), device=self.X.device, dtype=self.X.dtype)
+            arena = self._arena(kpos) if (not pad and self._graphs_wanted(kpos)) else None
+            if arena is not None:
+                HT, W = arena["HT"].zero_(), arena["W"].zero_()
+            else:
+                HT = torch.zeros((tot, N), device=self.X.device, dtype=self.X.dtype)
+                W = torch.zeros((tot, G), device=self.X.device, dtype=self.X.dtype)
             r0 = 0
             for K in np.unique(ks[pos]):
                 sel = pos[ks[pos] == K]
@@ -889,7 +918,8 @@ class NMFBatchSolver:
             if pad:
                 raise ValueError("explicit initial factors need K <= 32 on the GPU")
             HT, W = HT0.to(self.X.dtype).clone(), W0.to(self.X.dtype).clone()
-        st = _Batch(HT, W, kpos)
+        st = _Batch(HT, W, kpos, arena=arena)
+        st.graphs = arena is not None
         st.order = pos.astype(np.int64).copy()
         if on_retire is not None and not pad:
             st.on_retire = on_retire
@@ -1161,6 +1191,234 @@ class NMFBatchSolver:
         self.comm.allreduce_(tot)
         return torch.sqrt(torch.clamp(2.0 * tot.cpu(), min=0.0))
 
+    # ------------------------------------------------------------------ graphs / arena
+    def _graphs_wanted(self, kpos) -> bool:
+        """Replay the fused online passes from HIP graphs captured once per batch layout
+        and kept across runs (CNMF_GRAPHS: 'auto' (default) = batches of <= 256
+        replicates, whose passes are short enough for the host's per-pass enqueue to
+        show; '1' any batch; '0' never).  Needs the fused step's preconditions (checked
+        again per run by _fused_ok)."""
+        env = os.environ.get("CNMF_GRAPHS", "auto")
+        o = self.opts
+        if env == "0" or self.X.device.type != "cuda" or self.beta != 2.0 or o.mode != "online":
+            return False
+        if env != "1" and len(kpos) > 256:
+            return False
+        return (o.algo == "mu" and o.online_stats == "pass" and o.online_inner_conv == "loss"
+                and not self.comm.is_distributed and int(np.max(kpos)) <= 16
+                and os.environ.get("CNMF_FUSED_STEP", "1") != "0"
+                and all(v == 0.0 for v in (o.l1_H, o.l2_H, o.l1_W, o.l2_W)))
+
+    def _arena(self, kpos) -> dict:
+        """HT / W / state tensors of a batch with this rank vector, kept across runs on the
+        current stream (see _Batch's arena)."""
+        import collections
+
+        key = (tuple(int(k) for k in kpos), ops._stream_ptr(self.X))
+        if not hasattr(self, "_arenas"):
+            self._arenas = collections.OrderedDict()
+        a = self._arenas.get(key)
+        if a is None:
+            N, G = self.X.shape
+            dev, tot, R = self.X.device, int(np.sum(kpos)), len(kpos)
+            a = {"HT": torch.zeros((tot, N), device=dev, dtype=self.X.dtype),
+                 "W": torch.zeros((tot, G), device=dev, dtype=self.X.dtype),
+                 "state": {k: torch.zeros(R, dtype=torch.float64, device=dev)
+                           for k in ("err_init", "err_prev", "err")},
+                 "h_iters": torch.zeros(R, dtype=torch.int32, device=dev),
+                 "w_iters": torch.zeros(R, dtype=torch.int32, device=dev),
+                 "slots": collections.OrderedDict()}
+            for k in ("active", "converged", "n_pass"):
+                a["state"][k] = torch.zeros(R, dtype=torch.int32, device=dev)
+            self._arenas[key] = a
+            while len(self._arenas) > 4:
+                self._arenas.popitem(last=False)
+        else:
+            self._arenas.move_to_end(key)
+        return a
+
+    def _slot(self, st: _Batch, steps) -> dict:
+        """Per-layout slot of an arena batch: the fused step's workspaces (fixed addresses),
+        a capture stream and, once captured, the pass's HIP graph."""
+        a = st.arena
+        key = (st.n_act, tuple(int(k) for k in st.kpos[:st.n_act]),
+               tuple(tuple(b) for b in steps))
+        slots = a["slots"]
+        sl = slots.get(key)
+        if sl is None:
+            sl = {"fb": self._fused_bufs(st, steps), "graph": None, "failed": False,
+                  "stream": torch.cuda.Stream(self.X.device)}
+            slots[key] = sl
+            while len(slots) > 24:
+                slots.popitem(last=False)
+        else:
+            slots.move_to_end(key)
+        return sl
+
+    def _replay_slot(self, sl: dict, st: _Batch, steps) -> bool:
+        """Run one non-final fused pass from the slot's graph (captured on first use, on
+        the slot's own stream, from a pass whose operands are already in place).  False:
+        capture unavailable -- the caller runs the pass eagerly."""
+        if sl["failed"]:
+            return False
+        if sl["graph"] is None:
+            g = torch.cuda.CUDAGraph()
+            main = torch.cuda.current_stream(self.X.device)
+            sl["stream"].wait_stream(main)
+            try:
+                with torch.cuda.stream(sl["stream"]):
+                    g.capture_begin()
+                    try:
+                        self._fused_pass(st, steps, sl["fb"], False)
+                    finally:
+                        g.capture_end()
+            except RuntimeError:
+                sl["failed"] = True
+                return False
+            main.wait_stream(sl["stream"])
+            sl["graph"] = g
+        sl["graph"].replay()
+        return True
+
+    # ------------------------------------------------------------------ fused online step
+    def _fused_ok(self, st: _Batch, steps) -> bool:
+        """Whether the online Frobenius passes can run the FUSED step: GEMM -> pipelined
+        H-solve -> GEMM -> pipelined W-solve with no reduction or Gram launch between them
+        (split-K slabs summed by the consuming solve, the Grams passed between the solves
+        as per-slice partials; solve_pipe.hip).  Needs the split-GEMM planes, MU without
+        regularisation, the block-objective stop, one block per online step (8-aligned), a
+        single process (the DP path all-reduces the statistics), K <= 16 and solves whose
+        cooperative slices fit the pipelined kernel.  CNMF_FUSED_STEP=0 disables it."""
+        o = self.opts
+        if (self.X.device.type != "cuda" or os.environ.get("CNMF_FUSED_STEP", "1") == "0"
+                or ops._ENV["CNMF_SOLVE_PIPE"] == "0" or o.algo != "mu"
+                or o.online_stats != "pass" or o.online_inner_conv != "loss"
+                or self.comm.is_distributed or any(v != 0.0 for v in (o.l1_H, o.l2_H, o.l1_W, o.l2_W))
+                or self._planes() is None):
+            return False
+        G = self.X.shape[1]
+        for blocks in steps:
+            if len(blocks) != 1 or blocks[0][0] % 8 or blocks[0][1] <= blocks[0][0]:
+                return False
+        dev = self.X.device
+        for g in st.groups:
+            if g.K > 16:
+                return False
+            for n in {b - a for (a, b), in steps} | {G}:
+                S = ops._mfma_split(n, g.n, g.K, 1, "auto", dev)
+                if S is None or S > ops.kCoopMaxSlices or ops._hip.solve_pipe_tiles(g.K, -(-n // S)) == 0:
+                    return False
+        return True
+
+    def _fused_bufs(self, st: _Batch, steps) -> dict:
+        """Per-layout workspaces of the fused step (allocated when the layout changes)."""
+        xp = self._planes()
+        dev = self.X.device
+        rows, sq = st.rows_act, st.sq_act
+        G = self.X.shape[1]
+        cws = [b - a for (a, b), in steps]
+        bk = ops.planes_bk(xp.pb)
+        ks_n = max(ops.gemm_plan(rows, cw, xp.Gp, xp.pb)[1] for cw in cws)
+        ks_b = max(ops.gemm_plan(rows, G, -(-cw // bk) * bk, xp.pb)[1] for cw in cws)
+        S = ops.kCoopMaxSlices
+        ngp = sum(g.n * S * g.K * g.K for g in st.groups)
+        kd_max = max(-(-cw // bk) * bk for cw in cws)
+        fb = {
+            "wpl": torch.zeros((3, rows, xp.Gp), device=dev, dtype=torch.int16),
+            "hpl": torch.zeros((3, rows, kd_max), device=dev, dtype=torch.int16),
+            "wpl_key": None,
+            "slabN": torch.empty(ks_n * rows * max(cws), device=dev, dtype=torch.float32),
+            "slabB": torch.empty(ks_b * rows * G, device=dev, dtype=torch.float32),
+            "B": torch.empty((rows, G), device=dev, dtype=torch.float32),
+            "A": [torch.empty(sq, device=dev, dtype=torch.float32) for _ in range(2)],
+            "WWp": torch.empty(max(ngp, 1), device=dev, dtype=torch.float32),
+            "HHp": torch.empty(max(ngp, 1), device=dev, dtype=torch.float32),
+            "lin": torch.zeros(st.n_act, device=dev, dtype=torch.float32),
+            "quad": torch.zeros(st.n_act, device=dev, dtype=torch.float32),
+            "wwp_n": {}, "hhp_n": {}, "wwp_key": None,
+        }
+        off = 0
+        fb["parts"] = {}
+        for g in st.groups:
+            m = g.n * S * g.K * g.K
+            fb["parts"][g.p0] = (lambda t, o_=off, g_=g: t[o_:o_ + g_.n * S * g_.K * g_.K]
+                                 .view(g_.n, S, g_.K, g_.K))
+            off += m
+        return fb
+
+    def _fused_pass(self, st: _Batch, steps, fb: dict, final: bool) -> None:
+        """One online pass of the fused step (see _fused_ok); same updates, stopping rules
+        and statistics as the unfused pass -- the split-K sums and the accumulation of
+        B / A are bitwise the unfused ones, the Grams are summed per slice instead of per
+        Gram-kernel workgroup (fp32 rounding order only)."""
+        o = self.opts
+        xp = self._planes()
+        X = self.X
+        G = X.shape[1]
+        HT, W = st.views()
+        rows = st.rows_act
+        groups = st.groups
+        active = st.active_mask()
+        n = st.n_act
+        h_it, w_it = st.h_iters[:n], st.w_iters[:n]
+        bk = ops.planes_bk(xp.pb)
+        slabN, slabB, B = fb["slabN"], fb["slabB"], fb["B"]
+        # W W^T partials: recomputed by the Gram kernel whenever W changed outside the
+        # fused W-solve (init, compaction, an unfused pass), else the last W-solve's
+        wkey = (W.data_ptr(), rows, st.uid, st.layout_version)
+        if fb["wwp_key"] != wkey:
+            for g in groups:
+                ww = ops.gram(g.rep3(W), active=active[g.pos])
+                fb["parts"][g.p0](fb["WWp"])[:, 0].copy_(ww)
+                fb["wwp_n"][g.p0] = 1
+        last_s = len(steps) - 1
+        wpl = fb["wpl"]
+        if fb["wpl_key"] != wkey:      # spectra planes: split here only after such a change
+            ops.split_planes(W, wpl, col_mul=xp.unit)
+            fb["wpl_key"] = wkey
+        for s_, ((a, b),) in enumerate(steps):
+            cw = b - a
+            ks_n = ops.gemm_planes(None, wpl[:ops.gemm_a_planes(xp.Gp)], xp.x[:, a:], rows, cw,
+                                   xp.Gp, raw_slab=slabN, raw_max=_FUSED_MAX_SLABS)
+            kd = -(-cw // bk) * bk
+            hpl = fb["hpl"][:, :, :kd]
+            hpl_n = ops.gemm_a_planes(kd)
+            hcols = HT[:, a:b]
+            for g in groups:
+                numer = slabN.as_strided((g.n, g.K, cw), (g.K * cw, cw, 1), g.r0 * cw)
+                ga = active[g.pos]
+                fb["hhp_n"][g.p0] = ops.solve(
+                    "mu", g.rep3(hcols), numer, None, max_iter=o.online_chunk_max_iter,
+                    tol=o.online_h_tol, eps=o.eps, iters_out=h_it[g.pos], conv_mode=1,
+                    check_every=o.inner_check_every, active=ga, planes=hpl[:, g.rows],
+                    planes_n=hpl_n, numer_slabs=ks_n, numer_slab_stride=rows * cw,
+                    gram_parts=fb["parts"][g.p0](fb["WWp"]), gram_parts_n=fb["wwp_n"][g.p0],
+                    gram_parts_out=fb["parts"][g.p0](fb["HHp"]), coop_device_gen=True)
+            ks_b = ops.gemm_planes(None, hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd,
+                                   raw_slab=slabB, raw_max=_FUSED_MAX_SLABS)
+            last = s_ == last_s
+            wpl_out, unit = wpl, xp.unit
+            wpl_n = ops.gemm_a_planes(xp.Gp)
+            A_in, A_out = fb["A"][(s_ + 1) % 2], fb["A"][s_ % 2]
+            for g in groups:
+                numer = slabB.as_strided((g.n, g.K, G), (g.K * G, G, 1), g.r0 * G)
+                fb["wwp_n"][g.p0] = ops.solve(
+                    "mu", g.rep3(W), numer, None if s_ == 0 else g.gram3(A_in),
+                    max_iter=o.online_chunk_max_iter, tol=o.online_w_tol, eps=o.eps,
+                    lin_out=fb["lin"][g.pos] if last else None,
+                    quad_out=fb["quad"][g.pos] if last else None,
+                    iters_out=w_it[g.pos], conv_mode=1, check_every=o.inner_check_every,
+                    active=active[g.pos], planes=wpl_out[:, g.rows], planes_colmul=unit,
+                    planes_n=wpl_n, numer_slabs=ks_b, numer_slab_stride=rows * G,
+                    numer_scale=unit, numer_base=None if s_ == 0 else g.rep3(B),
+                    numer_out=None if last else g.rep3(B),
+                    gram_parts=fb["parts"][g.p0](fb["HHp"]), gram_parts_n=fb["hhp_n"][g.p0],
+                    gram_out=None if last else g.gram3(A_out),
+                    gram_parts_out=fb["parts"][g.p0](fb["WWp"]), coop_device_gen=True)
+            fb["wwp_key"] = fb["wpl_key"] = wkey
+        ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
+                        n, -1, o.tol, final=final)
+
     # ------------------------------------------------------------------ online frobenius
     def _online_frob(self, st: _Batch) -> None:
         o, comm = self.opts, self.comm
@@ -1181,10 +1439,24 @@ class NMFBatchSolver:
         n_alloc = None
         graphs = _graphs_enabled(X) and not dist
         graph, graph_key, last_key = None, None, None
+        fused = self._fused_ok(st, steps)
+        fb, fb_key, sl = None, None, None
         for p in range(max_pass):
             n = st.n_act
             if n == 0:
                 break
+            if fused:
+                key = (st.uid, st.layout_version)
+                final = p + 1 == max_pass
+                if fb_key != key:      # a new layout: its first pass runs eagerly
+                    sl = self._slot(st, steps) if st.graphs else None
+                    fb, fb_key = (sl["fb"] if sl is not None else self._fused_bufs(st, steps)), key
+                    self._fused_pass(st, steps, fb, final=final)
+                elif sl is None or final or not self._replay_slot(sl, st, steps):
+                    self._fused_pass(st, steps, fb, final=final)
+                if not pipe.after_enqueue():
+                    break
+                continue
             rows, sq = st.rows_act, st.sq_act
             if (rows, sq, n) != n_alloc:   # (re)allocate per-layout workspaces, not per pass
                 n_alloc = (rows, sq, n)

@@ -54,11 +54,11 @@ def _mean_var_ddof1(X):
     n = X.shape[0]
     if sp.issparse(X):
         # scanpy's sparse path: sklearn's centred two-pass variance (exact 0 for constant
-        # genes); the dense path below is scanpy's E[x^2] - E[x]^2
-        from sklearn.utils.sparsefuncs import mean_variance_axis
+        # genes; models.hvg.sparse_mean_var, the same float64 operations in the same
+        # order); the dense path below is scanpy's E[x^2] - E[x]^2
+        from .hvg import sparse_mean_var
 
-        mean, var = mean_variance_axis(sp.csr_matrix(X, dtype=np.float64), axis=0)
-        mean, var = np.asarray(mean, dtype=np.float64), np.asarray(var, dtype=np.float64)
+        mean, var = sparse_mean_var(sp.csr_matrix(X, dtype=np.float64))
     else:
         mean = np.mean(X, axis=0, dtype=np.float64)
         mean_sq = np.mean(np.multiply(X, X, dtype=np.float64), axis=0)

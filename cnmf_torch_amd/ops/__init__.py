@@ -115,7 +115,12 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           check_every: int = 10, variant: str = "auto",
           active: torch.Tensor | None = None, coop: int | str = "auto",
           planes: torch.Tensor | None = None, planes_colmul: torch.Tensor | None = None,
-          gram_of: torch.Tensor | None = None, planes_n: int = 3) -> None:
+          gram_of: torch.Tensor | None = None, planes_n: int = 3,
+          numer_slabs: int = 1, numer_slab_stride: int = 0,
+          numer_scale: torch.Tensor | None = None, numer_base: torch.Tensor | None = None,
+          numer_out: torch.Tensor | None = None, gram_parts: torch.Tensor | None = None,
+          gram_parts_n: int = 0, gram_out: torch.Tensor | None = None,
+          gram_parts_out: torch.Tensor | None = None, coop_device_gen: bool = False) -> int:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -143,10 +148,30 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     ``gemm_a_planes(Kd)`` A planes; the rest would be dead stores).
     MU with l1 = l2 = 0, the block-objective stop and K <= 16 runs the software-pipelined
     matrix-core kernel (solve_pipe.hip) unless ``CNMF_SOLVE_PIPE=0``.
+
+    Fused operands (pipelined kernel only; a launch that cannot take them raises):
+    ``numer_slabs`` / ``numer_slab_stride``: ``numer`` is slab 0 of that many raw split-K
+    partials (gemm_planes(raw_slab=...)) ``numer_slab_stride`` floats apart, summed in
+    slice order, times ``numer_scale`` (per column), plus ``numer_base`` (R, K, n);
+    ``numer_out`` (R, K, n) receives that sum.  ``gram_parts`` (R, >= gram_parts_n, K, K):
+    the system matrix is ``gram`` (optional base) + the sum of the first ``gram_parts_n``
+    partial Grams; ``gram_out`` (R, K, K) receives it.  ``gram_parts_out`` (R, >= S, K, K):
+    slice s of the launch writes its partial Gram sum_cols x x^T of the final x there.
+    ``coop_device_gen``: cooperative launches tag their granules from a device-side
+    generation the kernel itself advances (pipelined kernel only), so a launch captured
+    in a HIP graph needs no zeroing of the granules per replay.
+    Returns S, the number of column slices per replicate the launch used.
     """
     a = ALGOS[algo]
     R, K, n = x.shape
-    if gram is None:
+    fused = (numer_slabs > 1 or numer_scale is not None or numer_base is not None
+             or numer_out is not None or gram_parts is not None or gram_out is not None
+             or gram_parts_out is not None or coop_device_gen)
+    if fused and not use_native(x):
+        raise ValueError("solve: fused operands need the HIP kernels (CUDA tensors)")
+    if gram is None and gram_parts is not None:
+        pass
+    elif gram is None:
         if gram_of is None or gram_of.shape[:2] != (R, K):
             raise ValueError("solve: pass gram (R, K, K) or gram_of (R, K, m)")
     elif gram_of is not None:
@@ -159,7 +184,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                         active)
         if planes is not None:
             split_planes(x.reshape(R * K, n), planes, col_mul=planes_colmul)
-        return
+        return 1
     h = _hip
     # a GPU operand the kernels do not cover is an error, never a silent eager fallback:
     # fp32 only; K in 1..32 or a padded wide rank (the engine pads K <= 64 to a multiple
@@ -175,9 +200,10 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             raise ValueError(f"gram: expected float32 {(R, K, K)}, got {gram.dtype} "
                              f"{tuple(gram.shape)}")
         gram = gram.contiguous()
-    else:
+    elif gram_of is not None:
         _check_block_view("gram_of", gram_of, R, K, gram_of.shape[2])
-    devs = {x.device, numer.device, (gram if gram is not None else gram_of).device}
+    src = gram if gram is not None else (gram_of if gram_of is not None else gram_parts)
+    devs = {x.device, numer.device, src.device}
     if len(devs) != 1:
         raise ValueError(f"solve operands on different devices: {devs}")
     if rep_index is not None:
@@ -188,7 +214,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     else:
         nblocks, ri = R, 0
     if nblocks == 0 or n == 0:
-        return
+        return 0
     if nsplit > 1 and max_iter != 1:
         raise ValueError("nsplit > 1 requires max_iter == 1 (no convergence test)")
     for name, t, dt in (("lin_out", lin_out, torch.float32), ("quad_out", quad_out, torch.float32),
@@ -199,6 +225,9 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
         for t in (lin_out, quad_out):
             if t is not None:
                 t.zero_()
+    f_args = _fused_solve_args(R, K, n, x, numer, numer_slabs, numer_slab_stride, numer_scale,
+                               numer_base, numer_out, gram_parts, gram_parts_n, gram_out,
+                               gram_parts_out) if fused else (1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0)
     # matrix-core variant (csrc/kernels/solve_mfma.hip): MU with K <= 16 whenever every
     # slice fits one 256-thread workgroup's register tiles; four of its workgroups are
     # co-resident per CU, so its cooperative budget is 4x the 1024-thread one
@@ -206,6 +235,13 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     if variant in ("auto", "mfma") and a == 0 and h.solve_mfma_max_cols(K) > 0 \
             and (_ENV["CNMF_SOLVE_MFMA"] or "1") != "0":
         S = _mfma_split(n, nblocks, K, nsplit, coop, x.device)
+    if fused and (S is None or nsplit > 1 or conv_mode != 1 or l1_num or l1_den or l2
+                  or gram_of is not None or h.solve_pipe_tiles(K, -(-n // S)) == 0
+                  or _ENV["CNMF_SOLVE_PIPE"] == "0"):
+        raise ValueError("solve: fused operands need the pipelined MU kernel (K <= 16, "
+                         "l1 = l2 = 0, conv_mode 1, cooperative slices that fit)")
+    if fused and gram_parts_out is not None and gram_parts_out.shape[1] < S:
+        raise ValueError(f"gram_parts_out: {gram_parts_out.shape[1]} slots < {S} slices")
     if S is not None:
         vcode = 5 if _ENV["CNMF_SOLVE_PIPE"] == "0" else 3
     elif gram is None:      # a VALU kernel: form the Gram first
@@ -229,17 +265,22 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     if S > 1:
         epochs = (max_iter // max(1, check_every) + 3) if conv_mode == 1 else (max_iter + 2)
         ws = _coop_workspace(x.device, _stream_ptr(x), R, epochs, S)
-        if torch.cuda.is_current_stream_capturing():
+        if coop_device_gen:
+            gen = 0                         # unused: the kernel reads ws["gen_dev"]
+        elif torch.cuda.is_current_stream_capturing():
             # a graph replays fixed arguments: zero this launch's granules in the graph
             # and tag them with a generation eager launches never reach
             ws["slots"][: R * epochs * S * 2].zero_()
             gen = 0xFFFFFFFF
         else:
-            ws["gen"] += 1                  # tags this launch's arrivals: no zeroing
+            ws["gen"] = ws["gen"] % 0x7FFFFFFE + 1   # tags this launch's arrivals (< 2^31)
             gen = ws["gen"]
         ws_slots, ws_count, ws_flag = ws["slots"].data_ptr(), 0, ws["flag"].data_ptr()
+        gen_dev = (ws["gen_dev"].data_ptr(), ws["arrive"].data_ptr()) if coop_device_gen \
+            else (0, 0)
     else:
         gen = 0
+        gen_dev = (0, 0)
     pl_ptr = pl_rs = pl_ld = pl_plane = pl_cols = 0
     if planes is not None:
         if (planes.dtype != torch.int16 or planes.dim() != 3 or planes.shape[0] != 3
@@ -253,7 +294,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
         pl_ptr, pl_ld, pl_plane = planes.data_ptr(), planes.stride(1), planes.stride(0)
         pl_rs, pl_cols = K * pl_ld, planes.shape[2]
     gs_ptr = gs_rs = gs_ld = gs_cols = 0
-    if gram is None:
+    if gram is None and gram_of is not None:
         gs_ptr, gs_rs, gs_ld, gs_cols = (gram_of.data_ptr(), gram_of.stride(0),
                                          gram_of.stride(1), gram_of.shape[2])
     h.solve(a, K, x.data_ptr(), x.stride(0), x.stride(1), numer.data_ptr(), numer.stride(0),
@@ -268,7 +309,54 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             int(gen), int(epochs), ws_flag, pl_ptr, int(pl_rs), int(pl_ld), int(pl_plane),
             planes_colmul.data_ptr() if (planes is not None and planes_colmul is not None) else 0,
             int(pl_cols), int(planes_n), gs_ptr, int(gs_rs), int(gs_ld), int(gs_cols),
-            _stream_ptr(x))
+            *f_args, *gen_dev, _stream_ptr(x))
+    return int(S)
+
+
+def _fused_solve_args(R, K, n, x, numer, nslabs, nstride, nscale, nbase, nout, gparts,
+                      gparts_n, gout, gparts_out):
+    """Validated raw arguments of the fused solve operands (see solve)."""
+    if nslabs < 1 or (nslabs > 1 and nstride < 1):
+        raise ValueError("numer_slabs >= 1 with a positive slab stride")
+    if nslabs > 1:
+        need = numer.storage_offset() + (nslabs - 1) * nstride + numer.stride(0) * (R - 1) + \
+            numer.stride(1) * (K - 1) + n
+        if need > numer.untyped_storage().nbytes() // 4:
+            raise ValueError("numer slabs extend beyond numer's storage")
+    if nscale is not None and (nscale.dtype != torch.float32 or nscale.numel() < n
+                               or not nscale.is_contiguous()):
+        raise ValueError("numer_scale: contiguous float32 with >= n entries")
+    nb_rs = ldnb = 0
+    for name, t in (("numer_base", nbase), ("numer_out", nout)):
+        if t is not None:
+            _check_block_view(name, t, R, K, n)
+    if nbase is not None and nout is not None and nbase.stride()[:2] != nout.stride()[:2]:
+        raise ValueError("numer_base and numer_out need the same strides")
+    ref = nbase if nbase is not None else nout
+    if ref is not None:
+        nb_rs, ldnb = ref.stride(0), ref.stride(1)
+    gp_rs = gp_out_rs = 0
+    if gparts is not None:
+        if (gparts.dim() != 4 or gparts.shape[0] < R or gparts.shape[2:] != (K, K)
+                or gparts.dtype != torch.float32 or gparts.stride(3) != 1 or gparts.stride(2) != K
+                or gparts.stride(1) != K * K or not 1 <= gparts_n <= gparts.shape[1]):
+            raise ValueError("gram_parts: float32 (R, S, K, K) with K x K blocks contiguous")
+        gp_rs = gparts.stride(0)
+    if gparts_out is not None:
+        if (gparts_out.dim() != 4 or gparts_out.shape[0] < R or gparts_out.shape[2:] != (K, K)
+                or gparts_out.dtype != torch.float32 or gparts_out.stride(3) != 1
+                or gparts_out.stride(2) != K or gparts_out.stride(1) != K * K):
+            raise ValueError("gram_parts_out: float32 (R, S, K, K), K x K blocks contiguous")
+        gp_out_rs = gparts_out.stride(0)
+    if gout is not None and (gout.shape != (R, K, K) or not gout.is_contiguous()
+                             or gout.dtype != torch.float32):
+        raise ValueError("gram_out: contiguous float32 (R, K, K)")
+
+    def ptr(t):
+        return t.data_ptr() if t is not None else 0
+    return (int(nslabs), int(nstride), ptr(nscale), ptr(nbase), ptr(nout), int(nb_rs), int(ldnb),
+            ptr(gparts), int(gparts_n if gparts is not None else 0), int(gp_rs), ptr(gout),
+            ptr(gparts_out), int(gp_out_rs))
 
 
 # Cooperative-split bookkeeping.  A launch of S*nblocks 1024-thread workgroups is only safe
@@ -277,6 +365,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
 _COOP_WS: dict = {}
 _COOP_RESIDENT: dict = {}
 COOP_COLS_PER_WG = 1024
+kCoopMaxSlices = 32          # solve_core.h: cooperative slices per replicate
 _TLS = threading.local()
 
 
@@ -353,9 +442,13 @@ def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int)
     need_slots = R * epochs * S * 2
     if ws is None or ws["slots"].numel() < need_slots:
         flag = ws["flag"] if ws is not None else torch.zeros(1, dtype=torch.int32, device=dev)
+        # device-side generation (solve_pipe.hip): tags from 2^31 up, never a host tag
+        gen_dev = ws["gen_dev"] if ws is not None else \
+            torch.full((1,), -(1 << 31), dtype=torch.int32, device=dev)
+        arrive = ws["arrive"] if ws is not None else torch.zeros(1, dtype=torch.int32, device=dev)
         ws = {"slots": torch.zeros(max(need_slots, 1 << 16), dtype=torch.int64, device=dev),
               "gen": ws["gen"] if ws is not None else 0,
-              "flag": flag}
+              "flag": flag, "gen_dev": gen_dev, "arrive": arrive}
         _COOP_WS[key] = ws
     return ws
 
@@ -1193,15 +1286,25 @@ def split_planes(S: torch.Tensor, out: torch.Tensor, col_mul: torch.Tensor | Non
                       out.stride(0), P_, _stream_ptr(S))
 
 
-def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: int, Kd: int,
-                accumulate: bool = False, col_scale: torch.Tensor | None = None) -> None:
+def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int, N: int,
+                Kd: int, accumulate: bool = False, col_scale: torch.Tensor | None = None,
+                raw_slab: torch.Tensor | None = None, raw_max: int = 1 << 30) -> int:
     """C[:M, :N] (+)= col_scale * sum_{i + j <= 2} A[i][:M, :Kd] . B[j][:N, :Kd]^T on the bf16
     matrix cores (gemm_planes.hip): the fp32-accurate product of the fp32 matrices whose
     exact bf16 splits are A (3 planes; or its first 2, see gemm_a_planes) and B (1-3
     planes; 1 or 2 when B holds integers).
     A/B: int16 (P, rows, ld) views with unit k stride (row offsets / k offsets are just
     views); k must be zero-padded in A up to ``Kd`` (a multiple of 32; of planes_bk for
-    the deep k-step)."""
+    the deep k-step).
+
+    ``raw_slab`` (float32, >= ksplit * M * N elements; ``C`` unused, may be None): the raw
+    split-K partial products go to ``raw_slab`` as [ksplit][M][N] WITHOUT the reduction
+    pass, col_scale or accumulation -- the consuming solve sums them in slice order
+    (ops.solve ``numer_slabs``), bitwise the same as the reduction.  When the plan splits
+    k more than ``raw_max`` ways, the product is reduced here instead (into the first
+    M x N floats of ``raw_slab``): a consumer reading that many slabs per element costs
+    more than the reduction pass.  Returns the number of slabs in ``raw_slab`` (raw
+    mode; 1 otherwise)."""
     pa, a_rows, _ = A.shape
     pb, b_rows, _ = B.shape
     for name, t in (("A", A), ("B", B)):
@@ -1213,6 +1316,11 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
             raise ValueError(f"{name}: k extent {t.shape[2]} < Kd {Kd}")
     if not 2 <= pa <= 3 or not 1 <= pb <= 3 or Kd % 32 or M > a_rows or N > b_rows:
         raise ValueError(f"gemm_planes: planes {pa}/{pb}, Kd {Kd}, M {M}/{a_rows}, N {N}/{b_rows}")
+    if raw_slab is not None:
+        if raw_slab.dtype != torch.float32 or not raw_slab.is_contiguous():
+            raise ValueError("raw_slab: contiguous float32 required")
+        if C is None:
+            C = raw_slab.view(-1)[:M * N].view(M, N)
     if C.dtype != torch.float32 or C.stride(1) != 1 or C.shape[0] < M or C.shape[1] < N:
         raise ValueError("C: float32 (>= M, >= N) with unit column stride required")
     if col_scale is not None and (col_scale.dtype != torch.float32 or col_scale.numel() < N
@@ -1220,6 +1328,9 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
         raise ValueError("col_scale: contiguous float32 with >= N entries")
     if not use_native(C):
         prod = reference.gemm_planes(A[:, :M, :Kd], B[:, :N, :Kd])
+        if raw_slab is not None:
+            raw_slab.view(-1)[:M * N].copy_(prod.to(torch.float32).reshape(-1))
+            return 1
         if col_scale is not None:
             prod = prod * col_scale[:N].double()
         if accumulate:
@@ -1229,7 +1340,14 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
         return
     variant, ksplit = gemm_plan(M, N, Kd, pb)
     slab = 0
-    if ksplit > 1:
+    if raw_slab is not None and ksplit > raw_max:
+        gemm_planes(C, A, B, M, N, Kd, accumulate=False, col_scale=None)
+        return 1
+    if raw_slab is not None:
+        if raw_slab.numel() < ksplit * M * N:
+            raise ValueError(f"raw_slab: {raw_slab.numel()} < ksplit {ksplit} x {M} x {N}")
+        slab = raw_slab.data_ptr()
+    elif ksplit > 1:
         key = (str(C.device), _stream_ptr(C))
         ws = _GEMM_SLAB.get(key)
         if ws is None or ws.numel() < ksplit * M * N:
@@ -1240,7 +1358,9 @@ def gemm_planes(C: torch.Tensor, A: torch.Tensor, B: torch.Tensor, M: int, N: in
                      B.stride(0), b_rows, C.data_ptr(), C.stride(0),
                      col_scale.data_ptr() if col_scale is not None else 0, int(M), int(N),
                      int(Kd), pa, pb, int(bool(accumulate)), int(variant), int(ksplit), slab,
-                     gemm_stages(variant), gemm_kstep(variant), _stream_ptr(C))
+                     gemm_stages(variant), gemm_kstep(variant), int(raw_slab is not None),
+                     _stream_ptr(C))
+    return ksplit if raw_slab is not None else 1
 
 
 def gemm_stages(variant: int) -> int:

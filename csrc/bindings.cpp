@@ -47,7 +47,10 @@ PYBIND11_MODULE(_hip, m) {
            int coop_epochs,
            uintptr_t coop_timeout, uintptr_t planes, long long pl_rs, long long pl_ld,
            long long pl_plane, uintptr_t pl_colmul, int pl_cols, int pl_n, uintptr_t gsrc,
-           long long gs_rs, long long gs_ld, int gs_cols, uintptr_t stream) {
+           long long gs_rs, long long gs_ld, int gs_cols, int nslab_n, long long nslab_stride,
+           uintptr_t n_scale, uintptr_t nbase, uintptr_t nout, long long nb_rs, long long ldnb,
+           uintptr_t gpart, int gpart_n, long long gpart_rs, uintptr_t gout, uintptr_t gp_out,
+           long long gp_rs, uintptr_t coop_gen_dev, uintptr_t coop_arrive, uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
                            max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
@@ -57,8 +60,11 @@ PYBIND11_MODULE(_hip, m) {
                            coop_epochs,
                            P<int>(coop_timeout), P<unsigned short>(planes), pl_rs, pl_ld,
                            pl_plane, P<const float>(pl_colmul), pl_cols, pl_n,
-                           P<const float>(gsrc), gs_rs, gs_ld, gs_cols,
-                           reinterpret_cast<hipStream_t>(stream)),
+                           P<const float>(gsrc), gs_rs, gs_ld, gs_cols, nslab_n, nslab_stride,
+                           P<const float>(n_scale), P<const float>(nbase), P<float>(nout), nb_rs,
+                           ldnb, P<const float>(gpart), gpart_n, gpart_rs, P<float>(gout),
+                           P<float>(gp_out), gp_rs, P<unsigned>(coop_gen_dev),
+                           P<unsigned>(coop_arrive), reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");
         });
 
@@ -289,11 +295,12 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t A, long long lda, long long a_plane, int a_rows, uintptr_t B,
            long long ldb, long long b_plane, int b_rows, uintptr_t C, long long ldc,
            uintptr_t col_scale, int M, int N, int Kd, int pa, int pb, int accumulate,
-           int variant, int ksplit, uintptr_t slab, int stages, int kstep, uintptr_t stream) {
+           int variant, int ksplit, uintptr_t slab, int stages, int kstep, int raw,
+           uintptr_t stream) {
           check(cnmf_gemm_planes(P<const unsigned short>(A), lda, a_plane, a_rows,
                                  P<const unsigned short>(B), ldb, b_plane, b_rows, P<float>(C),
                                  ldc, P<const float>(col_scale), M, N, Kd, pa, pb, accumulate,
-                                 variant, ksplit, P<float>(slab), stages, kstep,
+                                 variant, ksplit, P<float>(slab), stages, kstep, raw,
                                  reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_gemm_planes");
         });

@@ -328,7 +328,9 @@ bool npy_f4_2d(const uint8_t* p, size_t n, long long& K, long long& G, size_t& h
   long long a = -1, b = -1;
   if (std::sscanf(h.c_str() + sp + 10, "%lld, %lld)", &a, &b) != 2 || a < 1 || b < 1) return false;
   hdr = start + hl;
-  if (hdr + (size_t)(a * b) * 4 > n) return false;
+  // a * b * 4 must not wrap: reject shapes beyond the payload before multiplying
+  if ((unsigned long long)a > (n / 4) || (unsigned long long)b > (n / 4) / (size_t)a) return false;
+  if (hdr + (size_t)a * (size_t)b * 4 > n) return false;
   K = a;
   G = b;
   return true;
@@ -345,18 +347,28 @@ void parse_npz(const std::string& path, NpzFile& f) {
   if (eocd == std::string::npos) { f.err = "no end of central directory: " + path; return; }
   const uint32_t entries = get16(b + eocd + 10);
   size_t cd = get32(b + eocd + 16);
+  // every offset below is size_t arithmetic on values read from the file, checked
+  // against the buffer before it is dereferenced (a truncated or malformed file is
+  // reported as unsupported and handed to the numpy path, never read out of bounds)
   for (uint32_t e = 0; e < entries; ++e) {
-    if (cd + 46 > n || get32(b + cd) != 0x02014B50) { f.err = "bad central record: " + path; return; }
-    const uint32_t method = get16(b + cd + 10), csize = get32(b + cd + 20);
-    const uint32_t nl = get16(b + cd + 28), xl = get16(b + cd + 30), cl = get16(b + cd + 32);
-    const uint32_t lo = get32(b + cd + 42);
+    if (cd > n || n - cd < 46 || get32(b + cd) != 0x02014B50) {
+      f.err = "bad central record: " + path;
+      return;
+    }
+    const size_t method = get16(b + cd + 10), csize = get32(b + cd + 20);
+    const size_t nl = get16(b + cd + 28), xl = get16(b + cd + 30), cl = get16(b + cd + 32);
+    const size_t lo = get32(b + cd + 42);
+    if (n - cd - 46 < nl + xl + cl) { f.err = "bad central record: " + path; return; }
     const std::string name((const char*)b + cd + 46, nl);
     cd += 46 + nl + xl + cl;
     if (name != "data.npy" && name != "columns.npy") continue;
     if (method != 0) { f.err = "compressed member: " + path; return; }
-    if (lo + 30 > n || get32(b + lo) != 0x04034B50) { f.err = "bad local header: " + path; return; }
-    const size_t pay = lo + 30 + get16(b + lo + 26) + get16(b + lo + 28);
-    if (pay + csize > n) { f.err = "truncated member: " + path; return; }
+    if (lo > n || n - lo < 30 || get32(b + lo) != 0x04034B50) {
+      f.err = "bad local header: " + path;
+      return;
+    }
+    const size_t pay = lo + 30 + (size_t)get16(b + lo + 26) + (size_t)get16(b + lo + 28);
+    if (pay > n || n - pay < csize) { f.err = "truncated member: " + path; return; }
     if (name == "columns.npy") {
       f.cols = b + pay;
       f.cols_n = csize;

@@ -52,6 +52,8 @@ struct PlaneGemmParams {
   int tiles_m, tiles_n;
   int ksplit;               // > 1: workgroup z-slice of k; raw partials to `slab`
   float* slab;              // [ksplit][M][N] partial products (split-K only)
+  int raw;                  // 1: raw partials to `slab` even at ksplit 1, and no reduce --
+                            // the consuming solve sums them (solve_pipe.hip numer slabs)
 };
 
 __device__ __forceinline__ unsigned short f2bf_rn(float f) {
@@ -204,7 +206,8 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
     }
   }
 
-  if (p.ksplit > 1) {   // raw partial tile -> slab ks (reduced in order by gemm_reduce)
+  if (p.ksplit > 1 || p.raw) {   // raw partial tile -> slab ks (reduced in slice order
+                                 // by gemm_reduce, or by the consumer when raw)
     float* sl = p.slab + (long long)ks * p.M * p.N;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
@@ -381,9 +384,10 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
                                        long long b_plane, int b_rows, float* C, long long ldc,
                                        const float* col_scale, int M, int N, int Kd, int pa,
                                        int pb, int accumulate, int variant, int ksplit,
-                                       float* slab, int stages, int kstep,
+                                       float* slab, int stages, int kstep, int raw,
                                        hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  if (raw && !slab) return hipErrorInvalidValue;
   const int bk = 32;   // smallest k-step depth: Kd must be a multiple of it
   if (pa < 2 || pa > 3 || pb < 1 || pb > 3 || Kd <= 0 || Kd % bk || lda % 8 || ldb % 8 ||
       a_plane % 8 || b_plane % 8 || a_rows < 1 || b_rows < 1 || variant < 0 || variant > 5 ||
@@ -395,7 +399,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   p.B = B; p.ldb = ldb; p.b_plane = b_plane; p.b_rows = b_rows;
   p.C = C; p.ldc = ldc; p.col_scale = col_scale;
   p.M = M; p.N = N; p.Kd = Kd; p.accumulate = accumulate;
-  p.ksplit = ksplit; p.slab = slab;
+  p.ksplit = ksplit; p.slab = slab; p.raw = raw ? 1 : 0;
   hipError_t e;
   switch (pa * 4 + pb) {
     case 9: e = cnmf::launch_variant<2, 1>(variant, p, stages, kstep, stream); break;
@@ -405,7 +409,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
     case 14: e = cnmf::launch_variant<3, 2>(variant, p, stages, kstep, stream); break;
     default: e = cnmf::launch_variant<3, 3>(variant, p, stages, kstep, stream); break;
   }
-  if (e != hipSuccess || ksplit == 1) return e;
+  if (e != hipSuccess || ksplit == 1 || raw) return e;
   const long long total = (long long)M * N;
   long long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;

@@ -18,7 +18,11 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       int* coop_timeout, unsigned short* planes, long long pl_rs,
                       long long pl_ld, long long pl_plane, const float* pl_colmul,
                       int pl_cols, int pl_n, const float* gsrc, long long gs_rs,
-                      long long gs_ld, int gs_cols, hipStream_t stream);
+                      long long gs_ld, int gs_cols, int nslab_n, long long nslab_stride,
+                      const float* n_scale, const float* nbase, float* nout, long long nb_rs,
+                      long long ldnb, const float* gpart, int gpart_n, long long gpart_rs,
+                      float* gout, float* gp_out, long long gp_rs, unsigned* coop_gen_dev,
+                      unsigned* coop_arrive, hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,
@@ -131,7 +135,7 @@ hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_
                             const unsigned short* B, long long ldb, long long b_plane, int b_rows,
                             float* C, long long ldc, const float* col_scale, int M, int N,
                             int Kd, int pa, int pb, int accumulate, int variant, int ksplit,
-                            float* slab, int stages, int kstep, hipStream_t stream);
+                            float* slab, int stages, int kstep, int raw, hipStream_t stream);
 hipError_t cnmf_split_planes(const float* S, long long lds, int rows, int cols, int cols_pad,
                              const float* col_mul, unsigned short* P, long long ldp,
                              long long plane, int nplanes, hipStream_t stream);

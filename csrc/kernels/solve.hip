@@ -37,7 +37,11 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  unsigned short* planes, long long pl_rs, long long pl_ld,
                                  long long pl_plane, const float* pl_colmul, int pl_cols,
                                  int pl_n, const float* gsrc, long long gs_rs, long long gs_ld,
-                                 int gs_cols, hipStream_t stream) {
+                                 int gs_cols, int nslab_n, long long nslab_stride, const float* n_scale, const float* nbase,
+                                 float* nout, long long nb_rs, long long ldnb, const float* gpart,
+                                 int gpart_n, long long gpart_rs, float* gout, float* gp_out,
+                                 long long gp_rs, unsigned* coop_gen_dev, unsigned* coop_arrive,
+                                 hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
   if ((long long)K * (ldx > ldn ? ldx : ldn) * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
@@ -63,6 +67,18 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.pl_colmul = pl_colmul; p.pl_cols = pl_cols;
   p.pl_n = pl_n < 1 ? 1 : (pl_n > 3 ? 3 : pl_n);
   p.gsrc = gsrc; p.gs_rs = gs_rs; p.gs_ld = gs_ld; p.gs_cols = gs_cols;
+  p.nslab_n = nslab_n < 1 ? 1 : nslab_n; p.nslab_stride = nslab_stride; p.n_scale = n_scale;
+  p.nbase = nbase; p.nout = nout; p.nb_rs = nb_rs; p.ldnb = ldnb;
+  p.gpart = gpart; p.gpart_n = gpart_n; p.gpart_rs = gpart_rs; p.gout = gout;
+  p.gp_out = gp_out; p.gp_rs = gp_rs;
+  p.coop_gen_dev = coop_split > 1 ? coop_gen_dev : nullptr;
+  p.coop_arrive = coop_arrive;
+  if (p.coop_gen_dev && !coop_arrive) return hipErrorInvalidValue;
+  const bool fused = p.nslab_n > 1 || n_scale || nbase || nout || gpart || gout || gp_out ||
+                     (coop_split > 1 && coop_gen_dev);
+  if (fused && (p.nslab_n > 1 && p.nslab_stride * 4 * (long long)p.nslab_n >= 0x7fffffffLL))
+    return hipErrorInvalidValue;
+  if (!gram && !gpart && !gsrc) return hipErrorInvalidValue;
   // the in-prologue Gram is a matrix-core kernel feature (K <= 16)
   if (gsrc && (variant != 3 || K > 16 || gs_cols < 1)) return hipErrorInvalidValue;
   if (planes && pl_cols < ncols) return hipErrorInvalidValue;
@@ -82,8 +98,11 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
     if (variant == 3 && Tp > 0 && conv_mode == 1 && nsplit <= 1 && !gsrc && l1_num == 0.f &&
         l1_den == 0.f && l2 == 0.f)
       return cnmf::launch_solve_pipe(K, p, nblocks, Tp, p.pl_n, stream);
+    // the fused operands exist only in the pipelined kernel: never drop them silently
+    if (fused || (!gram && !gsrc)) return hipErrorInvalidValue;
     return cnmf::launch_solve_mfma(K, p, nblocks, T < 1 ? 1 : T, stream);
   }
+  if (fused || !gram) return hipErrorInvalidValue;
   if (K > 32) return cnmf::launch_solve_wide(K, algo, p, nblocks, threads, stream);
   // variant: 0 auto, 1 streaming, 2 register-resident (3 = mfma above).  Resident needs every slice to
   // fit U <= res_max_cols(K) columns per thread of a <= 1024-thread workgroup; it runs

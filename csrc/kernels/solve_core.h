@@ -142,8 +142,14 @@ __device__ __forceinline__ void load_group(ColGroup<K, U>& cg, int j, int T, int
 // iterating, so slices that diverged never wait for each other again.
 typedef __attribute__((address_space(1))) unsigned long long gran_t;
 
+__device__ __forceinline__ bool coop_sum2_tag(const SolveParams& p, unsigned gen, int rep,
+                                              int e, float& a, float& b, float* sred);
 __device__ __forceinline__ bool coop_sum2(const SolveParams& p, int rep, int e, float& a,
                                           float& b, float* sred) {
+  return coop_sum2_tag(p, p.coop_gen, rep, e, a, b, sred);
+}
+__device__ __forceinline__ bool coop_sum2_tag(const SolveParams& p, unsigned gen, int rep,
+                                              int e, float& a, float& b, float* sred) {
   const int S = gridDim.y;
   const int slice = blockIdx.y;
   if (S <= 1) return true;
@@ -152,7 +158,7 @@ __device__ __forceinline__ bool coop_sum2(const SolveParams& p, int rep, int e, 
     return false;
   }
   gran_t* g = (gran_t*)(p.coop_slots + (((long long)rep * p.coop_epochs + e) * S) * 2);
-  const unsigned long long tag = (unsigned long long)p.coop_gen << 32;
+  const unsigned long long tag = (unsigned long long)gen << 32;
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     if (lane == 0) {

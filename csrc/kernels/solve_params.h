@@ -39,6 +39,34 @@ struct SolveParams {
   const float* pl_colmul;
   int pl_cols;
   int pl_n;                 // planes written (1..3): the consuming GEMM reads only its A planes
+  // Fused operands (solve_pipe.hip only; all off by default).  They let one online step
+  // run GEMM -> solve -> GEMM -> solve with no reduction or Gram launches in between:
+  //  * numerator = nbase + n_scale[col] * sum_{q < nslab_n} numer[q * nslab_stride + ..]
+  //    (the raw split-K slabs of gemm_planes(raw_slab=...), summed in slice order as
+  //    gemm_reduce_kernel does), optionally written back to nout (the accumulated B);
+  //  * Gram = gram (optional base) + sum_{q < gpart_n} gpart[rep * gpart_rs + q * K * K]
+  //    (partial Grams of the producing solve's slices), written by slice 0 to gout;
+  //  * gp_out: this slice's partial Gram sum_cols x x^T of the FINAL x, at
+  //    gp_out[rep * gp_rs + slice * K * K] -- the next solve's gpart.
+  int nslab_n;
+  long long nslab_stride;
+  const float* n_scale;
+  const float* nbase;
+  float* nout;
+  long long nb_rs, ldnb;
+  const float* gpart;
+  int gpart_n;
+  long long gpart_rs;
+  float* gout;
+  float* gp_out;
+  long long gp_rs;
+  // Device-side launch generation for the cooperative granules (solve_pipe.hip): the
+  // tag is read from *coop_gen_dev at kernel start instead of the host's coop_gen, and
+  // the last workgroup to finish (arrival counter coop_arrive) advances it.  A launch
+  // captured in a HIP graph then tags every replay differently without re-zeroing the
+  // granules (tags in [2^31, 2^32 - 1); host tags stay below 2^31).
+  unsigned* coop_gen_dev;
+  unsigned* coop_arrive;
   // Optional (matrix-core kernel only): the system matrix is the Gram F F^T of the factor
   // F_r = gsrc + r*gs_rs (K x gs_cols, row stride gs_ld), formed in the prologue on the
   // matrix cores instead of being read from `gram` (W W^T fused into

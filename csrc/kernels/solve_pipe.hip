@@ -44,6 +44,25 @@ __device__ __forceinline__ f32x4p pipe_chain(const float (&a)[KS], const float (
   return d;
 }
 
+// Launch-completion bookkeeping of the device-side generation (SolveParams.coop_gen_dev):
+// every workgroup arrives once; the last one resets the counter and advances the tag
+// (kernels on one stream never overlap, so the next launch reads the new value).
+__device__ __forceinline__ void pipe_arrive(const SolveParams& p) {
+  if (!p.coop_gen_dev) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned total = gridDim.x * gridDim.y;
+    const unsigned old = atomicAdd(p.coop_arrive, 1u);
+    if (old + 1 == total) {
+      atomicExch(p.coop_arrive, 0u);
+      const unsigned g = __hip_atomic_load(p.coop_gen_dev, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.coop_gen_dev, g >= 0xFFFFFFFEu ? 0x80000000u : g + 1u,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 __device__ __forceinline__ unsigned short pipe_bf16_rn(float f) {
   unsigned u = __float_as_uint(f);
   u += 0x7FFFu + ((u >> 16) & 1u);
@@ -57,12 +76,21 @@ __global__ __launch_bounds__(64 * kPipeWaves) __attribute__((amdgpu_waves_per_eu
 void solve_pipe_kernel(SolveParams p, int pl_n) {
   constexpr int KS = (K + 3) / 4;
   __shared__ float sred[3 + 2 * kCoopMaxSlices];
-  __shared__ float sN[T * KS * 64 * kPipeWaves];
+  // numerators of this lane's columns; also the partial-Gram scratch of the epilogue
+  // (one 16 x 16 tile per wave), hence at least 4 x 256 floats
+  __shared__ float sN[(T * KS >= 4 ? T * KS : 4) * 64 * kPipeWaves];
   const int rep = p.rep_index ? p.rep_index[blockIdx.x] : (int)blockIdx.x;
-  if (p.active && p.active[rep] == 0) return;   // converged replicate: untouched (uniform)
+  if (p.active && p.active[rep] == 0) {   // converged replicate: untouched (uniform)
+    pipe_arrive(p);
+    return;
+  }
+  // cooperative tag: the host's generation, or the device-side one (graph replays)
+  const unsigned gen = p.coop_gen_dev ? __hip_atomic_load(p.coop_gen_dev, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : p.coop_gen;
   float* __restrict__ x = p.x + (long long)rep * p.x_rs;
   const float* __restrict__ nu = p.numer + (long long)rep * p.n_rs;
-  const float* __restrict__ gm = p.gram + (long long)rep * p.g_rs;
+  const float* __restrict__ gm = p.gram ? p.gram + (long long)rep * p.g_rs : nullptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
 
@@ -74,7 +102,32 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int k = 4 * s + g;
-    a[s] = (pm < K && k < K) ? gm[pm * K + k] : 0.f;
+    a[s] = (gm && pm < K && k < K) ? gm[pm * K + k] : 0.f;
+  }
+  if (p.gpart) {
+    // + the producing solve's per-slice partial Grams, summed in slice order; eight
+    // slices' loads in flight per round (a sequential load-add chain per element cost
+    // ~gpart_n memory latencies)
+    const float* gp = p.gpart + (long long)rep * p.gpart_rs + pm * K;
+    float t[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) t[s] = 0.f;
+    for (int q0 = 0; q0 < p.gpart_n; q0 += 8) {
+      float v[8][KS];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int k = 4 * s + g;
+          v[j][s] = (q0 + j < p.gpart_n && pm < K && k < K) ? gp[(q0 + j) * K * K + k] : 0.f;
+        }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) t[s] += v[j][s];   // + 0 for q >= gpart_n: exact
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) a[s] = gm ? a[s] + t[s] : t[s];
   }
 
   int j0 = 0, n = p.ncols;
@@ -92,6 +145,11 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
   {
     int col0 = j0 + 16 * wave + c;
     asm volatile("" : "+v"(col0));
+    const int nsl = p.nslab_n > 1 ? p.nslab_n : 1;
+    const unsigned sstride = (unsigned)(p.nslab_stride * 4);   // host: < 2^31 bytes
+    float* __restrict__ nb_out = p.nout ? p.nout + (long long)rep * p.nb_rs : nullptr;
+    const float* __restrict__ nb_in = p.nbase ? p.nbase + (long long)rep * p.nb_rs : nullptr;
+    const int sb = (int)p.ldnb;
 #pragma unroll
     for (int i = 0; i < T; ++i) {
       const int cl = col0 + 16 * kPipeWaves * i;
@@ -105,6 +163,50 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
         xr[i][s] = v ? xv : 0.f;
         CNMF_PIPE_N(i, s) = v ? nv : 0.f;
       }
+    }
+    if (nsl > 1 || p.n_scale || nb_in || nb_out) {
+      // raw split-K slabs summed in slice order, then scaled and added to the base:
+      // bitwise gemm_reduce_kernel's "C (+)= col_scale * sum_s slab[s]".  Slab-outer
+      // rounds: every element's load of slab q is in flight at once, the running sum
+      // stays in the lane's own LDS slot
+      for (int q = 1; q < nsl; ++q) {
+#pragma unroll
+        for (int i = 0; i < T; ++i) {
+          const int cl = col0 + 16 * kPipeWaves * i;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const int kk = 4 * s + g;
+            const bool v = cl < n && kk < K;
+            const float t = buf_ld(rn, v ? (kk * sn + cl) * 4 : 0, q * sstride);
+            if (v) CNMF_PIPE_N(i, s) += t;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < T; ++i) {
+        const int cl = col0 + 16 * kPipeWaves * i;
+        const bool ok = cl < n;
+        const float scl = (ok && p.n_scale) ? p.n_scale[cl] : 1.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const int kk = 4 * s + g;
+          if (!(ok && kk < K)) continue;
+          float nv = CNMF_PIPE_N(i, s);
+          if (p.n_scale) nv *= scl;
+          if (nb_in) nv = nb_in[(long long)kk * sb + cl] + nv;
+          if (nb_out) nb_out[(long long)kk * sb + cl] = nv;
+          CNMF_PIPE_N(i, s) = nv;
+        }
+      }
+    }
+  }
+  // the summed Gram for the next solve that accumulates on it (slice 0 writes; every
+  // slice summed the same values in the same order)
+  if (p.gout && blockIdx.y == 0 && pm < K) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 4 * s + g;
+      if (k < K && wave == 0) p.gout[(long long)rep * p.g_rs + pm * K + k] = a[s];
     }
   }
 
@@ -141,7 +243,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       float f = q - 2.f * l;
       if (coop) {
         float unused = 0.f;
-        if (!coop_sum2(p, rep, epoch++, f, unused, sred)) break;
+        if (!coop_sum2_tag(p, gen, rep, epoch++, f, unused, sred)) break;
       }
       if (have_prev && fabsf(f_prev - f) <= p.tol * fabsf(f_prev)) break;
       f_prev = f;
@@ -227,13 +329,52 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       }
     }
     block_sum2(lin, quad, sred);
-    if (coop) (void)coop_sum2(p, rep, epoch++, lin, quad, sred);
+    if (coop) (void)coop_sum2_tag(p, gen, rep, epoch++, lin, quad, sred);
     if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
       if (p.lin_out) p.lin_out[rep] = lin;
       if (p.quad_out) p.quad_out[rep] = quad;
     }
   }
+  if (p.gp_out) {
+    // this slice's partial Gram sum_cols x x^T of the final x (the next solve's gpart):
+    // each wave transposes its tiles through LDS into [column][component] and runs
+    // gram.hip's trick -- lane (g, c) feeds F[c][col 4j + g] as both A[m = c][k = g] and
+    // B[k = g][n = c], so D[m][n] = sum over the 16 columns of F[m][col] F[n][col]
+    __syncthreads();                       // every wave is done with the numerators
+    float* sT = sN + wave * 256;
+    for (int e = lane; e < 256; e += 64) sT[e] = 0.f;   // components >= 4 KS stay zero
+    __builtin_amdgcn_wave_barrier();
+    f32x4p gacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) sT[c * 16 + 4 * s + g] = xr[i][s];
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the tile is in LDS
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = sT[(4 * j + g) * 16 + c];
+        gacc = __builtin_amdgcn_mfma_f32_16x16x4f32(v, v, gacc, 0, 0, 0);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();       // reads done before the next tile's writes
+    }
+    __syncthreads();
+    // lane (g, c) holds D[4 g + r][c]; the 4 wave partials summed in wave order
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sN[wave * 256 + (4 * g + r) * 16 + c] = gacc[r];
+    __syncthreads();
+    float* go = p.gp_out + (long long)rep * p.gp_rs + (long long)blockIdx.y * K * K;
+    for (int e = threadIdx.x; e < K * K; e += 64 * kPipeWaves) {
+      const int m = e / K, q = e - m * K;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < kPipeWaves; ++w) v += sN[w * 256 + m * 16 + q];
+      go[e] = v;
+    }
+  }
   if (p.iters_out && threadIdx.x == 0 && blockIdx.y == 0) p.iters_out[rep] += it;
+  pipe_arrive(p);
 }
 
 // tile counts instantiated per K (the host rounds up to the next one)

@@ -1287,3 +1287,109 @@ def test_solve_pipe_bitwise_equals_mfma_kernel(monkeypatch, K, n, coop):
                     None, None, None, 1, 1, 4)
     for r in (0, 3, 5):
         assert ((xp[r].double() - xr[r]).norm() / xr[r].norm()) < 1e-2
+
+
+@pytest.mark.parametrize("ks", [[10], [5, 7, 13]])
+def test_fused_online_step_matches_unfused(monkeypatch, ks):
+    """The fused online step (raw split-K slabs summed by the pipelined solves, Grams
+    handed between the solves as per-slice partials -- no gemm_reduce / gram launches)
+    factorises like the unfused step: same pass counts (+-1), errors to 1e-5, spectra to
+    fp32 rounding of a converged iteration."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(6000, 700, n_programs=8, seed=5)).cuda()
+    seeds = list(range(101, 101 + 12 * len(ks)))
+    kk = [k for k in ks for _ in range(12)]
+    opts = dict(n_components=ks[0], online_chunk_size=2000, online_chunk_max_iter=1000)
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CNMF_FUSED_STEP", fused)
+        solver = NMFBatchSolver(X, NMFOptions(**opts))
+        if fused == "1":
+            from cnmf_torch_amd.models.nmf import _Batch
+            st = _Batch(torch.zeros((sum(kk), 6000), device="cuda"),
+                        torch.zeros((sum(kk), 700), device="cuda"), sorted(kk))
+            assert solver._fused_ok(st, solver._steps(6000))
+        out[fused] = solver.run(seeds, ks=kk)
+    a, b = out["1"], out["0"]
+    assert np.abs(a.n_iter - b.n_iter).max() <= 1
+    same = a.n_iter == b.n_iter
+    assert same.mean() > 0.8
+    np.testing.assert_allclose(a.err[same], b.err[same], rtol=1e-5)
+    for r in np.flatnonzero(same):
+        wa, wb = a.spectra(r).cpu(), b.spectra(r).cpu()
+        assert float((wa - wb).norm() / wb.norm()) < 1e-3
+
+
+def test_fused_graph_replay_across_runs_is_bitwise_eager(monkeypatch):
+    """Fused online passes replayed from the per-layout HIP graphs (captured once, kept
+    across runs in the solver's arena) give bit-identical factorisations to the eager
+    fused passes, run after run (the second and third runs replay graphs captured in
+    the first), and the arena keeps the same buffers."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(5000, 600, n_programs=6, seed=8)).cuda()
+    opts = NMFOptions(n_components=6, online_chunk_size=2000, online_chunk_max_iter=1000)
+    batches = [list(range(1 + 40 * i, 41 + 40 * i)) for i in range(3)]
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("CNMF_GRAPHS", mode)
+        solver = NMFBatchSolver(X, opts)
+        res[mode] = [solver.run(b) for b in batches]
+        if mode == "1":
+            arenas = list(solver._arenas.values())
+            assert len(arenas) == 1
+            slots = arenas[0]["slots"]
+            assert any(sl["graph"] is not None for sl in slots.values())
+            assert not any(sl["failed"] for sl in slots.values())
+    for a, b in zip(res["1"], res["0"]):
+        np.testing.assert_array_equal(a.n_iter, b.n_iter)
+        np.testing.assert_array_equal(a.err, b.err)
+        assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
+
+
+@pytest.mark.parametrize("coop_gen", [False, True])
+def test_solve_fused_operands_bitwise(coop_gen):
+    """Fused operands of the pipelined solve: numer = base + scale * (sum of raw split-K
+    slabs) and Gram = base + sum of partial Grams reproduce, bit for bit, the same solve
+    fed the explicitly reduced operands (summed in the same order); numer_out / gram_out
+    receive those sums; gram_parts_out holds per-slice partial Grams of the final x."""
+    R, K, n, ns, npart = 5, 10, 3000, 3, 7
+    x0, numer, gram = _problem(R, K, n, seed=77)
+    g = torch.Generator().manual_seed(5)
+    dev = torch.device("cuda")
+    slabs = (torch.rand((ns, R, K, n), generator=g) * numer.unsqueeze(0) / ns).to(dev)
+    scale = (torch.rand(n, generator=g) + 0.5).to(dev)
+    base = (torch.rand((R, K, n), generator=g) * numer.mean()).to(dev)
+    parts = (torch.rand((R, npart, K, K), generator=g) * gram.unsqueeze(1) / npart).to(dev)
+    gbase = (gram * 0.1).to(dev)
+    nref = slabs[0].clone()
+    for q in range(1, ns):
+        nref = nref + slabs[q]
+    nref = base + nref * scale
+    t = parts[:, 0].clone()
+    for q in range(1, npart):
+        t = t + parts[:, q]
+    gref = gbase + t
+    kw = dict(max_iter=300, tol=1e-4, conv_mode=1, check_every=5)
+    x1 = x0.clone().to(dev)
+    S1 = ops.solve("mu", x1, nref, gref, **kw)
+    x2 = x0.clone().to(dev)
+    nout = torch.zeros_like(nref)
+    gout = torch.zeros_like(gref)
+    gp_out = torch.full((R, 32, K, K), float("nan"), device=dev)
+    flat = slabs.reshape(-1)
+    S2 = ops.solve("mu", x2, flat[:R * K * n].view(R, K, n), gbase, numer_slabs=ns,
+                   numer_slab_stride=R * K * n, numer_scale=scale, numer_base=base,
+                   numer_out=nout, gram_parts=parts, gram_parts_n=npart, gram_out=gout,
+                   gram_parts_out=gp_out, coop_device_gen=coop_gen, **kw)
+    ops.coop_check(dev)
+    assert S1 == S2 and S2 > 1
+    assert torch.equal(x1, x2)
+    assert torch.equal(nout, nref) and torch.equal(gout, gref)
+    full = torch.bmm(x2.double(), x2.double().transpose(1, 2))
+    got = gp_out[:, :S2].double().sum(dim=1)
+    torch.testing.assert_close(got, full, rtol=1e-5, atol=1e-6)
+    assert torch.isnan(gp_out[:, S2:]).all()

@@ -86,3 +86,26 @@ def test_norm_counts_semantics(tmp_path):
     st = load_df_from_npz(obj.paths["tpm_stats"])
     np.testing.assert_allclose(st["__mean"].values, tpm.mean(axis=0), rtol=1e-5)
     np.testing.assert_allclose(st["__std"].values, tpm.std(axis=0, ddof=0), rtol=1e-4)
+
+
+def test_sparse_mean_var_matches_sklearn_bitwise():
+    """models.hvg.sparse_mean_var (no sklearn import on the prepare path) == the
+    StandardScaler(with_mean=False) statistics cnmf.py:128-131 computes, bit for bit,
+    for float32 / float64 / int64 CSR inputs, incl. a fully dense and an empty column."""
+    import scipy.sparse as sp
+    from sklearn.preprocessing import StandardScaler
+
+    from cnmf_torch_amd.models.hvg import sparse_mean_var
+
+    rng = np.random.default_rng(3)
+    for dt in (np.float32, np.float64, np.int64):
+        X = sp.random(2000, 300, density=0.1, random_state=2, format="lil")
+        X[:, 7] = 3
+        X[:, 11] = 0
+        X = sp.csr_matrix(X)
+        X.data = (rng.poisson(3, X.nnz) + 1) * (1.0 if dt == np.int64 else 1.37)
+        X = X.astype(dt)
+        m, v = sparse_mean_var(X)
+        sc = StandardScaler(with_mean=False).fit(X)
+        np.testing.assert_array_equal(m, sc.mean_)
+        np.testing.assert_array_equal(v, sc.var_)
