@@ -851,20 +851,23 @@ class cNMF:
     def consensus(self, k, density_threshold=0.5, local_neighborhood_size=0.30,
                   show_clustering=True, build_ref=True, skip_density_and_return_after_stats=False,
                   close_clustergram_fig=False, refit_usage=True, normalize_tpm_spectra=False,
-                  norm_counts=None, kmeans_backend="auto", device=None, comm=None):
+                  norm_counts=None, kmeans_backend="auto", device=None, comm=None,
+                  wait_figures=True):
         """Consensus spectra/usages for one K (cnmf.py:997-1256).  With a multi-rank
         ``comm`` the two all-gene passes -- the TPM spectra refit and the OLS gene scores
         over G_all -- are sharded over the ranks by gene blocks (the clustering is
-        replicated); rank 0 writes the artifacts."""
+        replicated); rank 0 writes the artifacts.  ``wait_figures=False`` (closed figures
+        only): return before the clustergram PNG is written; it finishes while the caller
+        goes on (utils.plotting.flush_figures, which the CLI calls before exiting)."""
         with self.timer(f"consensus_k{k}"):
             return self._consensus(k, density_threshold, local_neighborhood_size, show_clustering,
                                    build_ref, skip_density_and_return_after_stats,
                                    close_clustergram_fig, refit_usage, normalize_tpm_spectra,
-                                   norm_counts, kmeans_backend, device, comm)
+                                   norm_counts, kmeans_backend, device, comm, wait_figures)
 
     def _consensus(self, k, density_threshold, local_neighborhood_size, show_clustering,
                    build_ref, skip_stats, close_fig, refit_usage, normalize_tpm_spectra,
-                   norm_counts, kmeans_backend, device, comm=None):
+                   norm_counts, kmeans_backend, device, comm=None, wait_figures=True):
         tp = comm is not None and comm.world_size > 1
         writer = not tp or comm.rank == 0
         # a closed clustergram is drawn by a child process that imports matplotlib while
@@ -910,6 +913,23 @@ class cNMF:
                                    "increasing density threshold")
         labels = kmeans(L2, k, n_init=10, random_state=1, backend=kmeans_backend) + 1
         label_series = pd.Series(labels, index=names)
+        if plot_worker is not None:
+            # the clustergram needs only the clustering: hand it to the figure child now,
+            # so it renders while the refits / OLS / writes below run
+            if topics_dist is None:
+                topics_dist = pairwise_distances(L2)
+            else:
+                keep_t = torch.as_tensor(np.flatnonzero(density_filter), device=topics_dist.device)
+                topics_dist = topics_dist.index_select(0, keep_t).index_select(1, keep_t)
+            plot_worker.submit(
+                "clustergram", self.paths["clustering_plot"] % (k, dt_repl),
+                dist=topics_dist.cpu().numpy(), labels=label_series.values,
+                names=np.asarray(label_series.index).astype(str),
+                local_density=(local_dens.values.reshape(-1) if local_dens is not None
+                               else np.zeros(0)),
+                density_filter=(density_filter if density_filter is not None
+                                else np.zeros(0, dtype=bool)),
+                density_threshold=np.float64(density_threshold))
         median_np = cluster_medians(L2, labels, sorted(set(labels))).cpu().numpy()
         median_spectra = pd.DataFrame(median_np, index=sorted(set(labels)), columns=merged.columns)
 
@@ -999,7 +1019,7 @@ class cNMF:
         save_df_to_npz(usage_coef, p["gene_spectra_score"] % (k, dt_repl))
         save_df_to_text(usage_coef, p["gene_spectra_score__txt"] % (k, dt_repl))
 
-        if show_clustering:
+        if show_clustering and plot_worker is None:
             from .utils.plotting import clustergram
 
             if topics_dist is None:
@@ -1007,27 +1027,15 @@ class cNMF:
             else:
                 keep = torch.as_tensor(np.flatnonzero(density_filter), device=topics_dist.device)
                 topics_dist = topics_dist.index_select(0, keep).index_select(1, keep)
-            if plot_worker is not None:
-                plot_worker.submit(
-                    "clustergram", p["clustering_plot"] % (k, dt_repl),
-                    dist=topics_dist.cpu().numpy(), labels=label_series.values,
-                    names=np.asarray(label_series.index).astype(str),
-                    local_density=(local_dens.values.reshape(-1) if local_dens is not None
-                                   else np.zeros(0)),
-                    density_filter=(density_filter if density_filter is not None
-                                    else np.zeros(0, dtype=bool)),
-                    density_threshold=np.float64(density_threshold))
-            else:
-                clustergram(topics_dist.cpu().numpy(), label_series, local_dens, density_filter,
-                            density_threshold, p["clustering_plot"] % (k, dt_repl),
-                            close=close_fig)
+            clustergram(topics_dist.cpu().numpy(), label_series, local_dens, density_filter,
+                        density_threshold, p["clustering_plot"] % (k, dt_repl), close=close_fig)
         if build_ref:
             # the reference re-reads the TSV it just wrote (cnmf.py:1273); float64 text is
             # an exact round trip, so the in-memory frame gives the same reference
             mem = spectra_tpm if (spectra_tpm.dtypes == np.float64).all() else None
             self.build_reference(k, density_threshold, _spectra_tpm=mem)
         if plot_worker is not None:
-            plot_worker.wait()
+            plot_worker.wait(defer=not wait_figures)
 
     def _load_density_cache(self, cache: str, n_neighbors: int, names):
         """Density cache keyed on K AND the neighbourhood (SURVEY.md §5.2 fix): a cache
@@ -1098,7 +1106,7 @@ class cNMF:
         save_df_to_text(ref, self.paths["starcat_spectra__txt"] % (k, dt))
 
     def k_selection_plot(self, close_fig=False, kmeans_backend="auto", comm=None,
-                         device=None):
+                         device=None, wait_figures=True):
         """Stability (silhouette) and error per K (cnmf.py:1293-1332).
 
         With ``comm`` (one rank per GPU) the Ks are dealt round-robin over the ranks, each
@@ -1132,7 +1140,7 @@ class cNMF:
                                silhouette=stats["silhouette"].to_numpy(dtype=np.float64),
                                prediction_error=stats["prediction_error"].to_numpy(
                                    dtype=np.float64))
-            plot_worker.wait()
+            plot_worker.wait(defer=not wait_figures)
         else:
             from .utils.plotting import k_selection
 

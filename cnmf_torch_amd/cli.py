@@ -155,7 +155,7 @@ def main(argv=None) -> int:
                 obj.consensus(k, args.local_density_threshold, args.local_neighborhood_size,
                               args.show_clustering, args.build_reference,
                               close_clustergram_fig=True, kmeans_backend=args.kmeans_backend,
-                              device=args.device)
+                              device=args.device, wait_figures=False)
     elif args.command == "k_selection_plot":
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:
             from .parallel.runner import distributed_k_selection
@@ -163,7 +163,11 @@ def main(argv=None) -> int:
             distributed_k_selection(obj, kmeans_backend=args.kmeans_backend)
         else:
             obj.k_selection_plot(close_fig=True, kmeans_backend=args.kmeans_backend,
-                                 device=args.device)
+                                 device=args.device, wait_figures=False)
+    # every K's clustergram rendered while the next K computed: finish them before exit
+    from .utils.plotting import flush_figures
+
+    flush_figures()
     return 0
 
 

@@ -1264,6 +1264,10 @@ class NMFBatchSolver:
         if sl["graph"] is None:
             g = torch.cuda.CUDAGraph()
             main = torch.cuda.current_stream(self.X.device)
+            o = self.opts
+            ops.coop_reserve(self.X.device, sl["stream"].cuda_stream,
+                             max(gr.n for gr in st.groups), int(o.online_chunk_max_iter),
+                             int(o.inner_check_every))
             sl["stream"].wait_stream(main)
             try:
                 with torch.cuda.stream(sl["stream"]):

@@ -453,6 +453,16 @@ def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int)
     return ws
 
 
+def coop_reserve(dev: torch.device, stream: int, R: int, max_iter: int, check_every: int) -> None:
+    """Allocate the cooperative workspace of ``stream`` for up to R replicates x the
+    epochs of a ``max_iter`` / ``check_every`` solve x the maximum slice count, NOW --
+    before a HIP-graph capture on that stream, which would otherwise record the
+    workspace's zero-fill (and the reset of its device-side generation) into the graph
+    and replay it every time."""
+    epochs = max_iter // max(1, check_every) + 3
+    _coop_workspace(dev, stream, R, epochs, kCoopMaxSlices)
+
+
 def coop_check(device: torch.device | None = None) -> None:
     """Raise if any cooperative solve on ``device`` gave up waiting (non-resident
     workgroups) -- its results would be wrong.  Synchronises; call once per run."""

@@ -13,6 +13,8 @@
 
 #include <array>
 #include <atomic>
+#include <charconv>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -438,12 +440,134 @@ static unsigned crc32_bytes(py::bytes b) {
   return crc_tables().update(0, (const uint8_t*)s.data(), s.size());
 }
 
+// ------------------------------------------------------------------------ TSV writer
+// DataFrame.to_csv(sep="\t") of an all-float frame (cnmf.py:35-36 save_df_to_text), byte
+// for byte: every value in its shortest round-trip form -- Python's repr for float64
+// (scientific below a decimal exponent of -4 or from 16 on), numpy's str for float32
+// (scientific below 1e-4 or from 1e16 in magnitude) -- NaN as the empty string, integral
+// values with ".0".  Rows are formatted on native threads.
+namespace {
+
+void fmt_value(double v, bool f32, std::string& out) {
+  if (std::isnan(v)) return;
+  if (std::isinf(v)) {
+    out += v > 0 ? "inf" : "-inf";
+    return;
+  }
+  char buf[64];
+  std::to_chars_result r = f32 ? std::to_chars(buf, buf + 64, (float)v, std::chars_format::scientific)
+                               : std::to_chars(buf, buf + 64, v, std::chars_format::scientific);
+  const char* p = buf;
+  const char* end = r.ptr;
+  std::string neg;
+  if (*p == '-') {
+    neg = "-";
+    ++p;
+  }
+  std::string dig;
+  while (p < end && *p != 'e') {
+    if (*p != '.') dig += *p;
+    ++p;
+  }
+  int ex = 0;                                // "e-05" / "e+16": parse within [p, end)
+  if (p < end) {
+    const char* q = p + 1;
+    const bool eneg = q < end && *q == '-';
+    if (q < end && (*q == '-' || *q == '+')) ++q;
+    std::from_chars(q, end, ex);
+    if (eneg) ex = -ex;
+  }
+  const double a = std::fabs(v);
+  const bool sci = (a != 0.0) && (f32 ? (a < 1e-4 || a >= 1e16) : (ex < -4 || ex >= 16));
+  out += neg;
+  if (sci) {
+    out += dig[0];
+    if (dig.size() > 1) {
+      out += '.';
+      out.append(dig, 1, std::string::npos);
+    }
+    char eb[16];
+    std::snprintf(eb, sizeof eb, "e%c%02d", ex < 0 ? '-' : '+', ex < 0 ? -ex : ex);
+    out += eb;
+  } else if (ex >= 0) {
+    if ((int)dig.size() <= ex + 1) {
+      out += dig;
+      out.append(ex + 1 - dig.size(), '0');
+      out += ".0";
+    } else {
+      out.append(dig, 0, ex + 1);
+      out += '.';
+      out.append(dig, ex + 1, std::string::npos);
+    }
+  } else {
+    out += "0.";
+    out.append(-ex - 1, '0');
+    out += dig;
+  }
+}
+
+}  // namespace
+
+static void write_tsv(const std::string& path, const std::string& corner,
+                      const std::vector<std::string>& columns,
+                      const std::vector<std::string>& index, py::array data, int threads) {
+  const bool f32 = py::isinstance<py::array_t<float>>(data);
+  if (!f32 && !py::isinstance<py::array_t<double>>(data))
+    throw std::invalid_argument("write_tsv: float32 or float64 data");
+  if (data.ndim() != 2) throw std::invalid_argument("write_tsv: 2-D data");
+  const size_t n = data.shape(0), g = data.shape(1);
+  if (n != index.size() || g != columns.size())
+    throw std::invalid_argument("write_tsv: shape does not match index / columns");
+  py::array c = py::array::ensure(data, py::array::c_style);
+  const char* base = (const char*)c.data();
+  std::vector<std::string> rows(n);
+  std::atomic<size_t> next{0};
+  {
+    py::gil_scoped_release nogil;
+    auto work = [&]() {
+      for (size_t i; (i = next.fetch_add(64)) < n;) {
+        for (size_t r = i; r < std::min(n, i + 64); ++r) {
+          std::string& s = rows[r];
+          s.reserve(g * 12 + index[r].size() + 2);
+          s += index[r];
+          for (size_t j = 0; j < g; ++j) {
+            s += '\t';
+            const double v = f32 ? (double)((const float*)base)[r * g + j]
+                                 : ((const double*)base)[r * g + j];
+            fmt_value(v, f32, s);
+          }
+          s += '\n';
+        }
+      }
+    };
+    const int nt = std::max(1, std::min<int>(threads, (int)(n / 64) + 1));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw std::runtime_error("write_tsv: cannot open " + path);
+    std::string head = corner;
+    for (const auto& col : columns) {
+      head += '\t';
+      head += col;
+    }
+    head += '\n';
+    bool ok = std::fwrite(head.data(), 1, head.size(), f) == head.size();
+    for (const auto& s : rows) ok = ok && std::fwrite(s.data(), 1, s.size(), f) == s.size();
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) throw std::runtime_error("write_tsv: write failed: " + path);
+  }
+}
+
 PYBIND11_MODULE(_npzio, m) {
   m.doc() = "cnmf_torch_amd native replicate-file writer/reader (stored npz, crc32, sha256)";
   m.def("write_spectra_batch", &write_spectra_batch, py::arg("paths"), py::arg("data"),
         py::arg("offs"), py::arg("ks"), py::arg("columns_npy"), py::arg("index_npy"),
         py::arg("data_hdr"), py::arg("threads") = 16);
   m.def("read_spectra_batch", &read_spectra_batch, py::arg("paths"), py::arg("threads") = 16);
+  m.def("write_tsv", &write_tsv, py::arg("path"), py::arg("corner"), py::arg("columns"),
+        py::arg("index"), py::arg("data"), py::arg("threads") = 16);
   m.def("sha256_hex", &sha256_hex);
   m.def("crc32", &crc32_bytes);
 }

@@ -122,3 +122,39 @@ def test_native_spectra_batch_reader(tmp_path):
     # a deflated file (e.g. written by the original cnmf) -> declined
     cio.save_df_to_npz(pd.DataFrame(data[:5], columns=cols), paths[0], level=6)
     assert cio.read_spectra_batch(paths) is None
+
+
+def test_native_tsv_writer_is_byte_identical_to_pandas(tmp_path):
+    """save_df_to_text's native writer (npzio.cpp write_tsv) produces the same bytes as
+    DataFrame.to_csv(sep='\\t') -- float64 repr / float32 str rules, NaN as '', inf,
+    -0.0, integral values, every decade -- and leaves other frames to pandas."""
+    import numpy as np
+    import pandas as pd
+
+    from cnmf_torch_amd.utils import io as cio
+
+    rng = np.random.default_rng(1)
+    with np.errstate(over="ignore"):
+        mags = 10.0 ** rng.uniform(-320, 320, 7000)
+    vals = np.concatenate([mags * rng.choice([-1, 1], mags.size),
+                           rng.random(7000) * 10.0 ** rng.integers(-7, 18, 7000),
+                           [0.0, -0.0, np.nan, np.inf, -np.inf, 1e-4, 1e16, 1e-5, 3.0,
+                            0.0001, 12345678901234567.0, 5e-324, 123456789.125]])
+    vals = vals[: (vals.size // 8) * 8].reshape(-1, 8)
+    for dt in (np.float64, np.float32):
+        with np.errstate(over="ignore"):
+            df = pd.DataFrame(vals.astype(dt), index=[f"cell{i}" for i in range(len(vals))],
+                              columns=[f"g{j}" for j in range(8)])
+        for name in (None, "idx"):
+            df.index.name = name
+            assert cio._tsv_native_args(df) is not None
+            a, b = tmp_path / "a.txt", tmp_path / "b.txt"
+            cio.save_df_to_text(df, a)
+            df.to_csv(b, sep="\t")
+            assert a.read_bytes() == b.read_bytes()
+    mixed = pd.DataFrame({"a": [1, 2], "b": [0.5, 1.5]})
+    assert cio._tsv_native_args(mixed) is None
+    quoted = pd.DataFrame([[1.0]], index=['x"y'], columns=["c"])
+    assert cio._tsv_native_args(quoted) is None
+    cio.save_df_to_text(quoted, tmp_path / "q.txt")
+    assert (tmp_path / "q.txt").read_text() == quoted.to_csv(sep="\t")

@@ -1344,6 +1344,14 @@ def test_fused_graph_replay_across_runs_is_bitwise_eager(monkeypatch):
             slots = arenas[0]["slots"]
             assert any(sl["graph"] is not None for sl in slots.values())
             assert not any(sl["failed"] for sl in slots.values())
+            # replays tag their cooperative exchanges from the device-side generation,
+            # which keeps advancing: the workspace was reserved before capture, so no
+            # zero-fill / reset of it was recorded into the graphs
+            for sl in slots.values():
+                if sl["graph"] is not None:
+                    ws = ops._COOP_WS[(str(X.device), sl["stream"].cuda_stream)]
+                    gen = int(ws["gen_dev"].item()) & 0xFFFFFFFF
+                    assert gen > 0x80000000 + 4, hex(gen)
     for a, b in zip(res["1"], res["0"]):
         np.testing.assert_array_equal(a.n_iter, b.n_iter)
         np.testing.assert_array_equal(a.err, b.err)

@@ -24,6 +24,7 @@ import torch  # noqa: E402
 from cnmf_torch_amd import cNMF  # noqa: E402
 from cnmf_torch_amd.utils.anndata_lite import AnnData  # noqa: E402
 from cnmf_torch_amd.utils.h5ad import write_h5ad  # noqa: E402
+from cnmf_torch_amd.utils.plotting import flush_figures  # noqa: E402
 from cnmf_torch_amd.utils.synthetic import simulate_counts  # noqa: E402
 
 
@@ -56,11 +57,16 @@ def main():
     stages = [("factorize", lambda: obj.factorize(verbose=False)),
               ("combine", obj.combine),
               ("k_selection_plot", lambda: obj.k_selection_plot(close_fig=True,
-                                                               kmeans_backend=a.kmeans_backend)),
+                                                               kmeans_backend=a.kmeans_backend,
+                                                               wait_figures=False)),
               ("consensus", lambda: obj.consensus(kmid, density_threshold=a.threshold,
                                                   show_clustering=True,
                                                   close_clustergram_fig=True,
-                                                  kmeans_backend=a.kmeans_backend))]
+                                                  kmeans_backend=a.kmeans_backend,
+                                                  wait_figures=False)),
+              # the figures render while later stages compute (as the CLI does); the
+              # pipeline is done once the last PNG is on disk
+              ("figures", flush_figures)]
     prof_out = open(a.profile, "w") if a.profile else None
     for name, fn in stages:
         if prof_out:
