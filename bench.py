@@ -75,6 +75,9 @@ def main() -> int:
     ap.add_argument("--max-nmf-iter", type=int, default=1000)
     ap.add_argument("--batch-size", type=int, default=5000)
     ap.add_argument("--cpu", action="store_true", help="run on CPU (plumbing check)")
+    ap.add_argument("--float-input", action="store_true",
+                    help="non-count data: X + 0.5 U(0,1) (e.g. batch-corrected counts), which "
+                         "the integer-count plane detection declines")
     ap.add_argument("--streams", type=int, default=1,
                     help="replicate groups solved concurrently on separate HIP streams")
     args = ap.parse_args()
@@ -114,6 +117,8 @@ def main() -> int:
     from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
 
     X = normalized_counts_matrix(args.cells, args.genes, n_programs=args.k, seed=0)
+    if args.float_input:
+        X = (X + 0.5 * np.random.default_rng(1).random(X.shape)).astype(X.dtype)
     comm = row_map = schedule = None
     if args.mode == "dp" and world > 1:
         segs = dp_row_segments(X.shape[0], args.batch_size, rank, world)
@@ -191,10 +196,16 @@ def main() -> int:
         step(i)
     barrier()
     t0 = time.perf_counter()
-    passes = []
+    passes, h_sweeps, w_sweeps = [], [], []
     for i in range(args.warmup, nsteps):
         res, _ = step(i)
         passes.append(float(np.mean(res.n_iter)))
+        # inner MU sweeps per (replicate, pass, chunk) -- the solve kernels' work unit
+        n_chunks = -(-args.cells // args.batch_size)
+        for key, acc in (("h_inner_iters", h_sweeps), ("w_inner_iters", w_sweeps)):
+            it = np.asarray(res.stats.get(key, []), dtype=np.float64)
+            if it.size:
+                acc.append(float(np.mean(it / np.maximum(res.n_iter, 1) / n_chunks)))
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed)
@@ -251,6 +262,9 @@ def main() -> int:
                 "streams_per_gpu": args.streams,
                 "device": "cpu" if not use_cuda else torch.cuda.get_device_name(dev),
                 "mean_passes": round(float(np.mean(passes)), 2) if passes else None,
+                "mean_sweeps_h_w": [round(float(np.mean(h_sweeps)), 1) if h_sweeps else None,
+                                    round(float(np.mean(w_sweeps)), 1) if w_sweeps else None],
+                "input": "float (X + 0.5 U(0,1))" if args.float_input else "counts / std",
                 "rccl_world": rccl_world,
                 "backend": backend,
                 "strong_value": None if strong_value is None else round(strong_value, 3),

@@ -107,6 +107,31 @@ def _dt_str(density_threshold) -> str:
     return str(density_threshold).replace(".", "_")
 
 
+def gpu_max_rank(beta_loss="frobenius", algo="mu") -> int | None:
+    """Largest K the native MI355X kernels factorise (None: no limit -- 'bpp' solves its
+    NNLS blocks with torch linear algebra).  Frobenius MU/HALS pad K to a multiple of 8
+    up to 64 (models.nmf.native_rank); the beta-divergence kernels take K <= 32."""
+    if algo == "bpp":
+        return None
+    from .models.nmf import beta_value
+
+    return 64 if beta_value(beta_loss) == 2.0 else 32
+
+
+def check_gpu_ranks(components, beta_loss="frobenius", algo="mu", use_gpu=True) -> None:
+    """Fail at once -- at ``prepare``, before any work -- for a rank the GPU kernels do not
+    cover (the reference's ``-k`` is unbounded, cnmf.py:1417; the CPU path takes any K)."""
+    if not use_gpu or not torch.cuda.is_available():
+        return
+    ks = [int(k) for k in np.atleast_1d(components)]
+    kmax = gpu_max_rank(beta_loss, algo)
+    if kmax is not None and ks and max(ks) > kmax:
+        raise ValueError(
+            f"K={max(ks)}: on the GPU this engine factorises K <= {kmax} "
+            f"(beta_loss={beta_loss!r}, algo={algo!r}); run without --use_gpu (the CPU "
+            f"path takes any K) or choose components <= {kmax}")
+
+
 def _device(use_gpu: bool, device=None) -> torch.device:
     """Explicit ``device`` > $CNMF_DEVICE > the local GPU when one is visible > CPU.
 
@@ -228,6 +253,7 @@ class cNMF:
         the reference's hard-coded 'mu'/'online').  With a multi-rank ``comm`` the cells
         are sharded over the ranks and the per-gene statistics are all-reduced
         (:meth:`_prepare_sharded`)."""
+        check_gpu_ranks(components, beta_loss, algo, use_gpu)
         if comm is not None and comm.world_size > 1:
             return self._prepare_sharded(
                 comm, counts_fn, components, n_iter=n_iter, densify=densify, tpm_fn=tpm_fn,
@@ -289,8 +315,10 @@ class cNMF:
         TPM mean/variance for tpm_stats and the over-dispersion model, the ddof=1 std of
         the HVG counts for the unit-variance scaling -- are combined across ranks by
         all-reduces (two-pass: global mean first, then centred sums of squares, so the
-        variances equal the single-process ones to summation order).  Rank 0 gathers the
-        row blocks and writes the artifacts of the single-process prepare."""
+        variances equal the single-process ones to summation order).  Rank 0 writes the
+        artifacts of the single-process prepare, receiving the other ranks' row blocks
+        one rank at a time (point-to-point) straight into the h5ad datasets: it never
+        holds more than its own block and one peer's (h5ad.write_h5ad_row_blocks)."""
         from .parallel.runner import row_block
         from .utils.h5ad import h5ad_shape, read_X_rows, read_h5ad_annotations
 
@@ -377,17 +405,32 @@ class cNMF:
                     "Error: %d cells have zero counts of overdispersed genes. E.g. %s. Filter "
                     "those cells and re-run or adjust the number of overdispersed genes. "
                     "Quitting!" % (n_zero, ", ".join(ex)))
-            parts = comm.gather_object((tpm.X, Xh, counts.obs), dst=0)
+            from .utils.h5ad import write_h5ad_row_blocks
+
+            def nnz(M):
+                return int(M.nnz) if sp.issparse(M) else 0
+            meta = comm.all_gather_object((int(tpm.X.shape[0]), nnz(tpm.X), nnz(Xh)))
             if rank == 0:
-                stack = (lambda ms: sp.vstack(ms, format="csr")) if sparse_in else np.concatenate
-                obs = pd.concat([p_[2] for p_ in parts])
-                write_h5ad(self.paths["tpm"], AnnData(X=stack([p_[0] for p_ in parts]), obs=obs,
-                                                      var=tpm.var))
+                self._initialize_dirs()
+            n_tot = sum(m_[0] for m_ in meta)
+            for which, local, total_nnz, path, var in (
+                    (0, tpm.X, sum(m_[1] for m_ in meta), self.paths["tpm"], tpm.var),
+                    (1, Xh, sum(m_[2] for m_ in meta), self.paths["normalized_counts"],
+                     counts.var.iloc[cols])):
+                if rank == 0:
+                    def blocks(local=local):
+                        yield counts.obs, local
+                        for src in range(1, world):       # one peer block at a time
+                            yield comm.recv_object(src)
+                    idx_dt = np.int64 if total_nnz >= 2 ** 31 else np.int32
+                    write_h5ad_row_blocks(path, n_tot, var, blocks(), sparse_in, local.dtype,
+                                          total_nnz, idx_dt)
+                else:
+                    comm.send_object((counts.obs, local), dst=0)
+                comm.barrier()
+            if rank == 0:
                 save_df_to_npz(stats, self.paths["tpm_stats"])
                 write_text_atomic(self.paths["nmf_genes_list"], "\n".join(hvgs))
-                norm = AnnData(X=stack([p_[1] for p_ in parts]), obs=obs,
-                               var=counts.var.iloc[cols])
-                self.save_norm_counts(norm)
                 replicate_params, run_params = self.get_nmf_iter_params(
                     ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
                     alpha_usage=alpha_usage, alpha_spectra=alpha_spectra, init=init,
@@ -820,7 +863,16 @@ class cNMF:
 
     # ------------------------------------------------------------------ refits
     def _refit_kwargs(self):
-        return load_yaml(self.paths["nmf_run_parameters"])
+        """The run parameters YAML, parsed once per file version (k-selection re-read it
+        twice per K: ~30 ms of PyYAML per run)."""
+        fn = self.paths["nmf_run_parameters"]
+        st = os.stat(fn)
+        key = (fn, st.st_mtime_ns, st.st_size)
+        cache = getattr(self, "_yaml_cache", None)
+        if cache is None or cache[0] != key:
+            cache = (key, load_yaml(fn))
+            self._yaml_cache = cache
+        return dict(cache[1])
 
     def refit_usage(self, X, spectra, usage=None, device=None):
         """Refit usages with spectra fixed (cnmf.py:923-976): online MU, h_tol 0.05."""
@@ -887,7 +939,10 @@ class cNMF:
         dt_repl = dt_str.replace(".", "_")
         n_neighbors = int(local_neighborhood_size * merged.shape[0] / k)
 
-        S = torch.as_tensor(merged.values, dtype=torch.float64, device=dev)
+        # float32 spectra cross to the device as float32 (half the bytes) and widen there
+        mv = np.ascontiguousarray(merged.values)
+        S = torch.from_numpy(mv).to(dev).to(torch.float64) if mv.dtype == np.float32 else \
+            torch.as_tensor(mv, dtype=torch.float64, device=dev)
         L2 = l2_normalize_rows(S)
         names = merged.index
         topics_dist = None

@@ -196,6 +196,12 @@ def cluster_medians(S: torch.Tensor, labels: np.ndarray, k_labels) -> torch.Tens
     counts = np.bincount(rk, minlength=len(k_labels))
     if (counts == 0).any():
         raise ValueError("cluster_medians: an empty cluster")
+    if R.dtype == torch.float64:
+        # GPU: one workgroup per gene ranks every value inside its cluster in LDS
+        # (seg_median.hip) -- no sort; beyond its limits the sorts below
+        med = ops.seg_median(R if R.stride(-1) == 1 else R.contiguous(), rk, len(k_labels))
+        if med is not None:
+            return med / med.sum(dim=1, keepdim=True)
     vals, i1 = torch.sort(R, dim=0)                                   # by value, per gene
     lab_t = torch.as_tensor(rk, device=S.device)
     _, i2 = torch.sort(lab_t[i1], dim=0, stable=True)                 # then by cluster

@@ -25,6 +25,12 @@ def sparse_mean_var(X):
     importing sklearn, whose import alone was ~1 s of every ``prepare``."""
     X = sp.csr_matrix(X)
     N, G = X.shape
+    from ..utils.io import _npzio
+    if _npzio is not None and X.dtype in (np.float32, np.float64):
+        mean, var = _npzio.csr_mean_var(X.data, X.indices, N, G)   # native, same bits
+        if X.dtype == np.float32:
+            return mean.astype(np.float32).astype(np.float64), var.astype(np.float32).astype(np.float64)
+        return mean, var
     data = np.asarray(X.data, dtype=np.float64)
     idx = X.indices
     nnz = np.bincount(idx, minlength=G)

@@ -684,7 +684,50 @@ def _inner_solve(algo: str, x3: torch.Tensor, numer3: torch.Tensor, gram3: torch
         ops.split_planes(x3.reshape(R * K, x3.shape[2]), planes, col_mul=colmul)
 
 
-def _count_units(X: torch.Tensor, stats=None):
+class RowBlocks:
+    """A cells x genes float32 matrix that is never whole on the device: ``blocks()``
+    yields (row_start, (rows, G) float32 device block) over all rows, in order, and may be
+    called several times (each call regenerates or re-reads the blocks).  Row starts must
+    be multiples of 4 (the split planes' k offsets).  ``RowBlocks.of(X)`` views a resident
+    tensor the same way."""
+
+    def __init__(self, n_rows: int, n_cols: int, blocks_fn, device):
+        self.shape = (int(n_rows), int(n_cols))
+        self.device = torch.device(device)
+        self.dtype = torch.float32
+        self._fn = blocks_fn
+
+    def blocks(self):
+        for a, blk in self._fn():
+            if a % 4:
+                raise ValueError(f"RowBlocks: block start {a} is not a multiple of 4")
+            yield a, blk
+
+    @classmethod
+    def of(cls, X: torch.Tensor, rows: int = 1 << 16) -> "RowBlocks":
+        N, G = X.shape
+        return cls(N, G, lambda: ((a, X[a:a + rows]) for a in range(0, N, rows)), X.device)
+
+
+def _block_colstats(src: RowBlocks):
+    """(min positive, float64 sum of squares, any-negative, float64 sum) per column over
+    every block (ops.colstats per block, combined)."""
+    N, G = src.shape
+    dev = src.device
+    mn = torch.full((G,), float("inf"), dtype=torch.float32, device=dev)
+    sq = torch.zeros(G, dtype=torch.float64, device=dev)
+    sm = torch.zeros(G, dtype=torch.float64, device=dev)
+    neg = torch.zeros(G, dtype=torch.int32, device=dev)
+    for _, blk in src.blocks():
+        m_, q_, n_ = ops.colstats(blk)
+        torch.minimum(mn, m_, out=mn)
+        sq += q_
+        neg |= n_.to(torch.int32)
+        sm += blk.sum(dim=0, dtype=torch.float64)
+    return mn, sq, neg, sm
+
+
+def _count_units(X, stats=None):
     """Per-gene unit u (G,) with X == C * u for a non-negative INTEGER matrix C, or None.
 
     cNMF's normalised counts are raw counts over a per-gene std (cnmf.py:670-681), so the
@@ -694,12 +737,24 @@ def _count_units(X: torch.Tensor, stats=None):
     gap the smallest difference between distinct entries; a column of zeros gets u = 1.
     Accepted only if every entry of every column is an integer multiple of its unit to
     fp32 rounding (|X/u - round(X/u)| <= 4e-7 * X/u + 1e-4) and C < 65536.  ``stats``:
-    the (min_pos, sumsq, neg) of ops.colstats when already computed."""
+    the (min_pos, sumsq, neg) of ops.colstats when already computed.  ``X`` may be a
+    :class:`RowBlocks` (the check then runs block by block)."""
     N, G = X.shape
     if N == 0:
         return None
-    mn_t, _, neg = stats if stats is not None else ops.colstats(X)
-    bad_t = ops.count_unit_check(X, mn_t)     # skips empty columns (min_pos = inf)
+    src = X if isinstance(X, RowBlocks) else None
+    if stats is not None:
+        mn_t, _, neg = stats[:3]
+    elif src is not None:
+        mn_t, _, neg, _ = _block_colstats(src)
+    else:
+        mn_t, _, neg = ops.colstats(X)
+    if src is None:
+        bad_t = ops.count_unit_check(X, mn_t)     # skips empty columns (min_pos = inf)
+    else:
+        bad_t = torch.zeros(G, dtype=torch.int32, device=src.device)
+        for _, blk in src.blocks():
+            bad_t |= ops.count_unit_check(blk, mn_t)
     # one host round trip for the per-gene decisions
     host = torch.stack([mn_t.double(), bad_t.double(), neg.double()]).cpu().numpy()
     mn, bad, neg_h = host[0], host[1].astype(np.int64), host[2] != 0
@@ -716,21 +771,28 @@ def _count_units(X: torch.Tensor, stats=None):
     todo = np.flatnonzero(np.isnan(unit))
     if todo.size > 64:
         return None
+    if todo.size and src is not None:     # the few columns the gap rule needs, gathered
+        tt = torch.as_tensor(todo, device=src.device)
+        cols = torch.cat([blk.index_select(1, tt) for _, blk in src.blocks()])
+        colmap = {g: cols[:, i] for i, g in enumerate(todo.tolist())}
+    else:
+        colmap = None
     for g in todo.tolist():
-        v = torch.unique(X[:, g])
+        xg = colmap[g] if colmap is not None else X[:, g]
+        v = torch.unique(xg)
         v = v[v > 0]
         dv = torch.diff(v)
         if dv.numel() == 0:
             return None
         u = float(mn[g]) / max(1.0, round(float(mn[g]) / float(dv.min())))
-        c = X[:, g] / u
+        c = xg / u
         if bool((((c - torch.round(c)).abs() > 4e-7 * c + 1e-4) | (c >= 65535.5)).any()):
             return None
         unit[g] = u
     # mn / d in float32 arithmetic, as the device check evaluated it
     return torch.from_numpy((mn.astype(np.float32) / np.maximum(d, 1).astype(np.float32))
                             .astype(np.float32) if todo.size == 0 else unit.astype(np.float32)
-                            ).to(X.device).contiguous()
+                            ).to(mn_t.device).contiguous()
 
 
 class _XPlanes:
@@ -741,32 +803,56 @@ class _XPlanes:
     bf16 plane (C <= 256) or two (C < 65536) with the per-gene ``unit`` folded into the
     other operand / the output columns; other data as three planes of X itself."""
 
-    def __init__(self, X: torch.Tensor, stats=None):
+    def __init__(self, X, stats=None):
+        """``X``: the resident fp32 matrix, or a :class:`RowBlocks` (planes built block by
+        block; no full fp32 copy is ever made -- nor is one needed for a resident X: the
+        count matrix is rounded per block)."""
         N, G = X.shape
         self.N, self.G = N, G
+        src = X if isinstance(X, RowBlocks) else RowBlocks.of(X)
+        dev = src.device
         unit = _count_units(X, stats)
         if unit is not None:
-            C = torch.empty_like(X)
-            for a in range(0, N, 1 << 16):
-                torch.round(X[a:a + (1 << 16)] / unit, out=C[a:a + (1 << 16)])
-            cmax = float(C.max()) if C.numel() else 0.0
+            cmax = 0.0
+            for _, blk in src.blocks():
+                if blk.numel():
+                    cmax = max(cmax, float(torch.round(blk / unit).max()))
             # integers 0..256 are exact in one bf16 plane, 0..65535 in two (hi + the
             # exact residual): the split below is lossless by construction
             self.pb = 1 if cmax <= 256 else 2
             if cmax >= 65536:
-                unit, C, self.pb = None, X, 3
+                unit, self.pb = None, self._float_planes(G)
         else:
-            C, self.pb = X, 3
+            self.pb = self._float_planes(G)
         self.unit = unit
         self.Gp = -(-G // 64) * 64
         self.Np = -(-N // 64) * 64 + 64
-        self.x = torch.zeros((self.pb, N + 128, self.Gp), dtype=torch.int16, device=X.device)
-        ops.split_planes(C, self.x)
-        self.xt = torch.zeros((self.pb, G, self.Np), dtype=torch.int16, device=X.device)
-        for a in range(0, N, 1 << 16):
-            blk = C[a:a + (1 << 16)].t().contiguous()          # (G, cells of the block)
-            ops.split_planes(blk, self.xt[:, :, a:a + -(-blk.shape[1] // 4) * 4])
-        del C
+        self.x = torch.zeros((self.pb, N + 128, self.Gp), dtype=torch.int16, device=dev)
+        self.xt = torch.zeros((self.pb, G, self.Np), dtype=torch.int16, device=dev)
+        for a, blk in src.blocks():
+            n = blk.shape[0]
+            C = torch.round(blk / unit) if unit is not None else blk
+            ops.split_planes(C, self.x[:, a:a + n])
+            Ct = C.t().contiguous()                               # (G, cells of the block)
+            ops.split_planes(Ct, self.xt[:, :, a:a + -(-n // 4) * 4])
+            del C, Ct
+
+    @staticmethod
+    def bytes_needed(N: int, G: int, pb: int) -> int:
+        """Device bytes of the two plane layouts for ``pb`` planes."""
+        return 2 * pb * ((N + 128) * (-(-G // 64) * 64) + G * (-(-N // 64) * 64 + 64))
+
+    @staticmethod
+    def _float_planes(G: int) -> int:
+        """B planes of non-count data: 2 (hi + mid, <= 2^-16 relative per element, the
+        same bound the engine accepts for the A operand, ops.gemm_a_planes) once the
+        numerator's reduction runs over >= 1024 genes -- inside the fp32 GEMM's own error
+        there (test_gemm_two_b_planes_within_fp32_library_error); else 3 (exact).
+        CNMF_GEMM_BPLANES=3 forces exact.  Two planes make a product 4 MFMAs instead of
+        5 (2 for counts) and halve nothing else."""
+        if G < 1024 or os.environ.get("CNMF_GEMM_BPLANES", "2") == "3":
+            return 3
+        return 2
 
     @staticmethod
     def build(X: torch.Tensor, stats=None):
@@ -775,11 +861,45 @@ class _XPlanes:
                 os.environ.get("CNMF_GEMM", "planes") != "planes":
             return None
         N, G = X.shape
-        need = 2 * 3 * ((N + 128) * (-(-G // 64) * 64) + G * (-(-N // 64) * 64 + 64)) + 8 * N * G
+        # sized by the plane count it will most likely use (2: counts above 256, or
+        # non-count data) plus one row block's temporaries -- not 3 planes + a full fp32
+        # copy of X as before (that refused 10M x 5k on one GPU)
+        need = _XPlanes.bytes_needed(N, G, 2) + 3 * 4 * min(N, 1 << 16) * G
         free, _ = torch.cuda.mem_get_info(X.device)
-        if need > 0.5 * free:
+        if need > 0.9 * free:
+            _warn_once(f"split-precision GEMM planes need {need / 1e9:.1f} GB, "
+                       f"{free / 1e9:.1f} GB free: the data-side GEMMs fall back to the fp32 "
+                       "library GEMM (pass the matrix as nmf.PlanesOnlyX to hold it as "
+                       "planes only)")
             return None
         return _XPlanes(X, stats)
+
+
+_WARNED: set = set()
+
+
+def _warn_once(msg: str) -> None:
+    if msg not in _WARNED:
+        _WARNED.add(msg)
+        import warnings
+
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
+
+
+class PlanesOnlyX:
+    """A cells x genes matrix held on the device ONLY as the split-GEMM planes (plus its
+    statistics), built block by block from a :class:`RowBlocks` source: the fp32 matrix is
+    never resident.  At 10M cells x 5k genes the fp32 matrix alone is 200 GB and its
+    count planes 100-200 GB, which do not fit one 288 GB MI355X together
+    (tools/bench_large.py --planes-only).  ``NMFBatchSolver`` takes it in place of X for
+    online Frobenius MU/HALS with random init -- every other use of X raises."""
+
+    def __init__(self, src: RowBlocks):
+        self.shape, self.device, self.dtype = src.shape, src.device, torch.float32
+        mn, sq, neg, sm = _block_colstats(src)
+        self.x_sq = float(sq.sum())
+        self.sum = float(sm.sum())
+        self.planes = _XPlanes(src, stats=(mn, sq, neg))
 
 
 def native_rank(K: int) -> int:
@@ -831,6 +951,19 @@ class NMFBatchSolver:
         self.schedule = schedule
         self.opts = opts
         self.comm = comm or LocalComm()
+        self._virtual = isinstance(X, PlanesOnlyX)
+        if self._virtual:
+            # planes only: X stands in as a NaN-valued (N, G) view of one element -- shape,
+            # device and dtype for the bookkeeping; any read of its values would surface as
+            # NaN errors, and every code path that reads X raises before it
+            if beta_value(opts.beta_loss) != 2.0 or \
+                    opts.mode != "online" or opts.online_stats != "pass" or \
+                    opts.init != "random" or opts.algo not in ("mu", "hals") or \
+                    opts.dtype != torch.float32:
+                raise ValueError("PlanesOnlyX supports online Frobenius MU/HALS with random "
+                                 "init in float32 (the planes are the only copy of X)")
+            src = X
+            X = torch.full((1, 1), float("nan"), device=src.device).expand(*src.shape)
         self.X = X if X.dtype == opts.dtype else X.to(opts.dtype)
         self.row_offset = row_offset
         # [(local_start, local_stop, global_start)]: where this rank's rows sit in the
@@ -842,14 +975,19 @@ class NMFBatchSolver:
         # ||X||_F^2 (global) for the trace-trick loss; on the GPU from the fused column
         # statistics pass that also feeds the split-GEMM count detection
         self._colstats = None
-        if self.X.device.type == "cuda" and self.X.dtype == torch.float32 and self.X.numel():
+        self._mean_x = None
+        self._xp = False            # split-GEMM planes of X: False = not built yet
+        if self._virtual:
+            local_sq = src.x_sq
+            self._xp = src.planes
+            self._mean_x = self.comm.allreduce_scalar(src.sum) / max(
+                self.comm.allreduce_scalar(float(src.shape[0] * src.shape[1])), 1.0)
+        elif self.X.device.type == "cuda" and self.X.dtype == torch.float32 and self.X.numel():
             self._colstats = ops.colstats(self.X)
             local_sq = float(self._colstats[1].sum())
         else:
             local_sq = _sq_norm(self.X)
         self.x_sq = self.comm.allreduce_scalar(local_sq)
-        self._mean_x = None
-        self._xp = False            # split-GEMM planes of X: False = not built yet
         self._ws: dict = {}
         self._w_fresh: dict = {}    # stream -> key of the W its "w" planes hold
         self._XT = None             # X^T (G, N padded to 4) for the beta W-side kernel
@@ -1043,6 +1181,7 @@ class NMFBatchSolver:
         """numer = W X[a:b]^T (rows(W), b - a) -- split-precision MFMA when available."""
         xp = self._planes()
         if xp is None or wpl is None:
+            self._need_x("the numerator GEMM without planes")
             return W @ self.X[a:b].t()
         out = torch.empty((W.shape[0], b - a), device=W.device, dtype=W.dtype)
         ops.gemm_planes(out, wpl[:ops.gemm_a_planes(xp.Gp)], xp.x[:, a:], W.shape[0], b - a,
@@ -1056,6 +1195,7 @@ class NMFBatchSolver:
         H-solve epilogue already wrote the usages planes (solve_planes('h'))."""
         xp = self._planes()
         if xp is None or a % 8:
+            self._need_x("a statistics GEMM at a chunk start that is not 8-aligned")
             B.addmm_(HT[:, a:b], self.X[a:b], beta=1.0 if accumulate else 0.0)
             return
         bk = ops.planes_bk(xp.pb)
@@ -1065,6 +1205,11 @@ class NMFBatchSolver:
             ops.split_planes(HT[:, a:b], hpl[:, :HT.shape[0]])
         ops.gemm_planes(B, hpl[:ops.gemm_a_planes(kd)], xp.xt[:, :, a:], HT.shape[0], xp.G, kd,
                         accumulate=accumulate, col_scale=xp.unit)
+
+    def _need_x(self, what: str) -> None:
+        if self._virtual:
+            raise ValueError(f"PlanesOnlyX: {what} needs the fp32 matrix, which is not held "
+                             "(online chunk starts must be multiples of 8)")
 
     def _mean(self) -> float:
         """Global mean of X (random init scale), one pass per solver."""

@@ -15,6 +15,7 @@ import contextlib
 import os
 import threading
 
+import numpy as np
 import torch
 
 from . import reference
@@ -1028,6 +1029,33 @@ def seg_argmin(D: torch.Tensor, k: int, row_add: torch.Tensor | None = None,
                     ca.data_ptr() if ca is not None else 0, lab.data_ptr(), mind.data_ptr(),
                     _stream_ptr(Dd))
     return lab.long(), mind
+
+
+def seg_median(S: torch.Tensor, rank: np.ndarray, k: int) -> torch.Tensor | None:
+    """(k, G) per-cluster column medians of the float64 matrix S (n, G) for cluster ids
+    ``rank`` (n,) in 0..k-1, every cluster non-empty (seg_median.hip: LDS rank counting,
+    one workgroup per column, pandas' median of the two middle values).  None when the
+    kernel's limits (n <= 4096 rows, k <= 256) do not hold -- the caller sorts instead."""
+    n, G = S.shape
+    if not use_native(S):
+        return None
+    if S.dtype != torch.float64 or (G > 1 and S.stride(1) != 1):
+        raise ValueError("seg_median: float64 with unit column stride")
+    if n > _hip.seg_median_max_rows() or k > _hip.seg_median_max_clusters():
+        return None
+    rank = np.asarray(rank, dtype=np.int64)
+    counts = np.bincount(rank, minlength=k)
+    if counts.size != k or (counts == 0).any():
+        raise ValueError("seg_median: every cluster needs a member")
+    perm = np.argsort(rank, kind="stable").astype(np.int32)
+    seg = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    dev = S.device
+    perm_t = torch.from_numpy(perm).to(dev)
+    seg_t = torch.from_numpy(seg).to(dev)
+    out = torch.empty((k, G), dtype=torch.float64, device=dev)
+    _hip.seg_median(S.data_ptr(), S.stride(0), n, G, perm_t.data_ptr(), seg_t.data_ptr(), k,
+                    out.data_ptr(), out.stride(0), _stream_ptr(S))
+    return out
 
 
 def kmeanspp_fused_ok(X: torch.Tensor, M: int) -> bool:

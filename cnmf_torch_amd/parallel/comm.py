@@ -36,6 +36,12 @@ class LocalComm:
     def gather_object(self, obj, dst: int = 0):
         return [obj]
 
+    def send_object(self, obj, dst: int) -> None:
+        raise RuntimeError("single process: nothing to send to")
+
+    def recv_object(self, src: int):
+        raise RuntimeError("single process: nothing to receive")
+
     def all_gather_(self, t: torch.Tensor) -> list[torch.Tensor]:
         return [t]
 
@@ -155,6 +161,16 @@ class DistComm(LocalComm):
         out = [torch.empty_like(src) for _ in range(self.world_size)]
         self._dist.all_gather(out, src.contiguous(), group=self.group)
         return out if src is t else [o.to(t.device) for o in out]
+
+    def send_object(self, obj, dst: int) -> None:
+        """Point-to-point: ``obj`` to rank ``dst`` (which must call recv_object(src=me))."""
+        self._dist.send_object_list([obj], dst=dst, group=self.group)
+
+    def recv_object(self, src: int):
+        """Point-to-point: the object rank ``src`` sends with send_object."""
+        box = [None]
+        self._dist.recv_object_list(box, src=src, group=self.group)
+        return box[0]
 
     def gather_object(self, obj, dst: int = 0):
         """Python objects of every rank on ``dst`` (list in rank order), None elsewhere."""

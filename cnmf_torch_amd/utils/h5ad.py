@@ -149,6 +149,61 @@ def write_h5ad(path: str, adata, compression=None) -> None:
             f.close()
 
 
+def write_h5ad_row_blocks(path: str, n_rows: int, var: pd.DataFrame, blocks, sparse: bool,
+                          dtype, nnz: int = 0, index_dtype=np.int32) -> None:
+    """Write an h5ad whose X arrives as row blocks, in row order, without ever holding
+    the whole matrix: ``blocks`` yields (obs_block DataFrame, X_block) with X_block a
+    CSR (``sparse``) or dense array of ``dtype``; ``nnz`` is the total non-zero count of
+    a CSR X.  X's datasets are created at their final size and filled by hyperslab
+    writes (the native layer's create_dataset / write_rows); obs is written at the end.
+    Same encoding as :func:`write_h5ad`."""
+    from .io import atomic_path
+
+    lib = _lib()
+    G = len(var)
+    with atomic_path(path, suffix=".h5ad") as tmp:
+        f = lib.File(tmp, "w")
+        try:
+            _set_enc(f, "/", "anndata", "0.1.0")
+            if sparse:
+                f.create_group("/X")
+                _set_enc(f, "/X", "csr_matrix", "0.1.0")
+                f.set_attr("/X", "shape", np.asarray([n_rows, G], dtype=np.int64))
+                f.create_dataset("/X/data", np.dtype(dtype), [int(nnz)])
+                f.create_dataset("/X/indices", np.dtype(index_dtype), [int(nnz)])
+                f.create_dataset("/X/indptr", np.dtype(np.int64), [int(n_rows) + 1])
+            else:
+                f.create_dataset("/X", np.dtype(dtype), [int(n_rows), G])
+                _set_enc(f, "/X", "array", "0.2.0")
+            obs_parts = []
+            r0 = e0 = 0
+            for obs_b, Xb in blocks:
+                n = Xb.shape[0]
+                if sparse:
+                    Xb = sp.csr_matrix(Xb)
+                    f.write_rows("/X/data", e0, np.ascontiguousarray(Xb.data, dtype=dtype))
+                    f.write_rows("/X/indices", e0,
+                                 np.ascontiguousarray(Xb.indices, dtype=index_dtype))
+                    ip = Xb.indptr.astype(np.int64) + e0
+                    f.write_rows("/X/indptr", r0, ip[:-1] if r0 + n < n_rows else ip)
+                    e0 += Xb.nnz
+                else:
+                    f.write_rows("/X", r0, np.ascontiguousarray(np.asarray(Xb), dtype=dtype))
+                r0 += n
+                obs_parts.append(obs_b)
+                del Xb, obs_b      # released before the next block is fetched
+            if r0 != n_rows or (sparse and e0 != nnz):
+                raise ValueError(f"row blocks gave {r0} rows / {e0} non-zeros, expected "
+                                 f"{n_rows} / {nnz}")
+            _write_frame(f, "/obs", pd.concat(obs_parts) if obs_parts else pd.DataFrame(), 0)
+            _write_frame(f, "/var", var, 0)
+            for key in ("obsm", "varm", "layers", "obsp", "varp", "uns"):
+                f.create_group("/" + key)
+                _set_enc(f, "/" + key, "dict", "0.1.0")
+        finally:
+            f.close()
+
+
 # ----------------------------------------------------------------------------- read
 def _enc(attrs: dict) -> str:
     e = attrs.get("encoding-type")

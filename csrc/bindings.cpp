@@ -289,6 +289,14 @@ PYBIND11_MODULE(_hip, m) {
                 "cnmf_philox_fill");
         });
 
+  m.def("seg_median_max_rows", []() { return cnmf_seg_median_max_rows(); });
+  m.def("seg_median_max_clusters", []() { return cnmf_seg_median_max_clusters(); });
+  m.def("seg_median", [](uintptr_t S, long long lds, int n, int G, uintptr_t perm, uintptr_t seg,
+                         int k, uintptr_t out, long long ldo, uintptr_t stream) {
+    check(cnmf_seg_median(P<const double>(S), lds, n, G, P<const int>(perm), P<const int>(seg),
+                          k, P<double>(out), ldo, reinterpret_cast<hipStream_t>(stream)),
+          "seg_median");
+  });
   m.def("gemm_planes_bk", [](int pb) { return cnmf_gemm_planes_bk(pb); });
   m.def("gemm_planes_tile", [](int v, int which) { return cnmf_gemm_planes_tile(v, which); });
   m.def("gemm_planes",

@@ -364,6 +364,45 @@ class File {
     if (total) chk(H5Dwrite(d, mt, H5S_ALL, H5S_ALL, H5P_DEFAULT, arr.data()), "write " + p, 0);
   }
 
+  // An empty (uncompressed, contiguous) dataset of `dtype` and `shape`, filled later by
+  // write_rows: a writer that receives row blocks one at a time (the sharded prepare's
+  // rank-0 writer) never holds the whole matrix.
+  void create_dataset(const std::string& p, py::dtype dtype, const std::vector<hsize_t>& dims) {
+    if (exists(p)) chk(H5Ldelete(fid(), p.c_str(), H5P_DEFAULT), "unlink " + p, 0);
+    if (dtype.kind() == 'b') throw H5Err("create_dataset: bool datasets unsupported");
+    const hid_t ft = native_type_for(dtype);
+    Hid sp(H5Screate_simple((int)dims.size(), dims.data(), nullptr), H5Sclose);
+    Hid dcpl(H5Pcreate(H5P_DATASET_CREATE), H5Pclose);
+    H5Pset_fill_time(dcpl, H5D_FILL_TIME_NEVER);
+    H5Pset_alloc_time(dcpl, H5D_ALLOC_TIME_LATE);
+    Hid l = lcpl_intermediate();
+    Hid d(chk(H5Dcreate2(fid(), p.c_str(), ft, sp, l, dcpl, H5P_DEFAULT), "create dataset " + p),
+          H5Dclose);
+  }
+
+  // rows [start, start + value.shape[0]) of an existing dataset (hyperslab along axis 0)
+  void write_rows(const std::string& p, long long start, py::array value) {
+    py::array arr = py::array::ensure(value, py::array::c_style);
+    if (!arr) throw H5Err("write_rows: array must be convertible to C-contiguous");
+    Hid d(chk(H5Dopen2(fid(), p.c_str(), H5P_DEFAULT), "open " + p), H5Dclose);
+    Hid fsp(H5Dget_space(d), H5Sclose);
+    const int nd = H5Sget_simple_extent_ndims(fsp);
+    if (nd < 1 || nd != arr.ndim()) throw H5Err("write_rows: rank mismatch for " + p);
+    std::vector<hsize_t> dims(nd);
+    H5Sget_simple_extent_dims(fsp, dims.data(), nullptr);
+    std::vector<hsize_t> cnt = shape_of(arr), off(nd, 0);
+    for (int i = 1; i < nd; ++i)
+      if (cnt[i] != dims[i]) throw H5Err("write_rows: trailing shape mismatch for " + p);
+    if (start < 0 || (hsize_t)start + cnt[0] > dims[0]) throw H5Err("write_rows: rows out of range: " + p);
+    if (cnt[0] == 0) return;
+    off[0] = (hsize_t)start;
+    chk(H5Sselect_hyperslab(fsp, H5S_SELECT_SET, off.data(), nullptr, cnt.data(), nullptr),
+        "hyperslab", 0);
+    Hid msp(H5Screate_simple(nd, cnt.data(), nullptr), H5Sclose);
+    chk(H5Dwrite(d, native_type_for(arr.dtype()), msp, fsp, H5P_DEFAULT, arr.data()),
+        "write rows " + p, 0);
+  }
+
   void write_strings(const std::string& p, const std::vector<std::string>& strs) {
     if (exists(p)) chk(H5Ldelete(fid(), p.c_str(), H5P_DEFAULT), "unlink " + p, 0);
     hsize_t n = strs.size();
@@ -500,6 +539,8 @@ PYBIND11_MODULE(_h5io, m) {
       .def("write_array", &File::write_array, py::arg("path"), py::arg("value"),
            py::arg("compression") = 0)
       .def("write_strings", &File::write_strings)
+      .def("create_dataset", &File::create_dataset)
+      .def("write_rows", &File::write_rows)
       .def("shape", &File::shape)
       .def("dtype_kind", &File::dtype_kind)
       .def("read", &File::read, py::arg("path"), py::arg("start") = 0, py::arg("stop") = -1)

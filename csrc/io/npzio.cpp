@@ -11,8 +11,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
+#include <type_traits>
 #include <charconv>
 #include <cmath>
 #include <cstdint>
@@ -560,6 +562,103 @@ static void write_tsv(const std::string& path, const std::string& corner,
   }
 }
 
+// ------------------------------------------------------------------------ CSR statistics
+// Column mean and ddof=0 variance of a CSR matrix by sklearn's corrected two-pass
+// algorithm (sklearn/utils/sparsefuncs_fast.pyx _csr_mean_variance_axis0, unit weights;
+// cnmf.py:128-131 runs it through StandardScaler): the same float64 operations in the
+// same order (row-major over the stored entries), hence the same bits -- at C++ speed and
+// without sklearn's ~1 s import on the prepare path.
+template <typename T, typename I>
+static void csr_mean_var_impl(const T* data, const I* indices, long long nnz, long long n_rows,
+                              long long G, double* mean, double* var) {
+  std::vector<double> corr(G, 0.0);
+  std::vector<long long> cnt(G, 0);
+  for (long long j = 0; j < G; ++j) mean[j] = var[j] = 0.0;
+  for (long long e = 0; e < nnz; ++e) {
+    const I c = indices[e];
+    mean[c] += (double)data[e];
+    cnt[c] += 1;
+  }
+  const double n = (double)n_rows;
+  for (long long j = 0; j < G; ++j) mean[j] /= n;
+  for (long long e = 0; e < nnz; ++e) {
+    const I c = indices[e];
+    const double d = (double)data[e] - mean[c];
+    corr[c] += d;
+    var[c] += d * d;
+  }
+  for (long long j = 0; j < G; ++j) {
+    const bool miss = cnt[j] != n_rows;
+    if (miss) corr[j] -= (n - (double)cnt[j]) * mean[j];
+    corr[j] = corr[j] * corr[j] / n;
+    if (miss) var[j] += (n - (double)cnt[j]) * (mean[j] * mean[j]);   // sklearn: means**2
+    var[j] = (var[j] - corr[j]) / n;
+  }
+}
+
+static py::tuple csr_mean_var(py::array data, py::array indices, long long n_rows, long long G) {
+  py::array_t<double> mean(G), var(G);
+  const long long nnz = data.size();
+  if (indices.size() != nnz) throw std::invalid_argument("csr_mean_var: data / indices sizes");
+  py::array d = py::array::ensure(data, py::array::c_style);
+  py::array ix = py::array::ensure(indices, py::array::c_style);
+  double* m = mean.mutable_data();
+  double* v = var.mutable_data();
+  const bool i64 = py::isinstance<py::array_t<long long>>(ix) || py::isinstance<py::array_t<int64_t>>(ix);
+  if (!i64 && !py::isinstance<py::array_t<int>>(ix))
+    throw std::invalid_argument("csr_mean_var: int32 or int64 indices");
+  auto run = [&](auto tag) {
+    using T = decltype(tag);
+    const T* dp = (const T*)d.data();
+    py::gil_scoped_release nogil;
+    if (i64) csr_mean_var_impl(dp, (const long long*)ix.data(), nnz, n_rows, G, m, v);
+    else csr_mean_var_impl(dp, (const int*)ix.data(), nnz, n_rows, G, m, v);
+  };
+  if (py::isinstance<py::array_t<double>>(d)) run(double{});
+  else if (py::isinstance<py::array_t<float>>(d)) run(float{});
+  else throw std::invalid_argument("csr_mean_var: float32 or float64 data");
+  return py::make_tuple(mean, var);
+}
+
+// data[e] *= scale[row(e)] in the data's own precision (normalize_total's row scaling:
+// float32 data times the float32-rounded factor, as numpy does), rows on native threads
+static void csr_scale_rows(py::array data, py::array indptr, py::array_t<double> scale,
+                           int threads) {
+  py::array ip = py::array::ensure(indptr, py::array::c_style);
+  const long long n = scale.size();
+  if (ip.size() != n + 1) throw std::invalid_argument("csr_scale_rows: indptr / scale sizes");
+  std::vector<long long> ptr(n + 1);
+  if (py::isinstance<py::array_t<int>>(ip)) {
+    const int* q = (const int*)ip.data();
+    for (long long i = 0; i <= n; ++i) ptr[i] = q[i];
+  } else {
+    const long long* q = (const long long*)ip.data();
+    for (long long i = 0; i <= n; ++i) ptr[i] = q[i];
+  }
+  const double* sc = scale.data();
+  auto go = [&](auto* dp) {
+    using T = std::remove_pointer_t<decltype(dp)>;
+    std::atomic<long long> next{0};
+    py::gil_scoped_release nogil;
+    auto work = [&]() {
+      for (long long r0; (r0 = next.fetch_add(256)) < n;)
+        for (long long r = r0; r < std::min(n, r0 + 256); ++r) {
+          const T f = (T)sc[r];
+          for (long long e = ptr[r]; e < ptr[r + 1]; ++e) dp[e] = dp[e] * f;
+        }
+    };
+    const int nt = std::max(1, std::min<int>(threads, (int)(n / 256) + 1));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  };
+  if (!(data.flags() & py::array::c_style)) throw std::invalid_argument("csr_scale_rows: contiguous data");
+  if (py::isinstance<py::array_t<float>>(data)) go((float*)data.mutable_data());
+  else if (py::isinstance<py::array_t<double>>(data)) go((double*)data.mutable_data());
+  else throw std::invalid_argument("csr_scale_rows: float32 or float64 data");
+}
+
 PYBIND11_MODULE(_npzio, m) {
   m.doc() = "cnmf_torch_amd native replicate-file writer/reader (stored npz, crc32, sha256)";
   m.def("write_spectra_batch", &write_spectra_batch, py::arg("paths"), py::arg("data"),
@@ -568,6 +667,9 @@ PYBIND11_MODULE(_npzio, m) {
   m.def("read_spectra_batch", &read_spectra_batch, py::arg("paths"), py::arg("threads") = 16);
   m.def("write_tsv", &write_tsv, py::arg("path"), py::arg("corner"), py::arg("columns"),
         py::arg("index"), py::arg("data"), py::arg("threads") = 16);
+  m.def("csr_mean_var", &csr_mean_var);
+  m.def("csr_scale_rows", &csr_scale_rows, py::arg("data"), py::arg("indptr"), py::arg("scale"),
+        py::arg("threads") = 16);
   m.def("sha256_hex", &sha256_hex);
   m.def("crc32", &crc32_bytes);
 }

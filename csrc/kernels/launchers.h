@@ -129,6 +129,10 @@ hipError_t cnmf_philox_fill(float* out, long long rows, long long cols, long lon
                             long long s_col, long long rep_stride, long long row_offset,
                             const unsigned long long* seeds, const float* scales, int R,
                             unsigned int stream_id, int mode, hipStream_t stream);
+int cnmf_seg_median_max_rows();
+int cnmf_seg_median_max_clusters();
+hipError_t cnmf_seg_median(const double* S, long long lds, int n, int G, const int* perm,
+                           const int* seg, int k, double* out, long long ldo, hipStream_t stream);
 int cnmf_gemm_planes_bk(int pb);
 int cnmf_gemm_planes_tile(int v, int which);
 hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_plane, int a_rows,

@@ -158,3 +158,42 @@ def test_native_tsv_writer_is_byte_identical_to_pandas(tmp_path):
     assert cio._tsv_native_args(quoted) is None
     cio.save_df_to_text(quoted, tmp_path / "q.txt")
     assert (tmp_path / "q.txt").read_text() == quoted.to_csv(sep="\t")
+
+
+def test_row_block_h5ad_writer_holds_one_block_at_a_time(tmp_path):
+    """write_h5ad_row_blocks (the sharded prepare's rank-0 writer) writes the same h5ad as
+    write_h5ad of the stacked matrix, CSR and dense, and releases every row block before
+    it asks for the next one -- so rank 0 never holds more than one peer block."""
+    import gc
+    import weakref
+
+    import numpy as np
+    import pandas as pd
+    import scipy.sparse as sp
+
+    from cnmf_torch_amd.utils.h5ad import read_h5ad, write_h5ad_row_blocks
+
+    rng = np.random.default_rng(0)
+    X = sp.random(70, 12, density=0.3, random_state=1, format="csr", dtype=np.float64)
+    obs = pd.DataFrame(index=[f"c{i}" for i in range(70)])
+    var = pd.DataFrame(index=[f"g{j}" for j in range(12)])
+    cuts = [0, 20, 21, 55, 70]
+    for sparse in (True, False):
+        live = []
+
+        def blocks():
+            for a, b in zip(cuts[:-1], cuts[1:]):
+                gc.collect()
+                assert all(r() is None for r in live), "a previous block is still held"
+                blk = X[a:b] if sparse else X[a:b].toarray()
+                arr = blk.data if sparse else blk
+                live.append(weakref.ref(arr))
+                yield obs.iloc[a:b], blk
+                del blk, arr       # (this generator's own references)
+        path = str(tmp_path / f"x{int(sparse)}.h5ad")
+        write_h5ad_row_blocks(path, 70, var, blocks(), sparse, np.float64, X.nnz)
+        got = read_h5ad(path)
+        gx = got.X.toarray() if sp.issparse(got.X) else got.X
+        np.testing.assert_array_equal(gx, X.toarray())
+        assert sp.issparse(got.X) == sparse
+        assert list(got.obs.index) == list(obs.index) and list(got.var.index) == list(var.index)

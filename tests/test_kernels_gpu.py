@@ -191,10 +191,19 @@ def test_nmf_batch_gpu_matches_cpu(algo, mode, beta_loss):
               beta_loss=beta_loss)
     g = run_nmf_batch(X, K, [11, 12, 13], device="cuda", **kw)
     c = run_nmf_batch(X, K, [11, 12, 13], device="cpu", **kw)
-    # same init, same algorithm: errors agree to fp32 reassociation noise
-    np.testing.assert_allclose(g.err, c.err, rtol=2e-2)
-    # ... and so do the factors and the convergence bookkeeping
+    # same init, same algorithm: errors agree to fp32 reassociation noise -- 1e-3 for
+    # Frobenius MU (replicates that stopped at the same pass; the split-precision GEMMs
+    # and MFMA solves only reorder fp32 sums); 3e-3 for HALS, whose coordinate-by-
+    # coordinate sweeps carry a reordering into every later coordinate (batch HALS after 40
+    # unconverged iterations measured 2.1e-3 on one replicate, 5e-10 on another); looser
+    # for KL (its MU step divides by the reconstruction element-wise)
     assert np.abs(g.n_iter - c.n_iter).max() <= 1, (g.n_iter, c.n_iter)
+    same = g.n_iter == c.n_iter
+    assert same.sum() >= 2, (g.n_iter, c.n_iter)
+    rel = np.abs(g.err - c.err) / np.abs(c.err)
+    tol = 2e-2 if beta_loss != "frobenius" else (1e-3 if algo == "mu" else 3e-3)
+    assert rel[same].max() <= tol, (rel, g.n_iter, c.n_iter)
+    assert rel.max() <= 2e-2, rel
     Wg, Wc = g.W.cpu().numpy(), c.W.cpu().numpy()
     cos = (Wg * Wc).sum(1) / (np.linalg.norm(Wg, axis=1) * np.linalg.norm(Wc, axis=1) + 1e-30)
     assert np.median(cos) > 0.99, np.sort(cos)[:5]
@@ -1401,3 +1410,47 @@ def test_solve_fused_operands_bitwise(coop_gen):
     got = gp_out[:, :S2].double().sum(dim=1)
     torch.testing.assert_close(got, full, rtol=1e-5, atol=1e-6)
     assert torch.isnan(gp_out[:, S2:]).all()
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 2000, 5024), (1000, 5000, 2016)])
+def test_gemm_two_b_planes_within_fp32_library_error(M, N, K):
+    """Non-count data in two B planes (hi + mid; models.nmf._XPlanes._float_planes) times
+    two A planes: the product's error vs fp64 is no larger than the fp32 library GEMM's
+    on the same operands at the engine's shapes (reduction >= 1024)."""
+    g = torch.Generator().manual_seed(M + 3 * K)
+    A = torch.rand((M, K), generator=g) * torch.rand((M, 1), generator=g) * 3
+    B = torch.rand((N, K), generator=g) * 7 + 0.5
+    bk = ops.planes_bk(2)
+    Kd = -(-K // bk) * bk
+    Ap = torch.zeros((3, M, Kd), dtype=torch.int16, device="cuda")
+    Bp = torch.zeros((3, N, Kd), dtype=torch.int16, device="cuda")
+    ops.split_planes(A.cuda(), Ap)
+    ops.split_planes(B.cuda(), Bp)
+    ref = A.double() @ B.double().t()
+    scale = ref.abs().max()
+    C22 = torch.empty((M, N), device="cuda")
+    ops.gemm_planes(C22, Ap[:2], Bp[:2], M, N, Kd)
+    lib = A.cuda() @ B.cuda().t()
+    e22 = float((C22.cpu().double() - ref).abs().max() / scale)
+    el = float((lib.cpu().double() - ref).abs().max() / scale)
+    assert e22 <= max(el, 2e-7), (e22, el)
+
+
+@pytest.mark.parametrize("n,G,k", [(1300, 2000, 10), (57, 33, 1), (4096, 50, 256), (900, 7, 13)])
+def test_seg_median_kernel_matches_pandas_with_ties(n, G, k):
+    """seg_median.hip (per-gene in-LDS rank counting) == pandas groupby().median(), bit
+    for bit, with heavy ties (values on a coarse grid) and odd / even cluster sizes; the
+    consensus medians run it (not the sort fallback) up to 4096 spectra."""
+    import pandas as pd
+
+    rs = np.random.default_rng(n + k)
+    S = np.round(rs.random((n, G)) * 40) / 40.0
+    lab = rs.integers(0, k, n)
+    lab[:k] = np.arange(k)                      # every cluster non-empty
+    St = torch.from_numpy(S).cuda()
+    got = ops.seg_median(St, lab, k)
+    assert got is not None
+    ref = pd.DataFrame(S).groupby(lab).median().values
+    np.testing.assert_array_equal(got.cpu().numpy(), ref)
+    assert ops.seg_median(torch.zeros((4097, 3), dtype=torch.float64, device="cuda"),
+                          np.arange(4097) % 3, 3) is None          # beyond the LDS stage

@@ -239,3 +239,29 @@ def test_mixed_k_beta_request_splits_by_k():
     ref4 = NMFBatchSolver(X, NMFOptions(n_components=4, **kw)).run([5, 7])
     np.testing.assert_allclose(res.spectra(2).numpy(), ref4.spectra(1).numpy(), rtol=1e-9)
     assert res.spectra(1).shape == (2, 60)
+
+
+def test_planes_only_x_factorises_like_the_resident_matrix():
+    """A matrix held only as split-GEMM planes, built block by block (nmf.PlanesOnlyX over
+    nmf.RowBlocks: the route for 10M x 5k on one GPU, where fp32 X and its planes do not
+    fit together) factorises like the resident fp32 matrix: same pass counts, errors to
+    fp32 rounding.  Count detection runs per block; reads of X raise."""
+    import torch
+
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions, PlanesOnlyX, RowBlocks
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(640, 96, n_programs=4, seed=2))
+    opts = NMFOptions(n_components=4, online_chunk_size=160, online_max_pass=6)
+    src = RowBlocks(640, 96, lambda: ((a, X[a:a + 98]) for a in range(0, 640, 98)), "cpu")
+    with pytest.raises(ValueError, match="multiple of 4"):
+        PlanesOnlyX(src)
+    src = RowBlocks(640, 96, lambda: ((a, X[a:a + 128]) for a in range(0, 640, 128)), "cpu")
+    px = PlanesOnlyX(src)
+    assert px.planes.unit is not None and px.planes.pb in (1, 2)   # exact count planes
+    ref = NMFBatchSolver(X, opts).run([5, 6, 7])
+    got = NMFBatchSolver(px, opts).run([5, 6, 7])
+    np.testing.assert_array_equal(got.n_iter, ref.n_iter)
+    np.testing.assert_allclose(got.err, ref.err, rtol=1e-5)
+    with pytest.raises(ValueError, match="PlanesOnlyX supports"):
+        NMFBatchSolver(px, NMFOptions(n_components=4, mode="batch"))

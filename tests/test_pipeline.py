@@ -335,3 +335,21 @@ def test_plot_worker_falls_back_when_the_child_dies(tmp_path):
               prediction_error=np.array([10.0, 9.0]))
     w2.wait(timeout=120)
     assert os.path.getsize(path2) > 1000
+
+
+def test_gpu_rank_limit_is_a_clear_prepare_error(monkeypatch, tmp_path):
+    """-k beyond what the GPU kernels cover fails at prepare with a message naming the
+    limit and the CPU alternative (instead of deep inside factorize)."""
+    import torch
+
+    from cnmf_torch_amd import api
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    with pytest.raises(ValueError, match=r"K=80: on the GPU this engine factorises K <= 64.*"
+                                         r"without --use_gpu"):
+        api.check_gpu_ranks([10, 80], "frobenius", "mu", use_gpu=True)
+    with pytest.raises(ValueError, match="K <= 32"):
+        api.check_gpu_ranks([40], "kullback-leibler", "mu", use_gpu=True)
+    api.check_gpu_ranks([80], "frobenius", "bpp", use_gpu=True)     # torch linalg: any K
+    api.check_gpu_ranks([80], "frobenius", "mu", use_gpu=False)     # CPU: any K
+    api.check_gpu_ranks([64], "frobenius", "mu", use_gpu=True)

@@ -32,8 +32,7 @@ from cnmf_torch_amd.parallel.comm import DistComm, LocalComm  # noqa: E402
 BLOCK = 1 << 17  # rows per generator block (seeded by block index)
 
 
-def device_counts(N, G, P, r0, r1, dev, comm, seed=0):
-    """Rows [r0, r1) of the planted-program matrix, scaled to global unit variance."""
+def _programs(G, P, dev, seed=0):
     gs = torch.Generator(device=dev).manual_seed(seed)
     base = torch.empty(G, device=dev).log_normal_(0.0, 1.0, generator=gs)
     S = base.repeat(P, 1)
@@ -42,20 +41,31 @@ def device_counts(N, G, P, r0, r1, dev, comm, seed=0):
         idx = torch.randperm(G, device=dev, generator=gs)[:nprog]
         S[k, idx] *= torch.empty(nprog, device=dev).log_normal_(1.5, 0.5, generator=gs)
     S /= S.sum(dim=1, keepdim=True)
+    return S
+
+
+def _count_block(S, b, dev, seed=0):
+    """Raw Poisson counts of generator block b (rows [b*BLOCK, (b+1)*BLOCK))."""
+    P = S.shape[0]
+    g = torch.Generator(device=dev).manual_seed(seed * 1_000_003 + b + 1)
+    gam = -torch.log(torch.rand((BLOCK, P), device=dev, generator=g).clamp_min_(1e-12))  # Exp(1)
+    U = gam ** (1.0 / 0.3)                                       # skewed mixture weights
+    U /= U.sum(dim=1, keepdim=True)
+    lib = torch.empty(BLOCK, device=dev).log_normal_(float(np.log(2000.0)), 0.35, generator=g)
+    lam = (U @ S) * lib[:, None]
+    return torch.poisson(lam, generator=g)
+
+
+def device_counts(N, G, P, r0, r1, dev, comm, seed=0):
+    """Rows [r0, r1) of the planted-program matrix, scaled to global unit variance."""
+    S = _programs(G, P, dev, seed)
     X = torch.empty((r1 - r0, G), device=dev, dtype=torch.float32)
     b0 = r0 // BLOCK
     for b in range(b0, (r1 + BLOCK - 1) // BLOCK):
         lo, hi = max(r0, b * BLOCK), min(r1, (b + 1) * BLOCK)
-        g = torch.Generator(device=dev).manual_seed(seed * 1_000_003 + b + 1)
-        n = (b + 1) * BLOCK - b * BLOCK
-        gam = -torch.log(torch.rand((n, P), device=dev, generator=g).clamp_min_(1e-12))  # Exp(1)
-        U = gam ** (1.0 / 0.3)                                       # skewed mixture weights
-        U /= U.sum(dim=1, keepdim=True)
-        lib = torch.empty(n, device=dev).log_normal_(float(np.log(2000.0)), 0.35, generator=g)
-        lam = (U @ S) * lib[:, None]
-        cnt = torch.poisson(lam, generator=g)
+        cnt = _count_block(S, b, dev, seed)
         X[lo - r0:hi - r0] = cnt[lo - b * BLOCK:hi - b * BLOCK]
-        del gam, U, lam, cnt
+        del cnt
     stats = torch.zeros(2 * G, dtype=torch.float64, device=dev)
     for i in range(0, X.shape[0], BLOCK):          # float64 sums without a float64 copy of X
         xb = X[i:i + BLOCK].double()
@@ -71,6 +81,34 @@ def device_counts(N, G, P, r0, r1, dev, comm, seed=0):
     return X
 
 
+def planes_only_counts(N, G, P, r0, r1, dev, comm, seed=0):
+    """The same matrix as device_counts, held ONLY as split-GEMM planes (nmf.PlanesOnlyX):
+    a statistics pass for the per-gene scale, then every planes pass regenerates the
+    blocks -- the 200 GB fp32 matrix of 10M x 5k is never resident."""
+    from cnmf_torch_amd.models.nmf import PlanesOnlyX, RowBlocks
+
+    S = _programs(G, P, dev, seed)
+    b0, b1 = r0 // BLOCK, (r1 + BLOCK - 1) // BLOCK
+    stats = torch.zeros(2 * G, dtype=torch.float64, device=dev)
+    for b in range(b0, b1):
+        lo, hi = max(r0, b * BLOCK), min(r1, (b + 1) * BLOCK)
+        xb = _count_block(S, b, dev, seed)[lo - b * BLOCK:hi - b * BLOCK].double()
+        stats[:G] += xb.sum(dim=0)
+        stats[G:] += (xb * xb).sum(dim=0)
+        del xb
+    comm.allreduce_(stats)
+    mean = stats[:G] / N
+    var = (stats[G:] / N - mean ** 2) * (N / max(N - 1, 1))
+    sd = torch.sqrt(var.clamp_min(0)).float()
+    sd[sd == 0] = 1.0
+
+    def blocks():
+        for b in range(b0, b1):
+            lo, hi = max(r0, b * BLOCK), min(r1, (b + 1) * BLOCK)
+            yield lo - r0, _count_block(S, b, dev, seed)[lo - b * BLOCK:hi - b * BLOCK] / sd
+    return PlanesOnlyX(RowBlocks(r1 - r0, G, blocks, dev))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cells", type=int, default=1_000_000)
@@ -81,6 +119,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=0)
     ap.add_argument("--dp", action="store_true", help="cell-sharded data parallel")
     ap.add_argument("--max-pass", type=int, default=20)
+    ap.add_argument("--planes-only", action="store_true",
+                    help="hold X only as split-GEMM planes (10M x 5k on one GPU: fp32 X "
+                         "and its planes do not fit together)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -97,7 +138,7 @@ def main():
     else:
         r0, r1 = 0, N
     t0 = time.perf_counter()
-    X = device_counts(N, G, a.k, r0, r1, dev, comm)
+    X = (planes_only_counts if a.planes_only else device_counts)(N, G, a.k, r0, r1, dev, comm)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
     opts = NMFOptions(n_components=a.k, tol=1e-4, online_chunk_size=5000,
@@ -138,7 +179,9 @@ def main():
             "data_gen_s": round(t_gen, 2), "dtype": "fp32",
             "config": {"cells": N, "genes": G, "k": a.k, "replicates_per_step": a.reps * (
                 1 if a.dp else world), "parallelism": f"{'dp' if a.dp else 'replicate'}x{world}",
-                "hbm_gb_X_per_gpu": round(X.numel() * 4 / 1e9, 2)},
+                "hbm_gb_X_per_gpu": round(N * G * 4 / 1e9 / (world if a.dp else 1), 2),
+                "x_storage": "split-GEMM planes only" if a.planes_only else "fp32 + planes",
+                "hbm_gb_peak": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
             "data": "synthetic planted-program Poisson counts generated on device"}), flush=True)
     if world > 1:
         dist.destroy_process_group()
