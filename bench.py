@@ -78,6 +78,9 @@ def main() -> int:
     ap.add_argument("--float-input", action="store_true",
                     help="non-count data: X + 0.5 U(0,1) (e.g. batch-corrected counts), which "
                          "the integer-count plane detection declines")
+    ap.add_argument("--density", type=float, default=None,
+                    help="keep only the largest DENSITY fraction of X's entries (the rest 0): "
+                         "sparse-input runs (KL switches to the CSR kernels at <= 0.15)")
     ap.add_argument("--streams", type=int, default=1,
                     help="replicate groups solved concurrently on separate HIP streams")
     args = ap.parse_args()
@@ -119,6 +122,8 @@ def main() -> int:
     X = normalized_counts_matrix(args.cells, args.genes, n_programs=args.k, seed=0)
     if args.float_input:
         X = (X + 0.5 * np.random.default_rng(1).random(X.shape)).astype(X.dtype)
+    if args.density is not None:
+        X[X < np.quantile(X, 1.0 - args.density)] = 0.0
     comm = row_map = schedule = None
     if args.mode == "dp" and world > 1:
         segs = dp_row_segments(X.shape[0], args.batch_size, rank, world)
@@ -264,7 +269,8 @@ def main() -> int:
                 "mean_passes": round(float(np.mean(passes)), 2) if passes else None,
                 "mean_sweeps_h_w": [round(float(np.mean(h_sweeps)), 1) if h_sweeps else None,
                                     round(float(np.mean(w_sweeps)), 1) if w_sweeps else None],
-                "input": "float (X + 0.5 U(0,1))" if args.float_input else "counts / std",
+                "input": ("float (X + 0.5 U(0,1))" if args.float_input else "counts / std")
+                + (f", density {float((X != 0).mean()):.3f}" if args.density is not None else ""),
                 "rccl_world": rccl_world,
                 "backend": backend,
                 "strong_value": None if strong_value is None else round(strong_value, 3),

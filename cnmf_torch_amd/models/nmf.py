@@ -100,6 +100,11 @@ class NMFOptions:
     online_beta_w_tol: float = 5e-3
     loss_every: int = 10
     eps: float = 1e-16
+    # KL on the GPU runs its MU statistics over the non-zeros only (CSR kernels,
+    # sparse_kl.hip) when X has at most this fraction of non-zero entries; 0 disables.
+    # CNMF_KL_SPARSE=1 / 0 forces / disables it.  At 15 % the CSR path measured 399 vs
+    # 364 rep/s (profiles/r3n_*); at the headline's 47 % the dense kernels win
+    kl_sparse_density: float = 0.15
 
     @classmethod
     def from_kwargs(cls, n_components: int, **kw) -> "NMFOptions":
@@ -1865,9 +1870,40 @@ class NMFBatchSolver:
             self._XT = buf[:, :N]
         return self._XT
 
-    def _beta_w_partials(self, xc, xtc, H3c, W3, active, panels=None):
-        """(splits, R, K, G) W-side partials: split-bf16 kernel through X^T, or the fp32
-        kernel reading X in place when X^T is not kept (see _xt)."""
+    def _kl_sparse(self):
+        """CSR of X (ops.KLCSR) when the KL MU statistics run on the sparse kernels
+        (sparse_kl.hip): KL on the native GPU path with X at most ``kl_sparse_density``
+        non-zero (``CNMF_KL_SPARSE=1`` forces it, ``=0`` disables it); else None (dense
+        split-precision kernels).  Decided once per solver (one host sync)."""
+        if "_kl_csr" in self.__dict__:
+            return self._kl_csr
+        csr = None
+        X = self.X
+        env = os.environ.get("CNMF_KL_SPARSE", "")
+        if (self.beta == 1.0 and env != "0" and isinstance(X, torch.Tensor)
+                and X.device.type == "cuda" and X.dtype == torch.float32
+                and self.opts.n_components <= 32 and ops.use_native(X)):
+            dens = float((X != 0).sum()) / max(X.numel(), 1)
+            if env == "1" or dens <= float(self.opts.kl_sparse_density):
+                csr = ops.kl_csr(X)
+        self._kl_csr = csr
+        self._kl_csrT = {}
+        return csr
+
+    def _kl_rows_T(self, a: int, b: int):
+        """Tiled CSRs of X[a:b]^T (genes x chunk cells) for the sparse spectra numerators."""
+        key = (a, b)
+        if key not in self._kl_csrT:
+            self._kl_csrT[key] = ops.kl_csr_tiles(self.X[a:b], self.opts.n_components)
+        return self._kl_csrT[key]
+
+    def _beta_w_partials(self, xc, xtc, H3c, W3, active, panels=None, rows=None):
+        """(splits, R, K, G) W-side partials: the sparse KL kernel over X[rows]^T, the
+        split-bf16 kernel through X^T, or the fp32 kernel reading X in place when X^T is
+        not kept (see _xt)."""
+        if rows is not None and self._kl_sparse() is not None:
+            return ops.kl_sparse_w_num(self._kl_rows_T(*rows), H3c, W3, self.opts.eps,
+                                       active=active, st=panels), None
         if xc.device.type == "cuda" and xtc is None:
             num, den, _ = ops.beta_contract("w", xc, H3c, W3, self.beta, self.opts.eps,
                                             active=active, reduce=False)
@@ -1885,17 +1921,28 @@ class NMFBatchSolver:
         return cache[key]
 
     def _beta_panels(self, F3: torch.Tensor):
-        """Split-bf16 panels of a factor that stays fixed over the next kernel launches
-        (GPU only; the CPU reference works on the fp32 factor directly)."""
-        return ops.beta_panels(F3) if F3.device.type == "cuda" else None
+        """Kernel operand of a factor that stays fixed over the next kernel launches: its
+        split-bf16 panels, or its padded transpose for the sparse KL kernels (GPU only; the
+        CPU reference works on the fp32 factor directly)."""
+        if F3.device.type != "cuda":
+            return None
+        if self._kl_sparse() is not None:
+            return ops.kl_st(F3)
+        return ops.beta_panels(F3, self.beta)
 
-    def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, panels=None):
+    def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, panels=None, rows=None):
         """One fused MU step of the usages H3c (R, K, c) in place against W3 on rows xc
         (replicates with act == 0 untouched)."""
+        csr = self._kl_sparse() if rows is not None else None
+        if csr is not None:
+            ops.kl_sparse_h_block(ops.kl_csr_rows(csr, *rows), H3c, W3, self.opts.eps, 1, l1,
+                                  l2, act=act, st=panels)
+            return
         ops.beta_h_block(xc, H3c, W3, self.beta, self.opts.eps, 1, l1, l2, self._beta_gamma(),
                          act=act, panels=panels)
 
-    def _beta_h_solve(self, xc, hc, W3, act, iters, wpan=None, block: int = 8) -> None:
+    def _beta_h_solve(self, xc, hc, W3, act, iters, wpan=None, block: int = 8,
+                      rows=None) -> None:
         """Inner usage loop of one chunk: up to ``online_chunk_max_iter`` fused MU steps.
         With ``online_inner_conv='loss'`` (default) one launch runs ``inner_check_every``
         steps, and the block objective -- the chunk's beta-divergence after the block
@@ -1910,8 +1957,9 @@ class NMFBatchSolver:
         cuda = xc.device.type == "cuda"
         den_vec = (W3.sum(dim=2, dtype=torch.float32).contiguous()
                    if self.beta == 1.0 and cuda else None)
+        csr = self._kl_sparse() if (cuda and rows is not None) else None
         if cuda and wpan is None:
-            wpan = ops.beta_panels(W3)
+            wpan = ops.kl_st(W3) if csr is not None else ops.beta_panels(W3, self.beta)
         cmode = 1 if o.online_inner_conv == "loss" else 0
         per = max(1, int(o.inner_check_every)) if cmode == 1 else 1
         group = 1 if cmode == 1 else block
@@ -1926,10 +1974,18 @@ class NMFBatchSolver:
                 if it >= max_it:
                     break
                 m = min(per, max_it - it)
-                ops.beta_h_block(xc, hc, W3, self.beta, o.eps, m, o.l1_H, o.l2_H,
-                                 self._beta_gamma(), act=act, tol=o.online_h_tol, iters=iters,
-                                 conv_mode=cmode, hstate=hstate, loss_entry=first,
-                                 den_vec=den_vec, panels=wpan, xsum=xsum)
+                if csr is not None:
+                    ops.kl_sparse_h_block(ops.kl_csr_rows(csr, *rows), hc, W3, o.eps, m,
+                                          o.l1_H, o.l2_H, act=act, tol=o.online_h_tol,
+                                          iters=iters, conv_mode=cmode, hstate=hstate,
+                                          loss_entry=first, den_vec=den_vec, st=wpan,
+                                          xsum=xsum)
+                else:
+                    ops.beta_h_block(xc, hc, W3, self.beta, o.eps, m, o.l1_H, o.l2_H,
+                                     self._beta_gamma(), act=act, tol=o.online_h_tol,
+                                     iters=iters, conv_mode=cmode, hstate=hstate,
+                                     loss_entry=first, den_vec=den_vec, panels=wpan,
+                                     xsum=xsum)
                 first = False
                 it += m
             if not cuda:
@@ -1946,9 +2002,9 @@ class NMFBatchSolver:
                 if int(prev[1][0]) == 0:
                     break
 
-    def _beta_w_stats(self, xc, H3c, W3, xtc=None, active=None):
+    def _beta_w_stats(self, xc, H3c, W3, xtc=None, active=None, rows=None):
         """(num, den) W-side MU statistics of rows xc (den broadcastable to (R,K,G))."""
-        num, den = self._beta_w_partials(xc, xtc, H3c, W3, active)
+        num, den = self._beta_w_partials(xc, xtc, H3c, W3, active, rows=rows)
         num = num.sum(0)
         if den is None:
             den = H3c.sum(dim=2, keepdim=True)              # KL: row sums of H
@@ -1986,10 +2042,11 @@ class NMFBatchSolver:
         act = live.clone()
         cuda = dev.type == "cuda"
         dist = self.comm.is_distributed
-        XT = self._xt()
+        sparse = cuda and self._kl_sparse() is not None
+        XT = None if sparse else self._xt()
         # the chunk's usages stay fixed over the spectra iterations: split them once
         hpan = {(a, b): self._beta_panels(H3[:, :, a:b]) for (a, b) in rows} \
-            if XT is not None else {}
+            if (XT is not None or sparse) else {}
         max_it = int(o.online_chunk_max_iter)
         pending = None
         it = 0
@@ -2000,7 +2057,8 @@ class NMFBatchSolver:
                 for (a, b) in rows:
                     nW, dW = self._beta_w_partials(X[a:b],
                                                    XT[:, a:b] if XT is not None else None,
-                                                   H3[:, :, a:b], W3, act, hpan.get((a, b)))
+                                                   H3[:, :, a:b], W3, act, hpan.get((a, b)),
+                                                   rows=(a, b))
                     if num is None:
                         num, den = nW, dW
                     else:   # several blocks of one step (single-process DP emulation)
@@ -2041,7 +2099,12 @@ class NMFBatchSolver:
         (no host round trip; all-reduced under DP)."""
         R = W.shape[0] // K
         N, G = self.X.shape
-        tot = ops.beta_loss(self.X, HT.view(R, K, N), W.view(R, K, G), self.beta, self.opts.eps)
+        csr = self._kl_sparse() if HT.device.type == "cuda" else None
+        if csr is not None:
+            tot = ops.kl_sparse_loss(csr, HT.view(R, K, N), W.view(R, K, G), self.opts.eps)
+        else:
+            tot = ops.beta_loss(self.X, HT.view(R, K, N), W.view(R, K, G), self.beta,
+                                self.opts.eps)
         tot = tot.to(torch.float64).contiguous()
         self.comm.allreduce_(tot)
         return torch.sqrt(torch.clamp(2.0 * tot, min=0.0))
@@ -2085,7 +2148,8 @@ class NMFBatchSolver:
                     if b <= a:
                         continue
                     act = live.clone()
-                    self._beta_h_solve(X[a:b], H3[:, :, a:b], W3, act, st.h_iters[:n], wpan)
+                    self._beta_h_solve(X[a:b], H3[:, :, a:b], W3, act, st.h_iters[:n], wpan,
+                                       rows=(a, b))
                 an, dn = self._beta_w_solve(blocks, H3, W3, An, Ad, live, st.w_iters[:n])
                 An += torch.where(keep, an, 0.0)
                 Ad += torch.where(keep_d, dn, 0.0)
@@ -2114,8 +2178,10 @@ class NMFBatchSolver:
             # finished replicates may sit in the batch until the next (stale-flag)
             # compaction: the active flags gate both updates and the iteration counts
             live = st.active_mask().clone()
-            self._beta_h_update(X, H3, W3, o.l1_H, o.l2_H, act=live)
-            nW, dW = self._beta_w_stats(X, H3, W3, self._xt(), active=live)
+            sparse = X.device.type == "cuda" and self._kl_sparse() is not None
+            self._beta_h_update(X, H3, W3, o.l1_H, o.l2_H, act=live, rows=(0, N))
+            nW, dW = self._beta_w_stats(X, H3, W3, None if sparse else self._xt(), active=live,
+                                        rows=(0, N))
             if comm.is_distributed:
                 flat = torch.cat([nW.reshape(-1), dW.expand(n, K, G).reshape(-1)])
                 comm.allreduce_(flat)

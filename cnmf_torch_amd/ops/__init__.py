@@ -14,6 +14,7 @@ from __future__ import annotations
 import contextlib
 import os
 import threading
+from typing import NamedTuple
 
 import numpy as np
 import torch
@@ -54,7 +55,7 @@ def _require_native():
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
 _ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
              "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES", "CNMF_GEMM_BK",
-             "CNMF_GEMM_SMALL", "CNMF_SOLVE_PIPE")
+             "CNMF_GEMM_SMALL", "CNMF_SOLVE_PIPE", "CNMF_BP_KL_CT")
 _ENV: dict = {}
 
 
@@ -62,6 +63,11 @@ def refresh_env() -> None:
     """Re-read the CNMF_* per-op knobs from the environment."""
     _ENV.clear()
     _ENV.update({k: os.environ.get(k) for k in _ENV_KEYS})
+    set_ct = getattr(_hip, "bp_set_kl_ct", None)   # absent from a stale build
+    if set_ct is not None:
+        # column tiles per wave of the KL beta kernels (beta_planes.hip; default 2:
+        # 325 vs 290 rep/s with 1 at the headline, profiles/r3l_*)
+        set_ct(int(_ENV["CNMF_BP_KL_CT"] or 2))
 
 
 refresh_env()
@@ -738,20 +744,30 @@ def _bp_check(name: str, t: torch.Tensor, dev) -> None:
                          f"{t.dtype} {tuple(t.stride())} on {t.device}")
 
 
-def beta_panels(F3: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """Split-bf16 operand panels of F3 (R, K, L), unit inner stride, K <= 32
-    (beta_planes.hip bp_panel_kernel): per replicate, chunks of 64 rows of the L axis,
-    each holding the three bf16 planes of the 6-term product layout and the two planes
-    of the permuted second-product layout.  Returns (R, panel_elems) int16."""
+def beta_panels(F3: torch.Tensor, beta: float, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Split operand panels of F3 (R, K, L), unit inner stride, K <= 32, for the beta-MU
+    kernels at ``beta`` (beta_planes.hip bp_panel_kernel): per replicate, chunks of 64 rows
+    of the L axis, each holding the bf16 planes of the P-product layout (6 terms; KL 3) and
+    the two planes of the permuted numerator layout (KL: fp16, row-scaled, with the scales
+    in a tail).  Returns (R, panel_elems) int16."""
     R, K, L = F3.shape
     _native_dtype_k("beta_panels", F3.dtype, K, _hip.bp_max_k())
     _bp_check("F3", F3, F3.device)
-    n = int(_hip.bp_panel_elems(K, L))
+    mode = beta_mode(beta)
+    n = int(_hip.bp_panel_elems(K, L, mode))
     if out is None or out.shape != (R, n) or out.dtype != torch.int16 or not out.is_contiguous():
         out = torch.empty((R, n), dtype=torch.int16, device=F3.device)
-    _hip.bp_panels(F3.data_ptr(), F3.stride(0), F3.stride(1), K, L, R, out.data_ptr(), n,
+    _hip.bp_panels(F3.data_ptr(), F3.stride(0), F3.stride(1), K, L, R, mode, out.data_ptr(), n,
                    _stream_ptr(F3))
     return out
+
+
+def _bp_panels_check(panels: torch.Tensor, R: int, K: int, L: int, mode: int) -> None:
+    n = int(_hip.bp_panel_elems(K, L, mode))
+    if (panels.dim() != 2 or panels.shape[0] < R or panels.shape[1] != n
+            or panels.dtype != torch.int16 or panels.stride(1) != 1):
+        raise ValueError(f"panels: int16 (R, {n}) for K={K}, L={L}, beta mode {mode} required "
+                         f"(beta_panels with the same beta), got {tuple(panels.shape)}")
 
 
 def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float, eps: float,
@@ -804,8 +820,9 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
     else:
         den_vec = None
     if panels is None:
-        panels = beta_panels(W3)
-    n_strips = -(-N // int(_hip.bp_strip_cols(K)))
+        panels = beta_panels(W3, beta)
+    _bp_panels_check(panels, R, K, G, mode)
+    n_strips = -(-N // int(_hip.bp_strip_cols(K, mode)))
     part = counter = 0
     if tol is not None:
         ws = _bp_ws(dev, _stream_ptr(HT3), R, n_strips)
@@ -843,12 +860,13 @@ def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float,
     if active is not None and (active.dtype != torch.int32 or active.numel() < R
                                or not active.is_contiguous()):
         raise ValueError("active: contiguous int32 with >= R entries")
-    if panels is None:
-        panels = beta_panels(W3)
     mode = beta_mode(beta)
+    if panels is None:
+        panels = beta_panels(W3, beta)
+    _bp_panels_check(panels, R, K, G, mode)
     # KL: the kernel sums x log(x/p) + p; the -sum(x) term is added here on the device
     wsum = W3.sum(dim=2, dtype=torch.float32).contiguous() if mode == 0 else None
-    n_strips = -(-N // int(_hip.bp_strip_cols(K)))
+    n_strips = -(-N // int(_hip.bp_strip_cols(K, mode)))
     loss = torch.zeros((R, n_strips), dtype=torch.float64, device=dev)
     _hip.bp_run(0, mode, X.data_ptr(), X.stride(0), panels.data_ptr(),
                 panels.stride(0), HT3.data_ptr(), HT3.stride(0), HT3.stride(1), K, N, G, R, 1,
@@ -886,11 +904,12 @@ def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
     if active is not None and (active.dtype != torch.int32 or active.numel() < R
                                or not active.is_contiguous()):
         raise ValueError("active: contiguous int32 with >= R entries")
-    if panels is None:
-        panels = beta_panels(HT3)
     mode = beta_mode(beta)
+    if panels is None:
+        panels = beta_panels(HT3, beta)
+    _bp_panels_check(panels, R, K, c, mode)
     if splits is None:
-        units = -(-G // int(_hip.bp_strip_cols(K))) * R
+        units = -(-G // int(_hip.bp_strip_cols(K, mode))) * R
         splits = max(1, min(16, -(-2048 // max(1, units))))
     n_split = int(_hip.bp_splits(c, int(splits)))
     num = torch.empty((n_split, R, K, G), dtype=torch.float32, device=dev)
@@ -901,6 +920,160 @@ def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
                 0, 0.0, 0.0, 1.0, 0.0, 0, 0, 0, 0, 0, 0,
                 active.data_ptr() if active is not None else 0, 0, 0.0, _stream_ptr(HT3))
     return num, den
+
+
+# ------------------------------------------------------------- sparse KL (CSR X)
+class KLCSR(NamedTuple):
+    """CSR of a non-negative matrix for the sparse KL kernels (sparse_kl.hip): row i owns
+    entries [rowptr[i], rowptr[i+1]) of col / val; a row range is a rowptr slice over the
+    same col / val (:func:`kl_csr_rows`)."""
+    rowptr: torch.Tensor    # int32 (n_rows + 1,), absolute offsets
+    col: torch.Tensor       # int32
+    val: torch.Tensor       # float32
+    n_rows: int
+    n_cols: int
+
+
+def kl_csr(X: torch.Tensor) -> KLCSR:
+    """CSR (x != 0 entries, row-major) of a dense float32 matrix on the device (one
+    nonzero() host sync)."""
+    n, m = X.shape
+    rows, cols = torch.nonzero(X, as_tuple=True)
+    rowptr = torch.zeros(n + 1, dtype=torch.int64, device=X.device)
+    rowptr[1:] = torch.bincount(rows, minlength=n).cumsum(0)
+    return KLCSR(rowptr.to(torch.int32), cols.to(torch.int32).contiguous(),
+                 X[rows, cols].to(torch.float32).contiguous(), n, m)
+
+
+def kl_csr_rows(csr: KLCSR, a: int, b: int) -> KLCSR:
+    return KLCSR(csr.rowptr[a:b + 1], csr.col, csr.val, b - a, csr.n_cols)
+
+
+def kl_tile_rows(K: int) -> int:
+    """Streamed rows per LDS tile of the sparse KL kernels (S^T staged in 128 KB)."""
+    return (128 * 1024 // (4 * int(_hip.sk_k4(K)))) // 64 * 64
+
+
+def kl_csr_tiles(Xc: torch.Tensor, K: int) -> list:
+    """The spectra-side CSRs of a row chunk Xc (c, G): [(t0, CSR of Xc[t0:t1]^T)] over
+    tiles of :func:`kl_tile_rows` cells, each sized to have its usages staged in LDS."""
+    c = Xc.shape[0]
+    tl = kl_tile_rows(K)
+    return [(t0, kl_csr(Xc[t0:min(c, t0 + tl)].t())) for t0 in range(0, c, tl)]
+
+
+def kl_st(F3: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """(R, L, K4) transpose of F3 (R, K, L), rows zero-padded to K4 = 4 ceil(K / 4) (the
+    sparse KL kernels gather one float4-aligned row per non-zero)."""
+    R, K, L = F3.shape
+    K4 = int(_hip.sk_k4(K))
+    if out is None or out.shape != (R, L, K4) or not out.is_contiguous():
+        out = torch.zeros((R, L, K4), dtype=torch.float32, device=F3.device)
+    out[:, :, :K].copy_(F3.transpose(1, 2))
+    return out
+
+
+def _sk_args(csr: KLCSR, F3: torch.Tensor, S3: torch.Tensor, st: torch.Tensor | None):
+    R, K, Lf = F3.shape
+    Ls = S3.shape[2]
+    if csr.n_rows != Lf or csr.n_cols != Ls or csr.rowptr.dtype != torch.int32:
+        raise ValueError(f"CSR {csr.n_rows} x {csr.n_cols} does not match fixed {Lf} x "
+                         f"streamed {Ls}")
+    _native_dtype_k("sparse KL", F3.dtype, K, 32)
+    for name, t in (("F3", F3), ("S3", S3)):
+        _bp_check(name, t, F3.device)
+    if st is None:
+        st = kl_st(S3)
+    if (st.shape != (R, Ls, int(_hip.sk_k4(K))) or st.stride(2) != 1
+            or st.stride(1) != st.shape[2] or st.data_ptr() % 16):
+        raise ValueError("st: kl_st(S3) (or a row range of it) required")
+    return st
+
+
+def kl_sparse_h_block(csr: KLCSR, HT3: torch.Tensor, W3: torch.Tensor, eps: float,
+                      nsteps: int, l1: float = 0.0, l2: float = 0.0,
+                      act: torch.Tensor | None = None, tol: float | None = None,
+                      iters: torch.Tensor | None = None, conv_mode: int = 1,
+                      hstate: torch.Tensor | None = None, loss_entry: bool = False,
+                      den_vec: torch.Tensor | None = None, st: torch.Tensor | None = None,
+                      xsum: float | None = None) -> None:
+    """:func:`beta_h_block` at beta = 1 over the CSR rows ``csr`` (cells x genes) of X:
+    ``nsteps`` fused KL MU steps of HT3 (R, K, c) in place against W3 (R, K, G), the same
+    on-device stopping rule (sparse_kl.hip side 0).  ``st``: :func:`kl_st` of W3."""
+    R, K, N = HT3.shape
+    if tol is not None and act is None:
+        raise ValueError("the stopping rule needs an act array")
+    if tol is not None and conv_mode == 1 and (
+            hstate is None or hstate.dtype != torch.float64 or hstate.numel() < 2 * R):
+        raise ValueError("conv_mode 1 needs hstate: contiguous float64 (R, 2)")
+    _require_native()
+    st = _sk_args(csr, HT3, W3, st)
+    if den_vec is None:
+        den_vec = W3.sum(dim=2, dtype=torch.float32).contiguous()
+    part = counter = 0
+    if tol is not None:
+        ws = _bp_ws(HT3.device, _stream_ptr(HT3), R, int(_hip.sk_groups(N, R, W3.shape[2], K)))
+        part, counter = ws["part"].data_ptr(), ws["counter"].data_ptr()
+    rule_loss = tol is not None and conv_mode == 1
+    if rule_loss and xsum is None:
+        xsum = float(csr.val[int(csr.rowptr[0]):int(csr.rowptr[-1])].sum(dtype=torch.float64))
+    _hip.sk_run(0, csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.val.data_ptr(), st.data_ptr(),
+                st.stride(0), HT3.data_ptr(), HT3.stride(0), HT3.stride(1), K, N, W3.shape[2], R,
+                float(eps),
+                0, int(nsteps), int(bool(loss_entry) and tol is not None), int(rule_loss),
+                den_vec.data_ptr(), float(l1), float(l2),
+                float(tol if tol is not None else 0.0), int(conv_mode),
+                hstate.data_ptr() if (hstate is not None and tol is not None) else 0, part,
+                counter, act.data_ptr() if act is not None else 0,
+                iters.data_ptr() if (iters is not None and tol is not None) else 0,
+                act.data_ptr() if act is not None else 0, 0,
+                float(xsum if xsum is not None else 0.0), _stream_ptr(HT3))
+
+
+def kl_sparse_loss(csr: KLCSR, HT3: torch.Tensor, W3: torch.Tensor, eps: float,
+                   active: torch.Tensor | None = None,
+                   st: torch.Tensor | None = None) -> torch.Tensor:
+    """sum D_KL(X || HT3^T W3) per replicate over the CSR rows ``csr``, float64 (R,)."""
+    R, K, N = HT3.shape
+    _require_native()
+    st = _sk_args(csr, HT3, W3, st)
+    wsum = W3.sum(dim=2, dtype=torch.float32).contiguous()
+    loss = torch.zeros((R, int(_hip.sk_groups(N, R, W3.shape[2], K))), dtype=torch.float64,
+                       device=HT3.device)
+    _hip.sk_run(0, csr.rowptr.data_ptr(), csr.col.data_ptr(), csr.val.data_ptr(), st.data_ptr(),
+                st.stride(0), HT3.data_ptr(), HT3.stride(0), HT3.stride(1), K, N, W3.shape[2], R,
+                float(eps),
+                0, 0, 0, 1, wsum.data_ptr(), 0.0, 0.0, 0.0, 0, 0, 0, 0, 0, 0,
+                active.data_ptr() if active is not None else 0, loss.data_ptr(), 0.0,
+                _stream_ptr(HT3))
+    lo, hi = int(csr.rowptr[0]), int(csr.rowptr[-1])
+    return loss.sum(1) - csr.val[lo:hi].sum(dtype=torch.float64)
+
+
+def kl_sparse_w_num(tiles: list, HT3: torch.Tensor, W3: torch.Tensor, eps: float,
+                    active: torch.Tensor | None = None,
+                    st: torch.Tensor | None = None) -> torch.Tensor:
+    """KL spectra numerators num = HT Q over a row chunk given as :func:`kl_csr_tiles`
+    (cells tiled so that each tile's usages fit in LDS), as (tiles, R, K, G) partials -- the
+    :func:`beta_w_partials` layout (sparse_kl.hip side 1).  ``st``: :func:`kl_st` of HT3."""
+    R, K, c = HT3.shape
+    G = W3.shape[2]
+    _require_native()
+    if st is None:
+        st = kl_st(HT3)
+    if active is not None and (active.dtype != torch.int32 or active.numel() < R):
+        raise ValueError("active: contiguous int32 with >= R entries")
+    num = torch.empty((len(tiles), R, K, G), dtype=torch.float32, device=W3.device)
+    for i, (t0, csrT) in enumerate(tiles):
+        t1 = t0 + csrT.n_cols
+        _sk_args(csrT, W3, HT3[:, :, t0:t1], st[:, t0:t1])
+        sub = st[:, t0:t1]
+        _hip.sk_run(1, csrT.rowptr.data_ptr(), csrT.col.data_ptr(), csrT.val.data_ptr(),
+                    sub.data_ptr(), sub.stride(0), W3.data_ptr(), W3.stride(0), W3.stride(1), K,
+                    G, t1 - t0, R, float(eps), num[i].data_ptr(), 1, 0, 0, 0, 0.0, 0.0, 0.0, 0,
+                    0, 0, 0, 0, 0, active.data_ptr() if active is not None else 0, 0, 0.0,
+                    _stream_ptr(W3))
+    return num
 
 
 # ----------------------------------------------------------------------------- gram

@@ -112,13 +112,15 @@ PYBIND11_MODULE(_hip, m) {
         });
 
   m.def("bp_max_k", []() { return cnmf_bp_max_k(); });
-  m.def("bp_panel_elems", [](int K, int L) { return cnmf_bp_panel_elems(K, L); });
-  m.def("bp_strip_cols", [](int K) { return cnmf_bp_strip_cols(K); });
+  m.def("bp_panel_elems",
+        [](int K, int L, int mode) { return cnmf_bp_panel_elems(K, L, mode); });
+  m.def("bp_strip_cols", [](int K, int mode) { return cnmf_bp_strip_cols(K, mode); });
+  m.def("bp_set_kl_ct", [](int ct) { return cnmf_bp_set_kl_ct(ct); });
   m.def("bp_splits", [](int Ls, int splits) { return cnmf_bp_splits(Ls, splits); });
   m.def("bp_panels",
-        [](uintptr_t F, long long f_rs, long long ldf, int K, int L, int R, uintptr_t out,
-           long long out_rs, uintptr_t stream) {
-          check(cnmf_bp_panels(P<const float>(F), f_rs, ldf, K, L, R, P<unsigned short>(out),
+        [](uintptr_t F, long long f_rs, long long ldf, int K, int L, int R, int mode,
+           uintptr_t out, long long out_rs, uintptr_t stream) {
+          check(cnmf_bp_panels(P<const float>(F), f_rs, ldf, K, L, R, mode, P<unsigned short>(out),
                                out_rs, reinterpret_cast<hipStream_t>(stream)),
                 "bp_panels");
         });
@@ -137,6 +139,25 @@ PYBIND11_MODULE(_hip, m) {
                             P<int>(iters), P<const int>(active), P<double>(loss), xsum,
                             reinterpret_cast<hipStream_t>(stream)),
                 "bp_run");
+        });
+  m.def("sk_k4", [](int K) { return cnmf_sk_k4(K); });
+  m.def("sk_groups", [](int Lf, int R, int Ls, int K) { return cnmf_sk_groups(Lf, R, Ls, K); });
+  m.def("sk_lds", [](int Ls, int K) { return cnmf_sk_lds(Ls, K); });
+  m.def("sk_run",
+        [](int side, uintptr_t rowptr, uintptr_t col, uintptr_t val, uintptr_t ST,
+           long long st_rs, uintptr_t F, long long f_rs, long long ldf, int K, int Lf, int Ls,
+           int R, float eps, uintptr_t num, int nsteps, int loss_entry, int loss_exit,
+           uintptr_t den_vec, float l1, float l2, float tol, int conv_mode, uintptr_t hstate,
+           uintptr_t part, uintptr_t counter, uintptr_t act, uintptr_t iters, uintptr_t active,
+           uintptr_t loss, double xsum, uintptr_t stream) {
+          check(cnmf_sk_run(side, P<const int>(rowptr), P<const int>(col), P<const float>(val),
+                            P<const float>(ST), st_rs, P<float>(F), f_rs, ldf, K, Lf, Ls, R, eps,
+                            P<float>(num), nsteps, loss_entry, loss_exit,
+                            P<const float>(den_vec), l1, l2, tol, conv_mode, P<double>(hstate),
+                            P<double>(part), P<int>(counter), P<int>(act), P<int>(iters),
+                            P<const int>(active), P<double>(loss), xsum,
+                            reinterpret_cast<hipStream_t>(stream)),
+                "sk_run");
         });
 
   m.def("pairdist", [](uintptr_t A, long long lda, uintptr_t B, long long ldb, uintptr_t na,

@@ -30,6 +30,22 @@
 //   <= 3 * 2^-16 relative per term, with random sign -- inside the fp32 accumulation
 //   error of the 2000-long reduction (the split-GEMM argument of gemm_planes.hip).
 //
+// KL (the reference CLI's common non-Frobenius loss) runs a cheaper variant of both
+// products, since its VALU work per element (rcp, mul, split) bounds the kernel, not the MFMAs:
+// * P from the three plane products {S0F0, S0F1, S1F0} only (relative error <= ~3 * 2^-16,
+//   far below the Q rounding below): 3K slots, so K <= 10 costs ONE MFMA per tile.
+// * Q = X / P goes into ONE fp16 plane (v_cvt_pk_f16_f32: half an instruction per element
+//   instead of the two-plane split's three), S into two fp16 planes scaled per row k by a
+//   power of two 2^-e_k (its max -> [0.5, 1): bp_rowscale_kernel), num = S0 Q + S1 Q on
+//   v_mfma_f32_16x16x32_f16.  Per term the error is <= 2^-11 relative (random sign):
+//   simulated over 200 batch KL MU iterations (2000 x 2000, K = 10) the factors drift
+//   1.8e-5 relative from an fp32 run and the objective 1e-8 (tests/test_kernels_gpu.py
+//   pins the online solver against the fp32 torch path).  fp16 has a narrower range than fp32:
+//   Q is computed as x / (2^s P) with a per-column shift s (F's planes and eps scaled
+//   by 2^s, exactly), s = 0 to start with (x / P stays below ~200 on count data), and a
+//   step whose numerator comes out non-finite for some column is redone with that
+//   column's s raised by 12 (at most 6 times), so overflow never reaches the result.
+//
 // The H-side kernel runs `nsteps` MU steps per launch: every workgroup's cells only
 // depend on their own usages and on W, so the steps need no cross-workgroup
 // synchronisation; the updated usages go back into the B-operand planes through a small
@@ -47,6 +63,7 @@ namespace cnmf {
 
 typedef short bp_v8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bp_b8 __attribute__((ext_vector_type(8)));
+typedef _Float16 bp_h8 __attribute__((ext_vector_type(8)));
 typedef float bp_f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int bp_u4 __attribute__((ext_vector_type(4)));
 
@@ -55,7 +72,15 @@ constexpr int kBpWaves = 4;        // waves per workgroup
 constexpr int kBpThreads = 64 * kBpWaves;
 constexpr int kBpNS = kBpCH + 8;   // N-panel row stride (bf16 elements)
 
-__host__ __device__ constexpr int bp_np(int K) { return (6 * K + 31) / 32; }
+enum BpMode { kBpKL = 0, kBpIS = 1, kBpGeneral = 2 };
+
+// plane-product terms of P: KL 3, IS / general beta 6 (exact to fp32 rounding)
+__host__ __device__ constexpr int bp_nt(int mode) { return mode == kBpKL ? 3 : 6; }
+__host__ __device__ constexpr int bp_np(int K, int mode = kBpIS) {
+  return (bp_nt(mode) * K + 31) / 32;
+}
+// per-replicate panel tail (KL): 32 row scales 2^-e_k and their inverses, fp32
+constexpr int kBpTail = 128;
 __host__ __device__ constexpr int bp_t(int K) { return (K + 15) / 16; }
 __host__ __device__ constexpr int bp_ps(int NP) { return 32 * NP + 8; }  // P-panel row stride
 // chunk stride (bf16 elements), padded to whole 16-byte pieces per thread so the staging
@@ -64,10 +89,13 @@ __host__ __device__ constexpr int bp_chunk(int NP, int T) {
   return (kBpCH * bp_ps(NP) + 2 * 16 * T * kBpNS + kBpThreads * 8 - 1) / (kBpThreads * 8) *
          (kBpThreads * 8);
 }
-__host__ __device__ constexpr int bp_ct(int T) { return 2; }  // column tiles per wave (4: 820 vs 510 us per usage step)
+// column tiles per wave: 2 (4: 820 vs 510 us per usage step).  The KL kernels can run 1
+// (cnmf_bp_set_kl_ct): fewer live registers (3-4 waves per SIMD instead of 2) and twice
+// the workgroups, but measured slower (290 vs 325 rep/s at the headline: the panel
+// chunks in LDS then serve 64 columns instead of 128)
+__host__ __device__ constexpr int bp_ct(int T) { return 2; }
+static int g_bp_kl_ct = 2;
 __host__ __device__ constexpr int bp_ks(int T) { return 16 * T + 1; }     // exchange stride
-
-enum BpMode { kBpKL = 0, kBpIS = 1, kBpGeneral = 2 };
 
 // plane of the streamed (a) / fixed (b) operand in product term t (0..5)
 __device__ __forceinline__ int bp_pa(int t) { return (0x210100 >> (4 * t)) & 15; }
@@ -94,11 +122,14 @@ __device__ __forceinline__ void bp_split3(float v, unsigned short& p0, unsigned 
 // streamed rows [64c, 64c + 64), zero beyond L:
 //   P panel  [64 rows][bp_ps(NP)]:  row l, slot t*K + k = plane bp_pa(t) of F[k][l]
 //   N panel  [2 planes][16T rows k][kBpNS]: plane p of F[k][l] at the permuted column of l
-//            (within a 32-row block: offset o = 16h + 4q + i  ->  8q + 4h + i)
+//            (within a 32-row block: offset o = 16h + 4q + i  ->  8q + 4h + i); KL: the
+//            two fp16 planes of F[k][l] * 2^-e_k instead
+//   (KL) tail [kBpTail]: fp32 2^-e_k (k < 32), then 2^e_k
 __global__ void __launch_bounds__(256) bp_panel_kernel(const float* __restrict__ F,
                                                        long long f_rs, long long ldf, int K,
                                                        int L, int nchunks, int R, int NP,
-                                                       int T, unsigned short* __restrict__ out,
+                                                       int T, int nt, int kl,
+                                                       unsigned short* __restrict__ out,
                                                        long long out_rs) {
   const long long per = (long long)nchunks * kBpCH;
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -106,6 +137,7 @@ __global__ void __launch_bounds__(256) bp_panel_kernel(const float* __restrict__
   const int r = (int)(idx / per), l = (int)(idx - (long long)r * per);
   const int PS = bp_ps(NP), CE = bp_chunk(NP, T);
   unsigned short* ch = out + r * out_rs + (long long)(l / kBpCH) * CE;
+  const float* rsc = reinterpret_cast<const float*>(out + r * out_rs + (long long)nchunks * CE);
   const int lr = l % kBpCH, o = lr & 31;
   unsigned short* prow = ch + lr * PS;
   unsigned short* np0 = ch + kBpCH * PS;
@@ -113,20 +145,57 @@ __global__ void __launch_bounds__(256) bp_panel_kernel(const float* __restrict__
   const int pos = (lr & 32) + ((o & 15) >> 2) * 8 + (o >> 4) * 4 + (o & 3);
   const float* f = F + r * f_rs + l;
   for (int k = 0; k < 16 * T; ++k) {
-    unsigned short a0 = 0, a1 = 0, a2 = 0;
-    if (k < K && l < L) bp_split3(f[(long long)k * ldf], a0, a1, a2);
-    if (k < K) {
-      prow[k] = a0;
-      prow[K + k] = a0;
-      prow[2 * K + k] = a1;
-      prow[3 * K + k] = a0;
-      prow[4 * K + k] = a1;
-      prow[5 * K + k] = a2;
+    unsigned short a0 = 0, a1 = 0, a2 = 0, n0 = 0, n1 = 0;
+    if (k < K && l < L) {
+      const float v = f[(long long)k * ldf];
+      bp_split3(v, a0, a1, a2);
+      if (kl) {
+        const float s = v * rsc[k];
+        const _Float16 h0 = (_Float16)s;
+        n0 = __builtin_bit_cast(unsigned short, h0);
+        n1 = __builtin_bit_cast(unsigned short, (_Float16)(s - (float)h0));
+      } else {
+        n0 = a0;
+        n1 = a1;
+      }
     }
-    np0[k * kBpNS + pos] = a0;
-    np1[k * kBpNS + pos] = a1;
+    if (k < K)
+      for (int t = 0; t < nt; ++t) {
+        const int pl = bp_pa(t);
+        prow[t * K + k] = pl == 0 ? a0 : (pl == 1 ? a1 : a2);
+      }
+    np0[k * kBpNS + pos] = n0;
+    np1[k * kBpNS + pos] = n1;
   }
-  for (int s = 6 * K; s < PS; ++s) prow[s] = 0;
+  for (int s = nt * K; s < PS; ++s) prow[s] = 0;
+}
+
+// KL panel row scales: per replicate r and row k < K, 2^-e_k with max_l |F[r][k][l]| * 2^-e_k
+// in [0.5, 1) (1 for an all-zero or non-finite row) and its inverse, into the panel tail.
+// One workgroup per replicate.
+__global__ void __launch_bounds__(256) bp_rowscale_kernel(const float* __restrict__ F,
+                                                          long long f_rs, long long ldf, int K,
+                                                          int L, unsigned short* __restrict__ out,
+                                                          long long out_rs, long long tail) {
+  __shared__ float red[4];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const float* f = F + r * f_rs;
+  float* dst = reinterpret_cast<float*>(out + r * out_rs + tail);
+  for (int k = 0; k < K; ++k) {
+    float m = 0.f;
+    for (int l = tid; l < L; l += 256) m = fmaxf(m, fabsf(f[(long long)k * ldf + l]));
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) {
+      const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      int e = 0;
+      if (mx > 0.f && mx <= 3.0e38f) frexpf(mx, &e);
+      dst[k] = ldexpf(1.f, -e);
+      dst[32 + k] = ldexpf(1.f, e);
+    }
+    __syncthreads();
+  }
 }
 
 // ------------------------------------------------------------------------------ main op
@@ -219,15 +288,16 @@ __device__ __forceinline__ void bp_load4(const float* __restrict__ row, int j, i
   }
 }
 
-template <int NP, int T, int MODE, bool UPD>
+template <int NP, int T, int MODE, bool UPD, int CT>
 __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
-  constexpr int CT = bp_ct(T);
   constexpr int PS = bp_ps(NP);
   constexpr int CE = bp_chunk(NP, T);
   constexpr int PIECES = CE * 2 / 16;
   constexpr int PER_T = (PIECES + kBpThreads - 1) / kBpThreads;
   constexpr int COLS = kBpWaves * CT * 16;
   constexpr int KS = bp_ks(T);
+  constexpr bool kH = MODE == kBpKL;   // fp16 numerator path (see the file comment)
+  constexpr int NT = bp_nt(MODE);
   static_assert(PIECES == PER_T * kBpThreads, "chunk must be whole pieces per thread");
   extern __shared__ __attribute__((aligned(16))) unsigned char bp_smem[];
   __shared__ double sred[4 * kBpWaves];
@@ -262,6 +332,24 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
     xrow[ct] = p.X + (long long)(cok[ct] ? col : 0) * p.ldx;
   }
 
+  // KL: per-column shift 2^s of F (csc) and s (csg); inverse panel row scales 2^e_k
+  float csc[CT], csg[CT], rinv[T][4];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    csc[ct] = 1.f;
+    csg[ct] = 0.f;
+  }
+  if (kH) {
+    const float* tail = reinterpret_cast<const float*>(pan + (long long)nch_all * CE);
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = 16 * t + 4 * q + i;
+        rinv[t][i] = k < K ? tail[32 + k] : 0.f;
+      }
+  }
+
   // fixed operand in the accumulator layout: hc[ct][t][i] = F[16t + 4q + i][col]
   bp_f4 hc[CT][T];
 #pragma unroll
@@ -283,7 +371,8 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
 #pragma unroll
       for (int t = 0; t < T; ++t)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sx[(16 * ct + m) * KS + 16 * t + 4 * q + i] = hc[ct][t][i];
+        for (int i = 0; i < 4; ++i)
+          sx[(16 * ct + m) * KS + 16 * t + 4 * q + i] = kH ? hc[ct][t][i] * csc[ct] : hc[ct][t][i];
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
@@ -291,11 +380,11 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
       int tt = s0 / K, kk = s0 - tt * K;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int pl = bp_pb(tt < 6 ? tt : 0);
+        const int pl = bp_pb(tt < NT ? tt : 0);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
           unsigned short a0 = 0, a1 = 0, a2 = 0;
-          if (tt < 6) bp_split3(sx[(16 * ct + m) * KS + kk], a0, a1, a2);
+          if (tt < NT) bp_split3(sx[(16 * ct + m) * KS + kk], a0, a1, a2);
           freg[ct][j][e] = (short)(pl == 0 ? a0 : (pl == 1 ? a1 : a2));
         }
         if (++kk == K) { kk = 0; ++tt; }
@@ -333,20 +422,7 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
     const bool is_entry = it == 0 && p.loss_entry && p.nsteps > 0;
     const bool want_loss = UPD && (is_entry || (is_exit && (p.loss_exit || p.nsteps == 0)));
     bp_f4 num[CT][T], den[CT][T];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-      for (int t = 0; t < T; ++t) {
-        num[ct][t] = bp_f4{0.f, 0.f, 0.f, 0.f};
-        den[ct][t] = bp_f4{0.f, 0.f, 0.f, 0.f};
-      }
     float lsum = 0.f;
-
-    if (c_begin < c_end) {
-      load_chunk(c_begin);
-      store_chunk(0);
-    }
-    __syncthreads();
     // X of block b (32 streamed rows) for this lane's columns: float4 loads while the
     // block is inside X (invalid columns read row 0 -- their F is zero and their outputs
     // are discarded), guarded scalar loads at the tail
@@ -374,7 +450,7 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
     // one 32-row block of the streamed axis: P tiles, elementwise terms, loss, numerator
     // (WN, WL: numerator / loss wanted, as compile-time constants so that the hot
     // variant -- numerator only -- is one straight-line block over both column tiles)
-    auto compute_block = [&](auto WN, auto WL, const float (&xv)[CT][8], int blk,
+    auto compute_block = [&](auto WN, auto WL, auto SAT, const float (&xv)[CT][8], int blk,
                              const unsigned short* pb, int j0) {
       constexpr bool kNum = decltype(WN)::value, kLoss = decltype(WL)::value;
       const unsigned short* nb0 = pb + kBpCH * PS;
@@ -400,7 +476,8 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
         bp_f4 P0[CT], P1[CT];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          P0[ct] = bp_f4{p.eps, p.eps, p.eps, p.eps};
+          const float e0 = kH ? p.eps * csc[ct] : p.eps;
+          P0[ct] = bp_f4{e0, e0, e0, e0};
           P1[ct] = P0[ct];
 #pragma unroll
           for (int jj = 0; jj < NP; ++jj) {
@@ -408,69 +485,155 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
             P1[ct] = bp_mfma(ap[1][jj], freg[ct][jj], P1[ct]);
           }
         }
-        // phase 2: elementwise terms, loss, bf16 planes; phase 3: numerator MFMAs
-        bp_v8 qb0[CT], qb1[CT], db0[CT], db1[CT];
+        // phase 2: elementwise terms, loss, operand planes; phase 3: numerator MFMAs
+        if constexpr (kH) {
+          bp_h8 qh[CT];
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          float qv[8], dv[8];
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            bp_terms<MODE>(xv[ct][e], e < 4 ? P0[ct][e] : P1[ct][e - 4], p.beta, qv[e], dv[e]);
-          if (kLoss) {
+          for (int ct = 0; ct < CT; ++ct) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const int j = j0 + (e >> 2) * 16 + 4 * q + (e & 3);
-              const float t = bp_loss<MODE>(xv[ct][e], e < 4 ? P0[ct][e] : P1[ct][e - 4], qv[e],
-                                            dv[e], p.beta, p.eps);
-              lsum += (cok[ct] && j < p.Ls) ? t : 0.f;
+              const float x = xv[ct][e];
+              const float qv = x * __builtin_amdgcn_rcpf(e < 4 ? P0[ct][e] : P1[ct][e - 4]);
+              if (kLoss) {
+                // x log2(x / p) with q' = q 2^-s: log2 q = log2 q' + s
+                const int j = j0 + (e >> 2) * 16 + 4 * q + (e & 3);
+                const float t = x > 0.f ? x * (__builtin_amdgcn_logf(qv) + csg[ct]) : 0.f;
+                lsum += (cok[ct] && j < p.Ls) ? t : 0.f;
+              }
+              if (kNum) qh[ct][e] = (_Float16)qv;
+            }
+            // the redo pass after an overflow saturates instead (x / p beyond 2^40)
+            if (decltype(SAT)::value) qh[ct] = __builtin_elementwise_min(qh[ct], bp_h8(65504.f16));
+          }
+          if (kNum) {
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+              for (int t = 0; t < T; ++t) {
+                num[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                    __builtin_bit_cast(bp_h8, an0[t]), qh[ct], num[ct][t], 0, 0, 0);
+                num[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                    __builtin_bit_cast(bp_h8, an1[t]), qh[ct], num[ct][t], 0, 0, 0);
+              }
+          }
+        } else {
+          bp_v8 qb0[CT], qb1[CT], db0[CT], db1[CT];
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) {
+            float qv[8], dv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              bp_terms<MODE>(xv[ct][e], e < 4 ? P0[ct][e] : P1[ct][e - 4], p.beta, qv[e], dv[e]);
+            if (kLoss) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const int j = j0 + (e >> 2) * 16 + 4 * q + (e & 3);
+                const float t = bp_loss<MODE>(xv[ct][e], e < 4 ? P0[ct][e] : P1[ct][e - 4], qv[e],
+                                              dv[e], p.beta, p.eps);
+                lsum += (cok[ct] && j < p.Ls) ? t : 0.f;
+              }
+            }
+            if (kNum) {
+              bp_split2(qv, qb0[ct], qb1[ct]);
+              if (MODE != kBpKL) bp_split2(dv, db0[ct], db1[ct]);
             }
           }
           if (kNum) {
-            bp_split2(qv, qb0[ct], qb1[ct]);
-            if (MODE != kBpKL) bp_split2(dv, db0[ct], db1[ct]);
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+              for (int t = 0; t < T; ++t) {
+                num[ct][t] = bp_mfma(an0[t], qb0[ct], num[ct][t]);
+                num[ct][t] = bp_mfma(an0[t], qb1[ct], num[ct][t]);
+                num[ct][t] = bp_mfma(an1[t], qb0[ct], num[ct][t]);
+                if (MODE != kBpKL) {
+                  den[ct][t] = bp_mfma(an0[t], db0[ct], den[ct][t]);
+                  den[ct][t] = bp_mfma(an0[t], db1[ct], den[ct][t]);
+                  den[ct][t] = bp_mfma(an1[t], db0[ct], den[ct][t]);
+                }
+              }
           }
         }
-        if (kNum) {
-#pragma unroll
-          for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-              num[ct][t] = bp_mfma(an0[t], qb0[ct], num[ct][t]);
-              num[ct][t] = bp_mfma(an0[t], qb1[ct], num[ct][t]);
-              num[ct][t] = bp_mfma(an1[t], qb0[ct], num[ct][t]);
-              if (MODE != kBpKL) {
-                den[ct][t] = bp_mfma(an0[t], db0[ct], den[ct][t]);
-                den[ct][t] = bp_mfma(an0[t], db1[ct], den[ct][t]);
-                den[ct][t] = bp_mfma(an1[t], db0[ct], den[ct][t]);
-              }
-            }
-        }
     };
-    // software pipeline over the chunks: block 0's X (xa) arrived during the previous
-    // chunk; block 1's X (xb), the next chunk's block-0 X and panels load behind the
-    // compute (the last chunk reloads itself into the idle buffer: no branch around the
-    // staging registers)
-    const int nblk = 2 * (c_end - c_begin);
-    float xa[CT][8], xb[CT][8];
-    if (nblk > 0) load_x(0, xa);
+    // one pass over the streamed axis into num / den / lsum.  Software pipeline over the
+    // chunks: block 0's X (xa) arrived during the previous chunk; block 1's X (xb), the
+    // next chunk's block-0 X and panels load behind the compute (the last chunk reloads
+    // itself into the idle buffer: no branch around the staging registers)
     using kT = std::integral_constant<bool, true>;
     using kF = std::integral_constant<bool, false>;
-    for (int c = c_begin; c < c_end; ++c) {
-      const int i2 = 2 * (c - c_begin), bi = (c - c_begin) & 1;
-      const unsigned short* pb = sbuf + bi * CE;
-      load_x(i2 + 1, xb);
-      load_chunk(min(c + 1, c_end - 1));
+    auto stream_pass = [&](auto SAT) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && i2 + 2 < nblk) load_x(i2 + 2, xa);
-        const float(&xv)[CT][8] = h == 0 ? xa : xb;
-        const int j0 = c * kBpCH + 32 * h;
-        if (want_num && !want_loss) compute_block(kT{}, kF{}, xv, h, pb, j0);
-        else if (want_num) compute_block(kT{}, kT{}, xv, h, pb, j0);
-        else compute_block(kF{}, kT{}, xv, h, pb, j0);
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          num[ct][t] = bp_f4{0.f, 0.f, 0.f, 0.f};
+          den[ct][t] = bp_f4{0.f, 0.f, 0.f, 0.f};
+        }
+      lsum = 0.f;
+      if (c_begin < c_end) {
+        load_chunk(c_begin);
+        store_chunk(0);
       }
-      store_chunk(bi ^ 1);
       __syncthreads();
+      const int nblk = 2 * (c_end - c_begin);
+      float xa[CT][8], xb[CT][8];
+      if (nblk > 0) load_x(0, xa);
+      for (int c = c_begin; c < c_end; ++c) {
+        const int i2 = 2 * (c - c_begin), bi = (c - c_begin) & 1;
+        const unsigned short* pb = sbuf + bi * CE;
+        load_x(i2 + 1, xb);
+        load_chunk(min(c + 1, c_end - 1));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          if (h == 1 && i2 + 2 < nblk) load_x(i2 + 2, xa);
+          const float(&xv)[CT][8] = h == 0 ? xa : xb;
+          const int j0 = c * kBpCH + 32 * h;
+          if (want_num && !want_loss) compute_block(kT{}, kF{}, SAT, xv, h, pb, j0);
+          else if (want_num) compute_block(kT{}, kT{}, SAT, xv, h, pb, j0);
+          else compute_block(kF{}, kT{}, SAT, xv, h, pb, j0);
+        }
+        store_chunk(bi ^ 1);
+        __syncthreads();
+      }
+    };
+    stream_pass(kF{});
+
+    if (kH && want_num) {
+      // fp16 overflow of some column's Q: redo the step with that column's shift raised
+      // (ballot over the lanes of one column: lane 16q + m, all q; padded columns ignored)
+      bool bad[CT];
+      int any = 0;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        bool b = false;
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) b |= !(fabsf(num[ct][t][i]) <= 3.0e38f);
+        const unsigned long long bal = __ballot(b && cok[ct]);
+        const unsigned c16 = (unsigned)((bal | (bal >> 16) | (bal >> 32) | (bal >> 48)) & 0xffffu);
+        bad[ct] = (c16 >> m) & 1u;
+        any |= c16 != 0u;
+      }
+      if (__syncthreads_or(any)) {
+        // rare: a second copy of the pass (no loop back-edge: a retry loop around the
+        // pass kept ~40 more VGPRs live in the hot loop) with the columns' shift raised
+        // by 2^24 for the rest of the launch, saturating what still overflows
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          if (bad[ct]) {
+            csc[ct] *= 16777216.f;
+            csg[ct] += 24.f;
+          }
+        build_freg();
+        stream_pass(kT{});
+      }
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) num[ct][t][i] *= rinv[t][i] * csc[ct];
     }
 
     if (want_loss) {
@@ -612,15 +775,14 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
   }
 }
 
-template <int NP, int T, int MODE, bool UPD>
+template <int NP, int T, int MODE, bool UPD, int CT = bp_ct(T)>
 hipError_t bp_launch(const BpParams& p, hipStream_t s) {
-  constexpr int CT = bp_ct(T);
   const size_t lds = (size_t)2 * bp_chunk(NP, T) * 2 +
                      (size_t)kBpWaves * CT * 16 * bp_ks(T) * sizeof(float);
   static bool attr_done = false;
   if (!attr_done) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&bp_kernel<NP, T, MODE, UPD>),
+        reinterpret_cast<const void*>(&bp_kernel<NP, T, MODE, UPD, CT>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_done = true;
@@ -628,20 +790,36 @@ hipError_t bp_launch(const BpParams& p, hipStream_t s) {
   const int units = p.n_strips * p.splits;
   const int per_xcd = (units + 7) / 8;
   const dim3 grid((unsigned)(per_xcd * p.R * 8));
-  hipLaunchKernelGGL((bp_kernel<NP, T, MODE, UPD>), grid, dim3(kBpThreads), lds, s, p);
+  hipLaunchKernelGGL((bp_kernel<NP, T, MODE, UPD, CT>), grid, dim3(kBpThreads), lds, s, p);
   return hipGetLastError();
 }
 
 template <int MODE, bool UPD>
 hipError_t bp_launch_k(const BpParams& p, hipStream_t s) {
-  switch (bp_np(p.K)) {
-    case 1: return bp_launch<1, 1, MODE, UPD>(p, s);
-    case 2: return bp_launch<2, 1, MODE, UPD>(p, s);
-    case 3: return bp_launch<3, 1, MODE, UPD>(p, s);
-    case 4: return bp_launch<4, 2, MODE, UPD>(p, s);
-    case 5: return bp_launch<5, 2, MODE, UPD>(p, s);
-    case 6: return bp_launch<6, 2, MODE, UPD>(p, s);
-    default: return hipErrorInvalidValue;
+  if constexpr (MODE == kBpKL) {
+    const int np = bp_np(p.K, kBpKL), t = bp_t(p.K);
+    if (g_bp_kl_ct == 1) {
+      if (np == 1 && t == 1) return bp_launch<1, 1, MODE, UPD, 1>(p, s);
+      if (np == 2 && t == 1) return bp_launch<2, 1, MODE, UPD, 1>(p, s);
+      if (np == 2 && t == 2) return bp_launch<2, 2, MODE, UPD, 1>(p, s);
+      if (np == 3 && t == 2) return bp_launch<3, 2, MODE, UPD, 1>(p, s);
+      return hipErrorInvalidValue;
+    }
+    if (np == 1 && t == 1) return bp_launch<1, 1, MODE, UPD>(p, s);
+    if (np == 2 && t == 1) return bp_launch<2, 1, MODE, UPD>(p, s);
+    if (np == 2 && t == 2) return bp_launch<2, 2, MODE, UPD>(p, s);
+    if (np == 3 && t == 2) return bp_launch<3, 2, MODE, UPD>(p, s);
+    return hipErrorInvalidValue;
+  } else {
+    switch (bp_np(p.K)) {
+      case 1: return bp_launch<1, 1, MODE, UPD>(p, s);
+      case 2: return bp_launch<2, 1, MODE, UPD>(p, s);
+      case 3: return bp_launch<3, 1, MODE, UPD>(p, s);
+      case 4: return bp_launch<4, 2, MODE, UPD>(p, s);
+      case 5: return bp_launch<5, 2, MODE, UPD>(p, s);
+      case 6: return bp_launch<6, 2, MODE, UPD>(p, s);
+      default: return hipErrorInvalidValue;
+    }
   }
 }
 
@@ -659,29 +837,45 @@ hipError_t bp_launch_mode(int mode, const BpParams& p, hipStream_t s) {
 
 extern "C" int cnmf_bp_max_k() { return 32; }
 
-// bf16 elements of one replicate's panel over a streamed axis of length L
-extern "C" long long cnmf_bp_panel_elems(int K, int L) {
-  if (K < 1 || K > 32) return -1;
-  const int NP = cnmf::bp_np(K), T = cnmf::bp_t(K);
-  return (long long)((L + cnmf::kBpCH - 1) / cnmf::kBpCH) * cnmf::bp_chunk(NP, T);
+// 16-bit elements of one replicate's panel over a streamed axis of length L (layout by
+// beta mode: KL panels hold 3-term P slots, fp16 numerator planes and the row-scale tail)
+extern "C" long long cnmf_bp_panel_elems(int K, int L, int mode) {
+  if (K < 1 || K > 32 || mode < 0 || mode > 2) return -1;
+  const int NP = cnmf::bp_np(K, mode), T = cnmf::bp_t(K);
+  return (long long)((L + cnmf::kBpCH - 1) / cnmf::kBpCH) * cnmf::bp_chunk(NP, T) +
+         (mode == cnmf::kBpKL ? cnmf::kBpTail : 0);
+}
+
+// column tiles per wave of the KL kernels (1 or 2); returns the previous setting
+extern "C" int cnmf_bp_set_kl_ct(int ct) {
+  const int prev = cnmf::g_bp_kl_ct;
+  if (ct == 1 || ct == 2) cnmf::g_bp_kl_ct = ct;
+  return prev;
 }
 
 // fixed-axis columns per workgroup strip
-extern "C" int cnmf_bp_strip_cols(int K) {
-  return cnmf::kBpWaves * cnmf::bp_ct(cnmf::bp_t(K)) * 16;
+extern "C" int cnmf_bp_strip_cols(int K, int mode) {
+  const int ct = mode == cnmf::kBpKL ? cnmf::g_bp_kl_ct : cnmf::bp_ct(cnmf::bp_t(K));
+  return cnmf::kBpWaves * ct * 16;
 }
 
 extern "C" hipError_t cnmf_bp_panels(const float* F, long long f_rs, long long ldf, int K, int L,
-                                     int R, unsigned short* out, long long out_rs,
+                                     int R, int mode, unsigned short* out, long long out_rs,
                                      hipStream_t stream) {
   if (R <= 0 || L <= 0) return hipSuccess;
-  if (K < 1 || K > 32) return hipErrorInvalidValue;
-  const int NP = cnmf::bp_np(K), T = cnmf::bp_t(K);
+  if (K < 1 || K > 32 || mode < 0 || mode > 2) return hipErrorInvalidValue;
+  if (out_rs < cnmf_bp_panel_elems(K, L, mode)) return hipErrorInvalidValue;
+  const int NP = cnmf::bp_np(K, mode), T = cnmf::bp_t(K);
   const int nchunks = (L + cnmf::kBpCH - 1) / cnmf::kBpCH;
+  const bool kl = mode == cnmf::kBpKL;
+  if (kl)
+    hipLaunchKernelGGL(cnmf::bp_rowscale_kernel, dim3((unsigned)R), dim3(256), 0, stream, F,
+                       f_rs, ldf, K, L, out, out_rs,
+                       (long long)nchunks * cnmf::bp_chunk(NP, T));
   const long long n = (long long)R * nchunks * cnmf::kBpCH;
   const dim3 grid((unsigned)((n + 255) / 256));
   hipLaunchKernelGGL(cnmf::bp_panel_kernel, grid, dim3(256), 0, stream, F, f_rs, ldf, K, L,
-                     nchunks, R, NP, T, out, out_rs);
+                     nchunks, R, NP, T, cnmf::bp_nt(mode), kl ? 1 : 0, out, out_rs);
   return hipGetLastError();
 }
 
@@ -695,13 +889,15 @@ extern "C" hipError_t cnmf_bp_run(
     const int* active, double* loss, double xsum, hipStream_t stream) {
   if (R <= 0 || Lf <= 0) return hipSuccess;
   if (K < 1 || K > 32 || Ls <= 0 || (side != 0 && side != 1)) return hipErrorInvalidValue;
+  if (mode < 0 || mode > 2 || panel_rs < cnmf_bp_panel_elems(K, Ls, mode))
+    return hipErrorInvalidValue;
   cnmf::BpParams p;
   p.X = X; p.ldx = ldx;
   p.xvec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
   p.panel = panel; p.panel_rs = panel_rs;
   p.F = F; p.f_rs = f_rs; p.ldf = ldf;
   p.K = K; p.Lf = Lf; p.Ls = Ls; p.R = R;
-  p.n_strips = (Lf + cnmf_bp_strip_cols(K) - 1) / cnmf_bp_strip_cols(K);
+  p.n_strips = (Lf + cnmf_bp_strip_cols(K, mode) - 1) / cnmf_bp_strip_cols(K, mode);
   const int nch = (Ls + cnmf::kBpCH - 1) / cnmf::kBpCH;
   if (side == 0) splits = 1;
   splits = splits < 1 ? 1 : (splits > nch ? nch : splits);

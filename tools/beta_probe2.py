@@ -40,16 +40,16 @@ def main():
     W = torch.rand(a.R, a.K, a.G, device="cuda", generator=g) + 0.1
     H0 = HT.clone()
     elems = a.R * a.c * a.G
-    pw = ops.beta_panels(W)
-    ph = ops.beta_panels(HT)
+    pw = ops.beta_panels(W, a.beta)
+    ph = ops.beta_panels(HT, a.beta)
     ns = 10
     cases = {
         "h_block10 (per step)": (lambda: (HT.copy_(H0), ops.beta_h_block(
             X, HT, W, a.beta, 1e-16, ns, panels=pw)), ns),
         "w_partials": (lambda: ops.beta_w_partials(X, XT, HT, W, a.beta, 1e-16, panels=ph), 1),
         "loss": (lambda: ops.beta_loss(X, HT, W, a.beta, 1e-16, panels=pw), 1),
-        "panels W": (lambda: ops.beta_panels(W, out=pw), 1),
-        "panels H": (lambda: ops.beta_panels(HT, out=ph), 1),
+        "panels W": (lambda: ops.beta_panels(W, a.beta, out=pw), 1),
+        "panels H": (lambda: ops.beta_panels(HT, a.beta, out=ph), 1),
         "old update_h": (lambda: (HT.copy_(H0), ops.beta_update_h(X, HT, W, a.beta, 1e-16)), 1),
         "old contract_w": (lambda: ops.beta_contract("w", X, HT, W, a.beta, 1e-16), 1),
     }

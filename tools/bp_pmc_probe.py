@@ -17,12 +17,12 @@ def main():
     HT = torch.rand(R, K, c, device="cuda", generator=g) + 0.1
     W = torch.rand(R, K, G, device="cuda", generator=g) + 0.1
     if which == "h":
-        pw = ops.beta_panels(W)
+        pw = ops.beta_panels(W, 1.0)
         for _ in range(3):
             ops.beta_h_block(X, HT, W, 1.0, 1e-16, 10, panels=pw)
     else:
         XT = X.t().contiguous()
-        ph = ops.beta_panels(HT)
+        ph = ops.beta_panels(HT, 1.0)
         for _ in range(3):
             ops.beta_w_partials(X, XT, HT, W, 1.0, 1e-16, panels=ph)
     torch.cuda.synchronize()

@@ -1,0 +1,9 @@
+# KL fp16-numerator kernels: beta GPU tests, KL bench, KL kernel trace
+set -e
+export TMPDIR=/tmp
+out=gpurun_out/r3i
+mkdir -p $out
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread -k "beta or kl or bf16 or nmf_batch_gpu" > $out/pytest.log 2>&1
+timeout -k 10 200 python bench.py --beta-loss kullback-leibler --steps 3 --warmup 1 > $out/bench_kl.log 2>&1
+timeout -k 10 200 rocprofv3 --kernel-trace -d $out/prof_kl -o run -- python3 bench.py --beta-loss kullback-leibler --steps 2 --warmup 1 > $out/prof_kl.log 2>&1
+echo done
