@@ -130,7 +130,7 @@ def build_h5(force: bool = False, verbose: bool = True) -> str:
 
 
 def build_npz(force: bool = False, verbose: bool = True) -> str:
-    """Native replicate-file writer (csrc/io/npzio.cpp): host C++, std::thread, no deps."""
+    """Native replicate-file writer (csrc/io/npzio.cpp): host C++, std::thread, zlib."""
     src = os.path.join(CSRC, "io", "npzio.cpp")
     if not (force or _stale(NPZ_OUT, [src])):
         return NPZ_OUT
@@ -139,7 +139,7 @@ def build_npz(force: bool = False, verbose: bool = True) -> str:
     if verbose:
         print("[cnmf build] compiling native npz writer", flush=True)
     _run([cxx, "-O3", "-shared", "-fPIC", "-std=c++17", "-pthread", src, "-o", tmp]
-         + _py_includes())
+         + _py_includes() + ["-lz"])
     os.replace(tmp, NPZ_OUT)
     return NPZ_OUT
 

@@ -28,9 +28,11 @@ import json
 import os
 import shutil
 import sys
+import threading
 import time
 import uuid
 import warnings
+import weakref
 
 import numpy as np
 import pandas as pd
@@ -200,6 +202,10 @@ def _resident_X(adata, dev: torch.device):
         cache[key] = (_device_csr(X, dev) if sp.issparse(X)
                       else torch.as_tensor(np.asarray(X, dtype=np.float32)).to(dev))
     return cache[key]
+
+
+# ||X||^2 of a device-resident X (api._prediction_error), weakly keyed by the tensor
+_XSQ: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
 
 def _load_npz_arrays(fn: str):
@@ -553,7 +559,16 @@ class cNMF:
         """Run this worker's share of the replicate ledger (cnmf.py:839-892).
 
         Jobs with the same K are solved together in batches of ``replicate_batch``
-        replicates (default: all of them that fit the device memory budget)."""
+        replicates (default: all of them that fit the device memory budget).
+
+        Worker 0 also starts the figure process (utils.plotting.prestart): it imports
+        matplotlib in the background, so when combine / k_selection_plot / consensus run
+        in this same process their closed figures do not wait for that import
+        (CNMF_PLOT_PRESTART=0 turns this off)."""
+        if worker_i == 0:
+            from .utils.plotting import prestart
+
+            prestart()
         run_params = load_df_from_npz(self.paths["nmf_replicate_parameters"])
         if not skip_completed_runs:
             jobs = list(worker_filter(range(len(run_params)), worker_i, total_workers))
@@ -1120,12 +1135,19 @@ class cNMF:
             UtX = sops.tspmm(X, U).t().to(torch.float64)              # (K, G)
             return float((d * d).sum()) - 2.0 * float((UtX * S).sum()) + quad
         if isinstance(X, torch.Tensor):
-            x_sq = cross = 0.0
+            # ||X||^2 is the same for every K of a k-selection: computed once per tensor
+            x_sq = _XSQ.get(X)
+            cross = torch.zeros((), dtype=torch.float64, device=dev)
+            xs = None if x_sq is not None else torch.zeros((), dtype=torch.float64, device=dev)
             for a in range(0, X.shape[0], 16384):
                 xb = X[a:a + 16384].to(device=dev, dtype=torch.float64)
-                x_sq += float((xb * xb).sum())
-                cross += float(((U[a:a + 16384].t() @ xb) * S).sum())
-            return x_sq - 2.0 * cross + quad
+                if xs is not None:
+                    xs += (xb * xb).sum()
+                cross += ((U[a:a + 16384].t() @ xb) * S).sum()
+            if xs is not None:
+                x_sq = float(xs)
+                _XSQ[X] = x_sq
+            return x_sq - 2.0 * float(cross) + quad
         n = X.shape[0]
         x_sq = 0.0
         cross = 0.0
@@ -1176,12 +1198,41 @@ class cNMF:
             plot_worker = PlotWorker()   # imports matplotlib while the stats compute
         norm_counts = read_h5ad(self.paths["normalized_counts"])
         ks = sorted(set(int(x) for x in run_params.n_components))
+        mine = ks[rank::world]
+
+        def stats_of(k):
+            return self.consensus(k, skip_density_and_return_after_stats=True,
+                                  show_clustering=False, close_clustergram_fig=True,
+                                  norm_counts=norm_counts, kmeans_backend=kmeans_backend,
+                                  device=device).stats
+
         rows = {}
-        for k in ks[rank::world]:
-            rows[k] = self.consensus(k, skip_density_and_return_after_stats=True,
-                                     show_clustering=False, close_clustergram_fig=True,
-                                     norm_counts=norm_counts, kmeans_backend=kmeans_backend,
-                                     device=device).stats
+        dev = _device(bool(self._refit_kwargs().get("use_gpu", False)), device)
+        if dev.type == "cuda" and len(mine) > 1:
+            # the Ks are independent and each is a chain of small kernels and host reads:
+            # run them on a few threads with a HIP stream each, so one K's host syncs,
+            # npz reads and k-means checks overlap the others' GPU work.  X is uploaded
+            # once, before the threads start
+            _resident_X(norm_counts, dev)
+            torch.cuda.synchronize(dev)
+
+            local = threading.local()
+
+            def on_stream(k):
+                s = getattr(local, "stream", None)
+                if s is None:
+                    s = local.stream = torch.cuda.Stream(dev)
+                with torch.cuda.stream(s):
+                    out = stats_of(k)
+                s.synchronize()
+                return out
+
+            with cf.ThreadPoolExecutor(max_workers=min(4, len(mine))) as ex:
+                for k, st in zip(mine, ex.map(on_stream, mine)):
+                    rows[k] = st
+        else:
+            for k in mine:
+                rows[k] = stats_of(k)
         if world > 1:
             for part in comm.all_gather_object(rows):
                 rows.update(part)

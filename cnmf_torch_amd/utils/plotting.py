@@ -11,14 +11,17 @@ only numpy/pandas at the top, so the worker never loads torch or touches the GPU
 from __future__ import annotations
 
 import atexit
+import concurrent.futures as cf
 import itertools
 import json
 import os
+import struct
 import subprocess
 import sys
 import tempfile
 import threading
 import time
+import zlib
 
 import numpy as np
 import pandas as pd
@@ -101,6 +104,59 @@ def clustergram(dist: np.ndarray, labels: pd.Series, local_density: pd.DataFrame
     return fig
 
 
+def _png_chunk(tag: bytes, data: bytes) -> bytes:
+    return (struct.pack(">I", len(data)) + tag + data
+            + struct.pack(">I", zlib.crc32(data, zlib.crc32(tag)) & 0xFFFFFFFF))
+
+
+def write_png_rgba(path: str, rgba: np.ndarray, dpi: float, threads: int = 8) -> None:
+    """RGBA8 PNG of ``rgba`` (H, W, 4) with the deflate stream compressed in row bands on
+    ``threads`` threads (native, csrc/io/npzio.cpp; this Python form is the fallback when
+    the module is not built).  Each band ends in a full flush, so the concatenated raw
+    deflate blocks are one valid stream -- the pigz construction.  Same
+    chunks as matplotlib's Agg/PIL output (IHDR, pHYs from ``dpi``, a Software tEXt, IDAT,
+    IEND) and the same pixels; filter 0 on every row, zlib level 1.  The clustergram
+    (3750 x 2375) encoded in ~0.45 s through PIL."""
+    import matplotlib
+
+    software = f"Matplotlib version{matplotlib.__version__}, https://matplotlib.org/"
+    try:
+        from . import _npzio
+    except ImportError:
+        _npzio = None
+    if _npzio is not None and hasattr(_npzio, "write_png_rgba"):
+        # native: the bands deflate on std::threads (Python 3.10's zlib holds the GIL)
+        _npzio.write_png_rgba(path, np.ascontiguousarray(rgba), float(dpi), software, 1,
+                              int(threads))
+        return
+    h, w, _ = rgba.shape
+    raw = np.empty((h, 1 + 4 * w), dtype=np.uint8)
+    raw[:, 0] = 0
+    raw[:, 1:] = rgba.reshape(h, 4 * w)
+    band = max(1, -(-h // max(1, threads)))
+    pieces = [raw[a:a + band] for a in range(0, h, band)]
+
+    def deflate(i):
+        co = zlib.compressobj(1, zlib.DEFLATED, -15)
+        out = co.compress(pieces[i].tobytes())
+        return out + co.flush(zlib.Z_FINISH if i == len(pieces) - 1 else zlib.Z_FULL_FLUSH)
+
+    with cf.ThreadPoolExecutor(max_workers=len(pieces)) as ex:
+        body = b"".join(ex.map(deflate, range(len(pieces))))
+    adler = 1
+    for pc in pieces:
+        adler = zlib.adler32(pc, adler)
+    idat = b"\x78\x01" + body + struct.pack(">I", adler & 0xFFFFFFFF)
+    ppm = int(round(dpi / 0.0254))
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n")
+        f.write(_png_chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 6, 0, 0, 0)))
+        f.write(_png_chunk(b"pHYs", struct.pack(">IIB", ppm, ppm, 1)))
+        f.write(_png_chunk(b"tEXt", b"Software\x00" + software.encode()))
+        f.write(_png_chunk(b"IDAT", idat))
+        f.write(_png_chunk(b"IEND", b""))
+
+
 def _save(fig, path: str) -> None:
     """Atomic PNG write (temp file in the destination directory + rename)."""
     d = os.path.dirname(os.path.abspath(path)) or "."
@@ -108,10 +164,20 @@ def _save(fig, path: str) -> None:
                                dir=d)
     os.close(fd)
     try:
-        # dpi 250 as cnmf.py:1251.  zlib level 1 instead of PIL's 6: the same pixels
-        # (PNG is lossless) in ~1/5 of the encode time -- encoding the 3750 x 2375
-        # clustergram was ~0.7 s of its ~1.1 s
-        fig.savefig(tmp, dpi=250, pil_kwargs={"compress_level": 1})
+        # dpi 250 as cnmf.py:1251.  The Agg canvas renders at that dpi and the PNG is
+        # encoded on several threads (write_png_rgba): PIL's single-threaded encode of the
+        # 3750 x 2375 clustergram was ~0.45 s of its ~1.5 s
+        if fig.canvas.get_default_filetype() == "png" and \
+                type(fig.canvas).__name__ == "FigureCanvasAgg":
+            old = fig.get_dpi()
+            fig.set_dpi(250)
+            try:
+                fig.canvas.draw()
+                write_png_rgba(tmp, np.asarray(fig.canvas.buffer_rgba()), 250)
+            finally:
+                fig.set_dpi(old)
+        else:
+            fig.savefig(tmp, dpi=250, pil_kwargs={"compress_level": 1})
         os.replace(tmp, path)
     except BaseException:
         if os.path.exists(tmp):
@@ -223,6 +289,17 @@ class _PlotProc:
                 # the child is still up, then it is closed
                 atexit.register(flush_figures)
             return cls._inst
+
+
+def prestart() -> None:
+    """Start the shared figure process now (it imports matplotlib while the caller
+    computes), unless this process already imported pyplot or CNMF_PLOT_PRESTART=0."""
+    if os.environ.get("CNMF_PLOT_PRESTART", "1") == "0" or "matplotlib.pyplot" in sys.modules:
+        return
+    try:
+        _PlotProc.get()
+    except Exception:
+        pass                       # figures then start their child (or draw) on demand
 
 
 class PlotWorker:

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include <unistd.h>
+#include <zlib.h>
 
 namespace py = pybind11;
 
@@ -659,6 +660,99 @@ static void csr_scale_rows(py::array data, py::array indptr, py::array_t<double>
   else throw std::invalid_argument("csr_scale_rows: float32 or float64 data");
 }
 
+// PNG (RGBA8, filter 0 on every row) of an (H, W, 4) uint8 image: the deflate stream is
+// compressed in row bands on `threads` threads, each band a raw deflate ending in a full
+// flush (the last in Z_FINISH), so the concatenated bands form one valid stream (the pigz
+// construction); the zlib adler32 over the whole filtered image closes it.  Chunks as
+// matplotlib's Agg/PIL output: IHDR, pHYs, tEXt "Software", IDAT, IEND.
+static void png_chunk(std::string& out, const char* tag, const std::string& data) {
+  const uint32_t n = (uint32_t)data.size();
+  const unsigned char len[4] = {(unsigned char)(n >> 24), (unsigned char)(n >> 16),
+                                (unsigned char)(n >> 8), (unsigned char)n};
+  out.append((const char*)len, 4);
+  out.append(tag, 4);
+  out += data;
+  uLong c = crc32(0L, (const Bytef*)tag, 4);
+  c = crc32(c, (const Bytef*)data.data(), (uInt)data.size());
+  const unsigned char cb[4] = {(unsigned char)(c >> 24), (unsigned char)(c >> 16),
+                               (unsigned char)(c >> 8), (unsigned char)c};
+  out.append((const char*)cb, 4);
+}
+
+static std::string be32(uint32_t v) {
+  const char b[4] = {(char)(v >> 24), (char)(v >> 16), (char)(v >> 8), (char)v};
+  return std::string(b, 4);
+}
+
+static void write_png_rgba(const std::string& path, py::array_t<uint8_t, py::array::c_style> img,
+                           double dpi, const std::string& software, int level, int threads) {
+  if (img.ndim() != 3 || img.shape(2) != 4) throw std::invalid_argument("write_png_rgba: (H, W, 4)");
+  const long long h = img.shape(0), w = img.shape(1), row = 1 + 4 * w;
+  const uint8_t* src = img.data();
+  std::string out;
+  {
+    py::gil_scoped_release nogil;
+    std::vector<uint8_t> raw((size_t)(h * row));
+    for (long long r = 0; r < h; ++r) {
+      raw[(size_t)(r * row)] = 0;
+      std::memcpy(&raw[(size_t)(r * row + 1)], src + r * 4 * w, (size_t)(4 * w));
+    }
+    const int nt = std::max(1, std::min<int>(threads, (int)std::max<long long>(1, h / 16)));
+    const long long band = (h + nt - 1) / nt;
+    std::vector<std::string> parts(nt);
+    std::vector<uLong> adl(nt, 1);
+    std::vector<int> err(nt, 0);
+    auto work = [&](int t) {
+      const long long r0 = t * band, r1 = std::min(h, r0 + band);
+      if (r0 >= r1) return;
+      const Bytef* in = raw.data() + r0 * row;
+      const uInt n = (uInt)((r1 - r0) * row);
+      adl[t] = adler32(1L, in, n);
+      z_stream zs;
+      std::memset(&zs, 0, sizeof(zs));
+      if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) { err[t] = 1; return; }
+      std::string& o = parts[t];
+      o.resize(deflateBound(&zs, n) + 64);
+      zs.next_in = const_cast<Bytef*>(in);
+      zs.avail_in = n;
+      zs.next_out = (Bytef*)&o[0];
+      zs.avail_out = (uInt)o.size();
+      const int rc = deflate(&zs, r1 == h ? Z_FINISH : Z_FULL_FLUSH);
+      if ((r1 == h && rc != Z_STREAM_END) || (r1 != h && rc != Z_OK) || zs.avail_in != 0) err[t] = 1;
+      o.resize(o.size() - zs.avail_out);
+      deflateEnd(&zs);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& t : pool) t.join();
+    for (int t = 0; t < nt; ++t)
+      if (err[t]) throw std::runtime_error("write_png_rgba: deflate failed");
+    uLong ad = adl[0];
+    for (int t = 1; t < nt; ++t) {
+      const long long r0 = t * band, r1 = std::min(h, r0 + band);
+      if (r0 < r1) ad = adler32_combine(ad, adl[t], (z_off_t)((r1 - r0) * row));
+    }
+    std::string idat("\x78\x01", 2);
+    for (auto& pt : parts) idat += pt;
+    idat += be32((uint32_t)ad);
+    const uint32_t ppm = (uint32_t)std::llround(dpi / 0.0254);
+    out.append("\x89PNG\r\n\x1a\n", 8);
+    std::string ihdr = be32((uint32_t)w) + be32((uint32_t)h);
+    ihdr += std::string("\x08\x06\x00\x00\x00", 5);
+    png_chunk(out, "IHDR", ihdr);
+    png_chunk(out, "pHYs", be32(ppm) + be32(ppm) + std::string("\x01", 1));
+    png_chunk(out, "tEXt", std::string("Software") + std::string("\0", 1) + software);
+    png_chunk(out, "IDAT", idat);
+    png_chunk(out, "IEND", std::string());
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) throw std::runtime_error("write_png_rgba: cannot open " + path);
+    const size_t wr = std::fwrite(out.data(), 1, out.size(), f);
+    const int cl = std::fclose(f);
+    if (wr != out.size() || cl != 0) throw std::runtime_error("write_png_rgba: write failed " + path);
+  }
+}
+
 PYBIND11_MODULE(_npzio, m) {
   m.doc() = "cnmf_torch_amd native replicate-file writer/reader (stored npz, crc32, sha256)";
   m.def("write_spectra_batch", &write_spectra_batch, py::arg("paths"), py::arg("data"),
@@ -672,4 +766,6 @@ PYBIND11_MODULE(_npzio, m) {
         py::arg("threads") = 16);
   m.def("sha256_hex", &sha256_hex);
   m.def("crc32", &crc32_bytes);
+  m.def("write_png_rgba", &write_png_rgba, py::arg("path"), py::arg("img"), py::arg("dpi"),
+        py::arg("software"), py::arg("level") = 1, py::arg("threads") = 8);
 }

@@ -315,6 +315,44 @@ print('ok')
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+def test_native_png_matches_matplotlib_pixels(tmp_path):
+    """utils.plotting._save (Agg canvas at 250 dpi + the banded-deflate PNG writer, native
+    and Python fallback) decodes to exactly the pixels of matplotlib's own savefig."""
+    import matplotlib
+
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    from PIL import Image
+
+    from cnmf_torch_amd.utils import plotting
+
+    rng = np.random.default_rng(0)
+    n = 120
+    D = rng.random((n, n))
+    D = (D + D.T) / 2
+    lab = pd.Series(rng.integers(1, 5, n), index=[f"s{i}" for i in range(n)])
+    fig = plotting.clustergram(D, lab, pd.DataFrame(rng.random(n), columns=["local_density"]),
+                               np.ones(n, bool), 0.5, str(tmp_path / "cg.png"))
+    fig.savefig(str(tmp_path / "ref.png"), dpi=250)
+    ref = np.asarray(Image.open(str(tmp_path / "ref.png")))
+    got = np.asarray(Image.open(str(tmp_path / "cg.png")))
+    assert got.shape == ref.shape and (got == ref).all()
+    info = Image.open(str(tmp_path / "cg.png")).info
+    assert abs(info["dpi"][0] - 250) < 0.1 and info["Software"].startswith("Matplotlib")
+    # the pure-Python writer (used when the native module is missing)
+    saved = sys.modules.get("cnmf_torch_amd.utils._npzio")
+    sys.modules["cnmf_torch_amd.utils._npzio"] = None          # ImportError on import
+    try:
+        plotting.write_png_rgba(str(tmp_path / "py.png"), ref, 250, threads=3)
+    finally:
+        if saved is None:
+            sys.modules.pop("cnmf_torch_amd.utils._npzio", None)
+        else:
+            sys.modules["cnmf_torch_amd.utils._npzio"] = saved
+    assert (np.asarray(Image.open(str(tmp_path / "py.png"))) == ref).all()
+    plt.close(fig)
+
+
 def test_plot_worker_falls_back_when_the_child_dies(tmp_path):
     """A dead figure child is replaced for the next stage, and a job it never acknowledged
     is drawn in this process: figures are never lost."""
