@@ -204,6 +204,9 @@ def _resident_X(adata, dev: torch.device):
     return cache[key]
 
 
+# cooperative (co-resident, spinning) solves of concurrent k-selection threads
+_COOP_LOCK = threading.RLock()
+
 # ||X||^2 of a device-resident X (api._prediction_error), weakly keyed by the tensor
 _XSQ: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 
@@ -1004,7 +1007,11 @@ class cNMF:
         median_spectra = pd.DataFrame(median_np, index=sorted(set(labels)), columns=merged.columns)
 
         ncX = _resident_X(norm_counts, dev)
-        rf_usages = self.refit_usage(ncX, median_spectra, device=dev)
+        # the usage refit's cooperative solves spin on their own workgroups' progress,
+        # so two of them must not share the GPU: serialised across the k-selection
+        # threads (everything else of a K -- npz read, k-means, medians -- overlaps)
+        with _COOP_LOCK:
+            rf_usages = self.refit_usage(ncX, median_spectra, device=dev)
         rf_usages = pd.DataFrame(rf_usages, index=norm_counts.obs.index, columns=median_spectra.index)
 
         if skip_stats:

@@ -478,7 +478,7 @@ def coop_check(device: torch.device | None = None) -> None:
         device = torch.device(device)
         want = str(torch.device("cuda", device.index if device.index is not None
                                 else torch.cuda.current_device()))
-    for key, ws in _COOP_WS.items():
+    for key, ws in list(_COOP_WS.items()):   # other threads may add streams
         if want is not None and key[0] != want:
             continue
         v = int(ws["flag"].item())
