@@ -1552,6 +1552,8 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
     variant, ksplit = gemm_plan(M, N, Kd, pb)
     slab = 0
     if raw_slab is not None and ksplit > raw_max:
+        # (capping ksplit at raw_max instead -- no reduction pass, fewer workgroups -- was
+        # slower on the tail passes: 232 vs 212 us, profiles/r3s_*)
         gemm_planes(C, A, B, M, N, Kd, accumulate=False, col_scale=None)
         return 1
     if raw_slab is not None:
