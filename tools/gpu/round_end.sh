@@ -1,5 +1,5 @@
 # Round-end validation: every GPU test, smoke, Frobenius/KL bench, K-grid bench, e2e
-# pipeline, kernel-trace profile.  usage: bash tools/gpu_final.sh <outdir under gpurun_out>
+# pipeline, kernel-trace profile.  usage: bash tools/gpu/round_end.sh <outdir under gpurun_out>
 set -e
 export TMPDIR=/tmp
 out=gpurun_out/$1
