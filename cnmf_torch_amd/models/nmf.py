@@ -1890,6 +1890,36 @@ class NMFBatchSolver:
         self._kl_csrT = {}
         return csr
 
+    def _kl_counts(self):
+        """(xh (N, G) float16, xth (G, N) float16, unit (G,), 1 / unit (G,)) when the dense
+        KL kernels read X as fp16 counts: cNMF's normalised counts are integer counts over
+        a per-gene std (X == C u_g, _count_units), and counts <= 2048 are exact in fp16.
+        Half the bytes of the per-step X re-reads that bound those kernels
+        (profiles/r3m_*), and xth replaces the fp32 X^T copy.  None for other data, the
+        sparse path, or CNMF_KL_FP16_COUNTS=0."""
+        if "_klc" in self.__dict__:
+            return self._klc
+        res = None
+        X = self.X
+        if (self.beta == 1.0 and isinstance(X, torch.Tensor) and X.device.type == "cuda"
+                and X.dtype == torch.float32 and ops.use_native(X)
+                and os.environ.get("CNMF_KL_FP16_COUNTS", "1") != "0"
+                and self._kl_sparse() is None):
+            unit = _count_units(X, self._colstats)
+            if unit is not None:
+                unit = unit.to(device=X.device, dtype=torch.float32).contiguous()
+                C = torch.round(X / unit)
+                if float(C.max()) <= 2048.0:
+                    N, G = X.shape
+                    xh = C.to(torch.float16)
+                    Np = -(-N // 4) * 4               # 8-byte rows: fp16 x4 loads
+                    xth = torch.zeros((G, Np), dtype=torch.float16, device=X.device)
+                    xth[:, :N] = xh.t()
+                    res = (xh, xth[:, :N], unit, (1.0 / unit).contiguous())
+                del C
+        self._klc = res
+        return res
+
     def _kl_rows_T(self, a: int, b: int):
         """Tiled CSRs of X[a:b]^T (genes x chunk cells) for the sparse spectra numerators."""
         key = (a, b)
@@ -1904,6 +1934,12 @@ class NMFBatchSolver:
         if rows is not None and self._kl_sparse() is not None:
             return ops.kl_sparse_w_num(self._kl_rows_T(*rows), H3c, W3, self.opts.eps,
                                        active=active, st=panels), None
+        klc = self._kl_counts() if rows is not None else None
+        if klc is not None:
+            a, b = rows
+            return ops.beta_w_partials(xc, None, H3c, W3, self.beta, self.opts.eps,
+                                       active=active, panels=panels, xth=klc[1][:, a:b],
+                                       unit_inv=klc[3])
         if xc.device.type == "cuda" and xtc is None:
             num, den, _ = ops.beta_contract("w", xc, H3c, W3, self.beta, self.opts.eps,
                                             active=active, reduce=False)
@@ -1920,15 +1956,18 @@ class NMFBatchSolver:
             cache[key] = float(xc.sum(dtype=torch.float64))
         return cache[key]
 
-    def _beta_panels(self, F3: torch.Tensor):
+    def _beta_panels(self, F3: torch.Tensor, usage_side: bool = False):
         """Kernel operand of a factor that stays fixed over the next kernel launches: its
         split-bf16 panels, or its padded transpose for the sparse KL kernels (GPU only; the
-        CPU reference works on the fp32 factor directly)."""
+        CPU reference works on the fp32 factor directly).  ``usage_side``: the spectra as
+        the usage solve's streamed operand -- with fp16 counts its P panel is S / unit."""
         if F3.device.type != "cuda":
             return None
         if self._kl_sparse() is not None:
             return ops.kl_st(F3)
-        return ops.beta_panels(F3, self.beta)
+        klc = self._kl_counts() if (usage_side and
+                                    os.environ.get("CNMF_KL_FP16_COUNTS", "1") != "w") else None
+        return ops.beta_panels(F3, self.beta, row_scale=klc[3] if klc is not None else None)
 
     def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, panels=None, rows=None):
         """One fused MU step of the usages H3c (R, K, c) in place against W3 on rows xc
@@ -1958,8 +1997,12 @@ class NMFBatchSolver:
         den_vec = (W3.sum(dim=2, dtype=torch.float32).contiguous()
                    if self.beta == 1.0 and cuda else None)
         csr = self._kl_sparse() if (cuda and rows is not None) else None
+        klc = self._kl_counts() if (cuda and rows is not None and csr is None
+                                    and os.environ.get("CNMF_KL_FP16_COUNTS", "1") != "w") \
+            else None
         if cuda and wpan is None:
-            wpan = ops.kl_st(W3) if csr is not None else ops.beta_panels(W3, self.beta)
+            wpan = ops.kl_st(W3) if csr is not None else ops.beta_panels(
+                W3, self.beta, row_scale=klc[3] if klc is not None else None)
         cmode = 1 if o.online_inner_conv == "loss" else 0
         per = max(1, int(o.inner_check_every)) if cmode == 1 else 1
         group = 1 if cmode == 1 else block
@@ -1985,7 +2028,9 @@ class NMFBatchSolver:
                                      self._beta_gamma(), act=act, tol=o.online_h_tol,
                                      iters=iters, conv_mode=cmode, hstate=hstate,
                                      loss_entry=first, den_vec=den_vec, panels=wpan,
-                                     xsum=xsum)
+                                     xsum=xsum,
+                                     xh=klc[0][rows[0]:rows[1]] if klc is not None else None,
+                                     unit=klc[2] if klc is not None else None)
                 first = False
                 it += m
             if not cuda:
@@ -2043,10 +2088,11 @@ class NMFBatchSolver:
         cuda = dev.type == "cuda"
         dist = self.comm.is_distributed
         sparse = cuda and self._kl_sparse() is not None
-        XT = None if sparse else self._xt()
+        counts = cuda and not sparse and self._kl_counts() is not None
+        XT = None if (sparse or counts) else self._xt()
         # the chunk's usages stay fixed over the spectra iterations: split them once
         hpan = {(a, b): self._beta_panels(H3[:, :, a:b]) for (a, b) in rows} \
-            if (XT is not None or sparse) else {}
+            if (XT is not None or sparse or counts) else {}
         max_it = int(o.online_chunk_max_iter)
         pending = None
         it = 0
@@ -2143,7 +2189,8 @@ class NMFBatchSolver:
             keep = (live != 0).view(n, 1, 1)
             keep_d = keep.view(n, 1) if kl else keep
             for blocks in steps:
-                wpan = self._beta_panels(W3)      # W is fixed over this step's usage solves
+                # W is fixed over this step's usage solves
+                wpan = self._beta_panels(W3, usage_side=True)
                 for (a, b) in blocks:
                     if b <= a:
                         continue

@@ -55,7 +55,7 @@ def _require_native():
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
 _ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
              "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES", "CNMF_GEMM_BK",
-             "CNMF_GEMM_SMALL", "CNMF_SOLVE_PIPE", "CNMF_BP_KL_CT")
+             "CNMF_GEMM_SMALL", "CNMF_SOLVE_PIPE")
 _ENV: dict = {}
 
 
@@ -63,11 +63,6 @@ def refresh_env() -> None:
     """Re-read the CNMF_* per-op knobs from the environment."""
     _ENV.clear()
     _ENV.update({k: os.environ.get(k) for k in _ENV_KEYS})
-    set_ct = getattr(_hip, "bp_set_kl_ct", None)   # absent from a stale build
-    if set_ct is not None:
-        # column tiles per wave of the KL beta kernels (beta_planes.hip; default 2:
-        # 325 vs 290 rep/s with 1 at the headline, profiles/r3l_*)
-        set_ct(int(_ENV["CNMF_BP_KL_CT"] or 2))
 
 
 refresh_env()
@@ -744,21 +739,31 @@ def _bp_check(name: str, t: torch.Tensor, dev) -> None:
                          f"{t.dtype} {tuple(t.stride())} on {t.device}")
 
 
-def beta_panels(F3: torch.Tensor, beta: float, out: torch.Tensor | None = None) -> torch.Tensor:
+def beta_panels(F3: torch.Tensor, beta: float, out: torch.Tensor | None = None,
+                row_scale: torch.Tensor | None = None) -> torch.Tensor:
     """Split operand panels of F3 (R, K, L), unit inner stride, K <= 32, for the beta-MU
     kernels at ``beta`` (beta_planes.hip bp_panel_kernel): per replicate, chunks of 64 rows
     of the L axis, each holding the bf16 planes of the P-product layout (6 terms; KL 3) and
     the two planes of the permuted numerator layout (KL: fp16, row-scaled, with the scales
-    in a tail).  Returns (R, panel_elems) int16."""
+    in a tail).  ``row_scale`` (L,) float32 (KL only): the P-product panel is built from
+    F[k][l] * row_scale[l] -- the usage-side panels for fp16 count X (x = c u_l, row_scale
+    = 1 / u, so c / P' = x / P; :func:`beta_h_block` ``xh``).  Returns (R, panel_elems)
+    int16."""
     R, K, L = F3.shape
     _native_dtype_k("beta_panels", F3.dtype, K, _hip.bp_max_k())
     _bp_check("F3", F3, F3.device)
     mode = beta_mode(beta)
+    if row_scale is not None and (mode != 0 or row_scale.dtype != torch.float32
+                                  or row_scale.numel() < L or not row_scale.is_contiguous()
+                                  or row_scale.device != F3.device):
+        raise ValueError("row_scale: KL only, contiguous float32 (L,) on the device")
     n = int(_hip.bp_panel_elems(K, L, mode))
     if out is None or out.shape != (R, n) or out.dtype != torch.int16 or not out.is_contiguous():
         out = torch.empty((R, n), dtype=torch.int16, device=F3.device)
-    _hip.bp_panels(F3.data_ptr(), F3.stride(0), F3.stride(1), K, L, R, mode, out.data_ptr(), n,
+    _hip.bp_panels(F3.data_ptr(), F3.stride(0), F3.stride(1), K, L, R, mode,
+                   row_scale.data_ptr() if row_scale is not None else 0, out.data_ptr(), n,
                    _stream_ptr(F3))
+    out._cnmf_row_scaled = row_scale is not None
     return out
 
 
@@ -776,7 +781,8 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
                  iters: torch.Tensor | None = None, conv_mode: int = 1,
                  hstate: torch.Tensor | None = None, loss_entry: bool = False,
                  den_vec: torch.Tensor | None = None,
-                 panels: torch.Tensor | None = None, xsum: float | None = None) -> None:
+                 panels: torch.Tensor | None = None, xsum: float | None = None,
+                 xh: torch.Tensor | None = None, unit: torch.Tensor | None = None) -> None:
     """``nsteps`` fused beta-MU steps of the usages HT3 (R, K, N) in place against the
     spectra W3 (R, K, G) on rows X (N, G), in ONE launch (beta_planes.hip, side 0):
     HT3 *= (num / (den + l1 + l2 HT3))^gamma with num/den of the split-bf16 MFMA
@@ -787,7 +793,10 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
     this launch; else the value ``hstate`` (float64 (R, 2): last objective, checks) holds);
     conv_mode 0 -- relative change of the last step.  act[r] -> 0 when the rule holds; iters[r] += nsteps.  ``panels``: the
     :func:`beta_panels` of W3 (built here when omitted); ``xsum``: sum(X) in float64 (KL
-    objective; computed here -- one host sync -- when omitted)."""
+    objective; computed here -- one host sync -- when omitted).  KL on fp16 counts: ``xh``
+    (N, G) float16 with X == xh * ``unit`` (per gene) is read instead of X (half the
+    bytes; X itself is only used for shapes), with ``panels`` built by
+    :func:`beta_panels` with ``row_scale = 1 / unit``."""
     R, K, N = HT3.shape
     G = W3.shape[2]
     if X.shape != (N, G) or W3.shape[:2] != (R, K):
@@ -819,15 +828,24 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
             raise ValueError("den_vec: contiguous float32 (R, K) on the device required")
     else:
         den_vec = None
+    if xh is not None:
+        if (mode != 0 or xh.dtype != torch.float16 or xh.shape != (N, G) or xh.stride(1) != 1
+                or unit is None or unit.numel() < G or unit.dtype != torch.float32):
+            raise ValueError("xh: KL, float16 (N, G) counts with a float32 (G,) unit")
+        if panels is None or not getattr(panels, "_cnmf_row_scaled", False):
+            raise ValueError("xh needs panels built with row_scale = 1 / unit")
     if panels is None:
         panels = beta_panels(W3, beta)
     _bp_panels_check(panels, R, K, G, mode)
+    if xh is None and getattr(panels, "_cnmf_row_scaled", False):
+        raise ValueError("row-scaled panels (fp16 counts) need xh")
     n_strips = -(-N // int(_hip.bp_strip_cols(K, mode)))
     part = counter = 0
     if tol is not None:
         ws = _bp_ws(dev, _stream_ptr(HT3), R, n_strips)
         part, counter = ws["part"].data_ptr(), ws["counter"].data_ptr()
-    _hip.bp_run(0, mode, X.data_ptr(), X.stride(0), panels.data_ptr(), panels.stride(0),
+    xs = xh if xh is not None else X
+    _hip.bp_run(0, mode, xs.data_ptr(), xs.stride(0), panels.data_ptr(), panels.stride(0),
                 HT3.data_ptr(), HT3.stride(0), HT3.stride(1), K, N, G, R, 1, float(beta),
                 float(eps), 0, 0, int(nsteps), int(bool(loss_entry) and tol is not None),
                 int(tol is not None and conv_mode == 1),
@@ -839,6 +857,7 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
                 act.data_ptr() if act is not None else 0, 0,
                 float(xsum if xsum is not None else (
                     float(X.sum(dtype=torch.float64)) if (mode == 0 and rule_loss) else 0.0)),
+                int(xh is not None), unit.data_ptr() if xh is not None else 0, 0,
                 _stream_ptr(HT3))
 
 
@@ -873,7 +892,7 @@ def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float,
                 float(beta), float(eps), 0, 0, 0, 0, 1,
                 wsum.data_ptr() if wsum is not None else 0, 0.0, 0.0, 1.0, 0.0, 0, 0, 0, 0, 0,
                 0, active.data_ptr() if active is not None else 0, loss.data_ptr(), 0.0,
-                _stream_ptr(HT3))
+                0, 0, 0, _stream_ptr(HT3))
     tot = loss.sum(1)
     if mode == 0:
         tot = tot - X.sum(dtype=torch.float64)
@@ -883,11 +902,14 @@ def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float,
 def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
                     W3: torch.Tensor, beta: float, eps: float,
                     active: torch.Tensor | None = None, splits: int | None = None,
-                    panels: torch.Tensor | None = None):
+                    panels: torch.Tensor | None = None, xth: torch.Tensor | None = None,
+                    unit_inv: torch.Tensor | None = None):
     """W-side beta-MU statistics of rows X (c, G) with the chunk's usages HT3 (R, K, c):
     num = HT Q, den = HT D (None for KL) as (splits, R, K, G) partials -- the operand
     layout of :func:`beta_w_update` (beta_planes.hip side 1: HT streamed from its split-bf16
-    panels, W3 the fixed operand, X read through its transpose ``XT`` (G, c))."""
+    panels, W3 the fixed operand, X read through its transpose ``XT`` (G, c)).  KL on fp16
+    counts: ``xth`` (G, c) float16 with X^T == xth * unit per row, ``unit_inv`` = 1 / unit
+    (G,) -- read instead of XT (which may then be None)."""
     R, K, c = HT3.shape
     G = W3.shape[2]
     if X.shape != (c, G) or W3.shape[:2] != (R, K):
@@ -897,9 +919,14 @@ def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
         return num.unsqueeze(0), (den.unsqueeze(0) if den is not None else None)
     dev = HT3.device
     _native_dtype_k("beta_w_partials", HT3.dtype, K, _hip.bp_max_k())
-    if XT is None or XT.shape != (G, c):
+    if xth is not None:
+        if (beta_mode(beta) != 0 or xth.dtype != torch.float16 or xth.shape != (G, c)
+                or xth.stride(1) != 1 or unit_inv is None or unit_inv.numel() < G
+                or unit_inv.dtype != torch.float32):
+            raise ValueError("xth: KL, float16 (G, c) counts with a float32 (G,) unit_inv")
+    elif XT is None or XT.shape != (G, c):
         raise ValueError("beta_w_partials: XT (G, c) required on the device")
-    for name, t in (("XT", XT), ("HT3", HT3), ("W3", W3)):
+    for name, t in (("HT3", HT3), ("W3", W3)) + ((("XT", XT),) if xth is None else ()):
         _bp_check(name, t, dev)
     if active is not None and (active.dtype != torch.int32 or active.numel() < R
                                or not active.is_contiguous()):
@@ -914,11 +941,13 @@ def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
     n_split = int(_hip.bp_splits(c, int(splits)))
     num = torch.empty((n_split, R, K, G), dtype=torch.float32, device=dev)
     den = torch.empty_like(num) if mode != 0 else None
-    _hip.bp_run(1, mode, XT.data_ptr(), XT.stride(0), panels.data_ptr(), panels.stride(0),
+    xs = xth if xth is not None else XT
+    _hip.bp_run(1, mode, xs.data_ptr(), xs.stride(0), panels.data_ptr(), panels.stride(0),
                 W3.data_ptr(), W3.stride(0), W3.stride(1), K, G, c, R, n_split, float(beta),
                 float(eps), num.data_ptr(), den.data_ptr() if den is not None else 0, 1, 0, 0,
                 0, 0.0, 0.0, 1.0, 0.0, 0, 0, 0, 0, 0, 0,
-                active.data_ptr() if active is not None else 0, 0, 0.0, _stream_ptr(HT3))
+                active.data_ptr() if active is not None else 0, 0, 0.0, int(xth is not None), 0,
+                unit_inv.data_ptr() if xth is not None else 0, _stream_ptr(HT3))
     return num, den
 
 

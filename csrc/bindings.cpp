@@ -115,12 +115,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("bp_panel_elems",
         [](int K, int L, int mode) { return cnmf_bp_panel_elems(K, L, mode); });
   m.def("bp_strip_cols", [](int K, int mode) { return cnmf_bp_strip_cols(K, mode); });
-  m.def("bp_set_kl_ct", [](int ct) { return cnmf_bp_set_kl_ct(ct); });
   m.def("bp_splits", [](int Ls, int splits) { return cnmf_bp_splits(Ls, splits); });
   m.def("bp_panels",
         [](uintptr_t F, long long f_rs, long long ldf, int K, int L, int R, int mode,
-           uintptr_t out, long long out_rs, uintptr_t stream) {
-          check(cnmf_bp_panels(P<const float>(F), f_rs, ldf, K, L, R, mode, P<unsigned short>(out),
+           uintptr_t prow, uintptr_t out, long long out_rs, uintptr_t stream) {
+          check(cnmf_bp_panels(P<const float>(F), f_rs, ldf, K, L, R, mode, P<const float>(prow),
+                               P<unsigned short>(out),
                                out_rs, reinterpret_cast<hipStream_t>(stream)),
                 "bp_panels");
         });
@@ -130,13 +130,15 @@ PYBIND11_MODULE(_hip, m) {
            float beta, float eps, uintptr_t num, uintptr_t den, int nsteps, int loss_entry,
            int loss_exit, uintptr_t den_vec, float l1, float l2, float gamma, float tol,
            int conv_mode, uintptr_t hstate, uintptr_t part, uintptr_t counter, uintptr_t act,
-           uintptr_t iters, uintptr_t active, uintptr_t loss, double xsum, uintptr_t stream) {
+           uintptr_t iters, uintptr_t active, uintptr_t loss, double xsum, int xh,
+           uintptr_t uvec, uintptr_t fscale, uintptr_t stream) {
           check(cnmf_bp_run(side, mode, P<const float>(X), ldx, P<const unsigned short>(panel),
                             panel_rs, P<float>(F), f_rs, ldf, K, Lf, Ls, R, splits, beta, eps,
                             P<float>(num), P<float>(den), nsteps, loss_entry, loss_exit,
                             P<const float>(den_vec), l1, l2, gamma, tol, conv_mode,
                             P<double>(hstate), P<double>(part), P<int>(counter), P<int>(act),
-                            P<int>(iters), P<const int>(active), P<double>(loss), xsum,
+                            P<int>(iters), P<const int>(active), P<double>(loss), xsum, xh,
+                            P<const float>(uvec), P<const float>(fscale),
                             reinterpret_cast<hipStream_t>(stream)),
                 "bp_run");
         });

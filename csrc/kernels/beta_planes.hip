@@ -64,6 +64,7 @@ namespace cnmf {
 typedef short bp_v8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bp_b8 __attribute__((ext_vector_type(8)));
 typedef _Float16 bp_h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 bp_h4 __attribute__((ext_vector_type(4)));
 typedef float bp_f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int bp_u4 __attribute__((ext_vector_type(4)));
 
@@ -89,12 +90,10 @@ __host__ __device__ constexpr int bp_chunk(int NP, int T) {
   return (kBpCH * bp_ps(NP) + 2 * 16 * T * kBpNS + kBpThreads * 8 - 1) / (kBpThreads * 8) *
          (kBpThreads * 8);
 }
-// column tiles per wave: 2 (4: 820 vs 510 us per usage step).  The KL kernels can run 1
-// (cnmf_bp_set_kl_ct): fewer live registers (3-4 waves per SIMD instead of 2) and twice
-// the workgroups, but measured slower (290 vs 325 rep/s at the headline: the panel
-// chunks in LDS then serve 64 columns instead of 128)
+// column tiles per wave: 2 (4: 820 vs 510 us per usage step; 1 for KL -- fewer live
+// registers, twice the workgroups -- measured 290 vs 325 rep/s: the panel chunks in LDS
+// then serve 64 columns instead of 128, profiles/r3l_*)
 __host__ __device__ constexpr int bp_ct(int T) { return 2; }
-static int g_bp_kl_ct = 2;
 __host__ __device__ constexpr int bp_ks(int T) { return 16 * T + 1; }     // exchange stride
 
 // plane of the streamed (a) / fixed (b) operand in product term t (0..5)
@@ -129,6 +128,7 @@ __global__ void __launch_bounds__(256) bp_panel_kernel(const float* __restrict__
                                                        long long f_rs, long long ldf, int K,
                                                        int L, int nchunks, int R, int NP,
                                                        int T, int nt, int kl,
+                                                       const float* __restrict__ rowsc,
                                                        unsigned short* __restrict__ out,
                                                        long long out_rs) {
   const long long per = (long long)nchunks * kBpCH;
@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) bp_panel_kernel(const float* __restrict__
     unsigned short a0 = 0, a1 = 0, a2 = 0, n0 = 0, n1 = 0;
     if (k < K && l < L) {
       const float v = f[(long long)k * ldf];
-      bp_split3(v, a0, a1, a2);
+      bp_split3(rowsc ? v * rowsc[l] : v, a0, a1, a2);   // P panel of S / u (fp16 counts)
       if (kl) {
         const float s = v * rsc[k];
         const _Float16 h0 = (_Float16)s;
@@ -203,6 +203,11 @@ struct BpParams {
   const float* X;              // element (fixed col c, streamed row j) at X[c * ldx + j]
   long long ldx;
   int xvec;                    // ldx % 4 == 0 and X 16-byte aligned: float4 loads
+  // KL on fp16 counts (x = c * u_g, c <= 2048 exact in fp16): X points at the counts
+  // (_Float16); the H side's P panel was built from S / u (so c / P' = x / P), the loss
+  // weights x by uvec (per streamed row); the W side scales its fixed operand by fscale
+  const float* uvec;
+  const float* fscale;
   const unsigned short* panel; // streamed operand panels, replicate r at panel + r*panel_rs
   long long panel_rs;
   float* F;                    // fixed operand, replicate r: F + r*f_rs, row k stride ldf
@@ -288,7 +293,7 @@ __device__ __forceinline__ void bp_load4(const float* __restrict__ row, int j, i
   }
 }
 
-template <int NP, int T, int MODE, bool UPD, int CT>
+template <int NP, int T, int MODE, bool UPD, int CT, bool XH>
 __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
   constexpr int PS = bp_ps(NP);
   constexpr int CE = bp_chunk(NP, T);
@@ -325,11 +330,15 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
 
   bool cok[CT];
   const float* xrow[CT];
+  const _Float16* xhrow[CT];
+  float fsc[CT];   // XH, W side: 1 / u of the column's gene
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) {
     const int col = col_w + 16 * ct + m;
     cok[ct] = col < p.Lf;
     xrow[ct] = p.X + (long long)(cok[ct] ? col : 0) * p.ldx;
+    xhrow[ct] = reinterpret_cast<const _Float16*>(p.X) + (long long)(cok[ct] ? col : 0) * p.ldx;
+    fsc[ct] = (XH && !UPD && cok[ct]) ? p.fscale[col] : 1.f;
   }
 
   // KL: per-column shift 2^s of F (csc) and s (csg); inverse panel row scales 2^e_k
@@ -372,7 +381,8 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
       for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          sx[(16 * ct + m) * KS + 16 * t + 4 * q + i] = kH ? hc[ct][t][i] * csc[ct] : hc[ct][t][i];
+          sx[(16 * ct + m) * KS + 16 * t + 4 * q + i] =
+              kH ? hc[ct][t][i] * (csc[ct] * fsc[ct]) : hc[ct][t][i];
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
@@ -428,6 +438,30 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
     // are discarded), guarded scalar loads at the tail
     auto load_x = [&](int b, float (&dst)[CT][8]) {
       const int j0 = (c_begin + (b >> 1)) * kBpCH + (b & 1) * 32;
+      if constexpr (XH) {
+        if (p.xvec && j0 + 32 <= p.Ls) {
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) {
+            const bp_h4 v0 = *reinterpret_cast<const bp_h4*>(xhrow[ct] + j0 + 4 * q);
+            const bp_h4 v1 = *reinterpret_cast<const bp_h4*>(xhrow[ct] + j0 + 16 + 4 * q);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              dst[ct][i] = (float)v0[i];
+              dst[ct][4 + i] = (float)v1[i];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int ja = j0 + 4 * q + i, jb = j0 + 16 + 4 * q + i;
+              dst[ct][i] = (cok[ct] && ja < p.Ls) ? (float)xhrow[ct][ja] : 0.f;
+              dst[ct][4 + i] = (cok[ct] && jb < p.Ls) ? (float)xhrow[ct][jb] : 0.f;
+            }
+        }
+        return;
+      }
       if (p.xvec && j0 + 32 <= p.Ls) {
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
@@ -488,6 +522,24 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
         // phase 2: elementwise terms, loss, operand planes; phase 3: numerator MFMAs
         if constexpr (kH) {
           bp_h8 qh[CT];
+          // XH: the loss weight x = c u_j of each streamed row (u from L1)
+          float uw[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) uw[e] = 1.f;
+          if (XH && kLoss) {
+            if (j0 + 32 <= p.Ls) {
+              const float4 u0 = *reinterpret_cast<const float4*>(p.uvec + j0 + 4 * q);
+              const float4 u1 = *reinterpret_cast<const float4*>(p.uvec + j0 + 16 + 4 * q);
+              uw[0] = u0.x; uw[1] = u0.y; uw[2] = u0.z; uw[3] = u0.w;
+              uw[4] = u1.x; uw[5] = u1.y; uw[6] = u1.z; uw[7] = u1.w;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                const int j = j0 + (e >> 2) * 16 + 4 * q + (e & 3);
+                uw[e] = j < p.Ls ? p.uvec[j] : 0.f;
+              }
+            }
+          }
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) {
 #pragma unroll
@@ -497,7 +549,8 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
               if (kLoss) {
                 // x log2(x / p) with q' = q 2^-s: log2 q = log2 q' + s
                 const int j = j0 + (e >> 2) * 16 + 4 * q + (e & 3);
-                const float t = x > 0.f ? x * (__builtin_amdgcn_logf(qv) + csg[ct]) : 0.f;
+                const float t = x > 0.f ? (x * uw[e]) * (__builtin_amdgcn_logf(qv) + csg[ct])
+                                        : 0.f;
                 lsum += (cok[ct] && j < p.Ls) ? t : 0.f;
               }
               if (kNum) qh[ct][e] = (_Float16)qv;
@@ -775,14 +828,14 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
   }
 }
 
-template <int NP, int T, int MODE, bool UPD, int CT = bp_ct(T)>
+template <int NP, int T, int MODE, bool UPD, bool XH = false, int CT = bp_ct(T)>
 hipError_t bp_launch(const BpParams& p, hipStream_t s) {
   const size_t lds = (size_t)2 * bp_chunk(NP, T) * 2 +
                      (size_t)kBpWaves * CT * 16 * bp_ks(T) * sizeof(float);
   static bool attr_done = false;
   if (!attr_done) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&bp_kernel<NP, T, MODE, UPD, CT>),
+        reinterpret_cast<const void*>(&bp_kernel<NP, T, MODE, UPD, CT, XH>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_done = true;
@@ -790,7 +843,7 @@ hipError_t bp_launch(const BpParams& p, hipStream_t s) {
   const int units = p.n_strips * p.splits;
   const int per_xcd = (units + 7) / 8;
   const dim3 grid((unsigned)(per_xcd * p.R * 8));
-  hipLaunchKernelGGL((bp_kernel<NP, T, MODE, UPD, CT>), grid, dim3(kBpThreads), lds, s, p);
+  hipLaunchKernelGGL((bp_kernel<NP, T, MODE, UPD, CT, XH>), grid, dim3(kBpThreads), lds, s, p);
   return hipGetLastError();
 }
 
@@ -798,11 +851,11 @@ template <int MODE, bool UPD>
 hipError_t bp_launch_k(const BpParams& p, hipStream_t s) {
   if constexpr (MODE == kBpKL) {
     const int np = bp_np(p.K, kBpKL), t = bp_t(p.K);
-    if (g_bp_kl_ct == 1) {
-      if (np == 1 && t == 1) return bp_launch<1, 1, MODE, UPD, 1>(p, s);
-      if (np == 2 && t == 1) return bp_launch<2, 1, MODE, UPD, 1>(p, s);
-      if (np == 2 && t == 2) return bp_launch<2, 2, MODE, UPD, 1>(p, s);
-      if (np == 3 && t == 2) return bp_launch<3, 2, MODE, UPD, 1>(p, s);
+    if (p.uvec != nullptr || p.fscale != nullptr) {   // fp16 counts
+      if (np == 1 && t == 1) return bp_launch<1, 1, MODE, UPD, true>(p, s);
+      if (np == 2 && t == 1) return bp_launch<2, 1, MODE, UPD, true>(p, s);
+      if (np == 2 && t == 2) return bp_launch<2, 2, MODE, UPD, true>(p, s);
+      if (np == 3 && t == 2) return bp_launch<3, 2, MODE, UPD, true>(p, s);
       return hipErrorInvalidValue;
     }
     if (np == 1 && t == 1) return bp_launch<1, 1, MODE, UPD>(p, s);
@@ -846,22 +899,15 @@ extern "C" long long cnmf_bp_panel_elems(int K, int L, int mode) {
          (mode == cnmf::kBpKL ? cnmf::kBpTail : 0);
 }
 
-// column tiles per wave of the KL kernels (1 or 2); returns the previous setting
-extern "C" int cnmf_bp_set_kl_ct(int ct) {
-  const int prev = cnmf::g_bp_kl_ct;
-  if (ct == 1 || ct == 2) cnmf::g_bp_kl_ct = ct;
-  return prev;
-}
-
 // fixed-axis columns per workgroup strip
 extern "C" int cnmf_bp_strip_cols(int K, int mode) {
-  const int ct = mode == cnmf::kBpKL ? cnmf::g_bp_kl_ct : cnmf::bp_ct(cnmf::bp_t(K));
-  return cnmf::kBpWaves * ct * 16;
+  (void)mode;
+  return cnmf::kBpWaves * cnmf::bp_ct(cnmf::bp_t(K)) * 16;
 }
 
 extern "C" hipError_t cnmf_bp_panels(const float* F, long long f_rs, long long ldf, int K, int L,
-                                     int R, int mode, unsigned short* out, long long out_rs,
-                                     hipStream_t stream) {
+                                     int R, int mode, const float* prow, unsigned short* out,
+                                     long long out_rs, hipStream_t stream) {
   if (R <= 0 || L <= 0) return hipSuccess;
   if (K < 1 || K > 32 || mode < 0 || mode > 2) return hipErrorInvalidValue;
   if (out_rs < cnmf_bp_panel_elems(K, L, mode)) return hipErrorInvalidValue;
@@ -875,7 +921,7 @@ extern "C" hipError_t cnmf_bp_panels(const float* F, long long f_rs, long long l
   const long long n = (long long)R * nchunks * cnmf::kBpCH;
   const dim3 grid((unsigned)((n + 255) / 256));
   hipLaunchKernelGGL(cnmf::bp_panel_kernel, grid, dim3(256), 0, stream, F, f_rs, ldf, K, L,
-                     nchunks, R, NP, T, cnmf::bp_nt(mode), kl ? 1 : 0, out, out_rs);
+                     nchunks, R, NP, T, cnmf::bp_nt(mode), kl ? 1 : 0, prow, out, out_rs);
   return hipGetLastError();
 }
 
@@ -886,14 +932,22 @@ extern "C" hipError_t cnmf_bp_run(
     int splits, float beta, float eps, float* num, float* den, int nsteps, int loss_entry,
     int loss_exit, const float* den_vec, float l1, float l2, float gamma, float tol,
     int conv_mode, double* hstate, double* part, int* counter, int* act, int* iters,
-    const int* active, double* loss, double xsum, hipStream_t stream) {
+    const int* active, double* loss, double xsum, int xh, const float* uvec,
+    const float* fscale, hipStream_t stream) {
   if (R <= 0 || Lf <= 0) return hipSuccess;
   if (K < 1 || K > 32 || Ls <= 0 || (side != 0 && side != 1)) return hipErrorInvalidValue;
+  // fp16 counts: KL only; the H side needs the loss weights, the W side the column scales
+  if (xh && (mode != cnmf::kBpKL || (side == 0 ? uvec == nullptr : fscale == nullptr)))
+    return hipErrorInvalidValue;
   if (mode < 0 || mode > 2 || panel_rs < cnmf_bp_panel_elems(K, Ls, mode))
     return hipErrorInvalidValue;
   cnmf::BpParams p;
   p.X = X; p.ldx = ldx;
-  p.xvec = (ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(X) & 15) == 0);
+  p.xvec = (ldx % 4 == 0) &&
+           ((reinterpret_cast<uintptr_t>(X) & (xh ? 7 : 15)) == 0);
+  p.uvec = xh ? (side == 0 ? uvec : nullptr) : nullptr;
+  p.fscale = xh ? (side == 1 ? fscale : nullptr) : nullptr;
+  if (xh && side == 0 && p.uvec == nullptr) return hipErrorInvalidValue;
   p.panel = panel; p.panel_rs = panel_rs;
   p.F = F; p.f_rs = f_rs; p.ldf = ldf;
   p.K = K; p.Lf = Lf; p.Ls = Ls; p.R = R;

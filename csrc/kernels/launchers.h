@@ -52,11 +52,10 @@ hipError_t cnmf_beta_w_update(int mode, float* W, long long w_rs, long long ldw,
 int cnmf_bp_max_k();
 long long cnmf_bp_panel_elems(int K, int L, int mode);
 int cnmf_bp_strip_cols(int K, int mode);
-int cnmf_bp_set_kl_ct(int ct);
 int cnmf_bp_splits(int Ls, int splits);
 hipError_t cnmf_bp_panels(const float* F, long long f_rs, long long ldf, int K, int L, int R,
-                          int mode,
-                          unsigned short* out, long long out_rs, hipStream_t stream);
+                          int mode, const float* prow, unsigned short* out, long long out_rs,
+                          hipStream_t stream);
 hipError_t cnmf_bp_run(int side, int mode, const float* X, long long ldx,
                        const unsigned short* panel, long long panel_rs, float* F, long long f_rs,
                        long long ldf, int K, int Lf, int Ls, int R, int splits, float beta,
@@ -64,7 +63,7 @@ hipError_t cnmf_bp_run(int side, int mode, const float* X, long long ldx,
                        int loss_exit, const float* den_vec, float l1, float l2, float gamma,
                        float tol, int conv_mode, double* hstate, double* part, int* counter,
                        int* act, int* iters, const int* active, double* loss, double xsum,
-                       hipStream_t stream);
+                       int xh, const float* uvec, const float* fscale, hipStream_t stream);
 
 // sparse_kl.hip: KL MU statistics over a CSR matrix
 int cnmf_sk_k4(int K);

@@ -803,6 +803,42 @@ def test_kl_fp16_numerator_overflow_is_redone_with_a_shift():
     torch.testing.assert_close(num.sum(0).cpu().double(), rn, rtol=1e-3, atol=1e-5)
 
 
+def test_kl_fp16_count_operands_match_fp64():
+    """KL kernels reading X as fp16 counts (X = C u_g; P panel of W / u, loss weights u,
+    spectra side's W scaled by 1 / u) vs the float64 reference on the fp32 X."""
+    g = torch.Generator().manual_seed(5)
+    R, K, N, G = 3, 10, 777, 300
+    C = torch.poisson(torch.rand((N, G), generator=g, dtype=torch.float64) * 3)
+    u = torch.rand(G, generator=g, dtype=torch.float64) * 2 + 0.1
+    X = C * u
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) + 0.05
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64) + 0.05
+    dev = torch.device("cuda")
+    eps = 1e-10
+    Xg, Hg, Wg = X.float().to(dev), HT.float().to(dev), W.float().to(dev)
+    ug = u.float().to(dev)
+    xh = C.to(torch.float16).to(dev)
+    pan = ops.beta_panels(Wg, 1.0, row_scale=(1.0 / ug).contiguous())
+    h1 = Hg.clone()
+    act = torch.ones(R, dtype=torch.int32, device=dev)
+    hs = torch.zeros((R, 2), dtype=torch.float64, device=dev)
+    ops.beta_h_block(Xg, h1, Wg, 1.0, eps, 4, act=act, tol=1e-12, hstate=hs, loss_entry=True,
+                     panels=pan, xh=xh, unit=ug)
+    h2 = HT.clone()
+    act_r = torch.ones(R, dtype=torch.int32)
+    hs_r = torch.zeros((R, 2), dtype=torch.float64)
+    reference.beta_h_block(X, h2, W, 1.0, eps, 4, act=act_r, tol=1e-12, hstate=hs_r,
+                           loss_entry=True)
+    torch.testing.assert_close(h1.cpu().double(), h2, rtol=1e-3, atol=1e-6)
+    torch.testing.assert_close(hs.cpu()[:, 0], hs_r[:, 0], rtol=1e-4, atol=1e-3)
+    rn, _, _ = reference.beta_contract(1, X, HT, W, 1.0, eps, True, False)
+    num, _ = ops.beta_w_partials(Xg, None, Hg, Wg, 1.0, eps, splits=2,
+                                 xth=xh.t().contiguous(), unit_inv=(1.0 / ug).contiguous())
+    torch.testing.assert_close(num.sum(0).cpu().double(), rn, rtol=5e-4, atol=1e-5)
+    with pytest.raises(ValueError):        # row-scaled panels without the counts
+        ops.beta_h_block(Xg, Hg.clone(), Wg, 1.0, eps, 1, panels=pan)
+
+
 def test_online_kl_matches_fp32_torch_path():
     """Online KL through the fp16-numerator kernels vs the same solver on plain fp32
     PyTorch ops (CNMF_FORCE_TORCH_OPS=1): final objectives within 1e-3, passes within 1."""
