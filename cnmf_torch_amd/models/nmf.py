@@ -909,16 +909,19 @@ class PlanesOnlyX:
 
 def native_rank(K: int) -> int:
     """The rank the GPU kernels run a rank-K replicate at: K itself for K <= 32, else K
-    padded to a multiple of 8 (<= 64) with zero components -- a zero row of W / H stays
-    zero under MU (rate 0 where the denominator vanishes) and HALS (zero diagonal), and
-    contributes nothing to the Gram matrices or the loss, so the padded solve IS the
-    rank-K solve (cnmf.py:1416 takes any -k)."""
+    padded with zero components to a multiple of 8 (<= 64) or of 16 (<= 128, MU only: the
+    matrix-core wide solve, solve_wmfma.hip) -- a zero row of W / H stays zero under MU
+    (rate 0 where the denominator vanishes) and HALS (zero diagonal), and contributes
+    nothing to the Gram matrices or the loss, so the padded solve IS the rank-K solve
+    (cnmf.py:1416 takes any -k)."""
     K = int(K)
     if K <= 32:
         return K
-    if K > 64:
-        raise ValueError(f"K={K}: the native kernels cover K <= 64")
-    return -(-K // 8) * 8
+    if K <= 64:
+        return -(-K // 8) * 8
+    if K > 128:
+        raise ValueError(f"K={K}: the native kernels cover K <= 128")
+    return -(-K // 16) * 16
 
 
 _GRAM_PROLOGUE = os.environ.get("CNMF_SOLVE_GRAM_PROLOGUE", "0") == "1"

@@ -81,8 +81,24 @@ def numer_cols(U: torch.Tensor, X, block: int = 16384) -> torch.Tensor:
 def chunked_solve(HT: torch.Tensor, numerT: torch.Tensor, gram: torch.Tensor, chunk_size: int,
                   chunk_max_iter: int, h_tol: float, l1_num: float = 0.0, l2: float = 0.0,
                   eps: float = 1e-16, algo: str = "mu") -> torch.Tensor:
-    """Independent per-chunk solves of HT (K x n) in place; one launch for all full chunks."""
+    """Independent per-chunk solves of HT (K x n) in place; one launch for all full chunks.
+    On the GPU a rank without its own kernel instantiation (K > 32 not a multiple of 8,
+    K > 64 not a multiple of 16) is solved padded with zero components, which stay zero
+    and leave the Gram products and the objective unchanged (models.nmf.native_rank)."""
     K, n = HT.shape
+    if HT.device.type == "cuda" and algo != "bpp" and ops.use_native(HT):
+        from .nmf import native_rank
+
+        Kp = native_rank(K)
+        if Kp != K:
+            HTp = torch.zeros((Kp, n), device=HT.device, dtype=HT.dtype)
+            Np = torch.zeros((Kp, n), device=HT.device, dtype=numerT.dtype)
+            Gp = torch.zeros((Kp, Kp), device=HT.device, dtype=gram.dtype)
+            HTp[:K], Np[:K], Gp[:K, :K] = HT, numerT, gram
+            chunked_solve(HTp, Np, Gp, chunk_size, chunk_max_iter, h_tol, l1_num=l1_num,
+                          l2=l2, eps=eps, algo=algo)
+            HT.copy_(HTp[:K])
+            return HT
     c = max(1, min(int(chunk_size), n))
     full = n // c
     g1 = gram.reshape(1, K, K).contiguous()

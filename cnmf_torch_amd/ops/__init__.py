@@ -190,11 +190,14 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     h = _hip
     # a GPU operand the kernels do not cover is an error, never a silent eager fallback:
     # fp32 only; K in 1..32 or a padded wide rank (the engine pads K <= 64 to a multiple
-    # of 8, models/nmf.py native_rank)
+    # of 8 and K <= 128 to a multiple of 16, models/nmf.py native_rank)
     _native_dtype_k("solve", x.dtype, K, h.solve_max_k())
     if not h.solve_native_k(K):
-        raise ValueError(f"solve: K={K} has no kernel instantiation (pad it to a multiple "
-                         "of 8, see models.nmf.native_rank)")
+        raise ValueError(f"solve: K={K} has no kernel instantiation (pad it with zero "
+                         "components, see models.nmf.native_rank)")
+    if K > 64 and a != 0:
+        raise ValueError(f"solve: K={K} > 64 runs the matrix-core MU solve only "
+                         f"(algo={algo!r}); use algo='mu' or 'bpp'")
     _check_block_view("x", x, R, K, n)
     _check_block_view("numer", numer, R, K, n)
     if gram is not None:
@@ -1109,7 +1112,8 @@ def kl_sparse_w_num(tiles: list, HT3: torch.Tensor, W3: torch.Tensor, eps: float
 def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
          active: torch.Tensor | None = None) -> torch.Tensor:
     """out[r] (+)= X3[r] X3[r]^T for X3 (R, K, n) with unit column stride (any row and
-    replicate strides), K <= 32: one MFMA workgroup per replicate (gram.hip).  Replicates
+    replicate strides), K <= 128: one MFMA workgroup per replicate (four for K > 64, one
+    per 64 x 64 block; gram.hip).  Replicates
     whose ``active`` flag is 0 keep their ``out`` untouched."""
     R, K, n = X3.shape
     if out is None:
@@ -1118,7 +1122,7 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
         out = torch.empty((R, K, K), device=X3.device, dtype=X3.dtype)
     native = use_native(X3)
     if native:
-        _native_dtype_k("gram", X3.dtype, K, 64)
+        _native_dtype_k("gram", X3.dtype, K, 128)
     else:
         g = torch.bmm(X3, X3.transpose(1, 2))
         if active is not None:

@@ -272,8 +272,8 @@ def spmm(A: DeviceCSR, B: torch.Tensor) -> torch.Tensor:
         out = torch.zeros((A.shape[0], K), dtype=torch.float32)
         return out.index_add_(0, rows, v[:, None] * B.float()[c])
     _require_native()
-    if K > 64:
-        raise ValueError("spmm: K <= 64 supported by the CSR kernel")
+    if K > 64:   # the CSR kernel takes <= 64 output columns: column blocks of B
+        return torch.cat([spmm(A, B[:, a:a + 64]) for a in range(0, K, 64)], dim=1)
     Bf = B.to(device=A.device, dtype=torch.float32).contiguous()
     out = torch.empty((A.shape[0], K), dtype=torch.float32, device=A.device)
     _hip.csr_spmm(A.indptr.data_ptr(), A.indices.data_ptr(), A.data.data_ptr(),
@@ -296,8 +296,8 @@ def tspmm(A: DeviceCSR, B: torch.Tensor) -> torch.Tensor:
         out = torch.zeros((n_out, K), dtype=torch.float64)
         return out.index_add_(0, c, v[:, None] * B.double()[rows])
     _require_native()
-    if K > 64:
-        raise ValueError("tspmm: K <= 64 supported by the CSR kernel")
+    if K > 64:   # the CSR kernel takes <= 64 output columns: column blocks of B
+        return torch.cat([tspmm(A, B[:, a:a + 64]) for a in range(0, K, 64)], dim=1)
     Bd = B.to(A.device)
     if Bd.dtype not in (torch.float32, torch.float64):
         Bd = Bd.double()

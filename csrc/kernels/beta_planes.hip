@@ -55,6 +55,7 @@
 // (beta_mu.hip), and the loss is only evaluated where the rule reads it.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -71,7 +72,11 @@ typedef unsigned int bp_u4 __attribute__((ext_vector_type(4)));
 constexpr int kBpCH = 64;          // streamed rows per panel chunk (two 32-row blocks)
 constexpr int kBpWaves = 4;        // waves per workgroup
 constexpr int kBpThreads = 64 * kBpWaves;
-constexpr int kBpNS = kBpCH + 8;   // N-panel row stride (bf16 elements)
+// N-panel row stride (bf16 elements): 160-B rows put the 16 lanes of every ds_read_b128
+// lane group on 16 distinct 4-bank slots (144-B rows: 2-way conflicts on most groups;
+// MI355X_MICROARCH.md §LDS lane groups, profiles/r3k_pmc_beta_kl_fp16.txt
+// SQ_LDS_BANK_CONFLICT 1.3x the LDS-active cycles)
+constexpr int kBpNS = kBpCH + 16;
 
 enum BpMode { kBpKL = 0, kBpIS = 1, kBpGeneral = 2 };
 
@@ -83,7 +88,9 @@ __host__ __device__ constexpr int bp_np(int K, int mode = kBpIS) {
 // per-replicate panel tail (KL): 32 row scales 2^-e_k and their inverses, fp32
 constexpr int kBpTail = 128;
 __host__ __device__ constexpr int bp_t(int K) { return (K + 15) / 16; }
-__host__ __device__ constexpr int bp_ps(int NP) { return 32 * NP + 8; }  // P-panel row stride
+// P-panel row stride: 32 NP + 16 bf16 (96, 160, 224 B rows) is conflict-free for the
+// ds_read_b128 fragment reads; 32 NP + 8 (80 B at NP = 1) was 2-way
+__host__ __device__ constexpr int bp_ps(int NP) { return 32 * NP + 16; }
 // chunk stride (bf16 elements), padded to whole 16-byte pieces per thread so the staging
 // loads are unconditional (the tail of a chunk is never written nor read by the MFMAs)
 __host__ __device__ constexpr int bp_chunk(int NP, int T) {
@@ -293,8 +300,11 @@ __device__ __forceinline__ void bp_load4(const float* __restrict__ row, int j, i
   }
 }
 
-template <int NP, int T, int MODE, bool UPD, int CT, bool XH>
-__global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
+// OCC: waves per SIMD the register allocation targets (2: the compiler's choice, ~235
+// VGPRs for the usage-side kernels; 3: <= 168, with spills outside the hot loop)
+template <int NP, int T, int MODE, bool UPD, int CT, bool XH, int OCC = 2>
+__global__ void __launch_bounds__(kBpThreads) __attribute__((amdgpu_waves_per_eu(OCC)))
+bp_kernel(BpParams p) {
   constexpr int PS = bp_ps(NP);
   constexpr int CE = bp_chunk(NP, T);
   constexpr int PIECES = CE * 2 / 16;
@@ -828,14 +838,14 @@ __global__ void __launch_bounds__(kBpThreads) bp_kernel(BpParams p) {
   }
 }
 
-template <int NP, int T, int MODE, bool UPD, bool XH = false, int CT = bp_ct(T)>
-hipError_t bp_launch(const BpParams& p, hipStream_t s) {
+template <int NP, int T, int MODE, bool UPD, bool XH, int CT, int OCC>
+hipError_t bp_launch_occ(const BpParams& p, hipStream_t s) {
   const size_t lds = (size_t)2 * bp_chunk(NP, T) * 2 +
                      (size_t)kBpWaves * CT * 16 * bp_ks(T) * sizeof(float);
   static bool attr_done = false;
   if (!attr_done) {
     const hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&bp_kernel<NP, T, MODE, UPD, CT, XH>),
+        reinterpret_cast<const void*>(&bp_kernel<NP, T, MODE, UPD, CT, XH, OCC>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_done = true;
@@ -843,8 +853,26 @@ hipError_t bp_launch(const BpParams& p, hipStream_t s) {
   const int units = p.n_strips * p.splits;
   const int per_xcd = (units + 7) / 8;
   const dim3 grid((unsigned)(per_xcd * p.R * 8));
-  hipLaunchKernelGGL((bp_kernel<NP, T, MODE, UPD, CT, XH>), grid, dim3(kBpThreads), lds, s, p);
+  hipLaunchKernelGGL((bp_kernel<NP, T, MODE, UPD, CT, XH, OCC>), grid, dim3(kBpThreads), lds, s,
+                     p);
   return hipGetLastError();
+}
+
+// CNMF_BP_OCC=3: the KL usage-side kernels at three waves per SIMD (A/B knob)
+inline int bp_occ() {
+  static const int v = [] {
+    const char* e = getenv("CNMF_BP_OCC");
+    return (e && e[0] == '3') ? 3 : 2;
+  }();
+  return v;
+}
+
+template <int NP, int T, int MODE, bool UPD, bool XH = false, int CT = bp_ct(T)>
+hipError_t bp_launch(const BpParams& p, hipStream_t s) {
+  if constexpr (MODE == kBpKL && UPD && NP == 1 && T == 1) {
+    if (bp_occ() == 3) return bp_launch_occ<NP, T, MODE, UPD, XH, CT, 3>(p, s);
+  }
+  return bp_launch_occ<NP, T, MODE, UPD, XH, CT, 2>(p, s);
 }
 
 template <int MODE, bool UPD>

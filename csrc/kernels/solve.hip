@@ -9,13 +9,15 @@ hipError_t launch_solve_stream(int K, int algo, const SolveParams& p, int nblock
 }
 }  // namespace cnmf
 
-extern "C" int cnmf_solve_max_k() { return 64; }
+extern "C" int cnmf_solve_max_k() { return 128; }
 extern "C" int cnmf_solve_mfma_max_cols(int K);
 extern "C" int cnmf_solve_pipe_tiles(int K, int per);
 
-// ranks the kernels are instantiated for: 1..32 and the padded wide ranks 40..64
+// ranks the kernels are instantiated for: 1..32, the padded wide ranks 40..64 (multiples
+// of 8) and 80..128 (multiples of 16, MU only: solve_wmfma.hip)
 extern "C" int cnmf_solve_native_k(int K) {
-  return (K >= 1 && K <= 32) || K == 40 || K == 48 || K == 56 || K == 64;
+  return (K >= 1 && K <= 32) || K == 40 || K == 48 || K == 56 || K == 64 || K == 80 ||
+         K == 96 || K == 112 || K == 128;
 }
 
 extern "C" int cnmf_solve_max_threads(int K) { return K > 32 ? 256 : 1024; }
@@ -103,6 +105,9 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
     return cnmf::launch_solve_mfma(K, p, nblocks, T < 1 ? 1 : T, stream);
   }
   if (fused || !gram) return hipErrorInvalidValue;
+  // K > 64: the matrix-core wide solve, MU only (HALS is Gauss-Seidel over components)
+  if (K > 64) return algo == 0 ? cnmf::launch_solve_wmfma(K, p, nblocks, stream)
+                               : hipErrorInvalidValue;
   if (K > 32) return cnmf::launch_solve_wide(K, algo, p, nblocks, threads, stream);
   // variant: 0 auto, 1 streaming, 2 register-resident (3 = mfma above).  Resident needs every slice to
   // fit U <= res_max_cols(K) columns per thread of a <= 1024-thread workgroup; it runs

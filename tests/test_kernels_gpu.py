@@ -1164,6 +1164,117 @@ def test_gram_wide_k_matches_bmm(K):
     np.testing.assert_allclose(out.cpu().double().numpy(), ref.numpy(), rtol=1e-5)
 
 
+@pytest.mark.parametrize("K", [80, 128])
+@pytest.mark.parametrize("conv_mode", [0, 1])
+@pytest.mark.parametrize("split", ["none", "coop", "nsplit"])
+def test_solve_wmfma_matches_fp64_reference(K, conv_mode, split):
+    """K in (64, 128]: the matrix-core wide MU solve (solve_wmfma.hip) against the fp64
+    torch reference of the same op, with l1/l2 terms, lin/quad epilogue and iteration
+    counts; cooperative slices and the fixed-step column split too."""
+    R, n = 3, 2999
+    x0, numer, gram = _problem(R, K, n, seed=K + conv_mode)
+    kw = dict(max_iter=30, tol=1e-3, conv_mode=conv_mode, l1_num=0.01, l2=0.05)
+    if split == "nsplit":
+        kw.update(max_iter=1, nsplit=3)
+    xg = x0.clone().cuda()
+    it_g = torch.zeros(R, dtype=torch.int32, device="cuda")
+    lin_g = torch.zeros(R, dtype=torch.float32, device="cuda")
+    quad_g = torch.zeros(R, dtype=torch.float32, device="cuda")
+    ops.solve("mu", xg, numer.cuda(), gram.cuda(), iters_out=it_g, lin_out=lin_g,
+              quad_out=quad_g, coop=3 if split == "coop" else 1, **kw)
+    ops.coop_check(xg.device)
+    xr = x0.double().clone()
+    it_r = torch.zeros(R, dtype=torch.int32)
+    lin_r = torch.zeros(R, dtype=torch.float64)
+    quad_r = torch.zeros(R, dtype=torch.float64)
+    ops.solve("mu", xr, numer.double(), gram.double(), iters_out=it_r, lin_out=lin_r,
+              quad_out=quad_r, **kw)
+    assert (it_g.cpu() - it_r).abs().max() <= 1
+    np.testing.assert_allclose(xg.cpu().double().numpy(), xr.numpy(), rtol=2e-3, atol=1e-4)
+    np.testing.assert_allclose(lin_g.cpu().double().numpy(), lin_r.numpy(), rtol=2e-3)
+    np.testing.assert_allclose(quad_g.cpu().double().numpy(), quad_r.numpy(), rtol=2e-3)
+
+
+def test_solve_wmfma_planes_and_rep_index():
+    """Wide solve: bf16-planes epilogue equals the split of the result; rep_index/active
+    gating leaves inactive replicates untouched."""
+    K, R, n = 96, 4, 1500
+    x0, numer, gram = _problem(R, K, n, seed=5)
+    xg = x0.clone().cuda()
+    planes = torch.zeros((3, R * K, n + 12), dtype=torch.int16, device="cuda")
+    active = torch.tensor([1, 0, 1, 1], dtype=torch.int32, device="cuda")
+    ri = torch.tensor([3, 1, 0], dtype=torch.int32, device="cuda")
+    ops.solve("mu", xg, numer.cuda(), gram.cuda(), max_iter=10, tol=0.0, rep_index=ri,
+              active=active, planes=planes)
+    xr = x0.double().clone()
+    ops.solve("mu", xr, numer.double(), gram.double(), max_iter=10, tol=0.0)
+    got = xg.cpu().double().numpy()
+    np.testing.assert_array_equal(got[1], x0[1].double().numpy())     # inactive
+    np.testing.assert_array_equal(got[2], x0[2].double().numpy())     # not in rep_index
+    for r in (0, 3):
+        np.testing.assert_allclose(got[r], xr[r].numpy(), rtol=2e-3, atol=1e-4)
+        ref = torch.zeros((3, K, n + 12), dtype=torch.int16)
+        ops.split_planes(xg[r].cpu(), ref)
+        np.testing.assert_array_equal(planes[:, r * K:(r + 1) * K].cpu().numpy(), ref.numpy())
+
+
+def test_solve_wmfma_rejects_hals():
+    x0, numer, gram = _problem(1, 80, 100)
+    with pytest.raises(ValueError, match="MU solve only"):
+        ops.solve("hals", x0.cuda(), numer.cuda(), gram.cuda(), max_iter=2)
+
+
+@pytest.mark.parametrize("K", [65, 100, 128])
+def test_gram_wmfma_k_matches_bmm(K):
+    """K in (64, 128]: four 64 x 64 blocks per replicate; also the column-split partials
+    (few replicates) and accumulate."""
+    for R in (2, 70):
+        X = torch.rand((R, K, 2001), dtype=torch.float32)
+        base = torch.rand((R, K, K), dtype=torch.float32)
+        out = base.cuda()
+        ops.gram(X.cuda(), out=out, accumulate=True)
+        ref = base.double() + torch.bmm(X.double(), X.double().transpose(1, 2))
+        np.testing.assert_allclose(out.cpu().double().numpy(), ref.numpy(), rtol=1e-5)
+
+
+@pytest.mark.parametrize("K", [70, 128])
+def test_nmf_wmfma_k_gpu_matches_cpu(K):
+    """K > 64: padded to a multiple of 16 (zero components) on the matrix-core wide solve;
+    same factorisation as the CPU oracle at the true K, online and batch."""
+    from cnmf_torch_amd.models.nmf import run_nmf_batch
+
+    rs = np.random.default_rng(K)
+    N, G = 1500, 400
+    X = (rs.gamma(1, 1, (N, 20)) @ rs.gamma(0.5, 1, (20, G)) + 0.1 * rs.random((N, G))).astype(
+        np.float32)
+    for kw in (dict(online_chunk_size=700, online_max_pass=4),
+               dict(mode="batch", batch_max_iter=40)):
+        g = run_nmf_batch(X, K, [3, 4], device="cuda", **kw)
+        c = run_nmf_batch(X, K, [3, 4], device="cpu", **kw)
+        assert g.W.shape == (2 * K, G) and g.HT.shape == (2 * K, N)
+        np.testing.assert_allclose(g.err, c.err, rtol=1e-3)
+        Wg, Wc = g.W.cpu().numpy(), c.W.cpu().numpy()
+        cos = (Wg * Wc).sum(1) / (np.linalg.norm(Wg, axis=1) * np.linalg.norm(Wc, axis=1) + 1e-30)
+        assert np.median(cos) > 0.99, np.sort(cos)[:5]
+
+
+def test_refit_wide_and_unpadded_k_on_gpu():
+    """fit_H_online / fit_spectra_online at ranks without their own instantiation (K = 37,
+    90) pad with zero components on the GPU and match the CPU refit."""
+    from cnmf_torch_amd.models.refit import fit_H_online, fit_spectra_online
+
+    rs = np.random.default_rng(0)
+    for K in (37, 90):
+        X = rs.random((900, 300)).astype(np.float32)
+        W = rs.random((K, 300)).astype(np.float32)
+        hg = fit_H_online(X, W, device="cuda", chunk_max_iter=30)
+        hc = fit_H_online(X, W, device="cpu", chunk_max_iter=30)
+        np.testing.assert_allclose(hg, hc, rtol=5e-3, atol=1e-5)
+        sg = fit_spectra_online(X, hc, device="cuda", chunk_max_iter=30)
+        sc = fit_spectra_online(X, hc, device="cpu", chunk_max_iter=30)
+        np.testing.assert_allclose(sg, sc, rtol=5e-3, atol=1e-5)
+
+
 def test_solve_rejects_uninstantiated_k_loudly():
     x0, numer, gram = _problem(2, 37, 100)
     with pytest.raises(ValueError, match="pad"):

@@ -383,9 +383,12 @@ def test_gpu_rank_limit_is_a_clear_prepare_error(monkeypatch, tmp_path):
     from cnmf_torch_amd import api
 
     monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
-    with pytest.raises(ValueError, match=r"K=80: on the GPU this engine factorises K <= 64.*"
+    with pytest.raises(ValueError, match=r"K=130: on the GPU this engine factorises K <= 128.*"
                                          r"without --use_gpu"):
-        api.check_gpu_ranks([10, 80], "frobenius", "mu", use_gpu=True)
+        api.check_gpu_ranks([10, 130], "frobenius", "mu", use_gpu=True)
+    with pytest.raises(ValueError, match=r"K=80: on the GPU this engine factorises K <= 64"):
+        api.check_gpu_ranks([10, 80], "frobenius", "hals", use_gpu=True)
+    api.check_gpu_ranks([80, 128], "frobenius", "mu", use_gpu=True)  # matrix-core wide solve
     with pytest.raises(ValueError, match="K <= 32"):
         api.check_gpu_ranks([40], "kullback-leibler", "mu", use_gpu=True)
     api.check_gpu_ranks([80], "frobenius", "bpp", use_gpu=True)     # torch linalg: any K
