@@ -383,10 +383,13 @@ class _Batch:
         self.arena = arena
         self.graphs = False       # NMFBatchSolver.run: replay graphs per layout (arena only)
         if arena is not None:
+            # the arena's per-replicate state is two packed buffers (float64 rows
+            # err_init/err_prev/err, int32 rows active/converged/n_pass/h_iters/w_iters):
+            # a reset or an in-place compaction is one launch per buffer, not one per field
             self.state = arena["state"]
-            for v in self.state.values():
-                v.zero_()
-            self.h_iters, self.w_iters = arena["h_iters"].zero_(), arena["w_iters"].zero_()
+            arena["sf"].zero_()
+            arena["si"].zero_()
+            self.h_iters, self.w_iters = arena["h_iters"], arena["w_iters"]
         else:
             self.state = {k: torch.zeros(R, dtype=torch.float64, device=dev)
                           for k in ("err_init", "err_prev", "err")}
@@ -485,11 +488,10 @@ class _Batch:
         rows = _to_device(_ranges(roff[perm], self.kpos[perm]), dev)
         pidx = _to_device(perm, dev)
         if self.inplace:     # same storage, permuted rows (arena: addresses never move)
-            for t, ix in ((self.HT, rows), (self.W, rows), (self.h_iters, pidx),
-                          (self.w_iters, pidx)):
+            for t, ix in ((self.HT, rows), (self.W, rows)):
                 t.copy_(t.index_select(0, ix))
-            for v in self.state.values():
-                v.copy_(v.index_select(0, pidx))
+            for t in (self.arena["sf"], self.arena["si"]):
+                t.copy_(t.index_select(1, pidx))
         else:
             self.HT = self.HT.index_select(0, rows)
             self.W = self.W.index_select(0, rows)
@@ -588,6 +590,7 @@ class _PassPipeline:
         self.frac_small = compact_frac if (explicit or not late_small) else \
             float(os.environ.get("CNMF_COMPACT_FRAC_SMALL", "0.75"))
         self.pending = None   # (event, host_flags, n)
+        self._side = None     # flag-copy stream (CUDA)
 
     def _frac(self, n: int) -> float:
         return self.frac_small if n <= 256 else self.frac
@@ -605,9 +608,26 @@ class _PassPipeline:
                 st.compact()
             return True
         flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
-        flags.copy_(st.state["active"][:n], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        # CNMF_FLAG_STREAM=1: the flag copy runs on a side stream behind an event of the
+        # compute stream, so the next pass's first kernel does not queue behind the copy's
+        # blit kernel.  Flags only go 1 -> 0: a copy that overlaps the next pass reads
+        # stale-or-newer flags, both valid
+        act = st.state["active"][:n]
+        if _FLAG_STREAM:
+            main = torch.cuda.current_stream(act.device)
+            side = self._side
+            if side is None:
+                side = self._side = torch.cuda.Stream(act.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                flags.copy_(act, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            act.record_stream(side)
+        else:
+            flags.copy_(act, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
         prev, self.pending = self.pending, (ev, flags, n)
         if prev is None:
             return True
@@ -925,6 +945,14 @@ def native_rank(K: int) -> int:
 
 
 _GRAM_PROLOGUE = os.environ.get("CNMF_SOLVE_GRAM_PROLOGUE", "0") == "1"
+# first pass of a recurring batch layout from its captured graph (CNMF_LAYOUT_REPLAY=0:
+# eager) -- removes the ~330 us of host-paced idle of the compaction pass
+# (profiles/r3y_passes.txt), same-box bench within noise either way.  The pass loop's flag
+# copy on a side stream (CNMF_FLAG_STREAM=1) removes the ~5 us gap per steady pass in the
+# trace but measured slower end to end (headline -2 %, K grid -5.5 %: the per-pass stream
+# switch and event sit on the host's enqueue path; profiles/r3y_*), so it is off
+_LAYOUT_REPLAY = os.environ.get("CNMF_LAYOUT_REPLAY", "1") != "0"
+_FLAG_STREAM = os.environ.get("CNMF_FLAG_STREAM", "0") == "1"
 # fused step: split-K GEMMs of up to this many k slices hand their raw slabs to the
 # consuming solve; deeper splits (the few-replicate tail) are reduced by the GEMM's own
 # pass -- the solve would read every slab per element (CNMF_FUSED_MAX_SLABS overrides)
@@ -1036,7 +1064,8 @@ class NMFBatchSolver:
             tot = int(kpos.sum())
             arena = self._arena(kpos) if (not pad and self._graphs_wanted(kpos)) else None
             if arena is not None:
-                HT, W = arena["HT"].zero_(), arena["W"].zero_()
+                # no padded ranks with an arena: init_into overwrites every row
+                HT, W = arena["HT"], arena["W"]
             else:
                 HT = torch.zeros((tot, N), device=self.X.device, dtype=self.X.dtype)
                 W = torch.zeros((tot, G), device=self.X.device, dtype=self.X.dtype)
@@ -1374,15 +1403,15 @@ class NMFBatchSolver:
         if a is None:
             N, G = self.X.shape
             dev, tot, R = self.X.device, int(np.sum(kpos)), len(kpos)
+            sf = torch.zeros((3, R), dtype=torch.float64, device=dev)
+            si = torch.zeros((5, R), dtype=torch.int32, device=dev)
             a = {"HT": torch.zeros((tot, N), device=dev, dtype=self.X.dtype),
                  "W": torch.zeros((tot, G), device=dev, dtype=self.X.dtype),
-                 "state": {k: torch.zeros(R, dtype=torch.float64, device=dev)
-                           for k in ("err_init", "err_prev", "err")},
-                 "h_iters": torch.zeros(R, dtype=torch.int32, device=dev),
-                 "w_iters": torch.zeros(R, dtype=torch.int32, device=dev),
+                 "sf": sf, "si": si,
+                 "state": {"err_init": sf[0], "err_prev": sf[1], "err": sf[2],
+                           "active": si[0], "converged": si[1], "n_pass": si[2]},
+                 "h_iters": si[3], "w_iters": si[4],
                  "slots": collections.OrderedDict()}
-            for k in ("active", "converged", "n_pass"):
-                a["state"][k] = torch.zeros(R, dtype=torch.int32, device=dev)
             self._arenas[key] = a
             while len(self._arenas) > 4:
                 self._arenas.popitem(last=False)
@@ -1503,6 +1532,32 @@ class NMFBatchSolver:
             off += m
         return fb
 
+    def _fused_prep(self, st: _Batch, fb: dict, keep_slices: bool):
+        """The fused pass's operands that depend on W when W changed outside the fused
+        W-solve (init, compaction, an unfused pass): the W W^T partials (the Gram kernel's
+        full Gram in partial slot 0) and the spectra's bf16 planes.  ``keep_slices``: the
+        pass will be a graph replay captured with the W-solve's slice count S_w as the
+        number of partials to sum -- slots 1..S_w-1 are zeroed instead of the count
+        dropping to 1 (the sum is the same Gram, bitwise).  Returns the W key."""
+        xp = self._planes()
+        HT, W = st.views()
+        active = st.active_mask()
+        wkey = (W.data_ptr(), st.rows_act, st.uid, st.layout_version)
+        if fb["wwp_key"] != wkey:
+            for g in st.groups:
+                parts = fb["parts"][g.p0](fb["WWp"])
+                parts[:, 0].copy_(ops.gram(g.rep3(W), active=active[g.pos]))
+                n_s = fb["wwp_n"].get(g.p0, 1) if keep_slices else 1
+                if n_s > 1:
+                    parts[:, 1:n_s].zero_()
+                fb["wwp_n"][g.p0] = n_s
+            if keep_slices:
+                fb["wwp_key"] = wkey
+        if fb["wpl_key"] != wkey:      # spectra planes: split here only after such a change
+            ops.split_planes(W, fb["wpl"], col_mul=xp.unit)
+            fb["wpl_key"] = wkey
+        return wkey
+
     def _fused_pass(self, st: _Batch, steps, fb: dict, final: bool) -> None:
         """One online pass of the fused step (see _fused_ok); same updates, stopping rules
         and statistics as the unfused pass -- the split-K sums and the accumulation of
@@ -1520,19 +1575,9 @@ class NMFBatchSolver:
         h_it, w_it = st.h_iters[:n], st.w_iters[:n]
         bk = ops.planes_bk(xp.pb)
         slabN, slabB, B = fb["slabN"], fb["slabB"], fb["B"]
-        # W W^T partials: recomputed by the Gram kernel whenever W changed outside the
-        # fused W-solve (init, compaction, an unfused pass), else the last W-solve's
-        wkey = (W.data_ptr(), rows, st.uid, st.layout_version)
-        if fb["wwp_key"] != wkey:
-            for g in groups:
-                ww = ops.gram(g.rep3(W), active=active[g.pos])
-                fb["parts"][g.p0](fb["WWp"])[:, 0].copy_(ww)
-                fb["wwp_n"][g.p0] = 1
+        wkey = self._fused_prep(st, fb, keep_slices=False)
         last_s = len(steps) - 1
         wpl = fb["wpl"]
-        if fb["wpl_key"] != wkey:      # spectra planes: split here only after such a change
-            ops.split_planes(W, wpl, col_mul=xp.unit)
-            fb["wpl_key"] = wkey
         for s_, ((a, b),) in enumerate(steps):
             cw = b - a
             ks_n = ops.gemm_planes(None, wpl[:ops.gemm_a_planes(xp.Gp)], xp.x[:, a:], rows, cw,
@@ -1605,10 +1650,17 @@ class NMFBatchSolver:
             if fused:
                 key = (st.uid, st.layout_version)
                 final = p + 1 == max_pass
-                if fb_key != key:      # a new layout: its first pass runs eagerly
+                if fb_key != key:
+                    # a new layout: its first pass replays the slot's graph when an earlier
+                    # run of the arena captured one (only the W-dependent operands are
+                    # rebuilt eagerly), else it runs eagerly
                     sl = self._slot(st, steps) if st.graphs else None
                     fb, fb_key = (sl["fb"] if sl is not None else self._fused_bufs(st, steps)), key
-                    self._fused_pass(st, steps, fb, final=final)
+                    if sl is not None and sl["graph"] is not None and not final and _LAYOUT_REPLAY:
+                        self._fused_prep(st, fb, keep_slices=True)
+                        sl["graph"].replay()
+                    else:
+                        self._fused_pass(st, steps, fb, final=final)
                 elif sl is None or final or not self._replay_slot(sl, st, steps):
                     self._fused_pass(st, steps, fb, final=final)
                 if not pipe.after_enqueue():

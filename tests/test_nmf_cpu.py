@@ -265,3 +265,39 @@ def test_planes_only_x_factorises_like_the_resident_matrix():
     np.testing.assert_allclose(got.err, ref.err, rtol=1e-5)
     with pytest.raises(ValueError, match="PlanesOnlyX supports"):
         NMFBatchSolver(px, NMFOptions(n_components=4, mode="batch"))
+
+
+def test_native_rank_padding_rule():
+    """GPU rank padding (models.nmf.native_rank): K <= 32 as is, multiples of 8 up to 64,
+    multiples of 16 up to 128 (the matrix-core wide MU solve), beyond that an error."""
+    from cnmf_torch_amd.models.nmf import native_rank
+
+    assert [native_rank(k) for k in (1, 10, 32)] == [1, 10, 32]
+    assert [native_rank(k) for k in (33, 40, 41, 64)] == [40, 40, 48, 64]
+    assert [native_rank(k) for k in (65, 80, 81, 100, 128)] == [80, 80, 96, 112, 128]
+    with pytest.raises(ValueError, match="K <= 128"):
+        native_rank(129)
+
+
+def test_padded_rank_solve_equals_unpadded_on_cpu():
+    """The padding argument itself: zero components appended to x, numer and the Gram stay
+    zero under MU and leave the true components' iterates unchanged (CPU reference op)."""
+    import torch
+
+    from cnmf_torch_amd import ops
+
+    g = torch.Generator().manual_seed(3)
+    K, Kp, n = 70, 80, 300
+    Wf = torch.rand((K, 50), generator=g, dtype=torch.float64)
+    gram = Wf @ Wf.t()
+    numer = gram @ torch.rand((K, n), generator=g, dtype=torch.float64)
+    x0 = torch.rand((K, n), generator=g, dtype=torch.float64) + 0.1
+    x = x0.clone()[None]
+    ops.solve("mu", x, numer[None], gram[None], max_iter=25, tol=0.0)
+    xp = torch.zeros((1, Kp, n), dtype=torch.float64)
+    npd = torch.zeros((1, Kp, n), dtype=torch.float64)
+    gp = torch.zeros((1, Kp, Kp), dtype=torch.float64)
+    xp[0, :K], npd[0, :K], gp[0, :K, :K] = x0, numer, gram
+    ops.solve("mu", xp, npd, gp, max_iter=25, tol=0.0)
+    assert torch.equal(xp[0, K:], torch.zeros((Kp - K, n), dtype=torch.float64))
+    torch.testing.assert_close(xp[0, :K], x[0], rtol=1e-12, atol=0)
