@@ -1389,7 +1389,8 @@ def harmony_block_update(Rt: torch.Tensor, distT: torch.Tensor, sigma: torch.Ten
             raise ValueError(f"{name}: contiguous {dt} on {Rt.device} required")
     if distT.shape != (N, K) or O.shape != (K, B) or bidx.shape[1] != N:
         raise ValueError("harmony_block_update: inconsistent shapes")
-    chunk = max(32, -(-nb // 256))
+    # ~512 workgroups of up to 4 waves (2 per CU): each wave walks a few dozen cells
+    chunk = max(16, -(-nb // 512))
     n_wg = -(-nb // chunk)
     need = n_wg * K * (B + 1)
     if ws.get("part") is None or ws["part"].numel() < need:
