@@ -49,7 +49,7 @@ from .models.refit import col_block, fit_H_online, fit_spectra_online, gene_bloc
 from .ops import sparse as sops
 from .parallel.ledger import worker_filter
 from .utils.anndata_lite import AnnData
-from .utils.h5ad import read_h5ad, write_h5ad
+from .utils.h5ad import read_h5ad, write_h5ad, write_h5ad_row_blocks
 from .utils.io import (check_dir_exists, dump_yaml, load_df_from_npz, load_yaml, read_10x_mtx,
                        read_any, read_counts_table, read_spectra_batch, save_arrays_npz_digest,
                        save_df_to_npz,
@@ -168,6 +168,51 @@ def _norm_counts_dense_device(counts, genes, guard_zero_std: bool, dev) -> AnnDa
     H2D of the counts and one D2H of the float64 result.  ``guard_zero_std`` selects
     scanpy's scale (E[x^2] - E[x]^2, ddof=1, std 0 -> 1; used when the TPM is sparse)
     over numpy's ``X / X.std(ddof=1)`` (two-pass, no guard)."""
+    T, cols = _norm_counts_tensor(counts, genes, guard_zero_std, dev)
+    out = AnnData(X=T.cpu().numpy(), obs=counts.obs, var=counts.var.iloc[cols],
+                  obsm=dict(counts.obsm), uns=dict(counts.uns))
+    out.uns["_scaled_on_device"] = True
+    return out
+
+
+def _save_norm_counts_streamed(path: str, counts, T: torch.Tensor, cols, rows: int = 16384):
+    """Write the device-resident float64 norm counts ``T`` as the h5ad of
+    get_norm_counts(...) without a whole-matrix host copy: row blocks go D2H into two
+    pinned staging buffers on a copy stream while the previous block is written, so the
+    copy overlaps the file write (500k x 2000 float64 = 8 GB: the whole-matrix .cpu() and
+    the numpy NaN / zero-row passes took ~1.3 s of prepare, profiles/r3ac_*)."""
+    n, G = T.shape
+    rows = max(1, min(rows, n))
+    bufs = [torch.empty((rows, G), dtype=T.dtype, pin_memory=True) for _ in range(2)]
+    evs = [torch.cuda.Event() for _ in range(2)]
+    cs = torch.cuda.Stream(T.device)
+    cs.wait_stream(torch.cuda.current_stream(T.device))
+
+    def issue(i):
+        a = i * rows
+        b = min(n, a + rows)
+        with torch.cuda.stream(cs):
+            bufs[i % 2][:b - a].copy_(T[a:b], non_blocking=True)
+            evs[i % 2].record(cs)
+        return b - a
+
+    nblk = -(-n // rows)
+
+    def blocks():
+        m = issue(0)
+        for i in range(nblk):
+            evs[i % 2].synchronize()
+            nxt = issue(i + 1) if i + 1 < nblk else 0
+            yield None, bufs[i % 2][:m].numpy()
+            m = nxt
+
+    write_h5ad_row_blocks(path, n, counts.var.iloc[cols], blocks(), sparse=False,
+                          dtype=np.float64, obs=counts.obs, obsm=dict(counts.obsm),
+                          uns=dict(counts.uns))
+
+
+def _norm_counts_tensor(counts, genes, guard_zero_std: bool, dev):
+    """(device float64 norm counts, gene column indices) of a dense count matrix."""
     cols = counts.var.index.get_indexer(list(genes))
     if (cols < 0).any():
         raise KeyError(f"genes missing from the counts: {list(np.array(genes)[cols < 0][:5])}")
@@ -184,10 +229,7 @@ def _norm_counts_dense_device(counts, genes, guard_zero_std: bool, dev) -> AnnDa
     else:
         std = T.std(dim=0, unbiased=True)
     T /= std
-    out = AnnData(X=T.cpu().numpy(), obs=counts.obs, var=counts.var.iloc[cols],
-                  obsm=dict(counts.obsm), uns=dict(counts.uns))
-    out.uns["_scaled_on_device"] = True
-    return out
+    return T, cols
 
 
 def _resident_X(adata, dev: torch.device):
@@ -308,10 +350,22 @@ class cNMF:
                 with open(genes_file) as fh:
                     highvargenes = fh.read().rstrip().split("\n")
 
-            norm_counts = self.get_norm_counts(input_counts, tpm,
-                                               num_highvar_genes=num_highvar_genes,
-                                               high_variance_genes_filter=highvargenes)
-            self.save_norm_counts(norm_counts)
+            dev = _device(False)
+            if not sp.issparse(input_counts.X) and dev.type == "cuda":
+                # dense counts on the GPU: scaled, checked and streamed to the h5ad from
+                # the device (same file and messages as get_norm_counts + save)
+                genes = self._hvg_filter(tpm, highvargenes, num_highvar_genes)
+                T, cols = _norm_counts_tensor(input_counts, genes, sp.issparse(tpm.X), dev)
+                self._check_norm_counts(T, input_counts.obs.index, genes)
+                self._initialize_dirs()
+                _save_norm_counts_streamed(self.paths["normalized_counts"], input_counts, T,
+                                           cols)
+                del T
+            else:
+                norm_counts = self.get_norm_counts(input_counts, tpm,
+                                                   num_highvar_genes=num_highvar_genes,
+                                                   high_variance_genes_filter=highvargenes)
+                self.save_norm_counts(norm_counts)
             replicate_params, run_params = self.get_nmf_iter_params(
                 ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
                 alpha_usage=alpha_usage, alpha_spectra=alpha_spectra, init=init,
@@ -451,15 +505,36 @@ class cNMF:
                 self.save_nmf_iter_params(replicate_params, run_params)
             comm.barrier()
 
-    def get_norm_counts(self, counts, tpm, high_variance_genes_filter=None,
-                        num_highvar_genes=None):
-        """HVG subset of the raw counts, genes scaled to unit variance (cnmf.py:624-693)."""
+    @staticmethod
+    def _hvg_filter(tpm, high_variance_genes_filter, num_highvar_genes):
+        """The over-dispersed genes (fano model on the TPM) unless a list is given."""
         if high_variance_genes_filter is None:
             if sp.issparse(tpm.X):
                 gstats, _ = get_highvar_genes_sparse(tpm.X, numgenes=num_highvar_genes)
             else:
                 gstats, _ = get_highvar_genes(np.array(tpm.X), numgenes=num_highvar_genes)
             high_variance_genes_filter = list(tpm.var.index[gstats.high_var.values])
+        return high_variance_genes_filter
+
+    def _check_norm_counts(self, T: torch.Tensor, obs_index, genes) -> None:
+        """get_norm_counts's NaN warning and zero-row error on a device tensor, plus the
+        genes list file (cnmf.py:683-693)."""
+        if bool(torch.isnan(T).any()):
+            print("Warning NaNs in normalized counts matrix")
+        write_text_atomic(self.paths["nmf_genes_list"], "\n".join(genes))
+        zerocells = (T.sum(dim=1) == 0).cpu().numpy()
+        if zerocells.sum() > 0:
+            examples = obs_index[np.ravel(zerocells)]
+            raise Exception(
+                "Error: %d cells have zero counts of overdispersed genes. E.g. %s. Filter those "
+                "cells and re-run or adjust the number of overdispersed genes. Quitting!"
+                % (zerocells.sum(), ", ".join(examples[:4])))
+
+    def get_norm_counts(self, counts, tpm, high_variance_genes_filter=None,
+                        num_highvar_genes=None):
+        """HVG subset of the raw counts, genes scaled to unit variance (cnmf.py:624-693)."""
+        high_variance_genes_filter = self._hvg_filter(tpm, high_variance_genes_filter,
+                                                      num_highvar_genes)
 
         dev = _device(False)
         if not sp.issparse(counts.X) and dev.type == "cuda":

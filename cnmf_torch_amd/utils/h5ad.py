@@ -150,13 +150,15 @@ def write_h5ad(path: str, adata, compression=None) -> None:
 
 
 def write_h5ad_row_blocks(path: str, n_rows: int, var: pd.DataFrame, blocks, sparse: bool,
-                          dtype, nnz: int = 0, index_dtype=np.int32) -> None:
+                          dtype, nnz: int = 0, index_dtype=np.int32, obs=None, obsm=None,
+                          uns=None) -> None:
     """Write an h5ad whose X arrives as row blocks, in row order, without ever holding
     the whole matrix: ``blocks`` yields (obs_block DataFrame, X_block) with X_block a
     CSR (``sparse``) or dense array of ``dtype``; ``nnz`` is the total non-zero count of
     a CSR X.  X's datasets are created at their final size and filled by hyperslab
-    writes (the native layer's create_dataset / write_rows); obs is written at the end.
-    Same encoding as :func:`write_h5ad`."""
+    writes (the native layer's create_dataset / write_rows); obs is written at the end
+    (``obs``: the whole frame, the blocks' obs parts are then ignored, may be None).
+    ``obsm`` / ``uns``: written as :func:`write_h5ad` does.  Same encoding."""
     from .io import atomic_path
 
     lib = _lib()
@@ -190,16 +192,26 @@ def write_h5ad_row_blocks(path: str, n_rows: int, var: pd.DataFrame, blocks, spa
                 else:
                     f.write_rows("/X", r0, np.ascontiguousarray(np.asarray(Xb), dtype=dtype))
                 r0 += n
-                obs_parts.append(obs_b)
+                if obs is None:
+                    obs_parts.append(obs_b)
                 del Xb, obs_b      # released before the next block is fetched
             if r0 != n_rows or (sparse and e0 != nnz):
                 raise ValueError(f"row blocks gave {r0} rows / {e0} non-zeros, expected "
                                  f"{n_rows} / {nnz}")
-            _write_frame(f, "/obs", pd.concat(obs_parts) if obs_parts else pd.DataFrame(), 0)
+            if obs is None:
+                obs = pd.concat(obs_parts) if obs_parts else pd.DataFrame()
+            _write_frame(f, "/obs", obs, 0)
             _write_frame(f, "/var", var, 0)
-            for key in ("obsm", "varm", "layers", "obsp", "varp", "uns"):
+            for key in ("obsm", "varm", "layers", "obsp", "varp"):
                 f.create_group("/" + key)
                 _set_enc(f, "/" + key, "dict", "0.1.0")
+                if key == "obsm":
+                    for k, v in dict(obsm or {}).items():
+                        if isinstance(v, pd.DataFrame):
+                            _write_frame(f, f"/obsm/{k}", v, 0)
+                        else:
+                            _write_matrix(f, f"/obsm/{k}", v, 0)
+            _write_dict(f, "/uns", dict(uns or {}), 0)
         finally:
             f.close()
 

@@ -44,3 +44,35 @@ def test_early_replicate_writes_equal_end_of_batch_writes(tmp_path, monkeypatch)
     ma, mb = manifest(a), manifest(b)
     assert len(ma) == 120 and ma == mb
     assert a.verify_replicates() == []
+
+
+def test_streamed_norm_counts_equal_get_norm_counts(tmp_path):
+    """prepare on the GPU with dense counts streams the float64 norm counts from the device
+    into the h5ad (api._save_norm_counts_streamed): X, obs, var, obsm and uns equal the
+    public get_norm_counts(...) AnnData, bit for bit; the genes list is written too."""
+    from cnmf_torch_amd.utils.anndata_lite import AnnData
+    from cnmf_torch_amd.utils.h5ad import read_h5ad, write_h5ad
+
+    X, cells, genes = simulate_counts(2100, 400, 5, seed=9, sparse=False)
+    ad = AnnData(X=X.astype(np.float32), obs=pd.DataFrame({"grp": ["a", "b", "c"] * 700},
+                                                          index=cells),
+                 var=pd.DataFrame(index=genes),
+                 obsm={"X_pca": np.random.default_rng(0).random((2100, 7))},
+                 uns={"note": "kept"})
+    fn = str(tmp_path / "counts.h5ad")
+    write_h5ad(fn, ad)
+    obj = cNMF(output_dir=str(tmp_path), name="s")
+    obj.prepare(fn, components=[5], n_iter=3, seed=1, num_highvar_genes=150)
+    got = read_h5ad(obj.paths["normalized_counts"])
+    with open(obj.paths["nmf_genes_list"]) as fh:
+        hv = fh.read().split("\n")
+    from cnmf_torch_amd.utils.io import read_any
+
+    tpm = read_h5ad(obj.paths["tpm"])
+    ref = obj.get_norm_counts(read_any(fn), tpm, high_variance_genes_filter=hv)
+    np.testing.assert_array_equal(np.asarray(got.X), np.asarray(ref.X))
+    assert got.X.dtype == np.float64
+    assert list(got.var.index) == list(ref.var.index) == hv
+    pd.testing.assert_frame_equal(got.obs, ref.obs, check_dtype=False, check_categorical=False)
+    np.testing.assert_array_equal(got.obsm["X_pca"], ad.obsm["X_pca"])
+    assert got.uns["note"] == "kept"

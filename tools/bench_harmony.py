@@ -66,7 +66,26 @@ def main():
     ap.add_argument("--n-iter", type=int, default=20)
     ap.add_argument("--max-iter-harmony", type=int, default=10)
     ap.add_argument("--profile", default=None, help="cProfile the Harmony stage into this file")
+    ap.add_argument("--profile-stages", default=None,
+                    help="cProfile prepare / factorize / combine+consensus into PREFIX.<stage>.txt")
     a = ap.parse_args()
+
+    def staged(name, fn):
+        if not a.profile_stages:
+            return fn()
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        try:
+            return fn()
+        finally:
+            pr.disable()
+            buf = io.StringIO()
+            pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(45)
+            with open(f"{a.profile_stages}.{name}.txt", "w") as fh:
+                fh.write(buf.getvalue())
     t = {}
     t0 = time.perf_counter()
     ad = simulate(a.cells, a.genes)
@@ -95,15 +114,20 @@ def main():
     t["preprocess_harmony"] = time.perf_counter() - t0
     obj = cNMF(output_dir=work, name="hm_cnmf")
     t0 = time.perf_counter()
-    obj.prepare(base + ".Corrected.HVG.Varnorm.h5ad", components=[a.k], n_iter=a.n_iter, seed=14,
-                tpm_fn=base + ".TP10K.h5ad", genes_file=base + ".Corrected.HVGs.txt")
+    staged("prepare", lambda: obj.prepare(
+        base + ".Corrected.HVG.Varnorm.h5ad", components=[a.k], n_iter=a.n_iter, seed=14,
+        tpm_fn=base + ".TP10K.h5ad", genes_file=base + ".Corrected.HVGs.txt"))
     t["prepare"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    obj.factorize(verbose=False)
+    staged("factorize", lambda: obj.factorize(verbose=False))
     t["factorize"] = time.perf_counter() - t0
     t0 = time.perf_counter()
-    obj.combine()
-    obj.consensus(a.k, density_threshold=2.0, show_clustering=False)
+
+    def cc():
+        obj.combine()
+        obj.consensus(a.k, density_threshold=2.0, show_clustering=False)
+
+    staged("combine_consensus", cc)
     t["combine_consensus"] = time.perf_counter() - t0
     print(json.dumps({
         "metric": "Harmony + cNMF end-to-end wall-clock", "unit": "s",
