@@ -46,6 +46,28 @@ class HarmonyResult:
         self.__dict__.update(kw)
 
 
+def _tall_matmul(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """A (m, N) @ B (N, n) for a long reduction (N = cells) into a small output (PCs x
+    clusters, clusters x batch pairs): one library GEMM gives such a product a single
+    output tile -- ONE workgroup walking 500k cells (27 ms per call at N = 500k, m = 50,
+    n = 100: profiles/r3aa_harmony_500k_kernel_summary.txt).  Here the reduction is cut
+    into ~512 chunks that run as one batched GEMM, then summed in chunk order
+    (deterministic)."""
+    m, N = A.shape
+    n = B.shape[1]
+    chunk = max(1024, N // 512)
+    nch = N // chunk
+    if nch < 4 or A.device.type != "cuda":
+        return A @ B
+    M = nch * chunk
+    A3 = A[:, :M].reshape(m, nch, chunk).transpose(0, 1)
+    B3 = B[:M].reshape(nch, chunk, n)
+    out = torch.bmm(A3, B3).sum(dim=0)
+    if M < N:
+        out += A[:, M:] @ B[M:]
+    return out
+
+
 def _entropy_sum(R: torch.Tensor, sigma: torch.Tensor) -> torch.Tensor:
     y = R * torch.log(R)
     y = torch.where(torch.isfinite(y), y, torch.zeros_like(y))
@@ -113,7 +135,7 @@ class Harmony:
                                          max_iter=25, backend="device",
                                          device_restart_factor=1), device=self.dev)
             onehot = (labels[None, :] == torch.arange(self.K, device=self.dev)[:, None]).to(self.dt)
-            Y = (X.t() @ onehot.t()) / onehot.sum(dim=1).clamp(min=1)[None, :]
+            Y = _tall_matmul(X.t(), onehot.t()) / onehot.sum(dim=1).clamp(min=1)[None, :]
         self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
         self._dist()
         R = -self.dist_mat / self.sigma[:, None]
@@ -124,7 +146,7 @@ class Harmony:
             self.Rt = self.R.t().contiguous()
             self.R = self.Rt.t()
         self.E = torch.outer(self.R.sum(dim=1), self.Pr_b)
-        self.O = self.R @ self.Phi.t()
+        self.O = _tall_matmul(self.R, self.Phi.t())
         self._objective()
         self.objective_harmony.append(self.objective_kmeans[-1])
 
@@ -158,7 +180,7 @@ class Harmony:
         self._dist()
         i = 0
         for i in range(self.max_iter_kmeans):
-            Y = self.Z_cos @ self.R.t()
+            Y = _tall_matmul(self.Z_cos, self.R.t())
             self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
             self._dist()
             self._update_R()
@@ -269,12 +291,12 @@ def _ridge_weights(Z: torch.Tensor, R: torch.Tensor, Phi_moe: torch.Tensor, lamb
     F = Z.shape[0]
     # sum_n R[k,n] P[b,n] P[c,n] via pair products: (K x N) @ (N x B1*B1)
     PP = (Phi_moe[:, None, :] * Phi_moe[None, :, :]).reshape(B1 * B1, N)
-    A = (R @ PP.t()).reshape(K, B1, B1) + lamb[None]
+    A = _tall_matmul(R, PP.t()).reshape(K, B1, B1) + lamb[None]
     Y = torch.zeros((K * B1, F), dtype=Z.dtype, device=Z.device)
     for a in range(0, N, chunk):
         b = min(N, a + chunk)
         RP = (R[:, None, a:b] * Phi_moe[None, :, a:b]).reshape(K * B1, b - a)
-        Y += RP @ Z[:, a:b].t()
+        Y += _tall_matmul(RP, Z[:, a:b].t())
     W = torch.linalg.solve(A, Y.view(K, B1, F))
     W[:, 0, :] = 0
     return W.reshape(K * B1, F)
