@@ -55,7 +55,7 @@ def _require_native():
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
 _ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
              "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES", "CNMF_GEMM_BK",
-             "CNMF_GEMM_SMALL", "CNMF_SOLVE_PIPE")
+             "CNMF_GEMM_SMALL", "CNMF_SOLVE_PIPE", "CNMF_WIDE_SOLVE")
 _ENV: dict = {}
 
 
@@ -258,6 +258,8 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                          f"with {nblocks} replicates")
     else:
         vcode = {"auto": 0, "stream": 1, "reg": 2}[variant]
+        if K > 64 and _ENV["CNMF_WIDE_SOLVE"] == "fp32":
+            vcode = 1      # the wide solve's fp32-MFMA Gram apply (default: split bf16)
         S = 1
         if nsplit <= 1:
             S = _coop_split(n, nblocks, x.device) if coop == "auto" else max(1, int(coop))

@@ -105,9 +105,13 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
     return cnmf::launch_solve_mfma(K, p, nblocks, T < 1 ? 1 : T, stream);
   }
   if (fused || !gram) return hipErrorInvalidValue;
-  // K > 64: the matrix-core wide solve, MU only (HALS is Gauss-Seidel over components)
-  if (K > 64) return algo == 0 ? cnmf::launch_solve_wmfma(K, p, nblocks, stream)
-                               : hipErrorInvalidValue;
+  // K > 64: the matrix-core wide solve, MU only (HALS is Gauss-Seidel over components).
+  // Split-bf16 Gram apply at K = 96 / 128 (whole 32-deep k-blocks); fp32 MFMA at 80 / 112
+  // and under variant 1 (streaming): padding those to 96 / 128 inside the kernel cost
+  // occupancy and measured slower (profiles/r3af_*)
+  if (K > 64)
+    return algo == 0 ? cnmf::launch_solve_wmfma(K, p, nblocks, variant != 1 && K % 32 == 0, stream)
+                     : hipErrorInvalidValue;
   if (K > 32) return cnmf::launch_solve_wide(K, algo, p, nblocks, threads, stream);
   // variant: 0 auto, 1 streaming, 2 register-resident (3 = mfma above).  Resident needs every slice to
   // fit U <= res_max_cols(K) columns per thread of a <= 1024-thread workgroup; it runs

@@ -685,7 +685,7 @@ hipError_t launch_solve_resident(int K, int U, int algo, const SolveParams& p, i
 hipError_t launch_solve_mfma(int K, const SolveParams& p, int nblocks, int T, hipStream_t s);
 hipError_t launch_solve_pipe(int K, const SolveParams& p, int nblocks, int T, int pl_n,
                              hipStream_t s);
-hipError_t launch_solve_wmfma(int K, const SolveParams& p, int nblocks, hipStream_t s);
+hipError_t launch_solve_wmfma(int K, const SolveParams& p, int nblocks, bool bf16, hipStream_t s);
 hipError_t launch_solve_resident34(int K, int U, int algo, const SolveParams& p, int nblocks,
                                    int threads, hipStream_t s);
 

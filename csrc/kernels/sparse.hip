@@ -88,20 +88,38 @@ __global__ void __launch_bounds__(256) csr_col_stats_kernel(
       smem[2 * kCsWaves * kCsTile + e] = 0.0;
     }
     __syncthreads();
+    // kCsU entries per lane per trip, their index / value loads issued together: one
+    // wave per SIMD paid a full memory latency per entry (12 ms per call on a 500k x 3000
+    // CSR, profiles/r3aa_harmony_500k_kernel_summary.txt).  A row's columns are distinct,
+    // so the lanes' LDS updates never collide.
+    constexpr int kCsU = 4;
     for (int row = r0 + wave; row < r1; row += kCsWaves) {
       const double rs = t.row_scale ? t.row_scale[row] : 1.0;
       const long long e = indptr[row + 1];
-      for (long long j = indptr[row] + lane; j < e; j += 64) {
-        int c = indices[j];
-        if (t.col_map) c = t.col_map[c];
-        c -= t0;
-        if (c < 0 || c >= tw) continue;
-        const int oc = c + t0;
-        const double v = xform(t, (double)data[j], rs, oc);
-        const double dv = center ? v - center[oc] : v;
-        aS[c] += v;
-        aQ[c] += dv * dv;
-        aC[c] += 1.0;
+      for (long long j0 = indptr[row] + lane; j0 < e; j0 += 64 * kCsU) {
+        int cc[kCsU];
+        T vv[kCsU];
+#pragma unroll
+        for (int u = 0; u < kCsU; ++u) {
+          const long long j = j0 + 64 * u;
+          const bool ok = j < e;
+          cc[u] = ok ? indices[j] : -1;
+          vv[u] = ok ? data[j] : T(0);
+        }
+#pragma unroll
+        for (int u = 0; u < kCsU; ++u) {
+          int c = cc[u];
+          if (c < 0) continue;
+          if (t.col_map) c = t.col_map[c];
+          c -= t0;
+          if (c < 0 || c >= tw) continue;
+          const int oc = c + t0;
+          const double v = xform(t, (double)vv[u], rs, oc);
+          const double dv = center ? v - center[oc] : v;
+          aS[c] += v;
+          aQ[c] += dv * dv;
+          aC[c] += 1.0;
+        }
       }
     }
     __syncthreads();

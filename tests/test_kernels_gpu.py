@@ -1164,13 +1164,15 @@ def test_gram_wide_k_matches_bmm(K):
     np.testing.assert_allclose(out.cpu().double().numpy(), ref.numpy(), rtol=1e-5)
 
 
-@pytest.mark.parametrize("K", [80, 128])
+@pytest.mark.parametrize("K", [80, 96, 128])
 @pytest.mark.parametrize("conv_mode", [0, 1])
 @pytest.mark.parametrize("split", ["none", "coop", "nsplit"])
-def test_solve_wmfma_matches_fp64_reference(K, conv_mode, split):
+@pytest.mark.parametrize("variant", ["auto", "stream"])
+def test_solve_wmfma_matches_fp64_reference(K, conv_mode, split, variant):
     """K in (64, 128]: the matrix-core wide MU solve (solve_wmfma.hip) against the fp64
     torch reference of the same op, with l1/l2 terms, lin/quad epilogue and iteration
-    counts; cooperative slices and the fixed-step column split too."""
+    counts; cooperative slices and the fixed-step column split too.  variant 'auto' =
+    split-bf16 Gram apply at K = 96 / 128 (fp32 MFMA at 80), 'stream' = fp32 MFMA."""
     R, n = 3, 2999
     x0, numer, gram = _problem(R, K, n, seed=K + conv_mode)
     kw = dict(max_iter=30, tol=1e-3, conv_mode=conv_mode, l1_num=0.01, l2=0.05)
@@ -1181,7 +1183,7 @@ def test_solve_wmfma_matches_fp64_reference(K, conv_mode, split):
     lin_g = torch.zeros(R, dtype=torch.float32, device="cuda")
     quad_g = torch.zeros(R, dtype=torch.float32, device="cuda")
     ops.solve("mu", xg, numer.cuda(), gram.cuda(), iters_out=it_g, lin_out=lin_g,
-              quad_out=quad_g, coop=3 if split == "coop" else 1, **kw)
+              quad_out=quad_g, coop=3 if split == "coop" else 1, variant=variant, **kw)
     ops.coop_check(xg.device)
     xr = x0.double().clone()
     it_r = torch.zeros(R, dtype=torch.int32)
