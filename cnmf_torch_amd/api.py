@@ -206,9 +206,12 @@ def _save_norm_counts_streamed(path: str, counts, T: torch.Tensor, cols, rows: i
             yield None, bufs[i % 2][:m].numpy()
             m = nxt
 
-    write_h5ad_row_blocks(path, n, counts.var.iloc[cols], blocks(), sparse=False,
-                          dtype=np.float64, obs=counts.obs, obsm=dict(counts.obsm),
-                          uns=dict(counts.uns))
+    try:
+        write_h5ad_row_blocks(path, n, counts.var.iloc[cols], blocks(), sparse=False,
+                              dtype=np.float64, obs=counts.obs, obsm=dict(counts.obsm),
+                              uns=dict(counts.uns))
+    finally:
+        cs.synchronize()   # no copy may still target a staging buffer (error path)
 
 
 def _norm_counts_tensor(counts, genes, guard_zero_std: bool, dev):

@@ -261,7 +261,13 @@ def init_into(HT: torch.Tensor, W: torch.Tensor, X: torch.Tensor, K: int, seeds,
             mean = _global_mean(X, comm)
         avg = math.sqrt(mean / K)
         seeds_t = torch.tensor([int(s) for s in seeds], dtype=torch.int64)
-        scales = torch.full((R,), avg, dtype=torch.float32)
+        if HT.device.type == "cuda":
+            # one async copy from pinned memory and a device fill, shared by the H and W
+            # draws (four pageable copies, each blocking the host, led every run)
+            seeds_t = seeds_t.pin_memory().to(HT.device, non_blocking=True)
+            scales = torch.full((R,), avg, dtype=torch.float32, device=HT.device)
+        else:
+            scales = torch.full((R,), avg, dtype=torch.float32)
         ld = HT.stride(0)
         for la, lb, ga in (row_map if row_map is not None else [(0, N, row_offset)]):
             if lb > la:
@@ -390,6 +396,7 @@ class _Batch:
             arena["sf"].zero_()
             arena["si"].zero_()
             self.h_iters, self.w_iters = arena["h_iters"], arena["w_iters"]
+            self.gate = arena["gate"]
         else:
             self.state = {k: torch.zeros(R, dtype=torch.float64, device=dev)
                           for k in ("err_init", "err_prev", "err")}
@@ -397,6 +404,10 @@ class _Batch:
                 self.state[k] = torch.zeros(R, dtype=torch.int32, device=dev)
             self.h_iters = torch.zeros(R, dtype=torch.int32, device=dev)
             self.w_iters = torch.zeros(R, dtype=torch.int32, device=dev)
+            self.gate = torch.ones(1, dtype=torch.int32, device=dev)
+        # device flag "some replicate still active", written by every conv_update: the
+        # split GEMMs of the speculative pass enqueued after the batch finished return at
+        # once (ops.gemm_planes gate) instead of re-running the last tail pass's products
         self.layout_version = 0   # bumped by compact(): captured graphs key on it
         # optional callback(orig_idx, kpos, host_rows, event): the final spectra of the
         # replicates a compaction retires, copied to pinned memory (ready at `event`), so
@@ -952,6 +963,12 @@ _GRAM_PROLOGUE = os.environ.get("CNMF_SOLVE_GRAM_PROLOGUE", "0") == "1"
 # trace but measured slower end to end (headline -2 %, K grid -5.5 %: the per-pass stream
 # switch and event sit on the host's enqueue path; profiles/r3y_*), so it is off
 _LAYOUT_REPLAY = os.environ.get("CNMF_LAYOUT_REPLAY", "1") != "0"
+# CNMF_GEMM_GATE=1: the fused pass's split GEMMs skip themselves once no replicate is
+# active (the speculative pass after a batch that converged before online_max_pass).
+# Off by default: the bench's slowest replicates stop AT max_pass, so no speculative pass
+# runs there, and reading the flag in every GEMM measured 1.2 % slower
+# (profiles/r3ah_bench_{on,off}_*)
+_GEMM_GATE = os.environ.get("CNMF_GEMM_GATE", "0") == "1"
 _FLAG_STREAM = os.environ.get("CNMF_FLAG_STREAM", "0") == "1"
 # fused step: split-K GEMMs of up to this many k slices hand their raw slabs to the
 # consuming solve; deeper splits (the few-replicate tail) are reduced by the GEMM's own
@@ -1340,7 +1357,7 @@ class NMFBatchSolver:
             lin[g.pos] = (g.rep3(B) * W3).sum(dim=(1, 2)).float()
             quad[g.pos] = (g.gram3(A) * ops.gram(W3)).sum(dim=(1, 2)).float()
         ops.conv_update(lin, quad, self.x_sq, st.state, st.n_act, 0, self.opts.tol, False,
-                        init=True)
+                        init=True, gate=st.gate)
         return A, B
 
     # ------------------------------------------------------------------ loss (any beta)
@@ -1411,6 +1428,7 @@ class NMFBatchSolver:
                  "state": {"err_init": sf[0], "err_prev": sf[1], "err": sf[2],
                            "active": si[0], "converged": si[1], "n_pass": si[2]},
                  "h_iters": si[3], "w_iters": si[4],
+                 "gate": torch.ones(1, dtype=torch.int32, device=dev),
                  "slots": collections.OrderedDict()}
             self._arenas[key] = a
             while len(self._arenas) > 4:
@@ -1581,7 +1599,8 @@ class NMFBatchSolver:
         for s_, ((a, b),) in enumerate(steps):
             cw = b - a
             ks_n = ops.gemm_planes(None, wpl[:ops.gemm_a_planes(xp.Gp)], xp.x[:, a:], rows, cw,
-                                   xp.Gp, raw_slab=slabN, raw_max=_FUSED_MAX_SLABS)
+                                   xp.Gp, raw_slab=slabN, raw_max=_FUSED_MAX_SLABS,
+                                   gate=st.gate)
             kd = -(-cw // bk) * bk
             hpl = fb["hpl"][:, :, :kd]
             hpl_n = ops.gemm_a_planes(kd)
@@ -1597,7 +1616,8 @@ class NMFBatchSolver:
                     gram_parts=fb["parts"][g.p0](fb["WWp"]), gram_parts_n=fb["wwp_n"][g.p0],
                     gram_parts_out=fb["parts"][g.p0](fb["HHp"]), coop_device_gen=True)
             ks_b = ops.gemm_planes(None, hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd,
-                                   raw_slab=slabB, raw_max=_FUSED_MAX_SLABS)
+                                   raw_slab=slabB, raw_max=_FUSED_MAX_SLABS,
+                                   gate=st.gate if _GEMM_GATE else None)
             last = s_ == last_s
             wpl_out, unit = wpl, xp.unit
             wpl_n = ops.gemm_a_planes(xp.Gp)
@@ -1619,7 +1639,7 @@ class NMFBatchSolver:
                     gram_parts_out=fb["parts"][g.p0](fb["WWp"]), coop_device_gen=True)
             fb["wwp_key"] = fb["wpl_key"] = wkey
         ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
-                        n, -1, o.tol, final=final)
+                        n, -1, o.tol, final=final, gate=st.gate)
 
     # ------------------------------------------------------------------ online frobenius
     def _online_frob(self, st: _Batch) -> None:

@@ -490,16 +490,21 @@ def coop_check(device: torch.device | None = None) -> None:
 
 # ----------------------------------------------------------------------------- convergence
 def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict, n: int,
-                pass_idx: int, tol: float, final: bool, init: bool = False) -> None:
+                pass_idx: int, tol: float, final: bool, init: bool = False,
+                gate: torch.Tensor | None = None) -> None:
     """Per-replicate Frobenius error from (lin, quad) and the (prev - cur)/init < tol
     stopping rule, entirely on the device (csrc/kernels/conv.hip).  ``state`` holds
     float64 err_init/err_prev/err and int32 active/converged/n_pass tensors.
     ``pass_idx < 0`` counts passes on the device (n_pass += 1), so the launch has no
-    per-pass host argument and can live in a captured graph."""
+    per-pass host argument and can live in a captured graph.  ``gate`` (int32 device
+    scalar): set to 1 while any replicate is active, else 0 (gemm_planes ``gate``)."""
     if n <= 0:
         return
     if not use_native(lin):
-        return reference.conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init)
+        reference.conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init)
+        if gate is not None:
+            gate.fill_(int(bool((state["active"][:n] != 0).any())))
+        return
     for t in (lin, quad):
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < n:
             raise ValueError("lin/quad must be contiguous float32 with >= n entries")
@@ -512,7 +517,7 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
                      state["err_prev"].data_ptr(), state["err"].data_ptr(),
                      state["active"].data_ptr(), state["converged"].data_ptr(),
                      state["n_pass"].data_ptr(), int(n), int(pass_idx), float(tol), int(final),
-                     int(init), _stream_ptr(lin))
+                     int(init), _gate_ptr(gate, lin.device), _stream_ptr(lin))
 
 
 # ----------------------------------------------------------------------------- beta MU
@@ -1535,7 +1540,8 @@ def split_planes(S: torch.Tensor, out: torch.Tensor, col_mul: torch.Tensor | Non
 
 def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int, N: int,
                 Kd: int, accumulate: bool = False, col_scale: torch.Tensor | None = None,
-                raw_slab: torch.Tensor | None = None, raw_max: int = 1 << 30) -> int:
+                raw_slab: torch.Tensor | None = None, raw_max: int = 1 << 30,
+                gate: torch.Tensor | None = None) -> int:
     """C[:M, :N] (+)= col_scale * sum_{i + j <= 2} A[i][:M, :Kd] . B[j][:N, :Kd]^T on the bf16
     matrix cores (gemm_planes.hip): the fp32-accurate product of the fp32 matrices whose
     exact bf16 splits are A (3 planes; or its first 2, see gemm_a_planes) and B (1-3
@@ -1551,7 +1557,9 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
     k more than ``raw_max`` ways, the product is reduced here instead (into the first
     M x N floats of ``raw_slab``): a consumer reading that many slabs per element costs
     more than the reduction pass.  Returns the number of slabs in ``raw_slab`` (raw
-    mode; 1 otherwise)."""
+    mode; 1 otherwise).  ``gate`` (int32 device scalar, GPU only): the kernels return at
+    once when it holds 0 (conv_update's "no replicate active": the speculative pass
+    after a batch finished)."""
     pa, a_rows, _ = A.shape
     pb, b_rows, _ = B.shape
     for name, t in (("A", A), ("B", B)):
@@ -1608,8 +1616,16 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
                      col_scale.data_ptr() if col_scale is not None else 0, int(M), int(N),
                      int(Kd), pa, pb, int(bool(accumulate)), int(variant), int(ksplit), slab,
                      gemm_stages(variant), gemm_kstep(variant), int(raw_slab is not None),
-                     _stream_ptr(C))
+                     _gate_ptr(gate, C.device), _stream_ptr(C))
     return ksplit if raw_slab is not None else 1
+
+
+def _gate_ptr(gate, dev) -> int:
+    if gate is None:
+        return 0
+    if gate.dtype != torch.int32 or gate.numel() < 1 or gate.device != dev:
+        raise ValueError("gate: int32 device tensor with >= 1 element")
+    return gate.data_ptr()
 
 
 def gemm_stages(variant: int) -> int:

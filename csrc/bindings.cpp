@@ -71,11 +71,12 @@ PYBIND11_MODULE(_hip, m) {
   m.def("conv_update",
         [](uintptr_t lin, uintptr_t quad, double x_sq, uintptr_t err_init, uintptr_t err_prev,
            uintptr_t err, uintptr_t active, uintptr_t converged, uintptr_t n_pass, int n,
-           int pass, double tol, int final_pass, int init, uintptr_t stream) {
+           int pass, double tol, int final_pass, int init, uintptr_t gate, uintptr_t stream) {
           check(cnmf_conv_update(P<const float>(lin), P<const float>(quad), x_sq,
                                  P<double>(err_init), P<double>(err_prev), P<double>(err),
                                  P<int>(active), P<int>(converged), P<int>(n_pass), n, pass, tol,
-                                 final_pass, init, reinterpret_cast<hipStream_t>(stream)),
+                                 final_pass, init, P<int>(gate),
+                                 reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_conv_update");
         });
 
@@ -327,12 +328,12 @@ PYBIND11_MODULE(_hip, m) {
            long long ldb, long long b_plane, int b_rows, uintptr_t C, long long ldc,
            uintptr_t col_scale, int M, int N, int Kd, int pa, int pb, int accumulate,
            int variant, int ksplit, uintptr_t slab, int stages, int kstep, int raw,
-           uintptr_t stream) {
+           uintptr_t gate, uintptr_t stream) {
           check(cnmf_gemm_planes(P<const unsigned short>(A), lda, a_plane, a_rows,
                                  P<const unsigned short>(B), ldb, b_plane, b_rows, P<float>(C),
                                  ldc, P<const float>(col_scale), M, N, Kd, pa, pb, accumulate,
                                  variant, ksplit, P<float>(slab), stages, kstep, raw,
-                                 reinterpret_cast<hipStream_t>(stream)),
+                                 P<const int>(gate), reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_gemm_planes");
         });
   m.def("split_planes",

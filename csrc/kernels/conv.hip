@@ -10,45 +10,55 @@
 
 namespace cnmf {
 
-__global__ void conv_update_kernel(const float* lin, const float* quad, double x_sq,
-                                   double* err_init, double* err_prev, double* err, int* active,
-                                   int* converged, int* n_pass, int n, int pass, double tol,
-                                   int final_pass, int init) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const double e = sqrt(fmax(x_sq - 2.0 * (double)lin[r] + (double)quad[r], 0.0));
-  if (init) {  // error of the initial factors
-    err_init[r] = e;
-    err_prev[r] = e;
+__global__ void __launch_bounds__(256) conv_update_kernel(
+    const float* lin, const float* quad, double x_sq, double* err_init, double* err_prev,
+    double* err, int* active, int* converged, int* n_pass, int n, int pass, double tol,
+    int final_pass, int init, int* gate) {
+  // one workgroup strides over the replicates, so `gate` (any replicate still active)
+  // is a plain block reduction: no atomics, nothing to reset between passes
+  int any = 0;
+  for (int r = threadIdx.x; r < n; r += blockDim.x) {
+    const double e = sqrt(fmax(x_sq - 2.0 * (double)lin[r] + (double)quad[r], 0.0));
+    if (init) {  // error of the initial factors
+      err_init[r] = e;
+      err_prev[r] = e;
+      err[r] = e;
+      active[r] = 1;
+      converged[r] = 0;
+      n_pass[r] = 0;
+      any = 1;
+      continue;
+    }
+    if (!active[r]) continue;
     err[r] = e;
-    active[r] = 1;
-    converged[r] = 0;
-    n_pass[r] = 0;
-    return;
+    n_pass[r] = pass >= 0 ? pass : n_pass[r] + 1;   // pass < 0: count on device (graphs)
+    const double denom = err_init[r] > 1e-300 ? err_init[r] : 1e-300;
+    if ((err_prev[r] - e) / denom < tol) {
+      active[r] = 0;
+      converged[r] = 1;
+    } else if (final_pass) {
+      active[r] = 0;
+    } else {
+      err_prev[r] = e;
+      any = 1;
+    }
   }
-  if (!active[r]) return;
-  err[r] = e;
-  n_pass[r] = pass >= 0 ? pass : n_pass[r] + 1;   // pass < 0: count on device (graphs)
-  const double denom = err_init[r] > 1e-300 ? err_init[r] : 1e-300;
-  if ((err_prev[r] - e) / denom < tol) {
-    active[r] = 0;
-    converged[r] = 1;
-  } else if (final_pass) {
-    active[r] = 0;
-  } else {
-    err_prev[r] = e;
-  }
+  any = __syncthreads_or(any);
+  if (gate && threadIdx.x == 0) *gate = any;
 }
 
 }  // namespace cnmf
 
+// gate (optional): set to 1 while any replicate is still active, 0 once none is -- the
+// split GEMMs of the next (speculative) pass then return at once (gemm_planes.hip)
 extern "C" hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq,
                                        double* err_init, double* err_prev, double* err,
                                        int* active, int* converged, int* n_pass, int n, int pass,
-                                       double tol, int final_pass, int init, hipStream_t stream) {
+                                       double tol, int final_pass, int init, int* gate,
+                                       hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cnmf::conv_update_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, lin,
-                     quad, x_sq, err_init, err_prev, err, active, converged, n_pass, n, pass, tol,
-                     final_pass, init);
+  hipLaunchKernelGGL(cnmf::conv_update_kernel, dim3(1), dim3(256), 0, stream, lin, quad, x_sq,
+                     err_init, err_prev, err, active, converged, n_pass, n, pass, tol, final_pass,
+                     init, gate);
   return hipGetLastError();
 }

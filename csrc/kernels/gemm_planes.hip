@@ -54,6 +54,8 @@ struct PlaneGemmParams {
   float* slab;              // [ksplit][M][N] partial products (split-K only)
   int raw;                  // 1: raw partials to `slab` even at ksplit 1, and no reduce --
                             // the consuming solve sums them (solve_pipe.hip numer slabs)
+  const int* gate;          // optional: *gate == 0 -> every workgroup returns at once (an
+                            // online pass enqueued after every replicate had finished)
 };
 
 __device__ __forceinline__ unsigned short f2bf_rn(float f) {
@@ -80,6 +82,9 @@ __device__ __forceinline__ void glds16(const unsigned short* g, unsigned char* l
 
 template <int PA, int PB, int BK, int WM, int WN, int NS, int MI = 4>
 __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmParams p) {
+  // gate: read now, tested after the prologue's loads are issued, so its latency hides
+  // behind theirs (testing it first cost ~1 % of the headline: every GEMM waited for it)
+  const int gate_v = p.gate ? *p.gate : 1;
   constexpr int NT = 64 * WM * WN;            // threads
   constexpr int WR = 16 * MI;                 // each wave owns a WR x 64 output block
   constexpr int BM = WR * WM, BN = 64 * WN;
@@ -157,6 +162,10 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (kb + s < ke) issue(s, (kb + s) * BK);
+  if (gate_v == 0) {   // uniform: nothing left to compute; drain the LDS-DMA first
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
   for (int kt = kb; kt < ke; ++kt) {
     const int cur = (kt - kb) % NS;
     // stage kt has landed once at most min(NS-2, ke-1-kt) later stages are outstanding
@@ -310,7 +319,11 @@ __global__ void split_planes_kernel(const float* __restrict__ S, long long lds, 
 // C (+)= col_scale * sum_s slab[s] in slice order (deterministic split-K reduction)
 __global__ void gemm_reduce_kernel(const float* __restrict__ slab, int ksplit, int M, int N,
                                    float* __restrict__ C, long long ldc,
-                                   const float* __restrict__ col_scale, int accumulate) {
+                                   const float* __restrict__ col_scale, int accumulate,
+                                   const int* gate) {
+  // (the gate is not tested here: a reduce of a skipped product writes an output no
+  // replicate reads, and waiting for the flag cost more than the rare skip saves)
+  (void)gate;
   const long long total = (long long)M * N;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
@@ -385,7 +398,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
                                        const float* col_scale, int M, int N, int Kd, int pa,
                                        int pb, int accumulate, int variant, int ksplit,
                                        float* slab, int stages, int kstep, int raw,
-                                       hipStream_t stream) {
+                                       const int* gate, hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (raw && !slab) return hipErrorInvalidValue;
   const int bk = 32;   // smallest k-step depth: Kd must be a multiple of it
@@ -399,7 +412,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   p.B = B; p.ldb = ldb; p.b_plane = b_plane; p.b_rows = b_rows;
   p.C = C; p.ldc = ldc; p.col_scale = col_scale;
   p.M = M; p.N = N; p.Kd = Kd; p.accumulate = accumulate;
-  p.ksplit = ksplit; p.slab = slab; p.raw = raw ? 1 : 0;
+  p.ksplit = ksplit; p.slab = slab; p.raw = raw ? 1 : 0; p.gate = gate;
   hipError_t e;
   switch (pa * 4 + pb) {
     case 9: e = cnmf::launch_variant<2, 1>(variant, p, stages, kstep, stream); break;
@@ -414,7 +427,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   long long blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(cnmf::gemm_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, slab,
-                     ksplit, M, N, C, ldc, col_scale, accumulate);
+                     ksplit, M, N, C, ldc, col_scale, accumulate, gate);
   return hipGetLastError();
 }
 

@@ -9,9 +9,9 @@
 //            the exact squared distance sum_j (x_j - c_j)^2 (first index on ties, as numpy
 //            argmin), writes its label (and the distance for the inertia).
 //   phase B  the round's points are added to the workgroup's centroid accumulator in LDS:
-//            thread j (< d) walks the round's 256 points IN ORDER and adds x[p][j] to
-//            acc[label[p]][j] (distinct addresses per lane, no atomics); thread 255 counts.
-//            Coalesced: for each p the d threads read one contiguous row of X.
+//            a stable counting sort groups them by label, then each thread sums whole
+//            (cluster, feature) segments in point order and adds them once (no float
+//            atomics; the label histogram uses integer LDS atomics).
 //   flush    the workgroup writes its partial sums/counts; the host sums the partials over
 //            workgroups with a fixed-order reduction -> bitwise deterministic centroids.
 // The (n x n_init*k) distance matrix of the MFMA path (4 GB at 500k cells x 10 x 100) is
@@ -37,6 +37,9 @@ __global__ void __launch_bounds__(kKmThreads)
   double* sAcc = sC + (long long)k * DP;   // k * DP accumulator
   double* sCnt = sAcc + (long long)k * DP; // k counts
   int* sLab = reinterpret_cast<int*>(sCnt + k);   // 256 labels of the current round
+  int* sPerm = sLab + kKmThreads;                   // round's points grouped by label
+  int* sHist = sPerm + kKmThreads;                  // k: points per label this round
+  int* sOff = sHist + k;                            // k: exclusive prefix of sHist
   const int r = blockIdx.y;
   const int n_init = gridDim.y;
   if (live != nullptr && live[r] == 0) return;    // frozen restart: partials unused
@@ -85,18 +88,44 @@ __global__ void __launch_bounds__(kKmThreads)
     }
     sLab[tid] = arg;
     __syncthreads();
-    // ---- phase B: ordered accumulation (only when partial sums are wanted)
+    // ---- phase B: ordered accumulation (only when partial sums are wanted).  The
+    // round's points are grouped by label with a stable counting sort (rank = earlier
+    // points with the same label: a broadcast LDS walk), then every thread owns
+    // (cluster, feature) pairs and sums its cluster's points in point order before one
+    // add into the accumulator -- all 256 threads busy and no chain of dependent LDS
+    // read-modify-writes (d threads walking 256 points serially took ~11 ms per Lloyd
+    // step at 500k x 50 x 100, profiles/r3ae_harmony_500k_kernel_summary.txt).
+    // Deterministic: fixed summation order for every (cluster, feature).
     if (psum != nullptr) {
-      const int np = (int)((n - p0) < kKmThreads ? (n - p0) : kKmThreads);
-      if (tid < d) {
-        const double* col = X + p0 * ldx + tid;
-        for (int p = 0; p < np; ++p) {
-          const int c = sLab[p];
-          sAcc[c * DP + tid] += col[(long long)p * ldx];
-        }
-      } else if (tid == kKmThreads - 1) {
-        for (int p = 0; p < np; ++p) sCnt[sLab[p]] += 1.0;
+      for (int c = tid; c < k; c += kKmThreads) sHist[c] = 0;
+      __syncthreads();
+      const int lab = sLab[tid];
+      int rank = 0;
+      if (lab >= 0) {
+        for (int q = 0; q < tid; ++q) rank += sLab[q] == lab ? 1 : 0;
+        atomicAdd(&sHist[lab], 1);
       }
+      __syncthreads();
+      if (tid == 0) {
+        int o = 0;
+        for (int c = 0; c < k; ++c) {
+          sOff[c] = o;
+          o += sHist[c];
+        }
+      }
+      __syncthreads();
+      if (lab >= 0) sPerm[sOff[lab] + rank] = tid;
+      __syncthreads();
+      for (int w = tid; w < k * d; w += kKmThreads) {
+        const int c = w / d, j = w - c * d;
+        const int cnt = sHist[c];
+        if (cnt == 0) continue;
+        const int o = sOff[c];
+        double acc = 0.0;
+        for (int t = 0; t < cnt; ++t) acc += X[(p0 + sPerm[o + t]) * ldx + j];
+        sAcc[c * DP + j] += acc;
+      }
+      for (int c = tid; c < k; c += kKmThreads) sCnt[c] += (double)sHist[c];
     }
     __syncthreads();
   }
@@ -112,7 +141,8 @@ template <int DP>
 static hipError_t launch_kmeans(const double* X, long long ldx, int n, int d, const double* C,
                                 int k, int n_init, const int* live, int* labels, double* mind,
                                 double* psum, double* pcnt, hipStream_t stream) {
-  const size_t lds = (size_t)(2 * (size_t)k * DP + k) * sizeof(double) + kKmThreads * sizeof(int);
+  const size_t lds = (size_t)(2 * (size_t)k * DP + k) * sizeof(double) +
+                     (2 * kKmThreads + 2 * (size_t)k) * sizeof(int);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_step_kernel<DP>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -235,7 +265,7 @@ extern "C" int cnmf_kmeans_fits(int k, int d) {
   if (k < 1 || d < 1 || d > 64) return 0;
   const int dp = (d + 15) / 16 * 16;
   const size_t lds = (size_t)(2 * (size_t)k * dp + k) * sizeof(double) +
-                     cnmf::kKmThreads * sizeof(int);
+                     (2 * cnmf::kKmThreads + 2 * (size_t)k) * sizeof(int);
   return lds <= 156 * 1024 ? 1 : 0;
 }
 

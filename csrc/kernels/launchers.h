@@ -27,7 +27,7 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,
                             int* n_pass, int n, int pass, double tol, int final_pass,
-                            int init, hipStream_t stream);
+                            int init, int* gate, hipStream_t stream);
 int cnmf_solve_reg_max_cols(int K);
 int cnmf_solve_mfma_max_cols(int K);
 int cnmf_solve_pipe_tiles(int K, int per);
@@ -154,7 +154,8 @@ hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_
                             const unsigned short* B, long long ldb, long long b_plane, int b_rows,
                             float* C, long long ldc, const float* col_scale, int M, int N,
                             int Kd, int pa, int pb, int accumulate, int variant, int ksplit,
-                            float* slab, int stages, int kstep, int raw, hipStream_t stream);
+                            float* slab, int stages, int kstep, int raw, const int* gate,
+                            hipStream_t stream);
 hipError_t cnmf_split_planes(const float* S, long long lds, int rows, int cols, int cols_pad,
                              const float* col_mul, unsigned short* P, long long ldp,
                              long long plane, int nplanes, hipStream_t stream);

@@ -1748,3 +1748,54 @@ def test_seg_median_kernel_matches_pandas_with_ties(n, G, k):
     np.testing.assert_array_equal(got.cpu().numpy(), ref)
     assert ops.seg_median(torch.zeros((4097, 3), dtype=torch.float64, device="cuda"),
                           np.arange(4097) % 3, 3) is None          # beyond the LDS stage
+
+
+def test_gemm_gate_skips_and_runs():
+    """gemm_planes(gate=...): a zero gate leaves the output untouched (every workgroup
+    returns once its prologue loads drained; without a k split nothing else runs), a one
+    gate computes the product (with and without a k split)."""
+    g = torch.Generator().manual_seed(7)
+    M, N, Kd = 200, 300, 512
+    a = torch.rand((M, Kd), generator=g)
+    b = torch.randint(0, 20, (N, Kd), generator=g).float()
+    A = torch.zeros((2, M, Kd), dtype=torch.int16, device="cuda")
+    B = torch.zeros((1, N, Kd), dtype=torch.int16, device="cuda")
+    ops.split_planes(a.cuda(), A)
+    ops.split_planes(b.cuda(), B)
+    ref = (a.double() @ b.double().t()).numpy()
+    for ksplit in ("1", "4"):
+        os.environ["CNMF_GEMM_KSPLIT"] = ksplit
+        ops.refresh_env()
+        try:
+            C = torch.full((M, N), -7.0, device="cuda")
+            if ksplit == "1":
+                ops.gemm_planes(C, A, B, M, N, Kd, gate=torch.zeros(1, dtype=torch.int32,
+                                                                      device="cuda"))
+                assert bool((C == -7.0).all())
+            ops.gemm_planes(C, A, B, M, N, Kd, gate=torch.ones(1, dtype=torch.int32,
+                                                                 device="cuda"))
+            np.testing.assert_allclose(C.cpu().double().numpy(), ref, rtol=1e-5)
+        finally:
+            os.environ.pop("CNMF_GEMM_KSPLIT", None)
+            ops.refresh_env()
+
+
+def test_gemm_gate_leaves_results_bitwise(monkeypatch):
+    """The fused pass's GEMM gate (CNMF_GEMM_GATE=1: the speculative pass after every
+    replicate finished skips its products) changes nothing: spectra, usages, errors and
+    pass counts are bitwise those of a run without the gate."""
+    from cnmf_torch_amd.models import nmf as nmf_mod
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(5000, 600, n_programs=6, seed=2)).cuda()
+    seeds = list(range(11, 51))
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(nmf_mod, "_GEMM_GATE", on)
+        solver = nmf_mod.NMFBatchSolver(X, nmf_mod.NMFOptions(n_components=7,
+                                                              online_chunk_size=2500))
+        out[on] = solver.run(seeds)
+    a, b = out[True], out[False]
+    np.testing.assert_array_equal(a.n_iter, b.n_iter)
+    np.testing.assert_array_equal(a.err, b.err)
+    assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
