@@ -1971,14 +1971,17 @@ class NMFBatchSolver:
         a per-gene std (X == C u_g, _count_units), and counts <= 2048 are exact in fp16.
         Half the bytes of the per-step X re-reads that bound those kernels
         (profiles/r3m_*), and xth replaces the fp32 X^T copy.  None for other data, the
-        sparse path, or CNMF_KL_FP16_COUNTS=0."""
+        sparse path, or CNMF_KL_FP16_COUNTS=0.  Default 'w': the spectra side reads the
+        fp16 counts and the usage side fp32 X -- on the usage side the fp16 -> fp32
+        conversion costs more issue than the halved bytes save (326-329 vs 314-317 rep/s
+        with both sides, profiles/r3v_*, r3w_*); '1' uses them on both sides."""
         if "_klc" in self.__dict__:
             return self._klc
         res = None
         X = self.X
         if (self.beta == 1.0 and isinstance(X, torch.Tensor) and X.device.type == "cuda"
                 and X.dtype == torch.float32 and ops.use_native(X)
-                and os.environ.get("CNMF_KL_FP16_COUNTS", "1") != "0"
+                and os.environ.get("CNMF_KL_FP16_COUNTS", "w") != "0"
                 and self._kl_sparse() is None):
             unit = _count_units(X, self._colstats)
             if unit is not None:
@@ -2041,7 +2044,7 @@ class NMFBatchSolver:
         if self._kl_sparse() is not None:
             return ops.kl_st(F3)
         klc = self._kl_counts() if (usage_side and
-                                    os.environ.get("CNMF_KL_FP16_COUNTS", "1") != "w") else None
+                                    os.environ.get("CNMF_KL_FP16_COUNTS", "w") != "w") else None
         return ops.beta_panels(F3, self.beta, row_scale=klc[3] if klc is not None else None)
 
     def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, panels=None, rows=None):
@@ -2073,7 +2076,7 @@ class NMFBatchSolver:
                    if self.beta == 1.0 and cuda else None)
         csr = self._kl_sparse() if (cuda and rows is not None) else None
         klc = self._kl_counts() if (cuda and rows is not None and csr is None
-                                    and os.environ.get("CNMF_KL_FP16_COUNTS", "1") != "w") \
+                                    and os.environ.get("CNMF_KL_FP16_COUNTS", "w") != "w") \
             else None
         if cuda and wpan is None:
             wpan = ops.kl_st(W3) if csr is not None else ops.beta_panels(
