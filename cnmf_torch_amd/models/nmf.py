@@ -556,9 +556,11 @@ class _Batch:
         st["active"][:n] = torch.where(stop, torch.zeros_like(st["active"][:n]),
                                        st["active"][:n])
 
-    def finalize(self):
+    def finalize(self, extra=()):
         """Restore original replicate order: (HT, W, ks, err, n_pass, converged,
-        h_iters, w_iters), rows of replicate r at offs[r] : offs[r] + ks[r]."""
+        h_iters, w_iters, extra_values), rows of replicate r at offs[r] : offs[r] + ks[r].
+        ``extra``: one-element int device tensors (the cooperative-solve flags) read back
+        in the same copy, as a float64 array."""
         inv = np.argsort(self.order)
         dev = self.W.device
         roff = np.concatenate([[0], np.cumsum(self.kpos)[:-1]])
@@ -568,11 +570,16 @@ class _Batch:
         idx = _to_device(inv, dev)
         # one packed device->host copy instead of eight small synchronising ones
         keys = ("err", "n_pass", "converged")
-        packed = torch.stack([self.state[k][idx].to(torch.float64) for k in keys] +
-                             [self.h_iters[idx].to(torch.float64),
-                              self.w_iters[idx].to(torch.float64)]).cpu().numpy()
+        rows5 = torch.stack([self.state[k][idx].to(torch.float64) for k in keys] +
+                            [self.h_iters[idx].to(torch.float64),
+                             self.w_iters[idx].to(torch.float64)])
+        flat = torch.cat([rows5.view(-1)] + [t.view(-1)[:1].to(torch.float64) for t in extra]) \
+            if len(extra) else rows5.view(-1)
+        flat = flat.cpu().numpy()
+        m = idx.numel()
+        packed, ext = flat[:5 * m].reshape(5, m), flat[5 * m:]
         return (HT, W, self.kpos[inv], packed[0], packed[1].astype(np.int64), packed[2] != 0,
-                packed[3].astype(np.int64), packed[4].astype(np.int64))
+                packed[3].astype(np.int64), packed[4].astype(np.int64), ext)
 
 
 class _PassPipeline:
@@ -1125,14 +1132,16 @@ class NMFBatchSolver:
                 self._online_beta(st)
             else:
                 self._batch_beta(st)
-        HT, W, ks_out, err, n_iter, conv, hi, wi = st.finalize()
+        # the cooperative solves' failure flags ride in finalize's one device->host copy
+        cflags = ops.coop_flags(self.X.device) if self.X.device.type == "cuda" else []
+        HT, W, ks_out, err, n_iter, conv, hi, wi, cvals = st.finalize([f for _, f in cflags])
         if pad:     # drop the zero padding components: rows [0, K) of each block
             offp = np.concatenate([[0], np.cumsum(ks_out)[:-1]])
             keep = _to_device(_ranges(offp, ks), HT.device)
             HT, W = HT.index_select(0, keep), W.index_select(0, keep)
             ks_out = ks
-        if self.X.device.type == "cuda":
-            ops.coop_check(self.X.device)
+        if cflags:
+            ops.coop_check(values=cvals, flags=cflags)
         check = getattr(self.comm, "check", None)
         if check is not None:     # one-shot xGMI all-reduce gave up on a peer?  Raise
             check()               # before any caller can persist these spectra

@@ -470,21 +470,35 @@ def coop_reserve(dev: torch.device, stream: int, R: int, max_iter: int, check_ev
     _coop_workspace(dev, stream, R, epochs, kCoopMaxSlices)
 
 
-def coop_check(device: torch.device | None = None) -> None:
-    """Raise if any cooperative solve on ``device`` gave up waiting (non-resident
-    workgroups) -- its results would be wrong.  Synchronises; call once per run."""
+def coop_flags(device: torch.device | None = None) -> list:
+    """[(key, flag)] of the cooperative workspaces on ``device`` (all devices if None):
+    the int32 device flags a solve sets when it gave up waiting.  A caller that already
+    copies results to the host packs them into that copy and hands the values to
+    coop_check, instead of one synchronising read per workspace."""
     want = None
     if device is not None:
         device = torch.device(device)
         want = str(torch.device("cuda", device.index if device.index is not None
                                 else torch.cuda.current_device()))
-    for key, ws in list(_COOP_WS.items()):   # other threads may add streams
-        if want is not None and key[0] != want:
-            continue
-        v = int(ws["flag"].item())
-        if v:
-            ws["flag"].zero_()
-            raise RuntimeError(f"cooperative solve failed on {key[0]} (code {v}): "
+    return [(key, ws["flag"]) for key, ws in list(_COOP_WS.items())   # other threads
+            if want is None or key[0] == want]                          # may add streams
+
+
+def coop_check(device: torch.device | None = None, values=None, flags=None) -> None:
+    """Raise if any cooperative solve on ``device`` gave up waiting (non-resident
+    workgroups) -- its results would be wrong.  ``values``: the flags of ``flags`` (a
+    coop_flags list) already read back by the caller; otherwise they are read here in
+    one synchronising copy.  Call once per run."""
+    if flags is None:
+        flags = coop_flags(device)
+    if not flags:
+        return
+    if values is None:
+        values = torch.cat([f.view(-1)[:1] for _, f in flags]).cpu().tolist()
+    for (key, f), v in zip(flags, values):
+        if int(v):
+            f.zero_()
+            raise RuntimeError(f"cooperative solve failed on {key[0]} (code {int(v)}): "
                                "workgroups were not co-resident; set CNMF_SOLVE_COOP=0")
 
 
