@@ -79,8 +79,10 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     # (the elementwise work reads every accumulator: AGPR copies cost ~30 % of the VALU)
     # the pipelined solve keeps its elementwise update scalar: SLP-packed v_pk_*_f32 beside
     # MFMAs cost more issue cycles than the scalar pair (MI355X_MICROARCH.md cycle table)
-    unit_flags = {"beta_planes.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-                  "solve_pipe.hip": ["-fno-slp-vectorize"]}
+    unit_flags = {"beta_planes.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+    for s in srcs:      # every instantiation unit of the pipelined solve (solve_pipe*.hip)
+        if os.path.basename(s).startswith("solve_pipe"):
+            unit_flags[os.path.basename(s)] = ["-fno-slp-vectorize"]
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)

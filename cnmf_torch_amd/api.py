@@ -32,12 +32,12 @@ import threading
 import time
 import uuid
 import warnings
-import weakref
 
 import numpy as np
 import pandas as pd
 import scipy.sparse as sp
 import torch
+from torch.utils.weak import WeakIdKeyDictionary
 
 from .models.consensus import (cluster_medians, kmeans, l2_normalize_rows, local_density,
                                pairwise_distances, silhouette)
@@ -255,8 +255,9 @@ def _resident_X(adata, dev: torch.device):
 # cooperative (co-resident, spinning) solves of concurrent k-selection threads
 _COOP_LOCK = threading.RLock()
 
-# ||X||^2 of a device-resident X (api._prediction_error), weakly keyed by the tensor
-_XSQ: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+# ||X||^2 of a device-resident X (api._prediction_error), weakly keyed by the tensor's
+# identity (a WeakKeyDictionary compares tensor keys with Tensor.__eq__, which raises)
+_XSQ = WeakIdKeyDictionary()
 
 
 def _load_npz_arrays(fn: str):

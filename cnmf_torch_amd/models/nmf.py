@@ -413,6 +413,7 @@ class _Batch:
         # replicates a compaction retires, copied to pinned memory (ready at `event`), so
         # the caller can persist them while the rest of the batch is still solving
         self.on_retire = None
+        self.dslots = None        # device-side ragged batching state (_dev_slots), fused runs
         self.uid = next(_BATCH_UIDS)   # never reused (unlike id()): plane-cache keys
         self.bucket = max(1, int(os.environ.get("CNMF_COMPACT_BUCKET",
                                                 "8" if W.device.type == "cuda" else "1")))
@@ -898,16 +899,20 @@ class _XPlanes:
         return 2
 
     @staticmethod
-    def build(X: torch.Tensor, stats=None):
-        """Planes for X when the split GEMM path applies (GPU, fp32, memory), else None."""
+    def build(X: torch.Tensor, stats=None, reserve: int = 0):
+        """Planes for X when the split GEMM path applies (GPU, fp32, memory), else None.
+        ``reserve``: device bytes the caller still has to allocate after the planes (the
+        fused step's slabs, plane buffers and statistics), kept free so a run that does
+        not fit takes the documented fp32 fallback here instead of failing partway."""
         if X.device.type != "cuda" or X.dtype != torch.float32 or \
                 os.environ.get("CNMF_GEMM", "planes") != "planes":
             return None
         N, G = X.shape
-        # sized by the plane count it will most likely use (2: counts above 256, or
-        # non-count data) plus one row block's temporaries -- not 3 planes + a full fp32
-        # copy of X as before (that refused 10M x 5k on one GPU)
-        need = _XPlanes.bytes_needed(N, G, 2) + 3 * 4 * min(N, 1 << 16) * G
+        # sized by the most planes the data can take (2 for counts above 256, 2 or 3 for
+        # non-count data: _float_planes) plus one row block's temporaries -- not 3 planes
+        # + a full fp32 copy of X as before (that refused 10M x 5k on one GPU)
+        pb = max(2, _XPlanes._float_planes(G))
+        need = _XPlanes.bytes_needed(N, G, pb) + 3 * 4 * min(N, 1 << 16) * G + int(reserve)
         free, _ = torch.cuda.mem_get_info(X.device)
         if need > 0.9 * free:
             _warn_once(f"split-precision GEMM planes need {need / 1e9:.1f} GB, "
@@ -977,6 +982,12 @@ _LAYOUT_REPLAY = os.environ.get("CNMF_LAYOUT_REPLAY", "1") != "0"
 # (profiles/r3ah_bench_{on,off}_*)
 _GEMM_GATE = os.environ.get("CNMF_GEMM_GATE", "0") == "1"
 _FLAG_STREAM = os.environ.get("CNMF_FLAG_STREAM", "0") == "1"
+# Device-side ragged batching of the fused step (CNMF_DEV_SLOTS=0: off).  conv_update gives
+# the live replicates compact row slots every pass; the solves write the GEMM operands and
+# read the GEMM outputs at those slots and the plane GEMMs skip the dead M-tiles, so GEMM
+# work falls with the active fraction on a FIXED launch shape (one captured graph per run,
+# no host compaction; SURVEY.md §7.4.3, the reference syncs per iteration at cnmf.py:377)
+_DEV_SLOTS = os.environ.get("CNMF_DEV_SLOTS", "1") != "0"
 # fused step: split-K GEMMs of up to this many k slices hand their raw slabs to the
 # consuming solve; deeper splits (the few-replicate tail) are reduced by the GEMM's own
 # pass -- the solve would read every slab per element (CNMF_FUSED_MAX_SLABS overrides)
@@ -1037,6 +1048,7 @@ class NMFBatchSolver:
         self._colstats = None
         self._mean_x = None
         self._xp = False            # split-GEMM planes of X: False = not built yet
+        self._ws_reserve = 0        # bytes of per-batch workspaces still to allocate (run)
         if self._virtual:
             local_sq = src.x_sq
             self._xp = src.planes
@@ -1086,10 +1098,14 @@ class NMFBatchSolver:
         if HT0 is None or W0 is None:
             N, G = self.X.shape
             tot = int(kpos.sum())
-            arena = self._arena(kpos) if (not pad and self._graphs_wanted(kpos)) else None
+            arena = self._arena(kpos) if self._graphs_wanted(kpos) else None
             if arena is not None:
-                # no padded ranks with an arena: init_into overwrites every row
+                # init_into overwrites every row of an unpadded block; the zero padding
+                # components of a padded one (native_rank) are cleared here
                 HT, W = arena["HT"], arena["W"]
+                if pad:
+                    HT.zero_()
+                    W.zero_()
             else:
                 HT = torch.zeros((tot, N), device=self.X.device, dtype=self.X.dtype)
                 W = torch.zeros((tot, G), device=self.X.device, dtype=self.X.dtype)
@@ -1117,6 +1133,14 @@ class NMFBatchSolver:
             if pad:
                 raise ValueError("explicit initial factors need K <= 32 on the GPU")
             HT, W = HT0.to(self.X.dtype).clone(), W0.to(self.X.dtype).clone()
+        if self._xp is False:
+            # the fused step's workspaces for this batch, allocated after the X planes:
+            # <= 4 raw split-K slabs of both GEMMs, the accumulated B, 3 bf16 planes of
+            # the usages and spectra (a generous bound; _fused_bufs)
+            N, G = self.X.shape
+            rows = int(kpos.sum())
+            cw = min(N, int(o.online_chunk_size))
+            self._ws_reserve = rows * (4 * 4 * (cw + G) + 4 * G + 6 * (cw + G))
         st = _Batch(HT, W, kpos, arena=arena)
         st.graphs = arena is not None
         st.order = pos.astype(np.int64).copy()
@@ -1182,7 +1206,7 @@ class NMFBatchSolver:
     def _planes(self):
         """X planes for the split-precision MFMA GEMMs, or None (CPU, fp64, memory)."""
         if self._xp is False:
-            self._xp = _XPlanes.build(self.X, self._colstats)
+            self._xp = _XPlanes.build(self.X, self._colstats, reserve=self._ws_reserve)
         return self._xp
 
     def _plane_buf(self, key: str, rows: int, cols: int) -> torch.Tensor:
@@ -1413,7 +1437,7 @@ class NMFBatchSolver:
         if env != "1" and len(kpos) > 256:
             return False
         return (o.algo == "mu" and o.online_stats == "pass" and o.online_inner_conv == "loss"
-                and not self.comm.is_distributed and int(np.max(kpos)) <= 16
+                and not self.comm.is_distributed and int(np.max(kpos)) <= 64
                 and os.environ.get("CNMF_FUSED_STEP", "1") != "0"
                 and all(v == 0.0 for v in (o.l1_H, o.l2_H, o.l1_W, o.l2_W)))
 
@@ -1500,7 +1524,7 @@ class NMFBatchSolver:
         (split-K slabs summed by the consuming solve, the Grams passed between the solves
         as per-slice partials; solve_pipe.hip).  Needs the split-GEMM planes, MU without
         regularisation, the block-objective stop, one block per online step (8-aligned), a
-        single process (the DP path all-reduces the statistics), K <= 16 and solves whose
+        single process (the DP path all-reduces the statistics), K <= 64 and solves whose
         cooperative slices fit the pipelined kernel.  CNMF_FUSED_STEP=0 disables it."""
         o = self.opts
         if (self.X.device.type != "cuda" or os.environ.get("CNMF_FUSED_STEP", "1") == "0"
@@ -1515,13 +1539,31 @@ class NMFBatchSolver:
                 return False
         dev = self.X.device
         for g in st.groups:
-            if g.K > 16:
-                return False
             for n in {b - a for (a, b), in steps} | {G}:
-                S = ops._mfma_split(n, g.n, g.K, 1, "auto", dev)
-                if S is None or S > ops.kCoopMaxSlices or ops._hip.solve_pipe_tiles(g.K, -(-n // S)) == 0:
+                if ops.pipe_slices(n, g.n, g.K, dev) is None:
                     return False
         return True
+
+    def _dev_slots(self, st: _Batch) -> dict:
+        """The device-side ragged batching state of a fused run (conv_update ``slots``):
+        per-replicate rank, current / previous compact row slots and the two live row
+        counts -- reset to the full layout (every replicate live) at the start of a run.
+        Arena batches keep the buffers (fixed addresses for the captured pass graphs)."""
+        n, dev = st.n_act, st.W.device
+        a = st.arena
+        ds = a.get("dslots") if a is not None else None
+        if ds is None or ds["kvec"].numel() != n:
+            kv = torch.as_tensor(np.asarray(st.kpos[:n], dtype=np.int32)).to(dev)
+            ds = {"kvec": kv, "cur": torch.empty(n, dtype=torch.int32, device=dev),
+                  "prev": torch.empty(n, dtype=torch.int32, device=dev),
+                  "live": torch.empty(2, dtype=torch.int32, device=dev)}
+            if a is not None:
+                a["dslots"] = ds
+        off = torch.cumsum(ds["kvec"], 0, dtype=torch.int32) - ds["kvec"]
+        ds["cur"].copy_(off)
+        ds["prev"].copy_(off)
+        ds["live"].fill_(int(st.rows_act))
+        return ds
 
     def _fused_bufs(self, st: _Batch, steps) -> dict:
         """Per-layout workspaces of the fused step (allocated when the layout changes)."""
@@ -1605,50 +1647,73 @@ class NMFBatchSolver:
         wkey = self._fused_prep(st, fb, keep_slices=False)
         last_s = len(steps) - 1
         wpl = fb["wpl"]
+        # device slots (see _dev_slots): the GEMM operands / outputs live at compact rows.
+        # The spectra planes the step-0 numerator reads were written last pass (previous
+        # slots, live[0]); everything else in the pass uses this pass's slots (live[1])
+        ds = st.dslots
         for s_, ((a, b),) in enumerate(steps):
             cw = b - a
             ks_n = ops.gemm_planes(None, wpl[:ops.gemm_a_planes(xp.Gp)], xp.x[:, a:], rows, cw,
                                    xp.Gp, raw_slab=slabN, raw_max=_FUSED_MAX_SLABS,
-                                   gate=st.gate)
+                                   gate=st.gate,
+                                   live=None if ds is None else ds["live"][int(s_ > 0):])
             kd = -(-cw // bk) * bk
             hpl = fb["hpl"][:, :, :kd]
             hpl_n = ops.gemm_a_planes(kd)
             hcols = HT[:, a:b]
             for g in groups:
-                numer = slabN.as_strided((g.n, g.K, cw), (g.K * cw, cw, 1), g.r0 * cw)
+                if ds is None:
+                    numer = slabN.as_strided((g.n, g.K, cw), (g.K * cw, cw, 1), g.r0 * cw)
+                    nsl = psl = None
+                    pl_g = hpl[:, g.rows]
+                else:
+                    numer = slabN.as_strided((g.n, g.K, cw), (g.K * cw, cw, 1), 0)
+                    nsl = (ds["prev"] if s_ == 0 else ds["cur"])[g.pos]
+                    psl = ds["cur"][g.pos]
+                    pl_g = hpl
                 ga = active[g.pos]
                 fb["hhp_n"][g.p0] = ops.solve(
                     "mu", g.rep3(hcols), numer, None, max_iter=o.online_chunk_max_iter,
                     tol=o.online_h_tol, eps=o.eps, iters_out=h_it[g.pos], conv_mode=1,
-                    check_every=o.inner_check_every, active=ga, planes=hpl[:, g.rows],
+                    check_every=o.inner_check_every, active=ga, planes=pl_g,
                     planes_n=hpl_n, numer_slabs=ks_n, numer_slab_stride=rows * cw,
                     gram_parts=fb["parts"][g.p0](fb["WWp"]), gram_parts_n=fb["wwp_n"][g.p0],
-                    gram_parts_out=fb["parts"][g.p0](fb["HHp"]), coop_device_gen=True)
+                    gram_parts_out=fb["parts"][g.p0](fb["HHp"]), coop_device_gen=True,
+                    numer_slot=nsl, planes_slot=psl)
             ks_b = ops.gemm_planes(None, hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd,
                                    raw_slab=slabB, raw_max=_FUSED_MAX_SLABS,
-                                   gate=st.gate if _GEMM_GATE else None)
+                                   gate=st.gate if _GEMM_GATE else None,
+                                   live=None if ds is None else ds["live"][1:])
             last = s_ == last_s
             wpl_out, unit = wpl, xp.unit
             wpl_n = ops.gemm_a_planes(xp.Gp)
             A_in, A_out = fb["A"][(s_ + 1) % 2], fb["A"][s_ % 2]
             for g in groups:
-                numer = slabB.as_strided((g.n, g.K, G), (g.K * G, G, 1), g.r0 * G)
+                if ds is None:
+                    numer = slabB.as_strided((g.n, g.K, G), (g.K * G, G, 1), g.r0 * G)
+                    nsl = None
+                    wpl_g = wpl_out[:, g.rows]
+                else:
+                    numer = slabB.as_strided((g.n, g.K, G), (g.K * G, G, 1), 0)
+                    nsl = ds["cur"][g.pos]
+                    wpl_g = wpl_out
                 fb["wwp_n"][g.p0] = ops.solve(
                     "mu", g.rep3(W), numer, None if s_ == 0 else g.gram3(A_in),
                     max_iter=o.online_chunk_max_iter, tol=o.online_w_tol, eps=o.eps,
                     lin_out=fb["lin"][g.pos] if last else None,
                     quad_out=fb["quad"][g.pos] if last else None,
                     iters_out=w_it[g.pos], conv_mode=1, check_every=o.inner_check_every,
-                    active=active[g.pos], planes=wpl_out[:, g.rows], planes_colmul=unit,
+                    active=active[g.pos], planes=wpl_g, planes_colmul=unit,
                     planes_n=wpl_n, numer_slabs=ks_b, numer_slab_stride=rows * G,
                     numer_scale=unit, numer_base=None if s_ == 0 else g.rep3(B),
                     numer_out=None if last else g.rep3(B),
                     gram_parts=fb["parts"][g.p0](fb["HHp"]), gram_parts_n=fb["hhp_n"][g.p0],
                     gram_out=None if last else g.gram3(A_out),
-                    gram_parts_out=fb["parts"][g.p0](fb["WWp"]), coop_device_gen=True)
+                    gram_parts_out=fb["parts"][g.p0](fb["WWp"]), coop_device_gen=True,
+                    numer_slot=nsl, planes_slot=nsl)
             fb["wwp_key"] = fb["wpl_key"] = wkey
         ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
-                        n, -1, o.tol, final=final, gate=st.gate)
+                        n, -1, o.tol, final=final, gate=st.gate, slots=ds)
 
     # ------------------------------------------------------------------ online frobenius
     def _online_frob(self, st: _Batch) -> None:
@@ -1666,11 +1731,15 @@ class NMFBatchSolver:
             st.A, st.B = A0.clone(), B0.clone()
         del A0, B0
         max_pass = int(o.online_max_pass)
-        pipe = _PassPipeline(st)
         n_alloc = None
         graphs = _graphs_enabled(X) and not dist
         graph, graph_key, last_key = None, None, None
         fused = self._fused_ok(st, steps)
+        # (early replicate writes hand over retired replicates at host compactions)
+        st.dslots = self._dev_slots(st) if (fused and _DEV_SLOTS and st.on_retire is None) \
+            else None
+        # device slots: the batch keeps one layout (no host compaction, never fires at 2.0)
+        pipe = _PassPipeline(st, compact_frac=2.0 if st.dslots is not None else None)
         fb, fb_key, sl = None, None, None
         for p in range(max_pass):
             n = st.n_act

@@ -122,7 +122,9 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           numer_scale: torch.Tensor | None = None, numer_base: torch.Tensor | None = None,
           numer_out: torch.Tensor | None = None, gram_parts: torch.Tensor | None = None,
           gram_parts_n: int = 0, gram_out: torch.Tensor | None = None,
-          gram_parts_out: torch.Tensor | None = None, coop_device_gen: bool = False) -> int:
+          gram_parts_out: torch.Tensor | None = None, coop_device_gen: bool = False,
+          numer_slot: torch.Tensor | None = None,
+          planes_slot: torch.Tensor | None = None) -> int:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -162,13 +164,20 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     ``coop_device_gen``: cooperative launches tag their granules from a device-side
     generation the kernel itself advances (pipelined kernel only), so a launch captured
     in a HIP graph needs no zeroing of the granules per replay.
+    ``numer_slot`` / ``planes_slot`` (int32 device, one per replicate of the call; the
+    pipelined kernel only): replicate r's numerator rows start at row numer_slot[r] of
+    ``numer`` (then pass ``numer`` as the (R, K, n) view of the slab from row 0) and its
+    planes go to row planes_slot[r] of ``planes`` -- the compact slots of conv_update's
+    device-side ragged batching (the slots of live replicates never overlap; the caller
+    sizes the slabs / planes for the batch's rows).
     Returns S, the number of column slices per replicate the launch used.
     """
     a = ALGOS[algo]
     R, K, n = x.shape
     fused = (numer_slabs > 1 or numer_scale is not None or numer_base is not None
              or numer_out is not None or gram_parts is not None or gram_out is not None
-             or gram_parts_out is not None or coop_device_gen)
+             or gram_parts_out is not None or coop_device_gen or numer_slot is not None
+             or planes_slot is not None)
     if fused and not use_native(x):
         raise ValueError("solve: fused operands need the HIP kernels (CUDA tensors)")
     if gram is None and gram_parts is not None:
@@ -223,7 +232,9 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     if nsplit > 1 and max_iter != 1:
         raise ValueError("nsplit > 1 requires max_iter == 1 (no convergence test)")
     for name, t, dt in (("lin_out", lin_out, torch.float32), ("quad_out", quad_out, torch.float32),
-                        ("iters_out", iters_out, torch.int32), ("active", active, torch.int32)):
+                        ("iters_out", iters_out, torch.int32), ("active", active, torch.int32),
+                        ("numer_slot", numer_slot, torch.int32),
+                        ("planes_slot", planes_slot, torch.int32)):
         if t is not None and (t.dtype != dt or t.numel() < R or not t.is_contiguous()):
             raise ValueError(f"{name}: expected contiguous {dt} with >= {R} elements")
     if nsplit > 1:
@@ -237,14 +248,28 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     # slice fits one 256-thread workgroup's register tiles; four of its workgroups are
     # co-resident per CU, so its cooperative budget is 4x the 1024-thread one
     S = None
+    rpl = 0
+    pipe_ok = (a == 0 and conv_mode == 1 and nsplit <= 1 and not (l1_num or l1_den or l2)
+               and _ENV["CNMF_SOLVE_PIPE"] != "0" and h.solve_pipe_k(K))
     if variant in ("auto", "mfma") and a == 0 and h.solve_mfma_max_cols(K) > 0 \
             and (_ENV["CNMF_SOLVE_MFMA"] or "1") != "0":
         S = _mfma_split(n, nblocks, K, nsplit, coop, x.device)
-    if fused and (S is None or nsplit > 1 or conv_mode != 1 or l1_num or l1_den or l2
-                  or gram_of is not None or h.solve_pipe_tiles(K, -(-n // S)) == 0
-                  or _ENV["CNMF_SOLVE_PIPE"] == "0"):
-        raise ValueError("solve: fused operands need the pipelined MU kernel (K <= 16, "
+    if S is None and pipe_ok and variant in ("auto", "mfma") \
+            and (_ENV["CNMF_SOLVE_MFMA"] or "1") != "0":
+        # the pipelined kernel alone (K > 16, or K <= 16 when every replicate's slices
+        # do not fit at once): co-resident rounds of `rpl` replicates
+        plan = _pipe_plan(n, nblocks, K, coop, x.device)
+        if plan is not None:
+            S, rpl = plan
+            if gram is None and gram_of is not None:
+                gram = _gram_op(gram_of, active=active)
+                gram_of = None
+    if fused and (S is None or not pipe_ok or gram_of is not None
+                  or h.solve_pipe_tiles(K, -(-n // S)) == 0):
+        raise ValueError("solve: fused operands need the pipelined MU kernel (K <= 64, "
                          "l1 = l2 = 0, conv_mode 1, cooperative slices that fit)")
+    if planes_slot is not None and planes is None:
+        raise ValueError("planes_slot needs planes")
     if fused and gram_parts_out is not None and gram_parts_out.shape[1] < S:
         raise ValueError(f"gram_parts_out: {gram_parts_out.shape[1]} slots < {S} slices")
     if S is not None:
@@ -316,7 +341,9 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             int(gen), int(epochs), ws_flag, pl_ptr, int(pl_rs), int(pl_ld), int(pl_plane),
             planes_colmul.data_ptr() if (planes is not None and planes_colmul is not None) else 0,
             int(pl_cols), int(planes_n), gs_ptr, int(gs_rs), int(gs_ld), int(gs_cols),
-            *f_args, *gen_dev, _stream_ptr(x))
+            *f_args, *gen_dev, int(rpl),
+            numer_slot.data_ptr() if numer_slot is not None else 0,
+            planes_slot.data_ptr() if planes_slot is not None else 0, _stream_ptr(x))
     return int(S)
 
 
@@ -439,6 +466,53 @@ def _mfma_split(n: int, nblocks: int, K: int, nsplit: int, coop, dev: torch.devi
     return max(1, S)
 
 
+def pipe_slices(n: int, nblocks: int, K: int, dev: torch.device) -> int | None:
+    """The slice count S an unregularised block-objective MU solve of ``nblocks``
+    replicates x ``n`` columns runs at under coop="auto" on the pipelined kernel (as
+    ops.solve picks it), or None when that kernel does not take it."""
+    if _hip is None or not _hip.solve_pipe_k(K) or _ENV["CNMF_SOLVE_PIPE"] == "0" \
+            or (_ENV["CNMF_SOLVE_MFMA"] or "1") == "0":
+        return None
+    S = _mfma_split(n, nblocks, K, 1, "auto", dev) if _hip.solve_mfma_max_cols(K) > 0 else None
+    if S is None:
+        plan = _pipe_plan(n, nblocks, K, "auto", dev)
+        S = None if plan is None else plan[0]
+    if S is None or S > kCoopMaxSlices or _hip.solve_pipe_tiles(K, -(-n // S)) == 0:
+        return None
+    return S
+
+
+def _pipe_plan(n: int, nblocks: int, K: int, coop, dev: torch.device):
+    """(S, reps_per_launch) for the pipelined matrix-core solve (solve_pipe.h), or None.
+    Every replicate's columns are split into S cooperative slices that each fit one
+    workgroup's register tiles (S >= s_min); the launch runs the replicates in rounds of
+    ``reps_per_launch`` (0: all at once) so that each round's rpl * S workgroups are
+    co-resident (pipe_wg_per_cu(K) per CU).  Rounds are balanced, and S grows while the
+    round's budget allows (more, shorter slices fill the chip), up to ~256 columns per
+    slice."""
+    cap = _hip.solve_pipe_max_cols(K)
+    if cap <= 0 or nblocks <= 0:
+        return None
+    s_min = -(-n // cap)
+    budget = _hip.solve_pipe_wg_per_cu(K) * _coop_resident(dev)
+    if s_min > kCoopMaxSlices or s_min > budget:
+        return None
+    if s_min > 1 and _ENV["CNMF_SOLVE_COOP"] == "0":
+        return None
+    if coop != "auto":
+        S = max(1, int(coop))
+        if S < s_min or S > kCoopMaxSlices or S > budget:
+            return None
+        rpl = max(1, budget // S) if S > 1 else nblocks
+    else:
+        rounds = -(-nblocks * s_min // budget)
+        rpl = -(-nblocks // rounds)
+        S = max(s_min, min(budget // rpl, -(-n // 256), kCoopMaxSlices))
+    if S == 1:              # no cooperative exchange: residency does not matter
+        return 1, 0
+    return S, (rpl if rpl < nblocks else 0)
+
+
 def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int) -> dict:
     """Per-(device, stream) scratch: {generation, value} granules [R*epochs*S*2] (int64,
     zeroed once at allocation; coop_sum2 in csrc/kernels/solve_core.h), the launch
@@ -505,20 +579,43 @@ def coop_check(device: torch.device | None = None, values=None, flags=None) -> N
 # ----------------------------------------------------------------------------- convergence
 def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict, n: int,
                 pass_idx: int, tol: float, final: bool, init: bool = False,
-                gate: torch.Tensor | None = None) -> None:
+                gate: torch.Tensor | None = None, slots: dict | None = None) -> None:
     """Per-replicate Frobenius error from (lin, quad) and the (prev - cur)/init < tol
     stopping rule, entirely on the device (csrc/kernels/conv.hip).  ``state`` holds
     float64 err_init/err_prev/err and int32 active/converged/n_pass tensors.
     ``pass_idx < 0`` counts passes on the device (n_pass += 1), so the launch has no
     per-pass host argument and can live in a captured graph.  ``gate`` (int32 device
-    scalar): set to 1 while any replicate is active, else 0 (gemm_planes ``gate``)."""
+    scalar): set to 1 while any replicate is active, else 0 (gemm_planes ``gate``).
+    ``slots`` (device-side ragged batching): {"kvec": int32 rank per replicate, "cur" /
+    "prev": int32 compact row slots per replicate, "live": int32 [2] live row counts} --
+    after the flags update, cur/live[1] become the exclusive prefix sums of kvec over the
+    still-active replicates (batch order) and the old values move to prev/live[0]."""
     if n <= 0:
         return
     if not use_native(lin):
         reference.conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init)
         if gate is not None:
             gate.fill_(int(bool((state["active"][:n] != 0).any())))
+        if slots is not None:
+            act = (state["active"][:n] != 0) | bool(init)
+            k = slots["kvec"][:n] * act.to(torch.int32)
+            off = (torch.cumsum(k, 0) - k).to(torch.int32)
+            slots["prev"][:n] = off if init else slots["cur"][:n]
+            slots["live"][0] = int(k.sum()) if init else slots["live"][1]
+            slots["cur"][:n] = off
+            slots["live"][1] = int(k.sum())
         return
+    sl = (0, 0, 0, 0)
+    if slots is not None:
+        for key in ("kvec", "cur", "prev"):
+            t = slots[key]
+            if t.dtype != torch.int32 or not t.is_contiguous() or t.numel() < n or t.device != lin.device:
+                raise ValueError(f"slots[{key}] must be contiguous int32 with >= {n} entries")
+        lv = slots["live"]
+        if lv.dtype != torch.int32 or not lv.is_contiguous() or lv.numel() < 2 or lv.device != lin.device:
+            raise ValueError("slots[live] must be contiguous int32 with >= 2 entries")
+        sl = (slots["kvec"].data_ptr(), slots["cur"].data_ptr(), slots["prev"].data_ptr(),
+              lv.data_ptr())
     for t in (lin, quad):
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < n:
             raise ValueError("lin/quad must be contiguous float32 with >= n entries")
@@ -531,7 +628,7 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
                      state["err_prev"].data_ptr(), state["err"].data_ptr(),
                      state["active"].data_ptr(), state["converged"].data_ptr(),
                      state["n_pass"].data_ptr(), int(n), int(pass_idx), float(tol), int(final),
-                     int(init), _gate_ptr(gate, lin.device), _stream_ptr(lin))
+                     int(init), _gate_ptr(gate, lin.device), *sl, _stream_ptr(lin))
 
 
 # ----------------------------------------------------------------------------- beta MU
@@ -1555,7 +1652,7 @@ def split_planes(S: torch.Tensor, out: torch.Tensor, col_mul: torch.Tensor | Non
 def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int, N: int,
                 Kd: int, accumulate: bool = False, col_scale: torch.Tensor | None = None,
                 raw_slab: torch.Tensor | None = None, raw_max: int = 1 << 30,
-                gate: torch.Tensor | None = None) -> int:
+                gate: torch.Tensor | None = None, live: torch.Tensor | None = None) -> int:
     """C[:M, :N] (+)= col_scale * sum_{i + j <= 2} A[i][:M, :Kd] . B[j][:N, :Kd]^T on the bf16
     matrix cores (gemm_planes.hip): the fp32-accurate product of the fp32 matrices whose
     exact bf16 splits are A (3 planes; or its first 2, see gemm_a_planes) and B (1-3
@@ -1573,7 +1670,9 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
     more than the reduction pass.  Returns the number of slabs in ``raw_slab`` (raw
     mode; 1 otherwise).  ``gate`` (int32 device scalar, GPU only): the kernels return at
     once when it holds 0 (conv_update's "no replicate active": the speculative pass
-    after a batch finished)."""
+    after a batch finished).  ``live`` (int32 device scalar, GPU only): output rows >= its
+    value are dead (conv_update's compact slots of the live replicates) -- M-tiles that
+    start there return at once, their rows of C / the slabs are left unspecified."""
     pa, a_rows, _ = A.shape
     pb, b_rows, _ = B.shape
     for name, t in (("A", A), ("B", B)):
@@ -1612,7 +1711,7 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
     if raw_slab is not None and ksplit > raw_max:
         # (capping ksplit at raw_max instead -- no reduction pass, fewer workgroups -- was
         # slower on the tail passes: 232 vs 212 us, profiles/r3s_*)
-        gemm_planes(C, A, B, M, N, Kd, accumulate=False, col_scale=None)
+        gemm_planes(C, A, B, M, N, Kd, accumulate=False, col_scale=None, gate=gate, live=live)
         return 1
     if raw_slab is not None:
         if raw_slab.numel() < ksplit * M * N:
@@ -1630,7 +1729,7 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
                      col_scale.data_ptr() if col_scale is not None else 0, int(M), int(N),
                      int(Kd), pa, pb, int(bool(accumulate)), int(variant), int(ksplit), slab,
                      gemm_stages(variant), gemm_kstep(variant), int(raw_slab is not None),
-                     _gate_ptr(gate, C.device), _stream_ptr(C))
+                     _gate_ptr(gate, C.device), _gate_ptr(live, C.device), _stream_ptr(C))
     return ksplit if raw_slab is not None else 1
 
 

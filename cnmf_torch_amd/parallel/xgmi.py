@@ -142,8 +142,12 @@ class XgmiAllReduce:
         return out
 
     def check(self) -> None:
-        """Raise if any call so far gave up waiting for a peer (host sync)."""
-        if int(self.timeout.item()) != 0:
+        """Raise on EVERY rank if any call so far gave up waiting for a peer on ANY rank
+        (host sync; collective).  The flags are max-reduced first: a rank that alone saw
+        the timeout would otherwise raise while its peers wait in the next collective."""
+        flag = self.timeout.clone()
+        self._dist.all_reduce(flag, op=self._dist.ReduceOp.MAX, group=self.group)
+        if int(flag.item()) != 0:
             raise XgmiTimeout("xgmi all-reduce: a peer did not arrive within the wait limit "
                               "(mismatched collective sequence or a dead rank); results of "
                               "the calls since are invalid")

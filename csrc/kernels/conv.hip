@@ -10,10 +10,48 @@
 
 namespace cnmf {
 
+// Device-side ragged batching (optional `slot` block, graph-replayable: no host decision).
+// After the flags are updated, the rows of the replicates still active are given compact
+// slots: slot_cur[r] = sum of kvec[r'] over active r' < r (batch order), live[1] = the
+// live row count; the previous pass's slots / count move to slot_prev / live[0].  The
+// fused online step writes the GEMM operands (bf16 planes) and reads the GEMM outputs
+// (split-K slabs) at those slots, and the plane GEMMs skip M-tiles past the live count,
+// so GEMM work shrinks with every converged replicate (models/nmf.py _fused_pass).
+__device__ void conv_slots(const int* active, const int* kvec, int* slot_cur, int* slot_prev,
+                           int* live, int n, int init) {
+  __shared__ int ssum[256];
+  const int per = (n + 255) / 256;
+  const int r0 = threadIdx.x * per, r1 = min(n, r0 + per);
+  int tot = 0;
+  for (int r = r0; r < r1; ++r) tot += (init || active[r]) ? kvec[r] : 0;
+  ssum[threadIdx.x] = tot;
+  __syncthreads();
+  // inclusive scan of the 256 per-thread sums (Hillis-Steele in LDS)
+  for (int d = 1; d < 256; d <<= 1) {
+    const int v = threadIdx.x >= d ? ssum[threadIdx.x - d] : 0;
+    __syncthreads();
+    ssum[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int off = ssum[threadIdx.x] - tot;
+  for (int r = r0; r < r1; ++r) {
+    const int old = slot_cur[r];
+    slot_prev[r] = init ? off : old;
+    slot_cur[r] = off;
+    off += (init || active[r]) ? kvec[r] : 0;
+  }
+  if (threadIdx.x == 0) {
+    const int total = ssum[255];
+    live[0] = init ? total : live[1];
+    live[1] = total;
+  }
+}
+
 __global__ void __launch_bounds__(256) conv_update_kernel(
     const float* lin, const float* quad, double x_sq, double* err_init, double* err_prev,
     double* err, int* active, int* converged, int* n_pass, int n, int pass, double tol,
-    int final_pass, int init, int* gate) {
+    int final_pass, int init, int* gate, const int* kvec, int* slot_cur, int* slot_prev,
+    int* live) {
   // one workgroup strides over the replicates, so `gate` (any replicate still active)
   // is a plain block reduction: no atomics, nothing to reset between passes
   int any = 0;
@@ -45,6 +83,7 @@ __global__ void __launch_bounds__(256) conv_update_kernel(
   }
   any = __syncthreads_or(any);
   if (gate && threadIdx.x == 0) *gate = any;
+  if (kvec) conv_slots(active, kvec, slot_cur, slot_prev, live, n, init);
 }
 
 }  // namespace cnmf
@@ -55,10 +94,12 @@ extern "C" hipError_t cnmf_conv_update(const float* lin, const float* quad, doub
                                        double* err_init, double* err_prev, double* err,
                                        int* active, int* converged, int* n_pass, int n, int pass,
                                        double tol, int final_pass, int init, int* gate,
-                                       hipStream_t stream) {
+                                       const int* kvec, int* slot_cur, int* slot_prev,
+                                       int* live, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
+  if (kvec && (!slot_cur || !slot_prev || !live)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(cnmf::conv_update_kernel, dim3(1), dim3(256), 0, stream, lin, quad, x_sq,
                      err_init, err_prev, err, active, converged, n_pass, n, pass, tol, final_pass,
-                     init, gate);
+                     init, gate, kvec, slot_cur, slot_prev, live);
   return hipGetLastError();
 }

@@ -22,15 +22,20 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       const float* n_scale, const float* nbase, float* nout, long long nb_rs,
                       long long ldnb, const float* gpart, int gpart_n, long long gpart_rs,
                       float* gout, float* gp_out, long long gp_rs, unsigned* coop_gen_dev,
-                      unsigned* coop_arrive, hipStream_t stream);
+                      unsigned* coop_arrive, int reps_per_launch, const int* nslot,
+                      const int* plslot, hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,
                             int* n_pass, int n, int pass, double tol, int final_pass,
-                            int init, int* gate, hipStream_t stream);
+                            int init, int* gate, const int* kvec, int* slot_cur,
+                            int* slot_prev, int* live, hipStream_t stream);
 int cnmf_solve_reg_max_cols(int K);
 int cnmf_solve_mfma_max_cols(int K);
 int cnmf_solve_pipe_tiles(int K, int per);
+int cnmf_solve_pipe_k(int K);
+int cnmf_solve_pipe_max_cols(int K);
+int cnmf_solve_pipe_wg_per_cu(int K);
 
 int cnmf_beta_max_k();
 hipError_t cnmf_beta_contract(int side, int mode, const float* X, long long ldx, const float* HT,
@@ -155,7 +160,7 @@ hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_
                             float* C, long long ldc, const float* col_scale, int M, int N,
                             int Kd, int pa, int pb, int accumulate, int variant, int ksplit,
                             float* slab, int stages, int kstep, int raw, const int* gate,
-                            hipStream_t stream);
+                            const int* live, hipStream_t stream);
 hipError_t cnmf_split_planes(const float* S, long long lds, int rows, int cols, int cols_pad,
                              const float* col_mul, unsigned short* P, long long ldp,
                              long long plane, int nplanes, hipStream_t stream);

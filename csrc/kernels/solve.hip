@@ -12,6 +12,7 @@ hipError_t launch_solve_stream(int K, int algo, const SolveParams& p, int nblock
 extern "C" int cnmf_solve_max_k() { return 128; }
 extern "C" int cnmf_solve_mfma_max_cols(int K);
 extern "C" int cnmf_solve_pipe_tiles(int K, int per);
+extern "C" int cnmf_solve_pipe_k(int K);
 
 // ranks the kernels are instantiated for: 1..32, the padded wide ranks 40..64 (multiples
 // of 8) and 80..128 (multiples of 16, MU only: solve_wmfma.hip)
@@ -43,6 +44,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  float* nout, long long nb_rs, long long ldnb, const float* gpart,
                                  int gpart_n, long long gpart_rs, float* gout, float* gp_out,
                                  long long gp_rs, unsigned* coop_gen_dev, unsigned* coop_arrive,
+                                 int reps_per_launch, const int* nslot, const int* plslot,
                                  hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
@@ -52,6 +54,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.numer = numer; p.n_rs = n_rs; p.ldn = ldn;
   p.gram = gram; p.g_rs = g_rs;
   p.rep_index = rep_index;
+  p.rep0 = 0;
   p.ncols = ncols; p.max_iter = max_iter;
   p.tol = tol; p.l1_num = l1_num; p.l1_den = l1_den; p.l2 = l2; p.eps = eps;
   p.lin_out = lin_out; p.quad_out = quad_out; p.iters_out = iters_out;
@@ -75,9 +78,11 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.gp_out = gp_out; p.gp_rs = gp_rs;
   p.coop_gen_dev = coop_split > 1 ? coop_gen_dev : nullptr;
   p.coop_arrive = coop_arrive;
+  p.nslot = nslot;
+  p.plslot = plslot;
   if (p.coop_gen_dev && !coop_arrive) return hipErrorInvalidValue;
   const bool fused = p.nslab_n > 1 || n_scale || nbase || nout || gpart || gout || gp_out ||
-                     (coop_split > 1 && coop_gen_dev);
+                     (coop_split > 1 && coop_gen_dev) || nslot || plslot;
   if (fused && (p.nslab_n > 1 && p.nslab_stride * 4 * (long long)p.nslab_n >= 0x7fffffffLL))
     return hipErrorInvalidValue;
   if (!gram && !gpart && !gsrc) return hipErrorInvalidValue;
@@ -88,18 +93,32 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   if (coop_split > cnmf::kCoopMaxSlices) return hipErrorInvalidValue;
   if (!cnmf_solve_native_k(K)) return hipErrorInvalidValue;
   if (variant == 3 || variant == 5) {
-    // matrix-core variants, MU, K <= 16, every slice within one workgroup's tiles; the
-    // host picks the slicing (ops.solve / _mfma_split).  The software-pipelined kernel
-    // (solve_pipe.hip) takes the unregularised block-objective solves; solve_mfma.hip
-    // the rest (and everything under variant 5 = CNMF_SOLVE_PIPE=0)
+    // matrix-core variants, MU, every slice within one workgroup's tiles; the host picks
+    // the slicing (ops.solve / _mfma_split / _pipe_plan).  The software-pipelined kernel
+    // (solve_pipe.h, K <= 64) takes the unregularised block-objective solves;
+    // solve_mfma.hip (K <= 16) the rest (and everything under variant 5 =
+    // CNMF_SOLVE_PIPE=0).  reps_per_launch > 0: the pipelined kernel runs the replicates
+    // in rounds of that many, each round's S * reps workgroups co-resident (the host's
+    // budget) -- the wide ranks' register tiles do not hold every replicate at once
     const int parts = nsplit > 1 ? nsplit : (coop_split > 1 ? coop_split : 1);
     const int per = (ncols + parts - 1) / parts;
     const int T = ((per + 15) / 16 + 3) / 4;
-    if (algo != 0 || per > cnmf_solve_mfma_max_cols(K)) return hipErrorInvalidValue;
+    if (algo != 0) return hipErrorInvalidValue;
     const int Tp = cnmf_solve_pipe_tiles(K, per);
-    if (variant == 3 && Tp > 0 && conv_mode == 1 && nsplit <= 1 && !gsrc && l1_num == 0.f &&
-        l1_den == 0.f && l2 == 0.f)
-      return cnmf::launch_solve_pipe(K, p, nblocks, Tp, p.pl_n, stream);
+    const bool pipe = variant == 3 && Tp > 0 && conv_mode == 1 && nsplit <= 1 && !gsrc &&
+                      l1_num == 0.f && l1_den == 0.f && l2 == 0.f;
+    if (pipe) {
+      const int rpl = reps_per_launch > 0 ? reps_per_launch : nblocks;
+      for (int r0 = 0; r0 < nblocks; r0 += rpl) {
+        p.rep0 = r0;
+        const hipError_t e = cnmf::launch_solve_pipe(K, p, nblocks - r0 < rpl ? nblocks - r0 : rpl,
+                                                     Tp, p.pl_n, stream);
+        if (e != hipSuccess) return e;
+      }
+      return hipSuccess;
+    }
+    if (reps_per_launch > 0 && reps_per_launch < nblocks) return hipErrorInvalidValue;
+    if (per > cnmf_solve_mfma_max_cols(K)) return hipErrorInvalidValue;
     // the fused operands exist only in the pipelined kernel: never drop them silently
     if (fused || (!gram && !gsrc)) return hipErrorInvalidValue;
     return cnmf::launch_solve_mfma(K, p, nblocks, T < 1 ? 1 : T, stream);

@@ -11,7 +11,8 @@ struct SolveParams {
   long long n_rs, ldn;
   const float* gram;        // K x K per replicate
   long long g_rs;
-  const int* rep_index;     // blockIdx.x -> replicate (nullptr = identity)
+  const int* rep_index;     // rep0 + blockIdx.x -> replicate (nullptr = identity)
+  int rep0;                 // first replicate slot of this launch (co-resident rounds)
   int ncols, max_iter;
   float tol, l1_num, l1_den, l2, eps;
   float* lin_out;           // optional <numer, x>
@@ -67,6 +68,11 @@ struct SolveParams {
   // granules (tags in [2^31, 2^32 - 1); host tags stay below 2^31).
   unsigned* coop_gen_dev;
   unsigned* coop_arrive;
+  // Device-side ragged batching (solve_pipe.h only; conv.hip conv_slots): the numerator of
+  // replicate rep is the `numer` row nslot[rep] on (K rows of stride ldn from there), its
+  // planes go to row plslot[rep] of `planes` -- compact slots of the live replicates.
+  const int* nslot;
+  const int* plslot;
   // Optional (matrix-core kernel only): the system matrix is the Gram F F^T of the factor
   // F_r = gsrc + r*gs_rs (K x gs_cols, row stride gs_ld), formed in the prologue on the
   // matrix cores instead of being read from `gram` (W W^T fused into

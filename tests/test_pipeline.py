@@ -394,3 +394,19 @@ def test_gpu_rank_limit_is_a_clear_prepare_error(monkeypatch, tmp_path):
     api.check_gpu_ranks([80], "frobenius", "bpp", use_gpu=True)     # torch linalg: any K
     api.check_gpu_ranks([80], "frobenius", "mu", use_gpu=False)     # CPU: any K
     api.check_gpu_ranks([64], "frobenius", "mu", use_gpu=True)
+
+
+def test_prediction_error_caches_x_sq_per_tensor():
+    """The ||X||^2 cache of a resident dense X is keyed by tensor identity: a second
+    lookup with the same tensor must not compare tensors (api._XSQ)."""
+    import torch
+
+    from cnmf_torch_amd.api import _XSQ
+    rng = np.random.default_rng(0)
+    X = torch.as_tensor(rng.random((50, 20)), dtype=torch.float32)
+    U, S = rng.random((50, 3)), rng.random((3, 20))
+    want = float(((X.double().numpy() - U @ S) ** 2).sum())
+    for _ in range(2):
+        got = cNMF._prediction_error(X, U, S, torch.device("cpu"))
+        assert abs(got - want) <= 1e-9 * want
+    assert X in _XSQ

@@ -76,3 +76,21 @@ def test_streamed_norm_counts_equal_get_norm_counts(tmp_path):
     pd.testing.assert_frame_equal(got.obs, ref.obs, check_dtype=False, check_categorical=False)
     np.testing.assert_array_equal(got.obsm["X_pca"], ad.obsm["X_pca"])
     assert got.uns["note"] == "kept"
+
+
+def test_k_selection_with_dense_device_counts_over_several_ks(tmp_path):
+    """Dense normalised counts stay device-resident across the Ks of k_selection_plot:
+    the cached ||X||^2 (api._XSQ) is looked up by tensor identity for the second K on
+    (a WeakKeyDictionary compared tensor keys with Tensor.__eq__ and raised there)."""
+    X, cells, genes = simulate_counts(1200, 400, 5, seed=8, sparse=False)
+    fn = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(X, index=cells, columns=genes), fn)
+    obj = cNMF(output_dir=str(tmp_path), name="dk")
+    obj.prepare(fn, components=[4, 5, 6], n_iter=8, seed=3, num_highvar_genes=300,
+                densify=True, use_gpu=True, batch_size=400)
+    obj.factorize(worker_i=0, total_workers=1, verbose=False)
+    obj.combine()
+    obj.k_selection_plot(close_fig=True)
+    stats = load_df_from_npz(obj.paths["k_selection_stats"])
+    assert list(stats["k"]) == [4, 5, 6]
+    assert np.all(np.isfinite(stats["prediction_error"].values))

@@ -1,0 +1,300 @@
+"""The pipelined matrix-core MU solve at 17 <= K <= 64 (csrc/kernels/solve_pipe.h: MB =
+K/16 output blocks of permuted Gram rows, register-resident iterate, co-resident launch
+rounds) and the fused online step / per-layout graphs that run on it, against the fp64
+reference solve, the VALU kernel, and the unfused / eager paths."""
+import numpy as np
+import pytest
+import torch
+
+from cnmf_torch_amd import ops
+from cnmf_torch_amd.ops import reference
+
+pytestmark = pytest.mark.gpu
+
+WIDE_K = [17, 20, 24, 32, 40, 48, 64]
+
+
+def _problem(R, K, n, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    W = torch.rand((R, K, 96), generator=g, dtype=torch.float64) + 0.05
+    gram = torch.bmm(W, W.transpose(1, 2))
+    x_true = torch.rand((R, K, n), generator=g, dtype=torch.float64)
+    numer = torch.bmm(gram, x_true) * (1 + 0.05 * torch.rand((R, K, n), generator=g,
+                                                             dtype=torch.float64))
+    x0 = torch.rand((R, K, n), generator=g, dtype=torch.float64) + 0.1
+    return x0.float(), numer.float(), gram.float()
+
+
+@pytest.mark.parametrize("K", WIDE_K)
+def test_solve_pipe_wide_k_matches_reference(K):
+    """Fixed steps == the fp64 reference (and the VALU kernel) in x, lin, quad and the
+    iteration count; converged cooperative solves agree with the VALU kernel's."""
+    R, n = 5, 2600
+    x0, numer, gram = _problem(R, K, n, seed=300 + K)
+    dev = torch.device("cuda")
+    numer_d, gram_d = numer.to(dev), gram.to(dev)
+    assert ops.pipe_slices(n, R, K, dev) is not None
+    outs = {}
+    for variant in ("auto", "stream"):
+        xg = x0.clone().to(dev)
+        lin = torch.zeros(R, device=dev)
+        quad = torch.zeros(R, device=dev)
+        it = torch.zeros(R, dtype=torch.int32, device=dev)
+        ops.solve("mu", xg, numer_d, gram_d, max_iter=6, tol=-1.0, lin_out=lin, quad_out=quad,
+                  iters_out=it, conv_mode=1, check_every=4, variant=variant)
+        outs[variant] = (xg.cpu(), lin.cpu(), quad.cpu(), it.cpu())
+    xr = x0.clone().double()
+    lr = torch.zeros(R, dtype=torch.float64)
+    qr = torch.zeros(R, dtype=torch.float64)
+    reference.solve(0, xr, numer.double(), gram.double(), None, 6, -1.0, 0.0, 0.0, 0.0, 1e-16,
+                    lr, qr, None, 1, 1, 4)
+    xm, lm, qm, im = outs["auto"]
+    assert im.tolist() == [6] * R
+    torch.testing.assert_close(xm.double(), xr, rtol=3e-4, atol=1e-5)
+    torch.testing.assert_close(xm, outs["stream"][0], rtol=3e-4, atol=1e-5)
+    torch.testing.assert_close(lm.double(), lr, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(qm.double(), qr, rtol=1e-4, atol=1e-3)
+    res = {}
+    for variant in ("auto", "stream"):
+        xg = x0.clone().to(dev)
+        lin = torch.zeros(R, device=dev)
+        it = torch.zeros(R, dtype=torch.int32, device=dev)
+        ops.solve("mu", xg, numer_d, gram_d, max_iter=300, tol=1e-4, lin_out=lin,
+                  iters_out=it, conv_mode=1, check_every=5, variant=variant)
+        res[variant] = (xg.cpu(), lin.cpu(), it.cpu())
+    ops.coop_check(dev)
+    (xm, lm, im), (xs, ls, is_) = res["auto"], res["stream"]
+    assert (im - is_).abs().max() <= 5
+    assert ((xm - xs).norm() / xs.norm()) < 1e-2
+    torch.testing.assert_close(lm, ls, rtol=2e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("K", [20, 40, 64])
+def test_solve_pipe_launch_rounds_bitwise_one_launch(monkeypatch, K):
+    """With a small co-residency budget the replicates run in several launch rounds
+    (reps_per_launch): same slices, so bit-identical to one launch; an inactive
+    replicate and rep_index are honoured across rounds."""
+    R, n = 7, 3000
+    x0, numer, gram = _problem(R, K, n, seed=400 + K)
+    dev = torch.device("cuda")
+    numer_d, gram_d = numer.to(dev), gram.to(dev)
+    active = torch.tensor([1, 1, 0, 1, 1, 1, 1], dtype=torch.int32, device=dev)
+    ri = torch.tensor([0, 1, 2, 4, 5, 6], dtype=torch.int32, device=dev)
+    S = 12
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    full = ops._coop_resident(dev)
+    out = []
+    for resident in (full, 2 * S // ops._hip.solve_pipe_wg_per_cu(K)):
+        monkeypatch.setitem(ops._COOP_RESIDENT, key, resident)
+        plan = ops._pipe_plan(n, ri.numel(), K, S, dev)
+        assert plan is not None and plan[0] == S
+        if resident != full:
+            assert 0 < plan[1] < ri.numel()      # several rounds
+        xg = x0.clone().to(dev)
+        lin = torch.zeros(R, device=dev)
+        quad = torch.zeros(R, device=dev)
+        it = torch.zeros(R, dtype=torch.int32, device=dev)
+        got = ops.solve("mu", xg, numer_d, gram_d, rep_index=ri, max_iter=200, tol=1e-4,
+                        lin_out=lin, quad_out=quad, iters_out=it, conv_mode=1, check_every=4,
+                        active=active, coop=S)
+        assert got == S
+        out.append((xg.cpu(), lin.cpu(), quad.cpu(), it.cpu()))
+    ops.coop_check(dev)
+    for a, b in zip(out[0], out[1]):
+        assert torch.equal(a, b)
+    xg, _, _, it = out[0]
+    assert torch.equal(xg[2], x0[2]) and torch.equal(xg[3], x0[3])
+    assert it[2].item() == 0 and it[3].item() == 0 and (it[[0, 1, 4, 5, 6]] > 0).all()
+
+
+@pytest.mark.parametrize("K", [20, 40])
+@pytest.mark.parametrize("coop_gen", [False, True])
+def test_solve_pipe_fused_operands_bitwise_wide(K, coop_gen):
+    """Fused operands at K > 16 (MB > 1 Gram blocks): raw slabs + scale + base, partial
+    Grams + base reproduce the explicitly reduced operands bit for bit; numer_out /
+    gram_out get those sums; the per-slice partial Grams (MB x MB 16 x 16 blocks each)
+    sum to x x^T."""
+    R, n, ns, npart = 5, 3000, 3, 7
+    x0, numer, gram = _problem(R, K, n, seed=77 + K)
+    g = torch.Generator().manual_seed(5)
+    dev = torch.device("cuda")
+    slabs = (torch.rand((ns, R, K, n), generator=g) * numer.unsqueeze(0) / ns).to(dev)
+    scale = (torch.rand(n, generator=g) + 0.5).to(dev)
+    base = (torch.rand((R, K, n), generator=g) * numer.mean()).to(dev)
+    parts = (torch.rand((R, npart, K, K), generator=g) * gram.unsqueeze(1) / npart).to(dev)
+    gbase = (gram * 0.1).to(dev)
+    nref = slabs[0].clone()
+    for q in range(1, ns):
+        nref = nref + slabs[q]
+    nref = base + nref * scale
+    t = parts[:, 0].clone()
+    for q in range(1, npart):
+        t = t + parts[:, q]
+    gref = gbase + t
+    kw = dict(max_iter=300, tol=1e-4, conv_mode=1, check_every=5)
+    x1 = x0.clone().to(dev)
+    S1 = ops.solve("mu", x1, nref, gref, **kw)
+    x2 = x0.clone().to(dev)
+    nout = torch.zeros_like(nref)
+    gout = torch.zeros_like(gref)
+    gp_out = torch.full((R, 32, K, K), float("nan"), device=dev)
+    flat = slabs.reshape(-1)
+    S2 = ops.solve("mu", x2, flat[:R * K * n].view(R, K, n), gbase, numer_slabs=ns,
+                   numer_slab_stride=R * K * n, numer_scale=scale, numer_base=base,
+                   numer_out=nout, gram_parts=parts, gram_parts_n=npart, gram_out=gout,
+                   gram_parts_out=gp_out, coop_device_gen=coop_gen, **kw)
+    ops.coop_check(dev)
+    assert S1 == S2 and S2 > 1
+    assert torch.equal(x1, x2)
+    assert torch.equal(nout, nref) and torch.equal(gout, gref)
+    full = torch.bmm(x2.double(), x2.double().transpose(1, 2))
+    got = gp_out[:, :S2].double().sum(dim=1)
+    torch.testing.assert_close(got, full, rtol=1e-5, atol=1e-6)
+    # every slice's partial is itself symmetric, bit for bit
+    p = gp_out[:, :S2]
+    assert torch.equal(p, p.transpose(2, 3))
+    assert torch.isnan(gp_out[:, S2:]).all()
+
+
+@pytest.mark.parametrize("ks", [[20], [17, 24, 32], [48]])
+def test_fused_online_step_matches_unfused_wide(monkeypatch, ks):
+    """The fused online step at K > 16 (the cNMF-typical ranks; K = 48 padded from 41)
+    factorises like the unfused step: pass counts +-1, errors to 1e-5, spectra to fp32
+    rounding of a converged iteration."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions, _Batch, native_rank
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(6000, 700, n_programs=12, seed=5)).cuda()
+    ks = [41 if k == 48 else k for k in ks]
+    seeds = list(range(101, 101 + 10 * len(ks)))
+    kk = [k for k in ks for _ in range(10)]
+    opts = dict(n_components=ks[0], online_chunk_size=2000, online_chunk_max_iter=1000)
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CNMF_FUSED_STEP", fused)
+        solver = NMFBatchSolver(X, NMFOptions(**opts))
+        if fused == "1":
+            kp = sorted(native_rank(k) for k in kk)
+            st = _Batch(torch.zeros((sum(kp), 6000), device="cuda"),
+                        torch.zeros((sum(kp), 700), device="cuda"), kp)
+            assert solver._fused_ok(st, solver._steps(6000))
+        out[fused] = solver.run(seeds, ks=kk)
+    a, b = out["1"], out["0"]
+    assert np.abs(a.n_iter - b.n_iter).max() <= 1
+    same = a.n_iter == b.n_iter
+    assert same.mean() > 0.8
+    np.testing.assert_allclose(a.err[same], b.err[same], rtol=1e-5)
+    for r in np.flatnonzero(same):
+        wa, wb = a.spectra(r).cpu(), b.spectra(r).cpu()
+        assert float((wa - wb).norm() / wb.norm()) < 1e-3
+
+
+@pytest.mark.parametrize("K", [20, 33])
+def test_fused_graph_replay_wide_k_bitwise_eager(monkeypatch, K):
+    """Per-layout HIP-graph replays of the fused passes at K > 16 (K = 33 runs padded to
+    40 inside a graph arena) equal the eager passes bit for bit, run after run."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(5000, 600, n_programs=10, seed=8)).cuda()
+    opts = NMFOptions(n_components=K, online_chunk_size=2000, online_chunk_max_iter=1000)
+    batches = [list(range(1 + 24 * i, 25 + 24 * i)) for i in range(3)]
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("CNMF_GRAPHS", mode)
+        solver = NMFBatchSolver(X, opts)
+        res[mode] = [solver.run(b) for b in batches]
+        if mode == "1":
+            arenas = list(solver._arenas.values())
+            assert len(arenas) == 1
+            slots = arenas[0]["slots"]
+            assert any(sl["graph"] is not None for sl in slots.values())
+            assert not any(sl["failed"] for sl in slots.values())
+    for a, b in zip(res["1"], res["0"]):
+        np.testing.assert_array_equal(a.n_iter, b.n_iter)
+        np.testing.assert_array_equal(a.err, b.err)
+        assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
+        assert a.W.shape[0] == 24 * K
+
+
+@pytest.mark.parametrize("ks", [[10], [5, 7, 13], [20]])
+def test_device_slots_bitwise_equal_uncompacted(monkeypatch, ks):
+    """Device-side ragged batching (conv_update slots; GEMMs skip dead M-tiles, solves
+    read / write at compact rows) changes where rows live, not what is computed: the
+    factorisation is bit-identical to the same fused run without slots and without host
+    compaction -- and within fp32 rounding of the host-compacted run."""
+    from cnmf_torch_amd.models import nmf
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(6000, 700, n_programs=10, seed=6)).cuda()
+    kk = [k for k in ks for _ in range(14)]
+    seeds = list(range(7, 7 + len(kk)))
+    opts = nmf.NMFOptions(n_components=ks[0], online_chunk_size=2000,
+                          online_chunk_max_iter=1000)
+    out = {}
+    for mode in ("slots", "plain", "compact"):
+        monkeypatch.setattr(nmf, "_DEV_SLOTS", mode == "slots")
+        frac = "2.0" if mode == "plain" else "0.25"
+        monkeypatch.setenv("CNMF_COMPACT_FRAC", frac)
+        monkeypatch.setenv("CNMF_COMPACT_FRAC_SMALL", frac)
+        out[mode] = nmf.NMFBatchSolver(X, opts).run(seeds, ks=kk)
+    a, b, c = out["slots"], out["plain"], out["compact"]
+    assert len(set(a.n_iter.tolist())) > 1          # replicates finished at different passes
+    np.testing.assert_array_equal(a.n_iter, b.n_iter)
+    np.testing.assert_array_equal(a.err, b.err)
+    assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
+    assert np.abs(a.n_iter - c.n_iter).max() <= 1
+    same = a.n_iter == c.n_iter
+    np.testing.assert_allclose(a.err[same], c.err[same], rtol=1e-5)
+
+
+def test_conv_update_slots_match_prefix_sums():
+    """conv_update's compact slots: exclusive prefix sums of the ranks of the replicates
+    still active (batch order), the previous slots / live count moved to prev / live[0]."""
+    dev = torch.device("cuda")
+    n = 700
+    g = torch.Generator().manual_seed(3)
+    kv = torch.randint(1, 33, (n,), generator=g, dtype=torch.int32)
+    st = {k: torch.zeros(n, dtype=torch.float64, device=dev) for k in ("err_init", "err_prev", "err")}
+    st.update({k: torch.zeros(n, dtype=torch.int32, device=dev) for k in ("active", "converged", "n_pass")})
+    sl = {"kvec": kv.to(dev), "cur": torch.zeros(n, dtype=torch.int32, device=dev),
+          "prev": torch.zeros(n, dtype=torch.int32, device=dev),
+          "live": torch.zeros(2, dtype=torch.int32, device=dev)}
+    lin = torch.rand(n, generator=g).to(dev)
+    quad = torch.rand(n, generator=g).to(dev)
+    ops.conv_update(lin, quad, 10.0, st, n, -1, 1e-4, final=False, init=True, slots=sl)
+    full = (torch.cumsum(kv, 0) - kv).to(torch.int32)
+    assert torch.equal(sl["cur"].cpu(), full) and torch.equal(sl["prev"].cpu(), full)
+    assert sl["live"].tolist() == [int(kv.sum())] * 2
+    # half the replicates stop improving (error unchanged): they deactivate
+    lin2 = lin.clone()
+    keep = torch.rand(n, generator=g) < 0.5
+    lin2[keep.to(dev)] += 0.3
+    ops.conv_update(lin2, quad, 10.0, st, n, -1, 1e-4, final=False, slots=sl)
+    act = st["active"].cpu() != 0
+    assert torch.equal(act, keep)
+    k = kv * act.to(torch.int32)
+    want = (torch.cumsum(k, 0) - k).to(torch.int32)
+    assert torch.equal(sl["cur"].cpu()[act], want[act])
+    assert torch.equal(sl["prev"].cpu(), full)
+    assert sl["live"].tolist() == [int(kv.sum()), int(k.sum())]
+
+
+def test_gemm_planes_live_rows_skip_dead_tiles():
+    """gemm_planes(live=...): rows below the live count equal the full product; M-tiles
+    that start at or past it are skipped (their output rows keep their old contents)."""
+    M, N, K = 1000, 640, 2048
+    g = torch.Generator().manual_seed(11)
+    A = torch.rand((M, K), generator=g)
+    B = torch.randint(0, 100, (N, K), generator=g).float()
+    Ap = torch.zeros((3, M, K), dtype=torch.int16, device="cuda")
+    Bp = torch.zeros((1, N, K), dtype=torch.int16, device="cuda")
+    ops.split_planes(A.cuda(), Ap)
+    ops.split_planes(B.cuda(), Bp)
+    full = torch.empty((M, N), device="cuda")
+    ops.gemm_planes(full, Ap[:2], Bp, M, N, K)
+    live = torch.tensor([333], dtype=torch.int32, device="cuda")
+    C = torch.full((M, N), float("nan"), device="cuda")
+    ops.gemm_planes(C, Ap[:2], Bp, M, N, K, live=live)
+    assert torch.equal(C[:333], full[:333])
+    assert torch.isnan(C[512:]).all()
