@@ -83,6 +83,11 @@ def main() -> int:
                          "sparse-input runs (KL switches to the CSR kernels at <= 0.15)")
     ap.add_argument("--streams", type=int, default=1,
                     help="replicate groups solved concurrently on separate HIP streams")
+    ap.add_argument("--emulate-world", type=int, default=None,
+                    help="dp mode on ONE process: run rank 0's cell shard of an N-rank job "
+                         "with every collective replaced by a device copy of its bytes "
+                         "(parallel.comm.EmulatedComm) -- the per-rank step time of the "
+                         "N-GPU DP job, collectives excluded; value = projected job rate")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -125,12 +130,19 @@ def main() -> int:
     if args.density is not None:
         X[X < np.quantile(X, 1.0 - args.density)] = 0.0
     comm = row_map = schedule = None
-    if args.mode == "dp" and world > 1:
-        segs = dp_row_segments(X.shape[0], args.batch_size, rank, world)
+    emu = args.emulate_world if (args.mode == "dp" and world == 1 and args.emulate_world
+                                 and args.emulate_world > 1) else None
+    if args.mode == "dp" and (world > 1 or emu):
+        segs = dp_row_segments(X.shape[0], args.batch_size, rank, emu or world)
         X = np.concatenate([X[a:b] for a, b in segs])
         row_map, schedule = dp_layout(segs)
-        os.environ["CNMF_ALLREDUCE"] = args.allreduce
-        comm = DistComm()
+        if emu:
+            from cnmf_torch_amd.parallel.comm import EmulatedComm
+
+            comm = EmulatedComm(emu)
+        else:
+            os.environ["CNMF_ALLREDUCE"] = args.allreduce
+            comm = DistComm()
     Xd = torch.from_numpy(X).to(dev)
     opts = NMFOptions(n_components=args.k, init="random", beta_loss=args.beta_loss,
                       algo=args.algo, mode=args.nmf_mode, tol=1e-4,
@@ -238,9 +250,11 @@ def main() -> int:
             if len(grid) > 1 else f"NMF replicates/sec (K={args.k}, n_iter={args.n_iter})"
         par = {"weak": f"replicate-parallel x{world}",
                "strong": f"replicate-parallel x{world} (fixed {n_total}-replicate ledger)",
-               "dp": f"cell-sharded DP x{world} ("
-                     f"{'one-shot xGMI' if args.allreduce == 'xgmi' else 'RCCL'} all-reduce "
-                     "per online step)"}[args.mode]
+               "dp": f"cell-sharded DP x{emu or world} ("
+                     + ("emulated: rank 0's shard on one GPU, collectives replaced by device "
+                        "copies" if emu else
+                        f"{'one-shot xGMI' if args.allreduce == 'xgmi' else 'RCCL'} "
+                        "reduce-scatter / all-gather per online step") + ")"}[args.mode]
         out = {
             "metric": metric,
             "value": round(reps_per_sec, 3),
@@ -278,8 +292,14 @@ def main() -> int:
                 "strong_global_batch": per_batch if strong_value is not None else None,
             },
         }
+        if emu:
+            out["config"]["emulated_world"] = emu
+            out["config"]["collective_bytes_per_step_per_rank"] = int(comm.bytes / nsteps)
+            out["config"]["projection"] = ("value = replicates/s of the emulated-world DP job "
+                                           "from rank 0's per-step compute time; collective "
+                                           "time not included (payload above)")
         print(json.dumps(out), flush=True)
-    if comm is not None:
+    if comm is not None and hasattr(comm, "close"):
         comm.close()
     if world > 1:
         dist.destroy_process_group()

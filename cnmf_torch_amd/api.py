@@ -123,18 +123,23 @@ def gpu_max_rank(beta_loss="frobenius", algo="mu") -> int | None:
     return 128 if algo == "mu" else 64
 
 
-def check_gpu_ranks(components, beta_loss="frobenius", algo="mu", use_gpu=True) -> None:
-    """Fail at once -- at ``prepare``, before any work -- for a rank the GPU kernels do not
-    cover (the reference's ``-k`` is unbounded, cnmf.py:1417; the CPU path takes any K)."""
+def check_gpu_ranks(components, beta_loss="frobenius", algo="mu", use_gpu=True) -> list:
+    """Say at once -- at ``prepare``, before any work -- which ranks the native GPU kernels
+    do not cover (the reference's ``-k`` is unbounded, cnmf.py:1417).  Those replicates
+    are routed to the eager PyTorch ops on the same GPU (NMFBatchSolver.run, ops.eager_ops)
+    instead of failing the job.  Returns the uncovered ranks."""
     if not use_gpu or not torch.cuda.is_available():
-        return
-    ks = [int(k) for k in np.atleast_1d(components)]
+        return []
+    ks = sorted({int(k) for k in np.atleast_1d(components)})
     kmax = gpu_max_rank(beta_loss, algo)
-    if kmax is not None and ks and max(ks) > kmax:
-        raise ValueError(
-            f"K={max(ks)}: on the GPU this engine factorises K <= {kmax} "
-            f"(beta_loss={beta_loss!r}, algo={algo!r}); run without --use_gpu (the CPU "
-            f"path takes any K) or choose components <= {kmax}")
+    over = [k for k in ks if kmax is not None and k > kmax]
+    if over:
+        msg = (f"K={over}: the native gfx950 kernels factorise K <= {kmax} "
+               f"(beta_loss={beta_loss!r}, algo={algo!r}); these ranks run the eager "
+               "PyTorch ops on the GPU (slower)")
+        warnings.warn(msg, RuntimeWarning, stacklevel=2)
+        log.warning(msg)
+    return over
 
 
 def _device(use_gpu: bool, device=None) -> torch.device:
@@ -258,6 +263,12 @@ _COOP_LOCK = threading.RLock()
 # ||X||^2 of a device-resident X (api._prediction_error), weakly keyed by the tensor's
 # identity (a WeakKeyDictionary compares tensor keys with Tensor.__eq__, which raises)
 _XSQ = WeakIdKeyDictionary()
+
+
+def sops_predict(X, U, S):
+    from . import ops as _ops
+
+    return _ops.predict_err_terms(X, U, S)
 
 
 def _load_npz_arrays(fn: str):
@@ -1223,6 +1234,11 @@ class cNMF:
             d = X.data.to(torch.float64)
             UtX = sops.tspmm(X, U).t().to(torch.float64)              # (K, G)
             return float((d * d).sum()) - 2.0 * float((UtX * S).sum()) + quad
+        if isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.float32 \
+                and U.shape[1] <= 128:
+            # one fused pass over the resident X (H8 kernel): <X, U S> and ||X||^2
+            cross, x_sq = sops_predict(X, U, S)
+            return x_sq - 2.0 * cross + quad
         if isinstance(X, torch.Tensor):
             # ||X||^2 is the same for every K of a k-selection: computed once per tensor
             x_sq = _XSQ.get(X)

@@ -58,6 +58,9 @@ from .. import ops
 from .bpp import nnls_bpp, objective_terms as bpp_objective_terms
 from ..parallel.comm import LocalComm
 from ..utils import rng
+from ..utils.log import get_logger
+
+log = get_logger("cnmf_torch_amd.nmf")
 
 BETA_LOSS = {"frobenius": 2.0, "kullback-leibler": 1.0, "itakura-saito": 0.0}
 
@@ -950,6 +953,18 @@ class PlanesOnlyX:
         self.planes = _XPlanes(src, stats=(mn, sq, neg))
 
 
+def kernel_max_rank(beta: float, algo: str) -> int | None:
+    """Largest K the native kernels factorise (None: no limit -- 'bpp' solves its NNLS
+    blocks with torch linear algebra): Frobenius MU 128 (padded, native_rank), HALS /
+    halsvar 64, the beta-divergence kernels 32.  Larger ranks are routed to the eager
+    PyTorch ops on the same GPU (NMFBatchSolver.run, logged)."""
+    if algo == "bpp":
+        return None
+    if beta != 2.0:
+        return 32
+    return 128 if algo == "mu" else 64
+
+
 def native_rank(K: int) -> int:
     """The rank the GPU kernels run a rank-K replicate at: K itself for K <= 32, else K
     padded with zero components to a multiple of 8 (<= 64) or of 16 (<= 128, MU only: the
@@ -1083,14 +1098,27 @@ class NMFBatchSolver:
             raise ValueError(f"{R} seeds but {ks.size} ranks")
         if R and ks.min() < 1:
             raise ValueError("every K must be >= 1")
-        if self.beta != 2.0 and np.unique(ks).size > 1:
+        kmax = kernel_max_rank(self.beta, o.algo)
+        uncovered = (self.X.device.type == "cuda" and not ops.eager_active() and R
+                     and kmax is not None and int(ks.max()) > kmax)
+        if (self.beta != 2.0 or uncovered) and np.unique(ks).size > 1:
             if on_retire is not None:
-                raise ValueError("on_retire needs a single K for beta != 2")
+                raise ValueError("on_retire needs a single K for beta != 2 or K > "
+                                 f"{kmax}")
             return self._run_split_by_k(seeds, ks)
+        if uncovered:
+            # no kernel instantiation for this rank: run the PyTorch reference ops on the
+            # same GPU instead of failing the job (logged once per K)
+            _warn_once(f"K={int(ks[0])}: the native gfx950 kernels cover K <= {kmax} for "
+                       f"beta_loss={self.opts.beta_loss!r}, algo={o.algo!r}; these "
+                       "replicates run the eager PyTorch ops on the GPU (slower)")
+            log.info("K=%d > %d: eager PyTorch routing on %s", int(ks[0]), kmax, self.X.device)
+            with ops.eager_ops():
+                return self.run(seeds, HT0=HT0, W0=W0, ks=ks, on_retire=None)
         t0 = time.perf_counter()
         # wide ranks run padded on the GPU kernels (native_rank); bpp solves on torch linalg
         pad = self.X.device.type == "cuda" and o.algo != "bpp" and self.beta == 2.0 \
-            and bool((ks > 32).any())
+            and bool((ks > 32).any()) and not ops.eager_active()
         kp = np.array([native_rank(k) for k in ks], dtype=np.int64) if pad else ks
         pos = np.lexsort((np.arange(R), kp, ks))     # positions grouped by K
         kpos = kp[pos]
@@ -1527,12 +1555,26 @@ class NMFBatchSolver:
         single process (the DP path all-reduces the statistics), K <= 64 and solves whose
         cooperative slices fit the pipelined kernel.  CNMF_FUSED_STEP=0 disables it."""
         o = self.opts
+        if self.comm.is_distributed:
+            # cell-sharded DP: every rank must take the same path (collective sequence)
+            ok = self._fused_ok_local(st, steps, dp=True)
+            return self.comm.allreduce_max_int(0 if ok else 1) == 0
+        return self._fused_ok_local(st, steps, dp=False)
+
+    def _fused_ok_local(self, st: _Batch, steps, dp: bool) -> bool:
+        o = self.opts
         if (self.X.device.type != "cuda" or os.environ.get("CNMF_FUSED_STEP", "1") == "0"
                 or ops._ENV["CNMF_SOLVE_PIPE"] == "0" or o.algo != "mu"
                 or o.online_stats != "pass" or o.online_inner_conv != "loss"
-                or self.comm.is_distributed or any(v != 0.0 for v in (o.l1_H, o.l2_H, o.l1_W, o.l2_W))
+                or any(v != 0.0 for v in (o.l1_H, o.l2_H, o.l1_W, o.l2_W))
                 or self._planes() is None):
             return False
+        if dp:
+            # the reduce-scattered W-solve partitions the replicates of ONE rank group
+            # (mixed-K DP batches take the unfused, all-reduced step)
+            if (len(st.groups) != 1 or os.environ.get("CNMF_DP_FUSED", "1") == "0"
+                    or not hasattr(self.comm, "reduce_scatter_")):
+                return False
         G = self.X.shape[1]
         for blocks in steps:
             if len(blocks) != 1 or blocks[0][0] % 8 or blocks[0][1] <= blocks[0][0]:
@@ -1626,6 +1668,163 @@ class NMFBatchSolver:
             ops.split_planes(W, fb["wpl"], col_mul=xp.unit)
             fb["wpl_key"] = wkey
         return wkey
+
+    # ------------------------------------------------------------------ DP fused step
+    def _fused_bufs_dp(self, st: _Batch, steps) -> dict:
+        """Workspaces of the cell-sharded fused step (_fused_pass_dp).  The replicates are
+        partitioned into ``world`` equal position chunks of Rr (the last rank's chunk may
+        hold fewer real ones); every exchanged buffer is padded to world * Rr positions so
+        each rank's chunk is one contiguous block for reduce-scatter / all-gather."""
+        comm = self.comm
+        xp = self._planes()
+        dev = self.X.device
+        G = self.X.shape[1]
+        (g,) = st.groups
+        K, R, world, me = g.K, g.n, comm.world_size, comm.rank
+        Rr = -(-R // world)
+        Rp = Rr * world
+        own0, own1 = min(R, me * Rr), min(R, (me + 1) * Rr)
+        cws = [b - a for (a, b), in steps]
+        bk = ops.planes_bk(xp.pb)
+        kd_max = max(-(-cw // bk) * bk for cw in cws)
+        ks_n = max(ops.gemm_plan(R * K, cw, xp.Gp, xp.pb)[1] for cw in cws)
+        # cooperative slice counts every rank uses (the partial-Gram exchange needs the
+        # same number of slots everywhere): from the widest step of ANY rank, and from
+        # the full chunk Rr for the W-solve
+        cw_max = comm.allreduce_max_int(max(cws))
+        S_h = ops.pipe_slices(cw_max, R, K, dev)
+        S_w = ops.pipe_slices(G, Rr, K, dev)
+        S_h = comm.allreduce_max_int(S_h or 0)
+        S_w = comm.allreduce_max_int(S_w or 0)
+        if not S_h or not S_w:
+            raise RuntimeError("DP fused step: no pipelined-solve slicing")
+        f32 = dict(device=dev, dtype=torch.float32)
+        fb = {
+            "K": K, "R": R, "Rr": Rr, "Rp": Rp, "own": (own0, own1), "S_h": S_h, "S_w": S_w,
+            "wpl": torch.zeros((3, Rp * K, xp.Gp), device=dev, dtype=torch.int16),
+            "hpl": torch.zeros((3, R * K, kd_max), device=dev, dtype=torch.int16),
+            "slabN": torch.empty(ks_n * R * K * max(cws), **f32),
+            "dB": torch.zeros((Rp * K, G), **f32),
+            "dB_own": torch.empty((Rr * K, G), **f32),
+            "B_own": torch.empty((Rr * K, G), **f32),
+            "A_own": [torch.empty((Rr, K, K), **f32) for _ in range(2)],
+            "HHp": torch.zeros((Rp, S_h, K, K), **f32),
+            "HHp_own": torch.empty((Rr, S_h, K, K), **f32),
+            "WWp": torch.zeros((Rp, S_w, K, K), **f32),
+            "lin": torch.zeros(Rp, **f32), "quad": torch.zeros(Rp, **f32),
+            "prepped": None,
+        }
+        return fb
+
+    def _fused_pass_dp(self, st: _Batch, steps, fb: dict, final: bool) -> None:
+        """One online pass of the fused step on a cell shard (SURVEY.md §2.5c / §2.6 item
+        1).  Per online step every rank runs the numerator GEMM and the pipelined H-solve
+        on its cells of the global chunk and the statistics GEMM dB = H_loc^T X_loc; then
+        ONE reduce-scatter per buffer hands each rank the rank-summed dB and per-slice
+        partial Grams of ITS replicate chunk, the rank W-solves only those (1/world of the
+        spectra work), and all-gathers return their bf16 spectra planes, the per-slice
+        W W^T partials and (last step) lin/quad -- the bytes of one all-reduce of dB, with
+        the W-solve no longer replicated on every rank (the unfused DP step all-reduces
+        [dB | dA] and re-solves every replicate everywhere).  Same updates and stopping
+        rules as the single-GPU fused step; rank-summed statistics in RCCL's order."""
+        o = self.opts
+        comm = self.comm
+        xp = self._planes()
+        X = self.X
+        G = X.shape[1]
+        HT, W = st.views()
+        (g,) = st.groups
+        K, R, Rr, Rp = fb["K"], fb["R"], fb["Rr"], fb["Rp"]
+        own0, own1 = fb["own"]
+        n_own = own1 - own0
+        S_h, S_w = fb["S_h"], fb["S_w"]
+        active = st.active_mask()
+        n = st.n_act
+        h_it, w_it = st.h_iters[:n], st.w_iters[:n]
+        bk = ops.planes_bk(xp.pb)
+        rows = R * K
+        wpl, hpl_all = fb["wpl"], fb["hpl"]
+        if fb["prepped"] != st.uid:
+            # W is replicated at the start of a run: every rank forms every Gram / plane
+            fb["WWp"].zero_()
+            fb["WWp"][:R, 0].copy_(ops.gram(g.rep3(W)))
+            ops.split_planes(W, wpl[:, :rows], col_mul=xp.unit)
+            fb["wwp_n"] = 1
+            fb["prepped"] = st.uid
+        unit = xp.unit
+        wpl_n = ops.gemm_a_planes(xp.Gp)
+        o0, o1 = own0 * K, own1 * K
+        Wown = W[o0:o1].view(n_own, K, G) if n_own else None
+        last_s = len(steps) - 1
+        for s_, ((a, b),) in enumerate(steps):
+            cw = b - a
+            last = s_ == last_s
+            ks_n = ops.gemm_planes(None, wpl[:wpl_n, :rows], xp.x[:, a:], rows, cw, xp.Gp,
+                                   raw_slab=fb["slabN"], raw_max=_FUSED_MAX_SLABS)
+            kd = -(-cw // bk) * bk
+            hpl = hpl_all[:, :, :kd]
+            hpl_n = ops.gemm_a_planes(kd)
+            if cw > 0:
+                numer = fb["slabN"].as_strided((R, K, cw), (K * cw, cw, 1), 0)
+                ops.solve("mu", g.rep3(HT[:, a:b]), numer, None,
+                          max_iter=o.online_chunk_max_iter, tol=o.online_h_tol, eps=o.eps,
+                          iters_out=h_it, conv_mode=1, check_every=o.inner_check_every,
+                          active=active, planes=hpl, planes_n=hpl_n, numer_slabs=ks_n,
+                          numer_slab_stride=rows * cw, coop=S_h,
+                          gram_parts=fb["WWp"][:R], gram_parts_n=fb["wwp_n"],
+                          gram_parts_out=fb["HHp"][:R], coop_device_gen=True)
+                ops.gemm_planes(fb["dB"], hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd)
+            else:      # no cells of this chunk here: zero contributions
+                fb["dB"][:rows].zero_()
+                fb["HHp"][:R].zero_()
+            comm.reduce_scatter_(fb["dB_own"], fb["dB"])
+            comm.reduce_scatter_(fb["HHp_own"], fb["HHp"])
+            A_in, A_out = fb["A_own"][(s_ + 1) % 2], fb["A_own"][s_ % 2]
+            wwp = fb["WWp"][comm.rank * Rr:(comm.rank + 1) * Rr]
+            if n_own:
+                lin_o = fb["lin"][comm.rank * Rr:comm.rank * Rr + n_own]
+                quad_o = fb["quad"][comm.rank * Rr:comm.rank * Rr + n_own]
+                ops.solve(
+                    "mu", Wown, fb["dB_own"][:n_own * K].view(n_own, K, G),
+                    None if s_ == 0 else A_in[:n_own], max_iter=o.online_chunk_max_iter,
+                    tol=o.online_w_tol, eps=o.eps, lin_out=lin_o if last else None,
+                    quad_out=quad_o if last else None, iters_out=w_it[own0:own1],
+                    conv_mode=1, check_every=o.inner_check_every, active=active[own0:own1],
+                    planes=wpl[:, o0:o1], planes_colmul=unit, planes_n=wpl_n,
+                    numer_scale=unit,
+                    numer_base=None if s_ == 0 else fb["B_own"][:n_own * K].view(n_own, K, G),
+                    numer_out=None if last else fb["B_own"][:n_own * K].view(n_own, K, G),
+                    gram_parts=fb["HHp_own"][:n_own], gram_parts_n=S_h,
+                    gram_out=None if last else A_out[:n_own],
+                    gram_parts_out=wwp[:n_own], coop=S_w, coop_device_gen=True)
+            fb["wwp_n"] = S_w
+            comm.all_gather_into_(fb["WWp"], wwp)
+            for pl in range(wpl_n):
+                comm.all_gather_into_(wpl[pl], wpl[pl, comm.rank * Rr * K:(comm.rank + 1) * Rr * K])
+            if last:
+                comm.all_gather_into_(fb["lin"], fb["lin"][comm.rank * Rr:(comm.rank + 1) * Rr])
+                comm.all_gather_into_(fb["quad"], fb["quad"][comm.rank * Rr:(comm.rank + 1) * Rr])
+        ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
+                        n, -1, o.tol, final=final, gate=st.gate)
+
+    def _dp_gather_w(self, st: _Batch, fb: dict) -> None:
+        """End of a DP fused run: every rank's W-solved spectra rows to every rank."""
+        _, W = st.views()
+        K, R, Rr, Rp = fb["K"], fb["R"], fb["Rr"], fb["Rp"]
+        G = W.shape[1]
+        me = self.comm.rank
+        Wp = torch.zeros((Rp * K, G), device=W.device, dtype=W.dtype)
+        o0, o1 = me * Rr * K, min(R, (me + 1) * Rr) * K
+        if o1 > o0:
+            Wp[o0:o1].copy_(W[o0:o1])
+        self.comm.all_gather_into_(Wp, Wp[me * Rr * K:(me + 1) * Rr * K])
+        W.copy_(Wp[:R * K])
+        it = torch.zeros(Rp, dtype=torch.int32, device=W.device)   # W-solve sweep counts
+        o0, o1 = me * Rr, min(R, (me + 1) * Rr)
+        if o1 > o0:
+            it[o0:o1].copy_(st.w_iters[o0:o1])
+        self.comm.all_gather_into_(it, it[me * Rr:(me + 1) * Rr])
+        st.w_iters[:R].copy_(it[:R])
 
     def _fused_pass(self, st: _Batch, steps, fb: dict, final: bool) -> None:
         """One online pass of the fused step (see _fused_ok); same updates, stopping rules
@@ -1736,10 +1935,13 @@ class NMFBatchSolver:
         graph, graph_key, last_key = None, None, None
         fused = self._fused_ok(st, steps)
         # (early replicate writes hand over retired replicates at host compactions)
-        st.dslots = self._dev_slots(st) if (fused and _DEV_SLOTS and st.on_retire is None) \
-            else None
-        # device slots: the batch keeps one layout (no host compaction, never fires at 2.0)
-        pipe = _PassPipeline(st, compact_frac=2.0 if st.dslots is not None else None)
+        st.dslots = self._dev_slots(st) if (fused and _DEV_SLOTS and st.on_retire is None
+                                            and not dist) else None
+        # device slots / DP fused: the batch keeps one layout (no host compaction: 2.0 never
+        # fires) -- the DP W-solve owns a fixed partition and only its rows of W are fresh
+        dp_fused = fused and dist
+        pipe = _PassPipeline(st, compact_frac=2.0 if (st.dslots is not None or dp_fused)
+                             else None)
         fb, fb_key, sl = None, None, None
         for p in range(max_pass):
             n = st.n_act
@@ -1753,12 +1955,19 @@ class NMFBatchSolver:
                     # run of the arena captured one (only the W-dependent operands are
                     # rebuilt eagerly), else it runs eagerly
                     sl = self._slot(st, steps) if st.graphs else None
-                    fb, fb_key = (sl["fb"] if sl is not None else self._fused_bufs(st, steps)), key
-                    if sl is not None and sl["graph"] is not None and not final and _LAYOUT_REPLAY:
+                    if dp_fused:
+                        fb, fb_key = self._fused_bufs_dp(st, steps), key
+                    else:
+                        fb, fb_key = (sl["fb"] if sl is not None else self._fused_bufs(st, steps)), key
+                    if dp_fused:
+                        self._fused_pass_dp(st, steps, fb, final=final)
+                    elif sl is not None and sl["graph"] is not None and not final and _LAYOUT_REPLAY:
                         self._fused_prep(st, fb, keep_slices=True)
                         sl["graph"].replay()
                     else:
                         self._fused_pass(st, steps, fb, final=final)
+                elif dp_fused:
+                    self._fused_pass_dp(st, steps, fb, final=final)
                 elif sl is None or final or not self._replay_slot(sl, st, steps):
                     self._fused_pass(st, steps, fb, final=final)
                 if not pipe.after_enqueue():
@@ -1914,6 +2123,8 @@ class NMFBatchSolver:
                 self.timings.setdefault("wait_pass", []).append((n, time.perf_counter() - t_w))
         if graph is not None:
             torch.cuda.current_stream().synchronize()
+        if fused and dist and fb is not None:
+            self._dp_gather_w(st, fb)
 
     # ------------------------------------------------------------------ batch frobenius
     def _batch_frob(self, st: _Batch) -> None:

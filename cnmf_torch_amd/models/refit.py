@@ -87,7 +87,15 @@ def chunked_solve(HT: torch.Tensor, numerT: torch.Tensor, gram: torch.Tensor, ch
     and leave the Gram products and the objective unchanged (models.nmf.native_rank)."""
     K, n = HT.shape
     if HT.device.type == "cuda" and algo != "bpp" and ops.use_native(HT):
-        from .nmf import native_rank
+        from .nmf import _warn_once, kernel_max_rank, native_rank
+
+        kmax = kernel_max_rank(2.0, algo)
+        if K > kmax:    # no kernel for this rank: the PyTorch ops on the same GPU, logged
+            _warn_once(f"refit K={K}: the native gfx950 solve covers K <= {kmax}; this "
+                       "refit runs the eager PyTorch ops on the GPU (slower)")
+            with ops.eager_ops():
+                return chunked_solve(HT, numerT, gram, chunk_size, chunk_max_iter, h_tol,
+                                     l1_num=l1_num, l2=l2, eps=eps, algo=algo)
 
         Kp = native_rank(K)
         if Kp != K:

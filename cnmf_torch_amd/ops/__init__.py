@@ -69,13 +69,35 @@ refresh_env()
 
 
 def use_native(t: torch.Tensor) -> bool:
-    """True when ``t`` lives on the GPU (the HIP path is then mandatory)."""
+    """True when ``t`` lives on the GPU (the HIP path is then mandatory) -- except inside
+    :func:`eager_ops`, the explicit, logged routing of ranks no kernel covers."""
     if t.device.type != "cuda":
         return False
     if _ENV["CNMF_FORCE_TORCH_OPS"] == "1":  # debugging aid only, never default
         return False
+    if getattr(_TLS, "eager", False):
+        return False
     _require_native()
     return True
+
+
+@contextlib.contextmanager
+def eager_ops():
+    """Within this context (per host thread) every op runs its PyTorch reference
+    (ops/reference.py) on the operands' own device.  This is the routing for factor ranks
+    the native kernels do not cover (K > 128 Frobenius MU, K > 64 HALS, K > 32 beta != 2;
+    the reference's -k is unbounded, cnmf.py:1417): the caller logs it per job
+    (models.nmf.NMFBatchSolver.run, models.refit).  Covered ranks never take it."""
+    prev = getattr(_TLS, "eager", False)
+    _TLS.eager = True
+    try:
+        yield
+    finally:
+        _TLS.eager = prev
+
+
+def eager_active() -> bool:
+    return bool(getattr(_TLS, "eager", False))
 
 
 # raw current-stream pointer without constructing a torch.cuda.Stream per op (700 per
@@ -459,6 +481,8 @@ def _mfma_split(n: int, nblocks: int, K: int, nsplit: int, coop, dev: torch.devi
                                     _coop_resident(dev)) else None
     if s_min > 1 and _ENV["CNMF_SOLVE_COOP"] == "0":
         return None
+    if _ENV["CNMF_SOLVE_COOP"] == "0":
+        return 1            # s_min == 1 here: one workgroup per replicate, no exchange
     budget = MFMA_WG_PER_CU * _coop_resident(dev)
     if nblocks * s_min > budget and s_min > 1:
         return None
@@ -499,6 +523,8 @@ def _pipe_plan(n: int, nblocks: int, K: int, coop, dev: torch.device):
         return None
     if s_min > 1 and _ENV["CNMF_SOLVE_COOP"] == "0":
         return None
+    if coop == "auto" and _ENV["CNMF_SOLVE_COOP"] == "0":
+        return 1, 0
     if coop != "auto":
         S = max(1, int(coop))
         if S < s_min or S > kCoopMaxSlices or S > budget:
@@ -1786,3 +1812,32 @@ def count_unit_check(X: torch.Tensor, mn: torch.Tensor) -> torch.Tensor:
     _hip.count_unit_check(X.data_ptr(), X.stride(0), N, G, mn.contiguous().data_ptr(),
                           bad.data_ptr(), _stream_ptr(X))
     return bad
+
+
+# ----------------------------------------------------------------------------- H8
+def predict_err_terms(X: torch.Tensor, U: torch.Tensor, S: torch.Tensor) -> tuple[float, float]:
+    """(<X, U S>, ||X||^2) in float64 for a resident dense X (N x G, float32, unit column
+    stride), usages U (N x K) and spectra S (K x G) -- the two data terms of the trace
+    identity ||X - U S||^2 = ||X||^2 - 2 <X, U S> + <U^T U, S S^T> (cnmf.py:1100-1104).
+    GPU: ONE pass over X (csrc/kernels/predict_err.hip: the U S tile on the f64 matrix
+    cores, folded with X in registers; U S never materialised).  CPU: float64 torch."""
+    N, G = X.shape
+    K = U.shape[1]
+    if U.shape[0] != N or S.shape != (K, G):
+        raise ValueError(f"predict_err_terms: X {tuple(X.shape)}, U {tuple(U.shape)}, "
+                         f"S {tuple(S.shape)}")
+    if not use_native(X):
+        Xd = X.to(torch.float64)
+        return float((Xd * (U.to(torch.float64) @ S.to(torch.float64))).sum()), \
+            float((Xd * Xd).sum())
+    if X.dtype != torch.float32 or (G > 1 and X.stride(1) != 1):
+        raise ValueError("X: float32 with unit column stride")
+    if K > 128:
+        raise ValueError(f"predict_err_terms: K={K} > 128")
+    Ud = U.to(device=X.device, dtype=torch.float64).contiguous()
+    Sd = S.to(device=X.device, dtype=torch.float64).contiguous()
+    part = torch.empty(2 * (-(-N // 64)), dtype=torch.float64, device=X.device)
+    _hip.predict_err(X.data_ptr(), X.stride(0), Ud.data_ptr(), K, Sd.data_ptr(), G, N, G, K,
+                     part.data_ptr(), _stream_ptr(X))
+    t = part.view(-1, 2).sum(dim=0).cpu()
+    return float(t[0]), float(t[1])

@@ -45,6 +45,17 @@ class LocalComm:
     def all_gather_(self, t: torch.Tensor) -> list[torch.Tensor]:
         return [t]
 
+    def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out = this rank's chunk of the sum over ranks of ``inp`` (world equal chunks,
+        contiguous, rank-major)."""
+        out.copy_(inp.reshape(-1)[:out.numel()].view_as(out))
+        return out
+
+    def all_gather_into_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """out (world equal chunks, rank-major, contiguous) = every rank's ``inp``."""
+        out.reshape(-1)[:inp.numel()].copy_(inp.reshape(-1))
+        return out
+
     @property
     def is_distributed(self) -> bool:
         return False
@@ -162,6 +173,39 @@ class DistComm(LocalComm):
         self._dist.all_gather(out, src.contiguous(), group=self.group)
         return out if src is t else [o.to(t.device) for o in out]
 
+    def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """One reduce-scatter (RCCL ring on the xGMI links): ``out`` = chunk ``rank`` of
+        the sum over ranks of ``inp`` (world * out.numel() elements, rank-major).  Moves
+        the same bytes per link as half an all-reduce.  Under gloo: an all-reduce of a
+        host copy, then the chunk."""
+        if self.world_size == 1:
+            return LocalComm.reduce_scatter_(self, out, inp)
+        m = out.numel()
+        if inp.numel() != m * self.world_size:
+            raise ValueError(f"reduce_scatter_: {inp.numel()} != {self.world_size} x {m}")
+        if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():
+            self._dist.reduce_scatter_tensor(out, inp, group=self.group)
+            return out
+        host = inp.reshape(-1).cpu()
+        self._dist.all_reduce(host, group=self.group)
+        out.copy_(host[self.rank * m:(self.rank + 1) * m].view_as(out))
+        return out
+
+    def all_gather_into_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """One all-gather into the rank-major ``out`` (world * inp.numel() elements)."""
+        if self.world_size == 1:
+            return LocalComm.all_gather_into_(self, out, inp)
+        m = inp.numel()
+        if out.numel() != m * self.world_size:
+            raise ValueError(f"all_gather_into_: {out.numel()} != {self.world_size} x {m}")
+        if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():
+            self._dist.all_gather_into_tensor(out, inp, group=self.group)
+            return out
+        parts = [torch.empty(m, dtype=inp.dtype) for _ in range(self.world_size)]
+        self._dist.all_gather(parts, inp.reshape(-1).cpu().contiguous(), group=self.group)
+        out.reshape(-1).copy_(torch.cat(parts))
+        return out
+
     def send_object(self, obj, dst: int) -> None:
         """Point-to-point: ``obj`` to rank ``dst`` (which must call recv_object(src=me))."""
         self._dist.send_object_list([obj], dst=dst, group=self.group)
@@ -178,4 +222,55 @@ class DistComm(LocalComm):
             return [obj]
         out = [None] * self.world_size if self.rank == dst else None
         self._dist.gather_object(obj, out, dst=dst, group=self.group)
+        return out
+
+
+class EmulatedComm(LocalComm):
+    """Rank 0 of a ``world``-rank cell-sharded (DP) solve, run alone on one GPU: every
+    collective is replaced by a device copy of the bytes it would deliver, scaled as if
+    every rank had contributed this rank's statistics (homogeneous shards).  The solver
+    then runs exactly rank 0's per-step work -- the same kernels, shapes and pass counts
+    -- so its step time is the per-rank compute time of the real N-GPU job, collectives
+    excluded (bench.py --mode dp --emulate-world N; their volume is reported beside it).
+    Never used to produce results."""
+
+    def __init__(self, world: int):
+        self.rank = 0
+        self.world_size = int(world)
+        self.bytes = 0          # collective payload bytes issued (per rank)
+        self._scratch = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    def _copy(self, t: torch.Tensor) -> None:
+        n = t.numel()
+        if self._scratch is None or self._scratch.numel() < n or self._scratch.dtype != t.dtype \
+                or self._scratch.device != t.device:
+            self._scratch = torch.empty(max(n, 1 << 20), dtype=t.dtype, device=t.device)
+        self._scratch[:n].copy_(t.reshape(-1))
+
+    def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
+        self._copy(t)
+        self.bytes += t.numel() * t.element_size()
+        if t.is_floating_point():
+            t.mul_(self.world_size)
+        return t
+
+    def allreduce_scalar(self, v: float) -> float:
+        return float(v) * self.world_size
+
+    def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        self.bytes += inp.numel() * inp.element_size()
+        out.copy_(inp.reshape(-1)[:out.numel()].view_as(out))
+        out.mul_(self.world_size)
+        return out
+
+    def all_gather_into_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        m = inp.numel()
+        self.bytes += out.numel() * out.element_size()
+        flat = out.reshape(-1)
+        for r in range(self.world_size):
+            flat[r * m:(r + 1) * m].copy_(inp.reshape(-1))
         return out

@@ -291,6 +291,9 @@ class Preprocess:
             src = scaled(None, raw_dt)
         res = run_harmony(X_pca, ad.obs, harmony_vars, max_iter_harmony=max_iter_harmony,
                           theta=theta, device=src.device, init_backend="device")
+        self.harmony_info_ = {"iterations": len(res.kmeans_rounds),
+                              "kmeans_rounds": [int(r) + 1 for r in res.kmeans_rounds],
+                              "max_iter_harmony": int(max_iter_harmony)}
         Xc = moe_correct_expression(src, res.R, res.Phi_moe, res.lamb, K=res.K)
         del src
         Xc.clamp_(min=0)
@@ -313,6 +316,9 @@ class Preprocess:
             init_backend = "device" if dev.type == "cuda" else "sklearn"
         res = run_harmony(pca, obs, harmony_vars, max_iter_harmony=max_iter_harmony, theta=theta,
                           device=dev, init_backend=init_backend)
+        self.harmony_info_ = {"iterations": len(res.kmeans_rounds),
+                              "kmeans_rounds": [int(r) + 1 for r in res.kmeans_rounds],
+                              "max_iter_harmony": int(max_iter_harmony)}
         X_pca_harmony = res.Z_corr.T
         _, X_corr, _, _ = moe_correct_ridge(np.asarray(X).T, None, None, res.R, None, res.K, None,
                                             res.Phi_moe, res.lamb, device=dev)

@@ -37,6 +37,14 @@ PYBIND11_MODULE(_hip, m) {
   m.def("solve_mfma_max_cols", [](int K) { return cnmf_solve_mfma_max_cols(K); });
   m.def("solve_pipe_tiles", [](int K, int per) { return cnmf_solve_pipe_tiles(K, per); });
   m.def("solve_pipe_k", [](int K) { return cnmf_solve_pipe_k(K); });
+  m.def("predict_err",
+        [](uintptr_t X, long long ldx, uintptr_t U, long long ldu, uintptr_t S, long long lds,
+           int N, int G, int K, uintptr_t part, uintptr_t stream) {
+          check(cnmf_predict_err(P<const float>(X), ldx, P<const double>(U), ldu,
+                                 P<const double>(S), lds, N, G, K, P<double>(part),
+                                 reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_predict_err");
+        });
   m.def("solve_pipe_max_cols", [](int K) { return cnmf_solve_pipe_max_cols(K); });
   m.def("solve_pipe_wg_per_cu", [](int K) { return cnmf_solve_pipe_wg_per_cu(K); });
 

@@ -225,3 +225,36 @@ def xgmi_dp_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, allreduce):
     comm.close()
     dist.barrier()
     dist.destroy_process_group()
+
+
+def dp_fused_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, fused):
+    """Cell-sharded DP solve on the GPU (both ranks share the one GPU of the box; the
+    collectives are staged through gloo): the reduce-scattered fused step
+    (CNMF_DP_FUSED=1) or the all-reduced unfused step (0)."""
+    os.environ["CNMF_DP_FUSED"] = fused
+    os.environ["CNMF_SOLVE_COOP"] = "0"      # two processes on one GPU: no spinning slices
+    _init(rank, world, port)
+    from cnmf_torch_amd import ops
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions, _Batch
+
+    ops.refresh_env()
+    from cnmf_torch_amd.parallel.comm import DistComm
+    from cnmf_torch_amd.parallel.runner import dp_layout, dp_row_segments
+
+    torch.cuda.set_device(0)
+    segs = dp_row_segments(X.shape[0], opts_kw["online_chunk_size"], rank, world)
+    row_map, sched = dp_layout(segs)
+    Xl = torch.from_numpy(np.concatenate([X[a:b] for a, b in segs])).cuda()
+    solver = NMFBatchSolver(Xl, NMFOptions(n_components=K, **opts_kw), comm=DistComm(),
+                            row_map=row_map, schedule=sched)
+    st = _Batch(torch.zeros((K * len(seeds), Xl.shape[0]), device="cuda"),
+                torch.zeros((K * len(seeds), Xl.shape[1]), device="cuda"), [K] * len(seeds))
+    took = solver._fused_ok(st, solver._steps(Xl.shape[0]))
+    res = solver.run(seeds)
+    np.save(os.path.join(out_dir, f"dpf{fused}_{rank}.npz.npy"),
+            np.array([took], dtype=bool))
+    np.save(os.path.join(out_dir, f"dpfW{fused}_{rank}.npy"), res.W.cpu().numpy())
+    np.save(os.path.join(out_dir, f"dpferr{fused}_{rank}.npy"), res.err)
+    np.save(os.path.join(out_dir, f"dpfit{fused}_{rank}.npy"), res.n_iter)
+    dist.barrier()
+    dist.destroy_process_group()

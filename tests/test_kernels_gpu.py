@@ -1286,21 +1286,25 @@ def test_solve_rejects_uninstantiated_k_loudly():
 @pytest.mark.parametrize("K", [37, 64])
 def test_nmf_wide_k_gpu_matches_cpu(K):
     """K > 32: padded to a multiple of 8 on the GPU (zero components), same factorisation
-    as the CPU oracle at the true K."""
+    as the CPU oracle at the true K.  Fixed sweep and pass counts (no tolerance-driven
+    stop that a rounding difference could flip), so the two runs do the same updates and
+    differ by fp32 reassociation only."""
     from cnmf_torch_amd.models.nmf import run_nmf_batch
 
     rs = np.random.default_rng(K)
     N, G = 1200, 300
     X = (rs.gamma(1, 1, (N, 12)) @ rs.gamma(0.5, 1, (12, G)) + 0.1 * rs.random((N, G))).astype(
         np.float32)
-    kw = dict(online_chunk_size=600, online_max_pass=4)
+    kw = dict(online_chunk_size=600, online_max_pass=4, online_h_tol=-1.0, online_w_tol=-1.0,
+              online_chunk_max_iter=15, tol=-1.0)
     g = run_nmf_batch(X, K, [3, 4], device="cuda", **kw)
     c = run_nmf_batch(X, K, [3, 4], device="cpu", **kw)
     assert g.W.shape == (2 * K, G) and g.HT.shape == (2 * K, N)
-    np.testing.assert_allclose(g.err, c.err, rtol=2e-2)
+    np.testing.assert_array_equal(g.n_iter, c.n_iter)
+    np.testing.assert_allclose(g.err, c.err, rtol=3e-3)
     Wg, Wc = g.W.cpu().numpy(), c.W.cpu().numpy()
     cos = (Wg * Wc).sum(1) / (np.linalg.norm(Wg, axis=1) * np.linalg.norm(Wc, axis=1) + 1e-30)
-    assert np.median(cos) > 0.98, np.sort(cos)[:5]
+    assert np.median(cos) > 0.999, np.sort(cos)[:5]
 
 
 def test_device_kmeans_inertia_matches_sklearn_over_seeds():

@@ -375,23 +375,22 @@ def test_plot_worker_falls_back_when_the_child_dies(tmp_path):
     assert os.path.getsize(path2) > 1000
 
 
-def test_gpu_rank_limit_is_a_clear_prepare_error(monkeypatch, tmp_path):
-    """-k beyond what the GPU kernels cover fails at prepare with a message naming the
-    limit and the CPU alternative (instead of deep inside factorize)."""
+def test_gpu_rank_limit_is_routed_with_a_message(monkeypatch, tmp_path):
+    """-k beyond what the native GPU kernels cover is announced at prepare (warning +
+    log naming the limit) and routed to the eager PyTorch ops -- not a failed job."""
     import torch
 
     from cnmf_torch_amd import api
 
     monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
-    with pytest.raises(ValueError, match=r"K=130: on the GPU this engine factorises K <= 128.*"
-                                         r"without --use_gpu"):
-        api.check_gpu_ranks([10, 130], "frobenius", "mu", use_gpu=True)
-    with pytest.raises(ValueError, match=r"K=80: on the GPU this engine factorises K <= 64"):
-        api.check_gpu_ranks([10, 80], "frobenius", "hals", use_gpu=True)
-    api.check_gpu_ranks([80, 128], "frobenius", "mu", use_gpu=True)  # matrix-core wide solve
-    with pytest.raises(ValueError, match="K <= 32"):
-        api.check_gpu_ranks([40], "kullback-leibler", "mu", use_gpu=True)
-    api.check_gpu_ranks([80], "frobenius", "bpp", use_gpu=True)     # torch linalg: any K
+    with pytest.warns(RuntimeWarning, match=r"K=\[130\]: the native gfx950 kernels factorise K <= 128"):
+        assert api.check_gpu_ranks([10, 130], "frobenius", "mu", use_gpu=True) == [130]
+    with pytest.warns(RuntimeWarning, match=r"K <= 64"):
+        assert api.check_gpu_ranks([10, 80], "frobenius", "hals", use_gpu=True) == [80]
+    assert api.check_gpu_ranks([80, 128], "frobenius", "mu", use_gpu=True) == []
+    with pytest.warns(RuntimeWarning, match="K <= 32"):
+        assert api.check_gpu_ranks([40], "kullback-leibler", "mu", use_gpu=True) == [40]
+    assert api.check_gpu_ranks([80], "frobenius", "bpp", use_gpu=True) == []  # torch linalg
     api.check_gpu_ranks([80], "frobenius", "mu", use_gpu=False)     # CPU: any K
     api.check_gpu_ranks([64], "frobenius", "mu", use_gpu=True)
 

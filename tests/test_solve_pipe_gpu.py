@@ -280,9 +280,10 @@ def test_conv_update_slots_match_prefix_sums():
     assert sl["live"].tolist() == [int(kv.sum()), int(k.sum())]
 
 
-def test_gemm_planes_live_rows_skip_dead_tiles():
+def test_gemm_planes_live_rows_skip_dead_tiles(monkeypatch):
     """gemm_planes(live=...): rows below the live count equal the full product; M-tiles
-    that start at or past it are skipped (their output rows keep their old contents)."""
+    that start at or past it are skipped (without a k split -- no reduction pass -- their
+    output rows keep their old contents)."""
     M, N, K = 1000, 640, 2048
     g = torch.Generator().manual_seed(11)
     A = torch.rand((M, K), generator=g)
@@ -297,4 +298,57 @@ def test_gemm_planes_live_rows_skip_dead_tiles():
     C = torch.full((M, N), float("nan"), device="cuda")
     ops.gemm_planes(C, Ap[:2], Bp, M, N, K, live=live)
     assert torch.equal(C[:333], full[:333])
-    assert torch.isnan(C[512:]).all()
+    monkeypatch.setenv("CNMF_GEMM_KSPLIT", "1")
+    ops.refresh_env()
+    try:
+        C = torch.full((M, N), float("nan"), device="cuda")
+        ops.gemm_planes(C, Ap[:2], Bp, M, N, K, live=live)
+        torch.cuda.synchronize()
+        assert torch.equal(C[:333], full[:333])
+        assert torch.isnan(C[512:]).all()
+    finally:
+        monkeypatch.delenv("CNMF_GEMM_KSPLIT")
+        ops.refresh_env()
+
+
+def test_rank_beyond_kernels_routes_to_eager_ops_on_the_gpu():
+    """K > 128 (no kernel instantiation) is routed to the eager PyTorch ops on the same
+    GPU with a warning -- the job completes and matches the CPU engine's factorisation of
+    the same seeds (same algorithm, fp32 rounding apart) -- and a mixed batch splits by K
+    (the covered K stays on the native kernels)."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.models.refit import fit_H_online
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    Xn = normalized_counts_matrix(900, 300, n_programs=6, seed=2)
+    opts = NMFOptions(n_components=130, online_chunk_size=450, online_max_pass=4)
+    with pytest.warns(RuntimeWarning, match="K=130: the native gfx950 kernels cover K <= 128"):
+        g = NMFBatchSolver(torch.from_numpy(Xn).cuda(), opts).run([5, 6], ks=[130, 10])
+    c = NMFBatchSolver(torch.from_numpy(Xn), opts).run([5, 6], ks=[130, 10])
+    assert g.W.shape == (140, 300) and torch.isfinite(g.W).all()
+    np.testing.assert_allclose(g.err, c.err, rtol=2e-3)
+    with pytest.warns(RuntimeWarning, match="refit K=130"):
+        U = fit_H_online(Xn, g.W[:130].cpu().numpy(), device="cuda")
+    assert U.shape == (900, 130) and np.isfinite(U).all() and (U >= 0).all()
+
+
+@pytest.mark.parametrize("N,G,K", [(1000, 300, 10), (777, 2001, 7), (4096, 128, 64), (130, 70, 128)])
+def test_predict_err_kernel_matches_float64(N, G, K):
+    """predict_err.hip (H8): <X, U S> and ||X||^2 in one pass over the resident float32 X
+    with the U S tile on the f64 matrix cores == float64 torch, and the k-selection
+    prediction error built from them == ||X - U S||^2 (cnmf.py:1100-1104)."""
+    from cnmf_torch_amd.api import cNMF
+
+    g = torch.Generator().manual_seed(N + G + K)
+    X = (torch.rand((N, G), generator=g) * (torch.rand((N, G), generator=g) < 0.3)).float()
+    U = torch.rand((N, K), generator=g, dtype=torch.float64)
+    S = torch.rand((K, G), generator=g, dtype=torch.float64)
+    cross, xsq = ops.predict_err_terms(X.cuda(), U, S)
+    Xd = X.double()
+    want_c = float((Xd * (U @ S)).sum())
+    want_x = float((Xd * Xd).sum())
+    assert abs(cross - want_c) <= 1e-12 * abs(want_c)
+    assert abs(xsq - want_x) <= 1e-12 * abs(want_x)
+    err = cNMF._prediction_error(X.cuda(), U.numpy(), S.numpy(), torch.device("cuda"))
+    full = float(((Xd - U @ S) ** 2).sum())
+    assert abs(err - full) <= 1e-9 * full

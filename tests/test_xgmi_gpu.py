@@ -50,3 +50,28 @@ def test_xgmi_dp_solve_matches_gloo_staged(tmp_path):
     np.testing.assert_allclose(Wx, Wg, rtol=1e-4, atol=1e-6)
     ref = NMFBatchSolver(torch.from_numpy(X).cuda(), NMFOptions(n_components=K, **kw)).run(seeds)
     np.testing.assert_allclose(np.load(tmp_path / "err_xgmi0.npy"), ref.err, rtol=1e-3)
+
+
+@pytest.mark.parametrize("K,R", [(6, 7), (20, 6)])
+def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
+    """Cell-sharded DP with the fused step -- reduce-scatter of dB and the per-slice
+    partial Grams, each rank W-solving only its replicate chunk (R not a multiple of the
+    world: a padded last chunk), all-gather of the spectra planes / W W^T partials /
+    lin-quad -- factorises like the all-reduced unfused DP step: identical W on both
+    ranks, pass counts +-1, errors of same-pass replicates to 1e-5."""
+    X = normalized_counts_matrix(1600, 200, n_programs=6, seed=9)
+    seeds = list(range(31, 31 + R))
+    kw = dict(online_chunk_size=400, online_max_pass=12)
+    for fused in ("1", "0"):
+        _spawn(W.dp_fused_worker, 2, X, K, seeds, kw, str(tmp_path), fused)
+    for r in range(2):
+        assert bool(np.load(tmp_path / f"dpf1_{r}.npz.npy")[0])
+        assert not bool(np.load(tmp_path / f"dpf0_{r}.npz.npy")[0])
+    Wf = np.load(tmp_path / "dpfW1_0.npy")
+    np.testing.assert_array_equal(Wf, np.load(tmp_path / "dpfW1_1.npy"))
+    ef, eu = np.load(tmp_path / "dpferr1_0.npy"), np.load(tmp_path / "dpferr0_0.npy")
+    itf, itu = np.load(tmp_path / "dpfit1_0.npy"), np.load(tmp_path / "dpfit0_0.npy")
+    assert np.abs(itf - itu).max() <= 1
+    same = itf == itu
+    assert same.mean() > 0.6
+    np.testing.assert_allclose(ef[same], eu[same], rtol=1e-5)

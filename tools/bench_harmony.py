@@ -64,13 +64,26 @@ def main():
     ap.add_argument("--hvg", type=int, default=2000)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--n-iter", type=int, default=20)
-    ap.add_argument("--max-iter-harmony", type=int, default=10)
+    ap.add_argument("--max-iter-harmony", type=int, default=20,
+                    help="the reference default (preprocess.py:138)")
+    ap.add_argument("--gpu-busy", action="store_true",
+                    help="also report GPU-busy seconds per stage (torch.profiler kernel time; "
+                         "adds profiler overhead to the wall-clocks)")
     ap.add_argument("--profile", default=None, help="cProfile the Harmony stage into this file")
     ap.add_argument("--profile-stages", default=None,
                     help="cProfile prepare / factorize / combine+consensus into PREFIX.<stage>.txt")
     a = ap.parse_args()
 
+    busy = {}
+
     def staged(name, fn):
+        if a.gpu_busy and torch.cuda.is_available():
+            from torch.profiler import ProfilerActivity, profile
+            with profile(activities=[ProfilerActivity.CUDA]) as pr:
+                out = fn()
+                torch.cuda.synchronize()
+            busy[name] = round(sum(e.self_device_time_total for e in pr.key_averages()) / 1e6, 3)
+            return out
         if not a.profile_stages:
             return fn()
         import cProfile
@@ -99,9 +112,9 @@ def main():
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
-    corrected, tp10k, hvgs = p.preprocess_for_cnmf(
+    corrected, tp10k, hvgs = staged("preprocess_harmony", lambda: p.preprocess_for_cnmf(
         ad, harmony_vars=["cov0", "cov1", "cov2", "cov3"], n_top_rna_genes=a.hvg,
-        makeplots=False, max_iter_harmony=a.max_iter_harmony, save_output_base=base)
+        makeplots=False, max_iter_harmony=a.max_iter_harmony, save_output_base=base))
     if prof is not None:
         import io
         import pstats
@@ -133,6 +146,8 @@ def main():
         "metric": "Harmony + cNMF end-to-end wall-clock", "unit": "s",
         "value": round(sum(v for k, v in t.items() if k != "simulate"), 2),
         "stages_s": {k: round(v, 2) for k, v in t.items()},
+        "gpu_busy_s": busy or None,
+        "harmony": getattr(p, "harmony_info_", None),
         "config": {"cells": a.cells, "genes": a.genes, "hvg": a.hvg, "covariates": 4,
                    "k": a.k, "n_iter": a.n_iter, "max_iter_harmony": a.max_iter_harmony,
                    "device": torch.cuda.get_device_name(0) if torch.cuda.is_available() else "cpu"},
