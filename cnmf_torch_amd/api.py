@@ -41,7 +41,8 @@ from torch.utils.weak import WeakIdKeyDictionary
 
 from .models.consensus import (cluster_medians, kmeans, l2_normalize_rows, local_density,
                                pairwise_distances, silhouette)
-from .models.hvg import compute_tpm, get_highvar_genes, get_highvar_genes_sparse, get_mean_var
+from .models.hvg import (compute_tpm, exact_mean_var, get_highvar_genes,
+                         get_highvar_genes_sparse, get_mean_var)
 from .models.nmf import NMFBatchSolver, NMFOptions
 from .models.ols import efficient_ols_all_cols
 from .models.pp import scale as pp_scale
@@ -227,7 +228,12 @@ def _norm_counts_tensor(counts, genes, guard_zero_std: bool, dev):
     T = torch.from_numpy(np.ascontiguousarray(counts.X)).to(dev)
     T = T.index_select(1, torch.as_tensor(cols, device=dev)).to(torch.float64)
     n = T.shape[0]
-    if guard_zero_std:
+    ex = exact_mean_var(T, 1)        # exact moments on the device (models.hvg)
+    if ex is not None:
+        std = torch.from_numpy(np.sqrt(ex[1])).to(dev)
+        if guard_zero_std:
+            std[std == 0] = 1.0
+    elif guard_zero_std:
         mean = T.mean(dim=0)
         var = (T * T).mean(dim=0) - mean * mean
         if n > 1:
@@ -348,7 +354,16 @@ class cNMF:
                 tpm = read_counts_table(tpm_fn, densify)
                 write_h5ad(self.paths["tpm"], tpm)
 
-            if sp.issparse(tpm.X):
+            # exact moments on the host matrix (models.hvg.exact_mean_var): the same bits
+            # as the cell-sharded prepare's all-reduced digits (_prepare_sharded)
+            ex = exact_mean_var(tpm.X, 0)
+            if ex is not None:
+                gene_tpm_mean, gene_tpm_var = ex
+                if tpm.X.dtype == np.float32:   # sklearn keeps float32 statistics
+                    gene_tpm_mean = gene_tpm_mean.astype(np.float32)
+                    gene_tpm_var = gene_tpm_var.astype(np.float32)
+                gene_tpm_std = gene_tpm_var ** 0.5
+            elif sp.issparse(tpm.X):
                 dT = _device_csr(tpm.X, _device(use_gpu))
                 gene_tpm_mean, gene_tpm_var = get_mean_var(dT if dT is not None else tpm.X)
                 del dT
@@ -400,26 +415,21 @@ class cNMF:
         artifacts of the single-process prepare, receiving the other ranks' row blocks
         one rank at a time (point-to-point) straight into the h5ad datasets: it never
         holds more than its own block and one peer's (h5ad.write_h5ad_row_blocks)."""
+        import pickle
+
         from .parallel.runner import row_block
-        from .utils.h5ad import h5ad_shape, read_X_rows, read_h5ad_annotations
+        from .utils.io import read_rows_any
 
         rank, world = comm.rank, comm.world_size
+        # bound of every point-to-point message of the row-block hand-over (bytes)
+        cb = int(os.environ.get("CNMF_PREPARE_CHUNK_BYTES", str(1 << 30)))
         with self.timer("prepare"):
             if tpm_fn is not None:
                 raise NotImplementedError("sharded prepare computes the TPM itself "
                                           "(tpm_fn: run prepare on one rank)")
-            if str(counts_fn).endswith(".h5ad"):
-                n_rows, _ = h5ad_shape(counts_fn)
-                a, b = row_block(n_rows, rank, world)
-                ann = read_h5ad_annotations(counts_fn)
-                counts = AnnData(X=read_X_rows(counts_fn, a, b), obs=ann.obs.iloc[a:b],
-                                 var=ann.var)
-            else:
-                full = read_any(counts_fn, densify)
-                n_rows = full.shape[0]
-                a, b = row_block(n_rows, rank, world)
-                counts = AnnData(X=full.X[a:b], obs=full.obs.iloc[a:b], var=full.var)
-                del full
+            # only this rank's cells are read (h5ad / 10x mtx / DataFrame npz / TSV)
+            counts, _, _ = read_rows_any(counts_fn, lambda n: row_block(n, rank, world),
+                                         densify)
             if sp.issparse(counts.X) and densify:
                 counts.X = np.asarray(counts.X.todense())
             sparse_in = sp.issparse(counts.X)
@@ -429,7 +439,12 @@ class cNMF:
                 return np.asarray(M.sum(axis=0), dtype=np.float64).reshape(-1)
 
             def mean_var(M, ddof):
-                """Global column mean / variance of the row-sharded M (two-pass)."""
+                """Global column mean / variance of the row-sharded M: the exact integer
+                moments all-reduced (models.hvg.exact_mean_var -- the single-process
+                prepare's statistics, bit for bit), else the float64 two-pass."""
+                ex = exact_mean_var(M, ddof, comm)
+                if ex is not None:
+                    return ex
                 n = comm.allreduce_scalar(float(M.shape[0]))
                 s1 = torch.from_numpy(col_sum(M))
                 comm.allreduce_(s1)
@@ -449,9 +464,13 @@ class cNMF:
                 return mean, m2.numpy() / max(n - ddof, 1.0)
 
             gene_tpm_mean, gene_tpm_var = mean_var(tpm.X, 0)
-            if tpm.X.dtype == np.float32:     # sklearn's StandardScaler keeps the input dtype
+            hv_mean, hv_var = gene_tpm_mean, gene_tpm_var
+            if tpm.X.dtype == np.float32:     # sklearn keeps float32 statistics
                 gene_tpm_mean = gene_tpm_mean.astype(np.float32)
                 gene_tpm_var = gene_tpm_var.astype(np.float32)
+                if sparse_in:     # get_highvar_genes_sparse sees get_mean_var's float32
+                    hv_mean = gene_tpm_mean.astype(np.float64)
+                    hv_var = gene_tpm_var.astype(np.float64)
             gene_tpm_std = gene_tpm_var ** 0.5
             stats = pd.DataFrame([gene_tpm_mean, gene_tpm_std], index=["__mean", "__std"],
                                  columns=tpm.var.index).T
@@ -461,7 +480,7 @@ class cNMF:
             else:
                 from .models.hvg import _fano_model
 
-                gstats, _ = _fano_model(pd.Series(gene_tpm_mean), pd.Series(gene_tpm_var),
+                gstats, _ = _fano_model(pd.Series(hv_mean), pd.Series(hv_var),
                                         None, 0.5, num_highvar_genes)
                 hvgs = list(tpm.var.index[gstats.high_var.values])
             cols = counts.var.index.get_indexer(hvgs)
@@ -469,8 +488,8 @@ class cNMF:
                 raise KeyError(f"genes missing from the counts: {list(np.array(hvgs)[cols < 0][:5])}")
             Xh = counts.X[:, cols]
             Xh = Xh.astype(np.float64) if sp.issparse(Xh) else np.asarray(Xh, dtype=np.float64)
-            _, hv_var = mean_var(Xh, 1)
-            std = np.sqrt(hv_var)
+            _, hv_cvar = mean_var(Xh, 1)
+            std = np.sqrt(hv_cvar)
             if sparse_in:          # scanpy scale(zero_center=False): std 0 -> 1
                 std[std == 0] = 1.0
                 Xh = sp.csr_matrix(Xh)
@@ -494,21 +513,54 @@ class cNMF:
             if rank == 0:
                 self._initialize_dirs()
             n_tot = sum(m_[0] for m_ in meta)
+
+            def send_block(obs, M):
+                """A peer's row block to rank 0: arrays in messages of <= cb bytes."""
+                comm.send_array(np.frombuffer(pickle.dumps(obs), dtype=np.uint8), 0, cb)
+                if sp.issparse(M):
+                    M = sp.csr_matrix(M)
+                    for arr in (M.data, M.indices, M.indptr.astype(np.int64)):
+                        comm.send_array(arr, 0, cb)
+                else:
+                    comm.send_array(np.asarray(M), 0, cb)
+
+            def recv_block(src, G_):
+                obs = pickle.loads(comm.recv_array(src).tobytes())
+                if sparse_in:
+                    data, ind, ptr = (comm.recv_array(src) for _ in range(3))
+                    return obs, sp.csr_matrix((data, ind, ptr), shape=(len(obs), G_))
+                return obs, comm.recv_array(src)
+
             for which, local, total_nnz, path, var in (
                     (0, tpm.X, sum(m_[1] for m_ in meta), self.paths["tpm"], tpm.var),
                     (1, Xh, sum(m_[2] for m_ in meta), self.paths["normalized_counts"],
                      counts.var.iloc[cols])):
+                failed = None
                 if rank == 0:
-                    def blocks(local=local):
+                    def blocks(local=local, G_=len(var)):
                         yield counts.obs, local
                         for src in range(1, world):       # one peer block at a time
-                            yield comm.recv_object(src)
+                            yield recv_block(src, G_)
+                    gen = blocks()
                     idx_dt = np.int64 if total_nnz >= 2 ** 31 else np.int32
-                    write_h5ad_row_blocks(path, n_tot, var, blocks(), sparse_in, local.dtype,
-                                          total_nnz, idx_dt)
+                    try:
+                        write_h5ad_row_blocks(path, n_tot, var, gen, sparse_in, local.dtype,
+                                              total_nnz, idx_dt)
+                    except Exception as e:       # noqa: BLE001 -- re-raised below
+                        failed = e
+                        for _ in gen:    # keep receiving: no peer is left blocked in a send
+                            pass
                 else:
-                    comm.send_object((counts.obs, local), dst=0)
-                comm.barrier()
+                    send_block(counts.obs, local)
+                # rank 0 tells every peer whether the file was written: a writer failure
+                # fails the stage on every rank instead of leaving peers in a barrier
+                st = torch.tensor([0 if failed is None else 1], dtype=torch.int64,
+                                  device=comm._dev() if hasattr(comm, "_dev") else "cpu")
+                comm.broadcast_(st, src=0)
+                if failed is not None:
+                    raise failed
+                if int(st.item()) != 0:
+                    raise RuntimeError(f"sharded prepare: rank 0 failed to write {path}")
             if rank == 0:
                 save_df_to_npz(stats, self.paths["tpm_stats"])
                 write_text_atomic(self.paths["nmf_genes_list"], "\n".join(hvgs))
@@ -567,8 +619,10 @@ class cNMF:
                 print("Warning NaNs in normalized counts matrix")
         else:
             X = norm_counts.X.toarray() if sp.issparse(norm_counts.X) else norm_counts.X
+            ex = exact_mean_var(X, 1)
+            std = np.sqrt(ex[1]) if ex is not None else X.std(axis=0, ddof=1)
             with np.errstate(divide="ignore", invalid="ignore"):
-                X = X / X.std(axis=0, ddof=1)
+                X = X / std
             norm_counts.X = X
             if np.isnan(norm_counts.X).sum().sum() > 0:
                 print("Warning NaNs in normalized counts matrix")

@@ -11,6 +11,8 @@ the GPU for device tensors (one pass, float64 accumulation).
 """
 from __future__ import annotations
 
+import math
+
 import numpy as np
 import pandas as pd
 import scipy.sparse as sp
@@ -49,11 +51,110 @@ def sparse_mean_var(X):
     return mean, var
 
 
+def _digits_to_ints(d: np.ndarray) -> list:
+    """Per-row Python ints of base-2^32 signed int64 digit vectors (carries propagated in
+    numpy, then one int.from_bytes per row)."""
+    d = np.array(d, dtype=np.int64, copy=True)
+    D = d.shape[1]
+    for i in range(D - 1):            # arithmetic shift: floor division by 2^32
+        carry = d[:, i] >> 32
+        d[:, i] -= carry << 32
+        d[:, i + 1] += carry
+    top = d[:, D - 1]
+    low = d[:, :D - 1].astype("<u4")  # every lower digit now in [0, 2^32)
+    out = []
+    for j in range(d.shape[0]):
+        v = int.from_bytes(low[j].tobytes(), "little") + (int(top[j]) << (32 * (D - 1)))
+        out.append(v)
+    return out
+
+
+def exact_moment_digits(X, threads: int = 16):
+    """Exact per-column (sum x, sum x^2) of a scipy sparse / numpy dense / torch matrix as
+    integer digit arrays ((G, D1), (G, D2) int64) plus the number of values outside the
+    exact window (|x| in [2^-126, 2^127]), or None without the native module.  Integer
+    digits add exactly: the sums of any row partition (threads, ranks) are the same
+    integers, so statistics built from them do not depend on how the cells are split."""
+    from ..utils.io import _npzio
+    if _npzio is None or not hasattr(_npzio, "exact_col_moments"):
+        return None
+    if isinstance(X, torch.Tensor):
+        if X.is_cuda:
+            from .. import ops
+            return ops.exact_moments(X)
+        X = X.numpy()
+    if sp.issparse(X):
+        Xc = sp.csr_matrix(X)
+        data = Xc.data if Xc.data.dtype in (np.float32, np.float64) else Xc.data.astype(np.float64)
+        return _npzio.exact_col_moments(data, Xc.indices, int(Xc.shape[1]), threads)
+    A = np.asarray(X)
+    if A.dtype not in (np.float32, np.float64):
+        A = A.astype(np.float64)
+    return _npzio.exact_col_moments(np.ascontiguousarray(A), None, int(A.shape[1]), threads)
+
+
+def exact_mean_var_from_digits(d1, d2, n: int, ddof: int = 0):
+    """Column mean and variance (ddof) from exact moment digits: mean = S1 / n and
+    var = (n S2 - S1^2) / (n (n - ddof)), each computed in integers and rounded ONCE to
+    float64 (numpy/sklearn's two-pass float64 sums round at every add)."""
+    from ..utils.io import _npzio
+    lsb1, lsb2 = int(_npzio.EXACT_LSB1), int(_npzio.EXACT_LSB2)
+    s1 = _digits_to_ints(d1)
+    s2 = _digits_to_ints(d2)
+    n = int(n)
+    G = len(s1)
+    mean = np.empty(G)
+    var = np.empty(G)
+    den = n * (n - ddof) if n > ddof else 0
+    for j in range(G):
+        mean[j] = math.ldexp(s1[j] / n, lsb1) if n else 0.0
+        if den:
+            num = n * s2[j] - s1[j] * s1[j]       # in units of 2^lsb2 (= 2^(2 lsb1))
+            var[j] = math.ldexp(num / den, lsb2) if num > 0 else 0.0
+        else:
+            var[j] = float("nan")
+    return mean, var
+
+
+def exact_mean_var(X, ddof: int = 0, comm=None):
+    """Exact column mean / variance (see exact_mean_var_from_digits) of a row block X; with
+    ``comm`` the digits are all-reduced first (integer sums: the sharded statistics equal
+    the single-process ones bit for bit).  None when the exact path is unavailable or a
+    value lies outside its window on any rank (callers then use floating point)."""
+    got = exact_moment_digits(X)
+    n_loc = int(X.shape[0])
+    flag = 1 if got is None else (1 if int(got[2]) else 0)
+    if comm is not None and comm.is_distributed:
+        flag = comm.allreduce_max_int(flag)
+    if flag:
+        return None
+    d1, d2 = torch.from_numpy(np.ascontiguousarray(got[0])), torch.from_numpy(np.ascontiguousarray(got[1]))
+    n = n_loc
+    if comm is not None and comm.is_distributed:
+        flat = torch.cat([d1.reshape(-1), d2.reshape(-1)])
+        comm.allreduce_(flat)
+        d1 = flat[:d1.numel()].view_as(d1)
+        d2 = flat[d1.numel():].view_as(d2)
+        n = int(round(comm.allreduce_scalar(float(n_loc))))
+    return exact_mean_var_from_digits(d1.numpy(), d2.numpy(), n, ddof)
+
+
 def get_mean_var(X):
     """Column mean and ddof=0 variance of a dense/sparse/torch matrix or a device CSR
-    (cnmf.py:128-131)."""
+    (cnmf.py:128-131).  Host and dense-device matrices take the exact path
+    (exact_mean_var: the moments summed in integers, rounded once), so the statistics do
+    not depend on the device or on a row sharding; float32 input keeps sklearn's float32
+    results."""
     from ..ops import sparse as sops
 
+    if not isinstance(X, sops.DeviceCSR):
+        ex = exact_mean_var(X, 0)
+        if ex is not None:
+            mean, var = ex
+            if getattr(X, "dtype", None) in (np.float32, torch.float32):
+                return mean.astype(np.float32).astype(np.float64), \
+                    var.astype(np.float32).astype(np.float64)
+            return mean, var
     if isinstance(X, sops.DeviceCSR):
         mean, var = sops.mean_var(X, ddof=0)
         return mean.cpu().numpy(), var.cpu().numpy()
@@ -107,8 +208,12 @@ def get_highvar_genes_sparse(expression, expected_fano_threshold=None, minimal_m
 def get_highvar_genes(input_counts, expected_fano_threshold=None, minimal_mean=0.5, numgenes=None):
     """Dense variant (cnmf.py:188-238): numpy mean / var(ddof=0)."""
     X = np.asarray(input_counts)
-    mean = pd.Series(X.mean(axis=0).astype(float))
-    var = pd.Series(X.var(ddof=0, axis=0).astype(float))
+    ex = exact_mean_var(X, 0)
+    if ex is not None:
+        mean, var = (pd.Series(v) for v in ex)
+    else:
+        mean = pd.Series(X.mean(axis=0).astype(float))
+        var = pd.Series(X.var(ddof=0, axis=0).astype(float))
     return _fano_model(mean, var, expected_fano_threshold, minimal_mean, numgenes)
 
 

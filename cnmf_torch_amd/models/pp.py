@@ -57,6 +57,11 @@ def normalize_total(adata, target_sum: float | None = None, copy: bool = False, 
 
 def _mean_var_ddof1(X):
     n = X.shape[0]
+    from .hvg import exact_mean_var
+
+    ex = exact_mean_var(X, 1)          # exact moments, one rounding (models.hvg)
+    if ex is not None:
+        return ex
     if sp.issparse(X):
         # scanpy's sparse path: sklearn's centred two-pass variance (exact 0 for constant
         # genes; models.hvg.sparse_mean_var, the same float64 operations in the same

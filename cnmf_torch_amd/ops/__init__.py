@@ -1841,3 +1841,30 @@ def predict_err_terms(X: torch.Tensor, U: torch.Tensor, S: torch.Tensor) -> tupl
                      part.data_ptr(), _stream_ptr(X))
     t = part.view(-1, 2).sum(dim=0).cpu()
     return float(t[0]), float(t[1])
+
+
+# ----------------------------------------------------------------------------- exact stats
+EXACT_D1, EXACT_D2 = 13, 25     # digits of sum x / sum x^2 (csrc/kernels/exact_moments.hip)
+
+
+def exact_moments(X: torch.Tensor):
+    """Exact per-column (sum x, sum x^2) of a dense device matrix (float32 / float64, unit
+    column stride) as integer digits ((G, 13), (G, 25) int64 numpy) plus the count of
+    values outside the exact window -- the same integers as the host path
+    (models.hvg.exact_moment_digits), so statistics do not depend on the device or on how
+    the rows are split (csrc/kernels/exact_moments.hip)."""
+    if not use_native(X):
+        raise ValueError("exact_moments: a device tensor is required")
+    if X.dim() != 2 or X.dtype not in (torch.float32, torch.float64) or \
+            (X.shape[1] > 1 and X.stride(1) != 1):
+        raise ValueError("exact_moments: 2-D float32/float64 with unit column stride")
+    rows, G = X.shape
+    D = EXACT_D1 + EXACT_D2
+    chunks = max(1, min(256, -(-rows // 4096), (1 << 14) // max(1, -(-G // 128))))
+    part = torch.empty(chunks * G * D, dtype=torch.int64, device=X.device)
+    out = torch.empty((G, D), dtype=torch.int64, device=X.device)
+    bad = torch.zeros(1, dtype=torch.int64, device=X.device)
+    _hip.exact_moments(X.data_ptr(), int(X.dtype == torch.float64), X.stride(0), rows, G, chunks,
+                       part.data_ptr(), out.data_ptr(), bad.data_ptr(), _stream_ptr(X))
+    o = out.cpu().numpy()
+    return o[:, :EXACT_D1].copy(), o[:, EXACT_D1:].copy(), int(bad.item())

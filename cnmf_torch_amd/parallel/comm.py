@@ -210,6 +210,52 @@ class DistComm(LocalComm):
         """Point-to-point: ``obj`` to rank ``dst`` (which must call recv_object(src=me))."""
         self._dist.send_object_list([obj], dst=dst, group=self.group)
 
+    # bounded point-to-point array transfer (sharded prepare's row blocks to the writer)
+    _DTYPES = ("<f4", "<f8", "<i4", "<i8", "|u1", "<u4", "<u8", "|b1", "<i2", "<u2", "|i1")
+    max_msg_bytes = 0           # largest single message sent so far (tests, logging)
+
+    def _p2p(self, t: torch.Tensor, peer: int, send: bool) -> torch.Tensor:
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" \
+            else torch.device("cpu")
+        x = t.to(dev) if t.device != dev else t
+        if send:
+            self._dist.send(x.contiguous(), dst=peer, group=self.group)
+            return t
+        self._dist.recv(x, src=peer, group=self.group)
+        return x.cpu() if x.device != t.device else x
+
+    def send_array(self, arr, dst: int, chunk_bytes: int = 1 << 30) -> None:
+        """``arr`` (numpy) to rank ``dst`` as a fixed-size header and payload messages of at
+        most ``chunk_bytes`` each (recv_array on the peer) -- never one message of the
+        whole block (a pickled row block of a 10M-cell shard would be tens of GB)."""
+        import numpy as np
+
+        a = np.ascontiguousarray(arr)
+        code = self._DTYPES.index(a.dtype.str)
+        if a.ndim > 4:
+            raise ValueError("send_array: at most 4 dimensions")
+        shp = list(a.shape) + [0] * (4 - a.ndim)
+        hdr = torch.tensor([a.ndim] + shp + [code, a.nbytes, int(chunk_bytes)], dtype=torch.int64)
+        self._p2p(hdr, dst, True)
+        raw = torch.from_numpy(a.reshape(-1).view(np.uint8)) if a.nbytes else None
+        for o in range(0, a.nbytes, int(chunk_bytes)):
+            piece = raw[o:o + int(chunk_bytes)]
+            self.max_msg_bytes = max(self.max_msg_bytes, piece.numel())
+            self._p2p(piece, dst, True)
+
+    def recv_array(self, src: int):
+        """The array rank ``src`` sends with send_array."""
+        import numpy as np
+
+        hdr = self._p2p(torch.zeros(8, dtype=torch.int64), src, False).tolist()
+        nd, shp, code, nbytes, cb = hdr[0], hdr[1:1 + hdr[0]], hdr[5], hdr[6], hdr[7]
+        out = np.empty(nbytes, dtype=np.uint8)
+        ot = torch.from_numpy(out)
+        for o in range(0, nbytes, cb):
+            n = min(cb, nbytes - o)
+            ot[o:o + n].copy_(self._p2p(torch.empty(n, dtype=torch.uint8), src, False))
+        return out.view(np.dtype(self._DTYPES[code])).reshape(shp)
+
     def recv_object(self, src: int):
         """Point-to-point: the object rank ``src`` sends with send_object."""
         box = [None]

@@ -439,3 +439,167 @@ def read_any(path: str, densify: bool = False):
     if path.endswith(".mtx") or path.endswith(".mtx.gz"):
         return read_10x_mtx(os.path.dirname(path))
     return read_counts_table(path, densify)
+
+
+# ----------------------------------------------------------------------------- row shards
+def count_table_rows(path: str) -> int:
+    """Data rows of a TSV counts table (lines after the header), counted in 16 MB reads."""
+    n = 0
+    last = b"\n"
+    with open(path, "rb") as fh:
+        while True:
+            buf = fh.read(1 << 24)
+            if not buf:
+                break
+            n += buf.count(b"\n")
+            last = buf[-1:]
+    if last != b"\n":
+        n += 1
+    return max(0, n - 1)
+
+
+def _npy_member(z, name: str):
+    """(file object positioned at the array data, shape, fortran_order, dtype) of a .npy
+    member of an open zip file."""
+    fh = z.open(name)
+    version = np.lib.format.read_magic(fh)
+    if version == (1, 0):
+        shape, fortran, dtype = np.lib.format.read_array_header_1_0(fh)
+    else:
+        shape, fortran, dtype = np.lib.format.read_array_header_2_0(fh)
+    return fh, shape, fortran, dtype
+
+
+def read_npz_df_rows(path: str, a: int, b: int):
+    """Rows [a, b) of a DataFrame-codec ``.df.npz`` (save_df_to_npz) without reading the
+    others into memory: the ``data`` member is streamed (stored members are sought past,
+    deflated ones decompressed and discarded in 16 MB pieces up to row a).  Returns
+    (values, index[a:b], columns, n_rows), or None when the member cannot be streamed
+    (object arrays of the original cnmf, Fortran order)."""
+    import zipfile
+
+    with zipfile.ZipFile(path) as z:
+        names = set(z.namelist())
+        if "data.npy" not in names:
+            return None
+        fh, shape, fortran, dtype = _npy_member(z, "data.npy")
+        with fh:
+            if dtype.hasobject or fortran or len(shape) != 2:
+                return None
+            n, G = shape
+            a, b = max(0, min(a, n)), max(0, min(b, n))
+            row_bytes = G * dtype.itemsize
+            skip = a * row_bytes
+            while skip > 0:
+                got = len(fh.read(min(skip, 1 << 24)))
+                if got == 0:
+                    raise ValueError(f"{path}: truncated data member")
+                skip -= got
+            raw = fh.read((b - a) * row_bytes)
+            vals = np.frombuffer(raw, dtype=dtype).reshape(b - a, G).copy()
+        with np.load(path, allow_pickle=False) as f:
+            index, columns = f["index"], f["columns"]
+    return vals, index[a:b], columns, n
+
+
+def read_10x_mtx_rows(path: str, a: int | None, b: int | None, rank_of=None,
+                      var_names: str = "gene_symbols", make_unique: bool = True):
+    """Cells [a, b) of a 10x ``matrix.mtx[.gz]`` directory (genes x cells on disk): the
+    coordinate entries are streamed in 4M-entry pieces and only this block's cells kept,
+    so a rank never holds more than its own cells.  ``a``/``b`` None: from ``rank_of``
+    (n_cells -> (a, b)).  Returns (AnnData of the block, n_cells)."""
+    import scipy.sparse as sp
+
+    from .anndata_lite import AnnData
+
+    with _open_maybe_gz(os.path.join(path, "matrix.mtx")) as fh:
+        line = fh.readline()
+        while line.startswith(b"%"):
+            line = fh.readline()
+        n_genes, n_cells, _ = (int(v) for v in line.split())
+        if a is None:
+            a, b = rank_of(n_cells)
+        rows_, cols_, vals_ = [], [], []
+        for part in pd.read_csv(fh, sep=r"\s+", header=None, chunksize=1 << 22,
+                                dtype={0: np.int64, 1: np.int64, 2: np.float64}, engine="c"):
+            g = part[0].to_numpy() - 1
+            c = part[1].to_numpy() - 1
+            keep = (c >= a) & (c < b)
+            if keep.any():
+                rows_.append(c[keep] - a)
+                cols_.append(g[keep])
+                vals_.append(part[2].to_numpy()[keep].astype(np.float32))
+    r = np.concatenate(rows_) if rows_ else np.zeros(0, np.int64)
+    cc = np.concatenate(cols_) if cols_ else np.zeros(0, np.int64)
+    v = np.concatenate(vals_) if vals_ else np.zeros(0, np.float32)
+    X = sp.csr_matrix((v, (r, cc)), shape=(b - a, n_genes), dtype=np.float32)
+    X.sum_duplicates()
+    genes_file = None
+    for cand in ("features.tsv", "genes.tsv"):
+        if os.path.exists(os.path.join(path, cand)) or os.path.exists(
+                os.path.join(path, cand + ".gz")):
+            genes_file = cand
+            break
+    if genes_file is None:
+        raise FileNotFoundError(f"no features.tsv/genes.tsv in {path}")
+    with _open_maybe_gz(os.path.join(path, genes_file)) as fh:
+        genes = pd.read_csv(fh, sep="\t", header=None)
+    with _open_maybe_gz(os.path.join(path, "barcodes.tsv")) as fh:
+        barcodes = pd.read_csv(fh, sep="\t", header=None)[0].astype(str).values[a:b]
+    ids = genes[0].astype(str).values
+    symbols = genes[1].astype(str).values if genes.shape[1] > 1 else ids
+    names = symbols if var_names == "gene_symbols" else ids
+    var = pd.DataFrame(index=pd.Index(names))
+    var["gene_ids"] = ids
+    if genes.shape[1] > 2:
+        var["feature_types"] = genes[2].astype(str).values
+    ad = AnnData(X=X, obs=pd.DataFrame(index=pd.Index(barcodes)), var=var)
+    if make_unique:
+        ad.var_names_make_unique()
+    return ad, n_cells
+
+
+def read_rows_any(path: str, rank_of, densify: bool = False):
+    """This rank's block of cells of any prepare input (cnmf.py:518-541 formats), read
+    without loading the other ranks' cells: ``rank_of(n_rows) -> (a, b)``.  h5ad: partial
+    HDF5 reads; 10x mtx: streamed entries; DataFrame npz: streamed ``data`` member; TSV:
+    the block's lines.  Returns (AnnData of rows [a, b), n_rows, (a, b))."""
+    import scipy.sparse as sp
+
+    from .anndata_lite import AnnData
+    from .h5ad import h5ad_shape, read_X_rows, read_h5ad_annotations
+
+    if path.endswith(".h5ad"):
+        n_rows, _ = h5ad_shape(path)
+        a, b = rank_of(n_rows)
+        ann = read_h5ad_annotations(path)
+        return AnnData(X=read_X_rows(path, a, b), obs=ann.obs.iloc[a:b], var=ann.var), n_rows, (a, b)
+    if path.endswith(".mtx") or path.endswith(".mtx.gz"):
+        holder = {}
+
+        def ro(n):
+            holder["ab"] = rank_of(n)
+            return holder["ab"]
+        ad, n_rows = read_10x_mtx_rows(os.path.dirname(path), None, None, rank_of=ro)
+        return ad, n_rows, holder["ab"]
+    if path.endswith(".npz"):
+        import zipfile
+
+        with zipfile.ZipFile(path) as z:
+            fh, shape, _, _ = _npy_member(z, "data.npy")
+            fh.close()
+        n_rows = int(shape[0])
+        a, b = rank_of(n_rows)
+        got = read_npz_df_rows(path, a, b)
+        if got is None:                      # not streamable: whole file (rare)
+            full = read_counts_table(path, densify)
+            return AnnData(X=full.X[a:b], obs=full.obs.iloc[a:b], var=full.var), n_rows, (a, b)
+        vals, index, columns, _ = got
+    else:
+        n_rows = count_table_rows(path)
+        a, b = rank_of(n_rows)
+        df = pd.read_csv(path, sep="\t", index_col=0, skiprows=range(1, a + 1), nrows=b - a)
+        vals, index, columns = df.values, df.index, df.columns
+    X = vals if densify else sp.csr_matrix(vals)
+    return AnnData(X=X, obs=pd.DataFrame(index=pd.Index(index).astype(str)),
+                   var=pd.DataFrame(index=pd.Index(columns).astype(str))), n_rows, (a, b)

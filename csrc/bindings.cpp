@@ -37,6 +37,15 @@ PYBIND11_MODULE(_hip, m) {
   m.def("solve_mfma_max_cols", [](int K) { return cnmf_solve_mfma_max_cols(K); });
   m.def("solve_pipe_tiles", [](int K, int per) { return cnmf_solve_pipe_tiles(K, per); });
   m.def("solve_pipe_k", [](int K) { return cnmf_solve_pipe_k(K); });
+  m.def("exact_moments",
+        [](uintptr_t X, int is_f64, long long ld, long long rows, int G, int chunks,
+           uintptr_t part, uintptr_t out, uintptr_t bad, uintptr_t stream) {
+          check(cnmf_exact_moments(reinterpret_cast<const void*>(X), is_f64, ld, rows, G, chunks,
+                                   P<long long>(part), P<long long>(out),
+                                   P<unsigned long long>(bad),
+                                   reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_exact_moments");
+        });
   m.def("predict_err",
         [](uintptr_t X, long long ldx, uintptr_t U, long long ldu, uintptr_t S, long long lds,
            int N, int G, int K, uintptr_t part, uintptr_t stream) {

@@ -753,6 +753,148 @@ static void write_png_rgba(const std::string& path, py::array_t<uint8_t, py::arr
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Exact column moments (sum x, sum x^2 per column) as integer digit vectors: every value
+// x = +-m 2^e (m < 2^53) is added EXACTLY into base-2^32 digits held in int64 (each add
+// contributes < 2^32 per digit, so 2^31 adds per digit cannot overflow).  Integer sums
+// are associative: any row partition -- threads, row blocks, the ranks of a sharded
+// prepare all-reducing the digits -- gives the identical totals, from which mean and
+// variance are rounded ONCE (cnmf_torch_amd.models.hvg.exact_mean_var).  Window: |x| in
+// [2^-126, 2^127] (float32's normal range); anything else is counted in `outside` and the
+// caller falls back to floating-point statistics.
+constexpr int kExLsb1 = -192, kExD1 = 13;     // sums: bits [2^-192, 2^224)
+constexpr int kExLsb2 = -384, kExD2 = 25;     // squares: bits [2^-384, 2^416)
+
+static inline bool ex_add(double x, long long* d1, long long* d2) {
+  if (x == 0.0) return true;
+  const double ax = std::fabs(x);
+  if (!(ax >= 0x1p-126 && ax <= 0x1p127)) return false;
+  int E;
+  const double f = std::frexp(ax, &E);                  // ax = f 2^E, f in [0.5, 1)
+  const uint64_t m = (uint64_t)std::ldexp(f, 53);        // exact: 53-bit integer
+  const int e = E - 53;                                  // ax = m 2^e
+  const long long sg = x < 0.0 ? -1 : 1;
+  {
+    const int s = e - kExLsb1, dd = s >> 5, o = s & 31;
+    const unsigned __int128 v = (unsigned __int128)m << o;
+    d1[dd] += sg * (long long)(uint64_t)(v & 0xFFFFFFFFu);
+    d1[dd + 1] += sg * (long long)(uint64_t)((v >> 32) & 0xFFFFFFFFu);
+    d1[dd + 2] += sg * (long long)(uint64_t)(v >> 64);
+  }
+  {
+    const unsigned __int128 mm = (unsigned __int128)m * m;   // < 2^106
+    const int s = 2 * e - kExLsb2, dd = s >> 5, o = s & 31;
+    const unsigned __int128 lo = mm << o;                      // low 128 bits
+    const uint64_t hi = o ? (uint64_t)(mm >> (128 - o)) : 0;   // bits >= 128
+    d2[dd] += (long long)(uint64_t)(lo & 0xFFFFFFFFu);
+    d2[dd + 1] += (long long)(uint64_t)((lo >> 32) & 0xFFFFFFFFu);
+    d2[dd + 2] += (long long)(uint64_t)((lo >> 64) & 0xFFFFFFFFu);
+    d2[dd + 3] += (long long)(uint64_t)(lo >> 96);
+    d2[dd + 4] += (long long)hi;
+  }
+  return true;
+}
+
+// CSR (any row partition): entries [0, nnz) with column indices; threads split the entries
+// and each keeps private digits, summed at the end (integer: exact in any order)
+template <typename T, typename I>
+static long long ex_csr_impl(const T* data, const I* idx, long long nnz, long long G,
+                             long long* out1, long long* out2, int threads) {
+  threads = std::max(1, std::min(threads, (int)std::max(1LL, nnz / 65536)));
+  std::vector<std::vector<long long>> p1(threads), p2(threads);
+  std::vector<long long> bad(threads, 0);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t) {
+    pool.emplace_back([&, t] {
+      p1[t].assign(G * kExD1, 0);
+      p2[t].assign(G * kExD2, 0);
+      const long long a = nnz * t / threads, b = nnz * (t + 1) / threads;
+      for (long long e = a; e < b; ++e) {
+        const long long c = (long long)idx[e];
+        if (!ex_add((double)data[e], p1[t].data() + c * kExD1, p2[t].data() + c * kExD2))
+          ++bad[t];
+      }
+    });
+  }
+  for (auto& th : pool) th.join();
+  long long nb = 0;
+  for (int t = 0; t < threads; ++t) {
+    nb += bad[t];
+    for (long long i = 0; i < G * kExD1; ++i) out1[i] += p1[t][i];
+    for (long long i = 0; i < G * kExD2; ++i) out2[i] += p2[t][i];
+  }
+  return nb;
+}
+
+// dense row-major (rows x G, row stride ld): rows split over threads
+template <typename T>
+static long long ex_dense_impl(const T* X, long long rows, long long G, long long ld,
+                               long long* out1, long long* out2, int threads) {
+  threads = std::max(1, std::min(threads, (int)std::max(1LL, rows * G / 65536)));
+  std::vector<std::vector<long long>> p1(threads), p2(threads);
+  std::vector<long long> bad(threads, 0);
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t) {
+    pool.emplace_back([&, t] {
+      p1[t].assign(G * kExD1, 0);
+      p2[t].assign(G * kExD2, 0);
+      const long long a = rows * t / threads, b = rows * (t + 1) / threads;
+      for (long long r = a; r < b; ++r)
+        for (long long c = 0; c < G; ++c)
+          if (!ex_add((double)X[r * ld + c], p1[t].data() + c * kExD1, p2[t].data() + c * kExD2))
+            ++bad[t];
+    });
+  }
+  for (auto& th : pool) th.join();
+  long long nb = 0;
+  for (int t = 0; t < threads; ++t) {
+    nb += bad[t];
+    for (long long i = 0; i < G * kExD1; ++i) out1[i] += p1[t][i];
+    for (long long i = 0; i < G * kExD2; ++i) out2[i] += p2[t][i];
+  }
+  return nb;
+}
+
+// returns (digits1 int64 (G, D1), digits2 int64 (G, D2), values outside the window)
+static py::tuple exact_col_moments(py::array data, py::object indices, long long G, int threads) {
+  py::array_t<long long> d1({G, (long long)kExD1}), d2({G, (long long)kExD2});
+  std::memset(d1.mutable_data(), 0, sizeof(long long) * G * kExD1);
+  std::memset(d2.mutable_data(), 0, sizeof(long long) * G * kExD2);
+  py::array d = py::array::ensure(data, py::array::c_style);
+  long long bad = 0;
+  auto run_dense = [&](auto tag) {
+    using T = decltype(tag);
+    if (d.ndim() != 2 || d.shape(1) != G) throw std::invalid_argument("exact_col_moments: (rows, G)");
+    const T* xp = (const T*)d.data();
+    const long long rows = d.shape(0);
+    py::gil_scoped_release nogil;
+    bad = ex_dense_impl(xp, rows, G, G, d1.mutable_data(), d2.mutable_data(), threads);
+  };
+  if (indices.is_none()) {
+    if (py::isinstance<py::array_t<double>>(d)) run_dense(double{});
+    else if (py::isinstance<py::array_t<float>>(d)) run_dense(float{});
+    else throw std::invalid_argument("exact_col_moments: float32 or float64 data");
+    return py::make_tuple(d1, d2, bad);
+  }
+  py::array ix = py::array::ensure(indices, py::array::c_style);
+  const long long nnz = d.size();
+  if (ix.size() != nnz) throw std::invalid_argument("exact_col_moments: data / indices sizes");
+  const bool i64 = py::isinstance<py::array_t<long long>>(ix) || py::isinstance<py::array_t<int64_t>>(ix);
+  if (!i64 && !py::isinstance<py::array_t<int>>(ix))
+    throw std::invalid_argument("exact_col_moments: int32 or int64 indices");
+  auto run = [&](auto tag) {
+    using T = decltype(tag);
+    const T* dp = (const T*)d.data();
+    py::gil_scoped_release nogil;
+    if (i64) bad = ex_csr_impl(dp, (const long long*)ix.data(), nnz, G, d1.mutable_data(), d2.mutable_data(), threads);
+    else bad = ex_csr_impl(dp, (const int*)ix.data(), nnz, G, d1.mutable_data(), d2.mutable_data(), threads);
+  };
+  if (py::isinstance<py::array_t<double>>(d)) run(double{});
+  else if (py::isinstance<py::array_t<float>>(d)) run(float{});
+  else throw std::invalid_argument("exact_col_moments: float32 or float64 data");
+  return py::make_tuple(d1, d2, bad);
+}
+
 PYBIND11_MODULE(_npzio, m) {
   m.doc() = "cnmf_torch_amd native replicate-file writer/reader (stored npz, crc32, sha256)";
   m.def("write_spectra_batch", &write_spectra_batch, py::arg("paths"), py::arg("data"),
@@ -762,6 +904,10 @@ PYBIND11_MODULE(_npzio, m) {
   m.def("write_tsv", &write_tsv, py::arg("path"), py::arg("corner"), py::arg("columns"),
         py::arg("index"), py::arg("data"), py::arg("threads") = 16);
   m.def("csr_mean_var", &csr_mean_var);
+  m.def("exact_col_moments", &exact_col_moments, py::arg("data"), py::arg("indices"),
+        py::arg("G"), py::arg("threads") = 16);
+  m.attr("EXACT_LSB1") = kExLsb1;
+  m.attr("EXACT_LSB2") = kExLsb2;
   m.def("csr_scale_rows", &csr_scale_rows, py::arg("data"), py::arg("indptr"), py::arg("scale"),
         py::arg("threads") = 16);
   m.def("sha256_hex", &sha256_hex);

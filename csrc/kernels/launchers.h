@@ -34,6 +34,9 @@ int cnmf_solve_reg_max_cols(int K);
 int cnmf_solve_mfma_max_cols(int K);
 int cnmf_solve_pipe_tiles(int K, int per);
 int cnmf_solve_pipe_k(int K);
+hipError_t cnmf_exact_moments(const void* X, int is_f64, long long ld, long long rows, int G,
+                              int chunks, long long* part, long long* out,
+                              unsigned long long* bad, hipStream_t stream);
 hipError_t cnmf_predict_err(const float* X, long long ldx, const double* U, long long ldu,
                             const double* S, long long lds, int N, int G, int K, double* part,
                             hipStream_t stream);

@@ -215,38 +215,64 @@ def test_rank_failure_then_resume_on_a_different_world_size(prepared):
             np.testing.assert_allclose(a, b, rtol=2e-3, atol=1e-6)
 
 
-@pytest.mark.parametrize("fmt", ["h5ad_sparse", "npz_dense"])
+def _write_10x(d, X, cells, genes):
+    import scipy.io
+    import scipy.sparse as sp
+
+    os.makedirs(d, exist_ok=True)
+    scipy.io.mmwrite(os.path.join(d, "matrix.mtx"), sp.coo_matrix(np.asarray(X).T))
+    with open(os.path.join(d, "features.tsv"), "w") as fh:
+        fh.write("".join(f"{g}\t{g}\tGene Expression\n" for g in genes))
+    with open(os.path.join(d, "barcodes.tsv"), "w") as fh:
+        fh.write("".join(f"{c}\n" for c in cells))
+    return os.path.join(d, "matrix.mtx")
+
+
+@pytest.mark.parametrize("fmt", ["h5ad_sparse", "npz_dense", "txt_sparse", "mtx_sparse",
+                                 "npz_densify"])
 def test_sharded_prepare_matches_single_process(tmp_path, fmt):
-    """Cell-sharded prepare over 3 gloo ranks (all-reduced two-pass gene statistics) writes
-    the same artifacts as the single-process prepare."""
+    """Cell-sharded prepare over 3 gloo ranks -- each rank reads ONLY its cells (partial
+    h5ad reads, streamed 10x mtx / npz member / TSV lines), gene statistics from exact
+    integer moments all-reduced, row blocks handed to rank 0's writer in messages of at
+    most CNMF_PREPARE_CHUNK_BYTES -- writes artifacts bit-identical to the single-process
+    prepare."""
     from cnmf_torch_amd.utils.anndata_lite import AnnData
     from cnmf_torch_amd.utils.h5ad import read_h5ad, write_h5ad
 
-    Xc, cells, genes = simulate_counts(500, 300, 4, seed=21, sparse=(fmt == "h5ad_sparse"))
+    sparse = fmt in ("h5ad_sparse", "mtx_sparse")
+    Xc, cells, genes = simulate_counts(500, 300, 4, seed=21, sparse=sparse)
     if fmt == "h5ad_sparse":
         fn = str(tmp_path / "counts.h5ad")
         write_h5ad(fn, AnnData(X=Xc, obs=pd.DataFrame(index=cells), var=pd.DataFrame(index=genes)))
+    elif fmt == "mtx_sparse":
+        fn = _write_10x(str(tmp_path / "tenx"), Xc.toarray(), cells, genes)
+    elif fmt == "txt_sparse":
+        fn = str(tmp_path / "counts.txt")
+        pd.DataFrame(np.asarray(Xc), index=cells, columns=genes).to_csv(fn, sep="\t")
     else:
         fn = str(tmp_path / "counts.df.npz")
         save_df_to_npz(pd.DataFrame(Xc, index=cells, columns=genes), fn)
-    kw = dict(components=[3, 4], n_iter=3, seed=7, num_highvar_genes=120)
-    _spawn(W.prepare_worker, 3, str(tmp_path), "sh", fn, kw)
+    bound = 4096
+    kw = dict(components=[3, 4], n_iter=3, seed=7, num_highvar_genes=120,
+              densify=fmt == "npz_densify")
+    _spawn(W.prepare_worker, 3, str(tmp_path), "sh", fn, dict(kw, _chunk_bytes=bound))
+    for r in range(1, 3):
+        m = int(np.load(tmp_path / f"maxmsg{r}.npy")[0])
+        assert 0 < m <= bound, m
     ser = cNMF(output_dir=str(tmp_path), name="se")
     ser.prepare(fn, **kw)
     sh = cNMF(output_dir=str(tmp_path), name="sh")
     assert open(sh.paths["nmf_genes_list"]).read() == open(ser.paths["nmf_genes_list"]).read()
-    # float32 TPM: sklearn accumulates the single-process statistics in float32
-    np.testing.assert_allclose(load_df_from_npz(sh.paths["tpm_stats"]).values,
-                               load_df_from_npz(ser.paths["tpm_stats"]).values, rtol=2e-6)
-    a, b = read_h5ad(sh.paths["normalized_counts"]), read_h5ad(ser.paths["normalized_counts"])
-    xa = a.X.toarray() if hasattr(a.X, "toarray") else a.X
-    xb = b.X.toarray() if hasattr(b.X, "toarray") else b.X
-    np.testing.assert_allclose(xa, xb, rtol=1e-10, atol=1e-12)
-    assert list(a.obs.index) == list(b.obs.index) and list(a.var.index) == list(b.var.index)
-    ta, tb = read_h5ad(sh.paths["tpm"]), read_h5ad(ser.paths["tpm"])
-    xa = ta.X.toarray() if hasattr(ta.X, "toarray") else ta.X
-    xb = tb.X.toarray() if hasattr(tb.X, "toarray") else tb.X
-    np.testing.assert_allclose(xa, xb, rtol=1e-6)
+    sa, sb = load_df_from_npz(sh.paths["tpm_stats"]), load_df_from_npz(ser.paths["tpm_stats"])
+    assert sa.values.dtype == sb.values.dtype
+    np.testing.assert_array_equal(sa.values, sb.values)
+    for key in ("normalized_counts", "tpm"):
+        a, b = read_h5ad(sh.paths[key]), read_h5ad(ser.paths[key])
+        xa = a.X.toarray() if hasattr(a.X, "toarray") else a.X
+        xb = b.X.toarray() if hasattr(b.X, "toarray") else b.X
+        assert xa.dtype == xb.dtype
+        np.testing.assert_array_equal(xa, xb)
+        assert list(a.obs.index) == list(b.obs.index) and list(a.var.index) == list(b.var.index)
     pa = load_df_from_npz(sh.paths["nmf_replicate_parameters"])
     pb = load_df_from_npz(ser.paths["nmf_replicate_parameters"])
     assert pa.equals(pb)

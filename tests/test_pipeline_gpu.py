@@ -16,7 +16,13 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(tmp, fn, early: str, monkeypatch):
+    from cnmf_torch_amd.models import nmf
+
     monkeypatch.setenv("CNMF_EARLY_WRITE", early)
+    # early writes retire replicates at host compactions: compare against the same
+    # compacting schedule (the default device-slot batching never compacts, so its GEMM
+    # split plans -- and fp32 rounding -- differ)
+    monkeypatch.setattr(nmf, "_DEV_SLOTS", False)
     obj = cNMF(output_dir=str(tmp / f"early{early}"), name="g")
     obj.prepare(fn, components=[4, 5, 6], n_iter=40, seed=5, num_highvar_genes=300,
                 batch_size=400)

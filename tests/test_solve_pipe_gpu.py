@@ -301,10 +301,12 @@ def test_gemm_planes_live_rows_skip_dead_tiles(monkeypatch):
     monkeypatch.setenv("CNMF_GEMM_KSPLIT", "1")
     ops.refresh_env()
     try:
+        full1 = torch.empty((M, N), device="cuda")      # the same plan, every row
+        ops.gemm_planes(full1, Ap[:2], Bp, M, N, K)
         C = torch.full((M, N), float("nan"), device="cuda")
         ops.gemm_planes(C, Ap[:2], Bp, M, N, K, live=live)
         torch.cuda.synchronize()
-        assert torch.equal(C[:333], full[:333])
+        assert torch.equal(C[:333], full1[:333])
         assert torch.isnan(C[512:]).all()
     finally:
         monkeypatch.delenv("CNMF_GEMM_KSPLIT")
@@ -352,3 +354,28 @@ def test_predict_err_kernel_matches_float64(N, G, K):
     err = cNMF._prediction_error(X.cuda(), U.numpy(), S.numpy(), torch.device("cuda"))
     full = float(((Xd - U @ S) ** 2).sum())
     assert abs(err - full) <= 1e-9 * full
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.float64])
+def test_exact_moments_device_equals_host_digits(dt):
+    """exact_moments.hip and the host exact_col_moments produce the SAME integer digits
+    (exact sums of x and x^2 per column), so statistics from either -- or from any row
+    split of either -- are bit-identical; they equal float64 numpy to rounding."""
+    from cnmf_torch_amd.models.hvg import (_digits_to_ints, exact_mean_var,
+                                           exact_moment_digits)
+
+    g = torch.Generator().manual_seed(4)
+    X = (torch.rand((9000, 333), generator=g) * 50 - 5).to(dt)
+    X[X.abs() < 1] = 0
+    hd = exact_moment_digits(X.numpy())
+    gd = exact_moment_digits(X.cuda())
+    assert hd[2] == 0 and gd[2] == 0
+    assert _digits_to_ints(hd[0]) == _digits_to_ints(gd[0])
+    assert _digits_to_ints(hd[1]) == _digits_to_ints(gd[1])
+    m_h, v_h = exact_mean_var(X.numpy(), 1)
+    m_g, v_g = exact_mean_var(X.cuda(), 1)
+    np.testing.assert_array_equal(m_h, m_g)
+    np.testing.assert_array_equal(v_h, v_g)
+    Xd = X.double().numpy()
+    np.testing.assert_allclose(m_h, Xd.mean(0), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(v_h, Xd.var(0, ddof=1), rtol=1e-10)
