@@ -88,6 +88,8 @@ class Harmony:
         self.Z_cos = Zc / torch.linalg.vector_norm(Zc, dim=0)
         self.Phi = torch.as_tensor(Phi, dtype=dt, device=dev)
         self.Phi_moe = torch.as_tensor(Phi_moe, dtype=dt, device=dev)
+        # level structure of the design for the matrix-core ridge kernels (ridge.hip)
+        self._lv = _levels(np.asarray(Phi_moe)) if dev.type == "cuda" else None
         self.Pr_b = torch.as_tensor(Pr_b, dtype=dt, device=dev)
         self.sigma = torch.as_tensor(sigma, dtype=dt, device=dev)
         self.theta = torch.as_tensor(theta, dtype=dt, device=dev)
@@ -164,7 +166,7 @@ class Harmony:
         for _ in range(1, iters + 1):
             self._cluster()
             self.Z_cos, self.Z_corr, self.W = moe_correct_ridge_pcs(
-                self.Z_orig, self.R, self.Phi_moe, self.lamb)
+                self.Z_orig, self.R, self.Phi_moe, self.lamb, levels=self._lv)
             if self._converged(1):
                 break
 
@@ -315,7 +317,14 @@ def _apply_correction(Z: torch.Tensor, W: torch.Tensor, R: torch.Tensor, Phi_moe
 
 
 def moe_correct_ridge_pcs(Z_orig: torch.Tensor, R: torch.Tensor, Phi_moe: torch.Tensor,
-                          lamb: torch.Tensor):
+                          lamb: torch.Tensor, levels=None):
+    if levels is not None and Z_orig.is_cuda and ops.use_native(Z_orig):
+        # the PCs (d x N) through the level-segment kernels (ridge.hip), cells x d
+        Zc, Wk = _ridge_native(Z_orig.t().contiguous(), R.t().contiguous(), levels, lamb,
+                               return_w=True)
+        Z_corr = Zc.t()
+        Z_cos = Z_corr / torch.linalg.vector_norm(Z_corr, dim=0)
+        return Z_cos, Z_corr, Wk.reshape(-1, Wk.shape[2])
     W = _ridge_weights(Z_orig, R, Phi_moe, lamb)
     Z_corr = _apply_correction(Z_orig, W, R, Phi_moe)
     Z_cos = Z_corr / torch.linalg.vector_norm(Z_corr, dim=0)
@@ -340,6 +349,97 @@ def moe_correct_ridge(Z_orig, Z_cos, Z_corr, R, W, K, Phi_Rk, Phi_moe, lamb, dev
     return Zcos.cpu().numpy(), Zc.cpu().numpy(), W_last, Phi_Rk
 
 
+def _levels(Phi_moe: np.ndarray):
+    """Level structure of a Harmony design [1; one-hot levels] (B1 x N): per row b the
+    cells of that level, and per cell its combination of levels (plus a per-device cache
+    of the index tensors the kernels read).  None when Phi_moe is not of that form (the
+    dense path then applies)."""
+    P = np.asarray(Phi_moe)
+    if P.ndim != 2 or P.shape[0] < 1 or not np.all(P[0] == 1.0) or \
+            not np.all((P == 0.0) | (P == 1.0)):
+        return None
+    B1, N = P.shape
+    cells = [np.arange(N)] + [np.flatnonzero(P[b]) for b in range(1, B1)]
+    keys, inv = np.unique(P[1:].T.astype(np.uint8), axis=0, return_inverse=True)
+    inv = np.asarray(inv).reshape(-1)
+    if keys.shape[0] > 4096:
+        return None
+    lev = [np.flatnonzero(row) + 1 for row in keys]
+    return {"cells": cells, "inv": inv, "lev": lev, "N": N, "B1": B1, "dev": {}}
+
+
+def _level_tensors(lv: dict, dev: torch.device) -> dict:
+    """Device index tensors of a level structure (built once per device)."""
+    key = str(dev)
+    t = lv["dev"].get(key)
+    if t is not None:
+        return t
+    cells, inv, lev = lv["cells"], lv["inv"], lv["lev"]
+    B1, N = lv["B1"], lv["N"]
+    Pm = np.zeros((N, B1))
+    for b, cl in enumerate(cells):
+        Pm[cl, b] = 1.0
+    L = max(len(v) for v in lev)
+    tab = np.zeros((len(lev), L), dtype=np.int64)
+    for c, v in enumerate(lev):
+        tab[c, :len(v)] = v
+    order = np.argsort(inv, kind="stable").astype(np.int32)
+    cnt = np.bincount(inv, minlength=len(lev))
+    starts = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    blk = [(c, int(starts[c]) + o, int(min(64, cnt[c] - o)))
+           for c in range(len(lev)) for o in range(0, int(cnt[c]), 64)]
+    t = {"idx": torch.from_numpy(np.concatenate(cells).astype(np.int32)).to(dev),
+         "seg": torch.from_numpy(np.concatenate([[0], np.cumsum([c.size for c in cells])])
+                                 .astype(np.int64)).to(dev),
+         "Pt": torch.from_numpy(Pm).to(dev),
+         "tab": torch.from_numpy(tab).to(dev),
+         "order": torch.from_numpy(order).to(dev),
+         "blk": torch.from_numpy(np.asarray(blk, dtype=np.int32).reshape(-1)).to(dev),
+         "nblk": len(blk)}
+    lv["dev"][key] = t
+    return t
+
+
+def _ridge_native(X: torch.Tensor, Rt: torch.Tensor, lv: dict, Lt: torch.Tensor,
+                  return_w: bool = False):
+    """The MOE ridge correction on the f64 matrix cores (csrc/kernels/ridge.hip) for a
+    cells x features X and R^T (cells x clusters): level-segment products for Y and the
+    ridge Grams, float64 solves of the (B+1) x (B+1) systems on the host (no library
+    GEMM), one combination-grouped correction pass rounded once."""
+    h = ops._hip
+    dev = X.device
+    t = _level_tensors(lv, dev)
+    N, F = X.shape
+    Kc = Rt.shape[1]
+    B1 = lv["B1"]
+    st = ops._stream_ptr(X)
+    # Y[b][k][f] = sum over level b's cells of R[k, n] X[n, f]
+    Y = torch.empty((B1, Kc, F), dtype=torch.float64, device=dev)
+    h.ridge_seg_tgemm(Rt.data_ptr(), Rt.stride(0), Kc, X.data_ptr(), int(X.dtype == torch.float64),
+                      X.stride(0), F, t["idx"].data_ptr(), t["seg"].data_ptr(), B1, Y.data_ptr(),
+                      Kc * F, F, st)
+    # A0[b][k][c] = sum over level b's cells of R[k, n] Phi[c, n]
+    Pt = t["Pt"]
+    A0 = torch.empty((B1, Kc, B1), dtype=torch.float64, device=dev)
+    h.ridge_seg_tgemm(Rt.data_ptr(), Rt.stride(0), Kc, Pt.data_ptr(), 1, Pt.stride(0), B1,
+                      t["idx"].data_ptr(), t["seg"].data_ptr(), B1, A0.data_ptr(), Kc * B1, B1, st)
+    A = A0.permute(1, 0, 2).cpu().numpy() + Lt.cpu().numpy()[None]        # (Kc, B1, B1)
+    Wh = np.linalg.solve(A, Y.permute(1, 0, 2).cpu().numpy())               # (Kc, B1, F)
+    Wh[:, 0, :] = 0.0                                    # keep the intercept
+    W = torch.from_numpy(Wh).to(dev)
+    # per level combination: Wc = sum of its levels' W_b (W_0 = 0 pads short lists)
+    tab = t["tab"]
+    Wc = torch.zeros((tab.shape[0], Kc, F), dtype=torch.float64, device=dev)
+    Wp = W.permute(1, 0, 2)                              # (B1, Kc, F) view
+    for j in range(tab.shape[1]):
+        Wc += Wp.index_select(0, tab[:, j])
+    out = torch.empty_like(X)
+    h.ridge_apply(Rt.data_ptr(), Rt.stride(0), Kc, X.data_ptr(), int(X.dtype == torch.float64),
+                  X.stride(0), out.data_ptr(), out.stride(0), F, t["order"].data_ptr(),
+                  t["blk"].data_ptr(), t["nblk"], Wc.data_ptr(), Kc * F, F, st)
+    return (out, W) if return_w else out
+
+
 def moe_correct_expression(X: torch.Tensor, R, Phi_moe, lamb, K: int | None = None,
                            chunk: int = 65536) -> torch.Tensor:
     """The MOE ridge correction of preprocess.py:9-18 applied to a device-resident
@@ -352,8 +452,13 @@ def moe_correct_expression(X: torch.Tensor, R, Phi_moe, lamb, K: int | None = No
     Rt = torch.as_tensor(np.asarray(R), dtype=torch.float64).to(dev)
     if K is not None:
         Rt = Rt[:int(K)]
-    Pt = torch.as_tensor(np.asarray(Phi_moe), dtype=torch.float64).to(dev)
     Lt = torch.as_tensor(np.asarray(lamb), dtype=torch.float64).to(dev)
+    if dev.type == "cuda" and ops.use_native(X) and X.dtype in (torch.float32, torch.float64) \
+            and X.dim() == 2 and (X.shape[1] <= 1 or X.stride(1) == 1):
+        lv = _levels(Phi_moe)
+        if lv is not None:   # the f64 matrix-core kernels (no materialised Phi_Rk)
+            return _ridge_native(X, Rt.t().contiguous(), lv, Lt)
+    Pt = torch.as_tensor(np.asarray(Phi_moe), dtype=torch.float64).to(dev)
     Kc, N = Rt.shape
     B1 = Pt.shape[0]
     F = X.shape[1]

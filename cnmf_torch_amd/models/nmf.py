@@ -997,12 +997,18 @@ _LAYOUT_REPLAY = os.environ.get("CNMF_LAYOUT_REPLAY", "1") != "0"
 # (profiles/r3ah_bench_{on,off}_*)
 _GEMM_GATE = os.environ.get("CNMF_GEMM_GATE", "0") == "1"
 _FLAG_STREAM = os.environ.get("CNMF_FLAG_STREAM", "0") == "1"
-# Device-side ragged batching of the fused step (CNMF_DEV_SLOTS=0: off).  conv_update gives
-# the live replicates compact row slots every pass; the solves write the GEMM operands and
-# read the GEMM outputs at those slots and the plane GEMMs skip the dead M-tiles, so GEMM
-# work falls with the active fraction on a FIXED launch shape (one captured graph per run,
-# no host compaction; SURVEY.md §7.4.3, the reference syncs per iteration at cnmf.py:377)
-_DEV_SLOTS = os.environ.get("CNMF_DEV_SLOTS", "1") != "0"
+# Device-side ragged batching of the fused step.  conv_update gives the live replicates
+# compact row slots every pass; the solves write the GEMM operands and read the GEMM
+# outputs at those slots and the plane GEMMs skip the dead M-tiles, so GEMM work falls
+# with the active fraction on a FIXED launch shape (one captured graph per run, no host
+# compaction; SURVEY.md §7.4.3, the reference syncs per iteration at cnmf.py:377).
+# Measured (profiles/r4b_*): K = 20 5,034 vs 4,803 rep/s without; K = 10 11,400 vs 12,735
+# -- at K <= 16 the split GEMMs are latency-bound (< 3 workgroup rounds), so dropping dead
+# M-tiles barely shortens them (195 -> 142 us per pass), while the host compaction it
+# replaces re-plans the few-replicate tail GEMMs with deeper k splits (212 vs 320 us per
+# tail pass).  CNMF_DEV_SLOTS: 'auto' (default) = batches whose largest K > 16, '1' always,
+# '0' never.
+_DEV_SLOTS = os.environ.get("CNMF_DEV_SLOTS", "auto")
 # fused step: split-K GEMMs of up to this many k slices hand their raw slabs to the
 # consuming solve; deeper splits (the few-replicate tail) are reduced by the GEMM's own
 # pass -- the solve would read every slab per element (CNMF_FUSED_MAX_SLABS overrides)
@@ -1935,7 +1941,9 @@ class NMFBatchSolver:
         graph, graph_key, last_key = None, None, None
         fused = self._fused_ok(st, steps)
         # (early replicate writes hand over retired replicates at host compactions)
-        st.dslots = self._dev_slots(st) if (fused and _DEV_SLOTS and st.on_retire is None
+        slots_on = (_DEV_SLOTS == "1" or _DEV_SLOTS is True
+                    or (_DEV_SLOTS == "auto" and int(np.max(st.kpos[:st.n_act])) > 16))
+        st.dslots = self._dev_slots(st) if (fused and slots_on and st.on_retire is None
                                             and not dist) else None
         # device slots / DP fused: the batch keeps one layout (no host compaction: 2.0 never
         # fires) -- the DP W-solve owns a fixed partition and only its rows of W are fresh

@@ -201,9 +201,11 @@ class DistComm(LocalComm):
         if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():
             self._dist.all_gather_into_tensor(out, inp, group=self.group)
             return out
-        parts = [torch.empty(m, dtype=inp.dtype) for _ in range(self.world_size)]
-        self._dist.all_gather(parts, inp.reshape(-1).cpu().contiguous(), group=self.group)
-        out.reshape(-1).copy_(torch.cat(parts))
+        # gloo: as raw bytes (it has no int16 / bfloat16 all-gather)
+        src = inp.reshape(-1).cpu().contiguous().view(torch.uint8)
+        parts = [torch.empty(src.numel(), dtype=torch.uint8) for _ in range(self.world_size)]
+        self._dist.all_gather(parts, src, group=self.group)
+        out.reshape(-1).copy_(torch.cat(parts).view(inp.dtype))
         return out
 
     def send_object(self, obj, dst: int) -> None:

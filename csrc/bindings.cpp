@@ -46,6 +46,26 @@ PYBIND11_MODULE(_hip, m) {
                                    reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_exact_moments");
         });
+  m.def("ridge_seg_tgemm",
+        [](uintptr_t Rt, long long ldr, int Kc, uintptr_t X, int x_f64, long long ldx, int F,
+           uintptr_t idx, uintptr_t seg, int nseg, uintptr_t out, long long seg_stride,
+           long long ldo, uintptr_t stream) {
+          check(cnmf_ridge_seg_tgemm(P<const double>(Rt), ldr, Kc, reinterpret_cast<const void*>(X),
+                                     x_f64, ldx, F, P<const int>(idx), P<const long long>(seg),
+                                     nseg, P<double>(out), seg_stride, ldo,
+                                     reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_ridge_seg_tgemm");
+        });
+  m.def("ridge_apply",
+        [](uintptr_t Rt, long long ldr, int Kc, uintptr_t X, int x_f64, long long ldx, uintptr_t Y,
+           long long ldy, int F, uintptr_t order, uintptr_t blk, int nblk, uintptr_t Wc,
+           long long wc_combo, long long ldw, uintptr_t stream) {
+          check(cnmf_ridge_apply(P<const double>(Rt), ldr, Kc, reinterpret_cast<const void*>(X),
+                                 x_f64, ldx, reinterpret_cast<void*>(Y), ldy, F, P<const int>(order),
+                                 P<const int>(blk), nblk, P<const double>(Wc), wc_combo, ldw,
+                                 reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_ridge_apply");
+        });
   m.def("predict_err",
         [](uintptr_t X, long long ldx, uintptr_t U, long long ldu, uintptr_t S, long long lds,
            int N, int G, int K, uintptr_t part, uintptr_t stream) {

@@ -34,6 +34,14 @@ int cnmf_solve_reg_max_cols(int K);
 int cnmf_solve_mfma_max_cols(int K);
 int cnmf_solve_pipe_tiles(int K, int per);
 int cnmf_solve_pipe_k(int K);
+hipError_t cnmf_ridge_seg_tgemm(const double* Rt, long long ldr, int Kc, const void* X, int x_f64,
+                                long long ldx, int F, const int* idx, const long long* seg,
+                                int nseg, double* out, long long seg_stride, long long ldo,
+                                hipStream_t stream);
+hipError_t cnmf_ridge_apply(const double* Rt, long long ldr, int Kc, const void* X, int x_f64,
+                            long long ldx, void* Y, long long ldy, int F, const int* order,
+                            const int* blk, int nblk, const double* Wc, long long wc_combo,
+                            long long ldw, hipStream_t stream);
 hipError_t cnmf_exact_moments(const void* X, int is_f64, long long ld, long long rows, int G,
                               int chunks, long long* part, long long* out,
                               unsigned long long* bad, hipStream_t stream);

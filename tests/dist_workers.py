@@ -203,6 +203,7 @@ def xgmi_dp_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, allreduce):
     """Cell-sharded DP solve on one GPU per process with the all-reduce over xGMI peer
     memory or staged through gloo."""
     os.environ["CNMF_ALLREDUCE"] = allreduce
+    os.environ["CNMF_DP_FUSED"] = "0"     # the all-reduced step (the fused one reduce-scatters)
     # both ranks share one GPU here: no cooperative (co-residency assuming) solves
     os.environ["CNMF_SOLVE_COOP"] = "0"
     _init(rank, world, port)

@@ -379,3 +379,44 @@ def test_exact_moments_device_equals_host_digits(dt):
     Xd = X.double().numpy()
     np.testing.assert_allclose(m_h, Xd.mean(0), rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(v_h, Xd.var(0, ddof=1), rtol=1e-10)
+
+
+@pytest.mark.parametrize("N,F,K,levels", [(5000, 300, 30, (4, 3, 2, 2)), (777, 50, 7, (3,)),
+                                          (20000, 70, 100, (6, 4, 3, 2))])
+def test_moe_ridge_kernels_match_reference_formula(N, F, K, levels):
+    """ridge.hip (level-segment products on the f64 matrix cores, host (B+1)^2 solves,
+    combination-grouped correction) == the reference's moe_correct_ridge formula
+    (preprocess.py:9-18) in float64 to 1e-10, for the expression matrix (cells x genes)
+    and for the PCs inside the Harmony loop; no dense Phi_Rk is formed."""
+    from cnmf_torch_amd.models.harmony import (_levels, moe_correct_expression,
+                                               moe_correct_ridge, moe_correct_ridge_pcs)
+
+    rs = np.random.default_rng(N + F)
+    X = rs.random((N, F)) * 3
+    R = rs.random((K, N))
+    R /= R.sum(0)
+    blocks = []
+    for nl in levels:
+        b = rs.integers(0, nl, N)
+        P = np.zeros((nl, N))
+        P[b, np.arange(N)] = 1
+        blocks.append(P)
+    Phi_moe = np.vstack([np.ones((1, N))] + blocks)
+    B1 = Phi_moe.shape[0]
+    lamb = np.diag([0.0] + [1.0] * (B1 - 1))
+    _, Zc, _, _ = moe_correct_ridge(X.T, None, None, R, None, K, None, Phi_moe, lamb)
+    got = moe_correct_expression(torch.from_numpy(X).cuda(), R, Phi_moe, lamb, K=K)
+    np.testing.assert_allclose(got.cpu().numpy(), Zc.T, rtol=1e-10, atol=1e-10)
+    got32 = moe_correct_expression(torch.from_numpy(X.astype(np.float32)).cuda(), R, Phi_moe,
+                                   lamb, K=K)
+    assert got32.dtype == torch.float32
+    np.testing.assert_allclose(got32.cpu().numpy(), Zc.T.astype(np.float32), rtol=2e-6, atol=2e-6)
+    # the PCs path of the Harmony loop (d x N), W included
+    lv = _levels(Phi_moe)
+    Z = torch.from_numpy(X.T.copy()).cuda()
+    Rd, Pd, Ld = (torch.from_numpy(a).cuda() for a in (R, Phi_moe, lamb))
+    zc_n, zr_n, w_n = moe_correct_ridge_pcs(Z, Rd, Pd, Ld, levels=lv)
+    zc_d, zr_d, w_d = moe_correct_ridge_pcs(Z, Rd, Pd, Ld, levels=None)
+    torch.testing.assert_close(zr_n, zr_d, rtol=1e-10, atol=1e-10)
+    torch.testing.assert_close(zc_n, zc_d, rtol=1e-10, atol=1e-10)
+    torch.testing.assert_close(w_n, w_d, rtol=1e-8, atol=1e-10)

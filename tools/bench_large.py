@@ -124,6 +124,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=0)
     ap.add_argument("--dp", action="store_true", help="cell-sharded data parallel")
     ap.add_argument("--max-pass", type=int, default=20)
+    ap.add_argument("--emulate-world", type=int, default=None,
+                    help="with --dp on ONE process: run rank 0's shard of an N-rank DP job, "
+                         "collectives replaced by device copies (parallel.comm.EmulatedComm): "
+                         "the per-rank step time, value = projected N-GPU job rate")
     ap.add_argument("--planes-only", action="store_true",
                     help="hold X only as split-GEMM planes (10M x 5k on one GPU: fp32 X "
                          "and its planes do not fit together)")
@@ -136,9 +140,18 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-    comm = DistComm() if (world > 1 and a.dp) else LocalComm()
+    emu = a.emulate_world if (a.dp and world == 1 and a.emulate_world and a.emulate_world > 1) \
+        else None
+    if emu:
+        from cnmf_torch_amd.parallel.comm import EmulatedComm
+
+        comm = EmulatedComm(emu)
+    else:
+        comm = DistComm() if (world > 1 and a.dp) else LocalComm()
     N, G = a.cells, a.genes
-    if a.dp:
+    if emu:
+        r0, r1 = 0, N // emu
+    elif a.dp:
         r0, r1 = N * rank // world, N * (rank + 1) // world
     else:
         r0, r1 = 0, N
@@ -183,8 +196,12 @@ def main():
             "s_per_step": round(el / a.steps, 3), "mean_passes": round(float(np.mean(passes)), 2),
             "data_gen_s": round(t_gen, 2), "dtype": "fp32",
             "config": {"cells": N, "genes": G, "k": a.k, "replicates_per_step": a.reps * (
-                1 if a.dp else world), "parallelism": f"{'dp' if a.dp else 'replicate'}x{world}",
-                "hbm_gb_X_per_gpu": round(N * G * 4 / 1e9 / (world if a.dp else 1), 2),
+                1 if a.dp else world),
+                "parallelism": (f"dp x{emu} emulated on one GPU (rank 0's shard; collectives "
+                                f"replaced by device copies, {comm.bytes / max(1, a.steps + a.warmup) / 1e6:.1f} "
+                                "MB per step per rank not timed)") if emu else
+                f"{'dp' if a.dp else 'replicate'}x{world}",
+                "hbm_gb_X_per_gpu": round(N * G * 4 / 1e9 / (emu or (world if a.dp else 1)), 2),
                 "x_storage": "split-GEMM planes only" if a.planes_only else "fp32 + planes",
                 "hbm_gb_peak": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
             "data": "synthetic planted-program Poisson counts generated on device"}), flush=True)

@@ -2,7 +2,7 @@
 export TMPDIR=/tmp
 out=gpurun_out/r4b
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_solve_pipe_gpu.py tests/test_kernels_gpu.py tests/test_pipeline_gpu.py tests/test_xgmi_gpu.py -k "pipe or fused or slots or live or gram_of or early or dense or rank_beyond or dp or predict or wide_k or exact" -x -q --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || { echo PYTEST_FAILED; tail -40 $out/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_solve_pipe_gpu.py tests/test_kernels_gpu.py tests/test_pipeline_gpu.py tests/test_xgmi_gpu.py -k "pipe or fused or slots or live or gram_of or early or dense or rank_beyond or dp or predict or wide_k or exact or ridge" -x -q --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || { echo PYTEST_FAILED; tail -40 $out/pytest.log; exit 1; }
 timeout -k 10 200 python bench.py --mode dp --emulate-world 8 --steps 3 --warmup 1 > $out/emu8.log 2>&1 || { echo EMU_FAILED; tail -20 $out/emu8.log; }
 for i in 1 2; do
 CNMF_DEV_SLOTS=1 timeout -k 10 120 python bench.py > $out/bench_on_$i.log 2>&1 &&
