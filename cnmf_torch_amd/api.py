@@ -50,6 +50,8 @@ from .models.refit import col_block, fit_H_online, fit_spectra_online, gene_bloc
 from .ops import sparse as sops
 from .parallel.ledger import worker_filter
 from .utils.anndata_lite import AnnData
+from .utils import resident
+from .utils.transfer import to_host
 from .utils.h5ad import read_h5ad, write_h5ad, write_h5ad_row_blocks
 from .utils.io import (check_dir_exists, dump_yaml, load_df_from_npz, load_yaml, read_10x_mtx,
                        read_any, read_counts_table, read_spectra_batch, save_arrays_npz_digest,
@@ -175,7 +177,7 @@ def _norm_counts_dense_device(counts, genes, guard_zero_std: bool, dev) -> AnnDa
     scanpy's scale (E[x^2] - E[x]^2, ddof=1, std 0 -> 1; used when the TPM is sparse)
     over numpy's ``X / X.std(ddof=1)`` (two-pass, no guard)."""
     T, cols = _norm_counts_tensor(counts, genes, guard_zero_std, dev)
-    out = AnnData(X=T.cpu().numpy(), obs=counts.obs, var=counts.var.iloc[cols],
+    out = AnnData(X=to_host(T), obs=counts.obs, var=counts.var.iloc[cols],
                   obsm=dict(counts.obsm), uns=dict(counts.uns))
     out.uns["_scaled_on_device"] = True
     return out
@@ -250,11 +252,14 @@ def _resident_X(adata, dev: torch.device):
     """``adata.X`` on the device, uploaded once per AnnData object and device and reused
     by every K of k_selection_plot (refit numerators, prediction error): a DeviceCSR for
     sparse X, a float32 tensor for dense X; the host matrix itself on the CPU.  The
-    cached copy is keyed on the identity of ``adata.X``."""
-    if dev.type != "cuda":
-        return adata.X
+    cached copy is keyed on the identity of ``adata.X``; an AnnData from
+    :meth:`cNMF._read_norm_counts` arrives with X = None and its resident mirror preset."""
     cache = adata.__dict__.setdefault("_cnmf_device_X", {})
     key = (str(dev), id(adata.X))
+    if key in cache:
+        return cache[key]
+    if dev.type != "cuda":
+        return adata.X
     if key not in cache:
         cache.clear()
         X = adata.X
@@ -390,6 +395,9 @@ class cNMF:
                 self._initialize_dirs()
                 _save_norm_counts_streamed(self.paths["normalized_counts"], input_counts, T,
                                            cols)
+                # factorize / consensus in this process read the device copy, not the file
+                # (utils.resident; the float32 cast is the one they apply to the file's data)
+                resident.remember(self.paths["normalized_counts"], "X32", T.to(torch.float32))
                 del T
             else:
                 norm_counts = self.get_norm_counts(input_counts, tpm,
@@ -638,6 +646,21 @@ class cNMF:
                 % (zerocells.sum(), ", ".join(examples[:4])))
         return norm_counts
 
+    def _read_norm_counts(self, dev: torch.device):
+        """The normalized-counts AnnData; when this process wrote the file and still
+        holds its device mirror (utils.resident, prepare's GPU path) only obs / var are
+        read and X is left None with the mirror preset for :func:`_resident_X`."""
+        path = self.paths["normalized_counts"]
+        Xr = resident.recall(path, "X32")
+        if Xr is not None and Xr.device == dev:
+            from .utils.h5ad import read_h5ad_annotations
+
+            ad = read_h5ad_annotations(path)
+            if tuple(ad.shape) == tuple(Xr.shape):
+                ad.__dict__["_cnmf_device_X"] = {(str(dev), id(None)): Xr}
+                return ad
+        return read_h5ad(path)
+
     def save_norm_counts(self, norm_counts):
         self._initialize_dirs()
         write_h5ad(self.paths["normalized_counts"], norm_counts)
@@ -758,8 +781,10 @@ class cNMF:
             if dev.type == "cpu" and kwargs.get("n_jobs", -1) not in (None, -1):
                 torch.set_num_threads(max(1, int(kwargs["n_jobs"])))
             row_map = schedule = None
+            Xd = None
             if row_segments is None:
-                norm_counts = read_h5ad(self.paths["normalized_counts"])
+                norm_counts = self._read_norm_counts(dev)
+                Xd = _resident_X(norm_counts, dev) if norm_counts.X is None else None
                 Xh = norm_counts.X
                 cell_idx = np.arange(norm_counts.shape[0])
             else:
@@ -773,8 +798,8 @@ class cNMF:
                     schedule = None
                 cell_idx = np.concatenate([np.arange(a, b) for a, b in row_segments]) \
                     if row_segments else np.zeros(0, dtype=np.int64)
-            X = torch.from_numpy(_dense32(Xh)).to(dev)
-            del Xh
+            X = Xd if Xd is not None else torch.from_numpy(_dense32(Xh)).to(dev)
+            del Xh, Xd
             genes = norm_counts.var.index
             cells = norm_counts.obs.index[cell_idx]
             writer = comm is None or comm.rank == 0
@@ -1099,7 +1124,7 @@ class cNMF:
         dev = _device(bool(kw.get("use_gpu", False)), device)
         merged = load_df_from_npz(self.paths["merged_spectra"] % k)
         if norm_counts is None:
-            norm_counts = read_h5ad(self.paths["normalized_counts"])
+            norm_counts = self._read_norm_counts(dev)
         dt_str = "2" if skip_stats else str(density_threshold)
         dt_repl = dt_str.replace(".", "_")
         n_neighbors = int(local_neighborhood_size * merged.shape[0] / k)
@@ -1355,7 +1380,8 @@ class cNMF:
             from .utils.plotting import PlotWorker
 
             plot_worker = PlotWorker()   # imports matplotlib while the stats compute
-        norm_counts = read_h5ad(self.paths["normalized_counts"])
+        dev = _device(bool(self._refit_kwargs().get("use_gpu", False)), device)
+        norm_counts = self._read_norm_counts(dev)
         ks = sorted(set(int(x) for x in run_params.n_components))
         mine = ks[rank::world]
 
@@ -1366,7 +1392,6 @@ class cNMF:
                                   device=device).stats
 
         rows = {}
-        dev = _device(bool(self._refit_kwargs().get("use_gpu", False)), device)
         if dev.type == "cuda" and len(mine) > 1:
             # the Ks are independent and each is a chain of small kernels and host reads:
             # run them on a few threads with a HIP stream each, so one K's host syncs,

@@ -242,7 +242,7 @@ class Harmony:
                              Phi_moe=self.Phi_moe.cpu().numpy(), lamb=self.lamb.cpu().numpy(),
                              objective_harmony=list(self.objective_harmony),
                              kmeans_rounds=list(self.kmeans_rounds), _R_t=self.R,
-                             _Phi_moe_t=self.Phi_moe, _lamb_t=self.lamb)
+                             _Phi_moe_t=self.Phi_moe, _lamb_t=self.lamb, _lv=self._lv)
 
 
 def run_harmony(data_mat, meta_data: pd.DataFrame, vars_use, theta=None, lamb=None,
@@ -360,11 +360,31 @@ def _levels(Phi_moe: np.ndarray):
         return None
     B1, N = P.shape
     cells = [np.arange(N)] + [np.flatnonzero(P[b]) for b in range(1, B1)]
-    keys, inv = np.unique(P[1:].T.astype(np.uint8), axis=0, return_inverse=True)
+    # a cell's combination of levels as one integer: its level rows (ascending) in base B1
+    # -- a 1-D unique (np.unique(axis=0) over the N x B one-hot rows lexsorts them: ~1 s of
+    # the 500k-cell Harmony stage, profiles/r4d_*)
+    lab = np.zeros(N, dtype=np.int64)
+    cnt = np.zeros(N, dtype=np.int64)
+    for b in range(1, B1):
+        on = cells[b]
+        lab[on] = lab[on] * B1 + b
+        cnt[on] += 1
+    m = int(cnt.max()) if N else 0
+    if N and (cnt.min() != m or m * np.log2(max(B1, 2)) > 62):
+        keys, inv = np.unique(P[1:].T.astype(np.uint8), axis=0, return_inverse=True)
+        lev = [np.flatnonzero(row) + 1 for row in keys]
+    else:
+        ukeys, inv = np.unique(lab, return_inverse=True)
+        lev = []
+        for v in ukeys.tolist():
+            rows = []
+            for _ in range(m):
+                rows.append(v % B1)
+                v //= B1
+            lev.append(np.asarray(rows[::-1], dtype=np.int64))
     inv = np.asarray(inv).reshape(-1)
-    if keys.shape[0] > 4096:
+    if len(lev) > 4096:
         return None
-    lev = [np.flatnonzero(row) + 1 for row in keys]
     return {"cells": cells, "inv": inv, "lev": lev, "N": N, "B1": B1, "dev": {}}
 
 
@@ -441,7 +461,7 @@ def _ridge_native(X: torch.Tensor, Rt: torch.Tensor, lv: dict, Lt: torch.Tensor,
 
 
 def moe_correct_expression(X: torch.Tensor, R, Phi_moe, lamb, K: int | None = None,
-                           chunk: int = 65536) -> torch.Tensor:
+                           chunk: int = 65536, levels=None) -> torch.Tensor:
     """The MOE ridge correction of preprocess.py:9-18 applied to a device-resident
     (cells x features) expression matrix, in place of the features x cells numpy
     round trip: W_k = (Phi_Rk Phi_moe^T + lamb)^-1 Phi_Rk X (W_k[0] = 0, intercept kept),
@@ -449,13 +469,14 @@ def moe_correct_expression(X: torch.Tensor, R, Phi_moe, lamb, K: int | None = No
     chunks, float64 arithmetic, result stored in X's dtype (numpy's in-place
     float32 -= float64 of the reference).  Returns the corrected matrix (new tensor)."""
     dev = X.device
-    Rt = torch.as_tensor(np.asarray(R), dtype=torch.float64).to(dev)
+    # (device tensors -- Harmony's own R / lamb -- are taken as they are, no host trip)
+    Rt = torch.as_tensor(R, dtype=torch.float64, device=dev)
     if K is not None:
         Rt = Rt[:int(K)]
-    Lt = torch.as_tensor(np.asarray(lamb), dtype=torch.float64).to(dev)
+    Lt = torch.as_tensor(lamb, dtype=torch.float64, device=dev)
     if dev.type == "cuda" and ops.use_native(X) and X.dtype in (torch.float32, torch.float64) \
             and X.dim() == 2 and (X.shape[1] <= 1 or X.stride(1) == 1):
-        lv = _levels(Phi_moe)
+        lv = levels if levels is not None else _levels(np.asarray(Phi_moe))
         if lv is not None:   # the f64 matrix-core kernels (no materialised Phi_Rk)
             return _ridge_native(X, Rt.t().contiguous(), lv, Lt)
     Pt = torch.as_tensor(np.asarray(Phi_moe), dtype=torch.float64).to(dev)

@@ -365,8 +365,25 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             int(pl_cols), int(planes_n), gs_ptr, int(gs_rs), int(gs_ld), int(gs_cols),
             *f_args, *gen_dev, int(rpl),
             numer_slot.data_ptr() if numer_slot is not None else 0,
-            planes_slot.data_ptr() if planes_slot is not None else 0, _stream_ptr(x))
+            planes_slot.data_ptr() if planes_slot is not None else 0,
+            _stamp_buffer(vcode, rpl, nblocks, S, K, x), _stream_ptr(x))
     return int(S)
+
+
+# Diagnostic phase stamps of the pipelined solve (CNMF_PIPE_STAMPS=1; tools/pipe_stamp_probe.py):
+# every launch gets a fresh buffer, kept with its (K, slices) in STAMP_LOG for the probe.
+STAMP_LOG: list = []
+
+
+def _stamp_buffer(vcode, rpl, nblocks, S, K, x) -> int:
+    if os.environ.get("CNMF_PIPE_STAMPS") != "1" or vcode != 3 or \
+            torch.cuda.is_current_stream_capturing():
+        return 0
+    wgs = (rpl if rpl else nblocks) * max(1, int(S))
+    buf = torch.zeros(wgs * 8, dtype=torch.int64, device=x.device)
+    STAMP_LOG.append({"K": int(K), "S": int(S), "rounds": -(-nblocks // (rpl or nblocks)),
+                      "buf": buf})
+    return buf.data_ptr()
 
 
 def _fused_solve_args(R, K, n, x, numer, nslabs, nstride, nscale, nbase, nout, gparts,

@@ -23,6 +23,7 @@ from .models.harmony import moe_correct_ridge, run_harmony
 from .utils.anndata_lite import AnnData, to_lite
 from .utils.h5ad import write_h5ad
 from .utils.io import write_text_atomic
+from .utils.transfer import to_host
 
 
 def _default_device():
@@ -156,7 +157,7 @@ class Preprocess:
             f64 = adata_RNA.X.dtype == np.float64       # normalize_total keeps float64
             data = sops.transform(dX, row_scale=rs, round_mid=not f64,
                                   out_dtype=torch.float64 if f64 else torch.float32)
-            data = data.cpu().numpy()
+            data = to_host(data)
             X0 = adata_RNA.X
             tp10k = AnnData(X=sp.csr_matrix((data, X0.indices, X0.indptr), shape=X0.shape),
                             obs=adata_RNA.obs, var=adata_RNA.var,
@@ -294,10 +295,12 @@ class Preprocess:
         self.harmony_info_ = {"iterations": len(res.kmeans_rounds),
                               "kmeans_rounds": [int(r) + 1 for r in res.kmeans_rounds],
                               "max_iter_harmony": int(max_iter_harmony)}
-        Xc = moe_correct_expression(src, res.R, res.Phi_moe, res.lamb, K=res.K)
+        Xc = moe_correct_expression(src, getattr(res, "_R_t", res.R), res.Phi_moe,
+                                    getattr(res, "_lamb_t", res.lamb), K=res.K,
+                                    levels=getattr(res, "_lv", None))
         del src
         Xc.clamp_(min=0)
-        out = AnnData(X=Xc.cpu().numpy(), obs=ad.obs, var=ad.var.iloc[cols],
+        out = AnnData(X=to_host(Xc), obs=ad.obs, var=ad.var.iloc[cols],
                       obsm=dict(ad.obsm),
                       varm={k: (v[cols] if not isinstance(v, pd.DataFrame) else v.iloc[cols])
                             for k, v in ad.varm.items()},

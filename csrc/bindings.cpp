@@ -91,7 +91,7 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t n_scale, uintptr_t nbase, uintptr_t nout, long long nb_rs, long long ldnb,
            uintptr_t gpart, int gpart_n, long long gpart_rs, uintptr_t gout, uintptr_t gp_out,
            long long gp_rs, uintptr_t coop_gen_dev, uintptr_t coop_arrive, int reps_per_launch,
-           uintptr_t nslot, uintptr_t plslot, uintptr_t stream) {
+           uintptr_t nslot, uintptr_t plslot, uintptr_t stamps, uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
                            max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
@@ -106,7 +106,8 @@ PYBIND11_MODULE(_hip, m) {
                            ldnb, P<const float>(gpart), gpart_n, gpart_rs, P<float>(gout),
                            P<float>(gp_out), gp_rs, P<unsigned>(coop_gen_dev),
                            P<unsigned>(coop_arrive), reps_per_launch, P<const int>(nslot),
-                           P<const int>(plslot), reinterpret_cast<hipStream_t>(stream)),
+                           P<const int>(plslot), P<unsigned long long>(stamps),
+                           reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");
         });
 

@@ -23,7 +23,7 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       long long ldnb, const float* gpart, int gpart_n, long long gpart_rs,
                       float* gout, float* gp_out, long long gp_rs, unsigned* coop_gen_dev,
                       unsigned* coop_arrive, int reps_per_launch, const int* nslot,
-                      const int* plslot, hipStream_t stream);
+                      const int* plslot, unsigned long long* stamps, hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,

@@ -45,7 +45,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  int gpart_n, long long gpart_rs, float* gout, float* gp_out,
                                  long long gp_rs, unsigned* coop_gen_dev, unsigned* coop_arrive,
                                  int reps_per_launch, const int* nslot, const int* plslot,
-                                 hipStream_t stream) {
+                                 unsigned long long* stamps, hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
   if ((long long)K * (ldx > ldn ? ldx : ldn) * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
@@ -80,6 +80,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.coop_arrive = coop_arrive;
   p.nslot = nslot;
   p.plslot = plslot;
+  p.stamps = stamps;
   if (p.coop_gen_dev && !coop_arrive) return hipErrorInvalidValue;
   const bool fused = p.nslab_n > 1 || n_scale || nbase || nout || gpart || gout || gp_out ||
                      (coop_split > 1 && coop_gen_dev) || nslot || plslot;

@@ -73,6 +73,12 @@ struct SolveParams {
   // planes go to row plslot[rep] of `planes` -- compact slots of the live replicates.
   const int* nslot;
   const int* plslot;
+  // Diagnostic (solve_pipe.h only; nullptr in every production launch): per workgroup 8
+  // uint64 at stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 8]: s_memrealtime at start
+  // and end, then cycles (s_memtime deltas) of the prologue, the sweep loop, the objective
+  // checks inside it (chain + block reduce + cooperative exchange), the epilogue; checks,
+  // sweeps.  Written only to this buffer; nothing in the kernel reads it.
+  unsigned long long* stamps;
   // Optional (matrix-core kernel only): the system matrix is the Gram F F^T of the factor
   // F_r = gsrc + r*gs_rs (K x gs_cols, row stride gs_ld), formed in the prologue on the
   // matrix cores instead of being read from `gram` (W W^T fused into

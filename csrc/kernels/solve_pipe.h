@@ -123,6 +123,12 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
   __shared__ float sred[3 + 2 * kCoopMaxSlices];
   // numerators of this lane's columns; also the partial-Gram scratch of the epilogue
   __shared__ float sN[pipe_lds_floats(K, T)];
+  const bool stp = p.stamps != nullptr;
+  unsigned long long st0 = 0, st1 = 0, st_chk = 0, n_chk = 0, rt0 = 0;
+  if (stp) {
+    rt0 = __builtin_amdgcn_s_memrealtime();
+    st0 = __builtin_amdgcn_s_memtime();
+  }
   const int bx = p.rep0 + (int)blockIdx.x;
   const int rep = p.rep_index ? p.rep_index[bx] : bx;
   if (p.active && p.active[rep] == 0) {   // converged replicate: untouched (uniform)
@@ -220,9 +226,77 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     }
     if (nsl > 1 || p.n_scale || nb_in || nb_out) {
       // raw split-K slabs summed in slice order, then scaled and added to the base:
-      // bitwise gemm_reduce_kernel's "C (+)= col_scale * sum_s slab[s]".  Slab-outer
-      // rounds: every element's load of slab q is in flight at once, the running sum
-      // stays in the lane's own LDS slot
+      // bitwise gemm_reduce_kernel's "C (+)= col_scale * sum_s slab[s]".
+      if constexpr (3 * T * KS <= 48) {
+        // few tiles (the spectra side): the loads of slabs 1..3 (clamped to the last
+        // one, masked to + 0 past nsl -- exact) and of the base all go out together, one
+        // memory round trip instead of one per slab (tools/pipe_stamp_probe.py: the
+        // per-slab rounds were half of this side's launch)
+        float sl[3][T][KS];
+        float bs[T][KS];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+          const unsigned so = (unsigned)(q < nsl ? q : nsl - 1) * sstride;
+#pragma unroll
+          for (int i = 0; i < T; ++i) {
+            const int cl = col0 + 16 * kPipeWaves * i;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+              const int kk = 4 * s + g;
+              const bool v = cl < n && kk < K;
+              const float t = buf_ld(rn, v ? (kk * sn + cl) * 4 : 0, so);
+              sl[q - 1][i][s] = v ? t : 0.f;
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < T; ++i) {
+          const int cl = col0 + 16 * kPipeWaves * i;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const int kk = 4 * s + g;
+            bs[i][s] = (nb_in && cl < n && kk < K) ? nb_in[(long long)kk * sb + cl] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+#pragma unroll
+          for (int i = 0; i < T; ++i)
+#pragma unroll
+            for (int s = 0; s < KS; ++s)
+              if (q < nsl) CNMF_PIPE_N(i, s) += sl[q - 1][i][s];
+        for (int q = 4; q < nsl; ++q) {       // CNMF_FUSED_MAX_SLABS > 4: the rest in rounds
+#pragma unroll
+          for (int i = 0; i < T; ++i) {
+            const int cl = col0 + 16 * kPipeWaves * i;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+              const int kk = 4 * s + g;
+              const bool v = cl < n && kk < K;
+              const float t = buf_ld(rn, v ? (kk * sn + cl) * 4 : 0, q * sstride);
+              if (v) CNMF_PIPE_N(i, s) += t;
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < T; ++i) {
+          const int cl = col0 + 16 * kPipeWaves * i;
+          const bool ok = cl < n;
+          const float scl = (ok && p.n_scale) ? p.n_scale[cl] : 1.f;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) {
+            const int kk = 4 * s + g;
+            if (!(ok && kk < K)) continue;
+            float nv = CNMF_PIPE_N(i, s);
+            if (p.n_scale) nv *= scl;
+            if (nb_in) nv = bs[i][s] + nv;
+            if (nb_out) nb_out[(long long)kk * sb + cl] = nv;
+            CNMF_PIPE_N(i, s) = nv;
+          }
+        }
+      } else {
+      // Slab-outer rounds: every element's load of slab q is in flight at once, the
+      // running sum stays in the lane's own LDS slot
       for (int q = 1; q < nsl; ++q) {
 #pragma unroll
         for (int i = 0; i < T; ++i) {
@@ -252,6 +326,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
           CNMF_PIPE_N(i, s) = nv;
         }
       }
+      }
     }
   }
   // the summed Gram for the next solve that accumulates on it (slice 0 writes; every
@@ -266,6 +341,11 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       }
   }
 
+  if (stp) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    st1 = __builtin_amdgcn_s_memtime();
+  }
   const int every = p.check_every > 0 ? p.check_every : 1;
   const float eps = p.eps;
   int epoch = 0, it = 0;
@@ -274,9 +354,18 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
   // <numer, x> and sum_j x_j^T Gram x_j of the CURRENT x from the last objective pass
   float lin_p = 0.f, quad_p = 0.f;
   bool lq_valid = false;
+  // The objective of the initial x is only ever the reference of the first convergence
+  // test: it is accumulated inside sweep 0 from the same (Gram x) accumulators (bitwise
+  // the separate objective pass's sums) and exchanged together with the first real check
+  // -- one chain pass and one cooperative exchange fewer per solve
+  // (tools/pipe_stamp_probe.py: the checks were ~30 % of a launch).
+  const bool defer0 = p.max_iter > 0;
+  float f0_part = 0.f;
+  bool f0_pending = false;
 
   while (true) {
-    if (it % every == 0) {
+    if (it % every == 0 && !(it == 0 && defer0)) {
+      const unsigned long long tc0 = stp ? __builtin_amdgcn_s_memtime() : 0ull;
       // block objective x^T Gram x - 2 numer . x, pipelined like the sweep
       float qd = 0.f, ln = 0.f;
       f32x4p acc[2][MB];
@@ -297,9 +386,18 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       float q = qd, l = ln;
       block_sum2(q, l, sred);
       float f = q - 2.f * l;
+      float f0 = f0_part;
       if (coop) {
-        float unused = 0.f;
-        if (!coop_sum2_tag(p, gen, rep, epoch++, f, unused, sred)) break;
+        if (!coop_sum2_tag(p, gen, rep, epoch++, f, f0, sred)) break;
+      }
+      if (f0_pending) {       // the initial objective, summed over the slices like f
+        f_prev = f0;
+        have_prev = true;
+        f0_pending = false;
+      }
+      if (stp) {
+        st_chk += __builtin_amdgcn_s_memtime() - tc0;
+        ++n_chk;
       }
       if (have_prev && fabsf(f_prev - f) <= p.tol * fabsf(f_prev)) break;
       f_prev = f;
@@ -307,6 +405,29 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     }
     if (it >= p.max_iter) break;
     // one MU sweep, software pipelined: chain(i + 1) in flight while tile i updates
+    if (it == 0 && defer0) {
+      // sweep 0 also sums the initial objective's terms from the pre-update x
+      float qd = 0.f, ln = 0.f;
+      f32x4p acc[2][MB];
+      pipe_chain<KS, MB>(a, xr[0], acc[0]);
+#pragma unroll
+      for (int i = 0; i < T; ++i) {
+        if (i + 1 < T) pipe_chain<KS, MB>(a, xr[i + 1], acc[(i + 1) & 1]);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+          const float den = acc[i & 1][s >> 2][s & 3];
+          const float xv = xr[i][s];
+          const float nv = CNMF_PIPE_N(i, s);
+          qd = fmaf(xv, den, qd);
+          ln = fmaf(xv, nv, ln);
+          const float rt = nv * __builtin_amdgcn_rcpf(den);
+          xr[i][s] = (den < eps) ? 0.f : xv * rt;
+        }
+      }
+      block_sum2(qd, ln, sred);
+      f0_part = qd - 2.f * ln;
+      f0_pending = true;
+    } else {
     f32x4p acc[2][MB];
     pipe_chain<KS, MB>(a, xr[0], acc[0]);
 #pragma unroll
@@ -320,10 +441,12 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
         xr[i][s] = (den < eps) ? 0.f : xv * rt;
       }
     }
+    }
     ++it;
     lq_valid = false;
   }
 
+  const unsigned long long st2 = stp ? __builtin_amdgcn_s_memtime() : 0ull;
   // the final iterate, and (optionally) its bf16 planes straight from the registers
   {
     int col0 = j0 + 16 * wave + c;
@@ -454,6 +577,17 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     }
   }
   if (p.iters_out && threadIdx.x == 0 && blockIdx.y == 0) p.iters_out[rep] += it;
+  if (stp) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long* o = p.stamps + ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+      const unsigned long long st3 = __builtin_amdgcn_s_memtime();
+      o[0] = rt0; o[1] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
+      o[2] = st1 - st0; o[3] = st2 - st1; o[4] = st_chk; o[5] = st3 - st2;   // cycles
+      o[6] = n_chk; o[7] = (unsigned long long)it;
+    }
+  }
   pipe_arrive(p);
 }
 

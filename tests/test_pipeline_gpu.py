@@ -100,3 +100,49 @@ def test_k_selection_with_dense_device_counts_over_several_ks(tmp_path):
     stats = load_df_from_npz(obj.paths["k_selection_stats"])
     assert list(stats["k"]) == [4, 5, 6]
     assert np.all(np.isfinite(stats["prediction_error"].values))
+
+
+def _pipeline(tmp, fn, name):
+    obj = cNMF(output_dir=str(tmp), name=name)
+    obj.prepare(fn, components=[4, 5], n_iter=6, seed=3, num_highvar_genes=300,
+                use_gpu=True, batch_size=400)
+    obj.factorize(worker_i=0, total_workers=1, verbose=False)
+    obj.combine()
+    obj.k_selection_plot(close_fig=True)
+    obj.consensus(5, density_threshold=2.0, show_clustering=False)
+    return obj
+
+
+def test_resident_norm_counts_mirror_equals_file_reads(tmp_path, monkeypatch):
+    """prepare's GPU path leaves a device mirror of the norm counts it wrote
+    (utils.resident); factorize, k_selection_plot and consensus in the same process read
+    it instead of the file.  Every artifact equals the file-reading run bit for bit, the
+    mirror is what the stages used, and a rewritten file invalidates it."""
+    from cnmf_torch_amd.utils import resident
+
+    X, cells, genes = simulate_counts(1300, 450, 5, seed=12, sparse=False)
+    fn = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(X, index=cells, columns=genes), fn)
+    resident.forget()
+    monkeypatch.setenv("CNMF_RESIDENT_BYTES", "0")
+    a = _pipeline(tmp_path, fn, "file")
+    assert resident.recall(a.paths["normalized_counts"], "X32") is None
+    monkeypatch.setenv("CNMF_RESIDENT_BYTES", str(1 << 30))
+    b = _pipeline(tmp_path, fn, "mirror")
+    Xr = resident.recall(b.paths["normalized_counts"], "X32")
+    assert Xr is not None and Xr.is_cuda
+    from cnmf_torch_amd.utils.h5ad import read_h5ad
+
+    np.testing.assert_array_equal(Xr.cpu().numpy(),
+                                  read_h5ad(b.paths["normalized_counts"]).X.astype(np.float32))
+    for key, args in (("iter_spectra", (5, 2)), ("merged_spectra", (4,)),
+                      ("consensus_spectra", (5, "2_0")), ("consensus_usages", (5, "2_0")),
+                      ("gene_spectra_score", (5, "2_0")), ("k_selection_stats", None)):
+        fa = a.paths[key] % args if args else a.paths[key]
+        fb = b.paths[key] % args if args else b.paths[key]
+        da, db = load_df_from_npz(fa), load_df_from_npz(fb)
+        np.testing.assert_array_equal(da.values, db.values)
+    # rewriting the file drops the mirror
+    os.utime(b.paths["normalized_counts"], ns=(1, 1))
+    assert resident.recall(b.paths["normalized_counts"], "X32") is None
+    resident.forget()

@@ -2,8 +2,10 @@
 export TMPDIR=/tmp
 out=gpurun_out/r4c
 mkdir -p $out
-timeout -k 10 400 python -u -m pytest tests/test_solve_pipe_gpu.py tests/test_preprocess.py tests/test_pipeline_gpu.py -k "ridge or exact or moe or harmony or dense or streamed" -x -q --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || { echo PYTEST_FAILED; tail -30 $out/pytest.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_solve_pipe_gpu.py tests/test_preprocess.py tests/test_pipeline_gpu.py -k "ridge or exact or moe or harmony or dense or streamed or pipe" -x -q --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || { echo PYTEST_FAILED; tail -30 $out/pytest.log; exit 1; }
 timeout -k 10 120 python bench.py > $out/bench.log 2>&1 &&
+timeout -k 10 200 python tools/pipe_stamp_probe.py --k 10 > $out/stamps_k10.log 2>&1 &&
+timeout -k 10 200 python tools/pipe_stamp_probe.py --k 20 > $out/stamps_k20.log 2>&1 &&
 timeout -k 10 120 python bench.py --k 20 --steps 5 --warmup 2 > $out/k20.log 2>&1 &&
 timeout -k 10 200 python tools/gemm_ceiling_probe.py > $out/gemm_ceiling.log 2>&1 &&
 timeout -k 10 300 python tools/bench_e2e.py > $out/e2e.log 2>&1 &&

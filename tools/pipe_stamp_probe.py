@@ -1,0 +1,76 @@
+"""Phase breakdown of the pipelined MU solve (csrc/kernels/solve_pipe.h) from in-kernel
+s_memtime stamps (diagnostic only: CNMF_PIPE_STAMPS=1 gives each launch a stamp buffer
+that nothing else reads).  Runs one bench-shaped factorisation (graphs off, so every pass
+is an eager, stamped launch) and prints, per K and side (slice count), the mean cycles per
+workgroup in: prologue (operand loads, slab / partial-Gram sums), the sweep loop minus
+the objective checks, the checks (objective chain + block reduce + cooperative exchange),
+and the epilogue (stores, planes, partial Gram), plus the launch span (first start to
+last end) against the mean workgroup time -- the load-imbalance tail.
+
+    CNMF_PIPE_STAMPS=1 CNMF_GRAPHS=0 python tools/pipe_stamp_probe.py --k 20
+"""
+import argparse
+import json
+import os
+import sys
+
+os.environ.setdefault("CNMF_PIPE_STAMPS", "1")
+os.environ.setdefault("CNMF_GRAPHS", "0")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from cnmf_torch_amd import ops  # noqa: E402
+from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions  # noqa: E402
+from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=100)
+    ap.add_argument("--cells", type=int, default=10000)
+    ap.add_argument("--genes", type=int, default=2000)
+    a = ap.parse_args()
+    X = torch.from_numpy(normalized_counts_matrix(a.cells, a.genes, n_programs=a.k, seed=0)).cuda()
+    opts = NMFOptions(n_components=a.k, tol=1e-4, online_chunk_size=5000,
+                      online_chunk_max_iter=1000)
+    solver = NMFBatchSolver(X, opts)
+    np.random.seed(14)
+    seeds = [int(s) for s in np.random.randint(1, 2 ** 31 - 1, size=a.reps)]
+    solver.run(seeds)            # warm-up (module loads, plans)
+    ops.STAMP_LOG.clear()
+    solver.run(seeds)
+    torch.cuda.synchronize()
+    groups = {}
+    for e in ops.STAMP_LOG:
+        s = e["buf"].view(-1, 8).cpu().numpy().astype(np.int64)
+        s = s[s[:, 1] > 0]                       # workgroups that ran (active replicates)
+        if s.size == 0:
+            continue
+        key = (e["K"], e["S"])
+        g = groups.setdefault(key, {"launches": 0, "pro": [], "loop": [], "chk": [], "epi": [],
+                                    "wg": [], "span": [], "sweeps": [], "checks": []})
+        g["launches"] += 1
+        g["pro"].append(np.mean(s[:, 2]))
+        g["chk"].append(np.mean(s[:, 4]))
+        g["loop"].append(np.mean(s[:, 3] - s[:, 4]))
+        g["epi"].append(np.mean(s[:, 5]))
+        g["wg"].append(np.mean(s[:, 1] - s[:, 0]) * 0.01)            # us (100 MHz)
+        g["span"].append(float(s[:, 1].max() - s[:, 0].min()) * 0.01)  # us
+        g["sweeps"].append(np.mean(s[:, 7]))
+        g["checks"].append(np.mean(s[:, 6]))
+    for (K, S), g in sorted(groups.items()):
+        print(json.dumps({
+            "K": K, "slices": S, "launches": g["launches"],
+            "cycles_per_wg": {k: round(float(np.mean(g[k])), 0)
+                              for k in ("pro", "loop", "chk", "epi")},
+            "wg_us": round(float(np.mean(g["wg"])), 2),
+            "launch_span_us": round(float(np.mean(g["span"])), 2),
+            "mean_sweeps": round(float(np.mean(g["sweeps"])), 2),
+            "mean_checks": round(float(np.mean(g["checks"])), 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
