@@ -404,6 +404,10 @@ class cNMF:
                                                    num_highvar_genes=num_highvar_genes,
                                                    high_variance_genes_filter=highvargenes)
                 self.save_norm_counts(norm_counts)
+                if dev.type == "cuda" and resident.wanted(norm_counts.X):
+                    # the float32 device matrix factorize would build from the file
+                    resident.remember(self.paths["normalized_counts"], "X32",
+                                      torch.from_numpy(_dense32(norm_counts.X)).to(dev))
             replicate_params, run_params = self.get_nmf_iter_params(
                 ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
                 alpha_usage=alpha_usage, alpha_spectra=alpha_spectra, init=init,

@@ -108,6 +108,9 @@ def main(argv=None) -> int:
 
     obj = cNMF(output_dir=args.output_dir, name=args.name)
     if args.command == "prepare":
+        # one stage per process: no later stage here could read a device mirror of the
+        # files (utils.resident)
+        os.environ.setdefault("CNMF_RESIDENT_BYTES", "0")
         comm = None
         if int(os.environ.get("WORLD_SIZE", "1")) > 1:     # under torchrun: cell-sharded
             from .parallel.runner import init_distributed

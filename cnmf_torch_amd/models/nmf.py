@@ -1604,13 +1604,19 @@ class NMFBatchSolver:
             kv = torch.as_tensor(np.asarray(st.kpos[:n], dtype=np.int32)).to(dev)
             ds = {"kvec": kv, "cur": torch.empty(n, dtype=torch.int32, device=dev),
                   "prev": torch.empty(n, dtype=torch.int32, device=dev),
-                  "live": torch.empty(2, dtype=torch.int32, device=dev)}
+                  "live": torch.empty(2, dtype=torch.int32, device=dev),
+                  # the active list (conv.hip): the solves' workgroups walk the live
+                  # replicates only (ops.solve rep_list)
+                  "alist": torch.empty(n, dtype=torch.int32, device=dev),
+                  "apos": torch.empty(n + 1, dtype=torch.int32, device=dev)}
             if a is not None:
                 a["dslots"] = ds
         off = torch.cumsum(ds["kvec"], 0, dtype=torch.int32) - ds["kvec"]
         ds["cur"].copy_(off)
         ds["prev"].copy_(off)
         ds["live"].fill_(int(st.rows_act))
+        ds["alist"].copy_(torch.arange(n, dtype=torch.int32, device=dev))
+        ds["apos"].copy_(torch.arange(n + 1, dtype=torch.int32, device=dev))
         return ds
 
     def _fused_bufs(self, st: _Batch, steps) -> dict:
@@ -1884,7 +1890,9 @@ class NMFBatchSolver:
                     planes_n=hpl_n, numer_slabs=ks_n, numer_slab_stride=rows * cw,
                     gram_parts=fb["parts"][g.p0](fb["WWp"]), gram_parts_n=fb["wwp_n"][g.p0],
                     gram_parts_out=fb["parts"][g.p0](fb["HHp"]), coop_device_gen=True,
-                    numer_slot=nsl, planes_slot=psl)
+                    numer_slot=nsl, planes_slot=psl,
+                    rep_list=None if ds is None else (ds["alist"], ds["apos"], g.p0,
+                                                      g.p0 + g.n, g.p0))
             ks_b = ops.gemm_planes(None, hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd,
                                    raw_slab=slabB, raw_max=_FUSED_MAX_SLABS,
                                    gate=st.gate if _GEMM_GATE else None,
@@ -1915,7 +1923,9 @@ class NMFBatchSolver:
                     gram_parts=fb["parts"][g.p0](fb["HHp"]), gram_parts_n=fb["hhp_n"][g.p0],
                     gram_out=None if last else g.gram3(A_out),
                     gram_parts_out=fb["parts"][g.p0](fb["WWp"]), coop_device_gen=True,
-                    numer_slot=nsl, planes_slot=nsl)
+                    numer_slot=nsl, planes_slot=nsl,
+                    rep_list=None if ds is None else (ds["alist"], ds["apos"], g.p0,
+                                                      g.p0 + g.n, g.p0))
             fb["wwp_key"] = fb["wpl_key"] = wkey
         ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
                         n, -1, o.tol, final=final, gate=st.gate, slots=ds)

@@ -146,7 +146,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           gram_parts_n: int = 0, gram_out: torch.Tensor | None = None,
           gram_parts_out: torch.Tensor | None = None, coop_device_gen: bool = False,
           numer_slot: torch.Tensor | None = None,
-          planes_slot: torch.Tensor | None = None) -> int:
+          planes_slot: torch.Tensor | None = None, rep_list: tuple | None = None) -> int:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -192,6 +192,10 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     planes go to row planes_slot[r] of ``planes`` -- the compact slots of conv_update's
     device-side ragged batching (the slots of live replicates never overlap; the caller
     sizes the slabs / planes for the batch's rows).
+    ``rep_list`` = (alist, apos, lo, hi, base) (pipelined kernel only; conv_update's
+    device active list): the workgroups walk alist[apos[lo] ..< apos[hi]] (replicate
+    alist[i] - base of this call) instead of replicates 0..R-1, so the live replicates of
+    a ragged batch occupy the first workgroups and the rest exit at once.
     Returns S, the number of column slices per replicate the launch used.
     """
     a = ALGOS[algo]
@@ -199,7 +203,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     fused = (numer_slabs > 1 or numer_scale is not None or numer_base is not None
              or numer_out is not None or gram_parts is not None or gram_out is not None
              or gram_parts_out is not None or coop_device_gen or numer_slot is not None
-             or planes_slot is not None)
+             or planes_slot is not None or rep_list is not None)
     if fused and not use_native(x):
         raise ValueError("solve: fused operands need the HIP kernels (CUDA tensors)")
     if gram is None and gram_parts is not None:
@@ -292,6 +296,18 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                          "l1 = l2 = 0, conv_mode 1, cooperative slices that fit)")
     if planes_slot is not None and planes is None:
         raise ValueError("planes_slot needs planes")
+    al = (0, 0, 0, 0)
+    if rep_list is not None:
+        alist, apos, lo, hi, base = rep_list
+        if rep_index is not None:
+            raise ValueError("rep_list and rep_index are exclusive")
+        for nm, t in (("alist", alist), ("apos", apos)):
+            if t.dtype != torch.int32 or not t.is_contiguous() or t.device != x.device:
+                raise ValueError(f"rep_list {nm}: contiguous int32 on {x.device}")
+        if not (0 <= int(lo) <= int(hi) < apos.numel()) or int(hi) - int(lo) > R:
+            raise ValueError("rep_list: bad [lo, hi) range")
+        al = (alist.data_ptr(), apos.data_ptr() + 4 * int(lo), apos.data_ptr() + 4 * int(hi),
+              int(base))
     if fused and gram_parts_out is not None and gram_parts_out.shape[1] < S:
         raise ValueError(f"gram_parts_out: {gram_parts_out.shape[1]} slots < {S} slices")
     if S is not None:
@@ -366,7 +382,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             *f_args, *gen_dev, int(rpl),
             numer_slot.data_ptr() if numer_slot is not None else 0,
             planes_slot.data_ptr() if planes_slot is not None else 0,
-            _stamp_buffer(vcode, rpl, nblocks, S, K, x), _stream_ptr(x))
+            _stamp_buffer(vcode, rpl, nblocks, S, K, x), *al, _stream_ptr(x))
     return int(S)
 
 
@@ -647,8 +663,15 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
             slots["live"][0] = int(k.sum()) if init else slots["live"][1]
             slots["cur"][:n] = off
             slots["live"][1] = int(k.sum())
+            if slots.get("alist") is not None:
+                ai = act.to(torch.int32)
+                pos = torch.cumsum(ai, 0, dtype=torch.int32) - ai
+                slots["apos"][:n] = pos
+                slots["apos"][n] = int(ai.sum())
+                idx = torch.nonzero(act).view(-1)
+                slots["alist"][pos[idx].long()] = idx.to(torch.int32)
         return
-    sl = (0, 0, 0, 0)
+    sl = (0, 0, 0, 0, 0, 0)
     if slots is not None:
         for key in ("kvec", "cur", "prev"):
             t = slots[key]
@@ -659,6 +682,14 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
             raise ValueError("slots[live] must be contiguous int32 with >= 2 entries")
         sl = (slots["kvec"].data_ptr(), slots["cur"].data_ptr(), slots["prev"].data_ptr(),
               lv.data_ptr())
+        if slots.get("alist") is not None:
+            al, ap = slots["alist"], slots["apos"]
+            if al.dtype != torch.int32 or ap.dtype != torch.int32 or al.numel() < n \
+                    or ap.numel() < n + 1 or not al.is_contiguous() or not ap.is_contiguous():
+                raise ValueError("slots[alist] / [apos]: contiguous int32 with >= n / n + 1")
+            sl = sl + (al.data_ptr(), ap.data_ptr())
+        else:
+            sl = sl + (0, 0)
     for t in (lin, quad):
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < n:
             raise ValueError("lin/quad must be contiguous float32 with >= n entries")

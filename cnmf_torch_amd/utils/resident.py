@@ -58,6 +58,14 @@ def _nbytes(value) -> int:
     return n
 
 
+def wanted(X) -> bool:
+    """Whether a dense float32 mirror of the (cells x genes) ``X`` fits the budget."""
+    try:
+        return int(X.shape[0]) * int(X.shape[1]) * 4 <= _budget()
+    except Exception:
+        return False
+
+
 def remember(path: str, tag: str, value) -> bool:
     """Mirror ``value`` as the contents of ``path`` (call right after writing it)."""
     budget = _budget()

@@ -91,7 +91,8 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t n_scale, uintptr_t nbase, uintptr_t nout, long long nb_rs, long long ldnb,
            uintptr_t gpart, int gpart_n, long long gpart_rs, uintptr_t gout, uintptr_t gp_out,
            long long gp_rs, uintptr_t coop_gen_dev, uintptr_t coop_arrive, int reps_per_launch,
-           uintptr_t nslot, uintptr_t plslot, uintptr_t stamps, uintptr_t stream) {
+           uintptr_t nslot, uintptr_t plslot, uintptr_t stamps, uintptr_t alist, uintptr_t alo,
+           uintptr_t ahi, int abase, uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
                            max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
@@ -107,6 +108,7 @@ PYBIND11_MODULE(_hip, m) {
                            P<float>(gp_out), gp_rs, P<unsigned>(coop_gen_dev),
                            P<unsigned>(coop_arrive), reps_per_launch, P<const int>(nslot),
                            P<const int>(plslot), P<unsigned long long>(stamps),
+                           P<const int>(alist), P<const int>(alo), P<const int>(ahi), abase,
                            reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");
         });
@@ -115,12 +117,14 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t lin, uintptr_t quad, double x_sq, uintptr_t err_init, uintptr_t err_prev,
            uintptr_t err, uintptr_t active, uintptr_t converged, uintptr_t n_pass, int n,
            int pass, double tol, int final_pass, int init, uintptr_t gate, uintptr_t kvec,
-           uintptr_t slot_cur, uintptr_t slot_prev, uintptr_t live, uintptr_t stream) {
+           uintptr_t slot_cur, uintptr_t slot_prev, uintptr_t live, uintptr_t alist,
+           uintptr_t apos, uintptr_t stream) {
           check(cnmf_conv_update(P<const float>(lin), P<const float>(quad), x_sq,
                                  P<double>(err_init), P<double>(err_prev), P<double>(err),
                                  P<int>(active), P<int>(converged), P<int>(n_pass), n, pass, tol,
                                  final_pass, init, P<int>(gate), P<const int>(kvec),
                                  P<int>(slot_cur), P<int>(slot_prev), P<int>(live),
+                                 P<int>(alist), P<int>(apos),
                                  reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_conv_update");
         });

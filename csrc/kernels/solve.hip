@@ -45,7 +45,9 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  int gpart_n, long long gpart_rs, float* gout, float* gp_out,
                                  long long gp_rs, unsigned* coop_gen_dev, unsigned* coop_arrive,
                                  int reps_per_launch, const int* nslot, const int* plslot,
-                                 unsigned long long* stamps, hipStream_t stream) {
+                                 unsigned long long* stamps, const int* alist,
+                                 const int* alo, const int* ahi, int abase,
+                                 hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
   if ((long long)K * (ldx > ldn ? ldx : ldn) * 4 >= 0x7fffffffLL) return hipErrorInvalidValue;
@@ -81,6 +83,22 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.nslot = nslot;
   p.plslot = plslot;
   p.stamps = stamps;
+  {
+    // workgroup order of the pipelined kernel (SolveParams.pipe_map); CNMF_PIPE_MAP
+    // overrides the default for A/B runs
+    static const int map_env = [] {
+      const char* e = getenv("CNMF_PIPE_MAP");
+      return (e && *e) ? atoi(e) : -1;
+    }();
+    p.pipe_map = map_env >= 0 ? map_env : 0;
+    p.pipe_nblocks = nblocks;
+  }
+  if ((alist != nullptr) != (alo != nullptr) || (alo != nullptr) != (ahi != nullptr))
+    return hipErrorInvalidValue;
+  p.alist = alist;
+  p.alo = alo;
+  p.ahi = ahi;
+  p.abase = abase;
   if (p.coop_gen_dev && !coop_arrive) return hipErrorInvalidValue;
   const bool fused = p.nslab_n > 1 || n_scale || nbase || nout || gpart || gout || gp_out ||
                      (coop_split > 1 && coop_gen_dev) || nslot || plslot;
@@ -119,6 +137,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
       return hipSuccess;
     }
     if (reps_per_launch > 0 && reps_per_launch < nblocks) return hipErrorInvalidValue;
+    if (alist) return hipErrorInvalidValue;     // the active list exists only in the pipe
     if (per > cnmf_solve_mfma_max_cols(K)) return hipErrorInvalidValue;
     // the fused operands exist only in the pipelined kernel: never drop them silently
     if (fused || (!gram && !gsrc)) return hipErrorInvalidValue;

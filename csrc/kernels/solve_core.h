@@ -148,10 +148,17 @@ __device__ __forceinline__ bool coop_sum2(const SolveParams& p, int rep, int e, 
                                           float& b, float* sred) {
   return coop_sum2_tag(p, p.coop_gen, rep, e, a, b, sred);
 }
+__device__ __forceinline__ bool coop_sum2_tag_s(const SolveParams& p, unsigned gen, int rep,
+                                                int e, float& a, float& b, float* sred, int S,
+                                                int slice);
 __device__ __forceinline__ bool coop_sum2_tag(const SolveParams& p, unsigned gen, int rep,
                                               int e, float& a, float& b, float* sred) {
-  const int S = gridDim.y;
-  const int slice = blockIdx.y;
+  return coop_sum2_tag_s(p, gen, rep, e, a, b, sred, (int)gridDim.y, (int)blockIdx.y);
+}
+// (S slices; this workgroup is slice `slice` of replicate rep)
+__device__ __forceinline__ bool coop_sum2_tag_s(const SolveParams& p, unsigned gen, int rep,
+                                                int e, float& a, float& b, float* sred, int S,
+                                                int slice) {
   if (S <= 1) return true;
   if (e >= p.coop_epochs) {  // workspace too small: treat as timeout (host sizes it)
     if (threadIdx.x == 0) atomicExch(p.coop_timeout, 2);

@@ -79,6 +79,20 @@ struct SolveParams {
   // checks inside it (chain + block reduce + cooperative exchange), the epilogue; checks,
   // sweeps.  Written only to this buffer; nothing in the kernel reads it.
   unsigned long long* stamps;
+  // solve_pipe.h workgroup order: 0 = grid (replicates, slices); 1 = a 1-D grid in which
+  // the S slices of one replicate are consecutive workgroups of ONE XCD (workgroup w runs
+  // on XCD w % 8): they start together and exchange through one L2.  pipe_nblocks: the
+  // launch's replicate count (set by the launcher).
+  int pipe_map;
+  int pipe_nblocks;
+  // Device active list (conv.hip conv_slots; solve_pipe.h only): when alist is set, the
+  // launch's workgroup block b handles replicate alist[*alo + b] - abase while
+  // *alo + b < *ahi, and exits otherwise -- the live replicates of a ragged batch take
+  // the first workgroups (balanced over the XCDs under pipe_map 1).
+  const int* alist;
+  const int* alo;
+  const int* ahi;
+  int abase;
   // Optional (matrix-core kernel only): the system matrix is the Gram F F^T of the factor
   // F_r = gsrc + r*gs_rs (K x gs_cols, row stride gs_ld), formed in the prologue on the
   // matrix cores instead of being read from `gram` (W W^T fused into

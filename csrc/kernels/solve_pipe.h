@@ -129,8 +129,34 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     rt0 = __builtin_amdgcn_s_memrealtime();
     st0 = __builtin_amdgcn_s_memtime();
   }
-  const int bx = p.rep0 + (int)blockIdx.x;
-  const int rep = p.rep_index ? p.rep_index[bx] : bx;
+  // (replicate block, slice) of this workgroup -- see SolveParams.pipe_map
+  int blk, slc, nsg;
+  if (p.pipe_map) {
+    nsg = p.coop_slots ? p.coop_epochs_split : 1;
+    const int w = (int)blockIdx.x, l = w >> 3;
+    blk = (l / nsg) * 8 + (w & 7);
+    slc = l - (l / nsg) * nsg;
+    if (blk >= p.pipe_nblocks) {         // padding of the last group of 8 replicates
+      pipe_arrive(p);
+      return;
+    }
+  } else {
+    blk = (int)blockIdx.x;
+    slc = (int)blockIdx.y;
+    nsg = (int)gridDim.y;
+  }
+  const int bx = p.rep0 + blk;
+  int rep;
+  if (p.alist) {
+    const int ai = *p.alo + bx;
+    if (ai >= *p.ahi) {                  // past the live replicates of this launch
+      pipe_arrive(p);
+      return;
+    }
+    rep = p.alist[ai] - p.abase;
+  } else {
+    rep = p.rep_index ? p.rep_index[bx] : bx;
+  }
   if (p.active && p.active[rep] == 0) {   // converged replicate: untouched (uniform)
     pipe_arrive(p);
     return;
@@ -191,10 +217,10 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
   }
 
   int j0 = 0, n = p.ncols;
-  const bool coop = p.coop_slots != nullptr && gridDim.y > 1;
+  const bool coop = p.coop_slots != nullptr && nsg > 1;
   if (coop) {
-    const int per = (p.ncols + (int)gridDim.y - 1) / (int)gridDim.y;
-    j0 = min(p.ncols, (int)blockIdx.y * per);
+    const int per = (p.ncols + nsg - 1) / nsg;
+    j0 = min(p.ncols, slc * per);
     n = min(p.ncols, j0 + per);
   }
 
@@ -331,7 +357,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
   }
   // the summed Gram for the next solve that accumulates on it (slice 0 writes; every
   // slice summed the same values in the same order)
-  if (p.gout && blockIdx.y == 0 && wave == 0) {
+  if (p.gout && slc == 0 && wave == 0) {
 #pragma unroll
     for (int b = 0; b < MB; ++b)
 #pragma unroll
@@ -388,7 +414,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       float f = q - 2.f * l;
       float f0 = f0_part;
       if (coop) {
-        if (!coop_sum2_tag(p, gen, rep, epoch++, f, f0, sred)) break;
+        if (!coop_sum2_tag_s(p, gen, rep, epoch++, f, f0, sred, nsg, slc)) break;
       }
       if (f0_pending) {       // the initial objective, summed over the slices like f
         f_prev = f0;
@@ -481,7 +507,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       }
     }
     // the last slice zeroes the GEMM's k padding [ncols, pl_cols) of every plane it reads
-    if (pl && (!coop || blockIdx.y == gridDim.y - 1)) {
+    if (pl && (!coop || slc == nsg - 1)) {
       const int pad = p.pl_cols - p.ncols;
       for (int e = threadIdx.x; e < pad * K; e += 64 * kPipeWaves) {
         const int kk = e / pad, cc = p.ncols + e % pad;
@@ -509,8 +535,8 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       }
     }
     block_sum2(lin, quad, sred);
-    if (coop) (void)coop_sum2_tag(p, gen, rep, epoch++, lin, quad, sred);
-    if (threadIdx.x == 0 && (!coop || blockIdx.y == 0)) {
+    if (coop) (void)coop_sum2_tag_s(p, gen, rep, epoch++, lin, quad, sred, nsg, slc);
+    if (threadIdx.x == 0 && (!coop || slc == 0)) {
       if (p.lin_out) p.lin_out[rep] = lin;
       if (p.quad_out) p.quad_out[rep] = quad;
     }
@@ -555,7 +581,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     __syncthreads();
     // lane (g, c) holds D_b1b2[4 g + r][c]; per 16-row band b1 the 4 wave partials are
     // summed in wave order
-    float* go = p.gp_out + (long long)rep * p.gp_rs + (long long)blockIdx.y * K * K;
+    float* go = p.gp_out + (long long)rep * p.gp_rs + (long long)slc * K * K;
 #pragma unroll
     for (int b1 = 0; b1 < MB; ++b1) {
 #pragma unroll
@@ -576,12 +602,12 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       __syncthreads();
     }
   }
-  if (p.iters_out && threadIdx.x == 0 && blockIdx.y == 0) p.iters_out[rep] += it;
+  if (p.iters_out && threadIdx.x == 0 && slc == 0) p.iters_out[rep] += it;
   if (stp) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) {
-      unsigned long long* o = p.stamps + ((unsigned long long)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+      unsigned long long* o = p.stamps + ((unsigned long long)slc * p.pipe_nblocks + blk) * 8;
       const unsigned long long st3 = __builtin_amdgcn_s_memtime();
       o[0] = rt0; o[1] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
       o[2] = st1 - st0; o[3] = st2 - st1; o[4] = st_chk; o[5] = st3 - st2;   // cycles
@@ -602,8 +628,10 @@ template <int K, int T>
 static hipError_t launch_pipe_kt(const SolveParams& p, int nblocks, int pl_n, hipStream_t s) {
   if constexpr (T <= pipe_tile_max(K)) {
     const int gy = p.coop_slots ? p.coop_epochs_split : 1;
-    hipLaunchKernelGGL((solve_pipe_kernel<K, T>), dim3(nblocks, gy), dim3(64 * kPipeWaves), 0,
-                       s, p, pl_n);
+    SolveParams q = p;
+    q.pipe_nblocks = nblocks;
+    const dim3 grid = q.pipe_map ? dim3(((nblocks + 7) / 8) * 8 * gy, 1) : dim3(nblocks, gy);
+    hipLaunchKernelGGL((solve_pipe_kernel<K, T>), grid, dim3(64 * kPipeWaves), 0, s, q, pl_n);
     return hipGetLastError();
   } else {
     return hipErrorInvalidValue;

@@ -102,10 +102,10 @@ def test_k_selection_with_dense_device_counts_over_several_ks(tmp_path):
     assert np.all(np.isfinite(stats["prediction_error"].values))
 
 
-def _pipeline(tmp, fn, name):
+def _pipeline(tmp, fn, name, densify):
     obj = cNMF(output_dir=str(tmp), name=name)
     obj.prepare(fn, components=[4, 5], n_iter=6, seed=3, num_highvar_genes=300,
-                use_gpu=True, batch_size=400)
+                use_gpu=True, batch_size=400, densify=densify)
     obj.factorize(worker_i=0, total_workers=1, verbose=False)
     obj.combine()
     obj.k_selection_plot(close_fig=True)
@@ -113,7 +113,8 @@ def _pipeline(tmp, fn, name):
     return obj
 
 
-def test_resident_norm_counts_mirror_equals_file_reads(tmp_path, monkeypatch):
+@pytest.mark.parametrize("densify", [False, True])
+def test_resident_norm_counts_mirror_equals_file_reads(tmp_path, monkeypatch, densify):
     """prepare's GPU path leaves a device mirror of the norm counts it wrote
     (utils.resident); factorize, k_selection_plot and consensus in the same process read
     it instead of the file.  Every artifact equals the file-reading run bit for bit, the
@@ -125,16 +126,17 @@ def test_resident_norm_counts_mirror_equals_file_reads(tmp_path, monkeypatch):
     save_df_to_npz(pd.DataFrame(X, index=cells, columns=genes), fn)
     resident.forget()
     monkeypatch.setenv("CNMF_RESIDENT_BYTES", "0")
-    a = _pipeline(tmp_path, fn, "file")
+    a = _pipeline(tmp_path, fn, "file", densify)
     assert resident.recall(a.paths["normalized_counts"], "X32") is None
     monkeypatch.setenv("CNMF_RESIDENT_BYTES", str(1 << 30))
-    b = _pipeline(tmp_path, fn, "mirror")
+    b = _pipeline(tmp_path, fn, "mirror", densify)
     Xr = resident.recall(b.paths["normalized_counts"], "X32")
     assert Xr is not None and Xr.is_cuda
     from cnmf_torch_amd.utils.h5ad import read_h5ad
 
-    np.testing.assert_array_equal(Xr.cpu().numpy(),
-                                  read_h5ad(b.paths["normalized_counts"]).X.astype(np.float32))
+    Xf = read_h5ad(b.paths["normalized_counts"]).X
+    Xf = Xf.toarray() if hasattr(Xf, "toarray") else np.asarray(Xf)
+    np.testing.assert_array_equal(Xr.cpu().numpy(), Xf.astype(np.float32))
     for key, args in (("iter_spectra", (5, 2)), ("merged_spectra", (4,)),
                       ("consensus_spectra", (5, "2_0")), ("consensus_usages", (5, "2_0")),
                       ("gene_spectra_score", (5, "2_0")), ("k_selection_stats", None)):

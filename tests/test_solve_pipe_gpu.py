@@ -2,6 +2,8 @@
 K/16 output blocks of permuted Gram rows, register-resident iterate, co-resident launch
 rounds) and the fused online step / per-layout graphs that run on it, against the fp64
 reference solve, the VALU kernel, and the unfused / eager paths."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -217,8 +219,15 @@ def test_fused_graph_replay_wide_k_bitwise_eager(monkeypatch, K):
         assert a.W.shape[0] == 24 * K
 
 
-@pytest.mark.parametrize("ks", [[10], [5, 7, 13], [20]])
-def test_device_slots_bitwise_equal_uncompacted(monkeypatch, ks):
+_SLOT_CASES = [([10], "0"), ([5, 7, 13], "0"), ([20], "0"), ([5, 7, 13], "1"), ([20], "1")]
+
+
+def _slot_id(ks, pmap):
+    return "k" + "_".join(map(str, ks)) + "-map" + pmap
+
+
+@pytest.mark.parametrize("ks,pmap", [pytest.param(k, m, id=_slot_id(k, m)) for k, m in _SLOT_CASES])
+def test_device_slots_bitwise_equal_uncompacted(monkeypatch, ks, pmap):
     """Device-side ragged batching (conv_update slots; GEMMs skip dead M-tiles, solves
     read / write at compact rows) changes where rows live, not what is computed: the
     factorisation is bit-identical to the same fused run without slots and without host
@@ -232,6 +241,19 @@ def test_device_slots_bitwise_equal_uncompacted(monkeypatch, ks):
     opts = nmf.NMFOptions(n_components=ks[0], online_chunk_size=2000,
                           online_chunk_max_iter=1000)
     out = {}
+    # (CNMF_PIPE_MAP: the pipelined solve's workgroup order, 1 = XCD-grouped slices; read
+    # once per process by the extension, so a case runs in a child process with it set)
+    if os.environ.get("CNMF_PIPE_MAP") != pmap:
+        import subprocess
+        import sys
+
+        env = dict(os.environ, CNMF_PIPE_MAP=pmap)
+        r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                            f"{__file__}::test_device_slots_bitwise_equal_uncompacted"
+                            f"[{_slot_id(ks, pmap)}]"], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        return
     for mode in ("slots", "plain", "compact"):
         monkeypatch.setattr(nmf, "_DEV_SLOTS", mode == "slots")
         frac = "2.0" if mode == "plain" else "0.25"
@@ -259,13 +281,17 @@ def test_conv_update_slots_match_prefix_sums():
     st.update({k: torch.zeros(n, dtype=torch.int32, device=dev) for k in ("active", "converged", "n_pass")})
     sl = {"kvec": kv.to(dev), "cur": torch.zeros(n, dtype=torch.int32, device=dev),
           "prev": torch.zeros(n, dtype=torch.int32, device=dev),
-          "live": torch.zeros(2, dtype=torch.int32, device=dev)}
+          "live": torch.zeros(2, dtype=torch.int32, device=dev),
+          "alist": torch.full((n,), -1, dtype=torch.int32, device=dev),
+          "apos": torch.full((n + 1,), -1, dtype=torch.int32, device=dev)}
     lin = torch.rand(n, generator=g).to(dev)
     quad = torch.rand(n, generator=g).to(dev)
     ops.conv_update(lin, quad, 10.0, st, n, -1, 1e-4, final=False, init=True, slots=sl)
     full = (torch.cumsum(kv, 0) - kv).to(torch.int32)
     assert torch.equal(sl["cur"].cpu(), full) and torch.equal(sl["prev"].cpu(), full)
     assert sl["live"].tolist() == [int(kv.sum())] * 2
+    assert torch.equal(sl["alist"].cpu(), torch.arange(n, dtype=torch.int32))
+    assert torch.equal(sl["apos"].cpu(), torch.arange(n + 1, dtype=torch.int32))
     # half the replicates stop improving (error unchanged): they deactivate
     lin2 = lin.clone()
     keep = torch.rand(n, generator=g) < 0.5
@@ -278,6 +304,11 @@ def test_conv_update_slots_match_prefix_sums():
     assert torch.equal(sl["cur"].cpu()[act], want[act])
     assert torch.equal(sl["prev"].cpu(), full)
     assert sl["live"].tolist() == [int(kv.sum()), int(k.sum())]
+    # the active list: apos = exclusive prefix count of the active flags, alist its inverse
+    ai = act.to(torch.int32)
+    pos = (torch.cumsum(ai, 0) - ai).to(torch.int32)
+    assert torch.equal(sl["apos"].cpu()[:n], pos) and int(sl["apos"][n]) == int(ai.sum())
+    assert torch.equal(sl["alist"].cpu()[:int(ai.sum())], torch.nonzero(act).view(-1).to(torch.int32))
 
 
 def test_gemm_planes_live_rows_skip_dead_tiles(monkeypatch):

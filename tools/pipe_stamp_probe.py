@@ -45,13 +45,25 @@ def main():
     torch.cuda.synchronize()
     groups = {}
     for e in ops.STAMP_LOG:
-        s = e["buf"].view(-1, 8).cpu().numpy().astype(np.int64)
-        s = s[s[:, 1] > 0]                       # workgroups that ran (active replicates)
+        s3 = e["buf"].view(-1, 8).cpu().numpy().astype(np.int64)
+        S = max(1, int(e["S"]))
+        # start skew among the slices of one replicate (buffer is slice-major: slice *
+        # blocks + block), in us of the 100 MHz realtime counter
+        skew = []
+        if S > 1 and s3.shape[0] % S == 0:
+            v = s3.reshape(S, -1, 8)
+            ran = (v[:, :, 1] > 0).all(axis=0)
+            if ran.any():
+                st = v[:, ran, 0]
+                skew = list((st.max(axis=0) - st.min(axis=0)) * 0.01)
+        s = s3[s3[:, 1] > 0]                     # workgroups that ran (active replicates)
         if s.size == 0:
             continue
         key = (e["K"], e["S"])
         g = groups.setdefault(key, {"launches": 0, "pro": [], "loop": [], "chk": [], "epi": [],
-                                    "wg": [], "span": [], "sweeps": [], "checks": []})
+                                    "wg": [], "span": [], "sweeps": [], "checks": [],
+                                    "skew": []})
+        g["skew"].extend(skew)
         g["launches"] += 1
         g["pro"].append(np.mean(s[:, 2]))
         g["chk"].append(np.mean(s[:, 4]))
@@ -69,7 +81,10 @@ def main():
             "wg_us": round(float(np.mean(g["wg"])), 2),
             "launch_span_us": round(float(np.mean(g["span"])), 2),
             "mean_sweeps": round(float(np.mean(g["sweeps"])), 2),
-            "mean_checks": round(float(np.mean(g["checks"])), 2)}), flush=True)
+            "mean_checks": round(float(np.mean(g["checks"])), 2),
+            "slice_start_skew_us": (round(float(np.mean(g["skew"])), 2) if g["skew"] else None),
+            "slice_start_skew_p90_us": (round(float(np.percentile(g["skew"], 90)), 2)
+                                        if g["skew"] else None)}), flush=True)
 
 
 if __name__ == "__main__":
