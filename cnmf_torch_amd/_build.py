@@ -80,22 +80,31 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     # the pipelined solve keeps its elementwise update scalar: SLP-packed v_pk_*_f32 beside
     # MFMAs cost more issue cycles than the scalar pair (MI355X_MICROARCH.md cycle table)
     unit_flags = {"beta_planes.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+    # CNMF_PIPE_STAMPS_BUILD=1: the pipelined solve with its diagnostic phase stamps
+    # (tools/pipe_stamp_probe.py); a changed flag set rebuilds the unit
+    stamps = os.environ.get("CNMF_PIPE_STAMPS_BUILD", "0") == "1"
     for s in srcs:      # every instantiation unit of the pipelined solve (solve_pipe*.hip)
         if os.path.basename(s).startswith("solve_pipe"):
-            unit_flags[os.path.basename(s)] = ["-fno-slp-vectorize"]
+            unit_flags[os.path.basename(s)] = ["-fno-slp-vectorize"] + \
+                (["-DCNMF_PIPE_STAMPS"] if stamps else [])
     for s in srcs:
         o = os.path.join(BUILD, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _stale(o, [s] + hdrs):
+        flags_fn = o + ".flags"
+        flags = " ".join(common + unit_flags.get(os.path.basename(s), []))
+        old_flags = open(flags_fn).read() if os.path.exists(flags_fn) else None
+        if force or old_flags != flags or _stale(o, [s] + hdrs):
             extra = _py_includes() if s.endswith(".cpp") else []
-            todo.append([hipcc, "-c", s, "-o", o] + common + extra +
-                        unit_flags.get(os.path.basename(s), []))
+            todo.append(([hipcc, "-c", s, "-o", o] + common + extra +
+                         unit_flags.get(os.path.basename(s), []), flags_fn, flags))
     if todo:
         if verbose:
             print(f"[cnmf build] compiling {len(todo)} HIP/C++ unit(s) for {ARCH}", flush=True)
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            for f in [ex.submit(_run, c) for c in todo]:
+            for f, (_, flags_fn, flags) in [(ex.submit(_run, c[0]), c) for c in todo]:
                 f.result()
+                with open(flags_fn, "w") as fh:      # recorded once the unit built
+                    fh.write(flags)
     if force or todo or _stale(HIP_OUT, objs):
         tmp = HIP_OUT + ".tmp"
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + objs)

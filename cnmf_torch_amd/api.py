@@ -170,6 +170,19 @@ def _device_csr(X, dev: torch.device):
     return sops.DeviceCSR.from_scipy(X, device=dev)
 
 
+def _device_csr_cached(adata, dev: torch.device):
+    """:func:`_device_csr` of ``adata.X``, kept on the AnnData (keyed on X's identity and
+    the device) so repeated consensus calls on one TPM upload it once."""
+    if dev.type != "cuda" or not sp.issparse(adata.X):
+        return None
+    cache = adata.__dict__.setdefault("_cnmf_device_csr", {})
+    key = (str(dev), id(adata.X))
+    if key not in cache:
+        cache.clear()
+        cache[key] = _device_csr(adata.X, dev)
+    return cache[key]
+
+
 def _norm_counts_dense_device(counts, genes, guard_zero_std: bool, dev) -> AnnData:
     """get_norm_counts for a dense count matrix on the GPU (cnmf.py:670-681): the HVG
     column gather, the float64 cast and the unit-variance scaling run on the device; one
@@ -358,6 +371,10 @@ class cNMF:
             else:
                 tpm = read_counts_table(tpm_fn, densify)
                 write_h5ad(self.paths["tpm"], tpm)
+            if _device(False).type == "cuda":
+                # consensus in this process takes this object instead of re-reading the
+                # file (utils.resident: only while the file is unchanged)
+                resident.remember(self.paths["tpm"], "adata", tpm)
 
             # exact moments on the host matrix (models.hvg.exact_mean_var): the same bits
             # as the cell-sharded prepare's all-reduced digits (_prepare_sharded)
@@ -406,7 +423,10 @@ class cNMF:
                 self.save_norm_counts(norm_counts)
                 if dev.type == "cuda" and resident.wanted(norm_counts.X):
                     # the float32 device matrix factorize would build from the file
-                    resident.remember(self.paths["normalized_counts"], "X32",
+                    # (a sparse file: only factorize densifies it; consensus reads the
+                    # file's CSR, see _read_norm_counts)
+                    resident.remember(self.paths["normalized_counts"],
+                                      "X32" if not sp.issparse(norm_counts.X) else "X32_factorize",
                                       torch.from_numpy(_dense32(norm_counts.X)).to(dev))
             replicate_params, run_params = self.get_nmf_iter_params(
                 ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
@@ -650,12 +670,16 @@ class cNMF:
                 % (zerocells.sum(), ", ".join(examples[:4])))
         return norm_counts
 
-    def _read_norm_counts(self, dev: torch.device):
+    def _read_norm_counts(self, dev: torch.device, factorize: bool = False):
         """The normalized-counts AnnData; when this process wrote the file and still
         holds its device mirror (utils.resident, prepare's GPU path) only obs / var are
-        read and X is left None with the mirror preset for :func:`_resident_X`."""
+        read and X is left None with the mirror preset for :func:`_resident_X`.  The
+        mirror of a sparse file serves ``factorize`` only (it densifies X; the other
+        stages run the CSR kernels on the file's matrix)."""
         path = self.paths["normalized_counts"]
         Xr = resident.recall(path, "X32")
+        if Xr is None and factorize:
+            Xr = resident.recall(path, "X32_factorize")
         if Xr is not None and Xr.device == dev:
             from .utils.h5ad import read_h5ad_annotations
 
@@ -787,7 +811,7 @@ class cNMF:
             row_map = schedule = None
             Xd = None
             if row_segments is None:
-                norm_counts = self._read_norm_counts(dev)
+                norm_counts = self._read_norm_counts(dev, factorize=True)
                 Xd = _resident_X(norm_counts, dev) if norm_counts.X is None else None
                 Xh = norm_counts.X
                 cell_idx = np.arange(norm_counts.shape[0])
@@ -1208,11 +1232,13 @@ class cNMF:
         norm_usages.columns = new_cols
         median_spectra.index = new_cols
 
-        tpm = read_h5ad(self.paths["tpm"])
+        tpm = resident.recall(self.paths["tpm"], "adata")
+        if tpm is None:
+            tpm = read_h5ad(self.paths["tpm"])
         tpm_stats = load_df_from_npz(self.paths["tpm_stats"])
         # sparse TPM on the GPU: uploaded once as CSR; the spectra refit, the OLS and the
         # scaled-HVG usage refit below are CSR kernel passes over it (ops.sparse)
-        dT = _device_csr(tpm.X, dev)
+        dT = _device_csr_cached(tpm, dev)
         tpmX = dT if dT is not None else tpm.X
         spectra_tpm = self.refit_spectra(tpmX, norm_usages.astype(tpm.X.dtype), device=dev,
                                          comm=comm if tp else None)
@@ -1263,14 +1289,19 @@ class cNMF:
         if not writer:
             return None
         p = self.paths
-        save_df_to_npz(median_spectra, p["consensus_spectra"] % (k, dt_repl))
-        save_df_to_npz(rf_usages, p["consensus_usages"] % (k, dt_repl))
-        save_df_to_text(median_spectra, p["consensus_spectra__txt"] % (k, dt_repl))
-        save_df_to_text(rf_usages, p["consensus_usages__txt"] % (k, dt_repl))
-        save_df_to_npz(spectra_tpm, p["gene_spectra_tpm"] % (k, dt_repl))
-        save_df_to_text(spectra_tpm, p["gene_spectra_tpm__txt"] % (k, dt_repl))
-        save_df_to_npz(usage_coef, p["gene_spectra_score"] % (k, dt_repl))
-        save_df_to_text(usage_coef, p["gene_spectra_score__txt"] % (k, dt_repl))
+        # the eight artifacts are independent atomic files: written by a few threads
+        # (zlib and the native TSV writer drop the GIL; ~1 s serial at 500k cells)
+        outs = [(save_df_to_npz, median_spectra, "consensus_spectra"),
+                (save_df_to_npz, rf_usages, "consensus_usages"),
+                (save_df_to_text, median_spectra, "consensus_spectra__txt"),
+                (save_df_to_text, rf_usages, "consensus_usages__txt"),
+                (save_df_to_npz, spectra_tpm, "gene_spectra_tpm"),
+                (save_df_to_text, spectra_tpm, "gene_spectra_tpm__txt"),
+                (save_df_to_npz, usage_coef, "gene_spectra_score"),
+                (save_df_to_text, usage_coef, "gene_spectra_score__txt")]
+        with cf.ThreadPoolExecutor(max_workers=4) as ex:
+            for f in [ex.submit(fn, df, p[key] % (k, dt_repl)) for fn, df, key in outs]:
+                f.result()
 
         if show_clustering and plot_worker is None:
             from .utils.plotting import clustergram

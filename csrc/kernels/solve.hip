@@ -13,6 +13,7 @@ extern "C" int cnmf_solve_max_k() { return 128; }
 extern "C" int cnmf_solve_mfma_max_cols(int K);
 extern "C" int cnmf_solve_pipe_tiles(int K, int per);
 extern "C" int cnmf_solve_pipe_k(int K);
+extern "C" int cnmf_solve_pipe_wg_per_cu(int K);
 
 // ranks the kernels are instantiated for: 1..32, the padded wide ranks 40..64 (multiples
 // of 8) and 80..128 (multiples of 16, MU only: solve_wmfma.hip)
@@ -90,7 +91,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
       const char* e = getenv("CNMF_PIPE_MAP");
       return (e && *e) ? atoi(e) : -1;
     }();
-    p.pipe_map = map_env >= 0 ? map_env : 0;
+    p.pipe_map = map_env >= 0 ? map_env : -1;     // -1: chosen per launch below
     p.pipe_nblocks = nblocks;
   }
   if ((alist != nullptr) != (alo != nullptr) || (alo != nullptr) != (ahi != nullptr))
@@ -128,6 +129,26 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                       l1_num == 0.f && l1_den == 0.f && l2 == 0.f;
     if (pipe) {
       const int rpl = reps_per_launch > 0 ? reps_per_launch : nblocks;
+      if (p.pipe_map < 0) {
+        // XCD-grouped slices (one L2 for a replicate's exchanges: the objective checks
+        // cost ~half) when each XCD's share of the round stays well inside its resident
+        // budget; near the budget the grouped order started workgroups late and lost
+        // (profiles/r4g_*: K = 10 +1 %, K = 20 / 30 -4 %)
+        static int n_cu[16] = {0};
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (dev < 0 || dev >= 16) dev = 0;
+        if (n_cu[dev] == 0) {
+          int v = 0;
+          if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+              v <= 0)
+            v = 256;
+          n_cu[dev] = v;
+        }
+        const int S = coop_split > 1 ? coop_split : 1;
+        const long long per_xcd = (long long)cnmf_solve_pipe_wg_per_cu(K) * n_cu[dev] / 8;
+        p.pipe_map = (S > 1 && 4LL * ((rpl + 7) / 8) * S <= 3LL * per_xcd) ? 1 : 0;
+      }
       for (int r0 = 0; r0 < nblocks; r0 += rpl) {
         p.rep0 = r0;
         const hipError_t e = cnmf::launch_solve_pipe(K, p, nblocks - r0 < rpl ? nblocks - r0 : rpl,

@@ -123,7 +123,14 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
   __shared__ float sred[3 + 2 * kCoopMaxSlices];
   // numerators of this lane's columns; also the partial-Gram scratch of the epilogue
   __shared__ float sN[pipe_lds_floats(K, T)];
+  // phase stamps are compiled in only for the probe build (CNMF_PIPE_STAMPS_BUILD=1 at
+  // build time, tools/pipe_stamp_probe.py): their 64-bit counters cost the production
+  // kernels registers (K = 10 / 20 instantiations went to scratch with them)
+#ifdef CNMF_PIPE_STAMPS
   const bool stp = p.stamps != nullptr;
+#else
+  constexpr bool stp = false;
+#endif
   unsigned long long st0 = 0, st1 = 0, st_chk = 0, n_chk = 0, rt0 = 0;
   if (stp) {
     rt0 = __builtin_amdgcn_s_memrealtime();
@@ -186,34 +193,39 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     }
   if (p.gpart) {
     // + the producing solve's per-slice partial Grams, summed in slice order; QB slices'
-    // loads in flight per round (a sequential load-add chain per element cost ~gpart_n
-    // memory latencies)
-    constexpr int QB = MB == 1 ? 8 : (MB == 2 ? 4 : 2);
+    // loads of EVERY output block in flight per round (a sequential load-add chain per
+    // element cost ~gpart_n memory latencies; one round per block and QB slices cost
+    // MB x as many -- tools/pipe_stamp_probe.py)
+    constexpr int QB = MB == 1 ? 8 : (MB == 2 ? 4 : 1);
     const float* gp = p.gpart + (long long)rep * p.gpart_rs;
+    float t[MB][KS];
 #pragma unroll
-    for (int b = 0; b < MB; ++b) {
-      const int row = 16 * b + pm;
-      float t[KS];
+    for (int b = 0; b < MB; ++b)
 #pragma unroll
-      for (int s = 0; s < KS; ++s) t[s] = 0.f;
-      for (int q0 = 0; q0 < p.gpart_n; q0 += QB) {
-        float v[QB][KS];
+      for (int s = 0; s < KS; ++s) t[b][s] = 0.f;
+    for (int q0 = 0; q0 < p.gpart_n; q0 += QB) {
+      float v[QB][MB][KS];
 #pragma unroll
-        for (int j = 0; j < QB; ++j)
+      for (int j = 0; j < QB; ++j)
+#pragma unroll
+        for (int b = 0; b < MB; ++b)
 #pragma unroll
           for (int s = 0; s < KS; ++s) {
-            const int k = 4 * s + g;
-            v[j][s] = (q0 + j < p.gpart_n && row < K && k < K)
-                          ? gp[(long long)(q0 + j) * K * K + row * K + k] : 0.f;
+            const int row = 16 * b + pm, k = 4 * s + g;
+            v[j][b][s] = (q0 + j < p.gpart_n && row < K && k < K)
+                             ? gp[(long long)(q0 + j) * K * K + row * K + k] : 0.f;
           }
 #pragma unroll
-        for (int j = 0; j < QB; ++j)
+      for (int j = 0; j < QB; ++j)
 #pragma unroll
-          for (int s = 0; s < KS; ++s) t[s] += v[j][s];   // + 0 for q >= gpart_n: exact
-      }
+        for (int b = 0; b < MB; ++b)
 #pragma unroll
-      for (int s = 0; s < KS; ++s) a[b][s] = gm ? a[b][s] + t[s] : t[s];
+          for (int s = 0; s < KS; ++s) t[b][s] += v[j][b][s];   // + 0 past gpart_n: exact
     }
+#pragma unroll
+    for (int b = 0; b < MB; ++b)
+#pragma unroll
+      for (int s = 0; s < KS; ++s) a[b][s] = gm ? a[b][s] + t[b][s] : t[b][s];
   }
 
   int j0 = 0, n = p.ncols;
@@ -381,16 +393,17 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
   float lin_p = 0.f, quad_p = 0.f;
   bool lq_valid = false;
   // The objective of the initial x is only ever the reference of the first convergence
-  // test: it is accumulated inside sweep 0 from the same (Gram x) accumulators (bitwise
-  // the separate objective pass's sums) and exchanged together with the first real check
-  // -- one chain pass and one cooperative exchange fewer per solve
-  // (tools/pipe_stamp_probe.py: the checks were ~30 % of a launch).
+  // test: this slice's part of it is kept and exchanged together with the first real
+  // check -- one cooperative exchange (a wait on the slowest slice) fewer per solve
+  // (tools/pipe_stamp_probe.py: the checks were ~30 % of a launch).  (Folding its terms
+  // into sweep 0 instead saved the chain pass too, but the second unrolled sweep body
+  // pushed K = 20 past 128 VGPRs into scratch.)
   const bool defer0 = p.max_iter > 0;
   float f0_part = 0.f;
   bool f0_pending = false;
 
   while (true) {
-    if (it % every == 0 && !(it == 0 && defer0)) {
+    if (it % every == 0) {
       const unsigned long long tc0 = stp ? __builtin_amdgcn_s_memtime() : 0ull;
       // block objective x^T Gram x - 2 numer . x, pipelined like the sweep
       float qd = 0.f, ln = 0.f;
@@ -412,6 +425,15 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       float q = qd, l = ln;
       block_sum2(q, l, sred);
       float f = q - 2.f * l;
+      if (it == 0 && defer0) {            // kept for the first real check
+        f0_part = f;
+        f0_pending = true;
+        if (stp) {
+          st_chk += __builtin_amdgcn_s_memtime() - tc0;
+          ++n_chk;
+        }
+        goto sweep;
+      }
       float f0 = f0_part;
       if (coop) {
         if (!coop_sum2_tag_s(p, gen, rep, epoch++, f, f0, sred, nsg, slc)) break;
@@ -429,31 +451,10 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       f_prev = f;
       have_prev = true;
     }
+  sweep:
     if (it >= p.max_iter) break;
     // one MU sweep, software pipelined: chain(i + 1) in flight while tile i updates
-    if (it == 0 && defer0) {
-      // sweep 0 also sums the initial objective's terms from the pre-update x
-      float qd = 0.f, ln = 0.f;
-      f32x4p acc[2][MB];
-      pipe_chain<KS, MB>(a, xr[0], acc[0]);
-#pragma unroll
-      for (int i = 0; i < T; ++i) {
-        if (i + 1 < T) pipe_chain<KS, MB>(a, xr[i + 1], acc[(i + 1) & 1]);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-          const float den = acc[i & 1][s >> 2][s & 3];
-          const float xv = xr[i][s];
-          const float nv = CNMF_PIPE_N(i, s);
-          qd = fmaf(xv, den, qd);
-          ln = fmaf(xv, nv, ln);
-          const float rt = nv * __builtin_amdgcn_rcpf(den);
-          xr[i][s] = (den < eps) ? 0.f : xv * rt;
-        }
-      }
-      block_sum2(qd, ln, sred);
-      f0_part = qd - 2.f * ln;
-      f0_pending = true;
-    } else {
+    {
     f32x4p acc[2][MB];
     pipe_chain<KS, MB>(a, xr[0], acc[0]);
 #pragma unroll

@@ -130,7 +130,9 @@ def test_resident_norm_counts_mirror_equals_file_reads(tmp_path, monkeypatch, de
     assert resident.recall(a.paths["normalized_counts"], "X32") is None
     monkeypatch.setenv("CNMF_RESIDENT_BYTES", str(1 << 30))
     b = _pipeline(tmp_path, fn, "mirror", densify)
-    Xr = resident.recall(b.paths["normalized_counts"], "X32")
+    # (a sparse norm-counts file is mirrored for factorize only: consensus runs CSR kernels)
+    tag = "X32" if densify else "X32_factorize"
+    Xr = resident.recall(b.paths["normalized_counts"], tag)
     assert Xr is not None and Xr.is_cuda
     from cnmf_torch_amd.utils.h5ad import read_h5ad
 
@@ -146,5 +148,5 @@ def test_resident_norm_counts_mirror_equals_file_reads(tmp_path, monkeypatch, de
         np.testing.assert_array_equal(da.values, db.values)
     # rewriting the file drops the mirror
     os.utime(b.paths["normalized_counts"], ns=(1, 1))
-    assert resident.recall(b.paths["normalized_counts"], "X32") is None
+    assert resident.recall(b.paths["normalized_counts"], tag) is None
     resident.forget()

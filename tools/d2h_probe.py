@@ -15,8 +15,8 @@ from cnmf_torch_amd.utils.transfer import to_host  # noqa: E402
 
 def main():
     for gb in (0.5, 4.0):
-        n = int(gb * (1 << 30) / 4)
-        t = torch.rand(n, device="cuda").view(-1, 2000)[: n // 2000]
+        n = int(gb * (1 << 30) / 4) // 2000 * 2000
+        t = torch.rand(n, device="cuda").view(-1, 2000)
         torch.cuda.synchronize()
         res = {}
         for name, fn in (("pageable_cpu", lambda: t.cpu().numpy()), ("to_host", lambda: to_host(t))):

@@ -2,7 +2,7 @@
 export TMPDIR=/tmp
 out=gpurun_out/r4g
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_solve_pipe_gpu.py tests/test_pipeline_gpu.py -x -q --timeout 300 --timeout-method thread > $out/pytest.log 2>&1 || { echo PYTEST_FAILED; tail -30 $out/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_pipeline_gpu.py tests/test_solve_pipe_gpu.py -x -q --timeout 300 --timeout-method thread > $out/pytest.log 2>&1 || { echo PYTEST_FAILED; tail -30 $out/pytest.log; exit 1; }
 for m in 0 1; do
   CNMF_PIPE_MAP=$m timeout -k 10 120 python bench.py > $out/bench_map$m.log 2>&1 &&
   CNMF_PIPE_MAP=$m timeout -k 10 120 python bench.py --k 20 --steps 5 --warmup 2 > $out/k20_map$m.log 2>&1 &&

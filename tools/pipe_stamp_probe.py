@@ -8,6 +8,10 @@ and the epilogue (stores, planes, partial Gram), plus the launch span (first sta
 last end) against the mean workgroup time -- the load-imbalance tail.
 
     CNMF_PIPE_STAMPS=1 CNMF_GRAPHS=0 python tools/pipe_stamp_probe.py --k 20
+
+The stamps exist only in a probe build of the extension: build with
+``CNMF_PIPE_STAMPS_BUILD=1 python -c "import cnmf_torch_amd._build as b; b.build_hip()"``
+(and rebuild without it afterwards: the production kernels carry no stamp code).
 """
 import argparse
 import json
@@ -73,6 +77,8 @@ def main():
         g["span"].append(float(s[:, 1].max() - s[:, 0].min()) * 0.01)  # us
         g["sweeps"].append(np.mean(s[:, 7]))
         g["checks"].append(np.mean(s[:, 6]))
+    if not groups:
+        sys.exit("no stamps were written: build the extension with CNMF_PIPE_STAMPS_BUILD=1")
     for (K, S), g in sorted(groups.items()):
         print(json.dumps({
             "K": K, "slices": S, "launches": g["launches"],
