@@ -129,7 +129,7 @@ def build_h5(force: bool = False, verbose: bool = True) -> str:
     prefix = _hdf5_prefix()
     cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
     tmp = H5_OUT + ".tmp"
-    cmd = [cxx, "-O2", "-shared", "-fPIC", "-std=c++17", src, "-o", tmp,
+    cmd = [cxx, "-O2", "-shared", "-fPIC", "-std=c++17", "-pthread", src, "-o", tmp,
            "-I" + os.path.join(prefix, "include")] + _py_includes() + [
            "-L" + os.path.join(prefix, "lib"), "-lhdf5",
            "-Wl,-rpath," + os.path.join(prefix, "lib")]
