@@ -105,9 +105,10 @@ class NMFOptions:
     eps: float = 1e-16
     # KL on the GPU runs its MU statistics over the non-zeros only (CSR kernels,
     # sparse_kl.hip) when X has at most this fraction of non-zero entries; 0 disables.
-    # CNMF_KL_SPARSE=1 / 0 forces / disables it.  At 15 % the CSR path measured 399 vs
-    # 364 rep/s (profiles/r3n_*); at the headline's 47 % the dense kernels win
-    kl_sparse_density: float = 0.15
+    # CNMF_KL_SPARSE=1 / 0 forces / disables it.  Measured crossover (profiles/r4h_kl_*,
+    # r4c_kl_*; CSR vs dense rep/s): 8 % 564 / 381, 15 % 403 / 365, 25 % 290 / 348,
+    # 35 % 228 / 338 -- equal near 19 %; at the headline's 47 % the dense kernels win
+    kl_sparse_density: float = 0.18
 
     @classmethod
     def from_kwargs(cls, n_components: int, **kw) -> "NMFOptions":

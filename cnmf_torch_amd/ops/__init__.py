@@ -539,6 +539,12 @@ def pipe_slices(n: int, nblocks: int, K: int, dev: torch.device) -> int | None:
     return S
 
 
+# target columns per cooperative slice of the pipelined solve (more, shorter slices fill
+# the chip; fewer, longer ones wait less on each other at the exchanges).  256 / 384 /
+# 512: K=10 13,172 / 13,229 / 13,204 rep/s, K=20 5,232 / 5,293 / 5,141 (profiles/r4i_*)
+_PIPE_SLICE_COLS = int(os.environ.get("CNMF_PIPE_SLICE_COLS", "384"))
+
+
 def _pipe_plan(n: int, nblocks: int, K: int, coop, dev: torch.device):
     """(S, reps_per_launch) for the pipelined matrix-core solve (solve_pipe.h), or None.
     Every replicate's columns are split into S cooperative slices that each fit one
@@ -566,7 +572,7 @@ def _pipe_plan(n: int, nblocks: int, K: int, coop, dev: torch.device):
     else:
         rounds = -(-nblocks * s_min // budget)
         rpl = -(-nblocks // rounds)
-        S = max(s_min, min(budget // rpl, -(-n // 256), kCoopMaxSlices))
+        S = max(s_min, min(budget // rpl, -(-n // _PIPE_SLICE_COLS), kCoopMaxSlices))
     if S == 1:              # no cooperative exchange: residency does not matter
         return 1, 0
     return S, (rpl if rpl < nblocks else 0)

@@ -947,6 +947,23 @@ def test_online_kl_sparse_path_matches_dense():
     assert np.abs(a.n_iter - b.n_iter).max() <= 1, (a.n_iter, b.n_iter)
 
 
+@pytest.mark.parametrize("density,sparse", [(0.08, True), (0.17, True), (0.21, False),
+                                            (0.47, False)])
+def test_kl_sparse_routing_follows_measured_crossover(monkeypatch, density, sparse):
+    """Without CNMF_KL_SPARSE, KL takes the CSR kernels up to kl_sparse_density (0.18,
+    the measured crossover: profiles/r4h_kl_*) and the dense kernels above it."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    monkeypatch.delenv("CNMF_KL_SPARSE", raising=False)
+    X = normalized_counts_matrix(2000, 300, n_programs=5, seed=1)
+    X[X < np.quantile(X, 1.0 - density)] = 0.0
+    s = NMFBatchSolver(torch.from_numpy(X).cuda(),
+                       NMFOptions(n_components=5, beta_loss="kullback-leibler"))
+    assert NMFOptions(n_components=5).kl_sparse_density == 0.18
+    assert (s._kl_sparse() is not None) == sparse
+
+
 def test_online_kl_without_xt_copy_matches():
     """When X^T does not fit beside X the spectra side falls back to the fp32 kernel that
     reads X in place (beta_mu.hip): same factorisation as the split-bf16 X^T path."""
