@@ -131,7 +131,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
 #else
   constexpr bool stp = false;
 #endif
-  unsigned long long st0 = 0, st1 = 0, st_chk = 0, n_chk = 0, rt0 = 0;
+  unsigned long long st0 = 0, st1 = 0, st_chk = 0, n_chk = 0, rt0 = 0, rt_x = 0;
   if (stp) {
     rt0 = __builtin_amdgcn_s_memrealtime();
     st0 = __builtin_amdgcn_s_memtime();
@@ -435,6 +435,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
         goto sweep;
       }
       float f0 = f0_part;
+      if (stp && rt_x == 0) rt_x = __builtin_amdgcn_s_memrealtime();   // first arrival
       if (coop) {
         if (!coop_sum2_tag_s(p, gen, rep, epoch++, f, f0, sred, nsg, slc)) break;
       }
@@ -612,7 +613,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       const unsigned long long st3 = __builtin_amdgcn_s_memtime();
       o[0] = rt0; o[1] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
       o[2] = st1 - st0; o[3] = st2 - st1; o[4] = st_chk; o[5] = st3 - st2;   // cycles
-      o[6] = n_chk; o[7] = (unsigned long long)it;
+      o[6] = rt_x; o[7] = (n_chk << 32) | (unsigned long long)(unsigned)it;
     }
   }
   pipe_arrive(p);

@@ -1,0 +1,13 @@
+# e2e with cProfile, float-input bench, KL at 0.08 (standard config), K=10 grid
+export TMPDIR=/tmp
+out=gpurun_out/r4k
+mkdir -p $out
+timeout -k 10 300 python tools/bench_e2e.py > $out/e2e.log 2>&1 &&
+timeout -k 10 300 python tools/bench_e2e.py --profile $out/e2e_prof.txt > $out/e2e_prof.log 2>&1 &&
+timeout -k 10 200 python bench.py --beta-loss kullback-leibler --density 0.08 --steps 3 --warmup 1 > $out/kl_d08.log 2>&1 &&
+timeout -k 10 200 python bench.py --float-input --steps 10 --warmup 3 > $out/float.log 2>&1 &&
+timeout -k 10 200 python bench.py --kmin 5 --kmax 13 --steps 5 --warmup 2 > $out/grid.log 2>&1
+echo rc=$?
+CNMF_FUSED_MAX_SLABS=8 timeout -k 10 120 python bench.py > gpurun_out/r4k/bench_slabs8.log 2>&1 &&
+timeout -k 10 120 python bench.py > gpurun_out/r4k/bench_slabs4.log 2>&1
+echo rc2=$?

@@ -53,21 +53,27 @@ def main():
         S = max(1, int(e["S"]))
         # start skew among the slices of one replicate (buffer is slice-major: slice *
         # blocks + block), in us of the 100 MHz realtime counter
-        skew = []
+        skew, askew = [], []
         if S > 1 and s3.shape[0] % S == 0:
             v = s3.reshape(S, -1, 8)
             ran = (v[:, :, 1] > 0).all(axis=0)
             if ran.any():
                 st = v[:, ran, 0]
                 skew = list((st.max(axis=0) - st.min(axis=0)) * 0.01)
+                # arrival spread at the first cooperative exchange (realtime, us)
+                ax = v[:, ran, 6]
+                ok = (ax > 0).all(axis=0)
+                if ok.any():
+                    askew = list((ax[:, ok].max(axis=0) - ax[:, ok].min(axis=0)) * 0.01)
         s = s3[s3[:, 1] > 0]                     # workgroups that ran (active replicates)
         if s.size == 0:
             continue
         key = (e["K"], e["S"])
         g = groups.setdefault(key, {"launches": 0, "pro": [], "loop": [], "chk": [], "epi": [],
                                     "wg": [], "span": [], "sweeps": [], "checks": [],
-                                    "skew": []})
+                                    "skew": [], "askew": []})
         g["skew"].extend(skew)
+        g["askew"].extend(askew)
         g["launches"] += 1
         g["pro"].append(np.mean(s[:, 2]))
         g["chk"].append(np.mean(s[:, 4]))
@@ -75,8 +81,8 @@ def main():
         g["epi"].append(np.mean(s[:, 5]))
         g["wg"].append(np.mean(s[:, 1] - s[:, 0]) * 0.01)            # us (100 MHz)
         g["span"].append(float(s[:, 1].max() - s[:, 0].min()) * 0.01)  # us
-        g["sweeps"].append(np.mean(s[:, 7]))
-        g["checks"].append(np.mean(s[:, 6]))
+        g["sweeps"].append(np.mean(s[:, 7] & 0xffffffff))
+        g["checks"].append(np.mean(s[:, 7] >> 32))
     if not groups:
         sys.exit("no stamps were written: build the extension with CNMF_PIPE_STAMPS_BUILD=1")
     for (K, S), g in sorted(groups.items()):
@@ -90,7 +96,12 @@ def main():
             "mean_checks": round(float(np.mean(g["checks"])), 2),
             "slice_start_skew_us": (round(float(np.mean(g["skew"])), 2) if g["skew"] else None),
             "slice_start_skew_p90_us": (round(float(np.percentile(g["skew"], 90)), 2)
-                                        if g["skew"] else None)}), flush=True)
+                                        if g["skew"] else None),
+            "first_exchange_arrival_spread_us": (round(float(np.mean(g["askew"])), 2)
+                                                 if g["askew"] else None),
+            "first_exchange_arrival_spread_p90_us": (
+                round(float(np.percentile(g["askew"], 90)), 2) if g["askew"] else None)}),
+            flush=True)
 
 
 if __name__ == "__main__":
