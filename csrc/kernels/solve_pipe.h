@@ -192,35 +192,45 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
       a[b][s] = (gm && row < K && k < K) ? gm[row * K + k] : 0.f;
     }
   if (p.gpart) {
-    // + the producing solve's per-slice partial Grams, summed in slice order; QB slices'
-    // loads of EVERY output block in flight per round (a sequential load-add chain per
-    // element cost ~gpart_n memory latencies; one round per block and QB slices cost
-    // MB x as many -- tools/pipe_stamp_probe.py)
-    constexpr int QB = MB == 1 ? 8 : (MB == 2 ? 4 : 1);
+    // + the producing solve's per-slice partial Grams, summed in slice order.  They are
+    // staged through LDS (sN, free until the numerators arrive) in chunks of whole
+    // partials: 256 threads load consecutive floats, 16 in flight each -- coalesced and
+    // one or two memory rounds per chunk, where per-lane (row, k) gathers took one round
+    // per QB partials and block (tools/pipe_stamp_probe.py: the spectra side's prologue
+    // was half its launch).  Each lane then sums its elements over the chunk's partials
+    // in slice order: bitwise the register version's sums.
     const float* gp = p.gpart + (long long)rep * p.gpart_rs;
+    constexpr int KK = K * K;
+    constexpr int QCH = pipe_lds_floats(K, T) / KK > 0 ? pipe_lds_floats(K, T) / KK : 1;
+    constexpr int NTH = 64 * kPipeWaves;
     float t[MB][KS];
 #pragma unroll
     for (int b = 0; b < MB; ++b)
 #pragma unroll
       for (int s = 0; s < KS; ++s) t[b][s] = 0.f;
-    for (int q0 = 0; q0 < p.gpart_n; q0 += QB) {
-      float v[QB][MB][KS];
+    for (int q0 = 0; q0 < p.gpart_n; q0 += QCH) {
+      const int qn = p.gpart_n - q0 < QCH ? p.gpart_n - q0 : QCH;
+      const int tot = qn * KK;
+      const float* src = gp + (long long)q0 * KK;
+      for (int e0 = (int)threadIdx.x; e0 < tot; e0 += 16 * NTH) {
+        float v[16];
 #pragma unroll
-      for (int j = 0; j < QB; ++j)
+        for (int j = 0; j < 16; ++j) v[j] = e0 + j * NTH < tot ? src[e0 + j * NTH] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (e0 + j * NTH < tot) sN[e0 + j * NTH] = v[j];
+      }
+      __syncthreads();
+      for (int q = 0; q < qn; ++q) {
 #pragma unroll
         for (int b = 0; b < MB; ++b)
 #pragma unroll
           for (int s = 0; s < KS; ++s) {
             const int row = 16 * b + pm, k = 4 * s + g;
-            v[j][b][s] = (q0 + j < p.gpart_n && row < K && k < K)
-                             ? gp[(long long)(q0 + j) * K * K + row * K + k] : 0.f;
+            t[b][s] += (row < K && k < K) ? sN[q * KK + row * K + k] : 0.f;   // exact + 0
           }
-#pragma unroll
-      for (int j = 0; j < QB; ++j)
-#pragma unroll
-        for (int b = 0; b < MB; ++b)
-#pragma unroll
-          for (int s = 0; s < KS; ++s) t[b][s] += v[j][b][s];   // + 0 past gpart_n: exact
+      }
+      __syncthreads();                 // the chunk is consumed before the next overwrites
     }
 #pragma unroll
     for (int b = 0; b < MB; ++b)

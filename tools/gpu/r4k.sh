@@ -11,3 +11,12 @@ echo rc=$?
 CNMF_FUSED_MAX_SLABS=8 timeout -k 10 120 python bench.py > gpurun_out/r4k/bench_slabs8.log 2>&1 &&
 timeout -k 10 120 python bench.py > gpurun_out/r4k/bench_slabs4.log 2>&1
 echo rc2=$?
+CNMF_PIPE_BALANCE=1 timeout -k 10 120 python bench.py > gpurun_out/r4k/bench_bal.log 2>&1 &&
+CNMF_PIPE_BALANCE=1 timeout -k 10 120 python bench.py --k 20 --steps 5 --warmup 2 > gpurun_out/r4k/k20_bal.log 2>&1 &&
+timeout -k 10 120 python bench.py --k 20 --steps 5 --warmup 2 > gpurun_out/r4k/k20.log 2>&1 &&
+CNMF_PIPE_BALANCE=1 timeout -k 10 120 python bench.py --k 30 --steps 5 --warmup 2 > gpurun_out/r4k/k30_bal.log 2>&1 &&
+timeout -k 10 120 python bench.py --k 30 --steps 5 --warmup 2 > gpurun_out/r4k/k30.log 2>&1
+echo rc3=$?
+CNMF_GEMM_KSPLIT=2 timeout -k 10 120 python bench.py > gpurun_out/r4k/bench_ks2.log 2>&1 &&
+CNMF_GEMM_KSPLIT=1 timeout -k 10 120 python bench.py > gpurun_out/r4k/bench_ks1.log 2>&1
+echo rc4=$?
