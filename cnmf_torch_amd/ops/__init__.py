@@ -396,7 +396,7 @@ def _stamp_buffer(vcode, rpl, nblocks, S, K, x) -> int:
             torch.cuda.is_current_stream_capturing():
         return 0
     wgs = (rpl if rpl else nblocks) * max(1, int(S))
-    buf = torch.zeros(wgs * 8, dtype=torch.int64, device=x.device)
+    buf = torch.zeros(wgs * 10, dtype=torch.int64, device=x.device)
     STAMP_LOG.append({"K": int(K), "S": int(S), "rounds": -(-nblocks // (rpl or nblocks)),
                       "buf": buf})
     return buf.data_ptr()

@@ -74,7 +74,7 @@ struct SolveParams {
   const int* nslot;
   const int* plslot;
   // Diagnostic (solve_pipe.h only; nullptr in every production launch): per workgroup 8
-  // uint64 at stamps[(blockIdx.y * gridDim.x + blockIdx.x) * 8]: s_memrealtime at start
+  // uint64 at stamps[(slice * blocks + block) * 10]: s_memrealtime at start
   // and end, then cycles (s_memtime deltas) of the prologue, the sweep loop, the objective
   // checks inside it (chain + block reduce + cooperative exchange), the epilogue; checks,
   // sweeps.  Written only to this buffer; nothing in the kernel reads it.

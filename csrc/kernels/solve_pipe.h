@@ -619,11 +619,16 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) {
-      unsigned long long* o = p.stamps + ((unsigned long long)slc * p.pipe_nblocks + blk) * 8;
+      unsigned long long* o = p.stamps + ((unsigned long long)slc * p.pipe_nblocks + blk) * 10;
       const unsigned long long st3 = __builtin_amdgcn_s_memtime();
       o[0] = rt0; o[1] = __builtin_amdgcn_s_memrealtime();   // 100 MHz, chip-wide
       o[2] = st1 - st0; o[3] = st2 - st1; o[4] = st_chk; o[5] = st3 - st2;   // cycles
       o[6] = rt_x; o[7] = (n_chk << 32) | (unsigned long long)(unsigned)it;
+      // where this workgroup ran: HW_ID (CU / SH / SE bits) and the XCD (XCC_ID)
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+      o[8] = hw;
+      o[9] = xcc;
     }
   }
   pipe_arrive(p);

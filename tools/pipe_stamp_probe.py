@@ -49,13 +49,13 @@ def main():
     torch.cuda.synchronize()
     groups = {}
     for e in ops.STAMP_LOG:
-        s3 = e["buf"].view(-1, 8).cpu().numpy().astype(np.int64)
+        s3 = e["buf"].view(-1, 10).cpu().numpy().astype(np.int64)
         S = max(1, int(e["S"]))
         # start skew among the slices of one replicate (buffer is slice-major: slice *
         # blocks + block), in us of the 100 MHz realtime counter
         skew, askew = [], []
         if S > 1 and s3.shape[0] % S == 0:
-            v = s3.reshape(S, -1, 8)
+            v = s3.reshape(S, -1, 10)
             ran = (v[:, :, 1] > 0).all(axis=0)
             if ran.any():
                 st = v[:, ran, 0]
@@ -74,6 +74,15 @@ def main():
                                     "skew": [], "askew": []})
         g["skew"].extend(skew)
         g["askew"].extend(askew)
+        # workgroups per CU of this launch: (XCD, SE, SH, CU) from HW_ID / XCC_ID
+        hw = s[:, 8]
+        cu = (s[:, 9] & 0xF) * 4096 + ((hw >> 13) & 0x7) * 512 + ((hw >> 12) & 1) * 256 + \
+            ((hw >> 8) & 0xF)
+        _, per_cu = np.unique(cu, return_counts=True)
+        g.setdefault("cus", []).append(len(per_cu))
+        g.setdefault("wpc_max", []).append(int(per_cu.max()))
+        g.setdefault("wpc_mean", []).append(float(per_cu.mean()))
+        g.setdefault("wgs", []).append(int(s.shape[0]))
         g["launches"] += 1
         g["pro"].append(np.mean(s[:, 2]))
         g["chk"].append(np.mean(s[:, 4]))
@@ -97,6 +106,10 @@ def main():
             "slice_start_skew_us": (round(float(np.mean(g["skew"])), 2) if g["skew"] else None),
             "slice_start_skew_p90_us": (round(float(np.percentile(g["skew"], 90)), 2)
                                         if g["skew"] else None),
+            "wgs": round(float(np.mean(g["wgs"])), 1),
+            "cus_used": round(float(np.mean(g["cus"])), 1),
+            "wg_per_cu_mean": round(float(np.mean(g["wpc_mean"])), 2),
+            "wg_per_cu_max": round(float(np.mean(g["wpc_max"])), 2),
             "first_exchange_arrival_spread_us": (round(float(np.mean(g["askew"])), 2)
                                                  if g["askew"] else None),
             "first_exchange_arrival_spread_p90_us": (
