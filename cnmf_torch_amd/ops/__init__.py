@@ -1659,6 +1659,9 @@ def gemm_a_planes(Kd: int) -> int:
     return 2
 
 
+_GEMM_WAVE_PLAN = os.environ.get("CNMF_GEMM_WAVE_PLAN", "1") != "0"
+
+
 def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
     """(tile variant, k split) for an M x N x Kd split GEMM: the largest tile that still
     gives every CU a workgroup, else k-split slices (deterministic slab reduction) until
@@ -1692,6 +1695,24 @@ def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
     ksplit = 1
     if k_env is not None:
         ksplit = int(k_env)
+    elif v_env is None and 1024 < M <= 4096 and _GEMM_WAVE_PLAN:
+        # K x replicates in (1024, 4096] (K = 11..40 at 100 replicates): 128 x 256 tiles
+        # with the k split that best fills whole waves of CUs -- cost ~ ceil(units / CUs)
+        # / ksplit per unit of work + 0.13 per extra split (slab traffic).  Measured
+        # (tools/gemm_plan_sweep.py, profiles/r4q_*): K=20 numerator 99.9 -> 86.7 us,
+        # statistics 85.0 -> 65.9; K=30 statistics 128.4 -> 115.1; K=30 numerator kept.
+        # Bench (profiles/r4r_*): K=20 5,325 -> 5,437, K=30 3,661 -> 3,738 rep/s; at K=50
+        # (M = 5000) the extra slabs cost the solves more than the GEMMs gain (1,300 ->
+        # 1,211), so larger M keeps the rule below
+        t = tiles(1)
+        best = None
+        for ks in (1, 2, 4):
+            if nk // ks < 4:
+                break
+            cost = -(-t * ks // cus) / ks + 0.13 * (ks - 1)
+            if best is None or cost < best[0] - 1e-9:
+                best = (cost, ks)
+        return 1, best[1] if best else 1
     else:
         t = tiles(v)
         while t * ksplit < target and nk // (2 * ksplit) >= 4:
