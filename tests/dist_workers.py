@@ -181,17 +181,18 @@ def xgmi_worker(rank, world, port, out_dir):
     res["comm"] = t.cpu().numpy()
     res["comm_is_xgmi"] = bool(comm._xgmi)
     comm.close()
-    # a rank that never arrives: the kernel gives up after the limit and the flag raises
+    # a rank that never arrives: the kernel gives up after the limit, and the (collective)
+    # check raises on EVERY rank, the one that waited and the one that never came
     timed_out = False
     dist.barrier()
     xg.limit = xg.limit // 3000 * 200                       # 200 ms
     if rank == 0:
         xg(torch.ones(64, device=dev))
         torch.cuda.synchronize()
-        try:
-            xg.check()
-        except XgmiTimeout:
-            timed_out = True
+    try:
+        xg.check()
+    except XgmiTimeout:
+        timed_out = True
     res["timed_out"] = timed_out
     xg.close()
     np.savez(os.path.join(out_dir, f"xgmi{rank}.npz"), **res)

@@ -24,8 +24,25 @@ def _port():
     return p
 
 
-def _spawn(fn, world, *args):
-    mp.spawn(fn, args=(world, _port()) + args, nprocs=world, join=True)
+def _spawn(fn, world, *args, timeout: float | None = None):
+    """Run fn(rank, world, port, *args) on `world` processes; a run that has not finished
+    within `timeout` seconds (CNMF_TEST_SPAWN_TIMEOUT, default 600) is terminated and
+    fails the test -- a mismatched collective must not hang the suite silently."""
+    import time
+
+    if timeout is None:
+        timeout = float(os.environ.get("CNMF_TEST_SPAWN_TIMEOUT", "600"))
+    ctx = mp.start_processes(fn, args=(world, _port()) + args, nprocs=world, join=False,
+                             start_method="spawn")
+    deadline = time.monotonic() + timeout
+    while not ctx.join(timeout=5):
+        if time.monotonic() > deadline:
+            for p in ctx.processes:
+                if p.is_alive():
+                    p.terminate()
+            for p in ctx.processes:
+                p.join(10)
+            raise TimeoutError(f"{fn.__name__}: {world} ranks still running after {timeout} s")
 
 
 @pytest.mark.parametrize("allreduce", ["rccl", "xgmi"])

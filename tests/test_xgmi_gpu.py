@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_xgmi_allreduce_matches_gloo(tmp_path):
-    _spawn(W.xgmi_worker, 2, str(tmp_path))
+    _spawn(W.xgmi_worker, 2, str(tmp_path), timeout=150)
     r0, r1 = (np.load(tmp_path / f"xgmi{r}.npz") for r in range(2))
     n_calls = sum(1 for k in r0.files if k.startswith("err"))
     assert n_calls == 61
@@ -27,7 +27,7 @@ def test_xgmi_allreduce_matches_gloo(tmp_path):
     for r in (r0, r1):
         assert bool(r["comm_is_xgmi"])
         np.testing.assert_array_equal(r["comm"], np.full(10, 3.0, dtype=np.float32))
-    assert bool(r0["timed_out"]) and not bool(r1["timed_out"])
+    assert bool(r0["timed_out"]) and bool(r1["timed_out"])     # every rank fails together
     # the workspace peers hand data over in is coherent across devices while kernels run:
     # uncached or fine-grained (hipPointerGetAttributes), never coarse-grained hipMalloc
     for r in (r0, r1):
@@ -42,7 +42,7 @@ def test_xgmi_dp_solve_matches_gloo_staged(tmp_path):
     kw = dict(online_chunk_size=200, online_max_pass=8, online_h_tol=-1.0,
               online_chunk_max_iter=10)
     for ar in ("xgmi", "rccl"):
-        _spawn(W.xgmi_dp_worker, 2, X, K, seeds, kw, str(tmp_path), ar)
+        _spawn(W.xgmi_dp_worker, 2, X, K, seeds, kw, str(tmp_path), ar, timeout=150)
     assert bool(np.load(tmp_path / "used_xgmi0.npy"))
     assert not bool(np.load(tmp_path / "used_rccl0.npy"))
     Wx, Wg = np.load(tmp_path / "W_xgmi0.npy"), np.load(tmp_path / "W_rccl0.npy")
@@ -63,7 +63,7 @@ def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
     seeds = list(range(31, 31 + R))
     kw = dict(online_chunk_size=400, online_max_pass=12)
     for fused in ("1", "0"):
-        _spawn(W.dp_fused_worker, 2, X, K, seeds, kw, str(tmp_path), fused)
+        _spawn(W.dp_fused_worker, 2, X, K, seeds, kw, str(tmp_path), fused, timeout=150)
     for r in range(2):
         assert bool(np.load(tmp_path / f"dpf1_{r}.npz.npy")[0])
         assert not bool(np.load(tmp_path / f"dpf0_{r}.npz.npy")[0])
