@@ -451,3 +451,17 @@ def test_moe_ridge_kernels_match_reference_formula(N, F, K, levels):
     torch.testing.assert_close(zr_n, zr_d, rtol=1e-10, atol=1e-10)
     torch.testing.assert_close(zc_n, zc_d, rtol=1e-10, atol=1e-10)
     torch.testing.assert_close(w_n, w_d, rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.parametrize("shape,dt", [((70_000, 300), torch.float32), ((9_000_001,), torch.float64),
+                                      ((5, 7), torch.float32)])
+def test_to_host_pinned_copy_is_bitwise(shape, dt):
+    """utils.transfer.to_host (pinned double-buffered chunks, threaded unpack) returns the
+    same bytes as .cpu() for chunk-spanning, odd-sized and small (pageable-path) tensors."""
+    from cnmf_torch_amd.utils.transfer import to_host
+
+    t = torch.randn(shape, dtype=dt, device="cuda")
+    a = to_host(t, chunk_bytes=16 << 20)
+    assert a.dtype == t.cpu().numpy().dtype and a.shape == tuple(shape)
+    np.testing.assert_array_equal(a, t.cpu().numpy())
+    np.testing.assert_array_equal(to_host(t[1:]), t[1:].cpu().numpy())   # an offset view

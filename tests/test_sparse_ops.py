@@ -226,3 +226,17 @@ def test_norm_counts_dense_device_matches_host(sparse_tpm, tmp_path, monkeypatch
     ref = obj.get_norm_counts(counts, tpm, high_variance_genes_filter=genes)
     assert list(got.var.index) == genes
     np.testing.assert_allclose(got.X, ref.X, rtol=1e-12, atol=0, equal_nan=True)
+
+
+def test_gemm_plan_fills_whole_waves_for_mid_size_batches():
+    """ops.gemm_plan: K x replicates in (1024, 4096] takes 128 x 256 tiles with the k split
+    that best fills whole waves of CUs (profiles/r4q_gemm_plan_sweep.json.log); the K = 10
+    and K = 50 shapes keep the measured plans of earlier rounds."""
+    from cnmf_torch_amd import ops
+
+    assert ops.gemm_plan(1000, 5000, 2048, 1) == (4, 1)      # K=10 numerator
+    assert ops.gemm_plan(1000, 2000, 5056, 1) == (1, 4)      # K=10 statistics
+    assert ops.gemm_plan(2000, 5000, 2048, 1) == (1, 2)      # K=20 numerator: 320 tiles
+    assert ops.gemm_plan(2000, 2000, 5056, 1) == (1, 2)      # K=20 statistics
+    assert ops.gemm_plan(3000, 5000, 2048, 1) == (1, 1)      # K=30 numerator
+    assert ops.gemm_plan(5000, 5000, 2048, 1) == (1, 1)      # K=50: the older rule
