@@ -158,7 +158,7 @@ def test_solve_pipe_fused_operands_bitwise_wide(K, coop_gen):
     assert torch.isnan(gp_out[:, S2:]).all()
 
 
-@pytest.mark.parametrize("ks", [[20], [17, 24, 32], [48]])
+@pytest.mark.parametrize("ks", [[20], [17, 24, 32], [48], [64]])
 def test_fused_online_step_matches_unfused_wide(monkeypatch, ks):
     """The fused online step at K > 16 (the cNMF-typical ranks; K = 48 padded from 41)
     factorises like the unfused step: pass counts +-1, errors to 1e-5, spectra to fp32
