@@ -131,9 +131,10 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
       const int rpl = reps_per_launch > 0 ? reps_per_launch : nblocks;
       if (p.pipe_map < 0) {
         // XCD-grouped slices (one L2 for a replicate's exchanges: the objective checks
-        // cost ~half) when each XCD's share of the round stays well inside its resident
-        // budget; near the budget the grouped order started workgroups late and lost
-        // (profiles/r4g_*: K = 10 +1 %, K = 20 / 30 -4 %)
+        // cost ~half) when the launch runs in ONE round and each XCD's share fits its
+        // resident budget.  Measured (profiles/r4za_*): headline 13,133-13,198 ->
+        // 13,482-13,535 rep/s, K=5..13 grid 18,972 -> 19,677; launches in several rounds
+        // (K = 20 / 30 usage side) lost with it (r4g, r4z), so they keep the plain order
         static int n_cu[16] = {0};
         int dev = 0;
         (void)hipGetDevice(&dev);
@@ -147,7 +148,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
         }
         const int S = coop_split > 1 ? coop_split : 1;
         const long long per_xcd = (long long)cnmf_solve_pipe_wg_per_cu(K) * n_cu[dev] / 8;
-        p.pipe_map = (S > 1 && 4LL * ((rpl + 7) / 8) * S <= 3LL * per_xcd) ? 1 : 0;
+        p.pipe_map = (S > 1 && rpl >= nblocks && (long long)((rpl + 7) / 8) * S <= per_xcd) ? 1 : 0;
       }
       for (int r0 = 0; r0 < nblocks; r0 += rpl) {
         p.rep0 = r0;
