@@ -541,8 +541,17 @@ def pipe_slices(n: int, nblocks: int, K: int, dev: torch.device) -> int | None:
 
 # target columns per cooperative slice of the pipelined solve (more, shorter slices fill
 # the chip; fewer, longer ones wait less on each other at the exchanges).  256 / 384 /
-# 512: K=10 13,172 / 13,229 / 13,204 rep/s, K=20 5,232 / 5,293 / 5,141 (profiles/r4i_*)
-_PIPE_SLICE_COLS = int(os.environ.get("CNMF_PIPE_SLICE_COLS", "384"))
+# 512: K=10 13,172 / 13,229 / 13,204 rep/s, K=20 5,232 / 5,293 / 5,141 (profiles/r4i_*).
+# With the single-round XCD order and the LDS-staged Grams, 17 <= K <= 32 prefers 320:
+# K=20 5,601 / 5,606 vs 5,253 / 5,455 at 384, K=30 3,767 / 3,772 vs 3,760 / 3,762
+# (profiles/r4zi_*)
+_PIPE_SLICE_COLS_ENV = os.environ.get("CNMF_PIPE_SLICE_COLS")
+
+
+def _pipe_slice_cols(K: int) -> int:
+    if _PIPE_SLICE_COLS_ENV:
+        return int(_PIPE_SLICE_COLS_ENV)
+    return 320 if 16 < K <= 32 else 384
 
 
 def _pipe_plan(n: int, nblocks: int, K: int, coop, dev: torch.device):
@@ -572,7 +581,7 @@ def _pipe_plan(n: int, nblocks: int, K: int, coop, dev: torch.device):
     else:
         rounds = -(-nblocks * s_min // budget)
         rpl = -(-nblocks // rounds)
-        S = max(s_min, min(budget // rpl, -(-n // _PIPE_SLICE_COLS), kCoopMaxSlices))
+        S = max(s_min, min(budget // rpl, -(-n // _pipe_slice_cols(K)), kCoopMaxSlices))
     if S == 1:              # no cooperative exchange: residency does not matter
         return 1, 0
     return S, (rpl if rpl < nblocks else 0)
