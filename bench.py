@@ -23,6 +23,16 @@ them).  ``value`` is whole-job replicates/sec.  ``--mode`` picks the multi-GPU s
 ``--kmin/--kmax`` replace the single K by the K x n_iter grid of BASELINE config 2
 (K = kmin..kmax, ``--n-iter`` replicates each) solved as ONE ragged batch per step.
 
+``--schedule stream`` (default; weak / strong modes): the timed steps' ledger batches are
+fed, in order, through ONE continuous-batching solve (NMFBatchSolver.run_stream): a fixed
+number of live replicate slots per K, each slot handed the next waiting replicate at the
+pass boundary after its replicate converged.  Every replicate still runs its own full
+solve to its own convergence (same init, rules and pass limit); what changes is that the
+tail of one batch -- the few slow replicates the GPU would otherwise run alone -- overlaps
+the next batch's first passes.  ``value`` is then replicates/s over the whole stream
+(``steps`` x ``n_iter`` replicates per rank, all persisted spectra copied to pinned host
+memory inside the timed region).  ``--schedule batch`` solves each step's batch alone.
+
 Run: ``python bench.py [--gpus N --steps K --warmup W --mode weak|strong|dp]``.  N > 1
 runs one process per GPU over RCCL (xGMI): either under ``torch.distributed.run`` (the
 driver's form; ``WORLD_SIZE`` must then equal ``--gpus``, else the run fails), or, when
@@ -83,6 +93,12 @@ def main() -> int:
                          "sparse-input runs (KL switches to the CSR kernels at <= 0.15)")
     ap.add_argument("--streams", type=int, default=1,
                     help="replicate groups solved concurrently on separate HIP streams")
+    ap.add_argument("--schedule", default="stream", choices=["stream", "batch"],
+                    help="stream: continuous batching over the timed steps' replicates "
+                         "(see module docstring); batch: one solve per step")
+    ap.add_argument("--live", type=int, default=None,
+                    help="stream schedule: live replicate slots per K (default: one "
+                         "co-resident round of the usage solve, NMFBatchSolver.stream_live)")
     ap.add_argument("--emulate-world", type=int, default=None,
                     help="dp mode on ONE process: run rank 0's cell shard of an N-rank job "
                          "with every collective replaced by a device copy of its bytes "
@@ -209,20 +225,57 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    for i in range(args.warmup):
-        step(i)
-    barrier()
-    t0 = time.perf_counter()
+    stream = args.schedule == "stream" and args.mode != "dp" and args.streams == 1
+    held = []          # pinned spectra of finished replicates (factorize writes them out)
+
+    def keep(ids, kk, host, ev):
+        held.append((host, ev))
+
+    def stream_steps(lo: int, hi: int, strong: bool = False):
+        """Steps [lo, hi) as ONE continuous-batching solve (this rank's replicates)."""
+        seeds, ks = [], []
+        for i in range(lo, hi):
+            if strong:
+                s_, k_ = all_seeds[i * per_batch:(i + 1) * per_batch], all_ks[:per_batch]
+            else:
+                s_, k_ = all_seeds[i * n_total:(i + 1) * n_total], all_ks
+            seeds += [int(v) for v in s_[rank::world]]
+            ks += [int(v) for v in k_[rank::world]]
+        held.clear()
+        return solver.run_stream(seeds, ks=ks, live=args.live, keep_usages=False,
+                                 on_result=keep)
+
+    n_chunks = -(-args.cells // args.batch_size)
     passes, h_sweeps, w_sweeps = [], [], []
-    for i in range(args.warmup, nsteps):
-        res, _ = step(i)
+
+    def record(res):
         passes.append(float(np.mean(res.n_iter)))
         # inner MU sweeps per (replicate, pass, chunk) -- the solve kernels' work unit
-        n_chunks = -(-args.cells // args.batch_size)
         for key, acc in (("h_inner_iters", h_sweeps), ("w_inner_iters", w_sweeps)):
             it = np.asarray(res.stats.get(key, []), dtype=np.float64)
             if it.size:
                 acc.append(float(np.mean(it / np.maximum(res.n_iter, 1) / n_chunks)))
+
+    stream_info = None
+    if stream:
+        if args.warmup:
+            stream_steps(0, args.warmup)
+        barrier()
+        t0 = time.perf_counter()
+        res = stream_steps(args.warmup, nsteps)
+        if res.stats.get("stream_slots") is None:      # fell back to per-batch solves
+            to_host(res.W)
+        record(res)
+        stream_info = {"slots": res.stats.get("stream_slots"),
+                       "refill_rounds": res.stats.get("stream_events")}
+    else:
+        for i in range(args.warmup):
+            step(i)
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(args.warmup, nsteps):
+            res, _ = step(i)
+            record(res)
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed)
@@ -232,12 +285,18 @@ def main() -> int:
     strong_value = strong_ms = None
     if world > 1 and args.mode == "weak":
         # the same ledger batch per step, now split over the ranks (strong scaling)
-        for i in range(min(2, args.warmup)):
-            step(i, strong=True)
-        barrier()
-        t0 = time.perf_counter()
-        for i in range(args.warmup, nsteps):
-            step(i, strong=True)
+        if stream:
+            stream_steps(0, min(2, args.warmup), strong=True) if args.warmup else None
+            barrier()
+            t0 = time.perf_counter()
+            stream_steps(args.warmup, nsteps, strong=True)
+        else:
+            for i in range(min(2, args.warmup)):
+                step(i, strong=True)
+            barrier()
+            t0 = time.perf_counter()
+            for i in range(args.warmup, nsteps):
+                step(i, strong=True)
         barrier()
         el_s = max_over_ranks(time.perf_counter() - t0)
         strong_ms = 1000.0 * el_s / args.steps
@@ -279,6 +338,10 @@ def main() -> int:
                 "parallelism": par,
                 "scaling_mode": args.mode,
                 "streams_per_gpu": args.streams,
+                "schedule": ("continuous batching over the timed steps (run_stream): "
+                             f"live slots per K {stream_info['slots']}, "
+                             f"{stream_info['refill_rounds']} refill rounds")
+                if stream_info and stream_info["slots"] else "one solve per step",
                 "device": "cpu" if not use_cuda else torch.cuda.get_device_name(dev),
                 "mean_passes": round(float(np.mean(passes)), 2) if passes else None,
                 "mean_sweeps_h_w": [round(float(np.mean(h_sweeps)), 1) if h_sweeps else None,

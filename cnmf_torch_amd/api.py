@@ -906,7 +906,11 @@ class cNMF:
                     solver.opts.n_components = ks[0]
                     res = solver.run_concurrent(seeds, n_streams=int(os.environ["CNMF_STREAMS"]))
                 else:
-                    res = solver.run(seeds, ks=ks, on_retire=on_retire)
+                    # continuous batching when a K has more replicates than one co-resident
+                    # round of its usage solve holds (NMFBatchSolver.run_stream; else the
+                    # one-batch run): usages are only kept when they are saved
+                    res = solver.run_stream(seeds, ks=ks, keep_usages=save_usages,
+                                            on_result=on_retire)
                 W = res.W.cpu().numpy()
                 wall = time.perf_counter() - t0
                 log.info("K=%s: %d replicates in %.3f s (%.1f replicates/s) on %s",

@@ -81,7 +81,11 @@ def exact_moment_digits(X, threads: int = 16):
     if isinstance(X, torch.Tensor):
         if X.is_cuda:
             from .. import ops
-            return ops.exact_moments(X)
+            if ops.use_native(X):
+                return ops.exact_moments(X)
+            # torch-ops debug mode (CNMF_FORCE_TORCH_OPS / eager_ops): the host digits of
+            # the same values -- the same integers the kernel sums
+            X = X.cpu()
         X = X.numpy()
     if sp.issparse(X):
         Xc = sp.csr_matrix(X)

@@ -44,6 +44,7 @@ decision are identical on all ranks while H rows stay rank-local.
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import math
 import os
@@ -417,12 +418,12 @@ class _Batch:
         # replicates a compaction retires, copied to pinned memory (ready at `event`), so
         # the caller can persist them while the rest of the batch is still solving
         self.on_retire = None
-        self.dslots = None        # device-side ragged batching state (_dev_slots), fused runs
         self.uid = next(_BATCH_UIDS)   # never reused (unlike id()): plane-cache keys
         self.bucket = max(1, int(os.environ.get("CNMF_COMPACT_BUCKET",
                                                 "8" if W.device.type == "cuda" else "1")))
         self.A = None   # flat per-position K*K sufficient statistics (online 'exact' mode)
         self.B = None   # (rows, G)
+        self.feed = None          # _Feed of a streaming run (NMFBatchSolver.run_stream)
         self._layout()
 
     def _layout(self) -> None:
@@ -497,7 +498,7 @@ class _Batch:
         keep, rest = self._plan(act)
         n_new = int(sum(k.size for k in keep))
         if n_new == n:
-            return
+            return None
         perm = np.concatenate(keep + rest + [np.arange(n, self.R)]).astype(np.int64)
         dev = self.W.device
         roff = np.concatenate([[0], np.cumsum(self.kpos)[:-1]])
@@ -535,6 +536,7 @@ class _Batch:
             ev = torch.cuda.Event()
             ev.record()
             self.on_retire(self.order[n_new:n].copy(), self.kpos[n_new:n].copy(), host, ev)
+        return perm
 
     def set_err(self, err: torch.Tensor, pass_idx: int, tol: float, final: bool,
                 init: bool = False) -> None:
@@ -613,7 +615,6 @@ class _PassPipeline:
         self.frac_small = compact_frac if (explicit or not late_small) else \
             float(os.environ.get("CNMF_COMPACT_FRAC_SMALL", "0.75"))
         self.pending = None   # (event, host_flags, n)
-        self._side = None     # flag-copy stream (CUDA)
 
     def _frac(self, n: int) -> float:
         return self.frac_small if n <= 256 else self.frac
@@ -631,26 +632,12 @@ class _PassPipeline:
                 st.compact()
             return True
         flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
-        # CNMF_FLAG_STREAM=1: the flag copy runs on a side stream behind an event of the
-        # compute stream, so the next pass's first kernel does not queue behind the copy's
-        # blit kernel.  Flags only go 1 -> 0: a copy that overlaps the next pass reads
-        # stale-or-newer flags, both valid
-        act = st.state["active"][:n]
-        if _FLAG_STREAM:
-            main = torch.cuda.current_stream(act.device)
-            side = self._side
-            if side is None:
-                side = self._side = torch.cuda.Stream(act.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                flags.copy_(act, non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(side)
-            act.record_stream(side)
-        else:
-            flags.copy_(act, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
+        # (a flag copy on a side stream removed the ~5 us gap per pass in the trace but was
+        # slower end to end -- headline -2 %, K grid -5.5 %, profiles/r3y_*: the stream
+        # switch and event sit on the host's enqueue path)
+        flags.copy_(st.state["active"][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
         prev, self.pending = self.pending, (ev, flags, n)
         if prev is None:
             return True
@@ -668,6 +655,38 @@ class _PassPipeline:
             self.pending = None
             return st.n_act > 0
         return True
+
+
+class _Feed:
+    """Host side of a streaming run (NMFBatchSolver.run_stream): the replicates still
+    waiting, one queue per K in ledger order; which replicate occupies each batch
+    position (``occ``, -1 = free) and after which host pass it was placed there
+    (``placed``: the active flags copied after pass q describe the occupant only when
+    q > placed); and the device result store every finished replicate is copied into
+    (rows of replicate i at ``offs[i]``, as NMFResult)."""
+
+    def __init__(self, seeds, ks, n_pos: int, dev, N: int, G: int, keep_usages: bool,
+                 dtype=torch.float32):
+        self.seeds = np.asarray(seeds, dtype=np.int64)
+        self.ks = np.asarray(ks, dtype=np.int64)
+        R = self.seeds.size
+        self.offs = np.concatenate([[0], np.cumsum(self.ks)[:-1]]).astype(np.int64)
+        self.queue = {int(K): collections.deque(np.flatnonzero(self.ks == K).tolist())
+                      for K in np.unique(self.ks)}
+        self.occ = np.full(n_pos, -1, dtype=np.int64)
+        self.placed = np.full(n_pos, -1, dtype=np.int64)
+        tot = int(self.ks.sum())
+        self.W = torch.empty((tot, G), device=dev, dtype=dtype)
+        self.HT = torch.empty((tot, N), device=dev, dtype=dtype) if keep_usages else None
+        # err_init, err_prev, err | active, converged, n_pass, h_iters, w_iters
+        self.sf = torch.zeros((3, R), dtype=torch.float64, device=dev)
+        self.si = torch.zeros((5, R), dtype=torch.int32, device=dev)
+        self.on_result = None     # callback(ids, ks, pinned host spectra rows, event)
+        self.n_done = 0
+        self.events = 0           # harvest / refill rounds (stats)
+
+    def pending(self) -> int:
+        return sum(len(q) for q in self.queue.values())
 
 
 _SQ_NORM_CACHE: dict = {}
@@ -983,33 +1002,10 @@ def native_rank(K: int) -> int:
     return -(-K // 16) * 16
 
 
-_GRAM_PROLOGUE = os.environ.get("CNMF_SOLVE_GRAM_PROLOGUE", "0") == "1"
 # first pass of a recurring batch layout from its captured graph (CNMF_LAYOUT_REPLAY=0:
 # eager) -- removes the ~330 us of host-paced idle of the compaction pass
-# (profiles/r3y_passes.txt), same-box bench within noise either way.  The pass loop's flag
-# copy on a side stream (CNMF_FLAG_STREAM=1) removes the ~5 us gap per steady pass in the
-# trace but measured slower end to end (headline -2 %, K grid -5.5 %: the per-pass stream
-# switch and event sit on the host's enqueue path; profiles/r3y_*), so it is off
+# (profiles/r3y_passes.txt), same-box bench within noise either way
 _LAYOUT_REPLAY = os.environ.get("CNMF_LAYOUT_REPLAY", "1") != "0"
-# CNMF_GEMM_GATE=1: the fused pass's split GEMMs skip themselves once no replicate is
-# active (the speculative pass after a batch that converged before online_max_pass).
-# Off by default: the bench's slowest replicates stop AT max_pass, so no speculative pass
-# runs there, and reading the flag in every GEMM measured 1.2 % slower
-# (profiles/r3ah_bench_{on,off}_*)
-_GEMM_GATE = os.environ.get("CNMF_GEMM_GATE", "0") == "1"
-_FLAG_STREAM = os.environ.get("CNMF_FLAG_STREAM", "0") == "1"
-# Device-side ragged batching of the fused step.  conv_update gives the live replicates
-# compact row slots every pass; the solves write the GEMM operands and read the GEMM
-# outputs at those slots and the plane GEMMs skip the dead M-tiles, so GEMM work falls
-# with the active fraction on a FIXED launch shape (one captured graph per run, no host
-# compaction; SURVEY.md §7.4.3, the reference syncs per iteration at cnmf.py:377).
-# Measured (profiles/r4b_*): K = 20 5,034 vs 4,803 rep/s without; K = 10 11,400 vs 12,735
-# -- at K <= 16 the split GEMMs are latency-bound (< 3 workgroup rounds), so dropping dead
-# M-tiles barely shortens them (195 -> 142 us per pass), while the host compaction it
-# replaces re-plans the few-replicate tail GEMMs with deeper k splits (212 vs 320 us per
-# tail pass).  CNMF_DEV_SLOTS: 'auto' (default) = batches whose largest K > 16, '1' always,
-# '0' never.
-_DEV_SLOTS = os.environ.get("CNMF_DEV_SLOTS", "auto")
 # fused step: split-K GEMMs of up to this many k slices hand their raw slabs to the
 # consuming solve; deeper splits (the few-replicate tail) are reduced by the GEMM's own
 # pass -- the solve would read every slab per element (CNMF_FUSED_MAX_SLABS overrides)
@@ -1236,6 +1232,122 @@ class NMFBatchSolver:
         stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": hi, "w_inner_iters": wi}
         return NMFResult(HT=HT, W=W, err=err, n_iter=n_iter, converged=conv, seeds=list(seeds),
                          K=None, stats=stats, ks=ks)
+
+    # ------------------------------------------------------------------ streaming
+    def stream_live(self, ks) -> dict:
+        """Live batch positions per K of a streaming run over the ranks ``ks``: per K the
+        replicates ONE co-resident round of the pipelined usage solve holds at the
+        online chunk width (ops.pipe_round_reps -- each K group is its own launch), at
+        most that K's count.  ``CNMF_STREAM_LIVE`` caps every K's slots."""
+        ks = np.asarray(ks, dtype=np.int64)
+        N = self.X.shape[0]
+        cw = min(N, max(1, int(self.opts.online_chunk_size)))
+        cap_env = int(os.environ.get("CNMF_STREAM_LIVE", "0") or 0)
+        out = {}
+        for K, cnt in zip(*np.unique(ks, return_counts=True)):
+            m = ops.pipe_round_reps(cw, int(K), self.X.device)
+            if cap_env > 0:
+                m = min(m, cap_env) if m > 0 else cap_env
+            out[int(K)] = int(min(cnt, m)) if m > 0 else int(cnt)
+        return out
+
+    def _stream_ok(self, ks) -> bool:
+        o = self.opts
+        return (self.X.device.type == "cuda" and self.X.dtype == torch.float32
+                and self.beta == 2.0 and o.mode == "online" and o.algo == "mu"
+                and o.online_stats == "pass" and o.online_inner_conv == "loss"
+                and o.init == "random" and not self.comm.is_distributed
+                and all(v == 0.0 for v in (o.l1_H, o.l2_H, o.l1_W, o.l2_W))
+                and int(np.max(ks)) <= 32 and not ops.eager_active()
+                and os.environ.get("CNMF_STREAM", "1") != "0")
+
+    def run_stream(self, seeds, ks=None, live=None, keep_usages: bool = True,
+                   on_result=None) -> NMFResult:
+        """Factorise one replicate per seed with CONTINUOUS batching: the batch holds a
+        fixed number of live positions per K (``live``: an int for every K or a {K: n}
+        dict; default :meth:`stream_live`), and every position whose replicate converged
+        is handed the next waiting replicate of the same K at the next pass boundary --
+        Philox init, its initial error, and its Gram / planes for the fused step, written
+        in place (the layout, and so the pass's captured HIP graph, never changes while
+        replicates wait).  Every replicate runs exactly its own solve: its own pass
+        count (the device applies ``online_max_pass`` per replicate), convergence rule
+        and statistics -- only WHICH replicates share a pass changes, so a 100-replicate
+        ledger batch that ends in a tail of a few slow replicates no longer idles the
+        GPU: the tail overlaps the next replicates' first passes (the
+        reference runs replicates serially, cnmf.py:882-892).  Results are in the
+        callers' order as from :meth:`run`; ``keep_usages`` False drops HT (factorize
+        discards usages, cnmf.py:889-892).  ``on_result``: as run's ``on_retire``.
+        Shapes the streaming path does not take (CPU, beta != 2, HALS, DP, K > 32, ...)
+        run :meth:`run` on the whole list."""
+        o = self.opts
+        seeds = [int(s_) for s_ in seeds]
+        R = len(seeds)
+        ks = np.full(R, int(o.n_components), dtype=np.int64) if ks is None else \
+            np.asarray([int(k) for k in ks], dtype=np.int64)
+        if ks.size != R:
+            raise ValueError(f"{R} seeds but {ks.size} ranks")
+        if R == 0 or not self._stream_ok(ks):
+            return self.run(seeds, ks=ks, on_retire=on_result)
+        if live is None:
+            slots = self.stream_live(ks)
+        elif isinstance(live, dict):
+            slots = {int(k): int(v) for k, v in live.items()}
+        else:
+            slots = {int(K): int(live) for K in np.unique(ks)}
+        cnt = dict(zip(*[a.tolist() for a in np.unique(ks, return_counts=True)]))
+        slots = {K: max(1, min(int(cnt[K]), int(slots.get(K, cnt[K])))) for K in cnt}
+        if all(slots[K] >= cnt[K] for K in cnt):
+            return self.run(seeds, ks=ks, on_retire=on_result)
+        t0 = time.perf_counter()
+        N, G = self.X.shape
+        dev = self.X.device
+        feed = _Feed(seeds, ks, sum(slots.values()), dev, N, G, keep_usages, self.X.dtype)
+        feed.on_result = on_result
+        first = []
+        for K in sorted(slots):
+            q = feed.queue[K]
+            first += [q.popleft() for _ in range(slots[K])]
+        first = np.asarray(first, dtype=np.int64)
+        kpos = ks[first]
+        if self._xp is False:
+            cw = min(N, int(o.online_chunk_size))
+            rows = int(kpos.sum())
+            self._ws_reserve = rows * (4 * 4 * (cw + G) + 4 * G + 6 * (cw + G))
+        arena = self._arena(kpos) if self._graphs_wanted(kpos) else None
+        if arena is not None:
+            HT, W = arena["HT"], arena["W"]
+        else:
+            HT = torch.empty((int(kpos.sum()), N), device=dev, dtype=self.X.dtype)
+            W = torch.empty((int(kpos.sum()), G), device=dev, dtype=self.X.dtype)
+        r0 = 0
+        for K in sorted(slots):
+            sel = first[kpos == K]
+            rws = slice(r0, r0 + sel.size * K)
+            init_into(HT[rws], W[rws], self.X, K, [seeds[i] for i in sel], o.init, self.comm,
+                      self.row_offset, mean=self._mean(), row_map=self.row_map)
+            r0 = rws.stop
+        st = _Batch(HT, W, kpos, arena=arena)
+        st.graphs = arena is not None
+        st.order = first.copy()
+        if not self._fused_ok(st, self._steps(N)):
+            return self.run(seeds, ks=ks, on_retire=on_result)
+        st.feed = feed
+        feed.occ[:] = first
+        self._online_frob(st)
+        cflags = ops.coop_flags(dev)
+        flat = torch.cat([feed.sf[2], feed.si[1:].to(torch.float64).reshape(-1)] +
+                         [f.view(-1)[:1].to(torch.float64) for _, f in cflags]).cpu().numpy()
+        err, rest = flat[:R], flat[R:5 * R].reshape(4, R)
+        if cflags:
+            ops.coop_check(values=flat[5 * R:], flags=cflags)
+        stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": rest[2].astype(np.int64).tolist(),
+                 "w_inner_iters": rest[3].astype(np.int64).tolist(),
+                 "stream_slots": slots, "stream_events": feed.events}
+        uni = np.unique(ks)
+        HTo = feed.HT if feed.HT is not None else torch.empty((0, N), device=dev)
+        return NMFResult(HT=HTo, W=feed.W, err=err, n_iter=rest[1].astype(np.int64),
+                         converged=rest[0] != 0, seeds=seeds,
+                         K=int(uni[0]) if uni.size == 1 else None, stats=stats, ks=ks)
 
     # ------------------------------------------------------------------ data-side GEMMs
     def _planes(self):
@@ -1593,33 +1705,6 @@ class NMFBatchSolver:
                     return False
         return True
 
-    def _dev_slots(self, st: _Batch) -> dict:
-        """The device-side ragged batching state of a fused run (conv_update ``slots``):
-        per-replicate rank, current / previous compact row slots and the two live row
-        counts -- reset to the full layout (every replicate live) at the start of a run.
-        Arena batches keep the buffers (fixed addresses for the captured pass graphs)."""
-        n, dev = st.n_act, st.W.device
-        a = st.arena
-        ds = a.get("dslots") if a is not None else None
-        if ds is None or ds["kvec"].numel() != n:
-            kv = torch.as_tensor(np.asarray(st.kpos[:n], dtype=np.int32)).to(dev)
-            ds = {"kvec": kv, "cur": torch.empty(n, dtype=torch.int32, device=dev),
-                  "prev": torch.empty(n, dtype=torch.int32, device=dev),
-                  "live": torch.empty(2, dtype=torch.int32, device=dev),
-                  # the active list (conv.hip): the solves' workgroups walk the live
-                  # replicates only (ops.solve rep_list)
-                  "alist": torch.empty(n, dtype=torch.int32, device=dev),
-                  "apos": torch.empty(n + 1, dtype=torch.int32, device=dev)}
-            if a is not None:
-                a["dslots"] = ds
-        off = torch.cumsum(ds["kvec"], 0, dtype=torch.int32) - ds["kvec"]
-        ds["cur"].copy_(off)
-        ds["prev"].copy_(off)
-        ds["live"].fill_(int(st.rows_act))
-        ds["alist"].copy_(torch.arange(n, dtype=torch.int32, device=dev))
-        ds["apos"].copy_(torch.arange(n + 1, dtype=torch.int32, device=dev))
-        return ds
-
     def _fused_bufs(self, st: _Batch, steps) -> dict:
         """Per-layout workspaces of the fused step (allocated when the layout changes)."""
         xp = self._planes()
@@ -1818,7 +1903,8 @@ class NMFBatchSolver:
                 comm.all_gather_into_(fb["lin"], fb["lin"][comm.rank * Rr:(comm.rank + 1) * Rr])
                 comm.all_gather_into_(fb["quad"], fb["quad"][comm.rank * Rr:(comm.rank + 1) * Rr])
         ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
-                        n, -1, o.tol, final=final, gate=st.gate)
+                        n, -1, o.tol, final=final, gate=st.gate,
+                        max_pass=int(o.online_max_pass))
 
     def _dp_gather_w(self, st: _Batch, fb: dict) -> None:
         """End of a DP fused run: every rank's W-solved spectra rows to every rank."""
@@ -1839,15 +1925,188 @@ class NMFBatchSolver:
         self.comm.all_gather_into_(it, it[me * Rr:(me + 1) * Rr])
         st.w_iters[:R].copy_(it[:R])
 
-    def _fused_pass(self, st: _Batch, steps, fb: dict, final: bool) -> None:
+    def _stream_loop(self, st: _Batch, steps, cur: dict) -> None:
+        """Pass loop of a streaming run (run_stream).  Each host iteration enqueues one
+        fused pass and a copy of the active flags, then reads the flags of the PREVIOUS
+        pass (the GPU never drains): positions whose occupant finished are harvested into
+        the result store and refilled from their K's queue, all in stream order behind the
+        pass just enqueued.  Once nothing waits, finished positions are compacted away as
+        in the batch pipeline.  Ends when every position is free."""
+        feed = st.feed
+        frac = _PassPipeline(st)._frac
+        min_fill = max(1, int(os.environ.get("CNMF_STREAM_MIN_FILL", "1") or 1))
+        pending = collections.deque()
+        hp = 0
+        while True:
+            self._enqueue_fused(st, steps, cur)
+            n = st.n_act
+            flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
+            flags.copy_(st.state["active"][:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            pending.append((hp, ev, flags, st.layout_version))
+            hp += 1
+            if len(pending) < 2:
+                continue
+            q, qev, qfl, qlv = pending.popleft()
+            qev.synchronize()
+            if qlv != st.layout_version:
+                continue
+            act = qfl.numpy() != 0
+            fresh = feed.placed[:n] < q           # the snapshot describes the occupant
+            done = np.flatnonzero(fresh & ~act & (feed.occ[:n] >= 0))
+            waiting = feed.pending()
+            if done.size and (done.size >= min_fill or waiting == 0
+                              or done.size == int((feed.occ[:n] >= 0).sum())):
+                self._stream_harvest(st, done)
+                if waiting:
+                    self._stream_fill(st, done, cur["fb"], hp - 1)
+            live = feed.occ[:n] >= 0
+            if not live.any() and feed.pending() == 0:
+                break
+            if feed.pending() == 0 and bool((feed.placed[:n] < q).all()):
+                # drain: every flag is current -> compact finished positions away
+                if n - st.prefix_len(live) >= max(1, int(frac(n) * n)):
+                    perm = st.compact(live)
+                    if perm is not None:
+                        feed.occ = feed.occ[perm]
+                        feed.placed = feed.placed[perm]
+                        pending.clear()
+        torch.cuda.current_stream(st.W.device).synchronize()
+
+    def _stream_harvest(self, st: _Batch, pos: np.ndarray) -> None:
+        """Copy the finished occupants of positions ``pos`` into the feed's result store
+        (spectra, usages, error / pass / convergence / iteration counters)."""
+        feed = st.feed
+        dev = st.W.device
+        ids = feed.occ[pos]
+        kk = st.kpos[pos]
+        roff = np.concatenate([[0], np.cumsum(st.kpos)[:-1]])
+        src = _to_device(_ranges(roff[pos], kk), dev)
+        dst = _to_device(_ranges(feed.offs[ids], kk), dev)
+        feed.W.index_copy_(0, dst, st.W.index_select(0, src))
+        if feed.HT is not None:
+            feed.HT.index_copy_(0, dst, st.HT.index_select(0, src))
+        pidx, iidx = _to_device(pos, dev), _to_device(ids, dev)
+        if st.inplace:
+            feed.sf.index_copy_(1, iidx, st.arena["sf"].index_select(1, pidx))
+            feed.si.index_copy_(1, iidx, st.arena["si"].index_select(1, pidx))
+        else:
+            sf = torch.stack([st.state[k].index_select(0, pidx)
+                              for k in ("err_init", "err_prev", "err")])
+            si = torch.stack([st.state[k].index_select(0, pidx)
+                              for k in ("active", "converged", "n_pass")] +
+                             [st.h_iters.index_select(0, pidx), st.w_iters.index_select(0, pidx)])
+            feed.sf.index_copy_(1, iidx, sf)
+            feed.si.index_copy_(1, iidx, si)
+        if feed.on_result is not None:
+            host = torch.empty((int(kk.sum()), st.W.shape[1]), dtype=st.W.dtype, pin_memory=True)
+            host.copy_(feed.W.index_select(0, dst), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            feed.on_result(ids.copy(), kk.copy(), host, ev)
+        feed.occ[pos] = -1
+        feed.n_done += int(pos.size)
+
+    def _stream_fill(self, st: _Batch, pos: np.ndarray, fb: dict, hp: int) -> None:
+        """Place the next waiting replicates (same K) at the free positions ``pos``: their
+        Philox init, initial error (the batch's init-mode convergence step), and the
+        fused step's W-dependent operands -- the W W^T Gram in partial slot 0 (the other
+        slots zeroed) and the spectra's bf16 planes -- written in place, so the next pass
+        (a graph replay) finds them where the finished replicates were."""
+        feed = st.feed
+        o = self.opts
+        dev = st.W.device
+        N, G = self.X.shape
+        xp = self._planes()
+        roff = np.concatenate([[0], np.cumsum(st.kpos)[:-1]])
+        take = {}
+        for j in pos.tolist():
+            K = int(st.kpos[j])
+            qu = feed.queue.get(K)
+            if qu:
+                take.setdefault(K, []).append((j, qu.popleft()))
+        if not take:
+            return
+        for K, pairs in take.items():
+            P = np.asarray([a for a, _ in pairs], dtype=np.int64)
+            I = np.asarray([b for _, b in pairs], dtype=np.int64)
+            m = P.size
+            HT_t = torch.empty((m * K, N), device=dev, dtype=self.X.dtype)
+            W_t = torch.empty((m * K, G), device=dev, dtype=self.X.dtype)
+            init_into(HT_t, W_t, self.X, K, feed.seeds[I].tolist(), o.init, self.comm,
+                      self.row_offset, mean=self._mean(), row_map=self.row_map)
+            # initial error: _init_err_frob's statistics for these replicates
+            B_t = torch.empty((m * K, G), device=dev, dtype=self.X.dtype)
+            self.stats_gemm(B_t, HT_t, 0, N, accumulate=False)
+            W3 = W_t.view(m, K, G)
+            WW = ops.gram(W3)
+            lin = (B_t.view(m, K, G) * W3).sum(dim=(1, 2)).float()
+            quad = (ops.gram(HT_t.view(m, K, N)) * WW).sum(dim=(1, 2)).float()
+            stt = {k: torch.zeros(m, dtype=torch.float64, device=dev)
+                   for k in ("err_init", "err_prev", "err")}
+            stt.update({k: torch.zeros(m, dtype=torch.int32, device=dev)
+                        for k in ("active", "converged", "n_pass")})
+            ops.conv_update(lin, quad, self.x_sq, stt, m, 0, o.tol, False, init=True)
+            rows = _to_device(_ranges(roff[P], np.full(m, K)), dev)
+            st.HT.index_copy_(0, rows, HT_t)
+            st.W.index_copy_(0, rows, W_t)
+            pidx = _to_device(P, dev)
+            zero = torch.zeros(m, dtype=torch.int32, device=dev)
+            if st.inplace:
+                st.arena["sf"].index_copy_(1, pidx, torch.stack(
+                    [stt[k] for k in ("err_init", "err_prev", "err")]))
+                st.arena["si"].index_copy_(1, pidx, torch.stack(
+                    [stt[k] for k in ("active", "converged", "n_pass")] + [zero, zero]))
+            else:
+                for k, v in stt.items():
+                    st.state[k].index_copy_(0, pidx, v)
+                st.h_iters.index_copy_(0, pidx, zero)
+                st.w_iters.index_copy_(0, pidx, zero)
+            (g,) = [g_ for g_ in st.groups if g_.p0 <= P.min() and P.max() < g_.p0 + g_.n]
+            parts = fb["parts"][g.p0](fb["WWp"])
+            blk = torch.zeros((m,) + tuple(parts.shape[1:]), device=dev, dtype=parts.dtype)
+            blk[:, 0] = WW
+            parts.index_copy_(0, _to_device(P - g.p0, dev), blk)
+            wtmp = torch.zeros((3, m * K, xp.Gp), device=dev, dtype=torch.int16)
+            ops.split_planes(W_t, wtmp, col_mul=xp.unit)
+            fb["wpl"].index_copy_(1, rows, wtmp)
+            feed.occ[P] = I
+            feed.placed[P] = hp
+            st.order[P] = I
+        st.gate.fill_(1)          # a pass after an all-finished one skips its GEMMs otherwise
+        feed.events += 1
+
+    def _enqueue_fused(self, st: _Batch, steps, cur: dict) -> None:
+        """Enqueue one single-process fused pass: from the layout's captured graph when
+        the batch has an arena (captured on the layout's second pass; a layout an earlier
+        run captured replays from its first, with only the W-dependent operands rebuilt
+        eagerly), else eagerly.  ``cur`` carries the layout's workspaces between calls."""
+        key = (st.uid, st.layout_version)
+        if cur["key"] != key:
+            sl = cur["sl"] = self._slot(st, steps) if st.graphs else None
+            cur["fb"] = sl["fb"] if sl is not None else self._fused_bufs(st, steps)
+            cur["key"] = key
+            if sl is not None and sl["graph"] is not None and _LAYOUT_REPLAY:
+                self._fused_prep(st, cur["fb"], keep_slices=True)
+                sl["graph"].replay()
+            else:
+                self._fused_pass(st, steps, cur["fb"])
+            return
+        sl = cur["sl"]
+        if sl is None or not self._replay_slot(sl, st, steps):
+            self._fused_pass(st, steps, cur["fb"])
+
+    def _fused_pass(self, st: _Batch, steps, fb: dict, final: bool = False) -> None:
         """One online pass of the fused step (see _fused_ok); same updates, stopping rules
         and statistics as the unfused pass -- the split-K sums and the accumulation of
         B / A are bitwise the unfused ones, the Grams are summed per slice instead of per
-        Gram-kernel workgroup (fp32 rounding order only)."""
+        Gram-kernel workgroup (fp32 rounding order only).  The pass limit is applied per
+        replicate on the device (conv_update max_pass), so every pass -- the last one
+        included -- is the same launch sequence and replays from one graph."""
         o = self.opts
         xp = self._planes()
-        X = self.X
-        G = X.shape[1]
+        G = self.X.shape[1]
         HT, W = st.views()
         rows = st.rows_act
         groups = st.groups
@@ -1859,77 +2118,48 @@ class NMFBatchSolver:
         wkey = self._fused_prep(st, fb, keep_slices=False)
         last_s = len(steps) - 1
         wpl = fb["wpl"]
-        # device slots (see _dev_slots): the GEMM operands / outputs live at compact rows.
-        # The spectra planes the step-0 numerator reads were written last pass (previous
-        # slots, live[0]); everything else in the pass uses this pass's slots (live[1])
-        ds = st.dslots
+        wpl_n = ops.gemm_a_planes(xp.Gp)
         for s_, ((a, b),) in enumerate(steps):
             cw = b - a
-            ks_n = ops.gemm_planes(None, wpl[:ops.gemm_a_planes(xp.Gp)], xp.x[:, a:], rows, cw,
-                                   xp.Gp, raw_slab=slabN, raw_max=_FUSED_MAX_SLABS,
-                                   gate=st.gate,
-                                   live=None if ds is None else ds["live"][int(s_ > 0):])
+            ks_n = ops.gemm_planes(None, wpl[:wpl_n], xp.x[:, a:], rows, cw, xp.Gp,
+                                   raw_slab=slabN, raw_max=_FUSED_MAX_SLABS, gate=st.gate)
             kd = -(-cw // bk) * bk
             hpl = fb["hpl"][:, :, :kd]
             hpl_n = ops.gemm_a_planes(kd)
             hcols = HT[:, a:b]
             for g in groups:
-                if ds is None:
-                    numer = slabN.as_strided((g.n, g.K, cw), (g.K * cw, cw, 1), g.r0 * cw)
-                    nsl = psl = None
-                    pl_g = hpl[:, g.rows]
-                else:
-                    numer = slabN.as_strided((g.n, g.K, cw), (g.K * cw, cw, 1), 0)
-                    nsl = (ds["prev"] if s_ == 0 else ds["cur"])[g.pos]
-                    psl = ds["cur"][g.pos]
-                    pl_g = hpl
-                ga = active[g.pos]
+                numer = slabN.as_strided((g.n, g.K, cw), (g.K * cw, cw, 1), g.r0 * cw)
                 fb["hhp_n"][g.p0] = ops.solve(
                     "mu", g.rep3(hcols), numer, None, max_iter=o.online_chunk_max_iter,
                     tol=o.online_h_tol, eps=o.eps, iters_out=h_it[g.pos], conv_mode=1,
-                    check_every=o.inner_check_every, active=ga, planes=pl_g,
-                    planes_n=hpl_n, numer_slabs=ks_n, numer_slab_stride=rows * cw,
+                    check_every=o.inner_check_every, active=active[g.pos],
+                    planes=hpl[:, g.rows], planes_n=hpl_n, numer_slabs=ks_n,
+                    numer_slab_stride=rows * cw,
                     gram_parts=fb["parts"][g.p0](fb["WWp"]), gram_parts_n=fb["wwp_n"][g.p0],
-                    gram_parts_out=fb["parts"][g.p0](fb["HHp"]), coop_device_gen=True,
-                    numer_slot=nsl, planes_slot=psl,
-                    rep_list=None if ds is None else (ds["alist"], ds["apos"], g.p0,
-                                                      g.p0 + g.n, g.p0))
+                    gram_parts_out=fb["parts"][g.p0](fb["HHp"]), coop_device_gen=True)
             ks_b = ops.gemm_planes(None, hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd,
-                                   raw_slab=slabB, raw_max=_FUSED_MAX_SLABS,
-                                   gate=st.gate if _GEMM_GATE else None,
-                                   live=None if ds is None else ds["live"][1:])
+                                   raw_slab=slabB, raw_max=_FUSED_MAX_SLABS)
             last = s_ == last_s
-            wpl_out, unit = wpl, xp.unit
-            wpl_n = ops.gemm_a_planes(xp.Gp)
             A_in, A_out = fb["A"][(s_ + 1) % 2], fb["A"][s_ % 2]
             for g in groups:
-                if ds is None:
-                    numer = slabB.as_strided((g.n, g.K, G), (g.K * G, G, 1), g.r0 * G)
-                    nsl = None
-                    wpl_g = wpl_out[:, g.rows]
-                else:
-                    numer = slabB.as_strided((g.n, g.K, G), (g.K * G, G, 1), 0)
-                    nsl = ds["cur"][g.pos]
-                    wpl_g = wpl_out
+                numer = slabB.as_strided((g.n, g.K, G), (g.K * G, G, 1), g.r0 * G)
                 fb["wwp_n"][g.p0] = ops.solve(
                     "mu", g.rep3(W), numer, None if s_ == 0 else g.gram3(A_in),
                     max_iter=o.online_chunk_max_iter, tol=o.online_w_tol, eps=o.eps,
                     lin_out=fb["lin"][g.pos] if last else None,
                     quad_out=fb["quad"][g.pos] if last else None,
                     iters_out=w_it[g.pos], conv_mode=1, check_every=o.inner_check_every,
-                    active=active[g.pos], planes=wpl_g, planes_colmul=unit,
+                    active=active[g.pos], planes=wpl[:, g.rows], planes_colmul=xp.unit,
                     planes_n=wpl_n, numer_slabs=ks_b, numer_slab_stride=rows * G,
-                    numer_scale=unit, numer_base=None if s_ == 0 else g.rep3(B),
+                    numer_scale=xp.unit, numer_base=None if s_ == 0 else g.rep3(B),
                     numer_out=None if last else g.rep3(B),
                     gram_parts=fb["parts"][g.p0](fb["HHp"]), gram_parts_n=fb["hhp_n"][g.p0],
                     gram_out=None if last else g.gram3(A_out),
-                    gram_parts_out=fb["parts"][g.p0](fb["WWp"]), coop_device_gen=True,
-                    numer_slot=nsl, planes_slot=nsl,
-                    rep_list=None if ds is None else (ds["alist"], ds["apos"], g.p0,
-                                                      g.p0 + g.n, g.p0))
+                    gram_parts_out=fb["parts"][g.p0](fb["WWp"]), coop_device_gen=True)
             fb["wwp_key"] = fb["wpl_key"] = wkey
         ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
-                        n, -1, o.tol, final=final, gate=st.gate, slots=ds)
+                        n, -1, o.tol, final=final, gate=st.gate,
+                        max_pass=int(o.online_max_pass))
 
     # ------------------------------------------------------------------ online frobenius
     def _online_frob(self, st: _Batch) -> None:
@@ -1951,44 +2181,26 @@ class NMFBatchSolver:
         graphs = _graphs_enabled(X) and not dist
         graph, graph_key, last_key = None, None, None
         fused = self._fused_ok(st, steps)
-        # (early replicate writes hand over retired replicates at host compactions)
-        slots_on = (_DEV_SLOTS == "1" or _DEV_SLOTS is True
-                    or (_DEV_SLOTS == "auto" and int(np.max(st.kpos[:st.n_act])) > 16))
-        st.dslots = self._dev_slots(st) if (fused and slots_on and st.on_retire is None
-                                            and not dist) else None
-        # device slots / DP fused: the batch keeps one layout (no host compaction: 2.0 never
-        # fires) -- the DP W-solve owns a fixed partition and only its rows of W are fresh
+        # DP fused: the batch keeps one layout (no host compaction: 2.0 never fires) -- the
+        # DP W-solve owns a fixed partition and only its rows of W are fresh
         dp_fused = fused and dist
-        pipe = _PassPipeline(st, compact_frac=2.0 if (st.dslots is not None or dp_fused)
-                             else None)
-        fb, fb_key, sl = None, None, None
+        pipe = _PassPipeline(st, compact_frac=2.0 if dp_fused else None)
+        fcur = {"fb": None, "key": None, "sl": None}
+        if fused and st.feed is not None:
+            self._stream_loop(st, steps, fcur)
+            return
         for p in range(max_pass):
             n = st.n_act
             if n == 0:
                 break
             if fused:
-                key = (st.uid, st.layout_version)
-                final = p + 1 == max_pass
-                if fb_key != key:
-                    # a new layout: its first pass replays the slot's graph when an earlier
-                    # run of the arena captured one (only the W-dependent operands are
-                    # rebuilt eagerly), else it runs eagerly
-                    sl = self._slot(st, steps) if st.graphs else None
-                    if dp_fused:
-                        fb, fb_key = self._fused_bufs_dp(st, steps), key
-                    else:
-                        fb, fb_key = (sl["fb"] if sl is not None else self._fused_bufs(st, steps)), key
-                    if dp_fused:
-                        self._fused_pass_dp(st, steps, fb, final=final)
-                    elif sl is not None and sl["graph"] is not None and not final and _LAYOUT_REPLAY:
-                        self._fused_prep(st, fb, keep_slices=True)
-                        sl["graph"].replay()
-                    else:
-                        self._fused_pass(st, steps, fb, final=final)
-                elif dp_fused:
-                    self._fused_pass_dp(st, steps, fb, final=final)
-                elif sl is None or final or not self._replay_slot(sl, st, steps):
-                    self._fused_pass(st, steps, fb, final=final)
+                if dp_fused:
+                    key = (st.uid, st.layout_version)
+                    if fcur["key"] != key:
+                        fcur["fb"], fcur["key"] = self._fused_bufs_dp(st, steps), key
+                    self._fused_pass_dp(st, steps, fcur["fb"], final=p + 1 == max_pass)
+                else:
+                    self._enqueue_fused(st, steps, fcur)
                 if not pipe.after_enqueue():
                     break
                 continue
@@ -2041,15 +2253,12 @@ class NMFBatchSolver:
                         hpl_n = 3 if hpl is None else ops.gemm_a_planes(hpl.shape[2])
                         for g in groups:
                             ga = active[g.pos]
-                            # W W^T: its own Gram launch.  CNMF_SOLVE_GRAM_PROLOGUE=1 has
-                            # the matrix-core solve form it in its prologue instead --
-                            # measured slower on the bench (every usage-slice workgroup
-                            # re-reads W at L2 latency: +9.4 ms of solve against -4.2 ms
-                            # of Gram launches per 13 steps; profiles/README.md)
-                            WWT = None if (algo == "mu" and _GRAM_PROLOGUE) else \
-                                ops.gram(g.rep3(W), out=g.gram3(wwt_buf), active=ga)
+                            # W W^T: its own Gram launch (forming it in the matrix-core
+                            # solve's prologue, ops.solve gram_of, measured slower: every
+                            # usage-slice workgroup re-reads W at L2 latency;
+                            # profiles/README.md)
+                            WWT = ops.gram(g.rep3(W), out=g.gram3(wwt_buf), active=ga)
                             _inner_solve(algo, g.rep3(hcols), g.rep3(numerT), WWT,
-                                         gram_of=g.rep3(W) if WWT is None else None,
                                          max_iter=o.online_chunk_max_iter, tol=o.online_h_tol,
                                          l1_den=o.l1_H, l2=o.l2_H, eps=o.eps,
                                          iters_out=h_it[g.pos], conv_mode=cmode,
@@ -2142,8 +2351,8 @@ class NMFBatchSolver:
                 self.timings.setdefault("wait_pass", []).append((n, time.perf_counter() - t_w))
         if graph is not None:
             torch.cuda.current_stream().synchronize()
-        if fused and dist and fb is not None:
-            self._dp_gather_w(st, fb)
+        if fused and dist and fcur["fb"] is not None:
+            self._dp_gather_w(st, fcur["fb"])
 
     # ------------------------------------------------------------------ batch frobenius
     def _batch_frob(self, st: _Batch) -> None:

@@ -144,9 +144,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
           numer_scale: torch.Tensor | None = None, numer_base: torch.Tensor | None = None,
           numer_out: torch.Tensor | None = None, gram_parts: torch.Tensor | None = None,
           gram_parts_n: int = 0, gram_out: torch.Tensor | None = None,
-          gram_parts_out: torch.Tensor | None = None, coop_device_gen: bool = False,
-          numer_slot: torch.Tensor | None = None,
-          planes_slot: torch.Tensor | None = None, rep_list: tuple | None = None) -> int:
+          gram_parts_out: torch.Tensor | None = None, coop_device_gen: bool = False) -> int:
     """In-place fused inner solve on ``x`` (R, K, n) given ``numer`` (R, K, n) and
     ``gram`` (R, K, K); see csrc/kernels/solve.hip for the update rules.
 
@@ -186,24 +184,13 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     ``coop_device_gen``: cooperative launches tag their granules from a device-side
     generation the kernel itself advances (pipelined kernel only), so a launch captured
     in a HIP graph needs no zeroing of the granules per replay.
-    ``numer_slot`` / ``planes_slot`` (int32 device, one per replicate of the call; the
-    pipelined kernel only): replicate r's numerator rows start at row numer_slot[r] of
-    ``numer`` (then pass ``numer`` as the (R, K, n) view of the slab from row 0) and its
-    planes go to row planes_slot[r] of ``planes`` -- the compact slots of conv_update's
-    device-side ragged batching (the slots of live replicates never overlap; the caller
-    sizes the slabs / planes for the batch's rows).
-    ``rep_list`` = (alist, apos, lo, hi, base) (pipelined kernel only; conv_update's
-    device active list): the workgroups walk alist[apos[lo] ..< apos[hi]] (replicate
-    alist[i] - base of this call) instead of replicates 0..R-1, so the live replicates of
-    a ragged batch occupy the first workgroups and the rest exit at once.
     Returns S, the number of column slices per replicate the launch used.
     """
     a = ALGOS[algo]
     R, K, n = x.shape
     fused = (numer_slabs > 1 or numer_scale is not None or numer_base is not None
              or numer_out is not None or gram_parts is not None or gram_out is not None
-             or gram_parts_out is not None or coop_device_gen or numer_slot is not None
-             or planes_slot is not None or rep_list is not None)
+             or gram_parts_out is not None or coop_device_gen)
     if fused and not use_native(x):
         raise ValueError("solve: fused operands need the HIP kernels (CUDA tensors)")
     if gram is None and gram_parts is not None:
@@ -258,9 +245,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     if nsplit > 1 and max_iter != 1:
         raise ValueError("nsplit > 1 requires max_iter == 1 (no convergence test)")
     for name, t, dt in (("lin_out", lin_out, torch.float32), ("quad_out", quad_out, torch.float32),
-                        ("iters_out", iters_out, torch.int32), ("active", active, torch.int32),
-                        ("numer_slot", numer_slot, torch.int32),
-                        ("planes_slot", planes_slot, torch.int32)):
+                        ("iters_out", iters_out, torch.int32), ("active", active, torch.int32)):
         if t is not None and (t.dtype != dt or t.numel() < R or not t.is_contiguous()):
             raise ValueError(f"{name}: expected contiguous {dt} with >= {R} elements")
     if nsplit > 1:
@@ -294,20 +279,6 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                   or h.solve_pipe_tiles(K, -(-n // S)) == 0):
         raise ValueError("solve: fused operands need the pipelined MU kernel (K <= 64, "
                          "l1 = l2 = 0, conv_mode 1, cooperative slices that fit)")
-    if planes_slot is not None and planes is None:
-        raise ValueError("planes_slot needs planes")
-    al = (0, 0, 0, 0)
-    if rep_list is not None:
-        alist, apos, lo, hi, base = rep_list
-        if rep_index is not None:
-            raise ValueError("rep_list and rep_index are exclusive")
-        for nm, t in (("alist", alist), ("apos", apos)):
-            if t.dtype != torch.int32 or not t.is_contiguous() or t.device != x.device:
-                raise ValueError(f"rep_list {nm}: contiguous int32 on {x.device}")
-        if not (0 <= int(lo) <= int(hi) < apos.numel()) or int(hi) - int(lo) > R:
-            raise ValueError("rep_list: bad [lo, hi) range")
-        al = (alist.data_ptr(), apos.data_ptr() + 4 * int(lo), apos.data_ptr() + 4 * int(hi),
-              int(base))
     if fused and gram_parts_out is not None and gram_parts_out.shape[1] < S:
         raise ValueError(f"gram_parts_out: {gram_parts_out.shape[1]} slots < {S} slices")
     if S is not None:
@@ -379,10 +350,8 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             int(gen), int(epochs), ws_flag, pl_ptr, int(pl_rs), int(pl_ld), int(pl_plane),
             planes_colmul.data_ptr() if (planes is not None and planes_colmul is not None) else 0,
             int(pl_cols), int(planes_n), gs_ptr, int(gs_rs), int(gs_ld), int(gs_cols),
-            *f_args, *gen_dev, int(rpl),
-            numer_slot.data_ptr() if numer_slot is not None else 0,
-            planes_slot.data_ptr() if planes_slot is not None else 0,
-            _stamp_buffer(vcode, rpl, nblocks, S, K, x), *al, _stream_ptr(x))
+            *f_args, *gen_dev, int(rpl), _stamp_buffer(vcode, rpl, nblocks, S, K, x),
+            _stream_ptr(x))
     return int(S)
 
 
@@ -539,6 +508,23 @@ def pipe_slices(n: int, nblocks: int, K: int, dev: torch.device) -> int | None:
     return S
 
 
+def pipe_round_reps(n: int, K: int, dev: torch.device) -> int:
+    """How many replicates of ``n`` columns at rank K the pipelined MU solve runs in ONE
+    co-resident launch round (every cooperative slice resident at once), or 0 when it
+    does not take the shape.  The streaming solver sizes its live slots by this: a batch
+    past it splits the usage solve into launch rounds whose lengths are each set by
+    their slowest replicate."""
+    if _hip is None or not _hip.solve_pipe_k(K) or n <= 0:
+        return 0
+    mf = _hip.solve_mfma_max_cols(K)
+    cap = mf if mf > 0 else _hip.solve_pipe_max_cols(K)
+    if cap <= 0:
+        return 0
+    s_min = -(-n // cap)
+    per_cu = MFMA_WG_PER_CU if mf > 0 else _hip.solve_pipe_wg_per_cu(K)
+    return max(0, per_cu * _coop_resident(dev) // s_min)
+
+
 # target columns per cooperative slice of the pipelined solve (more, shorter slices fill
 # the chip; fewer, longer ones wait less on each other at the exchanges).  256 / 384 /
 # 512: K=10 13,172 / 13,229 / 13,204 rep/s, K=20 5,232 / 5,293 / 5,141 (profiles/r4i_*).
@@ -653,58 +639,23 @@ def coop_check(device: torch.device | None = None, values=None, flags=None) -> N
 # ----------------------------------------------------------------------------- convergence
 def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict, n: int,
                 pass_idx: int, tol: float, final: bool, init: bool = False,
-                gate: torch.Tensor | None = None, slots: dict | None = None) -> None:
+                gate: torch.Tensor | None = None, max_pass: int = 0) -> None:
     """Per-replicate Frobenius error from (lin, quad) and the (prev - cur)/init < tol
     stopping rule, entirely on the device (csrc/kernels/conv.hip).  ``state`` holds
     float64 err_init/err_prev/err and int32 active/converged/n_pass tensors.
     ``pass_idx < 0`` counts passes on the device (n_pass += 1), so the launch has no
-    per-pass host argument and can live in a captured graph.  ``gate`` (int32 device
-    scalar): set to 1 while any replicate is active, else 0 (gemm_planes ``gate``).
-    ``slots`` (device-side ragged batching): {"kvec": int32 rank per replicate, "cur" /
-    "prev": int32 compact row slots per replicate, "live": int32 [2] live row counts} --
-    after the flags update, cur/live[1] become the exclusive prefix sums of kvec over the
-    still-active replicates (batch order) and the old values move to prev/live[0]."""
+    per-pass host argument and can live in a captured graph.  ``max_pass`` > 0: a
+    replicate stops after its own max_pass-th pass (replicates of a streaming batch sit
+    at different passes).  ``gate`` (int32 device scalar): set to 1 while any replicate
+    is active, else 0 (gemm_planes ``gate``)."""
     if n <= 0:
         return
     if not use_native(lin):
-        reference.conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init)
+        reference.conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init,
+                              max_pass=max_pass)
         if gate is not None:
             gate.fill_(int(bool((state["active"][:n] != 0).any())))
-        if slots is not None:
-            act = (state["active"][:n] != 0) | bool(init)
-            k = slots["kvec"][:n] * act.to(torch.int32)
-            off = (torch.cumsum(k, 0) - k).to(torch.int32)
-            slots["prev"][:n] = off if init else slots["cur"][:n]
-            slots["live"][0] = int(k.sum()) if init else slots["live"][1]
-            slots["cur"][:n] = off
-            slots["live"][1] = int(k.sum())
-            if slots.get("alist") is not None:
-                ai = act.to(torch.int32)
-                pos = torch.cumsum(ai, 0, dtype=torch.int32) - ai
-                slots["apos"][:n] = pos
-                slots["apos"][n] = int(ai.sum())
-                idx = torch.nonzero(act).view(-1)
-                slots["alist"][pos[idx].long()] = idx.to(torch.int32)
         return
-    sl = (0, 0, 0, 0, 0, 0)
-    if slots is not None:
-        for key in ("kvec", "cur", "prev"):
-            t = slots[key]
-            if t.dtype != torch.int32 or not t.is_contiguous() or t.numel() < n or t.device != lin.device:
-                raise ValueError(f"slots[{key}] must be contiguous int32 with >= {n} entries")
-        lv = slots["live"]
-        if lv.dtype != torch.int32 or not lv.is_contiguous() or lv.numel() < 2 or lv.device != lin.device:
-            raise ValueError("slots[live] must be contiguous int32 with >= 2 entries")
-        sl = (slots["kvec"].data_ptr(), slots["cur"].data_ptr(), slots["prev"].data_ptr(),
-              lv.data_ptr())
-        if slots.get("alist") is not None:
-            al, ap = slots["alist"], slots["apos"]
-            if al.dtype != torch.int32 or ap.dtype != torch.int32 or al.numel() < n \
-                    or ap.numel() < n + 1 or not al.is_contiguous() or not ap.is_contiguous():
-                raise ValueError("slots[alist] / [apos]: contiguous int32 with >= n / n + 1")
-            sl = sl + (al.data_ptr(), ap.data_ptr())
-        else:
-            sl = sl + (0, 0)
     for t in (lin, quad):
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < n:
             raise ValueError("lin/quad must be contiguous float32 with >= n entries")
@@ -717,7 +668,7 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
                      state["err_prev"].data_ptr(), state["err"].data_ptr(),
                      state["active"].data_ptr(), state["converged"].data_ptr(),
                      state["n_pass"].data_ptr(), int(n), int(pass_idx), float(tol), int(final),
-                     int(init), _gate_ptr(gate, lin.device), *sl, _stream_ptr(lin))
+                     int(init), _gate_ptr(gate, lin.device), int(max_pass), _stream_ptr(lin))
 
 
 # ----------------------------------------------------------------------------- beta MU
@@ -1762,7 +1713,7 @@ def split_planes(S: torch.Tensor, out: torch.Tensor, col_mul: torch.Tensor | Non
 def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int, N: int,
                 Kd: int, accumulate: bool = False, col_scale: torch.Tensor | None = None,
                 raw_slab: torch.Tensor | None = None, raw_max: int = 1 << 30,
-                gate: torch.Tensor | None = None, live: torch.Tensor | None = None) -> int:
+                gate: torch.Tensor | None = None) -> int:
     """C[:M, :N] (+)= col_scale * sum_{i + j <= 2} A[i][:M, :Kd] . B[j][:N, :Kd]^T on the bf16
     matrix cores (gemm_planes.hip): the fp32-accurate product of the fp32 matrices whose
     exact bf16 splits are A (3 planes; or its first 2, see gemm_a_planes) and B (1-3
@@ -1780,9 +1731,7 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
     more than the reduction pass.  Returns the number of slabs in ``raw_slab`` (raw
     mode; 1 otherwise).  ``gate`` (int32 device scalar, GPU only): the kernels return at
     once when it holds 0 (conv_update's "no replicate active": the speculative pass
-    after a batch finished).  ``live`` (int32 device scalar, GPU only): output rows >= its
-    value are dead (conv_update's compact slots of the live replicates) -- M-tiles that
-    start there return at once, their rows of C / the slabs are left unspecified."""
+    after a batch finished)."""
     pa, a_rows, _ = A.shape
     pb, b_rows, _ = B.shape
     for name, t in (("A", A), ("B", B)):
@@ -1821,7 +1770,7 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
     if raw_slab is not None and ksplit > raw_max:
         # (capping ksplit at raw_max instead -- no reduction pass, fewer workgroups -- was
         # slower on the tail passes: 232 vs 212 us, profiles/r3s_*)
-        gemm_planes(C, A, B, M, N, Kd, accumulate=False, col_scale=None, gate=gate, live=live)
+        gemm_planes(C, A, B, M, N, Kd, accumulate=False, col_scale=None, gate=gate)
         return 1
     if raw_slab is not None:
         if raw_slab.numel() < ksplit * M * N:
@@ -1839,7 +1788,7 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
                      col_scale.data_ptr() if col_scale is not None else 0, int(M), int(N),
                      int(Kd), pa, pb, int(bool(accumulate)), int(variant), int(ksplit), slab,
                      gemm_stages(variant), gemm_kstep(variant), int(raw_slab is not None),
-                     _gate_ptr(gate, C.device), _gate_ptr(live, C.device), _stream_ptr(C))
+                     _gate_ptr(gate, C.device), _stream_ptr(C))
     return ksplit if raw_slab is not None else 1
 
 

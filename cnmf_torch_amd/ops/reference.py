@@ -105,7 +105,7 @@ def philox_fill(out: torch.Tensor, seeds, scales, stream: int, mode: int = 0,
         out[r].copy_((m * scales[r]).to(out.dtype))
 
 
-def conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init=False):
+def conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init=False, max_pass=0):
     e = torch.sqrt(torch.clamp(x_sq - 2.0 * lin[:n].double() + quad[:n].double(), min=0.0))
     e = e.to(state["err"].device)
     if init:
@@ -122,7 +122,8 @@ def conv_update(lin, quad, x_sq, state, n, pass_idx, tol, final, init=False):
     state["n_pass"][:n] = torch.where(act, new_pass, state["n_pass"][:n])
     rel = (state["err_prev"][:n] - e) / torch.clamp(state["err_init"][:n], min=1e-300)
     conv = act & (rel < tol)
-    stop = conv | (act & bool(final))
+    over = (new_pass >= max_pass) if max_pass > 0 else torch.zeros_like(act)
+    stop = conv | (act & (bool(final) | over))
     state["converged"][:n] = torch.where(conv, torch.ones_like(state["converged"][:n]),
                                          state["converged"][:n])
     keep = act & ~stop

@@ -120,10 +120,13 @@ class DistComm(LocalComm):
         xg = self._xgmi_for(t)
         if xg is not None:
             return xg(t)
-        if self.backend != "nccl" and t.device.type != "cpu":
-            host = t.cpu()
-            self._dist.all_reduce(host, group=self.group)
-            t.copy_(host)
+        if (self.backend == "nccl") != (t.device.type == "cuda"):
+            # stage through the backend's device: gloo reduces host tensors, RCCL device
+            # ones (a host int64 digit vector from the sharded prepare's exact moments
+            # travels over RCCL exactly -- integer sums are order-independent)
+            st = t.to(self._dev(), copy=True)
+            self._dist.all_reduce(st, group=self.group)
+            t.copy_(st)
             return t
         self._dist.all_reduce(t, group=self.group)
         return t

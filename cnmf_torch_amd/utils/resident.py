@@ -49,13 +49,24 @@ def _budget() -> int:
 
 
 def _nbytes(value) -> int:
-    n = 0
-    for v in (value.values() if isinstance(value, dict) else (value,)):
-        if hasattr(v, "element_size") and hasattr(v, "numel"):
-            n += int(v.element_size() * v.numel())
-        elif hasattr(v, "nbytes"):
-            n += int(v.nbytes)
-    return n
+    """Bytes held by a mirror: tensors / arrays, dicts of them, sparse matrices (data +
+    indices + indptr), CSR objects with those fields (ops.sparse.DeviceCSR), and
+    AnnData-like containers by their X plus the device CSR consensus attaches to them
+    (api._device_csr_cached) -- which appears AFTER remember(), so totals are recounted
+    on every remember (see there)."""
+    if value is None:
+        return 0
+    if isinstance(value, dict):
+        return sum(_nbytes(v) for v in value.values())
+    if hasattr(value, "element_size") and hasattr(value, "numel"):
+        return int(value.element_size() * value.numel())
+    if all(hasattr(value, a) for a in ("data", "indices", "indptr")):
+        return sum(_nbytes(getattr(value, a)) for a in ("data", "indices", "indptr"))
+    if hasattr(value, "nbytes"):
+        return int(value.nbytes)
+    if hasattr(value, "X") and hasattr(value, "obs"):
+        return _nbytes(value.X) + _nbytes(value.__dict__.get("_cnmf_device_csr"))
+    return 0
 
 
 def wanted(X) -> bool:
@@ -80,10 +91,13 @@ def remember(path: str, tag: str, value) -> bool:
         # drop every other tag of this path too (they mirror an older write)
         for k in [k for k in _CACHE if k[0] == key[0]]:
             del _CACHE[k]
-        total = sum(e[2] for e in _CACHE.values())
+        # recounted: an entry may have grown since it was remembered (the device CSR
+        # consensus attaches to a remembered TPM AnnData)
+        sizes = {k: _nbytes(e[1]) for k, e in _CACHE.items()}
+        total = sum(sizes.values())
         while _CACHE and total + nb > budget:
-            _, e = _CACHE.popitem(last=False)
-            total -= e[2]
+            k, _ = _CACHE.popitem(last=False)
+            total -= sizes[k]
         _CACHE[key] = (sig, value, nb)
     return True
 

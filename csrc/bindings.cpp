@@ -91,8 +91,7 @@ PYBIND11_MODULE(_hip, m) {
            uintptr_t n_scale, uintptr_t nbase, uintptr_t nout, long long nb_rs, long long ldnb,
            uintptr_t gpart, int gpart_n, long long gpart_rs, uintptr_t gout, uintptr_t gp_out,
            long long gp_rs, uintptr_t coop_gen_dev, uintptr_t coop_arrive, int reps_per_launch,
-           uintptr_t nslot, uintptr_t plslot, uintptr_t stamps, uintptr_t alist, uintptr_t alo,
-           uintptr_t ahi, int abase, uintptr_t stream) {
+           uintptr_t stamps, uintptr_t stream) {
           check(cnmf_solve(algo, K, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
                            P<const float>(gram), g_rs, P<const int>(rep_index), nblocks, ncols,
                            max_iter, tol, l1_num, l1_den, l2, eps, P<float>(lin_out),
@@ -106,25 +105,20 @@ PYBIND11_MODULE(_hip, m) {
                            P<const float>(n_scale), P<const float>(nbase), P<float>(nout), nb_rs,
                            ldnb, P<const float>(gpart), gpart_n, gpart_rs, P<float>(gout),
                            P<float>(gp_out), gp_rs, P<unsigned>(coop_gen_dev),
-                           P<unsigned>(coop_arrive), reps_per_launch, P<const int>(nslot),
-                           P<const int>(plslot), P<unsigned long long>(stamps),
-                           P<const int>(alist), P<const int>(alo), P<const int>(ahi), abase,
-                           reinterpret_cast<hipStream_t>(stream)),
+                           P<unsigned>(coop_arrive), reps_per_launch,
+                           P<unsigned long long>(stamps), reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_solve");
         });
 
   m.def("conv_update",
         [](uintptr_t lin, uintptr_t quad, double x_sq, uintptr_t err_init, uintptr_t err_prev,
            uintptr_t err, uintptr_t active, uintptr_t converged, uintptr_t n_pass, int n,
-           int pass, double tol, int final_pass, int init, uintptr_t gate, uintptr_t kvec,
-           uintptr_t slot_cur, uintptr_t slot_prev, uintptr_t live, uintptr_t alist,
-           uintptr_t apos, uintptr_t stream) {
+           int pass, double tol, int final_pass, int init, uintptr_t gate, int max_pass,
+           uintptr_t stream) {
           check(cnmf_conv_update(P<const float>(lin), P<const float>(quad), x_sq,
                                  P<double>(err_init), P<double>(err_prev), P<double>(err),
                                  P<int>(active), P<int>(converged), P<int>(n_pass), n, pass, tol,
-                                 final_pass, init, P<int>(gate), P<const int>(kvec),
-                                 P<int>(slot_cur), P<int>(slot_prev), P<int>(live),
-                                 P<int>(alist), P<int>(apos),
+                                 final_pass, init, P<int>(gate), max_pass,
                                  reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_conv_update");
         });
@@ -377,13 +371,12 @@ PYBIND11_MODULE(_hip, m) {
            long long ldb, long long b_plane, int b_rows, uintptr_t C, long long ldc,
            uintptr_t col_scale, int M, int N, int Kd, int pa, int pb, int accumulate,
            int variant, int ksplit, uintptr_t slab, int stages, int kstep, int raw,
-           uintptr_t gate, uintptr_t live, uintptr_t stream) {
+           uintptr_t gate, uintptr_t stream) {
           check(cnmf_gemm_planes(P<const unsigned short>(A), lda, a_plane, a_rows,
                                  P<const unsigned short>(B), ldb, b_plane, b_rows, P<float>(C),
                                  ldc, P<const float>(col_scale), M, N, Kd, pa, pb, accumulate,
                                  variant, ksplit, P<float>(slab), stages, kstep, raw,
-                                 P<const int>(gate), P<const int>(live),
-                                 reinterpret_cast<hipStream_t>(stream)),
+                                 P<const int>(gate), reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_gemm_planes");
         });
   m.def("split_planes",

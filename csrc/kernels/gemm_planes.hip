@@ -56,10 +56,6 @@ struct PlaneGemmParams {
                             // the consuming solve sums them (solve_pipe.hip numer slabs)
   const int* gate;          // optional: *gate == 0 -> every workgroup returns at once (an
                             // online pass enqueued after every replicate had finished)
-  const int* live;          // optional: rows >= *live are dead (converged replicates past
-                            // the compact slots, conv.hip conv_slots): M-tiles starting
-                            // there return at once -- a fixed, graph-replayable grid whose
-                            // work shrinks with the live rows
 };
 
 __device__ __forceinline__ unsigned short f2bf_rn(float f) {
@@ -89,7 +85,6 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
   // gate: read now, tested after the prologue's loads are issued, so its latency hides
   // behind theirs (testing it first cost ~1 % of the headline: every GEMM waited for it)
   const int gate_v = p.gate ? *p.gate : 1;
-  const int live_v = p.live ? *p.live : 0x7fffffff;
   constexpr int NT = 64 * WM * WN;            // threads
   constexpr int WR = 16 * MI;                 // each wave owns a WR x 64 output block
   constexpr int BM = WR * WM, BN = 64 * WN;
@@ -167,7 +162,7 @@ __global__ __launch_bounds__(64 * WM * WN) void gemm_planes_kernel(PlaneGemmPara
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (kb + s < ke) issue(s, (kb + s) * BK);
-  if (gate_v == 0 || m0 >= live_v) {   // uniform: nothing to compute; drain the LDS-DMA first
+  if (gate_v == 0) {   // uniform: nothing to compute; drain the LDS-DMA first
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
@@ -403,7 +398,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
                                        const float* col_scale, int M, int N, int Kd, int pa,
                                        int pb, int accumulate, int variant, int ksplit,
                                        float* slab, int stages, int kstep, int raw,
-                                       const int* gate, const int* live, hipStream_t stream) {
+                                       const int* gate, hipStream_t stream) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (raw && !slab) return hipErrorInvalidValue;
   const int bk = 32;   // smallest k-step depth: Kd must be a multiple of it
@@ -417,7 +412,7 @@ extern "C" hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, l
   p.B = B; p.ldb = ldb; p.b_plane = b_plane; p.b_rows = b_rows;
   p.C = C; p.ldc = ldc; p.col_scale = col_scale;
   p.M = M; p.N = N; p.Kd = Kd; p.accumulate = accumulate;
-  p.ksplit = ksplit; p.slab = slab; p.raw = raw ? 1 : 0; p.gate = gate; p.live = live;
+  p.ksplit = ksplit; p.slab = slab; p.raw = raw ? 1 : 0; p.gate = gate;
   hipError_t e;
   switch (pa * 4 + pb) {
     case 9: e = cnmf::launch_variant<2, 1>(variant, p, stages, kstep, stream); break;

@@ -22,16 +22,13 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       const float* n_scale, const float* nbase, float* nout, long long nb_rs,
                       long long ldnb, const float* gpart, int gpart_n, long long gpart_rs,
                       float* gout, float* gp_out, long long gp_rs, unsigned* coop_gen_dev,
-                      unsigned* coop_arrive, int reps_per_launch, const int* nslot,
-                      const int* plslot, unsigned long long* stamps, const int* alist,
-                      const int* alo, const int* ahi, int abase, hipStream_t stream);
+                      unsigned* coop_arrive, int reps_per_launch, unsigned long long* stamps,
+                      hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,
                             int* n_pass, int n, int pass, double tol, int final_pass,
-                            int init, int* gate, const int* kvec, int* slot_cur,
-                            int* slot_prev, int* live, int* alist, int* apos,
-                            hipStream_t stream);
+                            int init, int* gate, int max_pass, hipStream_t stream);
 int cnmf_solve_reg_max_cols(int K);
 int cnmf_solve_mfma_max_cols(int K);
 int cnmf_solve_pipe_tiles(int K, int per);
@@ -176,7 +173,7 @@ hipError_t cnmf_gemm_planes(const unsigned short* A, long long lda, long long a_
                             float* C, long long ldc, const float* col_scale, int M, int N,
                             int Kd, int pa, int pb, int accumulate, int variant, int ksplit,
                             float* slab, int stages, int kstep, int raw, const int* gate,
-                            const int* live, hipStream_t stream);
+                            hipStream_t stream);
 hipError_t cnmf_split_planes(const float* S, long long lds, int rows, int cols, int cols_pad,
                              const float* col_mul, unsigned short* P, long long ldp,
                              long long plane, int nplanes, hipStream_t stream);

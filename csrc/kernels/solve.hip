@@ -45,9 +45,7 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
                                  float* nout, long long nb_rs, long long ldnb, const float* gpart,
                                  int gpart_n, long long gpart_rs, float* gout, float* gp_out,
                                  long long gp_rs, unsigned* coop_gen_dev, unsigned* coop_arrive,
-                                 int reps_per_launch, const int* nslot, const int* plslot,
-                                 unsigned long long* stamps, const int* alist,
-                                 const int* alo, const int* ahi, int abase,
+                                 int reps_per_launch, unsigned long long* stamps,
                                  hipStream_t stream) {
   if (nblocks <= 0) return hipSuccess;
   // buffer offsets are 32-bit: a replicate's block must span < 2 GiB
@@ -81,8 +79,6 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
   p.gp_out = gp_out; p.gp_rs = gp_rs;
   p.coop_gen_dev = coop_split > 1 ? coop_gen_dev : nullptr;
   p.coop_arrive = coop_arrive;
-  p.nslot = nslot;
-  p.plslot = plslot;
   p.stamps = stamps;
   {
     // workgroup order of the pipelined kernel (SolveParams.pipe_map); CNMF_PIPE_MAP
@@ -94,15 +90,9 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
     p.pipe_map = map_env >= 0 ? map_env : -1;     // -1: chosen per launch below
     p.pipe_nblocks = nblocks;
   }
-  if ((alist != nullptr) != (alo != nullptr) || (alo != nullptr) != (ahi != nullptr))
-    return hipErrorInvalidValue;
-  p.alist = alist;
-  p.alo = alo;
-  p.ahi = ahi;
-  p.abase = abase;
   if (p.coop_gen_dev && !coop_arrive) return hipErrorInvalidValue;
   const bool fused = p.nslab_n > 1 || n_scale || nbase || nout || gpart || gout || gp_out ||
-                     (coop_split > 1 && coop_gen_dev) || nslot || plslot;
+                     (coop_split > 1 && coop_gen_dev);
   if (fused && (p.nslab_n > 1 && p.nslab_stride * 4 * (long long)p.nslab_n >= 0x7fffffffLL))
     return hipErrorInvalidValue;
   if (!gram && !gpart && !gsrc) return hipErrorInvalidValue;
@@ -159,7 +149,6 @@ extern "C" hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long
       return hipSuccess;
     }
     if (reps_per_launch > 0 && reps_per_launch < nblocks) return hipErrorInvalidValue;
-    if (alist) return hipErrorInvalidValue;     // the active list exists only in the pipe
     if (per > cnmf_solve_mfma_max_cols(K)) return hipErrorInvalidValue;
     // the fused operands exist only in the pipelined kernel: never drop them silently
     if (fused || (!gram && !gsrc)) return hipErrorInvalidValue;

@@ -68,11 +68,6 @@ struct SolveParams {
   // granules (tags in [2^31, 2^32 - 1); host tags stay below 2^31).
   unsigned* coop_gen_dev;
   unsigned* coop_arrive;
-  // Device-side ragged batching (solve_pipe.h only; conv.hip conv_slots): the numerator of
-  // replicate rep is the `numer` row nslot[rep] on (K rows of stride ldn from there), its
-  // planes go to row plslot[rep] of `planes` -- compact slots of the live replicates.
-  const int* nslot;
-  const int* plslot;
   // Diagnostic (solve_pipe.h only; nullptr in every production launch): per workgroup 8
   // uint64 at stamps[(slice * blocks + block) * 10]: s_memrealtime at start
   // and end, then cycles (s_memtime deltas) of the prologue, the sweep loop, the objective
@@ -85,14 +80,6 @@ struct SolveParams {
   // launch's replicate count (set by the launcher).
   int pipe_map;
   int pipe_nblocks;
-  // Device active list (conv.hip conv_slots; solve_pipe.h only): when alist is set, the
-  // launch's workgroup block b handles replicate alist[*alo + b] - abase while
-  // *alo + b < *ahi, and exits otherwise -- the live replicates of a ragged batch take
-  // the first workgroups (balanced over the XCDs under pipe_map 1).
-  const int* alist;
-  const int* alo;
-  const int* ahi;
-  int abase;
   // Optional (matrix-core kernel only): the system matrix is the Gram F F^T of the factor
   // F_r = gsrc + r*gs_rs (K x gs_cols, row stride gs_ld), formed in the prologue on the
   // matrix cores instead of being read from `gram` (W W^T fused into

@@ -153,17 +153,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     nsg = (int)gridDim.y;
   }
   const int bx = p.rep0 + blk;
-  int rep;
-  if (p.alist) {
-    const int ai = *p.alo + bx;
-    if (ai >= *p.ahi) {                  // past the live replicates of this launch
-      pipe_arrive(p);
-      return;
-    }
-    rep = p.alist[ai] - p.abase;
-  } else {
-    rep = p.rep_index ? p.rep_index[bx] : bx;
-  }
+  const int rep = p.rep_index ? p.rep_index[bx] : bx;
   if (p.active && p.active[rep] == 0) {   // converged replicate: untouched (uniform)
     pipe_arrive(p);
     return;
@@ -173,8 +163,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
                                                           __HIP_MEMORY_SCOPE_AGENT)
                                       : p.coop_gen;
   float* __restrict__ x = p.x + (long long)rep * p.x_rs;
-  const float* __restrict__ nu = p.numer + (p.nslot ? (long long)p.nslot[rep] * p.ldn
-                                                    : (long long)rep * p.n_rs);
+  const float* __restrict__ nu = p.numer + (long long)rep * p.n_rs;
   const float* __restrict__ gm = p.gram ? p.gram + (long long)rep * p.g_rs : nullptr;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, c = lane & 15;
@@ -490,8 +479,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     int col0 = j0 + 16 * wave + c;
     asm volatile("" : "+v"(col0));
     unsigned short* __restrict__ pl =
-        p.planes ? p.planes + (p.plslot ? (long long)p.plslot[rep] * p.pl_ld
-                                        : (long long)rep * p.pl_rs) : nullptr;
+        p.planes ? p.planes + (long long)rep * p.pl_rs : nullptr;
 #pragma unroll
     for (int i = 0; i < T; ++i) {
       const int cl = col0 + 16 * kPipeWaves * i;

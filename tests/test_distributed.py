@@ -367,3 +367,27 @@ def test_solver_raises_when_the_communicator_reports_a_failed_collective():
                                           online_max_pass=2), comm=FailedComm())
     with pytest.raises(RuntimeError, match="peer did not arrive"):
         solver.run([1, 2])
+
+
+def test_nccl_comm_stages_host_tensors_through_the_device():
+    """DistComm.allreduce_ of a HOST tensor under an RCCL ("nccl") group -- the sharded
+    prepare's int64 moment digits -- is staged through the backend's device buffer:
+    RCCL has no CPU backend.  The process group is faked; the staging copy must be what
+    the collective sees, and the reduced values must land in the caller's tensor."""
+    from cnmf_torch_amd.parallel.comm import DistComm
+
+    seen = []
+
+    class _FakeDist:
+        def all_reduce(self, x, group=None, op=None):
+            seen.append(x)
+            x.mul_(2)
+
+    c = DistComm.__new__(DistComm)
+    c._dist, c.group, c.rank, c.world_size, c.backend, c._xgmi = _FakeDist(), None, 0, 2, \
+        "nccl", None
+    c._dev = lambda: torch.device("cpu")        # stands in for the rank's GPU
+    t = torch.arange(5, dtype=torch.int64)
+    c.allreduce_(t)
+    assert len(seen) == 1 and seen[0] is not t
+    assert t.tolist() == [0, 2, 4, 6, 8]

@@ -1799,24 +1799,3 @@ def test_gemm_gate_skips_and_runs():
         finally:
             os.environ.pop("CNMF_GEMM_KSPLIT", None)
             ops.refresh_env()
-
-
-def test_gemm_gate_leaves_results_bitwise(monkeypatch):
-    """The fused pass's GEMM gate (CNMF_GEMM_GATE=1: the speculative pass after every
-    replicate finished skips its products) changes nothing: spectra, usages, errors and
-    pass counts are bitwise those of a run without the gate."""
-    from cnmf_torch_amd.models import nmf as nmf_mod
-    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
-
-    X = torch.from_numpy(normalized_counts_matrix(5000, 600, n_programs=6, seed=2)).cuda()
-    seeds = list(range(11, 51))
-    out = {}
-    for on in (True, False):
-        monkeypatch.setattr(nmf_mod, "_GEMM_GATE", on)
-        solver = nmf_mod.NMFBatchSolver(X, nmf_mod.NMFOptions(n_components=7,
-                                                              online_chunk_size=2500))
-        out[on] = solver.run(seeds)
-    a, b = out[True], out[False]
-    np.testing.assert_array_equal(a.n_iter, b.n_iter)
-    np.testing.assert_array_equal(a.err, b.err)
-    assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)

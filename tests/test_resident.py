@@ -45,3 +45,29 @@ def test_budget_evicts_oldest_and_zero_disables(tmp_path, monkeypatch):
     assert not resident.remember(paths[1], "X", np.zeros(100))
     assert resident.recall(paths[1], "X") is None
     resident.forget()
+
+
+def test_anndata_mirrors_count_their_matrix_and_attached_device_csr(tmp_path, monkeypatch):
+    """A remembered TPM AnnData counts X (sparse: data + indices + indptr) against the
+    budget, and so does the device CSR consensus attaches to it afterwards: the next
+    remember recounts and evicts it."""
+    import scipy.sparse as sp
+
+    from cnmf_torch_amd.utils.anndata_lite import AnnData
+
+    resident.forget()
+    X = sp.random(50, 40, density=0.2, format="csr", random_state=0, dtype=np.float32)
+    a = AnnData(X=X)
+    xb = X.data.nbytes + X.indices.nbytes + X.indptr.nbytes
+    assert resident._nbytes(a) == xb
+    monkeypatch.setenv("CNMF_RESIDENT_BYTES", str(2 * xb + 100))
+    p, q = tmp_path / "tpm", tmp_path / "other"
+    p.write_bytes(b"a")
+    q.write_bytes(b"b")
+    assert resident.remember(str(p), "adata", a)
+    # consensus attaches an (emulated) device CSR of the same size
+    a.__dict__["_cnmf_device_csr"] = {("cuda:0", id(X)): X.copy()}
+    assert resident._nbytes(a) == 2 * xb
+    assert resident.remember(str(q), "X", np.zeros(xb // 8 + 1))   # no longer fits beside it
+    assert resident.recall(str(p), "adata") is None
+    resident.forget()

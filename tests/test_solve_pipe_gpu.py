@@ -219,19 +219,20 @@ def test_fused_graph_replay_wide_k_bitwise_eager(monkeypatch, K):
         assert a.W.shape[0] == 24 * K
 
 
-_SLOT_CASES = [([10], "0"), ([5, 7, 13], "0"), ([20], "0"), ([5, 7, 13], "1"), ([20], "1")]
+_COMPACT_CASES = [([10], "0"), ([5, 7, 13], "0"), ([20], "0"), ([5, 7, 13], "1"), ([20], "1")]
 
 
-def _slot_id(ks, pmap):
+def _case_id(ks, pmap):
     return "k" + "_".join(map(str, ks)) + "-map" + pmap
 
 
-@pytest.mark.parametrize("ks,pmap", [pytest.param(k, m, id=_slot_id(k, m)) for k, m in _SLOT_CASES])
-def test_device_slots_bitwise_equal_uncompacted(monkeypatch, ks, pmap):
-    """Device-side ragged batching (conv_update slots; GEMMs skip dead M-tiles, solves
-    read / write at compact rows) changes where rows live, not what is computed: the
-    factorisation is bit-identical to the same fused run without slots and without host
-    compaction -- and within fp32 rounding of the host-compacted run."""
+@pytest.mark.parametrize("ks,pmap", [pytest.param(k, m, id=_case_id(k, m))
+                                     for k, m in _COMPACT_CASES])
+def test_host_compaction_matches_uncompacted(monkeypatch, ks, pmap):
+    """Host compaction of finished replicates (in-place row permutation of the arena on
+    one-pass-stale flags) changes where rows live, not what is computed: the fused run
+    with compaction equals the run that never compacts (finished replicates skipped in
+    place) to fp32 rounding -- the compacted GEMMs re-plan their k split."""
     from cnmf_torch_amd.models import nmf
     from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
 
@@ -249,99 +250,22 @@ def test_device_slots_bitwise_equal_uncompacted(monkeypatch, ks, pmap):
 
         env = dict(os.environ, CNMF_PIPE_MAP=pmap)
         r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
-                            f"{__file__}::test_device_slots_bitwise_equal_uncompacted"
-                            f"[{_slot_id(ks, pmap)}]"], env=env, capture_output=True, text=True,
+                            f"{__file__}::test_host_compaction_matches_uncompacted"
+                            f"[{_case_id(ks, pmap)}]"], env=env, capture_output=True, text=True,
                            timeout=300)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         return
-    for mode in ("slots", "plain", "compact"):
-        monkeypatch.setattr(nmf, "_DEV_SLOTS", mode == "slots")
+    for mode in ("plain", "compact"):
         frac = "2.0" if mode == "plain" else "0.25"
         monkeypatch.setenv("CNMF_COMPACT_FRAC", frac)
         monkeypatch.setenv("CNMF_COMPACT_FRAC_SMALL", frac)
         out[mode] = nmf.NMFBatchSolver(X, opts).run(seeds, ks=kk)
-    a, b, c = out["slots"], out["plain"], out["compact"]
-    assert len(set(a.n_iter.tolist())) > 1          # replicates finished at different passes
-    np.testing.assert_array_equal(a.n_iter, b.n_iter)
-    np.testing.assert_array_equal(a.err, b.err)
-    assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
-    assert np.abs(a.n_iter - c.n_iter).max() <= 1
-    same = a.n_iter == c.n_iter
-    np.testing.assert_allclose(a.err[same], c.err[same], rtol=1e-5)
-
-
-def test_conv_update_slots_match_prefix_sums():
-    """conv_update's compact slots: exclusive prefix sums of the ranks of the replicates
-    still active (batch order), the previous slots / live count moved to prev / live[0]."""
-    dev = torch.device("cuda")
-    n = 700
-    g = torch.Generator().manual_seed(3)
-    kv = torch.randint(1, 33, (n,), generator=g, dtype=torch.int32)
-    st = {k: torch.zeros(n, dtype=torch.float64, device=dev) for k in ("err_init", "err_prev", "err")}
-    st.update({k: torch.zeros(n, dtype=torch.int32, device=dev) for k in ("active", "converged", "n_pass")})
-    sl = {"kvec": kv.to(dev), "cur": torch.zeros(n, dtype=torch.int32, device=dev),
-          "prev": torch.zeros(n, dtype=torch.int32, device=dev),
-          "live": torch.zeros(2, dtype=torch.int32, device=dev),
-          "alist": torch.full((n,), -1, dtype=torch.int32, device=dev),
-          "apos": torch.full((n + 1,), -1, dtype=torch.int32, device=dev)}
-    lin = torch.rand(n, generator=g).to(dev)
-    quad = torch.rand(n, generator=g).to(dev)
-    ops.conv_update(lin, quad, 10.0, st, n, -1, 1e-4, final=False, init=True, slots=sl)
-    full = (torch.cumsum(kv, 0) - kv).to(torch.int32)
-    assert torch.equal(sl["cur"].cpu(), full) and torch.equal(sl["prev"].cpu(), full)
-    assert sl["live"].tolist() == [int(kv.sum())] * 2
-    assert torch.equal(sl["alist"].cpu(), torch.arange(n, dtype=torch.int32))
-    assert torch.equal(sl["apos"].cpu(), torch.arange(n + 1, dtype=torch.int32))
-    # half the replicates stop improving (error unchanged): they deactivate
-    lin2 = lin.clone()
-    keep = torch.rand(n, generator=g) < 0.5
-    lin2[keep.to(dev)] += 0.3
-    ops.conv_update(lin2, quad, 10.0, st, n, -1, 1e-4, final=False, slots=sl)
-    act = st["active"].cpu() != 0
-    assert torch.equal(act, keep)
-    k = kv * act.to(torch.int32)
-    want = (torch.cumsum(k, 0) - k).to(torch.int32)
-    assert torch.equal(sl["cur"].cpu()[act], want[act])
-    assert torch.equal(sl["prev"].cpu(), full)
-    assert sl["live"].tolist() == [int(kv.sum()), int(k.sum())]
-    # the active list: apos = exclusive prefix count of the active flags, alist its inverse
-    ai = act.to(torch.int32)
-    pos = (torch.cumsum(ai, 0) - ai).to(torch.int32)
-    assert torch.equal(sl["apos"].cpu()[:n], pos) and int(sl["apos"][n]) == int(ai.sum())
-    assert torch.equal(sl["alist"].cpu()[:int(ai.sum())], torch.nonzero(act).view(-1).to(torch.int32))
-
-
-def test_gemm_planes_live_rows_skip_dead_tiles(monkeypatch):
-    """gemm_planes(live=...): rows below the live count equal the full product; M-tiles
-    that start at or past it are skipped (without a k split -- no reduction pass -- their
-    output rows keep their old contents)."""
-    M, N, K = 1000, 640, 2048
-    g = torch.Generator().manual_seed(11)
-    A = torch.rand((M, K), generator=g)
-    B = torch.randint(0, 100, (N, K), generator=g).float()
-    Ap = torch.zeros((3, M, K), dtype=torch.int16, device="cuda")
-    Bp = torch.zeros((1, N, K), dtype=torch.int16, device="cuda")
-    ops.split_planes(A.cuda(), Ap)
-    ops.split_planes(B.cuda(), Bp)
-    full = torch.empty((M, N), device="cuda")
-    ops.gemm_planes(full, Ap[:2], Bp, M, N, K)
-    live = torch.tensor([333], dtype=torch.int32, device="cuda")
-    C = torch.full((M, N), float("nan"), device="cuda")
-    ops.gemm_planes(C, Ap[:2], Bp, M, N, K, live=live)
-    assert torch.equal(C[:333], full[:333])
-    monkeypatch.setenv("CNMF_GEMM_KSPLIT", "1")
-    ops.refresh_env()
-    try:
-        full1 = torch.empty((M, N), device="cuda")      # the same plan, every row
-        ops.gemm_planes(full1, Ap[:2], Bp, M, N, K)
-        C = torch.full((M, N), float("nan"), device="cuda")
-        ops.gemm_planes(C, Ap[:2], Bp, M, N, K, live=live)
-        torch.cuda.synchronize()
-        assert torch.equal(C[:333], full1[:333])
-        assert torch.isnan(C[512:]).all()
-    finally:
-        monkeypatch.delenv("CNMF_GEMM_KSPLIT")
-        ops.refresh_env()
+    b, c = out["plain"], out["compact"]
+    assert len(set(b.n_iter.tolist())) > 1          # replicates finished at different passes
+    assert np.abs(b.n_iter - c.n_iter).max() <= 1
+    same = b.n_iter == c.n_iter
+    assert same.mean() > 0.8
+    np.testing.assert_allclose(b.err[same], c.err[same], rtol=1e-5)
 
 
 def test_rank_beyond_kernels_routes_to_eager_ops_on_the_gpu():
@@ -465,3 +389,63 @@ def test_to_host_pinned_copy_is_bitwise(shape, dt):
     assert a.dtype == t.cpu().numpy().dtype and a.shape == tuple(shape)
     np.testing.assert_array_equal(a, t.cpu().numpy())
     np.testing.assert_array_equal(to_host(t[1:]), t[1:].cpu().numpy())   # an offset view
+
+
+@pytest.mark.parametrize("ks", [[10], [5, 7, 13], [20]])
+def test_stream_matches_batch_solves(ks):
+    """Continuous batching (run_stream: live slots refilled from the queue as replicates
+    converge) solves every replicate as the one-batch run does: each its own pass count
+    (+-1 where fp32 summation orders of different batch compositions tip a stop test),
+    errors of same-pass replicates to 1e-5, and every replicate harvested exactly once
+    into the callers' order."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(6000, 700, n_programs=10, seed=6)).cuda()
+    kk = [k for k in ks for _ in range(30)]
+    seeds = list(range(101, 101 + len(kk)))
+    opts = NMFOptions(n_components=ks[0], online_chunk_size=2000, online_chunk_max_iter=1000)
+    solver = NMFBatchSolver(X, opts)
+    got = []
+    s = solver.run_stream(seeds, ks=kk, live=8,
+                          on_result=lambda ids, k_, host, ev: got.extend(ids.tolist()))
+    assert s.stats["stream_events"] > 0 and s.stats["stream_slots"] == {k: 8 for k in ks}
+    assert sorted(got) == list(range(len(kk)))
+    b = NMFBatchSolver(X, opts).run(seeds, ks=kk)
+    assert (s.ks == b.ks).all()
+    assert np.abs(s.n_iter - b.n_iter).max() <= 1
+    same = s.n_iter == b.n_iter
+    assert same.mean() > 0.8
+    np.testing.assert_allclose(s.err[same], b.err[same], rtol=1e-5)
+    for r in np.flatnonzero(same)[:20]:
+        wa, wb = s.spectra(r).cpu(), b.spectra(r).cpu()
+        assert float((wa - wb).norm() / wb.norm()) < 1e-3
+        ua, ub = s.usages(r).cpu(), b.usages(r).cpu()
+        assert float((ua - ub).norm() / ub.norm()) < 1e-3
+
+
+def test_stream_graph_replays_bitwise_eager_and_pass_limit(monkeypatch):
+    """A streaming run whose passes replay the layout's captured HIP graph (refills are
+    written in place between replays) equals the all-eager streaming run bit for bit, and
+    the device applies online_max_pass to every replicate separately."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(5000, 600, n_programs=10, seed=8)).cuda()
+    opts = NMFOptions(n_components=10, online_chunk_size=2500, online_chunk_max_iter=1000,
+                      online_max_pass=6)
+    seeds = list(range(3, 3 + 48))
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("CNMF_GRAPHS", mode)
+        solver = NMFBatchSolver(X, opts)
+        res[mode] = solver.run_stream(seeds, live=16)
+        if mode == "1":
+            slots = list(solver._arenas.values())[0]["slots"]
+            assert any(sl["graph"] is not None for sl in slots.values())
+    a, b = res["1"], res["0"]
+    np.testing.assert_array_equal(a.n_iter, b.n_iter)
+    np.testing.assert_array_equal(a.err, b.err)
+    assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
+    assert a.n_iter.max() == 6 and a.n_iter.min() >= 1
+    assert np.isfinite(a.err).all() and bool((a.W >= 0).all())
