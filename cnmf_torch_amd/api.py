@@ -44,6 +44,7 @@ from .models.consensus import (cluster_medians, kmeans, l2_normalize_rows, local
 from .models.hvg import (compute_tpm, exact_mean_var, get_highvar_genes,
                          get_highvar_genes_sparse, get_mean_var)
 from .models.nmf import NMFBatchSolver, NMFOptions
+from . import ops
 from .models.ols import efficient_ols_all_cols
 from .models.pp import scale as pp_scale
 from .models.refit import col_block, fit_H_online, fit_spectra_online, gene_blocks
@@ -470,11 +471,17 @@ class cNMF:
             def col_sum(M):
                 return np.asarray(M.sum(axis=0), dtype=np.float64).reshape(-1)
 
+            # the per-gene moments of this rank's block run on its GPU when there is one
+            # (exact integer digits either way: the same statistics bit for bit)
+            sdev = None
+            if torch.cuda.is_available() and ops.native_available():
+                sdev = torch.device("cuda", torch.cuda.current_device())
+
             def mean_var(M, ddof):
                 """Global column mean / variance of the row-sharded M: the exact integer
                 moments all-reduced (models.hvg.exact_mean_var -- the single-process
                 prepare's statistics, bit for bit), else the float64 two-pass."""
-                ex = exact_mean_var(M, ddof, comm)
+                ex = exact_mean_var(M, ddof, comm, device=sdev)
                 if ex is not None:
                     return ex
                 n = comm.allreduce_scalar(float(M.shape[0]))

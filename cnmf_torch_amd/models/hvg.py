@@ -69,13 +69,58 @@ def _digits_to_ints(d: np.ndarray) -> list:
     return out
 
 
-def exact_moment_digits(X, threads: int = 16):
+DEVICE_MOMENT_BLOCKS = 0      # row blocks whose digits ran on the GPU (tests, tracing)
+
+
+def _device_moment_digits(X, device, block_bytes: int = 2 << 30):
+    """exact_moment_digits of a HOST scipy-sparse / numpy matrix on the GPU: row blocks
+    of at most ``block_bytes`` dense bytes go to the device (CSR blocks are densified
+    there), exact_moments.hip adds each block's digits into one int64 accumulator --
+    integer sums, so the digits are the host path's bit for bit."""
+    global DEVICE_MOMENT_BLOCKS
+    from .. import ops
+
+    N, G = X.shape
+    dt = torch.float64 if X.dtype == np.float64 else torch.float32
+    esz = 8 if dt == torch.float64 else 4
+    rows = max(1, min(N, block_bytes // max(1, G * esz)))
+    acc = torch.zeros((G, ops.EXACT_D1 + ops.EXACT_D2), dtype=torch.int64, device=device)
+    bad = torch.zeros(1, dtype=torch.int64, device=device)
+    Xc = sp.csr_matrix(X) if sp.issparse(X) else None
+    for a in range(0, N, rows):
+        b = min(N, a + rows)
+        if Xc is not None:
+            blk = Xc[a:b]
+            dense = torch.zeros((b - a, G), dtype=dt, device=device)
+            if blk.nnz:
+                r = np.repeat(np.arange(b - a, dtype=np.int64), np.diff(blk.indptr))
+                idx = torch.from_numpy(r * G + blk.indices.astype(np.int64)).to(device)
+                dense.view(-1).index_copy_(0, idx, torch.from_numpy(
+                    np.asarray(blk.data, dtype=np.float64 if esz == 8 else np.float32)).to(device))
+        else:
+            dense = torch.from_numpy(np.ascontiguousarray(
+                X[a:b], dtype=np.float64 if esz == 8 else np.float32)).to(device)
+        ops.exact_moments(dense, acc=acc, bad_acc=bad)
+        DEVICE_MOMENT_BLOCKS += 1
+        del dense
+    o = acc.cpu().numpy()
+    return o[:, :ops.EXACT_D1].copy(), o[:, ops.EXACT_D1:].copy(), int(bad.item())
+
+
+def exact_moment_digits(X, threads: int = 16, device=None):
     """Exact per-column (sum x, sum x^2) of a scipy sparse / numpy dense / torch matrix as
     integer digit arrays ((G, D1), (G, D2) int64) plus the number of values outside the
     exact window (|x| in [2^-126, 2^127]), or None without the native module.  Integer
     digits add exactly: the sums of any row partition (threads, ranks) are the same
-    integers, so statistics built from them do not depend on how the cells are split."""
+    integers, so statistics built from them do not depend on how the cells are split.
+    ``device`` (a GPU): a host matrix's digits are formed there, block by block
+    (_device_moment_digits) -- the same integers."""
     from ..utils.io import _npzio
+    if device is not None and torch.device(device).type == "cuda" and \
+            not isinstance(X, torch.Tensor) and X.dtype in (np.float32, np.float64):
+        from .. import ops
+        if ops.native_available() and X.shape[1] > 0:
+            return _device_moment_digits(X, torch.device(device))
     if _npzio is None or not hasattr(_npzio, "exact_col_moments"):
         return None
     if isinstance(X, torch.Tensor):
@@ -120,12 +165,13 @@ def exact_mean_var_from_digits(d1, d2, n: int, ddof: int = 0):
     return mean, var
 
 
-def exact_mean_var(X, ddof: int = 0, comm=None):
+def exact_mean_var(X, ddof: int = 0, comm=None, device=None):
     """Exact column mean / variance (see exact_mean_var_from_digits) of a row block X; with
     ``comm`` the digits are all-reduced first (integer sums: the sharded statistics equal
     the single-process ones bit for bit).  None when the exact path is unavailable or a
-    value lies outside its window on any rank (callers then use floating point)."""
-    got = exact_moment_digits(X)
+    value lies outside its window on any rank (callers then use floating point).
+    ``device``: form a host X's digits on that GPU (exact_moment_digits)."""
+    got = exact_moment_digits(X, device=device)
     n_loc = int(X.shape[0])
     flag = 1 if got is None else (1 if int(got[2]) else 0)
     if comm is not None and comm.is_distributed:

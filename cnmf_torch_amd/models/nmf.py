@@ -684,9 +684,14 @@ class _Feed:
         self.on_result = None     # callback(ids, ks, pinned host spectra rows, event)
         self.n_done = 0
         self.events = 0           # harvest / refill rounds (stats)
+        self.stage: dict = {}     # K -> staged (initialised, not yet placed) replicates
+        self.stage_n: dict = {}   # K -> replicates staged at a time
+        self.t_wait = self.t_swap = 0.0   # host seconds blocked on flags / in swaps
+        self.passes = 0
 
     def pending(self) -> int:
-        return sum(len(q) for q in self.queue.values())
+        return sum(len(q) for q in self.queue.values()) + \
+            sum(int(sg["ids"].size - sg["cur"]) for sg in self.stage.values())
 
 
 _SQ_NORM_CACHE: dict = {}
@@ -1303,6 +1308,7 @@ class NMFBatchSolver:
         dev = self.X.device
         feed = _Feed(seeds, ks, sum(slots.values()), dev, N, G, keep_usages, self.X.dtype)
         feed.on_result = on_result
+        feed.stage_n = dict(slots)
         first = []
         for K in sorted(slots):
             q = feed.queue[K]
@@ -1342,7 +1348,9 @@ class NMFBatchSolver:
             ops.coop_check(values=flat[5 * R:], flags=cflags)
         stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": rest[2].astype(np.int64).tolist(),
                  "w_inner_iters": rest[3].astype(np.int64).tolist(),
-                 "stream_slots": slots, "stream_events": feed.events}
+                 "stream_slots": slots, "stream_events": feed.events,
+                 "stream_passes": feed.passes, "stream_host_wait_s": round(feed.t_wait, 4),
+                 "stream_host_swap_s": round(feed.t_swap, 4)}
         uni = np.unique(ks)
         HTo = feed.HT if feed.HT is not None else torch.empty((0, N), device=dev)
         return NMFResult(HT=HTo, W=feed.W, err=err, n_iter=rest[1].astype(np.int64),
@@ -1656,8 +1664,10 @@ class NMFBatchSolver:
                         self._fused_pass(st, steps, sl["fb"], False)
                     finally:
                         g.capture_end()
-            except RuntimeError:
+            except RuntimeError as e:
                 sl["failed"] = True
+                sl["error"] = str(e)
+                log.warning("pass graph capture failed (%s); eager passes for this layout", e)
                 return False
             main.wait_stream(sl["stream"])
             sl["graph"] = g
@@ -1934,11 +1944,15 @@ class NMFBatchSolver:
         in the batch pipeline.  Ends when every position is free."""
         feed = st.feed
         frac = _PassPipeline(st)._frac
-        min_fill = max(1, int(os.environ.get("CNMF_STREAM_MIN_FILL", "1") or 1))
+        # refill once this many positions are free (or nothing else is live): fewer,
+        # larger refill rounds -- each costs ~15 host-enqueued copies
+        env = os.environ.get("CNMF_STREAM_MIN_FILL", "")
+        min_fill = max(1, int(env) if env else st.n_act // 16)
         pending = collections.deque()
         hp = 0
         while True:
             self._enqueue_fused(st, steps, cur)
+            feed.passes += 1
             n = st.n_act
             flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
             flags.copy_(st.state["active"][:n], non_blocking=True)
@@ -1949,7 +1963,9 @@ class NMFBatchSolver:
             if len(pending) < 2:
                 continue
             q, qev, qfl, qlv = pending.popleft()
+            t_ = time.perf_counter()
             qev.synchronize()
+            feed.t_wait += time.perf_counter() - t_
             if qlv != st.layout_version:
                 continue
             act = qfl.numpy() != 0
@@ -1958,9 +1974,9 @@ class NMFBatchSolver:
             waiting = feed.pending()
             if done.size and (done.size >= min_fill or waiting == 0
                               or done.size == int((feed.occ[:n] >= 0).sum())):
-                self._stream_harvest(st, done)
-                if waiting:
-                    self._stream_fill(st, done, cur["fb"], hp - 1)
+                t_ = time.perf_counter()
+                self._stream_swap(st, done, cur["fb"], hp - 1, fill=waiting > 0)
+                feed.t_swap += time.perf_counter() - t_
             live = feed.occ[:n] >= 0
             if not live.any() and feed.pending() == 0:
                 break
@@ -1974,20 +1990,92 @@ class NMFBatchSolver:
                         pending.clear()
         torch.cuda.current_stream(st.W.device).synchronize()
 
-    def _stream_harvest(self, st: _Batch, pos: np.ndarray) -> None:
-        """Copy the finished occupants of positions ``pos`` into the feed's result store
-        (spectra, usages, error / pass / convergence / iteration counters)."""
+    def _stream_stage(self, st: _Batch, K: int, fb: dict) -> bool:
+        """Initialise the next waiting replicates of rank K into a staging block, in a
+        few large launches: Philox factors, their initial error (the init-mode
+        convergence step on the same statistics _init_err_frob forms) and the fused
+        step's W-dependent operands (W W^T as partial-Gram slot 0, the spectra's bf16
+        planes).  Refills then only copy rows out of it.  False when nothing waits."""
+        feed = st.feed
+        qu = feed.queue.get(K)
+        if not qu:
+            return False
+        o = self.opts
+        dev = st.W.device
+        N, G = self.X.shape
+        xp = self._planes()
+        per_rep = K * (N + G) * 4 * 3 + K * K * 4 * ops.kCoopMaxSlices
+        m = max(1, min(len(qu), feed.stage_n.get(K, 1), (2 << 30) // max(per_rep, 1)))
+        ids = np.asarray([qu.popleft() for _ in range(m)], dtype=np.int64)
+        HT_s = torch.empty((m * K, N), device=dev, dtype=self.X.dtype)
+        W_s = torch.empty((m * K, G), device=dev, dtype=self.X.dtype)
+        init_into(HT_s, W_s, self.X, K, feed.seeds[ids].tolist(), o.init, self.comm,
+                  self.row_offset, mean=self._mean(), row_map=self.row_map)
+        B_s = torch.empty((m * K, G), device=dev, dtype=self.X.dtype)
+        self.stats_gemm(B_s, HT_s, 0, N, accumulate=False)
+        W3 = W_s.view(m, K, G)
+        WW = ops.gram(W3)
+        lin = (B_s.view(m, K, G) * W3).sum(dim=(1, 2)).float()
+        quad = (ops.gram(HT_s.view(m, K, N)) * WW).sum(dim=(1, 2)).float()
+        del B_s
+        sf = torch.zeros((3, m), dtype=torch.float64, device=dev)
+        si = torch.zeros((5, m), dtype=torch.int32, device=dev)
+        stt = {"err_init": sf[0], "err_prev": sf[1], "err": sf[2], "active": si[0],
+               "converged": si[1], "n_pass": si[2]}
+        ops.conv_update(lin, quad, self.x_sq, stt, m, 0, o.tol, False, init=True)
+        (g,) = [g_ for g_ in st.groups if g_.K == K]
+        S = fb["parts"][g.p0](fb["WWp"]).shape[1]
+        parts = torch.zeros((m, S, K, K), device=dev, dtype=torch.float32)
+        parts[:, 0] = WW
+        wpl = torch.zeros((3, m * K, xp.Gp), device=dev, dtype=torch.int16)
+        ops.split_planes(W_s, wpl, col_mul=xp.unit)
+        feed.stage[K] = {"ids": ids, "cur": 0, "HT": HT_s, "W": W_s, "sf": sf, "si": si,
+                         "parts": parts, "wpl": wpl}
+        return True
+
+    def _stream_swap(self, st: _Batch, pos: np.ndarray, fb: dict, hp: int, fill: bool) -> None:
+        """Harvest the finished occupants of positions ``pos`` into the feed's result
+        store (spectra, usages, error / pass / convergence / iteration counters) and, when
+        ``fill``, hand those positions the next staged replicates of the same K -- their
+        rows, state and fused-step operands copied in place, so the next pass (a graph
+        replay) finds them where the finished replicates were.  Every index the copies
+        need travels to the device in ONE pinned copy."""
         feed = st.feed
         dev = st.W.device
+        roff = np.concatenate([[0], np.cumsum(st.kpos)[:-1]])
         ids = feed.occ[pos]
         kk = st.kpos[pos]
-        roff = np.concatenate([[0], np.cumsum(st.kpos)[:-1]])
-        src = _to_device(_ranges(roff[pos], kk), dev)
-        dst = _to_device(_ranges(feed.offs[ids], kk), dev)
+        # fills: (K, positions, stage slice) -- staging first (its launches precede the
+        # copies below in stream order)
+        fills = []
+        if fill:
+            byk: dict = {}
+            for j in pos.tolist():
+                byk.setdefault(int(st.kpos[j]), []).append(j)
+            for K, js in byk.items():
+                js = list(js)
+                while js:
+                    sg = feed.stage.get(K)
+                    if sg is None or sg["cur"] >= sg["ids"].size:
+                        if not self._stream_stage(st, K, fb):
+                            break
+                        sg = feed.stage[K]
+                    c = min(len(js), sg["ids"].size - sg["cur"])
+                    fills.append((K, np.asarray(js[:c], dtype=np.int64), sg, sg["cur"], c))
+                    sg["cur"] += c
+                    js = js[c:]
+        parts_h = [_ranges(roff[pos], kk), _ranges(feed.offs[ids], kk), pos, ids]
+        for K, P, sg, c0, c in fills:
+            (g,) = [g_ for g_ in st.groups if g_.K == K]
+            parts_h += [_ranges(roff[P], np.full(c, K)), P, P - g.p0]
+        sizes = [a.size for a in parts_h]
+        flat = _to_device(np.concatenate(parts_h), dev)
+        views = list(torch.split(flat, sizes))
+        src, dst, pidx, iidx = views[:4]
+        # harvest
         feed.W.index_copy_(0, dst, st.W.index_select(0, src))
         if feed.HT is not None:
             feed.HT.index_copy_(0, dst, st.HT.index_select(0, src))
-        pidx, iidx = _to_device(pos, dev), _to_device(ids, dev)
         if st.inplace:
             feed.sf.index_copy_(1, iidx, st.arena["sf"].index_select(1, pidx))
             feed.si.index_copy_(1, iidx, st.arena["si"].index_select(1, pidx))
@@ -2007,74 +2095,30 @@ class NMFBatchSolver:
             feed.on_result(ids.copy(), kk.copy(), host, ev)
         feed.occ[pos] = -1
         feed.n_done += int(pos.size)
-
-    def _stream_fill(self, st: _Batch, pos: np.ndarray, fb: dict, hp: int) -> None:
-        """Place the next waiting replicates (same K) at the free positions ``pos``: their
-        Philox init, initial error (the batch's init-mode convergence step), and the
-        fused step's W-dependent operands -- the W W^T Gram in partial slot 0 (the other
-        slots zeroed) and the spectra's bf16 planes -- written in place, so the next pass
-        (a graph replay) finds them where the finished replicates were."""
-        feed = st.feed
-        o = self.opts
-        dev = st.W.device
-        N, G = self.X.shape
-        xp = self._planes()
-        roff = np.concatenate([[0], np.cumsum(st.kpos)[:-1]])
-        take = {}
-        for j in pos.tolist():
-            K = int(st.kpos[j])
-            qu = feed.queue.get(K)
-            if qu:
-                take.setdefault(K, []).append((j, qu.popleft()))
-        if not take:
-            return
-        for K, pairs in take.items():
-            P = np.asarray([a for a, _ in pairs], dtype=np.int64)
-            I = np.asarray([b for _, b in pairs], dtype=np.int64)
-            m = P.size
-            HT_t = torch.empty((m * K, N), device=dev, dtype=self.X.dtype)
-            W_t = torch.empty((m * K, G), device=dev, dtype=self.X.dtype)
-            init_into(HT_t, W_t, self.X, K, feed.seeds[I].tolist(), o.init, self.comm,
-                      self.row_offset, mean=self._mean(), row_map=self.row_map)
-            # initial error: _init_err_frob's statistics for these replicates
-            B_t = torch.empty((m * K, G), device=dev, dtype=self.X.dtype)
-            self.stats_gemm(B_t, HT_t, 0, N, accumulate=False)
-            W3 = W_t.view(m, K, G)
-            WW = ops.gram(W3)
-            lin = (B_t.view(m, K, G) * W3).sum(dim=(1, 2)).float()
-            quad = (ops.gram(HT_t.view(m, K, N)) * WW).sum(dim=(1, 2)).float()
-            stt = {k: torch.zeros(m, dtype=torch.float64, device=dev)
-                   for k in ("err_init", "err_prev", "err")}
-            stt.update({k: torch.zeros(m, dtype=torch.int32, device=dev)
-                        for k in ("active", "converged", "n_pass")})
-            ops.conv_update(lin, quad, self.x_sq, stt, m, 0, o.tol, False, init=True)
-            rows = _to_device(_ranges(roff[P], np.full(m, K)), dev)
-            st.HT.index_copy_(0, rows, HT_t)
-            st.W.index_copy_(0, rows, W_t)
-            pidx = _to_device(P, dev)
-            zero = torch.zeros(m, dtype=torch.int32, device=dev)
+        # fill
+        for i, (K, P, sg, c0, c) in enumerate(fills):
+            rows, fp, gi = views[4 + 3 * i: 7 + 3 * i]
+            st.HT.index_copy_(0, rows, sg["HT"][c0 * K:(c0 + c) * K])
+            st.W.index_copy_(0, rows, sg["W"][c0 * K:(c0 + c) * K])
             if st.inplace:
-                st.arena["sf"].index_copy_(1, pidx, torch.stack(
-                    [stt[k] for k in ("err_init", "err_prev", "err")]))
-                st.arena["si"].index_copy_(1, pidx, torch.stack(
-                    [stt[k] for k in ("active", "converged", "n_pass")] + [zero, zero]))
+                st.arena["sf"].index_copy_(1, fp, sg["sf"][:, c0:c0 + c])
+                st.arena["si"].index_copy_(1, fp, sg["si"][:, c0:c0 + c])
             else:
-                for k, v in stt.items():
-                    st.state[k].index_copy_(0, pidx, v)
-                st.h_iters.index_copy_(0, pidx, zero)
-                st.w_iters.index_copy_(0, pidx, zero)
-            (g,) = [g_ for g_ in st.groups if g_.p0 <= P.min() and P.max() < g_.p0 + g_.n]
-            parts = fb["parts"][g.p0](fb["WWp"])
-            blk = torch.zeros((m,) + tuple(parts.shape[1:]), device=dev, dtype=parts.dtype)
-            blk[:, 0] = WW
-            parts.index_copy_(0, _to_device(P - g.p0, dev), blk)
-            wtmp = torch.zeros((3, m * K, xp.Gp), device=dev, dtype=torch.int16)
-            ops.split_planes(W_t, wtmp, col_mul=xp.unit)
-            fb["wpl"].index_copy_(1, rows, wtmp)
-            feed.occ[P] = I
+                for r_, k in enumerate(("err_init", "err_prev", "err")):
+                    st.state[k].index_copy_(0, fp, sg["sf"][r_, c0:c0 + c])
+                for r_, k in enumerate(("active", "converged", "n_pass")):
+                    st.state[k].index_copy_(0, fp, sg["si"][r_, c0:c0 + c])
+                st.h_iters.index_copy_(0, fp, sg["si"][3, c0:c0 + c])
+                st.w_iters.index_copy_(0, fp, sg["si"][4, c0:c0 + c])
+            (g,) = [g_ for g_ in st.groups if g_.K == K]
+            fb["parts"][g.p0](fb["WWp"]).index_copy_(0, gi, sg["parts"][c0:c0 + c])
+            fb["wpl"].index_copy_(1, rows, sg["wpl"][:, c0 * K:(c0 + c) * K])
+            ids_f = sg["ids"][c0:c0 + c]
+            feed.occ[P] = ids_f
             feed.placed[P] = hp
-            st.order[P] = I
-        st.gate.fill_(1)          # a pass after an all-finished one skips its GEMMs otherwise
+            st.order[P] = ids_f
+        if fills:
+            st.gate.fill_(1)      # a pass after an all-finished one skips its GEMMs otherwise
         feed.events += 1
 
     def _enqueue_fused(self, st: _Batch, steps, cur: dict) -> None:

@@ -1880,12 +1880,15 @@ def predict_err_terms(X: torch.Tensor, U: torch.Tensor, S: torch.Tensor) -> tupl
 EXACT_D1, EXACT_D2 = 13, 25     # digits of sum x / sum x^2 (csrc/kernels/exact_moments.hip)
 
 
-def exact_moments(X: torch.Tensor):
+def exact_moments(X: torch.Tensor, acc: torch.Tensor | None = None,
+                  bad_acc: torch.Tensor | None = None):
     """Exact per-column (sum x, sum x^2) of a dense device matrix (float32 / float64, unit
     column stride) as integer digits ((G, 13), (G, 25) int64 numpy) plus the count of
     values outside the exact window -- the same integers as the host path
     (models.hvg.exact_moment_digits), so statistics do not depend on the device or on how
-    the rows are split (csrc/kernels/exact_moments.hip)."""
+    the rows are split (csrc/kernels/exact_moments.hip).  With ``acc`` ((G, 38) int64
+    device) and ``bad_acc`` ((1,) int64 device) the digits are ADDED there instead (row
+    blocks of a larger matrix; integer sums, exact) and nothing is returned."""
     if not use_native(X):
         raise ValueError("exact_moments: a device tensor is required")
     if X.dim() != 2 or X.dtype not in (torch.float32, torch.float64) or \
@@ -1899,5 +1902,9 @@ def exact_moments(X: torch.Tensor):
     bad = torch.zeros(1, dtype=torch.int64, device=X.device)
     _hip.exact_moments(X.data_ptr(), int(X.dtype == torch.float64), X.stride(0), rows, G, chunks,
                        part.data_ptr(), out.data_ptr(), bad.data_ptr(), _stream_ptr(X))
+    if acc is not None:
+        acc += out
+        bad_acc += bad
+        return None
     o = out.cpu().numpy()
     return o[:, :EXACT_D1].copy(), o[:, EXACT_D1:].copy(), int(bad.item())

@@ -122,9 +122,13 @@ def prepare_worker(rank, world, port, output_dir, name, counts_fn, kw):
     from cnmf_torch_amd.parallel.comm import DistComm
 
     os.environ["CNMF_PREPARE_CHUNK_BYTES"] = str(kw.pop("_chunk_bytes", 1 << 30))
+    from cnmf_torch_amd.models import hvg
+
     comm = DistComm()
     cNMF(output_dir=output_dir, name=name).prepare(counts_fn, comm=comm, **kw)
     np.save(os.path.join(output_dir, f"maxmsg{rank}.npy"), np.array([comm.max_msg_bytes]))
+    np.save(os.path.join(output_dir, f"devblocks{rank}.npy"),
+            np.array([hvg.DEVICE_MOMENT_BLOCKS]))
     dist.destroy_process_group()
 
 

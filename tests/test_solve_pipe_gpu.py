@@ -432,7 +432,7 @@ def test_stream_graph_replays_bitwise_eager_and_pass_limit(monkeypatch):
     from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
 
     X = torch.from_numpy(normalized_counts_matrix(5000, 600, n_programs=10, seed=8)).cuda()
-    opts = NMFOptions(n_components=10, online_chunk_size=2500, online_chunk_max_iter=1000,
+    opts = NMFOptions(n_components=10, online_chunk_size=2000, online_chunk_max_iter=1000,
                       online_max_pass=6)
     seeds = list(range(3, 3 + 48))
     res = {}
@@ -440,9 +440,11 @@ def test_stream_graph_replays_bitwise_eager_and_pass_limit(monkeypatch):
         monkeypatch.setenv("CNMF_GRAPHS", mode)
         solver = NMFBatchSolver(X, opts)
         res[mode] = solver.run_stream(seeds, live=16)
+        assert res[mode].stats["stream_events"] > 0
         if mode == "1":
             slots = list(solver._arenas.values())[0]["slots"]
-            assert any(sl["graph"] is not None for sl in slots.values())
+            assert any(sl["graph"] is not None for sl in slots.values()), \
+                [sl.get("error") for sl in slots.values()]
     a, b = res["1"], res["0"]
     np.testing.assert_array_equal(a.n_iter, b.n_iter)
     np.testing.assert_array_equal(a.err, b.err)
