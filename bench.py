@@ -267,10 +267,10 @@ def main() -> int:
             to_host(res.W)
         record(res)
         stream_info = {"slots": res.stats.get("stream_slots"),
-                       "refill_rounds": res.stats.get("stream_events"),
+                       "stagings": res.stats.get("stream_stagings"),
                        "passes": res.stats.get("stream_passes"),
                        "host_wait_s": res.stats.get("stream_host_wait_s"),
-                       "host_swap_s": res.stats.get("stream_host_swap_s")}
+                       "host_stage_s": res.stats.get("stream_host_stage_s")}
     else:
         for i in range(args.warmup):
             step(i)
@@ -343,10 +343,10 @@ def main() -> int:
                 "streams_per_gpu": args.streams,
                 "schedule": ("continuous batching over the timed steps (run_stream): "
                              f"live slots per K {stream_info['slots']}, "
-                             f"{stream_info['refill_rounds']} refill rounds, "
-                             f"{stream_info['passes']} passes; host blocked on flags "
-                             f"{stream_info['host_wait_s']} s, in refills "
-                             f"{stream_info['host_swap_s']} s")
+                             f"{stream_info['stagings']} ring stagings, "
+                             f"{stream_info['passes']} passes; host blocked on counters "
+                             f"{stream_info['host_wait_s']} s, staging "
+                             f"{stream_info['host_stage_s']} s")
                 if stream_info and stream_info["slots"] else "one solve per step",
                 "device": "cpu" if not use_cuda else torch.cuda.get_device_name(dev),
                 "mean_passes": round(float(np.mean(passes)), 2) if passes else None,

@@ -657,41 +657,50 @@ class _PassPipeline:
         return True
 
 
-class _Feed:
-    """Host side of a streaming run (NMFBatchSolver.run_stream): the replicates still
-    waiting, one queue per K in ledger order; which replicate occupies each batch
-    position (``occ``, -1 = free) and after which host pass it was placed there
-    (``placed``: the active flags copied after pass q describe the occupant only when
-    q > placed); and the device result store every finished replicate is copied into
-    (rows of replicate i at ``offs[i]``, as NMFResult)."""
+_FEED_UIDS = itertools.count()
 
-    def __init__(self, seeds, ks, n_pos: int, dev, N: int, G: int, keep_usages: bool,
+
+class _Feed:
+    """State of a streaming run (NMFBatchSolver.run_stream).  Host side: the replicates
+    still waiting, one queue per K in ledger order, and per K group a RING of staged
+    (initialised) replicates with the count the host has published into it.  Device side:
+    the result store every finished replicate is copied into (rows of replicate i at
+    ``offs[i]``, as NMFResult), the per-position occupant tables, the rings, and a small
+    counter block (harvested count, each ring's consumed count) the host reads one pass
+    late (stream.hip: the swap runs inside the pass)."""
+
+    def __init__(self, seeds, ks, dev, N: int, G: int, keep_usages: bool,
                  dtype=torch.float32):
+        self.uid = next(_FEED_UIDS)
         self.seeds = np.asarray(seeds, dtype=np.int64)
         self.ks = np.asarray(ks, dtype=np.int64)
         R = self.seeds.size
         self.offs = np.concatenate([[0], np.cumsum(self.ks)[:-1]]).astype(np.int64)
         self.queue = {int(K): collections.deque(np.flatnonzero(self.ks == K).tolist())
                       for K in np.unique(self.ks)}
-        self.occ = np.full(n_pos, -1, dtype=np.int64)
-        self.placed = np.full(n_pos, -1, dtype=np.int64)
         tot = int(self.ks.sum())
-        self.W = torch.empty((tot, G), device=dev, dtype=dtype)
-        self.HT = torch.empty((tot, N), device=dev, dtype=dtype) if keep_usages else None
-        # err_init, err_prev, err | active, converged, n_pass, h_iters, w_iters
-        self.sf = torch.zeros((3, R), dtype=torch.float64, device=dev)
-        self.si = torch.zeros((5, R), dtype=torch.int32, device=dev)
-        self.on_result = None     # callback(ids, ks, pinned host spectra rows, event)
-        self.n_done = 0
-        self.events = 0           # harvest / refill rounds (stats)
-        self.stage: dict = {}     # K -> staged (initialised, not yet placed) replicates
-        self.stage_n: dict = {}   # K -> replicates staged at a time
-        self.t_wait = self.t_swap = 0.0   # host seconds blocked on flags / in swaps
+        self.store = {
+            "offs": torch.from_numpy(self.offs).to(dev),
+            "W": torch.empty((tot, G), device=dev, dtype=dtype),
+            "HT": torch.empty((tot, N), device=dev, dtype=dtype) if keep_usages else None,
+            # err_init, err_prev, err | active, converged, n_pass, h_iters, w_iters
+            "sf": torch.zeros((3, R), dtype=torch.float64, device=dev),
+            "si": torch.zeros((5, R), dtype=torch.int32, device=dev),
+        }
+        self.R = R
+        self.rings: dict = {}     # K -> ring (see NMFBatchSolver._stream_ring)
+        self.ctr = None           # int32 device [1 + n_rings]: harvested, ring heads
+        self.occ: dict = {}       # K -> int32 device occupant table of the group
+        self.plan: dict = {}      # K -> int32 device [2 n] swap plan scratch
+        self.known_head: dict = {}
+        self.done = 0             # harvested count the host has seen
         self.passes = 0
+        self.stagings = 0
+        self.t_wait = self.t_stage = 0.0
+        self.box_misses = 0       # mailbox rows that did not carry the expected pass
 
-    def pending(self) -> int:
-        return sum(len(q) for q in self.queue.values()) + \
-            sum(int(sg["ids"].size - sg["cur"]) for sg in self.stage.values())
+    def waiting(self) -> int:
+        return sum(len(q) for q in self.queue.values())
 
 
 _SQ_NORM_CACHE: dict = {}
@@ -1243,13 +1252,21 @@ class NMFBatchSolver:
         """Live batch positions per K of a streaming run over the ranks ``ks``: per K the
         replicates ONE co-resident round of the pipelined usage solve holds at the
         online chunk width (ops.pipe_round_reps -- each K group is its own launch), at
-        most that K's count.  ``CNMF_STREAM_LIVE`` caps every K's slots."""
+        most that K's count.  K > 16 does not stream by default (its count is returned):
+        there the usage solve runs in several launch rounds at 100 replicates and the
+        replicates run close to online_max_pass (mean 16.8 of 20 passes at K = 20), so
+        the batch's tail is short -- measured (profiles/r5e_*): K = 20 streamed 4,928
+        (80 slots) / 5,275 (100) vs 5,742 rep/s as one batch; K = 10: 17,570 streamed vs
+        14,071.  ``CNMF_STREAM_LIVE`` caps every K's slots (and streams any K)."""
         ks = np.asarray(ks, dtype=np.int64)
         N = self.X.shape[0]
         cw = min(N, max(1, int(self.opts.online_chunk_size)))
         cap_env = int(os.environ.get("CNMF_STREAM_LIVE", "0") or 0)
         out = {}
         for K, cnt in zip(*np.unique(ks, return_counts=True)):
+            if K > 16 and cap_env <= 0:
+                out[int(K)] = int(cnt)
+                continue
             m = ops.pipe_round_reps(cw, int(K), self.X.device)
             if cap_env > 0:
                 m = min(m, cap_env) if m > 0 else cap_env
@@ -1270,20 +1287,21 @@ class NMFBatchSolver:
                    on_result=None) -> NMFResult:
         """Factorise one replicate per seed with CONTINUOUS batching: the batch holds a
         fixed number of live positions per K (``live``: an int for every K or a {K: n}
-        dict; default :meth:`stream_live`), and every position whose replicate converged
-        is handed the next waiting replicate of the same K at the next pass boundary --
-        Philox init, its initial error, and its Gram / planes for the fused step, written
-        in place (the layout, and so the pass's captured HIP graph, never changes while
-        replicates wait).  Every replicate runs exactly its own solve: its own pass
-        count (the device applies ``online_max_pass`` per replicate), convergence rule
-        and statistics -- only WHICH replicates share a pass changes, so a 100-replicate
-        ledger batch that ends in a tail of a few slow replicates no longer idles the
-        GPU: the tail overlaps the next replicates' first passes (the
-        reference runs replicates serially, cnmf.py:882-892).  Results are in the
-        callers' order as from :meth:`run`; ``keep_usages`` False drops HT (factorize
-        discards usages, cnmf.py:889-892).  ``on_result``: as run's ``on_retire``.
-        Shapes the streaming path does not take (CPU, beta != 2, HALS, DP, K > 32, ...)
-        run :meth:`run` on the whole list."""
+        dict; default :meth:`stream_live`), and every position whose replicate stopped is
+        handed the next staged replicate of the same K at the end of that very pass, on
+        the device (stream.hip, inside the pass's captured graph): the finished replicate
+        goes to the result store, the staged one -- initialised ahead by the host in a few
+        large launches (Philox factors, initial error, W W^T and spectra planes) -- takes
+        its position.  Every replicate runs exactly its own solve: its own pass count (the
+        device applies ``online_max_pass`` per replicate), convergence rule and
+        statistics; only WHICH replicates share a pass changes, so the tail of a ledger
+        batch (a few slow replicates the GPU would run alone) overlaps the next
+        replicates' passes (the reference runs replicates serially,
+        cnmf.py:882-892).  Results are in the callers' order as from :meth:`run`;
+        ``keep_usages`` False drops HT (factorize discards usages, cnmf.py:889-892).
+        ``on_result`` is called once at the end with (ids, ks, pinned spectra, event) for
+        every replicate.  Shapes the streaming path does not take (CPU, beta != 2, HALS,
+        DP, K > 32, ...) and requests no larger than the live slots run :meth:`run`."""
         o = self.opts
         seeds = [int(s_) for s_ in seeds]
         R = len(seeds)
@@ -1306,9 +1324,7 @@ class NMFBatchSolver:
         t0 = time.perf_counter()
         N, G = self.X.shape
         dev = self.X.device
-        feed = _Feed(seeds, ks, sum(slots.values()), dev, N, G, keep_usages, self.X.dtype)
-        feed.on_result = on_result
-        feed.stage_n = dict(slots)
+        feed = _Feed(seeds, ks, dev, N, G, keep_usages, self.X.dtype)
         first = []
         for K in sorted(slots):
             q = feed.queue[K]
@@ -1319,12 +1335,10 @@ class NMFBatchSolver:
             cw = min(N, int(o.online_chunk_size))
             rows = int(kpos.sum())
             self._ws_reserve = rows * (4 * 4 * (cw + G) + 4 * G + 6 * (cw + G))
-        arena = self._arena(kpos) if self._graphs_wanted(kpos) else None
-        if arena is not None:
-            HT, W = arena["HT"], arena["W"]
-        else:
-            HT = torch.empty((int(kpos.sum()), N), device=dev, dtype=self.X.dtype)
-            W = torch.empty((int(kpos.sum()), G), device=dev, dtype=self.X.dtype)
+        # the stream's batch always lives in an arena (packed state rows the swap kernel
+        # reads and writes); graphs follow the usual rule
+        arena = self._arena(kpos)
+        HT, W = arena["HT"], arena["W"]
         r0 = 0
         for K in sorted(slots):
             sel = first[kpos == K]
@@ -1333,27 +1347,42 @@ class NMFBatchSolver:
                       self.row_offset, mean=self._mean(), row_map=self.row_map)
             r0 = rws.stop
         st = _Batch(HT, W, kpos, arena=arena)
-        st.graphs = arena is not None
+        st.graphs = self._graphs_wanted(kpos)
         st.order = first.copy()
         if not self._fused_ok(st, self._steps(N)):
             return self.run(seeds, ks=ks, on_retire=on_result)
+        feed.ctr = torch.zeros(1 + len(st.groups), dtype=torch.int32, device=dev)
+        feed.seq = torch.zeros(1, dtype=torch.int32, device=dev)
+        feed.box = ops.HostMailbox(1 + len(st.groups))
+        for i, g in enumerate(st.groups):
+            feed.occ[g.K] = torch.from_numpy(first[g.p0:g.p0 + g.n].astype(np.int32)).to(dev)
+            feed.plan[g.K] = torch.empty(2 * g.n, dtype=torch.int32, device=dev)
+            feed.known_head[g.K] = 0
         st.feed = feed
-        feed.occ[:] = first
         self._online_frob(st)
+        store = feed.store
         cflags = ops.coop_flags(dev)
-        flat = torch.cat([feed.sf[2], feed.si[1:].to(torch.float64).reshape(-1)] +
+        flat = torch.cat([store["sf"][2], store["si"][1:].to(torch.float64).reshape(-1)] +
                          [f.view(-1)[:1].to(torch.float64) for _, f in cflags]).cpu().numpy()
         err, rest = flat[:R], flat[R:5 * R].reshape(4, R)
         if cflags:
             ops.coop_check(values=flat[5 * R:], flags=cflags)
-        stats = {"wall_s": time.perf_counter() - t0, "h_inner_iters": rest[2].astype(np.int64).tolist(),
+        if on_result is not None:
+            host = torch.empty(tuple(store["W"].shape), dtype=store["W"].dtype, pin_memory=True)
+            host.copy_(store["W"], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            on_result(np.arange(R), ks.copy(), host, ev)
+        stats = {"wall_s": time.perf_counter() - t0,
+                 "h_inner_iters": rest[2].astype(np.int64).tolist(),
                  "w_inner_iters": rest[3].astype(np.int64).tolist(),
-                 "stream_slots": slots, "stream_events": feed.events,
+                 "stream_slots": slots, "stream_stagings": feed.stagings,
                  "stream_passes": feed.passes, "stream_host_wait_s": round(feed.t_wait, 4),
-                 "stream_host_swap_s": round(feed.t_swap, 4)}
+                 "stream_host_stage_s": round(feed.t_stage, 4),
+                 "stream_mailbox_misses": feed.box_misses}
         uni = np.unique(ks)
-        HTo = feed.HT if feed.HT is not None else torch.empty((0, N), device=dev)
-        return NMFResult(HT=HTo, W=feed.W, err=err, n_iter=rest[1].astype(np.int64),
+        HTo = store["HT"] if store["HT"] is not None else torch.empty((0, N), device=dev)
+        return NMFResult(HT=HTo, W=store["W"], err=err, n_iter=rest[1].astype(np.int64),
                          converged=rest[0] != 0, seeds=seeds,
                          K=int(uni[0]) if uni.size == 1 else None, stats=stats, ks=ks)
 
@@ -1629,8 +1658,9 @@ class NMFBatchSolver:
         """Per-layout slot of an arena batch: the fused step's workspaces (fixed addresses),
         a capture stream and, once captured, the pass's HIP graph."""
         a = st.arena
+        # (a streaming run's pass graph holds its feed's ring / store addresses)
         key = (st.n_act, tuple(int(k) for k in st.kpos[:st.n_act]),
-               tuple(tuple(b) for b in steps))
+               tuple(tuple(b) for b in steps), st.feed.uid if st.feed is not None else None)
         slots = a["slots"]
         sl = slots.get(key)
         if sl is None:
@@ -1936,79 +1966,140 @@ class NMFBatchSolver:
         st.w_iters[:R].copy_(it[:R])
 
     def _stream_loop(self, st: _Batch, steps, cur: dict) -> None:
-        """Pass loop of a streaming run (run_stream).  Each host iteration enqueues one
-        fused pass and a copy of the active flags, then reads the flags of the PREVIOUS
-        pass (the GPU never drains): positions whose occupant finished are harvested into
-        the result store and refilled from their K's queue, all in stream order behind the
-        pass just enqueued.  Once nothing waits, finished positions are compacted away as
-        in the batch pipeline.  Ends when every position is free."""
+        """Pass loop of a streaming run (run_stream).  Each host iteration keeps every
+        ring stocked, enqueues one fused pass -- whose end harvests and refills positions
+        on the device (_stream_swap_dev) -- and a copy of the counter block, then reads the
+        PREVIOUS pass's counters (the GPU never drains): how many replicates were
+        harvested (stop at all of them) and how far each ring was consumed (staging room).
+        Once nothing waits, positions that emptied are compacted away as in the batch
+        pipeline."""
         feed = st.feed
         frac = _PassPipeline(st)._frac
-        # refill once this many positions are free (or nothing else is live): fewer,
-        # larger refill rounds -- each costs ~15 host-enqueued copies
-        env = os.environ.get("CNMF_STREAM_MIN_FILL", "")
-        min_fill = max(1, int(env) if env else st.n_act // 16)
         pending = collections.deque()
-        hp = 0
+        dev = st.W.device
+        fb = self._stream_fb(st, cur)
+        for g in st.groups:            # every ring exists (and is stocked) before any capture
+            self._stream_ring(st, g.K, fb)
+            self._stream_stock(st, g.K, cur)
         while True:
-            self._enqueue_fused(st, steps, cur)
-            feed.passes += 1
-            n = st.n_act
-            flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
-            flags.copy_(st.state["active"][:n], non_blocking=True)
+            self._enqueue_fused(st, steps, cur)      # ends with the mailbox publish
             ev = torch.cuda.Event()
             ev.record()
-            pending.append((hp, ev, flags, st.layout_version))
-            hp += 1
+            pending.append((ev, feed.passes, st.layout_version))
+            feed.passes += 1
             if len(pending) < 2:
                 continue
-            q, qev, qfl, qlv = pending.popleft()
+            qev, q, qlv = pending.popleft()
             t_ = time.perf_counter()
             qev.synchronize()
             feed.t_wait += time.perf_counter() - t_
+            c = feed.box.read(q)
+            if c is None:                           # (never expected) fall back to a copy
+                feed.box_misses += 1
+                c = feed.ctr.tolist()
+            feed.done = c[0]
+            if feed.done >= feed.R:
+                break
             if qlv != st.layout_version:
                 continue
-            act = qfl.numpy() != 0
-            fresh = feed.placed[:n] < q           # the snapshot describes the occupant
-            done = np.flatnonzero(fresh & ~act & (feed.occ[:n] >= 0))
-            waiting = feed.pending()
-            if done.size and (done.size >= min_fill or waiting == 0
-                              or done.size == int((feed.occ[:n] >= 0).sum())):
-                t_ = time.perf_counter()
-                self._stream_swap(st, done, cur["fb"], hp - 1, fill=waiting > 0)
-                feed.t_swap += time.perf_counter() - t_
-            live = feed.occ[:n] >= 0
-            if not live.any() and feed.pending() == 0:
-                break
-            if feed.pending() == 0 and bool((feed.placed[:n] < q).all()):
-                # drain: every flag is current -> compact finished positions away
+            for i, g in enumerate(st.groups):
+                feed.known_head[g.K] = c[1 + i]
+            t_ = time.perf_counter()
+            for g in st.groups:
+                self._stream_stock(st, g.K, cur)
+            feed.t_stage += time.perf_counter() - t_
+            # drain: nothing waits and every ring is consumed -> a position that emptied
+            # stays empty; compact them away (the occupant tables are read back here)
+            if feed.waiting() == 0 and all(feed.known_head[g.K] >= feed.rings[g.K]["published"]
+                                           for g in st.groups):
+                n = st.n_act
+                occ_dev = torch.cat([feed.occ[g.K][:g.n] for g in st.groups])
+                live = occ_dev.cpu().numpy() >= 0     # (a -1 here is final: nothing to place)
+                if not live.any():       # every replicate harvested (done is one pass late)
+                    break
                 if n - st.prefix_len(live) >= max(1, int(frac(n) * n)):
                     perm = st.compact(live)
                     if perm is not None:
-                        feed.occ = feed.occ[perm]
-                        feed.placed = feed.placed[perm]
+                        self._stream_relayout(st, perm, occ_dev)
                         pending.clear()
-        torch.cuda.current_stream(st.W.device).synchronize()
+        torch.cuda.current_stream(dev).synchronize()
 
-    def _stream_stage(self, st: _Batch, K: int, fb: dict) -> bool:
-        """Initialise the next waiting replicates of rank K into a staging block, in a
-        few large launches: Philox factors, their initial error (the init-mode
-        convergence step on the same statistics _init_err_frob forms) and the fused
-        step's W-dependent operands (W W^T as partial-Gram slot 0, the spectra's bf16
-        planes).  Refills then only copy rows out of it.  False when nothing waits."""
+    def _stream_relayout(self, st: _Batch, perm: np.ndarray, occ_dev: torch.Tensor) -> None:
+        """After a drain compaction: the occupant tables follow the position permutation
+        (st.groups is the new layout), gathered on the DEVICE in stream order -- the pass
+        still in flight may harvest more positions after the host read its copy."""
+        feed = st.feed
+        dev = st.W.device
+        occ_new = occ_dev.index_select(0, _to_device(perm[:st.n_act], dev))
+        feed.ctr = torch.cat([feed.ctr[:1]] + [
+            feed.ctr.new_full((1,), feed.rings[g.K]["published"]) for g in st.groups])
+        for g in st.groups:
+            feed.occ[g.K] = occ_new[g.p0:g.p0 + g.n].clone()
+            feed.plan[g.K] = torch.empty(2 * g.n, dtype=torch.int32, device=dev)
+            ring = feed.rings[g.K]
+            ring["head"] = feed.ctr[1 + st.groups.index(g):2 + st.groups.index(g)]
+
+    def _stream_ring(self, st: _Batch, K: int, fb: dict) -> dict:
+        """The staging ring of K group: 2 x its live positions of initialised replicates
+        (factors, state, W W^T partial-Gram block, spectra planes) at fixed device
+        addresses the swap kernel copies from; head (consumed, device, in the feed's
+        counter block) / tail (published, device) counters."""
+        feed = st.feed
+        ring = feed.rings.get(K)
+        if ring is not None:
+            return ring
+        (g,) = [g_ for g_ in st.groups if g_.K == K]
+        gi = st.groups.index(g)
+        dev = st.W.device
+        N, G = self.X.shape
+        xp = self._planes()
+        S = fb["parts"][g.p0](fb["WWp"]).shape[1]
+        qc = 2 * g.n
+        ring = {"qc": qc, "block": g.n, "published": 0,
+                "head": feed.ctr[1 + gi:2 + gi],
+                "tail": torch.zeros(1, dtype=torch.int32, device=dev),
+                "ids": torch.full((qc,), -1, dtype=torch.int32, device=dev),
+                "W": torch.zeros((qc * K, G), device=dev, dtype=self.X.dtype),
+                "HT": torch.zeros((qc * K, N), device=dev, dtype=self.X.dtype),
+                "sf": torch.zeros((3, qc), dtype=torch.float64, device=dev),
+                "si": torch.zeros((5, qc), dtype=torch.int32, device=dev),
+                "parts": torch.zeros((qc, S, K, K), device=dev, dtype=torch.float32),
+                "wpl": torch.zeros((3, qc * K, fb["wpl"].shape[2]), device=dev,
+                                   dtype=torch.int16)}
+        assert fb["wpl"].shape[2] == xp.Gp
+        feed.rings[K] = ring
+        return ring
+
+    def _stream_stock(self, st: _Batch, K: int, cur: dict) -> None:
+        """Stage the next block of waiting replicates of rank K into its ring when the
+        ring has a block of room (by the consumed count the host last read): Philox
+        factors, their initial error (the init-mode convergence step on the statistics
+        _init_err_frob forms), W W^T as partial-Gram slot 0 and the spectra's bf16
+        planes, written into the ring slots; then the published count is raised, in
+        stream order behind them."""
         feed = st.feed
         qu = feed.queue.get(K)
         if not qu:
-            return False
+            return
+        fb = cur["fb"] if cur.get("fb") is not None else self._stream_fb(st, cur)
+        ring = self._stream_ring(st, K, fb)
+        qc, pub = ring["qc"], ring["published"]
+        room = qc - (pub - feed.known_head[K])
+        if room < ring["block"]:
+            return
+        m = min(len(qu), ring["block"])
         o = self.opts
         dev = st.W.device
         N, G = self.X.shape
         xp = self._planes()
-        per_rep = K * (N + G) * 4 * 3 + K * K * 4 * ops.kCoopMaxSlices
-        m = max(1, min(len(qu), feed.stage_n.get(K, 1), (2 << 30) // max(per_rep, 1)))
         ids = np.asarray([qu.popleft() for _ in range(m)], dtype=np.int64)
-        HT_s = torch.empty((m * K, N), device=dev, dtype=self.X.dtype)
-        W_s = torch.empty((m * K, G), device=dev, dtype=self.X.dtype)
+        # every staging but the last is a whole block and the ring holds two: a block
+        # always starts at slot 0 or `block`, so the replicates are initialised straight
+        # into their ring slots (no copies)
+        a0 = pub % qc
+        assert a0 + m <= qc, "stream ring: staging across the wrap"
+        HT_s = ring["HT"][a0 * K:(a0 + m) * K]
+        W_s = ring["W"][a0 * K:(a0 + m) * K]
         init_into(HT_s, W_s, self.X, K, feed.seeds[ids].tolist(), o.init, self.comm,
                   self.row_offset, mean=self._mean(), row_map=self.row_map)
         B_s = torch.empty((m * K, G), device=dev, dtype=self.X.dtype)
@@ -2018,108 +2109,48 @@ class NMFBatchSolver:
         lin = (B_s.view(m, K, G) * W3).sum(dim=(1, 2)).float()
         quad = (ops.gram(HT_s.view(m, K, N)) * WW).sum(dim=(1, 2)).float()
         del B_s
-        sf = torch.zeros((3, m), dtype=torch.float64, device=dev)
-        si = torch.zeros((5, m), dtype=torch.int32, device=dev)
+        sf, si = ring["sf"][:, a0:a0 + m], ring["si"][:, a0:a0 + m]
+        si.zero_()
         stt = {"err_init": sf[0], "err_prev": sf[1], "err": sf[2], "active": si[0],
                "converged": si[1], "n_pass": si[2]}
         ops.conv_update(lin, quad, self.x_sq, stt, m, 0, o.tol, False, init=True)
-        (g,) = [g_ for g_ in st.groups if g_.K == K]
-        S = fb["parts"][g.p0](fb["WWp"]).shape[1]
-        parts = torch.zeros((m, S, K, K), device=dev, dtype=torch.float32)
+        parts = ring["parts"][a0:a0 + m]
+        parts.zero_()
         parts[:, 0] = WW
-        wpl = torch.zeros((3, m * K, xp.Gp), device=dev, dtype=torch.int16)
-        ops.split_planes(W_s, wpl, col_mul=xp.unit)
-        feed.stage[K] = {"ids": ids, "cur": 0, "HT": HT_s, "W": W_s, "sf": sf, "si": si,
-                         "parts": parts, "wpl": wpl}
-        return True
+        ops.split_planes(W_s, ring["wpl"][:, a0 * K:(a0 + m) * K], col_mul=xp.unit)
+        ring["ids"][a0:a0 + m].copy_(_to_device(ids, dev).to(torch.int32))
+        ring["published"] = pub + m
+        ring["tail"].fill_(pub + m)
+        feed.stagings += 1
 
-    def _stream_swap(self, st: _Batch, pos: np.ndarray, fb: dict, hp: int, fill: bool) -> None:
-        """Harvest the finished occupants of positions ``pos`` into the feed's result
-        store (spectra, usages, error / pass / convergence / iteration counters) and, when
-        ``fill``, hand those positions the next staged replicates of the same K -- their
-        rows, state and fused-step operands copied in place, so the next pass (a graph
-        replay) finds them where the finished replicates were.  Every index the copies
-        need travels to the device in ONE pinned copy."""
+    def _stream_fb(self, st: _Batch, cur: dict) -> dict:
+        """The fused workspaces of the stream's current layout before its first pass."""
+        key = (st.uid, st.layout_version)
+        if cur.get("key") != key:
+            sl = cur["sl"] = self._slot(st, self._steps(self.X.shape[0])) if st.graphs else None
+            cur["fb"] = sl["fb"] if sl is not None else self._fused_bufs(st, self._steps(self.X.shape[0]))
+            cur["key"] = key
+            cur["fresh"] = True
+        return cur["fb"]
+
+    def _stream_swap_dev(self, st: _Batch, fb: dict) -> None:
+        """End of a streaming pass: per K group, harvest the stopped replicates and place
+        staged ones (ops.stream_swap, stream.hip) -- part of the captured pass."""
         feed = st.feed
-        dev = st.W.device
-        roff = np.concatenate([[0], np.cumsum(st.kpos)[:-1]])
-        ids = feed.occ[pos]
-        kk = st.kpos[pos]
-        # fills: (K, positions, stage slice) -- staging first (its launches precede the
-        # copies below in stream order)
-        fills = []
-        if fill:
-            byk: dict = {}
-            for j in pos.tolist():
-                byk.setdefault(int(st.kpos[j]), []).append(j)
-            for K, js in byk.items():
-                js = list(js)
-                while js:
-                    sg = feed.stage.get(K)
-                    if sg is None or sg["cur"] >= sg["ids"].size:
-                        if not self._stream_stage(st, K, fb):
-                            break
-                        sg = feed.stage[K]
-                    c = min(len(js), sg["ids"].size - sg["cur"])
-                    fills.append((K, np.asarray(js[:c], dtype=np.int64), sg, sg["cur"], c))
-                    sg["cur"] += c
-                    js = js[c:]
-        parts_h = [_ranges(roff[pos], kk), _ranges(feed.offs[ids], kk), pos, ids]
-        for K, P, sg, c0, c in fills:
-            (g,) = [g_ for g_ in st.groups if g_.K == K]
-            parts_h += [_ranges(roff[P], np.full(c, K)), P, P - g.p0]
-        sizes = [a.size for a in parts_h]
-        flat = _to_device(np.concatenate(parts_h), dev)
-        views = list(torch.split(flat, sizes))
-        src, dst, pidx, iidx = views[:4]
-        # harvest
-        feed.W.index_copy_(0, dst, st.W.index_select(0, src))
-        if feed.HT is not None:
-            feed.HT.index_copy_(0, dst, st.HT.index_select(0, src))
-        if st.inplace:
-            feed.sf.index_copy_(1, iidx, st.arena["sf"].index_select(1, pidx))
-            feed.si.index_copy_(1, iidx, st.arena["si"].index_select(1, pidx))
-        else:
-            sf = torch.stack([st.state[k].index_select(0, pidx)
-                              for k in ("err_init", "err_prev", "err")])
-            si = torch.stack([st.state[k].index_select(0, pidx)
-                              for k in ("active", "converged", "n_pass")] +
-                             [st.h_iters.index_select(0, pidx), st.w_iters.index_select(0, pidx)])
-            feed.sf.index_copy_(1, iidx, sf)
-            feed.si.index_copy_(1, iidx, si)
-        if feed.on_result is not None:
-            host = torch.empty((int(kk.sum()), st.W.shape[1]), dtype=st.W.dtype, pin_memory=True)
-            host.copy_(feed.W.index_select(0, dst), non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            feed.on_result(ids.copy(), kk.copy(), host, ev)
-        feed.occ[pos] = -1
-        feed.n_done += int(pos.size)
-        # fill
-        for i, (K, P, sg, c0, c) in enumerate(fills):
-            rows, fp, gi = views[4 + 3 * i: 7 + 3 * i]
-            st.HT.index_copy_(0, rows, sg["HT"][c0 * K:(c0 + c) * K])
-            st.W.index_copy_(0, rows, sg["W"][c0 * K:(c0 + c) * K])
-            if st.inplace:
-                st.arena["sf"].index_copy_(1, fp, sg["sf"][:, c0:c0 + c])
-                st.arena["si"].index_copy_(1, fp, sg["si"][:, c0:c0 + c])
-            else:
-                for r_, k in enumerate(("err_init", "err_prev", "err")):
-                    st.state[k].index_copy_(0, fp, sg["sf"][r_, c0:c0 + c])
-                for r_, k in enumerate(("active", "converged", "n_pass")):
-                    st.state[k].index_copy_(0, fp, sg["si"][r_, c0:c0 + c])
-                st.h_iters.index_copy_(0, fp, sg["si"][3, c0:c0 + c])
-                st.w_iters.index_copy_(0, fp, sg["si"][4, c0:c0 + c])
-            (g,) = [g_ for g_ in st.groups if g_.K == K]
-            fb["parts"][g.p0](fb["WWp"]).index_copy_(0, gi, sg["parts"][c0:c0 + c])
-            fb["wpl"].index_copy_(1, rows, sg["wpl"][:, c0 * K:(c0 + c) * K])
-            ids_f = sg["ids"][c0:c0 + c]
-            feed.occ[P] = ids_f
-            feed.placed[P] = hp
-            st.order[P] = ids_f
-        if fills:
-            st.gate.fill_(1)      # a pass after an all-finished one skips its GEMMs otherwise
-        feed.events += 1
+        HT, W = st.views()
+        sf, si = st.arena["sf"], st.arena["si"]
+        store = dict(feed.store)
+        store["done"] = feed.ctr[:1]
+        for g in st.groups:
+            ring = feed.rings.get(g.K)
+            if ring is None:
+                ring = self._stream_ring(st, g.K, fb)
+            grp = {"n": g.n, "K": g.K, "active": st.state["active"][g.pos],
+                   "occ": feed.occ[g.K], "plan": feed.plan[g.K],
+                   "W": W[g.rows], "HT": HT[g.rows],
+                   "parts": fb["parts"][g.p0](fb["WWp"]), "wpl": fb["wpl"][:, g.rows]}
+            ops.stream_swap(grp, ring, store, (sf[:, g.p0:], si[:, g.p0:]), st.gate)
+        ops.stream_publish(feed.ctr, feed.seq, feed.box)
 
     def _enqueue_fused(self, st: _Batch, steps, cur: dict) -> None:
         """Enqueue one single-process fused pass: from the layout's captured graph when
@@ -2127,10 +2158,12 @@ class NMFBatchSolver:
         run captured replays from its first, with only the W-dependent operands rebuilt
         eagerly), else eagerly.  ``cur`` carries the layout's workspaces between calls."""
         key = (st.uid, st.layout_version)
-        if cur["key"] != key:
-            sl = cur["sl"] = self._slot(st, steps) if st.graphs else None
-            cur["fb"] = sl["fb"] if sl is not None else self._fused_bufs(st, steps)
-            cur["key"] = key
+        if cur["key"] != key or cur.pop("fresh", False):
+            if cur["key"] != key:
+                sl = cur["sl"] = self._slot(st, steps) if st.graphs else None
+                cur["fb"] = sl["fb"] if sl is not None else self._fused_bufs(st, steps)
+                cur["key"] = key
+            sl = cur["sl"]
             if sl is not None and sl["graph"] is not None and _LAYOUT_REPLAY:
                 self._fused_prep(st, cur["fb"], keep_slices=True)
                 sl["graph"].replay()
@@ -2204,6 +2237,8 @@ class NMFBatchSolver:
         ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
                         n, -1, o.tol, final=final, gate=st.gate,
                         max_pass=int(o.online_max_pass))
+        if st.feed is not None:        # streaming: harvest / refill in this pass (stream.hip)
+            self._stream_swap_dev(st, fb)
 
     # ------------------------------------------------------------------ online frobenius
     def _online_frob(self, st: _Batch) -> None:

@@ -671,6 +671,92 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
                      int(init), _gate_ptr(gate, lin.device), int(max_pass), _stream_ptr(lin))
 
 
+# ----------------------------------------------------------------------------- streaming
+def stream_swap(grp: dict, ring: dict, store: dict, state: tuple, gate: torch.Tensor,
+                chunks: int = 32) -> None:
+    """Harvest the stopped replicates of one K group of a streaming batch into the result
+    store and place the next staged replicates of its ring at their positions, on the
+    device (csrc/kernels/stream.hip; NMFBatchSolver.run_stream).  ``grp``: the group's
+    views -- n, K, active (n,) int32, occ (n,) int32, plan (2n,) int32, W (nK, G), HT
+    (nK, N), parts (n, S, K, K), wpl (3, rows >= nK, Gp) int16; ``ring``: qc, head / tail
+    (int32 device scalars), ids (qc,), W (qc K, G), HT (qc K, N), sf (3, qc) float64, si
+    (5, qc) int32, parts (qc, S, K, K), wpl (3, qc K, Gp); ``store``: offs (R,) int64, W,
+    HT (or None), sf (3, R), si (5, R), done (int32 scalar); ``state``: the batch's (sf,
+    si) row views at the group's first position (3 / 5 rows, any row stride)."""
+    n, K = int(grp["n"]), int(grp["K"])
+    if n <= 0:
+        return
+    W, HT, rW, rHT = grp["W"], grp["HT"], ring["W"], ring["HT"]
+    G, N = W.shape[1], HT.shape[1]
+    sf, si = state
+    wpl, rwpl = grp["wpl"], ring["wpl"]
+    for name, t, dt in (("W", W, torch.float32), ("HT", HT, torch.float32),
+                        ("ring W", rW, torch.float32), ("ring HT", rHT, torch.float32),
+                        ("store W", store["W"], torch.float32)):
+        if t.dtype != dt or t.stride(1) != 1 or t.device != W.device:
+            raise ValueError(f"stream_swap: {name} must be {dt} rows with unit column stride")
+    if W.shape[0] < n * K or rW.shape[0] < ring["qc"] * K or rW.stride(0) != W.stride(0) or \
+            rHT.stride(0) != HT.stride(0) or store["W"].stride(0) != W.stride(0) or \
+            (store["HT"] is not None and store["HT"].stride(0) != HT.stride(0)):
+        raise ValueError("stream_swap: row pitches of batch, ring and store must agree")
+    if wpl.shape[0] != 3 or rwpl.shape[0] != 3 or wpl.stride(1) != rwpl.stride(1) or \
+            wpl.dtype != torch.int16 or rwpl.dtype != torch.int16:
+        raise ValueError("stream_swap: planes must be (3, rows, Gp) int16 with one pitch")
+    parts, rparts = grp["parts"], ring["parts"]
+    S = parts.shape[1]
+    if tuple(parts.shape[1:]) != (S, K, K) or tuple(rparts.shape[1:]) != (S, K, K) or \
+            not parts.is_contiguous() or not rparts.is_contiguous():
+        raise ValueError("stream_swap: contiguous (., S, K, K) partial-Gram blocks")
+    for name, t, m in (("active", grp["active"], n), ("occ", grp["occ"], n),
+                       ("plan", grp["plan"], 2 * n), ("ring ids", ring["ids"], ring["qc"])):
+        if t.dtype != torch.int32 or not t.is_contiguous() or t.numel() < m:
+            raise ValueError(f"stream_swap: {name} must be contiguous int32 (>= {m})")
+    oHT = store["HT"]
+    vals = [n, K, G, N, S, wpl.shape[2],
+            grp["active"].data_ptr(), grp["occ"].data_ptr(), grp["plan"].data_ptr(),
+            sf.data_ptr(), sf.stride(0), si.data_ptr(), si.stride(0),
+            W.data_ptr(), W.stride(0), HT.data_ptr(), HT.stride(0),
+            parts.data_ptr(),
+            wpl.data_ptr(), wpl.stride(1), wpl.stride(0),
+            int(ring["qc"]), ring["head"].data_ptr(), ring["tail"].data_ptr(),
+            ring["ids"].data_ptr(), rW.data_ptr(),
+            rHT.data_ptr(), ring["sf"].data_ptr(),
+            ring["si"].data_ptr(), rparts.data_ptr(),
+            rwpl.data_ptr(), rwpl.stride(0),
+            store["offs"].data_ptr(), store["W"].data_ptr(),
+            oHT.data_ptr() if oHT is not None else 0,
+            store["sf"].data_ptr(), store["sf"].stride(0), store["si"].data_ptr(),
+            store["si"].stride(0), store["done"].data_ptr(), gate.data_ptr()]
+    if ring["sf"].stride(0) != ring["qc"] or ring["si"].stride(0) != ring["qc"]:
+        raise ValueError("stream_swap: ring state rows must have stride qc")
+    _hip.stream_swap(vals, int(chunks), _stream_ptr(W))
+
+
+class HostMailbox:
+    """Pinned host int32 rows a kernel writes directly (device-mapped pinned memory): a
+    pass's small results reach the host with no copy launch.  Row s % slots holds
+    [sequence number, values...]; ``read(q)`` returns pass q's values once its event
+    completed (None if the row does not carry sequence q -- the caller then copies)."""
+
+    def __init__(self, width: int, slots: int = 8):
+        self.width, self.slots = int(width) + 1, int(slots)
+        self.host = torch.full((self.slots, self.width), -1, dtype=torch.int32, pin_memory=True)
+        self.dev_ptr = _hip.host_dev_ptr(self.host.data_ptr())
+
+    def read(self, q: int):
+        row = self.host[q % self.slots].tolist()
+        return row[1:] if row[0] == q else None
+
+
+def stream_publish(ctr: torch.Tensor, seq: torch.Tensor, box: HostMailbox) -> None:
+    """Write the counter block ``ctr`` (int32 device) into the host mailbox row of the
+    device sequence counter ``seq`` (int32 device scalar, advanced) -- stream.hip."""
+    if ctr.dtype != torch.int32 or not ctr.is_contiguous() or seq.dtype != torch.int32:
+        raise ValueError("stream_publish: contiguous int32 counters and sequence")
+    _hip.stream_publish(ctr.data_ptr(), ctr.numel(), seq.data_ptr(), box.dev_ptr, box.slots,
+                        box.width, _stream_ptr(ctr))
+
+
 # ----------------------------------------------------------------------------- beta MU
 def beta_mode(beta: float) -> int:
     return 0 if beta == 1.0 else (1 if beta == 0.0 else 2)

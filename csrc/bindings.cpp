@@ -110,6 +110,46 @@ PYBIND11_MODULE(_hip, m) {
                 "cnmf_solve");
         });
 
+  // continuous batching: the swap block in StreamSwap field order (ints, then pointers /
+  // strides as 64-bit integers; ops.stream_swap builds the list)
+  m.def("stream_swap", [](py::sequence v, int chunks, uintptr_t stream) {
+    if (py::len(v) != 41) throw std::runtime_error("stream_swap: 41 fields expected");
+    auto I = [&](int i) { return v[i].cast<long long>(); };
+    cnmf::StreamSwap p;
+    int i = 0;
+    p.n = (int)I(i++); p.K = (int)I(i++); p.G = (int)I(i++); p.N = (int)I(i++);
+    p.S = (int)I(i++); p.Gp = (int)I(i++);
+    p.active = P<const int>(I(i++)); p.occ = P<int>(I(i++)); p.plan = P<int>(I(i++));
+    p.sf = P<double>(I(i++)); p.sf_ld = I(i++); p.si = P<int>(I(i++)); p.si_ld = I(i++);
+    p.W = P<float>(I(i++)); p.ldw = I(i++); p.HT = P<float>(I(i++)); p.ldh = I(i++);
+    p.parts = P<float>(I(i++));
+    p.wpl = P<unsigned short>(I(i++)); p.pl_ld = I(i++); p.pl_plane = I(i++);
+    p.qc = (int)I(i++); p.head = P<int>(I(i++)); p.tail = P<const int>(I(i++));
+    p.ring_id = P<const int>(I(i++)); p.rW = P<const float>(I(i++));
+    p.rHT = P<const float>(I(i++)); p.rsf = P<const double>(I(i++));
+    p.rsi = P<const int>(I(i++)); p.rparts = P<const float>(I(i++));
+    p.rwpl = P<const unsigned short>(I(i++)); p.rpl_plane = I(i++);
+    p.offs = P<const long long>(I(i++)); p.oW = P<float>(I(i++)); p.oHT = P<float>(I(i++));
+    p.osf = P<double>(I(i++)); p.osf_ld = I(i++); p.osi = P<int>(I(i++)); p.osi_ld = I(i++);
+    p.done = P<int>(I(i++)); p.gate = P<int>(I(i++));
+    (void)i;
+    check(cnmf_stream_swap(&p, chunks, reinterpret_cast<hipStream_t>(stream)),
+          "cnmf_stream_swap");
+  });
+
+  m.def("stream_publish", [](uintptr_t ctr, int n, uintptr_t seq, uintptr_t mail, int slots,
+                             int width, uintptr_t stream) {
+    check(cnmf_stream_publish(P<const int>(ctr), n, P<int>(seq), P<int>(mail), slots, width,
+                              reinterpret_cast<hipStream_t>(stream)),
+          "cnmf_stream_publish");
+  });
+  // device address of pinned host memory (kernels write host mailboxes directly)
+  m.def("host_dev_ptr", [](uintptr_t host) {
+    void* d = nullptr;
+    check(hipHostGetDevicePointer(&d, reinterpret_cast<void*>(host), 0), "hipHostGetDevicePointer");
+    return reinterpret_cast<uintptr_t>(d);
+  });
+
   m.def("conv_update",
         [](uintptr_t lin, uintptr_t quad, double x_sq, uintptr_t err_init, uintptr_t err_prev,
            uintptr_t err, uintptr_t active, uintptr_t converged, uintptr_t n_pass, int n,

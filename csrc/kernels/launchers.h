@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "stream.h"
+
 extern "C" {
 
 int cnmf_solve_max_k();
@@ -24,6 +26,10 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       float* gout, float* gp_out, long long gp_rs, unsigned* coop_gen_dev,
                       unsigned* coop_arrive, int reps_per_launch, unsigned long long* stamps,
                       hipStream_t stream);
+
+hipError_t cnmf_stream_swap(const cnmf::StreamSwap* args, int chunks, hipStream_t stream);
+hipError_t cnmf_stream_publish(const int* ctr, int n, int* seq, int* mail, int slots, int width,
+                               hipStream_t stream);
 
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,

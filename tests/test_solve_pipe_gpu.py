@@ -409,7 +409,7 @@ def test_stream_matches_batch_solves(ks):
     got = []
     s = solver.run_stream(seeds, ks=kk, live=8,
                           on_result=lambda ids, k_, host, ev: got.extend(ids.tolist()))
-    assert s.stats["stream_events"] > 0 and s.stats["stream_slots"] == {k: 8 for k in ks}
+    assert s.stats["stream_stagings"] > 0 and s.stats["stream_slots"] == {k: 8 for k in ks}
     assert sorted(got) == list(range(len(kk)))
     b = NMFBatchSolver(X, opts).run(seeds, ks=kk)
     assert (s.ks == b.ks).all()
@@ -440,7 +440,7 @@ def test_stream_graph_replays_bitwise_eager_and_pass_limit(monkeypatch):
         monkeypatch.setenv("CNMF_GRAPHS", mode)
         solver = NMFBatchSolver(X, opts)
         res[mode] = solver.run_stream(seeds, live=16)
-        assert res[mode].stats["stream_events"] > 0
+        assert res[mode].stats["stream_stagings"] > 0
         if mode == "1":
             slots = list(solver._arenas.values())[0]["slots"]
             assert any(sl["graph"] is not None for sl in slots.values()), \

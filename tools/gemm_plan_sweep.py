@@ -36,9 +36,11 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     h = ops._hip
     shapes = []
-    for K in (10, 20, 30):
-        M = 100 * K
-        shapes += [(f"numerator K={K}", M, 5000, 2048), (f"statistics K={K}", M, 2000, 5056)]
+    # rows = replicates x K; default the fused step's main-pass rows at K = 10 / 20 / 30
+    # (100 replicates) -- or the M values given on the command line
+    Ms = [int(a) for a in sys.argv[1:]] or [1000, 2000, 3000]
+    for M in Ms:
+        shapes += [(f"numerator M={M}", M, 5000, 2048), (f"statistics M={M}", M, 2000, 5056)]
     for name, M, N, Kd in shapes:
         A = torch.rand((M, Kd), device=dev, generator=g)
         B = torch.randint(0, 60, (N, Kd), device=dev, generator=g).float()
@@ -59,7 +61,7 @@ def main():
                     h.gemm_planes(Ap.data_ptr(), Ap.stride(1), Ap.stride(0), M, Bp.data_ptr(),
                                   Bp.stride(1), Bp.stride(0), N, slab.data_ptr(), N, 0, M, N,
                                   Kd, pa, pb, 0, v, ks, slab.data_ptr(), ops.gemm_stages(v),
-                                  ops.gemm_kstep(v), 1, 0, 0, ops._stream_ptr(slab))
+                                  ops.gemm_kstep(v), 1, 0, ops._stream_ptr(slab))
                 try:
                     res[f"v{v}k{ks}"] = round(_time(run), 1)
                 except Exception as e:      # a variant the shape / LDS does not allow
