@@ -886,29 +886,10 @@ class cNMF:
                 seeds = [int(sdv[i]) for i in grp]
                 ks = [int(nc[i]) for i in grp]
                 t0 = time.perf_counter()
-                # opt-in (CNMF_EARLY_WRITE=1): replicates that finish early are written
-                # while the rest still solve -- each compaction hands over the retired
-                # replicates' final spectra (pinned copy + event) to the writer pool.
-                # Measured SLOWER on the PBMC-scale grid (factorize 350-456 vs 157-250 ms,
-                # profiles/r2_early_write_probe.log): the writer threads take the CPU from
-                # the host enqueue that bounds the convergence tail
-                early: set = set()
-                on_retire = None
-                if writer and not fault_after and comm is None and dev.type == "cuda" \
-                        and os.environ.get("CNMF_EARLY_WRITE", "0") == "1":
-                    def on_retire(idx_, kpos_, host_, ev_, grp=grp, ks=ks):
-                        idx_ = [int(i) for i in idx_]
-                        early.update(idx_)
-                        offs_ = np.concatenate([[0], np.cumsum(kpos_)[:-1]]).astype(np.int64)
-                        paths_e = [self.paths["iter_spectra"] % (ks[r], int(itv[grp[r]]))
-                                   for r in idx_]
-                        its_e = [int(itv[grp[r]]) for r in idx_]
-                        ks_e = [ks[r] for r in idx_]
-
-                        def job():
-                            ev_.synchronize()
-                            return _write_batch(paths_e, host_.numpy(), offs_, ks_e, its_e)
-                        pending.append(pool.submit(job))
+                # (writing replicates that finish early while the batch still solves was
+                # measured SLOWER on the PBMC-scale grid -- factorize 350-456 vs 157-250
+                # ms, profiles/r2_early_write_probe.log: the writer threads take the CPU
+                # from the host enqueue -- so every file is written after its batch)
                 if len(set(ks)) == 1 and int(os.environ.get("CNMF_STREAMS", "1")) > 1:
                     solver.opts.n_components = ks[0]
                     res = solver.run_concurrent(seeds, n_streams=int(os.environ["CNMF_STREAMS"]))
@@ -916,8 +897,7 @@ class cNMF:
                     # continuous batching when a K has more replicates than one co-resident
                     # round of its usage solve holds (NMFBatchSolver.run_stream; else the
                     # one-batch run): usages are only kept when they are saved
-                    res = solver.run_stream(seeds, ks=ks, keep_usages=save_usages,
-                                            on_result=on_retire)
+                    res = solver.run_stream(seeds, ks=ks, keep_usages=save_usages)
                 W = res.W.cpu().numpy()
                 wall = time.perf_counter() - t0
                 log.info("K=%s: %d replicates in %.3f s (%.1f replicates/s) on %s",
@@ -929,7 +909,7 @@ class cNMF:
                     # every replicate file of the batch not written early, in one native
                     # multi-threaded call (utils.io.write_spectra_batch), overlapped with
                     # the next batch's solve
-                    rest_ = [r for r in range(n_ok) if r not in early]
+                    rest_ = list(range(n_ok))
                     if rest_:
                         paths_b = [self.paths["iter_spectra"] % (ks[r], int(itv[grp[r]]))
                                    for r in rest_]

@@ -1,13 +1,12 @@
-"""factorize on the GPU with CNMF_EARLY_WRITE=1 (opt-in): replicates that finish early
-are written while the rest of the ragged batch still solves (NMFBatchSolver.run(
-on_retire=...), api.factorize_jobs).  The files and their manifest hashes equal the
-default write-everything-at-the-end path."""
+"""GPU pipeline pieces: the solver's early hand-over of retired replicates
+(NMFBatchSolver.run(on_retire=...)) and the device-streamed norm counts of prepare."""
 import json
 import os
 
 import numpy as np
 import pandas as pd
 import pytest
+import torch
 
 from cnmf_torch_amd import cNMF, load_df_from_npz, save_df_to_npz
 from cnmf_torch_amd.utils.synthetic import simulate_counts
@@ -15,41 +14,29 @@ from cnmf_torch_amd.utils.synthetic import simulate_counts
 pytestmark = pytest.mark.gpu
 
 
-def _run(tmp, fn, early: str, monkeypatch):
-    from cnmf_torch_amd.models import nmf
+def test_retired_replicates_handed_over_equal_final_spectra():
+    """run(on_retire=cb): every replicate a host compaction retires is handed over once
+    (pinned spectra + event) while the rest still solve, and those spectra equal the
+    final result rows bit for bit."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
 
-    monkeypatch.setenv("CNMF_EARLY_WRITE", early)
-    # early writes retire replicates at host compactions: compare against the same
-    # compacting schedule (the default device-slot batching never compacts, so its GEMM
-    # split plans -- and fp32 rounding -- differ)
-    monkeypatch.setattr(nmf, "_DEV_SLOTS", False)
-    obj = cNMF(output_dir=str(tmp / f"early{early}"), name="g")
-    obj.prepare(fn, components=[4, 5, 6], n_iter=40, seed=5, num_highvar_genes=300,
-                batch_size=400)
-    obj.factorize(worker_i=0, total_workers=1, verbose=False)
-    return obj
+    X = torch.from_numpy(normalized_counts_matrix(3000, 400, n_programs=6, seed=4)).cuda()
+    got = {}
 
+    def cb(idx, kpos, host, ev):
+        ev.synchronize()
+        off = np.concatenate([[0], np.cumsum(kpos)[:-1]])
+        for i, o, k in zip(idx, off, kpos):
+            assert int(i) not in got
+            got[int(i)] = host[o:o + k].clone()
 
-def test_early_replicate_writes_equal_end_of_batch_writes(tmp_path, monkeypatch):
-    X, cells, genes = simulate_counts(1500, 500, 5, seed=4, sparse=False)
-    fn = str(tmp_path / "counts.df.npz")
-    save_df_to_npz(pd.DataFrame(X, index=cells, columns=genes), fn)
-    a = _run(tmp_path, fn, "1", monkeypatch)
-    b = _run(tmp_path, fn, "0", monkeypatch)
-    for k in (4, 5, 6):
-        for it in range(40):
-            fa, fb = a.paths["iter_spectra"] % (k, it), b.paths["iter_spectra"] % (k, it)
-            da, db = load_df_from_npz(fa), load_df_from_npz(fb)
-            np.testing.assert_array_equal(da.values, db.values)
-            assert list(da.columns) == list(db.columns) and list(da.index) == list(db.index)
-
-    def manifest(o):
-        recs = [json.loads(l) for l in open(o.paths["replicate_manifest"])]
-        return {(r["k"], r["iter"]): r["sha256"] for r in recs}
-
-    ma, mb = manifest(a), manifest(b)
-    assert len(ma) == 120 and ma == mb
-    assert a.verify_replicates() == []
+    kk = [4] * 30 + [6] * 30
+    res = NMFBatchSolver(X, NMFOptions(n_components=4, online_chunk_size=1000)).run(
+        list(range(50, 110)), ks=kk, on_retire=cb)
+    assert len(got) > 10
+    for i, w in got.items():
+        assert torch.equal(w, res.spectra(i).cpu())
 
 
 def test_streamed_norm_counts_equal_get_norm_counts(tmp_path):
