@@ -79,7 +79,8 @@ def build_hip(force: bool = False, jobs: int = 8, verbose: bool = True) -> str:
     # (the elementwise work reads every accumulator: AGPR copies cost ~30 % of the VALU)
     # the pipelined solve keeps its elementwise update scalar: SLP-packed v_pk_*_f32 beside
     # MFMAs cost more issue cycles than the scalar pair (MI355X_MICROARCH.md cycle table)
-    unit_flags = {"beta_planes.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+    unit_flags = {os.path.basename(s): ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+                  for s in srcs if os.path.basename(s).startswith("beta_planes")}
     # CNMF_PIPE_STAMPS_BUILD=1: the pipelined solve with its diagnostic phase stamps
     # (tools/pipe_stamp_probe.py); a changed flag set rebuilds the unit
     stamps = os.environ.get("CNMF_PIPE_STAMPS_BUILD", "0") == "1"

@@ -13,7 +13,13 @@ the published algorithm (Korsunsky et al. 2019) with the harmonypy conventions:
   with the diversity penalty ((E+1)/(O+1))^theta;
 * objective = sum R*dist + sigma*sum R log R + cross-entropy term.
 
-Everything except the block order and convergence bookkeeping runs as batched tensor
+On the GPU (harmony.hip) a k-means round is four kinds of launches and no library GEMM:
+the centroid product Y = Z_cos R^T as chunked partials with a deterministic reduction,
+the blocked R update whose assign kernel forms each cell's distances 2 (1 - Y_k . z_n)
+itself (no N x K distance matrix) and accumulates the round's k-means error and entropy,
+and one tiny kernel adding the cross-entropy term, which O = R Phi^T reduces to K x B
+numbers -- one device-to-host read per round for the convergence test.  Elsewhere
+everything except the block order and convergence bookkeeping runs as batched tensor
 ops on the GPU.  ``moe_correct_ridge`` is batched over clusters: the K ridge systems
 are formed with two GEMMs over cells and the correction is ONE
 (features x K(B+1)) x (K(B+1) x cells) GEMM, streamed over cell chunks, instead of the
@@ -115,6 +121,14 @@ class Harmony:
             bidx = np.stack([o + Pn[o:o + c].argmax(axis=0) for o, c in zip(offs, phi_n)])
             self.bidx = torch.as_tensor(bidx.astype(np.int32), device=dev).contiguous()
             self._ws: dict = {}
+            # fused distances need the centroid table in the assign kernel's LDS and the
+            # centroid kernel's d x K outputs (harmony.hip)
+            self._fused = self.Z_orig.shape[0] * self.K <= ops._hip.harmony_centroid_max()
+            self.Zt = self.Z_cos.t().contiguous()              # cells x PCs
+            self._obj = torch.zeros(2, dtype=dt, device=dev)    # round's assign sums
+            self._obj_out = torch.zeros(1, dtype=dt, device=dev)
+        else:
+            self._fused = False
         self._init_cluster(init_backend)
         self._harmonize(max_iter_harmony)
 
@@ -123,6 +137,16 @@ class Harmony:
         from .consensus import kmeans as _km
 
         X = self.Z_cos.t()
+        if self._fused and backend != "sklearn":
+            # device k-means init; the centroids by the centroid kernel on a one-hot R
+            labels = torch.as_tensor(_km(X, self.K, n_init=10, random_state=self.random_state,
+                                         max_iter=25, backend="device",
+                                         device_restart_factor=1), device=self.dev)
+            onehot = (labels[:, None] == torch.arange(self.K, device=self.dev)[None, :]).to(self.dt)
+            Y = ops.harmony_centroids(self.Zt, onehot.contiguous(), self._ws)
+            Y = Y / onehot.sum(dim=0).clamp(min=1)[None, :]
+            self._init_fused(Y)
+            return
         if backend == "sklearn":
             from sklearn.cluster import KMeans
 
@@ -138,6 +162,9 @@ class Harmony:
                                          device_restart_factor=1), device=self.dev)
             onehot = (labels[None, :] == torch.arange(self.K, device=self.dev)[:, None]).to(self.dt)
             Y = _tall_matmul(X.t(), onehot.t()) / onehot.sum(dim=1).clamp(min=1)[None, :]
+        if self._fused:
+            self._init_fused(Y)
+            return
         self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
         self._dist()
         R = -self.dist_mat / self.sigma[:, None]
@@ -152,7 +179,35 @@ class Harmony:
         self._objective()
         self.objective_harmony.append(self.objective_kmeans[-1])
 
+    def _init_fused(self, Y: torch.Tensor):
+        """Initial soft assignment on the device: one assign pass over every cell with a
+        flat penalty (1 / nvar per covariate: R = softmax(-dist / sigma)), which also
+        builds E = outer(sum R, Pr_b) and O = R Phi^T from zero and the initial
+        objective's terms."""
+        self.Y = (Y / torch.linalg.vector_norm(Y, dim=0)).contiguous()
+        K, B = self.K, self.Phi.shape[0]
+        self.Rt = torch.zeros((self.N, K), dtype=self.dt, device=self.dev)
+        self.R = self.Rt.t()
+        self.E = torch.zeros((K, B), dtype=self.dt, device=self.dev)
+        self.O = torch.zeros((K, B), dtype=self.dt, device=self.dev)
+        ws = self._ws
+        ws["pen"] = torch.full((K, B), 1.0 / self.bidx.shape[0], dtype=self.dt, device=self.dev)
+        cells = torch.arange(self.N, dtype=torch.int32, device=self.dev)
+        self._obj.zero_()
+        ops.harmony_block_update(self.Rt, None, self.sigma, cells, self.bidx, self.E, self.O,
+                                 self.Pr_b, self.theta, ws, Y=self.Y, Zt=self.Zt, obj=self._obj,
+                                 steps=(1,))
+        self._objective_fused()
+        self.objective_harmony.append(self.objective_kmeans[-1])
+
+    def _objective_fused(self):
+        ops.harmony_objective(self.O, self.E, self.sigma, self.theta, self._obj, self._obj_out)
+        self.objective_kmeans.append(float(self._obj_out.item()))
+
     def _objective(self):
+        if self._fused:
+            self._objective_fused()
+            return
         kmeans_error = (self.R * self.dist_mat).sum()
         ent = _entropy_sum(self.R, self.sigma)
         x = self.R * self.sigma[:, None]
@@ -167,6 +222,8 @@ class Harmony:
             self._cluster()
             self.Z_cos, self.Z_corr, self.W = moe_correct_ridge_pcs(
                 self.Z_orig, self.R, self.Phi_moe, self.lamb, levels=self._lv)
+            if self._fused:
+                self.Zt = self.Z_cos.t().contiguous()
             if self._converged(1):
                 break
 
@@ -179,12 +236,17 @@ class Harmony:
             self.dist_mat = 2 * (1 - self.Y.t() @ self.Z_cos)
 
     def _cluster(self):
-        self._dist()
+        if not self._fused:
+            self._dist()
         i = 0
         for i in range(self.max_iter_kmeans):
-            Y = _tall_matmul(self.Z_cos, self.R.t())
-            self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
-            self._dist()
+            if self._fused:
+                Y = ops.harmony_centroids(self.Zt, self.Rt, self._ws)
+                self.Y = (Y / torch.linalg.vector_norm(Y, dim=0)).contiguous()
+            else:
+                Y = _tall_matmul(self.Z_cos, self.R.t())
+                self.Y = Y / torch.linalg.vector_norm(Y, dim=0)
+                self._dist()
             self._update_R()
             self._objective()
             if i > self.window_size and self._converged(0):
@@ -205,8 +267,13 @@ class Harmony:
             for b in np.array_split(order, n_blocks):
                 cells = order_d[a:a + b.size]
                 a += b.size
-                ops.harmony_block_update(self.Rt, self.distT, self.sigma, cells, self.bidx,
-                                         self.E, self.O, self.Pr_b, self.theta, self._ws)
+                if self._fused:
+                    ops.harmony_block_update(self.Rt, None, self.sigma, cells, self.bidx,
+                                             self.E, self.O, self.Pr_b, self.theta, self._ws,
+                                             Y=self.Y, Zt=self.Zt, obj=self._obj)
+                else:
+                    ops.harmony_block_update(self.Rt, self.distT, self.sigma, cells, self.bidx,
+                                             self.E, self.O, self.Pr_b, self.theta, self._ws)
             return
         sd = -self.dist_mat / self.sigma[:, None]
         sd = sd - sd.max(dim=0).values

@@ -990,12 +990,14 @@ class PlanesOnlyX:
 def kernel_max_rank(beta: float, algo: str) -> int | None:
     """Largest K the native kernels factorise (None: no limit -- 'bpp' solves its NNLS
     blocks with torch linear algebra): Frobenius MU 128 (padded, native_rank), HALS /
-    halsvar 64, the beta-divergence kernels 32.  Larger ranks are routed to the eager
-    PyTorch ops on the same GPU (NMFBatchSolver.run, logged)."""
+    halsvar 64, KL 64 and the other beta-divergences 56 (padded to a multiple of 8 above
+    32; beta_planes_wide*.hip -- an IS / general-beta K = 64 panel pair exceeds the LDS).
+    Larger ranks are routed to the eager PyTorch ops on the same GPU (NMFBatchSolver.run,
+    logged)."""
     if algo == "bpp":
         return None
     if beta != 2.0:
-        return 32
+        return 64 if beta == 1.0 else 56
     return 128 if algo == "mu" else 64
 
 
@@ -1095,6 +1097,7 @@ class NMFBatchSolver:
         self._ws: dict = {}
         self._w_fresh: dict = {}    # stream -> key of the W its "w" planes hold
         self._XT = None             # X^T (G, N padded to 4) for the beta W-side kernel
+        self._beta_K = 0            # rank of the beta != 2 batch being solved (padded)
 
     # ------------------------------------------------------------------ public
     def run(self, seeds, HT0=None, W0=None, ks=None, on_retire=None) -> NMFResult:
@@ -1134,7 +1137,7 @@ class NMFBatchSolver:
                 return self.run(seeds, HT0=HT0, W0=W0, ks=ks, on_retire=None)
         t0 = time.perf_counter()
         # wide ranks run padded on the GPU kernels (native_rank); bpp solves on torch linalg
-        pad = self.X.device.type == "cuda" and o.algo != "bpp" and self.beta == 2.0 \
+        pad = self.X.device.type == "cuda" and o.algo != "bpp" \
             and bool((ks > 32).any()) and not ops.eager_active()
         kp = np.array([native_rank(k) for k in ks], dtype=np.int64) if pad else ks
         pos = np.lexsort((np.arange(R), kp, ks))     # positions grouped by K
@@ -2546,6 +2549,8 @@ class NMFBatchSolver:
         (sparse_kl.hip): KL on the native GPU path with X at most ``kl_sparse_density``
         non-zero (``CNMF_KL_SPARSE=1`` forces it, ``=0`` disables it); else None (dense
         split-precision kernels).  Decided once per solver (one host sync)."""
+        if getattr(self, "_beta_K", 0) > 32:     # the CSR kernels stop at K = 32
+            return None
         if "_kl_csr" in self.__dict__:
             return self._kl_csr
         csr = None
@@ -2598,7 +2603,7 @@ class NMFBatchSolver:
         """Tiled CSRs of X[a:b]^T (genes x chunk cells) for the sparse spectra numerators."""
         key = (a, b)
         if key not in self._kl_csrT:
-            self._kl_csrT[key] = ops.kl_csr_tiles(self.X[a:b], self.opts.n_components)
+            self._kl_csrT[key] = ops.kl_csr_tiles(self.X[a:b], self._beta_K or self.opts.n_components)
         return self._kl_csrT[key]
 
     def _beta_w_partials(self, xc, xtc, H3c, W3, active, panels=None, rows=None):
@@ -2838,7 +2843,7 @@ class NMFBatchSolver:
         (prev - cur) / init < tol stop rule stay on the device; the host reads the active
         flags one pass late through the same speculative pass pipeline."""
         o = self.opts
-        K = st.K
+        K = self._beta_K = st.K
         X = self.X
         N, G = X.shape
         steps = self._steps(N)
@@ -2884,7 +2889,7 @@ class NMFBatchSolver:
         the W-side statistics are all-reduced under DP, the loss is checked every
         ``loss_every`` iterations."""
         o, comm = self.opts, self.comm
-        K = st.K
+        K = self._beta_K = st.K
         X = self.X
         N, G = X.shape
         self._init_err(st)

@@ -1614,41 +1614,89 @@ def harmony_native_ok(t: torch.Tensor, K: int, B: int) -> bool:
     return use_native(t) and K <= 128 and K * B <= _hip.harmony_max_kb()
 
 
-def harmony_block_update(Rt: torch.Tensor, distT: torch.Tensor, sigma: torch.Tensor,
+def harmony_block_update(Rt: torch.Tensor, distT: torch.Tensor | None, sigma: torch.Tensor,
                          cells: torch.Tensor, bidx: torch.Tensor, E: torch.Tensor,
                          O: torch.Tensor, Pr_b: torch.Tensor, theta: torch.Tensor,
-                         ws: dict) -> None:
+                         ws: dict, Y: torch.Tensor | None = None, Zt: torch.Tensor | None = None,
+                         obj: torch.Tensor | None = None, steps=(0, 1)) -> None:
     """One Harmony block update on device (harmony.hip): remove the block's old R from
-    E/O, recompute the diversity penalty, reassign R for the block's cells, add back.
-    Rt/distT (N, K) float64 contiguous; cells int32 (nb,); bidx int32 (nvar, N);
-    E/O (K, B) float64; ``ws`` caches the partial-sum workspace and arrival counter."""
+    E/O and recompute the diversity penalty (step 0), reassign R for the block's cells and
+    add it back (step 1).  Rt (N, K) float64 contiguous; cells int32 (nb,); bidx int32
+    (nvar, N); E/O (K, B) float64.  ``distT`` (N, K) float64, or None: the distances
+    2 (1 - Y_k . z_n) are formed inside the assign from ``Y`` (d, K) and ``Zt`` (N, d),
+    and the assignment's objective terms (sum R dist, sum sigma R log R) are added to
+    ``obj`` (2,) float64.  ``ws`` caches the partial-sum workspace and the penalty table
+    (ws["pen"], which step 1 reads)."""
     N, K = Rt.shape
     B = E.shape[1]
     nvar = bidx.shape[0]
     nb = int(cells.numel())
-    for name, t, dt in (("Rt", Rt, torch.float64), ("distT", distT, torch.float64),
-                        ("E", E, torch.float64), ("O", O, torch.float64),
-                        ("cells", cells, torch.int32), ("bidx", bidx, torch.int32)):
+    for name, t, dt in (("Rt", Rt, torch.float64), ("E", E, torch.float64),
+                        ("O", O, torch.float64), ("cells", cells, torch.int32),
+                        ("bidx", bidx, torch.int32)):
         if t.dtype != dt or not t.is_contiguous() or t.device != Rt.device:
             raise ValueError(f"{name}: contiguous {dt} on {Rt.device} required")
-    if distT.shape != (N, K) or O.shape != (K, B) or bidx.shape[1] != N:
+    if O.shape != (K, B) or bidx.shape[1] != N:
         raise ValueError("harmony_block_update: inconsistent shapes")
+    d = 0
+    if distT is None:
+        if Y is None or Zt is None or obj is None:
+            raise ValueError("harmony_block_update: Y, Zt and obj for the fused distances")
+        d = int(Y.shape[0])
+        for name, t, shp in (("Y", Y, (d, K)), ("Zt", Zt, (N, d)), ("obj", obj, (2,))):
+            if t.dtype != torch.float64 or not t.is_contiguous() or tuple(t.shape) != shp:
+                raise ValueError(f"{name}: contiguous float64 {shp} required")
+    elif distT.dtype != torch.float64 or not distT.is_contiguous() or distT.shape != (N, K):
+        raise ValueError("distT: contiguous float64 (N, K) required")
     # ~512 workgroups of up to 4 waves (2 per CU): each wave walks a few dozen cells
     chunk = max(16, -(-nb // 512))
     n_wg = -(-nb // chunk)
-    need = n_wg * K * (B + 1)
+    need = n_wg * (K * (B + 1) + 2)
     if ws.get("part") is None or ws["part"].numel() < need:
         ws["part"] = torch.empty(need, dtype=torch.float64, device=Rt.device)
-    if ws.get("counter") is None:
-        ws["counter"] = torch.zeros(1, dtype=torch.int32, device=Rt.device)
+    if ws.get("pen") is None:
         ws["pen"] = torch.empty((K, B), dtype=torch.float64, device=Rt.device)
     st = _stream_ptr(Rt)
-    args = (Rt.data_ptr(), distT.data_ptr(), sigma.data_ptr(), cells.data_ptr(), bidx.data_ptr(),
-            nb, N, K, B, nvar, chunk, E.data_ptr(), O.data_ptr(), Pr_b.data_ptr(),
-            theta.data_ptr(), ws["pen"].data_ptr(), ws["part"].data_ptr(),
-            ws["counter"].data_ptr(), st)
-    _hip.harmony_block(0, *args)
-    _hip.harmony_block(1, *args)
+    args = (Rt.data_ptr(), distT.data_ptr() if distT is not None else 0, sigma.data_ptr(),
+            cells.data_ptr(), bidx.data_ptr(), nb, N, K, B, nvar, chunk, E.data_ptr(),
+            O.data_ptr(), Pr_b.data_ptr(), theta.data_ptr(), ws["pen"].data_ptr(),
+            ws["part"].data_ptr(), Y.data_ptr() if Y is not None else 0,
+            Zt.data_ptr() if Zt is not None else 0, d, obj.data_ptr() if obj is not None else 0,
+            st)
+    for op in steps:
+        _hip.harmony_block(op, *args)
+
+
+def harmony_centroids(Zt: torch.Tensor, Rt: torch.Tensor, ws: dict) -> torch.Tensor:
+    """Y = Z_cos R^T (d, K) from the cell-major Zt (N, d) and Rt (N, K), float64, on the
+    device in two deterministic stages (harmony.hip: chunked partials, per-output wave
+    sums) -- never a library GEMM with one output tile walking every cell."""
+    N, d = Zt.shape
+    K = Rt.shape[1]
+    for name, t in (("Zt", Zt), ("Rt", Rt)):
+        if t.dtype != torch.float64 or not t.is_contiguous() or t.shape[0] != N:
+            raise ValueError(f"harmony_centroids: {name} contiguous float64 with N rows")
+    if d * K > _hip.harmony_centroid_max():
+        raise ValueError(f"harmony_centroids: d * K = {d * K} beyond the kernel's outputs")
+    chunk = max(64, -(-N // 512))
+    n_wg = -(-N // chunk)
+    need = n_wg * d * K
+    if ws.get("cpart") is None or ws["cpart"].numel() < need:
+        ws["cpart"] = torch.empty(need, dtype=torch.float64, device=Zt.device)
+    Y = torch.empty((d, K), dtype=torch.float64, device=Zt.device)
+    _hip.harmony_centroid(Zt.data_ptr(), Rt.data_ptr(), N, d, K, chunk, ws["cpart"].data_ptr(),
+                          Y.data_ptr(), _stream_ptr(Zt))
+    return Y
+
+
+def harmony_objective(O: torch.Tensor, E: torch.Tensor, sigma: torch.Tensor,
+                      theta: torch.Tensor, obj: torch.Tensor, out: torch.Tensor) -> None:
+    """out[0] = obj[0] + obj[1] + sum_{k,b} sigma_k theta_b O log((O + 1) / (E + 1)) (the
+    round's Harmony objective from the assign passes' sums and the cross-entropy term,
+    which O = R Phi^T reduces to K x B numbers); resets obj."""
+    K, B = O.shape
+    _hip.harmony_objective(O.data_ptr(), E.data_ptr(), sigma.data_ptr(), theta.data_ptr(), K, B,
+                           obj.data_ptr(), out.data_ptr(), _stream_ptr(O))
 
 
 # ----------------------------------------------------------------------------- init

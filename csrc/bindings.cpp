@@ -367,14 +367,30 @@ PYBIND11_MODULE(_hip, m) {
   m.def("harmony_block", [](int op, uintptr_t Rt, uintptr_t distT, uintptr_t sigma,
                             uintptr_t cells, uintptr_t bidx, int nb, int N, int K, int B,
                             int nvar, int chunk, uintptr_t E, uintptr_t O, uintptr_t Pr_b,
-                            uintptr_t theta, uintptr_t Pen, uintptr_t part, uintptr_t counter,
-                            uintptr_t stream) {
+                            uintptr_t theta, uintptr_t Pen, uintptr_t part, uintptr_t Y,
+                            uintptr_t Zt, int d, uintptr_t obj, uintptr_t stream) {
     check(cnmf_harmony_block(op, P<double>(Rt), P<const double>(distT), P<const double>(sigma),
                              P<const int>(cells), P<const int>(bidx), nb, N, K, B, nvar, chunk,
                              P<double>(E), P<double>(O), P<const double>(Pr_b),
                              P<const double>(theta), P<double>(Pen), P<double>(part),
-                             P<int>(counter), reinterpret_cast<hipStream_t>(stream)),
+                             P<const double>(Y), P<const double>(Zt), d, P<double>(obj),
+                             reinterpret_cast<hipStream_t>(stream)),
           "harmony_block");
+  });
+  m.def("harmony_centroid_max", []() { return cnmf_harmony_centroid_max(); });
+  m.def("harmony_centroid", [](uintptr_t Zt, uintptr_t Rt, int N, int d, int K, int chunk,
+                               uintptr_t part, uintptr_t Y, uintptr_t stream) {
+    check(cnmf_harmony_centroid(P<const double>(Zt), P<const double>(Rt), N, d, K, chunk,
+                                P<double>(part), P<double>(Y),
+                                reinterpret_cast<hipStream_t>(stream)),
+          "harmony_centroid");
+  });
+  m.def("harmony_objective", [](uintptr_t O, uintptr_t E, uintptr_t sigma, uintptr_t theta,
+                                int K, int B, uintptr_t obj, uintptr_t out, uintptr_t stream) {
+    check(cnmf_harmony_objective(P<const double>(O), P<const double>(E), P<const double>(sigma),
+                                 P<const double>(theta), K, B, P<double>(obj), P<double>(out),
+                                 reinterpret_cast<hipStream_t>(stream)),
+          "harmony_objective");
   });
 
   m.def("gram", [](uintptr_t X, long long x_rs, long long ldx, int R, int K, int n,

@@ -516,13 +516,18 @@ hipError_t launch_beta_mode(int side, const BetaParams& p, hipStream_t s) {
     case 6: return launch_beta<6, MODE>(side, p, s);
     case 7: return launch_beta<7, MODE>(side, p, s);
     case 8: return launch_beta<8, MODE>(side, p, s);
+    // K > 32, padded to a multiple of 8 by the engine (models.nmf.native_rank)
+    case 10: return launch_beta<10, MODE>(side, p, s);
+    case 12: return launch_beta<12, MODE>(side, p, s);
+    case 14: return launch_beta<14, MODE>(side, p, s);
+    case 16: return launch_beta<16, MODE>(side, p, s);
     default: return hipErrorInvalidValue;
   }
 }
 
 }  // namespace cnmf
 
-extern "C" int cnmf_beta_max_k() { return 32; }
+extern "C" int cnmf_beta_max_k() { return 64; }
 
 // side 0 = H (num/den: (R,K,N), loss partials (R, ceil(N/64))),
 // side 1 = W (num/den: (splits,R,K,G)).  mode: 0 KL, 1 IS, 2 general beta.
@@ -537,7 +542,8 @@ extern "C" hipError_t cnmf_beta_contract(int side, int mode, const float* X, lon
                                          int conv_mode, int check_every, double* hstate,
                                          hipStream_t stream) {
   if (R <= 0 || N <= 0 || G <= 0) return hipSuccess;
-  if (K < 1 || K > 32 || (side != 0 && side != 1)) return hipErrorInvalidValue;
+  if (K < 1 || K > 64 || (K > 32 && K % 8) || (side != 0 && side != 1))
+    return hipErrorInvalidValue;
   if (side == 1 && num == nullptr) return hipErrorInvalidValue;
   if (mode != 0 && num != nullptr && den == nullptr) return hipErrorInvalidValue;
   if (upd && (side != 0 || (mode == 0 && den_vec == nullptr) ||

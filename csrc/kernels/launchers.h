@@ -116,8 +116,14 @@ int cnmf_harmony_max_kb();
 hipError_t cnmf_harmony_block(int op, double* Rt, const double* distT, const double* sigma,
                               const int* cells, const int* bidx, int nb, int N, int K, int B,
                               int nvar, int chunk, double* E, double* O, const double* Pr_b,
-                              const double* theta, double* Pen, double* part, int* counter,
-                              hipStream_t stream);
+                              const double* theta, double* Pen, double* part, const double* Y,
+                              const double* Zt, int d, double* obj, hipStream_t stream);
+int cnmf_harmony_centroid_max();
+hipError_t cnmf_harmony_centroid(const double* Zt, const double* Rt, int N, int d, int K,
+                                 int chunk, double* part, double* Y, hipStream_t stream);
+hipError_t cnmf_harmony_objective(const double* O, const double* E, const double* sigma,
+                                  const double* theta, int K, int B, double* obj, double* out,
+                                  hipStream_t stream);
 
 hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K, int n,
                      float* out, long long o_rs, int accumulate, const int* active,

@@ -212,7 +212,7 @@ def test_nmf_batch_gpu_matches_cpu(algo, mode, beta_loss):
 
 
 @pytest.mark.parametrize("beta", [1.0, 0.0, 1.5])
-@pytest.mark.parametrize("K", [3, 10, 17, 32])
+@pytest.mark.parametrize("K", [3, 10, 17, 32, 40, 64])
 def test_beta_contract_matches_reference(beta, K):
     """Fused MFMA beta-MU contraction (beta_mu.hip) vs a float64 PyTorch reference."""
     g = torch.Generator().manual_seed(K)
@@ -322,6 +322,42 @@ def test_split_bf16_beta_kernels_match_fp64(beta, K, N, G):
     h2 = HT.clone()
     reference.beta_h_block(X, h2, W, beta, eps, 1, gamma=1.0 if beta else 0.5)
     torch.testing.assert_close(h1.cpu().double(), h2, rtol=5e-4 if kl else 5e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("beta,K,N,G", [(1.0, 40, 300, 131), (1.0, 48, 257, 200),
+                                        (1.0, 56, 200, 100), (1.0, 64, 129, 64),
+                                        (0.0, 40, 300, 131), (1.5, 48, 257, 200),
+                                        (0.0, 56, 200, 100)])
+def test_split_bf16_beta_kernels_wide_k_match_fp64(beta, K, N, G):
+    """The K > 32 instantiations of beta_planes (beta_planes_wide*.hip: KL to 64, IS /
+    general beta to 56; one column tile per wave, one wave per SIMD) against the float64
+    reference: loss, W-side partials and one fused usage step, with the K <= 32 test's
+    tolerances (KL: the fp16 numerator plane, longer sums at wide K)."""
+    test_split_bf16_beta_kernels_match_fp64(beta, K, N, G)
+
+
+@pytest.mark.parametrize("beta_loss", ["kullback-leibler", "itakura-saito"])
+def test_online_beta_wide_k_runs_native_and_matches_cpu(beta_loss):
+    """Online KL at K = 48 (IS at K = 40) runs on the native kernels -- padded to a
+    multiple of 8, no eager-PyTorch routing warning -- and factorises like the CPU
+    engine from the same seeds: objectives within 2e-3, passes within 2."""
+    import warnings
+
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    K = 48 if beta_loss == "kullback-leibler" else 40
+    Xn = normalized_counts_matrix(1200, 300, n_programs=8, seed=3)
+    opts = NMFOptions(n_components=K, beta_loss=beta_loss, online_chunk_size=600,
+                      online_chunk_max_iter=200, online_max_pass=6)
+    seeds = [5, 6, 7]
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        g = NMFBatchSolver(torch.from_numpy(Xn).cuda(), opts).run(seeds)
+    c = NMFBatchSolver(torch.from_numpy(Xn), opts).run(seeds)
+    assert g.W.shape == (3 * K, 300) and bool((g.W >= 0).all())
+    np.testing.assert_allclose(g.err, c.err, rtol=2e-3)
+    assert np.abs(g.n_iter - c.n_iter).max() <= 2, (g.n_iter, c.n_iter)
 
 
 @pytest.mark.parametrize("beta", [1.0, 0.0])
@@ -493,6 +529,74 @@ def test_harmony_native_matches_cpu():
         np.testing.assert_allclose(gpu.R, cpu.R, rtol=1e-6, atol=1e-9)
         np.testing.assert_allclose(gpu.Z_corr, cpu.Z_corr, rtol=1e-6, atol=1e-8)
         assert gpu.kmeans_rounds == cpu.kmeans_rounds
+
+
+def test_harmony_fused_round_matches_float64_reference():
+    """One Harmony k-means round on the fused kernels (harmony.hip) against float64 torch
+    on the host, from identical state: the centroid kernel vs Z_cos R^T, a block R update
+    whose assign forms the distances itself vs the same update from an explicit distance
+    matrix, and the round objective (assign sums + K x B cross term) vs harmonypy's
+    formula -- all to 1e-10."""
+    import math
+
+    g = torch.Generator().manual_seed(4)
+    N, d, K, nb_var = 3000, 20, 30, 2
+    B_per = [3, 2]
+    B = sum(B_per)
+    Z = torch.randn((d, N), generator=g, dtype=torch.float64)
+    Zc = Z / torch.linalg.vector_norm(Z, dim=0)
+    R = torch.rand((K, N), generator=g, dtype=torch.float64)
+    R = R / R.sum(dim=0)
+    labels = [torch.randint(0, b, (N,), generator=g) for b in B_per]
+    Phi = torch.cat([torch.nn.functional.one_hot(l, b).t().double() for l, b in zip(labels, B_per)])
+    bidx = torch.stack([labels[0], labels[1] + B_per[0]]).to(torch.int32)
+    sigma = torch.full((K,), 0.1, dtype=torch.float64)
+    theta = torch.ones(B, dtype=torch.float64)
+    Pr_b = Phi.sum(dim=1) / N
+    dev = torch.device("cuda")
+    ws = {}
+    # centroids
+    Zt = Zc.t().contiguous()
+    Y = ops.harmony_centroids(Zt.to(dev), R.t().contiguous().to(dev), ws).cpu()
+    torch.testing.assert_close(Y, Zc @ R.t(), rtol=1e-10, atol=1e-12)
+    Y = Y / torch.linalg.vector_norm(Y, dim=0)
+    # one block update, fused distances vs explicit distances
+    E = torch.outer(R.sum(dim=1), Pr_b)
+    O = R @ Phi.t()
+    cells = torch.randperm(N, generator=g)[:700].to(torch.int32)
+    out = {}
+    for fused in (True, False):
+        Rt = R.t().contiguous().to(dev)
+        Eg, Og = E.clone().to(dev), O.clone().to(dev)
+        obj = torch.zeros(2, dtype=torch.float64, device=dev)
+        w = {}
+        if fused:
+            ops.harmony_block_update(Rt, None, sigma.to(dev), cells.to(dev), bidx.to(dev), Eg, Og,
+                                     Pr_b.to(dev), theta.to(dev), w, Y=Y.contiguous().to(dev),
+                                     Zt=Zt.to(dev), obj=obj)
+        else:
+            distT = (2 * (1 - Zc.t() @ Y)).contiguous().to(dev)
+            ops.harmony_block_update(Rt, distT, sigma.to(dev), cells.to(dev), bidx.to(dev), Eg,
+                                     Og, Pr_b.to(dev), theta.to(dev), w)
+        out[fused] = (Rt.cpu(), Eg.cpu(), Og.cpu(), obj.cpu())
+    for a, b in zip(out[True][:3], out[False][:3]):
+        torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-13)
+    # the block's objective terms and the round objective
+    Rn = out[True][0].t()
+    dist = 2 * (1 - Y.t() @ Zc)
+    cl = cells.long()
+    km = (Rn[:, cl] * dist[:, cl]).sum()
+    ent = (sigma[:, None] * torch.where(Rn[:, cl] > 0, Rn[:, cl] * torch.log(Rn[:, cl]),
+                                        torch.zeros(()))).sum()
+    torch.testing.assert_close(out[True][3], torch.stack([km, ent]), rtol=1e-10, atol=1e-12)
+    En, On = out[True][1], out[True][2]
+    res = torch.zeros(1, dtype=torch.float64, device=dev)
+    obj = out[True][3].to(dev)
+    ops.harmony_objective(On.to(dev), En.to(dev), sigma.to(dev), theta.to(dev), obj, res)
+    cross = (sigma[:, None] * theta[None, :] * On * torch.log((On + 1) / (En + 1))).sum()
+    torch.testing.assert_close(res.cpu()[0], km + ent + cross, rtol=1e-10, atol=1e-12)
+    assert float(obj.abs().sum()) == 0.0          # the accumulators are reset
+    assert math.isfinite(float(res.cpu()[0]))
 
 
 @pytest.mark.parametrize("algo,K", [("mu", 3), ("mu", 10), ("mu", 13), ("hals", 10), ("hals", 16),

@@ -63,7 +63,7 @@ def main():
     ap.add_argument("--genes", type=int, default=3000)
     ap.add_argument("--hvg", type=int, default=2000)
     ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--n-iter", type=int, default=20)
+    ap.add_argument("--n-iter", type=int, default=100)
     ap.add_argument("--max-iter-harmony", type=int, default=20,
                     help="the reference default (preprocess.py:138)")
     ap.add_argument("--gpu-busy", action="store_true",
