@@ -75,12 +75,16 @@ def _kmeanspp_batched(X: torch.Tensor, k: int, gen: torch.Generator, n_init: int
     if fused:
         closest = closest.contiguous()
     for c in range(1, k):
-        # inverse CDF of each restart's potential; the scan runs along the contiguous
-        # dimension ((n_init, n) layout: the outer-dimension scan of an (n, n_init) tensor
-        # took 40 ms per centre at 200k points)
-        cum = torch.cumsum(closest.t().contiguous().double(), 1)      # (n_init, n)
-        r = u[c - 1] * cum[:, -1:]                                    # (n_init, trials)
-        cand = torch.searchsorted(cum, r).clamp(max=n - 1)
+        if fused:
+            # inverse CDF of each restart's potential (block sums + one workgroup per
+            # restart, kmeans.hip ppsample_kernel)
+            cand = ops.kmeanspp_sample(closest, u[c - 1])
+        else:
+            # the scan runs along the contiguous dimension ((n_init, n) layout: the
+            # outer-dimension scan of an (n, n_init) tensor took 40 ms per centre at 200k)
+            cum = torch.cumsum(closest.t().contiguous().double(), 1)  # (n_init, n)
+            r = u[c - 1] * cum[:, -1:]                                # (n_init, trials)
+            cand = torch.searchsorted(cum, r).clamp(max=n - 1)
         if fused:
             pot = ops.kmeanspp_step(X, X[cand.reshape(-1)], closest, trials)
             best = torch.argmin(pot, dim=1)                           # (n_init,)

@@ -48,8 +48,22 @@ def _design(meta: pd.DataFrame, vars_use) -> tuple[np.ndarray, np.ndarray]:
 
 
 class HarmonyResult:
-    def __init__(self, **kw):
+    """harmonypy's result attributes as numpy arrays, copied from the device on first
+    access (a 500k-cell R is 400 MB the device pipeline never reads on the host)."""
+
+    _LAZY = ("Z_corr", "Z_cos", "R", "Phi", "Phi_moe", "lamb")
+
+    def __init__(self, tensors: dict | None = None, **kw):
+        self._t = dict(tensors or {})
         self.__dict__.update(kw)
+
+    def __getattr__(self, name):
+        t = self.__dict__.get("_t", {})
+        if name in t:
+            v = t[name].cpu().numpy()
+            self.__dict__[name] = v
+            return v
+        raise AttributeError(name)
 
 
 def _tall_matmul(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
@@ -304,9 +318,8 @@ class Harmony:
         return (old - new) / abs(old) < self.eps_h
 
     def result(self) -> HarmonyResult:
-        return HarmonyResult(Z_corr=self.Z_corr.cpu().numpy(), Z_cos=self.Z_cos.cpu().numpy(),
-                             R=self.R.cpu().numpy(), K=self.K, Phi=self.Phi.cpu().numpy(),
-                             Phi_moe=self.Phi_moe.cpu().numpy(), lamb=self.lamb.cpu().numpy(),
+        return HarmonyResult(dict(Z_corr=self.Z_corr, Z_cos=self.Z_cos, R=self.R, Phi=self.Phi,
+                                  Phi_moe=self.Phi_moe, lamb=self.lamb), K=self.K,
                              objective_harmony=list(self.objective_harmony),
                              kmeans_rounds=list(self.kmeans_rounds), _R_t=self.R,
                              _Phi_moe_t=self.Phi_moe, _lamb_t=self.lamb, _lv=self._lv)
@@ -416,6 +429,10 @@ def moe_correct_ridge(Z_orig, Z_cos, Z_corr, R, W, K, Phi_Rk, Phi_moe, lamb, dev
     return Zcos.cpu().numpy(), Zc.cpu().numpy(), W_last, Phi_Rk
 
 
+def _host(a) -> np.ndarray:
+    return a.cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+
+
 def _levels(Phi_moe: np.ndarray):
     """Level structure of a Harmony design [1; one-hot levels] (B1 x N): per row b the
     cells of that level, and per cell its combination of levels (plus a per-device cache
@@ -487,6 +504,57 @@ def _level_tensors(lv: dict, dev: torch.device) -> dict:
     return t
 
 
+# workgroups a ridge_seg_tgemm launch should have before the levels are cut into chunks
+# (256 CUs; the kernel is one 4-wave workgroup per (segment, 32 clusters, 64 features))
+_SEG_TARGET_WG = 2048
+
+
+def _seg_chunks(lv: dict, t: dict, tiles: int, dev: torch.device):
+    """Chunk table for a ridge_seg_tgemm with ``tiles`` (cluster x feature) tiles per
+    segment: (chunk boundaries into the level cell list (int64, nchunk + 1), first chunk
+    of every level (int32, B1 + 1), nchunk), or None when the levels alone fill the chip."""
+    B1 = lv["B1"]
+    if B1 * tiles >= _SEG_TARGET_WG:
+        return None
+    seg = np.concatenate([[0], np.cumsum([c.size for c in lv["cells"]])]).astype(np.int64)
+    want = -(-_SEG_TARGET_WG // tiles)
+    size = max(256, -(-int(seg[-1]) // want))
+    size = -(-size // 16) * 16               # whole 4-cell steps of the 4 waves
+    key = ("chunks", size)
+    c = t.get(key)
+    if c is None:
+        bounds, first = [], [0]
+        for b in range(B1):
+            s0, s1 = int(seg[b]), int(seg[b + 1])
+            starts = list(range(s0, s1, size)) or [s0]
+            bounds.extend(starts)
+            first.append(first[-1] + len(starts))
+        bounds.append(int(seg[-1]))
+        c = (torch.from_numpy(np.asarray(bounds, dtype=np.int64)).to(dev),
+             torch.from_numpy(np.asarray(first, dtype=np.int32)).to(dev), len(bounds) - 1)
+        t[key] = c
+    return c
+
+
+def _seg_tgemm(h, lv, t, Rt, Kc, X, ldx, F, x_f64, out, st):
+    """out[b][k][f] = sum over level b's cells of R[k, n] X[n, f] (out: B1 x Kc x F)."""
+    B1 = lv["B1"]
+    tiles = -(-Kc // 32) * -(-F // 64)
+    ch = _seg_chunks(lv, t, tiles, X.device if isinstance(X, torch.Tensor) else Rt.device)
+    xp = X.data_ptr()
+    if ch is None:
+        h.ridge_seg_tgemm(Rt.data_ptr(), Rt.stride(0), Kc, xp, x_f64, ldx, F,
+                          t["idx"].data_ptr(), t["seg"].data_ptr(), B1, out.data_ptr(),
+                          Kc * F, F, st)
+        return
+    bounds, first, nch = ch
+    part = torch.empty((nch, Kc, F), dtype=torch.float64, device=out.device)
+    h.ridge_seg_tgemm(Rt.data_ptr(), Rt.stride(0), Kc, xp, x_f64, ldx, F, t["idx"].data_ptr(),
+                      bounds.data_ptr(), nch, part.data_ptr(), Kc * F, F, st)
+    h.ridge_seg_reduce(part.data_ptr(), first.data_ptr(), B1, Kc, F, out.data_ptr(), Kc * F, F,
+                       st)
+
+
 def _ridge_native(X: torch.Tensor, Rt: torch.Tensor, lv: dict, Lt: torch.Tensor,
                   return_w: bool = False):
     """The MOE ridge correction on the f64 matrix cores (csrc/kernels/ridge.hip) for a
@@ -502,14 +570,11 @@ def _ridge_native(X: torch.Tensor, Rt: torch.Tensor, lv: dict, Lt: torch.Tensor,
     st = ops._stream_ptr(X)
     # Y[b][k][f] = sum over level b's cells of R[k, n] X[n, f]
     Y = torch.empty((B1, Kc, F), dtype=torch.float64, device=dev)
-    h.ridge_seg_tgemm(Rt.data_ptr(), Rt.stride(0), Kc, X.data_ptr(), int(X.dtype == torch.float64),
-                      X.stride(0), F, t["idx"].data_ptr(), t["seg"].data_ptr(), B1, Y.data_ptr(),
-                      Kc * F, F, st)
+    _seg_tgemm(h, lv, t, Rt, Kc, X, X.stride(0), F, int(X.dtype == torch.float64), Y, st)
     # A0[b][k][c] = sum over level b's cells of R[k, n] Phi[c, n]
     Pt = t["Pt"]
     A0 = torch.empty((B1, Kc, B1), dtype=torch.float64, device=dev)
-    h.ridge_seg_tgemm(Rt.data_ptr(), Rt.stride(0), Kc, Pt.data_ptr(), 1, Pt.stride(0), B1,
-                      t["idx"].data_ptr(), t["seg"].data_ptr(), B1, A0.data_ptr(), Kc * B1, B1, st)
+    _seg_tgemm(h, lv, t, Rt, Kc, Pt, Pt.stride(0), B1, 1, A0, st)
     A = A0.permute(1, 0, 2).cpu().numpy() + Lt.cpu().numpy()[None]        # (Kc, B1, B1)
     Wh = np.linalg.solve(A, Y.permute(1, 0, 2).cpu().numpy())               # (Kc, B1, F)
     Wh[:, 0, :] = 0.0                                    # keep the intercept
@@ -543,10 +608,10 @@ def moe_correct_expression(X: torch.Tensor, R, Phi_moe, lamb, K: int | None = No
     Lt = torch.as_tensor(lamb, dtype=torch.float64, device=dev)
     if dev.type == "cuda" and ops.use_native(X) and X.dtype in (torch.float32, torch.float64) \
             and X.dim() == 2 and (X.shape[1] <= 1 or X.stride(1) == 1):
-        lv = levels if levels is not None else _levels(np.asarray(Phi_moe))
+        lv = levels if levels is not None else _levels(_host(Phi_moe))
         if lv is not None:   # the f64 matrix-core kernels (no materialised Phi_Rk)
             return _ridge_native(X, Rt.t().contiguous(), lv, Lt)
-    Pt = torch.as_tensor(np.asarray(Phi_moe), dtype=torch.float64).to(dev)
+    Pt = torch.as_tensor(Phi_moe, dtype=torch.float64, device=dev)
     Kc, N = Rt.shape
     B1 = Pt.shape[0]
     F = X.shape[1]

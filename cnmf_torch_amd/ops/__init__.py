@@ -1553,6 +1553,29 @@ def kmeanspp_step(X: torch.Tensor, C: torch.Tensor, closest: torch.Tensor, trial
     return pot.sum(dim=0).view(n_init, trials)
 
 
+def kmeanspp_sample(closest: torch.Tensor, u: torch.Tensor) -> torch.Tensor:
+    """k-means++ candidate draw for every restart: closest (n, n_init) float64 contiguous,
+    u (n_init, trials) uniforms -> (n_init, trials) int64 point indices, the first point
+    whose inclusive running sum of closest[:, r] reaches u * total (torch.searchsorted of
+    the cumsum, clamped to n - 1).  GPU: kmeans.hip ppsum/ppsample kernels."""
+    n, n_init = closest.shape
+    if not use_native(closest) or _hip.kmeanspp_sample_blocks(n) > 15360:
+        cum = torch.cumsum(closest.t().contiguous().double(), 1)
+        return torch.searchsorted(cum, u * cum[:, -1:]).clamp(max=n - 1)
+    if closest.dtype != torch.float64 or not closest.is_contiguous():
+        raise ValueError("closest: contiguous float64 required")
+    trials = u.shape[1]
+    uu = u.to(torch.float64).contiguous()
+    if uu.shape[0] != n_init:
+        raise ValueError("u: one row per restart")
+    nb = int(_hip.kmeanspp_sample_blocks(n))
+    bsum = torch.empty((n_init, nb), dtype=torch.float64, device=closest.device)
+    cand = torch.empty((n_init, trials), dtype=torch.int64, device=closest.device)
+    _hip.kmeanspp_sample(closest.data_ptr(), n, n_init, uu.data_ptr(), trials, bsum.data_ptr(),
+                         cand.data_ptr(), _stream_ptr(closest))
+    return cand
+
+
 def kmeans_fused_ok(X: torch.Tensor, k: int) -> bool:
     """True when the fused low-dimensional Lloyd step (kmeans.hip) handles (X, k)."""
     return use_native(X) and bool(_hip.kmeans_fits(int(k), int(X.shape[1])))

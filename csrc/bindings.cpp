@@ -56,6 +56,14 @@ PYBIND11_MODULE(_hip, m) {
                                      reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_ridge_seg_tgemm");
         });
+  m.def("ridge_seg_reduce",
+        [](uintptr_t part, uintptr_t cfirst, int nseg, int Kc, int F, uintptr_t out,
+           long long seg_stride, long long ldo, uintptr_t stream) {
+          check(cnmf_ridge_seg_reduce(P<const double>(part), P<const int>(cfirst), nseg, Kc, F,
+                                      P<double>(out), seg_stride, ldo,
+                                      reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_ridge_seg_reduce");
+        });
   m.def("ridge_apply",
         [](uintptr_t Rt, long long ldr, int Kc, uintptr_t X, int x_f64, long long ldx, uintptr_t Y,
            long long ldy, int F, uintptr_t order, uintptr_t blk, int nblk, uintptr_t Wc,
@@ -270,6 +278,14 @@ PYBIND11_MODULE(_hip, m) {
 
   m.def("kmeans_blocks", [](int n) { return cnmf_kmeans_blocks(n); });
   m.def("kmeanspp_blocks", [](int n) { return cnmf_kmeanspp_blocks(n); });
+  m.def("kmeanspp_sample_blocks", [](int n) { return cnmf_kmeanspp_sample_blocks(n); });
+  m.def("kmeanspp_sample", [](uintptr_t closest, int n, int n_init, uintptr_t u, int trials,
+                              uintptr_t bsum, uintptr_t cand, uintptr_t stream) {
+    check(cnmf_kmeanspp_sample(P<const double>(closest), n, n_init, P<const double>(u), trials,
+                               P<double>(bsum), P<long long>(cand),
+                               reinterpret_cast<hipStream_t>(stream)),
+          "kmeanspp_sample");
+  });
   m.def("kmeanspp_fits", [](int M, int d) { return cnmf_kmeanspp_fits(M, d); });
   m.def("kmeanspp", [](uintptr_t X, long long ldx, int n, int d, uintptr_t C, int M, int trials,
                        uintptr_t closest, int n_init, int mode, uintptr_t pot, uintptr_t stream) {

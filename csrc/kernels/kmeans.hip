@@ -3,11 +3,16 @@
 // d <= 64; consensus k-means at K x G spectra keeps the MFMA distance path).
 //
 // One launch per Lloyd iteration for ALL restarts (grid.y = restart):
-//   phase A  every thread owns one point per round: the point lives in registers
-//            (d padded to DP, a compile-time multiple of 16), the restart's centroids sit
-//            in LDS and are read as broadcast b128 loads; the thread keeps the argmin of
-//            the exact squared distance sum_j (x_j - c_j)^2 (first index on ties, as numpy
-//            argmin), writes its label (and the distance for the inertia).
+//   phase A  assignment on the f64 matrix cores: wave w owns 64 points of the round as 4
+//            tiles of 16; the restart's centroids sit in LDS transposed (coordinate-major,
+//            A operand), the points are the B operand straight from global memory, and
+//            v_mfma_f64_16x16x4f64 forms 16 x 16 blocks of x . c; the score
+//            |c|^2 - 2 x . c (sklearn's expanded distance, |x|^2 added only for the
+//            distance output) picks the nearest centroid per point (first index on ties,
+//            as numpy argmin) with a cross-lane reduction over the 4 lane groups.  The
+//            previous thread-per-point form (exact (x - c)^2 sums, broadcast LDS reads of
+//            every centroid) ran at ~12 ms per step at 500k x 50 x 100 x 10 restarts
+//            (profiles/r5i_*).
 //   phase B  the round's points are added to the workgroup's centroid accumulator in LDS:
 //            a stable counting sort groups them by label, then each thread sums whole
 //            (cluster, feature) segments in point order and adds them once (no float
@@ -16,7 +21,10 @@
 //            workgroups with a fixed-order reduction -> bitwise deterministic centroids.
 // The (n x n_init*k) distance matrix of the MFMA path (4 GB at 500k cells x 10 x 100) is
 // never materialised.
+// f64 16x16x4 MFMA: A lane l = A[l&15][l>>4], B lane l = B[l>>4][l&15];
+// D: col = lane&15, row = (lane>>4) + 4*reg.
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 #include "common.h"
@@ -26,6 +34,27 @@ namespace cnmf {
 constexpr int kKmThreads = 256;
 constexpr int kKmRounds = 4;   // rounds of 256 points per workgroup
 
+typedef double km_f64x4 __attribute__((ext_vector_type(4)));
+
+// centroid tile pitch of the transposed LDS table: 16 (mod 32) doubles, so the 4 lane
+// groups of an A-operand read fall on disjoint bank halves
+__host__ __device__ constexpr int km_kps(int k) {
+  return ((k + 15) / 16 * 16) % 32 == 16 ? (k + 15) / 16 * 16 : (k + 15) / 16 * 16 + 16;
+}
+
+__host__ __device__ constexpr size_t km_lds_bytes(int k, int dp) {
+  return ((size_t)dp * km_kps(k) + (size_t)(k + 15) / 16 * 16 + (size_t)k * dp + k) *
+             sizeof(double) +
+         (2 * kKmThreads + 2 * (size_t)k) * sizeof(int);
+}
+
+__device__ __forceinline__ void km_take(double v, int c, double& best, int& arg) {
+  if (v < best || (v == best && c < arg)) {
+    best = v;
+    arg = c;
+  }
+}
+
 template <int DP>
 __global__ void __launch_bounds__(kKmThreads)
     kmeans_step_kernel(const double* __restrict__ X, long long ldx, int n, int d,
@@ -33,9 +62,11 @@ __global__ void __launch_bounds__(kKmThreads)
                        int* __restrict__ labels, double* __restrict__ mind,
                        double* __restrict__ psum, double* __restrict__ pcnt) {
   extern __shared__ double smem[];
-  double* sC = smem;                       // k * DP centroids (zero padded)
-  double* sAcc = sC + (long long)k * DP;   // k * DP accumulator
-  double* sCnt = sAcc + (long long)k * DP; // k counts
+  const int KP = (k + 15) / 16 * 16, KPS = km_kps(k);
+  double* sCt = smem;                       // DP x KPS centroids, coordinate-major
+  double* sCsq = sCt + (long long)DP * KPS; // KP squared norms (+inf for the padding)
+  double* sAcc = sCsq + KP;                 // k * DP accumulator
+  double* sCnt = sAcc + (long long)k * DP;  // k counts
   int* sLab = reinterpret_cast<int*>(sCnt + k);   // 256 labels of the current round
   int* sPerm = sLab + kKmThreads;                   // round's points grouped by label
   int* sHist = sPerm + kKmThreads;                  // k: points per label this round
@@ -45,48 +76,86 @@ __global__ void __launch_bounds__(kKmThreads)
   if (live != nullptr && live[r] == 0) return;    // frozen restart: partials unused
   const int tid = threadIdx.x;
   const double* Cr = C + (long long)r * k * d;
-  for (int e = tid; e < k * DP; e += kKmThreads) {
-    const int c = e / DP, j = e % DP;
-    sC[e] = j < d ? Cr[(long long)c * d + j] : 0.0;
-    sAcc[e] = 0.0;
+  for (int e = tid; e < DP * KPS; e += kKmThreads) {
+    const int j = e / KPS, c = e - j * KPS;
+    sCt[e] = (c < k && j < d) ? Cr[(long long)c * d + j] : 0.0;
+  }
+  for (int e = tid; e < k * DP; e += kKmThreads) sAcc[e] = 0.0;
+  for (int c = tid; c < KP; c += kKmThreads) {
+    double s = 0.0;
+    if (c < k)
+      for (int j = 0; j < d; ++j) {
+        const double v = Cr[(long long)c * d + j];
+        s = fma(v, v, s);
+      }
+    sCsq[c] = c < k ? s : INFINITY;
   }
   for (int c = tid; c < k; c += kKmThreads) sCnt[c] = 0.0;
   __syncthreads();
 
+  const int lane = tid & 63, wave = tid >> 6, col = lane & 15, grp = lane >> 4;
+  const int nks = (d + 3) >> 2, nct = KP >> 4;
   const long long base = (long long)blockIdx.x * (kKmThreads * kKmRounds);
   for (int round = 0; round < kKmRounds; ++round) {
     const long long p0 = base + (long long)round * kKmThreads;
     if (p0 >= n) break;                              // uniform across the workgroup
-    const long long i = p0 + tid;
-    // ---- phase A: assignment
-    int arg = -1;
-    if (i < n) {
-      double x[DP];
-      const double* xr = X + i * ldx;
+    // ---- phase A: assignment (MFMA scores)
+    for (int pt = 0; pt < 4; ++pt) {
+      const int slot = 64 * wave + 16 * pt + col;
+      const long long i = p0 + slot;
+      const bool ok = i < n;
+      const double* xr = X + (ok ? i : 0) * ldx;
+      double bx[DP / 4];
+      double xsq = 0.0;
 #pragma unroll
-      for (int j = 0; j < DP; ++j) x[j] = j < d ? xr[j] : 0.0;
-      double best = 0.0;
-      arg = 0;
-      for (int c = 0; c < k; ++c) {
-        const double2* cc = reinterpret_cast<const double2*>(sC + (long long)c * DP);
-        double s0 = 0.0, s1 = 0.0;
+      for (int ks = 0; ks < DP / 4; ++ks) {
+        const int j = 4 * ks + grp;
+        bx[ks] = (ok && j < d) ? xr[j] : 0.0;
+        xsq = fma(bx[ks], bx[ks], xsq);
+      }
+      double best = INFINITY;
+      int arg = 0x7fffffff;
+      for (int ct = 0; ct < nct; ct += 2) {
+        const bool two = ct + 1 < nct;                 // uniform
+        km_f64x4 a0 = km_f64x4{0.0, 0.0, 0.0, 0.0}, a1 = a0;
+        const double* ap = sCt + (long long)grp * KPS + 16 * ct + col;
 #pragma unroll
-        for (int j = 0; j < DP / 2; ++j) {
-          const double2 v = cc[j];
-          const double a = x[2 * j] - v.x, b = x[2 * j + 1] - v.y;
-          s0 = fma(a, a, s0);
-          s1 = fma(b, b, s1);
+        for (int ks = 0; ks < DP / 4; ++ks) {
+          if (ks < nks) {                              // uniform
+            const double* row = ap + (long long)(4 * ks) * KPS;
+            a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(row[0], bx[ks], a0, 0, 0, 0);
+            if (two) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(row[16], bx[ks], a1, 0, 0, 0);
+          }
         }
-        const double s = s0 + s1;
-        if (c == 0 || s < best) {
-          best = s;
-          arg = c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = 16 * ct + grp + 4 * q;
+          km_take(sCsq[c] - 2.0 * a0[q], c, best, arg);
+        }
+        if (two) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = 16 * (ct + 1) + grp + 4 * q;
+            km_take(sCsq[c] - 2.0 * a1[q], c, best, arg);
+          }
         }
       }
-      labels[(long long)r * n + i] = arg;
-      if (mind != nullptr) mind[(long long)r * n + i] = best;
+      // the point's 4 lane groups hold disjoint centroid subsets: min over them
+#pragma unroll
+      for (int m = 16; m <= 32; m <<= 1) {
+        const double ob = __shfl_xor(best, m);
+        const int oa = __shfl_xor(arg, m);
+        km_take(ob, oa, best, arg);
+        xsq += __shfl_xor(xsq, m);
+      }
+      if (grp == 0) {
+        sLab[slot] = ok ? arg : -1;
+        if (ok) {
+          labels[(long long)r * n + i] = arg;
+          if (mind != nullptr) mind[(long long)r * n + i] = fmax(xsq + best, 0.0);
+        }
+      }
     }
-    sLab[tid] = arg;
     __syncthreads();
     // ---- phase B: ordered accumulation (only when partial sums are wanted).  The
     // round's points are grouped by label with a stable counting sort (rank = earlier
@@ -141,8 +210,7 @@ template <int DP>
 static hipError_t launch_kmeans(const double* X, long long ldx, int n, int d, const double* C,
                                 int k, int n_init, const int* live, int* labels, double* mind,
                                 double* psum, double* pcnt, hipStream_t stream) {
-  const size_t lds = (size_t)(2 * (size_t)k * DP + k) * sizeof(double) +
-                     (2 * kKmThreads + 2 * (size_t)k) * sizeof(int);
+  const size_t lds = km_lds_bytes(k, DP);
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_step_kernel<DP>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -227,7 +295,116 @@ static hipError_t launch_kmeanspp(const double* X, long long ldx, int n, int d, 
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------- k-means++ candidate sampling
+// Inverse-CDF draw of every restart's candidates from its potential (torch.searchsorted of
+// the inclusive prefix sum of closest[:, r], side left): the first point whose running sum
+// reaches u * total.  A (n_init x n) cumsum + searchsorted cost ~1.3 ms per centre at 500k
+// points (the scan of 10 long rows runs on few workgroups, profiles/r5i_*); here
+//   1. ppsum_kernel: block sums of 1024 points per restart (fixed order);
+//   2. ppsample_kernel (one workgroup per restart): prefix of the block sums in LDS, a
+//      binary search per trial for the block, then a scan of that block's 1024 values.
+constexpr int kPpBlock = 1024;
+
+__global__ void __launch_bounds__(256) ppsum_kernel(const double* __restrict__ closest, int n,
+                                                    int n_init, double* __restrict__ bsum) {
+  __shared__ double red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long p0 = (long long)blockIdx.x * kPpBlock + 4 * tid;
+  for (int r = 0; r < n_init; ++r) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (p0 + j < n) s += closest[(p0 + j) * n_init + r];
+    s = wave_sum(s);
+    if (lane == 0) red[wave] = s;
+    __syncthreads();
+    if (tid == 0) bsum[(long long)r * gridDim.x + blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+    __syncthreads();
+  }
+}
+
+// inclusive scan of v over the 1024 threads (Hillis-Steele in LDS)
+__device__ __forceinline__ double pp_scan(double v, double* s) {
+  const int tid = threadIdx.x;
+  s[tid] = v;
+  __syncthreads();
+  for (int d = 1; d < kPpBlock; d <<= 1) {
+    const double a = tid >= d ? s[tid - d] : 0.0;
+    __syncthreads();
+    s[tid] += a;
+    __syncthreads();
+  }
+  return s[tid];
+}
+
+__global__ void __launch_bounds__(kPpBlock) ppsample_kernel(
+    const double* __restrict__ closest, int n, int n_init, const double* __restrict__ bsum, int nb,
+    const double* __restrict__ u, int trials, long long* __restrict__ cand) {
+  extern __shared__ double pre[];          // nb block prefix sums
+  __shared__ double sc[kPpBlock];
+  __shared__ int s_hit;
+  const int r = blockIdx.x, tid = threadIdx.x;
+  double carry = 0.0;
+  for (int b0 = 0; b0 < nb; b0 += kPpBlock) {
+    const int b = b0 + tid;
+    const double v = b < nb ? bsum[(long long)r * nb + b] : 0.0;
+    const double inc = pp_scan(v, sc) + carry;
+    if (b < nb) pre[b] = inc;
+    carry = sc[kPpBlock - 1] + carry;
+    __syncthreads();
+  }
+  const double total = pre[nb - 1];
+  for (int t = 0; t < trials; ++t) {
+    const double target = u[(long long)r * trials + t] * total;
+    // first block whose prefix reaches the target (the last block if none does)
+    int lo = 0, hi = nb - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (pre[mid] >= target) hi = mid; else lo = mid + 1;
+    }
+    const int b = lo;
+    const double base = b > 0 ? pre[b - 1] : 0.0;
+    const long long i = (long long)b * kPpBlock + tid;
+    const double v = i < n ? closest[i * n_init + r] : 0.0;
+    if (tid == 0) s_hit = kPpBlock;
+    __syncthreads();
+    const double inc = base + pp_scan(v, sc);
+    if (inc >= target && i < n) atomicMin(&s_hit, tid);
+    __syncthreads();
+    if (tid == 0) {
+      long long idx = (long long)b * kPpBlock + (s_hit < kPpBlock ? s_hit : kPpBlock - 1);
+      if (idx > n - 1) idx = n - 1;
+      cand[(long long)r * trials + t] = idx;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace cnmf
+
+extern "C" int cnmf_kmeanspp_sample_blocks(int n) {
+  return (n + cnmf::kPpBlock - 1) / cnmf::kPpBlock;
+}
+
+// cand (n_init x trials, int64) from closest (n x n_init, f64) and u (n_init x trials);
+// bsum: workspace of n_init * cnmf_kmeanspp_sample_blocks(n) doubles
+extern "C" hipError_t cnmf_kmeanspp_sample(const double* closest, int n, int n_init,
+                                           const double* u, int trials, double* bsum,
+                                           long long* cand, hipStream_t stream) {
+  if (n <= 0 || n_init <= 0 || trials <= 0) return hipErrorInvalidValue;
+  const int nb = cnmf_kmeanspp_sample_blocks(n);
+  const size_t lds = (size_t)nb * sizeof(double);
+  if (lds > 120 * 1024) return hipErrorInvalidValue;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cnmf::ppsample_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cnmf::ppsum_kernel, dim3(nb), dim3(256), 0, stream, closest, n, n_init, bsum);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(cnmf::ppsample_kernel, dim3(n_init), dim3(cnmf::kPpBlock), lds, stream,
+                     closest, n, n_init, bsum, nb, u, trials, cand);
+  return hipGetLastError();
+}
 
 extern "C" int cnmf_kmeanspp_blocks(int n) {
   return (n + cnmf::kKmThreads - 1) / cnmf::kKmThreads;
@@ -260,13 +437,12 @@ extern "C" int cnmf_kmeans_blocks(int n) {
   return (n + per - 1) / per;
 }
 
-// Largest k * DP the LDS budget (160 KiB per CU) holds: 2 * k * DP + k doubles + labels.
+// Whether the LDS budget (160 KiB per CU) holds the transposed centroid table, the
+// accumulator and the label arrays of (k, d).
 extern "C" int cnmf_kmeans_fits(int k, int d) {
   if (k < 1 || d < 1 || d > 64) return 0;
   const int dp = (d + 15) / 16 * 16;
-  const size_t lds = (size_t)(2 * (size_t)k * dp + k) * sizeof(double) +
-                     (2 * cnmf::kKmThreads + 2 * (size_t)k) * sizeof(int);
-  return lds <= 156 * 1024 ? 1 : 0;
+  return cnmf::km_lds_bytes(k, dp) <= 156 * 1024 ? 1 : 0;
 }
 
 extern "C" hipError_t cnmf_kmeans_step(const double* X, long long ldx, int n, int d,

@@ -43,6 +43,9 @@ hipError_t cnmf_ridge_seg_tgemm(const double* Rt, long long ldr, int Kc, const v
                                 long long ldx, int F, const int* idx, const long long* seg,
                                 int nseg, double* out, long long seg_stride, long long ldo,
                                 hipStream_t stream);
+hipError_t cnmf_ridge_seg_reduce(const double* part, const int* cfirst, int nseg, int Kc, int F,
+                                 double* out, long long seg_stride, long long ldo,
+                                 hipStream_t stream);
 hipError_t cnmf_ridge_apply(const double* Rt, long long ldr, int Kc, const void* X, int x_f64,
                             long long ldx, void* Y, long long ldy, int F, const int* order,
                             const int* blk, int nblk, const double* Wc, long long wc_combo,
@@ -131,6 +134,9 @@ hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K
 
 int cnmf_kmeans_blocks(int n);
 int cnmf_kmeanspp_blocks(int n);
+int cnmf_kmeanspp_sample_blocks(int n);
+hipError_t cnmf_kmeanspp_sample(const double* closest, int n, int n_init, const double* u,
+                                int trials, double* bsum, long long* cand, hipStream_t stream);
 int cnmf_kmeanspp_fits(int M, int d);
 hipError_t cnmf_kmeanspp(const double* X, long long ldx, int n, int d, const double* C, int M,
                          int trials, double* closest, int n_init, int mode, double* pot,

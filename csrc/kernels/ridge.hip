@@ -82,6 +82,25 @@ __global__ void __launch_bounds__(256) ridge_seg_tgemm_kernel(
   }
 }
 
+// Chunked segments: when (levels x tiles) gives too few workgroups to fill the chip (the
+// 50-PC Harmony ridge: 16 levels x 4 cluster tiles x 1 feature tile = 64 workgroups each
+// walking up to all 500k cells, 35 ms per call, profiles/r5i_*), the host cuts every
+// level's cell list into chunks, ridge_seg_tgemm_kernel writes one partial per chunk and
+// this kernel sums a level's chunks in chunk order (deterministic):
+//   out[s][k][f] = sum_{c in [cfirst[s], cfirst[s+1])} part[c][k][f]   (part: Kc x F dense)
+__global__ void __launch_bounds__(256) ridge_seg_reduce_kernel(
+    const double* __restrict__ part, const int* __restrict__ cfirst, int Kc, int F,
+    double* __restrict__ out, long long seg_stride, long long ldo) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long kf = (long long)Kc * F;
+  if (e >= kf) return;
+  const int s = blockIdx.y;
+  const int k = (int)(e / F), f = (int)(e - (long long)k * F);
+  double acc = 0.0;
+  for (int c = cfirst[s]; c < cfirst[s + 1]; ++c) acc += part[(long long)c * kf + e];
+  out[(long long)s * seg_stride + (long long)k * ldo + f] = acc;
+}
+
 // Y[n][f] = (TY)((double)X[n][f] - sum_k Rt[n][k] * Wc[combo][k][f]) for the cells of
 // every block: blk[b] = (combo, first position in the combo-sorted cell order, count <= 64);
 // grid (blocks, f tiles of 64); 4 waves x 16 cells
@@ -142,6 +161,18 @@ extern "C" hipError_t cnmf_ridge_seg_tgemm(const double* Rt, long long ldr, int 
   else
     hipLaunchKernelGGL(cnmf::ridge_seg_tgemm_kernel<float>, grid, dim3(256), 0, stream, Rt, ldr, Kc,
                        (const float*)X, ldx, F, idx, seg, out, seg_stride, ldo);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t cnmf_ridge_seg_reduce(const double* part, const int* cfirst, int nseg,
+                                            int Kc, int F, double* out, long long seg_stride,
+                                            long long ldo, hipStream_t stream) {
+  if (nseg <= 0 || F <= 0 || Kc <= 0) return hipSuccess;
+  if (ldo < F || seg_stride < (long long)(Kc - 1) * ldo + F) return hipErrorInvalidValue;
+  const long long kf = (long long)Kc * F;
+  const dim3 grid((unsigned)((kf + 255) / 256), (unsigned)nseg);
+  hipLaunchKernelGGL(cnmf::ridge_seg_reduce_kernel, grid, dim3(256), 0, stream, part, cfirst, Kc,
+                     F, out, seg_stride, ldo);
   return hipGetLastError();
 }
 

@@ -417,6 +417,26 @@ def test_kmeanspp_fused_step_matches_reference(d):
     torch.testing.assert_close(cg.cpu(), cr, rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("n", [1000, 300000 + 37])
+def test_kmeanspp_sample_matches_cumsum_searchsorted(n):
+    """Device k-means++ draw (kmeans.hip ppsum/ppsample) == torch cumsum + searchsorted
+    (side left, clamped), including u = 0 and u = 1 and zero-potential stretches."""
+    rs = np.random.default_rng(n)
+    n_init, trials = 10, 6
+    closest = torch.from_numpy(rs.random((n, n_init)) ** 3)
+    closest[: n // 3, 2] = 0.0                   # a restart with a zero-potential prefix
+    u = torch.from_numpy(rs.random((n_init, trials)))
+    u[0, 0], u[1, 1], u[2, 0] = 0.0, 1.0, 1e-300
+    cum = torch.cumsum(closest.t().contiguous(), 1)
+    ref = torch.searchsorted(cum, u * cum[:, -1:]).clamp(max=n - 1)
+    got = ops.kmeanspp_sample(closest.cuda().contiguous(), u.cuda()).cpu()
+    # a draw may land one point over where the two summation orders round the running
+    # sum differently right at the target; away from such ties the draws are identical
+    diff = (got - ref).abs()
+    assert int((diff > 0).sum()) <= 1 and int(diff.max()) <= 1
+    assert got[0, 0] == 0 and got[2, 0] == n // 3
+
+
 def test_device_kmeans_large_n_uses_fused_init():
     """Harmony-sized k-means (many points, few PCs) goes through the fused k-means++ path
     and still separates planted clusters."""

@@ -32,7 +32,22 @@ from cnmf_torch_amd import Preprocess, cNMF  # noqa: E402
 from cnmf_torch_amd.utils.anndata_lite import AnnData  # noqa: E402
 
 
-def simulate(n, g, programs=8, n_cov=4, levels=(6, 4, 3, 2), seed=0, block=20000):
+def _sim_part(args):
+    S, effects, covs, seed, a, b, programs = args
+    # one generator per row block: the matrix does not depend on the worker count
+    r = np.random.default_rng([seed, a])
+    U = r.dirichlet(np.full(programs, 0.3), b - a)
+    lib = r.lognormal(np.log(1500.0), 0.35, b - a)
+    lam = (U @ S) * lib[:, None]
+    for i, e in enumerate(effects):
+        lam *= e[covs[i]]
+    x = r.poisson(lam)
+    m = x != 0
+    return (np.cumsum(m.sum(axis=1)), np.nonzero(m)[1].astype(np.int32),
+            x[m].astype(np.float32))
+
+
+def simulate(n, g, programs=8, n_cov=4, levels=(6, 4, 3, 2), seed=0, block=2500):
     rs = np.random.default_rng(seed)
     base = rs.lognormal(0.0, 1.0, g)
     S = np.tile(base, (programs, 1))
@@ -42,16 +57,18 @@ def simulate(n, g, programs=8, n_cov=4, levels=(6, 4, 3, 2), seed=0, block=20000
     S /= S.sum(1, keepdims=True)
     covs = {f"cov{i}": rs.integers(0, levels[i], n) for i in range(n_cov)}
     effects = [rs.lognormal(0.0, 0.3, (levels[i], g)) for i in range(n_cov)]
-    parts = []
-    for a in range(0, n, block):
-        b = min(n, a + block)
-        U = rs.dirichlet(np.full(programs, 0.3), b - a)
-        lib = rs.lognormal(np.log(1500.0), 0.35, b - a)
-        lam = (U @ S) * lib[:, None]
-        for i in range(n_cov):
-            lam *= effects[i][covs[f"cov{i}"][a:b]]
-        parts.append(sp.csr_matrix(rs.poisson(lam).astype(np.float32)))
-    X = sp.vstack(parts).tocsr()
+    jobs = [(S, effects, [covs[f"cov{i}"][a:min(n, a + block)] for i in range(n_cov)], seed,
+             a, min(n, a + block), programs) for a in range(0, n, block)]
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(min(16, os.cpu_count() or 1, len(jobs))) as pool:
+        parts = pool.map(_sim_part, jobs)
+    ptr = [np.zeros(1, dtype=np.int64)]
+    base = 0
+    for c, _, _ in parts:
+        ptr.append(c + base)
+        base += int(c[-1]) if c.size else 0
+    X = sp.csr_matrix((np.concatenate([p[2] for p in parts]),
+                       np.concatenate([p[1] for p in parts]), np.concatenate(ptr)), shape=(n, g))
     obs = pd.DataFrame({k: pd.Categorical([f"{k}_{v}" for v in val]) for k, val in covs.items()},
                        index=[f"c{i}" for i in range(n)])
     return AnnData(X=X, obs=obs, var=pd.DataFrame(index=[f"g{j}" for j in range(g)]))
