@@ -127,7 +127,7 @@ class Harmony:
         self.kmeans_rounds: list[int] = []
         self.verbose = verbose
         # fused HIP R-update (harmony.hip) needs each cell's batch index per covariate
-        self._native = (phi_n is not None and
+        self._native = (phi_n is not None and len(phi_n) <= 64 and
                         ops.harmony_native_ok(self.Phi, self.K, self.Phi.shape[0]))
         if self._native:
             offs = np.concatenate([[0], np.cumsum(phi_n)[:-1]]).astype(np.int64)
@@ -137,7 +137,7 @@ class Harmony:
             self._ws: dict = {}
             # fused distances need the centroid table in the assign kernel's LDS and the
             # centroid kernel's d x K outputs (harmony.hip)
-            self._fused = self.Z_orig.shape[0] * self.K <= ops._hip.harmony_centroid_max()
+            self._fused = ops.harmony_centroids_ok(self.Z_orig.shape[0], self.K)
             self.Zt = self.Z_cos.t().contiguous()              # cells x PCs
             self._obj = torch.zeros(2, dtype=dt, device=dev)    # round's assign sums
             self._obj_out = torch.zeros(1, dtype=dt, device=dev)

@@ -1690,6 +1690,12 @@ def harmony_block_update(Rt: torch.Tensor, distT: torch.Tensor | None, sigma: to
         _hip.harmony_block(op, *args)
 
 
+def harmony_centroids_ok(d: int, K: int) -> bool:
+    """True when the centroid kernel (and the fused-distance assign) take d PCs x K
+    clusters: one lane per PC, 4 x 8 MFMA tiles."""
+    return 1 <= d <= int(_hip.harmony_centroid_max_d()) and 1 <= K <= 128
+
+
 def harmony_centroids(Zt: torch.Tensor, Rt: torch.Tensor, ws: dict) -> torch.Tensor:
     """Y = Z_cos R^T (d, K) from the cell-major Zt (N, d) and Rt (N, K), float64, on the
     device in two deterministic stages (harmony.hip: chunked partials, per-output wave
@@ -1699,9 +1705,11 @@ def harmony_centroids(Zt: torch.Tensor, Rt: torch.Tensor, ws: dict) -> torch.Ten
     for name, t in (("Zt", Zt), ("Rt", Rt)):
         if t.dtype != torch.float64 or not t.is_contiguous() or t.shape[0] != N:
             raise ValueError(f"harmony_centroids: {name} contiguous float64 with N rows")
-    if d * K > _hip.harmony_centroid_max():
-        raise ValueError(f"harmony_centroids: d * K = {d * K} beyond the kernel's outputs")
-    chunk = max(64, -(-N // 512))
+    if not harmony_centroids_ok(d, K):
+        raise ValueError(f"harmony_centroids: d = {d}, K = {K} beyond the kernel's tiles")
+    # ~1024 workgroups (4 per CU), whole 4-cell MFMA steps
+    chunk = max(64, -(-N // 1024))
+    chunk = -(-chunk // 4) * 4
     n_wg = -(-N // chunk)
     need = n_wg * d * K
     if ws.get("cpart") is None or ws["cpart"].numel() < need:

@@ -393,7 +393,7 @@ PYBIND11_MODULE(_hip, m) {
                              reinterpret_cast<hipStream_t>(stream)),
           "harmony_block");
   });
-  m.def("harmony_centroid_max", []() { return cnmf_harmony_centroid_max(); });
+  m.def("harmony_centroid_max_d", []() { return cnmf_harmony_centroid_max_d(); });
   m.def("harmony_centroid", [](uintptr_t Zt, uintptr_t Rt, int N, int d, int K, int chunk,
                                uintptr_t part, uintptr_t Y, uintptr_t stream) {
     check(cnmf_harmony_centroid(P<const double>(Zt), P<const double>(Rt), N, d, K, chunk,

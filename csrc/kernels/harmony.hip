@@ -45,18 +45,31 @@ struct HarmonyParams {
   double* obj;           // [2] objective accumulators of the round (reduce kernel adds)
 };
 
+// lane l's value of a wave-uniform lane index, as a scalar (v_readlane)
+__device__ __forceinline__ int rl_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ double rl_d(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ double wave_max_d(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
   return v;
 }
 
-// LDS doubles of a W-wave block kernel: W O-tables, the penalty table (assign), W K-sums,
-// and (fused-distance assign) the d x K centroids and W x 2 objective sums
+// LDS doubles of a W-wave block kernel: W O-tables, the penalty table (assign), W K-sums
+// (rounded up to an even count), and (fused-distance assign) the centroids as
+// [PC, padded to 8][lane][2] -- lane l's clusters l and l + 64 side by side, one 16-byte
+// read per PC -- and W x 2 objective sums
+__host__ __device__ constexpr long long harmony_sy_offset(int W, int K, int B, bool assign) {
+  return ((long long)W * K * B + (assign ? (long long)K * B : 0) + (long long)W * K + 1) / 2 * 2;
+}
 __host__ __device__ constexpr long long harmony_lds_doubles(int W, int K, int B, bool assign,
                                                             int d = 0) {
-  return (long long)W * K * B + (assign ? (long long)K * B : 0) + (long long)W * K +
-         (assign ? (long long)d * K + 2LL * W : 0);
+  return harmony_sy_offset(W, K, B, assign) +
+         (assign && d > 0 ? (long long)(d + 7) / 8 * 8 * 128 + 2LL * W : 0);
 }
 
 template <bool ASSIGN>
@@ -67,14 +80,18 @@ __global__ void __launch_bounds__(4 * kHarmLanes) harmony_block_kernel(HarmonyPa
   double* o_w = hsm + (long long)wave * KB;          // this wave's O table, [b][k]
   double* spen = hsm + (long long)W * KB;            // penalty table (assign)
   double* ksum = spen + (ASSIGN ? KB : 0);           // [W][K] cluster sums
-  double* sY = ksum + (long long)W * K;              // [d][K] centroids (fused distance)
-  double* sobj = sY + (ASSIGN && !p.distT ? (long long)p.d * K : 0);   // [W][2]
   const bool fused = ASSIGN && p.distT == nullptr;
+  const int dpad = (p.d + 7) / 8 * 8;
+  double* sY = hsm + harmony_sy_offset(W, K, B, ASSIGN);   // [dpad][64][2] (fused distance)
+  double* sobj = sY + (fused ? (long long)dpad * 128 : 0);  // [W][2]
   for (int e = threadIdx.x; e < W * KB; e += blockDim.x) hsm[e] = 0.0;
   if (ASSIGN)
     for (int e = threadIdx.x; e < KB; e += blockDim.x) spen[e] = p.Pen[e];
   if (fused)
-    for (int e = threadIdx.x; e < p.d * K; e += blockDim.x) sY[e] = p.Y[e];
+    for (int e = threadIdx.x; e < dpad * 128; e += blockDim.x) {
+      const int dd = e >> 7, l = (e & 127) >> 1, k = l + 64 * (e & 1);
+      sY[e] = (dd < p.d && k < K) ? p.Y[(long long)dd * K + k] : 0.0;
+    }
   __syncthreads();
   double okm = 0.0, oent = 0.0;     // this lane's sum R dist and sum sigma R log R
   double isig[kHarmKPL];
@@ -84,24 +101,54 @@ __global__ void __launch_bounds__(4 * kHarmLanes) harmony_block_kernel(HarmonyPa
     isig[j] = (ASSIGN && k < K) ? 1.0 / p.sigma[k] : 0.0;
   }
   double s[kHarmKPL] = {0.0, 0.0};
+  double sg[kHarmKPL];
+#pragma unroll
+  for (int j = 0; j < kHarmKPL; ++j) {
+    const int k = lane + kHarmLanes * j;
+    sg[j] = (ASSIGN && k < K) ? p.sigma[k] : 0.0;
+  }
   const int i0 = blockIdx.x * p.chunk, i1 = min(p.nb, i0 + p.chunk);
+  // a cell's per-cell operands are fetched by the wave as ONE vector load each (lane v:
+  // its batch index of covariate v; lane dd: its PC dd) and handed out with v_readlane --
+  // the first version read them word by word in the loops, a dependent global load per
+  // PC: ~300 us per 25k-cell block (profiles/r5j_*).  The next cell's loads are issued
+  // before the current cell is processed.
+  int n_nx = i0 + wave < i1 ? p.cells[i0 + wave] : 0;
+  int bl_nx = 0;
+  double zl_nx = 0.0;
+  if (i0 + wave < i1) {
+    if (lane < p.nvar) bl_nx = p.bidx[(long long)lane * p.N + n_nx];
+    if (fused && lane < p.d) zl_nx = p.Zt[(long long)n_nx * p.d + lane];
+  }
   for (int i = i0 + wave; i < i1; i += W) {
-    const int n = p.cells[i];
+    const int n = n_nx;
+    const int bl = bl_nx;
+    const double zl = zl_nx;
+    if (i + W < i1) {
+      n_nx = p.cells[i + W];
+      if (lane < p.nvar) bl_nx = p.bidx[(long long)lane * p.N + n_nx];
+      if (fused && lane < p.d) zl_nx = p.Zt[(long long)n_nx * p.d + lane];
+    }
     double* rr = p.Rt + (long long)n * K;
     double r[kHarmKPL];
     if (ASSIGN) {
       // dist[n, k] = 2 (1 - Y_k . z_n): read, or formed here from the centroids in LDS
-      // and the cell's PCs (every lane reads the same z_n word: one broadcast load)
+      // and the cell's PCs
       double dk[kHarmKPL];
       if (fused) {
         double dot[kHarmKPL] = {0.0, 0.0};
-        const double* z = p.Zt + (long long)n * p.d;
-        for (int dd = 0; dd < p.d; ++dd) {
-          const double zv = z[dd];
+        // 8 PCs per step: 8 independent 16-byte LDS reads, then the FMAs (zero padding
+        // beyond d on both sides)
+        for (int d0 = 0; d0 < dpad; d0 += 8) {
+          double2 y[8];
 #pragma unroll
-          for (int j = 0; j < kHarmKPL; ++j) {
-            const int k = lane + kHarmLanes * j;
-            if (k < K) dot[j] = fma(sY[dd * K + k], zv, dot[j]);
+          for (int u = 0; u < 8; ++u)
+            y[u] = *reinterpret_cast<const double2*>(sY + (long long)(d0 + u) * 128 + 2 * lane);
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const double zv = rl_d(zl, d0 + u);
+            dot[0] = fma(y[u].x, zv, dot[0]);
+            dot[1] = fma(y[u].y, zv, dot[1]);
           }
         }
 #pragma unroll
@@ -129,7 +176,7 @@ __global__ void __launch_bounds__(4 * kHarmLanes) harmony_block_kernel(HarmonyPa
         const int k = lane + kHarmLanes * j;
         double pen = 0.0;
         if (k < K)
-          for (int v_ = 0; v_ < p.nvar; ++v_) pen += spen[k * B + p.bidx[(long long)v_ * p.N + n]];
+          for (int v_ = 0; v_ < p.nvar; ++v_) pen += spen[k * B + rl_i(bl, v_)];
         r[j] = k < K ? exp(sd[j] - mx) * pen : 0.0;
         tot += fabs(r[j]);
       }
@@ -144,7 +191,7 @@ __global__ void __launch_bounds__(4 * kHarmLanes) harmony_block_kernel(HarmonyPa
           // the round's objective terms of this cell (harmonypy compute_objective: the
           // k-means error and the entropy, both with the assignment just made)
           okm = fma(r[j], dk[j], okm);
-          if (r[j] > 0.0) oent = fma(p.sigma[k] * r[j], log(r[j]), oent);
+          if (r[j] > 0.0) oent = fma(sg[j] * r[j], log(r[j]), oent);
         }
       }
     } else {
@@ -159,7 +206,7 @@ __global__ void __launch_bounds__(4 * kHarmLanes) harmony_block_kernel(HarmonyPa
       const int k = lane + kHarmLanes * j;
       if (k < K) {
         s[j] += r[j];
-        for (int v_ = 0; v_ < p.nvar; ++v_) o_w[p.bidx[(long long)v_ * p.N + n] * K + k] += r[j];
+        for (int v_ = 0; v_ < p.nvar; ++v_) o_w[rl_i(bl, v_) * K + k] += r[j];
       }
     }
   }
@@ -244,48 +291,73 @@ __global__ void __launch_bounds__(256) harmony_reduce_kernel(HarmonyParams p, in
   if (pen) p.Pen[kb] = pow((ev + 1.0) / (ov + 1.0), p.theta[b]);
 }
 
-// Centroid product Y = Z_cos R^T (d x K) over all cells, in two deterministic stages:
-// workgroup g sums its chunk of cells into a partial (tiles of 32 cells staged in LDS,
-// thread t owns outputs t, t + 256, ...), then one wave per output sums the partials
-// lane-strided + xor tree.  (A library GEMM gives this long-reduction / small-output
-// product one output tile: one workgroup walking every cell.)
-constexpr int kHarmCenTile = 32;
-constexpr int kHarmCenMaxJ = 40;             // outputs per thread: d * K <= 10240
+// Centroid product Y = Z_cos R^T (d x K) over all cells, in two deterministic stages on
+// the f64 matrix cores: workgroup g sums its chunk of cells into a partial d x K block --
+// the cells are the MFMA reduction dimension, A = Zt rows (16 PCs x 4 cells), B = Rt rows
+// (4 cells x 16 clusters), both read straight from global memory (16 consecutive doubles
+// per lane group); wave w owns cluster tiles w and w + 4 for every PC tile (<= 8
+// accumulators) -- then one wave per output sums the partials lane-strided + xor tree.
+// (A library GEMM gives this long-reduction / small-output product one output tile: one
+// workgroup walking every cell; the scalar LDS version took 1.8 ms per call at 500k x 50
+// x 100, profiles/r5j_*.)
+typedef double hm_f64x4 __attribute__((ext_vector_type(4)));
+constexpr int kHarmCenMaxD = 64;             // 4 PC tiles
+constexpr int kHarmCenMaxK = 128;            // 8 cluster tiles = 2 per wave
 
 __global__ void __launch_bounds__(256) harmony_centroid_kernel(const double* __restrict__ Zt,
                                                                const double* __restrict__ Rt,
                                                                int N, int d, int K, int chunk,
                                                                double* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) double csm[];
-  double* sz = csm;                                  // [tile][d]
-  double* sr = csm + kHarmCenTile * d;               // [tile][K]
-  const int P = d * K, tid = threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int dT = (d + 15) >> 4, kT = (K + 15) >> 4;
   const int n0 = blockIdx.x * chunk, n1 = min(N, n0 + chunk);
-  double acc[kHarmCenMaxJ];
+  hm_f64x4 acc[4][2];
 #pragma unroll
-  for (int j = 0; j < kHarmCenMaxJ; ++j) acc[j] = 0.0;
-  for (int c0 = n0; c0 < n1; c0 += kHarmCenTile) {
-    const int tc = min(kHarmCenTile, n1 - c0);
-    for (int e = tid; e < tc * d; e += 256) sz[e] = Zt[(long long)c0 * d + e];
-    for (int e = tid; e < tc * K; e += 256) sr[e] = Rt[(long long)c0 * K + e];
-    __syncthreads();
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int j = 0; j < kHarmCenMaxJ; ++j) {
-      const int q = tid + 256 * j;
-      if (q < P) {
-        const int dd = q / K, k = q - dd * K;
-        double a = acc[j];
-        for (int c = 0; c < tc; ++c) a = fma(sz[c * d + dd], sr[c * K + k], a);
-        acc[j] = a;
+    for (int b = 0; b < 2; ++b) acc[a][b] = hm_f64x4{0.0, 0.0, 0.0, 0.0};
+  const int kt0 = wave, kt1 = wave + 4;
+  const bool has0 = kt0 < kT, has1 = kt1 < kT;          // wave-uniform
+  if (!has0) return;                                   // no LDS / barriers below
+  for (int c0 = n0; c0 < n1; c0 += 4) {
+    const int c = c0 + grp;
+    const bool ok = c < n1;
+    const double* zr = Zt + (long long)(ok ? c : 0) * d;
+    const double* rr = Rt + (long long)(ok ? c : 0) * K;
+    double av[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int dd = 16 * a + col;
+      av[a] = (ok && a < dT && dd < d) ? zr[dd] : 0.0;
+    }
+    const int k0 = 16 * kt0 + col, k1 = 16 * kt1 + col;
+    const double b0 = (ok && k0 < K) ? rr[k0] : 0.0;
+    const double b1 = (ok && has1 && k1 < K) ? rr[k1] : 0.0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      if (a < dT) {                                    // uniform
+        acc[a][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], b0, acc[a][0], 0, 0, 0);
+        if (has1) acc[a][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], b1, acc[a][1], 0, 0, 0);
       }
     }
-    __syncthreads();
   }
-  double* o = part + (long long)blockIdx.x * P;
+  // D (16 PCs x 16 clusters): col = cluster lane&15, row = PC (lane>>4) + 4 * reg
+  double* o = part + (long long)blockIdx.x * d * K;
 #pragma unroll
-  for (int j = 0; j < kHarmCenMaxJ; ++j) {
-    const int q = tid + 256 * j;
-    if (q < P) o[q] = acc[j];
+  for (int a = 0; a < 4; ++a) {
+    if (a >= dT) break;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int kt = b == 0 ? kt0 : kt1;
+      if (b == 1 && !has1) break;
+      const int k = 16 * kt + col;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int dd = 16 * a + grp + 4 * q;
+        if (dd < d && k < K) o[(long long)dd * K + k] = acc[a][b][q];
+      }
+    }
   }
 }
 
@@ -333,19 +405,17 @@ __global__ void __launch_bounds__(256) harmony_objective_kernel(const double* __
 }  // namespace cnmf
 
 extern "C" int cnmf_harmony_max_kb() { return cnmf::kHarmMaxKB; }
-extern "C" int cnmf_harmony_centroid_max() { return 256 * cnmf::kHarmCenMaxJ; }
+extern "C" int cnmf_harmony_centroid_max_d() { return cnmf::kHarmCenMaxD; }
 
 // Y (d x K) = Zt^T Rt over N cells; part needs ceil(N / chunk) * d * K doubles
 extern "C" hipError_t cnmf_harmony_centroid(const double* Zt, const double* Rt, int N, int d,
                                             int K, int chunk, double* part, double* Y,
                                             hipStream_t stream) {
   if (N <= 0) return hipSuccess;
-  if (d < 1 || K < 1 || (long long)d * K > 256LL * cnmf::kHarmCenMaxJ || chunk < 1)
+  if (d < 1 || K < 1 || d > cnmf::kHarmCenMaxD || K > cnmf::kHarmCenMaxK || chunk < 1)
     return hipErrorInvalidValue;
   const int n_wg = (N + chunk - 1) / chunk;
-  const size_t lds = (size_t)cnmf::kHarmCenTile * (d + K) * sizeof(double);
-  if (lds > 64 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(cnmf::harmony_centroid_kernel, dim3(n_wg), dim3(256), lds, stream, Zt, Rt, N,
+  hipLaunchKernelGGL(cnmf::harmony_centroid_kernel, dim3(n_wg), dim3(256), 0, stream, Zt, Rt, N,
                      d, K, chunk, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -378,7 +448,10 @@ extern "C" hipError_t cnmf_harmony_block(int op, double* Rt, const double* distT
   if (K < 1 || K > cnmf::kHarmLanes * cnmf::kHarmKPL || (long long)K * B > cnmf::kHarmMaxKB ||
       chunk < 1 || nvar < 1)
     return hipErrorInvalidValue;
-  if (op != 0 && !distT && (!Y || !Zt || d < 1)) return hipErrorInvalidValue;
+  // (one lane per covariate / per PC for the per-cell vector loads)
+  if (nvar > cnmf::kHarmLanes) return hipErrorInvalidValue;
+  if (op != 0 && !distT && (!Y || !Zt || d < 1 || d > cnmf::kHarmLanes))
+    return hipErrorInvalidValue;
   cnmf::HarmonyParams p{Rt, distT, sigma, cells, bidx, nb, N, K, B, nvar, chunk,
                         E, O, Pr_b, theta, Pen, part, Y, Zt, distT ? 0 : d, obj};
   const int n_wg = (nb + chunk - 1) / chunk;

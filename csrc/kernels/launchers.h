@@ -121,7 +121,7 @@ hipError_t cnmf_harmony_block(int op, double* Rt, const double* distT, const dou
                               int nvar, int chunk, double* E, double* O, const double* Pr_b,
                               const double* theta, double* Pen, double* part, const double* Y,
                               const double* Zt, int d, double* obj, hipStream_t stream);
-int cnmf_harmony_centroid_max();
+int cnmf_harmony_centroid_max_d();
 hipError_t cnmf_harmony_centroid(const double* Zt, const double* Rt, int N, int d, int K,
                                  int chunk, double* part, double* Y, hipStream_t stream);
 hipError_t cnmf_harmony_objective(const double* O, const double* E, const double* sigma,
