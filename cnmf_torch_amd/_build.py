@@ -27,7 +27,7 @@ CSRC = os.path.join(ROOT, "csrc")
 BUILD = os.path.join(ROOT, "build", "native")
 PKG = os.path.join(ROOT, "cnmf_torch_amd")
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-ARCH = os.environ.get("CNMF_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"       # MI355X (CDNA4) only
 
 HIP_OUT = os.path.join(PKG, "ops", "_hip" + EXT)
 H5_OUT = os.path.join(PKG, "utils", "_h5io" + EXT)

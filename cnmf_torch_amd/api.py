@@ -771,8 +771,7 @@ class cNMF:
 
         Worker 0 also starts the figure process (utils.plotting.prestart): it imports
         matplotlib in the background, so when combine / k_selection_plot / consensus run
-        in this same process their closed figures do not wait for that import
-        (CNMF_PLOT_PRESTART=0 turns this off)."""
+        in this same process their closed figures do not wait for that import."""
         if worker_i == 0:
             from .utils.plotting import prestart
 
@@ -890,14 +889,10 @@ class cNMF:
                 # measured SLOWER on the PBMC-scale grid -- factorize 350-456 vs 157-250
                 # ms, profiles/r2_early_write_probe.log: the writer threads take the CPU
                 # from the host enqueue -- so every file is written after its batch)
-                if len(set(ks)) == 1 and int(os.environ.get("CNMF_STREAMS", "1")) > 1:
-                    solver.opts.n_components = ks[0]
-                    res = solver.run_concurrent(seeds, n_streams=int(os.environ["CNMF_STREAMS"]))
-                else:
-                    # continuous batching when a K has more replicates than one co-resident
-                    # round of its usage solve holds (NMFBatchSolver.run_stream; else the
-                    # one-batch run): usages are only kept when they are saved
-                    res = solver.run_stream(seeds, ks=ks, keep_usages=save_usages)
+                # continuous batching when a K has more replicates than one co-resident
+                # round of its usage solve holds (NMFBatchSolver.run_stream; else the
+                # one-batch run): usages are only kept when they are saved
+                res = solver.run_stream(seeds, ks=ks, keep_usages=save_usages)
                 W = res.W.cpu().numpy()
                 wall = time.perf_counter() - t0
                 log.info("K=%s: %d replicates in %.3f s (%.1f replicates/s) on %s",

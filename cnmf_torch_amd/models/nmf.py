@@ -419,8 +419,8 @@ class _Batch:
         # the caller can persist them while the rest of the batch is still solving
         self.on_retire = None
         self.uid = next(_BATCH_UIDS)   # never reused (unlike id()): plane-cache keys
-        self.bucket = max(1, int(os.environ.get("CNMF_COMPACT_BUCKET",
-                                                "8" if W.device.type == "cuda" else "1")))
+        # compacted layouts are rounded to this many positions (fewer distinct graphs)
+        self.bucket = 8 if W.device.type == "cuda" else 1
         self.A = None   # flat per-position K*K sufficient statistics (online 'exact' mode)
         self.B = None   # (rows, G)
         self.feed = None          # _Feed of a streaming run (NMFBatchSolver.run_stream)
@@ -928,12 +928,9 @@ class _XPlanes:
         """B planes of non-count data: 2 (hi + mid, <= 2^-16 relative per element, the
         same bound the engine accepts for the A operand, ops.gemm_a_planes) once the
         numerator's reduction runs over >= 1024 genes -- inside the fp32 GEMM's own error
-        there (test_gemm_two_b_planes_within_fp32_library_error); else 3 (exact).
-        CNMF_GEMM_BPLANES=3 forces exact.  Two planes make a product 4 MFMAs instead of
-        5 (2 for counts) and halve nothing else."""
-        if G < 1024 or os.environ.get("CNMF_GEMM_BPLANES", "2") == "3":
-            return 3
-        return 2
+        there (test_gemm_two_b_planes_within_fp32_library_error); else 3 (exact).  Two
+        planes make a product 4 MFMAs instead of 5 (2 for counts) and halve nothing else."""
+        return 3 if G < 1024 else 2
 
     @staticmethod
     def build(X: torch.Tensor, stats=None, reserve: int = 0):
@@ -1018,14 +1015,13 @@ def native_rank(K: int) -> int:
     return -(-K // 16) * 16
 
 
-# first pass of a recurring batch layout from its captured graph (CNMF_LAYOUT_REPLAY=0:
-# eager) -- removes the ~330 us of host-paced idle of the compaction pass
-# (profiles/r3y_passes.txt), same-box bench within noise either way
-_LAYOUT_REPLAY = os.environ.get("CNMF_LAYOUT_REPLAY", "1") != "0"
+# first pass of a recurring batch layout from its captured graph (not eager) -- removes
+# the ~330 us of host-paced idle of the compaction pass (profiles/r3y_passes.txt)
+_LAYOUT_REPLAY = True
 # fused step: split-K GEMMs of up to this many k slices hand their raw slabs to the
 # consuming solve; deeper splits (the few-replicate tail) are reduced by the GEMM's own
-# pass -- the solve would read every slab per element (CNMF_FUSED_MAX_SLABS overrides)
-_FUSED_MAX_SLABS = int(os.environ.get("CNMF_FUSED_MAX_SLABS", "4"))
+# pass -- the solve would read every slab per element
+_FUSED_MAX_SLABS = 4
 
 
 def _graphs_enabled(X: torch.Tensor) -> bool:
@@ -1260,19 +1256,16 @@ class NMFBatchSolver:
         replicates run close to online_max_pass (mean 16.8 of 20 passes at K = 20), so
         the batch's tail is short -- measured (profiles/r5e_*): K = 20 streamed 4,928
         (80 slots) / 5,275 (100) vs 5,742 rep/s as one batch; K = 10: 17,570 streamed vs
-        14,071.  ``CNMF_STREAM_LIVE`` caps every K's slots (and streams any K)."""
+        14,071.  (run_stream's ``live`` sets the slots explicitly, any K.)"""
         ks = np.asarray(ks, dtype=np.int64)
         N = self.X.shape[0]
         cw = min(N, max(1, int(self.opts.online_chunk_size)))
-        cap_env = int(os.environ.get("CNMF_STREAM_LIVE", "0") or 0)
         out = {}
         for K, cnt in zip(*np.unique(ks, return_counts=True)):
-            if K > 16 and cap_env <= 0:
+            if K > 16:
                 out[int(K)] = int(cnt)
                 continue
             m = ops.pipe_round_reps(cw, int(K), self.X.device)
-            if cap_env > 0:
-                m = min(m, cap_env) if m > 0 else cap_env
             out[int(K)] = int(min(cnt, m)) if m > 0 else int(cnt)
         return out
 
@@ -1283,8 +1276,7 @@ class NMFBatchSolver:
                 and o.online_stats == "pass" and o.online_inner_conv == "loss"
                 and o.init == "random" and not self.comm.is_distributed
                 and all(v == 0.0 for v in (o.l1_H, o.l2_H, o.l1_W, o.l2_W))
-                and int(np.max(ks)) <= 32 and not ops.eager_active()
-                and os.environ.get("CNMF_STREAM", "1") != "0")
+                and int(np.max(ks)) <= 32 and not ops.eager_active())
 
     def run_stream(self, seeds, ks=None, live=None, keep_usages: bool = True,
                    on_result=None) -> NMFResult:
@@ -1501,7 +1493,7 @@ class NMFBatchSolver:
         Measured on the bench shape (100 replicates, 10k x 2k, K=10) this is SLOWER than
         one stream (2 streams 34 ms, 3: 40 ms, 4: 70 ms vs 19.9 ms): the halved coop
         budget lengthens the tail solves and the host threads contend for the GIL.  Kept
-        opt-in (bench --streams, CNMF_STREAMS) for shapes with few, long passes."""
+        opt-in (bench --streams) for shapes with few, long passes."""
         seeds = list(seeds)
         if (self.X.device.type != "cuda" or n_streams <= 1 or self.comm.is_distributed
                 or len(seeds) < n_streams * min_group):
@@ -2572,17 +2564,15 @@ class NMFBatchSolver:
         a per-gene std (X == C u_g, _count_units), and counts <= 2048 are exact in fp16.
         Half the bytes of the per-step X re-reads that bound those kernels
         (profiles/r3m_*), and xth replaces the fp32 X^T copy.  None for other data, the
-        sparse path, or CNMF_KL_FP16_COUNTS=0.  Default 'w': the spectra side reads the
-        fp16 counts and the usage side fp32 X -- on the usage side the fp16 -> fp32
-        conversion costs more issue than the halved bytes save (326-329 vs 314-317 rep/s
-        with both sides, profiles/r3v_*, r3w_*); '1' uses them on both sides."""
+        sparse path.  Only the spectra side reads the fp16 counts, the usage side fp32 X
+        -- on the usage side the fp16 -> fp32 conversion costs more issue than the halved
+        bytes save (326-329 vs 314-317 rep/s with both sides, profiles/r3v_*, r3w_*)."""
         if "_klc" in self.__dict__:
             return self._klc
         res = None
         X = self.X
         if (self.beta == 1.0 and isinstance(X, torch.Tensor) and X.device.type == "cuda"
                 and X.dtype == torch.float32 and ops.use_native(X)
-                and os.environ.get("CNMF_KL_FP16_COUNTS", "w") != "0"
                 and self._kl_sparse() is None):
             unit = _count_units(X, self._colstats)
             if unit is not None:
@@ -2635,18 +2625,15 @@ class NMFBatchSolver:
             cache[key] = float(xc.sum(dtype=torch.float64))
         return cache[key]
 
-    def _beta_panels(self, F3: torch.Tensor, usage_side: bool = False):
+    def _beta_panels(self, F3: torch.Tensor):
         """Kernel operand of a factor that stays fixed over the next kernel launches: its
         split-bf16 panels, or its padded transpose for the sparse KL kernels (GPU only; the
-        CPU reference works on the fp32 factor directly).  ``usage_side``: the spectra as
-        the usage solve's streamed operand -- with fp16 counts its P panel is S / unit."""
+        CPU reference works on the fp32 factor directly)."""
         if F3.device.type != "cuda":
             return None
         if self._kl_sparse() is not None:
             return ops.kl_st(F3)
-        klc = self._kl_counts() if (usage_side and
-                                    os.environ.get("CNMF_KL_FP16_COUNTS", "w") != "w") else None
-        return ops.beta_panels(F3, self.beta, row_scale=klc[3] if klc is not None else None)
+        return ops.beta_panels(F3, self.beta)
 
     def _beta_h_update(self, xc, H3c, W3, l1, l2, act=None, panels=None, rows=None):
         """One fused MU step of the usages H3c (R, K, c) in place against W3 on rows xc
@@ -2676,12 +2663,9 @@ class NMFBatchSolver:
         den_vec = (W3.sum(dim=2, dtype=torch.float32).contiguous()
                    if self.beta == 1.0 and cuda else None)
         csr = self._kl_sparse() if (cuda and rows is not None) else None
-        klc = self._kl_counts() if (cuda and rows is not None and csr is None
-                                    and os.environ.get("CNMF_KL_FP16_COUNTS", "w") != "w") \
-            else None
+        klc = None      # the usage side reads fp32 X (see _kl_counts)
         if cuda and wpan is None:
-            wpan = ops.kl_st(W3) if csr is not None else ops.beta_panels(
-                W3, self.beta, row_scale=klc[3] if klc is not None else None)
+            wpan = ops.kl_st(W3) if csr is not None else ops.beta_panels(W3, self.beta)
         cmode = 1 if o.online_inner_conv == "loss" else 0
         per = max(1, int(o.inner_check_every)) if cmode == 1 else 1
         group = 1 if cmode == 1 else block
@@ -2869,7 +2853,7 @@ class NMFBatchSolver:
             keep_d = keep.view(n, 1) if kl else keep
             for blocks in steps:
                 # W is fixed over this step's usage solves
-                wpan = self._beta_panels(W3, usage_side=True)
+                wpan = self._beta_panels(W3)
                 for (a, b) in blocks:
                     if b <= a:
                         continue

@@ -53,9 +53,8 @@ def _require_native():
 
 # Per-op debug / tuning knobs, read ONCE (at import, or by refresh_env()): every op
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
-_ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_MFMA", "CNMF_SOLVE_COOP", "CNMF_GEMM_APLANES",
-             "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT", "CNMF_GEMM_STAGES", "CNMF_GEMM_BK",
-             "CNMF_GEMM_SMALL", "CNMF_SOLVE_PIPE", "CNMF_WIDE_SOLVE")
+_ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_COOP", "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT",
+             "CNMF_GEMM_STAGES", "CNMF_GEMM_BK", "CNMF_SOLVE_PIPE")
 _ENV: dict = {}
 
 
@@ -262,11 +261,9 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     rpl = 0
     pipe_ok = (a == 0 and conv_mode == 1 and nsplit <= 1 and not (l1_num or l1_den or l2)
                and _ENV["CNMF_SOLVE_PIPE"] != "0" and h.solve_pipe_k(K))
-    if variant in ("auto", "mfma") and a == 0 and h.solve_mfma_max_cols(K) > 0 \
-            and (_ENV["CNMF_SOLVE_MFMA"] or "1") != "0":
+    if variant in ("auto", "mfma") and a == 0 and h.solve_mfma_max_cols(K) > 0:
         S = _mfma_split(n, nblocks, K, nsplit, coop, x.device)
-    if S is None and pipe_ok and variant in ("auto", "mfma") \
-            and (_ENV["CNMF_SOLVE_MFMA"] or "1") != "0":
+    if S is None and pipe_ok and variant in ("auto", "mfma"):
         # the pipelined kernel alone (K > 16, or K <= 16 when every replicate's slices
         # do not fit at once): co-resident rounds of `rpl` replicates
         plan = _pipe_plan(n, nblocks, K, coop, x.device)
@@ -292,8 +289,6 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                          f"with {nblocks} replicates")
     else:
         vcode = {"auto": 0, "stream": 1, "reg": 2}[variant]
-        if K > 64 and _ENV["CNMF_WIDE_SOLVE"] == "fp32":
-            vcode = 1      # the wide solve's fp32-MFMA Gram apply (default: split bf16)
         S = 1
         if nsplit <= 1:
             S = _coop_split(n, nblocks, x.device) if coop == "auto" else max(1, int(coop))
@@ -355,14 +350,15 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     return int(S)
 
 
-# Diagnostic phase stamps of the pipelined solve (CNMF_PIPE_STAMPS=1; tools/pipe_stamp_probe.py):
-# every launch gets a fresh buffer, kept with its (K, slices) in STAMP_LOG for the probe.
+# Diagnostic phase stamps of the pipelined solve (tools/pipe_stamp_probe.py sets
+# STAMPS_ON with an extension built with CNMF_PIPE_STAMPS_BUILD=1): every launch gets a
+# fresh buffer, kept with its (K, slices) in STAMP_LOG for the probe.
 STAMP_LOG: list = []
+STAMPS_ON = False
 
 
 def _stamp_buffer(vcode, rpl, nblocks, S, K, x) -> int:
-    if os.environ.get("CNMF_PIPE_STAMPS") != "1" or vcode != 3 or \
-            torch.cuda.is_current_stream_capturing():
+    if not STAMPS_ON or vcode != 3 or torch.cuda.is_current_stream_capturing():
         return 0
     wgs = (rpl if rpl else nblocks) * max(1, int(S))
     buf = torch.zeros(wgs * 10, dtype=torch.int64, device=x.device)
@@ -496,8 +492,7 @@ def pipe_slices(n: int, nblocks: int, K: int, dev: torch.device) -> int | None:
     """The slice count S an unregularised block-objective MU solve of ``nblocks``
     replicates x ``n`` columns runs at under coop="auto" on the pipelined kernel (as
     ops.solve picks it), or None when that kernel does not take it."""
-    if _hip is None or not _hip.solve_pipe_k(K) or _ENV["CNMF_SOLVE_PIPE"] == "0" \
-            or (_ENV["CNMF_SOLVE_MFMA"] or "1") == "0":
+    if _hip is None or not _hip.solve_pipe_k(K) or _ENV["CNMF_SOLVE_PIPE"] == "0":
         return None
     S = _mfma_split(n, nblocks, K, 1, "auto", dev) if _hip.solve_mfma_max_cols(K) > 0 else None
     if S is None:
@@ -531,12 +526,7 @@ def pipe_round_reps(n: int, K: int, dev: torch.device) -> int:
 # With the single-round XCD order and the LDS-staged Grams, 17 <= K <= 32 prefers 320:
 # K=20 5,601 / 5,606 vs 5,253 / 5,455 at 384, K=30 3,767 / 3,772 vs 3,760 / 3,762
 # (profiles/r4zi_*)
-_PIPE_SLICE_COLS_ENV = os.environ.get("CNMF_PIPE_SLICE_COLS")
-
-
 def _pipe_slice_cols(K: int) -> int:
-    if _PIPE_SLICE_COLS_ENV:
-        return int(_PIPE_SLICE_COLS_ENV)
     return 320 if 16 < K <= 32 else 384
 
 
@@ -1403,7 +1393,7 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
 
 _GRAM_WS: dict = {}
 # replicate count from which one workgroup per replicate fills the chip (no column split)
-_GRAM_SPLIT_MIN_R = int(os.environ.get("CNMF_GRAM_SPLIT_MIN_R", "64"))
+_GRAM_SPLIT_MIN_R = 64
 _gram_op = gram    # ops.solve's `gram` argument shadows the function there
 
 
@@ -1778,13 +1768,8 @@ def gemm_a_planes(Kd: int) -> int:
     representation error <= 2^-16 relative) once Kd >= 1024 -- that bound is inside the
     fp32 GEMM's own n * 2^-24 bound from n = 256 on, and from ~1000 on the measured error
     is also below the fp32 library GEMM's (test_gemm_two_a_planes_within_fp32_library_error)
-    -- else 3 (exact).  CNMF_GEMM_APLANES=3 forces exact."""
-    if Kd < 1024 or (_ENV["CNMF_GEMM_APLANES"] or "2") == "3":
-        return 3
-    return 2
-
-
-_GEMM_WAVE_PLAN = os.environ.get("CNMF_GEMM_WAVE_PLAN", "1") != "0"
+    -- else 3 (exact)."""
+    return 3 if Kd < 1024 else 2
 
 
 def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
@@ -1811,8 +1796,8 @@ def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
     elif tiles(3) >= 2 * cus:
         # 64 x 128 tiles as 4 waves of 32 x 64 (variant 4): twice the waves per output to
         # hide LDS / barrier latency -- K=10 numerator 63.4 -> 60.1 us in the bench
-        # (profiles/r2_gemm_small_tile_sweep.log); CNMF_GEMM_SMALL=3: 2 waves of 64 x 64
-        v = 3 if (_ENV["CNMF_GEMM_SMALL"] or "4") == "3" else 4
+        # (profiles/r2_gemm_small_tile_sweep.log; 2 waves of 64 x 64, variant 3, lost)
+        v = 4
     elif M > 128:
         v = 1
     else:
@@ -1820,7 +1805,7 @@ def gemm_plan(M: int, N: int, Kd: int, pb: int) -> tuple[int, int]:
     ksplit = 1
     if k_env is not None:
         ksplit = int(k_env)
-    elif v_env is None and 1024 < M <= 4096 and _GEMM_WAVE_PLAN:
+    elif v_env is None and 1024 < M <= 4096:
         # K x replicates in (1024, 4096] (K = 11..40 at 100 replicates): 128 x 256 tiles
         # with the k split that best fills whole waves of CUs -- cost ~ ceil(units / CUs)
         # / ksplit per unit of work + 0.13 per extra split (slab traffic).  Measured

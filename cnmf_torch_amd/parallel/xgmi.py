@@ -11,7 +11,7 @@ crosses one link once, all 7 links at the same time, with one flag handshake per
 The sum is in rank order on every rank, so all ranks hold bitwise identical results.
 
 Opt in with ``CNMF_ALLREDUCE=xgmi`` (``DistComm`` then routes float32 device buffers of
-up to ``CNMF_XGMI_CAP`` floats here and everything else to RCCL).  All ranks must be on
+up to ``cap`` floats here and everything else to RCCL).  All ranks must be on
 one node, each on its own GPU -- or, for tests, several processes on one GPU.  A peer that
 never arrives raises the kernel's timeout flag instead of hanging the GPU;
 :meth:`XgmiAllReduce.check` turns that into an exception.
@@ -65,12 +65,11 @@ class XgmiAllReduce:
             raise ValueError(f"xgmi all-reduce handles up to {hip.xgmi_max_ranks()} ranks")
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
-        cap = int(cap if cap is not None else os.environ.get("CNMF_XGMI_CAP", DEFAULT_CAP))
+        cap = int(cap if cap is not None else DEFAULT_CAP)
         self.cap = -(-cap // 4) * 4
         self.blocks = int(blocks or min(hip.xgmi_max_blocks(),
                                         max(1, hip.cu_count(self.device.index or 0) // 2)))
-        ms = int(timeout_ms if timeout_ms is not None
-                 else os.environ.get("CNMF_XGMI_TIMEOUT_MS", DEFAULT_TIMEOUT_MS))
+        ms = int(timeout_ms if timeout_ms is not None else DEFAULT_TIMEOUT_MS)
         self.limit = int(hip.xgmi_wall_clock_khz(self.device.index or 0)) * max(1, ms)
         # Workspace memory: uncached (or fine-grained) device memory, never coarse-grained
         # hipMalloc -- peers hand data over INSIDE a kernel, across GPUs, and only those

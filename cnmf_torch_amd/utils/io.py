@@ -79,11 +79,11 @@ def _plain_values(df: pd.DataFrame) -> np.ndarray:
     return vals
 
 
-NPZ_COMPRESSLEVEL = int(os.environ.get("CNMF_NPZ_LEVEL", "1"))
+NPZ_COMPRESSLEVEL = 1
 # Intermediate files under cnmf_tmp/ that only this pipeline re-reads (per-replicate and
 # merged spectra): stored uncompressed by default -- float64 spectra barely deflate and
 # zlib dominated combine.  Still a standard .npz that np.load reads.
-NPZ_TMP_LEVEL = int(os.environ.get("CNMF_NPZ_TMP_LEVEL", "0"))
+NPZ_TMP_LEVEL = 0
 
 
 def _savez_deflate(path: str, arrays: dict, level: int) -> None:

@@ -293,8 +293,8 @@ class _PlotProc:
 
 def prestart() -> None:
     """Start the shared figure process now (it imports matplotlib while the caller
-    computes), unless this process already imported pyplot or CNMF_PLOT_PRESTART=0."""
-    if os.environ.get("CNMF_PLOT_PRESTART", "1") == "0" or "matplotlib.pyplot" in sys.modules:
+    computes), unless this process already imported pyplot."""
+    if "matplotlib.pyplot" in sys.modules:
         return
     try:
         _PlotProc.get()

@@ -30,8 +30,7 @@ def _pool():
 
 def to_host(t: torch.Tensor, chunk_bytes: int = 128 << 20) -> np.ndarray:
     """``t.cpu().numpy()`` for a (large) device tensor, through pinned staging buffers."""
-    if not t.is_cuda or t.numel() * t.element_size() < _MIN_BYTES or \
-            os.environ.get("CNMF_PINNED_D2H", "1") == "0":
+    if not t.is_cuda or t.numel() * t.element_size() < _MIN_BYTES:
         return t.detach().cpu().numpy()
     t = t.detach().contiguous()
     flat = t.view(-1)

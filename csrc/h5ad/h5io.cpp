@@ -269,11 +269,7 @@ constexpr size_t kRawPiece = size_t(32) << 20;
 
 // (buffered writes to one file serialise on its inode lock: a few threads only keep the
 // page-cache copy going while another waits; reads scale with threads)
-int raw_threads(bool write) {
-  const char* e = getenv("CNMF_H5_IO_THREADS");
-  int n = e && *e ? atoi(e) : (write ? 4 : 8);
-  return std::max(1, std::min(n, 32));
-}
+int raw_threads(bool write) { return write ? 4 : 8; }
 
 // pread / pwrite of [0, nbytes) of buf at file offset off, in pieces over threads
 bool raw_io(const std::string& path, bool write, haddr_t off, char* buf, size_t nbytes) {

@@ -788,20 +788,8 @@ hipError_t bp_launch_occ(const BpParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-// CNMF_BP_OCC=3: the KL usage-side kernels at three waves per SIMD (A/B knob)
-inline int bp_occ() {
-  static const int v = [] {
-    const char* e = getenv("CNMF_BP_OCC");
-    return (e && e[0] == '3') ? 3 : 2;
-  }();
-  return v;
-}
-
 template <int NP, int T, int MODE, bool UPD, bool XH = false, int CT = bp_ct(T)>
 hipError_t bp_launch(const BpParams& p, hipStream_t s) {
-  if constexpr (MODE == kBpKL && UPD && NP == 1 && T == 1) {
-    if (bp_occ() == 3) return bp_launch_occ<NP, T, MODE, UPD, XH, CT, 3>(p, s);
-  }
   // K > 32: two panel chunks (74-156 KB of LDS) already hold a CU per workgroup, so the
   // register budget of one wave per SIMD costs no occupancy (at two waves the usage-side
   // kernels spilled 300-1500 bytes per lane)

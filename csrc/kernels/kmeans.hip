@@ -43,9 +43,10 @@ __host__ __device__ constexpr int km_kps(int k) {
 }
 
 __host__ __device__ constexpr size_t km_lds_bytes(int k, int dp) {
-  return ((size_t)dp * km_kps(k) + (size_t)(k + 15) / 16 * 16 + (size_t)k * dp + k) *
+  return ((size_t)dp * km_kps(k) + (size_t)(k + 15) / 16 * 16 + (size_t)k * dp + k +
+          (size_t)(kKmThreads / 64) * dp) *
              sizeof(double) +
-         (2 * kKmThreads + 2 * (size_t)k) * sizeof(int);
+         (2 * kKmThreads + 2 * (size_t)k + kKmThreads / 64) * sizeof(int);
 }
 
 __device__ __forceinline__ void km_take(double v, int c, double& best, int& arg) {
@@ -67,10 +68,12 @@ __global__ void __launch_bounds__(kKmThreads)
   double* sCsq = sCt + (long long)DP * KPS; // KP squared norms (+inf for the padding)
   double* sAcc = sCsq + KP;                 // k * DP accumulator
   double* sCnt = sAcc + (long long)k * DP;  // k counts
-  int* sLab = reinterpret_cast<int*>(sCnt + k);   // 256 labels of the current round
+  double* sEdge = sCnt + k;                 // [wave][DP] first-run partials (phase B)
+  int* sLab = reinterpret_cast<int*>(sEdge + (kKmThreads / 64) * DP);   // 256 round labels
   int* sPerm = sLab + kKmThreads;                   // round's points grouped by label
   int* sHist = sPerm + kKmThreads;                  // k: points per label this round
   int* sOff = sHist + k;                            // k: exclusive prefix of sHist
+  int* sEdgeLab = sOff + k;                         // [wave] label of the first run
   const int r = blockIdx.y;
   const int n_init = gridDim.y;
   if (live != nullptr && live[r] == 0) return;    // frozen restart: partials unused
@@ -159,12 +162,16 @@ __global__ void __launch_bounds__(kKmThreads)
     __syncthreads();
     // ---- phase B: ordered accumulation (only when partial sums are wanted).  The
     // round's points are grouped by label with a stable counting sort (rank = earlier
-    // points with the same label: a broadcast LDS walk), then every thread owns
-    // (cluster, feature) pairs and sums its cluster's points in point order before one
-    // add into the accumulator -- all 256 threads busy and no chain of dependent LDS
-    // read-modify-writes (d threads walking 256 points serially took ~11 ms per Lloyd
-    // step at 500k x 50 x 100, profiles/r3ae_harmony_500k_kernel_summary.txt).
-    // Deterministic: fixed summation order for every (cluster, feature).
+    // points with the same label: a broadcast LDS walk); wave w then walks sorted
+    // positions [64 w, 64 w + 64) with one lane per coordinate -- coalesced row loads, 8
+    // in flight -- keeping a register running sum per run of equal labels.  Every run
+    // but the wave's first is a whole cluster of this round and is added to the
+    // accumulator directly (no other wave holds that cluster); the first runs may
+    // continue a run of the previous wave and are added after a barrier, in wave order.
+    // Deterministic: fixed summation order for every (cluster, feature).  (One thread per
+    // (cluster, feature) summing its points -- dependent gathered loads -- spent ~4 ms of
+    // a 5 ms step at 500k x 50 x 100 x 10 restarts, profiles/r5l_*; d threads walking all
+    // 256 points with LDS read-modify-writes took ~11 ms, profiles/r3ae_*.)
     if (psum != nullptr) {
       for (int c = tid; c < k; c += kKmThreads) sHist[c] = 0;
       __syncthreads();
@@ -185,15 +192,60 @@ __global__ void __launch_bounds__(kKmThreads)
       __syncthreads();
       if (lab >= 0) sPerm[sOff[lab] + rank] = tid;
       __syncthreads();
-      for (int w = tid; w < k * d; w += kKmThreads) {
-        const int c = w / d, j = w - c * d;
-        const int cnt = sHist[c];
-        if (cnt == 0) continue;
-        const int o = sOff[c];
+      const int nval = (int)min((long long)kKmThreads, (long long)n - p0);
+      const int q0 = 64 * wave, q1 = min(q0 + 64, nval);
+      const bool jok = lane < d;
+      double* edge = sEdge + wave * DP;
+      int elab = -1;
+      if (q0 < q1) {                                   // uniform
+        int cur = sLab[sPerm[q0]];
         double acc = 0.0;
-        for (int t = 0; t < cnt; ++t) acc += X[(p0 + sPerm[o + t]) * ldx + j];
-        sAcc[c * DP + j] += acc;
+        bool first = true;
+        for (int q = q0; q < q1; q += 8) {
+          double xv[8];
+          int lb[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int qq = q + u;
+            lb[u] = -2;
+            xv[u] = 0.0;
+            if (qq < q1) {
+              const int pp = sPerm[qq];
+              lb[u] = sLab[pp];
+              if (jok) xv[u] = X[(p0 + pp) * ldx + lane];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (lb[u] == -2) break;                    // uniform: past the range
+            if (lb[u] != cur) {                        // uniform: a run ends
+              if (first) {
+                if (jok) edge[lane] = acc;
+                elab = cur;
+                first = false;
+              } else if (jok) {
+                sAcc[cur * DP + lane] += acc;
+              }
+              cur = lb[u];
+              acc = 0.0;
+            }
+            acc += xv[u];
+          }
+        }
+        if (first) {
+          if (jok) edge[lane] = acc;
+          elab = cur;
+        } else if (jok) {
+          sAcc[cur * DP + lane] += acc;
+        }
       }
+      if (lane == 0) sEdgeLab[wave] = elab;
+      __syncthreads();
+      if (tid < d)
+        for (int w = 0; w < kKmThreads / 64; ++w) {
+          const int c = sEdgeLab[w];
+          if (c >= 0) sAcc[c * DP + tid] += sEdge[w * DP + tid];
+        }
       for (int c = tid; c < k; c += kKmThreads) sCnt[c] += (double)sHist[c];
     }
     __syncthreads();

@@ -309,7 +309,7 @@ static hipError_t launch_wmfma_kb(const SolveParams& p, int nblocks, hipStream_t
 }
 
 // bf16: the split-bf16 Gram apply (default); else the fp32-MFMA one (ops.solve
-// variant='stream' or CNMF_WIDE_SOLVE=fp32)
+// variant="stream")
 template <int K>
 static hipError_t launch_wmfma_k(const SolveParams& p, int nblocks, bool bf16, hipStream_t s) {
   return bf16 ? launch_wmfma_kb<K, true>(p, nblocks, s) : launch_wmfma_kb<K, false>(p, nblocks, s);

@@ -1,5 +1,5 @@
 """Phase breakdown of the pipelined MU solve (csrc/kernels/solve_pipe.h) from in-kernel
-s_memtime stamps (diagnostic only: CNMF_PIPE_STAMPS=1 gives each launch a stamp buffer
+s_memtime stamps (diagnostic only: ops.STAMPS_ON gives each launch a stamp buffer
 that nothing else reads).  Runs one bench-shaped factorisation (graphs off, so every pass
 is an eager, stamped launch) and prints, per K and side (slice count), the mean cycles per
 workgroup in: prologue (operand loads, slab / partial-Gram sums), the sweep loop minus
@@ -7,7 +7,7 @@ the objective checks, the checks (objective chain + block reduce + cooperative e
 and the epilogue (stores, planes, partial Gram), plus the launch span (first start to
 last end) against the mean workgroup time -- the load-imbalance tail.
 
-    CNMF_PIPE_STAMPS=1 CNMF_GRAPHS=0 python tools/pipe_stamp_probe.py --k 20
+    CNMF_GRAPHS=0 python tools/pipe_stamp_probe.py --k 20
 
 The stamps exist only in a probe build of the extension: build with
 ``CNMF_PIPE_STAMPS_BUILD=1 python -c "import cnmf_torch_amd._build as b; b.build_hip()"``
@@ -18,7 +18,6 @@ import json
 import os
 import sys
 
-os.environ.setdefault("CNMF_PIPE_STAMPS", "1")
 os.environ.setdefault("CNMF_GRAPHS", "0")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -26,6 +25,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from cnmf_torch_amd import ops  # noqa: E402
+
+ops.STAMPS_ON = True
 from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions  # noqa: E402
 from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix  # noqa: E402
 
