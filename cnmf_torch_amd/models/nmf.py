@@ -1832,34 +1832,80 @@ class NMFBatchSolver:
         if not S_h or not S_w:
             raise RuntimeError("DP fused step: no pipelined-solve slicing")
         f32 = dict(device=dev, dtype=torch.float32)
+        wpl_n = ops.gemm_a_planes(xp.Gp)
+        # ONE reduce-scatter per online step: rank r's chunk is [dB rows of its replicates
+        # | their per-slice partial H^T H], and ONE all-gather: rank r's chunk is [the
+        # spectra bf16 planes of its replicates | their W W^T partials | lin | quad] as
+        # bytes -- the W-solve writes its outputs straight into that chunk
+        n_db, n_hh = Rr * K * G, Rr * S_h * K * K
+        pl_b, ww_b = wpl_n * Rr * K * xp.Gp * 2, Rr * S_w * K * K * 4
+        n_ag = pl_b + ww_b + 8 * Rr
+        rs_own = torch.empty(n_db + n_hh, **f32)
+        ag_own = torch.zeros(n_ag, device=dev, dtype=torch.uint8)
         fb = {
             "K": K, "R": R, "Rr": Rr, "Rp": Rp, "own": (own0, own1), "S_h": S_h, "S_w": S_w,
+            "wpl_n": wpl_n,
             "wpl": torch.zeros((3, Rp * K, xp.Gp), device=dev, dtype=torch.int16),
             "hpl": torch.zeros((3, R * K, kd_max), device=dev, dtype=torch.int16),
             "slabN": torch.empty(ks_n * R * K * max(cws), **f32),
             "dB": torch.zeros((Rp * K, G), **f32),
-            "dB_own": torch.empty((Rr * K, G), **f32),
             "B_own": torch.empty((Rr * K, G), **f32),
             "A_own": [torch.empty((Rr, K, K), **f32) for _ in range(2)],
             "HHp": torch.zeros((Rp, S_h, K, K), **f32),
-            "HHp_own": torch.empty((Rr, S_h, K, K), **f32),
             "WWp": torch.zeros((Rp, S_w, K, K), **f32),
             "lin": torch.zeros(Rp, **f32), "quad": torch.zeros(Rp, **f32),
+            "rs": torch.empty((world, n_db + n_hh), **f32), "rs_own": rs_own,
+            "dB_own": rs_own[:n_db].view(Rr * K, G),
+            "HHp_own": rs_own[n_db:].view(Rr, S_h, K, K),
+            "ag": torch.empty((world, n_ag), device=dev, dtype=torch.uint8), "ag_own": ag_own,
+            "ag_pl": ag_own[:pl_b].view(torch.int16).view(wpl_n, Rr * K, xp.Gp),
+            "ag_wwp": ag_own[pl_b:pl_b + ww_b].view(torch.float32).view(Rr, S_w, K, K),
+            "ag_lin": ag_own[pl_b + ww_b:pl_b + ww_b + 4 * Rr].view(torch.float32),
+            "ag_quad": ag_own[pl_b + ww_b + 4 * Rr:].view(torch.float32),
+            "ag_offs": (pl_b, ww_b),
             "prepped": None,
         }
         return fb
+
+    @staticmethod
+    def _dp_pack_rs(fb: dict) -> None:
+        """[dB | HHp] of every replicate into the reduce-scatter buffer, rank-chunked."""
+        world, Rr, K = fb["rs"].shape[0], fb["Rr"], fb["K"]
+        n_db = fb["dB_own"].numel()
+        rs = fb["rs"]
+        rs[:, :n_db].copy_(fb["dB"].view(world, n_db))
+        rs[:, n_db:].copy_(fb["HHp"].view(world, -1))
+
+    @staticmethod
+    def _dp_unpack_ag(fb: dict, last: bool) -> None:
+        """Every rank's chunk of the all-gather into the full-batch planes, W W^T partials
+        and (last step) lin / quad."""
+        ag = fb["ag"]
+        world, Rr, K = ag.shape[0], fb["Rr"], fb["K"]
+        pl_b, ww_b = fb["ag_offs"]
+        wpl_n = fb["wpl_n"]
+        Gp = fb["wpl"].shape[2]
+        src = ag[:, :pl_b].view(torch.int16).view(world, wpl_n, Rr * K, Gp)
+        fb["wpl"][:wpl_n].view(wpl_n, world, Rr * K, Gp).copy_(src.transpose(0, 1))
+        fb["WWp"].view(world, -1).copy_(ag[:, pl_b:pl_b + ww_b].view(torch.float32))
+        if last:
+            o = pl_b + ww_b
+            fb["lin"].view(world, Rr).copy_(ag[:, o:o + 4 * Rr].view(torch.float32))
+            fb["quad"].view(world, Rr).copy_(ag[:, o + 4 * Rr:].view(torch.float32))
 
     def _fused_pass_dp(self, st: _Batch, steps, fb: dict, final: bool) -> None:
         """One online pass of the fused step on a cell shard (SURVEY.md §2.5c / §2.6 item
         1).  Per online step every rank runs the numerator GEMM and the pipelined H-solve
         on its cells of the global chunk and the statistics GEMM dB = H_loc^T X_loc; then
-        ONE reduce-scatter per buffer hands each rank the rank-summed dB and per-slice
-        partial Grams of ITS replicate chunk, the rank W-solves only those (1/world of the
-        spectra work), and all-gathers return their bf16 spectra planes, the per-slice
-        W W^T partials and (last step) lin/quad -- the bytes of one all-reduce of dB, with
-        the W-solve no longer replicated on every rank (the unfused DP step all-reduces
-        [dB | dA] and re-solves every replicate everywhere).  Same updates and stopping
-        rules as the single-GPU fused step; rank-summed statistics in RCCL's order."""
+        ONE reduce-scatter of the packed [dB | partial H^T H] hands each rank the
+        rank-summed statistics of ITS replicate chunk, the rank W-solves only those (1/world
+        of the spectra work) straight into its chunk of ONE all-gather of [bf16 spectra
+        planes | per-slice W W^T partials | lin | quad] -- two collectives per step (five
+        before the packing: dB, HHp, WWp and one per plane, +2 on the last step), the bytes
+        of one all-reduce of dB, the W-solve no longer replicated on every rank (the
+        unfused DP step all-reduces [dB | dA] and re-solves every replicate everywhere).
+        Same updates and stopping rules as the single-GPU fused step; rank-summed
+        statistics in RCCL's order."""
         o = self.opts
         comm = self.comm
         xp = self._planes()
@@ -1910,20 +1956,20 @@ class NMFBatchSolver:
             else:      # no cells of this chunk here: zero contributions
                 fb["dB"][:rows].zero_()
                 fb["HHp"][:R].zero_()
-            comm.reduce_scatter_(fb["dB_own"], fb["dB"])
-            comm.reduce_scatter_(fb["HHp_own"], fb["HHp"])
+            self._dp_pack_rs(fb)
+            comm.reduce_scatter_(fb["rs_own"], fb["rs"])
             A_in, A_out = fb["A_own"][(s_ + 1) % 2], fb["A_own"][s_ % 2]
-            wwp = fb["WWp"][comm.rank * Rr:(comm.rank + 1) * Rr]
+            wwp = fb["ag_wwp"]
             if n_own:
-                lin_o = fb["lin"][comm.rank * Rr:comm.rank * Rr + n_own]
-                quad_o = fb["quad"][comm.rank * Rr:comm.rank * Rr + n_own]
+                lin_o = fb["ag_lin"][:n_own]
+                quad_o = fb["ag_quad"][:n_own]
                 ops.solve(
                     "mu", Wown, fb["dB_own"][:n_own * K].view(n_own, K, G),
                     None if s_ == 0 else A_in[:n_own], max_iter=o.online_chunk_max_iter,
                     tol=o.online_w_tol, eps=o.eps, lin_out=lin_o if last else None,
                     quad_out=quad_o if last else None, iters_out=w_it[own0:own1],
                     conv_mode=1, check_every=o.inner_check_every, active=active[own0:own1],
-                    planes=wpl[:, o0:o1], planes_colmul=unit, planes_n=wpl_n,
+                    planes=fb["ag_pl"][:, :n_own * K], planes_colmul=unit, planes_n=wpl_n,
                     numer_scale=unit,
                     numer_base=None if s_ == 0 else fb["B_own"][:n_own * K].view(n_own, K, G),
                     numer_out=None if last else fb["B_own"][:n_own * K].view(n_own, K, G),
@@ -1931,12 +1977,8 @@ class NMFBatchSolver:
                     gram_out=None if last else A_out[:n_own],
                     gram_parts_out=wwp[:n_own], coop=S_w, coop_device_gen=True)
             fb["wwp_n"] = S_w
-            comm.all_gather_into_(fb["WWp"], wwp)
-            for pl in range(wpl_n):
-                comm.all_gather_into_(wpl[pl], wpl[pl, comm.rank * Rr * K:(comm.rank + 1) * Rr * K])
-            if last:
-                comm.all_gather_into_(fb["lin"], fb["lin"][comm.rank * Rr:(comm.rank + 1) * Rr])
-                comm.all_gather_into_(fb["quad"], fb["quad"][comm.rank * Rr:(comm.rank + 1) * Rr])
+            comm.all_gather_into_(fb["ag"], fb["ag_own"])
+            self._dp_unpack_ag(fb, last)
         ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
                         n, -1, o.tol, final=final, gate=st.gate,
                         max_pass=int(o.online_max_pass))

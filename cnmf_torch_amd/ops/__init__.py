@@ -164,7 +164,7 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
     ``variant``: "auto" runs MU with K <= 16 on the matrix-core kernel (solve_mfma.hip:
     Gram x on v_mfma_f32_16x16x4_f32, iterate in VGPRs) whenever its slices fit, else
     the VALU kernels ("stream" / "reg" force those; "mfma" forces the former).
-    ``planes`` (3, R*K, cols_pad) int16, optional: the kernel's epilogue also writes the
+    ``planes`` (>= planes_n, R*K, cols_pad) int16, optional: the kernel's epilogue also writes the
     final x (times ``planes_colmul`` per column) as exact bf16 planes -- the A operand of
     the next split-precision GEMM (ops.gemm_planes) -- zeroing columns [n, cols_pad).
     ``planes_n``: how many of the three planes to write (the GEMM reads only its
@@ -206,7 +206,8 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                         eps, lin_out, quad_out, iters_out, nsplit, conv_mode, check_every,
                         active)
         if planes is not None:
-            split_planes(x.reshape(R * K, n), planes, col_mul=planes_colmul)
+            split_planes(x.reshape(R * K, n), planes[:min(int(planes_n), planes.shape[0])],
+                         col_mul=planes_colmul)
         return 1
     h = _hip
     # a GPU operand the kernels do not cover is an error, never a silent eager fallback:
@@ -319,10 +320,12 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
         gen_dev = (0, 0)
     pl_ptr = pl_rs = pl_ld = pl_plane = pl_cols = 0
     if planes is not None:
-        if (planes.dtype != torch.int16 or planes.dim() != 3 or planes.shape[0] != 3
+        if (planes.dtype != torch.int16 or planes.dim() != 3
+                or planes.shape[0] < min(3, int(planes_n))
                 or planes.shape[1] < R * K or planes.stride(2) != 1 or planes.shape[2] < n
                 or planes.device != x.device):
-            raise ValueError("planes: int16 (3, >= R*K, >= n) with unit column stride")
+            raise ValueError("planes: int16 (>= planes_n, >= R*K, >= n) with unit column "
+                             "stride")
         if planes_colmul is not None and (planes_colmul.dtype != torch.float32
                                           or planes_colmul.numel() < n
                                           or not planes_colmul.is_contiguous()):

@@ -2,9 +2,12 @@
 
 ``LocalComm`` is the single-process no-op.  ``DistComm`` wraps a ``torch.distributed``
 process group: backend ``nccl`` (= RCCL on ROCm, over xGMI between the GPUs of a
-node) for device tensors, ``gloo`` for CPU tests.  The NMF solvers only ever issue
-*one fused all-reduce per online step* (the flat ``[B | A]`` sufficient-statistics
-buffer) plus a few scalars at init, so the interface is tiny.
+node) for device tensors, ``gloo`` for CPU tests; ``CNMF_ALLREDUCE=xgmi`` routes device
+all-reduce / reduce-scatter / all-gather calls to the one-shot peer-memory kernels
+(parallel/xgmi.py).  Per online step the cell-sharded solvers issue ONE collective of
+the flat ``[B | A]`` statistics (unfused step: all-reduce) or one packed reduce-scatter
+and one packed all-gather (fused step), SURVEY.md §2.6 item 1, plus a few scalars at
+init, so the interface is small.
 """
 from __future__ import annotations
 
@@ -85,10 +88,11 @@ class DistComm(LocalComm):
             return torch.device("cuda", torch.cuda.current_device())
         return torch.device("cpu")
 
-    def _xgmi_for(self, t: torch.Tensor):
-        """The one-shot xGMI reducer when it is enabled and takes ``t`` (float32 device
-        buffers up to its capacity; parallel/xgmi.py), else None.  Created collectively on
-        the first device all-reduce: every rank of a DP solve issues the same sequence."""
+    def _xgmi_for(self, t: torch.Tensor, any_dtype: bool = False):
+        """The one-shot xGMI collectives when they are enabled and take ``t`` (float32
+        device buffers up to its capacity -- any dtype for an all-gather, which moves bit
+        patterns; parallel/xgmi.py), else None.  Created collectively on the first device
+        collective: every rank of a DP solve issues the same sequence."""
         if t.device.type != "cuda":
             return None
         if self._xgmi is None:
@@ -102,7 +106,9 @@ class DistComm(LocalComm):
                     import warnings
 
                     warnings.warn(f"CNMF_ALLREDUCE=xgmi unavailable ({e}); using RCCL")
-        return self._xgmi if (self._xgmi and self._xgmi.supports(t)) else None
+        if not self._xgmi:
+            return None
+        return self._xgmi if (any_dtype or self._xgmi.supports(t)) else None
 
     def check(self) -> None:
         """Raise if a one-shot xGMI all-reduce gave up on a peer (host sync)."""
@@ -186,6 +192,9 @@ class DistComm(LocalComm):
         m = out.numel()
         if inp.numel() != m * self.world_size:
             raise ValueError(f"reduce_scatter_: {inp.numel()} != {self.world_size} x {m}")
+        xg = self._xgmi_for(inp)
+        if xg is not None and xg.reduce_scatter(out, inp):
+            return out
         if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():
             self._dist.reduce_scatter_tensor(out, inp, group=self.group)
             return out
@@ -201,6 +210,9 @@ class DistComm(LocalComm):
         m = inp.numel()
         if out.numel() != m * self.world_size:
             raise ValueError(f"all_gather_into_: {out.numel()} != {self.world_size} x {m}")
+        xg = self._xgmi_for(inp, any_dtype=True)
+        if xg is not None and xg.all_gather(out, inp):
+            return out
         if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():
             self._dist.all_gather_into_tensor(out, inp, group=self.group)
             return out
@@ -289,7 +301,15 @@ class EmulatedComm(LocalComm):
         self.rank = 0
         self.world_size = int(world)
         self.bytes = 0          # collective payload bytes issued (per rank)
+        # collective launches by kind, and per launch (kind, payload bytes) in order
+        self.calls = {"all_reduce": 0, "reduce_scatter": 0, "all_gather": 0}
+        self.log: list = []
         self._scratch = None
+
+    def _count(self, kind: str, nbytes: int) -> None:
+        self.calls[kind] += 1
+        self.bytes += nbytes
+        self.log.append((kind, int(nbytes)))
 
     @property
     def is_distributed(self) -> bool:
@@ -304,7 +324,7 @@ class EmulatedComm(LocalComm):
 
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
         self._copy(t)
-        self.bytes += t.numel() * t.element_size()
+        self._count("all_reduce", t.numel() * t.element_size())
         if t.is_floating_point():
             t.mul_(self.world_size)
         return t
@@ -313,14 +333,14 @@ class EmulatedComm(LocalComm):
         return float(v) * self.world_size
 
     def reduce_scatter_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
-        self.bytes += inp.numel() * inp.element_size()
+        self._count("reduce_scatter", inp.numel() * inp.element_size())
         out.copy_(inp.reshape(-1)[:out.numel()].view_as(out))
         out.mul_(self.world_size)
         return out
 
     def all_gather_into_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         m = inp.numel()
-        self.bytes += out.numel() * out.element_size()
+        self._count("all_gather", out.numel() * out.element_size())
         flat = out.reshape(-1)
         for r in range(self.world_size):
             flat[r * m:(r + 1) * m].copy_(inp.reshape(-1))

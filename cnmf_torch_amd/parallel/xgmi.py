@@ -106,7 +106,10 @@ class XgmiAllReduce:
                     peers.append(p)
         self.peers = torch.tensor(peers, dtype=torch.int64, device=self.device)
         self.timeout = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.epoch = 0
+        # the call counter lives on the device (advanced by each launch's last block), so
+        # the collectives replay correctly from a captured HIP graph
+        self.ep = torch.zeros(2, dtype=torch.int32, device=self.device)   # [epoch, arrivals]
+        self.epoch = 0          # host-side count of calls issued (diagnostics)
         self.closed = False
         # nobody's first flag store may land before every rank has mapped every workspace
         dist.barrier(group=group)
@@ -124,6 +127,29 @@ class XgmiAllReduce:
         return (not self.closed and t.device == self.device and t.dtype == torch.float32
                 and t.is_contiguous() and t.numel() <= self.cap)
 
+    @staticmethod
+    def _f32(t: torch.Tensor) -> torch.Tensor | None:
+        """A contiguous device buffer as float32 words (byte / int16 payloads of the DP
+        step travel as their bit patterns), or None."""
+        if not t.is_contiguous():
+            return None
+        if t.dtype == torch.float32:
+            return t.reshape(-1)
+        nb = t.numel() * t.element_size()
+        if nb % 4 or t.data_ptr() % 4:
+            return None
+        return t.reshape(-1).view(torch.uint8).view(torch.float32)
+
+    def _launch(self, mode: int, src: torch.Tensor, dst: torch.Tensor, m: int) -> None:
+        from ..ops import _stream_ptr
+
+        self.epoch += 1
+        e = self.ep
+        _hip().xgmi_collective(mode, self.peers.data_ptr(), self.world, self.rank,
+                               src.data_ptr(), dst.data_ptr(), int(m), self.cap, 0,
+                               e.data_ptr(), e.data_ptr() + 4, self.limit,
+                               self.timeout.data_ptr(), self.blocks, _stream_ptr(src))
+
     def __call__(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """Sum of ``t`` over the ranks into ``out`` (default: in place)."""
         if not self.supports(t):
@@ -132,13 +158,31 @@ class XgmiAllReduce:
         out = t if out is None else out
         if out.shape != t.shape or not self.supports(out):
             raise ValueError("xgmi all-reduce: out must match t")
-        self.epoch = (self.epoch + 1) & 0xFFFFFFFF     # compares are wrap-safe
-        from ..ops import _stream_ptr
-
-        _hip().xgmi_allreduce(self.peers.data_ptr(), self.world, self.rank, t.data_ptr(),
-                              out.data_ptr(), t.numel(), self.cap, self.epoch, self.limit,
-                              self.timeout.data_ptr(), self.blocks, _stream_ptr(t))
+        self._launch(0, t, out, t.numel())
         return out
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> bool:
+        """out = chunk ``rank`` of the rank-ordered sum of ``inp`` (world equal chunks,
+        rank-major): each rank reads only its chunk from every peer -- one hop per link.
+        float32 only (a sum).  Returns False when the buffers do not qualify."""
+        if self.closed or inp.dtype != torch.float32 or out.dtype != torch.float32 or \
+                inp.device != self.device or out.device != self.device or \
+                not (inp.is_contiguous() and out.is_contiguous()) or \
+                inp.numel() != out.numel() * self.world or inp.numel() > self.cap:
+            return False
+        self._launch(1, inp, out, out.numel())
+        return True
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> bool:
+        """out (world equal chunks, rank-major) = every rank's ``inp``; any dtype whose
+        buffers are whole 4-byte words.  Returns False when the buffers do not qualify."""
+        src, dst = self._f32(inp), self._f32(out)
+        if self.closed or src is None or dst is None or inp.device != self.device or \
+                out.device != self.device or dst.numel() != src.numel() * self.world or \
+                src.numel() > self.cap:
+            return False
+        self._launch(2, src, dst, src.numel())
+        return True
 
     def check(self) -> None:
         """Raise on EVERY rank if any call so far gave up waiting for a peer on ANY rank

@@ -528,4 +528,15 @@ PYBIND11_MODULE(_hip, m) {
                                     reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_xgmi_allreduce");
         });
+  m.def("xgmi_collective",
+        [](int mode, uintptr_t peers, int world, int rank, uintptr_t in, uintptr_t out,
+           long long m, long long cap, unsigned epoch, uintptr_t ep, uintptr_t arrive,
+           unsigned long long limit, uintptr_t timeout, int blocks, uintptr_t stream) {
+          check(cnmf_xgmi_collective(mode, P<const unsigned long long>(peers), world, rank,
+                                     P<const float>(in), P<float>(out), m, cap, epoch,
+                                     P<unsigned>(ep), P<unsigned>(arrive), limit,
+                                     P<int>(timeout), blocks,
+                                     reinterpret_cast<hipStream_t>(stream)),
+                "cnmf_xgmi_collective");
+        });
 }

@@ -103,19 +103,29 @@ __global__ void __launch_bounds__(kKmThreads)
     const long long p0 = base + (long long)round * kKmThreads;
     if (p0 >= n) break;                              // uniform across the workgroup
     // ---- phase A: assignment (MFMA scores)
+    // the wave's 4 point tiles are loaded up front (one wave per SIMD: the registers are
+    // there, and one memory round trip instead of one per tile)
+    double bxa[4][DP / 4];
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) {
+      const long long i = p0 + 64 * wave + 16 * pt + col;
+      const bool ok = i < n;
+      const double* xr = X + (ok ? i : 0) * ldx;
+#pragma unroll
+      for (int ks = 0; ks < DP / 4; ++ks) {
+        const int j = 4 * ks + grp;
+        bxa[pt][ks] = (ok && j < d) ? xr[j] : 0.0;
+      }
+    }
+#pragma unroll
     for (int pt = 0; pt < 4; ++pt) {
       const int slot = 64 * wave + 16 * pt + col;
       const long long i = p0 + slot;
       const bool ok = i < n;
-      const double* xr = X + (ok ? i : 0) * ldx;
-      double bx[DP / 4];
+      const double* bx = bxa[pt];
       double xsq = 0.0;
 #pragma unroll
-      for (int ks = 0; ks < DP / 4; ++ks) {
-        const int j = 4 * ks + grp;
-        bx[ks] = (ok && j < d) ? xr[j] : 0.0;
-        xsq = fma(bx[ks], bx[ks], xsq);
-      }
+      for (int ks = 0; ks < DP / 4; ++ks) xsq = fma(bx[ks], bx[ks], xsq);
       double best = INFINITY;
       int arg = 0x7fffffff;
       for (int ct = 0; ct < nct; ct += 2) {

@@ -213,5 +213,10 @@ hipError_t cnmf_xgmi_allreduce(const unsigned long long* peers, int world, int r
                                const float* in, float* out, long long n, long long cap,
                                unsigned epoch, unsigned long long limit, int* timeout,
                                int blocks, hipStream_t stream);
+hipError_t cnmf_xgmi_collective(int mode, const unsigned long long* peers, int world, int rank,
+                                const float* in, float* out, long long m, long long cap,
+                                unsigned epoch, unsigned* ep, unsigned* arrive,
+                                unsigned long long limit, int* timeout, int blocks,
+                                hipStream_t stream);
 
 }

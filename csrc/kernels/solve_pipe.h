@@ -36,19 +36,11 @@
 // from K = 17 on the matrix core has MB chains in flight even inside one tile.  fp32 MFMA
 // is exact fp32 (a k-ordered fmaf chain), so the solve is the fp32 MU step.
 //
-// Occupancy.  x lives in VGPRs (T * KS), the Gram fragments in VGPRs (MB * KS: 16 at
-// K = 32, 64 at K = 64), the numerators of the first TL = pipe_tile_lds(K) tiles in LDS
-// (TL * KS KB per workgroup) and those of tiles TL.. in VGPRs as well.  K <= 32: <= 128
-// VGPRs, <= 36 KB of LDS numerators, four 256-thread workgroups per CU; K in (32, 64]:
-// <= 256 VGPRs, <= 78 KB, two per CU (pipe_weu).  At 17 <= K <= 20 the eighth tile's
-// numerators are register-held (7 LDS tiles of KS = 5): 512 columns per workgroup, so the
-// usage-side solve of a 100-replicate batch at 5,000 cells fits ONE co-resident launch
-// round (1,000 of the 1,024 resident workgroups) where 448 columns took two, each as long
-// as its slowest replicate (profiles/r4i_k20_kernel_summary.txt: 2 x 86 us per pass).
-// Measured alternatives (-Rpass-analysis=kernel-resource-usage): two workgroups per CU
-// with 78 KB of LDS numerators spill from 14 tiles on and hold 768 columns (two rounds
-// again); register tiles at 21..24 spill 36-148 bytes per lane.  A replicate set whose slices still do not all fit at once is launched in
-// co-resident rounds by the host (cnmf_solve: reps_per_launch).
+// Occupancy.  x lives in VGPRs (T * KS), the numerators in LDS (T * KS KB per workgroup),
+// the Gram fragments in VGPRs (MB * KS: 16 at K = 32, 64 at K = 64).  K <= 32: <= 128
+// VGPRs, <= 36 KB of numerators, four 256-thread workgroups per CU; K in (32, 64]: <= 256
+// VGPRs, <= 78 KB, two per CU (pipe_weu).  A replicate set whose slices do not all fit at
+// once is launched in co-resident rounds by the host (cnmf_solve: reps_per_launch).
 //
 // The planes epilogue emits the final x straight from registers (no re-read from L2) and
 // only the `pl_n` planes the consuming GEMM reads (2 with a >= 1024-deep reduction,
@@ -69,16 +61,11 @@ __host__ __device__ constexpr int pipe_mb(int K) { return (K + 15) / 16; }
 __host__ __device__ constexpr int pipe_weu(int K) { return K <= 32 ? 4 : 2; }
 // 256-thread workgroups co-resident per CU (one wave per SIMD each): VGPR- and LDS-bound
 __host__ __device__ constexpr int pipe_wg_per_cu(int K) { return pipe_weu(K); }
-// tiles per wave whose numerators sit in LDS (T * KS KB within 160 KB / pipe_wg_per_cu(K)
-// minus scratch) -- K <= 12: 12 tiles (36 KB), 13..16: 9 (36 KB), 17..32: 36 / KS
-// (<= 36 KB), 40..64: 78 / KS (<= 78 KB)
-__host__ __device__ constexpr int pipe_tile_lds(int K) {
-  return K <= 12 ? 12 : K <= 16 ? 9 : K <= 32 ? 36 / pipe_ks(K) : 78 / pipe_ks(K);
-}
-// tiles per wave: the LDS tiles plus, for 17 <= K <= 20, one tile whose numerators are held
-// in VGPRs beside x (16 bytes per lane of scratch at T = 8, 12 already at T = 7)
+// tiles per wave: the numerators' LDS (T * KS KB) within 160 KB / pipe_wg_per_cu(K) minus
+// scratch -- K <= 12: 12 tiles (36 KB), 13..16: 9 (36 KB), 17..32: 36 / KS (<= 36 KB),
+// 40..64: 78 / KS (<= 78 KB)
 __host__ __device__ constexpr int pipe_tile_max(int K) {
-  return K <= 16 ? pipe_tile_lds(K) : K <= 20 ? 8 : pipe_tile_lds(K);
+  return K <= 12 ? 12 : K <= 16 ? 9 : K <= 32 ? 36 / pipe_ks(K) : 78 / pipe_ks(K);
 }
 // LDS floats of the numerator / epilogue-scratch array: T * KS 256-float slots, and at
 // least the partial-Gram epilogue's 4 waves x 16 x (16 MB + 1)
@@ -88,11 +75,7 @@ __host__ __device__ constexpr int pipe_lds_floats(int K, int T) {
              : 64 * (16 * pipe_mb(K) + 1);
 }
 
-// numerator (tile i, register s) of this lane: LDS for i < TL, else the register array nr
-// (i is a constant once the tile loops are unrolled: the select folds, nr stays in VGPRs)
-#define CNMF_PIPE_N(i, s)                                                         \
-  (*((i) < TL ? &sN[((i) * KS + (s)) * (64 * kPipeWaves) + threadIdx.x]          \
-              : &nr[(i) < TL ? 0 : (i) - TL][s]))
+#define CNMF_PIPE_N(i, s) sN[((i) * KS + (s)) * (64 * kPipeWaves) + threadIdx.x]
 
 // (Gram x) of one tile: d[b][r] = component 16 b + 4 r + g of the lane's column
 template <int KS, int MB>
@@ -137,11 +120,9 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
   constexpr int KS = pipe_ks(K);
   constexpr int MB = pipe_mb(K);
   constexpr int KP = 16 * MB;          // Gram rows covered by the output blocks
-  constexpr int TL = T < pipe_tile_lds(K) ? T : pipe_tile_lds(K);   // tiles numerated in LDS
   __shared__ float sred[3 + 2 * kCoopMaxSlices];
-  // numerators of this lane's first TL tiles; also the partial-Gram scratch of the epilogue
-  __shared__ float sN[pipe_lds_floats(K, TL)];
-  float nr[T > TL ? T - TL : 1][KS];   // numerators of tiles TL.. (register-held)
+  // numerators of this lane's columns; also the partial-Gram scratch of the epilogue
+  __shared__ float sN[pipe_lds_floats(K, T)];
   // phase stamps are compiled in only for the probe build (CNMF_PIPE_STAMPS_BUILD=1 at
   // build time, tools/pipe_stamp_probe.py): their 64-bit counters cost the production
   // kernels registers (K = 10 / 20 instantiations went to scratch with them)
@@ -209,7 +190,7 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
     // in slice order: bitwise the register version's sums.
     const float* gp = p.gpart + (long long)rep * p.gpart_rs;
     constexpr int KK = K * K;
-    constexpr int QCH = pipe_lds_floats(K, TL) / KK > 0 ? pipe_lds_floats(K, TL) / KK : 1;
+    constexpr int QCH = pipe_lds_floats(K, T) / KK > 0 ? pipe_lds_floats(K, T) / KK : 1;
     constexpr int NTH = 64 * kPipeWaves;
     float t[MB][KS];
 #pragma unroll
@@ -643,7 +624,8 @@ void solve_pipe_kernel(SolveParams p, int pl_n) {
 
 // tile counts instantiated (the host rounds up to the next one within pipe_tile_max(K))
 __host__ __device__ constexpr int pipe_t_of(int idx) {
-  return idx < 10 ? idx + 1 : 12;
+  return idx == 0 ? 1 : idx == 1 ? 2 : idx == 2 ? 3 : idx == 3 ? 4 : idx == 4 ? 5 :
+         idx == 5 ? 6 : idx == 6 ? 7 : idx == 7 ? 8 : idx == 8 ? 9 : idx == 9 ? 10 : 12;
 }
 constexpr int kPipeTCount = 11;
 

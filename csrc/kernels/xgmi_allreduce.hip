@@ -1,4 +1,5 @@
-// One-shot all-reduce over xGMI peer memory (optional custom op).
+// One-shot all-reduce / reduce-scatter / all-gather over xGMI peer memory (SURVEY.md §2.6
+// item 4, optional custom ops).
 //
 // Every rank of a node owns one IPC-exported workspace:
 //
@@ -39,86 +40,129 @@ constexpr int kXgBlocks = 128;                     // slices per call (<= CUs: c
 constexpr long long kXgDataOff = 64 * 1024;        // data after the flag page
 constexpr int kXgThreads = 256;
 
-__global__ __launch_bounds__(kXgThreads) void xgmi_allreduce_kernel(
+// Collectives of one launch each (MODE), over m floats per block-slice index range:
+//   kXgAllReduce      in n = m floats, out n: sum over ranks;
+//   kXgReduceScatter  in world x m (rank-major chunks), out m: chunk `rank` of the sum --
+//                     block b stages slice b of EVERY chunk, so one flag per (peer, block)
+//                     still covers everything block b of any rank reads;
+//   kXgAllGather      in m, out world x m: every rank's input, no arithmetic.
+// The call's epoch is either the host's (`epoch` > 0) or kept on the device (`epoch` == 0:
+// read from *ep at start; the last block to finish advances it -- graph replays then
+// advance it too, exactly like the host counter would).
+constexpr int kXgAllReduce = 0, kXgReduceScatter = 1, kXgAllGather = 2;
+
+template <int MODE>
+__global__ __launch_bounds__(kXgThreads) void xgmi_coll_kernel(
     const unsigned long long* __restrict__ peers, int world, int rank, const float* in,
-    float* out, long long n, long long cap, unsigned epoch, unsigned long long limit,
-    int* timeout) {
+    float* out, long long m, long long cap, unsigned host_epoch, unsigned* ep, unsigned* arrive,
+    unsigned long long limit, int* timeout) {
   __shared__ int s_abort;
+  __shared__ unsigned s_epoch;
   const int b = blockIdx.x;
   const int nb = gridDim.x;
   const int tid = threadIdx.x;
-  if (tid == 0)
+  if (tid == 0) {
     s_abort = __hip_atomic_load(timeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (s_abort) return;
-
-  // slice of this block: a multiple of 4 floats so every interior access is a float4
-  const long long per = (((n + nb - 1) / nb) + 3) & ~3LL;
-  const long long lo = min(n, (long long)b * per);
-  const long long hi = min(n, lo + per);
-  const unsigned par = epoch & 1u;
-  char* mine = reinterpret_cast<char*>(peers[rank]);
-  float* stage = reinterpret_cast<float*>(mine + kXgDataOff) + par * cap;
-
-  // 1. stage the slice, make it visible system-wide, raise this block's flag in every peer
-  {
-    const long long v0 = lo >> 2, v1 = hi >> 2;    // lo is 4-aligned; tail handled below
-    const float4* src = reinterpret_cast<const float4*>(in);
-    float4* dst = reinterpret_cast<float4*>(stage);
-    const bool aligned = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
-    if (aligned) {
-      for (long long v = v0 + tid; v < v1; v += kXgThreads) dst[v] = src[v];
-      for (long long i = (v1 << 2) + tid; i < hi; i += kXgThreads) stage[i] = in[i];
-    } else {
-      for (long long i = lo + tid; i < hi; i += kXgThreads) stage[i] = in[i];
-    }
+    s_epoch = host_epoch ? host_epoch
+                         : __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   }
-  __threadfence_system();
   __syncthreads();
-  if (tid < world) {
-    unsigned* f = reinterpret_cast<unsigned*>(peers[tid]) + rank * kXgBlocks + b;
-    __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  const unsigned epoch = s_epoch;
+  if (!s_abort) {
+    // slice of this block within [0, m): a multiple of 4 floats so interior accesses are
+    // float4 (whole chunks stay 16-byte aligned when m % 4 == 0)
+    const long long per = (((m + nb - 1) / nb) + 3) & ~3LL;
+    const long long lo = min(m, (long long)b * per);
+    const long long hi = min(m, lo + per);
+    const unsigned par = epoch & 1u;
+    char* mine = reinterpret_cast<char*>(peers[rank]);
+    float* stage = reinterpret_cast<float*>(mine + kXgDataOff) + par * cap;
+    const bool vec = (m & 3) == 0 && (reinterpret_cast<uintptr_t>(in) & 15) == 0 &&
+                     (reinterpret_cast<uintptr_t>(out) & 15) == 0;
 
-  // 2. wait for the matching block of every peer (wrap-safe epoch compare, bounded)
-  if (tid < world) {
-    unsigned* f = reinterpret_cast<unsigned*>(mine) + tid * kXgBlocks + b;
-    const unsigned long long t0 = wall_clock64();
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      __builtin_amdgcn_s_sleep(4);
-      if (wall_clock64() - t0 > limit) {
-        atomicExch(timeout, 1);
-        break;
+    // 1. stage, make visible system-wide, raise this block's flag in every peer
+    const int nchunk = MODE == kXgReduceScatter ? world : 1;
+    for (int c = 0; c < nchunk; ++c) {
+      const long long o = (long long)c * m;
+      if (vec) {
+        const float4* src = reinterpret_cast<const float4*>(in + o);
+        float4* dst = reinterpret_cast<float4*>(stage + o);
+        for (long long v = (lo >> 2) + tid; v < (hi >> 2); v += kXgThreads) dst[v] = src[v];
+      } else {
+        for (long long i = lo + tid; i < hi; i += kXgThreads) stage[o + i] = in[o + i];
       }
     }
-  }
-  __syncthreads();
-  // system-scope acquire: the flag loads above were system-scope acquires by the polling
-  // lanes; this fence orders every lane's slice loads after them.  The slices live in
-  // uncached / fine-grained memory (cnmf_xgmi_alloc), so the loads read the peer's HBM.
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    __threadfence_system();
+    __syncthreads();
+    if (tid < world) {
+      unsigned* f = reinterpret_cast<unsigned*>(peers[tid]) + rank * kXgBlocks + b;
+      __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 
-  // 3. sum the peers' slices in rank order
-  const long long v0 = lo >> 2, v1 = hi >> 2;
-  const bool oaligned = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
-  if (oaligned) {
-    for (long long v = v0 + tid; v < v1; v += kXgThreads) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    // 2. wait for the matching block of every peer (wrap-safe epoch compare, bounded)
+    if (tid < world) {
+      unsigned* f = reinterpret_cast<unsigned*>(mine) + tid * kXgBlocks + b;
+      const unsigned long long t0 = wall_clock64();
+      while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+        __builtin_amdgcn_s_sleep(4);
+        if (wall_clock64() - t0 > limit) {
+          atomicExch(timeout, 1);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    // system-scope acquire: the flag loads above were system-scope acquires by the polling
+    // lanes; this fence orders every lane's slice loads after them.  The slices live in
+    // uncached / fine-grained memory (cnmf_xgmi_alloc), so the loads read the peer's HBM.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+
+    // 3. read the peers' slices: sum in rank order, or copy
+    auto pstage = [&](int q) {
+      return reinterpret_cast<const float*>(reinterpret_cast<const char*>(peers[q]) + kXgDataOff) +
+             par * cap;
+    };
+    if (MODE == kXgAllGather) {
       for (int q = 0; q < world; ++q) {
-        const float4* p = reinterpret_cast<const float4*>(
-            reinterpret_cast<const char*>(peers[q]) + kXgDataOff) + (par * cap >> 2);
-        const float4 t = p[v];
-        acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+        const float* p = pstage(q);
+        float* o = out + (long long)q * m;
+        if (vec) {
+          for (long long v = (lo >> 2) + tid; v < (hi >> 2); v += kXgThreads)
+            reinterpret_cast<float4*>(o)[v] = reinterpret_cast<const float4*>(p)[v];
+        } else {
+          for (long long i = lo + tid; i < hi; i += kXgThreads) o[i] = p[i];
+        }
       }
-      reinterpret_cast<float4*>(out)[v] = acc;
+    } else {
+      const long long src0 = MODE == kXgReduceScatter ? (long long)rank * m : 0;
+      if (vec) {
+        for (long long v = (lo >> 2) + tid; v < (hi >> 2); v += kXgThreads) {
+          float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+          for (int q = 0; q < world; ++q) {
+            const float4 t = reinterpret_cast<const float4*>(pstage(q) + src0)[v];
+            acc.x += t.x; acc.y += t.y; acc.z += t.z; acc.w += t.w;
+          }
+          reinterpret_cast<float4*>(out)[v] = acc;
+        }
+      } else {
+        for (long long i = lo + tid; i < hi; i += kXgThreads) {
+          float acc = 0.f;
+          for (int q = 0; q < world; ++q) acc += pstage(q)[src0 + i];
+          out[i] = acc;
+        }
+      }
     }
   }
-  for (long long i = (oaligned ? (v1 << 2) : lo) + tid; i < hi; i += kXgThreads) {
-    float acc = 0.f;
-    for (int q = 0; q < world; ++q)
-      acc += reinterpret_cast<const float*>(reinterpret_cast<const char*>(peers[q]) +
-                                            kXgDataOff)[par * cap + i];
-    out[i] = acc;
+  // device epoch: the last block of the launch advances it (every block read it above)
+  if (!host_epoch) {
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = atomicAdd(arrive, 1u);
+      if (old + 1 == (unsigned)nb) {
+        atomicExch(arrive, 0u);
+        __hip_atomic_store(ep, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
@@ -171,18 +215,42 @@ hipError_t cnmf_ptr_alloc_flags(const void* p, unsigned* flags) {
   return hipSuccess;
 }
 
+// mode 0 all-reduce (m = n floats), 1 reduce-scatter (in world x m, out m), 2 all-gather
+// (in m, out world x m); epoch > 0: the host's call counter, 0: the device counter at
+// `ep` (+ its arrival counter `arrive`) -- capturable in a HIP graph
+hipError_t cnmf_xgmi_collective(int mode, const unsigned long long* peers, int world, int rank,
+                                const float* in, float* out, long long m, long long cap,
+                                unsigned epoch, unsigned* ep, unsigned* arrive,
+                                unsigned long long limit, int* timeout, int blocks,
+                                hipStream_t stream) {
+  if (world < 1 || world > cnmf::kXgRanks || rank < 0 || rank >= world || m < 0 ||
+      mode < 0 || mode > 2)
+    return hipErrorInvalidValue;
+  if ((mode == 1 ? (long long)world * m : m) > cap) return hipErrorInvalidValue;
+  if (epoch == 0 && (!ep || !arrive)) return hipErrorInvalidValue;
+  if (m == 0) return hipSuccess;
+  if (blocks < 1) blocks = 1;
+  if (blocks > cnmf::kXgBlocks) blocks = cnmf::kXgBlocks;
+  const dim3 g(blocks), t(cnmf::kXgThreads);
+  if (mode == 0)
+    hipLaunchKernelGGL(cnmf::xgmi_coll_kernel<cnmf::kXgAllReduce>, g, t, 0, stream, peers, world,
+                       rank, in, out, m, cap, epoch, ep, arrive, limit, timeout);
+  else if (mode == 1)
+    hipLaunchKernelGGL(cnmf::xgmi_coll_kernel<cnmf::kXgReduceScatter>, g, t, 0, stream, peers,
+                       world, rank, in, out, m, cap, epoch, ep, arrive, limit, timeout);
+  else
+    hipLaunchKernelGGL(cnmf::xgmi_coll_kernel<cnmf::kXgAllGather>, g, t, 0, stream, peers, world,
+                       rank, in, out, m, cap, epoch, ep, arrive, limit, timeout);
+  return hipGetLastError();
+}
+
 hipError_t cnmf_xgmi_allreduce(const unsigned long long* peers, int world, int rank,
                                const float* in, float* out, long long n, long long cap,
                                unsigned epoch, unsigned long long limit, int* timeout,
                                int blocks, hipStream_t stream) {
-  if (world < 1 || world > cnmf::kXgRanks || rank < 0 || rank >= world || n > cap || n < 0)
-    return hipErrorInvalidValue;
-  if (n == 0) return hipSuccess;
-  if (blocks < 1) blocks = 1;
-  if (blocks > cnmf::kXgBlocks) blocks = cnmf::kXgBlocks;
-  hipLaunchKernelGGL(cnmf::xgmi_allreduce_kernel, dim3(blocks), dim3(cnmf::kXgThreads), 0,
-                     stream, peers, world, rank, in, out, n, cap, epoch, limit, timeout);
-  return hipGetLastError();
+  if (epoch == 0) return hipErrorInvalidValue;
+  return cnmf_xgmi_collective(0, peers, world, rank, in, out, n, cap, epoch, nullptr, nullptr,
+                              limit, timeout, blocks, stream);
 }
 
 }  // extern "C"

@@ -236,11 +236,103 @@ def xgmi_dp_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, allreduce):
     dist.destroy_process_group()
 
 
-def dp_fused_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, fused):
+def xgmi_rsag_worker(rank, world, port, out_dir):
+    """One-shot xGMI reduce-scatter / all-gather (and all-reduce between them, one device
+    call counter for all three) against gloo, eagerly and replayed from a HIP graph."""
+    _init(rank, world, port)
+    from cnmf_torch_amd.parallel.comm import DistComm
+    from cnmf_torch_amd.parallel.xgmi import XgmiAllReduce
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    xg = XgmiAllReduce(None, dev, cap=1 << 16, timeout_ms=3000)
+    res = {}
+    k = 0
+
+    def rs_ref(inp):
+        h = inp.cpu().clone()
+        dist.all_reduce(h)
+        m = h.numel() // world
+        return h[rank * m:(rank + 1) * m]
+
+    def ag_ref(inp):          # (gloo has no int16 all-gather: as bytes)
+        h = inp.cpu().contiguous().view(torch.uint8)
+        parts = [torch.empty_like(h) for _ in range(world)]
+        dist.all_gather(parts, h)
+        return torch.cat(parts).view(inp.dtype)
+
+    for i, m in enumerate([5, 1000, 4096, 777, 8, 4097] * 2):
+        g = torch.Generator().manual_seed(100 * i + rank)
+        a = torch.randn(world * m, generator=g).to(dev)
+        o = torch.empty(m, device=dev)
+        assert xg.reduce_scatter(o, a)
+        b = torch.randn(m, generator=g).to(dev)
+        ob = torch.empty(world * m, device=dev)
+        assert xg.all_gather(ob, b)
+        c = torch.randint(-30000, 30000, (2 * m,), generator=g, dtype=torch.int16).to(dev)
+        oc = torch.empty(world * 2 * m, dtype=torch.int16, device=dev)
+        assert xg.all_gather(oc, c)
+        d = torch.randn(m, generator=g).to(dev)
+        dd = d.clone()
+        xg(dd)
+        torch.cuda.synchronize()
+        res[f"rs{k}"] = float((o.cpu() - rs_ref(a)).abs().max())
+        res[f"ag{k}"] = float((ob.cpu() - ag_ref(b)).abs().max())
+        res[f"agi{k}"] = int((oc.cpu() != ag_ref(c)).sum())
+        dref = d.cpu().clone()
+        dist.all_reduce(dref)
+        res[f"ar{k}"] = float((dd.cpu() - dref).abs().max())
+        k += 1
+    # the same calls captured once and replayed with new inputs: the device call counter
+    # advances on every replay
+    m = 1000
+    a = torch.zeros(world * m, device=dev)
+    o = torch.empty(m, device=dev)
+    b = torch.zeros(m, device=dev)
+    ob = torch.empty(world * m, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            xg.reduce_scatter(o, a)
+            xg.all_gather(ob, b)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    for r_ in range(3):
+        g = torch.Generator().manual_seed(7000 + 10 * r_ + rank)
+        a.copy_(torch.randn(world * m, generator=g))
+        b.copy_(torch.randn(m, generator=g))
+        graph.replay()
+        torch.cuda.synchronize()
+        res[f"grs{r_}"] = float((o.cpu() - rs_ref(a)).abs().max())
+        res[f"gag{r_}"] = float((ob.cpu() - ag_ref(b)).abs().max())
+    xg.check()
+    res["n"] = k
+    xg.close()
+    # DistComm routes reduce-scatter / all-gather here under CNMF_ALLREDUCE=xgmi
+    os.environ["CNMF_ALLREDUCE"] = "xgmi"
+    comm = DistComm()
+    o = torch.empty(3, device=dev)
+    comm.reduce_scatter_(o, torch.full((3 * world,), float(rank + 1), device=dev))
+    ob = torch.empty(4 * world, dtype=torch.int16, device=dev)
+    comm.all_gather_into_(ob, torch.full((4,), rank + 7, dtype=torch.int16, device=dev))
+    comm.check()
+    res["comm_rs"] = o.cpu().numpy()
+    res["comm_ag"] = ob.cpu().numpy()
+    res["comm_is_xgmi"] = bool(comm._xgmi)
+    comm.close()
+    np.savez(os.path.join(out_dir, f"rsag{rank}.npz"), **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def dp_fused_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, fused, allreduce="rccl"):
     """Cell-sharded DP solve on the GPU (both ranks share the one GPU of the box; the
-    collectives are staged through gloo): the reduce-scattered fused step
+    collectives are staged through gloo, or -- allreduce="xgmi" -- run as the one-shot
+    peer-memory kernels): the packed reduce-scatter / all-gather fused step
     (CNMF_DP_FUSED=1) or the all-reduced unfused step (0)."""
     os.environ["CNMF_DP_FUSED"] = fused
+    os.environ["CNMF_ALLREDUCE"] = allreduce
     os.environ["CNMF_SOLVE_COOP"] = "0"      # two processes on one GPU: no spinning slices
     _init(rank, world, port)
     from cnmf_torch_amd import ops
@@ -260,10 +352,12 @@ def dp_fused_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, fused):
                 torch.zeros((K * len(seeds), Xl.shape[1]), device="cuda"), [K] * len(seeds))
     took = solver._fused_ok(st, solver._steps(Xl.shape[0]))
     res = solver.run(seeds)
-    np.save(os.path.join(out_dir, f"dpf{fused}_{rank}.npz.npy"),
-            np.array([took], dtype=bool))
-    np.save(os.path.join(out_dir, f"dpfW{fused}_{rank}.npy"), res.W.cpu().numpy())
-    np.save(os.path.join(out_dir, f"dpferr{fused}_{rank}.npy"), res.err)
-    np.save(os.path.join(out_dir, f"dpfit{fused}_{rank}.npy"), res.n_iter)
+    tag = fused + ("x" if allreduce == "xgmi" else "")
+    np.save(os.path.join(out_dir, f"dpf{tag}_{rank}.npz.npy"),
+            np.array([took, bool(solver.comm._xgmi)], dtype=bool))
+    np.save(os.path.join(out_dir, f"dpfW{tag}_{rank}.npy"), res.W.cpu().numpy())
+    np.save(os.path.join(out_dir, f"dpferr{tag}_{rank}.npy"), res.err)
+    np.save(os.path.join(out_dir, f"dpfit{tag}_{rank}.npy"), res.n_iter)
+    solver.comm.close()
     dist.barrier()
     dist.destroy_process_group()

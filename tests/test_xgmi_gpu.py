@@ -52,6 +52,26 @@ def test_xgmi_dp_solve_matches_gloo_staged(tmp_path):
     np.testing.assert_allclose(np.load(tmp_path / "err_xgmi0.npy"), ref.err, rtol=1e-3)
 
 
+def test_xgmi_reduce_scatter_all_gather_match_gloo(tmp_path):
+    """One-shot reduce-scatter and all-gather (float32 and int16 bit patterns), mixed with
+    all-reduces on one device call counter, == gloo's results bitwise on both ranks --
+    eagerly and from a replayed HIP graph; DistComm routes both under
+    CNMF_ALLREDUCE=xgmi."""
+    _spawn(W.xgmi_rsag_worker, 2, str(tmp_path), timeout=150)
+    for r in range(2):
+        z = np.load(tmp_path / f"rsag{r}.npz")
+        n = int(z["n"])
+        assert n == 12
+        for i in range(n):
+            assert z[f"rs{i}"] == 0.0 and z[f"ag{i}"] == 0.0 and z[f"ar{i}"] == 0.0, i
+            assert int(z[f"agi{i}"]) == 0, i
+        for i in range(3):
+            assert z[f"grs{i}"] == 0.0 and z[f"gag{i}"] == 0.0, i
+        assert bool(z["comm_is_xgmi"])
+        np.testing.assert_array_equal(z["comm_rs"], np.full(3, 3.0, dtype=np.float32))
+        np.testing.assert_array_equal(z["comm_ag"], np.repeat([7, 8], 4).astype(np.int16))
+
+
 @pytest.mark.parametrize("K,R", [(6, 7), (20, 6)])
 def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
     """Cell-sharded DP with the fused step -- reduce-scatter of dB and the per-slice
@@ -64,11 +84,20 @@ def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
     kw = dict(online_chunk_size=400, online_max_pass=12)
     for fused in ("1", "0"):
         _spawn(W.dp_fused_worker, 2, X, K, seeds, kw, str(tmp_path), fused, timeout=150)
+    # the packed step with its reduce-scatter / all-gather as one-shot xGMI kernels
+    _spawn(W.dp_fused_worker, 2, X, K, seeds, kw, str(tmp_path), "1", "xgmi", timeout=150)
     for r in range(2):
         assert bool(np.load(tmp_path / f"dpf1_{r}.npz.npy")[0])
         assert not bool(np.load(tmp_path / f"dpf0_{r}.npz.npy")[0])
+        took, used = np.load(tmp_path / f"dpf1x_{r}.npz.npy")
+        assert bool(took) and bool(used)
     Wf = np.load(tmp_path / "dpfW1_0.npy")
     np.testing.assert_array_equal(Wf, np.load(tmp_path / "dpfW1_1.npy"))
+    # 2 ranks: gloo's and the kernels' sums are the same float32 a + b -- bitwise
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"dpfW1x_{r}.npy"), Wf)
+        np.testing.assert_array_equal(np.load(tmp_path / f"dpferr1x_{r}.npy"),
+                                      np.load(tmp_path / "dpferr1_0.npy"))
     ef, eu = np.load(tmp_path / "dpferr1_0.npy"), np.load(tmp_path / "dpferr0_0.npy")
     itf, itu = np.load(tmp_path / "dpfit1_0.npy"), np.load(tmp_path / "dpfit0_0.npy")
     assert np.abs(itf - itu).max() <= 1

@@ -128,6 +128,12 @@ def main():
                     help="with --dp on ONE process: run rank 0's shard of an N-rank DP job, "
                          "collectives replaced by device copies (parallel.comm.EmulatedComm): "
                          "the per-rank step time, value = projected N-GPU job rate")
+    ap.add_argument("--coll-latency-us", type=float, default=None,
+                    help="--emulate-world: per-call latency of the one-shot xGMI collectives "
+                         "(tools/xgmi_latency.py, 2 ranks on one GPU); default: the measured "
+                         "value in profiles/r5_xgmi_latency.json")
+    ap.add_argument("--link-gbps", type=float, default=153.0,
+                    help="--emulate-world: xGMI bandwidth per link and direction, GB/s")
     ap.add_argument("--planes-only", action="store_true",
                     help="hold X only as split-GEMM planes (10M x 5k on one GPU: fp32 X "
                          "and its planes do not fit together)")
@@ -168,6 +174,9 @@ def main():
         solver.run([int(s) for s in seeds[i * a.reps:(i + 1) * a.reps]])
     if world > 1:
         dist.barrier()
+    if emu:         # count the timed steps' collectives only
+        comm.bytes, comm.log = 0, []
+        comm.calls = {k: 0 for k in comm.calls}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     passes = []
@@ -189,6 +198,30 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     total_reps = a.reps * a.steps * (1 if a.dp else world)
+    proj = None
+    if emu:
+        # collective term of the projection: per call the one-shot kernels' latency plus the
+        # bytes each rank pulls over ONE of its 7 links (all 7 in parallel): all-reduce the
+        # whole payload from every peer, reduce-scatter / all-gather 1 / world of it
+        lat = a.coll_latency_us
+        if lat is None:
+            path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "profiles", "r5_xgmi_latency.json")
+            lat = (json.loads(open(path).read().strip().splitlines()[-1])["latency_us"]
+                   if os.path.exists(path) else 20.0)
+        per_link = {"all_reduce": 1.0, "reduce_scatter": 1.0 / emu, "all_gather": 1.0 / emu}
+        t_coll = sum(lat * 1e-6 + nb * per_link[k] / (a.link_gbps * 1e9) for k, nb in comm.log)
+        n_steps_online = sum(1 for k, _ in comm.log if k == "reduce_scatter") or None
+        proj = {
+            "collectives_per_step": {k: v / a.steps for k, v in comm.calls.items()},
+            "collective_bytes_per_step_per_rank": int(comm.bytes / a.steps),
+            "online_steps_per_step": (n_steps_online / a.steps) if n_steps_online else None,
+            "latency_us_per_call": lat, "link_gbps": a.link_gbps,
+            "collective_s_per_step": round(t_coll / a.steps, 4),
+            "compute_s_per_step": round(el / a.steps, 4),
+            "value_with_collectives": round(total_reps / (el + t_coll), 4),
+            "collective_model": "latency + per-link bytes / link bandwidth per call, serial "
+                                "with compute (no overlap)"}
     if rank == 0:
         print(json.dumps({
             "metric": "NMF replicates/sec (large N)", "value": round(total_reps / el, 4),
@@ -204,6 +237,7 @@ def main():
                 "hbm_gb_X_per_gpu": round(N * G * 4 / 1e9 / (emu or (world if a.dp else 1)), 2),
                 "x_storage": "split-GEMM planes only" if a.planes_only else "fp32 + planes",
                 "hbm_gb_peak": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1)},
+            "projection": proj,
             "data": "synthetic planted-program Poisson counts generated on device"}), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,10 @@
+# k-means: point tiles loaded up front
+export TMPDIR=/tmp
+R=$(pwd)
+out=$R/gpurun_out/r5o
+mkdir -p $out
+timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 170 --timeout-method thread -k "kmeans or harmony" > $out/pytest.log 2>&1 || { echo PYTEST_FAILED; grep -E "Error|assert|FAILED|passed|failed" $out/pytest.log | head -30; exit 1; }
+tail -n 1 $out/pytest.log
+timeout -k 10 300 python tools/harmony_stage.py --repeat 2 > $out/stage.log 2>&1 && tail -n 1 $out/stage.log | cut -c1-120 &&
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o hs -- python $R/tools/harmony_stage.py > $out/stage_prof.log 2>&1) && echo profiled
+echo rc=$?
