@@ -46,7 +46,8 @@ __host__ __device__ constexpr size_t km_lds_bytes(int k, int dp) {
   return ((size_t)dp * km_kps(k) + (size_t)(k + 15) / 16 * 16 + (size_t)k * dp + k +
           (size_t)(kKmThreads / 64) * dp) *
              sizeof(double) +
-         (2 * kKmThreads + 2 * (size_t)k + kKmThreads / 64) * sizeof(int);
+         (2 * kKmThreads + 2 * (size_t)k + kKmThreads / 64 + (kKmThreads / 64) * (size_t)k) *
+             sizeof(int);
 }
 
 __device__ __forceinline__ void km_take(double v, int c, double& best, int& arg) {
@@ -74,6 +75,7 @@ __global__ void __launch_bounds__(kKmThreads)
   int* sHist = sPerm + kKmThreads;                  // k: points per label this round
   int* sOff = sHist + k;                            // k: exclusive prefix of sHist
   int* sEdgeLab = sOff + k;                         // [wave] label of the first run
+  int* sWH = sEdgeLab + kKmThreads / 64;            // [wave][k] per-wave label counts
   const int r = blockIdx.y;
   const int n_init = gridDim.y;
   if (live != nullptr && live[r] == 0) return;    // frozen restart: partials unused
@@ -84,20 +86,23 @@ __global__ void __launch_bounds__(kKmThreads)
     sCt[e] = (c < k && j < d) ? Cr[(long long)c * d + j] : 0.0;
   }
   for (int e = tid; e < k * DP; e += kKmThreads) sAcc[e] = 0.0;
+  for (int c = tid; c < k; c += kKmThreads) sCnt[c] = 0.0;
+  __syncthreads();
+  // squared norms from the LDS table (independent reads; a walk over the global rows was
+  // a chain of dependent loads per centroid)
   for (int c = tid; c < KP; c += kKmThreads) {
     double s = 0.0;
-    if (c < k)
-      for (int j = 0; j < d; ++j) {
-        const double v = Cr[(long long)c * d + j];
-        s = fma(v, v, s);
-      }
+#pragma unroll
+    for (int j = 0; j < DP; ++j) {
+      const double v = sCt[j * KPS + c];
+      s = fma(v, v, s);
+    }
     sCsq[c] = c < k ? s : INFINITY;
   }
-  for (int c = tid; c < k; c += kKmThreads) sCnt[c] = 0.0;
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6, col = lane & 15, grp = lane >> 4;
-  const int nks = (d + 3) >> 2, nct = KP >> 4;
+  const int nct = KP >> 4;
   const long long base = (long long)blockIdx.x * (kKmThreads * kKmRounds);
   for (int round = 0; round < kKmRounds; ++round) {
     const long long p0 = base + (long long)round * kKmThreads;
@@ -132,13 +137,19 @@ __global__ void __launch_bounds__(kKmThreads)
         const bool two = ct + 1 < nct;                 // uniform
         km_f64x4 a0 = km_f64x4{0.0, 0.0, 0.0, 0.0}, a1 = a0;
         const double* ap = sCt + (long long)grp * KPS + 16 * ct + col;
+        // every k-step of the padded DP (the padding is zero on both sides): no branch
+        // between the LDS operand loads and their MFMAs, so the loads issue ahead
+        double av0[DP / 4], av1[DP / 4];
 #pragma unroll
         for (int ks = 0; ks < DP / 4; ++ks) {
-          if (ks < nks) {                              // uniform
-            const double* row = ap + (long long)(4 * ks) * KPS;
-            a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(row[0], bx[ks], a0, 0, 0, 0);
-            if (two) a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(row[16], bx[ks], a1, 0, 0, 0);
-          }
+          const double* row = ap + (long long)(4 * ks) * KPS;
+          av0[ks] = row[0];
+          av1[ks] = two ? row[16] : 0.0;
+        }
+#pragma unroll
+        for (int ks = 0; ks < DP / 4; ++ks) {
+          a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0[ks], bx[ks], a0, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av1[ks], bx[ks], a1, 0, 0, 0);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -173,7 +184,7 @@ __global__ void __launch_bounds__(kKmThreads)
     // ---- phase B: ordered accumulation (only when partial sums are wanted).  The
     // round's points are grouped by label with a stable counting sort (rank = earlier
     // points with the same label: a broadcast LDS walk); wave w then walks sorted
-    // positions [64 w, 64 w + 64) with one lane per coordinate -- coalesced row loads, 8
+    // positions [64 w, 64 w + 64) with one lane per coordinate -- coalesced row loads, 16
     // in flight -- keeping a register running sum per run of equal labels.  Every run
     // but the wave's first is a whole cluster of this round and is added to the
     // accumulator directly (no other wave holds that cluster); the first runs may
@@ -183,24 +194,41 @@ __global__ void __launch_bounds__(kKmThreads)
     // a 5 ms step at 500k x 50 x 100 x 10 restarts, profiles/r5l_*; d threads walking all
     // 256 points with LDS read-modify-writes took ~11 ms, profiles/r3ae_*.)
     if (psum != nullptr) {
-      for (int c = tid; c < k; c += kKmThreads) sHist[c] = 0;
+      // stable counting sort of the round's points by label: a point's rank among the
+      // earlier points of its label = the same label's count in the earlier waves (per-wave
+      // histograms: integer LDS atomics, order-free) + the earlier lanes of its own wave
+      // (a v_readlane walk over the 64 labels); cluster offsets by a block scan
+      for (int e = tid; e < (kKmThreads / 64) * k; e += kKmThreads) sWH[e] = 0;
       __syncthreads();
       const int lab = sLab[tid];
       int rank = 0;
+      for (int j = 0; j < 64; ++j) {
+        const int lj = __builtin_amdgcn_readlane(lab, j);
+        rank += (j < lane && lj == lab) ? 1 : 0;
+      }
+      if (lab >= 0) atomicAdd(&sWH[wave * k + lab], 1);
+      __syncthreads();
+      int tot = 0;
+      if (tid < k)
+        for (int w = 0; w < kKmThreads / 64; ++w) tot += sWH[w * k + tid];
+      int* sScan = sPerm;                        // scratch until the permutation is written
+      sScan[tid] = tot;
+      __syncthreads();
+      for (int dd = 1; dd < kKmThreads; dd <<= 1) {
+        const int v = tid >= dd ? sScan[tid - dd] : 0;
+        __syncthreads();
+        sScan[tid] += v;
+        __syncthreads();
+      }
+      if (tid < k) {
+        sOff[tid] = sScan[tid] - tot;
+        sHist[tid] = tot;
+      }
+      __syncthreads();
       if (lab >= 0) {
-        for (int q = 0; q < tid; ++q) rank += sLab[q] == lab ? 1 : 0;
-        atomicAdd(&sHist[lab], 1);
+        for (int w = 0; w < wave; ++w) rank += sWH[w * k + lab];
+        sPerm[sOff[lab] + rank] = tid;
       }
-      __syncthreads();
-      if (tid == 0) {
-        int o = 0;
-        for (int c = 0; c < k; ++c) {
-          sOff[c] = o;
-          o += sHist[c];
-        }
-      }
-      __syncthreads();
-      if (lab >= 0) sPerm[sOff[lab] + rank] = tid;
       __syncthreads();
       const int nval = (int)min((long long)kKmThreads, (long long)n - p0);
       const int q0 = 64 * wave, q1 = min(q0 + 64, nval);
@@ -211,11 +239,11 @@ __global__ void __launch_bounds__(kKmThreads)
         int cur = sLab[sPerm[q0]];
         double acc = 0.0;
         bool first = true;
-        for (int q = q0; q < q1; q += 8) {
-          double xv[8];
-          int lb[8];
+        for (int q = q0; q < q1; q += 16) {
+          double xv[16];
+          int lb[16];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < 16; ++u) {
             const int qq = q + u;
             lb[u] = -2;
             xv[u] = 0.0;
@@ -226,7 +254,7 @@ __global__ void __launch_bounds__(kKmThreads)
             }
           }
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < 16; ++u) {
             if (lb[u] == -2) break;                    // uniform: past the range
             if (lb[u] != cur) {                        // uniform: a run ends
               if (first) {
@@ -502,7 +530,7 @@ extern "C" int cnmf_kmeans_blocks(int n) {
 // Whether the LDS budget (160 KiB per CU) holds the transposed centroid table, the
 // accumulator and the label arrays of (k, d).
 extern "C" int cnmf_kmeans_fits(int k, int d) {
-  if (k < 1 || d < 1 || d > 64) return 0;
+  if (k < 1 || k > cnmf::kKmThreads || d < 1 || d > 64) return 0;
   const int dp = (d + 15) / 16 * 16;
   return cnmf::km_lds_bytes(k, dp) <= 156 * 1024 ? 1 : 0;
 }

@@ -128,10 +128,10 @@ def main():
                     help="with --dp on ONE process: run rank 0's shard of an N-rank DP job, "
                          "collectives replaced by device copies (parallel.comm.EmulatedComm): "
                          "the per-rank step time, value = projected N-GPU job rate")
-    ap.add_argument("--coll-latency-us", type=float, default=None,
+    ap.add_argument("--coll-latency-us", type=float, default=33.4,
                     help="--emulate-world: per-call latency of the one-shot xGMI collectives "
-                         "(tools/xgmi_latency.py, 2 ranks on one GPU); default: the measured "
-                         "value in profiles/r5_xgmi_latency.json")
+                         "(default: tools/xgmi_latency.py, 2 ranks on one GPU, the slowest "
+                         "kind at 4 KB -- profiles/r5_xgmi_latency.json)")
     ap.add_argument("--link-gbps", type=float, default=153.0,
                     help="--emulate-world: xGMI bandwidth per link and direction, GB/s")
     ap.add_argument("--planes-only", action="store_true",
@@ -204,11 +204,6 @@ def main():
         # bytes each rank pulls over ONE of its 7 links (all 7 in parallel): all-reduce the
         # whole payload from every peer, reduce-scatter / all-gather 1 / world of it
         lat = a.coll_latency_us
-        if lat is None:
-            path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                "profiles", "r5_xgmi_latency.json")
-            lat = (json.loads(open(path).read().strip().splitlines()[-1])["latency_us"]
-                   if os.path.exists(path) else 20.0)
         per_link = {"all_reduce": 1.0, "reduce_scatter": 1.0 / emu, "all_gather": 1.0 / emu}
         t_coll = sum(lat * 1e-6 + nb * per_link[k] / (a.link_gbps * 1e9) for k, nb in comm.log)
         n_steps_online = sum(1 for k, _ in comm.log if k == "reduce_scatter") or None
