@@ -13,7 +13,8 @@
 //            previous thread-per-point form (exact (x - c)^2 sums, broadcast LDS reads of
 //            every centroid) ran at ~12 ms per step at 500k x 50 x 100 x 10 restarts
 //            (profiles/r5i_*).
-//   phase B  the round's points are added to the workgroup's centroid accumulator in LDS:
+//   phase B  the round's points are added to the workgroup's centroid accumulator (its
+//            own partial slot of psum, in global memory):
 //            a stable counting sort groups them by label, then each thread sums whole
 //            (cluster, feature) segments in point order and adds them once (no float
 //            atomics; the label histogram uses integer LDS atomics).
@@ -43,7 +44,7 @@ __host__ __device__ constexpr int km_kps(int k) {
 }
 
 __host__ __device__ constexpr size_t km_lds_bytes(int k, int dp) {
-  return ((size_t)dp * km_kps(k) + (size_t)(k + 15) / 16 * 16 + (size_t)k * dp + k +
+  return ((size_t)dp * km_kps(k) + (size_t)(k + 15) / 16 * 16 + k +
           (size_t)(kKmThreads / 64) * dp) *
              sizeof(double) +
          (2 * kKmThreads + 2 * (size_t)k + kKmThreads / 64 + (kKmThreads / 64) * (size_t)k) *
@@ -57,8 +58,9 @@ __device__ __forceinline__ void km_take(double v, int c, double& best, int& arg)
   }
 }
 
+// two workgroups per CU (LDS ~65 KB each at k = 100, DP = 64): at most 256 registers
 template <int DP>
-__global__ void __launch_bounds__(kKmThreads)
+__global__ void __launch_bounds__(kKmThreads) __attribute__((amdgpu_waves_per_eu(2)))
     kmeans_step_kernel(const double* __restrict__ X, long long ldx, int n, int d,
                        const double* __restrict__ C, int k, const int* __restrict__ live,
                        int* __restrict__ labels, double* __restrict__ mind,
@@ -67,8 +69,7 @@ __global__ void __launch_bounds__(kKmThreads)
   const int KP = (k + 15) / 16 * 16, KPS = km_kps(k);
   double* sCt = smem;                       // DP x KPS centroids, coordinate-major
   double* sCsq = sCt + (long long)DP * KPS; // KP squared norms (+inf for the padding)
-  double* sAcc = sCsq + KP;                 // k * DP accumulator
-  double* sCnt = sAcc + (long long)k * DP;  // k counts
+  double* sCnt = sCsq + KP;                 // k counts
   double* sEdge = sCnt + k;                 // [wave][DP] first-run partials (phase B)
   int* sLab = reinterpret_cast<int*>(sEdge + (kKmThreads / 64) * DP);   // 256 round labels
   int* sPerm = sLab + kKmThreads;                   // round's points grouped by label
@@ -85,7 +86,12 @@ __global__ void __launch_bounds__(kKmThreads)
     const int j = e / KPS, c = e - j * KPS;
     sCt[e] = (c < k && j < d) ? Cr[(long long)c * d + j] : 0.0;
   }
-  for (int e = tid; e < k * DP; e += kKmThreads) sAcc[e] = 0.0;
+  // the cluster sums accumulate straight in this workgroup's partial slot of psum
+  // ([k][d], global memory: only this workgroup touches it) -- in LDS they took 51 KB,
+  // which held the kernel to one workgroup (one wave per SIMD) per CU
+  double* acc_g = psum != nullptr ? psum + ((long long)blockIdx.x * n_init + r) * k * d : nullptr;
+  if (acc_g != nullptr)
+    for (int e = tid; e < k * d; e += kKmThreads) acc_g[e] = 0.0;
   for (int c = tid; c < k; c += kKmThreads) sCnt[c] = 0.0;
   __syncthreads();
   // squared norms from the LDS table (independent reads; a walk over the global rows was
@@ -262,7 +268,7 @@ __global__ void __launch_bounds__(kKmThreads)
                 elab = cur;
                 first = false;
               } else if (jok) {
-                sAcc[cur * DP + lane] += acc;
+                acc_g[(long long)cur * d + lane] += acc;
               }
               cur = lb[u];
               acc = 0.0;
@@ -274,7 +280,7 @@ __global__ void __launch_bounds__(kKmThreads)
           if (jok) edge[lane] = acc;
           elab = cur;
         } else if (jok) {
-          sAcc[cur * DP + lane] += acc;
+          acc_g[(long long)cur * d + lane] += acc;
         }
       }
       if (lane == 0) sEdgeLab[wave] = elab;
@@ -282,7 +288,7 @@ __global__ void __launch_bounds__(kKmThreads)
       if (tid < d)
         for (int w = 0; w < kKmThreads / 64; ++w) {
           const int c = sEdgeLab[w];
-          if (c >= 0) sAcc[c * DP + tid] += sEdge[w * DP + tid];
+          if (c >= 0) acc_g[(long long)c * d + tid] += sEdge[w * DP + tid];
         }
       for (int c = tid; c < k; c += kKmThreads) sCnt[c] += (double)sHist[c];
     }
@@ -290,8 +296,6 @@ __global__ void __launch_bounds__(kKmThreads)
   }
   if (psum != nullptr) {
     const long long slot = (long long)blockIdx.x * n_init + r;
-    double* ps = psum + slot * k * d;
-    for (int e = tid; e < k * d; e += kKmThreads) ps[e] = sAcc[(e / d) * DP + (e % d)];
     for (int c = tid; c < k; c += kKmThreads) pcnt[slot * k + c] = sCnt[c];
   }
 }
