@@ -144,7 +144,12 @@ class Harmony:
         else:
             self._fused = False
         self._init_cluster(init_backend)
-        self._harmonize(max_iter_harmony)
+        try:
+            self._harmonize(max_iter_harmony)
+        finally:
+            if getattr(self, "_order_next", None) is not None:
+                self._order_pool.shutdown(wait=True)
+                self._order_next = None
 
     # ------------------------------------------------------------------ init
     def _init_cluster(self, backend: str):
@@ -268,19 +273,36 @@ class Harmony:
         self.kmeans_rounds.append(i)
         self.objective_harmony.append(self.objective_kmeans[-1])
 
+    def _shuffled(self):
+        """The next round's block order (RandomState.shuffle of 0..N-1, the k-th call
+        for the k-th round whichever thread runs it) as pinned int32."""
+        order = np.arange(self.N)
+        self.rs.shuffle(order)
+        t = torch.from_numpy(order.astype(np.int32))
+        return t.pin_memory() if self.dev.type == "cuda" else t
+
     def _update_R(self):
         order = np.arange(self.N)
         if self._native:
-            self.rs.shuffle(order)
+            # the shuffle of 500k indices is ~10 ms of host time per round: the next
+            # round's order is drawn on a helper thread while the GPU runs this one (same
+            # RandomState sequence -- the draws stay in round order)
+            if getattr(self, "_order_next", None) is None:
+                import concurrent.futures as cf
+
+                self._order_pool = cf.ThreadPoolExecutor(max_workers=1)
+                self._order_next = self._order_pool.submit(self._shuffled)
+            order_h = self._order_next.result()
+            self._order_next = self._order_pool.submit(self._shuffled)
             n_blocks = int(math.ceil(1 / self.block_size))
             self.E = self.E.contiguous()
             self.O = self.O.contiguous()
             # one host->device copy of the round's order; blocks are device slices of it
-            order_d = torch.from_numpy(order.astype(np.int32)).to(self.dev, non_blocking=False)
+            order_d = order_h.to(self.dev, non_blocking=True)
             a = 0
-            for b in np.array_split(order, n_blocks):
-                cells = order_d[a:a + b.size]
-                a += b.size
+            for size in (len(b) for b in np.array_split(np.empty(self.N, np.int8), n_blocks)):
+                cells = order_d[a:a + size]
+                a += size
                 if self._fused:
                     ops.harmony_block_update(self.Rt, None, self.sigma, cells, self.bidx,
                                              self.E, self.O, self.Pr_b, self.theta, self._ws,

@@ -152,10 +152,16 @@ __global__ void __launch_bounds__(kKmThreads) __attribute__((amdgpu_waves_per_eu
           av0[ks] = row[0];
           av1[ks] = two ? row[16] : 0.0;
         }
+        if (two) {
 #pragma unroll
-        for (int ks = 0; ks < DP / 4; ++ks) {
-          a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0[ks], bx[ks], a0, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av1[ks], bx[ks], a1, 0, 0, 0);
+          for (int ks = 0; ks < DP / 4; ++ks) {
+            a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0[ks], bx[ks], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av1[ks], bx[ks], a1, 0, 0, 0);
+          }
+        } else {              // the odd last tile alone
+#pragma unroll
+          for (int ks = 0; ks < DP / 4; ++ks)
+            a0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0[ks], bx[ks], a0, 0, 0, 0);
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -531,12 +537,15 @@ extern "C" int cnmf_kmeans_blocks(int n) {
   return (n + per - 1) / per;
 }
 
+// padded dimension of the Lloyd kernel: a multiple of 16, or 52 for the common 50 PCs (13
+// MFMA k-steps instead of 16)
+static int km_dp(int d) { return d <= 48 ? (d + 15) / 16 * 16 : d <= 52 ? 52 : 64; }
+
 // Whether the LDS budget (160 KiB per CU) holds the transposed centroid table, the
 // accumulator and the label arrays of (k, d).
 extern "C" int cnmf_kmeans_fits(int k, int d) {
   if (k < 1 || k > cnmf::kKmThreads || d < 1 || d > 64) return 0;
-  const int dp = (d + 15) / 16 * 16;
-  return cnmf::km_lds_bytes(k, dp) <= 156 * 1024 ? 1 : 0;
+  return cnmf::km_lds_bytes(k, km_dp(d)) <= 156 * 1024 ? 1 : 0;
 }
 
 extern "C" hipError_t cnmf_kmeans_step(const double* X, long long ldx, int n, int d,
@@ -545,11 +554,11 @@ extern "C" hipError_t cnmf_kmeans_step(const double* X, long long ldx, int n, in
                                        hipStream_t stream) {
   if (n <= 0 || n_init <= 0) return hipSuccess;
   if (!cnmf_kmeans_fits(k, d)) return hipErrorInvalidValue;
-  const int dp = (d + 15) / 16 * 16;
-  switch (dp) {
+  switch (km_dp(d)) {
     case 16: return cnmf::launch_kmeans<16>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
     case 32: return cnmf::launch_kmeans<32>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
     case 48: return cnmf::launch_kmeans<48>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
+    case 52: return cnmf::launch_kmeans<52>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
     default: return cnmf::launch_kmeans<64>(X, ldx, n, d, C, k, n_init, live, labels, mind, psum, pcnt, stream);
   }
 }
