@@ -1,0 +1,214 @@
+"""NMFBatchSolver: the cell-sharded (DP) fused online step: packed reduce-scatter / all-
+gather (split out of models/nmf.py)."""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from .nmf_base import _FUSED_MAX_SLABS
+from .nmf_batch import _Batch
+
+
+class _DPMixin:
+    """NMFBatchSolver methods: the cell-sharded (DP) fused online step: packed reduce-
+    scatter / all-gather."""
+
+    # ------------------------------------------------------------------ DP fused step
+    def _fused_bufs_dp(self, st: _Batch, steps) -> dict:
+        """Workspaces of the cell-sharded fused step (_fused_pass_dp).  The replicates are
+        partitioned into ``world`` equal position chunks of Rr (the last rank's chunk may
+        hold fewer real ones); every exchanged buffer is padded to world * Rr positions so
+        each rank's chunk is one contiguous block for reduce-scatter / all-gather."""
+        comm = self.comm
+        xp = self._planes()
+        dev = self.X.device
+        G = self.X.shape[1]
+        (g,) = st.groups
+        K, R, world, me = g.K, g.n, comm.world_size, comm.rank
+        Rr = -(-R // world)
+        Rp = Rr * world
+        own0, own1 = min(R, me * Rr), min(R, (me + 1) * Rr)
+        cws = [b - a for (a, b), in steps]
+        bk = ops.planes_bk(xp.pb)
+        kd_max = max(-(-cw // bk) * bk for cw in cws)
+        ks_n = max(ops.gemm_plan(R * K, cw, xp.Gp, xp.pb)[1] for cw in cws)
+        # cooperative slice counts every rank uses (the partial-Gram exchange needs the
+        # same number of slots everywhere): from the widest step of ANY rank, and from
+        # the full chunk Rr for the W-solve
+        cw_max = comm.allreduce_max_int(max(cws))
+        S_h = ops.pipe_slices(cw_max, R, K, dev)
+        S_w = ops.pipe_slices(G, Rr, K, dev)
+        S_h = comm.allreduce_max_int(S_h or 0)
+        S_w = comm.allreduce_max_int(S_w or 0)
+        if not S_h or not S_w:
+            raise RuntimeError("DP fused step: no pipelined-solve slicing")
+        f32 = dict(device=dev, dtype=torch.float32)
+        wpl_n = ops.gemm_a_planes(xp.Gp)
+        # ONE reduce-scatter per online step: rank r's chunk is [dB rows of its replicates
+        # | their per-slice partial H^T H], and ONE all-gather: rank r's chunk is [the
+        # spectra bf16 planes of its replicates | their W W^T partials | lin | quad] as
+        # bytes -- the W-solve writes its outputs straight into that chunk
+        n_db, n_hh = Rr * K * G, Rr * S_h * K * K
+        pl_b, ww_b = wpl_n * Rr * K * xp.Gp * 2, Rr * S_w * K * K * 4
+        n_ag = pl_b + ww_b + 8 * Rr
+        rs_own = torch.empty(n_db + n_hh, **f32)
+        ag_own = torch.zeros(n_ag, device=dev, dtype=torch.uint8)
+        fb = {
+            "K": K, "R": R, "Rr": Rr, "Rp": Rp, "own": (own0, own1), "S_h": S_h, "S_w": S_w,
+            "wpl_n": wpl_n,
+            "wpl": torch.zeros((3, Rp * K, xp.Gp), device=dev, dtype=torch.int16),
+            "hpl": torch.zeros((3, R * K, kd_max), device=dev, dtype=torch.int16),
+            "slabN": torch.empty(ks_n * R * K * max(cws), **f32),
+            "dB": torch.zeros((Rp * K, G), **f32),
+            "B_own": torch.empty((Rr * K, G), **f32),
+            "A_own": [torch.empty((Rr, K, K), **f32) for _ in range(2)],
+            "HHp": torch.zeros((Rp, S_h, K, K), **f32),
+            "WWp": torch.zeros((Rp, S_w, K, K), **f32),
+            "lin": torch.zeros(Rp, **f32), "quad": torch.zeros(Rp, **f32),
+            "rs": torch.empty((world, n_db + n_hh), **f32), "rs_own": rs_own,
+            "dB_own": rs_own[:n_db].view(Rr * K, G),
+            "HHp_own": rs_own[n_db:].view(Rr, S_h, K, K),
+            "ag": torch.empty((world, n_ag), device=dev, dtype=torch.uint8), "ag_own": ag_own,
+            "ag_pl": ag_own[:pl_b].view(torch.int16).view(wpl_n, Rr * K, xp.Gp),
+            "ag_wwp": ag_own[pl_b:pl_b + ww_b].view(torch.float32).view(Rr, S_w, K, K),
+            "ag_lin": ag_own[pl_b + ww_b:pl_b + ww_b + 4 * Rr].view(torch.float32),
+            "ag_quad": ag_own[pl_b + ww_b + 4 * Rr:].view(torch.float32),
+            "ag_offs": (pl_b, ww_b),
+            "prepped": None,
+        }
+        return fb
+
+    @staticmethod
+    def _dp_pack_rs(fb: dict) -> None:
+        """[dB | HHp] of every replicate into the reduce-scatter buffer, rank-chunked."""
+        world, Rr, K = fb["rs"].shape[0], fb["Rr"], fb["K"]
+        n_db = fb["dB_own"].numel()
+        rs = fb["rs"]
+        rs[:, :n_db].copy_(fb["dB"].view(world, n_db))
+        rs[:, n_db:].copy_(fb["HHp"].view(world, -1))
+
+    @staticmethod
+    def _dp_unpack_ag(fb: dict, last: bool) -> None:
+        """Every rank's chunk of the all-gather into the full-batch planes, W W^T partials
+        and (last step) lin / quad."""
+        ag = fb["ag"]
+        world, Rr, K = ag.shape[0], fb["Rr"], fb["K"]
+        pl_b, ww_b = fb["ag_offs"]
+        wpl_n = fb["wpl_n"]
+        Gp = fb["wpl"].shape[2]
+        src = ag[:, :pl_b].view(torch.int16).view(world, wpl_n, Rr * K, Gp)
+        fb["wpl"][:wpl_n].view(wpl_n, world, Rr * K, Gp).copy_(src.transpose(0, 1))
+        fb["WWp"].view(world, -1).copy_(ag[:, pl_b:pl_b + ww_b].view(torch.float32))
+        if last:
+            o = pl_b + ww_b
+            fb["lin"].view(world, Rr).copy_(ag[:, o:o + 4 * Rr].view(torch.float32))
+            fb["quad"].view(world, Rr).copy_(ag[:, o + 4 * Rr:].view(torch.float32))
+
+    def _fused_pass_dp(self, st: _Batch, steps, fb: dict, final: bool) -> None:
+        """One online pass of the fused step on a cell shard (SURVEY.md §2.5c / §2.6 item
+        1).  Per online step every rank runs the numerator GEMM and the pipelined H-solve
+        on its cells of the global chunk and the statistics GEMM dB = H_loc^T X_loc; then
+        ONE reduce-scatter of the packed [dB | partial H^T H] hands each rank the
+        rank-summed statistics of ITS replicate chunk, the rank W-solves only those (1/world
+        of the spectra work) straight into its chunk of ONE all-gather of [bf16 spectra
+        planes | per-slice W W^T partials | lin | quad] -- two collectives per step (five
+        before the packing: dB, HHp, WWp and one per plane, +2 on the last step), the bytes
+        of one all-reduce of dB, the W-solve no longer replicated on every rank (the
+        unfused DP step all-reduces [dB | dA] and re-solves every replicate everywhere).
+        Same updates and stopping rules as the single-GPU fused step; rank-summed
+        statistics in RCCL's order."""
+        o = self.opts
+        comm = self.comm
+        xp = self._planes()
+        X = self.X
+        G = X.shape[1]
+        HT, W = st.views()
+        (g,) = st.groups
+        K, R, Rr, Rp = fb["K"], fb["R"], fb["Rr"], fb["Rp"]
+        own0, own1 = fb["own"]
+        n_own = own1 - own0
+        S_h, S_w = fb["S_h"], fb["S_w"]
+        active = st.active_mask()
+        n = st.n_act
+        h_it, w_it = st.h_iters[:n], st.w_iters[:n]
+        bk = ops.planes_bk(xp.pb)
+        rows = R * K
+        wpl, hpl_all = fb["wpl"], fb["hpl"]
+        if fb["prepped"] != st.uid:
+            # W is replicated at the start of a run: every rank forms every Gram / plane
+            fb["WWp"].zero_()
+            fb["WWp"][:R, 0].copy_(ops.gram(g.rep3(W)))
+            ops.split_planes(W, wpl[:, :rows], col_mul=xp.unit)
+            fb["wwp_n"] = 1
+            fb["prepped"] = st.uid
+        unit = xp.unit
+        wpl_n = ops.gemm_a_planes(xp.Gp)
+        o0, o1 = own0 * K, own1 * K
+        Wown = W[o0:o1].view(n_own, K, G) if n_own else None
+        last_s = len(steps) - 1
+        for s_, ((a, b),) in enumerate(steps):
+            cw = b - a
+            last = s_ == last_s
+            ks_n = ops.gemm_planes(None, wpl[:wpl_n, :rows], xp.x[:, a:], rows, cw, xp.Gp,
+                                   raw_slab=fb["slabN"], raw_max=_FUSED_MAX_SLABS)
+            kd = -(-cw // bk) * bk
+            hpl = hpl_all[:, :, :kd]
+            hpl_n = ops.gemm_a_planes(kd)
+            if cw > 0:
+                numer = fb["slabN"].as_strided((R, K, cw), (K * cw, cw, 1), 0)
+                ops.solve("mu", g.rep3(HT[:, a:b]), numer, None,
+                          max_iter=o.online_chunk_max_iter, tol=o.online_h_tol, eps=o.eps,
+                          iters_out=h_it, conv_mode=1, check_every=o.inner_check_every,
+                          active=active, planes=hpl, planes_n=hpl_n, numer_slabs=ks_n,
+                          numer_slab_stride=rows * cw, coop=S_h,
+                          gram_parts=fb["WWp"][:R], gram_parts_n=fb["wwp_n"],
+                          gram_parts_out=fb["HHp"][:R], coop_device_gen=True)
+                ops.gemm_planes(fb["dB"], hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd)
+            else:      # no cells of this chunk here: zero contributions
+                fb["dB"][:rows].zero_()
+                fb["HHp"][:R].zero_()
+            self._dp_pack_rs(fb)
+            comm.reduce_scatter_(fb["rs_own"], fb["rs"])
+            A_in, A_out = fb["A_own"][(s_ + 1) % 2], fb["A_own"][s_ % 2]
+            wwp = fb["ag_wwp"]
+            if n_own:
+                lin_o = fb["ag_lin"][:n_own]
+                quad_o = fb["ag_quad"][:n_own]
+                ops.solve(
+                    "mu", Wown, fb["dB_own"][:n_own * K].view(n_own, K, G),
+                    None if s_ == 0 else A_in[:n_own], max_iter=o.online_chunk_max_iter,
+                    tol=o.online_w_tol, eps=o.eps, lin_out=lin_o if last else None,
+                    quad_out=quad_o if last else None, iters_out=w_it[own0:own1],
+                    conv_mode=1, check_every=o.inner_check_every, active=active[own0:own1],
+                    planes=fb["ag_pl"][:, :n_own * K], planes_colmul=unit, planes_n=wpl_n,
+                    numer_scale=unit,
+                    numer_base=None if s_ == 0 else fb["B_own"][:n_own * K].view(n_own, K, G),
+                    numer_out=None if last else fb["B_own"][:n_own * K].view(n_own, K, G),
+                    gram_parts=fb["HHp_own"][:n_own], gram_parts_n=S_h,
+                    gram_out=None if last else A_out[:n_own],
+                    gram_parts_out=wwp[:n_own], coop=S_w, coop_device_gen=True)
+            fb["wwp_n"] = S_w
+            comm.all_gather_into_(fb["ag"], fb["ag_own"])
+            self._dp_unpack_ag(fb, last)
+        ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
+                        n, -1, o.tol, final=final, gate=st.gate,
+                        max_pass=int(o.online_max_pass))
+
+    def _dp_gather_w(self, st: _Batch, fb: dict) -> None:
+        """End of a DP fused run: every rank's W-solved spectra rows to every rank."""
+        _, W = st.views()
+        K, R, Rr, Rp = fb["K"], fb["R"], fb["Rr"], fb["Rp"]
+        G = W.shape[1]
+        me = self.comm.rank
+        Wp = torch.zeros((Rp * K, G), device=W.device, dtype=W.dtype)
+        o0, o1 = me * Rr * K, min(R, (me + 1) * Rr) * K
+        if o1 > o0:
+            Wp[o0:o1].copy_(W[o0:o1])
+        self.comm.all_gather_into_(Wp, Wp[me * Rr * K:(me + 1) * Rr * K])
+        W.copy_(Wp[:R * K])
+        it = torch.zeros(Rp, dtype=torch.int32, device=W.device)   # W-solve sweep counts
+        o0, o1 = me * Rr, min(R, (me + 1) * Rr)
+        if o1 > o0:
+            it[o0:o1].copy_(st.w_iters[o0:o1])
+        self.comm.all_gather_into_(it, it[me * Rr:(me + 1) * Rr])
+        st.w_iters[:R].copy_(it[:R])
