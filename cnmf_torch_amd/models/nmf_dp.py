@@ -53,6 +53,7 @@ class _DPMixin:
         n_ag = pl_b + ww_b + 8 * Rr
         rs_own = torch.empty(n_db + n_hh, **f32)
         ag_own = torch.zeros(n_ag, device=dev, dtype=torch.uint8)
+        self.dp_slices = (int(S_h), int(S_w))      # (diagnostics / tests)
         fb = {
             "K": K, "R": R, "Rr": Rr, "Rp": Rp, "own": (own0, own1), "S_h": S_h, "S_w": S_w,
             "wpl_n": wpl_n,

@@ -333,7 +333,10 @@ def dp_fused_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, fused, all
     (CNMF_DP_FUSED=1) or the all-reduced unfused step (0)."""
     os.environ["CNMF_DP_FUSED"] = fused
     os.environ["CNMF_ALLREDUCE"] = allreduce
-    os.environ["CNMF_SOLVE_COOP"] = "0"      # two processes on one GPU: no spinning slices
+    # the production cooperative-slice solves (S_h, S_w > 1): both processes share one
+    # GPU here, and a launch of these sizes is a few dozen workgroups -- every slice of
+    # both ranks' launches is resident at once
+    os.environ.pop("CNMF_SOLVE_COOP", None)
     _init(rank, world, port)
     from cnmf_torch_amd import ops
     from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions, _Batch
@@ -355,6 +358,8 @@ def dp_fused_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, fused, all
     tag = fused + ("x" if allreduce == "xgmi" else "")
     np.save(os.path.join(out_dir, f"dpf{tag}_{rank}.npz.npy"),
             np.array([took, bool(solver.comm._xgmi)], dtype=bool))
+    np.save(os.path.join(out_dir, f"dpfS{tag}_{rank}.npy"),
+            np.array(getattr(solver, "dp_slices", (0, 0)), dtype=np.int64))
     np.save(os.path.join(out_dir, f"dpfW{tag}_{rank}.npy"), res.W.cpu().numpy())
     np.save(os.path.join(out_dir, f"dpferr{tag}_{rank}.npy"), res.err)
     np.save(os.path.join(out_dir, f"dpfit{tag}_{rank}.npy"), res.n_iter)

@@ -78,10 +78,12 @@ def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
     partial Grams, each rank W-solving only its replicate chunk (R not a multiple of the
     world: a padded last chunk), all-gather of the spectra planes / W W^T partials /
     lin-quad -- factorises like the all-reduced unfused DP step: identical W on both
-    ranks, pass counts +-1, errors of same-pass replicates to 1e-5."""
-    X = normalized_counts_matrix(1600, 200, n_programs=6, seed=9)
+    ranks, pass counts +-1, errors of same-pass replicates to 1e-5.  Shapes large enough
+    that both solves run the production cooperative slices (800 cells per rank and step,
+    800 genes: S > 1 on both sides)."""
+    X = normalized_counts_matrix(3200, 800, n_programs=6, seed=9)
     seeds = list(range(31, 31 + R))
-    kw = dict(online_chunk_size=400, online_max_pass=12)
+    kw = dict(online_chunk_size=1600, online_max_pass=12)
     for fused in ("1", "0"):
         _spawn(W.dp_fused_worker, 2, X, K, seeds, kw, str(tmp_path), fused, timeout=150)
     # the packed step with its reduce-scatter / all-gather as one-shot xGMI kernels
@@ -89,6 +91,9 @@ def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
     for r in range(2):
         assert bool(np.load(tmp_path / f"dpf1_{r}.npz.npy")[0])
         assert not bool(np.load(tmp_path / f"dpf0_{r}.npz.npy")[0])
+        # the cooperative-slice solves ran multi-process (both sides sliced)
+        S_h, S_w = np.load(tmp_path / f"dpfS1_{r}.npy")
+        assert S_h > 1 and S_w > 1, (S_h, S_w)
         took, used = np.load(tmp_path / f"dpf1x_{r}.npz.npy")
         assert bool(took) and bool(used)
     Wf = np.load(tmp_path / "dpfW1_0.npy")
