@@ -564,9 +564,9 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
                 or self._planes() is None):
             return False
         if dp:
-            # the reduce-scattered W-solve partitions the replicates of ONE rank group
-            # (mixed-K DP batches take the unfused, all-reduced step)
-            if (len(st.groups) != 1 or os.environ.get("CNMF_DP_FUSED", "1") == "0"
+            # the reduce-scattered W-solve partitions the replicates of every K group of
+            # the batch over the ranks (mixed-K batches: one packed exchange per group)
+            if (os.environ.get("CNMF_DP_FUSED", "1") == "0"
                     or not hasattr(self.comm, "reduce_scatter_")):
                 return False
         G = self.X.shape[1]

@@ -15,15 +15,29 @@ class _DPMixin:
 
     # ------------------------------------------------------------------ DP fused step
     def _fused_bufs_dp(self, st: _Batch, steps) -> dict:
-        """Workspaces of the cell-sharded fused step (_fused_pass_dp).  The replicates are
+        """Workspaces of the cell-sharded fused step (_fused_pass_dp), per K group of the
+        batch (a cNMF K grid is one mixed-K batch).  Each group's replicates are
         partitioned into ``world`` equal position chunks of Rr (the last rank's chunk may
         hold fewer real ones); every exchanged buffer is padded to world * Rr positions so
         each rank's chunk is one contiguous block for reduce-scatter / all-gather."""
+        xp = self._planes()
+        dev = self.X.device
+        cws = [b - a for (a, b), in steps]
+        ks_n = max(ops.gemm_plan(g.n * g.K, cw, xp.Gp, xp.pb)[1] for cw in cws
+                   for g in st.groups)
+        rows_max = max(g.n * g.K for g in st.groups)
+        f32 = dict(device=dev, dtype=torch.float32)
+        groups = [self._fused_bufs_dp_group(g, steps) for g in st.groups]
+        self.dp_slices = (min(f["S_h"] for f in groups), min(f["S_w"] for f in groups))
+        return {"groups": groups, "prepped": None,
+                "slabN": torch.empty(ks_n * rows_max * max(cws), **f32),
+                "lin": torch.zeros(st.n_act, **f32), "quad": torch.zeros(st.n_act, **f32)}
+
+    def _fused_bufs_dp_group(self, g, steps) -> dict:
         comm = self.comm
         xp = self._planes()
         dev = self.X.device
         G = self.X.shape[1]
-        (g,) = st.groups
         K, R, world, me = g.K, g.n, comm.world_size, comm.rank
         Rr = -(-R // world)
         Rp = Rr * world
@@ -31,7 +45,6 @@ class _DPMixin:
         cws = [b - a for (a, b), in steps]
         bk = ops.planes_bk(xp.pb)
         kd_max = max(-(-cw // bk) * bk for cw in cws)
-        ks_n = max(ops.gemm_plan(R * K, cw, xp.Gp, xp.pb)[1] for cw in cws)
         # cooperative slice counts every rank uses (the partial-Gram exchange needs the
         # same number of slots everywhere): from the widest step of ANY rank, and from
         # the full chunk Rr for the W-solve
@@ -44,22 +57,20 @@ class _DPMixin:
             raise RuntimeError("DP fused step: no pipelined-solve slicing")
         f32 = dict(device=dev, dtype=torch.float32)
         wpl_n = ops.gemm_a_planes(xp.Gp)
-        # ONE reduce-scatter per online step: rank r's chunk is [dB rows of its replicates
-        # | their per-slice partial H^T H], and ONE all-gather: rank r's chunk is [the
-        # spectra bf16 planes of its replicates | their W W^T partials | lin | quad] as
-        # bytes -- the W-solve writes its outputs straight into that chunk
+        # ONE reduce-scatter per online step and group: rank r's chunk is [dB rows of its
+        # replicates | their per-slice partial H^T H], and ONE all-gather: rank r's chunk
+        # is [the spectra bf16 planes of its replicates | their W W^T partials | lin |
+        # quad] as bytes -- the W-solve writes its outputs straight into that chunk
         n_db, n_hh = Rr * K * G, Rr * S_h * K * K
         pl_b, ww_b = wpl_n * Rr * K * xp.Gp * 2, Rr * S_w * K * K * 4
         n_ag = pl_b + ww_b + 8 * Rr
         rs_own = torch.empty(n_db + n_hh, **f32)
         ag_own = torch.zeros(n_ag, device=dev, dtype=torch.uint8)
-        self.dp_slices = (int(S_h), int(S_w))      # (diagnostics / tests)
-        fb = {
+        return {
             "K": K, "R": R, "Rr": Rr, "Rp": Rp, "own": (own0, own1), "S_h": S_h, "S_w": S_w,
             "wpl_n": wpl_n,
             "wpl": torch.zeros((3, Rp * K, xp.Gp), device=dev, dtype=torch.int16),
             "hpl": torch.zeros((3, R * K, kd_max), device=dev, dtype=torch.int16),
-            "slabN": torch.empty(ks_n * R * K * max(cws), **f32),
             "dB": torch.zeros((Rp * K, G), **f32),
             "B_own": torch.empty((Rr * K, G), **f32),
             "A_own": [torch.empty((Rr, K, K), **f32) for _ in range(2)],
@@ -75,14 +86,14 @@ class _DPMixin:
             "ag_lin": ag_own[pl_b + ww_b:pl_b + ww_b + 4 * Rr].view(torch.float32),
             "ag_quad": ag_own[pl_b + ww_b + 4 * Rr:].view(torch.float32),
             "ag_offs": (pl_b, ww_b),
-            "prepped": None,
+            "wwp_n": 1,
         }
-        return fb
 
     @staticmethod
     def _dp_pack_rs(fb: dict) -> None:
-        """[dB | HHp] of every replicate into the reduce-scatter buffer, rank-chunked."""
-        world, Rr, K = fb["rs"].shape[0], fb["Rr"], fb["K"]
+        """[dB | HHp] of every replicate of a group into its reduce-scatter buffer,
+        rank-chunked."""
+        world = fb["rs"].shape[0]
         n_db = fb["dB_own"].numel()
         rs = fb["rs"]
         rs[:, :n_db].copy_(fb["dB"].view(world, n_db))
@@ -90,8 +101,8 @@ class _DPMixin:
 
     @staticmethod
     def _dp_unpack_ag(fb: dict, last: bool) -> None:
-        """Every rank's chunk of the all-gather into the full-batch planes, W W^T partials
-        and (last step) lin / quad."""
+        """Every rank's chunk of a group's all-gather into the group's planes, W W^T
+        partials and (last step) lin / quad."""
         ag = fb["ag"]
         world, Rr, K = ag.shape[0], fb["Rr"], fb["K"]
         pl_b, ww_b = fb["ag_offs"]
@@ -105,111 +116,128 @@ class _DPMixin:
             fb["lin"].view(world, Rr).copy_(ag[:, o:o + 4 * Rr].view(torch.float32))
             fb["quad"].view(world, Rr).copy_(ag[:, o + 4 * Rr:].view(torch.float32))
 
-    def _fused_pass_dp(self, st: _Batch, steps, fb: dict, final: bool) -> None:
+    def _fused_pass_dp(self, st: _Batch, steps, fball: dict, final: bool) -> None:
         """One online pass of the fused step on a cell shard (SURVEY.md §2.5c / §2.6 item
-        1).  Per online step every rank runs the numerator GEMM and the pipelined H-solve
-        on its cells of the global chunk and the statistics GEMM dB = H_loc^T X_loc; then
-        ONE reduce-scatter of the packed [dB | partial H^T H] hands each rank the
-        rank-summed statistics of ITS replicate chunk, the rank W-solves only those (1/world
-        of the spectra work) straight into its chunk of ONE all-gather of [bf16 spectra
-        planes | per-slice W W^T partials | lin | quad] -- two collectives per step (five
-        before the packing: dB, HHp, WWp and one per plane, +2 on the last step), the bytes
-        of one all-reduce of dB, the W-solve no longer replicated on every rank (the
-        unfused DP step all-reduces [dB | dA] and re-solves every replicate everywhere).
-        Same updates and stopping rules as the single-GPU fused step; rank-summed
-        statistics in RCCL's order."""
+        1).  Per online step, and per K group of the batch, every rank runs the numerator
+        GEMM and the pipelined H-solve on its cells of the global chunk and the statistics
+        GEMM dB = H_loc^T X_loc; then ONE reduce-scatter of the packed [dB | partial H^T H]
+        hands each rank the rank-summed statistics of ITS replicate chunk, the rank
+        W-solves only those (1/world of the spectra work) straight into its chunk of ONE
+        all-gather of [bf16 spectra planes | per-slice W W^T partials | lin | quad] -- two
+        collectives per step and group (five before the packing: dB, HHp, WWp and one per
+        plane, +2 on the last step), the bytes of one all-reduce of dB, the W-solve no
+        longer replicated on every rank (the unfused DP step all-reduces [dB | dA] and
+        re-solves every replicate everywhere).  Same updates and stopping rules as the
+        single-GPU fused step; rank-summed statistics in RCCL's order."""
         o = self.opts
-        comm = self.comm
         xp = self._planes()
-        X = self.X
-        G = X.shape[1]
         HT, W = st.views()
-        (g,) = st.groups
-        K, R, Rr, Rp = fb["K"], fb["R"], fb["Rr"], fb["Rp"]
-        own0, own1 = fb["own"]
-        n_own = own1 - own0
-        S_h, S_w = fb["S_h"], fb["S_w"]
         active = st.active_mask()
         n = st.n_act
-        h_it, w_it = st.h_iters[:n], st.w_iters[:n]
-        bk = ops.planes_bk(xp.pb)
-        rows = R * K
-        wpl, hpl_all = fb["wpl"], fb["hpl"]
-        if fb["prepped"] != st.uid:
+        if fball["prepped"] != st.uid:
             # W is replicated at the start of a run: every rank forms every Gram / plane
-            fb["WWp"].zero_()
-            fb["WWp"][:R, 0].copy_(ops.gram(g.rep3(W)))
-            ops.split_planes(W, wpl[:, :rows], col_mul=xp.unit)
-            fb["wwp_n"] = 1
-            fb["prepped"] = st.uid
-        unit = xp.unit
-        wpl_n = ops.gemm_a_planes(xp.Gp)
-        o0, o1 = own0 * K, own1 * K
-        Wown = W[o0:o1].view(n_own, K, G) if n_own else None
+            for g, fb in zip(st.groups, fball["groups"]):
+                fb["WWp"].zero_()
+                fb["WWp"][:g.n, 0].copy_(ops.gram(g.rep3(W)))
+                ops.split_planes(W[g.rows], fb["wpl"][:, :g.n * g.K], col_mul=xp.unit)
+                fb["wwp_n"] = 1
+            fball["prepped"] = st.uid
         last_s = len(steps) - 1
         for s_, ((a, b),) in enumerate(steps):
-            cw = b - a
-            last = s_ == last_s
-            ks_n = ops.gemm_planes(None, wpl[:wpl_n, :rows], xp.x[:, a:], rows, cw, xp.Gp,
-                                   raw_slab=fb["slabN"], raw_max=_FUSED_MAX_SLABS)
-            kd = -(-cw // bk) * bk
-            hpl = hpl_all[:, :, :kd]
-            hpl_n = ops.gemm_a_planes(kd)
-            if cw > 0:
-                numer = fb["slabN"].as_strided((R, K, cw), (K * cw, cw, 1), 0)
-                ops.solve("mu", g.rep3(HT[:, a:b]), numer, None,
-                          max_iter=o.online_chunk_max_iter, tol=o.online_h_tol, eps=o.eps,
-                          iters_out=h_it, conv_mode=1, check_every=o.inner_check_every,
-                          active=active, planes=hpl, planes_n=hpl_n, numer_slabs=ks_n,
-                          numer_slab_stride=rows * cw, coop=S_h,
-                          gram_parts=fb["WWp"][:R], gram_parts_n=fb["wwp_n"],
-                          gram_parts_out=fb["HHp"][:R], coop_device_gen=True)
-                ops.gemm_planes(fb["dB"], hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd)
-            else:      # no cells of this chunk here: zero contributions
-                fb["dB"][:rows].zero_()
-                fb["HHp"][:R].zero_()
-            self._dp_pack_rs(fb)
-            comm.reduce_scatter_(fb["rs_own"], fb["rs"])
-            A_in, A_out = fb["A_own"][(s_ + 1) % 2], fb["A_own"][s_ % 2]
-            wwp = fb["ag_wwp"]
-            if n_own:
-                lin_o = fb["ag_lin"][:n_own]
-                quad_o = fb["ag_quad"][:n_own]
-                ops.solve(
-                    "mu", Wown, fb["dB_own"][:n_own * K].view(n_own, K, G),
-                    None if s_ == 0 else A_in[:n_own], max_iter=o.online_chunk_max_iter,
-                    tol=o.online_w_tol, eps=o.eps, lin_out=lin_o if last else None,
-                    quad_out=quad_o if last else None, iters_out=w_it[own0:own1],
-                    conv_mode=1, check_every=o.inner_check_every, active=active[own0:own1],
-                    planes=fb["ag_pl"][:, :n_own * K], planes_colmul=unit, planes_n=wpl_n,
-                    numer_scale=unit,
-                    numer_base=None if s_ == 0 else fb["B_own"][:n_own * K].view(n_own, K, G),
-                    numer_out=None if last else fb["B_own"][:n_own * K].view(n_own, K, G),
-                    gram_parts=fb["HHp_own"][:n_own], gram_parts_n=S_h,
-                    gram_out=None if last else A_out[:n_own],
-                    gram_parts_out=wwp[:n_own], coop=S_w, coop_device_gen=True)
-            fb["wwp_n"] = S_w
-            comm.all_gather_into_(fb["ag"], fb["ag_own"])
-            self._dp_unpack_ag(fb, last)
-        ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
+            for g, fb in zip(st.groups, fball["groups"]):
+                self._dp_group_step(st, g, fb, fball["slabN"], HT, W, active, a, b, s_,
+                                    s_ == last_s)
+        lin, quad = fball["lin"], fball["quad"]
+        for g, fb in zip(st.groups, fball["groups"]):
+            lin[g.pos].copy_(fb["lin"][:g.n])
+            quad[g.pos].copy_(fb["quad"][:g.n])
+        ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
                         n, -1, o.tol, final=final, gate=st.gate,
                         max_pass=int(o.online_max_pass))
 
-    def _dp_gather_w(self, st: _Batch, fb: dict) -> None:
+    def _dp_group_step(self, st: _Batch, g, fb: dict, slabN, HT, W, active, a: int, b: int,
+                       s_: int, last: bool) -> None:
+        """One online step of one K group (see _fused_pass_dp)."""
+        o = self.opts
+        comm = self.comm
+        xp = self._planes()
+        G = self.X.shape[1]
+        K, R = fb["K"], fb["R"]
+        own0, own1 = fb["own"]
+        n_own = own1 - own0
+        S_h, S_w = fb["S_h"], fb["S_w"]
+        pos = g.pos
+        act_g = active[pos]
+        h_it, w_it = st.h_iters[pos], st.w_iters[pos]
+        bk = ops.planes_bk(xp.pb)
+        rows = R * K
+        wpl, hpl_all = fb["wpl"], fb["hpl"]
+        unit = xp.unit
+        wpl_n = fb["wpl_n"]
+        W_g = W[g.rows]
+        o0, o1 = own0 * K, own1 * K
+        Wown = W_g[o0:o1].view(n_own, K, G) if n_own else None
+        cw = b - a
+        ks_n = ops.gemm_planes(None, wpl[:wpl_n, :rows], xp.x[:, a:], rows, cw, xp.Gp,
+                               raw_slab=slabN, raw_max=_FUSED_MAX_SLABS)
+        kd = -(-cw // bk) * bk
+        hpl = hpl_all[:, :, :kd]
+        hpl_n = ops.gemm_a_planes(kd)
+        if cw > 0:
+            numer = slabN.as_strided((R, K, cw), (K * cw, cw, 1), 0)
+            ops.solve("mu", g.rep3(HT[:, a:b]), numer, None,
+                      max_iter=o.online_chunk_max_iter, tol=o.online_h_tol, eps=o.eps,
+                      iters_out=h_it, conv_mode=1, check_every=o.inner_check_every,
+                      active=act_g, planes=hpl, planes_n=hpl_n, numer_slabs=ks_n,
+                      numer_slab_stride=rows * cw, coop=S_h,
+                      gram_parts=fb["WWp"][:R], gram_parts_n=fb["wwp_n"],
+                      gram_parts_out=fb["HHp"][:R], coop_device_gen=True)
+            ops.gemm_planes(fb["dB"], hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd)
+        else:      # no cells of this chunk here: zero contributions
+            fb["dB"][:rows].zero_()
+            fb["HHp"][:R].zero_()
+        self._dp_pack_rs(fb)
+        comm.reduce_scatter_(fb["rs_own"], fb["rs"])
+        A_in, A_out = fb["A_own"][(s_ + 1) % 2], fb["A_own"][s_ % 2]
+        wwp = fb["ag_wwp"]
+        if n_own:
+            lin_o = fb["ag_lin"][:n_own]
+            quad_o = fb["ag_quad"][:n_own]
+            ops.solve(
+                "mu", Wown, fb["dB_own"][:n_own * K].view(n_own, K, G),
+                None if s_ == 0 else A_in[:n_own], max_iter=o.online_chunk_max_iter,
+                tol=o.online_w_tol, eps=o.eps, lin_out=lin_o if last else None,
+                quad_out=quad_o if last else None, iters_out=w_it[own0:own1],
+                conv_mode=1, check_every=o.inner_check_every, active=act_g[own0:own1],
+                planes=fb["ag_pl"][:, :n_own * K], planes_colmul=unit, planes_n=wpl_n,
+                numer_scale=unit,
+                numer_base=None if s_ == 0 else fb["B_own"][:n_own * K].view(n_own, K, G),
+                numer_out=None if last else fb["B_own"][:n_own * K].view(n_own, K, G),
+                gram_parts=fb["HHp_own"][:n_own], gram_parts_n=S_h,
+                gram_out=None if last else A_out[:n_own],
+                gram_parts_out=wwp[:n_own], coop=S_w, coop_device_gen=True)
+        fb["wwp_n"] = S_w
+        comm.all_gather_into_(fb["ag"], fb["ag_own"])
+        self._dp_unpack_ag(fb, last)
+
+    def _dp_gather_w(self, st: _Batch, fball: dict) -> None:
         """End of a DP fused run: every rank's W-solved spectra rows to every rank."""
         _, W = st.views()
-        K, R, Rr, Rp = fb["K"], fb["R"], fb["Rr"], fb["Rp"]
-        G = W.shape[1]
         me = self.comm.rank
-        Wp = torch.zeros((Rp * K, G), device=W.device, dtype=W.dtype)
-        o0, o1 = me * Rr * K, min(R, (me + 1) * Rr) * K
-        if o1 > o0:
-            Wp[o0:o1].copy_(W[o0:o1])
-        self.comm.all_gather_into_(Wp, Wp[me * Rr * K:(me + 1) * Rr * K])
-        W.copy_(Wp[:R * K])
-        it = torch.zeros(Rp, dtype=torch.int32, device=W.device)   # W-solve sweep counts
-        o0, o1 = me * Rr, min(R, (me + 1) * Rr)
-        if o1 > o0:
-            it[o0:o1].copy_(st.w_iters[o0:o1])
-        self.comm.all_gather_into_(it, it[me * Rr:(me + 1) * Rr])
-        st.w_iters[:R].copy_(it[:R])
+        for g, fb in zip(st.groups, fball["groups"]):
+            K, R, Rr, Rp = fb["K"], fb["R"], fb["Rr"], fb["Rp"]
+            W_g = W[g.rows]
+            G = W.shape[1]
+            Wp = torch.zeros((Rp * K, G), device=W.device, dtype=W.dtype)
+            o0, o1 = me * Rr * K, min(R, (me + 1) * Rr) * K
+            if o1 > o0:
+                Wp[o0:o1].copy_(W_g[o0:o1])
+            self.comm.all_gather_into_(Wp, Wp[me * Rr * K:(me + 1) * Rr * K])
+            W_g.copy_(Wp[:R * K])
+            it = torch.zeros(Rp, dtype=torch.int32, device=W.device)   # W-solve sweeps
+            o0, o1 = me * Rr, min(R, (me + 1) * Rr)
+            wi = st.w_iters[g.pos]
+            if o1 > o0:
+                it[o0:o1].copy_(wi[o0:o1])
+            self.comm.all_gather_into_(it, it[me * Rr:(me + 1) * Rr])
+            wi[:R].copy_(it[:R])

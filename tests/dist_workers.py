@@ -349,12 +349,13 @@ def dp_fused_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, fused, all
     segs = dp_row_segments(X.shape[0], opts_kw["online_chunk_size"], rank, world)
     row_map, sched = dp_layout(segs)
     Xl = torch.from_numpy(np.concatenate([X[a:b] for a, b in segs])).cuda()
-    solver = NMFBatchSolver(Xl, NMFOptions(n_components=K, **opts_kw), comm=DistComm(),
+    ks = list(K) if isinstance(K, (list, tuple)) else [K] * len(seeds)   # mixed-K batch
+    solver = NMFBatchSolver(Xl, NMFOptions(n_components=ks[0], **opts_kw), comm=DistComm(),
                             row_map=row_map, schedule=sched)
-    st = _Batch(torch.zeros((K * len(seeds), Xl.shape[0]), device="cuda"),
-                torch.zeros((K * len(seeds), Xl.shape[1]), device="cuda"), [K] * len(seeds))
+    st = _Batch(torch.zeros((sum(ks), Xl.shape[0]), device="cuda"),
+                torch.zeros((sum(ks), Xl.shape[1]), device="cuda"), sorted(ks))
     took = solver._fused_ok(st, solver._steps(Xl.shape[0]))
-    res = solver.run(seeds)
+    res = solver.run(seeds, ks=ks)
     tag = fused + ("x" if allreduce == "xgmi" else "")
     np.save(os.path.join(out_dir, f"dpf{tag}_{rank}.npz.npy"),
             np.array([took, bool(solver.comm._xgmi)], dtype=bool))

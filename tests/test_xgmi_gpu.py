@@ -72,13 +72,14 @@ def test_xgmi_reduce_scatter_all_gather_match_gloo(tmp_path):
         np.testing.assert_array_equal(z["comm_ag"], np.repeat([7, 8], 4).astype(np.int16))
 
 
-@pytest.mark.parametrize("K,R", [(6, 7), (20, 6)])
+@pytest.mark.parametrize("K,R", [(6, 7), (20, 6), ((5, 5, 5, 8, 8, 8, 8), 7)])
 def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
     """Cell-sharded DP with the fused step -- reduce-scatter of dB and the per-slice
     partial Grams, each rank W-solving only its replicate chunk (R not a multiple of the
     world: a padded last chunk), all-gather of the spectra planes / W W^T partials /
     lin-quad -- factorises like the all-reduced unfused DP step: identical W on both
-    ranks, pass counts +-1, errors of same-pass replicates to 1e-5.  Shapes large enough
+    ranks, pass counts +-1, errors of same-pass replicates to 1e-5.  The third case is a
+    mixed-K batch (a cNMF K grid): one packed exchange per K group and step.  Shapes large enough
     that both solves run the production cooperative slices (800 cells per rank and step,
     800 genes: S > 1 on both sides)."""
     X = normalized_counts_matrix(3200, 800, n_programs=6, seed=9)
