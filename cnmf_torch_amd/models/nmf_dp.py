@@ -6,7 +6,29 @@ import torch
 
 from .. import ops
 from .nmf_base import _FUSED_MAX_SLABS
-from .nmf_batch import _Batch
+from .nmf_batch import _Batch, _Group
+
+# split a single-K batch into two exchange units (halves of its replicates), so each
+# half's reduce-scatter / all-gather runs under the other half's compute.  Off: measured
+# on MI355X (emulated 8-rank shard, 1M cells x 2000 genes, K=10, 100 replicates) the
+# halves' per-rank compute is 0.074 s per step against 0.043 s for one unit -- twice the
+# launches of half the size on a launch-bound step -- more than the 0.014 s of
+# collectives an ideal overlap could hide (profiles/r5z_emu8_1m_split.json)
+_DP_SPLIT = False
+
+
+def _dp_units(groups, world: int, split: bool | None = None) -> list:
+    """The exchange units of a DP fused step: the batch's K groups (a cNMF K grid), or --
+    with ``split`` (default _DP_SPLIT) and a batch of ONE K -- its two halves when each
+    keeps at least one replicate per rank.  Units are issued in turn, so each unit's
+    collectives overlap the other units' compute (_fused_pass_dp)."""
+    split = _DP_SPLIT if split is None else split
+    if len(groups) != 1 or not split or groups[0].n < 2 * world:
+        return list(groups)
+    g = groups[0]
+    h = (g.n + 1) // 2
+    return [_Group(g.K, g.p0, h, g.r0, g.q0),
+            _Group(g.K, g.p0 + h, g.n - h, g.r0 + h * g.K, g.q0 + h * g.K * g.K)]
 
 
 class _DPMixin:
@@ -23,14 +45,16 @@ class _DPMixin:
         xp = self._planes()
         dev = self.X.device
         cws = [b - a for (a, b), in steps]
-        ks_n = max(ops.gemm_plan(g.n * g.K, cw, xp.Gp, xp.pb)[1] for cw in cws
-                   for g in st.groups)
-        rows_max = max(g.n * g.K for g in st.groups)
+        units = _dp_units(st.groups, self.comm.world_size)
+        # the numerator slab of the widest unit's GEMM plan (a half's split can be deeper)
+        slab = max(ops.gemm_plan(g.n * g.K, cw, xp.Gp, xp.pb)[1] * g.n * g.K * cw
+                   for cw in cws for g in units)
         f32 = dict(device=dev, dtype=torch.float32)
-        groups = [self._fused_bufs_dp_group(g, steps) for g in st.groups]
+        groups = [self._fused_bufs_dp_group(g, steps) for g in units]
         self.dp_slices = (min(f["S_h"] for f in groups), min(f["S_w"] for f in groups))
-        return {"groups": groups, "prepped": None,
-                "slabN": torch.empty(ks_n * rows_max * max(cws), **f32),
+        self.dp_units = len(units)
+        return {"units": units, "groups": groups, "prepped": None,
+                "slabN": torch.empty(slab, **f32),
                 "lin": torch.zeros(st.n_act, **f32), "quad": torch.zeros(st.n_act, **f32)}
 
     def _fused_bufs_dp_group(self, g, steps) -> dict:
@@ -136,47 +160,55 @@ class _DPMixin:
         n = st.n_act
         if fball["prepped"] != st.uid:
             # W is replicated at the start of a run: every rank forms every Gram / plane
-            for g, fb in zip(st.groups, fball["groups"]):
+            for g, fb in zip(fball["units"], fball["groups"]):
                 fb["WWp"].zero_()
                 fb["WWp"][:g.n, 0].copy_(ops.gram(g.rep3(W)))
                 ops.split_planes(W[g.rows], fb["wpl"][:, :g.n * g.K], col_mul=xp.unit)
                 fb["wwp_n"] = 1
             fball["prepped"] = st.uid
+        units = list(zip(fball["units"], fball["groups"]))
         last_s = len(steps) - 1
+        ag_wait = [None] * len(units)
         for s_, ((a, b),) in enumerate(steps):
-            for g, fb in zip(st.groups, fball["groups"]):
-                self._dp_group_step(st, g, fb, fball["slabN"], HT, W, active, a, b, s_,
-                                    s_ == last_s)
+            # phase 1, per unit: (previous step's all-gather in) numerator GEMM, H-solve,
+            # dB GEMM, reduce-scatter issued -- it runs under the next unit's phase 1
+            rs_wait = []
+            for u, (g, fb) in enumerate(units):
+                if ag_wait[u] is not None:
+                    ag_wait[u].wait()
+                    self._dp_unpack_ag(fb, False)
+                rs_wait.append(self._dp_unit_stats(st, g, fb, fball["slabN"], HT, active,
+                                                   a, b))
+            # phase 2, per unit: W-solve of the owned replicates, all-gather issued -- it
+            # runs under the next unit's W-solve (and the next step's phase 1)
+            for u, (g, fb) in enumerate(units):
+                rs_wait[u].wait()
+                ag_wait[u] = self._dp_unit_wsolve(st, g, fb, W, active, s_, s_ == last_s)
+        for u, (g, fb) in enumerate(units):
+            ag_wait[u].wait()
+            self._dp_unpack_ag(fb, True)
         lin, quad = fball["lin"], fball["quad"]
-        for g, fb in zip(st.groups, fball["groups"]):
+        for g, fb in units:
             lin[g.pos].copy_(fb["lin"][:g.n])
             quad[g.pos].copy_(fb["quad"][:g.n])
         ops.conv_update(lin, quad, self.x_sq, {k: v[:n] for k, v in st.state.items()},
                         n, -1, o.tol, final=final, gate=st.gate,
                         max_pass=int(o.online_max_pass))
 
-    def _dp_group_step(self, st: _Batch, g, fb: dict, slabN, HT, W, active, a: int, b: int,
-                       s_: int, last: bool) -> None:
-        """One online step of one K group (see _fused_pass_dp)."""
+    def _dp_unit_stats(self, st: _Batch, g, fb: dict, slabN, HT, active, a: int, b: int):
+        """Phase 1 of one unit's online step (see _fused_pass_dp): numerator GEMM and
+        pipelined H-solve on this rank's cells of chunk [a, b), the statistics GEMM dB,
+        then the packed reduce-scatter, issued in the background; returns its handle."""
         o = self.opts
-        comm = self.comm
         xp = self._planes()
-        G = self.X.shape[1]
         K, R = fb["K"], fb["R"]
-        own0, own1 = fb["own"]
-        n_own = own1 - own0
-        S_h, S_w = fb["S_h"], fb["S_w"]
         pos = g.pos
         act_g = active[pos]
-        h_it, w_it = st.h_iters[pos], st.w_iters[pos]
+        h_it = st.h_iters[pos]
         bk = ops.planes_bk(xp.pb)
         rows = R * K
         wpl, hpl_all = fb["wpl"], fb["hpl"]
-        unit = xp.unit
         wpl_n = fb["wpl_n"]
-        W_g = W[g.rows]
-        o0, o1 = own0 * K, own1 * K
-        Wown = W_g[o0:o1].view(n_own, K, G) if n_own else None
         cw = b - a
         ks_n = ops.gemm_planes(None, wpl[:wpl_n, :rows], xp.x[:, a:], rows, cw, xp.Gp,
                                raw_slab=slabN, raw_max=_FUSED_MAX_SLABS)
@@ -189,15 +221,32 @@ class _DPMixin:
                       max_iter=o.online_chunk_max_iter, tol=o.online_h_tol, eps=o.eps,
                       iters_out=h_it, conv_mode=1, check_every=o.inner_check_every,
                       active=act_g, planes=hpl, planes_n=hpl_n, numer_slabs=ks_n,
-                      numer_slab_stride=rows * cw, coop=S_h,
+                      numer_slab_stride=rows * cw, coop=fb["S_h"],
                       gram_parts=fb["WWp"][:R], gram_parts_n=fb["wwp_n"],
                       gram_parts_out=fb["HHp"][:R], coop_device_gen=True)
-            ops.gemm_planes(fb["dB"], hpl[:hpl_n], xp.xt[:, :, a:], rows, G, kd)
+            ops.gemm_planes(fb["dB"], hpl[:hpl_n], xp.xt[:, :, a:], rows, self.X.shape[1], kd)
         else:      # no cells of this chunk here: zero contributions
             fb["dB"][:rows].zero_()
             fb["HHp"][:R].zero_()
         self._dp_pack_rs(fb)
-        comm.reduce_scatter_(fb["rs_own"], fb["rs"])
+        return self.comm.reduce_scatter_async(fb["rs_own"], fb["rs"])
+
+    def _dp_unit_wsolve(self, st: _Batch, g, fb: dict, W, active, s_: int, last: bool):
+        """Phase 2 of one unit's online step: W-solve of the replicates this rank owns,
+        from the rank-summed statistics the reduce-scatter delivered, straight into its
+        chunk of the packed all-gather, issued in the background; returns its handle."""
+        o = self.opts
+        xp = self._planes()
+        G = self.X.shape[1]
+        K = fb["K"]
+        own0, own1 = fb["own"]
+        n_own = own1 - own0
+        pos = g.pos
+        act_g = active[pos]
+        w_it = st.w_iters[pos]
+        unit = xp.unit
+        W_g = W[g.rows]
+        Wown = W_g[own0 * K:own1 * K].view(n_own, K, G) if n_own else None
         A_in, A_out = fb["A_own"][(s_ + 1) % 2], fb["A_own"][s_ % 2]
         wwp = fb["ag_wwp"]
         if n_own:
@@ -209,22 +258,21 @@ class _DPMixin:
                 tol=o.online_w_tol, eps=o.eps, lin_out=lin_o if last else None,
                 quad_out=quad_o if last else None, iters_out=w_it[own0:own1],
                 conv_mode=1, check_every=o.inner_check_every, active=act_g[own0:own1],
-                planes=fb["ag_pl"][:, :n_own * K], planes_colmul=unit, planes_n=wpl_n,
+                planes=fb["ag_pl"][:, :n_own * K], planes_colmul=unit, planes_n=fb["wpl_n"],
                 numer_scale=unit,
                 numer_base=None if s_ == 0 else fb["B_own"][:n_own * K].view(n_own, K, G),
                 numer_out=None if last else fb["B_own"][:n_own * K].view(n_own, K, G),
-                gram_parts=fb["HHp_own"][:n_own], gram_parts_n=S_h,
+                gram_parts=fb["HHp_own"][:n_own], gram_parts_n=fb["S_h"],
                 gram_out=None if last else A_out[:n_own],
-                gram_parts_out=wwp[:n_own], coop=S_w, coop_device_gen=True)
-        fb["wwp_n"] = S_w
-        comm.all_gather_into_(fb["ag"], fb["ag_own"])
-        self._dp_unpack_ag(fb, last)
+                gram_parts_out=wwp[:n_own], coop=fb["S_w"], coop_device_gen=True)
+        fb["wwp_n"] = fb["S_w"]
+        return self.comm.all_gather_into_async(fb["ag"], fb["ag_own"])
 
     def _dp_gather_w(self, st: _Batch, fball: dict) -> None:
         """End of a DP fused run: every rank's W-solved spectra rows to every rank."""
         _, W = st.views()
         me = self.comm.rank
-        for g, fb in zip(st.groups, fball["groups"]):
+        for g, fb in zip(fball["units"], fball["groups"]):
             K, R, Rr, Rp = fb["K"], fb["R"], fb["Rr"], fb["Rp"]
             W_g = W[g.rows]
             G = W.shape[1]

@@ -14,6 +14,29 @@ from __future__ import annotations
 import torch
 
 
+class _Done:
+    """Handle of a collective that completed when it was issued."""
+    __slots__ = ()
+
+    def wait(self) -> None:
+        return None
+
+
+_DONE = _Done()
+
+
+class _SideStreamWork:
+    """Handle of a one-shot xGMI collective running on the communicator's side stream:
+    wait() orders the CURRENT stream after it (no host sync)."""
+    __slots__ = ("ev",)
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self) -> None:
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
 class LocalComm:
     rank = 0
     world_size = 1
@@ -59,6 +82,18 @@ class LocalComm:
         out.reshape(-1)[:inp.numel()].copy_(inp.reshape(-1))
         return out
 
+    # asynchronous forms (the DP fused step overlaps each exchange with the next unit's
+    # compute, models/nmf_dp.py): issue now, ``.wait()`` on the returned handle orders
+    # the current stream after the collective.  Here (and wherever a backend cannot run
+    # one in the background) the collective completes when issued.
+    def reduce_scatter_async(self, out: torch.Tensor, inp: torch.Tensor):
+        self.reduce_scatter_(out, inp)
+        return _DONE
+
+    def all_gather_into_async(self, out: torch.Tensor, inp: torch.Tensor):
+        self.all_gather_into_(out, inp)
+        return _DONE
+
     @property
     def is_distributed(self) -> bool:
         return False
@@ -78,6 +113,7 @@ class DistComm(LocalComm):
         self.world_size = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
         self._xgmi = None           # one-shot xGMI all-reduce (CNMF_ALLREDUCE=xgmi), lazy
+        self._side = None           # the stream every one-shot xGMI collective runs on
 
     @property
     def is_distributed(self) -> bool:
@@ -110,12 +146,29 @@ class DistComm(LocalComm):
             return None
         return self._xgmi if (any_dtype or self._xgmi.supports(t)) else None
 
+    def _on_side(self, fn):
+        """Run the one-shot xGMI launch ``fn`` on the side stream, after everything
+        issued so far on the current stream; returns (fn's result, handle).  EVERY xGMI
+        collective goes through here, so they keep one order on one stream (they share
+        the device epoch and the peer staging) while compute proceeds beside them."""
+        cur = torch.cuda.current_stream()
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=cur.device)
+        self._side.wait_stream(cur)
+        with torch.cuda.stream(self._side):
+            ok = fn()
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        return ok, _SideStreamWork(ev)
+
     def check(self) -> None:
         """Raise if a one-shot xGMI all-reduce gave up on a peer (host sync)."""
         if self._xgmi:
             self._xgmi.check()
 
     def close(self) -> None:
+        if self._side is not None:
+            self._side.synchronize()
         if self._xgmi:
             self._xgmi.close()
         self._xgmi = None
@@ -125,7 +178,8 @@ class DistComm(LocalComm):
             return t
         xg = self._xgmi_for(t)
         if xg is not None:
-            return xg(t)
+            self._on_side(lambda: xg(t))[1].wait()
+            return t
         if (self.backend == "nccl") != (t.device.type == "cuda"):
             # stage through the backend's device: gloo reduces host tensors, RCCL device
             # ones (a host int64 digit vector from the sharded prepare's exact moments
@@ -187,41 +241,56 @@ class DistComm(LocalComm):
         the sum over ranks of ``inp`` (world * out.numel() elements, rank-major).  Moves
         the same bytes per link as half an all-reduce.  Under gloo: an all-reduce of a
         host copy, then the chunk."""
+        self.reduce_scatter_async(out, inp).wait()
+        return out
+
+    def reduce_scatter_async(self, out: torch.Tensor, inp: torch.Tensor):
+        """reduce_scatter_ issued in the background: the one-shot xGMI kernel on the side
+        stream, or on RCCL's own stream (async_op); gloo completes it here."""
         if self.world_size == 1:
-            return LocalComm.reduce_scatter_(self, out, inp)
+            LocalComm.reduce_scatter_(self, out, inp)
+            return _DONE
         m = out.numel()
         if inp.numel() != m * self.world_size:
             raise ValueError(f"reduce_scatter_: {inp.numel()} != {self.world_size} x {m}")
         xg = self._xgmi_for(inp)
-        if xg is not None and xg.reduce_scatter(out, inp):
-            return out
+        if xg is not None:
+            ok, h = self._on_side(lambda: xg.reduce_scatter(out, inp))
+            if ok:
+                return h
         if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():
-            self._dist.reduce_scatter_tensor(out, inp, group=self.group)
-            return out
+            return self._dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=True)
         host = inp.reshape(-1).cpu()
         self._dist.all_reduce(host, group=self.group)
         out.copy_(host[self.rank * m:(self.rank + 1) * m].view_as(out))
-        return out
+        return _DONE
 
     def all_gather_into_(self, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
         """One all-gather into the rank-major ``out`` (world * inp.numel() elements)."""
+        self.all_gather_into_async(out, inp).wait()
+        return out
+
+    def all_gather_into_async(self, out: torch.Tensor, inp: torch.Tensor):
+        """all_gather_into_ issued in the background (see reduce_scatter_async)."""
         if self.world_size == 1:
-            return LocalComm.all_gather_into_(self, out, inp)
+            LocalComm.all_gather_into_(self, out, inp)
+            return _DONE
         m = inp.numel()
         if out.numel() != m * self.world_size:
             raise ValueError(f"all_gather_into_: {out.numel()} != {self.world_size} x {m}")
         xg = self._xgmi_for(inp, any_dtype=True)
-        if xg is not None and xg.all_gather(out, inp):
-            return out
+        if xg is not None:
+            ok, h = self._on_side(lambda: xg.all_gather(out, inp))
+            if ok:
+                return h
         if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():
-            self._dist.all_gather_into_tensor(out, inp, group=self.group)
-            return out
+            return self._dist.all_gather_into_tensor(out, inp, group=self.group, async_op=True)
         # gloo: as raw bytes (it has no int16 / bfloat16 all-gather)
         src = inp.reshape(-1).cpu().contiguous().view(torch.uint8)
         parts = [torch.empty(src.numel(), dtype=torch.uint8) for _ in range(self.world_size)]
         self._dist.all_gather(parts, src, group=self.group)
         out.reshape(-1).copy_(torch.cat(parts).view(inp.dtype))
-        return out
+        return _DONE
 
     def send_object(self, obj, dst: int) -> None:
         """Point-to-point: ``obj`` to rank ``dst`` (which must call recv_object(src=me))."""

@@ -63,8 +63,18 @@ def comm_worker(rank, world, port, out_dir):
     s = c.allreduce_scalar(rank + 0.5)
     m = c.allreduce_max_int(rank * 10)
     g = c.all_gather_object({"r": rank})
+    # the background forms: both issued before either is waited on
+    o = torch.empty(2)
+    ob = torch.empty(3 * world, dtype=torch.int16)
+    h1 = c.reduce_scatter_async(o, torch.arange(2 * world, dtype=torch.float32) + rank)
+    h2 = c.all_gather_into_async(ob, torch.full((3,), rank + 7, dtype=torch.int16))
+    h1.wait()
+    h2.wait()
+    exp_o = sum(torch.arange(2 * world, dtype=torch.float32) + r for r in range(world))
+    ok = bool(torch.equal(o, exp_o[2 * rank:2 * rank + 2])) and \
+        bool(torch.equal(ob, torch.arange(world, dtype=torch.int16).repeat_interleave(3) + 7))
     np.save(os.path.join(out_dir, f"comm{rank}.npy"),
-            np.array([t[0].item(), s, m, len(g), g[world - 1]["r"]]))
+            np.array([t[0].item(), s, m, len(g), g[world - 1]["r"], float(ok)]))
     dist.destroy_process_group()
 
 
@@ -316,9 +326,21 @@ def xgmi_rsag_worker(rank, world, port, out_dir):
     comm.reduce_scatter_(o, torch.full((3 * world,), float(rank + 1), device=dev))
     ob = torch.empty(4 * world, dtype=torch.int16, device=dev)
     comm.all_gather_into_(ob, torch.full((4,), rank + 7, dtype=torch.int16, device=dev))
+    # two exchanges in flight on the side stream while the current stream computes
+    o2 = torch.empty(5, device=dev)
+    ob2 = torch.empty(6 * world, dtype=torch.int16, device=dev)
+    h1 = comm.reduce_scatter_async(o2, torch.full((5 * world,), 2.0 * (rank + 1), device=dev))
+    busy = torch.randn(2048, 2048, device=dev)
+    busy = busy @ busy
+    h2 = comm.all_gather_into_async(ob2, torch.full((6,), rank + 3, dtype=torch.int16,
+                                                    device=dev))
+    h1.wait()
+    h2.wait()
     comm.check()
     res["comm_rs"] = o.cpu().numpy()
     res["comm_ag"] = ob.cpu().numpy()
+    res["comm_rs_async"] = o2.cpu().numpy()
+    res["comm_ag_async"] = ob2.cpu().numpy()
     res["comm_is_xgmi"] = bool(comm._xgmi)
     comm.close()
     np.savez(os.path.join(out_dir, f"rsag{rank}.npz"), **res)
@@ -360,7 +382,8 @@ def dp_fused_worker(rank, world, port, X, K, seeds, opts_kw, out_dir, fused, all
     np.save(os.path.join(out_dir, f"dpf{tag}_{rank}.npz.npy"),
             np.array([took, bool(solver.comm._xgmi)], dtype=bool))
     np.save(os.path.join(out_dir, f"dpfS{tag}_{rank}.npy"),
-            np.array(getattr(solver, "dp_slices", (0, 0)), dtype=np.int64))
+            np.array(tuple(getattr(solver, "dp_slices", (0, 0)))
+                     + (getattr(solver, "dp_units", 0),), dtype=np.int64))
     np.save(os.path.join(out_dir, f"dpfW{tag}_{rank}.npy"), res.W.cpu().numpy())
     np.save(os.path.join(out_dir, f"dpferr{tag}_{rank}.npy"), res.err)
     np.save(os.path.join(out_dir, f"dpfit{tag}_{rank}.npy"), res.n_iter)

@@ -60,8 +60,25 @@ def test_comm_primitives(tmp_path, monkeypatch, allreduce):
     monkeypatch.setenv("CNMF_ALLREDUCE", allreduce)
     _spawn(W.comm_worker, 3, str(tmp_path))
     for r in range(3):
-        t, s, m, n, last = np.load(tmp_path / f"comm{r}.npy")
+        t, s, m, n, last, async_ok = np.load(tmp_path / f"comm{r}.npy")
         assert t == 6.0 and abs(s - 4.5) < 1e-12 and m == 20 and n == 3 and last == 2
+        assert async_ok == 1.0      # reduce_scatter_async / all_gather_into_async
+
+
+def test_dp_exchange_units():
+    """The DP fused step's exchange units: a K grid's groups (each group's collectives
+    overlap the other groups' compute); a one-K batch stays one unit unless split into
+    halves (off by default: measured slower)."""
+    from cnmf_torch_amd.models import nmf_dp
+    from cnmf_torch_amd.models.nmf_batch import _Group
+
+    g = _Group(K=7, p0=0, n=9, r0=0, q0=0)
+    assert nmf_dp._dp_units([g], 2) == [g]
+    u = nmf_dp._dp_units([g], 2, split=True)
+    assert [(x.p0, x.n, x.r0, x.q0) for x in u] == [(0, 5, 0, 0), (5, 4, 35, 245)]
+    assert nmf_dp._dp_units([_Group(7, 0, 3, 0, 0)], 2, split=True) == [_Group(7, 0, 3, 0, 0)]
+    two = [_Group(5, 0, 3, 0, 0), _Group(8, 3, 4, 15, 75)]
+    assert nmf_dp._dp_units(two, 2, split=True) == two
 
 
 @pytest.mark.parametrize("algo,mode,beta_loss", [("mu", "online", "frobenius"),

@@ -70,6 +70,9 @@ def test_xgmi_reduce_scatter_all_gather_match_gloo(tmp_path):
         assert bool(z["comm_is_xgmi"])
         np.testing.assert_array_equal(z["comm_rs"], np.full(3, 3.0, dtype=np.float32))
         np.testing.assert_array_equal(z["comm_ag"], np.repeat([7, 8], 4).astype(np.int16))
+        np.testing.assert_array_equal(z["comm_rs_async"], np.full(5, 6.0, dtype=np.float32))
+        np.testing.assert_array_equal(z["comm_ag_async"],
+                                      np.repeat([3, 4], 6).astype(np.int16))
 
 
 @pytest.mark.parametrize("K,R", [(6, 7), (20, 6), ((5, 5, 5, 8, 8, 8, 8), 7)])
@@ -79,7 +82,8 @@ def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
     world: a padded last chunk), all-gather of the spectra planes / W W^T partials /
     lin-quad -- factorises like the all-reduced unfused DP step: identical W on both
     ranks, pass counts +-1, errors of same-pass replicates to 1e-5.  The third case is a
-    mixed-K batch (a cNMF K grid): one packed exchange per K group and step.  Shapes large enough
+    mixed-K batch (a cNMF K grid): one packed exchange per K group and step, issued in
+    the background under the other group's compute.  Shapes large enough
     that both solves run the production cooperative slices (800 cells per rank and step,
     800 genes: S > 1 on both sides)."""
     X = normalized_counts_matrix(3200, 800, n_programs=6, seed=9)
@@ -93,8 +97,11 @@ def test_dp_fused_reduce_scatter_step_matches_unfused(tmp_path, K, R):
         assert bool(np.load(tmp_path / f"dpf1_{r}.npz.npy")[0])
         assert not bool(np.load(tmp_path / f"dpf0_{r}.npz.npy")[0])
         # the cooperative-slice solves ran multi-process (both sides sliced)
-        S_h, S_w = np.load(tmp_path / f"dpfS1_{r}.npy")
+        S_h, S_w, units = np.load(tmp_path / f"dpfS1_{r}.npy")
         assert S_h > 1 and S_w > 1, (S_h, S_w)
+        # the mixed-K batch: two exchange units per step (its K groups), each one's
+        # collectives issued in the background under the other's compute
+        assert units == (2 if isinstance(K, tuple) else 1)
         took, used = np.load(tmp_path / f"dpf1x_{r}.npz.npy")
         assert bool(took) and bool(used)
     Wf = np.load(tmp_path / "dpfW1_0.npy")
