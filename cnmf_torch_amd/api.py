@@ -341,12 +341,20 @@ class cNMF:
     def prepare(self, counts_fn, components, n_iter=100, densify=False, tpm_fn=None, seed=None,
                 beta_loss="frobenius", num_highvar_genes=2000, genes_file=None, alpha_usage=0.0,
                 alpha_spectra=0.0, init="random", total_workers=-1, use_gpu=False,
-                batch_size=5000, max_NMF_iter=1000, algo="mu", mode="online", comm=None):
+                batch_size=5000, max_NMF_iter=1000, algo="mu", mode="online", comm=None,
+                prewarm=True):
         """Load counts, select over-dispersed genes, variance-normalise, write the
         replicate ledger (cnmf.py:458-596).  ``algo``/``mode`` are additions (defaults =
         the reference's hard-coded 'mu'/'online').  With a multi-rank ``comm`` the cells
         are sharded over the ranks and the per-gene statistics are all-reduced
-        (:meth:`_prepare_sharded`)."""
+        (:meth:`_prepare_sharded`).
+
+        ``prewarm`` (GPU): while this stage runs, a background thread makes the first
+        launches of the k-selection / consensus kernels in this process
+        (utils.prewarm), so those stages do not pay HIP's first-use code loading later
+        in the same process (joined before returning), and the figure process starts
+        (utils.plotting.prestart).  The CLI, whose later stages are other processes,
+        turns it off."""
         check_gpu_ranks(components, beta_loss, algo, use_gpu)
         if comm is not None and comm.world_size > 1:
             return self._prepare_sharded(
@@ -355,6 +363,28 @@ class cNMF:
                 genes_file=genes_file, alpha_usage=alpha_usage, alpha_spectra=alpha_spectra,
                 init=init, total_workers=total_workers, use_gpu=use_gpu, batch_size=batch_size,
                 max_NMF_iter=max_NMF_iter, algo=algo, mode=mode)
+        warm = prewarm and _device(False).type == "cuda"
+        if warm:
+            from .utils import prewarm as _prewarm
+            from .utils.plotting import prestart
+
+            _prewarm.start(_device(False))
+            # and the figure process (matplotlib's import) a stage earlier than factorize
+            # would start it: with the later stages warm it is the pipeline's last wait
+            prestart()
+        try:
+            self._prepare_local(counts_fn, components, n_iter, densify, tpm_fn, seed,
+                                beta_loss, num_highvar_genes, genes_file, alpha_usage,
+                                alpha_spectra, init, total_workers, use_gpu, batch_size,
+                                max_NMF_iter, algo, mode)
+        finally:
+            if warm:
+                _prewarm.wait()
+
+    def _prepare_local(self, counts_fn, components, n_iter, densify, tpm_fn, seed, beta_loss,
+                       num_highvar_genes, genes_file, alpha_usage, alpha_spectra, init,
+                       total_workers, use_gpu, batch_size, max_NMF_iter, algo, mode):
+        """Single-process prepare (see prepare)."""
         with self.timer("prepare"):
             input_counts = read_any(counts_fn, densify)
             if sp.issparse(input_counts.X) and densify:

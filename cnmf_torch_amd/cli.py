@@ -116,7 +116,8 @@ def main(argv=None) -> int:
             from .parallel.runner import init_distributed
 
             comm, _ = init_distributed()
-        obj.prepare(comm=comm, **_prepare_kwargs(args))
+        # (no background prewarm: the later stages run in other processes)
+        obj.prepare(comm=comm, prewarm=False, **_prepare_kwargs(args))
     elif args.command == "factorize":
         world = int(os.environ.get("WORLD_SIZE", "1"))
         if args.dp:

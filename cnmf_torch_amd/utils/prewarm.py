@@ -1,0 +1,95 @@
+"""Background first-use loading of the device code the later pipeline stages call.
+
+HIP loads a kernel's code object on its first launch in a process.  For the small
+consensus / k-selection kernels that load, not the work, is the cost: one K's
+k-selection statistics take 26 ms warm and 1.0 s on the first call of a process
+(``profiles/r5ze_kstats_{warm,cold}.txt``: the first ``pow`` / ``minimum`` / ``clamp`` /
+``sqrt`` / ``unique`` each ~0.05-0.13 s, the first f32 / f64 library GEMM another ~0.15 s).
+``start`` runs those stages' building blocks once on tiny inputs, on a thread of its own
+and a stream of its own, while the caller's stage (``cNMF.prepare``) does its own work;
+``wait`` joins it.  Best effort: a failure here only leaves a first call cold.
+
+Nothing cooperative runs here (no solve: a cooperative launch must not share the GPU with
+another one), and the caller joins before any later stage could capture a HIP graph.
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+import torch
+
+from .log import get_logger
+
+log = get_logger("cnmf_torch_amd.prewarm")
+
+_LOCK = threading.Lock()
+_THREADS: dict = {}
+
+
+def start(device) -> threading.Thread | None:
+    """Start warming ``device`` (once per process and device); None off the GPU."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    with _LOCK:
+        t = _THREADS.get(idx)
+        if t is None:
+            t = threading.Thread(target=_run, args=(torch.device("cuda", idx),),
+                                 name="cnmf-prewarm", daemon=True)
+            _THREADS[idx] = t
+            t.start()
+    return t
+
+
+def wait(timeout: float | None = None) -> None:
+    """Join every warming thread started so far."""
+    with _LOCK:
+        threads = list(_THREADS.values())
+    for t in threads:
+        t.join(timeout)
+
+
+def _run(dev: torch.device) -> None:
+    try:
+        with torch.cuda.device(dev):
+            s = torch.cuda.Stream(dev)
+            with torch.cuda.stream(s):
+                _stages(dev)
+            s.synchronize()
+    except Exception as e:      # best effort: the stage's own first call stays cold
+        log.debug("prewarm stopped: %s", e)
+
+
+def _stages(dev: torch.device) -> None:
+    """The k-selection / consensus chain (api.cNMF._consensus) on a toy problem: 24
+    "spectra" of 16 genes in 3 clusters, and the refit / prediction-error products."""
+    from ..models.consensus import (cluster_medians, kmeans, l2_normalize_rows, local_density,
+                                    pairwise_distances, silhouette)
+
+    g = torch.Generator().manual_seed(0)
+    S = (torch.rand((24, 16), generator=g, dtype=torch.float64) + 0.1).to(dev)
+    L2 = l2_normalize_rows(S)
+    d = pairwise_distances(L2)
+    local_density(d, 3)
+    lab = kmeans(L2, 3, n_init=1, backend="device", device_restart_factor=1)
+    silhouette(d, lab)
+    cluster_medians(L2, lab, sorted(set(np.asarray(lab).tolist())))
+    # refit (numerator / Gram products, f32) and the prediction error (f64 products)
+    W = torch.rand((3, 16), generator=g).to(dev)
+    X = torch.rand((40, 16), generator=g).to(dev)
+    _ = W @ W.t()
+    _ = X @ W.t()
+    U = torch.rand((40, 3), generator=g, dtype=torch.float64).to(dev)
+    S3 = L2[:3]
+    q = ((U.t() @ U) * (S3 @ S3.t())).sum()
+    xb = X.to(torch.float64)
+    q = q + ((U.t() @ xb) * S3).sum() + (xb * xb).sum()
+    # elementwise / reduction kernels of those stages
+    t = torch.rand(64, generator=g).to(dev)
+    _ = torch.clamp(t, min=0.0), torch.minimum(t, t), torch.maximum(t, t), t.pow(2)
+    _ = torch.where(t > 0.5, t, torch.zeros_like(t)), torch.nan_to_num(t), t.sqrt()
+    _ = t.var(), t.min(), t.any(), torch.argmin(t), torch.cumsum(t, 0), t.sort()
+    _ = torch.unique(t.round()), torch.searchsorted(t.sort().values, t)
+    float(q)

@@ -28,6 +28,31 @@ from cnmf_torch_amd.utils.plotting import flush_figures  # noqa: E402
 from cnmf_torch_amd.utils.synthetic import simulate_counts  # noqa: E402
 
 
+def _profile_kstats(obj, kmid, a, warm: bool) -> None:
+    """cProfile one K's k-selection statistics (consensus up to its stats), serially."""
+    import cProfile
+    import pstats
+
+    def kstats():
+        obj.consensus(kmid, skip_density_and_return_after_stats=True, show_clustering=False,
+                      close_clustergram_fig=True, kmeans_backend=a.kmeans_backend)
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    if warm:
+        kstats()
+    pr = cProfile.Profile()
+    t0 = time.perf_counter()
+    pr.enable()
+    kstats()
+    pr.disable()
+    with open(a.profile_kstats, "w") as fh:
+        fh.write(f"==== k-selection statistics of K={kmid}, serial, "
+                 f"{'warm' if warm else 'first call'}: {time.perf_counter() - t0:.3f} s ====\n")
+        pstats.Stats(pr, stream=fh).sort_stats("cumulative").print_stats(45)
+        pstats.Stats(pr, stream=fh).sort_stats("tottime").print_stats(25)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cells", type=int, default=10000)
@@ -42,6 +67,13 @@ def main():
     ap.add_argument("--profile", default=None, help="cProfile every stage into this file")
     ap.add_argument("--kmeans-backend", default="auto", choices=["auto", "sklearn", "device"],
                     help="sklearn = the reference's exact KMeans; device = batched GPU restarts")
+    ap.add_argument("--profile-kstats", default=None,
+                    help="after the pipeline: cProfile ONE K's k-selection statistics "
+                         "(consensus up to its stats, serial, warm) into this file -- the "
+                         "stage itself runs them on worker threads cProfile does not see")
+    ap.add_argument("--kstats-cold", action="store_true",
+                    help="with --profile-kstats: profile the FIRST call instead (right after "
+                         "combine, before the k-selection stage): the first-use costs")
     a = ap.parse_args()
     work = a.workdir or tempfile.mkdtemp(prefix="cnmf_e2e_")
     X, cells, genes = simulate_counts(a.cells, a.genes, a.programs, seed=0, sparse=True)
@@ -68,6 +100,13 @@ def main():
               # pipeline is done once the last PNG is on disk
               ("figures", flush_figures)]
     prof_out = open(a.profile, "w") if a.profile else None
+    if a.profile_kstats and a.kstats_cold:      # factorize + combine, then the cold probe
+        for name, fn in stages[:2]:
+            t0 = time.perf_counter()
+            fn()
+            t[name] = time.perf_counter() - t0
+        stages = stages[2:]
+        _profile_kstats(obj, kmid, a, warm=False)
     for name, fn in stages:
         if prof_out:
             import cProfile
@@ -86,6 +125,8 @@ def main():
             pstats.Stats(pr, stream=prof_out).sort_stats("cumulative").print_stats(30)
     if prof_out:
         prof_out.close()
+    if a.profile_kstats and not a.kstats_cold:
+        _profile_kstats(obj, kmid, a, warm=True)
     total = sum(t.values())
     n_rep = len(ks) * a.n_iter
     print(json.dumps({
