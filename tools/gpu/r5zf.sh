@@ -1,4 +1,4 @@
-# background prewarm of the k-selection / consensus kernels during prepare: e2e x3
+# e2e x3: prewarm + figure prestart in prepare; replicate log / manifest appends on the writer threads
 export TMPDIR=/tmp
 out=gpurun_out/r5zf
 mkdir -p $out
