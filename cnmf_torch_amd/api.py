@@ -369,6 +369,7 @@ class cNMF:
             from .utils.plotting import prestart
 
             _prewarm.start(_device(False))
+            self._prebuild = True
             # and the figure process (matplotlib's import) a stage earlier than factorize
             # would start it: with the later stages warm it is the pipeline's last wait
             prestart()
@@ -378,6 +379,7 @@ class cNMF:
                                 alpha_spectra, init, total_workers, use_gpu, batch_size,
                                 max_NMF_iter, algo, mode)
         finally:
+            self._prebuild = False
             if warm:
                 _prewarm.wait()
 
@@ -447,6 +449,7 @@ class cNMF:
                 # (utils.resident; the float32 cast is the one they apply to the file's data)
                 resident.remember(self.paths["normalized_counts"], "X32", T.to(torch.float32))
                 del T
+                self._prebuild_planes(dev)
             else:
                 norm_counts = self.get_norm_counts(input_counts, tpm,
                                                    num_highvar_genes=num_highvar_genes,
@@ -459,12 +462,36 @@ class cNMF:
                     resident.remember(self.paths["normalized_counts"],
                                       "X32" if not sp.issparse(norm_counts.X) else "X32_factorize",
                                       torch.from_numpy(_dense32(norm_counts.X)).to(dev))
+                    self._prebuild_planes(dev)
             replicate_params, run_params = self.get_nmf_iter_params(
                 ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
                 alpha_usage=alpha_usage, alpha_spectra=alpha_spectra, init=init,
                 total_workers=total_workers, use_gpu=use_gpu, batch_size=batch_size,
                 max_iter=max_NMF_iter, algo=algo, mode=mode)
             self.save_nmf_iter_params(replicate_params, run_params)
+
+    def _prebuild_planes(self, dev) -> None:
+        """With prepare's prewarm on: build the resident matrix's split-GEMM planes on a
+        background thread (models.nmf_base.planes_ahead) for factorize in this process."""
+        if not getattr(self, "_prebuild", False):
+            return
+        path = self.paths["normalized_counts"]
+        X = resident.recall(path, "X32")
+        if X is None:
+            X = resident.recall(path, "X32_factorize")
+        if X is None or X.device != dev:
+            return
+        from .models.nmf_base import planes_ahead
+        from .utils import prewarm as _prewarm
+
+        X_ready = torch.cuda.Event()
+        X_ready.record()            # the mirror's upload, on this thread's stream
+
+        def build():
+            torch.cuda.current_stream().wait_event(X_ready)
+            planes_ahead(X)
+
+        _prewarm.run(dev, build)
 
     def _prepare_sharded(self, comm, counts_fn, components, n_iter, densify, tpm_fn, seed,
                          beta_loss, num_highvar_genes, genes_file, alpha_usage, alpha_spectra,

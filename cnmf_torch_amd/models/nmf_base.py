@@ -9,6 +9,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 import torch
+from torch.utils.weak import WeakIdKeyDictionary
 
 from .. import ops
 from .bpp import nnls_bpp, objective_terms as bpp_objective_terms
@@ -515,6 +516,9 @@ class _XPlanes:
         ``reserve``: device bytes the caller still has to allocate after the planes (the
         fused step's slabs, plane buffers and statistics), kept free so a run that does
         not fit takes the documented fp32 fallback here instead of failing partway."""
+        ahead = _PLANES_AHEAD.get(X) if isinstance(X, torch.Tensor) else None
+        if ahead is not None and ahead[0] == (X.data_ptr(), X._version):
+            return ahead[1]
         if X.device.type != "cuda" or X.dtype != torch.float32 or \
                 os.environ.get("CNMF_GEMM", "planes") != "planes":
             return None
@@ -533,6 +537,28 @@ class _XPlanes:
             return None
         return _XPlanes(X, stats)
 
+
+
+# planes built ahead of the solver for a resident X (cNMF.prepare's background thread,
+# planes_ahead), keyed by the tensor's identity and valid while its storage and version
+# are unchanged
+_PLANES_AHEAD = WeakIdKeyDictionary()
+
+
+def planes_ahead(X: torch.Tensor) -> None:
+    """Build and keep ``X``'s split-GEMM planes now, for the solver that will factorise
+    this same resident tensor (factorize after prepare in one process): the unit check,
+    two host round trips and the plane split leave factorize's critical path.  Only when
+    they take under a quarter of the free device memory (no workspace reserve is known
+    yet)."""
+    if not isinstance(X, torch.Tensor) or X.device.type != "cuda" or X.dtype != torch.float32:
+        return
+    free, _ = torch.cuda.mem_get_info(X.device)
+    if _XPlanes.bytes_needed(X.shape[0], X.shape[1], 2) > 0.25 * free:
+        return
+    xp = _XPlanes.build(X)
+    if xp is not None:
+        _PLANES_AHEAD[X] = ((X.data_ptr(), X._version), xp)
 
 
 _WARNED: set = set()

@@ -43,10 +43,39 @@ def start(device) -> threading.Thread | None:
     return t
 
 
-def wait(timeout: float | None = None) -> None:
-    """Join every warming thread started so far."""
+_EXTRA: list = []
+
+
+def run(device, fn) -> threading.Thread | None:
+    """Run ``fn()`` now on a background thread with a stream of its own (device work a
+    later stage of this process will reuse, e.g. the data matrix's GEMM planes);
+    joined -- and its stream drained -- by :func:`wait`.  None off the GPU."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return None
+
+    def body():
+        try:
+            with torch.cuda.device(dev):
+                s = torch.cuda.Stream(dev)
+                with torch.cuda.stream(s):
+                    fn()
+                s.synchronize()
+        except Exception as e:      # best effort: the later stage builds it itself
+            log.debug("background build stopped: %s", e)
+
+    t = threading.Thread(target=body, name="cnmf-prebuild", daemon=True)
     with _LOCK:
-        threads = list(_THREADS.values())
+        _EXTRA.append(t)
+    t.start()
+    return t
+
+
+def wait(timeout: float | None = None) -> None:
+    """Join every warming / building thread started so far."""
+    with _LOCK:
+        threads = list(_THREADS.values()) + list(_EXTRA)
+        _EXTRA.clear()
     for t in threads:
         t.join(timeout)
 

@@ -40,3 +40,46 @@ def test_prewarm_runs_the_consensus_chain_and_joins():
                    for i in range(3)]).to(dev)
     lab = kmeans(X, 3, backend="device")
     assert len(set(lab[:20])) == 1 and len(set(lab.tolist())) == 3
+
+
+@pytest.mark.gpu
+def test_prepare_builds_the_factorize_planes_ahead(tmp_path):
+    """prepare (prewarm on) builds the resident matrix's split-GEMM planes in the
+    background; factorize in the same process takes them (no second build) and
+    factorises bitwise as with a prepare that built nothing ahead."""
+    import numpy as np
+    import pandas as pd
+
+    from cnmf_torch_amd import cNMF
+    from cnmf_torch_amd.models import nmf_base
+    from cnmf_torch_amd.utils import resident
+    from cnmf_torch_amd.utils.io import load_df_from_npz, save_df_to_npz
+    from cnmf_torch_amd.utils.synthetic import simulate_counts
+
+    X, cells, genes = simulate_counts(800, 400, 4, seed=5, sparse=False)
+    fn = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(X, index=cells, columns=genes), fn)
+    spectra = {}
+    for warm in (True, False):
+        obj = cNMF(output_dir=str(tmp_path / f"w{int(warm)}"), name="p")
+        obj.prepare(fn, components=[4], n_iter=3, seed=2, num_highvar_genes=200,
+                    prewarm=warm)
+        Xr = resident.recall(obj.paths["normalized_counts"], "X32")
+        ahead = nmf_base._PLANES_AHEAD.get(Xr) if Xr is not None else None
+        assert (ahead is not None) == warm
+        calls = []
+        orig = nmf_base._XPlanes.__init__
+
+        def counting(self, *a, **kw):
+            calls.append(1)
+            orig(self, *a, **kw)
+
+        nmf_base._XPlanes.__init__ = counting
+        try:
+            obj.factorize(verbose=False)
+        finally:
+            nmf_base._XPlanes.__init__ = orig
+        assert len(calls) == (0 if warm else 1)
+        spectra[warm] = np.concatenate([
+            load_df_from_npz(obj.paths["iter_spectra"] % (4, i)).values for i in range(3)])
+    np.testing.assert_array_equal(spectra[True], spectra[False])
