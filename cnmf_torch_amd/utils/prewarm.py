@@ -25,6 +25,7 @@ log = get_logger("cnmf_torch_amd.prewarm")
 
 _LOCK = threading.Lock()
 _THREADS: dict = {}
+errors: list = []       # (what, repr of the exception) of background work that stopped
 
 
 def start(device) -> threading.Thread | None:
@@ -62,6 +63,7 @@ def run(device, fn) -> threading.Thread | None:
                     fn()
                 s.synchronize()
         except Exception as e:      # best effort: the later stage builds it itself
+            errors.append(("build", repr(e)))
             log.debug("background build stopped: %s", e)
 
     t = threading.Thread(target=body, name="cnmf-prebuild", daemon=True)
@@ -88,6 +90,7 @@ def _run(dev: torch.device) -> None:
                 _stages(dev)
             s.synchronize()
     except Exception as e:      # best effort: the stage's own first call stays cold
+        errors.append(("prewarm", repr(e)))
         log.debug("prewarm stopped: %s", e)
 
 

@@ -32,6 +32,7 @@ def test_prewarm_runs_the_consensus_chain_and_joins():
     assert prewarm.start(dev) is t          # once per process and device
     prewarm.wait(timeout=120)
     assert not t.is_alive()
+    assert not prewarm.errors, prewarm.errors
     # the warmed stages still compute correctly afterwards
     from cnmf_torch_amd.models.consensus import kmeans
 
@@ -65,7 +66,11 @@ def test_prepare_builds_the_factorize_planes_ahead(tmp_path):
         obj.prepare(fn, components=[4], n_iter=3, seed=2, num_highvar_genes=200,
                     prewarm=warm)
         Xr = resident.recall(obj.paths["normalized_counts"], "X32")
-        ahead = nmf_base._PLANES_AHEAD.get(Xr) if Xr is not None else None
+        if Xr is None:          # a sparse-stored input: the mirror serves factorize only
+            Xr = resident.recall(obj.paths["normalized_counts"], "X32_factorize")
+        assert Xr is not None, "prepare kept no device mirror of the normalized counts"
+        assert not prewarm.errors, prewarm.errors
+        ahead = nmf_base._PLANES_AHEAD.get(Xr)
         assert (ahead is not None) == warm
         calls = []
         orig = nmf_base._XPlanes.__init__
