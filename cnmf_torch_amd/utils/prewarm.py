@@ -28,20 +28,25 @@ _THREADS: dict = {}
 errors: list = []       # (what, repr of the exception) of background work that stopped
 
 
-def start(device) -> threading.Thread | None:
-    """Start warming ``device`` (once per process and device); None off the GPU."""
+def start(device, parallel: bool = True) -> list:
+    """Start warming ``device`` (once per process and device): the groups below on one
+    thread each (``parallel``; the code-object loads of different groups overlap) or
+    all on one.  [] off the GPU."""
     dev = torch.device(device)
     if dev.type != "cuda":
-        return None
+        return []
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     with _LOCK:
-        t = _THREADS.get(idx)
-        if t is None:
-            t = threading.Thread(target=_run, args=(torch.device("cuda", idx),),
-                                 name="cnmf-prewarm", daemon=True)
-            _THREADS[idx] = t
-            t.start()
-    return t
+        ts = _THREADS.get(idx)
+        if ts is None:
+            d = torch.device("cuda", idx)
+            groups = [[g] for g in _GROUPS] if parallel else [list(_GROUPS)]
+            ts = [threading.Thread(target=_run, args=(d, grp), name="cnmf-prewarm",
+                                   daemon=True) for grp in groups]
+            _THREADS[idx] = ts
+            for t in ts:
+                t.start()
+    return ts
 
 
 _EXTRA: list = []
@@ -76,27 +81,28 @@ def run(device, fn) -> threading.Thread | None:
 def wait(timeout: float | None = None) -> None:
     """Join every warming / building thread started so far."""
     with _LOCK:
-        threads = list(_THREADS.values()) + list(_EXTRA)
+        threads = [t for ts in _THREADS.values() for t in ts] + list(_EXTRA)
         _EXTRA.clear()
     for t in threads:
         t.join(timeout)
 
 
-def _run(dev: torch.device) -> None:
+def _run(dev: torch.device, groups) -> None:
     try:
         with torch.cuda.device(dev):
             s = torch.cuda.Stream(dev)
             with torch.cuda.stream(s):
-                _stages(dev)
+                for grp in groups:
+                    grp(dev)
             s.synchronize()
     except Exception as e:      # best effort: the stage's own first call stays cold
         errors.append(("prewarm", repr(e)))
         log.debug("prewarm stopped: %s", e)
 
 
-def _stages(dev: torch.device) -> None:
+def _consensus_chain(dev: torch.device) -> None:
     """The k-selection / consensus chain (api.cNMF._consensus) on a toy problem: 24
-    "spectra" of 16 genes in 3 clusters, and the refit / prediction-error products."""
+    "spectra" of 16 genes in 3 clusters."""
     from ..models.consensus import (cluster_medians, kmeans, l2_normalize_rows, local_density,
                                     pairwise_distances, silhouette)
 
@@ -108,20 +114,32 @@ def _stages(dev: torch.device) -> None:
     lab = kmeans(L2, 3, n_init=1, backend="device", device_restart_factor=1)
     silhouette(d, lab)
     cluster_medians(L2, lab, sorted(set(np.asarray(lab).tolist())))
-    # refit (numerator / Gram products, f32) and the prediction error (f64 products)
+
+
+def _library_gemms(dev: torch.device) -> None:
+    """The refit's numerator / Gram products (f32) and the prediction error's (f64)."""
+    g = torch.Generator().manual_seed(1)
     W = torch.rand((3, 16), generator=g).to(dev)
     X = torch.rand((40, 16), generator=g).to(dev)
     _ = W @ W.t()
     _ = X @ W.t()
     U = torch.rand((40, 3), generator=g, dtype=torch.float64).to(dev)
-    S3 = L2[:3]
+    S3 = torch.rand((3, 16), generator=g, dtype=torch.float64).to(dev)
     q = ((U.t() @ U) * (S3 @ S3.t())).sum()
     xb = X.to(torch.float64)
     q = q + ((U.t() @ xb) * S3).sum() + (xb * xb).sum()
-    # elementwise / reduction kernels of those stages
+    float(q)
+
+
+def _elementwise(dev: torch.device) -> None:
+    """Elementwise / reduction / sort kernels of those stages."""
+    g = torch.Generator().manual_seed(2)
     t = torch.rand(64, generator=g).to(dev)
     _ = torch.clamp(t, min=0.0), torch.minimum(t, t), torch.maximum(t, t), t.pow(2)
     _ = torch.where(t > 0.5, t, torch.zeros_like(t)), torch.nan_to_num(t), t.sqrt()
     _ = t.var(), t.min(), t.any(), torch.argmin(t), torch.cumsum(t, 0), t.sort()
     _ = torch.unique(t.round()), torch.searchsorted(t.sort().values, t)
-    float(q)
+    t.sum().item()
+
+
+_GROUPS = (_consensus_chain, _library_gemms, _elementwise)

@@ -6,7 +6,7 @@ from cnmf_torch_amd.utils import prewarm
 
 
 def test_prewarm_is_a_noop_off_the_gpu():
-    assert prewarm.start("cpu") is None
+    assert prewarm.start("cpu") == []
     prewarm.wait()          # nothing started: returns at once
 
 
@@ -27,11 +27,11 @@ def test_cli_prepare_turns_prewarm_off(monkeypatch, tmp_path):
 @pytest.mark.gpu
 def test_prewarm_runs_the_consensus_chain_and_joins():
     dev = torch.device("cuda", 0)
-    t = prewarm.start(dev)
-    assert t is not None
-    assert prewarm.start(dev) is t          # once per process and device
+    ts = prewarm.start(dev)
+    assert len(ts) == 3
+    assert prewarm.start(dev) is ts         # once per process and device
     prewarm.wait(timeout=120)
-    assert not t.is_alive()
+    assert not any(t.is_alive() for t in ts)
     assert not prewarm.errors, prewarm.errors
     # the warmed stages still compute correctly afterwards
     from cnmf_torch_amd.models.consensus import kmeans
