@@ -71,7 +71,15 @@ def clustergram(dist: np.ndarray, labels: pd.Series, local_density: pd.DataFrame
     gs = gridspec.GridSpec(2, 5, fig, 0.01, 0.01, 0.98, 0.98, height_ratios=heights,
                            width_ratios=widths, wspace=0, hspace=0)
     ax = fig.add_subplot(gs[1, 1], xticks=[], yticks=[])
-    im = ax.imshow(D, interpolation="none", cmap="viridis", aspect="auto", rasterized=True)
+    # the heatmap colour-mapped once at its own 900 x 900 size, then drawn as RGBA: Agg
+    # resamples an RGBA image without re-mapping the ~5 M output pixels through the
+    # colormap (the same nearest-pixel picture); the colour bar keeps the scalar mapping
+    from matplotlib import cm, colors
+
+    norm = colors.Normalize(vmin=float(D.min()), vmax=float(D.max()))
+    im = cm.ScalarMappable(norm=norm, cmap="viridis")
+    ax.imshow(im.to_rgba(D, bytes=True), interpolation="none", aspect="auto",
+              rasterized=True)
     lab = labels.values[order]
     left = fig.add_subplot(gs[1, 0], xticks=[], yticks=[])
     left.imshow(lab.reshape(-1, 1), interpolation="none", cmap="Spectral", aspect="auto",
