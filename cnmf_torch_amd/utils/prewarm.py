@@ -28,10 +28,13 @@ _THREADS: dict = {}
 errors: list = []       # (what, repr of the exception) of background work that stopped
 
 
-def start(device, parallel: bool = True) -> list:
-    """Start warming ``device`` (once per process and device): the groups below on one
-    thread each (``parallel``; the code-object loads of different groups overlap) or
-    all on one.  [] off the GPU."""
+def start(device, parallel: bool = False) -> list:
+    """Start warming ``device`` (once per process and device): the groups below all on
+    one thread (default), or on one thread each (``parallel``: the code-object loads
+    overlap, 0.24 s against 0.53 s, but the shorter prepare then leaves the figure
+    process's matplotlib import running under factorize, whose host-bound stage time
+    varied 0.094-0.125 s against 0.095-0.100 s: profiles/r5zj_*, r5zk_*).  [] off the
+    GPU."""
     dev = torch.device(device)
     if dev.type != "cuda":
         return []
