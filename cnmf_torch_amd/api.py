@@ -1431,8 +1431,12 @@ class cNMF:
             spectra_tpm = _spectra_tpm.copy()
             spectra_tpm.columns = spectra_tpm.columns.astype(str)
         else:
+            # the reference's read (cnmf.py:1273), whole-file and memory-mapped: the same
+            # C parser and values, without the per-chunk type inference (0.15 -> 0.09 s
+            # for 8000 genes)
             spectra_tpm = pd.read_csv(self.paths["gene_spectra_tpm__txt"] % (k, dt),
-                                      index_col=0, sep="\t")
+                                      index_col=0, sep="\t", low_memory=False,
+                                      memory_map=True)
         with open(self.paths["nmf_genes_list"]) as fh:
             hvgs = fh.read().split("\n")
         tpm_stats = load_df_from_npz(self.paths["tpm_stats"])
