@@ -516,7 +516,9 @@ class _XPlanes:
         ``reserve``: device bytes the caller still has to allocate after the planes (the
         fused step's slabs, plane buffers and statistics), kept free so a run that does
         not fit takes the documented fp32 fallback here instead of failing partway."""
-        ahead = _PLANES_AHEAD.get(X) if isinstance(X, torch.Tensor) else None
+        # planes built ahead for this tensor: handed over once (the solver owns them
+        # from here and frees them with itself; nothing keeps a second copy alive)
+        ahead = _PLANES_AHEAD.pop(X, None) if isinstance(X, torch.Tensor) else None
         if ahead is not None and ahead[0] == (X.data_ptr(), X._version):
             return ahead[1]
         if X.device.type != "cuda" or X.dtype != torch.float32 or \
