@@ -284,6 +284,8 @@ def _resident_X(adata, dev: torch.device):
 
 # cooperative (co-resident, spinning) solves of concurrent k-selection threads
 _COOP_LOCK = threading.RLock()
+# k-selection worker threads (one HIP stream each; 8 measured the same as 4: profiles/r5zo_*)
+_KSEL_THREADS = 4
 
 # ||X||^2 of a device-resident X (api._prediction_error), weakly keyed by the tensor's
 # identity (a WeakKeyDictionary compares tensor keys with Tensor.__eq__, which raises)
@@ -1493,7 +1495,7 @@ class cNMF:
                 s.synchronize()
                 return out
 
-            with cf.ThreadPoolExecutor(max_workers=min(4, len(mine))) as ex:
+            with cf.ThreadPoolExecutor(max_workers=min(_KSEL_THREADS, len(mine))) as ex:
                 for k, st in zip(mine, ex.map(on_stream, mine)):
                     rows[k] = st
         else:
