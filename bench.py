@@ -225,7 +225,12 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    stream = args.schedule == "stream" and args.mode != "dp" and args.streams == 1
+    # continuous batching where it pays: ranks K <= 16 (NMFBatchSolver.stream_live does
+    # not stream wider ranks; a stream over every timed step's replicates would then be ONE
+    # batch of all of them).  K = 20 / 30 measured 5,264-5,337 / 3,404-3,499 rep/s as that
+    # single batch against 5,730 / 3,779-3,860 one batch per step (profiles/r5zp_*)
+    stream = args.schedule == "stream" and args.mode != "dp" and args.streams == 1 and \
+        int(np.max(grid)) <= 16
     held = []          # pinned spectra of finished replicates (factorize writes them out)
 
     def keep(ids, kk, host, ev):
