@@ -23,15 +23,17 @@ them).  ``value`` is whole-job replicates/sec.  ``--mode`` picks the multi-GPU s
 ``--kmin/--kmax`` replace the single K by the K x n_iter grid of BASELINE config 2
 (K = kmin..kmax, ``--n-iter`` replicates each) solved as ONE ragged batch per step.
 
-``--schedule stream`` (default; weak / strong modes): the timed steps' ledger batches are
-fed, in order, through ONE continuous-batching solve (NMFBatchSolver.run_stream): a fixed
-number of live replicate slots per K, each slot handed the next waiting replicate at the
-pass boundary after its replicate converged.  Every replicate still runs its own full
-solve to its own convergence (same init, rules and pass limit); what changes is that the
-tail of one batch -- the few slow replicates the GPU would otherwise run alone -- overlaps
-the next batch's first passes.  ``value`` is then replicates/s over the whole stream
-(``steps`` x ``n_iter`` replicates per rank, all persisted spectra copied to pinned host
-memory inside the timed region).  ``--schedule batch`` solves each step's batch alone.
+``--schedule batch`` (default): each step solves its ledger batch ALONE, to the last
+replicate -- exactly the work ``cnmf factorize`` does for a ledger of ``--n-iter``
+replicates of K (one solver batch, cnmf.py:876-892), so ``value`` does not depend on
+``--steps``.  ``--schedule stream``: the timed steps' ledger batches are fed, in order,
+through ONE continuous-batching solve (NMFBatchSolver.run_stream: a fixed number of live
+replicate slots per K, each refilled with the next waiting replicate when its replicate
+converged), so the tail of one batch overlaps the next batch's first passes -- the rate of
+a multi-batch job (a K grid or several ledgers in one process).  With the default
+schedule, a single-K run at K <= 16 ALSO times that stream over the same replicates and
+reports it as ``config.stream_value`` (with ``config.stream_replicates``); ``value`` stays
+the per-batch rate.
 
 Run: ``python bench.py [--gpus N --steps K --warmup W --mode weak|strong|dp]``.  N > 1
 runs one process per GPU over RCCL (xGMI): either under ``torch.distributed.run`` (the
@@ -93,9 +95,11 @@ def main() -> int:
                          "sparse-input runs (KL switches to the CSR kernels at <= 0.15)")
     ap.add_argument("--streams", type=int, default=1,
                     help="replicate groups solved concurrently on separate HIP streams")
-    ap.add_argument("--schedule", default="stream", choices=["stream", "batch"],
-                    help="stream: continuous batching over the timed steps' replicates "
-                         "(see module docstring); batch: one solve per step")
+    ap.add_argument("--schedule", default="batch", choices=["stream", "batch"],
+                    help="batch: one solve per step (the factorize job); stream: continuous "
+                         "batching over the timed steps' replicates (see module docstring)")
+    ap.add_argument("--no-stream-value", action="store_true",
+                    help="batch schedule: skip the extra continuous-batching timing")
     ap.add_argument("--live", type=int, default=None,
                     help="stream schedule: live replicate slots per K (default: one "
                          "co-resident round of the usage solve, NMFBatchSolver.stream_live)")
@@ -229,8 +233,8 @@ def main() -> int:
     # not stream wider ranks; a stream over every timed step's replicates would then be ONE
     # batch of all of them).  K = 20 / 30 measured 5,264-5,337 / 3,404-3,499 rep/s as that
     # single batch against 5,730 / 3,779-3,860 one batch per step (profiles/r5zp_*)
-    stream = args.schedule == "stream" and args.mode != "dp" and args.streams == 1 and \
-        int(np.max(grid)) <= 16
+    stream_ok = args.mode != "dp" and args.streams == 1 and int(np.max(grid)) <= 16
+    stream = args.schedule == "stream" and stream_ok
     held = []          # pinned spectra of finished replicates (factorize writes them out)
 
     def keep(ids, kk, host, ev):
@@ -289,6 +293,23 @@ def main() -> int:
     elapsed = max_over_ranks(elapsed)
     ms_per_step = 1000.0 * elapsed / args.steps
     reps_per_sec = n_total * args.steps / elapsed
+
+    # the multi-batch rate of the same replicates (continuous batching), beside the per-batch
+    # value: timed separately, after the headline region
+    stream_value = stream_reps = None
+    if (not stream and stream_ok and len(grid) == 1 and args.schedule == "batch"
+            and not args.no_stream_value and use_cuda):
+        if args.warmup:
+            stream_steps(0, args.warmup)
+        barrier()
+        t1 = time.perf_counter()
+        sres = stream_steps(args.warmup, nsteps)
+        if sres.stats.get("stream_slots") is None:
+            to_host(sres.W)
+        barrier()
+        el_st = max_over_ranks(time.perf_counter() - t1)
+        stream_reps = n_total * args.steps
+        stream_value = stream_reps / el_st
 
     strong_value = strong_ms = None
     if world > 1 and args.mode == "weak":
@@ -361,6 +382,8 @@ def main() -> int:
                 + (f", density {float((X != 0).mean()):.3f}" if args.density is not None else ""),
                 "rccl_world": rccl_world,
                 "backend": backend,
+                "stream_value": None if stream_value is None else round(stream_value, 3),
+                "stream_replicates": stream_reps,
                 "strong_value": None if strong_value is None else round(strong_value, 3),
                 "strong_ms_per_step": None if strong_ms is None else round(strong_ms, 3),
                 "strong_global_batch": per_batch if strong_value is not None else None,

@@ -11,7 +11,7 @@ All run on the device of their input tensor (HIP GPU or CPU):
                                  reproduces ``KMeans(n_clusters=k, n_init=10, random_state=1)``
                                  of cnmf.py:1082 exactly (CPU); ``'device'`` runs on the GPU.
 * ``cluster_medians``         -- H5, per-cluster per-gene median, rows renormalised to 1
-* ``silhouette``              -- H6, from the same distance matrix
+* ``silhouette``              -- H6, from the same distance matrix (segmented row sums)
 """
 from __future__ import annotations
 
@@ -109,19 +109,18 @@ def _lloyd_batched(X: torch.Tensor, centers: torch.Tensor, max_iter: int, tol: f
     if ops.kmeans_fused_ok(X, k):
         return _lloyd_fused(X, centers, max_iter, tol)
     live = torch.ones(n_init, dtype=torch.bool, device=X.device)
-    offs = (torch.arange(n_init, device=X.device) * k)[None, :]
-    onehot = torch.zeros((n, n_init * k), dtype=X.dtype, device=X.device)
-    ones = torch.ones((n, n_init), dtype=X.dtype, device=X.device)
+    ones = torch.ones((n_init, n), dtype=torch.float64, device=X.device)
     for it in range(max_iter):
         C = centers.reshape(n_init * k, d)
         lab, _ = ops.seg_argmin(ops.pairwise_dist(X, C, squared=True), k)
-        # cluster sums of every restart as ONE (n_init*k x n)(n x d) GEMM of the one-hot
-        # assignment (deterministic, no scatter loop over restarts)
-        onehot.zero_().scatter_(1, lab + offs, ones)
-        sums = onehot.t() @ X
-        counts = onehot.sum(dim=0)
-        newc = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], C)
-        newc = newc.view(n_init, k, d)
+        # cluster sums of every restart in one segmented-sum launch (segsum.hip: float64,
+        # points summed in index order -- no one-hot matrix, no library GEMM)
+        labT = lab.t().contiguous()                                   # (n_init, n)
+        sums = ops.seg_colsum(X, labT, k)                              # (n_init, k, d)
+        counts = torch.zeros((n_init, k), dtype=torch.float64, device=X.device)
+        counts.scatter_add_(1, labT, ones)                             # exact (integers)
+        newc = torch.where(counts[..., None] > 0,
+                           sums / counts.clamp(min=1)[..., None], centers).to(X.dtype)
         shift = ((newc - centers) ** 2).sum(dim=(1, 2))
         centers = torch.where(live[:, None, None], newc, centers)
         live = live & (shift > tol)
@@ -221,11 +220,10 @@ def silhouette(dist: torch.Tensor, labels: np.ndarray) -> float:
     """Mean silhouette coefficient from a precomputed distance matrix (sklearn semantics:
     singleton clusters score 0)."""
     lab = torch.as_tensor(np.asarray(labels), device=dist.device)
-    uniq = torch.unique(lab)
-    onehot = (lab[:, None] == uniq[None, :]).to(dist.dtype)       # n x c
-    sums = dist @ onehot                                           # n x c
-    counts = onehot.sum(dim=0)
-    own = (onehot * torch.arange(len(uniq), device=dist.device)[None, :]).sum(dim=1).long()
+    uniq, own = torch.unique(lab, return_inverse=True)
+    # per-row cluster sums of the distances (segsum.hip: float64, fixed order, no GEMM)
+    sums = ops.seg_rowsum(dist, own, len(uniq))                    # n x c
+    counts = torch.bincount(own, minlength=len(uniq)).to(torch.float64)
     own_cnt = counts[own]
     a = sums[torch.arange(len(lab)), own] / torch.clamp(own_cnt - 1, min=1)
     other = sums / counts[None, :]

@@ -10,6 +10,7 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from .. import ops
 from .nmf_base import _to_device
 
 
@@ -208,6 +209,62 @@ class _Batch:
         n_new = int(sum(k.size for k in keep))
         if n_new == n:
             return None
+        dev = self.W.device
+        if self.swap_ok:
+            perm = self._compact_swap(act, n_new)
+        else:
+            perm = self._compact_gather(keep, rest, n)
+        self.order = self.order[perm]
+        self.kpos = self.kpos[perm]
+        self.n_act = n_new
+        self.layout_version += 1
+        self._layout()
+        if self.on_retire is not None and dev.type == "cuda":
+            # positions [n_new, n) are the newly finished ones (flags only go 1 -> 0); their
+            # spectra are final: every later kernel skips them, and this copy is in stream
+            # order after the last one that wrote them
+            roff_new = np.concatenate([[0], np.cumsum(self.kpos)])
+            ra, rb = int(roff_new[n_new]), int(roff_new[n])
+            host = torch.empty((rb - ra, self.W.shape[1]), dtype=self.W.dtype, pin_memory=True)
+            host.copy_(self.W[ra:rb], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self.on_retire(self.order[n_new:n].copy(), self.kpos[n_new:n].copy(), host, ev)
+        return perm
+
+    @property
+    def swap_ok(self) -> bool:
+        """Compaction by in-place position swaps (``_compact_swap``): a single-K arena batch
+        without per-position statistics (the 'exact' online mode's A / B).  Mixed-K
+        batches shift whole groups when one shrinks and keep the gather form."""
+        return (self.inplace and len(self.groups) == 1 and self.B is None
+                and os.environ.get("CNMF_COMPACT_SWAP", "1") != "0")
+
+    def _compact_swap(self, act: np.ndarray, n_new: int) -> np.ndarray:
+        """The live replicates beyond the new prefix [0, n_new) trade places with finished
+        ones inside it -- disjoint swaps, one kernel (ops.rows_swap), and only the movers'
+        rows are touched.  Positions [n_new, n) then hold finished replicates only, as
+        after the gather form (the padding of the bucketed prefix stays finished ones)."""
+        n = self.n_act
+        K = int(self.kpos[0])
+        idx = np.arange(n)
+        holes = idx[:n_new][~act[:n_new]]
+        movers = idx[n_new:][act[n_new:]]
+        m = movers.size
+        assert m <= holes.size
+        perm = np.arange(self.R, dtype=np.int64)
+        perm[holes[:m]] = movers
+        perm[movers] = holes[:m]
+        if m:
+            pairs = np.empty(2 * m, dtype=np.int32)
+            pairs[0::2], pairs[1::2] = holes[:m], movers
+            pt = torch.from_numpy(pairs)
+            if self.W.device.type == "cuda":
+                pt = pt.pin_memory().to(self.W.device, non_blocking=True)
+            ops.rows_swap(pt, K, [self.HT, self.W], self.arena["sf"], self.arena["si"])
+        return perm
+
+    def _compact_gather(self, keep, rest, n: int) -> np.ndarray:
         perm = np.concatenate(keep + rest + [np.arange(n, self.R)]).astype(np.int64)
         dev = self.W.device
         roff = np.concatenate([[0], np.cumsum(self.kpos)[:-1]])
@@ -229,22 +286,6 @@ class _Batch:
             sq = self.kpos * self.kpos
             qoff = np.concatenate([[0], np.cumsum(sq)[:-1]])
             self.A = self.A.index_select(0, _to_device(_ranges(qoff[perm], sq[perm]), dev))
-        self.order = self.order[perm]
-        self.kpos = self.kpos[perm]
-        self.n_act = n_new
-        self.layout_version += 1
-        self._layout()
-        if self.on_retire is not None and dev.type == "cuda":
-            # positions [n_new, n) are the newly finished ones (flags only go 1 -> 0); their
-            # spectra are final: every later kernel skips them, and this copy is in stream
-            # order after the last one that wrote them
-            roff_new = np.concatenate([[0], np.cumsum(self.kpos)])
-            ra, rb = int(roff_new[n_new]), int(roff_new[n])
-            host = torch.empty((rb - ra, self.W.shape[1]), dtype=self.W.dtype, pin_memory=True)
-            host.copy_(self.W[ra:rb], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            self.on_retire(self.order[n_new:n].copy(), self.kpos[n_new:n].copy(), host, ev)
         return perm
 
     def set_err(self, err: torch.Tensor, pass_idx: int, tol: float, final: bool,
@@ -324,9 +365,16 @@ class _PassPipeline:
         # their elementwise passes over X shrink with every retired replicate)
         self.frac_small = compact_frac if (explicit or not late_small) else \
             float(os.environ.get("CNMF_COMPACT_FRAC_SMALL", "0.75"))
+        # single-K arena batches compact by in-place swaps (_Batch._compact_swap: only the
+        # movers' rows, one launch), cheap enough to shrink the batch at every bucket of
+        # finished replicates (CNMF_COMPACT_FRAC_SWAP; 0 = any shrink of the prefix)
+        self.swap = not explicit and "CNMF_COMPACT_FRAC_SMALL" not in os.environ
+        self.frac_swap = float(os.environ.get("CNMF_COMPACT_FRAC_SWAP", "0"))
         self.pending = None   # (event, host_flags, n)
 
     def _frac(self, n: int) -> float:
+        if self.swap and self.st.swap_ok:
+            return self.frac_swap
         return self.frac_small if n <= 256 else self.frac
 
     def after_enqueue(self) -> bool:

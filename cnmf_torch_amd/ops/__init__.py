@@ -725,6 +725,56 @@ def stream_swap(grp: dict, ring: dict, store: dict, state: tuple, gate: torch.Te
     _hip.stream_swap(vals, int(chunks), _stream_ptr(W))
 
 
+def rows_swap(pairs: torch.Tensor, K: int, mats, sf: torch.Tensor | None = None,
+              si: torch.Tensor | None = None, chunks: int = 16) -> None:
+    """Exchange positions ``pairs[2i]`` <-> ``pairs[2i+1]`` in place (disjoint pairs;
+    stream.hip rows_swap_kernel -- _Batch.compact's swap form): K rows per position of
+    every matrix in ``mats`` (2-D float32 / int16 views with unit column stride, or 3-D
+    (planes, rows, cols) int16 plane stacks) and one column of the per-position state
+    tables ``sf`` (rows x R float64) / ``si`` (rows x R int32).  Only the replicates that
+    change position are read or written."""
+    npairs = pairs.numel() // 2
+    if npairs == 0:
+        return
+    if pairs.dtype != torch.int32 or not pairs.is_contiguous() or pairs.numel() % 2:
+        raise ValueError("rows_swap: contiguous int32 pairs [2 npairs]")
+    if not use_native(pairs):
+        a, b = pairs[0::2].long(), pairs[1::2].long()
+        if torch.unique(torch.cat([a, b])).numel() != 2 * npairs:
+            raise ValueError("rows_swap: pairs must be disjoint")
+        ra = (a[:, None] * K + torch.arange(K)).reshape(-1)
+        rb = (b[:, None] * K + torch.arange(K)).reshape(-1)
+        for t in mats:
+            t3 = t if t.dim() == 3 else t.unsqueeze(0)
+            ta = t3[:, ra].clone()
+            t3[:, ra] = t3[:, rb]
+            t3[:, rb] = ta
+        for t in (sf, si):
+            if t is not None:
+                ta = t[:, a].clone()
+                t[:, a] = t[:, b]
+                t[:, b] = ta
+        return
+    if len(mats) > 4:
+        raise ValueError("rows_swap: at most 4 matrices")
+    desc = []
+    for t in mats:
+        t3 = t if t.dim() == 3 else t.unsqueeze(0)
+        if t3.dtype not in (torch.float32, torch.int16) or t3.stride(2) != 1 or \
+                t3.device != pairs.device or t3.shape[0] > 3:
+            raise ValueError("rows_swap: float32 / int16 rows with unit column stride")
+        desc.append((t3.data_ptr(), t3.stride(1), t3.stride(0) if t3.shape[0] > 1 else 0,
+                     t3.shape[2], t3.element_size(), t3.shape[0]))
+    for name, t, dt in (("sf", sf, torch.float64), ("si", si, torch.int32)):
+        if t is not None and (t.dtype != dt or t.stride(1) != 1 or t.shape[0] > 8):
+            raise ValueError(f"rows_swap: {name} must be (<= 8, R) {dt} rows")
+    _hip.rows_swap(pairs.data_ptr(), npairs, int(K), desc,
+                   sf.data_ptr() if sf is not None else 0, sf.stride(0) if sf is not None else 0,
+                   sf.shape[0] if sf is not None else 0,
+                   si.data_ptr() if si is not None else 0, si.stride(0) if si is not None else 0,
+                   si.shape[0] if si is not None else 0, int(chunks), _stream_ptr(pairs))
+
+
 class HostMailbox:
     """Pinned host int32 rows a kernel writes directly (device-mapped pinned memory): a
     pass's small results reach the host with no copy launch.  Row s % slots holds
@@ -1472,6 +1522,47 @@ def seg_argmin(D: torch.Tensor, k: int, row_add: torch.Tensor | None = None,
                     ca.data_ptr() if ca is not None else 0, lab.data_ptr(), mind.data_ptr(),
                     _stream_ptr(Dd))
     return lab.long(), mind
+
+
+def seg_colsum(X: torch.Tensor, lab: torch.Tensor, k: int) -> torch.Tensor:
+    """k-means centroid sums of every restart (segsum.hip, H4): for X (n, d) and labels
+    ``lab`` (n_init, n) in [0, k), out[r, c] = sum of the rows i with lab[r, i] == c --
+    float64, summed in point order (no one-hot matrix, no library GEMM)."""
+    n, d = X.shape
+    nr = lab.shape[0]
+    if lab.dim() != 2 or lab.shape[1] != n or k < 1:
+        raise ValueError(f"seg_colsum: lab (n_init, {n}) and k >= 1 required")
+    if not use_native(X) or k > 256:     # (k > 256: the LDS tables do not fit; torch op)
+        out = torch.zeros((nr, k, d), dtype=torch.float64, device=X.device)
+        Xd = X.to(torch.float64)
+        for r in range(nr):
+            out[r].index_add_(0, lab[r].long(), Xd)
+        return out
+    Xd = _f64_rows(X)
+    lb = lab.to(torch.int32).contiguous()
+    out = torch.empty((nr, k, d), dtype=torch.float64, device=X.device)
+    _hip.seg_colsum(Xd.data_ptr(), Xd.stride(0), n, d, lb.data_ptr(), lb.stride(0), nr, int(k),
+                    out.data_ptr(), _stream_ptr(Xd))
+    return out
+
+
+def seg_rowsum(D: torch.Tensor, lab: torch.Tensor, k: int) -> torch.Tensor:
+    """Per-row cluster sums of a distance matrix (segsum.hip, H6): for D (n, m) and column
+    labels ``lab`` (m,) in [0, k), out[i, c] = sum_j D[i, j] over lab[j] == c -- float64
+    in a fixed order (the silhouette's a / b terms, no one-hot GEMM)."""
+    n, m = D.shape
+    if lab.dim() != 1 or lab.shape[0] != m or k < 1:
+        raise ValueError(f"seg_rowsum: lab ({m},) and k >= 1 required")
+    if not use_native(D) or k > 256:
+        out = torch.zeros((k, n), dtype=torch.float64, device=D.device)
+        out.index_add_(0, lab.long(), D.to(torch.float64).t())
+        return out.t().contiguous()
+    Dd = _f64_rows(D)
+    lb = lab.to(torch.int32).contiguous()
+    out = torch.empty((n, k), dtype=torch.float64, device=D.device)
+    _hip.seg_rowsum(Dd.data_ptr(), Dd.stride(0), n, m, lb.data_ptr(), int(k), out.data_ptr(),
+                    out.stride(0), _stream_ptr(Dd))
+    return out
 
 
 def seg_median(S: torch.Tensor, rank: np.ndarray, k: int) -> torch.Tensor | None:

@@ -145,6 +145,32 @@ PYBIND11_MODULE(_hip, m) {
           "cnmf_stream_swap");
   });
 
+  // in-place compaction swap: pairs ptr, K, [(ptr, ld, plane, cols, esz, planes) x nmat],
+  // (sf, sf_ld, nsf), (si, si_ld, nsi)
+  m.def("rows_swap", [](uintptr_t pairs, int npairs, int K, py::sequence mats, uintptr_t sf,
+                        long long sf_ld, int nsf, uintptr_t si, long long si_ld, int nsi,
+                        int chunks, uintptr_t stream) {
+    cnmf::RowsSwap p{};
+    p.K = K;
+    p.pairs = P<const int>(pairs);
+    p.nmat = (int)py::len(mats);
+    if (p.nmat > 4) throw std::runtime_error("rows_swap: at most 4 matrices");
+    for (int m_ = 0; m_ < p.nmat; ++m_) {
+      py::sequence q = mats[m_];
+      if (py::len(q) != 6) throw std::runtime_error("rows_swap: 6 fields per matrix");
+      p.mat[m_].p = reinterpret_cast<void*>(q[0].cast<uintptr_t>());
+      p.mat[m_].ld = q[1].cast<long long>();
+      p.mat[m_].plane = q[2].cast<long long>();
+      p.mat[m_].cols = q[3].cast<int>();
+      p.mat[m_].esz = q[4].cast<int>();
+      p.mat[m_].planes = q[5].cast<int>();
+    }
+    p.sf = P<double>(sf); p.sf_ld = sf_ld; p.nsf = nsf;
+    p.si = P<int>(si); p.si_ld = si_ld; p.nsi = nsi;
+    check(cnmf_rows_swap(&p, npairs, chunks, reinterpret_cast<hipStream_t>(stream)),
+          "cnmf_rows_swap");
+  });
+
   m.def("stream_publish", [](uintptr_t ctr, int n, uintptr_t seq, uintptr_t mail, int slots,
                              int width, uintptr_t stream) {
     check(cnmf_stream_publish(P<const int>(ctr), n, P<int>(seq), P<int>(mail), slots, width,
@@ -267,6 +293,18 @@ PYBIND11_MODULE(_hip, m) {
     check(cnmf_knn_sum(P<const double>(D), ldd, n, mm, k, P<double>(out),
                        reinterpret_cast<hipStream_t>(stream)),
           "knn_sum");
+  });
+  m.def("seg_colsum", [](uintptr_t X, long long ldx, int n, int d, uintptr_t lab, long long ldl,
+                         int nrest, int k, uintptr_t out, uintptr_t stream) {
+    check(cnmf_seg_colsum(P<const double>(X), ldx, n, d, P<const int>(lab), ldl, nrest, k,
+                          P<double>(out), reinterpret_cast<hipStream_t>(stream)),
+          "seg_colsum");
+  });
+  m.def("seg_rowsum", [](uintptr_t D, long long ldd, int n, int m_, uintptr_t lab, int k,
+                         uintptr_t out, long long ldo, uintptr_t stream) {
+    check(cnmf_seg_rowsum(P<const double>(D), ldd, n, m_, P<const int>(lab), k, P<double>(out),
+                          ldo, reinterpret_cast<hipStream_t>(stream)),
+          "seg_rowsum");
   });
   m.def("seg_argmin", [](uintptr_t D, long long ldd, int n, int nseg, int k, uintptr_t row_add,
                          uintptr_t col_add, uintptr_t labels, uintptr_t mind, uintptr_t stream) {

@@ -28,6 +28,7 @@ hipError_t cnmf_solve(int algo, int K, float* x, long long x_rs, long long ldx, 
                       hipStream_t stream);
 
 hipError_t cnmf_stream_swap(const cnmf::StreamSwap* args, int chunks, hipStream_t stream);
+hipError_t cnmf_rows_swap(const cnmf::RowsSwap* args, int npairs, int chunks, hipStream_t stream);
 hipError_t cnmf_stream_publish(const int* ctr, int n, int* seq, int* mail, int slots, int width,
                                hipStream_t stream);
 
@@ -111,6 +112,10 @@ hipError_t cnmf_pairdist(const double* A, long long lda, const double* B, long l
                          long long ldd, int same, int squared, hipStream_t stream);
 hipError_t cnmf_knn_sum(const double* D, long long ldd, int n, int m, int k, double* out,
                         hipStream_t stream);
+hipError_t cnmf_seg_colsum(const double* X, long long ldx, int n, int d, const int* lab,
+                           long long ldl, int nrest, int k, double* out, hipStream_t stream);
+hipError_t cnmf_seg_rowsum(const double* D, long long ldd, int n, int m, const int* lab, int k,
+                           double* out, long long ldo, hipStream_t stream);
 hipError_t cnmf_seg_argmin(const double* D, long long ldd, int n, int nseg, int k,
                            const double* row_add, const double* col_add, int* labels,
                            double* mind, hipStream_t stream);

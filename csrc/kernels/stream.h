@@ -32,4 +32,19 @@ struct StreamSwap {
   int* gate;
 };
 
+// One matrix of a compaction swap (rows_swap_kernel): `planes` planes `plane` elements
+// apart, K rows per position at row pitch `ld`, `cols` columns of `esz`-byte elements.
+struct SwapMat {
+  void* p; long long ld; long long plane; int cols; int esz; int planes;
+};
+
+struct RowsSwap {
+  int K;                       // rows per position
+  const int* pairs;            // [2 npairs] disjoint position pairs
+  int nmat;                    // matrices in `mat` (<= 4)
+  SwapMat mat[4];
+  double* sf; long long sf_ld; int nsf;   // per-position float64 state rows
+  int* si; long long si_ld; int nsi;      // per-position int32 state rows
+};
+
 }  // namespace cnmf

@@ -163,7 +163,108 @@ __global__ void stream_publish_kernel(const int* __restrict__ ctr, int n, int* _
   *seq = s + 1;
 }
 
+// In-place batch compaction by disjoint position swaps (models/nmf_batch.py _Batch.compact,
+// single-K batches): pair i exchanges positions pairs[2i] and pairs[2i+1] -- K rows of
+// every listed matrix and one column of each per-replicate state table.  The pairs are
+// disjoint, so every workgroup owns its rows and nothing is staged: only the replicates
+// that change position move (a host gather-and-copy of the whole HT / W moved every row
+// twice).  grid (npairs, chunks): workgroup (i, y) swaps column slice y.
+template <typename T>
+__device__ __forceinline__ void swap_rows(T* __restrict__ a, T* __restrict__ b, long long ld,
+                                          int rows, int cols, int y, int ny) {
+  constexpr int V = 16 / sizeof(T);
+  const int bd = blockDim.x;
+  const bool vec = ((cols | ld) % V) == 0 &&
+                   ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+  if (vec) {
+    const int cv = cols / V;
+    const long long tot = (long long)rows * cv, ldv = ld / V;
+    const long long lo = tot * y / ny, hi = tot * (y + 1) / ny;
+    uint4* a4 = reinterpret_cast<uint4*>(a);
+    uint4* b4 = reinterpret_cast<uint4*>(b);
+    for (long long i0 = lo + threadIdx.x; i0 < hi; i0 += 2LL * bd) {
+      uint4 va[2], vb[2];
+      long long o[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const long long i = i0 + (long long)u * bd;
+        o[u] = -1;
+        if (i < hi) {
+          const long long r = i / cv;
+          o[u] = r * ldv + (i - r * cv);
+          va[u] = a4[o[u]];
+          vb[u] = b4[o[u]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (o[u] >= 0) {
+          a4[o[u]] = vb[u];
+          b4[o[u]] = va[u];
+        }
+    }
+  } else {
+    const long long tot = (long long)rows * cols;
+    const long long lo = tot * y / ny, hi = tot * (y + 1) / ny;
+    for (long long i = lo + threadIdx.x; i < hi; i += bd) {
+      const long long r = i / cols, off = r * ld + (i - r * cols);
+      const T t = a[off];
+      a[off] = b[off];
+      b[off] = t;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) rows_swap_kernel(RowsSwap p) {
+  const int i = blockIdx.x, y = blockIdx.y, ny = gridDim.y;
+  const int pa = p.pairs[2 * i], pb = p.pairs[2 * i + 1];
+  const long long ra = (long long)pa * p.K, rb = (long long)pb * p.K;
+  for (int m = 0; m < p.nmat; ++m) {
+    const SwapMat& q = p.mat[m];
+    for (int pl = 0; pl < q.planes; ++pl) {
+      if (q.esz == 4) {
+        float* base = reinterpret_cast<float*>(q.p) + pl * q.plane;
+        swap_rows(base + ra * q.ld, base + rb * q.ld, q.ld, p.K, q.cols, y, ny);
+      } else {
+        unsigned short* base = reinterpret_cast<unsigned short*>(q.p) + pl * q.plane;
+        swap_rows(base + ra * q.ld, base + rb * q.ld, q.ld, p.K, q.cols, y, ny);
+      }
+    }
+  }
+  if (y != 0) return;
+  const int t = threadIdx.x;
+  if (t < p.nsf) {
+    double* r = p.sf + t * p.sf_ld;
+    const double v = r[pa];
+    r[pa] = r[pb];
+    r[pb] = v;
+  } else if (t >= 64 && t < 64 + p.nsi) {
+    int* r = p.si + (t - 64) * p.si_ld;
+    const int v = r[pa];
+    r[pa] = r[pb];
+    r[pb] = v;
+  }
+}
+
 }  // namespace cnmf
+
+extern "C" hipError_t cnmf_rows_swap(const cnmf::RowsSwap* args, int npairs, int chunks,
+                                     hipStream_t stream) {
+  const cnmf::RowsSwap& p = *args;
+  if (npairs <= 0) return hipSuccess;
+  if (p.K < 1 || chunks < 1 || !p.pairs || p.nmat < 0 || p.nmat > 4 || p.nsf < 0 || p.nsf > 8 ||
+      p.nsi < 0 || p.nsi > 8 || (p.nsf && !p.sf) || (p.nsi && !p.si))
+    return hipErrorInvalidValue;
+  for (int m = 0; m < p.nmat; ++m) {
+    const cnmf::SwapMat& q = p.mat[m];
+    if (!q.p || q.cols < 1 || q.ld < q.cols || (q.esz != 4 && q.esz != 2) || q.planes < 1 ||
+        q.planes > 3)
+      return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(cnmf::rows_swap_kernel, dim3((unsigned)npairs, (unsigned)chunks), dim3(256), 0,
+                     stream, p);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t cnmf_stream_publish(const int* ctr, int n, int* seq, int* mail, int slots,
                                           int width, hipStream_t stream) {

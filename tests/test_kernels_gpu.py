@@ -1923,3 +1923,39 @@ def test_gemm_gate_skips_and_runs():
         finally:
             os.environ.pop("CNMF_GEMM_KSPLIT", None)
             ops.refresh_env()
+
+
+@pytest.mark.parametrize("n,d,k,nr", [(900, 2000, 10, 40), (1234, 333, 7, 3), (64, 70, 200, 2),
+                                      (5, 130, 3, 1)])
+def test_seg_colsum_matches_float64_reference(n, d, k, nr):
+    """segsum.hip seg_colsum (the k-means centroid sums of every restart) == float64
+    index_add over the same labels, to 1e-12 relative; deterministic across calls."""
+    g = torch.Generator().manual_seed(n + d + k)
+    X = torch.rand((n, d), generator=g, dtype=torch.float64)
+    lab = torch.randint(0, k, (nr, n), generator=g)
+    want = ops.seg_colsum(X, lab, k)                  # CPU: index_add in point order
+    got = ops.seg_colsum(X.cuda(), lab.cuda(), k)
+    torch.testing.assert_close(got.cpu(), want, rtol=1e-12, atol=1e-12)
+    assert torch.equal(got, ops.seg_colsum(X.cuda(), lab.cuda(), k))
+
+
+@pytest.mark.parametrize("n,m,k", [(1000, 1000, 10), (333, 777, 57), (65, 64, 250)])
+def test_seg_rowsum_and_device_silhouette_match_sklearn(n, m, k):
+    """segsum.hip seg_rowsum == float64 reference sums; the device silhouette built on
+    it == sklearn.metrics.silhouette_score(precomputed) to 1e-10."""
+    from sklearn.metrics import silhouette_score
+
+    from cnmf_torch_amd.models.consensus import pairwise_distances, silhouette
+
+    g = torch.Generator().manual_seed(n + m + k)
+    D = torch.rand((n, m), generator=g, dtype=torch.float64)
+    lab = torch.randint(0, k, (m,), generator=g)
+    torch.testing.assert_close(ops.seg_rowsum(D.cuda(), lab.cuda(), k).cpu(),
+                               ops.seg_rowsum(D, lab, k), rtol=1e-12, atol=1e-12)
+    rs = np.random.default_rng(k)
+    X = rs.random((n, 12))
+    labs = rs.integers(0, min(k, n // 3), n)
+    Dx = pairwise_distances(torch.from_numpy(X).cuda())
+    got = silhouette(Dx, labs)
+    want = silhouette_score(Dx.cpu().numpy(), labs, metric="precomputed")
+    assert abs(got - want) <= 1e-10

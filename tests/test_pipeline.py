@@ -409,3 +409,22 @@ def test_prediction_error_caches_x_sq_per_tensor():
         got = cNMF._prediction_error(X, U, S, torch.device("cpu"))
         assert abs(got - want) <= 1e-9 * want
     assert X in _XSQ
+
+
+@pytest.mark.parametrize("n,c,seed", [(300, 5, 0), (257, 13, 1), (90, 2, 2)])
+def test_silhouette_matches_sklearn_precomputed(n, c, seed):
+    """consensus.silhouette (segmented per-row cluster sums, ops.seg_rowsum) ==
+    sklearn.metrics.silhouette_score(metric='precomputed') on the same float64 distance
+    matrix to 1e-10 -- singleton clusters included (score 0, as sklearn)."""
+    from sklearn.metrics import silhouette_score
+
+    from cnmf_torch_amd.models.consensus import pairwise_distances, silhouette
+
+    rs = np.random.default_rng(seed)
+    X = rs.random((n, 7)) + rs.integers(0, c, n)[:, None] * 0.5
+    lab = rs.integers(0, c, n)
+    lab[0] = c + 3                       # a singleton cluster with a non-contiguous label
+    D = pairwise_distances(torch.from_numpy(X))
+    got = silhouette(D, lab)
+    want = silhouette_score(D.numpy(), lab, metric="precomputed")
+    assert abs(got - want) <= 1e-10 * max(1.0, abs(want))

@@ -451,3 +451,50 @@ def test_stream_graph_replays_bitwise_eager_and_pass_limit(monkeypatch):
     assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
     assert a.n_iter.max() == 6 and a.n_iter.min() >= 1
     assert np.isfinite(a.err).all() and bool((a.W >= 0).all())
+
+
+def test_rows_swap_kernel_matches_reference():
+    """stream.hip rows_swap_kernel (in-place compaction swaps) == the torch reference swap
+    on float32 rows, int16 plane stacks and the float64 / int32 state columns, bitwise;
+    odd widths take the scalar path, aligned ones the 16-byte one."""
+    g = torch.Generator().manual_seed(3)
+    K, R = 7, 40
+    pairs = torch.tensor([3, 30, 0, 39, 12, 5, 21, 22], dtype=torch.int32)
+    for cols in (2000, 333):
+        HT = torch.randn((R * K, cols), generator=g)
+        W = torch.randn((R * K, cols + 8), generator=g)[:, :cols]       # strided rows
+        pl = torch.randint(-30000, 30000, (3, R * K, 64), generator=g, dtype=torch.int16)
+        sf = torch.randn((3, R), generator=g, dtype=torch.float64)
+        si = torch.randint(0, 100, (5, R), generator=g, dtype=torch.int32)
+        ref = [t.clone() for t in (HT, W, pl, sf, si)]
+        ops.rows_swap(pairs, K, ref[:3], ref[3], ref[4])
+        dev = [t.cuda() for t in (HT, W, pl, sf, si)]
+        ops.rows_swap(pairs.cuda(), K, dev[:3], dev[3], dev[4])
+        for a, b in zip(ref, dev):
+            assert torch.equal(a, b.cpu())
+        # the reference really swapped: position 3 <-> 30
+        assert torch.equal(ref[0][3 * K:4 * K], HT[30 * K:31 * K])
+        assert torch.equal(ref[3][:, 30], sf[:, 3])
+
+
+@pytest.mark.parametrize("K", [10, 20])
+def test_swap_compaction_equals_gather_compaction(monkeypatch, K):
+    """Single-K arena batches compact by in-place swaps of the movers only
+    (_Batch._compact_swap): the run equals the gather-form compaction of the same layouts
+    bit for bit (positions differ, per-replicate arithmetic does not)."""
+    from cnmf_torch_amd.models import nmf
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(6000, 700, n_programs=10, seed=6)).cuda()
+    seeds = list(range(40, 88))
+    opts = nmf.NMFOptions(n_components=K, online_chunk_size=2000, online_chunk_max_iter=1000)
+    monkeypatch.setenv("CNMF_COMPACT_FRAC_SMALL", "0.1")
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("CNMF_COMPACT_SWAP", mode)
+        out[mode] = nmf.NMFBatchSolver(X, opts).run(seeds)
+    a, b = out["0"], out["1"]
+    assert len(set(a.n_iter.tolist())) > 2
+    np.testing.assert_array_equal(a.n_iter, b.n_iter)
+    np.testing.assert_array_equal(a.err, b.err)
+    assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)

@@ -30,6 +30,9 @@ def main():
               f"H iters/solve {hi.sum() / (passes.sum() * nch):.1f} "
               f"(max rep {hi.max() / passes[hi.argmax()] / nch:.1f}); "
               f"W iters/solve {wi.sum() / (passes.sum() * nch):.1f}", flush=True)
+        h = np.bincount(passes.astype(np.int64))
+        print("  replicates per pass count: " +
+              ", ".join(f"{p}:{c}" for p, c in enumerate(h) if c), flush=True)
 
 
 if __name__ == "__main__":
