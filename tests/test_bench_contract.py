@@ -1,5 +1,6 @@
 """bench.py contract: one JSON line from rank 0, whole-job value, max-over-ranks timing.
-Runs the multi-rank path on the CPU (gloo, 2 ranks via torch.distributed.run)."""
+Runs the multi-rank path on the CPU (gloo, 2 and 8 ranks via torch.distributed.run) --
+8 is the driver's scaling world."""
 import json
 import os
 import socket
@@ -102,3 +103,22 @@ def test_bench_world_size_mismatch_fails():
     assert r.returncode != 0
     assert "WORLD_SIZE=3" in r.stderr
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_eight_ranks_weak_strong_dp():
+    """The driver's N=8 launch shape on gloo: weak (3 replicates per rank, 24 per step),
+    strong (ONE 3-replicate ledger batch over 8 ranks: five ranks own nothing) and dp
+    (300 cells in 100-cell chunks over 8 ranks: 12-13 cells per rank and chunk) all
+    complete and print one whole-job JSON line; weak reports its strong form too."""
+    weak = _bench([], 8)
+    assert weak["n_gpus"] == 8 and weak["config"]["rccl_world"] == 8
+    assert weak["config"]["global_batch"] == 24 and weak["scaling"] == "weak"
+    assert weak["config"]["strong_value"] > 0 and weak["config"]["strong_global_batch"] == 3
+    rate = 24 * 2 / (weak["ms_per_step"] * 2 / 1000.0)
+    assert abs(weak["value"] - rate) / weak["value"] < 0.01
+    strong = _bench(["--mode", "strong"], 8)
+    assert strong["config"]["global_batch"] == 3 and strong["scaling"] == "strong"
+    dp = _bench(["--mode", "dp"], 8)
+    assert dp["config"]["parallelism"].startswith("cell-sharded DP x8")
+    one = _bench(["--mode", "dp"], 1)
+    assert abs(one["config"]["mean_passes"] - dp["config"]["mean_passes"]) <= 0.5

@@ -1,6 +1,8 @@
-"""Multi-process tests on the gloo backend (world size 2-3, CPU) -- the fake-cluster
-strategy of SURVEY.md §4 item 4: cell-sharded DP == single process (same schedule),
-replicate-parallel == serial, bit for bit where the math allows."""
+"""Multi-process tests on the gloo backend (world size 2, 3 and 8, CPU) -- the
+fake-cluster strategy of SURVEY.md §4 item 4: cell-sharded DP == single process (same
+schedule), replicate-parallel == serial, bit for bit where the math allows.  The world-8
+cases use the driver's 8-GPU world with uneven shards: fewer replicates than ranks (ranks
+that own none), R mod 8 != 0, and cell shards of unequal length."""
 import os
 import socket
 
@@ -86,7 +88,7 @@ def test_dp_exchange_units():
                                                  ("mu", "batch", "frobenius"),
                                                  ("mu", "batch", "kullback-leibler"),
                                                  ("mu", "online", "kullback-leibler")])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, pytest.param(8, id="8")])
 def test_dp_solver_matches_single_process(tmp_path, algo, mode, beta_loss, world):
     """Chunk-interleaved cell sharding: every online step all-reduces the statistics of
     the SAME global chunk the single-process solver uses, so the DP factorisation equals
@@ -94,6 +96,9 @@ def test_dp_solver_matches_single_process(tmp_path, algo, mode, beta_loss, world
     rank-local decision is the usages' inner stopping rule (its block objective covers
     the rank's slice of the chunk), so it is pinned to a fixed count here
     (online_h_tol < 0); test_dp_default_tolerances_close_to_single_process covers it."""
+    if world == 8 and (algo, mode, beta_loss) not in (("mu", "online", "frobenius"),
+                                                      ("mu", "batch", "kullback-leibler")):
+        pytest.skip("world 8: one online and one batch case")
     X = normalized_counts_matrix(603, 120, n_programs=4, seed=1).astype(np.float64)
     K, seeds = 4, [5, 6, 7]
     kw = dict(algo=algo, mode=mode, online_chunk_size=100, online_max_pass=6, batch_max_iter=30,
@@ -146,23 +151,37 @@ def prepared(tmp_path_factory):
     return d, str(fn)
 
 
-@pytest.mark.parametrize("mode", ["replicate", "dp"])
-def test_distributed_factorize_matches_serial(prepared, mode):
+@pytest.mark.parametrize("mode,world", [("replicate", 2), ("dp", 2), ("replicate", 8),
+                                        ("dp", 8)])
+def test_distributed_factorize_matches_serial(prepared, mode, world):
+    """Replicate-parallel (worker_filter dealing, cnmf.py:53-54) and cell-sharded DP
+    factorize == serial.  World 8: 6 replicates, so ranks 6 and 7 own none (replicate
+    mode), and 400 cells in 150-cell chunks give every rank a shard of 18-19 cells of each
+    chunk (DP)."""
     d, fn = prepared
-    name = f"d_{mode}"
+    name = f"d_{mode}_{world}"
     obj = cNMF(output_dir=str(d), name=name)
     obj.prepare(fn, components=[3, 4], n_iter=3, seed=11, num_highvar_genes=120, batch_size=150)
-    _spawn(W.factorize_worker, 2, str(d), name, mode)
+    _spawn(W.factorize_worker, world, str(d), name, mode)
     par = {(k, i): load_df_from_npz(obj.paths["iter_spectra"] % (k, i)).values
            for k in (3, 4) for i in range(3)}
     serial = cNMF(output_dir=str(d), name=name + "_serial")
     serial.prepare(fn, components=[3, 4], n_iter=3, seed=11, num_highvar_genes=120, batch_size=150)
     serial.factorize()
+    # DP at 8 ranks: each rank stops its usages' inner solve on the block objective of its
+    # OWN ~19 cells of the chunk (the one rank-local decision of the DP schedule,
+    # test_dp_solver_matches_single_process pins it and is exact at world 8), so the
+    # iterates drift from the serial ones by more than summation order
+    loose = mode == "dp" and world > 3
     for (k, i), v in par.items():
         ref = load_df_from_npz(serial.paths["iter_spectra"] % (k, i)).values
         # replicate-parallel: same solves; DP: the chunk-interleaved shard all-reduces the
         # same global chunks as the serial solver -- both differ by fp32 summation only
-        np.testing.assert_allclose(v, ref, rtol=2e-3, atol=1e-6)
+        if loose:
+            cos = (v * ref).sum(1) / np.linalg.norm(v, axis=1) / np.linalg.norm(ref, axis=1)
+            assert cos.min() > 0.99, (k, i, cos)
+        else:
+            np.testing.assert_allclose(v, ref, rtol=2e-3, atol=1e-6)
     if mode == "dp":
         from cnmf_torch_amd.utils.timing import read_jsonl
 
@@ -170,7 +189,8 @@ def test_distributed_factorize_matches_serial(prepared, mode):
         e_se = {(r["k"], r["iter"]): r["err"] for r in read_jsonl(serial.paths["replicate_log"])}
         assert set(e_dp) == set(e_se)
         for key in e_dp:
-            np.testing.assert_allclose(e_dp[key], e_se[key], rtol=1e-4, err_msg=str(key))
+            np.testing.assert_allclose(e_dp[key], e_se[key], rtol=1e-2 if loose else 1e-4,
+                                       err_msg=str(key))
 
 
 def test_gathered_merged_spectra_equal_file_combine(prepared):
@@ -271,9 +291,10 @@ def _write_10x(d, X, cells, genes):
     return os.path.join(d, "matrix.mtx")
 
 
-@pytest.mark.parametrize("fmt", ["h5ad_sparse", "npz_dense", "txt_sparse", "mtx_sparse",
-                                 "npz_densify"])
-def test_sharded_prepare_matches_single_process(tmp_path, fmt):
+@pytest.mark.parametrize("fmt,world", [("h5ad_sparse", 3), ("npz_dense", 3), ("txt_sparse", 3),
+                                       ("mtx_sparse", 3), ("npz_densify", 3),
+                                       ("h5ad_sparse", 8), ("npz_dense", 8)])
+def test_sharded_prepare_matches_single_process(tmp_path, fmt, world):
     """Cell-sharded prepare over 3 gloo ranks -- each rank reads ONLY its cells (partial
     h5ad reads, streamed 10x mtx / npz member / TSV lines), gene statistics from exact
     integer moments all-reduced, row blocks handed to rank 0's writer in messages of at
@@ -298,8 +319,8 @@ def test_sharded_prepare_matches_single_process(tmp_path, fmt):
     bound = 4096
     kw = dict(components=[3, 4], n_iter=3, seed=7, num_highvar_genes=120,
               densify=fmt == "npz_densify")
-    _spawn(W.prepare_worker, 3, str(tmp_path), "sh", fn, dict(kw, _chunk_bytes=bound))
-    for r in range(1, 3):
+    _spawn(W.prepare_worker, world, str(tmp_path), "sh", fn, dict(kw, _chunk_bytes=bound))
+    for r in range(1, world):
         m = int(np.load(tmp_path / f"maxmsg{r}.npy")[0])
         assert 0 < m <= bound, m
     ser = cNMF(output_dir=str(tmp_path), name="se")
@@ -321,12 +342,13 @@ def test_sharded_prepare_matches_single_process(tmp_path, fmt):
     assert pa.equals(pb)
 
 
-def test_gene_sharded_consensus_matches_serial(prepared):
-    """One K on 3 gloo ranks: the TPM spectra refit and the OLS gene scores over G_all are
-    sharded by whole refit chunks (tensor / gene-axis parallelism) and all-gathered; the
-    artifacts equal the serial consensus."""
+@pytest.mark.parametrize("world", [3, 8])
+def test_gene_sharded_consensus_matches_serial(prepared, world):
+    """One K on 3 / 8 gloo ranks: the TPM spectra refit and the OLS gene scores over G_all
+    are sharded by whole refit chunks (tensor / gene-axis parallelism) and all-gathered;
+    the artifacts equal the serial consensus (at 8 ranks some ranks own no gene block)."""
     d, fn = prepared
-    obj = cNMF(output_dir=str(d), name="tp")
+    obj = cNMF(output_dir=str(d), name=f"tp{world}")
     obj.prepare(fn, components=[4], n_iter=4, seed=8, num_highvar_genes=120, batch_size=60)
     obj.factorize(verbose=False)
     obj.combine()
@@ -336,7 +358,7 @@ def test_gene_sharded_consensus_matches_serial(prepared):
     ser = {key: load_df_from_npz(obj.paths[key] % (4, "0_5")) for key in keys}
     for key in keys:
         os.remove(obj.paths[key] % (4, "0_5"))
-    _spawn(W.tp_consensus_worker, 3, str(d), "tp", 4)
+    _spawn(W.tp_consensus_worker, world, str(d), f"tp{world}", 4)
     for key in keys:
         got = load_df_from_npz(obj.paths[key] % (4, "0_5"))
         assert list(got.columns) == list(ser[key].columns), key
