@@ -520,6 +520,14 @@ class _XPlanes:
         # from here and frees them with itself; nothing keeps a second copy alive)
         ahead = _PLANES_AHEAD.pop(X, None) if isinstance(X, torch.Tensor) else None
         if ahead is not None and ahead[0] == (X.data_ptr(), X._version):
+            # allocated on the background builder's (pooled) stream and used from here on
+            # on this one: without record_stream their blocks would return to the builder
+            # stream's pool at free while this stream's kernels may still read them
+            cur = torch.cuda.current_stream(X.device)
+            for v in vars(ahead[1]).values():
+                for t in (v if isinstance(v, (list, tuple)) else (v,)):
+                    if isinstance(t, torch.Tensor) and t.is_cuda:
+                        t.record_stream(cur)
             return ahead[1]
         if X.device.type != "cuda" or X.dtype != torch.float32 or \
                 os.environ.get("CNMF_GEMM", "planes") != "planes":

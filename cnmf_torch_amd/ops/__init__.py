@@ -84,7 +84,8 @@ def use_native(t: torch.Tensor) -> bool:
 def eager_ops():
     """Within this context (per host thread) every op runs its PyTorch reference
     (ops/reference.py) on the operands' own device.  This is the routing for factor ranks
-    the native kernels do not cover (K > 128 Frobenius MU, K > 64 HALS, K > 32 beta != 2;
+    the native kernels do not cover (K > 128 Frobenius MU, K > 64 HALS / KL, K > 56 IS and
+    general beta (models.nmf_base.kernel_max_rank);
     the reference's -k is unbounded, cnmf.py:1417): the caller logs it per job
     (models.nmf.NMFBatchSolver.run, models.refit).  Covered ranks never take it."""
     prev = getattr(_TLS, "eager", False)
@@ -446,6 +447,11 @@ def coop_prepare(dev: torch.device) -> None:
         _coop_resident(dev)
 
 
+# CUs the cooperative solves' co-residency budget leaves to other kernels (RCCL, the
+# overlapped one-shot xGMI collectives -- parallel/xgmi.py caps their blocks at this)
+COOP_MARGIN_CUS = 16
+
+
 def _coop_resident(dev: torch.device) -> int:
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     if key not in _COOP_RESIDENT:
@@ -453,7 +459,7 @@ def _coop_resident(dev: torch.device) -> int:
         # initialises amdsmi (~26 ms inside the first factorize)
         cus = _hip.cu_count(key) if _hip is not None else \
             torch.cuda.get_device_properties(key).multi_processor_count
-        _COOP_RESIDENT[key] = max(1, cus - 16)
+        _COOP_RESIDENT[key] = max(1, cus - COOP_MARGIN_CUS)
     return max(1, _COOP_RESIDENT[key] // getattr(_TLS, "share", 1))
 
 

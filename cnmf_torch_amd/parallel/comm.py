@@ -153,7 +153,8 @@ class DistComm(LocalComm):
         the device epoch and the peer staging) while compute proceeds beside them."""
         cur = torch.cuda.current_stream()
         if self._side is None:
-            self._side = torch.cuda.Stream(device=cur.device)
+            # the collectives' own stream: launches on it run without a further fork
+            self._side = self._xgmi.stream if self._xgmi else torch.cuda.Stream(device=cur.device)
         self._side.wait_stream(cur)
         with torch.cuda.stream(self._side):
             ok = fn()
@@ -255,7 +256,7 @@ class DistComm(LocalComm):
             raise ValueError(f"reduce_scatter_: {inp.numel()} != {self.world_size} x {m}")
         xg = self._xgmi_for(inp)
         if xg is not None:
-            ok, h = self._on_side(lambda: xg.reduce_scatter(out, inp))
+            ok, h = self._on_side(lambda: xg.reduce_scatter(out, inp, overlap=True))
             if ok:
                 return h
         if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():
@@ -280,7 +281,7 @@ class DistComm(LocalComm):
             raise ValueError(f"all_gather_into_: {out.numel()} != {self.world_size} x {m}")
         xg = self._xgmi_for(inp, any_dtype=True)
         if xg is not None:
-            ok, h = self._on_side(lambda: xg.all_gather(out, inp))
+            ok, h = self._on_side(lambda: xg.all_gather(out, inp, overlap=True))
             if ok:
                 return h
         if self.backend == "nccl" and inp.is_cuda and out.is_contiguous() and inp.is_contiguous():

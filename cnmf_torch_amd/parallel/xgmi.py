@@ -69,6 +69,17 @@ class XgmiAllReduce:
         self.cap = -(-cap // 4) * 4
         self.blocks = int(blocks or min(hip.xgmi_max_blocks(),
                                         max(1, hip.cu_count(self.device.index or 0) // 2)))
+        # a collective issued to OVERLAP compute (DistComm's async reduce-scatter /
+        # all-gather under the DP step's cooperative solves) spins inside the kernel until
+        # its peers arrive; its blocks must fit the CUs the cooperative solves' co-residency
+        # budget leaves free (ops._coop_resident keeps COOP_MARGIN_CUS), or a solve's
+        # workgroups could wait on siblings that cannot be placed
+        from ..ops import COOP_MARGIN_CUS
+
+        self.overlap_blocks = max(1, min(self.blocks, COOP_MARGIN_CUS))
+        # every launch runs on this ONE stream (ordered behind the caller's): the calls
+        # share the device epoch counter and the two staging parities
+        self.stream = torch.cuda.Stream(device=self.device)
         ms = int(timeout_ms if timeout_ms is not None else DEFAULT_TIMEOUT_MS)
         self.limit = int(hip.xgmi_wall_clock_khz(self.device.index or 0)) * max(1, ms)
         # Workspace memory: uncached (or fine-grained) device memory, never coarse-grained
@@ -140,15 +151,25 @@ class XgmiAllReduce:
             return None
         return t.reshape(-1).view(torch.uint8).view(torch.float32)
 
-    def _launch(self, mode: int, src: torch.Tensor, dst: torch.Tensor, m: int) -> None:
-        from ..ops import _stream_ptr
-
+    def _launch(self, mode: int, src: torch.Tensor, dst: torch.Tensor, m: int,
+                overlap: bool = False) -> None:
+        # every collective shares one device epoch counter and two staging parities, which
+        # is only sound when all launches are ordered on one stream: a call from another
+        # stream forks onto self.stream and joins back (also inside a graph capture)
+        cur = torch.cuda.current_stream(self.device)
+        fork = cur.cuda_stream != self.stream.cuda_stream
+        if fork:
+            self.stream.wait_stream(cur)
         self.epoch += 1
         e = self.ep
         _hip().xgmi_collective(mode, self.peers.data_ptr(), self.world, self.rank,
                                src.data_ptr(), dst.data_ptr(), int(m), self.cap, 0,
                                e.data_ptr(), e.data_ptr() + 4, self.limit,
-                               self.timeout.data_ptr(), self.blocks, _stream_ptr(src))
+                               self.timeout.data_ptr(),
+                               self.overlap_blocks if overlap else self.blocks,
+                               self.stream.cuda_stream)
+        if fork:      # (the caller's stream waits: its later frees of src / dst are safe)
+            cur.wait_stream(self.stream)
 
     def __call__(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """Sum of ``t`` over the ranks into ``out`` (default: in place)."""
@@ -161,7 +182,7 @@ class XgmiAllReduce:
         self._launch(0, t, out, t.numel())
         return out
 
-    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor) -> bool:
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False) -> bool:
         """out = chunk ``rank`` of the rank-ordered sum of ``inp`` (world equal chunks,
         rank-major): each rank reads only its chunk from every peer -- one hop per link.
         float32 only (a sum).  Returns False when the buffers do not qualify."""
@@ -170,10 +191,10 @@ class XgmiAllReduce:
                 not (inp.is_contiguous() and out.is_contiguous()) or \
                 inp.numel() != out.numel() * self.world or inp.numel() > self.cap:
             return False
-        self._launch(1, inp, out, out.numel())
+        self._launch(1, inp, out, out.numel(), overlap)
         return True
 
-    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> bool:
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, overlap: bool = False) -> bool:
         """out (world equal chunks, rank-major) = every rank's ``inp``; any dtype whose
         buffers are whole 4-byte words.  Returns False when the buffers do not qualify."""
         src, dst = self._f32(inp), self._f32(out)
@@ -181,7 +202,7 @@ class XgmiAllReduce:
                 out.device != self.device or dst.numel() != src.numel() * self.world or \
                 src.numel() > self.cap:
             return False
-        self._launch(2, src, dst, src.numel())
+        self._launch(2, src, dst, src.numel(), overlap)
         return True
 
     def check(self) -> None:

@@ -442,7 +442,7 @@ __global__ void __launch_bounds__(kPpBlock) ppsample_kernel(
     const double* __restrict__ u, int trials, long long* __restrict__ cand) {
   extern __shared__ double pre[];          // nb block prefix sums
   __shared__ double sc[kPpBlock];
-  __shared__ int s_hit;
+  __shared__ int s_hit, s_last;
   const int r = blockIdx.x, tid = threadIdx.x;
   double carry = 0.0;
   for (int b0 = 0; b0 < nb; b0 += kPpBlock) {
@@ -466,13 +466,22 @@ __global__ void __launch_bounds__(kPpBlock) ppsample_kernel(
     const double base = b > 0 ? pre[b - 1] : 0.0;
     const long long i = (long long)b * kPpBlock + tid;
     const double v = i < n ? closest[i * n_init + r] : 0.0;
-    if (tid == 0) s_hit = kPpBlock;
+    if (tid == 0) {
+      s_hit = kPpBlock;
+      s_last = -1;
+    }
     __syncthreads();
     const double inc = base + pp_scan(v, sc);
     if (inc >= target && i < n) atomicMin(&s_hit, tid);
+    if (v > 0.0 && i < n) atomicMax(&s_last, tid);
     __syncthreads();
     if (tid == 0) {
-      long long idx = (long long)b * kPpBlock + (s_hit < kPpBlock ? s_hit : kPpBlock - 1);
+      // the block sums (ppsum, tree order) and this in-block scan round differently: a
+      // target the block's prefix reached may stay just above base + scan.  Then take the
+      // block's last point of positive weight (never a zero-potential point: an existing
+      // centre or padding), as searchsorted does for a target at the running total
+      const int hit = s_hit < kPpBlock ? s_hit : (s_last >= 0 ? s_last : kPpBlock - 1);
+      long long idx = (long long)b * kPpBlock + hit;
       if (idx > n - 1) idx = n - 1;
       cand[(long long)r * trials + t] = idx;
     }

@@ -73,13 +73,25 @@ __global__ void __launch_bounds__(1024) stream_plan_kernel(StreamSwap p) {
 // rows x cols of T from src (row pitch lds) to dst (ldd), slice y of ny of the flattened
 // (row, 16-byte vector) index space -- every thread issues 4 independent loads before
 // its stores; scalar when a pitch or a base does not allow 16-byte vectors
+// ``vec`` (16-byte vectors) is decided ONCE per matrix by the caller from every base the
+// harvest and the placement of a position touch: both phases then cut the (rows x cols)
+// range into the same slices, so the __syncthreads between them orders every element's
+// read-out before its overwrite (per-call decisions could slice the two differently).
+template <typename T>
+__device__ __forceinline__ bool sw_vec(int cols, long long ld, const void* a, const void* b,
+                                       const void* c) {
+  constexpr int V = 16 / sizeof(T);
+  return ((cols | ld) % V) == 0 &&
+         ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) |
+           reinterpret_cast<uintptr_t>(c)) & 15) == 0;
+}
+
 template <typename T>
 __device__ __forceinline__ void sw_rows(const T* __restrict__ src, long long lds, T* __restrict__ dst,
-                                        long long ldd, int rows, int cols, int y, int ny) {
+                                        long long ldd, int rows, int cols, int y, int ny,
+                                        bool vec) {
   constexpr int V = 16 / sizeof(T);
   const int bd = blockDim.x;
-  const bool vec = ((cols | lds | ldd) % V) == 0 &&
-                   ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15) == 0;
   if (vec) {
     const int cv = cols / V;
     const long long tot = (long long)rows * cv;
@@ -121,10 +133,17 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(StreamSwap p) {
   if (e < 0 && h < 0) return;
   const int K = p.K, tid = threadIdx.x;
   const long long r0 = (long long)pos * K;
+  const int slot = e >= 0 ? e % p.qc : 0;
+  const long long s0 = (long long)slot * K;
+  const long long o = h >= 0 ? p.offs[h] : 0;
+  float* Wp = p.W + r0 * p.ldw;
+  float* Hp = p.HT + r0 * p.ldh;
+  const bool vw = sw_vec<float>(p.G, p.ldw, Wp, p.oW + o * p.ldw, p.rW + s0 * p.ldw);
+  const bool vh = sw_vec<float>(p.N, p.ldh, Hp, p.oHT ? p.oHT + o * p.ldh : Hp,
+                                p.N > 0 ? p.rHT + s0 * p.ldh : Hp);
   if (h >= 0) {
-    const long long o = p.offs[h];
-    sw_rows(p.W + r0 * p.ldw, p.ldw, p.oW + o * p.ldw, p.ldw, K, p.G, y, ny);
-    if (p.oHT) sw_rows(p.HT + r0 * p.ldh, p.ldh, p.oHT + o * p.ldh, p.ldh, K, p.N, y, ny);
+    sw_rows(Wp, p.ldw, p.oW + o * p.ldw, p.ldw, K, p.G, y, ny, vw);
+    if (p.oHT) sw_rows(Hp, p.ldh, p.oHT + o * p.ldh, p.ldh, K, p.N, y, ny, vh);
     if (y == 0) {
       if (tid < 3) p.osf[tid * p.osf_ld + h] = p.sf[tid * p.sf_ld + pos];
       else if (tid < 8) p.osi[(tid - 3) * p.osi_ld + h] = p.si[(tid - 3) * p.si_ld + pos];
@@ -132,13 +151,13 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(StreamSwap p) {
   }
   if (e < 0) return;
   __syncthreads();     // this slice of the position is read out before it is overwritten
-  const int slot = e % p.qc;
-  const long long s0 = (long long)slot * K;
-  sw_rows(p.rW + s0 * p.ldw, p.ldw, p.W + r0 * p.ldw, p.ldw, K, p.G, y, ny);
-  if (p.N > 0) sw_rows(p.rHT + s0 * p.ldh, p.ldh, p.HT + r0 * p.ldh, p.ldh, K, p.N, y, ny);
-  for (int pl = 0; pl < 3; ++pl)
-    sw_rows(p.rwpl + pl * p.rpl_plane + s0 * p.pl_ld, p.pl_ld,
-            p.wpl + pl * p.pl_plane + r0 * p.pl_ld, p.pl_ld, K, p.Gp, y, ny);
+  sw_rows(p.rW + s0 * p.ldw, p.ldw, Wp, p.ldw, K, p.G, y, ny, vw);
+  if (p.N > 0) sw_rows(p.rHT + s0 * p.ldh, p.ldh, Hp, p.ldh, K, p.N, y, ny, vh);
+  for (int pl = 0; pl < 3; ++pl) {
+    const unsigned short* ps = p.rwpl + pl * p.rpl_plane + s0 * p.pl_ld;
+    unsigned short* pd = p.wpl + pl * p.pl_plane + r0 * p.pl_ld;
+    sw_rows(ps, p.pl_ld, pd, p.pl_ld, K, p.Gp, y, ny, sw_vec<unsigned short>(p.Gp, p.pl_ld, ps, pd, pd));
+  }
   if (y == 0) {
     const int blk = p.S * K * K;
     const float* sp = p.rparts + (long long)slot * blk;

@@ -435,6 +435,18 @@ def test_kmeanspp_sample_matches_cumsum_searchsorted(n):
     diff = (got - ref).abs()
     assert int((diff > 0).sum()) <= 1 and int(diff.max()) <= 1
     assert got[0, 0] == 0 and got[2, 0] == n // 3
+    # zeroed tails and u at (or a hair below) 1: the draw is the LAST point of positive
+    # potential, never a zero-potential one past it (existing centres, padding)
+    tail = closest.clone()
+    last = (3 * n) // 5
+    tail[last + 1:, :] = 0.0
+    ut = torch.full((n_init, trials), 1.0 - 1e-16, dtype=torch.float64)
+    ut[:, 0] = 1.0
+    got_t = ops.kmeanspp_sample(tail.cuda().contiguous(), ut.cuda()).cpu()
+    assert int(got_t.max()) <= last
+    pos = tail.t() > 0
+    assert bool(pos[torch.arange(n_init)[:, None], got_t].all())
+    assert (got_t[:, 0] == last).all()
 
 
 def test_device_kmeans_large_n_uses_fused_init():
