@@ -449,7 +449,10 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
             s_.wait_stream(main)
 
         def work(i):
+            from .nmf_graphs import _TLS
+
             torch.cuda.set_device(dev)
+            _TLS.no_graphs = True            # eager passes in the worker threads
             with torch.cuda.stream(streams[i]), ops.coop_share(n_streams):
                 return self.run(groups[i])
 
@@ -894,7 +897,7 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
                 if graph_key != key:
                     try:
                         graph = torch.cuda.CUDAGraph()
-                        with torch.cuda.graph(graph):
+                        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
                             enqueue_pass(-1, False)
                         graph_key = key
                     except RuntimeError:          # capture unsupported here: stay eager

@@ -373,7 +373,11 @@ class _PassPipeline:
         self.pending = None   # (event, host_flags, n)
 
     def _frac(self, n: int) -> float:
-        if self.swap and self.st.swap_ok:
+        # (the policy depends on the batch's shape only, never on whether it compacts by
+        # swaps or gathers: the compacted layouts re-plan the GEMMs' k split, so two runs
+        # of the same replicates agree bit for bit only through the same layouts)
+        if self.swap and self.cuda and len(self.st.groups) == 1 and \
+                os.environ.get("CNMF_COMPACT_SWAP", "1") != "0":
             return self.frac_swap
         return self.frac_small if n <= 256 else self.frac
 

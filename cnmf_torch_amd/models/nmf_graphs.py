@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import collections
 import os
+import threading
 
 import numpy as np
 import torch
@@ -11,6 +12,12 @@ import torch
 from .. import ops
 from .nmf_base import log
 from .nmf_batch import _Batch
+
+
+# per host thread: no graph capture (NMFBatchSolver.run_concurrent's workers -- a capture
+# in one thread while another thread allocates and frees on its own stream is outside
+# what the caching allocator's capture pools guarantee)
+_TLS = threading.local()
 
 
 class _GraphMixin:
@@ -27,6 +34,8 @@ class _GraphMixin:
         env = os.environ.get("CNMF_GRAPHS", "auto")
         o = self.opts
         if env == "0" or self.X.device.type != "cuda" or self.beta != 2.0 or o.mode != "online":
+            return False
+        if getattr(_TLS, "no_graphs", False):     # run_concurrent's worker threads
             return False
         if env != "1" and len(kpos) > 256:
             return False
@@ -99,7 +108,9 @@ class _GraphMixin:
             sl["stream"].wait_stream(main)
             try:
                 with torch.cuda.stream(sl["stream"]):
-                    g.capture_begin()
+                    # thread-local capture: run_concurrent's other host threads keep
+                    # issuing (and synchronising) their own streams meanwhile
+                    g.capture_begin(capture_error_mode="thread_local")
                     try:
                         self._fused_pass(st, steps, sl["fb"], False)
                     finally:

@@ -586,9 +586,13 @@ def _coop_workspace(dev: torch.device, stream: int, R: int, epochs: int, S: int)
         gen_dev = ws["gen_dev"] if ws is not None else \
             torch.full((1,), -(1 << 31), dtype=torch.int32, device=dev)
         arrive = ws["arrive"] if ws is not None else torch.zeros(1, dtype=torch.int32, device=dev)
+        # a grown workspace never frees the one it replaces: HIP graphs captured earlier
+        # (other layouts, other solvers -- torch hands out streams from a small pool, so
+        # unrelated captures share this key) keep writing their granules there
+        retired = (ws["retired"] + [ws["slots"]]) if ws is not None else []
         ws = {"slots": torch.zeros(max(need_slots, 1 << 16), dtype=torch.int64, device=dev),
               "gen": ws["gen"] if ws is not None else 0,
-              "flag": flag, "gen_dev": gen_dev, "arrive": arrive}
+              "flag": flag, "gen_dev": gen_dev, "arrive": arrive, "retired": retired}
         _COOP_WS[key] = ws
     return ws
 

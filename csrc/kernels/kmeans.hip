@@ -462,7 +462,11 @@ __global__ void __launch_bounds__(kPpBlock) ppsample_kernel(
       const int mid = (lo + hi) >> 1;
       if (pre[mid] >= target) hi = mid; else lo = mid + 1;
     }
-    const int b = lo;
+    // the block sums' own scan can round a later all-zero block's prefix above the last
+    // positive block's: step back to the block holding the last positive weight before it
+    // (the target lies past every earlier block's prefix, so the draw is in that block)
+    int b = lo;
+    while (b > 0 && !(bsum[(long long)r * nb + b] > 0.0)) --b;
     const double base = b > 0 ? pre[b - 1] : 0.0;
     const long long i = (long long)b * kPpBlock + tid;
     const double v = i < n ? closest[i * n_init + r] : 0.0;
@@ -472,7 +476,10 @@ __global__ void __launch_bounds__(kPpBlock) ppsample_kernel(
     }
     __syncthreads();
     const double inc = base + pp_scan(v, sc);
-    if (inc >= target && i < n) atomicMin(&s_hit, tid);
+    // only points of positive weight can be drawn: the scan's tree order rounds the
+    // running sums of different positions differently, and across a stretch of zeros a
+    // later (zero-weight) position can reach a target the last positive one missed
+    if (inc >= target && i < n && v > 0.0) atomicMin(&s_hit, tid);
     if (v > 0.0 && i < n) atomicMax(&s_last, tid);
     __syncthreads();
     if (tid == 0) {

@@ -420,7 +420,8 @@ def test_kmeanspp_fused_step_matches_reference(d):
 @pytest.mark.parametrize("n", [1000, 300000 + 37])
 def test_kmeanspp_sample_matches_cumsum_searchsorted(n):
     """Device k-means++ draw (kmeans.hip ppsum/ppsample) == torch cumsum + searchsorted
-    (side left, clamped), including u = 0 and u = 1 and zero-potential stretches."""
+    (side left, clamped), including u = 0 and u = 1 and zero-potential stretches; a
+    zero-potential point is never drawn."""
     rs = np.random.default_rng(n)
     n_init, trials = 10, 6
     closest = torch.from_numpy(rs.random((n, n_init)) ** 3)
