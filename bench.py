@@ -108,6 +108,10 @@ def main() -> int:
                          "with every collective replaced by a device copy of its bytes "
                          "(parallel.comm.EmulatedComm) -- the per-rank step time of the "
                          "N-GPU DP job, collectives excluded; value = projected job rate")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="(testing) every rank on GPU 0: gloo process group, device "
+                         "collectives on the one-shot xGMI kernels, no cooperative solves -- "
+                         "RCCL takes one rank per GPU")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -125,19 +129,25 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # device_count() does not initialise the GPU on this image; is_available() does
-    if not args.cpu and world > 1 and 0 < torch.cuda.device_count() < world:
+    if args.share_gpu:
+        os.environ["CNMF_SOLVE_COOP"] = "0"
+        os.environ["CNMF_ALLREDUCE"] = "xgmi"
+        args.allreduce = "xgmi"
+    if not args.cpu and not args.share_gpu and world > 1 and 0 < torch.cuda.device_count() < world:
         print(f"bench.py: {world} ranks but only {torch.cuda.device_count()} GPUs visible",
               file=sys.stderr, flush=True)
         return 2
     use_cuda = torch.cuda.is_available() and not args.cpu
     if use_cuda:
+        if args.share_gpu:
+            local_rank = 0
         torch.cuda.set_device(local_rank)
         dev = torch.device("cuda", local_rank)
     else:
         dev = torch.device("cpu")
     if world > 1:
-        dist.init_process_group(backend="nccl" if use_cuda else "gloo",
-                                device_id=dev if use_cuda else None)
+        dist.init_process_group(backend="nccl" if (use_cuda and not args.share_gpu) else "gloo",
+                                device_id=dev if (use_cuda and not args.share_gpu) else None)
 
     from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
     from cnmf_torch_amd.parallel.comm import DistComm
@@ -150,6 +160,7 @@ def main() -> int:
     if args.density is not None:
         X[X < np.quantile(X, 1.0 - args.density)] = 0.0
     comm = row_map = schedule = None
+    coll_calls = None
     emu = args.emulate_world if (args.mode == "dp" and world == 1 and args.emulate_world
                                  and args.emulate_world > 1) else None
     if args.mode == "dp" and (world > 1 or emu):
@@ -225,7 +236,8 @@ def main() -> int:
     def max_over_ranks(sec: float) -> float:
         if world <= 1:
             return sec
-        t = torch.tensor([sec], dtype=torch.float64, device=dev)
+        t = torch.tensor([sec], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -282,7 +294,11 @@ def main() -> int:
                        "host_stage_s": res.stats.get("stream_host_stage_s")}
     else:
         for i in range(args.warmup):
+            if i == args.warmup - 1 and comm is not None and hasattr(comm, "record"):
+                comm.record = []      # the collectives of one whole step (dp mode)
             step(i)
+            if comm is not None and getattr(comm, "record", None) is not None:
+                coll_calls, comm.record = comm.record, None
         barrier()
         t0 = time.perf_counter()
         for i in range(args.warmup, nsteps):
@@ -296,6 +312,11 @@ def main() -> int:
 
     # the multi-batch rate of the same replicates (continuous batching), beside the per-batch
     # value: timed separately, after the headline region
+    # dp mode: the recorded collective sequence of one step, replayed alone and timed
+    # between barriers -- the measured collective term, beside the emulated projection
+    coll_s = None
+    if coll_calls:
+        coll_s = comm.replay(coll_calls, reps=5)
     stream_value = stream_reps = None
     if (not stream and stream_ok and len(grid) == 1 and args.schedule == "batch"
             and not args.no_stream_value and use_cuda):
@@ -389,6 +410,13 @@ def main() -> int:
                 "strong_global_batch": per_batch if strong_value is not None else None,
             },
         }
+        if coll_calls:
+            out["config"]["collective_s_per_step"] = round(coll_s, 6)
+            out["config"]["collective_calls_per_step"] = len(coll_calls)
+            out["config"]["collective_bytes_per_step_per_rank"] = int(sum(
+                ni * torch.tensor([], dtype=dt).element_size() for _, ni, _, dt in coll_calls))
+            out["config"]["collective_timing"] = ("one warmup step's collectives replayed "
+                                                  "alone, each waited for, between barriers")
         if emu:
             out["config"]["emulated_world"] = emu
             out["config"]["collective_bytes_per_step_per_rank"] = int(comm.bytes / nsteps)

@@ -54,7 +54,7 @@ def _require_native():
 # Per-op debug / tuning knobs, read ONCE (at import, or by refresh_env()): every op
 # consults them, and os.environ lookups were ~0.5 ms of host time per bench step.
 _ENV_KEYS = ("CNMF_FORCE_TORCH_OPS", "CNMF_SOLVE_COOP", "CNMF_GEMM_VARIANT", "CNMF_GEMM_KSPLIT",
-             "CNMF_GEMM_STAGES", "CNMF_GEMM_BK", "CNMF_SOLVE_PIPE")
+             "CNMF_GEMM_STAGES", "CNMF_GEMM_BK", "CNMF_SOLVE_PIPE", "CNMF_KL_FP16")
 _ENV: dict = {}
 
 
@@ -736,7 +736,7 @@ def stream_swap(grp: dict, ring: dict, store: dict, state: tuple, gate: torch.Te
 
 
 def rows_swap(pairs: torch.Tensor, K: int, mats, sf: torch.Tensor | None = None,
-              si: torch.Tensor | None = None, chunks: int = 16) -> None:
+              si: torch.Tensor | None = None, chunks: int | None = None) -> None:
     """Exchange positions ``pairs[2i]`` <-> ``pairs[2i+1]`` in place (disjoint pairs;
     stream.hip rows_swap_kernel -- _Batch.compact's swap form): K rows per position of
     every matrix in ``mats`` (2-D float32 / int16 views with unit column stride, or 3-D
@@ -767,6 +767,8 @@ def rows_swap(pairs: torch.Tensor, K: int, mats, sf: torch.Tensor | None = None,
         return
     if len(mats) > 4:
         raise ValueError("rows_swap: at most 4 matrices")
+    if chunks is None:      # ~2048 workgroups: a few pairs still spread over every CU
+        chunks = max(8, min(256, 2048 // npairs))
     desc = []
     for t in mats:
         t3 = t if t.dim() == 3 else t.unsqueeze(0)
@@ -813,6 +815,25 @@ def stream_publish(ctr: torch.Tensor, seq: torch.Tensor, box: HostMailbox) -> No
 # ----------------------------------------------------------------------------- beta MU
 def beta_mode(beta: float) -> int:
     return 0 if beta == 1.0 else (1 if beta == 0.0 else 2)
+
+
+BP_KL_FP16, BP_KL = 0, 3
+
+
+def bp_mode(beta: float) -> int:
+    """Mode of the split-bf16 beta kernels (beta_planes.h BpMode): KL runs the
+    fp32-accurate numerator (kBpKLX = 3: Q = X / P in two bf16 planes, S in two -- <= 3 *
+    2^-16 relative per term, random sign, inside the fp32 accumulation error of the
+    reduction, as the reference's fp32 nmf-torch run) unless ``CNMF_KL_FP16=1`` selects the
+    faster fp16 numerator (kBpKL = 0: <= 2^-11 per term); IS 1, other beta 2."""
+    m = beta_mode(beta)
+    if m == 0 and _ENV["CNMF_KL_FP16"] != "1":
+        return BP_KL
+    return m
+
+
+def _bp_kl(mode: int) -> bool:
+    return mode in (BP_KL_FP16, BP_KL)
 
 
 def beta_contract(side: str, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor,
@@ -1052,11 +1073,12 @@ def beta_panels(F3: torch.Tensor, beta: float, out: torch.Tensor | None = None,
     R, K, L = F3.shape
     _native_dtype_k("beta_panels", F3.dtype, K, _hip.bp_max_k())
     _bp_check("F3", F3, F3.device)
-    mode = beta_mode(beta)
-    if row_scale is not None and (mode != 0 or row_scale.dtype != torch.float32
+    mode = bp_mode(beta)
+    if row_scale is not None and (mode != BP_KL_FP16 or row_scale.dtype != torch.float32
                                   or row_scale.numel() < L or not row_scale.is_contiguous()
                                   or row_scale.device != F3.device):
-        raise ValueError("row_scale: KL only, contiguous float32 (L,) on the device")
+        raise ValueError("row_scale: fp16 KL (CNMF_KL_FP16=1) only, contiguous float32 (L,) "
+                         "on the device")
     n = int(_hip.bp_panel_elems(K, L, mode))
     if out is None or out.shape != (R, n) or out.dtype != torch.int16 or not out.is_contiguous():
         out = torch.empty((R, n), dtype=torch.int16, device=F3.device)
@@ -1118,9 +1140,9 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
     for name, t in (("act", act), ("iters", iters)):
         if t is not None and (t.dtype != torch.int32 or t.numel() < R or not t.is_contiguous()):
             raise ValueError(f"{name}: contiguous int32 with >= R entries")
-    mode = beta_mode(beta)
+    mode = bp_mode(beta)
     rule_loss = tol is not None and conv_mode == 1
-    if mode == 0 and (nsteps > 0 or rule_loss):
+    if _bp_kl(mode) and (nsteps > 0 or rule_loss):
         if den_vec is None:
             den_vec = W3.sum(dim=2, dtype=torch.float32).contiguous()
         elif (den_vec.shape != (R, K) or den_vec.dtype != torch.float32
@@ -1129,7 +1151,7 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
     else:
         den_vec = None
     if xh is not None:
-        if (mode != 0 or xh.dtype != torch.float16 or xh.shape != (N, G) or xh.stride(1) != 1
+        if (mode != BP_KL_FP16 or xh.dtype != torch.float16 or xh.shape != (N, G) or xh.stride(1) != 1
                 or unit is None or unit.numel() < G or unit.dtype != torch.float32):
             raise ValueError("xh: KL, float16 (N, G) counts with a float32 (G,) unit")
         if panels is None or not getattr(panels, "_cnmf_row_scaled", False):
@@ -1156,7 +1178,7 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
                 iters.data_ptr() if (iters is not None and tol is not None) else 0,
                 act.data_ptr() if act is not None else 0, 0,
                 float(xsum if xsum is not None else (
-                    float(X.sum(dtype=torch.float64)) if (mode == 0 and rule_loss) else 0.0)),
+                    float(X.sum(dtype=torch.float64)) if (_bp_kl(mode) and rule_loss) else 0.0)),
                 int(xh is not None), unit.data_ptr() if xh is not None else 0, 0,
                 _stream_ptr(HT3))
 
@@ -1179,12 +1201,12 @@ def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float,
     if active is not None and (active.dtype != torch.int32 or active.numel() < R
                                or not active.is_contiguous()):
         raise ValueError("active: contiguous int32 with >= R entries")
-    mode = beta_mode(beta)
+    mode = bp_mode(beta)
     if panels is None:
         panels = beta_panels(W3, beta)
     _bp_panels_check(panels, R, K, G, mode)
     # KL: the kernel sums x log(x/p) + p; the -sum(x) term is added here on the device
-    wsum = W3.sum(dim=2, dtype=torch.float32).contiguous() if mode == 0 else None
+    wsum = W3.sum(dim=2, dtype=torch.float32).contiguous() if _bp_kl(mode) else None
     n_strips = -(-N // int(_hip.bp_strip_cols(K, mode)))
     loss = torch.zeros((R, n_strips), dtype=torch.float64, device=dev)
     _hip.bp_run(0, mode, X.data_ptr(), X.stride(0), panels.data_ptr(),
@@ -1194,7 +1216,7 @@ def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float,
                 0, active.data_ptr() if active is not None else 0, loss.data_ptr(), 0.0,
                 0, 0, 0, _stream_ptr(HT3))
     tot = loss.sum(1)
-    if mode == 0:
+    if _bp_kl(mode):
         tot = tot - X.sum(dtype=torch.float64)
     return tot
 
@@ -1231,7 +1253,7 @@ def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
     if active is not None and (active.dtype != torch.int32 or active.numel() < R
                                or not active.is_contiguous()):
         raise ValueError("active: contiguous int32 with >= R entries")
-    mode = beta_mode(beta)
+    mode = bp_mode(beta)
     if panels is None:
         panels = beta_panels(HT3, beta)
     _bp_panels_check(panels, R, K, c, mode)
@@ -1240,7 +1262,7 @@ def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
         splits = max(1, min(16, -(-2048 // max(1, units))))
     n_split = int(_hip.bp_splits(c, int(splits)))
     num = torch.empty((n_split, R, K, G), dtype=torch.float32, device=dev)
-    den = torch.empty_like(num) if mode != 0 else None
+    den = torch.empty_like(num) if not _bp_kl(mode) else None
     xs = xth if xth is not None else XT
     _hip.bp_run(1, mode, xs.data_ptr(), xs.stride(0), panels.data_ptr(), panels.stride(0),
                 W3.data_ptr(), W3.stride(0), W3.stride(1), K, G, c, R, n_split, float(beta),

@@ -114,6 +114,9 @@ class DistComm(LocalComm):
         self.backend = dist.get_backend(group)
         self._xgmi = None           # one-shot xGMI all-reduce (CNMF_ALLREDUCE=xgmi), lazy
         self._side = None           # the stream every one-shot xGMI collective runs on
+        # when a list: every device collective appends (kind, in numel, out numel, dtype)
+        # -- bench.py --mode dp replays one step's sequence to time the collective term
+        self.record = None
 
     @property
     def is_distributed(self) -> bool:
@@ -174,9 +177,44 @@ class DistComm(LocalComm):
             self._xgmi.close()
         self._xgmi = None
 
+    def _rec(self, kind: str, inp: torch.Tensor, out: torch.Tensor) -> None:
+        if self.record is not None and inp.is_cuda:
+            self.record.append((kind, inp.numel(), out.numel(), inp.dtype))
+
+    def replay(self, calls, reps: int = 10) -> float:
+        """Seconds per replay of a recorded collective sequence (``record``), each call
+        issued as in the solve and waited for on the current stream: the collective term
+        of one step on this fabric, timed between barriers."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        bufs = [(k, torch.zeros(ni, dtype=dt, device=dev), torch.zeros(no, dtype=dt, device=dev))
+                for k, ni, no, dt in calls]
+
+        def once():
+            for k, a, b in bufs:
+                if k == "all_reduce":
+                    self.allreduce_(a)
+                elif k == "reduce_scatter":
+                    self.reduce_scatter_(b, a)
+                else:
+                    self.all_gather_into_(b, a)
+
+        once()
+        self.barrier()
+        torch.cuda.synchronize()
+        import time as _t
+
+        t0 = _t.perf_counter()
+        for _ in range(reps):
+            once()
+        torch.cuda.synchronize()
+        el = _t.perf_counter() - t0
+        self.barrier()
+        return el / max(1, reps)
+
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
         if self.world_size == 1:
             return t
+        self._rec("all_reduce", t, t)
         xg = self._xgmi_for(t)
         if xg is not None:
             self._on_side(lambda: xg(t))[1].wait()
@@ -254,6 +292,7 @@ class DistComm(LocalComm):
         m = out.numel()
         if inp.numel() != m * self.world_size:
             raise ValueError(f"reduce_scatter_: {inp.numel()} != {self.world_size} x {m}")
+        self._rec("reduce_scatter", inp, out)
         xg = self._xgmi_for(inp)
         if xg is not None:
             ok, h = self._on_side(lambda: xg.reduce_scatter(out, inp, overlap=True))
@@ -279,6 +318,7 @@ class DistComm(LocalComm):
         m = inp.numel()
         if out.numel() != m * self.world_size:
             raise ValueError(f"all_gather_into_: {out.numel()} != {self.world_size} x {m}")
+        self._rec("all_gather", inp, out)
         xg = self._xgmi_for(inp, any_dtype=True)
         if xg is not None:
             ok, h = self._on_side(lambda: xg.all_gather(out, inp, overlap=True))

@@ -79,10 +79,17 @@ constexpr int kBpThreads = 64 * kBpWaves;
 // SQ_LDS_BANK_CONFLICT 1.3x the LDS-active cycles)
 constexpr int kBpNS = kBpCH + 16;
 
-enum BpMode { kBpKL = 0, kBpIS = 1, kBpGeneral = 2 };
+// kBpKLX: KL with the fp32-accurate numerator (the default KL mode): P from KL's three
+// plane products, Q = X / P split into two bf16 planes and S into two (num = S0 Q0 +
+// S0 Q1 + S1 Q0, <= 3 * 2^-16 relative per term with random sign -- inside the fp32
+// accumulation error of the reduction, as for IS / general beta), den = S 1 a host vector
+// as for KL.  kBpKL is the opt-in fp16 numerator (CNMF_KL_FP16=1, see the file comment).
+enum BpMode { kBpKL = 0, kBpIS = 1, kBpGeneral = 2, kBpKLX = 3 };
+
+__host__ __device__ constexpr bool bp_is_kl(int mode) { return mode == kBpKL || mode == kBpKLX; }
 
 // plane-product terms of P: KL 3, IS / general beta 6 (exact to fp32 rounding)
-__host__ __device__ constexpr int bp_nt(int mode) { return mode == kBpKL ? 3 : 6; }
+__host__ __device__ constexpr int bp_nt(int mode) { return bp_is_kl(mode) ? 3 : 6; }
 __host__ __device__ constexpr int bp_np(int K, int mode = kBpIS) {
   return (bp_nt(mode) * K + 31) / 32;
 }
@@ -171,7 +178,7 @@ struct BpParams {
 
 template <int MODE>
 __device__ __forceinline__ void bp_terms(float x, float p, float beta, float& q, float& d) {
-  if (MODE == kBpKL) {
+  if (bp_is_kl(MODE)) {
     q = x * __builtin_amdgcn_rcpf(p);
     d = 1.f;
   } else if (MODE == kBpIS) {
@@ -189,7 +196,7 @@ __device__ __forceinline__ void bp_terms(float x, float p, float beta, float& q,
 template <int MODE>
 __device__ __forceinline__ float bp_loss(float x, float p, float q, float d, float beta,
                                          float eps) {
-  if (MODE == kBpKL) {
+  if (bp_is_kl(MODE)) {
     // x log2(x / p) only (q = x / p): the linear part sum(p) - sum(x) of the KL objective
     // is added per workgroup from the usage and spectra sums (bp_kernel)
     return x > 0.f ? x * __builtin_amdgcn_logf(q) : 0.f;
@@ -242,6 +249,7 @@ bp_kernel(BpParams p) {
   constexpr int COLS = kBpWaves * CT * 16;
   constexpr int KS = bp_ks(T);
   constexpr bool kH = MODE == kBpKL;   // fp16 numerator path (see the file comment)
+  constexpr bool kKL = bp_is_kl(MODE); // den = S 1 (host vector), KL objective
   constexpr int NT = bp_nt(MODE);
   static_assert(PIECES == PER_T * kBpThreads, "chunk must be whole pieces per thread");
   extern __shared__ __attribute__((aligned(16))) unsigned char bp_smem[];
@@ -322,7 +330,7 @@ bp_kernel(BpParams p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           sx[(16 * ct + m) * KS + 16 * t + 4 * q + i] =
-              kH ? hc[ct][t][i] * (csc[ct] * fsc[ct]) : hc[ct][t][i];
+              (kH || XH) ? hc[ct][t][i] * (csc[ct] * fsc[ct]) : hc[ct][t][i];
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
@@ -528,7 +536,7 @@ bp_kernel(BpParams p) {
             }
             if (kNum) {
               bp_split2(qv, qb0[ct], qb1[ct]);
-              if (MODE != kBpKL) bp_split2(dv, db0[ct], db1[ct]);
+              if (!kKL) bp_split2(dv, db0[ct], db1[ct]);
             }
           }
           if (kNum) {
@@ -539,7 +547,7 @@ bp_kernel(BpParams p) {
                 num[ct][t] = bp_mfma(an0[t], qb0[ct], num[ct][t]);
                 num[ct][t] = bp_mfma(an0[t], qb1[ct], num[ct][t]);
                 num[ct][t] = bp_mfma(an1[t], qb0[ct], num[ct][t]);
-                if (MODE != kBpKL) {
+                if (!kKL) {
                   den[ct][t] = bp_mfma(an0[t], db0[ct], den[ct][t]);
                   den[ct][t] = bp_mfma(an0[t], db1[ct], den[ct][t]);
                   den[ct][t] = bp_mfma(an1[t], db0[ct], den[ct][t]);
@@ -631,7 +639,7 @@ bp_kernel(BpParams p) {
 
     if (want_loss) {
       double l = (double)lsum;
-      if (MODE == kBpKL) {
+      if (kKL) {
         // sum x log(x/p) = ln 2 * sum x log2(x/p);  sum p = sum_k (sum_cols h_k) (sum_g w_k)
         // (+ eps per element, negligible); - sum x is subtracted once per replicate
         l *= 0.69314718055994530942;
@@ -661,7 +669,7 @@ bp_kernel(BpParams p) {
             const int k = 16 * t + 4 * q + i;
             if (k < K && cok[ct]) {
               const float h = hc[ct][t][i];
-              float dn = (MODE == kBpKL) ? p.den_vec[(long long)rep * K + k] : den[ct][t][i];
+              float dn = kKL ? p.den_vec[(long long)rep * K + k] : den[ct][t][i];
               dn = dn + p.l1 + p.l2 * h;
               if (dn == 0.f) dn = p.eps;
               float delta = num[ct][t][i] / dn;
@@ -688,7 +696,7 @@ bp_kernel(BpParams p) {
             if (k < K && cok[ct]) {
               const long long o = base + (long long)k * p.Lf + col_w + 16 * ct + m;
               p.num[o] = num[ct][t][i];
-              if (MODE != kBpKL) p.den[o] = den[ct][t][i];
+              if (!kKL) p.den[o] = den[ct][t][i];
             }
           }
     }
@@ -748,7 +756,7 @@ bp_kernel(BpParams p) {
     for (int s2 = 0; s2 < p.n_strips; ++s2)
       for (int v = 0; v < 4; ++v)
         tot[v] += __hip_atomic_load(pr + 4 * s2 + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (MODE == kBpKL) {
+    if (kKL) {
       tot[2] -= p.xsum;
       tot[3] -= p.xsum;
     }
@@ -801,6 +809,7 @@ hipError_t bp_launch(const BpParams& p, hipStream_t s) {
 // wide ranks (K in 33..64, padded to a multiple of 8): instantiated in their own units
 // (beta_planes_wide*.hip) so the K <= 32 kernels keep compiling in parallel
 hipError_t bp_launch_wide_kl(bool upd, bool xh, int np, int t, const BpParams& p, hipStream_t s);
+hipError_t bp_launch_wide_klx(bool upd, bool xh, int np, int t, const BpParams& p, hipStream_t s);
 hipError_t bp_launch_wide_gen(int mode, bool upd, int np, int t, const BpParams& p,
                               hipStream_t s);
 

@@ -80,9 +80,12 @@ __global__ void __launch_bounds__(256) bp_rowscale_kernel(const float* __restric
 
 template <int MODE, bool UPD>
 hipError_t bp_launch_k(const BpParams& p, hipStream_t s) {
-  if constexpr (MODE == kBpKL) {
-    const int np = bp_np(p.K, kBpKL), t = bp_t(p.K);
-    if (t >= 3) return bp_launch_wide_kl(UPD, p.uvec != nullptr || p.fscale != nullptr, np, t, p, s);
+  if constexpr (bp_is_kl(MODE)) {
+    const int np = bp_np(p.K, MODE), t = bp_t(p.K);
+    if (t >= 3)
+      return MODE == kBpKL
+                 ? bp_launch_wide_kl(UPD, p.uvec != nullptr || p.fscale != nullptr, np, t, p, s)
+                 : bp_launch_wide_klx(UPD, p.uvec != nullptr || p.fscale != nullptr, np, t, p, s);
     if (p.uvec != nullptr || p.fscale != nullptr) {   // fp16 counts
       if (np == 1 && t == 1) return bp_launch<1, 1, MODE, UPD, true>(p, s);
       if (np == 2 && t == 1) return bp_launch<2, 1, MODE, UPD, true>(p, s);
@@ -115,6 +118,7 @@ hipError_t bp_launch_mode(int mode, const BpParams& p, hipStream_t s) {
     case kBpKL: return bp_launch_k<kBpKL, UPD>(p, s);
     case kBpIS: return bp_launch_k<kBpIS, UPD>(p, s);
     case kBpGeneral: return bp_launch_k<kBpGeneral, UPD>(p, s);
+    case kBpKLX: return bp_launch_k<kBpKLX, UPD>(p, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -126,7 +130,7 @@ extern "C" int cnmf_bp_max_k() { return cnmf::kBpMaxK; }
 // 16-bit elements of one replicate's panel over a streamed axis of length L (layout by
 // beta mode: KL panels hold 3-term P slots, fp16 numerator planes and the row-scale tail)
 extern "C" long long cnmf_bp_panel_elems(int K, int L, int mode) {
-  if (K < 1 || K > cnmf::kBpMaxK || mode < 0 || mode > 2) return -1;
+  if (K < 1 || K > cnmf::kBpMaxK || mode < 0 || mode > 3) return -1;
   const int NP = cnmf::bp_np(K, mode), T = cnmf::bp_t(K);
   return (long long)((L + cnmf::kBpCH - 1) / cnmf::kBpCH) * cnmf::bp_chunk(NP, T) +
          (mode == cnmf::kBpKL ? cnmf::kBpTail : 0);
@@ -142,8 +146,9 @@ extern "C" hipError_t cnmf_bp_panels(const float* F, long long f_rs, long long l
                                      int R, int mode, const float* prow, unsigned short* out,
                                      long long out_rs, hipStream_t stream) {
   if (R <= 0 || L <= 0) return hipSuccess;
-  if (K < 1 || K > cnmf::kBpMaxK || mode < 0 || mode > 2) return hipErrorInvalidValue;
+  if (K < 1 || K > cnmf::kBpMaxK || mode < 0 || mode > 3) return hipErrorInvalidValue;
   if (out_rs < cnmf_bp_panel_elems(K, L, mode)) return hipErrorInvalidValue;
+  // (KLX panels: KL's 3-term P slots with the two bf16 numerator planes of IS / general)
   const int NP = cnmf::bp_np(K, mode), T = cnmf::bp_t(K);
   const int nchunks = (L + cnmf::kBpCH - 1) / cnmf::kBpCH;
   const bool kl = mode == cnmf::kBpKL;
@@ -170,9 +175,11 @@ extern "C" hipError_t cnmf_bp_run(
   if (R <= 0 || Lf <= 0) return hipSuccess;
   if (K < 1 || K > cnmf::kBpMaxK || Ls <= 0 || (side != 0 && side != 1)) return hipErrorInvalidValue;
   // fp16 counts: KL only; the H side needs the loss weights, the W side the column scales
-  if (xh && (mode != cnmf::kBpKL || (side == 0 ? uvec == nullptr : fscale == nullptr)))
+  // (the fp32-accurate KL mode reads them on the W side only: its loss has no weights)
+  if (xh && (!cnmf::bp_is_kl(mode) || (mode == cnmf::kBpKLX && side == 0) ||
+             (side == 0 ? uvec == nullptr : fscale == nullptr)))
     return hipErrorInvalidValue;
-  if (mode < 0 || mode > 2 || panel_rs < cnmf_bp_panel_elems(K, Ls, mode))
+  if (mode < 0 || mode > 3 || panel_rs < cnmf_bp_panel_elems(K, Ls, mode))
     return hipErrorInvalidValue;
   cnmf::BpParams p;
   p.X = X; p.ldx = ldx;
@@ -199,10 +206,10 @@ extern "C" hipError_t cnmf_bp_run(
   p.counter = counter; p.act = act; p.iters = iters; p.active = active; p.loss = loss;
   p.xsum = xsum;
   if (side == 1) {
-    if (num == nullptr || (mode != cnmf::kBpKL && den == nullptr)) return hipErrorInvalidValue;
+    if (num == nullptr || (!cnmf::bp_is_kl(mode) && den == nullptr)) return hipErrorInvalidValue;
     return cnmf::bp_launch_mode<false>(mode, p, stream);
   }
-  if (nsteps < 0 || (mode == cnmf::kBpKL && den_vec == nullptr) ||
+  if (nsteps < 0 || (cnmf::bp_is_kl(mode) && den_vec == nullptr) ||
       (part != nullptr && (counter == nullptr || act == nullptr)) ||
       (part != nullptr && conv_mode == 1 && hstate == nullptr) ||
       (nsteps == 0 && loss == nullptr && part == nullptr))

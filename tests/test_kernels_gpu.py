@@ -280,15 +280,34 @@ def test_beta_update_h_fused_matches_reference(beta):
     torch.testing.assert_close(h1.cpu().double(), h2, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("beta", [1.0, 0.0, 1.5])
+@pytest.fixture
+def kl_fp16(monkeypatch):
+    """The opt-in fp16-numerator KL kernels (CNMF_KL_FP16=1) for the duration of a test."""
+    monkeypatch.setenv("CNMF_KL_FP16", "1")
+    ops.refresh_env()
+    assert ops.bp_mode(1.0) == ops.BP_KL_FP16
+    yield
+    monkeypatch.delenv("CNMF_KL_FP16")
+    ops.refresh_env()
+
+
+@pytest.mark.parametrize("beta", [1.0, 0.0, 1.5, "kl16"])
 @pytest.mark.parametrize("K,N,G", [(3, 1037, 305), (10, 777, 320), (17, 300, 131),
                                    (32, 129, 64)])
-def test_split_bf16_beta_kernels_match_fp64(beta, K, N, G):
-    """beta_planes.hip (split-bf16 MFMA: exact 6-term P, 3-term num/den) vs the float64
-    reference: loss-only pass, W-side partials (float4 and scalar X paths: ragged G/N),
-    and one fused usage step.  KL runs the fp16-numerator variant (one fp16 plane of
-    X / P, <= 2^-11 relative per term, random sign; 3-term P): its numerators and steps are
-    held to 5e-4 relative instead of 5e-5 (129-term sums at K = 32)."""
+def test_split_bf16_beta_kernels_match_fp64(beta, K, N, G, request):
+    """beta_planes.hip (split-bf16 MFMA: 3-term num/den; P exact (6 terms) or KL's 3
+    terms) vs the float64 reference: loss-only pass, W-side partials (float4 and scalar X
+    paths: ragged G/N), and one fused usage step.  The default KL mode (kBpKLX: Q = X / P
+    in two bf16 planes) is held to the same 5e-5 as IS / general beta -- the fp32
+    accumulation bound of these sums.  "kl16" is the opt-in fp16 numerator
+    (CNMF_KL_FP16=1: one fp16 plane of X / P, <= 2^-11 relative per term, random sign):
+    5e-4 relative (129-term sums at K = 32)."""
+    fp16 = beta == "kl16"
+    if fp16:
+        request.getfixturevalue("kl_fp16")
+        beta = 1.0
+    else:
+        assert ops.bp_mode(beta) != ops.BP_KL_FP16
     g = torch.Generator().manual_seed(K + N)
     R = 3
     X = torch.rand((N, G), generator=g, dtype=torch.float64)
@@ -300,10 +319,11 @@ def test_split_bf16_beta_kernels_match_fp64(beta, K, N, G):
     Xg, Hg, Wg = X.float().to(dev), HT.float().to(dev), W.float().to(dev)
     active = torch.tensor([1, 0, 1], dtype=torch.int32, device=dev)
     # loss
-    kl = beta == 1.0
+    kl = fp16
     ref_loss = reference.beta_contract(0, X, HT, W, beta, eps, False, True)[2]
     got = ops.beta_loss(Xg, Hg, Wg, beta, eps)
-    torch.testing.assert_close(got.cpu(), ref_loss, rtol=1e-4 if kl else 2e-5, atol=1e-6)
+    torch.testing.assert_close(got.cpu(), ref_loss, rtol=1e-4 if beta == 1.0 else 2e-5,
+                               atol=1e-6)
     # W-side partials, two split counts
     rn, rd, _ = reference.beta_contract(1, X, HT, W, beta, eps, True, False)
     XT = Xg.t().contiguous()
@@ -326,14 +346,15 @@ def test_split_bf16_beta_kernels_match_fp64(beta, K, N, G):
 
 @pytest.mark.parametrize("beta,K,N,G", [(1.0, 40, 300, 131), (1.0, 48, 257, 200),
                                         (1.0, 56, 200, 100), (1.0, 64, 129, 64),
+                                        ("kl16", 48, 257, 200), ("kl16", 64, 129, 64),
                                         (0.0, 40, 300, 131), (1.5, 48, 257, 200),
                                         (0.0, 56, 200, 100)])
-def test_split_bf16_beta_kernels_wide_k_match_fp64(beta, K, N, G):
-    """The K > 32 instantiations of beta_planes (beta_planes_wide*.hip: KL to 64, IS /
-    general beta to 56; one column tile per wave, one wave per SIMD) against the float64
-    reference: loss, W-side partials and one fused usage step, with the K <= 32 test's
-    tolerances (KL: the fp16 numerator plane, longer sums at wide K)."""
-    test_split_bf16_beta_kernels_match_fp64(beta, K, N, G)
+def test_split_bf16_beta_kernels_wide_k_match_fp64(beta, K, N, G, request):
+    """The K > 32 instantiations of beta_planes (beta_planes_wide*.hip: KL (both numerator
+    modes) to 64, IS / general beta to 56; one column tile per wave, one wave per SIMD)
+    against the float64 reference: loss, W-side partials and one fused usage step, with
+    the K <= 32 test's tolerances."""
+    test_split_bf16_beta_kernels_match_fp64(beta, K, N, G, request)
 
 
 @pytest.mark.parametrize("beta_loss", ["kullback-leibler", "itakura-saito"])
@@ -910,7 +931,7 @@ def test_online_beta_gpu_converges_like_cpu(beta_loss):
     assert np.abs(on_g.n_iter - on_c.n_iter).max() <= 3, (on_g.n_iter, on_c.n_iter)
 
 
-def test_kl_fp16_numerator_overflow_is_redone_with_a_shift():
+def test_kl_fp16_numerator_overflow_is_redone_with_a_shift(kl_fp16):
     """x / p far beyond the fp16 range (65504) in a few (cell, gene) entries: the KL kernels
     redo such a step with the affected columns' Q shifted by 2^-12 (beta_planes.hip), so
     usages, spectra partials and the loss stay finite and match the float64 reference."""
@@ -940,9 +961,13 @@ def test_kl_fp16_numerator_overflow_is_redone_with_a_shift():
     torch.testing.assert_close(num.sum(0).cpu().double(), rn, rtol=1e-3, atol=1e-5)
 
 
-def test_kl_fp16_count_operands_match_fp64():
+def test_kl_fp16_count_operands_match_fp64(monkeypatch):
     """KL kernels reading X as fp16 counts (X = C u_g; P panel of W / u, loss weights u,
-    spectra side's W scaled by 1 / u) vs the float64 reference on the fp32 X."""
+    spectra side's W scaled by 1 / u) vs the float64 reference on the fp32 X: the
+    fp16-numerator kernels on both sides, and the default (fp32-accurate) KL spectra side,
+    the one the engine feeds counts, at its 5e-5."""
+    monkeypatch.setenv("CNMF_KL_FP16", "1")
+    ops.refresh_env()
     g = torch.Generator().manual_seed(5)
     R, K, N, G = 3, 10, 777, 300
     C = torch.poisson(torch.rand((N, G), generator=g, dtype=torch.float64) * 3)
@@ -974,11 +999,21 @@ def test_kl_fp16_count_operands_match_fp64():
     torch.testing.assert_close(num.sum(0).cpu().double(), rn, rtol=5e-4, atol=1e-5)
     with pytest.raises(ValueError):        # row-scaled panels without the counts
         ops.beta_h_block(Xg, Hg.clone(), Wg, 1.0, eps, 1, panels=pan)
+    monkeypatch.delenv("CNMF_KL_FP16")
+    ops.refresh_env()
+    num, _ = ops.beta_w_partials(Xg, None, Hg, Wg, 1.0, eps, splits=2,
+                                 xth=xh.t().contiguous(), unit_inv=(1.0 / ug).contiguous())
+    torch.testing.assert_close(num.sum(0).cpu().double(), rn, rtol=5e-5, atol=1e-5)
 
 
-def test_online_kl_matches_fp32_torch_path():
-    """Online KL through the fp16-numerator kernels vs the same solver on plain fp32
-    PyTorch ops (CNMF_FORCE_TORCH_OPS=1): final objectives within 1e-3, passes within 1."""
+@pytest.mark.parametrize("numer", ["default", "fp16"])
+def test_online_kl_matches_fp32_torch_path(numer, monkeypatch):
+    """Online KL through the split-bf16 kernels (default fp32-accurate numerator; opt-in
+    fp16 one) vs the same solver on plain fp32 PyTorch ops (CNMF_FORCE_TORCH_OPS=1):
+    final objectives within 1e-4 (fp16: 1e-3), passes within 1."""
+    if numer == "fp16":
+        monkeypatch.setenv("CNMF_KL_FP16", "1")
+    ops.refresh_env()
     from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
     from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
 
@@ -999,8 +1034,10 @@ def test_online_kl_matches_fp32_torch_path():
             os.environ["CNMF_FORCE_TORCH_OPS"] = old
         ops.refresh_env()
     assert a.converged.all() and b.converged.all()
-    np.testing.assert_allclose(a.err, b.err, rtol=1e-3)
+    np.testing.assert_allclose(a.err, b.err, rtol=1e-3 if numer == "fp16" else 1e-4)
     assert np.abs(a.n_iter - b.n_iter).max() <= 1, (a.n_iter, b.n_iter)
+    monkeypatch.delenv("CNMF_KL_FP16", raising=False)
+    ops.refresh_env()
 
 
 @pytest.mark.parametrize("K,G", [(3, 333), (10, 333), (17, 333), (32, 1200)])
