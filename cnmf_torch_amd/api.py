@@ -146,6 +146,17 @@ def check_gpu_ranks(components, beta_loss="frobenius", algo="mu", use_gpu=True) 
     return over
 
 
+_GPU_VISIBLE: list = []
+
+
+def _gpu_visible() -> bool:
+    """torch.cuda.is_available(), asked once per process (each call was ~4 ms of host
+    time in prepare -- a HIP device-count query)."""
+    if not _GPU_VISIBLE:
+        _GPU_VISIBLE.append(bool(torch.cuda.is_available()))
+    return _GPU_VISIBLE[0]
+
+
 def _device(use_gpu: bool, device=None) -> torch.device:
     """Explicit ``device`` > $CNMF_DEVICE > the local GPU when one is visible > CPU.
 
@@ -157,7 +168,7 @@ def _device(use_gpu: bool, device=None) -> torch.device:
         device = os.environ.get("CNMF_DEVICE") or None
     if device is not None:
         return torch.device(device)
-    if torch.cuda.is_available():
+    if _gpu_visible():
         return torch.device("cuda", torch.cuda.current_device())
     if use_gpu:
         warnings.warn("use_gpu=True but no GPU is visible; running on the CPU")
@@ -370,7 +381,10 @@ class cNMF:
             from .utils import prewarm as _prewarm
             from .utils.plotting import prestart
 
-            _prewarm.start(_device(False))
+            # one thread per group: the code-object loads overlap (0.24 vs 0.53 s on one
+            # thread, profiles/r5zj_*), inside prepare's own host work once the planes
+            # build is factorize's again (_prebuild_planes)
+            _prewarm.start(_device(False), parallel=True)
             self._prebuild = True
             # and the figure process (matplotlib's import) a stage earlier than factorize
             # would start it: with the later stages warm it is the pipeline's last wait
@@ -473,9 +487,12 @@ class cNMF:
             self.save_nmf_iter_params(replicate_params, run_params)
 
     def _prebuild_planes(self, dev) -> None:
-        """With prepare's prewarm on: build the resident matrix's split-GEMM planes on a
-        background thread (models.nmf_base.planes_ahead) for factorize in this process."""
-        if not getattr(self, "_prebuild", False):
+        """Opt-in (CNMF_PREBUILD_PLANES=1, with prepare's prewarm on): build the resident
+        matrix's split-GEMM planes on a background thread (models.nmf_base.planes_ahead)
+        for factorize in this process.  Off by default: factorize builds and times its
+        own planes (the build is factorize work, not prepare's)."""
+        if not getattr(self, "_prebuild", False) or \
+                os.environ.get("CNMF_PREBUILD_PLANES", "0") != "1":
             return
         path = self.paths["normalized_counts"]
         X = resident.recall(path, "X32")
@@ -918,13 +935,20 @@ class cNMF:
                          "sha256": d_, "bytes": int(n_)}
                         for p_, k_, i_, (d_, n_) in zip(paths_b, ks_, its_, done)]
 
+            # where the stage's time goes (bench_e2e reports it): the solves vs the wait for
+            # the replicate files -- a filesystem-bound tail (900 atomic small-file writes)
+            # that varies from host to host
+            self.factorize_stats = {"solve_s": 0.0, "write_wait_s": 0.0}
+
             def _flush():
                 recs = []
+                t_w = time.perf_counter()
                 for f in pending:
                     r_ = f.result()
                     if isinstance(r_, list):
                         recs.extend(r_)
                 pending.clear()
+                self.factorize_stats["write_wait_s"] += time.perf_counter() - t_w
                 append_jsonl_many(manifest, recs)
 
             nc = run_params["n_components"].to_numpy().astype(np.int64)
@@ -954,6 +978,7 @@ class cNMF:
                 res = solver.run_stream(seeds, ks=ks, keep_usages=save_usages)
                 W = res.W.cpu().numpy()
                 wall = time.perf_counter() - t0
+                self.factorize_stats["solve_s"] += wall
                 log.info("K=%s: %d replicates in %.3f s (%.1f replicates/s) on %s",
                          sorted(set(ks)), len(grp), wall, len(grp) / max(wall, 1e-9), dev)
                 recs = []

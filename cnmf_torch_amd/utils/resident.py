@@ -38,14 +38,22 @@ def _budget() -> int:
     env = os.environ.get("CNMF_RESIDENT_BYTES")
     if env is not None and env != "":
         return int(float(env))
-    try:
-        import torch
+    if not _GPU_TOTAL:
+        tot = 0
+        try:
+            import torch
 
-        if torch.cuda.is_available():
-            return int(torch.cuda.get_device_properties(0).total_memory // 4)
-    except Exception:
-        pass
-    return 0
+            if torch.cuda.is_available():
+                # hipMemGetInfo (get_device_properties' first call initialises amdsmi,
+                # ~0.1 s); asked once per process
+                tot = int(torch.cuda.mem_get_info(torch.cuda.current_device())[1])
+        except Exception:
+            pass
+        _GPU_TOTAL.append(tot)
+    return _GPU_TOTAL[0] // 4
+
+
+_GPU_TOTAL: list = []
 
 
 def _nbytes(value) -> int:
