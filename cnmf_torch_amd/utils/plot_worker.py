@@ -15,8 +15,11 @@ import matplotlib.pyplot  # noqa: E402,F401
 # parent computes, instead of inside the first job
 import matplotlib.backends.backend_agg  # noqa: E402,F401
 import numpy as np  # noqa: E402
+# the clustergram's leaf order (average linkage), loaded before the first job too
+import scipy.cluster.hierarchy  # noqa: E402,F401
+import scipy.spatial.distance  # noqa: E402,F401
 
-import plotting  # noqa: E402  (this directory: numpy / pandas / matplotlib only)
+import plotting  # noqa: E402  (this directory: numpy / matplotlib only -- no pandas)
 
 
 def main() -> int:

@@ -6,7 +6,8 @@ by :class:`PlotWorker`, a child Python process started when the first such stage
 it imports matplotlib (~0.8 s on a fresh box, where its .pyc files are compiled) while the
 stage computes on the GPU, then draws the same figure with the same code, and stays up for
 the following stages.  This module imports
-only numpy/pandas at the top, so the worker never loads torch or touches the GPU.
+only numpy at the top (pandas objects are only passed in by the API), so the worker
+never loads torch or pandas or touches the GPU.
 """
 from __future__ import annotations
 
@@ -24,7 +25,6 @@ import time
 import zlib
 
 import numpy as np
-import pandas as pd
 
 
 def _plt():
@@ -369,14 +369,19 @@ def flush_figures(timeout: float = 300.0) -> None:
 
 
 def draw_job(kind: str, path: str, a: dict) -> None:
-    """Draw one PlotWorker job from its arrays (in the worker, or as the fallback)."""
+    """Draw one PlotWorker job from its arrays (in the worker, or as the fallback).  The
+    drawing functions read only ``.k`` / ``.silhouette`` / ``.prediction_error`` and
+    ``.values`` of their pandas arguments, so the job passes plain namespaces: the figure
+    process never imports pandas (0.6 s of its start-up, profiles/r6j_*)."""
+    from types import SimpleNamespace as _NS
+
     if kind == "k_selection":
-        stats = pd.DataFrame({"k": a["k"], "silhouette": a["silhouette"],
-                              "prediction_error": a["prediction_error"]})
+        stats = _NS(k=a["k"], silhouette=a["silhouette"],
+                    prediction_error=a["prediction_error"])
         k_selection(stats, path, close=True)
     elif kind == "clustergram":
-        labels = pd.Series(a["labels"], index=a["names"])
-        dens = (pd.DataFrame(a["local_density"], columns=["local_density"])
+        labels = _NS(values=np.asarray(a["labels"]))
+        dens = (_NS(values=np.asarray(a["local_density"]).reshape(-1, 1))
                 if a["local_density"].size else None)
         filt = a["density_filter"].astype(bool) if a["density_filter"].size else None
         clustergram(a["dist"], labels, dens, filt, float(a["density_threshold"]), path,
