@@ -642,6 +642,8 @@ _LAYOUT_REPLAY = True
 # fused step: split-K GEMMs of up to this many k slices hand their raw slabs to the
 # consuming solve; deeper splits (the few-replicate tail) are reduced by the GEMM's own
 # pass -- the solve would read every slab per element
+# (re-measured in round 6 with the swap compaction: caps 4 / 8 / 16 gave 13,930-14,010 /
+# 13,774-13,872 / 13,369-13,373 rep/s, profiles/r6k_*)
 _FUSED_MAX_SLABS = 4
 
 
