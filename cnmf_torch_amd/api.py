@@ -1413,7 +1413,7 @@ class cNMF:
         device-resident X (dense tensor or DeviceCSR, see _resident_X) is used in place."""
         U = torch.as_tensor(usages, dtype=torch.float64, device=dev)
         S = torch.as_tensor(spectra, dtype=torch.float64, device=dev)
-        quad = float(((U.t() @ U) * (S @ S.t())).sum())
+        quad = float((ops.small_gram(U) * ops.small_gram(S, rows_are_points=False)).sum())
         if isinstance(X, sops.DeviceCSR) and not X.xf:
             d = X.data.to(torch.float64)
             UtX = sops.tspmm(X, U).t().to(torch.float64)              # (K, G)
@@ -1447,7 +1447,7 @@ class cNMF:
             xb = torch.as_tensor(blk, dtype=torch.float64, device=dev)
             x_sq += float((xb * xb).sum())
             cross += float(((U[a:b].t() @ xb) * S).sum())
-        quad = float(((U.t() @ U) * (S @ S.t())).sum())
+        quad = float((ops.small_gram(U) * ops.small_gram(S, rows_are_points=False)).sum())
         return x_sq - 2.0 * cross + quad
 
     # ------------------------------------------------------------------ reference / k-sel

@@ -16,6 +16,7 @@ import numpy as np
 import scipy.sparse as sp
 import torch
 
+from .. import ops
 from ..ops import sparse as sops
 from .hvg import get_mean_var
 
@@ -29,7 +30,7 @@ def efficient_ols_all_cols(X, Y, batch_size: int = 1024, normalize_y: bool = Fal
     if isinstance(Y, sops.DeviceCSR):
         dev = Y.device
     Xt = torch.as_tensor(np.asarray(X), dtype=torch.float64).to(dev)
-    XtX = Xt.t() @ Xt
+    XtX = ops.small_gram(Xt)          # (segsum.hip; a library GEMM beyond 64 columns)
     if isinstance(Y, sops.DeviceCSR):     # resident CSR: one transposed-SpMM kernel pass
         XtY = sops.tspmm(Y, Xt).t()
     else:

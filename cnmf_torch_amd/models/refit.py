@@ -178,7 +178,7 @@ def fit_H_online(X, W, H_init=None, chunk_size: int = 5000, chunk_max_iter: int 
     K = Wt.shape[0]
     n = Xv.shape[0]
     numerT = numer_rows(Wt, Xv)
-    gram = Wt @ Wt.t()
+    gram = ops.small_gram(Wt, rows_are_points=False)      # W W^T (segsum.hip)
     HT = _init_HT(K, n, H_init, dev, dtype, random_state)
     chunked_solve(HT, numerT, gram, chunk_size, chunk_max_iter, h_tol, l1_num=l1_reg_H,
                   l2=l2_reg_H, eps=epsilon)
@@ -202,7 +202,7 @@ def fit_spectra_online(X, usage, chunk_size: int = 5000, chunk_max_iter: int = 2
     K = Ut.shape[1]
     G = Xv.shape[1]
     numerT = numer_cols(Ut, Xv)          # (K x G) = (X^T U)^T
-    gram = Ut.t() @ Ut
+    gram = ops.small_gram(Ut)                             # U^T U (segsum.hip)
     ST = _init_HT(K, G, None, dev, torch.float32, random_state, row_offset=col_offset)
     chunked_solve(ST, numerT, gram, chunk_size, chunk_max_iter, h_tol, l1_num=l1_reg, eps=epsilon)
     return ST.cpu().numpy()

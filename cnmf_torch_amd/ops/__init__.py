@@ -1556,6 +1556,29 @@ def seg_argmin(D: torch.Tensor, k: int, row_add: torch.Tensor | None = None,
     return lab.long(), mind
 
 
+def small_gram(A: torch.Tensor, rows_are_points: bool = True) -> torch.Tensor:
+    """K x K Gram of a tall operand on the device (segsum.hip small_gram_kernel; float32 /
+    float64 as A): A^T A for A (n x K) (``rows_are_points``), else A A^T for A (K x n) --
+    the consensus / refit / OLS Grams, without a library GEMM.  Row chunks summed in chunk
+    order (deterministic)."""
+    if A.dim() != 2:
+        raise ValueError("small_gram: a 2-D operand")
+    if rows_are_points:
+        n, K = A.shape
+        s_i, s_a = A.stride(0), A.stride(1)
+    else:
+        K, n = A.shape
+        s_i, s_a = A.stride(1), A.stride(0)
+    if not use_native(A) or K > 64 or A.dtype not in (torch.float32, torch.float64) or n == 0:
+        return A.t() @ A if rows_are_points else A @ A.t()
+    rows_per = max(64, -(-n // 256))
+    chunks = -(-n // rows_per)
+    part = torch.empty((chunks, K, K), dtype=A.dtype, device=A.device)
+    _hip.small_gram(A.data_ptr(), s_i, s_a, n, K, A.element_size(), rows_per, part.data_ptr(),
+                    _stream_ptr(A))
+    return part.sum(0)
+
+
 def seg_colsum(X: torch.Tensor, lab: torch.Tensor, k: int) -> torch.Tensor:
     """k-means centroid sums of every restart (segsum.hip, H4): for X (n, d) and labels
     ``lab`` (n_init, n) in [0, k), out[r, c] = sum of the rows i with lab[r, i] == c --

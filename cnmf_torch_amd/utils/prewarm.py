@@ -120,15 +120,18 @@ def _consensus_chain(dev: torch.device) -> None:
 
 
 def _library_gemms(dev: torch.device) -> None:
-    """The refit's numerator / Gram products (f32) and the prediction error's (f64)."""
+    """The refit's and the prediction error's K x K Grams (segsum.hip small_gram, f32 and
+    f64) and the dense-input numerator products (library GEMMs: a resident dense X)."""
+    from .. import ops
+
     g = torch.Generator().manual_seed(1)
     W = torch.rand((3, 16), generator=g).to(dev)
     X = torch.rand((40, 16), generator=g).to(dev)
-    _ = W @ W.t()
+    _ = ops.small_gram(W, rows_are_points=False)
     _ = X @ W.t()
     U = torch.rand((40, 3), generator=g, dtype=torch.float64).to(dev)
     S3 = torch.rand((3, 16), generator=g, dtype=torch.float64).to(dev)
-    q = ((U.t() @ U) * (S3 @ S3.t())).sum()
+    q = (ops.small_gram(U) * ops.small_gram(S3, rows_are_points=False)).sum()
     xb = X.to(torch.float64)
     q = q + ((U.t() @ xb) * S3).sum() + (xb * xb).sum()
     float(q)

@@ -294,6 +294,12 @@ PYBIND11_MODULE(_hip, m) {
                        reinterpret_cast<hipStream_t>(stream)),
           "knn_sum");
   });
+  m.def("small_gram", [](uintptr_t A, long long s_i, long long s_a, int n, int K, int esz,
+                         int rows_per, uintptr_t part, uintptr_t stream) {
+    check(cnmf_small_gram(reinterpret_cast<const void*>(A), s_i, s_a, n, K, esz, rows_per,
+                          reinterpret_cast<void*>(part), reinterpret_cast<hipStream_t>(stream)),
+          "small_gram");
+  });
   m.def("seg_colsum", [](uintptr_t X, long long ldx, int n, int d, uintptr_t lab, long long ldl,
                          int nrest, int k, uintptr_t out, uintptr_t stream) {
     check(cnmf_seg_colsum(P<const double>(X), ldx, n, d, P<const int>(lab), ldl, nrest, k,

@@ -112,6 +112,8 @@ hipError_t cnmf_pairdist(const double* A, long long lda, const double* B, long l
                          long long ldd, int same, int squared, hipStream_t stream);
 hipError_t cnmf_knn_sum(const double* D, long long ldd, int n, int m, int k, double* out,
                         hipStream_t stream);
+hipError_t cnmf_small_gram(const void* A, long long s_i, long long s_a, int n, int K, int esz,
+                           int rows_per, void* part, hipStream_t stream);
 hipError_t cnmf_seg_colsum(const double* X, long long ldx, int n, int d, const int* lab,
                            long long ldl, int nrest, int k, double* out, hipStream_t stream);
 hipError_t cnmf_seg_rowsum(const double* D, long long ldd, int n, int m, const int* lab, int k,

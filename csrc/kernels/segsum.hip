@@ -83,6 +83,51 @@ __global__ void __launch_bounds__(256) seg_rowsum_kernel(const double* __restric
   }
 }
 
+
+// Small Gram G = A^T A of a tall strided operand (H4-H6 helpers: the K x K Grams of the
+// usage / spectra refits, the prediction error's trace term and the OLS normal matrix):
+// element (i, a) of A (n x K) at A[i * s_i + a * s_a] -- so both U^T U (n x K rows) and
+// S S^T (K x n, s_i = 1) take it.  Grid: row chunks; a chunk's rows are staged in LDS
+// (64 at a time), thread t owns the pairs p = t, t + 256, .. of the K x K output and sums
+// them over the chunk's rows in order; the per-chunk partials are reduced by the host in
+// chunk order (a fixed order: deterministic).
+template <typename T>
+__global__ void __launch_bounds__(256) small_gram_kernel(const T* __restrict__ A, long long s_i,
+                                                         long long s_a, int n, int K, int rows_per,
+                                                         T* __restrict__ part) {
+  extern __shared__ unsigned char sg_raw[];
+  T* tile = reinterpret_cast<T*>(sg_raw);          // [64][K]
+  const int i0 = blockIdx.x * rows_per, i1 = min(n, i0 + rows_per);
+  const int npair = K * K;
+  T acc[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) acc[u] = T(0);
+  for (int r0 = i0; r0 < i1; r0 += 64) {
+    const int nr = min(64, i1 - r0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nr * K; e += 256) {
+      const int rr = e / K, a = e - rr * K;
+      tile[rr * K + a] = A[(long long)(r0 + rr) * s_i + (long long)a * s_a];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int pq = threadIdx.x + 256 * u;
+      if (pq < npair) {
+        const int a = pq / K, b = pq - a * K;
+        T v = acc[u];
+        for (int rr = 0; rr < nr; ++rr) v += tile[rr * K + a] * tile[rr * K + b];
+        acc[u] = v;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int pq = threadIdx.x + 256 * u;
+    if (pq < npair) part[(long long)blockIdx.x * npair + pq] = acc[u];
+  }
+}
+
 }  // namespace cnmf
 
 static int ss_waves(int k) {
@@ -124,5 +169,23 @@ extern "C" hipError_t cnmf_seg_rowsum(const double* D, long long ldd, int n, int
   }
   hipLaunchKernelGGL(cnmf::seg_rowsum_kernel, dim3((unsigned)((n + nw - 1) / nw)), dim3(64 * nw),
                      lds, stream, D, ldd, n, m, lab, k, out, ldo);
+  return hipGetLastError();
+}
+
+// chunks of rows_per rows; part: chunks x K x K partials (T = float / double by esz)
+extern "C" hipError_t cnmf_small_gram(const void* A, long long s_i, long long s_a, int n, int K,
+                                      int esz, int rows_per, void* part, hipStream_t stream) {
+  if (n < 1 || K < 1 || K > 64 || rows_per < 1 || !A || !part || (esz != 4 && esz != 8))
+    return hipErrorInvalidValue;
+  const unsigned chunks = (unsigned)((n + rows_per - 1) / rows_per);
+  const size_t lds = (size_t)64 * K * esz;
+  if (esz == 8)
+    hipLaunchKernelGGL(cnmf::small_gram_kernel<double>, dim3(chunks), dim3(256), lds, stream,
+                       static_cast<const double*>(A), s_i, s_a, n, K, rows_per,
+                       static_cast<double*>(part));
+  else
+    hipLaunchKernelGGL(cnmf::small_gram_kernel<float>, dim3(chunks), dim3(256), lds, stream,
+                       static_cast<const float*>(A), s_i, s_a, n, K, rows_per,
+                       static_cast<float*>(part));
   return hipGetLastError();
 }

@@ -2009,3 +2009,21 @@ def test_seg_rowsum_and_device_silhouette_match_sklearn(n, m, k):
     got = silhouette(Dx, labs)
     want = silhouette_score(Dx.cpu().numpy(), labs, metric="precomputed")
     assert abs(got - want) <= 1e-10
+
+
+@pytest.mark.parametrize("n,K,dt", [(10000, 13, torch.float64), (2000, 9, torch.float32),
+                                    (77, 64, torch.float64), (5, 3, torch.float32)])
+def test_small_gram_matches_float64(n, K, dt):
+    """segsum.hip small_gram_kernel (the consensus / refit / OLS K x K Grams) == the
+    float64 product, for A^T A of an (n x K) operand and A A^T of a (K x n) one, strided
+    views included; deterministic across calls."""
+    g = torch.Generator().manual_seed(n + K)
+    A = torch.rand((n, K + 3), generator=g, dtype=torch.float64)[:, 1:K + 1]   # strided
+    want = A.t() @ A
+    tol = 1e-12 if dt == torch.float64 else 2e-6
+    got = ops.small_gram(A.to(dt).cuda())
+    torch.testing.assert_close(got.double().cpu(), want, rtol=tol, atol=tol)
+    assert torch.equal(got, ops.small_gram(A.to(dt).cuda()))
+    B = A.t().contiguous()                                   # (K x n)
+    got2 = ops.small_gram(B.to(dt).cuda(), rows_are_points=False)
+    torch.testing.assert_close(got2.double().cpu(), want, rtol=tol, atol=tol)
