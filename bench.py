@@ -98,6 +98,9 @@ def main() -> int:
     ap.add_argument("--schedule", default="batch", choices=["stream", "batch"],
                     help="batch: one solve per step (the factorize job); stream: continuous "
                          "batching over the timed steps' replicates (see module docstring)")
+    ap.add_argument("--batch-live", type=int, default=None,
+                    help="batch schedule: solve each step's batch with this many live slots "
+                         "(continuous batching inside the one ledger batch)")
     ap.add_argument("--no-stream-value", action="store_true",
                     help="batch schedule: skip the extra continuous-batching timing")
     ap.add_argument("--live", type=int, default=None,
@@ -201,7 +204,12 @@ def main() -> int:
             ks = all_ks
         if args.mode != "dp":
             seeds, ks = seeds[rank::world], ks[rank::world]
-        if len(grid) == 1:
+        if args.batch_live is not None and args.mode != "dp":
+            # the step's ledger batch through continuous batching INSIDE the batch (fewer
+            # live slots than replicates; what factorize runs for that ledger)
+            res = solver.run_stream([int(s) for s in seeds], ks=[int(k) for k in ks],
+                                    live=args.batch_live, keep_usages=False)
+        elif len(grid) == 1:
             res = solver.run_concurrent([int(s) for s in seeds], n_streams=args.streams)
         else:
             res = solver.run([int(s) for s in seeds], ks=[int(k) for k in ks])

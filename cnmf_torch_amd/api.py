@@ -146,15 +146,11 @@ def check_gpu_ranks(components, beta_loss="frobenius", algo="mu", use_gpu=True) 
     return over
 
 
-_GPU_VISIBLE: list = []
-
-
 def _gpu_visible() -> bool:
-    """torch.cuda.is_available(), asked once per process (each call was ~4 ms of host
-    time in prepare -- a HIP device-count query)."""
-    if not _GPU_VISIBLE:
-        _GPU_VISIBLE.append(bool(torch.cuda.is_available()))
-    return _GPU_VISIBLE[0]
+    """torch.cuda.is_available(), asked once per process (utils.gpu)."""
+    from .utils.gpu import visible
+
+    return visible()
 
 
 def _device(use_gpu: bool, device=None) -> torch.device:

@@ -376,7 +376,9 @@ class _PassPipeline:
         # (the policy depends on the batch's shape only, never on whether it compacts by
         # swaps or gathers: the compacted layouts re-plan the GEMMs' k split, so two runs
         # of the same replicates agree bit for bit only through the same layouts)
-        if self.swap and self.cuda and len(self.st.groups) == 1 and \
+        # (a streaming run's drain compactions read its occupant tables back: they keep
+        # the late policy)
+        if self.swap and self.cuda and len(self.st.groups) == 1 and self.st.feed is None and \
                 os.environ.get("CNMF_COMPACT_SWAP", "1") != "0":
             return self.frac_swap
         return self.frac_small if n <= 256 else self.frac
@@ -434,7 +436,12 @@ class _Feed:
     late (stream.hip: the swap runs inside the pass)."""
 
     def __init__(self, seeds, ks, dev, N: int, G: int, keep_usages: bool,
-                 dtype=torch.float32):
+                 dtype=torch.float32, bufs: dict | None = None):
+        """``bufs`` (a dict the caller keeps per arena and feed shape): the device buffers
+        -- result store, rings, counters, occupant tables, mailbox -- persist there across
+        runs at fixed addresses, so a pass graph captured by one run replays in the next
+        (``buf_uid`` keys the graph slots); they are reset here, and the results handed
+        out are copies (the next run reuses the store)."""
         self.uid = next(_FEED_UIDS)
         self.seeds = np.asarray(seeds, dtype=np.int64)
         self.ks = np.asarray(ks, dtype=np.int64)
@@ -443,16 +450,31 @@ class _Feed:
         self.queue = {int(K): collections.deque(np.flatnonzero(self.ks == K).tolist())
                       for K in np.unique(self.ks)}
         tot = int(self.ks.sum())
-        self.store = {
-            "offs": torch.from_numpy(self.offs).to(dev),
-            "W": torch.empty((tot, G), device=dev, dtype=dtype),
-            "HT": torch.empty((tot, N), device=dev, dtype=dtype) if keep_usages else None,
-            # err_init, err_prev, err | active, converged, n_pass, h_iters, w_iters
-            "sf": torch.zeros((3, R), dtype=torch.float64, device=dev),
-            "si": torch.zeros((5, R), dtype=torch.int32, device=dev),
-        }
+        self.bufs = bufs
+        if bufs is not None and "store" in bufs:
+            self.store = bufs["store"]
+            self.store["sf"].zero_()
+            self.store["si"].zero_()
+        else:
+            self.store = {
+                "offs": torch.from_numpy(self.offs).to(dev),
+                "W": torch.empty((tot, G), device=dev, dtype=dtype),
+                "HT": torch.empty((tot, N), device=dev, dtype=dtype) if keep_usages else None,
+                # err_init, err_prev, err | active, converged, n_pass, h_iters, w_iters
+                "sf": torch.zeros((3, R), dtype=torch.float64, device=dev),
+                "si": torch.zeros((5, R), dtype=torch.int32, device=dev),
+            }
+            if bufs is not None:
+                bufs["store"] = self.store
+                bufs["uid"] = next(_FEED_UIDS)
+        self.buf_uid = bufs["uid"] if bufs is not None else self.uid
         self.R = R
-        self.rings: dict = {}     # K -> ring (see NMFBatchSolver._stream_ring)
+        # K -> ring (see NMFBatchSolver._stream_ring); persistent rings restart empty
+        self.rings: dict = bufs.setdefault("rings", {}) if bufs is not None else {}
+        for ring in self.rings.values():
+            ring["published"] = 0
+            ring["tail"].zero_()
+            ring["ids"].fill_(-1)
         self.ctr = None           # int32 device [1 + n_rings]: harvested, ring heads
         self.occ: dict = {}       # K -> int32 device occupant table of the group
         self.plan: dict = {}      # K -> int32 device [2 n] swap plan scratch

@@ -79,7 +79,7 @@ class _GraphMixin:
         a = st.arena
         # (a streaming run's pass graph holds its feed's ring / store addresses)
         key = (st.n_act, tuple(int(k) for k in st.kpos[:st.n_act]),
-               tuple(tuple(b) for b in steps), st.feed.uid if st.feed is not None else None)
+               tuple(tuple(b) for b in steps), st.feed.buf_uid if st.feed is not None else None)
         slots = a["slots"]
         sl = slots.get(key)
         if sl is None:

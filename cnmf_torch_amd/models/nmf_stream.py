@@ -90,7 +90,21 @@ class _StreamMixin:
         t0 = time.perf_counter()
         N, G = self.X.shape
         dev = self.X.device
-        feed = _Feed(seeds, ks, dev, N, G, keep_usages, self.X.dtype)
+        # the feed's device buffers persist per (arena, feed shape): a later run of the same
+        # shape (the next ledger batch) replays the passes captured by this one
+        kpos_all = np.sort(ks)
+        arena = self._arena(np.concatenate([np.repeat(K, slots[K]) for K in sorted(slots)]))
+        fkey = (R, tuple(ks.tolist()), bool(keep_usages), tuple(sorted(slots.items())))
+        feeds = arena.setdefault("feeds", collections.OrderedDict())
+        bufs = feeds.get(fkey)
+        if bufs is None:
+            bufs = feeds[fkey] = {}
+            while len(feeds) > 4:
+                feeds.popitem(last=False)
+        else:
+            feeds.move_to_end(fkey)
+        feed = _Feed(seeds, ks, dev, N, G, keep_usages, self.X.dtype, bufs=bufs)
+        del kpos_all
         first = []
         for K in sorted(slots):
             q = feed.queue[K]
@@ -102,8 +116,9 @@ class _StreamMixin:
             rows = int(kpos.sum())
             self._ws_reserve = rows * (4 * 4 * (cw + G) + 4 * G + 6 * (cw + G))
         # the stream's batch always lives in an arena (packed state rows the swap kernel
-        # reads and writes); graphs follow the usual rule
-        arena = self._arena(kpos)
+        # reads and writes; the same arena as the feed's above); graphs follow the usual
+        # rule
+        assert arena is self._arena(kpos)
         HT, W = arena["HT"], arena["W"]
         r0 = 0
         for K in sorted(slots):
@@ -117,12 +132,28 @@ class _StreamMixin:
         st.order = first.copy()
         if not self._fused_ok(st, self._steps(N)):
             return self.run(seeds, ks=ks, on_retire=on_result)
-        feed.ctr = torch.zeros(1 + len(st.groups), dtype=torch.int32, device=dev)
-        feed.seq = torch.zeros(1, dtype=torch.int32, device=dev)
-        feed.box = ops.HostMailbox(1 + len(st.groups))
+        if "ctr" in bufs:          # persistent counters / tables, reset for this run
+            feed.ctr, feed.seq, feed.box = bufs["ctr"], bufs["seq"], bufs["box"]
+            feed.ctr.zero_()
+            feed.seq.zero_()
+            feed.box.host.fill_(-1)
+        else:
+            feed.ctr = bufs["ctr"] = torch.zeros(1 + len(st.groups), dtype=torch.int32, device=dev)
+            feed.seq = bufs["seq"] = torch.zeros(1, dtype=torch.int32, device=dev)
+            feed.box = bufs["box"] = ops.HostMailbox(1 + len(st.groups))
+        for gi, g in enumerate(st.groups):      # rings of an earlier run: heads re-pointed
+            if g.K in feed.rings:
+                feed.rings[g.K]["head"] = feed.ctr[1 + gi:2 + gi]
+        occ_b, plan_b = bufs.setdefault("occ", {}), bufs.setdefault("plan", {})
         for i, g in enumerate(st.groups):
-            feed.occ[g.K] = torch.from_numpy(first[g.p0:g.p0 + g.n].astype(np.int32)).to(dev)
-            feed.plan[g.K] = torch.empty(2 * g.n, dtype=torch.int32, device=dev)
+            occ = torch.from_numpy(first[g.p0:g.p0 + g.n].astype(np.int32))
+            if g.K in occ_b:
+                occ_b[g.K].copy_(occ)
+            else:
+                occ_b[g.K] = occ.to(dev)
+                plan_b[g.K] = torch.empty(2 * g.n, dtype=torch.int32, device=dev)
+            feed.occ[g.K] = occ_b[g.K]
+            feed.plan[g.K] = plan_b[g.K]
             feed.known_head[g.K] = 0
         st.feed = feed
         self._online_frob(st)
@@ -147,8 +178,9 @@ class _StreamMixin:
                  "stream_host_stage_s": round(feed.t_stage, 4),
                  "stream_mailbox_misses": feed.box_misses}
         uni = np.unique(ks)
-        HTo = store["HT"] if store["HT"] is not None else torch.empty((0, N), device=dev)
-        return NMFResult(HT=HTo, W=store["W"], err=err, n_iter=rest[1].astype(np.int64),
+        # (the store is the next run's: hand out copies)
+        HTo = store["HT"].clone() if store["HT"] is not None else torch.empty((0, N), device=dev)
+        return NMFResult(HT=HTo, W=store["W"].clone(), err=err, n_iter=rest[1].astype(np.int64),
                          converged=rest[0] != 0, seeds=seeds,
                          K=int(uni[0]) if uni.size == 1 else None, stats=stats, ks=ks)
 
@@ -218,13 +250,15 @@ class _StreamMixin:
         feed = st.feed
         dev = st.W.device
         occ_new = occ_dev.index_select(0, _to_device(perm[:st.n_act], dev))
-        feed.ctr = torch.cat([feed.ctr[:1]] + [
-            feed.ctr.new_full((1,), feed.rings[g.K]["published"]) for g in st.groups])
-        for g in st.groups:
-            feed.occ[g.K] = occ_new[g.p0:g.p0 + g.n].clone()
-            feed.plan[g.K] = torch.empty(2 * g.n, dtype=torch.int32, device=dev)
+        # in place, in the persistent counter block and occupant tables: the new layout's
+        # pass graph (captured now or by an earlier run) holds their addresses
+        heads = torch.tensor([feed.rings[g.K]["published"] for g in st.groups],
+                             dtype=torch.int32)
+        feed.ctr[1:1 + len(st.groups)].copy_(heads)
+        for gi, g in enumerate(st.groups):
+            feed.occ[g.K][:g.n].copy_(occ_new[g.p0:g.p0 + g.n])
             ring = feed.rings[g.K]
-            ring["head"] = feed.ctr[1 + st.groups.index(g):2 + st.groups.index(g)]
+            ring["head"] = feed.ctr[1 + gi:2 + gi]
 
     def _stream_ring(self, st: _Batch, K: int, fb: dict) -> dict:
         """The staging ring of K group: 2 x its live positions of initialised replicates

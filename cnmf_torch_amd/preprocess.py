@@ -42,7 +42,9 @@ def _default_device():
     env = os.environ.get("CNMF_DEVICE")
     if env:
         return torch.device(env)
-    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+    from .utils.gpu import visible
+
+    return torch.device("cuda") if visible() else torch.device("cpu")
 
 
 def stdscale_quantile_celing(_adata, max_value=None, quantile_thresh=None):

@@ -21,7 +21,7 @@ _lock = threading.Lock()
 
 
 def _sync():
-    if torch.cuda.is_available() and torch.cuda.is_initialized():
+    if torch.cuda.is_initialized():     # (only initialised when a GPU is visible)
         torch.cuda.synchronize()
 
 
