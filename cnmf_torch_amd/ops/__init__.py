@@ -2012,7 +2012,7 @@ def split_planes(S: torch.Tensor, out: torch.Tensor, col_mul: torch.Tensor | Non
 def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int, N: int,
                 Kd: int, accumulate: bool = False, col_scale: torch.Tensor | None = None,
                 raw_slab: torch.Tensor | None = None, raw_max: int = 1 << 30,
-                gate: torch.Tensor | None = None) -> int:
+                gate: torch.Tensor | None = None, plan: tuple | None = None) -> int:
     """C[:M, :N] (+)= col_scale * sum_{i + j <= 2} A[i][:M, :Kd] . B[j][:N, :Kd]^T on the bf16
     matrix cores (gemm_planes.hip): the fp32-accurate product of the fp32 matrices whose
     exact bf16 splits are A (3 planes; or its first 2, see gemm_a_planes) and B (1-3
@@ -2064,7 +2064,7 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
         else:
             C[:M, :N] = prod.to(C.dtype)
         return
-    variant, ksplit = gemm_plan(M, N, Kd, pb)
+    variant, ksplit = plan if plan is not None else gemm_plan(M, N, Kd, pb)
     slab = 0
     if raw_slab is not None and ksplit > raw_max:
         # (capping ksplit at raw_max instead -- no reduction pass, fewer workgroups -- was
