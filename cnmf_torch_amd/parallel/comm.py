@@ -178,7 +178,7 @@ class DistComm(LocalComm):
         self._xgmi = None
 
     def _rec(self, kind: str, inp: torch.Tensor, out: torch.Tensor) -> None:
-        if self.record is not None and inp.is_cuda:
+        if getattr(self, "record", None) is not None and inp.is_cuda:
             self.record.append((kind, inp.numel(), out.numel(), inp.dtype))
 
     def replay(self, calls, reps: int = 10) -> float:
