@@ -530,13 +530,16 @@ def pipe_round_reps(n: int, K: int, dev: torch.device) -> int:
 
 
 # target columns per cooperative slice of the pipelined solve (more, shorter slices fill
-# the chip; fewer, longer ones wait less on each other at the exchanges).  256 / 384 /
-# 512: K=10 13,172 / 13,229 / 13,204 rep/s, K=20 5,232 / 5,293 / 5,141 (profiles/r4i_*).
+# the chip; fewer, longer ones wait less on each other at the exchanges).  Round 4: 256 /
+# 384 / 512: K=10 13,172 / 13,229 / 13,204 rep/s, K=20 5,232 / 5,293 / 5,141 (r4i_*).
 # With the single-round XCD order and the LDS-staged Grams, 17 <= K <= 32 prefers 320:
 # K=20 5,601 / 5,606 vs 5,253 / 5,455 at 384, K=30 3,767 / 3,772 vs 3,760 / 3,762
 # (profiles/r4zi_*)
 def _pipe_slice_cols(K: int) -> int:
-    return 320 if 16 < K <= 32 else 384
+    # (round 6, one batch per step: K = 10 at 640 columns 14,083 / 14,149 / 14,163 against
+    # 13,969 / 13,983 / 14,019 at 384 -- fewer slices wait less at the exchanges; 768
+    # 14,105, 1024 13,930; K grid 21,265 vs 21,175: profiles/r6u_*, r6v_*)
+    return 320 if 16 < K <= 32 else 640
 
 
 def _pipe_plan(n: int, nblocks: int, K: int, coop, dev: torch.device):
