@@ -398,89 +398,105 @@ class cNMF:
     def _prepare_local(self, counts_fn, components, n_iter, densify, tpm_fn, seed, beta_loss,
                        num_highvar_genes, genes_file, alpha_usage, alpha_spectra, init,
                        total_workers, use_gpu, batch_size, max_NMF_iter, algo, mode):
-        """Single-process prepare (see prepare)."""
+        """Single-process prepare (see prepare).  An .h5ad ``tpm_fn`` is copied on a
+        background thread while the rest of the stage runs on the object read from the
+        source (joined before the stage ends, also on an error) -- the copy of the 5 GB
+        TP10K file was 0.5 s of the 500k-cell prepare (profiles/r4h_*)."""
+        copies = []
         with self.timer("prepare"):
-            input_counts = read_any(counts_fn, densify)
-            if sp.issparse(input_counts.X) and densify:
-                input_counts.X = np.array(input_counts.X.todense())
+            try:
+                input_counts = read_any(counts_fn, densify)
+                if sp.issparse(input_counts.X) and densify:
+                    input_counts.X = np.array(input_counts.X.todense())
 
-            if tpm_fn is None:
-                tpm = compute_tpm(input_counts)
-                write_h5ad(self.paths["tpm"], tpm)
-            elif tpm_fn.endswith(".mtx") or tpm_fn.endswith(".mtx.gz"):
-                tpm = read_10x_mtx(os.path.dirname(tpm_fn))
-                write_h5ad(self.paths["tpm"], tpm)
-            elif tpm_fn.endswith(".h5ad"):
-                shutil.copyfile(tpm_fn, self.paths["tpm"])
-                tpm = read_h5ad(self.paths["tpm"])
-            else:
-                tpm = read_counts_table(tpm_fn, densify)
-                write_h5ad(self.paths["tpm"], tpm)
-            if _device(False).type == "cuda":
-                # consensus in this process takes this object instead of re-reading the
-                # file (utils.resident: only while the file is unchanged)
-                resident.remember(self.paths["tpm"], "adata", tpm)
+                if tpm_fn is None:
+                    tpm = compute_tpm(input_counts)
+                    write_h5ad(self.paths["tpm"], tpm)
+                elif tpm_fn.endswith(".mtx") or tpm_fn.endswith(".mtx.gz"):
+                    tpm = read_10x_mtx(os.path.dirname(tpm_fn))
+                    write_h5ad(self.paths["tpm"], tpm)
+                elif tpm_fn.endswith(".h5ad"):
+                    pool = cf.ThreadPoolExecutor(1, thread_name_prefix="cnmf-tpm-copy")
+                    copies.append(pool.submit(shutil.copyfile, tpm_fn, self.paths["tpm"]))
+                    pool.shutdown(wait=False)
+                    tpm = read_h5ad(tpm_fn)
+                else:
+                    tpm = read_counts_table(tpm_fn, densify)
+                    write_h5ad(self.paths["tpm"], tpm)
+                if not copies and _device(False).type == "cuda":
+                    # consensus in this process takes this object instead of re-reading the
+                    # file (utils.resident: only while the file is unchanged)
+                    resident.remember(self.paths["tpm"], "adata", tpm)
 
-            # exact moments on the host matrix (models.hvg.exact_mean_var): the same bits
-            # as the cell-sharded prepare's all-reduced digits (_prepare_sharded)
-            ex = exact_mean_var(tpm.X, 0)
-            if ex is not None:
-                gene_tpm_mean, gene_tpm_var = ex
-                if tpm.X.dtype == np.float32:   # sklearn keeps float32 statistics
-                    gene_tpm_mean = gene_tpm_mean.astype(np.float32)
-                    gene_tpm_var = gene_tpm_var.astype(np.float32)
-                gene_tpm_std = gene_tpm_var ** 0.5
-            elif sp.issparse(tpm.X):
-                dT = _device_csr(tpm.X, _device(use_gpu))
-                gene_tpm_mean, gene_tpm_var = get_mean_var(dT if dT is not None else tpm.X)
-                del dT
-                gene_tpm_std = gene_tpm_var ** 0.5
-            else:
-                gene_tpm_mean = np.array(tpm.X.mean(axis=0)).reshape(-1)
-                gene_tpm_std = np.array(tpm.X.std(axis=0, ddof=0)).reshape(-1)
-            stats = pd.DataFrame([gene_tpm_mean, gene_tpm_std], index=["__mean", "__std"],
-                                 columns=tpm.var.index).T
-            save_df_to_npz(stats, self.paths["tpm_stats"])
+                # exact moments on the host matrix (models.hvg.exact_mean_var): the same bits
+                # as the cell-sharded prepare's all-reduced digits (_prepare_sharded)
+                ex = exact_mean_var(tpm.X, 0)
+                if ex is not None:
+                    gene_tpm_mean, gene_tpm_var = ex
+                    if tpm.X.dtype == np.float32:   # sklearn keeps float32 statistics
+                        gene_tpm_mean = gene_tpm_mean.astype(np.float32)
+                        gene_tpm_var = gene_tpm_var.astype(np.float32)
+                    gene_tpm_std = gene_tpm_var ** 0.5
+                elif sp.issparse(tpm.X):
+                    dT = _device_csr(tpm.X, _device(use_gpu))
+                    gene_tpm_mean, gene_tpm_var = get_mean_var(dT if dT is not None else tpm.X)
+                    del dT
+                    gene_tpm_std = gene_tpm_var ** 0.5
+                else:
+                    gene_tpm_mean = np.array(tpm.X.mean(axis=0)).reshape(-1)
+                    gene_tpm_std = np.array(tpm.X.std(axis=0, ddof=0)).reshape(-1)
+                stats = pd.DataFrame([gene_tpm_mean, gene_tpm_std], index=["__mean", "__std"],
+                                     columns=tpm.var.index).T
+                save_df_to_npz(stats, self.paths["tpm_stats"])
 
-            highvargenes = None
-            if genes_file is not None:
-                with open(genes_file) as fh:
-                    highvargenes = fh.read().rstrip().split("\n")
+                highvargenes = None
+                if genes_file is not None:
+                    with open(genes_file) as fh:
+                        highvargenes = fh.read().rstrip().split("\n")
 
-            dev = _device(False)
-            if not sp.issparse(input_counts.X) and dev.type == "cuda":
-                # dense counts on the GPU: scaled, checked and streamed to the h5ad from
-                # the device (same file and messages as get_norm_counts + save)
-                genes = self._hvg_filter(tpm, highvargenes, num_highvar_genes)
-                T, cols = _norm_counts_tensor(input_counts, genes, sp.issparse(tpm.X), dev)
-                self._check_norm_counts(T, input_counts.obs.index, genes)
-                self._initialize_dirs()
-                _save_norm_counts_streamed(self.paths["normalized_counts"], input_counts, T,
-                                           cols)
-                # factorize / consensus in this process read the device copy, not the file
-                # (utils.resident; the float32 cast is the one they apply to the file's data)
-                resident.remember(self.paths["normalized_counts"], "X32", T.to(torch.float32))
-                del T
-                self._prebuild_planes(dev)
-            else:
-                norm_counts = self.get_norm_counts(input_counts, tpm,
-                                                   num_highvar_genes=num_highvar_genes,
-                                                   high_variance_genes_filter=highvargenes)
-                self.save_norm_counts(norm_counts)
-                if dev.type == "cuda" and resident.wanted(norm_counts.X):
-                    # the float32 device matrix factorize would build from the file
-                    # (a sparse file: only factorize densifies it; consensus reads the
-                    # file's CSR, see _read_norm_counts)
-                    resident.remember(self.paths["normalized_counts"],
-                                      "X32" if not sp.issparse(norm_counts.X) else "X32_factorize",
-                                      torch.from_numpy(_dense32(norm_counts.X)).to(dev))
+                dev = _device(False)
+                if not sp.issparse(input_counts.X) and dev.type == "cuda":
+                    # dense counts on the GPU: scaled, checked and streamed to the h5ad from
+                    # the device (same file and messages as get_norm_counts + save)
+                    genes = self._hvg_filter(tpm, highvargenes, num_highvar_genes)
+                    T, cols = _norm_counts_tensor(input_counts, genes, sp.issparse(tpm.X), dev)
+                    self._check_norm_counts(T, input_counts.obs.index, genes)
+                    self._initialize_dirs()
+                    _save_norm_counts_streamed(self.paths["normalized_counts"], input_counts, T,
+                                               cols)
+                    # factorize / consensus in this process read the device copy, not the file
+                    # (utils.resident; the float32 cast is the one they apply to the file's data)
+                    resident.remember(self.paths["normalized_counts"], "X32", T.to(torch.float32))
+                    del T
                     self._prebuild_planes(dev)
-            replicate_params, run_params = self.get_nmf_iter_params(
-                ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
-                alpha_usage=alpha_usage, alpha_spectra=alpha_spectra, init=init,
-                total_workers=total_workers, use_gpu=use_gpu, batch_size=batch_size,
-                max_iter=max_NMF_iter, algo=algo, mode=mode)
-            self.save_nmf_iter_params(replicate_params, run_params)
+                else:
+                    norm_counts = self.get_norm_counts(input_counts, tpm,
+                                                       num_highvar_genes=num_highvar_genes,
+                                                       high_variance_genes_filter=highvargenes)
+                    self.save_norm_counts(norm_counts)
+                    if dev.type == "cuda" and resident.wanted(norm_counts.X):
+                        # the float32 device matrix factorize would build from the file
+                        # (a sparse file: only factorize densifies it; consensus reads the
+                        # file's CSR, see _read_norm_counts)
+                        tag = "X32_factorize" if sp.issparse(norm_counts.X) else "X32"
+                        resident.remember(self.paths["normalized_counts"], tag,
+                                          torch.from_numpy(_dense32(norm_counts.X)).to(dev))
+                        self._prebuild_planes(dev)
+                replicate_params, run_params = self.get_nmf_iter_params(
+                    ks=components, n_iter=n_iter, random_state_seed=seed, beta_loss=beta_loss,
+                    alpha_usage=alpha_usage, alpha_spectra=alpha_spectra, init=init,
+                    total_workers=total_workers, use_gpu=use_gpu, batch_size=batch_size,
+                    max_iter=max_NMF_iter, algo=algo, mode=mode)
+                self.save_nmf_iter_params(replicate_params, run_params)
+                for c in copies:
+                    c.result()
+            except BaseException:
+                for c in copies:        # no copy left running behind the error
+                    c.exception()
+                raise
+        if copies and _device(False).type == "cuda":
+            # (after the copy: the mirror is keyed on the finished file's identity)
+            resident.remember(self.paths["tpm"], "adata", tpm)
 
     def _prebuild_planes(self, dev) -> None:
         """Opt-in (CNMF_PREBUILD_PLANES=1, with prepare's prewarm on): build the resident

@@ -55,19 +55,25 @@ class DeviceCSR:
     @classmethod
     def from_scipy(cls, m, device=None, dtype=None) -> "DeviceCSR":
         m = m if sp.isspmatrix_csr(m) else sp.csr_matrix(m)
-        if not m.has_canonical_format:
-            m = m.copy()
-            m.sum_duplicates()       # kernels rely on distinct columns within a row
-        data = m.data
-        if dtype is None:
-            dtype = np.float64 if data.dtype == np.float64 else np.float32
         dev = torch.device(device) if device is not None else torch.device("cpu")
+        if dtype is None:
+            dtype = np.float64 if m.data.dtype == np.float64 else np.float32
 
         def up(a, dt):
             return torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)
 
-        A = cls(up(m.indptr, np.int64), up(m.indices, np.int32), up(data, dtype), m.shape)
-        return A
+        # kernels rely on distinct columns within a row: a matrix scipy has not checked
+        # yet is checked after the upload on the device (scipy's single-threaded host
+        # check was 0.11 s of the 500k-cell Harmony stage, profiles/r6w_*)
+        if dev.type == "cuda" and getattr(m, "_has_canonical_format", None) is None:
+            A = cls(up(m.indptr, np.int64), up(m.indices, np.int32), up(m.data, dtype), m.shape)
+            if _sorted_distinct(A):
+                return A
+            del A
+        if not m.has_canonical_format:
+            m = m.copy()
+            m.sum_duplicates()
+        return cls(up(m.indptr, np.int64), up(m.indices, np.int32), up(m.data, dtype), m.shape)
 
     def to_scipy(self, data: torch.Tensor | None = None) -> sp.csr_matrix:
         d = (self.data if data is None else data).cpu().numpy()
@@ -89,6 +95,18 @@ class DeviceCSR:
             self._rows = torch.repeat_interleave(
                 torch.arange(self.shape[0], device=self.device), counts)
         return self._rows
+
+
+def _sorted_distinct(A: DeviceCSR) -> bool:
+    """Whether every row's column indices strictly increase (scipy's canonical format),
+    checked where ``A`` lives."""
+    nnz = A.indices.numel()
+    if nnz < 2:
+        return True
+    start = torch.zeros(nnz, dtype=torch.bool, device=A.indices.device)
+    p = A.indptr[1:-1]
+    start[p[p < nnz]] = True         # first entry of each row (empty rows repeat a position)
+    return bool(((A.indices[1:] > A.indices[:-1]) | start[1:]).all())
 
 
 def _ptr(t):

@@ -428,3 +428,30 @@ def test_silhouette_matches_sklearn_precomputed(n, c, seed):
     got = silhouette(D, lab)
     want = silhouette_score(D.numpy(), lab, metric="precomputed")
     assert abs(got - want) <= 1e-10 * max(1.0, abs(want))
+
+
+def test_prepare_with_h5ad_tpm_copies_it_in_the_background(tmp_path, counts_file):
+    """An .h5ad tpm_fn is copied on a worker thread while prepare runs on the object read
+    from the source: the copy is complete (byte-identical) when prepare returns, and the
+    statistics / norm counts equal those of prepare computing the TPM itself."""
+    from cnmf_torch_amd.models.hvg import compute_tpm
+    from cnmf_torch_amd.utils.h5ad import write_h5ad
+    from cnmf_torch_amd.utils.io import read_any
+
+    tpm_fn = str(tmp_path / "tpm.h5ad")
+    write_h5ad(tpm_fn, compute_tpm(read_any(counts_file[0], False)))
+    out = {}
+    for name, tfn in (("own", None), ("given", tpm_fn)):
+        obj = cNMF(output_dir=str(tmp_path), name=name)
+        obj.prepare(counts_file[0], components=[5], n_iter=2, seed=1, num_highvar_genes=200,
+                    tpm_fn=tfn, prewarm=False)
+        out[name] = obj
+    with open(tpm_fn, "rb") as a, open(out["given"].paths["tpm"], "rb") as b:
+        assert a.read() == b.read()
+    for key in ("tpm_stats", "normalized_counts"):
+        if key == "tpm_stats":
+            x, y = (load_df_from_npz(o.paths[key]) for o in out.values())
+            pd.testing.assert_frame_equal(x, y)
+        else:
+            x, y = (read_any(o.paths[key], False).X for o in out.values())
+            np.testing.assert_array_equal(x.toarray(), y.toarray())

@@ -240,3 +240,28 @@ def test_gemm_plan_fills_whole_waves_for_mid_size_batches():
     assert ops.gemm_plan(2000, 2000, 5056, 1) == (1, 2)      # K=20 statistics
     assert ops.gemm_plan(3000, 5000, 2048, 1) == (1, 1)      # K=30 numerator
     assert ops.gemm_plan(5000, 5000, 2048, 1) == (1, 1)      # K=50: the older rule
+
+
+@pytest.mark.gpu
+def test_from_scipy_canonical_check_on_device():
+    """An unchecked CSR is checked for sorted, distinct columns on the device after the
+    upload; one that is not canonical is summed on the host like scipy's own path."""
+    m = sp.random(300, 120, density=0.1, format="csr", random_state=1, dtype=np.float32)
+    for case in ("sorted", "reversed", "duplicate"):
+        ind = m.indices.copy()
+        data = m.data.copy()
+        if case == "reversed":
+            for r in range(m.shape[0]):
+                a, b = m.indptr[r], m.indptr[r + 1]
+                ind[a:b] = ind[a:b][::-1].copy()
+                data[a:b] = data[a:b][::-1].copy()
+        elif case == "duplicate":
+            r = int(np.flatnonzero(np.diff(m.indptr) >= 2)[0])
+            ind[m.indptr[r] + 1] = ind[m.indptr[r]]
+        x = sp.csr_matrix((data, ind, m.indptr.copy()), shape=m.shape)
+        A = sops.DeviceCSR.from_scipy(x, device="cuda")
+        assert sops._sorted_distinct(A)
+        ref = x.copy()
+        ref.sum_duplicates()
+        np.testing.assert_array_equal(A.to_scipy().toarray(), ref.toarray())
+        np.testing.assert_array_equal(A.indptr.cpu().numpy(), ref.indptr)
