@@ -114,17 +114,13 @@ def _dt_str(density_threshold) -> str:
 
 
 def gpu_max_rank(beta_loss="frobenius", algo="mu") -> int | None:
-    """Largest K the native MI355X kernels factorise (None: no limit -- 'bpp' solves its
-    NNLS blocks with torch linear algebra).  Frobenius MU pads K to a multiple of 8 up to
-    64 and of 16 up to 128 (models.nmf.native_rank; K > 64 on the matrix-core wide solve),
-    HALS up to 64; the beta-divergence kernels take K <= 32."""
-    if algo == "bpp":
-        return None
-    from .models.nmf import beta_value
+    """Largest K the native MI355X kernels factorise (None: no limit), as
+    models.nmf_base.kernel_max_rank: Frobenius MU any K (register-tiled kernels to 128,
+    the rank-general solve beyond), HALS 512, KL 64, the other beta-divergences 56,
+    'bpp' any K (torch linear algebra)."""
+    from .models.nmf import beta_value, kernel_max_rank
 
-    if beta_value(beta_loss) != 2.0:
-        return 32
-    return 128 if algo == "mu" else 64
+    return kernel_max_rank(beta_value(beta_loss), algo)
 
 
 def check_gpu_ranks(components, beta_loss="frobenius", algo="mu", use_gpu=True) -> list:

@@ -602,24 +602,26 @@ class PlanesOnlyX:
 
 
 def kernel_max_rank(beta: float, algo: str) -> int | None:
-    """Largest K the native kernels factorise (None: no limit -- 'bpp' solves its NNLS
-    blocks with torch linear algebra): Frobenius MU 128 (padded, native_rank), HALS /
-    halsvar 64, KL 64 and the other beta-divergences 56 (padded to a multiple of 8 above
-    32; beta_planes_wide*.hip -- an IS / general-beta K = 64 panel pair exceeds the LDS).
-    Larger ranks are routed to the eager PyTorch ops on the same GPU (NMFBatchSolver.run,
-    logged)."""
+    """Largest K the native kernels factorise (None: no limit).  Frobenius MU: any K --
+    register-tiled kernels up to 128 (padded, native_rank), the rank-general solve beyond
+    (solve_any.hip: library Gram-x GEMM + HIP update / stop kernels); HALS / halsvar: 512
+    (64 on the tiled kernels, solve_any.hip's LDS-resident Gauss-Seidel sweep above);
+    'bpp' solves its NNLS blocks with torch linear algebra.  KL 64 and the other
+    beta-divergences 56 (padded to a multiple of 8 above 32; beta_planes_wide*.hip -- an
+    IS / general-beta K = 64 panel pair exceeds the LDS).  Larger ranks are routed to the
+    eager PyTorch ops on the same GPU (NMFBatchSolver.run, logged)."""
     if algo == "bpp":
         return None
     if beta != 2.0:
         return 64 if beta == 1.0 else 56
-    return 128 if algo == "mu" else 64
-
+    return None if algo == "mu" else 512
 
 
 def native_rank(K: int) -> int:
     """The rank the GPU kernels run a rank-K replicate at: K itself for K <= 32, else K
-    padded with zero components to a multiple of 8 (<= 64) or of 16 (<= 128, MU only: the
-    matrix-core wide solve, solve_wmfma.hip) -- a zero row of W / H stays zero under MU
+    padded with zero components to a multiple of 8 (<= 64) or of 16 (<= 128: MU's
+    matrix-core wide solve, solve_wmfma.hip), and K itself above 128 (the rank-general
+    solve, solve_any.hip) -- a zero row of W / H stays zero under MU
     (rate 0 where the denominator vanishes) and HALS (zero diagonal), and contributes
     nothing to the Gram matrices or the loss, so the padded solve IS the rank-K solve
     (cnmf.py:1416 takes any -k)."""
@@ -629,7 +631,7 @@ def native_rank(K: int) -> int:
     if K <= 64:
         return -(-K // 8) * 8
     if K > 128:
-        raise ValueError(f"K={K}: the native kernels cover K <= 128")
+        return K        # the rank-general solve (solve_any.hip) takes K as it is
     return -(-K // 16) * 16
 
 

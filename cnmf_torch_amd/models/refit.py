@@ -83,14 +83,14 @@ def chunked_solve(HT: torch.Tensor, numerT: torch.Tensor, gram: torch.Tensor, ch
                   eps: float = 1e-16, algo: str = "mu") -> torch.Tensor:
     """Independent per-chunk solves of HT (K x n) in place; one launch for all full chunks.
     On the GPU a rank without its own kernel instantiation (K > 32 not a multiple of 8,
-    K > 64 not a multiple of 16) is solved padded with zero components, which stay zero
+    64 < K <= 128 not a multiple of 16) is solved padded with zero components, which stay zero
     and leave the Gram products and the objective unchanged (models.nmf.native_rank)."""
     K, n = HT.shape
     if HT.device.type == "cuda" and algo != "bpp" and ops.use_native(HT):
         from .nmf import _warn_once, kernel_max_rank, native_rank
 
         kmax = kernel_max_rank(2.0, algo)
-        if K > kmax:    # no kernel for this rank: the PyTorch ops on the same GPU, logged
+        if kmax is not None and K > kmax:    # no kernel for this rank: the PyTorch ops on the same GPU, logged
             _warn_once(f"refit K={K}: the native gfx950 solve covers K <= {kmax}; this "
                        "refit runs the eager PyTorch ops on the GPU (slower)")
             with ops.eager_ops():

@@ -211,6 +211,19 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
                          col_mul=planes_colmul)
         return 1
     h = _hip
+    if solve_any_k(a, K):
+        # ranks beyond the register-tiled kernels: library Gram-x GEMM + solve_any.hip
+        if fused or variant == "mfma":
+            raise ValueError(f"solve: K={K} runs the rank-general solve (solve_any.hip), "
+                             "which takes no fused operands / variant='mfma'")
+        if gram is None:
+            gram = _gram_op(gram_of, active=active)
+        _solve_any(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2, eps,
+                   lin_out, quad_out, iters_out, nsplit, conv_mode, check_every, active)
+        if planes is not None:
+            split_planes(x.reshape(R * K, n), planes[:min(int(planes_n), planes.shape[0])],
+                         col_mul=planes_colmul)
+        return 1
     # a GPU operand the kernels do not cover is an error, never a silent eager fallback:
     # fp32 only; K in 1..32 or a padded wide rank (the engine pads K <= 64 to a multiple
     # of 8 and K <= 128 to a multiple of 16, models/nmf.py native_rank)
@@ -352,6 +365,116 @@ def solve(algo: str, x: torch.Tensor, numer: torch.Tensor, gram: torch.Tensor,
             *f_args, *gen_dev, int(rpl), _stamp_buffer(vcode, rpl, nblocks, S, K, x),
             _stream_ptr(x))
     return int(S)
+
+
+def solve_any_k(algo: int, K: int) -> bool:
+    """Whether a rank-K solve runs the rank-general kernels (solve_any.hip): K beyond the
+    register-tiled instantiations -- MU K > 128 or not an instantiated rank, HALS K > 64."""
+    if _hip is None:
+        return False
+    return (not _hip.solve_native_k(K)) or (K > 64 and algo != ALGO_MU)
+
+
+def solve_any_max_k(algo: int) -> int | None:
+    """Largest K the rank-general solve takes (None: any -- MU's sweep is a library GEMM
+    plus elementwise kernels; HALS keeps a 64-column tile of every component in LDS)."""
+    return None if algo == ALGO_MU else int(_hip.solve_any_hals_max_k())
+
+
+def _solve_any(a, x, numer, gram, rep_index, max_iter, tol, l1_num, l1_den, l2, eps,
+               lin_out, quad_out, iters_out, nsplit, conv_mode, check_every, active) -> None:
+    """ops.solve at any K (csrc/kernels/solve_any.hip; contract = reference.solve): per
+    sweep D = Gram x is one batched library GEMM (torch.bmm -> rocBLAS / hipBLASLt), the
+    objective / update / stop decisions are HIP kernels with device-side live flags.  The
+    host looks at the flags once per objective check (outside graph capture) to end the
+    loop when every replicate has stopped."""
+    h = _hip
+    R, K, n = x.shape
+    mk = solve_any_max_k(a)
+    if mk is not None and K > mk:
+        raise ValueError(f"solve: HALS at K={K} exceeds the rank-general kernel's maximum {mk} "
+                         "(use algo='mu' or 'bpp')")
+    for name, t in (("x", x), ("numer", numer)):
+        if t.dtype != torch.float32 or (n > 1 and t.stride(2) != 1):
+            raise ValueError(f"solve: {name} must be float32 with unit column stride")
+    dev = x.device
+    st = _stream_ptr(x)
+    ident = rep_index is None
+    reps = None if ident else rep_index.to(device=dev, dtype=torch.int32).contiguous()
+    m = R if ident else int(reps.numel())
+    if m == 0 or n == 0:
+        return
+    reps_l = None if ident else reps.long()
+    act = torch.ones(m, dtype=torch.int32, device=dev)
+    if active is not None:
+        act = (active[:R] if ident else active[reps_l]).ne(0).to(torch.int32)
+    act0 = act.clone()
+    G = gram.contiguous()
+    Gm = G if ident else G.index_select(0, reps_l)
+    D = torch.empty((m, K, n), dtype=torch.float32, device=dev)
+
+    def gram_x():
+        torch.bmm(Gm, x if ident else x.index_select(0, reps_l), out=D)
+
+    per = max(256, -(-n // max(1, min(-(-n // 256), 2048 // m))))
+    nblk_s = -(-n // per)
+    nblk_h = -(-n // 64)
+    part = torch.empty(m * max(nblk_s, nblk_h) * 2, dtype=torch.float64, device=dev)
+    f_prev = torch.zeros(m, dtype=torch.float64, device=dev)
+    it_ptr = iters_out.data_ptr() if iters_out is not None else 0
+    if iters_out is not None and (iters_out.dtype != torch.int32 or not iters_out.is_contiguous()):
+        raise ValueError("iters_out: contiguous int32")
+    rp = reps.data_ptr() if reps is not None else 0
+
+    def launch(op):
+        h.solve_any(op, x.data_ptr(), x.stride(0), x.stride(1), numer.data_ptr(), numer.stride(0),
+                    numer.stride(1), D.data_ptr(), G.data_ptr(), K * K, rp, act.data_ptr(), m, K,
+                    n, per, float(l1_num), float(l1_den), float(l2), float(eps), part.data_ptr(),
+                    it_ptr if op >= 2 else 0, st)
+
+    def decide(mode, nblk, have_prev=0, lin=None, quad=None):
+        h.solve_any_conv(mode, part.data_ptr(), nblk, m, act.data_ptr(), act0.data_ptr(), rp,
+                         f_prev.data_ptr(), int(have_prev), float(tol), float(eps),
+                         lin.data_ptr() if lin is not None else 0,
+                         quad.data_ptr() if quad is not None else 0, st)
+
+    check = nsplit <= 1
+    loss_conv = check and conv_mode == 1
+    every = max(1, int(check_every))
+    capturing = torch.cuda.is_current_stream_capturing()
+    have_prev = False
+    it = 0
+    while True:
+        fresh = False
+        if loss_conv and it % every == 0:
+            if it > 0 and not capturing and not bool(act.any()):
+                break
+            gram_x()
+            fresh = True
+            launch(0)
+            decide(0, nblk_s, have_prev)
+            have_prev = True
+        if it >= int(max_iter):
+            break
+        if check and not loss_conv and it > 0 and it % every == 0 and not capturing \
+                and not bool(act.any()):
+            break
+        if a == ALGO_MU:
+            if not fresh:
+                gram_x()
+            launch(3 if (check and not loss_conv) else 2)
+        else:
+            launch(5 if (check and not loss_conv) else 4)
+        it += 1
+        if check and not loss_conv:
+            decide(1, nblk_s if a == ALGO_MU else nblk_h)
+    if lin_out is not None or quad_out is not None:
+        for name, t in (("lin_out", lin_out), ("quad_out", quad_out)):
+            if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+                raise ValueError(f"{name}: contiguous float32")
+        gram_x()
+        launch(1)
+        decide(2, nblk_s, lin=lin_out, quad=quad_out)
 
 
 # Diagnostic phase stamps of the pipelined solve (tools/pipe_stamp_probe.py sets
@@ -1434,8 +1557,8 @@ def kl_sparse_w_num(tiles: list, HT3: torch.Tensor, W3: torch.Tensor, eps: float
 def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = False,
          active: torch.Tensor | None = None) -> torch.Tensor:
     """out[r] (+)= X3[r] X3[r]^T for X3 (R, K, n) with unit column stride (any row and
-    replicate strides), K <= 128: one MFMA workgroup per replicate (four for K > 64, one
-    per 64 x 64 block; gram.hip).  Replicates
+    replicate strides).  K <= 128: one MFMA workgroup per replicate (four for K > 64, one
+    per 64 x 64 block; gram.hip); larger K: the library batched GEMM.  Replicates
     whose ``active`` flag is 0 keep their ``out`` untouched."""
     R, K, n = X3.shape
     if out is None:
@@ -1444,8 +1567,10 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
         out = torch.empty((R, K, K), device=X3.device, dtype=X3.dtype)
     native = use_native(X3)
     if native:
-        _native_dtype_k("gram", X3.dtype, K, 128)
-    else:
+        _native_dtype_k("gram", X3.dtype, K, 1 << 30)
+    if not native or K > 128:
+        # (K > 128 on the GPU: a plain batched GEMM for the library, the rank-general
+        # solve's system matrix -- solve_any.hip)
         g = torch.bmm(X3, X3.transpose(1, 2))
         if active is not None:
             keep = (active[:R] != 0).view(R, 1, 1)

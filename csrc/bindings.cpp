@@ -453,6 +453,28 @@ PYBIND11_MODULE(_hip, m) {
           "harmony_objective");
   });
 
+  m.def("solve_any_hals_max_k", []() { return cnmf_solve_any_hals_max_k(); });
+  m.def("solve_any", [](int op, uintptr_t x, long long x_rs, long long ldx, uintptr_t numer,
+                        long long n_rs, long long ldn, uintptr_t D, uintptr_t G, long long g_rs,
+                        uintptr_t reps, uintptr_t act, int m_, int K, int n, int per,
+                        float l1_num, float l1_den, float l2, float eps, uintptr_t part,
+                        uintptr_t iters, uintptr_t stream) {
+    check(cnmf_solve_any(op, P<float>(x), x_rs, ldx, P<const float>(numer), n_rs, ldn,
+                         P<const float>(D), P<const float>(G), g_rs, P<const int>(reps),
+                         P<int>(act), m_, K, n, per, l1_num, l1_den, l2, eps, P<double>(part),
+                         P<int>(iters), reinterpret_cast<hipStream_t>(stream)),
+          "solve_any");
+  });
+  m.def("solve_any_conv", [](int mode, uintptr_t part, int nblk, int m_, uintptr_t act,
+                             uintptr_t act0, uintptr_t reps, uintptr_t f_prev, int have_prev,
+                             float tol, float eps, uintptr_t lin_out, uintptr_t quad_out,
+                             uintptr_t stream) {
+    check(cnmf_solve_any_conv(mode, P<const double>(part), nblk, m_, P<int>(act),
+                              P<const int>(act0), P<const int>(reps), P<double>(f_prev),
+                              have_prev, tol, eps, P<float>(lin_out), P<float>(quad_out),
+                              reinterpret_cast<hipStream_t>(stream)),
+          "solve_any_conv");
+  });
   m.def("gram", [](uintptr_t X, long long x_rs, long long ldx, int R, int K, int n,
                    uintptr_t out, long long o_rs, int accumulate, uintptr_t active,
                    uintptr_t part, int S, uintptr_t stream) {

@@ -135,6 +135,17 @@ hipError_t cnmf_harmony_objective(const double* O, const double* E, const double
                                   const double* theta, int K, int B, double* obj, double* out,
                                   hipStream_t stream);
 
+int cnmf_solve_any_hals_max_k();
+hipError_t cnmf_solve_any(int op, float* x, long long x_rs, long long ldx, const float* numer,
+                          long long n_rs, long long ldn, const float* D, const float* G,
+                          long long g_rs, const int* reps, int* act, int m, int K, int n, int per,
+                          float l1_num, float l1_den, float l2, float eps, double* part,
+                          int* iters, hipStream_t stream);
+hipError_t cnmf_solve_any_conv(int mode, const double* part, int nblk, int m, int* act,
+                               const int* act0, const int* reps, double* f_prev, int have_prev,
+                               float tol, float eps, float* lin_out, float* quad_out,
+                               hipStream_t stream);
+
 hipError_t cnmf_gram(const float* X, long long x_rs, long long ldx, int R, int K, int n,
                      float* out, long long o_rs, int accumulate, const int* active,
                      float* part, int S, hipStream_t stream);

@@ -269,14 +269,16 @@ def test_planes_only_x_factorises_like_the_resident_matrix():
 
 def test_native_rank_padding_rule():
     """GPU rank padding (models.nmf.native_rank): K <= 32 as is, multiples of 8 up to 64,
-    multiples of 16 up to 128 (the matrix-core wide MU solve), beyond that an error."""
-    from cnmf_torch_amd.models.nmf import native_rank
+    multiples of 16 up to 128 (the matrix-core wide MU solve), K itself beyond (the
+    rank-general solve, solve_any.hip)."""
+    from cnmf_torch_amd.models.nmf import kernel_max_rank, native_rank
 
     assert [native_rank(k) for k in (1, 10, 32)] == [1, 10, 32]
     assert [native_rank(k) for k in (33, 40, 41, 64)] == [40, 40, 48, 64]
     assert [native_rank(k) for k in (65, 80, 81, 100, 128)] == [80, 80, 96, 112, 128]
-    with pytest.raises(ValueError, match="K <= 128"):
-        native_rank(129)
+    assert [native_rank(k) for k in (129, 200, 1000)] == [129, 200, 1000]
+    assert kernel_max_rank(2.0, "mu") is None and kernel_max_rank(2.0, "hals") == 512
+    assert kernel_max_rank(1.0, "mu") == 64 and kernel_max_rank(0.0, "mu") == 56
 
 
 def test_padded_rank_solve_equals_unpadded_on_cpu():

@@ -268,25 +268,86 @@ def test_host_compaction_matches_uncompacted(monkeypatch, ks, pmap):
     np.testing.assert_allclose(b.err[same], c.err[same], rtol=1e-5)
 
 
-def test_rank_beyond_kernels_routes_to_eager_ops_on_the_gpu():
-    """K > 128 (no kernel instantiation) is routed to the eager PyTorch ops on the same
-    GPU with a warning -- the job completes and matches the CPU engine's factorisation of
-    the same seeds (same algorithm, fp32 rounding apart) -- and a mixed batch splits by K
-    (the covered K stays on the native kernels)."""
+def test_rank_beyond_tiled_kernels_runs_native_on_the_gpu(recwarn):
+    """K > 128 Frobenius runs the rank-general solve (solve_any.hip) on the GPU -- no eager
+    routing, no warning -- and factorises like the CPU engine (same seeds, same algorithm,
+    fp32 rounding apart); a mixed batch keeps every K in one ragged batch; refits at that
+    rank run natively too."""
     from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
     from cnmf_torch_amd.models.refit import fit_H_online
     from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
 
     Xn = normalized_counts_matrix(900, 300, n_programs=6, seed=2)
     opts = NMFOptions(n_components=130, online_chunk_size=450, online_max_pass=4)
-    with pytest.warns(RuntimeWarning, match="K=130: the native gfx950 kernels cover K <= 128"):
-        g = NMFBatchSolver(torch.from_numpy(Xn).cuda(), opts).run([5, 6], ks=[130, 10])
+    g = NMFBatchSolver(torch.from_numpy(Xn).cuda(), opts).run([5, 6], ks=[130, 10])
     c = NMFBatchSolver(torch.from_numpy(Xn), opts).run([5, 6], ks=[130, 10])
     assert g.W.shape == (140, 300) and torch.isfinite(g.W).all()
     np.testing.assert_allclose(g.err, c.err, rtol=2e-3)
-    with pytest.warns(RuntimeWarning, match="refit K=130"):
-        U = fit_H_online(Xn, g.W[:130].cpu().numpy(), device="cuda")
+    U = fit_H_online(Xn, g.W[:130].cpu().numpy(), device="cuda")
     assert U.shape == (900, 130) and np.isfinite(U).all() and (U >= 0).all()
+    Uc = fit_H_online(Xn, g.W[:130].cpu().numpy(), device="cpu")
+    np.testing.assert_allclose(U, Uc, rtol=5e-3, atol=1e-4 * float(np.abs(Uc).max()))
+    hals = NMFOptions(n_components=100, algo="hals", online_chunk_size=450, online_max_pass=3)
+    gh = NMFBatchSolver(torch.from_numpy(Xn).cuda(), hals).run([3])
+    ch = NMFBatchSolver(torch.from_numpy(Xn), hals).run([3])
+    np.testing.assert_allclose(gh.err, ch.err, rtol=2e-3)
+    assert not [w for w in recwarn.list if "eager" in str(w.message)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo,K,conv,tol", [("mu", 130, 1, 0.0), ("mu", 200, 0, 0.0),
+                                              ("mu", 144, 1, 1e-3), ("mu", 136, 0, 1e-3),
+                                              ("hals", 80, 1, 0.0), ("hals", 200, 0, 0.0),
+                                              ("hals", 72, 1, 1e-3), ("hals", 130, 0, 1e-3)])
+def test_solve_any_rank_matches_float64_reference(algo, K, conv, tol):
+    """The rank-general solve (ops.solve at K beyond the tiled kernels) == the float64
+    reference solve: strided x, a replicate subset (rep_index) with one replicate inactive,
+    l1 / l2, both stop rules, lin / quad / iters outputs.  tol = 0 runs every step (x to
+    fp32 accuracy, iteration counts exact); tol > 0 stops on the device (counts within one
+    check interval, x pinned where the counts agree)."""
+    from cnmf_torch_amd import ops
+    from cnmf_torch_amd.ops import reference
+
+    g = torch.Generator().manual_seed(K + conv)
+    R, n, m = 5, 700, 300
+    F = torch.rand((R, K, m), generator=g, dtype=torch.float64)
+    gram = torch.bmm(F, F.transpose(1, 2)) / m
+    numer = torch.bmm(gram, torch.rand((R, K, n), generator=g, dtype=torch.float64))
+    numer *= 0.5 + torch.rand((R, K, n), generator=g, dtype=torch.float64)
+    x0 = torch.rand((R, K, n), generator=g, dtype=torch.float64)
+    reps = torch.tensor([0, 2, 3, 4], dtype=torch.int32)
+    act = torch.tensor([1, 1, 1, 0, 1], dtype=torch.int32)
+    kw = dict(max_iter=25, tol=tol, l1_num=1e-3, l1_den=1e-2, l2=2e-2, eps=1e-16,
+              conv_mode=conv, check_every=5)
+    xr = x0.clone()
+    lin_r, quad_r = torch.zeros(R, dtype=torch.float64), torch.zeros(R, dtype=torch.float64)
+    it_r = torch.zeros(R, dtype=torch.int32)
+    reference.solve(ops.ALGOS[algo], xr, numer, gram, reps, kw["max_iter"], tol, 1e-3, 1e-2,
+                    2e-2, 1e-16, lin_r, quad_r, it_r, 1, conv, 5, act)
+    buf = torch.zeros((R, K, n + 37), dtype=torch.float32, device="cuda")
+    xg = buf[:, :, :n]
+    xg.copy_(x0)
+    lin_g = torch.zeros(R, dtype=torch.float32, device="cuda")
+    quad_g = torch.zeros_like(lin_g)
+    it_g = torch.zeros(R, dtype=torch.int32, device="cuda")
+    assert ops.solve_any_k(ops.ALGOS[algo], K)
+    ops.solve(algo, xg, numer.float().cuda(), gram.float().cuda(), rep_index=reps.cuda(),
+              lin_out=lin_g, quad_out=quad_g, iters_out=it_g, active=act.cuda(), **kw)
+    torch.cuda.synchronize()
+    it_g = it_g.cpu()
+    assert it_g[1] == 0 and it_g[3] == 0 and float(lin_g[3]) == 0.0     # untouched
+    np.testing.assert_array_equal(xg[3].cpu().numpy(), x0[3].float().numpy())
+    if tol == 0.0:
+        assert torch.equal(it_g, it_r) and int(it_r[0]) == 25
+    else:
+        assert (it_g - it_r).abs().max() <= 5
+    for r in (0, 2, 4):
+        if it_g[r] != it_r[r]:
+            continue
+        np.testing.assert_allclose(xg[r].cpu().double().numpy(), xr[r].numpy(), rtol=2e-3,
+                                   atol=2e-5 * float(xr[r].abs().max()))
+        np.testing.assert_allclose(float(lin_g[r]), float(lin_r[r]), rtol=1e-4)
+        np.testing.assert_allclose(float(quad_g[r]), float(quad_r[r]), rtol=1e-4)
 
 
 @pytest.mark.parametrize("N,G,K", [(1000, 300, 10), (777, 2001, 7), (4096, 128, 64), (130, 70, 128)])
