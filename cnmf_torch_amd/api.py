@@ -115,8 +115,8 @@ def _dt_str(density_threshold) -> str:
 
 def gpu_max_rank(beta_loss="frobenius", algo="mu") -> int | None:
     """Largest K the native MI355X kernels factorise (None: no limit), as
-    models.nmf_base.kernel_max_rank: Frobenius MU any K (register-tiled kernels to 128,
-    the rank-general solve beyond), HALS 512, KL 64, the other beta-divergences 56,
+    models.nmf_base.kernel_max_rank: Frobenius MU and the beta-divergences any K
+    (register-tiled kernels to 128 / 64 / 56, the rank-general paths beyond), HALS 512,
     'bpp' any K (torch linear algebra)."""
     from .models.nmf import beta_value, kernel_max_rank
 

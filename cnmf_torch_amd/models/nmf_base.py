@@ -604,16 +604,14 @@ class PlanesOnlyX:
 def kernel_max_rank(beta: float, algo: str) -> int | None:
     """Largest K the native kernels factorise (None: no limit).  Frobenius MU: any K --
     register-tiled kernels up to 128 (padded, native_rank), the rank-general solve beyond
-    (solve_any.hip: library Gram-x GEMM + HIP update / stop kernels); HALS / halsvar: 512
-    (64 on the tiled kernels, solve_any.hip's LDS-resident Gauss-Seidel sweep above);
-    'bpp' solves its NNLS blocks with torch linear algebra.  KL 64 and the other
-    beta-divergences 56 (padded to a multiple of 8 above 32; beta_planes_wide*.hip -- an
-    IS / general-beta K = 64 panel pair exceeds the LDS).  Larger ranks are routed to the
-    eager PyTorch ops on the same GPU (NMFBatchSolver.run, logged)."""
-    if algo == "bpp":
+    (solve_any.hip: library Gram-x GEMM + HIP update / objective / stop kernels); HALS /
+    halsvar: 512 (64 on the tiled kernels, solve_any.hip's LDS-resident Gauss-Seidel sweep
+    above); the beta-divergences: any K (split-bf16 panel kernels to KL 64 / IS 56, the
+    rank-general path beyond: library GEMMs for P and the contractions, beta_any.hip for
+    the terms); 'bpp' solves its NNLS blocks with torch linear algebra.  Larger ranks are
+    routed to the eager PyTorch ops on the same GPU (NMFBatchSolver.run, logged)."""
+    if algo == "bpp" or beta != 2.0:
         return None
-    if beta != 2.0:
-        return 64 if beta == 1.0 else 56
     return None if algo == "mu" else 512
 
 

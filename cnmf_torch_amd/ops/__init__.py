@@ -962,6 +962,63 @@ def _bp_kl(mode: int) -> bool:
     return mode in (BP_KL_FP16, BP_KL)
 
 
+def beta_any_k(K: int, beta: float) -> bool:
+    """Whether the beta-MU ops run rank K on the rank-general path (beta_any.hip): beyond
+    the split-bf16 panel kernels -- KL K > 64, IS / general beta K > 56 (an IS K = 64 panel
+    pair exceeds the LDS)."""
+    if _hip is None:
+        return False
+    return K > (int(_hip.bp_max_k()) if beta == 1.0 else 56)
+
+
+def _beta_contract_any(side: int, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor,
+                       beta: float, eps: float, want_num: bool = True, want_loss: bool = False,
+                       active: torch.Tensor | None = None):
+    """reference.beta_contract's contract at any K on the GPU: per block of rows, P =
+    H^T W and the numerator / denominator contractions are batched library GEMMs (real
+    GEMMs at these ranks), Q = X p^(beta-2), D = p^(beta-1) and the divergence sums one
+    pass of beta_any_terms (csrc/kernels/beta_any.hip) over P, in place."""
+    R, K, N = HT3.shape
+    G = W3.shape[2]
+    dev = HT3.device
+    mode = beta_mode(beta)
+    out_n = N if side == 0 else G
+    num = torch.zeros((R, K, out_n), dtype=torch.float32, device=dev) if want_num else None
+    den = (torch.zeros((R, K, out_n), dtype=torch.float32, device=dev)
+           if (want_num and mode != 0) else None)
+    loss = (torch.zeros(R, dtype=torch.float64, device=dev) if (want_loss and side == 0)
+            else None)
+    act = None if active is None else active[:R].to(torch.int32).contiguous()
+    Xf = X if (X.dtype == torch.float32 and X.stride(-1) == 1) else X.float().contiguous()
+    Wf = W3.float()
+    rows = int(_hip.beta_any_rows())
+    c = max(rows, min(N, (1 << 28) // max(1, R * G)))     # <= 1 GiB of P per block
+    st = _stream_ptr(HT3)
+    for a in range(0, N, c):
+        b = min(N, a + c)
+        h = HT3[:, :, a:b].float()
+        P = torch.bmm(h.transpose(1, 2), Wf)            # (R, c, G)
+        Dm = torch.empty_like(P) if den is not None else None
+        part = (torch.empty((R, -(-(b - a) // rows)), dtype=torch.float64, device=dev)
+                if loss is not None else None)
+        _hip.beta_any_terms(mode, Xf[a:b].data_ptr(), Xf.stride(0), P.data_ptr(),
+                            Dm.data_ptr() if Dm is not None else 0, R, b - a, G, float(beta),
+                            float(eps), act.data_ptr() if act is not None else 0,
+                            int(bool(want_num)), part.data_ptr() if part is not None else 0, st)
+        if want_num:
+            if side == 0:
+                num[:, :, a:b] = torch.bmm(Wf, P.transpose(1, 2))
+                if Dm is not None:
+                    den[:, :, a:b] = torch.bmm(Wf, Dm.transpose(1, 2))
+            else:
+                num.baddbmm_(h, P)
+                if Dm is not None:
+                    den.baddbmm_(h, Dm)
+        if part is not None:
+            loss += part.sum(1)
+    return num, den, loss
+
+
 def beta_contract(side: str, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor,
                   beta: float, eps: float, want_num: bool = True, want_loss: bool = False,
                   active: torch.Tensor | None = None, splits: int | None = None,
@@ -986,6 +1043,13 @@ def beta_contract(side: str, X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tenso
     if not use_native(HT3):
         num, den, loss = reference.beta_contract(s, X, HT3, W3, beta, eps, want_num, want_loss,
                                                  active)
+        if not reduce and num is not None:
+            num = num.unsqueeze(0)
+            den = den.unsqueeze(0) if den is not None else None
+        return num, den, loss
+    if beta_any_k(K, beta):
+        num, den, loss = _beta_contract_any(s, X, HT3, W3, beta, eps, want_num, want_loss,
+                                            active)
         if not reduce and num is not None:
             num = num.unsqueeze(0)
             den = den.unsqueeze(0) if den is not None else None
@@ -1068,6 +1132,10 @@ def beta_update_h(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: fl
     if not use_native(HT3):
         return reference.beta_update_h(X, HT3, W3, beta, eps, l1, l2, gamma, act, tol, iters,
                                        conv_mode, check_every, hstate)
+    if beta_any_k(K, beta):
+        return reference.beta_update_h(X, HT3, W3, beta, eps, l1, l2, gamma, act, tol, iters,
+                                       conv_mode, check_every, hstate,
+                                       contract=_beta_contract_any)
     _native_dtype_k("beta_update_h", HT3.dtype, K, _hip.beta_max_k())
     if X.shape != (N, G) or W3.shape[:2] != (R, K):
         raise ValueError("beta_update_h: inconsistent shapes")
@@ -1197,6 +1265,9 @@ def beta_panels(F3: torch.Tensor, beta: float, out: torch.Tensor | None = None,
     = 1 / u, so c / P' = x / P; :func:`beta_h_block` ``xh``).  Returns (R, panel_elems)
     int16."""
     R, K, L = F3.shape
+    if use_native(F3) and beta_any_k(K, beta):
+        # the rank-general path reads F3 itself (an empty placeholder keeps callers uniform)
+        return torch.empty((R, 0), dtype=torch.int16, device=F3.device)
     _native_dtype_k("beta_panels", F3.dtype, K, _hip.bp_max_k())
     _bp_check("F3", F3, F3.device)
     mode = bp_mode(beta)
@@ -1259,6 +1330,10 @@ def beta_h_block(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: flo
     if not use_native(HT3):
         return reference.beta_h_block(X, HT3, W3, beta, eps, nsteps, l1, l2, gamma, act, tol,
                                       iters, conv_mode, hstate, loss_entry)
+    if beta_any_k(K, beta):
+        return reference.beta_h_block(X, HT3, W3, beta, eps, nsteps, l1, l2, gamma, act, tol,
+                                      iters, conv_mode, hstate, loss_entry,
+                                      contract=_beta_contract_any)
     dev = HT3.device
     _native_dtype_k("beta_h_block", HT3.dtype, K, _hip.bp_max_k())
     for name, t in (("X", X), ("HT3", HT3), ("W3", W3)):
@@ -1320,6 +1395,8 @@ def beta_loss(X: torch.Tensor, HT3: torch.Tensor, W3: torch.Tensor, beta: float,
         raise ValueError("beta_loss: inconsistent shapes")
     if not use_native(HT3):
         return reference.beta_contract(0, X, HT3, W3, beta, eps, False, True, active)[2]
+    if beta_any_k(K, beta):
+        return _beta_contract_any(0, X, HT3, W3, beta, eps, False, True, active)[2]
     dev = HT3.device
     _native_dtype_k("beta_loss", HT3.dtype, K, _hip.bp_max_k())
     for name, t in (("X", X), ("HT3", HT3), ("W3", W3)):
@@ -1364,6 +1441,9 @@ def beta_w_partials(X: torch.Tensor, XT: torch.Tensor | None, HT3: torch.Tensor,
         raise ValueError("beta_w_partials: inconsistent shapes")
     if not use_native(HT3):
         num, den, _ = reference.beta_contract(1, X, HT3, W3, beta, eps, True, False, active)
+        return num.unsqueeze(0), (den.unsqueeze(0) if den is not None else None)
+    if beta_any_k(K, beta):
+        num, den, _ = _beta_contract_any(1, X, HT3, W3, beta, eps, True, False, active)
         return num.unsqueeze(0), (den.unsqueeze(0) if den is not None else None)
     dev = HT3.device
     _native_dtype_k("beta_w_partials", HT3.dtype, K, _hip.bp_max_k())

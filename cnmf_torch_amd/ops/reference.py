@@ -193,11 +193,13 @@ def beta_contract(side: int, X, HT3, W3, beta: float, eps: float, want_num: bool
 
 
 def beta_update_h(X, HT3, W3, beta, eps, l1=0.0, l2=0.0, gamma=1.0, act=None, tol=None,
-                  iters=None, conv_mode=0, check_every=10, hstate=None):
-    """Reference of the fused in-place usage update (beta_mu.hip, upd != 0)."""
+                  iters=None, conv_mode=0, check_every=10, hstate=None, contract=None):
+    """Reference of the fused in-place usage update (beta_mu.hip, upd != 0).  ``contract``:
+    the beta_contract implementation to use (ops: the rank-general native one)."""
+    beta_contract_ = contract or beta_contract
     R = HT3.shape[0]
     loss_rule = tol is not None and conv_mode == 1
-    num, den, f = beta_contract(0, X, HT3, W3, beta, eps, True, loss_rule, act)
+    num, den, f = beta_contract_(0, X, HT3, W3, beta, eps, True, loss_rule, act)
     if den is None:
         den = W3.sum(dim=2, keepdim=True)
     d = den + l1 + l2 * HT3
@@ -230,27 +232,28 @@ def beta_update_h(X, HT3, W3, beta, eps, l1=0.0, l2=0.0, gamma=1.0, act=None, to
 
 
 def beta_h_block(X, HT3, W3, beta, eps, nsteps, l1=0.0, l2=0.0, gamma=1.0, act=None, tol=None,
-                 iters=None, conv_mode=1, hstate=None, loss_entry=False):
+                 iters=None, conv_mode=1, hstate=None, loss_entry=False, contract=None):
     """Reference of the multi-step usage solve block (beta_planes.hip, side 0): ``nsteps``
     MU steps of the live replicates, then the stopping rule: conv_mode 1 compares the
     block's exit objective -- the beta-divergence at the iterate its last step starts from
     (after the block for a one-step block) -- with the previous one (``loss_entry``: the
     objective before the block, evaluated here; else the value ``hstate`` recorded);
     conv_mode 0 reads the relative change of the block's last step."""
+    beta_contract_ = contract or beta_contract
     R = HT3.shape[0]
     live = torch.ones(R, dtype=torch.bool, device=HT3.device) if act is None else (act[:R] != 0)
     rule = tol is not None
     f_entry = None
     if rule and conv_mode == 1 and loss_entry and nsteps > 0:
-        f_entry = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
+        f_entry = beta_contract_(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
     dn = hn = None
     f_exit = None
     exit_in_last = nsteps >= 2
     for s in range(nsteps):
         if rule and conv_mode == 1 and exit_in_last and s == nsteps - 1:
             # the kernel reads the exit objective off the last step's P pass
-            f_exit = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
-        num, den, _ = beta_contract(0, X, HT3, W3, beta, eps, True, False, act)
+            f_exit = beta_contract_(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
+        num, den, _ = beta_contract_(0, X, HT3, W3, beta, eps, True, False, act)
         if den is None:
             den = W3.sum(dim=2, keepdim=True)
         d = den + l1 + l2 * HT3
@@ -267,7 +270,7 @@ def beta_h_block(X, HT3, W3, beta, eps, nsteps, l1=0.0, l2=0.0, gamma=1.0, act=N
         return
     if conv_mode == 1:
         if f_exit is None:
-            f_exit = beta_contract(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
+            f_exit = beta_contract_(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
         hs = hstate.view(-1, 2)[:R]
         f_prev = f_entry if loss_entry else hs[:, 0]
         checked = torch.full_like(live, bool(loss_entry)) | (hs[:, 1] > 0)

@@ -453,6 +453,15 @@ PYBIND11_MODULE(_hip, m) {
           "harmony_objective");
   });
 
+  m.def("beta_any_rows", []() { return cnmf_beta_any_rows(); });
+  m.def("beta_any_terms", [](int mode, uintptr_t X, long long ldx, uintptr_t Pm, uintptr_t D, int m_,
+                             int c, int G, float beta, float eps, uintptr_t act, int want_q,
+                             uintptr_t part, uintptr_t stream) {
+    check(cnmf_beta_any_terms(mode, P<const float>(X), ldx, P<float>(Pm), P<float>(D), m_, c, G,
+                              beta, eps, P<const int>(act), want_q, P<double>(part),
+                              reinterpret_cast<hipStream_t>(stream)),
+          "beta_any_terms");
+  });
   m.def("solve_any_hals_max_k", []() { return cnmf_solve_any_hals_max_k(); });
   m.def("solve_any", [](int op, uintptr_t x, long long x_rs, long long ldx, uintptr_t numer,
                         long long n_rs, long long ldn, uintptr_t D, uintptr_t G, long long g_rs,

@@ -135,6 +135,10 @@ hipError_t cnmf_harmony_objective(const double* O, const double* E, const double
                                   const double* theta, int K, int B, double* obj, double* out,
                                   hipStream_t stream);
 
+int cnmf_beta_any_rows();
+hipError_t cnmf_beta_any_terms(int mode, const float* X, long long ldx, float* P, float* D, int m,
+                               int c, int G, float beta, float eps, const int* act, int want_q,
+                               double* part, hipStream_t stream);
 int cnmf_solve_any_hals_max_k();
 hipError_t cnmf_solve_any(int op, float* x, long long x_rs, long long ldx, const float* numer,
                           long long n_rs, long long ldn, const float* D, const float* G,

@@ -559,3 +559,55 @@ def test_swap_compaction_equals_gather_compaction(monkeypatch, K):
     np.testing.assert_array_equal(a.n_iter, b.n_iter)
     np.testing.assert_array_equal(a.err, b.err)
     assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
+
+
+@pytest.mark.parametrize("beta,K", [(1.0, 80), (0.0, 60), (1.5, 72), (0.5, 130)])
+def test_beta_any_contract_matches_float64_reference(beta, K):
+    """The rank-general beta contraction (KL beyond 64, IS / general beta beyond 56:
+    library GEMMs + beta_any.hip's terms pass) == the float64 reference on both sides,
+    with an inactive replicate (zero outputs) and the divergence sums."""
+    from cnmf_torch_amd import ops
+    from cnmf_torch_amd.ops import reference
+
+    assert ops.beta_any_k(K, beta)
+    g = torch.Generator().manual_seed(K)
+    R, N, G = 3, 500, 301
+    X = torch.rand((N, G), generator=g, dtype=torch.float64) * \
+        (torch.rand((N, G), generator=g, dtype=torch.float64) < 0.4)
+    HT = torch.rand((R, K, N), generator=g, dtype=torch.float64) / K
+    W = torch.rand((R, K, G), generator=g, dtype=torch.float64)
+    act = torch.tensor([1, 0, 1], dtype=torch.int32)
+    d = dict(device="cuda", dtype=torch.float32)
+    for side in ("h", "w"):
+        s = {"h": 0, "w": 1}[side]
+        nr, dr, lr = reference.beta_contract(s, X, HT, W, beta, 1e-16, True, s == 0, act)
+        ng, dg, lg = ops.beta_contract(side, X.to(**d), HT.to(**d), W.to(**d), beta, 1e-16,
+                                       want_loss=s == 0, active=act.cuda())
+        for r in (0, 2):
+            np.testing.assert_allclose(ng[r].cpu().double().numpy(), nr[r].numpy(), rtol=2e-4,
+                                       atol=1e-6 * float(nr[r].abs().max()))
+            if dr is not None:
+                np.testing.assert_allclose(dg[r].cpu().double().numpy(), dr[r].numpy(),
+                                           rtol=2e-4, atol=1e-6 * float(dr[r].abs().max()))
+        assert float(ng[1].abs().max()) == 0.0
+        assert (dg is None) == (dr is None)
+        if s == 0:
+            np.testing.assert_allclose(lg[[0, 2]].cpu().numpy(), lr[[0, 2]].numpy(), rtol=1e-4)
+            assert float(lg[1]) == 0.0
+
+
+@pytest.mark.parametrize("loss,K", [("kullback-leibler", 80), ("itakura-saito", 60)])
+def test_beta_rank_beyond_panels_runs_native(loss, K, recwarn):
+    """KL at K > 64 and IS at K > 56 factorise on the rank-general path (no eager routing,
+    no warning) like the CPU engine of the same seeds."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    Xn = normalized_counts_matrix(600, 200, n_programs=6, seed=4)
+    opts = NMFOptions(n_components=K, beta_loss=loss, online_chunk_size=300,
+                      online_max_pass=3)
+    g = NMFBatchSolver(torch.from_numpy(Xn).cuda(), opts).run([7, 8])
+    c = NMFBatchSolver(torch.from_numpy(Xn), opts).run([7, 8])
+    assert torch.isfinite(g.W).all() and (g.W >= 0).all()
+    np.testing.assert_allclose(g.err, c.err, rtol=5e-3)
+    assert not [w for w in recwarn.list if "eager" in str(w.message)]
