@@ -250,10 +250,12 @@ def beta_h_block(X, HT3, W3, beta, eps, nsteps, l1=0.0, l2=0.0, gamma=1.0, act=N
     f_exit = None
     exit_in_last = nsteps >= 2
     for s in range(nsteps):
-        if rule and conv_mode == 1 and exit_in_last and s == nsteps - 1:
-            # the kernel reads the exit objective off the last step's P pass
-            f_exit = beta_contract_(0, X, HT3, W3, beta, eps, False, True, act)[2].to(HT3.device)
-        num, den, _ = beta_contract_(0, X, HT3, W3, beta, eps, True, False, act)
+        # the kernel reads the exit objective off the last step's P pass (here: the same
+        # contraction returns it)
+        at_exit = rule and conv_mode == 1 and exit_in_last and s == nsteps - 1
+        num, den, f = beta_contract_(0, X, HT3, W3, beta, eps, True, at_exit, act)
+        if at_exit:
+            f_exit = f.to(HT3.device)
         if den is None:
             den = W3.sum(dim=2, keepdim=True)
         d = den + l1 + l2 * HT3

@@ -1411,10 +1411,27 @@ def test_solve_wmfma_planes_and_rep_index():
         np.testing.assert_array_equal(planes[:, r * K:(r + 1) * K].cpu().numpy(), ref.numpy())
 
 
-def test_solve_wmfma_rejects_hals():
-    x0, numer, gram = _problem(1, 80, 100)
-    with pytest.raises(ValueError, match="MU solve only"):
-        ops.solve("hals", x0.cuda(), numer.cuda(), gram.cuda(), max_iter=2)
+def test_hals_beyond_64_takes_the_rank_general_solve():
+    """HALS at K > 64 (no tiled instantiation) runs solve_any.hip's Gauss-Seidel sweep and
+    matches the reference; past its LDS bound (512) the op raises instead of guessing."""
+    from cnmf_torch_amd.ops import reference
+
+    x0, numer, gram = _problem(2, 80, 100)
+    assert ops.solve_any_k(ops.ALGOS["hals"], 80)
+    xg = x0.cuda()
+    ops.solve("hals", xg, numer.cuda(), gram.cuda(), max_iter=3)
+    xr = x0.double()
+    reference.solve(ops.ALGOS["hals"], xr, numer.double(), gram.double(), None, 3, -1.0, 0.0,
+                    0.0, 0.0, 1e-16, None, None, None)
+    np.testing.assert_allclose(xg.cpu().double().numpy(), xr.numpy(), rtol=2e-3, atol=1e-5)
+    big = torch.rand((1, 520, 64), device="cuda")
+    with pytest.raises(ValueError, match="rank-general kernel's maximum 512"):
+        ops.solve("hals", big, big.clone(), torch.eye(520, device="cuda")[None].contiguous(),
+                  max_iter=1)
+    with pytest.raises(ValueError, match="rank-general solve"):
+        ops.solve("mu", torch.rand((1, 200, 64), device="cuda"),
+                  torch.rand((1, 200, 64), device="cuda"),
+                  torch.eye(200, device="cuda")[None].contiguous(), variant="mfma")
 
 
 @pytest.mark.parametrize("K", [65, 100, 128])
