@@ -1485,10 +1485,19 @@ def test_refit_wide_and_unpadded_k_on_gpu():
         np.testing.assert_allclose(sg, sc, rtol=5e-3, atol=1e-5)
 
 
-def test_solve_rejects_uninstantiated_k_loudly():
+def test_solve_at_uninstantiated_k_runs_the_rank_general_solve():
+    """A rank without a tiled instantiation (K = 37; the engine pads it, a direct caller
+    need not) runs solve_any.hip, never an eager fallback, and matches the reference."""
+    from cnmf_torch_amd.ops import reference
+
     x0, numer, gram = _problem(2, 37, 100)
-    with pytest.raises(ValueError, match="pad"):
-        ops.solve("mu", x0.cuda(), numer.cuda(), gram.cuda(), max_iter=2)
+    assert ops.solve_any_k(ops.ALGOS["mu"], 37)
+    xg = x0.cuda()
+    ops.solve("mu", xg, numer.cuda(), gram.cuda(), max_iter=2)
+    xr = x0.double()
+    reference.solve(ops.ALGOS["mu"], xr, numer.double(), gram.double(), None, 2, -1.0, 0.0,
+                    0.0, 0.0, 1e-16, None, None, None)
+    np.testing.assert_allclose(xg.cpu().double().numpy(), xr.numpy(), rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("K", [37, 64])
