@@ -152,6 +152,7 @@ def main() -> int:
         dist.init_process_group(backend="nccl" if (use_cuda and not args.share_gpu) else "gloo",
                                 device_id=dev if (use_cuda and not args.share_gpu) else None)
 
+    from cnmf_torch_amd.models import nmf_graphs as _graphs
     from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
     from cnmf_torch_amd.parallel.comm import DistComm
     from cnmf_torch_amd.parallel.runner import dp_layout, dp_row_segments
@@ -286,6 +287,7 @@ def main() -> int:
                 acc.append(float(np.mean(it / np.maximum(res.n_iter, 1) / n_chunks)))
 
     stream_info = None
+    captures_timed = None
     if stream:
         if args.warmup:
             stream_steps(0, args.warmup)
@@ -309,9 +311,11 @@ def main() -> int:
                 coll_calls, comm.record = comm.record, None
         barrier()
         t0 = time.perf_counter()
+        cap0 = _graphs.CAPTURES[0]
         for i in range(args.warmup, nsteps):
             res, _ = step(i)
             record(res)
+        captures_timed = _graphs.CAPTURES[0] - cap0
     barrier()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed)
@@ -405,6 +409,7 @@ def main() -> int:
                 if stream_info and stream_info["slots"] else "one solve per step",
                 "device": "cpu" if not use_cuda else torch.cuda.get_device_name(dev),
                 "mean_passes": round(float(np.mean(passes)), 2) if passes else None,
+                "graph_captures_timed": captures_timed,
                 "mean_sweeps_h_w": [round(float(np.mean(h_sweeps)), 1) if h_sweeps else None,
                                     round(float(np.mean(w_sweeps)), 1) if w_sweeps else None],
                 "input": ("float (X + 0.5 U(0,1))" if args.float_input else "counts / std")

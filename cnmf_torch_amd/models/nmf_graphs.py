@@ -19,6 +19,9 @@ from .nmf_batch import _Batch
 # what the caching allocator's capture pools guarantee)
 _TLS = threading.local()
 
+# pass-graph captures made by this process (bench.py reports those inside its timed region)
+CAPTURES = [0]
+
 
 class _GraphMixin:
     """NMFBatchSolver methods: HIP-graph capture / replay of the online passes per batch
@@ -122,5 +125,6 @@ class _GraphMixin:
                 return False
             main.wait_stream(sl["stream"])
             sl["graph"] = g
+            CAPTURES[0] += 1
         sl["graph"].replay()
         return True
