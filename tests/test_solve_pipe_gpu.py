@@ -611,3 +611,32 @@ def test_beta_rank_beyond_panels_runs_native(loss, K, recwarn):
     assert torch.isfinite(g.W).all() and (g.W >= 0).all()
     np.testing.assert_allclose(g.err, c.err, rtol=5e-3)
     assert not [w for w in recwarn.list if "eager" in str(w.message)]
+
+
+def test_rank_general_batch_mode_and_pipeline_at_k_140(tmp_path, recwarn):
+    """The rank-general solve under the batch-mode engine (fixed-step column splits) and
+    through the cNMF pipeline (prepare -> factorize -> combine) at
+    K = 140 on the GPU, no eager routing."""
+    import pandas as pd
+
+    from cnmf_torch_amd import cNMF, load_df_from_npz, save_df_to_npz
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix, simulate_counts
+
+    Xn = normalized_counts_matrix(700, 260, n_programs=6, seed=5)
+    opts = NMFOptions(n_components=140, mode="batch", batch_max_iter=30)
+    g = NMFBatchSolver(torch.from_numpy(Xn).cuda(), opts).run([3, 4])
+    c = NMFBatchSolver(torch.from_numpy(Xn), opts).run([3, 4])
+    np.testing.assert_allclose(g.err, c.err, rtol=2e-3)
+    X, cells, genes = simulate_counts(600, 300, 6, seed=2, sparse=False)
+    fn = str(tmp_path / "counts.df.npz")
+    save_df_to_npz(pd.DataFrame(X, index=cells, columns=genes), fn)
+    obj = cNMF(output_dir=str(tmp_path), name="k140")
+    obj.prepare(fn, components=[140], n_iter=3, seed=1, num_highvar_genes=250, prewarm=False)
+    obj.factorize(verbose=False)
+    obj.combine()
+    # (no consensus: at K = 140 on 250 genes some components die to exact zeros, whose
+    # l2 normalisation is NaN -- in the reference's formula too, cnmf.py:1056)
+    merged = load_df_from_npz(obj.paths["merged_spectra"] % 140)
+    assert merged.shape == (3 * 140, 250) and np.isfinite(merged.values).all()
+    assert not [w for w in recwarn.list if "eager" in str(w.message)]
