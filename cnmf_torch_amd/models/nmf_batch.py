@@ -324,19 +324,36 @@ class _Batch:
         rows = _to_device(_ranges(roff[inv], self.kpos[inv]), dev)
         HT = self.HT.index_select(0, rows)
         W = self.W.index_select(0, rows)
-        idx = _to_device(inv, dev)
-        # one packed device->host copy instead of eight small synchronising ones
-        keys = ("err", "n_pass", "converged")
-        rows5 = torch.stack([self.state[k][idx].to(torch.float64) for k in keys] +
-                            [self.h_iters[idx].to(torch.float64),
-                             self.w_iters[idx].to(torch.float64)])
-        flat = torch.cat([rows5.view(-1)] + [t.view(-1)[:1].to(torch.float64) for t in extra]) \
-            if len(extra) else rows5.view(-1)
-        flat = flat.cpu().numpy()
-        m = idx.numel()
-        packed, ext = flat[:5 * m].reshape(5, m), flat[5 * m:]
-        return (HT, W, self.kpos[inv], packed[0], packed[1].astype(np.int64), packed[2] != 0,
-                packed[3].astype(np.int64), packed[4].astype(np.int64), ext)
+        # the raw per-position state goes to the host as it lies (an arena batch: its two
+        # packed buffers, two copies) and is put in replicate order there -- the device
+        # gather / cast / stack of every field cost ~10 small launches at each run's end,
+        # host-latency bound (profiles/r6zl_*)
+        R = self.R
+        if self.arena is not None:
+            srcs = [self.arena["sf"], self.arena["si"]]
+        else:
+            srcs = [self.state["err"], self.state["n_pass"], self.state["converged"],
+                    self.h_iters, self.w_iters]
+        srcs = srcs + [t.view(-1)[:1] for t in extra]
+        if dev.type == "cuda":
+            host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in srcs]
+            for hb, t in zip(host, srcs):
+                hb.copy_(t, non_blocking=True)
+            torch.cuda.current_stream(dev).synchronize()
+            host = [hb.numpy() for hb in host]
+        else:
+            host = [t.numpy().copy() for t in srcs]
+        if self.arena is not None:
+            sf, si = host[0], host[1]
+            err, conv, n_pass, hi, wi = sf[2, :R], si[1, :R], si[2, :R], si[3, :R], si[4, :R]
+            ext_h = host[2:]
+        else:
+            err, n_pass, conv, hi, wi = (h[:R] for h in host[:5])
+            ext_h = host[5:]
+        ext = np.array([float(e.reshape(-1)[0]) for e in ext_h], dtype=np.float64)
+        return (HT, W, self.kpos[inv], err[inv].astype(np.float64),
+                n_pass[inv].astype(np.int64), conv[inv] != 0, hi[inv].astype(np.int64),
+                wi[inv].astype(np.int64), ext)
 
 
 
