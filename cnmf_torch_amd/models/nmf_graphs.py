@@ -78,7 +78,7 @@ class _GraphMixin:
 
     def _slot(self, st: _Batch, steps) -> dict:
         """Per-layout slot of an arena batch: the fused step's workspaces (fixed addresses),
-        a capture stream and, once captured, the pass's HIP graph."""
+        the solver's capture stream and, once captured, the pass's HIP graph."""
         a = st.arena
         # (a streaming run's pass graph holds its feed's ring / store addresses)
         key = (st.n_act, tuple(int(k) for k in st.kpos[:st.n_act]),
@@ -87,13 +87,24 @@ class _GraphMixin:
         sl = slots.get(key)
         if sl is None:
             sl = {"fb": self._fused_bufs(st, steps), "graph": None, "failed": False,
-                  "stream": torch.cuda.Stream(self.X.device)}
+                  "stream": self._capture_stream()}
             slots[key] = sl
             while len(slots) > 24:
                 slots.popitem(last=False)
         else:
             slots.move_to_end(key)
         return sl
+
+    def _capture_stream(self):
+        """The one side stream this solver captures pass graphs on (captures are serial,
+        the graphs replay on the caller's stream).  One per solver, not one per layout:
+        a new HIP stream cost ~0.6 ms of host time at each new layout's first pass
+        (hipStreamCreateWithPriority while torch's stream pool fills,
+        profiles/r6zl_boundary_gaps.txt)."""
+        s = getattr(self, "_cap_stream", None)
+        if s is None or s.device != self.X.device:
+            s = self._cap_stream = torch.cuda.Stream(self.X.device)
+        return s
 
     def _replay_slot(self, sl: dict, st: _Batch, steps) -> bool:
         """Run one non-final fused pass from the slot's graph (captured on first use, on
