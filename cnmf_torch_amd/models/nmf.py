@@ -329,11 +329,15 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
         """(3, rows, cols) int16 workspace, reused while the shape holds."""
         if self.X.device.type == "cuda":     # run_concurrent: one workspace per stream
             key = (key, ops._stream_ptr(self.X))
-        buf = self._ws.get(key)
-        if buf is None or buf.shape[1] < rows or buf.shape[2] != cols:
-            buf = torch.zeros((3, rows, cols), dtype=torch.int16, device=self.X.device)
-            self._ws[key] = buf
-        return buf
+        ent = self._ws.get(key)
+        if ent is None or ent[0].shape[1] < rows or ent[0].shape[2] != cols:
+            if ent is not None and ent[1]:      # a captured graph holds its address
+                ops._GRAPH_HELD.append(ent[0])
+            ent = [torch.zeros((3, rows, cols), dtype=torch.int16, device=self.X.device), False]
+            self._ws[key] = ent
+        if self.X.device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            ent[1] = True
+        return ent[0]
 
     def _stream_key(self):
         return ops._stream_ptr(self.X) if self.X.device.type == "cuda" else None

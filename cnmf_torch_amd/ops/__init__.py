@@ -1505,11 +1505,8 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
     S = 1 if R >= _GRAM_SPLIT_MIN_R else max(1, min((n + 255) // 256, 512 // max(1, R)))
     part = 0
     if S > 1:
-        key = (str(X3.device), _stream_ptr(X3))
-        ws = _GRAM_WS.get(key)
-        if ws is None or ws.numel() < S * R * K * K:
-            ws = torch.empty(max(S * R * K * K, 1 << 14), dtype=torch.float32, device=X3.device)
-            _GRAM_WS[key] = ws
+        ws = scratch(_GRAM_WS, (str(X3.device), _stream_ptr(X3)), S * R * K * K,
+                     torch.float32, X3.device, 1 << 14)
         part = ws.data_ptr()
     _hip.gram(X3.data_ptr(), X3.stride(0), X3.stride(1), R, K, n, out.data_ptr(), K * K,
               int(bool(accumulate)), active.data_ptr() if active is not None else 0,
@@ -1518,6 +1515,26 @@ def gram(X3: torch.Tensor, out: torch.Tensor | None = None, accumulate: bool = F
 
 
 _GRAM_WS: dict = {}
+
+# scratch buffers a captured HIP graph has used: never freed while the process runs (a
+# replaced cache entry would otherwise return memory a graph still writes to)
+_GRAPH_HELD: list = []
+
+
+def scratch(cache: dict, key, numel: int, dtype, device, min_numel: int = 0) -> torch.Tensor:
+    """A per-key scratch tensor of >= ``numel`` elements from ``cache``, grown on demand.
+    An entry handed out during a graph capture is marked; when a marked entry is replaced
+    by a larger one, the old buffer is held for the life of the process (graphs captured
+    with it keep its address)."""
+    ent = cache.get(key)
+    if ent is None or ent[0].numel() < numel:
+        if ent is not None and ent[1]:
+            _GRAPH_HELD.append(ent[0])
+        ent = [torch.empty(max(numel, min_numel), dtype=dtype, device=device), False]
+        cache[key] = ent
+    if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        ent[1] = True
+    return ent[0]
 # replicate count from which one workgroup per replicate fills the chip (no column split)
 _GRAM_SPLIT_MIN_R = 64
 _gram_op = gram    # ops.solve's `gram` argument shadows the function there
@@ -2117,11 +2134,8 @@ def gemm_planes(C: torch.Tensor | None, A: torch.Tensor, B: torch.Tensor, M: int
             raise ValueError(f"raw_slab: {raw_slab.numel()} < ksplit {ksplit} x {M} x {N}")
         slab = raw_slab.data_ptr()
     elif ksplit > 1:
-        key = (str(C.device), _stream_ptr(C))
-        ws = _GEMM_SLAB.get(key)
-        if ws is None or ws.numel() < ksplit * M * N:
-            ws = torch.empty(max(ksplit * M * N, 1 << 20), dtype=torch.float32, device=C.device)
-            _GEMM_SLAB[key] = ws
+        ws = scratch(_GEMM_SLAB, (str(C.device), _stream_ptr(C)), ksplit * M * N,
+                     torch.float32, C.device, 1 << 20)
         slab = ws.data_ptr()
     _hip.gemm_planes(A.data_ptr(), A.stride(1), A.stride(0), a_rows, B.data_ptr(), B.stride(1),
                      B.stride(0), b_rows, C.data_ptr(), C.stride(0),
