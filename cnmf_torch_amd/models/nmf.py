@@ -601,6 +601,11 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
         ngp = sum(g.n * S * g.K * g.K for g in st.groups)
         kd_max = max(-(-cw // bk) * bk for cw in cws)
         fb = {
+            # the passes' active flags, stored by conv_update through the host mapping into
+            # two alternating slots, and its launch counter (device, plus the host's mirror)
+            "hflags": torch.ones((2, st.n_act), dtype=torch.int32, pin_memory=True),
+            "hcnt": torch.zeros(1, dtype=torch.int32, device=dev),
+            "hcnt_host": [0],
             "wpl": torch.zeros((3, rows, xp.Gp), device=dev, dtype=torch.int16),
             "hpl": torch.zeros((3, rows, kd_max), device=dev, dtype=torch.int16),
             "wpl_key": None,
@@ -650,6 +655,17 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
         return wkey
 
     def _enqueue_fused(self, st: _Batch, steps, cur: dict) -> None:
+        """Enqueue one single-process fused pass (_enqueue_fused_pass) and point
+        ``st.host_flags`` at the host-mapped slot its conv_update stores the active flags
+        in (the layout's launch count, mirrored on the host, picks the slot)."""
+        self._enqueue_fused_pass(st, steps, cur)
+        fb = cur["fb"]
+        if "hflags" in fb:
+            c = fb["hcnt_host"][0]
+            fb["hcnt_host"][0] = c + 1
+            st.host_flags = fb["hflags"][c & 1]
+
+    def _enqueue_fused_pass(self, st: _Batch, steps, cur: dict) -> None:
         """Enqueue one single-process fused pass: from the layout's captured graph when
         the batch has an arena (captured on the layout's second pass; a layout an earlier
         run captured replays from its first, with only the W-dependent operands rebuilt
@@ -733,7 +749,8 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
             fb["wwp_key"] = fb["wpl_key"] = wkey
         ops.conv_update(fb["lin"], fb["quad"], self.x_sq, {k: v[:n] for k, v in st.state.items()},
                         n, -1, o.tol, final=final, gate=st.gate,
-                        max_pass=int(o.online_max_pass))
+                        max_pass=int(o.online_max_pass),
+                        host_flags=(fb["hflags"], fb["hcnt"]) if "hflags" in fb else None)
         if st.feed is not None:        # streaming: harvest / refill in this pass (stream.hip)
             self._stream_swap_dev(st, fb)
 

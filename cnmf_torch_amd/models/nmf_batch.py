@@ -103,6 +103,9 @@ class _Batch:
         self.inplace = arena is not None
         self.arena = arena
         self.graphs = False       # NMFBatchSolver.run: replay graphs per layout (arena only)
+        # host-mapped flags slot the last enqueued fused pass stores into (ops.conv_update
+        # host_flags), else None: _PassPipeline copies the flags
+        self.host_flags = None
         if arena is not None:
             # the arena's per-replicate state is two packed buffers (float64 rows
             # err_init/err_prev/err, int32 rows active/converged/n_pass/h_iters/w_iters):
@@ -412,11 +415,18 @@ class _PassPipeline:
             if n - st.prefix_len(st.state["active"][:n].numpy() != 0) >= max(1, int(self._frac(n) * n)):
                 st.compact()
             return True
-        flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
-        # (a flag copy on a side stream removed the ~5 us gap per pass in the trace but was
-        # slower end to end -- headline -2 %, K grid -5.5 %, profiles/r3y_*: the stream
-        # switch and event sit on the host's enqueue path)
-        flags.copy_(st.state["active"][:n], non_blocking=True)
+        hf, st.host_flags = st.host_flags, None
+        if hf is not None and hf.numel() == n:
+            # this pass's flags, stored by its conv_update into a host-mapped slot; the next
+            # pass stores into the other slot, so the read below (after this pass's event,
+            # one pass later) sees exactly this pass's flags -- no copy launch
+            flags = hf
+        else:
+            flags = torch.empty(n, dtype=torch.int32, pin_memory=True)
+            # (a flag copy on a side stream removed the ~5 us gap per pass in the trace but
+            # was slower end to end -- headline -2 %, K grid -5.5 %, profiles/r3y_*: the
+            # stream switch and event sit on the host's enqueue path)
+            flags.copy_(st.state["active"][:n], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         prev, self.pending = self.pending, (ev, flags, n)

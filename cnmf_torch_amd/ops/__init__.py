@@ -658,7 +658,8 @@ def coop_check(device: torch.device | None = None, values=None, flags=None) -> N
 # ----------------------------------------------------------------------------- convergence
 def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict, n: int,
                 pass_idx: int, tol: float, final: bool, init: bool = False,
-                gate: torch.Tensor | None = None, max_pass: int = 0) -> None:
+                gate: torch.Tensor | None = None, max_pass: int = 0,
+                host_flags: tuple | None = None) -> None:
     """Per-replicate Frobenius error from (lin, quad) and the (prev - cur)/init < tol
     stopping rule, entirely on the device (csrc/kernels/conv.hip).  ``state`` holds
     float64 err_init/err_prev/err and int32 active/converged/n_pass tensors.
@@ -666,7 +667,11 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
     per-pass host argument and can live in a captured graph.  ``max_pass`` > 0: a
     replicate stops after its own max_pass-th pass (replicates of a streaming batch sit
     at different passes).  ``gate`` (int32 device scalar): set to 1 while any replicate
-    is active, else 0 (gemm_planes ``gate``)."""
+    is active, else 0 (gemm_planes ``gate``).  ``host_flags`` (GPU): (flags, counter) --
+    pinned int32 (2, >= n) and an int32 device scalar; the launch also stores the active
+    flags into ``flags[counter % 2]`` through the host mapping and advances the counter,
+    so the host reads a pass's flags after its event without a copy launch (the caller
+    mirrors the counter: _PassPipeline)."""
     if n <= 0:
         return
     if not use_native(lin):
@@ -675,6 +680,14 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
         if gate is not None:
             gate.fill_(int(bool((state["active"][:n] != 0).any())))
         return
+    hf_ptr = hc_ptr = 0
+    if host_flags is not None:
+        hf, hc = host_flags
+        if (hf.dtype != torch.int32 or hf.dim() != 2 or hf.shape[0] != 2 or hf.shape[1] != n
+                or not hf.is_pinned() or not hf.is_contiguous() or hc.dtype != torch.int32
+                or hc.device != lin.device):
+            raise ValueError("host_flags: (pinned contiguous int32 (2, n), int32 device scalar)")
+        hf_ptr, hc_ptr = hf.data_ptr(), hc.data_ptr()
     for t in (lin, quad):
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() < n:
             raise ValueError("lin/quad must be contiguous float32 with >= n entries")
@@ -687,7 +700,8 @@ def conv_update(lin: torch.Tensor, quad: torch.Tensor, x_sq: float, state: dict,
                      state["err_prev"].data_ptr(), state["err"].data_ptr(),
                      state["active"].data_ptr(), state["converged"].data_ptr(),
                      state["n_pass"].data_ptr(), int(n), int(pass_idx), float(tol), int(final),
-                     int(init), _gate_ptr(gate, lin.device), int(max_pass), _stream_ptr(lin))
+                     int(init), _gate_ptr(gate, lin.device), int(max_pass), hf_ptr, hc_ptr,
+                     _stream_ptr(lin))
 
 
 # ----------------------------------------------------------------------------- streaming

@@ -188,12 +188,12 @@ PYBIND11_MODULE(_hip, m) {
         [](uintptr_t lin, uintptr_t quad, double x_sq, uintptr_t err_init, uintptr_t err_prev,
            uintptr_t err, uintptr_t active, uintptr_t converged, uintptr_t n_pass, int n,
            int pass, double tol, int final_pass, int init, uintptr_t gate, int max_pass,
-           uintptr_t stream) {
+           uintptr_t hflags, uintptr_t hcnt, uintptr_t stream) {
           check(cnmf_conv_update(P<const float>(lin), P<const float>(quad), x_sq,
                                  P<double>(err_init), P<double>(err_prev), P<double>(err),
                                  P<int>(active), P<int>(converged), P<int>(n_pass), n, pass, tol,
-                                 final_pass, init, P<int>(gate), max_pass,
-                                 reinterpret_cast<hipStream_t>(stream)),
+                                 final_pass, init, P<int>(gate), max_pass, P<int>(hflags),
+                                 P<int>(hcnt), reinterpret_cast<hipStream_t>(stream)),
                 "cnmf_conv_update");
         });
 

@@ -35,7 +35,8 @@ hipError_t cnmf_stream_publish(const int* ctr, int n, int* seq, int* mail, int s
 hipError_t cnmf_conv_update(const float* lin, const float* quad, double x_sq, double* err_init,
                             double* err_prev, double* err, int* active, int* converged,
                             int* n_pass, int n, int pass, double tol, int final_pass,
-                            int init, int* gate, int max_pass, hipStream_t stream);
+                            int init, int* gate, int max_pass, int* hflags, int* hcnt,
+                            hipStream_t stream);
 int cnmf_solve_reg_max_cols(int K);
 int cnmf_solve_mfma_max_cols(int K);
 int cnmf_solve_pipe_tiles(int K, int per);
