@@ -601,11 +601,6 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
         ngp = sum(g.n * S * g.K * g.K for g in st.groups)
         kd_max = max(-(-cw // bk) * bk for cw in cws)
         fb = {
-            # the passes' active flags, stored by conv_update through the host mapping into
-            # two alternating slots, and its launch counter (device, plus the host's mirror)
-            "hflags": torch.ones((2, st.n_act), dtype=torch.int32, pin_memory=True),
-            "hcnt": torch.zeros(1, dtype=torch.int32, device=dev),
-            "hcnt_host": [0],
             "wpl": torch.zeros((3, rows, xp.Gp), device=dev, dtype=torch.int16),
             "hpl": torch.zeros((3, rows, kd_max), device=dev, dtype=torch.int16),
             "wpl_key": None,
@@ -626,6 +621,12 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
             fb["parts"][g.p0] = (lambda t, o_=off, g_=g: t[o_:o_ + g_.n * S * g_.K * g_.K]
                                  .view(g_.n, S, g_.K, g_.K))
             off += m
+        if os.environ.get("CNMF_HOST_FLAGS", "1") != "0":
+            # the passes' active flags, stored by conv_update through the host mapping into
+            # two alternating slots, and its launch counter (device, plus the host's mirror)
+            fb["hflags"] = torch.ones((2, st.n_act), dtype=torch.int32, pin_memory=True)
+            fb["hcnt"] = torch.zeros(1, dtype=torch.int32, device=dev)
+            fb["hcnt_host"] = [0]
         return fb
 
     def _fused_prep(self, st: _Batch, fb: dict, keep_slices: bool):

@@ -640,3 +640,24 @@ def test_rank_general_batch_mode_and_pipeline_at_k_140(tmp_path, recwarn):
     merged = load_df_from_npz(obj.paths["merged_spectra"] % 140)
     assert merged.shape == (3 * 140, 250) and np.isfinite(merged.values).all()
     assert not [w for w in recwarn.list if "eager" in str(w.message)]
+
+
+def test_host_mapped_flags_match_copied_flags_bitwise(monkeypatch):
+    """The fused passes' active flags stored by conv_update into alternating host-mapped
+    slots (CNMF_HOST_FLAGS, default) give exactly the compactions -- and so the
+    factorisations -- of the per-pass device->host copy, run after run."""
+    from cnmf_torch_amd.models.nmf import NMFBatchSolver, NMFOptions
+    from cnmf_torch_amd.utils.synthetic import normalized_counts_matrix
+
+    X = torch.from_numpy(normalized_counts_matrix(3000, 500, n_programs=8, seed=9)).cuda()
+    opts = NMFOptions(n_components=8, online_chunk_size=1500)
+    seeds = [[7 + 100 * i + j for j in range(24)] for i in range(3)]
+    out = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("CNMF_HOST_FLAGS", flag)
+        solver = NMFBatchSolver(X, opts)
+        out[flag] = [solver.run(s) for s in seeds]
+    for a, b in zip(out["1"], out["0"]):
+        assert torch.equal(a.W, b.W) and torch.equal(a.HT, b.HT)
+        np.testing.assert_array_equal(a.err, b.err)
+        np.testing.assert_array_equal(a.n_iter, b.n_iter)
