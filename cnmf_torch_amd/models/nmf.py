@@ -677,6 +677,12 @@ class NMFBatchSolver(_GraphMixin, _StreamMixin, _DPMixin, _BetaMixin):
                 sl = cur["sl"] = self._slot(st, steps) if st.graphs else None
                 cur["fb"] = sl["fb"] if sl is not None else self._fused_bufs(st, steps)
                 cur["key"] = key
+                if "hflags" in cur["fb"]:
+                    # the layout's first pass in this run: the flag kernel's launch counter
+                    # and the host's mirror restart together (whatever an earlier run, or
+                    # one that raised, left behind), ahead of this pass's launch
+                    cur["fb"]["hcnt"].zero_()
+                    cur["fb"]["hcnt_host"][0] = 0
             sl = cur["sl"]
             if sl is not None and sl["graph"] is not None and _LAYOUT_REPLAY:
                 self._fused_prep(st, cur["fb"], keep_slices=True)
