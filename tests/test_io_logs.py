@@ -197,3 +197,29 @@ def test_row_block_h5ad_writer_holds_one_block_at_a_time(tmp_path):
         np.testing.assert_array_equal(gx, X.toarray())
         assert sp.issparse(got.X) == sparse
         assert list(got.obs.index) == list(obs.index) and list(got.var.index) == list(var.index)
+
+
+def test_parallel_deflate_npz_is_a_standard_npz(tmp_path, monkeypatch):
+    """Members >= the parallel threshold are deflated in independent full-flushed chunks
+    on threads: the archive is a standard ZIP_DEFLATED npz (zipfile's CRC check, np.load,
+    load_df_from_npz) with the same contents as the one-thread writer."""
+    import zipfile
+
+    import numpy as np
+    import pandas as pd
+
+    from cnmf_torch_amd.utils import io as cio
+
+    monkeypatch.setattr(cio, "_PAR_DEFLATE_MIN", 1 << 16)
+    monkeypatch.setattr(cio, "_PAR_DEFLATE_CHUNK", 1 << 14)
+    rng = np.random.default_rng(3)
+    df = pd.DataFrame(np.round(rng.random((3000, 7)), 3), index=[f"c{i}" for i in range(3000)],
+                      columns=[f"g{j}" for j in range(7)])
+    fn = str(tmp_path / "p.npz")
+    cio.save_df_to_npz(df, fn)
+    with zipfile.ZipFile(fn) as z:
+        assert z.testzip() is None
+        assert all(i.compress_type == zipfile.ZIP_DEFLATED for i in z.infolist())
+    pd.testing.assert_frame_equal(cio.load_df_from_npz(fn, allow_pickle_fallback=False), df)
+    with np.load(fn, allow_pickle=False) as f:
+        np.testing.assert_array_equal(f["data"], df.values)
