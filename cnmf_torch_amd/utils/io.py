@@ -16,6 +16,7 @@ import gzip
 import io
 import os
 import tempfile
+import threading
 import warnings
 
 import numpy as np
@@ -89,6 +90,22 @@ NPZ_TMP_LEVEL = 0
 # members at least this large are deflated in parallel chunks (_deflate_parallel)
 _PAR_DEFLATE_MIN = 8 << 20
 _PAR_DEFLATE_CHUNK = 4 << 20
+_DEFLATE_POOL = None
+_DEFLATE_LOCK = threading.Lock()
+
+
+def _deflate_pool():
+    """The chunk-deflate threads (their own pool: a caller may itself run on another
+    pool's worker)."""
+    global _DEFLATE_POOL
+    with _DEFLATE_LOCK:
+        if _DEFLATE_POOL is None:
+            import concurrent.futures as cf
+
+            n = max(2, min(8, (os.cpu_count() or 4) // 2))
+            _DEFLATE_POOL = cf.ThreadPoolExecutor(max_workers=n,
+                                                  thread_name_prefix="cnmf-deflate")
+    return _DEFLATE_POOL
 
 
 def _deflate_parallel(payload, level: int):
@@ -98,8 +115,6 @@ def _deflate_parallel(payload, level: int):
     stream -- the pigz construction.  A 500k-cell usage table (two 40 MB members) took
     ~0.6 s of the Harmony pipeline's consensus on one thread."""
     import zlib
-
-    from .transfer import _pool
 
     mv = memoryview(payload)
     n = len(mv)
@@ -111,7 +126,7 @@ def _deflate_parallel(payload, level: int):
         return c.compress(mv[a:b]) + c.flush(zlib.Z_FINISH if i == len(parts) - 1
                                               else zlib.Z_FULL_FLUSH)
 
-    fut = _pool().map(comp, range(len(parts)))
+    fut = _deflate_pool().map(comp, range(len(parts)))
     crc = zlib.crc32(mv) & 0xFFFFFFFF      # one pass on this thread meanwhile
     return b"".join(fut), crc
 
