@@ -63,12 +63,18 @@ class DeviceCSR:
             return torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)
 
         # kernels rely on distinct columns within a row: a matrix scipy has not checked
-        # yet is checked after the upload on the device (scipy's single-threaded host
-        # check was 0.11 s of the 500k-cell Harmony stage, profiles/r6w_*)
+        # yet is checked on a worker thread while the arrays upload (scipy's check drops
+        # the GIL; it was 0.11 s of the 500k-cell Harmony stage, profiles/r6w_*, and a
+        # device-side check after the upload exposed the transfers instead, r6zzb)
         if dev.type == "cuda" and getattr(m, "_has_canonical_format", None) is None:
-            A = cls(up(m.indptr, np.int64), up(m.indices, np.int32), up(m.data, dtype), m.shape)
-            if _sorted_distinct(A):
-                return A
+            import concurrent.futures as cf
+
+            with cf.ThreadPoolExecutor(1, thread_name_prefix="cnmf-csr-check") as ex:
+                canon = ex.submit(lambda: bool(m.has_canonical_format))
+                A = cls(up(m.indptr, np.int64), up(m.indices, np.int32), up(m.data, dtype),
+                        m.shape)
+                if canon.result():
+                    return A
             del A
         if not m.has_canonical_format:
             m = m.copy()
@@ -99,7 +105,7 @@ class DeviceCSR:
 
 def _sorted_distinct(A: DeviceCSR) -> bool:
     """Whether every row's column indices strictly increase (scipy's canonical format),
-    checked where ``A`` lives."""
+    checked where ``A`` lives (a test / debugging check: it synchronises the device)."""
     nnz = A.indices.numel()
     if nnz < 2:
         return True

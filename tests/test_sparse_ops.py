@@ -244,8 +244,9 @@ def test_gemm_plan_fills_whole_waves_for_mid_size_batches():
 
 @pytest.mark.gpu
 def test_from_scipy_canonical_check_on_device():
-    """An unchecked CSR is checked for sorted, distinct columns on the device after the
-    upload; one that is not canonical is summed on the host like scipy's own path."""
+    """An unchecked CSR is checked for sorted, distinct columns (scipy's check, on a
+    worker thread while the arrays upload); one that is not canonical is summed on the
+    host like scipy's own path -- the device result is canonical either way."""
     m = sp.random(300, 120, density=0.1, format="csr", random_state=1, dtype=np.float32)
     for case in ("sorted", "reversed", "duplicate"):
         ind = m.indices.copy()
